@@ -1,0 +1,180 @@
+// Test infrastructure (oracle) — C entry points used by tests/ (ctypes) and bench.py's
+// cpu_baseline leg.  Not linked by the product.
+#include <algorithm>
+#include <chrono>
+#include "orc.h"
+
+using namespace orc;
+
+namespace {
+struct OrcResult {
+  ResultSet rs;
+  uint64_t edgesScanned = 0;
+  std::vector<std::string> strings;
+  std::vector<std::vector<int64_t>> paths;
+};
+}  // namespace
+
+extern "C" {
+
+void* orc_create(int32_t num_parts) {
+  auto* s = new Store();
+  s->numParts = num_parts;
+  for (int32_t p = 1; p <= num_parts; ++p) s->parts[p];
+  return s;
+}
+void orc_destroy(void* h) { delete static_cast<Store*>(h); }
+
+void orc_set_config(void* h, int32_t max_edge_per_vertex, int32_t min_vertices_per_bucket,
+                    int32_t max_handlers_per_req, int32_t threads) {
+  auto* s = static_cast<Store*>(h);
+  s->maxEdgePerVertex = max_edge_per_vertex;
+  s->minVerticesPerBucket = min_vertices_per_bucket;
+  s->maxHandlersPerReq = max_handlers_per_req;
+  s->threads = threads;
+}
+
+int32_t orc_register_schema(void* h, int32_t is_edge, int32_t id, const char* name, int64_t ver,
+                            int32_t ncols, const char* const* names, const int32_t* types) {
+  auto* s = static_cast<Store*>(h);
+  Schema sc;
+  sc.version = ver;
+  for (int32_t i = 0; i < ncols; ++i) sc.cols.push_back({names[i], static_cast<SType>(types[i])});
+  if (is_edge) {
+    s->edgeSchemas[id][ver] = sc;
+    s->edgeNames[id] = name;
+    s->edgeByName[name] = id;
+  } else {
+    s->tagSchemas[id][ver] = sc;
+    s->tagNames[id] = name;
+    s->tagByName[name] = id;
+  }
+  return 0;
+}
+
+// Records are appended in the given order; a later record with an identical key overwrites
+// the earlier one (RocksDB write-batch semantics).
+int32_t orc_load_part_kv(void* h, int32_t part, const uint8_t* kdata, const uint64_t* koffs,
+                         const uint8_t* vdata, const uint64_t* voffs, uint64_t n) {
+  auto* s = static_cast<Store*>(h);
+  auto& v = s->parts[part];
+  v.reserve(v.size() + n);
+  for (uint64_t i = 0; i < n; ++i) {
+    v.push_back({std::string(reinterpret_cast<const char*>(kdata) + koffs[i], koffs[i + 1] - koffs[i]),
+                 std::string(reinterpret_cast<const char*>(vdata) + voffs[i], voffs[i + 1] - voffs[i])});
+  }
+  return 0;
+}
+
+int32_t orc_finalize(void* h) {
+  auto* s = static_cast<Store*>(h);
+  for (auto& kv : s->parts) {
+    auto& v = kv.second;
+    // stable sort then keep the LAST of equal keys (last write wins)
+    std::stable_sort(v.begin(), v.end(), [](const KV& a, const KV& b) { return a.key < b.key; });
+    std::vector<KV> out;
+    out.reserve(v.size());
+    for (size_t i = 0; i < v.size(); ++i) {
+      if (i + 1 < v.size() && v[i + 1].key == v[i].key) continue;
+      out.push_back(std::move(v[i]));
+    }
+    v.swap(out);
+  }
+  return 0;
+}
+
+int32_t orc_go(void* h, const int64_t* starts, uint64_t nstarts, const int32_t* etypes, int32_t ntypes,
+               int32_t over_all, uint32_t steps, const uint8_t* where, uint32_t where_len,
+               const uint8_t* yields_blob, const uint32_t* yield_lens, int32_t nyields, int32_t distinct,
+               void** result) {
+  auto* s = static_cast<Store*>(h);
+  GoQuery q;
+  q.starts.assign(starts, starts + nstarts);
+  q.etypes.assign(etypes, etypes + ntypes);
+  q.overAll = over_all != 0;
+  q.steps = steps;
+  if (where_len) q.where.assign(reinterpret_cast<const char*>(where), where_len);
+  size_t off = 0;
+  for (int32_t i = 0; i < nyields; ++i) {
+    q.yields.emplace_back(reinterpret_cast<const char*>(yields_blob) + off, yield_lens[i]);
+    off += yield_lens[i];
+  }
+  q.distinct = distinct != 0;
+  auto* r = new OrcResult();
+  r->rs = runGo(*s, q);
+  *result = r;
+  return r->rs.code;
+}
+
+int32_t orc_result_code(void* r) { return static_cast<OrcResult*>(r)->rs.code; }
+const char* orc_result_error(void* r) { return static_cast<OrcResult*>(r)->rs.err.c_str(); }
+int64_t orc_result_rows(void* r) { return (int64_t) static_cast<OrcResult*>(r)->rs.rows.size(); }
+int32_t orc_result_cols(void* r) {
+  auto* x = static_cast<OrcResult*>(r);
+  return x->rs.rows.empty() ? (int32_t)x->rs.colNames.size() : (int32_t)x->rs.rows[0].size();
+}
+const char* orc_result_colname(void* r, int32_t c) { return static_cast<OrcResult*>(r)->rs.colNames[c].c_str(); }
+// cells: bits (int64 / double bits / bool / string index) + type tag per cell
+void orc_result_cells(void* r, int64_t* bits, uint8_t* types) {
+  auto* x = static_cast<OrcResult*>(r);
+  x->strings.clear();
+  size_t k = 0;
+  for (auto& row : x->rs.rows) {
+    for (auto& v : row) {
+      types[k] = static_cast<uint8_t>(v.index());
+      switch (v.index()) {
+        case 0: bits[k] = std::get<0>(v); break;
+        case 1: { double d = std::get<1>(v); memcpy(&bits[k], &d, 8); break; }
+        case 2: bits[k] = std::get<2>(v) ? 1 : 0; break;
+        default: bits[k] = (int64_t)x->strings.size(); x->strings.push_back(std::get<3>(v)); break;
+      }
+      ++k;
+    }
+  }
+}
+const char* orc_result_string(void* r, int64_t idx) { return static_cast<OrcResult*>(r)->strings[idx].c_str(); }
+void orc_result_free(void* r) { delete static_cast<OrcResult*>(r); }
+
+int32_t orc_find_path(void* h, const int64_t* from, uint64_t nf, const int64_t* to, uint64_t nt,
+                      const int32_t* etypes, int32_t ntypes, int32_t over_all, uint32_t upto,
+                      int32_t shortest, int32_t mode, void** result) {
+  auto* s = static_cast<Store*>(h);
+  FindPathQuery q;
+  q.from.assign(from, from + nf);
+  q.to.assign(to, to + nt);
+  q.etypes.assign(etypes, etypes + ntypes);
+  q.overAll = over_all != 0;
+  q.upto = upto;
+  q.shortest = shortest != 0;
+  auto* r = new OrcResult();
+  int32_t rc = mode == 0 ? runFindPath(*s, q, r->paths) : runShortestBfs(*s, q, r->paths);
+  *result = r;
+  return rc;
+}
+int64_t orc_paths_count(void* r) { return (int64_t) static_cast<OrcResult*>(r)->paths.size(); }
+int64_t orc_path_len(void* r, int64_t i) { return (int64_t) static_cast<OrcResult*>(r)->paths[i].size(); }
+void orc_path_get(void* r, int64_t i, int64_t* out) {
+  auto& p = static_cast<OrcResult*>(r)->paths[i];
+  std::copy(p.begin(), p.end(), out);
+}
+
+// CPU baseline helper: GO over the store, returning wall seconds and the number of adjacency
+// entries scanned (Σ_s E_s: edges returned by getBound at every step).
+double orc_go_timed(void* h, const int64_t* starts, uint64_t nstarts, const int32_t* etypes, int32_t ntypes,
+                    uint32_t steps, const uint8_t* where, uint32_t where_len, int64_t* rows_out,
+                    uint64_t* scanned_out) {
+  auto* s = static_cast<Store*>(h);
+  GoQuery q;
+  q.starts.assign(starts, starts + nstarts);
+  q.etypes.assign(etypes, etypes + ntypes);
+  q.steps = steps;
+  if (where_len) q.where.assign(reinterpret_cast<const char*>(where), where_len);
+  auto t0 = std::chrono::steady_clock::now();
+  auto rs = runGo(*s, q);
+  auto t1 = std::chrono::steady_clock::now();
+  if (rows_out) *rows_out = rs.code ? -1 : (int64_t)rs.rows.size();
+  if (scanned_out) *scanned_out = rs.scanned;
+  return std::chrono::duration<double>(t1 - t0).count();
+}
+
+}  // extern "C"

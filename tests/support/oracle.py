@@ -1,0 +1,178 @@
+"""ctypes binding of the CPU oracle (oracle/liborc.so) — test infrastructure only."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import struct
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+LIB = os.path.join(ROOT, "oracle", "liborc.so")
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+        L = C.CDLL(LIB)
+        vp, i32, i64, u32, u64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_uint64
+        P = C.POINTER
+        L.orc_create.restype = vp
+        L.orc_create.argtypes = [i32]
+        L.orc_destroy.argtypes = [vp]
+        L.orc_set_config.argtypes = [vp, i32, i32, i32, i32]
+        L.orc_register_schema.argtypes = [vp, i32, i32, C.c_char_p, i64, i32, P(C.c_char_p), P(i32)]
+        L.orc_load_part_kv.argtypes = [vp, i32, vp, vp, vp, vp, u64]
+        L.orc_finalize.argtypes = [vp]
+        L.orc_go.argtypes = [vp, vp, u64, vp, i32, i32, u32, vp, u32, vp, vp, i32, i32, P(vp)]
+        L.orc_go.restype = i32
+        L.orc_result_code.argtypes = [vp]
+        L.orc_result_error.argtypes = [vp]
+        L.orc_result_error.restype = C.c_char_p
+        L.orc_result_rows.argtypes = [vp]
+        L.orc_result_rows.restype = i64
+        L.orc_result_cols.argtypes = [vp]
+        L.orc_result_cells.argtypes = [vp, vp, vp]
+        L.orc_result_string.argtypes = [vp, i64]
+        L.orc_result_string.restype = C.c_char_p
+        L.orc_result_free.argtypes = [vp]
+        L.orc_find_path.argtypes = [vp, vp, u64, vp, u64, vp, i32, i32, u32, i32, i32, P(vp)]
+        L.orc_paths_count.argtypes = [vp]
+        L.orc_paths_count.restype = i64
+        L.orc_path_len.argtypes = [vp, i64]
+        L.orc_path_len.restype = i64
+        L.orc_path_get.argtypes = [vp, i64, vp]
+        L.orc_go_timed.argtypes = [vp, vp, u64, vp, i32, u32, vp, u32, P(i64), P(u64)]
+        L.orc_go_timed.restype = C.c_double
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None and len(a) else None
+
+
+class OracleError(Exception):
+    def __init__(self, code, msg):
+        super().__init__(f"{code}: {msg}")
+        self.code = code
+
+
+class Oracle:
+    """storaged+graphd restated on the CPU, over the same KV records the engine loads."""
+
+    def __init__(self, parts: int, max_edge_per_vertex: int = 0x7FFFFFFF, threads: int = 1):
+        self.L = lib()
+        self.h = self.L.orc_create(parts)
+        self.L.orc_set_config(self.h, max_edge_per_vertex, 3, 10, threads)
+        self.edge_types, self.edge_names = {}, {}
+        self.tag_ids = {}
+
+    def close(self):
+        if self.h:
+            self.L.orc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def register(self, is_edge: bool, ident: int, name: str, cols, ver: int = 0):
+        names = (C.c_char_p * max(1, len(cols)))(*[c[0].encode() for c in cols])
+        types = (C.c_int32 * max(1, len(cols)))(*[c[1] for c in cols])
+        self.L.orc_register_schema(self.h, int(is_edge), ident, name.encode(), ver, len(cols), names, types)
+        if is_edge:
+            self.edge_types[name] = ident
+            self.edge_names[ident] = name
+        else:
+            self.tag_ids[name] = ident
+
+    def load_part(self, part, kd, ko, vd, vo, n):
+        self.L.orc_load_part_kv(self.h, part, _ptr(kd), _ptr(ko), _ptr(vd), _ptr(vo), n)
+
+    def load_builder(self, kb):
+        for p in sorted(kb.recs):
+            self.load_part(p, *kb.flat(p))
+        self.L.orc_finalize(self.h)
+
+    # ---------------------------------------------------------------- ngql backend API
+    def go(self, starts, etypes, steps, where=b"", yields=(), distinct=False, over_all=False):
+        s = np.asarray(starts, np.int64)
+        t = np.asarray(etypes, np.int32)
+        blob = b"".join(yields)
+        lens = np.asarray([len(y) for y in yields], np.uint32)
+        wb = np.frombuffer(where, np.uint8) if where else None
+        yb = np.frombuffer(blob, np.uint8) if blob else None
+        out = C.c_void_p()
+        self.L.orc_go(self.h, _ptr(s), len(s), _ptr(t), len(t), int(over_all), steps,
+                      _ptr(wb), len(where), _ptr(yb), _ptr(lens), len(yields), int(distinct),
+                      C.byref(out))
+        try:
+            code = self.L.orc_result_code(out)
+            if code:
+                raise OracleError(code, self.L.orc_result_error(out).decode())
+            nr, nc = self.L.orc_result_rows(out), self.L.orc_result_cols(out)
+            bits = np.zeros(max(1, nr * nc), np.int64)
+            types = np.zeros(max(1, nr * nc), np.uint8)
+            if nr:
+                self.L.orc_result_cells(out, _ptr(bits), _ptr(types))
+            rows = []
+            for r in range(nr):
+                row = []
+                for c in range(nc):
+                    k = r * nc + c
+                    t_ = types[k]
+                    b = int(bits[k])
+                    if t_ == 0:
+                        row.append(b)
+                    elif t_ == 1:
+                        row.append(struct.unpack("<d", struct.pack("<q", b))[0])
+                    elif t_ == 2:
+                        row.append(bool(b))
+                    else:
+                        row.append(self.L.orc_result_string(out, b).decode())
+                rows.append(row)
+            return rows
+        finally:
+            self.L.orc_result_free(out)
+
+    def find_path(self, frm, to, etypes, upto=5, shortest=True, mode=0, over_all=False):
+        f = np.asarray(frm, np.int64)
+        t = np.asarray(to, np.int64)
+        e = np.asarray(etypes, np.int32)
+        out = C.c_void_p()
+        self.L.orc_find_path(self.h, _ptr(f), len(f), _ptr(t), len(t), _ptr(e), len(e), int(over_all),
+                             upto, int(shortest), mode, C.byref(out))
+        try:
+            paths = []
+            for i in range(self.L.orc_paths_count(out)):
+                n = self.L.orc_path_len(out, i)
+                a = np.zeros(n, np.int64)
+                self.L.orc_path_get(out, i, _ptr(a))
+                paths.append([int(x) for x in a])
+            return paths
+        finally:
+            self.L.orc_result_free(out)
+
+    def go_timed(self, starts, etypes, steps, where=b""):
+        s = np.asarray(starts, np.int64)
+        t = np.asarray(etypes, np.int32)
+        wb = np.frombuffer(where, np.uint8) if where else None
+        rows, scanned = C.c_int64(), C.c_uint64()
+        sec = self.L.orc_go_timed(self.h, _ptr(s), len(s), _ptr(t), len(t), steps, _ptr(wb), len(where),
+                                  C.byref(rows), C.byref(scanned))
+        return sec, rows.value, scanned.value
+
+
+def nba_oracle(data, parts=1):
+    from nebula_amd import kvgen
+    o = Oracle(parts)
+    for (kind, name), cols in kvgen.NBA_SCHEMAS.items():
+        ident = kvgen.NBA_EDGES[name] if kind == "edge" else kvgen.NBA_TAGS[name]
+        o.register(kind == "edge", ident, name, cols)
+    o.load_builder(kvgen.nba_kv(data, parts))
+    return o
