@@ -1,0 +1,193 @@
+/*
+ * nbg.h — C ABI of nebula_amd, the MI355X-native multi-hop traversal engine for Nebula Graph's
+ * GO N STEPS / FIND PATH hot path.
+ *
+ * Plain C, no exceptions, no callbacks, no torch types.  Every entry point returns an int32_t
+ * status: 0 on success, otherwise a storage::cpp2::ErrorCode / graph::cpp2::ErrorCode value
+ * (src/interface/storage.thrift:13-44, graph.thrift:12-35) or one of the NBG_E_* codes below.
+ * The caller owns every input; outputs are allocated by the library and released with the
+ * matching *_free call.  Engines are immutable after nbg_finalize(); queries on one engine are
+ * serialised internally (one HIP stream per engine).
+ *
+ * Reference interfaces this ABI replaces (paths relative to the reference checkout):
+ *   nbg_create/…/nbg_finalize  ≙ the storaged data a kvstore part holds: NebulaStore parts
+ *       filled through AddEdgesProcessor / AddVerticesProcessor
+ *       (src/storage/AddEdgesProcessor.cpp:15-37, src/kvstore/NebulaStore.cpp:326-336)
+ *   nbg_get_neighbors          ≙ StorageServiceHandler::future_getBound → QueryBoundProcessor
+ *       (src/storage/StorageServiceHandler.cpp:33-40, src/storage/QueryBoundProcessor.cpp:16-220)
+ *   nbg_go / nbg_go_device     ≙ GoExecutor result semantics (src/graph/GoExecutor.cpp:83-984)
+ *   nbg_find_path              ≙ FindPathExecutor result semantics
+ *       (src/graph/FindPathExecutor.cpp:145-715)
+ */
+#ifndef NEBULA_AMD_NBG_H_
+#define NEBULA_AMD_NBG_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (storage.thrift ErrorCode / graph.thrift ErrorCode values) ---------- */
+#define NBG_OK                     0
+#define NBG_E_EXECUTION_ERROR     (-8)    /* graph E_EXECUTION_ERROR: eval error in WHERE/YIELD */
+#define NBG_E_PART_NOT_FOUND      (-14)
+#define NBG_E_EDGE_PROP_NOT_FOUND (-21)
+#define NBG_E_TAG_PROP_NOT_FOUND  (-22)
+#define NBG_E_IMPROPER_DATA_TYPE  (-23)
+#define NBG_E_INVALID_FILTER      (-31)
+#define NBG_E_UNKNOWN             (-100)
+/* nebula_amd specific */
+#define NBG_E_INVALID_ARGUMENT    (-1001)
+#define NBG_E_UNSUPPORTED         (-1002) /* valid nGQL, not implemented on the device path */
+#define NBG_E_DEVICE              (-1003) /* HIP runtime / kernel failure (message in last_error) */
+#define NBG_E_OUT_OF_MEMORY       (-1004)
+#define NBG_E_STATE               (-1005) /* e.g. query before nbg_finalize */
+
+/* ---- common.thrift SupportedType ------------------------------------------------------ */
+#define NBG_T_BOOL      1
+#define NBG_T_INT       2
+#define NBG_T_VID       3
+#define NBG_T_FLOAT     4
+#define NBG_T_DOUBLE    5
+#define NBG_T_STRING    6
+#define NBG_T_TIMESTAMP 7
+
+/* Value tags of result cells: VariantType alternatives (src/common/base/Base.h:140). */
+#define NBG_V_INT    0
+#define NBG_V_DOUBLE 1
+#define NBG_V_BOOL   2
+#define NBG_V_STRING 3
+
+typedef struct nbg_engine nbg_engine;
+typedef struct nbg_rows nbg_rows;
+typedef struct nbg_paths nbg_paths;
+
+typedef struct {
+  int32_t num_parts;     /* partition_num of the space: part = uint64(vid) % num_parts + 1   */
+  int32_t num_gpus;      /* G: part p is served by GPU rank p % G (CreateSpaceProcessor:84-95) */
+  int32_t rank;          /* this engine's GPU rank in [0, G)                                   */
+  int32_t device;        /* HIP device ordinal to use                                          */
+  int32_t max_edge_returned_per_vertex; /* FLAGS_max_edge_returned_per_vertex (INT32_MAX)       */
+  int32_t min_vertices_per_bucket;      /* accepted for flag parity; no device effect           */
+  int32_t max_handlers_per_req;         /* accepted for flag parity; no device effect           */
+} nbg_config;
+
+typedef struct {
+  const char* name;
+  int32_t type;          /* NBG_T_* */
+} nbg_column_def;
+
+/* ---- engine lifecycle ------------------------------------------------------------------ */
+int32_t nbg_create(const nbg_config* cfg, nbg_engine** out);
+void nbg_destroy(nbg_engine* e);
+/* Message of the last failing call on this engine (valid until the next call). */
+const char* nbg_last_error(const nbg_engine* e);
+
+/* Schemas (meta SchemaManager view, src/meta/SchemaManager.h:20-48). */
+int32_t nbg_register_tag(nbg_engine* e, int32_t tag_id, const char* name, int64_t schema_ver,
+                         const nbg_column_def* cols, int32_t ncols);
+int32_t nbg_register_edge(nbg_engine* e, int32_t edge_type, const char* name, int64_t schema_ver,
+                          const nbg_column_def* cols, int32_t ncols);
+
+/* Loader: KV records exactly as a kvstore part holds them — NebulaKeyUtils keys
+ * (src/common/base/NebulaKeyUtils.cpp:12-47) and RowWriter values (src/dataman/RowWriter.cpp).
+ * Record i is key_data[key_offs[i] .. key_offs[i+1]) / val_data[val_offs[i] .. val_offs[i+1]).
+ * Later records with an identical key overwrite earlier ones (write-batch semantics).
+ * Records of parts this rank does not serve (part % num_gpus != rank) are ignored. */
+int32_t nbg_load_part_kv(nbg_engine* e, int32_t part,
+                         const uint8_t* key_data, const uint64_t* key_offs,
+                         const uint8_t* val_data, const uint64_t* val_offs, uint64_t n);
+
+/* Bulk loader (SST-ingest analogue): n edges of one positive edge type, inserted the way
+ * InsertEdgeExecutor does (out-edge with props + in-edge (dst,-type,rank,src) with no props,
+ * src/graph/InsertEdgeExecutor.cpp:180-196), all with one version; a later duplicate
+ * (src,dst,rank) overwrites an earlier one.  prop_cols[c] points at n values of schema column c:
+ * int64 for INT/TIMESTAMP/VID, double for FLOAT/DOUBLE, uint8 for BOOL; STRING columns are not
+ * accepted here (use nbg_load_part_kv).  rank may be NULL (all 0). */
+int32_t nbg_load_edges(nbg_engine* e, int32_t edge_type, const int64_t* src, const int64_t* dst,
+                       const int64_t* rank, uint64_t n, const void* const* prop_cols, int32_t ncols);
+
+/* Build the device snapshot (version de-dup, CSR/CSC per edge type, SoA prop columns) and upload
+ * it to HBM.  Host-side staging is released afterwards. */
+int32_t nbg_finalize(nbg_engine* e);
+
+typedef struct {
+  uint64_t num_vertices;      /* vertices with at least one record in this rank's parts        */
+  uint64_t num_edges;         /* live (latest-version) edge records, all signed types          */
+  uint64_t device_bytes;      /* HBM held by the snapshot                                      */
+  int32_t num_edge_types;     /* signed edge types present                                     */
+  int32_t reserved;
+} nbg_stats;
+int32_t nbg_get_stats(const nbg_engine* e, nbg_stats* out);
+
+/* ---- GO N STEPS (GoExecutor semantics) ------------------------------------------------- */
+typedef struct {
+  const int64_t* starts;          /* FROM vids; duplicates are kept (GoExecutor.cpp:136-195)  */
+  uint64_t num_starts;
+  const int32_t* edge_types;      /* OVER list, positive types, in order                      */
+  int32_t num_edge_types;
+  int32_t over_all;               /* OVER *: every registered positive edge type               */
+  uint32_t steps;                 /* N >= 1                                                    */
+  const uint8_t* where;           /* Expression::encode bytes of WHERE; NULL/0 = none         */
+  uint32_t where_len;
+  const uint8_t* const* yields;   /* Expression::encode bytes per YIELD column; 0 = default    */
+  const uint32_t* yield_lens;     /*   (<edge>._dst per OVER edge, parser.yy:518-531)          */
+  int32_t num_yields;
+  int32_t distinct;               /* YIELD DISTINCT                                            */
+} nbg_go_request;
+
+/* Rows are copied to host memory. */
+int32_t nbg_go(nbg_engine* e, const nbg_go_request* req, nbg_rows** out);
+/* Rows stay in HBM (engine-owned buffers, valid until the next query on this engine or
+ * nbg_rows_free); nbg_rows_fetch() copies them to the host on demand. */
+int32_t nbg_go_device(nbg_engine* e, const nbg_go_request* req, nbg_rows** out);
+
+int64_t nbg_rows_count(const nbg_rows* r);
+int32_t nbg_rows_num_cols(const nbg_rows* r);
+/* Σ_s E_s: adjacency entries scanned over all steps (the TEPS numerator). */
+uint64_t nbg_rows_edges_scanned(const nbg_rows* r);
+/* Per-step counters: frontier size |F_s| and edges E_s, s = 1..steps (arrays of length steps). */
+int32_t nbg_rows_step_stats(const nbg_rows* r, uint64_t* frontier, uint64_t* edges, int32_t cap);
+int32_t nbg_rows_fetch(nbg_rows* r);
+/* Host views (after nbg_go, or after nbg_rows_fetch): 8-byte cell payloads (int64, double bits,
+ * bool as 0/1, string id) and value tags NBG_V_* per row. */
+const int64_t* nbg_rows_col_bits(const nbg_rows* r, int32_t col);
+const uint8_t* nbg_rows_col_tags(const nbg_rows* r, int32_t col);
+const char* nbg_rows_string(const nbg_rows* r, int64_t string_id);
+/* Device view of a column's 8-byte payloads (valid for nbg_go_device results). */
+const void* nbg_rows_device_col(const nbg_rows* r, int32_t col);
+void nbg_rows_free(nbg_rows* r);
+
+/* ---- FIND SHORTEST | ALL PATH (FindPathExecutor semantics) ----------------------------- */
+typedef struct {
+  const int64_t* from;            /* de-duplicated by the callee (VerticesClause::prepare)    */
+  uint64_t num_from;
+  const int32_t* edge_types;
+  int32_t num_edge_types;
+  int32_t over_all;
+  const int64_t* to;
+  uint64_t num_to;
+  uint32_t upto;                  /* UPTO N STEPS, default 5 (parser.yy:858-861)              */
+  int32_t shortest;               /* 1 = SHORTEST, 0 = ALL                                     */
+} nbg_path_request;
+
+/* Each path is an entry list [v0, t0, r0, v1, t1, r1, ..., vk] (vertex, edge type, ranking …)
+ * — the graph.thrift Path entry_list (graph.thrift:58-73) with edge names as types.
+ * SHORTEST returns at most one path per target: the minimum hop count, ties broken by the
+ * lexicographically smallest entry list (the reference's tie-break is iteration order). */
+int32_t nbg_find_path(nbg_engine* e, const nbg_path_request* req, nbg_paths** out);
+int64_t nbg_paths_count(const nbg_paths* p);
+int64_t nbg_path_len(const nbg_paths* p, int64_t i);
+const int64_t* nbg_path_entries(const nbg_paths* p, int64_t i);
+void nbg_paths_free(nbg_paths* p);
+
+/* ---- multi-GPU (one process per GPU, RCCL over xGMI) ----------------------------------- */
+#define NBG_UNIQUE_ID_BYTES 128
+int32_t nbg_comm_unique_id(uint8_t out[NBG_UNIQUE_ID_BYTES]);
+int32_t nbg_comm_init(nbg_engine* e, const uint8_t id[NBG_UNIQUE_ID_BYTES], int32_t world, int32_t rank);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NEBULA_AMD_NBG_H_ */

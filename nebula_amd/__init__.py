@@ -1,0 +1,9 @@
+"""nebula_amd — MI355X-native GO N STEPS / FIND PATH engine for Nebula Graph's traversal path.
+
+The product is the C ABI in ``include/nbg.h`` implemented by ``nebula_amd/libnbg.so``
+(host C++ + gfx950 HIP kernels).  This package is the Python host binding plus fixture
+tooling (KV record builders, an nGQL front end for GO / FIND PATH).
+"""
+from .engine import Engine, NbgError, DeviceRows, nba_engine  # noqa: F401
+
+__all__ = ["Engine", "NbgError", "DeviceRows", "nba_engine"]

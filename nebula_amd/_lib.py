@@ -1,0 +1,105 @@
+"""ctypes declarations of include/nbg.h (the product's C ABI).
+
+The shared library is built in-tree (``nebula_amd/libnbg.so``, see ``__graft_entry__.build``).
+There is no fallback: if the library is missing, importing the engine fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("NBG_LIB", os.path.join(HERE, "libnbg.so"))
+
+vp, i32, i64, u32, u64, u8 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_uint64, C.c_uint8
+P = C.POINTER
+
+# status codes (nbg.h)
+OK = 0
+E_EXECUTION_ERROR = -8
+E_PART_NOT_FOUND = -14
+E_EDGE_PROP_NOT_FOUND = -21
+E_TAG_PROP_NOT_FOUND = -22
+E_IMPROPER_DATA_TYPE = -23
+E_INVALID_FILTER = -31
+E_UNKNOWN = -100
+E_INVALID_ARGUMENT = -1001
+E_UNSUPPORTED = -1002
+E_DEVICE = -1003
+E_OUT_OF_MEMORY = -1004
+E_STATE = -1005
+
+
+class nbg_config(C.Structure):
+    _fields_ = [("num_parts", i32), ("num_gpus", i32), ("rank", i32), ("device", i32),
+                ("max_edge_returned_per_vertex", i32), ("min_vertices_per_bucket", i32),
+                ("max_handlers_per_req", i32)]
+
+
+class nbg_column_def(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("type", i32)]
+
+
+class nbg_stats(C.Structure):
+    _fields_ = [("num_vertices", u64), ("num_edges", u64), ("device_bytes", u64),
+                ("num_edge_types", i32), ("reserved", i32)]
+
+
+class nbg_go_request(C.Structure):
+    _fields_ = [("starts", P(i64)), ("num_starts", u64), ("edge_types", P(i32)), ("num_edge_types", i32),
+                ("over_all", i32), ("steps", u32), ("where", P(u8)), ("where_len", u32),
+                ("yields", P(P(u8))), ("yield_lens", P(u32)), ("num_yields", i32), ("distinct", i32)]
+
+
+class nbg_path_request(C.Structure):
+    _fields_ = [("from_", P(i64)), ("num_from", u64), ("edge_types", P(i32)), ("num_edge_types", i32),
+                ("over_all", i32), ("to", P(i64)), ("num_to", u64), ("upto", u32), ("shortest", i32)]
+
+
+# (name, restype, argtypes) for every symbol include/nbg.h declares
+SIGNATURES = [
+    ("nbg_create", i32, [P(nbg_config), P(vp)]),
+    ("nbg_destroy", None, [vp]),
+    ("nbg_last_error", C.c_char_p, [vp]),
+    ("nbg_register_tag", i32, [vp, i32, C.c_char_p, i64, P(nbg_column_def), i32]),
+    ("nbg_register_edge", i32, [vp, i32, C.c_char_p, i64, P(nbg_column_def), i32]),
+    ("nbg_load_part_kv", i32, [vp, i32, vp, vp, vp, vp, u64]),
+    ("nbg_load_edges", i32, [vp, i32, vp, vp, vp, u64, P(vp), i32]),
+    ("nbg_finalize", i32, [vp]),
+    ("nbg_get_stats", i32, [vp, P(nbg_stats)]),
+    ("nbg_go", i32, [vp, P(nbg_go_request), P(vp)]),
+    ("nbg_go_device", i32, [vp, P(nbg_go_request), P(vp)]),
+    ("nbg_rows_count", i64, [vp]),
+    ("nbg_rows_num_cols", i32, [vp]),
+    ("nbg_rows_edges_scanned", u64, [vp]),
+    ("nbg_rows_step_stats", i32, [vp, P(u64), P(u64), i32]),
+    ("nbg_rows_fetch", i32, [vp]),
+    ("nbg_rows_col_bits", P(i64), [vp, i32]),
+    ("nbg_rows_col_tags", P(u8), [vp, i32]),
+    ("nbg_rows_string", C.c_char_p, [vp, i64]),
+    ("nbg_rows_device_col", vp, [vp, i32]),
+    ("nbg_rows_free", None, [vp]),
+    ("nbg_find_path", i32, [vp, P(nbg_path_request), P(vp)]),
+    ("nbg_paths_count", i64, [vp]),
+    ("nbg_path_len", i64, [vp, i64]),
+    ("nbg_path_entries", P(i64), [vp, i64]),
+    ("nbg_paths_free", None, [vp]),
+    ("nbg_comm_unique_id", i32, [P(u8)]),
+    ("nbg_comm_init", i32, [vp, P(u8), i32, i32]),
+]
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"nebula_amd native library not built: {LIB_PATH} (run __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib

@@ -1,0 +1,496 @@
+// C ABI implementation (include/nbg.h) and the GO N STEPS driver.
+//
+// GO N STEPS follows GoExecutor (src/graph/GoExecutor.cpp):
+//   * starts keep duplicates (prepareFrom :136-195); unknown vids contribute nothing;
+//   * steps 1..N-1: frontier_{s+1} = SET of _dst over every live edge of every OVER type
+//     (getDstIdsFromResp :501-541) — no global visited set; empty frontier -> empty result
+//     (onEmptyInputs :791-800);
+//   * step N: one row per (frontier entry, live edge) passing WHERE; WHERE/YIELD evaluation
+//     errors fail the query (processFinalResult :948-969).
+// Each hop runs on the device: degree scan -> merge-path partition -> expand (+ byte-flag
+// dedup and compaction, or the final-step bytecode + row compaction).
+#include <algorithm>
+#include <cstring>
+
+#include "engine.h"
+
+using namespace nbg;
+
+namespace nbg {
+
+uint32_t Engine::dense(int64_t vid) const {
+  auto& v = snap.h_vids;
+  auto it = std::lower_bound(v.begin(), v.end(), vid);
+  return (it != v.end() && *it == vid) ? (uint32_t)(it - v.begin()) : NO_ROW;
+}
+
+}  // namespace nbg
+
+// ============================================================================= result objects
+struct nbg_rows {
+  struct Seg {
+    uint64_t begin = 0, end = 0;
+    std::vector<VKind> kinds;
+    std::vector<std::string> const_str;   // string constants absent from the dictionary
+  };
+  Engine* eng = nullptr;
+  int ncols = 0;
+  uint64_t count = 0;
+  bool on_device = false;
+  bool fetched = false;
+  std::vector<int64_t*> dcols;
+  std::vector<std::vector<int64_t>> bits;
+  std::vector<std::vector<uint8_t>> tags;
+  std::vector<std::string> strings;
+  std::vector<Seg> segs;
+  uint64_t scanned = 0;
+  std::vector<uint64_t> step_frontier, step_edges;
+};
+
+struct nbg_paths {
+  std::vector<std::vector<int64_t>> paths;
+};
+
+namespace {
+
+int32_t materialize_rows(nbg_rows* r) {
+  if (r->fetched) return NBG_OK;
+  const auto& dict = r->eng->snap.strings;
+  r->bits.assign(r->ncols, std::vector<int64_t>(r->count));
+  r->tags.assign(r->ncols, std::vector<uint8_t>(r->count));
+  for (int c = 0; c < r->ncols; ++c) {
+    if (r->count && hipMemcpy(r->bits[c].data(), r->dcols[c], r->count * 8, hipMemcpyDeviceToHost) != hipSuccess)
+      return NBG_E_DEVICE;
+  }
+  std::unordered_map<int64_t, int64_t> sidx;
+  for (auto& s : r->segs) {
+    for (int c = 0; c < r->ncols; ++c) {
+      VKind k = s.kinds[c];
+      for (uint64_t i = s.begin; i < s.end; ++i) {
+        r->tags[c][i] = (uint8_t)k;
+        if (k == VK_STRING) {
+          int64_t code = r->bits[c][i];
+          auto it = sidx.find(code);
+          if (it == sidx.end()) {
+            std::string txt = (code >= 0 && (code & 1) == 0 && (uint64_t)(code / 2) < dict.size())
+                                  ? dict[code / 2] : s.const_str[c];
+            it = sidx.emplace(code, (int64_t)r->strings.size()).first;
+            r->strings.push_back(txt);
+          }
+          r->bits[c][i] = it->second;
+        }
+      }
+    }
+  }
+  r->fetched = true;
+  return NBG_OK;
+}
+
+const char* kGoUnsupportedDistinct = "YIELD DISTINCT is not supported on the device path yet";
+
+}  // namespace
+
+// ============================================================================= GO driver
+static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_rows** out) {
+  if (!rq || !out) return E.fail(NBG_E_INVALID_ARGUMENT, "null argument");
+  *out = nullptr;
+  std::lock_guard<std::mutex> lg(E.mu);
+  if (!E.finalized) return E.fail(NBG_E_STATE, "engine not finalized");
+  if (rq->steps < 1) return E.fail(NBG_E_INVALID_ARGUMENT, "steps must be >= 1");
+  // OVER (prepareOver / prepareOverAll, GoExecutor.cpp:197-263)
+  std::vector<int32_t> over;
+  if (rq->over_all) {
+    for (auto& kv : E.edges) over.push_back(kv.first);
+  } else {
+    for (int32_t i = 0; i < rq->num_edge_types; ++i) {
+      int32_t t = rq->edge_types[i];
+      if (t <= 0) return E.fail(NBG_E_EXECUTION_ERROR, "`REVERSELY' not supported yet");
+      if (!E.edges.count(t)) return E.fail(NBG_E_EXECUTION_ERROR, "edge type not found");
+      over.push_back(t);
+    }
+  }
+  if (over.empty()) return E.fail(NBG_E_EXECUTION_ERROR, "empty OVER clause");
+  if (rq->distinct) return E.fail(NBG_E_UNSUPPORTED, kGoUnsupportedDistinct);
+  // WHERE / YIELD
+  std::string err;
+  std::unique_ptr<Node> where;
+  if (rq->where && rq->where_len) {
+    where = decode_expr(rq->where, rq->where_len, &err);
+    if (!where) return E.fail(NBG_E_INVALID_ARGUMENT, "WHERE: " + err);
+  }
+  std::vector<std::unique_ptr<Node>> yields;
+  for (int32_t i = 0; i < rq->num_yields; ++i) {
+    auto y = decode_expr(rq->yields[i], rq->yield_lens[i], &err);
+    if (!y) return E.fail(NBG_E_INVALID_ARGUMENT, "YIELD: " + err);
+    yields.push_back(std::move(y));
+  }
+  if (yields.empty()) {   // default YIELD <edge>._dst per OVER edge (parser.yy:518-531)
+    for (int32_t t : over) {
+      auto n = std::make_unique<Node>();
+      n->kind = EK_DST;
+      n->alias = E.edges[t].name;
+      n->prop = "_dst";
+      yields.push_back(std::move(n));
+    }
+  }
+  if ((int)yields.size() > MAX_YIELDS) return E.fail(NBG_E_UNSUPPORTED, "too many YIELD columns");
+  const int ncols = (int)yields.size();
+  // compile per OVER type; name-resolution errors are reported only if the final step runs
+  std::map<int32_t, TypeProgram> progs;
+  int32_t deferred = NBG_OK;
+  std::string deferred_msg;
+  for (int32_t t : over) {
+    auto it = E.snap.types.find(t);
+    CompileEnv env{t, &over, &E.edges, &E.snap.strings,
+                   it != E.snap.types.end() && it->second.valid != nullptr,
+                   it != E.snap.types.end() && it->second.rank != nullptr};
+    ProgramBuilder pb;
+    TypeProgram tp;
+    tp.etype = t;
+    int32_t rc = NBG_OK;
+    if (where) {
+      Compiled c;
+      rc = compile_expr(*where, env, pb, &c, &err);
+      if (rc == NBG_OK) {
+        tp.where_len = (int)pb.code.size();
+        if (c.is_const) {
+          bool tv;
+          switch (c.kind) {
+            case VK_STRING: tv = c.const_str.empty(); break;
+            case VK_DOUBLE: { double d; memcpy(&d, &c.const_bits, 8); tv = d != 0.0; break; }
+            default: tv = c.const_bits != 0;
+          }
+          tp.where_const = true;
+          tp.where_const_val = tv;
+          tp.where_len = 0;
+          pb.code.clear();
+        } else {
+          // asBool of the WHERE value (GoExecutor.cpp:954)
+          int r = c.reg;
+          if (c.kind == VK_INT) pb.code.push_back(Ins{OP_TRUTHY_I, (uint8_t)r, (uint8_t)r, 0, 0, 0});
+          else if (c.kind == VK_DOUBLE) pb.code.push_back(Ins{OP_TRUTHY_F, (uint8_t)r, (uint8_t)r, 0, 0, 0});
+          else if (c.kind == VK_STRING)
+            pb.code.push_back(Ins{OP_TRUTHY_S, (uint8_t)r, (uint8_t)r, 0, 0, string_code(E.snap.strings, "")});
+          tp.where_len = (int)pb.code.size();
+          tp.where_reg = r;
+          tp.where_always_error = c.always_error;
+        }
+        pb.next_reg = 0;   // WHERE registers are dead once its value is read
+      }
+    }
+    for (int y = 0; rc == NBG_OK && y < ncols; ++y) {
+      Compiled c;
+      rc = compile_expr(*yields[y], env, pb, &c, &err);
+      if (rc) break;
+      tp.yield_kind.push_back(c.kind);
+      if (c.is_const) {
+        tp.yield_reg.push_back(-1);
+        tp.yield_const.push_back(c.const_bits);
+        tp.yield_const_str.push_back(c.const_str);
+      } else {
+        tp.yield_const_str.push_back(std::string());
+        tp.yield_reg.push_back(c.reg);
+        tp.yield_const.push_back(0);
+      }
+    }
+    if (rc == NBG_E_UNSUPPORTED || rc == NBG_E_INVALID_ARGUMENT) return E.fail(rc, err);
+    if (rc) {
+      if (!deferred) { deferred = rc; deferred_msg = err; }
+      continue;
+    }
+    tp.code = pb.code;
+    tp.nregs = std::max(1, pb.max_reg);
+    if ((int)tp.code.size() > MAX_PROGRAM) return E.fail(NBG_E_UNSUPPORTED, "program too long");
+    progs[t] = std::move(tp);
+  }
+  // starts -> dense ids (duplicates kept)
+  std::vector<uint32_t> f0;
+  f0.reserve(rq->num_starts);
+  for (uint64_t i = 0; i < rq->num_starts; ++i) {
+    uint32_t d = E.dense(rq->starts[i]);
+    if (d != NO_ROW) f0.push_back(d);
+  }
+  auto* rows = new nbg_rows();
+  rows->eng = &E;
+  rows->ncols = ncols;
+  rows->on_device = device;
+  auto finish_empty = [&]() {
+    *out = rows;
+    return NBG_OK;
+  };
+  if (f0.empty()) return finish_empty();
+  if (f0.size() > E.snap.nv + 1024) {
+    // recreate the workspace with room for the duplicated start list
+    ws_destroy(E.ws);
+    E.ws = ws_create(f0.size(), E.snap.nv, E.stream, &err);
+    if (!E.ws) { delete rows; return E.fail(NBG_E_OUT_OF_MEMORY, err); }
+  }
+  Workspace* ws = E.ws;
+  int cur = 0;
+  if (hipMemcpyAsync(ws_frontier(ws, 0), f0.data(), f0.size() * 4, hipMemcpyHostToDevice, E.stream) != hipSuccess) {
+    delete rows;
+    return E.fail(NBG_E_DEVICE, "frontier upload failed");
+  }
+  uint64_t n = f0.size();
+  const uint32_t cap = (uint32_t)(E.cfg.max_edge_returned_per_vertex <= 0 ? 0x7fffffff
+                                                                          : E.cfg.max_edge_returned_per_vertex);
+  auto args_for = [&](int32_t t, const DevEdgeType& dt) {
+    ExpandArgs a{};
+    a.frontier = ws_frontier(ws, cur);
+    a.n = n;
+    a.row_ptr = dt.row_ptr;
+    a.col = dt.col;
+    a.dst_vid = dt.dst_vid;
+    a.rank = dt.rank;
+    a.valid = dt.valid;
+    a.visible = E.snap.d_visible;
+    a.vids = E.snap.d_vids;
+    a.props = dt.d_props;
+    a.cap = cap;
+    (void)t;
+    return a;
+  };
+  hipError_t he = hipSuccess;
+  for (uint32_t s = 1; s <= rq->steps; ++s) {
+    const bool final = s == rq->steps;
+    rows->step_frontier.push_back(n);
+    uint64_t step_edges = 0;
+    if (!final) {
+      for (int32_t t : over) {
+        auto it = E.snap.types.find(t);
+        if (it == E.snap.types.end()) continue;
+        ExpandArgs a = args_for(t, it->second);
+        uint64_t total = 0;
+        if ((he = k_degree_scan(ws, a, &total)) != hipSuccess) break;
+        step_edges += total;
+        if ((he = k_expand_mark(ws, a, total)) != hipSuccess) break;
+      }
+      if (he != hipSuccess) break;
+      rows->step_edges.push_back(step_edges);
+      rows->scanned += step_edges;
+      uint64_t nn = 0;
+      if ((he = k_compact(ws, E.snap.nv, ws_frontier(ws, cur ^ 1), &nn)) != hipSuccess) break;
+      cur ^= 1;
+      n = nn;
+      if (n == 0) return finish_empty();
+      continue;
+    }
+    if (deferred) { delete rows; return E.fail(deferred, deferred_msg); }
+    // final step: rows for every OVER type
+    uint64_t cap_rows = 0;
+    for (int32_t t : over) {
+      auto it = E.snap.types.find(t);
+      if (it != E.snap.types.end()) cap_rows += it->second.num_edges;
+    }
+    if ((he = ws_reserve_rows(ws, cap_rows, ncols)) != hipSuccess) break;
+    uint64_t row_base = 0;
+    bool error = false;
+    for (int32_t t : over) {
+      auto it = E.snap.types.find(t);
+      if (it == E.snap.types.end()) continue;
+      const TypeProgram& tp = progs[t];
+      ExpandArgs a = args_for(t, it->second);
+      uint64_t total = 0;
+      if ((he = k_degree_scan(ws, a, &total)) != hipSuccess) break;
+      step_edges += total;
+      if (total == 0 || (tp.where_const && !tp.where_const_val)) continue;
+      if (!tp.code.empty() &&
+          (he = hipMemcpyAsync(ws_program(ws), tp.code.data(), tp.code.size() * sizeof(Ins), hipMemcpyHostToDevice,
+                               E.stream)) != hipSuccess)
+        break;
+      uint64_t nrows = 0;
+      int eflag = 0;
+      if ((he = k_expand_final(ws, a, total, tp, ws_program(ws), ws_row_cols(ws), row_base, &nrows, &eflag)) !=
+          hipSuccess)
+        break;
+      if (eflag) { error = true; break; }
+      nbg_rows::Seg seg;
+      seg.begin = row_base;
+      seg.end = row_base + nrows;
+      seg.kinds = tp.yield_kind;
+      seg.const_str = tp.yield_const_str;
+      row_base += nrows;
+      rows->segs.push_back(std::move(seg));
+    }
+    if (he != hipSuccess) break;
+    rows->step_edges.push_back(step_edges);
+    rows->scanned += step_edges;
+    if (error) { delete rows; return E.fail(NBG_E_EXECUTION_ERROR, "WHERE/YIELD evaluation error"); }
+    rows->count = row_base;
+    for (int c = 0; c < ncols; ++c) rows->dcols.push_back(ws_row_col(ws, c));
+  }
+  if (he != hipSuccess) {
+    delete rows;
+    return E.fail(NBG_E_DEVICE, std::string("HIP: ") + hipGetErrorString(he));
+  }
+  if (!device) {
+    int32_t rc = materialize_rows(rows);
+    if (rc) { delete rows; return E.fail(rc, "row fetch failed"); }
+  }
+  *out = rows;
+  return NBG_OK;
+}
+
+// ============================================================================= C ABI
+extern "C" {
+
+int32_t nbg_create(const nbg_config* cfg, nbg_engine** out) {
+  if (!cfg || !out) return NBG_E_INVALID_ARGUMENT;
+  if (cfg->num_parts <= 0 || cfg->num_gpus <= 0 || cfg->rank < 0 || cfg->rank >= cfg->num_gpus)
+    return NBG_E_INVALID_ARGUMENT;
+  auto* h = new nbg_engine();
+  h->e.cfg = *cfg;
+  if (h->e.cfg.max_edge_returned_per_vertex <= 0) h->e.cfg.max_edge_returned_per_vertex = 0x7fffffff;
+  *out = h;
+  return NBG_OK;
+}
+
+void nbg_destroy(nbg_engine* h) {
+  if (!h) return;
+  Engine& E = h->e;
+  if (E.ws) ws_destroy(E.ws);
+  for (auto& kv : E.snap.types) {
+    auto& d = kv.second;
+    for (void* p : {(void*)d.row_ptr, (void*)d.col, (void*)d.dst_vid, (void*)d.rank, (void*)d.valid,
+                    (void*)d.d_props})
+      if (p) (void)hipFree(p);
+    for (auto* p : d.props)
+      if (p) (void)hipFree(p);
+  }
+  if (E.snap.d_vids) (void)hipFree(E.snap.d_vids);
+  if (E.snap.d_visible) (void)hipFree(E.snap.d_visible);
+  if (E.stream) (void)hipStreamDestroy(E.stream);
+  delete h;
+}
+
+const char* nbg_last_error(const nbg_engine* h) { return h ? h->e.last_error.c_str() : "null engine"; }
+
+static int32_t reg_schema(std::map<int32_t, SchemaSet>& m, int32_t id, const char* name, int64_t ver,
+                          const nbg_column_def* cols, int32_t ncols) {
+  if (!name || ncols < 0 || (ncols && !cols)) return NBG_E_INVALID_ARGUMENT;
+  SchemaSet& ss = m[id];
+  ss.name = name;
+  Schema s;
+  s.version = ver;
+  for (int32_t i = 0; i < ncols; ++i) {
+    if (!cols[i].name) return NBG_E_INVALID_ARGUMENT;
+    s.cols.push_back(Column{cols[i].name, cols[i].type});
+  }
+  ss.versions[ver] = s;
+  return NBG_OK;
+}
+
+int32_t nbg_register_tag(nbg_engine* h, int32_t tag_id, const char* name, int64_t ver, const nbg_column_def* cols,
+                         int32_t ncols) {
+  if (!h) return NBG_E_INVALID_ARGUMENT;
+  if (h->e.finalized) return h->e.fail(NBG_E_STATE, "engine already finalized");
+  return reg_schema(h->e.tags, tag_id, name, ver, cols, ncols);
+}
+
+int32_t nbg_register_edge(nbg_engine* h, int32_t edge_type, const char* name, int64_t ver,
+                          const nbg_column_def* cols, int32_t ncols) {
+  if (!h) return NBG_E_INVALID_ARGUMENT;
+  if (h->e.finalized) return h->e.fail(NBG_E_STATE, "engine already finalized");
+  if (edge_type <= 0) return h->e.fail(NBG_E_INVALID_ARGUMENT, "edge types are positive");
+  return reg_schema(h->e.edges, edge_type, name, ver, cols, ncols);
+}
+
+int32_t nbg_load_part_kv(nbg_engine* h, int32_t part, const uint8_t* kd, const uint64_t* ko, const uint8_t* vd,
+                         const uint64_t* vo, uint64_t n) {
+  if (!h || (n && (!kd || !ko || !vd || !vo))) return NBG_E_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lg(h->e.mu);
+  return h->e.load_part_kv(part, kd, ko, vd, vo, n);
+}
+
+int32_t nbg_load_edges(nbg_engine* h, int32_t edge_type, const int64_t* src, const int64_t* dst, const int64_t* rank,
+                       uint64_t n, const void* const* prop_cols, int32_t ncols) {
+  if (!h || (n && (!src || !dst)) || (ncols && !prop_cols)) return NBG_E_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lg(h->e.mu);
+  return h->e.load_edges(edge_type, src, dst, rank, n, prop_cols, ncols);
+}
+
+int32_t nbg_finalize(nbg_engine* h) {
+  if (!h) return NBG_E_INVALID_ARGUMENT;
+  Engine& E = h->e;
+  std::lock_guard<std::mutex> lg(E.mu);
+  if (hipSetDevice(E.cfg.device) != hipSuccess) return E.fail(NBG_E_DEVICE, "hipSetDevice failed");
+  if (!E.stream && hipStreamCreateWithFlags(&E.stream, hipStreamNonBlocking) != hipSuccess)
+    return E.fail(NBG_E_DEVICE, "hipStreamCreate failed");
+  int32_t rc = E.finalize();
+  if (rc) return rc;
+  std::string err;
+  E.ws = ws_create(E.snap.nv + 1024, E.snap.nv, E.stream, &err);
+  if (!E.ws) return E.fail(NBG_E_OUT_OF_MEMORY, err);
+  return NBG_OK;
+}
+
+int32_t nbg_get_stats(const nbg_engine* h, nbg_stats* out) {
+  if (!h || !out) return NBG_E_INVALID_ARGUMENT;
+  const Engine& E = h->e;
+  memset(out, 0, sizeof(*out));
+  out->num_vertices = E.snap.nv;
+  for (auto& kv : E.snap.types) out->num_edges += kv.second.num_edges;
+  out->device_bytes = E.snap.device_bytes;
+  out->num_edge_types = (int32_t)E.snap.types.size();
+  return NBG_OK;
+}
+
+int32_t nbg_go(nbg_engine* h, const nbg_go_request* req, nbg_rows** out) {
+  if (!h) return NBG_E_INVALID_ARGUMENT;
+  return go_impl(h->e, req, false, out);
+}
+
+int32_t nbg_go_device(nbg_engine* h, const nbg_go_request* req, nbg_rows** out) {
+  if (!h) return NBG_E_INVALID_ARGUMENT;
+  return go_impl(h->e, req, true, out);
+}
+
+int64_t nbg_rows_count(const nbg_rows* r) { return r ? (int64_t)r->count : -1; }
+int32_t nbg_rows_num_cols(const nbg_rows* r) { return r ? r->ncols : -1; }
+uint64_t nbg_rows_edges_scanned(const nbg_rows* r) { return r ? r->scanned : 0; }
+
+int32_t nbg_rows_step_stats(const nbg_rows* r, uint64_t* frontier, uint64_t* edges, int32_t cap) {
+  if (!r) return NBG_E_INVALID_ARGUMENT;
+  int32_t k = 0;
+  for (; k < cap && k < (int32_t)r->step_frontier.size(); ++k) {
+    if (frontier) frontier[k] = r->step_frontier[k];
+    if (edges) edges[k] = k < (int32_t)r->step_edges.size() ? r->step_edges[k] : 0;
+  }
+  return k;
+}
+
+int32_t nbg_rows_fetch(nbg_rows* r) {
+  if (!r) return NBG_E_INVALID_ARGUMENT;
+  return materialize_rows(r);
+}
+
+const int64_t* nbg_rows_col_bits(const nbg_rows* r, int32_t col) {
+  if (!r || !r->fetched || col < 0 || col >= r->ncols) return nullptr;
+  return r->bits[col].data();
+}
+const uint8_t* nbg_rows_col_tags(const nbg_rows* r, int32_t col) {
+  if (!r || !r->fetched || col < 0 || col >= r->ncols) return nullptr;
+  return r->tags[col].data();
+}
+const char* nbg_rows_string(const nbg_rows* r, int64_t id) {
+  if (!r || id < 0 || id >= (int64_t)r->strings.size()) return nullptr;
+  return r->strings[id].c_str();
+}
+const void* nbg_rows_device_col(const nbg_rows* r, int32_t col) {
+  if (!r || col < 0 || col >= (int32_t)r->dcols.size()) return nullptr;
+  return r->dcols[col];
+}
+void nbg_rows_free(nbg_rows* r) { delete r; }
+
+int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* req, nbg_paths** out);
+
+int64_t nbg_paths_count(const nbg_paths* p) { return p ? (int64_t)p->paths.size() : -1; }
+int64_t nbg_path_len(const nbg_paths* p, int64_t i) {
+  return (p && i >= 0 && i < (int64_t)p->paths.size()) ? (int64_t)p->paths[i].size() : -1;
+}
+const int64_t* nbg_path_entries(const nbg_paths* p, int64_t i) {
+  return (p && i >= 0 && i < (int64_t)p->paths.size()) ? p->paths[i].data() : nullptr;
+}
+void nbg_paths_free(nbg_paths* p) { delete p; }
+
+}  // extern "C"

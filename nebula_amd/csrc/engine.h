@@ -1,0 +1,52 @@
+// Engine object behind the C ABI.
+#pragma once
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "exprc.h"
+#include "nbg_internal.h"
+
+namespace nbg {
+
+struct Engine {
+  nbg_config cfg{};
+  std::string last_error;
+  std::map<int32_t, SchemaSet> edges;   // positive edge types
+  std::map<int32_t, SchemaSet> tags;
+  // staging (until finalize)
+  std::map<int32_t, EdgeStage> stage;   // signed type -> records
+  std::vector<std::pair<int64_t, int32_t>> tag_vertices;
+  std::vector<std::string> pool;        // string props, load order
+  std::unordered_map<std::string, int64_t> pool_index;
+  uint64_t seq = 0;
+  bool finalized = false;
+  // device
+  Snapshot snap;
+  hipStream_t stream = nullptr;
+  Workspace* ws = nullptr;
+  std::mutex mu;
+  // multi-GPU
+  void* comm = nullptr;
+  int32_t world = 1;
+
+  int32_t fail(int32_t code, const std::string& msg) {
+    last_error = msg;
+    return code;
+  }
+  int64_t intern(const std::string& s);
+  bool decode_row(const SchemaSet& ss, const uint8_t* v, size_t n, int64_t* out);
+  int32_t load_part_kv(int32_t part, const uint8_t* kd, const uint64_t* ko, const uint8_t* vd, const uint64_t* vo,
+                       uint64_t n);
+  int32_t load_edges(int32_t type, const int64_t* src, const int64_t* dst, const int64_t* rank, uint64_t n,
+                     const void* const* cols, int32_t ncols);
+  int32_t finalize();
+  uint32_t dense(int64_t vid) const;
+};
+
+}  // namespace nbg
+
+struct nbg_engine {
+  nbg::Engine e;
+};

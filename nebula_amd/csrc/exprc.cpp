@@ -1,0 +1,597 @@
+// Expression wire decoding + static typing + constant folding + bytecode emission.
+//
+// The reference evaluates WHERE / YIELD by walking an Expression tree of VariantType values
+// per edge (src/common/filter/Expressions.cpp:133-1131, GoExecutor.cpp:803-984).  On the
+// device every leaf has a static type (schema column types, key props, literals), so each
+// node's VariantType alternative is known per OVER edge type and the tree compiles to typed
+// 3-address code.  Type errors the reference raises at run time become statically known
+// "always error" nodes (OP_ERR): they still fail the query exactly when the reference would,
+// i.e. when at least one row evaluates them.  Integer /0 and INT64_MIN/-1 (undefined
+// behaviour in the reference) are defined as evaluation errors.
+#include "exprc.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+namespace nbg {
+
+// ============================================================================= decode
+namespace {
+struct Rd {
+  const uint8_t* p;
+  const uint8_t* e;
+  bool ok = true;
+  bool need(size_t n) { if (p + n > e) ok = false; return ok; }
+  uint8_t u8() { if (!need(1)) return 0; return *p++; }
+  std::string s16() {
+    if (!need(2)) return {};
+    uint16_t n; memcpy(&n, p, 2); p += 2;
+    if (!need(n)) return {};
+    std::string s(reinterpret_cast<const char*>(p), n);
+    p += n;
+    return s;
+  }
+};
+
+std::unique_ptr<Node> dec(Rd& r, int depth) {
+  if (depth > 64) { r.ok = false; return nullptr; }
+  uint8_t k = r.u8();
+  if (!r.ok) return nullptr;
+  auto n = std::make_unique<Node>();
+  n->kind = static_cast<EKind>(k);
+  switch (k) {
+    case EK_PRIMARY: {
+      uint8_t which = r.u8();
+      if (which == 0) { if (!r.need(8)) return nullptr; int64_t v; memcpy(&v, r.p, 8); r.p += 8; n->prim = v; }
+      else if (which == 1) { if (!r.need(8)) return nullptr; double v; memcpy(&v, r.p, 8); r.p += 8; n->prim = v; }
+      else if (which == 2) { n->prim = r.u8() != 0; }
+      else if (which == 3) { n->prim = r.s16(); }
+      else return nullptr;
+      break;
+    }
+    case EK_UNARY: case EK_CAST:
+      n->op = r.u8();
+      n->kids.push_back(dec(r, depth + 1));
+      if (!n->kids[0]) return nullptr;
+      break;
+    case EK_ARITH: case EK_REL: case EK_LOGIC:
+      n->op = r.u8();
+      for (int i = 0; i < 2; ++i) {
+        n->kids.push_back(dec(r, depth + 1));
+        if (!n->kids.back()) return nullptr;
+      }
+      break;
+    case EK_FUNC: {
+      n->alias = r.s16();
+      if (!r.need(2)) return nullptr;
+      uint16_t c; memcpy(&c, r.p, 2); r.p += 2;
+      for (uint16_t i = 0; i < c; ++i) {
+        n->kids.push_back(dec(r, depth + 1));
+        if (!n->kids.back()) return nullptr;
+      }
+      break;
+    }
+    case EK_SRCPROP: case EK_ALIAS: case EK_VAR: case EK_DSTPROP:
+      n->alias = r.s16();
+      n->prop = r.s16();
+      break;
+    case EK_INPUT:
+      n->prop = r.s16();
+      break;
+    case EK_RANK: case EK_DST: case EK_SRCID: case EK_TYPE:
+      n->alias = r.s16();
+      n->prop = k == EK_RANK ? "_rank" : k == EK_DST ? "_dst" : k == EK_SRCID ? "_src" : "_type";
+      break;
+    default:
+      return nullptr;
+  }
+  return r.ok ? std::move(n) : nullptr;
+}
+}  // namespace
+
+std::unique_ptr<Node> decode_expr(const uint8_t* p, size_t n, std::string* err) {
+  Rd r{p, p + n};
+  auto e = dec(r, 0);
+  if (!e || !r.ok || r.p != r.e) {
+    if (err) *err = "malformed expression bytes";
+    return nullptr;
+  }
+  return e;
+}
+
+int64_t string_code(const std::vector<std::string>& dict, const std::string& s) {
+  auto it = std::lower_bound(dict.begin(), dict.end(), s);
+  int64_t idx = it - dict.begin();
+  return (it != dict.end() && *it == s) ? 2 * idx : 2 * idx - 1;
+}
+
+// ============================================================================= constant folding
+namespace {
+
+bool truthy(const CVal& v) {   // Expression::asBool (Expressions.h:228-241)
+  switch (v.index()) {
+    case 0: return std::get<0>(v) != 0;
+    case 1: return std::get<1>(v) != 0.0;
+    case 2: return std::get<2>(v);
+    default: return std::get<3>(v).empty();
+  }
+}
+double toD(const CVal& v) {
+  switch (v.index()) {
+    case 0: return (double)std::get<0>(v);
+    case 1: return std::get<1>(v);
+    case 2: return std::get<2>(v) ? 1.0 : 0.0;
+    default: return 0.0;
+  }
+}
+int64_t toI(const CVal& v) {
+  switch (v.index()) {
+    case 0: return std::get<0>(v);
+    case 1: return (int64_t)std::get<1>(v);
+    case 2: return std::get<2>(v) ? 1 : 0;
+    default: return 0;
+  }
+}
+bool isArith(const CVal& v) { return v.index() <= 1; }
+
+// variant '<' on same alternatives
+bool vless(const CVal& a, const CVal& b) {
+  switch (a.index()) {
+    case 0: return std::get<0>(a) < std::get<0>(b);
+    case 1: return std::get<1>(a) < std::get<1>(b);
+    case 2: return std::get<2>(a) < std::get<2>(b);
+    default: return std::get<3>(a) < std::get<3>(b);
+  }
+}
+bool veq(const CVal& a, const CVal& b) {
+  switch (a.index()) {
+    case 0: return std::get<0>(a) == std::get<0>(b);
+    case 1: return std::get<1>(a) == std::get<1>(b);
+    case 2: return std::get<2>(a) == std::get<2>(b);
+    default: return std::get<3>(a) == std::get<3>(b);
+  }
+}
+
+bool evalUnary(uint8_t op, const CVal& v, CVal* out) {      // Expressions.cpp:698-716
+  if (op == 0) { *out = v; return true; }
+  if (op == 1) {
+    if (v.index() == 0) { *out = (int64_t)(0ull - (uint64_t)std::get<0>(v)); return true; }
+    if (v.index() == 1) { *out = -std::get<1>(v); return true; }
+    return false;
+  }
+  *out = !truthy(v);
+  return true;
+}
+
+bool evalCast(uint8_t ct, const CVal& v, CVal* out) {       // Expressions.cpp:773-793
+  switch (ct) {
+    case 0: case 5:
+      if (v.index() == 3) {
+        const std::string& s = std::get<3>(v);
+        char* end = nullptr; errno = 0;
+        long long r = strtoll(s.c_str(), &end, 10);
+        if (s.empty() || *end || errno) return false;
+        *out = (int64_t)r; return true;
+      }
+      *out = toI(v); return true;
+    case 1:
+      if (v.index() == 0) { *out = std::to_string(std::get<0>(v)); return true; }
+      if (v.index() == 2) { *out = std::string(std::get<2>(v) ? "true" : "false"); return true; }
+      if (v.index() == 3) { *out = v; return true; }
+      return false;   // folly::to<std::string>(double): not restated (unpinned)
+    case 2:
+      if (v.index() == 3) {
+        const std::string& s = std::get<3>(v);
+        char* end = nullptr;
+        double r = strtod(s.c_str(), &end);
+        if (s.empty() || *end) return false;
+        *out = r; return true;
+      }
+      *out = toD(v); return true;
+    case 4: *out = truthy(v); return true;
+    default: return false;   // BIGINT
+  }
+}
+
+bool evalArith(uint8_t op, const CVal& l, const CVal& r, CVal* out) {   // Expressions.cpp:835-909
+  if (isArith(l) && isArith(r)) {
+    bool dbl = l.index() == 1 || r.index() == 1;
+    if (dbl) {
+      double a = toD(l), b = toD(r);
+      switch (op) {
+        case 0: *out = a + b; return true;
+        case 1: *out = a - b; return true;
+        case 2: *out = a * b; return true;
+        case 3: *out = a / b; return true;
+        case 4: *out = std::fmod(a, b); return true;
+        case 5: *out = (int64_t)std::llround(a) ^ (int64_t)std::llround(b); return true;
+        default: return false;
+      }
+    }
+    uint64_t a = (uint64_t)std::get<0>(l), b = (uint64_t)std::get<0>(r);
+    int64_t sa = std::get<0>(l), sb = std::get<0>(r);
+    switch (op) {
+      case 0: *out = (int64_t)(a + b); return true;
+      case 1: *out = (int64_t)(a - b); return true;
+      case 2: *out = (int64_t)(a * b); return true;
+      case 3: case 4:
+        if (sb == 0 || (sa == INT64_MIN && sb == -1)) return false;
+        *out = op == 3 ? sa / sb : sa % sb; return true;
+      case 5: *out = sa ^ sb; return true;
+      default: return false;
+    }
+  }
+  if (op == 0 && l.index() == 3 && r.index() == 3) { *out = std::get<3>(l) + std::get<3>(r); return true; }
+  return false;
+}
+
+bool evalRel(uint8_t op, CVal l, CVal r, CVal* out) {       // Expressions.cpp:976-1045
+  if (l.index() != r.index()) {
+    if (l.index() == 3 || r.index() == 3) return false;
+    if (l.index() == 1 || r.index() == 1) { l = toD(l); r = toD(r); }
+    else { l = toI(l); r = toI(r); }
+  }
+  if ((op == 4 || op == 5) && isArith(l) && isArith(r) && (l.index() == 1 || r.index() == 1)) {
+    bool eq = std::fabs(toD(l) - toD(r)) < 1e-8;
+    *out = op == 4 ? eq : !eq;
+    return true;
+  }
+  switch (op) {
+    case 0: *out = vless(l, r); return true;
+    case 1: *out = !vless(r, l); return true;
+    case 2: *out = vless(r, l); return true;
+    case 3: *out = !vless(l, r); return true;
+    case 4: *out = veq(l, r); return true;
+    case 5: *out = !veq(l, r); return true;
+    default: return false;
+  }
+}
+
+bool evalLogic(uint8_t op, const CVal& l, const CVal& r, CVal* out) {   // Expressions.cpp:1103-1131
+  bool a = truthy(l), b = truthy(r);
+  *out = op == 0 ? (a && b) : op == 1 ? (a || b) : (a != b);
+  return true;
+}
+
+}  // namespace
+
+bool fold_constant(const Node& e, CVal* out, bool* error) {
+  *error = false;
+  switch (e.kind) {
+    case EK_PRIMARY: *out = e.prim; return true;
+    case EK_UNARY: case EK_CAST: {
+      CVal v; bool er;
+      if (!fold_constant(*e.kids[0], &v, &er)) return false;
+      if (er) { *error = true; return true; }
+      bool ok = e.kind == EK_UNARY ? evalUnary(e.op, v, out) : evalCast(e.op, v, out);
+      *error = !ok;
+      return true;
+    }
+    case EK_ARITH: case EK_REL: case EK_LOGIC: {
+      CVal a, b; bool ea, eb;
+      if (!fold_constant(*e.kids[0], &a, &ea) || !fold_constant(*e.kids[1], &b, &eb)) return false;
+      if (ea || eb) { *error = true; return true; }
+      bool ok = e.kind == EK_ARITH ? evalArith(e.op, a, b, out)
+              : e.kind == EK_REL ? evalRel(e.op, a, b, out) : evalLogic(e.op, a, b, out);
+      *error = !ok;
+      return true;
+    }
+    default: return false;   // props, EdgeType (validated against OVER first), functions
+  }
+}
+
+// ============================================================================= emission
+namespace {
+
+struct Ctx {
+  const CompileEnv& env;
+  ProgramBuilder& pb;
+  std::string* err;
+  int max_reg = 0;
+  int top = 0;               // stack discipline: next free register
+
+  int push() {
+    int r = top++;
+    if (top > max_reg) max_reg = top;
+    return r;
+  }
+  void emit(uint8_t op, int d, int a = 0, int b = 0, int32_t aux = 0, int64_t imm = 0) {
+    pb.code.push_back(Ins{op, (uint8_t)d, (uint8_t)a, (uint8_t)b, aux, imm});
+  }
+  VKind kind_of(const CVal& v) { return static_cast<VKind>(v.index()); }
+  int64_t bits_of(const CVal& v) {
+    switch (v.index()) {
+      case 0: return std::get<0>(v);
+      case 1: { double d = std::get<1>(v); int64_t b; memcpy(&b, &d, 8); return b; }
+      case 2: return std::get<2>(v) ? 1 : 0;
+      default: return string_code(*env.strings, std::get<3>(v));
+    }
+  }
+  Compiled make_const(const CVal& v) {
+    Compiled c;
+    c.kind = kind_of(v);
+    c.is_const = true;
+    c.const_bits = bits_of(v);
+    c.cval = v;
+    if (v.index() == 3) c.const_str = std::get<3>(v);
+    return c;
+  }
+  Compiled make_error() {
+    Compiled c;
+    c.always_error = true;
+    c.kind = VK_INT;
+    c.reg = push();
+    emit(OP_ERR, c.reg);
+    return c;
+  }
+  // materialise a constant operand into the top register
+  int materialize(Compiled& c) {
+    if (!c.is_const) return c.reg;
+    c.reg = push();
+    emit(OP_CONST, c.reg, 0, 0, 0, c.const_bits);
+    return c.reg;
+  }
+  int truthy_reg(Compiled& c) {
+    int r = materialize(c);
+    switch (c.kind) {
+      case VK_INT: emit(OP_TRUTHY_I, r, r); break;
+      case VK_DOUBLE: emit(OP_TRUTHY_F, r, r); break;
+      case VK_BOOL: break;
+      case VK_STRING: emit(OP_TRUTHY_S, r, r, 0, 0, string_code(*env.strings, "")); break;
+    }
+    return r;
+  }
+  const SchemaSet* edge_by_name(const std::string& name, int32_t* type) {
+    for (auto& kv : *env.edges) {
+      if (kv.second.name == name) { *type = kv.first; return &kv.second; }
+    }
+    return nullptr;
+  }
+
+  int32_t leaf_alias(const Node& e, Compiled* out) {
+    // GoExecutor::processFinalResult getAliasProp (GoExecutor.cpp:851-878)
+    int32_t et;
+    const SchemaSet* ss = edge_by_name(e.alias, &et);
+    if (!ss || std::find(env.over->begin(), env.over->end(), et) == env.over->end()) {
+      *err = "the edge was not found '" + e.alias + "'";
+      return NBG_E_EXECUTION_ERROR;   // deferred to the final step (getStepOutProps)
+    }
+    bool key = e.prop == "_dst" || e.prop == "_src" || e.prop == "_rank" || e.prop == "_type";
+    const Schema* sc = ss->latest();
+    int col = (!key && sc) ? sc->find(e.prop) : -1;
+    if (!key && col < 0) {
+      *err = "prop `" + e.alias + "." + e.prop + "' not found";
+      return NBG_E_IMPROPER_DATA_TYPE;   // storage rejects the request (inl:275-286); deferred
+    }
+    if (et != env.etype) {
+      // another OVER edge: the schema default of its response column (RowReader::getDefaultProp)
+      if (key) { *out = make_const(CVal(int64_t(0))); return NBG_OK; }
+      switch (kindOfType(sc->cols[col].type)) {
+        case VK_BOOL: *out = make_const(CVal(false)); break;
+        case VK_DOUBLE: *out = make_const(CVal(0.0)); break;
+        case VK_STRING: *out = make_const(CVal(std::string())); break;
+        default: *out = make_const(CVal(int64_t(0))); break;
+      }
+      return NBG_OK;
+    }
+    Compiled c;
+    c.kind = VK_INT;
+    if (e.prop == "_type") { *out = make_const(CVal((int64_t)et)); return NBG_OK; }
+    c.reg = push();
+    if (e.prop == "_dst") emit(OP_DST, c.reg);
+    else if (e.prop == "_src") emit(OP_SRC, c.reg);
+    else if (e.prop == "_rank") emit(OP_RANK, c.reg);
+    else {
+      c.kind = kindOfType(sc->cols[col].type);
+      emit(env.has_valid ? OP_COLV : OP_COL, c.reg, 0, 0, col);
+    }
+    *out = c;
+    return NBG_OK;
+  }
+
+  int32_t compile(const Node& e, Compiled* out) {
+    // constant subtrees fold on the host with the reference's exact rules
+    {
+      CVal v; bool error;
+      if (fold_constant(e, &v, &error)) {
+        *out = error ? make_error() : make_const(v);
+        return NBG_OK;
+      }
+    }
+    switch (e.kind) {
+      case EK_ALIAS: case EK_DST: case EK_SRCID: case EK_RANK:
+        return leaf_alias(e, out);
+      case EK_TYPE: {
+        int32_t et;
+        const SchemaSet* ss = edge_by_name(e.alias, &et);
+        if (!ss || std::find(env.over->begin(), env.over->end(), et) == env.over->end()) {
+          *err = "the edge was not found '" + e.alias + "'";
+          return NBG_E_EXECUTION_ERROR;
+        }
+        *out = make_const(CVal(e.alias));
+        return NBG_OK;
+      }
+      case EK_SRCPROP: *err = "$^ tag props are not supported on the device path yet"; return NBG_E_UNSUPPORTED;
+      case EK_DSTPROP: *err = "$$ tag props are not supported on the device path yet"; return NBG_E_UNSUPPORTED;
+      case EK_INPUT: case EK_VAR: *err = "input/variable props are not supported"; return NBG_E_UNSUPPORTED;
+      case EK_FUNC: *err = "function calls are not supported"; return NBG_E_UNSUPPORTED;
+      case EK_UNARY: {
+        Compiled a;
+        int32_t rc = compile(*e.kids[0], &a);
+        if (rc) return rc;
+        if (a.always_error) { *out = a; return NBG_OK; }
+        if (a.is_const) {
+          CVal v;
+          *out = evalUnary(e.op, a.cval, &v) ? make_const(v) : make_error();
+          return NBG_OK;
+        }
+        if (e.op == 0) { *out = a; return NBG_OK; }
+        if (e.op == 1) {
+          if (a.kind == VK_INT || a.kind == VK_DOUBLE) {
+            int r = materialize(a);
+            emit(a.kind == VK_INT ? OP_NEG_I : OP_NEG_F, r, r);
+            *out = a;
+            return NBG_OK;
+          }
+          *out = make_error();
+          return NBG_OK;
+        }
+        int r = truthy_reg(a);
+        emit(OP_NOT, r, r);
+        Compiled c; c.kind = VK_BOOL; c.reg = r;
+        *out = c;
+        return NBG_OK;
+      }
+      case EK_CAST: {
+        Compiled a;
+        int32_t rc = compile(*e.kids[0], &a);
+        if (rc) return rc;
+        if (a.always_error) { *out = a; return NBG_OK; }
+        if (a.is_const) {
+          CVal v;
+          *out = evalCast(e.op, a.cval, &v) ? make_const(v) : make_error();
+          return NBG_OK;
+        }
+        Compiled c; c.reg = materialize(a);
+        switch (e.op) {
+          case 0: case 5:
+            c.kind = VK_INT;
+            if (a.kind == VK_DOUBLE) emit(OP_F2I, c.reg, c.reg);
+            else if (a.kind == VK_BOOL) emit(OP_B2I, c.reg, c.reg);
+            else if (a.kind == VK_STRING) { *err = "string->int cast of a column"; return NBG_E_UNSUPPORTED; }
+            break;
+          case 2:
+            c.kind = VK_DOUBLE;
+            if (a.kind == VK_INT) emit(OP_I2F, c.reg, c.reg);
+            else if (a.kind == VK_BOOL) emit(OP_B2F, c.reg, c.reg);
+            else if (a.kind == VK_STRING) { *err = "string->double cast of a column"; return NBG_E_UNSUPPORTED; }
+            break;
+          case 4:
+            c.reg = truthy_reg(a);
+            c.kind = VK_BOOL;
+            break;
+          case 1:
+            if (a.kind == VK_STRING) { c.kind = VK_STRING; break; }
+            *err = "cast of a column to string";
+            return NBG_E_UNSUPPORTED;
+          default:
+            *out = make_error();
+            return NBG_OK;
+        }
+        *out = c;
+        return NBG_OK;
+      }
+      case EK_ARITH: case EK_REL: case EK_LOGIC: {
+        Compiled a, b;
+        int32_t rc = compile(*e.kids[0], &a);
+        if (rc) return rc;
+        rc = compile(*e.kids[1], &b);
+        if (rc) return rc;
+        if (a.always_error || b.always_error) {
+          Compiled c = a.always_error ? a : b;
+          c.always_error = true;
+          *out = c;
+          return NBG_OK;
+        }
+        return binary(e, a, b, out);
+      }
+      default:
+        *err = "unsupported expression kind";
+        return NBG_E_UNSUPPORTED;
+    }
+  }
+
+  // Registers of a (left) and b (right): constants are materialised lazily so that the
+  // result ends up in the lower slot.
+  int32_t binary(const Node& e, Compiled& a, Compiled& b, Compiled* out) {
+    Compiled c;
+    if (a.is_const && b.is_const) {   // e.g. EdgeType constants once validated
+      CVal v;
+      bool ok = e.kind == EK_ARITH ? evalArith(e.op, a.cval, b.cval, &v)
+              : e.kind == EK_REL ? evalRel(e.op, a.cval, b.cval, &v) : evalLogic(e.op, a.cval, b.cval, &v);
+      *out = ok ? make_const(v) : make_error();
+      return NBG_OK;
+    }
+    if (e.kind == EK_LOGIC) {
+      // both operands are always evaluated; asBool on each
+      int lr = truthy_reg(a);
+      int rr = truthy_reg(b);
+      emit(e.op == 0 ? OP_AND : e.op == 1 ? OP_OR : OP_XORB, std::min(lr, rr), lr, rr);
+      c.kind = VK_BOOL;
+      c.reg = std::min(lr, rr);
+      top = c.reg + 1;
+      *out = c;
+      return NBG_OK;
+    }
+    if (e.kind == EK_ARITH) {
+      bool arith = (a.kind == VK_INT || a.kind == VK_DOUBLE) && (b.kind == VK_INT || b.kind == VK_DOUBLE);
+      if (!arith) {
+        if (e.op == 0 && a.kind == VK_STRING && b.kind == VK_STRING) {
+          *err = "string concatenation of columns";
+          return NBG_E_UNSUPPORTED;
+        }
+        *out = make_error();
+        return NBG_OK;
+      }
+      bool dbl = a.kind == VK_DOUBLE || b.kind == VK_DOUBLE;
+      int lr = materialize(a);
+      if (dbl && a.kind == VK_INT) emit(OP_I2F, lr, lr);
+      int rr = materialize(b);
+      if (dbl && b.kind == VK_INT) emit(OP_I2F, rr, rr);
+      static const uint8_t iops[] = {OP_ADD_I, OP_SUB_I, OP_MUL_I, OP_DIV_I, OP_MOD_I, OP_XOR_I};
+      static const uint8_t fops[] = {OP_ADD_F, OP_SUB_F, OP_MUL_F, OP_DIV_F, OP_MOD_F, OP_XOR_F};
+      if (e.op > 5) { *out = make_error(); return NBG_OK; }
+      int d = std::min(lr, rr);
+      emit(dbl ? fops[e.op] : iops[e.op], d, lr, rr);
+      c.kind = (dbl && e.op != 5) ? VK_DOUBLE : VK_INT;
+      c.reg = d;
+      top = d + 1;
+      *out = c;
+      return NBG_OK;
+    }
+    // relational with implicit casting bool -> int -> double (Expressions.cpp:1027-1045)
+    if (e.op > 5) { *out = make_error(); return NBG_OK; }
+    VKind ka = a.kind, kb = b.kind;
+    if (ka != kb && (ka == VK_STRING || kb == VK_STRING)) { *out = make_error(); return NBG_OK; }
+    bool dbl = (ka != kb) ? (ka == VK_DOUBLE || kb == VK_DOUBLE) : ka == VK_DOUBLE;
+    int lr = materialize(a);
+    if (ka != kb) {
+      if (dbl) { if (ka == VK_INT) emit(OP_I2F, lr, lr); else if (ka == VK_BOOL) emit(OP_B2F, lr, lr); }
+      else if (ka == VK_BOOL) emit(OP_B2I, lr, lr);
+    }
+    int rr = materialize(b);
+    if (ka != kb) {
+      if (dbl) { if (kb == VK_INT) emit(OP_I2F, rr, rr); else if (kb == VK_BOOL) emit(OP_B2F, rr, rr); }
+      else if (kb == VK_BOOL) emit(OP_B2I, rr, rr);
+    }
+    static const uint8_t iops[] = {OP_LT_I, OP_LE_I, OP_GT_I, OP_GE_I, OP_EQ_I, OP_NE_I};
+    static const uint8_t fops[] = {OP_LT_F, OP_LE_F, OP_GT_F, OP_GE_F, OP_EQ_F, OP_NE_F};
+    int d = std::min(lr, rr);
+    emit(dbl ? fops[e.op] : iops[e.op], d, lr, rr);
+    c.kind = VK_BOOL;
+    c.reg = d;
+    top = d + 1;
+    *out = c;
+    return NBG_OK;
+  }
+};
+
+}  // namespace
+
+int32_t compile_expr(const Node& e, const CompileEnv& env, ProgramBuilder& pb, Compiled* out, std::string* err) {
+  Ctx c{env, pb, err};
+  c.top = pb.next_reg;
+  c.max_reg = pb.next_reg;
+  int32_t rc = c.compile(e, out);
+  if (rc) return rc;
+  if (!out->is_const && out->reg >= 0) pb.next_reg = out->reg + 1;
+  if (c.max_reg > MAX_REGS) {
+    *err = "expression too deep for the device register file";
+    return NBG_E_UNSUPPORTED;
+  }
+  pb.max_reg = std::max(pb.max_reg, c.max_reg);
+  return NBG_OK;
+}
+
+}  // namespace nbg

@@ -1,0 +1,67 @@
+// Expression wire decoding and compilation to the per-edge device bytecode.
+#pragma once
+#include <memory>
+#include <string>
+#include <variant>
+#include <vector>
+
+#include "nbg_internal.h"
+
+namespace nbg {
+
+// Expression::Kind (src/common/filter/Expressions.h:326-347)
+enum EKind : uint8_t {
+  EK_PRIMARY = 1, EK_FUNC, EK_UNARY, EK_CAST, EK_ARITH, EK_REL, EK_LOGIC, EK_SRCPROP,
+  EK_RANK, EK_DST, EK_SRCID, EK_TYPE, EK_ALIAS, EK_VAR, EK_DSTPROP, EK_INPUT,
+};
+
+using CVal = std::variant<int64_t, double, bool, std::string>;   // VariantType
+
+struct Node {
+  EKind kind{};
+  uint8_t op = 0;
+  CVal prim;
+  std::string alias, prop;
+  std::vector<std::unique_ptr<Node>> kids;
+};
+
+// Decodes Expression::encode bytes; nullptr + *err on malformed input.
+std::unique_ptr<Node> decode_expr(const uint8_t* p, size_t n, std::string* err);
+
+struct CompileEnv {
+  int32_t etype;                                   // edge type of the rows being evaluated
+  const std::vector<int32_t>* over;                // OVER types
+  const std::map<int32_t, SchemaSet>* edges;       // registered edge schemas
+  const std::vector<std::string>* strings;         // sorted string dictionary
+  bool has_valid;                                  // the type has edges without a decoded value
+  bool has_rank;
+};
+
+// Result of compiling one expression for one edge type.
+struct Compiled {
+  VKind kind = VK_INT;
+  bool is_const = false;
+  int64_t const_bits = 0;     // payload when is_const (strings: dictionary code)
+  std::string const_str;      // string constant text (may be absent from the dictionary)
+  CVal cval;                  // the constant value when is_const
+  bool always_error = false;
+  int reg = -1;
+};
+
+// Status codes: NBG_OK, NBG_E_UNSUPPORTED, NBG_E_IMPROPER_DATA_TYPE (deferred: the reference
+// reports it only when the final step is reached), NBG_E_INVALID_ARGUMENT.
+struct ProgramBuilder {
+  std::vector<Ins> code;
+  int next_reg = 0;
+  int max_reg = 0;
+};
+
+int32_t compile_expr(const Node& e, const CompileEnv& env, ProgramBuilder& pb, Compiled* out, std::string* err);
+
+// Evaluate constant-only expressions on the host with the reference's exact rules
+// (Expressions.cpp eval); returns false if the expression is not constant.
+bool fold_constant(const Node& e, CVal* out, bool* error);
+
+int64_t string_code(const std::vector<std::string>& dict, const std::string& s);
+
+}  // namespace nbg

@@ -1,0 +1,382 @@
+// Loader: kvstore records (or bulk edge columns) -> device-resident CSR per signed edge type.
+//
+// What a storaged part holds (and what GetNeighbors reads back) is defined by
+//   NebulaKeyUtils::edgeKey  (src/common/base/NebulaKeyUtils.cpp:28-47)
+//   AddEdgesProcessor        (src/storage/AddEdgesProcessor.cpp:15-37)  version = BE(INT64_MAX-now)
+//   RowWriter / RowReader    (src/dataman/RowWriter.cpp:49-75, RowReader.cpp:117-258)
+//   collectEdgeProps         (src/storage/QueryBaseProcessor.inl:381-458)
+// A prefix scan of (part, src, type) visits keys in memcmp order of (rank LE | dst LE |
+// version BE) and keeps the first key of each (rank, dst) group.  The snapshot bakes exactly
+// that view: rows sorted by (bswap64(rank), bswap64(dst)) as unsigned, one live edge per
+// (src, type, rank, dst) — the one with the smallest version bytes (newest write); identical
+// keys resolve to the record loaded last (write-batch overwrite).
+#include <omp.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <numeric>
+#include <parallel/algorithm>
+
+#include "engine.h"
+
+namespace nbg {
+
+static inline uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
+
+static int32_t hash_part(int64_t vid, int32_t parts) {
+  return (int32_t)((uint64_t)vid % (uint64_t)parts + 1);
+}
+
+// ----------------------------------------------------------------------------- row decoding
+// RowReader::processHeader + sequential field walk (RowReader.cpp:217-258, :307-375)
+static bool decode_varint(const uint8_t* p, size_t avail, uint64_t& v, size_t& len) {
+  v = 0;
+  len = 0;
+  for (int shift = 0; shift < 64 && len < avail; shift += 7) {
+    uint8_t b = p[len++];
+    v |= (uint64_t)(b & 0x7f) << shift;
+    if (!(b & 0x80)) return true;
+  }
+  return false;
+}
+
+int64_t Engine::intern(const std::string& s) {
+  auto it = pool_index.find(s);
+  if (it != pool_index.end()) return it->second;
+  int64_t id = (int64_t)pool.size();
+  pool.push_back(s);
+  pool_index.emplace(s, id);
+  return id;
+}
+
+// Decodes a RowWriter value into the latest schema's column order.  Returns false if the row
+// cannot be decoded (the reference would then fail reading the prop).
+bool Engine::decode_row(const SchemaSet& ss, const uint8_t* v, size_t n, int64_t* out) {
+  if (n == 0) return false;
+  uint8_t h = v[0];
+  size_t offBytes = (h & 0x07) + 1, verBytes = h >> 5;
+  int64_t ver = 0;
+  if (1 + verBytes > n) return false;
+  for (size_t i = 0; i < verBytes; ++i) ver |= (int64_t)v[1 + i] << (8 * i);
+  const Schema* sc = ss.at(ver);
+  const Schema* latest = ss.latest();
+  if (!sc || !latest) return false;
+  size_t numOffsets = sc->cols.size() >> 4;
+  size_t pos = 1 + verBytes + offBytes * numOffsets;
+  if (pos > n) return false;
+  std::vector<int64_t> vals(sc->cols.size());
+  for (size_t c = 0; c < sc->cols.size(); ++c) {
+    const uint8_t* p = v + pos;
+    size_t avail = n - pos;
+    switch (sc->cols[c].type) {
+      case NBG_T_BOOL: if (avail < 1) return false; vals[c] = p[0] != 0; pos += 1; break;
+      case NBG_T_INT: case NBG_T_TIMESTAMP: {
+        uint64_t x; size_t l;
+        if (!decode_varint(p, avail, x, l)) return false;
+        vals[c] = (int64_t)x; pos += l; break;
+      }
+      case NBG_T_VID: if (avail < 8) return false; memcpy(&vals[c], p, 8); pos += 8; break;
+      case NBG_T_FLOAT: {
+        if (avail < 4) return false;
+        float f; memcpy(&f, p, 4);
+        double d = f; memcpy(&vals[c], &d, 8); pos += 4; break;
+      }
+      case NBG_T_DOUBLE: if (avail < 8) return false; memcpy(&vals[c], p, 8); pos += 8; break;
+      case NBG_T_STRING: {
+        uint64_t len; size_t l;
+        if (!decode_varint(p, avail, len, l) || l + len > avail) return false;
+        vals[c] = intern(std::string(reinterpret_cast<const char*>(p + l), len));
+        pos += l + len; break;
+      }
+      default: return false;
+    }
+  }
+  for (size_t c = 0; c < latest->cols.size(); ++c) {
+    int k = sc == latest ? (int)c : sc->find(latest->cols[c].name);
+    if (k < 0) return false;
+    out[c] = vals[k];
+  }
+  return true;
+}
+
+// ----------------------------------------------------------------------------- ingest
+int32_t Engine::load_part_kv(int32_t part, const uint8_t* kd, const uint64_t* ko, const uint8_t* vd,
+                             const uint64_t* vo, uint64_t n) {
+  if (finalized) return fail(NBG_E_STATE, "engine already finalized");
+  if (cfg.num_gpus > 1 && part % cfg.num_gpus != cfg.rank) return NBG_OK;   // not served here
+  std::vector<int64_t> props;
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint8_t* k = kd + ko[i];
+    uint64_t klen = ko[i + 1] - ko[i];
+    const uint8_t* v = vd + vo[i];
+    uint64_t vlen = vo[i + 1] - vo[i];
+    if (klen < 4) continue;
+    int32_t item;
+    memcpy(&item, k, 4);
+    if ((item & 0xFF) != 1) continue;   // NebulaKeyType::kData only
+    if (klen == 40) {
+      int32_t t;
+      memcpy(&t, k + 12, 4);
+      if (!(t & 0x40000000)) continue;
+      int32_t type = t > 0 ? (t & (int32_t)0xBFFFFFFF) : t;
+      int64_t src, rank, dst;
+      uint64_t ver;
+      memcpy(&src, k + 4, 8);
+      memcpy(&rank, k + 16, 8);
+      memcpy(&dst, k + 24, 8);
+      memcpy(&ver, k + 32, 8);
+      EdgeStage& st = stage[type];
+      st.src.push_back(src);
+      st.dst.push_back(dst);
+      st.rank.push_back(rank);
+      st.verkey.push_back(bswap64(ver));
+      st.seq.push_back(seq++);
+      st.part.push_back(item >> 8);
+      if (type > 0) {
+        auto es = edges.find(type);
+        const Schema* latest = es == edges.end() ? nullptr : es->second.latest();
+        size_t nc = latest ? latest->cols.size() : 0;
+        if (st.props.size() < nc) st.props.resize(nc);
+        props.assign(nc, 0);
+        bool ok = latest && decode_row(es->second, v, vlen, props.data());
+        for (size_t c = 0; c < nc; ++c) st.props[c].push_back(ok ? props[c] : 0);
+        st.valid.push_back(ok ? 1 : 0);
+      }
+    } else if (klen == 24) {
+      int64_t vid;
+      memcpy(&vid, k + 4, 8);
+      tag_vertices.emplace_back(vid, item >> 8);   // tag records (props: §8(f) next)
+    }
+  }
+  return NBG_OK;
+}
+
+int32_t Engine::load_edges(int32_t type, const int64_t* src, const int64_t* dst, const int64_t* rank, uint64_t n,
+                           const void* const* cols, int32_t ncols) {
+  if (finalized) return fail(NBG_E_STATE, "engine already finalized");
+  auto es = edges.find(type);
+  if (type <= 0 || es == edges.end()) return fail(NBG_E_EDGE_PROP_NOT_FOUND, "edge type not registered");
+  const Schema* latest = es->second.latest();
+  if ((int32_t)latest->cols.size() != ncols) return fail(NBG_E_INVALID_ARGUMENT, "column count mismatch");
+  for (auto& c : latest->cols)
+    if (c.type == NBG_T_STRING) return fail(NBG_E_UNSUPPORTED, "bulk load of STRING columns");
+  EdgeStage& out = stage[type];
+  EdgeStage& in = stage[-type];
+  if (out.props.size() < (size_t)ncols) out.props.resize(ncols);
+  const uint64_t ver = bswap64((uint64_t)(INT64_MAX - 1));   // one version for the whole batch
+  const int32_t P = cfg.num_parts, G = cfg.num_gpus;
+  for (uint64_t i = 0; i < n; ++i) {
+    int64_t r = rank ? rank[i] : 0;
+    int32_t ps = hash_part(src[i], P), pd = hash_part(dst[i], P);
+    if (G <= 1 || ps % G == cfg.rank) {
+      out.src.push_back(src[i]);
+      out.dst.push_back(dst[i]);
+      out.rank.push_back(r);
+      out.verkey.push_back(ver);
+      out.seq.push_back(seq + i);
+      out.part.push_back(ps);
+      for (int32_t c = 0; c < ncols; ++c) {
+        int64_t b = 0;
+        switch (latest->cols[c].type) {
+          case NBG_T_BOOL: b = static_cast<const uint8_t*>(cols[c])[i] != 0; break;
+          case NBG_T_FLOAT: case NBG_T_DOUBLE: memcpy(&b, static_cast<const double*>(cols[c]) + i, 8); break;
+          default: b = static_cast<const int64_t*>(cols[c])[i]; break;
+        }
+        out.props[c].push_back(b);
+      }
+      out.valid.push_back(1);
+    }
+    if (G <= 1 || pd % G == cfg.rank) {
+      in.src.push_back(dst[i]);
+      in.dst.push_back(src[i]);
+      in.rank.push_back(r);
+      in.verkey.push_back(ver);
+      in.seq.push_back(seq + i);
+      in.part.push_back(pd);
+    }
+  }
+  seq += n;
+  return NBG_OK;
+}
+
+// ----------------------------------------------------------------------------- finalize
+namespace {
+struct RowKey {   // memcmp order of (rank | dst | version) then newest load first
+  uint64_t rank_be, dst_be, ver;
+  uint64_t seq;
+  uint64_t idx;
+};
+inline bool rowkey_less(const RowKey& a, const RowKey& b) {
+  if (a.rank_be != b.rank_be) return a.rank_be < b.rank_be;
+  if (a.dst_be != b.dst_be) return a.dst_be < b.dst_be;
+  if (a.ver != b.ver) return a.ver < b.ver;
+  return a.seq > b.seq;
+}
+}  // namespace
+
+int32_t Engine::finalize() {
+  if (finalized) return fail(NBG_E_STATE, "engine already finalized");
+  // 1. string dictionary: sorted; device code = 2 * rank
+  std::vector<int64_t> remap(pool.size());
+  {
+    std::vector<int64_t> order(pool.size());
+    std::iota(order.begin(), order.end(), 0);
+    std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return pool[a] < pool[b]; });
+    snap.strings.clear();
+    for (auto id : order) {
+      if (snap.strings.empty() || snap.strings.back() != pool[id]) snap.strings.push_back(pool[id]);
+      remap[id] = 2 * (int64_t)(snap.strings.size() - 1);
+    }
+  }
+  // 2. vertex dictionary: every vid that owns a row (src of any signed type)
+  std::vector<int64_t> all;
+  {
+    size_t tot = 0;
+    for (auto& kv : stage) tot += kv.second.src.size();
+    all.reserve(tot);
+    for (auto& kv : stage) all.insert(all.end(), kv.second.src.begin(), kv.second.src.end());
+    __gnu_parallel::sort(all.begin(), all.end());
+    all.erase(std::unique(all.begin(), all.end()), all.end());
+  }
+  const uint64_t nv = all.size();
+  if (nv >= NO_ROW) return fail(NBG_E_UNSUPPORTED, "more than 2^32-1 vertices on one GPU");
+  snap.nv = nv;
+  snap.h_vids = all;
+  auto dense = [&](int64_t vid) -> uint32_t {
+    auto it = std::lower_bound(all.begin(), all.end(), vid);
+    return (it != all.end() && *it == vid) ? (uint32_t)(it - all.begin()) : NO_ROW;
+  };
+  // home part per vertex; a vid whose rows sit in two parts is not representable
+  std::vector<int32_t> home(nv, 0);
+  bool all_visible = true;
+  for (auto& kv : stage) {
+    auto& st = kv.second;
+    for (size_t i = 0; i < st.src.size(); ++i) {
+      uint32_t d = dense(st.src[i]);
+      if (home[d] == 0) home[d] = st.part[i];
+      else if (home[d] != st.part[i]) return fail(NBG_E_UNSUPPORTED, "vertex rows split across partitions");
+    }
+  }
+  std::vector<uint8_t> visible(nv, 1);
+  for (uint64_t d = 0; d < nv; ++d) {
+    if (home[d] != hash_part(all[d], cfg.num_parts)) { visible[d] = 0; all_visible = false; }
+  }
+  snap.h_part = home;
+
+  // 3. per signed type: bucket by src, sort rows in key order, keep the live version
+  int32_t rc = NBG_OK;
+  for (auto& kv : stage) {
+    const int32_t type = kv.first;
+    EdgeStage& st = kv.second;
+    const uint64_t n = st.src.size();
+    std::vector<uint32_t> sd(n);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < (int64_t)n; ++i) sd[i] = dense(st.src[i]);
+    std::vector<uint64_t> cnt(nv + 1, 0);
+    for (uint64_t i = 0; i < n; ++i) cnt[sd[i] + 1]++;
+    for (uint64_t d = 0; d < nv; ++d) cnt[d + 1] += cnt[d];
+    std::vector<RowKey> keys(n);
+    {
+      std::vector<uint64_t> cur(cnt.begin(), cnt.end() - 1);
+      for (uint64_t i = 0; i < n; ++i) {
+        uint64_t p = cur[sd[i]]++;
+        keys[p] = RowKey{bswap64((uint64_t)st.rank[i]), bswap64((uint64_t)st.dst[i]), st.verkey[i], st.seq[i], i};
+      }
+    }
+    std::vector<uint32_t> live(nv + 1, 0);
+#pragma omp parallel for schedule(dynamic, 4096)
+    for (int64_t d = 0; d < (int64_t)nv; ++d) {
+      auto b = keys.begin() + cnt[d], e = keys.begin() + cnt[d + 1];
+      if (e - b > 1) std::sort(b, e, rowkey_less);
+      uint32_t m = 0;
+      for (auto it = b; it != e; ++it) {
+        if (it != b && it->rank_be == (it - 1)->rank_be && it->dst_be == (it - 1)->dst_be) continue;
+        b[m++] = *it;   // compact in place (m <= position)
+      }
+      live[d + 1] = m;
+    }
+    std::vector<uint64_t> rp(nv + 1, 0);
+    for (uint64_t d = 0; d < nv; ++d) rp[d + 1] = rp[d] + live[d + 1];
+    const uint64_t E = rp[nv];
+    if (E >= 0xFFFFFFFFull) return fail(NBG_E_UNSUPPORTED, "more than 2^32-1 edges of one type on one GPU");
+    DevEdgeType& dt = snap.types[type];
+    dt.type = type;
+    dt.num_edges = E;
+    dt.h_row_ptr.resize(nv + 1);
+    for (uint64_t d = 0; d <= nv; ++d) dt.h_row_ptr[d] = (uint32_t)rp[d];
+    std::vector<uint32_t> col(E);
+    std::vector<int64_t> dvid(E), rk(E);
+    const size_t nc = type > 0 ? st.props.size() : 0;
+    std::vector<std::vector<int64_t>> pc(nc, std::vector<int64_t>(E));
+    std::vector<uint8_t> valid(type > 0 ? E : 0);
+    bool any_rank = false, any_invalid = false;
+    std::vector<VKind> kinds(nc, VK_INT);
+    if (nc) {
+      const Schema* latest = edges[type].latest();
+      for (size_t c = 0; c < nc; ++c) kinds[c] = kindOfType(latest->cols[c].type);
+    }
+#pragma omp parallel for schedule(dynamic, 4096) reduction(|| : any_rank, any_invalid)
+    for (int64_t d = 0; d < (int64_t)nv; ++d) {
+      uint64_t o = rp[d];
+      for (uint32_t m = 0; m < live[d + 1]; ++m) {
+        const RowKey& k = keys[cnt[d] + m];
+        uint64_t i = k.idx;
+        col[o + m] = dense(st.dst[i]);
+        dvid[o + m] = st.dst[i];
+        rk[o + m] = st.rank[i];
+        if (st.rank[i]) any_rank = true;
+        for (size_t c = 0; c < nc; ++c) {
+          int64_t b = st.props[c][i];
+          if (kinds[c] == VK_STRING && st.valid[i]) b = remap[b];
+          pc[c][o + m] = b;
+        }
+        if (type > 0) {
+          valid[o + m] = st.valid[i];
+          if (!st.valid[i]) any_invalid = true;
+        }
+      }
+    }
+    // upload
+    auto up = [&](void** dst, const void* src, size_t bytes) -> bool {
+      if (!bytes) bytes = 8;
+      if (hipMalloc(dst, bytes) != hipSuccess) return false;
+      snap.device_bytes += bytes;
+      if (src && hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice) != hipSuccess) return false;
+      return true;
+    };
+    bool ok = up((void**)&dt.row_ptr, dt.h_row_ptr.data(), (nv + 1) * 4) &&
+              up((void**)&dt.col, col.data(), E * 4) && up((void**)&dt.dst_vid, dvid.data(), E * 8);
+    if (ok && any_rank) ok = up((void**)&dt.rank, rk.data(), E * 8);
+    dt.prop_kind = kinds;
+    dt.props.assign(nc, nullptr);
+    for (size_t c = 0; ok && c < nc; ++c) ok = up((void**)&dt.props[c], pc[c].data(), E * 8);
+    if (ok && any_invalid) ok = up((void**)&dt.valid, valid.data(), E);
+    if (ok && nc) {
+      ok = up((void**)&dt.d_props, dt.props.data(), nc * sizeof(int64_t*));
+    }
+    if (!ok) { rc = fail(NBG_E_OUT_OF_MEMORY, "device allocation failed for the snapshot"); break; }
+    uint32_t md = 0;
+    for (uint64_t d = 0; d < nv; ++d) md = std::max(md, live[d + 1]);
+    dt.max_degree = (int)md;
+    EdgeStage().src.swap(st.src);   // release staging as we go
+    st = EdgeStage();
+  }
+  if (rc) return rc;
+  bool ok = hipMalloc((void**)&snap.d_vids, std::max<uint64_t>(nv, 1) * 8) == hipSuccess &&
+            hipMemcpy(snap.d_vids, all.data(), nv * 8, hipMemcpyHostToDevice) == hipSuccess;
+  snap.device_bytes += nv * 8;
+  if (ok && !all_visible) {
+    ok = hipMalloc((void**)&snap.d_visible, nv) == hipSuccess &&
+         hipMemcpy(snap.d_visible, visible.data(), nv, hipMemcpyHostToDevice) == hipSuccess;
+    snap.device_bytes += nv;
+  }
+  if (!ok) return fail(NBG_E_OUT_OF_MEMORY, "device allocation failed for the vertex table");
+  stage.clear();
+  pool.clear();
+  pool_index.clear();
+  finalized = true;
+  return NBG_OK;
+}
+
+}  // namespace nbg

@@ -1,0 +1,189 @@
+// nebula_amd internal declarations (host side + kernel launch interface).
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/nbg.h"
+
+namespace nbg {
+
+constexpr uint32_t NO_ROW = 0xFFFFFFFFu;   // dst vertex has no rows on this rank
+
+// ----------------------------------------------------------------------------- schema
+struct Column {
+  std::string name;
+  int32_t type;   // NBG_T_*
+};
+struct Schema {
+  int64_t version = 0;
+  std::vector<Column> cols;
+  int find(const std::string& n) const {
+    for (size_t i = 0; i < cols.size(); ++i)
+      if (cols[i].name == n) return static_cast<int>(i);
+    return -1;
+  }
+};
+struct SchemaSet {   // all versions of one tag / edge type
+  std::string name;
+  std::map<int64_t, Schema> versions;
+  const Schema* latest() const { return versions.empty() ? nullptr : &versions.rbegin()->second; }
+  const Schema* at(int64_t v) const {
+    auto it = versions.find(v);
+    return it == versions.end() ? nullptr : &it->second;
+  }
+};
+
+// Value kinds on the device (VariantType alternatives).
+enum VKind : uint8_t { VK_INT = 0, VK_DOUBLE = 1, VK_BOOL = 2, VK_STRING = 3 };
+inline VKind kindOfType(int32_t t) {
+  switch (t) {
+    case NBG_T_BOOL: return VK_BOOL;
+    case NBG_T_FLOAT: case NBG_T_DOUBLE: return VK_DOUBLE;
+    case NBG_T_STRING: return VK_STRING;
+    default: return VK_INT;
+  }
+}
+
+// ----------------------------------------------------------------------------- host staging
+struct EdgeStage {              // one signed edge type, before finalize
+  std::vector<int64_t> src, dst, rank;
+  std::vector<uint64_t> verkey; // version bytes read big-endian (memcmp order)
+  std::vector<uint64_t> seq;    // load order (identical keys: later wins)
+  std::vector<int32_t> part;
+  std::vector<std::vector<int64_t>> props;   // [col][i] 8-byte payload (positive types)
+  std::vector<uint8_t> valid;                // value decoded (positive types)
+};
+
+// ----------------------------------------------------------------------------- device snapshot
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+struct DevEdgeType {            // CSR for one signed edge type over this rank's vertices
+  int32_t type = 0;
+  uint64_t num_edges = 0;
+  uint32_t* row_ptr = nullptr;  // [nV + 1]
+  uint32_t* col = nullptr;      // [E] dense id of dst, NO_ROW if the dst has no rows here
+  int64_t* dst_vid = nullptr;   // [E]
+  int64_t* rank = nullptr;      // [E] or nullptr when every rank is 0
+  std::vector<int64_t*> props;  // [ncols][E] (positive types)
+  int64_t** d_props = nullptr;  // device copy of `props`
+  std::vector<VKind> prop_kind;
+  uint8_t* valid = nullptr;     // [E] or nullptr when every value decoded
+  int max_degree = 0;
+  std::vector<uint32_t> h_row_ptr;   // host copy (path reconstruction, host planning)
+};
+
+struct Snapshot {
+  uint64_t nv = 0;
+  int64_t* d_vids = nullptr;            // dense id -> vid (sorted ascending, signed)
+  std::vector<int64_t> h_vids;
+  uint8_t* d_visible = nullptr;         // home part == hash part; nullptr when all visible
+  std::vector<int32_t> h_part;          // home part per dense id
+  std::map<int32_t, DevEdgeType> types; // signed type -> CSR
+  std::vector<std::string> strings;     // sorted dictionary; device code = 2 * index
+  uint64_t device_bytes = 0;
+};
+
+// ----------------------------------------------------------------------------- bytecode
+// One instruction of the per-edge program (WHERE / YIELD).  Registers are 8-byte slots.
+enum Op : uint8_t {
+  OP_END = 0,
+  OP_CONST,      // r[d] = imm
+  OP_COL,        // r[d] = props[aux][j]                (8-byte payload)
+  OP_COLV,       // like OP_COL but sets the error flag when the edge value is missing
+  OP_DST,        // r[d] = dst_vid[j]
+  OP_SRC,        // r[d] = vid of the source vertex
+  OP_RANK,       // r[d] = rank[j] (0 when no rank column)
+  OP_ERR,        // error flag := 1 (statically ill-typed node, still evaluated)
+  // int64
+  OP_ADD_I, OP_SUB_I, OP_MUL_I, OP_DIV_I, OP_MOD_I, OP_XOR_I, OP_NEG_I,
+  OP_LT_I, OP_LE_I, OP_GT_I, OP_GE_I, OP_EQ_I, OP_NE_I,
+  // double
+  OP_ADD_F, OP_SUB_F, OP_MUL_F, OP_DIV_F, OP_MOD_F, OP_XOR_F, OP_NEG_F,
+  OP_LT_F, OP_LE_F, OP_GT_F, OP_GE_F, OP_EQ_F, OP_NE_F,
+  // conversions / bool
+  OP_I2F, OP_B2I, OP_B2F, OP_F2I, OP_NOT,
+  OP_TRUTHY_I, OP_TRUTHY_F, OP_TRUTHY_S,   // asBool (string: code == imm, the empty string)
+  OP_AND, OP_OR, OP_XORB,
+  OP_COUNT_
+};
+
+struct Ins {
+  uint8_t op, d, a, b;
+  int32_t aux;
+  int64_t imm;
+};
+static_assert(sizeof(Ins) == 16, "Ins layout");
+
+constexpr int MAX_REGS = 16;
+constexpr int MAX_PROGRAM = 256;   // instructions per query/type (WHERE + all YIELDs)
+constexpr int MAX_YIELDS = 16;
+
+// A compiled query for one OVER edge type.
+struct TypeProgram {
+  int32_t etype = 0;
+  std::vector<Ins> code;           // WHERE first (if any), then each YIELD
+  int where_len = 0;               // instructions of the WHERE part
+  int where_reg = -1;              // register holding the WHERE value (-1: no WHERE)
+  VKind where_kind = VK_BOOL;
+  bool where_const = false;        // WHERE folded to a constant
+  bool where_const_val = true;
+  bool where_always_error = false;
+  std::vector<int> yield_reg;      // register per YIELD column (-1 = constant)
+  std::vector<VKind> yield_kind;
+  std::vector<int64_t> yield_const;   // constant payload when yield_reg == -1
+  std::vector<std::string> yield_const_str;   // string constants (may be absent from the dictionary)
+  bool needs_error_check = false;  // any op can raise an error
+  int nregs = 0;
+};
+
+// ----------------------------------------------------------------------------- kernel interface
+struct ExpandArgs {                // one (step, edge type) expansion
+  const uint32_t* frontier;        // [n] dense ids
+  uint64_t n;
+  const uint32_t* row_ptr;
+  const uint32_t* col;
+  const int64_t* dst_vid;
+  const int64_t* rank;
+  const uint8_t* valid;
+  const uint8_t* visible;
+  const int64_t* vids;             // dense id -> vid (for _src)
+  const int64_t* const* props;     // device array of column pointers
+  uint32_t cap;                    // max_edge_returned_per_vertex
+};
+
+struct Workspace;   // kernels.hip
+
+Workspace* ws_create(uint64_t max_frontier, uint64_t nv, hipStream_t s, std::string* err);
+void ws_destroy(Workspace* w);
+hipError_t ws_reserve_rows(Workspace* w, uint64_t rows, int ncols);
+
+// Returns total edges of this expansion (host sync inside).
+hipError_t k_degree_scan(Workspace* w, const ExpandArgs& a, uint64_t* total);
+// Intermediate step: mark next-frontier flags for every scanned edge.
+hipError_t k_expand_mark(Workspace* w, const ExpandArgs& a, uint64_t total);
+// Compact flags into the next frontier (sorted), clearing flags.  Returns the new size.
+hipError_t k_compact(Workspace* w, uint64_t nv, uint32_t* next, uint64_t* count);
+// Final step: evaluate program, emit rows at w->row_count.  err_out != 0 if any lane errored.
+hipError_t k_expand_final(Workspace* w, const ExpandArgs& a, uint64_t total, const TypeProgram& prog,
+                          const Ins* d_prog, int64_t** d_out_cols, uint64_t row_base,
+                          uint64_t* rows_out, int* err_out);
+
+// Frontier double buffers and other workspace accessors.
+uint32_t* ws_frontier(Workspace* w, int which);
+int64_t** ws_row_cols(Workspace* w);        // device array of output column pointers
+int64_t* ws_row_col(Workspace* w, int c);   // device pointer of output column c
+Ins* ws_program(Workspace* w);
+
+// Path kernels (FIND PATH) — kernels.hip
+struct BfsSide;
+
+}  // namespace nbg

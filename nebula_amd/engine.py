@@ -1,0 +1,234 @@
+"""Python host binding of the nebula_amd engine (include/nbg.h).
+
+Mirrors the reference's storage/graph operator surface for this path:
+  * ``Engine.register_edge/register_tag``  — meta SchemaManager (src/meta/SchemaManager.h:20-48)
+  * ``Engine.load_builder / load_part``     — KV records of a kvstore part
+  * ``Engine.go``                           — GoExecutor result semantics
+  * ``Engine.find_path``                    — FindPathExecutor result semantics
+The engine also implements the backend interface of ``nebula_amd.ngql.Session`` so nGQL text
+(GO / FIND PATH, pipes, variables) can be run against it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import struct
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib as L
+
+
+class NbgError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"nbg error {code}: {msg}")
+        self.code = code
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None and len(a) else None
+
+
+class DeviceRows:
+    """Rows of a ``go_device`` call, resident in HBM until freed or the next query."""
+
+    def __init__(self, eng, h):
+        self.eng, self.h = eng, h
+
+    @property
+    def count(self) -> int:
+        return self.eng.lib.nbg_rows_count(self.h)
+
+    @property
+    def edges_scanned(self) -> int:
+        return self.eng.lib.nbg_rows_edges_scanned(self.h)
+
+    def step_stats(self, cap=16):
+        f = (C.c_uint64 * cap)()
+        e = (C.c_uint64 * cap)()
+        k = self.eng.lib.nbg_rows_step_stats(self.h, f, e, cap)
+        return list(f[:k]), list(e[:k])
+
+    def device_col(self, c: int) -> int:
+        return self.eng.lib.nbg_rows_device_col(self.h, c) or 0
+
+    def fetch(self) -> List[list]:
+        rc = self.eng.lib.nbg_rows_fetch(self.h)
+        if rc:
+            raise NbgError(rc, "fetch failed")
+        return self.eng._host_rows(self.h)
+
+    def free(self):
+        if self.h:
+            self.eng.lib.nbg_rows_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.free()
+
+
+class Engine:
+    def __init__(self, num_parts: int, num_gpus: int = 1, rank: int = 0, device: int = 0,
+                 max_edge_returned_per_vertex: int = 0x7FFFFFFF):
+        self.lib = L.load()
+        cfg = L.nbg_config(num_parts, num_gpus, rank, device, max_edge_returned_per_vertex, 3, 10)
+        h = C.c_void_p()
+        rc = self.lib.nbg_create(C.byref(cfg), C.byref(h))
+        if rc:
+            raise NbgError(rc, "nbg_create failed")
+        self.h = h
+        self.edge_types, self.edge_names, self.tag_ids = {}, {}, {}
+        self.last_step_stats = None
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.nbg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def _check(self, rc, what):
+        if rc:
+            msg = self.lib.nbg_last_error(self.h)
+            raise NbgError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+    def _cols(self, cols):
+        arr = (L.nbg_column_def * max(1, len(cols)))()
+        self._keep = [c[0].encode() for c in cols]
+        for i, (name, t) in enumerate(cols):
+            arr[i].name = self._keep[i]
+            arr[i].type = t
+        return arr
+
+    def register_edge(self, etype: int, name: str, cols, ver: int = 0):
+        self._check(self.lib.nbg_register_edge(self.h, etype, name.encode(), ver, self._cols(cols), len(cols)),
+                    "register_edge")
+        self.edge_types[name] = etype
+        self.edge_names[etype] = name
+
+    def register_tag(self, tag: int, name: str, cols, ver: int = 0):
+        self._check(self.lib.nbg_register_tag(self.h, tag, name.encode(), ver, self._cols(cols), len(cols)),
+                    "register_tag")
+        self.tag_ids[name] = tag
+
+    def load_part(self, part, kd, ko, vd, vo, n):
+        self._check(self.lib.nbg_load_part_kv(self.h, part, _ptr(kd), _ptr(ko), _ptr(vd), _ptr(vo), n),
+                    "load_part_kv")
+
+    def load_builder(self, kb, finalize=True):
+        for p in sorted(kb.recs):
+            self.load_part(p, *kb.flat(p))
+        if finalize:
+            self.finalize()
+
+    def load_edges(self, etype: int, src: np.ndarray, dst: np.ndarray, props: Sequence[np.ndarray] = (),
+                   rank: Optional[np.ndarray] = None):
+        src = np.ascontiguousarray(src, np.int64)
+        dst = np.ascontiguousarray(dst, np.int64)
+        props = [np.ascontiguousarray(p) for p in props]
+        arr = (C.c_void_p * max(1, len(props)))(*[_ptr(p) for p in props])
+        rk = None if rank is None else np.ascontiguousarray(rank, np.int64)
+        self._check(self.lib.nbg_load_edges(self.h, etype, _ptr(src), _ptr(dst), _ptr(rk), len(src), arr,
+                                            len(props)), "load_edges")
+
+    def finalize(self):
+        self._check(self.lib.nbg_finalize(self.h), "finalize")
+
+    def stats(self):
+        s = L.nbg_stats()
+        self._check(self.lib.nbg_get_stats(self.h, C.byref(s)), "stats")
+        return {"num_vertices": s.num_vertices, "num_edges": s.num_edges, "device_bytes": s.device_bytes,
+                "num_edge_types": s.num_edge_types}
+
+    # ------------------------------------------------------------------ GO
+    def _go_request(self, starts, etypes, steps, where, yields, distinct, over_all):
+        s = np.ascontiguousarray(starts, np.int64)
+        t = np.ascontiguousarray(etypes, np.int32)
+        wb = np.frombuffer(where, np.uint8).copy() if where else None
+        ybufs = [np.frombuffer(y, np.uint8).copy() for y in yields]
+        yptrs = (C.POINTER(C.c_uint8) * max(1, len(ybufs)))(
+            *[y.ctypes.data_as(C.POINTER(C.c_uint8)) for y in ybufs])
+        ylens = (C.c_uint32 * max(1, len(ybufs)))(*[len(y) for y in ybufs])
+        req = L.nbg_go_request(
+            s.ctypes.data_as(C.POINTER(C.c_int64)) if len(s) else None, len(s),
+            t.ctypes.data_as(C.POINTER(C.c_int32)) if len(t) else None, len(t), int(over_all), steps,
+            wb.ctypes.data_as(C.POINTER(C.c_uint8)) if wb is not None else None, len(where or b""),
+            yptrs, ylens, len(ybufs), int(distinct))
+        return req, (s, t, wb, ybufs, yptrs, ylens)
+
+    def _host_rows(self, h):
+        n, nc = self.lib.nbg_rows_count(h), self.lib.nbg_rows_num_cols(h)
+        cols = []
+        for c in range(nc):
+            bits = np.ctypeslib.as_array(self.lib.nbg_rows_col_bits(h, c), shape=(n,)) if n else np.zeros(0, np.int64)
+            tags = np.ctypeslib.as_array(self.lib.nbg_rows_col_tags(h, c), shape=(n,)) if n else np.zeros(0, np.uint8)
+            col = []
+            for b, t in zip(bits.tolist(), tags.tolist()):
+                if t == 0:
+                    col.append(b)
+                elif t == 1:
+                    col.append(struct.unpack("<d", struct.pack("<q", b))[0])
+                elif t == 2:
+                    col.append(bool(b))
+                else:
+                    col.append(self.lib.nbg_rows_string(h, b).decode())
+            cols.append(col)
+        return [list(r) for r in zip(*cols)] if nc else [[] for _ in range(n)]
+
+    def go(self, starts, etypes, steps=1, where=b"", yields=(), distinct=False, over_all=False):
+        req, keep = self._go_request(starts, etypes, steps, where, yields, distinct, over_all)
+        out = C.c_void_p()
+        rc = self.lib.nbg_go(self.h, C.byref(req), C.byref(out))
+        self._check(rc, "go")
+        try:
+            self.last_step_stats = DeviceRows(self, None)
+            f = (C.c_uint64 * 16)()
+            e = (C.c_uint64 * 16)()
+            k = self.lib.nbg_rows_step_stats(out, f, e, 16)
+            self.last_step_stats = (list(f[:k]), list(e[:k]), self.lib.nbg_rows_edges_scanned(out))
+            return self._host_rows(out)
+        finally:
+            self.lib.nbg_rows_free(out)
+
+    def go_device(self, starts, etypes, steps=1, where=b"", yields=(), distinct=False, over_all=False) -> DeviceRows:
+        req, keep = self._go_request(starts, etypes, steps, where, yields, distinct, over_all)
+        out = C.c_void_p()
+        rc = self.lib.nbg_go_device(self.h, C.byref(req), C.byref(out))
+        self._check(rc, "go_device")
+        return DeviceRows(self, out)
+
+    # ------------------------------------------------------------------ FIND PATH
+    def find_path(self, frm, to, etypes, upto=5, shortest=True, over_all=False):
+        f = np.ascontiguousarray(frm, np.int64)
+        t = np.ascontiguousarray(to, np.int64)
+        e = np.ascontiguousarray(etypes, np.int32)
+        req = L.nbg_path_request(
+            f.ctypes.data_as(C.POINTER(C.c_int64)) if len(f) else None, len(f),
+            e.ctypes.data_as(C.POINTER(C.c_int32)) if len(e) else None, len(e), int(over_all),
+            t.ctypes.data_as(C.POINTER(C.c_int64)) if len(t) else None, len(t), upto, int(shortest))
+        out = C.c_void_p()
+        self._check(self.lib.nbg_find_path(self.h, C.byref(req), C.byref(out)), "find_path")
+        try:
+            paths = []
+            for i in range(self.lib.nbg_paths_count(out)):
+                n = self.lib.nbg_path_len(out, i)
+                ptr = self.lib.nbg_path_entries(out, i)
+                paths.append([int(ptr[k]) for k in range(n)])
+            return sorted(paths)
+        finally:
+            self.lib.nbg_paths_free(out)
+
+
+def nba_engine(data, parts=1, device=0):
+    """The TraverseTestBase dataset loaded through the KV path."""
+    from . import kvgen
+    e = Engine(parts, device=device)
+    for (kind, name), cols in kvgen.NBA_SCHEMAS.items():
+        if kind == "edge":
+            e.register_edge(kvgen.NBA_EDGES[name], name, cols)
+        else:
+            e.register_tag(kvgen.NBA_TAGS[name], name, cols)
+    e.load_builder(kvgen.nba_kv(data, parts))
+    return e

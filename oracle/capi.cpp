@@ -66,6 +66,25 @@ int32_t orc_load_part_kv(void* h, int32_t part, const uint8_t* kdata, const uint
   return 0;
 }
 
+// InsertEdgeExecutor restated for bulk fixtures (src/graph/InsertEdgeExecutor.cpp:180-196):
+// out-edge (src,+type,rank 0,dst) with RowWriter(schema) << props, in-edge (dst,-type,0,src)
+// with an empty value, one version for the batch (AddEdgesProcessor.cpp:17-20).
+int32_t orc_load_edges(void* h, int32_t etype, const int64_t* src, const int64_t* dst, uint64_t n,
+                       const int64_t* const* int_cols, int32_t ncols) {
+  auto* s = static_cast<Store*>(h);
+  const Schema* sc = s->edgeSchema(etype);
+  if (!sc || (int32_t)sc->cols.size() != ncols) return -1;
+  int64_t ver = (int64_t)__builtin_bswap64((uint64_t)(INT64_MAX - 1));
+  for (uint64_t i = 0; i < n; ++i) {
+    RowWriter w(sc);
+    for (int32_t c = 0; c < ncols; ++c) w.putInt(int_cols[c][i]);
+    int32_t ps = partOf(src[i], s->numParts), pd = partOf(dst[i], s->numParts);
+    s->parts[ps].push_back({edgeKey(ps, src[i], etype, 0, dst[i], ver), w.encode()});
+    s->parts[pd].push_back({edgeKey(pd, dst[i], -etype, 0, src[i], ver), std::string()});
+  }
+  return 0;
+}
+
 int32_t orc_finalize(void* h) {
   auto* s = static_cast<Store*>(h);
   for (auto& kv : s->parts) {

@@ -49,6 +49,8 @@ def lib():
         L.orc_path_get.argtypes = [vp, i64, vp]
         L.orc_go_timed.argtypes = [vp, vp, u64, vp, i32, u32, vp, u32, P(i64), P(u64)]
         L.orc_go_timed.restype = C.c_double
+        L.orc_load_edges.argtypes = [vp, i32, vp, vp, u64, P(vp), i32]
+        L.orc_load_edges.restype = i32
         _lib = L
     return _lib
 
@@ -93,6 +95,17 @@ class Oracle:
 
     def load_part(self, part, kd, ko, vd, vo, n):
         self.L.orc_load_part_kv(self.h, part, _ptr(kd), _ptr(ko), _ptr(vd), _ptr(vo), n)
+
+    def load_edges(self, etype, src, dst, int_cols=()):
+        src = np.ascontiguousarray(src, np.int64)
+        dst = np.ascontiguousarray(dst, np.int64)
+        cols = [np.ascontiguousarray(c, np.int64) for c in int_cols]
+        arr = (C.c_void_p * max(1, len(cols)))(*[_ptr(c) for c in cols])
+        rc = self.L.orc_load_edges(self.h, etype, _ptr(src), _ptr(dst), len(src), arr, len(cols))
+        assert rc == 0
+
+    def finalize(self):
+        self.L.orc_finalize(self.h)
 
     def load_builder(self, kb):
         for p in sorted(kb.recs):

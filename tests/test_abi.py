@@ -1,0 +1,61 @@
+"""CPU-side checks of the C ABI: the library loads, exports every symbol include/nbg.h declares,
+and the host-only calls (schemas, loading) behave without a GPU."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from nebula_amd import _lib, kvgen
+from nebula_amd.engine import Engine, NbgError
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    with open(os.path.join(ROOT, "include", "nbg.h")) as f:
+        src = f.read()
+    return sorted(set(re.findall(r"\b(nbg_[a-z_]+)\s*\(", src)))
+
+
+def test_header_symbols_exported():
+    L = _lib.load()
+    syms = header_symbols()
+    assert len(syms) >= 25
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+
+
+def test_signatures_cover_header():
+    declared = {n for n, _, _ in _lib.SIGNATURES}
+    assert set(header_symbols()) == declared
+
+
+def test_create_register_load_without_gpu():
+    e = Engine(num_parts=3)
+    e.register_edge(1, "e", [("w", kvgen.INT)])
+    e.register_tag(2, "t", [("name", kvgen.STRING)])
+    kb = kvgen.KVBuilder(3)
+    kb.insert_edge(1, 2, 1, 0, [("w", kvgen.INT)], [5], 1)
+    for p in sorted(kb.recs):
+        e.load_part(p, *kb.flat(p))
+    e.load_edges(1, np.array([3, 4]), np.array([4, 5]), [np.array([1, 2])])
+    # querying before finalize is a state error, not a crash
+    with pytest.raises(NbgError) as ex:
+        e.go([1], [1], 1)
+    assert ex.value.code == _lib.E_STATE
+    e.close()
+
+
+def test_invalid_config_rejected():
+    with pytest.raises(NbgError):
+        Engine(num_parts=0)
+    with pytest.raises(NbgError):
+        Engine(num_parts=4, num_gpus=2, rank=2)
+
+
+def test_bulk_load_rejects_unknown_type():
+    e = Engine(num_parts=1)
+    with pytest.raises(NbgError) as ex:
+        e.load_edges(9, np.array([1]), np.array([2]))
+    assert ex.value.code == _lib.E_EDGE_PROP_NOT_FOUND
