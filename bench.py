@@ -1,0 +1,218 @@
+#!/usr/bin/env python3
+"""nebula_amd benchmark — GO 3 STEPS traversed edges/sec (TEPS) on MI355X.
+
+Workload (BASELINE.json configs[1]): RMAT scale-22 (A .57/B .19/C .19,
+edge factor 16, seeded), 100 partitions, edge type e(w int); one "step" = the 64 queries
+``GO 3 STEPS FROM <root> OVER e WHERE e.w < 50`` (roots: seed 42, out-degree >= 1), each a
+separate query through the C ABI (nbg_go_device: result rows stay in HBM).
+TEPS = Σ_s E_s (adjacency entries scanned at every step, after version de-dup) / wall time.
+
+Multi-GPU (torch.distributed.run, one rank per GPU): every rank holds a replica of the
+snapshot and runs the same 64-query step ("replicas", weak scaling); value = Σ edges over
+ranks / max time over ranks.  The partitioned all-to-all path is not in this build yet.
+
+Also reported: the dominant kernel's achieved algorithmic HBM bandwidth (HIP events inside
+the library over the timed region) against the 8 TB/s peak, and the CPU oracle
+(storaged+graphd restatement, oracle/) on a bounded sample of the same queries.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scale", type=int, default=22)
+    ap.add_argument("--roots", type=int, default=64)
+    ap.add_argument("--parts", type=int, default=100)
+    ap.add_argument("--go-steps", type=int, default=3)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    import torch
+
+    from nebula_amd import Engine, expr as E, rmat
+
+    t0 = time.time()
+    src, dst, w = rmat.rmat_edges_fast(args.scale)
+    gen_s = time.time() - t0
+    eng = Engine(args.parts, device=local)
+    eng.register_edge(1, "e", [("w", 2)])
+    t0 = time.time()
+    eng.load_edges(1, src, dst, [w])
+    eng.finalize()
+    load_s = time.time() - t0
+    st = eng.stats()
+    log(f"[rank {rank}] RMAT-{args.scale}: {len(src)} samples, snapshot {st}, gen {gen_s:.1f}s load {load_s:.1f}s")
+    roots = [int(x) for x in rmat.pick_roots(src, args.roots, 42)]
+    where = E.binop("<", E.edge_prop("e", "w"), E.const(50)).encode()
+
+    def one_step():
+        scanned = rows = 0
+        lat = []
+        for r in roots:
+            q0 = time.perf_counter()
+            res = eng.go_device([r], [1], args.go_steps, where)
+            lat.append(time.perf_counter() - q0)
+            scanned += res.edges_scanned
+            rows += res.count
+            res.free()
+        return scanned, rows, lat
+
+    for _ in range(args.warmup):
+        one_step()
+    if not args.no_profile:
+        eng.profile(True)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    scanned = rows = 0
+    lats = []
+    for _ in range(args.steps):
+        s, r, lat = one_step()
+        scanned += s
+        rows += r
+        lats += lat
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kstats = eng.profile_read() if not args.no_profile else {}
+    if not args.no_profile:
+        eng.profile(False)
+
+    tot_scanned, max_elapsed = float(scanned), elapsed
+    if dist is not None:
+        t = torch.tensor([float(scanned), elapsed], dtype=torch.float64)
+        s_ = t.clone()
+        dist.all_reduce(s_[:1], op=dist.ReduceOp.SUM)
+        m_ = t.clone()
+        dist.all_reduce(m_[1:], op=dist.ReduceOp.MAX)
+        tot_scanned, max_elapsed = float(s_[0]), float(m_[1])
+
+    if rank != 0:
+        if dist is not None:
+            dist.barrier()
+        return
+
+    value = tot_scanned / max_elapsed
+    # dominant kernel roofline (HIP events over the timed region, inside the library)
+    roofline = None
+    kernels = {}
+    if kstats:
+        for k, v in kstats.items():
+            if v["launches"]:
+                kernels[k] = {"launches": v["launches"], "ms": round(v["ms"], 3),
+                              "algo_GBs": round(v["algo_bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None}
+        dom = max(kstats.items(), key=lambda kv: kv[1]["ms"])
+        name, v = dom
+        achieved = v["algo_bytes"] / (v["ms"] * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "avg_launch_us": round(v["ms"] * 1e3 / v["launches"], 2),
+                    "algo_bytes_per_launch": v["algo_bytes"] / v["launches"]}
+        total_ms = sum(x["ms"] for x in kstats.values())
+        total_bytes = sum(x["algo_bytes"] for x in kstats.values())
+        roofline["all_kernels_GBs"] = round(total_bytes / (total_ms * 1e-3) / 1e9, 1) if total_ms else None
+        roofline["kernel_time_frac_of_wall"] = round(total_ms * 1e-3 / elapsed, 3)
+
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(src, dst, w, roots, where, args)
+
+    lat_ms = np.array(lats) * 1e3
+    out = {
+        "metric": "GO 3 STEPS traversed edges/sec (TEPS)",
+        "value": value,
+        "unit": "TEPS",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": max_elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": f"synthetic RMAT-{args.scale} (seeded Graph500 Kronecker, edge factor 16, w uniform 0-99)",
+        "config": {"workload": f"GO {args.go_steps} STEPS FROM <root> OVER e WHERE e.w < 50 YIELD e._dst, "
+                               f"{len(roots)} single-root queries per step",
+                   "graph": f"RMAT-{args.scale}", "parts": args.parts, "roots": len(roots),
+                   "parallelism": "single" if world == 1 else f"replicas{world}",
+                   "vertices": st["num_vertices"], "live_edges_out_plus_in": st["num_edges"]},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "query_latency_ms": {"p50": float(np.percentile(lat_ms, 50)), "p90": float(np.percentile(lat_ms, 90)),
+                             "max": float(lat_ms.max())},
+        "rows_per_step": rows // max(1, args.steps),
+        "edges_per_step": scanned // max(1, args.steps),
+        "kernels": kernels,
+        "load_seconds": round(load_s, 2),
+    }
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+
+
+def cpu_baseline(src, dst, w, roots, where, args):
+    """oracle/ (storaged+graphd restated, RocksDB/thrift excluded) timed on the host cores."""
+    try:
+        from tests.support.oracle import Oracle
+    except Exception as ex:  # pragma: no cover
+        log(f"cpu baseline unavailable: {ex}")
+        return None
+    t0 = time.time()
+    handlers = 10   # FLAGS_max_handlers_per_req
+    o = Oracle(args.parts, threads=handlers)
+    o.L.orc_set_hosts(o.h, 1)
+    o.register(True, 1, "e", [("w", 2)])
+    o.load_edges(1, src, dst, [w])
+    o.finalize()
+    log(f"cpu baseline store built in {time.time() - t0:.1f}s")
+    secs = scanned = 0.0
+    n = 0
+    for r in roots:
+        s, rows, sc = o.go_timed([r], [1], args.go_steps, where)
+        secs += s
+        scanned += sc
+        n += 1
+        if secs >= args.cpu_seconds:
+            break
+    o.close()
+    return {"value": scanned / secs if secs else None, "unit": "TEPS", "cores": handlers, "kind": "port",
+            "sample": f"first {n} of the {len(roots)} roots (same graph and query), {secs:.1f}s; one storaged "
+                      f"host, {handlers} handler threads (max_handlers_per_req), RowSet encode/decode per hop, "
+                      f"RocksDB/thrift/RPC excluded"}
+
+
+if __name__ == "__main__":
+    main()

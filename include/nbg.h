@@ -182,6 +182,18 @@ int64_t nbg_path_len(const nbg_paths* p, int64_t i);
 const int64_t* nbg_path_entries(const nbg_paths* p, int64_t i);
 void nbg_paths_free(nbg_paths* p);
 
+/* ---- in-library kernel timing (HIP events on the engine's stream) ----------------------- */
+typedef struct {
+  const char* name;           /* kernel name (static string)                                  */
+  uint64_t launches;
+  double total_ms;            /* sum of event-measured launch durations                        */
+  double algo_bytes;          /* algorithmic HBM bytes of those launches */
+} nbg_kernel_stat;
+/* enable != 0 starts (and resets) per-kernel timing; 0 stops it. */
+int32_t nbg_profile(nbg_engine* e, int32_t enable);
+/* Copies up to cap kernel records; returns the number of kernels. */
+int32_t nbg_profile_read(const nbg_engine* e, nbg_kernel_stat* out, int32_t cap);
+
 /* ---- multi-GPU (one process per GPU, RCCL over xGMI) ----------------------------------- */
 #define NBG_UNIQUE_ID_BYTES 128
 int32_t nbg_comm_unique_id(uint8_t out[NBG_UNIQUE_ID_BYTES]);

@@ -45,6 +45,10 @@ class nbg_stats(C.Structure):
                 ("num_edge_types", i32), ("reserved", i32)]
 
 
+class nbg_kernel_stat(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("launches", u64), ("total_ms", C.c_double), ("algo_bytes", C.c_double)]
+
+
 class nbg_go_request(C.Structure):
     _fields_ = [("starts", P(i64)), ("num_starts", u64), ("edge_types", P(i32)), ("num_edge_types", i32),
                 ("over_all", i32), ("steps", u32), ("where", P(u8)), ("where_len", u32),
@@ -84,6 +88,8 @@ SIGNATURES = [
     ("nbg_path_len", i64, [vp, i64]),
     ("nbg_path_entries", P(i64), [vp, i64]),
     ("nbg_paths_free", None, [vp]),
+    ("nbg_profile", i32, [vp, i32]),
+    ("nbg_profile_read", i32, [vp, vp, i32]),
     ("nbg_comm_unique_id", i32, [P(u8)]),
     ("nbg_comm_init", i32, [vp, P(u8), i32, i32]),
 ]

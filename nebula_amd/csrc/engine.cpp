@@ -482,6 +482,19 @@ const void* nbg_rows_device_col(const nbg_rows* r, int32_t col) {
 }
 void nbg_rows_free(nbg_rows* r) { delete r; }
 
+int32_t nbg_profile(nbg_engine* h, int32_t enable) {
+  if (!h) return NBG_E_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lg(h->e.mu);
+  if (!h->e.ws) return h->e.fail(NBG_E_STATE, "engine not finalized");
+  ws_profile(h->e.ws, enable != 0);
+  return NBG_OK;
+}
+
+int32_t nbg_profile_read(const nbg_engine* h, nbg_kernel_stat* out, int32_t cap) {
+  if (!h || !out || !h->e.ws) return 0;
+  return ws_profile_read(h->e.ws, out, cap);
+}
+
 int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* req, nbg_paths** out);
 
 int64_t nbg_paths_count(const nbg_paths* p) { return p ? (int64_t)p->paths.size() : -1; }

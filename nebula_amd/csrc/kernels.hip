@@ -33,7 +33,29 @@ constexpr int VT = 4;                            // k_expand: path items per thr
 constexpr int TILE = BLOCK * VT;                 // 1024 path items per tile
 constexpr int FLAG_BYTES = BLOCK * 16;           // k_flag_*: bytes per block
 
+enum KernelId { K_DEGREE = 0, K_SCAN, K_PARTITION, K_EXPAND_MARK, K_FLAG_COUNT, K_FLAG_WRITE, K_EXPAND_FINAL,
+                K_BFS, K_COUNT };
+static const char* const kKernelNames[K_COUNT] = {"k_degree", "k_scan_blocks", "k_partition", "k_expand<MARK>",
+                                                  "k_flag_count", "k_flag_write", "k_expand<FINAL>", "k_expand<BFS>"};
+
+struct Prof {
+  bool on = false;
+  struct Rec { int kid; hipEvent_t a, b; double bytes; };
+  std::vector<Rec> pending;
+  std::vector<hipEvent_t> pool;
+  uint64_t launches[K_COUNT] = {};
+  double ms[K_COUNT] = {};
+  double bytes[K_COUNT] = {};
+  hipEvent_t get() {
+    if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+};
+
 struct Workspace {
+  Prof prof;
   hipStream_t stream = nullptr;
   uint64_t cap_frontier = 0;      // entries in each frontier / scan buffer
   uint64_t nv = 0;
@@ -447,6 +469,56 @@ __global__ void __launch_bounds__(BLOCK) k_flag_write(uint8_t* __restrict__ flag
 // ============================================================================= host wrappers
 static inline uint64_t cdiv(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
+// Kernel timing: an event pair around each launch on the workspace stream, resolved at the
+// next host synchronisation point.
+static hipEvent_t prof_begin(Workspace* w) {
+  if (!w->prof.on) return nullptr;
+  hipEvent_t a = w->prof.get();
+  (void)hipEventRecord(a, w->stream);
+  return a;
+}
+static void prof_end(Workspace* w, hipEvent_t a, int kid, double bytes) {
+  if (!a) return;
+  hipEvent_t b = w->prof.get();
+  (void)hipEventRecord(b, w->stream);
+  w->prof.pending.push_back({kid, a, b, bytes});
+}
+static void prof_flush(Workspace* w) {
+  for (auto& r : w->prof.pending) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+      w->prof.launches[r.kid]++;
+      w->prof.ms[r.kid] += ms;
+      w->prof.bytes[r.kid] += r.bytes;
+    }
+    w->prof.pool.push_back(r.a);
+    w->prof.pool.push_back(r.b);
+  }
+  w->prof.pending.clear();
+}
+
+void ws_profile(Workspace* w, bool on) {
+  if (!w) return;
+  prof_flush(w);
+  w->prof.on = on;
+  if (on) {
+    for (int k = 0; k < K_COUNT; ++k) { w->prof.launches[k] = 0; w->prof.ms[k] = 0; w->prof.bytes[k] = 0; }
+  }
+}
+
+int ws_profile_read(Workspace* w, nbg_kernel_stat* out, int cap) {
+  if (!w) return 0;
+  int n = 0;
+  for (int k = 0; k < K_COUNT && n < cap; ++k) {
+    out[n].name = kKernelNames[k];
+    out[n].launches = w->prof.launches[k];
+    out[n].total_ms = w->prof.ms[k];
+    out[n].algo_bytes = w->prof.bytes[k];
+    ++n;
+  }
+  return n;
+}
+
 Workspace* ws_create(uint64_t max_frontier, uint64_t nv, hipStream_t s, std::string* err) {
   auto* w = new Workspace();
   w->stream = s;
@@ -521,12 +593,17 @@ hipError_t k_degree_scan(Workspace* w, const ExpandArgs& a, uint64_t* total) {
   if (a.n == 0) { *total = 0; return hipSuccess; }
   if (a.n > w->cap_frontier) return hipErrorInvalidValue;
   uint64_t nb = cdiv(a.n, SCAN_TILE);
+  hipEvent_t p = prof_begin(w);
   hipLaunchKernelGGL(k_degree, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, a.frontier, a.n, a.row_ptr,
                      a.visible, a.cap, w->seg_end, w->seg_rs, w->block_sum);
+  prof_end(w, p, K_DEGREE, 12.0 * (double)a.n);   // 4|F| ids + 8|F| row_ptr pairs
+  p = prof_begin(w);
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, w->stream, w->block_sum, nb, w->counters);
+  prof_end(w, p, K_SCAN, 0.0);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(w->h_pinned, w->counters, 8, hipMemcpyDeviceToHost, w->stream));
   HIP_TRY(hipStreamSynchronize(w->stream));
+  prof_flush(w);
   *total = w->h_pinned[0];
   return hipSuccess;
 }
@@ -534,8 +611,10 @@ hipError_t k_degree_scan(Workspace* w, const ExpandArgs& a, uint64_t* total) {
 static hipError_t launch_partition(Workspace* w, const ExpandArgs& a, uint64_t total, uint64_t* ntiles_out) {
   uint64_t ntiles = cdiv(a.n + total, TILE);
   HIP_TRY(ensure_tiles(w, ntiles));
+  hipEvent_t p = prof_begin(w);
   hipLaunchKernelGGL(k_partition, dim3((unsigned)cdiv(ntiles + 1, 256)), dim3(256), 0, w->stream, w->seg_end,
                      w->block_sum, a.n, total, ntiles, w->part);
+  prof_end(w, p, K_PARTITION, 0.0);
   *ntiles_out = ntiles;
   return hipGetLastError();
 }
@@ -545,23 +624,47 @@ hipError_t k_expand_mark(Workspace* w, const ExpandArgs& a, uint64_t total) {
   uint64_t ntiles;
   HIP_TRY(launch_partition(w, a, total, &ntiles));
   FinalParams fp{};
+  hipEvent_t p = prof_begin(w);
   hipLaunchKernelGGL(k_expand<MARK>, dim3((unsigned)ntiles), dim3(BLOCK), 0, w->stream, a, w->seg_end,
                      w->block_sum, w->seg_rs, w->part, total, w->flags, fp);
+  prof_end(w, p, K_EXPAND_MARK, 4.0 * (double)total);   // 4 E_s neighbour ids
   return hipGetLastError();
 }
 
 hipError_t k_compact(Workspace* w, uint64_t nv, uint32_t* next, uint64_t* count) {
   uint64_t nb = w->flag_bytes / FLAG_BYTES;
+  hipEvent_t p = prof_begin(w);
   hipLaunchKernelGGL(k_flag_count, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->flags, w->flag_bytes,
                      w->flag_blocks);
+  prof_end(w, p, K_FLAG_COUNT, 0.0);
+  p = prof_begin(w);
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, w->stream, w->flag_blocks, nb, w->counters);
+  prof_end(w, p, K_SCAN, 0.0);
+  p = prof_begin(w);
   hipLaunchKernelGGL(k_flag_write, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->flags, w->flag_bytes, nv,
                      w->flag_blocks, next);
+  prof_end(w, p, K_FLAG_WRITE, 0.0);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(w->h_pinned, w->counters, 8, hipMemcpyDeviceToHost, w->stream));
   HIP_TRY(hipStreamSynchronize(w->stream));
   *count = w->h_pinned[0];
+  if (!w->prof.pending.empty()) w->prof.pending.back().bytes = 4.0 * (double)*count;   // write F_{s+1}
+  prof_flush(w);
   return hipSuccess;
+}
+
+// distinct 8-byte edge columns a program reads per edge (props, _dst, _rank)
+static int edge_columns_read(const TypeProgram& prog) {
+  uint64_t seen = 0;
+  int n = 0;
+  for (auto& ins : prog.code) {
+    int key = -1;
+    if (ins.op == OP_COL || ins.op == OP_COLV) key = 2 + (ins.aux & 31);
+    else if (ins.op == OP_DST) key = 0;
+    else if (ins.op == OP_RANK) key = 1;
+    if (key >= 0 && !(seen & (1ull << key))) { seen |= 1ull << key; ++n; }
+  }
+  return n;
 }
 
 hipError_t k_expand_final(Workspace* w, const ExpandArgs& a, uint64_t total, const TypeProgram& prog,
@@ -578,9 +681,11 @@ hipError_t k_expand_final(Workspace* w, const ExpandArgs& a, uint64_t total, con
   fp.where_reg = prog.where_reg;
   fp.prog_len = (int)prog.code.size();
   fp.nyields = (int)prog.yield_reg.size();
+  int kout = 0;
   for (int y = 0; y < fp.nyields; ++y) {
     fp.yield_reg[y] = prog.yield_reg[y];
     fp.yield_const[y] = prog.yield_const[y];
+    kout += 1;
   }
   fp.out_cols = d_out_cols;
   fp.row_base = row_base;
@@ -588,13 +693,17 @@ hipError_t k_expand_final(Workspace* w, const ExpandArgs& a, uint64_t total, con
   fp.err_flag = w->counters + 2;
   HIP_TRY(hipMemsetAsync(w->counters + 1, 0, 2 * sizeof(uint64_t), w->stream));
   size_t lds = (size_t)(prog.nregs > 0 ? prog.nregs : 1) * BLOCK * sizeof(int64_t);
+  hipEvent_t p = prof_begin(w);
   hipLaunchKernelGGL(k_expand<FINAL>, dim3((unsigned)ntiles), dim3(BLOCK), lds, w->stream, a, w->seg_end,
                      w->block_sum, w->seg_rs, w->part, total, w->flags, fp);
+  prof_end(w, p, K_EXPAND_FINAL, 8.0 * (double)total * edge_columns_read(prog));
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(w->h_pinned, w->counters, 24, hipMemcpyDeviceToHost, w->stream));
   HIP_TRY(hipStreamSynchronize(w->stream));
   *rows_out = w->h_pinned[1];
   *err_out = w->h_pinned[2] != 0;
+  if (!w->prof.pending.empty()) w->prof.pending.back().bytes += 8.0 * (double)*rows_out * kout;   // R * 8k
+  prof_flush(w);
   return hipSuccess;
 }
 

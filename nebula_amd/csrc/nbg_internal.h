@@ -164,6 +164,8 @@ struct Workspace;   // kernels.hip
 
 Workspace* ws_create(uint64_t max_frontier, uint64_t nv, hipStream_t s, std::string* err);
 void ws_destroy(Workspace* w);
+void ws_profile(Workspace* w, bool on);
+int ws_profile_read(Workspace* w, nbg_kernel_stat* out, int cap);
 hipError_t ws_reserve_rows(Workspace* w, uint64_t rows, int ncols);
 
 // Returns total edges of this expansion (host sync inside).

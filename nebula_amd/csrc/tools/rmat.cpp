@@ -1,0 +1,37 @@
+// Bench/test tooling (not the engine): the deterministic RMAT generator of nebula_amd/rmat.py
+// restated in C++/OpenMP so RMAT-22..26 inputs are produced in seconds.  Bit-identical to the
+// numpy version (tests/test_rmat.py checks it).
+#include <omp.h>
+
+#include <cstdint>
+
+namespace {
+inline uint64_t mix(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+inline uint64_t splitmix64(uint64_t x) { return mix(x + 0x9E3779B97F4A7C15ull); }
+}  // namespace
+
+extern "C" int nbgtool_rmat(int scale, int edge_factor, uint64_t seed, int64_t* src, int64_t* dst, int64_t* w) {
+  const uint64_t n = (uint64_t)edge_factor << scale;
+  const uint64_t ta = (uint64_t)(0.57 * 9007199254740992.0);
+  const uint64_t tab = (uint64_t)((0.57 + 0.19) * 9007199254740992.0);
+  const uint64_t tabc = (uint64_t)((0.57 + 0.19 + 0.19) * 9007199254740992.0);
+#pragma omp parallel for schedule(static, 65536)
+  for (int64_t ii = 0; ii < (int64_t)n; ++ii) {
+    uint64_t i = (uint64_t)ii, u = 0, v = 0, base = i * 64;
+    for (int l = 0; l < scale; ++l) {
+      uint64_t r = splitmix64(seed ^ (base + (uint64_t)l)) >> 11;
+      uint64_t bu = r >= tab;
+      uint64_t bv = ((r >= ta) && (r < tab)) || (r >= tabc);
+      u |= bu << l;
+      v |= bv << l;
+    }
+    src[i] = (int64_t)(mix(u + seed) & 0x7FFFFFFFFFFFFFFFull);
+    dst[i] = (int64_t)(mix(v + seed) & 0x7FFFFFFFFFFFFFFFull);
+    w[i] = (int64_t)(splitmix64(seed ^ ~i) % 100);
+  }
+  return 0;
+}

@@ -142,6 +142,16 @@ class Engine:
         return {"num_vertices": s.num_vertices, "num_edges": s.num_edges, "device_bytes": s.device_bytes,
                 "num_edge_types": s.num_edge_types}
 
+    # ------------------------------------------------------------------ profiling
+    def profile(self, enable: bool = True):
+        self._check(self.lib.nbg_profile(self.h, int(enable)), "profile")
+
+    def profile_read(self):
+        arr = (L.nbg_kernel_stat * 32)()
+        n = self.lib.nbg_profile_read(self.h, arr, 32)
+        return {arr[i].name.decode(): {"launches": arr[i].launches, "ms": arr[i].total_ms,
+                                       "algo_bytes": arr[i].algo_bytes} for i in range(n)}
+
     # ------------------------------------------------------------------ GO
     def _go_request(self, starts, etypes, steps, where, yields, distinct, over_all):
         s = np.ascontiguousarray(starts, np.int64)

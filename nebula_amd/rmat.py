@@ -62,6 +62,23 @@ def rmat_edges(scale: int, edge_factor: int = 16, seed: int | None = None, chunk
     return src, dst, w
 
 
+def rmat_edges_fast(scale: int, edge_factor: int = 16, seed: int | None = None):
+    """Same output as rmat_edges, produced by the C++/OpenMP tool (libnbgtools.so)."""
+    import ctypes as C
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libnbgtools.so")
+    if not os.path.exists(path):
+        return rmat_edges(scale, edge_factor, seed)
+    lib = C.CDLL(path)
+    lib.nbgtool_rmat.argtypes = [C.c_int, C.c_int, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
+    seed = (SEED_BASE ^ scale) if seed is None else seed
+    n = edge_factor << scale
+    src, dst, w = (np.empty(n, np.int64) for _ in range(3))
+    lib.nbgtool_rmat(scale, edge_factor, seed & 0xFFFFFFFFFFFFFFFF, src.ctypes.data, dst.ctypes.data,
+                     w.ctypes.data)
+    return src, dst, w
+
+
 def dedup_last(src, dst, w):
     """Collapse duplicate (src, dst) samples keeping the last one (for reference counting)."""
     key = np.stack([src, dst], axis=1)

@@ -34,6 +34,8 @@ void orc_set_config(void* h, int32_t max_edge_per_vertex, int32_t min_vertices_p
   s->threads = threads;
 }
 
+void orc_set_hosts(void* h, int32_t hosts) { static_cast<Store*>(h)->hosts = hosts < 1 ? 1 : hosts; }
+
 int32_t orc_register_schema(void* h, int32_t is_edge, int32_t id, const char* name, int64_t ver,
                             int32_t ncols, const char* const* names, const int32_t* types) {
   auto* s = static_cast<Store*>(h);
@@ -58,10 +60,9 @@ int32_t orc_load_part_kv(void* h, int32_t part, const uint8_t* kdata, const uint
                          const uint8_t* vdata, const uint64_t* voffs, uint64_t n) {
   auto* s = static_cast<Store*>(h);
   auto& v = s->parts[part];
-  v.reserve(v.size() + n);
   for (uint64_t i = 0; i < n; ++i) {
-    v.push_back({std::string(reinterpret_cast<const char*>(kdata) + koffs[i], koffs[i + 1] - koffs[i]),
-                 std::string(reinterpret_cast<const char*>(vdata) + voffs[i], voffs[i + 1] - voffs[i])});
+    v.add({reinterpret_cast<const char*>(kdata) + koffs[i], koffs[i + 1] - koffs[i]},
+          {reinterpret_cast<const char*>(vdata) + voffs[i], voffs[i + 1] - voffs[i]});
   }
   return 0;
 }
@@ -79,26 +80,18 @@ int32_t orc_load_edges(void* h, int32_t etype, const int64_t* src, const int64_t
     RowWriter w(sc);
     for (int32_t c = 0; c < ncols; ++c) w.putInt(int_cols[c][i]);
     int32_t ps = partOf(src[i], s->numParts), pd = partOf(dst[i], s->numParts);
-    s->parts[ps].push_back({edgeKey(ps, src[i], etype, 0, dst[i], ver), w.encode()});
-    s->parts[pd].push_back({edgeKey(pd, dst[i], -etype, 0, src[i], ver), std::string()});
+    s->parts[ps].add(edgeKey(ps, src[i], etype, 0, dst[i], ver), w.encode());
+    s->parts[pd].add(edgeKey(pd, dst[i], -etype, 0, src[i], ver), std::string_view());
   }
   return 0;
 }
 
 int32_t orc_finalize(void* h) {
   auto* s = static_cast<Store*>(h);
-  for (auto& kv : s->parts) {
-    auto& v = kv.second;
-    // stable sort then keep the LAST of equal keys (last write wins)
-    std::stable_sort(v.begin(), v.end(), [](const KV& a, const KV& b) { return a.key < b.key; });
-    std::vector<KV> out;
-    out.reserve(v.size());
-    for (size_t i = 0; i < v.size(); ++i) {
-      if (i + 1 < v.size() && v[i + 1].key == v[i].key) continue;
-      out.push_back(std::move(v[i]));
-    }
-    v.swap(out);
-  }
+  std::vector<PartKV*> ps;
+  for (auto& kv : s->parts) ps.push_back(&kv.second);
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int64_t i = 0; i < (int64_t)ps.size(); ++i) ps[i]->finalize();
   return 0;
 }
 

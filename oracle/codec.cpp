@@ -155,7 +155,7 @@ std::string RowWriter::encode() {
 
 // ---------------------------------------------------------------- RowReader
 // RowReader::getSchemaVer (RowReader.cpp:172-200)
-int32_t rowSchemaVer(const std::string& row) {
+int32_t rowSchemaVer(std::string_view row) {
   if (row.empty()) return 0;
   const uint8_t* it = reinterpret_cast<const uint8_t*>(row.data());
   size_t vb = it[0] >> 5;
@@ -168,7 +168,7 @@ int32_t rowSchemaVer(const std::string& row) {
 }
 
 // RowReader::processHeader (RowReader.cpp:217-258)
-RowReader::RowReader(const std::string& row, const Schema* s) : schema(s) {
+RowReader::RowReader(std::string_view row, const Schema* s) : schema(s) {
   if (row.empty() || !s) return;
   const uint8_t* it = reinterpret_cast<const uint8_t*>(row.data());
   int offBytes = (it[0] & 0x07) + 1;

@@ -561,7 +561,7 @@ int32_t runShortestBfs(const Store& st, const FindPathQuery& q, std::vector<std:
       auto rng = st.prefixRange(part, edgePrefix(part, v, t));
       int64_t lr = -1, ld = 0; bool first = true; int cnt = 0;
       for (size_t i = rng.first; i < rng.second && cnt < st.maxEdgePerVertex; ++i) {
-        int64_t rk = keyRank(kvs[i].key.data()), d = keyDst(kvs[i].key.data());
+        int64_t rk = keyRank(kvs.key(i).data()), d = keyDst(kvs.key(i).data());
         if (!first && rk == lr && d == ld) continue;
         lr = rk; ld = d; first = false; ++cnt;
         res.push_back({d, t, rk});

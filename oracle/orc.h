@@ -16,6 +16,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <string_view>
 #include <unordered_map>
 #include <unordered_set>
 #include <variant>
@@ -128,14 +129,14 @@ struct RowReader {
   size_t len = 0;
   bool valid = false;
   std::vector<int64_t> offsets;    // offset of field i (computed lazily, sequential)
-  RowReader(const std::string& row, const Schema* s);
+  RowReader(std::string_view row, const Schema* s);
   // returns false on invalid data
   bool fieldOffset(int idx, int64_t& off);
   // getPropByName semantics; error -> !ok
   OptValue get(const std::string& name);
   OptValue getIdx(int idx);
 };
-int32_t rowSchemaVer(const std::string& row);
+int32_t rowSchemaVer(std::string_view row);
 bool decodeVarint(const uint8_t* p, size_t avail, uint64_t& v, int& len);
 // RowReader::getDefaultProp (src/dataman/RowReader.h:91-116)
 OptValue defaultProp(const Schema& s, const std::string& prop);
@@ -179,7 +180,23 @@ std::unique_ptr<Expr> decodeExpr(const uint8_t* buf, size_t len, std::string* er
 bool asBool(const Value& v);
 
 // ---------------------------------------------------------------- store
-struct KV { std::string key, val; };
+// One kvstore part: records appended in write order into byte arenas; finalize() sorts them
+// bytewise (RocksDB's default comparator) keeping the last write of identical keys.
+struct PartKV {
+  std::string karena, varena;
+  std::vector<uint64_t> koff{0}, voff{0};
+  std::vector<uint32_t> order;   // sorted record ids (after finalize)
+  void add(std::string_view k, std::string_view v) {
+    karena.append(k.data(), k.size()); koff.push_back(karena.size());
+    varena.append(v.data(), v.size()); voff.push_back(varena.size());
+  }
+  std::string_view rkey(uint32_t r) const { return {karena.data() + koff[r], koff[r + 1] - koff[r]}; }
+  std::string_view rval(uint32_t r) const { return {varena.data() + voff[r], voff[r + 1] - voff[r]}; }
+  size_t size() const { return order.size(); }
+  std::string_view key(size_t i) const { return rkey(order[i]); }
+  std::string_view val(size_t i) const { return rval(order[i]); }
+  void finalize();
+};
 
 struct Store {
   int32_t numParts = 1;
@@ -187,7 +204,8 @@ struct Store {
   int32_t minVerticesPerBucket = 3;        // FLAGS_min_vertices_per_bucket
   int32_t maxHandlersPerReq = 10;          // FLAGS_max_handlers_per_req
   int32_t threads = 1;                     // worker threads for bucket parallelism
-  std::map<int32_t, std::vector<KV>> parts;        // part -> sorted KV (memcmp)
+  std::map<int32_t, PartKV> parts;                 // part -> sorted KV (memcmp)
+  int32_t hosts = 1;                       // storaged hosts (part p -> host p % hosts)
   std::unordered_map<int32_t, std::map<int64_t, Schema>> edgeSchemas, tagSchemas;
   std::unordered_map<int32_t, std::string> edgeNames, tagNames;
   std::unordered_map<std::string, int32_t> edgeByName, tagByName;

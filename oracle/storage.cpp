@@ -32,12 +32,29 @@ const Schema* Store::tagSchema(int32_t tag, int64_t ver) const {
 std::pair<size_t, size_t> Store::prefixRange(int32_t part, const std::string& prefix) const {
   auto it = parts.find(part);
   if (it == parts.end()) return {0, 0};
-  const auto& v = it->second;
-  auto lo = std::lower_bound(v.begin(), v.end(), prefix,
-                             [](const KV& a, const std::string& p) { return a.key < p; });
-  auto hi = lo;
-  while (hi != v.end() && hi->key.compare(0, prefix.size(), prefix) == 0) ++hi;
-  return {static_cast<size_t>(lo - v.begin()), static_cast<size_t>(hi - v.begin())};
+  const PartKV& v = it->second;
+  size_t lo = 0, hi = v.size();
+  while (lo < hi) {
+    size_t mid = (lo + hi) / 2;
+    if (v.key(mid) < std::string_view(prefix)) lo = mid + 1; else hi = mid;
+  }
+  size_t e = lo;
+  while (e < v.size() && v.key(e).substr(0, prefix.size()) == prefix) ++e;
+  return {lo, e};
+}
+
+// stable bytewise sort; identical keys keep the LAST write (RocksDB write-batch semantics)
+void PartKV::finalize() {
+  uint32_t n = (uint32_t)(koff.size() - 1);
+  std::vector<uint32_t> idx(n);
+  for (uint32_t i = 0; i < n; ++i) idx[i] = i;
+  std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return rkey(a) < rkey(b); });
+  order.clear();
+  order.reserve(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (i + 1 < n && rkey(idx[i + 1]) == rkey(idx[i])) continue;
+    order.push_back(idx[i]);
+  }
 }
 
 namespace {
@@ -215,8 +232,8 @@ struct Processor {
     bool firstLoop = true;
     int cnt = 0;
     for (size_t i = rng.first; i < rng.second && cnt < st.maxEdgePerVertex; ++i) {
-      const std::string& key = kvs[i].key;
-      const std::string& val = kvs[i].val;
+      std::string_view key = kvs.key(i);
+      std::string_view val = kvs.val(i);
       int64_t rank = keyRank(key.data()), dst = keyDst(key.data());
       if (!firstLoop && rank == lastRank && lastDst == dst) continue;   // older version
       lastRank = rank; lastDst = dst;
@@ -244,9 +261,9 @@ struct Processor {
                              TagFilters* tf, RowWriter& w) {
     auto rng = st.prefixRange(part, vertexPrefix(part, vid, tag));
     if (rng.first == rng.second) return E_KEY_NOT_FOUND;
-    const auto& kv = st.parts.at(part)[rng.first];
-    RowReader r(kv.val, st.tagSchema(tag, rowSchemaVer(kv.val)));
-    collectProps(&r, kv.key.data(), props, tf, w);
+    const PartKV& kvs = st.parts.at(part);
+    RowReader r(kvs.val(rng.first), st.tagSchema(tag, rowSchemaVer(kvs.val(rng.first))));
+    collectProps(&r, kvs.key(rng.first).data(), props, tf, w);
     return E_SUCCEEDED;
   }
 
@@ -355,12 +372,33 @@ QueryResponse getVertexProps(const Store& st, const GNRequest& req) { return pro
 QueryResponse getNeighbors(const Store& st, const std::vector<int64_t>& vids,
                            const std::vector<int32_t>& etypes, const std::string& filter,
                            const std::vector<PropDef>& returns) {
-  GNRequest req;
-  for (auto v : vids) req.parts[partOf(v, st.numParts)].push_back(v);
-  req.edgeTypes = etypes;
-  req.filter = filter;
-  req.returns = returns;
-  return getBound(st, req);
+  // clusterIdsToHosts: one request per storaged host holding all of that host's parts
+  // (StorageClient.h:240-260); part p lives on host p % hosts (CreateSpaceProcessor.cpp:84-95).
+  const int32_t H = std::max(1, st.hosts);
+  std::vector<GNRequest> reqs(H);
+  for (auto v : vids) {
+    int32_t p = partOf(v, st.numParts);
+    reqs[p % H].parts[p].push_back(v);
+  }
+  for (auto& r : reqs) { r.edgeTypes = etypes; r.filter = filter; r.returns = returns; }
+  if (H == 1) return getBound(st, reqs[0]);
+  // collectResponse (StorageClient.inl:73-160): fan out, gather
+  std::vector<std::future<QueryResponse>> fs;
+  for (auto& r : reqs) {
+    if (r.parts.empty()) continue;
+    fs.push_back(std::async(std::launch::async, [&st, &r]() { return getBound(st, r); }));
+  }
+  QueryResponse all;
+  for (auto& f : fs) {
+    QueryResponse q = f.get();
+    all.failed.insert(all.failed.end(), q.failed.begin(), q.failed.end());
+    for (auto& kv : q.vertexSchema) all.vertexSchema.emplace(kv.first, kv.second);
+    for (auto& kv : q.edgeSchema) all.edgeSchema.emplace(kv.first, kv.second);
+    for (auto& v : q.vertices) all.vertices.push_back(std::move(v));
+  }
+  all.hasVertexSchema = !all.vertexSchema.empty();
+  all.hasEdgeSchema = !all.edgeSchema.empty();
+  return all;
 }
 
 }  // namespace orc

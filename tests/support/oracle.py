@@ -51,6 +51,7 @@ def lib():
         L.orc_go_timed.restype = C.c_double
         L.orc_load_edges.argtypes = [vp, i32, vp, vp, u64, P(vp), i32]
         L.orc_load_edges.restype = i32
+        L.orc_set_hosts.argtypes = [vp, i32]
         _lib = L
     return _lib
 
