@@ -38,7 +38,7 @@ struct nbg_rows {
   uint64_t count = 0;
   bool on_device = false;
   bool fetched = false;
-  std::vector<int64_t*> dcols;
+  std::vector<int64_t*> dcols;           // column bases; rows live in segs (disjoint regions)
   std::vector<std::vector<int64_t>> bits;
   std::vector<std::vector<uint8_t>> tags;
   std::vector<std::string> strings;
@@ -58,15 +58,15 @@ int32_t materialize_rows(nbg_rows* r) {
   const auto& dict = r->eng->snap.strings;
   r->bits.assign(r->ncols, std::vector<int64_t>(r->count));
   r->tags.assign(r->ncols, std::vector<uint8_t>(r->count));
-  for (int c = 0; c < r->ncols; ++c) {
-    if (r->count && hipMemcpy(r->bits[c].data(), r->dcols[c], r->count * 8, hipMemcpyDeviceToHost) != hipSuccess)
-      return NBG_E_DEVICE;
-  }
   std::unordered_map<int64_t, int64_t> sidx;
+  uint64_t o = 0;
   for (auto& s : r->segs) {
+    uint64_t len = s.end - s.begin;
     for (int c = 0; c < r->ncols; ++c) {
+      if (hipMemcpy(r->bits[c].data() + o, r->dcols[c] + s.begin, len * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return NBG_E_DEVICE;
       VKind k = s.kinds[c];
-      for (uint64_t i = s.begin; i < s.end; ++i) {
+      for (uint64_t i = o; i < o + len; ++i) {
         r->tags[c][i] = (uint8_t)k;
         if (k == VK_STRING) {
           int64_t code = r->bits[c][i];
@@ -81,6 +81,7 @@ int32_t materialize_rows(nbg_rows* r) {
         }
       }
     }
+    o += len;
   }
   r->fetched = true;
   return NBG_OK;
@@ -214,30 +215,21 @@ static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_row
   rows->eng = &E;
   rows->ncols = ncols;
   rows->on_device = device;
-  auto finish_empty = [&]() {
-    *out = rows;
-    return NBG_OK;
-  };
-  if (f0.empty()) return finish_empty();
-  if (f0.size() > E.snap.nv + 1024) {
-    // recreate the workspace with room for the duplicated start list
+  if (f0.empty()) { *out = rows; return NBG_OK; }
+  if ((int)over.size() > MAX_TYPES_Q || rq->steps > (uint32_t)MAX_STEPS) {
+    delete rows;
+    return E.fail(NBG_E_UNSUPPORTED, "too many OVER types or steps");
+  }
+  if (f0.size() > ws_cap_frontier(E.ws)) {   // room for a duplicated start list
     ws_destroy(E.ws);
     E.ws = ws_create(f0.size(), E.snap.nv, E.stream, &err);
     if (!E.ws) { delete rows; return E.fail(NBG_E_OUT_OF_MEMORY, err); }
   }
   Workspace* ws = E.ws;
-  int cur = 0;
-  if (hipMemcpyAsync(ws_frontier(ws, 0), f0.data(), f0.size() * 4, hipMemcpyHostToDevice, E.stream) != hipSuccess) {
-    delete rows;
-    return E.fail(NBG_E_DEVICE, "frontier upload failed");
-  }
-  uint64_t n = f0.size();
   const uint32_t cap = (uint32_t)(E.cfg.max_edge_returned_per_vertex <= 0 ? 0x7fffffff
                                                                           : E.cfg.max_edge_returned_per_vertex);
-  auto args_for = [&](int32_t t, const DevEdgeType& dt) {
+  auto args_for = [&](const DevEdgeType& dt) {
     ExpandArgs a{};
-    a.frontier = ws_frontier(ws, cur);
-    a.n = n;
     a.row_ptr = dt.row_ptr;
     a.col = dt.col;
     a.dst_vid = dt.dst_vid;
@@ -247,82 +239,86 @@ static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_row
     a.vids = E.snap.d_vids;
     a.props = dt.d_props;
     a.cap = cap;
-    (void)t;
     return a;
   };
-  hipError_t he = hipSuccess;
-  for (uint32_t s = 1; s <= rq->steps; ++s) {
-    const bool final = s == rq->steps;
-    rows->step_frontier.push_back(n);
-    uint64_t step_edges = 0;
-    if (!final) {
-      for (int32_t t : over) {
-        auto it = E.snap.types.find(t);
-        if (it == E.snap.types.end()) continue;
-        ExpandArgs a = args_for(t, it->second);
-        uint64_t total = 0;
-        if ((he = k_degree_scan(ws, a, &total)) != hipSuccess) break;
-        step_edges += total;
-        if ((he = k_expand_mark(ws, a, total)) != hipSuccess) break;
-      }
-      if (he != hipSuccess) break;
-      rows->step_edges.push_back(step_edges);
-      rows->scanned += step_edges;
-      uint64_t nn = 0;
-      if ((he = k_compact(ws, E.snap.nv, ws_frontier(ws, cur ^ 1), &nn)) != hipSuccess) break;
-      cur ^= 1;
-      n = nn;
-      if (n == 0) return finish_empty();
-      continue;
-    }
-    if (deferred) { delete rows; return E.fail(deferred, deferred_msg); }
-    // final step: rows for every OVER type
-    uint64_t cap_rows = 0;
-    for (int32_t t : over) {
-      auto it = E.snap.types.find(t);
-      if (it != E.snap.types.end()) cap_rows += it->second.num_edges;
-    }
-    if ((he = ws_reserve_rows(ws, cap_rows, ncols)) != hipSuccess) break;
-    uint64_t row_base = 0;
-    bool error = false;
-    for (int32_t t : over) {
-      auto it = E.snap.types.find(t);
-      if (it == E.snap.types.end()) continue;
-      const TypeProgram& tp = progs[t];
-      ExpandArgs a = args_for(t, it->second);
-      uint64_t total = 0;
-      if ((he = k_degree_scan(ws, a, &total)) != hipSuccess) break;
-      step_edges += total;
-      if (total == 0 || (tp.where_const && !tp.where_const_val)) continue;
-      if (!tp.code.empty() &&
-          (he = hipMemcpyAsync(ws_program(ws), tp.code.data(), tp.code.size() * sizeof(Ins), hipMemcpyHostToDevice,
-                               E.stream)) != hipSuccess)
-        break;
-      uint64_t nrows = 0;
-      int eflag = 0;
-      if ((he = k_expand_final(ws, a, total, tp, ws_program(ws), ws_row_cols(ws), row_base, &nrows, &eflag)) !=
-          hipSuccess)
-        break;
-      if (eflag) { error = true; break; }
-      nbg_rows::Seg seg;
-      seg.begin = row_base;
-      seg.end = row_base + nrows;
-      seg.kinds = tp.yield_kind;
-      seg.const_str = tp.yield_const_str;
-      row_base += nrows;
-      rows->segs.push_back(std::move(seg));
-    }
-    if (he != hipSuccess) break;
-    rows->step_edges.push_back(step_edges);
-    rows->scanned += step_edges;
-    if (error) { delete rows; return E.fail(NBG_E_EXECUTION_ERROR, "WHERE/YIELD evaluation error"); }
-    rows->count = row_base;
-    for (int c = 0; c < ncols; ++c) rows->dcols.push_back(ws_row_col(ws, c));
+  // programs in OVER order (slot = index in `over`)
+  std::vector<TypeProgram> plist(over.size());
+  for (size_t i = 0; i < over.size(); ++i) {
+    auto it = progs.find(over[i]);
+    if (it != progs.end()) plist[i] = it->second;
   }
+  // final-step row regions: the frontier entering step N is a set (N >= 2) or the start list
+  // (N == 1, exact edge count known on the host)
+  const uint64_t n_final = rq->steps == 1 ? f0.size() : E.snap.nv;
+  std::vector<uint64_t> region(over.size()), shard_cap(over.size()), ebound(over.size());
+  uint64_t cap_rows = 0;
+  for (size_t i = 0; i < over.size(); ++i) {
+    auto it = E.snap.types.find(over[i]);
+    uint64_t eb = 0;
+    if (it != E.snap.types.end()) {
+      if (rq->steps == 1) {
+        for (uint32_t d : f0) eb += std::min<uint64_t>(it->second.h_row_ptr[d + 1] - it->second.h_row_ptr[d], cap);
+      } else {
+        eb = it->second.num_edges;
+      }
+    }
+    ebound[i] = eb;
+    shard_cap[i] = ws_shard_cap(n_final, eb);
+    region[i] = cap_rows;
+    cap_rows += shard_cap[i] * NSHARD;
+  }
+  hipError_t he = ws_reserve_rows(ws, cap_rows, ncols);
+  if (he == hipSuccess) he = ws_begin_query(ws, f0.data(), f0.size(), &plist);
+  uint64_t n_bound = f0.size();
+  for (uint32_t s = 1; he == hipSuccess && s <= rq->steps; ++s) {
+    const bool final = s == rq->steps;
+    for (size_t i = 0; he == hipSuccess && i < over.size(); ++i) {
+      auto it = E.snap.types.find(over[i]);
+      if (it == E.snap.types.end()) continue;
+      ExpandArgs a = args_for(it->second);
+      if (!final) {
+        he = ws_expand_mark(ws, a, n_bound, it->second.num_edges, (int)s, (int)i);
+      } else if (deferred || (plist[i].where_const && !plist[i].where_const_val)) {
+        he = ws_scan_only(ws, a, n_bound, (int)s, (int)i);
+      } else {
+        he = ws_expand_final(ws, a, n_bound, ebound[i], (int)s, (int)i, plist[i], region[i], shard_cap[i]);
+      }
+    }
+    if (!final && he == hipSuccess) {
+      he = ws_compact(ws, (int)s);
+      n_bound = E.snap.nv;
+    }
+  }
+  if (he == hipSuccess) he = ws_end_query(ws);
   if (he != hipSuccess) {
     delete rows;
     return E.fail(NBG_E_DEVICE, std::string("HIP: ") + hipGetErrorString(he));
   }
+  const QState& q = *ws_host_state(ws);
+  for (uint32_t s = 1; s <= rq->steps; ++s) {
+    uint64_t es = 0;
+    for (size_t i = 0; i < over.size(); ++i) es += q.e_st[s][i];
+    rows->step_frontier.push_back(q.step_n[s]);
+    rows->step_edges.push_back(es);
+    rows->scanned += es;
+  }
+  const bool reached_final = q.step_n[rq->steps] > 0;
+  if (reached_final && deferred) { delete rows; return E.fail(deferred, deferred_msg); }
+  if (q.err) { delete rows; return E.fail(NBG_E_EXECUTION_ERROR, "WHERE/YIELD evaluation error"); }
+  for (size_t i = 0; i < over.size(); ++i) {
+    for (int sh = 0; sh < NSHARD; ++sh) {
+      uint64_t c = q.rows[i][sh];
+      if (!c) continue;
+      nbg_rows::Seg seg;
+      seg.begin = region[i] + (uint64_t)sh * shard_cap[i];
+      seg.end = seg.begin + c;
+      seg.kinds = plist[i].yield_kind;
+      seg.const_str = plist[i].yield_const_str;
+      rows->segs.push_back(std::move(seg));
+      rows->count += c;
+    }
+  }
+  for (int c = 0; c < ncols; ++c) rows->dcols.push_back(ws_row_col(ws, c));
   if (!device) {
     int32_t rc = materialize_rows(rows);
     if (rc) { delete rows; return E.fail(rc, "row fetch failed"); }

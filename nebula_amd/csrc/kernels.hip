@@ -1,17 +1,24 @@
 // nebula_amd — gfx950 (CDNA4) kernels for the GO N STEPS / FIND PATH hot path.
 //
+// A query is enqueued on the workspace stream with NO host synchronisation until its end:
+// every size the kernels need (frontier size n, edges of the current expansion, next frontier
+// size) lives in a device-resident QState and grids are sized from host-known upper bounds.
+//
 // Per hop over one edge type (CSR):
 //   k_degree      frontier degrees (row_ptr gathers, capped by max_edge_returned_per_vertex)
 //                 + block-local inclusive scan                       (wave64 shuffles + LDS)
-//   k_scan_blocks exclusive scan of the per-block totals (one workgroup)
-//   k_partition   merge-path split of (frontier segments ⊕ edges) into equal tiles
-//   k_expand<M>   load-balanced expansion: each tile owns TILE path items whatever the degree
-//                 skew; items are processed striped across the block so neighbour reads are
-//                 coalesced.  M = MARK (intermediate steps: set next-frontier byte flags) or
-//                 FINAL (evaluate the WHERE/YIELD bytecode per edge, wave-ballot compaction of
-//                 the emitted rows, one atomic per block-iteration).
-//   k_flag_count / k_flag_write  dense compaction of the byte flags into the next (sorted)
-//                 frontier, clearing the flags in the same pass.
+//   k_scan_blocks exclusive scan of the per-block totals (one workgroup); publishes the total
+//   k_expand<M>   persistent, load-balanced expansion over merge-path tiles: a tile owns TILE
+//                 path items (frontier segments + edges) whatever the degree skew, its split is
+//                 found by a wave-wide 64-ary search over the global scan; items are processed striped
+//                 across the block so neighbour / property reads are coalesced.
+//                 M = MARK  (steps 1..N-1: set next-frontier byte flags, idempotent plain stores)
+//                 M = FINAL (step N: WHERE/YIELD bytecode per edge, wave-ballot compaction, rows
+//                           appended to one of NSHARD per-shard regions: one atomic per
+//                           tile on a sharded counter, never a single hot word; simple
+//                           `col <cmp> const` / leaf-yield programs skip the interpreter)
+//   k_flag_count / k_scan_blocks / k_flag_write  dense compaction of the byte flags into the
+//                 next (sorted) frontier, clearing the flags in the same pass.
 // Semantics follow QueryBaseProcessor::collectEdgeProps (version de-dup is done at load,
 // neighbours are in memcmp key order, the cap counts edges in that order) and
 // GoExecutor::getDstIdsFromResp (per-step dst SET, no global visited set).
@@ -19,6 +26,7 @@
 
 #include <cstdio>
 #include <cstring>
+#include <vector>
 
 #include "nbg_internal.h"
 
@@ -29,18 +37,17 @@ constexpr int WAVES = BLOCK / 64;
 constexpr int SCAN_ITEMS = 8;                    // k_degree: items per thread
 constexpr int SCAN_TILE = BLOCK * SCAN_ITEMS;    // 2048 frontier entries per block
 constexpr int SCAN_SHIFT = 11;
-constexpr int VT = 4;                            // k_expand: path items per thread
-constexpr int TILE = BLOCK * VT;                 // 1024 path items per tile
 constexpr int FLAG_BYTES = BLOCK * 16;           // k_flag_*: bytes per block
+constexpr int EXPAND_GRID = 2048;                // persistent k_expand grid (8 blocks / CU)
 
-enum KernelId { K_DEGREE = 0, K_SCAN, K_PARTITION, K_EXPAND_MARK, K_FLAG_COUNT, K_FLAG_WRITE, K_EXPAND_FINAL,
-                K_BFS, K_COUNT };
-static const char* const kKernelNames[K_COUNT] = {"k_degree", "k_scan_blocks", "k_partition", "k_expand<MARK>",
-                                                  "k_flag_count", "k_flag_write", "k_expand<FINAL>", "k_expand<BFS>"};
+enum KernelId { K_DEGREE = 0, K_SCAN, K_EXPAND_MARK, K_FLAG_COUNT, K_FLAG_WRITE, K_EXPAND_FINAL, K_BFS,
+                K_COUNT };
+static const char* const kKernelNames[K_COUNT] = {"k_degree", "k_scan_blocks", "k_expand<MARK>", "k_flag_count",
+                                                  "k_flag_write", "k_expand<FINAL>", "k_expand<BFS>"};
 
 struct Prof {
   bool on = false;
-  struct Rec { int kid; hipEvent_t a, b; double bytes; };
+  struct Rec { int kid, step, tix; hipEvent_t a, b; double cols, kout; };
   std::vector<Rec> pending;
   std::vector<hipEvent_t> pool;
   uint64_t launches[K_COUNT] = {};
@@ -60,29 +67,25 @@ struct Workspace {
   uint64_t cap_frontier = 0;      // entries in each frontier / scan buffer
   uint64_t nv = 0;
   uint32_t* frontier[2] = {nullptr, nullptr};
+  int cur = 0;
   uint32_t* seg_end = nullptr;    // block-local inclusive scan of degrees
   uint32_t* seg_rs = nullptr;     // row start per frontier entry
   uint32_t* block_sum = nullptr;  // per-block totals -> exclusive prefix (in place)
   uint64_t cap_blocks = 0;
-  uint32_t* part = nullptr;       // merge-path tile splits
-  uint64_t cap_tiles = 0;
   uint8_t* flags = nullptr;       // [nv rounded up to FLAG_BYTES], kept all-zero between steps
   uint64_t flag_bytes = 0;
   uint32_t* flag_blocks = nullptr;
-  uint64_t* counters = nullptr;   // [0] total, [1] row counter, [2] error, [3] scratch
-  uint64_t* h_pinned = nullptr;   // pinned readback
+  QState* q = nullptr;            // device query state
+  QState* h_q = nullptr;          // pinned host mirror
+  uint32_t* h_starts = nullptr;   // pinned staging for start ids
+  uint64_t cap_starts = 0;
+  Ins* h_prog = nullptr;          // pinned staging for programs
   int64_t* rows = nullptr;        // [ncols][cap_rows]
   uint64_t cap_rows = 0;
   int ncols_alloc = 0;
   int64_t** d_row_cols = nullptr; // device array of column pointers
-  Ins* d_prog = nullptr;
+  Ins* d_prog = nullptr;          // [MAX_TYPES_Q][MAX_PROGRAM]
 };
-
-#define HIP_TRY(x)                         \
-  do {                                     \
-    hipError_t e_ = (x);                   \
-    if (e_ != hipSuccess) return e_;       \
-  } while (0)
 
 // ----------------------------------------------------------------------------- helpers
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
@@ -114,12 +117,14 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* total,
 }
 
 // ----------------------------------------------------------------------------- k_degree
-__global__ void __launch_bounds__(BLOCK) k_degree(const uint32_t* __restrict__ frontier, uint64_t n,
+__global__ void __launch_bounds__(BLOCK) k_degree(const uint32_t* __restrict__ frontier, const QState* __restrict__ q,
                                                   const uint32_t* __restrict__ row_ptr,
                                                   const uint8_t* __restrict__ visible, uint32_t cap,
                                                   uint32_t* __restrict__ seg_end, uint32_t* __restrict__ seg_rs,
                                                   uint32_t* __restrict__ block_sum) {
   __shared__ uint32_t lds[WAVES];
+  const uint64_t n = q->n;
+  if ((uint64_t)blockIdx.x * SCAN_TILE >= n) return;
   const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
   uint32_t deg[SCAN_ITEMS], rs[SCAN_ITEMS];
   uint32_t sum = 0;
@@ -153,17 +158,18 @@ __global__ void __launch_bounds__(BLOCK) k_degree(const uint32_t* __restrict__ f
   if (threadIdx.x == 0) block_sum[blockIdx.x] = total;
 }
 
-// One workgroup: exclusive scan of nb uint32 in place; out[0] = grand total (uint64).
-__global__ void __launch_bounds__(1024) k_scan_blocks(uint32_t* __restrict__ v, uint64_t nb,
-                                                      uint64_t* __restrict__ out) {
+// One workgroup: exclusive scan of nb uint32 in place.  nb = fixed_nb, or ceil(q->n / 2048) when
+// fixed_nb == 0.  The grand total goes to *total_out and is added to *accum (stats).
+__global__ void __launch_bounds__(1024) k_scan_blocks(uint32_t* __restrict__ v, const QState* qn, uint64_t fixed_nb,
+                                                      unsigned long long* total_out, unsigned long long* accum) {
   __shared__ uint64_t lds[16];
   __shared__ uint64_t carry;
+  const uint64_t nb = fixed_nb ? fixed_nb : (qn->n + SCAN_TILE - 1) / SCAN_TILE;
   if (threadIdx.x == 0) carry = 0;
   __syncthreads();
   for (uint64_t base = 0; base < nb; base += 1024) {
     uint64_t i = base + threadIdx.x;
     uint64_t x = i < nb ? v[i] : 0;
-    // wave inclusive scan (64-bit)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint64_t inc = x;
     for (int o = 1; o < 64; o <<= 1) {
@@ -183,7 +189,10 @@ __global__ void __launch_bounds__(1024) k_scan_blocks(uint32_t* __restrict__ v, 
     if (threadIdx.x == 0) carry = c + tot;
     __syncthreads();
   }
-  if (threadIdx.x == 0) out[0] = carry;
+  if (threadIdx.x == 0) {
+    *total_out = carry;
+    if (accum) *accum += carry;
+  }
 }
 
 __device__ __forceinline__ uint32_t seg_end_at(const uint32_t* __restrict__ seg_end,
@@ -191,21 +200,52 @@ __device__ __forceinline__ uint32_t seg_end_at(const uint32_t* __restrict__ seg_
   return seg_end[i] + block_pre[i >> SCAN_SHIFT];
 }
 
-// ----------------------------------------------------------------------------- k_partition
-__global__ void k_partition(const uint32_t* __restrict__ seg_end, const uint32_t* __restrict__ block_pre,
-                            uint64_t n, uint64_t total, uint64_t ntiles, uint32_t* __restrict__ part) {
-  uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t > ntiles) return;
-  uint64_t d = t * TILE;
-  if (d > n + total) d = n + total;
+// Merge-path split: number of frontier segments fully consumed in the first d path items, i.e.
+// the smallest i with NOT(end(i) <= d-1-i).  Computed by one whole wave as a 64-ary search:
+// each round the 64 lanes probe 64 evenly spaced candidates in parallel (one memory round trip)
+// and a ballot narrows the range 64x, so a split costs ceil(log64(n)) <= 5 round trips instead
+// of ~25 dependent loads of a binary search.
+__device__ __forceinline__ uint64_t wave_merge_split(const uint32_t* __restrict__ seg_end,
+                                                     const uint32_t* __restrict__ block_pre, uint64_t n,
+                                                     uint64_t total, uint64_t d) {
+  const int lane = threadIdx.x & 63;
   uint64_t lo = d > total ? d - total : 0;
   uint64_t hi = d < n ? d : n;
   while (lo < hi) {
-    uint64_t mid = (lo + hi) >> 1;
-    if ((uint64_t)seg_end_at(seg_end, block_pre, mid) <= d - 1 - mid) lo = mid + 1;
-    else hi = mid;
+    const uint64_t step = (hi - lo + 63) >> 6;
+    const uint64_t p = lo + (uint64_t)lane * step;
+    bool t = p < hi && (uint64_t)seg_end_at(seg_end, block_pre, p) <= d - 1 - p;
+    const int c = __popcll(__ballot(t));
+    const uint64_t nlo = c > 0 ? lo + (uint64_t)(c - 1) * step + 1 : lo;
+    uint64_t nhi = lo + (uint64_t)c * step;
+    if (nhi > hi) nhi = hi;
+    lo = nlo;
+    hi = nhi;
   }
-  part[t] = (uint32_t)lo;
+  return lo;
+}
+
+// Fast path for the common final-step program shape: WHERE absent or `col <cmp> const` on an
+// INT column, YIELD columns that are plain edge fields / key props / constants.  No
+// interpreter, no LDS registers; the generic bytecode path handles everything else.
+struct FastProg {
+  int enabled;
+  int where_col;           // -1: no WHERE
+  int where_op;            // 0 LT 1 LE 2 GT 3 GE 4 EQ 5 NE (int64)
+  int64_t where_const;
+  int ykind[MAX_YIELDS];   // 0 DST, 1 SRC, 2 RANK, 3 COL, 4 CONST
+  int ycol[MAX_YIELDS];
+};
+
+__device__ __forceinline__ bool cmp_i(int op, int64_t x, int64_t y) {
+  switch (op) {
+    case 0: return x < y;
+    case 1: return x <= y;
+    case 2: return x > y;
+    case 3: return x >= y;
+    case 4: return x == y;
+    default: return x != y;
+  }
 }
 
 // ----------------------------------------------------------------------------- bytecode
@@ -300,126 +340,195 @@ struct FinalParams {
   int yield_reg[MAX_YIELDS];
   int64_t yield_const[MAX_YIELDS];
   int64_t** out_cols;
-  uint64_t row_base;
-  uint64_t* row_counter;
-  uint64_t* err_flag;
+  uint64_t region_base;   // first row of this type's region
+  uint64_t shard_cap;     // rows per shard region
+  unsigned long long* shard_rows;   // [NSHARD] counters of this type
+  unsigned long long* err_flag;
+  FastProg fast;
 };
 
 template <int M>
-__global__ void __launch_bounds__(BLOCK) k_expand(ExpandArgs a, const uint32_t* __restrict__ seg_end,
+__global__ void __launch_bounds__(BLOCK) k_expand(ExpandArgs a, const QState* __restrict__ q,
+                                                  const uint32_t* __restrict__ seg_end,
                                                   const uint32_t* __restrict__ block_pre,
-                                                  const uint32_t* __restrict__ seg_rs,
-                                                  const uint32_t* __restrict__ part, uint64_t total,
-                                                  uint8_t* __restrict__ flags, FinalParams fp) {
+                                                  const uint32_t* __restrict__ seg_rs, uint8_t* __restrict__ flags,
+                                                  FinalParams fp) {
   __shared__ uint32_t sEnd[TILE + 2];   // seg_end for i in [a0-1, a1]
   __shared__ uint32_t sRs[TILE + 1];    // seg_rs for i in [a0, a1]
   __shared__ uint32_t sSeg[TILE];       // segment of each edge item in this tile
-  __shared__ uint32_t sWave[WAVES];
+  __shared__ uint32_t sCnt[VT * WAVES]; // FINAL: passing items per (iteration, wave) -> offsets
+  __shared__ uint64_t sSplit[2];
   __shared__ uint64_t sBase;
-  extern __shared__ int64_t regs[];     // FINAL: [MAX_REGS][BLOCK]
+  extern __shared__ int64_t regs[];     // FINAL generic path: [nregs][BLOCK]
 
-  const uint64_t t = blockIdx.x;
-  const uint64_t n = a.n;
-  const uint64_t d0 = t * TILE;
-  const uint64_t d1 = (d0 + TILE < n + total) ? d0 + TILE : n + total;
-  const uint64_t a0 = part[t], a1 = part[t + 1];
-  const uint64_t b0 = d0 - a0, b1 = d1 - a1;
-  const int na = (int)(a1 - a0), nb = (int)(b1 - b0);
+  const uint64_t n = q->n;
+  const uint64_t total = q->total;
+  const uint64_t npath = n + total;
+  const uint64_t ntiles = (npath + TILE - 1) / TILE;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  bool anyErr = false;
 
-  // stage the tile's segment ends / row starts in LDS
-  for (int k = threadIdx.x; k <= na + 1; k += BLOCK) {
-    int64_t i = (int64_t)a0 - 1 + k;
-    sEnd[k] = (i < 0) ? 0u : (i < (int64_t)n ? seg_end_at(seg_end, block_pre, (uint64_t)i) : 0xFFFFFFFFu);
-  }
-  for (int k = threadIdx.x; k <= na; k += BLOCK) {
-    uint64_t i = a0 + k;
-    sRs[k] = i < n ? seg_rs[i] : 0u;
-  }
-  __syncthreads();
-  const uint32_t* A = sEnd + 1;   // A[k] = end of segment a0 + k
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const uint64_t d0 = t * TILE;
+    const uint64_t d1 = (d0 + TILE < npath) ? d0 + TILE : npath;
+    if (w < 2) {
+      uint64_t sp = wave_merge_split(seg_end, block_pre, n, total, w ? d1 : d0);
+      if (lane == 0) sSplit[w] = sp;
+    }
+    __syncthreads();
+    const uint64_t a0 = sSplit[0], a1 = sSplit[1];
+    const uint64_t b0 = d0 - a0, b1 = d1 - a1;
+    const int na = (int)(a1 - a0), nb = (int)(b1 - b0);
 
-  // thread-level merge path over this tile: assign a segment to every edge item
-  {
-    int diag = threadIdx.x * VT;
-    int dmax = na + nb;
-    if (diag < dmax) {
-      int lo = diag > nb ? diag - nb : 0;
-      int hi = diag < na ? diag : na;
-      while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if ((uint64_t)A[mid] <= b0 + (uint64_t)(diag - 1 - mid)) lo = mid + 1;
-        else hi = mid;
-      }
-      int ai = lo, bi = diag - lo;
+    // stage the tile's segment ends / row starts in LDS
+    for (int k = threadIdx.x; k <= na + 1; k += BLOCK) {
+      int64_t i = (int64_t)a0 - 1 + k;
+      sEnd[k] = (i < 0) ? 0u : (i < (int64_t)n ? seg_end_at(seg_end, block_pre, (uint64_t)i) : 0xFFFFFFFFu);
+    }
+    for (int k = threadIdx.x; k <= na; k += BLOCK) {
+      uint64_t i = a0 + k;
+      sRs[k] = i < n ? seg_rs[i] : 0u;
+    }
+    __syncthreads();
+    const uint32_t* A = sEnd + 1;   // A[k] = end of segment a0 + k
+
+    // thread-level merge path over this tile: assign a segment to every edge item
+    {
+      int diag = threadIdx.x * VT;
+      int dmax = na + nb;
+      if (diag < dmax) {
+        int lo = diag > nb ? diag - nb : 0;
+        int hi = diag < na ? diag : na;
+        while (lo < hi) {
+          int mid = (lo + hi) >> 1;
+          if ((uint64_t)A[mid] <= b0 + (uint64_t)(diag - 1 - mid)) lo = mid + 1;
+          else hi = mid;
+        }
+        int ai = lo, bi = diag - lo;
 #pragma unroll
-      for (int k = 0; k < VT; ++k) {
-        if (ai + bi >= dmax) break;
-        if (ai < na && (bi >= nb || (uint64_t)A[ai] <= b0 + (uint64_t)bi)) {
-          ++ai;
-        } else {
-          sSeg[bi] = (uint32_t)ai;
-          ++bi;
+        for (int k = 0; k < VT; ++k) {
+          if (ai + bi >= dmax) break;
+          if (ai < na && (bi >= nb || (uint64_t)A[ai] <= b0 + (uint64_t)bi)) {
+            ++ai;
+          } else {
+            sSeg[bi] = (uint32_t)ai;
+            ++bi;
+          }
         }
       }
     }
-  }
-  __syncthreads();
+    __syncthreads();
 
-  if (M == MARK) {
-    for (int k = threadIdx.x; k < nb; k += BLOCK) {
-      uint32_t s = sSeg[k];
-      uint64_t e = b0 + k;
-      uint64_t j = (uint64_t)sRs[s] + (e - (uint64_t)sEnd[s]);   // sEnd[s] = start of segment a0+s
-      uint32_t u = a.col[j];
-      if (u != NO_ROW) flags[u] = 1;
-    }
-  } else {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    bool anyErr = false;
-    for (int k0 = 0; k0 < nb; k0 += BLOCK) {
-      int k = k0 + threadIdx.x;
-      bool active = k < nb;
-      EdgeCtx c{0, 0};
-      if (active) {
+    if (M == MARK) {
+      for (int k = threadIdx.x; k < nb; k += BLOCK) {
         uint32_t s = sSeg[k];
         uint64_t e = b0 + k;
-        c.j = (uint64_t)sRs[s] + (e - (uint64_t)sEnd[s]);
-        c.v = a.frontier[a0 + s];
+        uint64_t j = (uint64_t)sRs[s] + (e - (uint64_t)sEnd[s]);   // sEnd[s] = start of segment a0+s
+        uint32_t u = a.col[j];
+        if (u != NO_ROW) flags[u] = 1;
       }
-      bool werr = false, pass = active;
-      if (fp.where_reg >= 0) {
-        run_program(fp.prog, 0, fp.where_len, c, a, regs, active, werr);
-        pass = active && !werr && regs[fp.where_reg * BLOCK + threadIdx.x] != 0;
-      }
-      bool yerr = false;
-      // the YIELD programs follow the WHERE part; they run for passing lanes only
-      run_program(fp.prog, fp.where_len, fp.prog_len, c, a, regs, pass, yerr);
-      if (active && (werr || (pass && yerr))) anyErr = true;
-
-      unsigned long long bal = __ballot(pass);
-      uint32_t wcount = __popcll(bal);
-      uint32_t lpre = __popcll(bal & ((1ull << lane) - 1ull));
-      if (lane == 0) sWave[w] = wcount;
-      __syncthreads();
-      uint32_t wpre = 0, btot = 0;
+    } else {
+      // phase A: WHERE for every item of the tile (VT items per thread, striped)
+      uint64_t jj[VT];
+      uint32_t vv[VT];
+      uint32_t pmask = 0;
 #pragma unroll
-      for (int i = 0; i < WAVES; ++i) {
-        wpre += (i < w) ? sWave[i] : 0u;
-        btot += sWave[i];
-      }
-      if (threadIdx.x == 0 && btot) sBase = atomicAdd((unsigned long long*)fp.row_counter, (unsigned long long)btot);
-      __syncthreads();
-      if (pass) {
-        uint64_t row = fp.row_base + sBase + wpre + lpre;
-        for (int y = 0; y < fp.nyields; ++y) {
-          int r = fp.yield_reg[y];
-          fp.out_cols[y][row] = r >= 0 ? regs[r * BLOCK + threadIdx.x] : fp.yield_const[y];
+      for (int i = 0; i < VT; ++i) {
+        const int k = i * BLOCK + threadIdx.x;
+        jj[i] = 0;
+        vv[i] = 0;
+        if (k < nb) {
+          uint32_t s = sSeg[k];
+          jj[i] = (uint64_t)sRs[s] + (b0 + k - (uint64_t)sEnd[s]);
+          vv[i] = s;
         }
       }
+      if (fp.fast.enabled) {
+        if (fp.fast.where_col < 0) {
+#pragma unroll
+          for (int i = 0; i < VT; ++i) pmask |= (uint32_t)(i * BLOCK + (int)threadIdx.x < nb) << i;
+        } else {
+          const int64_t* __restrict__ wc = a.props[fp.fast.where_col];
+          int64_t x[VT];
+#pragma unroll
+          for (int i = 0; i < VT; ++i) x[i] = (i * BLOCK + (int)threadIdx.x < nb) ? wc[jj[i]] : 0;
+#pragma unroll
+          for (int i = 0; i < VT; ++i)
+            pmask |= (uint32_t)((i * BLOCK + (int)threadIdx.x < nb) && cmp_i(fp.fast.where_op, x[i],
+                                                                               fp.fast.where_const)) << i;
+        }
+      } else {
+        for (int i = 0; i < VT; ++i) {
+          const int k = i * BLOCK + threadIdx.x;
+          const bool active = k < nb;
+          bool pass = active;
+          if (fp.where_reg >= 0) {
+            bool werr = false;
+            EdgeCtx c{jj[i], active ? a.frontier[a0 + vv[i]] : 0u};
+            run_program(fp.prog, 0, fp.where_len, c, a, regs, active, werr);
+            pass = active && !werr && regs[fp.where_reg * BLOCK + threadIdx.x] != 0;
+            if (active && werr) anyErr = true;
+          }
+          pmask |= (uint32_t)pass << i;
+        }
+      }
+      // one atomic per tile on a sharded counter: offsets for (iteration, wave) in item order
+#pragma unroll
+      for (int i = 0; i < VT; ++i) {
+        unsigned long long bal = __ballot((pmask >> i) & 1u);
+        if (lane == 0) sCnt[i * WAVES + w] = (uint32_t)__popcll(bal);
+      }
       __syncthreads();
+      const uint64_t shard = t % NSHARD;
+      if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int k = 0; k < VT * WAVES; ++k) {
+          uint32_t c = sCnt[k];
+          sCnt[k] = run;
+          run += c;
+        }
+        sBase = run ? atomicAdd(fp.shard_rows + shard, (unsigned long long)run) : 0ull;
+      }
+      __syncthreads();
+      // phase B: YIELD for the passing items, written at their final rows
+      const uint64_t region = fp.region_base + shard * fp.shard_cap + sBase;
+      int64_t* const* cols = fp.out_cols;
+      for (int i = 0; i < VT; ++i) {
+        const bool pass = (pmask >> i) & 1u;
+        unsigned long long bal = __ballot(pass);
+        if (!bal) continue;
+        const uint64_t row = region + sCnt[i * WAVES + w] + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+        if (fp.fast.enabled) {
+          if (pass) {
+            for (int y = 0; y < fp.nyields; ++y) {
+              int64_t val;
+              switch (fp.fast.ykind[y]) {
+                case 0: val = a.dst_vid[jj[i]]; break;
+                case 1: val = a.vids[a.frontier[a0 + vv[i]]]; break;
+                case 2: val = a.rank ? a.rank[jj[i]] : 0; break;
+                case 3: val = a.props[fp.fast.ycol[y]][jj[i]]; break;
+                default: val = fp.yield_const[y]; break;
+              }
+              cols[y][row] = val;
+            }
+          }
+        } else {
+          bool yerr = false;
+          EdgeCtx c{jj[i], pass ? a.frontier[a0 + vv[i]] : 0u};
+          run_program(fp.prog, fp.where_len, fp.prog_len, c, a, regs, pass, yerr);
+          if (pass && yerr) anyErr = true;
+          if (pass) {
+            for (int y = 0; y < fp.nyields; ++y) {
+              int r = fp.yield_reg[y];
+              cols[y][row] = r >= 0 ? regs[r * BLOCK + threadIdx.x] : fp.yield_const[y];
+            }
+          }
+        }
+      }
     }
-    if (anyErr) atomicOr((unsigned long long*)fp.err_flag, 1ull);
+    __syncthreads();   // LDS reuse by the next tile
   }
+  if (M == FINAL && anyErr) atomicOr(fp.err_flag, 1ull);
 }
 
 // ----------------------------------------------------------------------------- flag compaction
@@ -466,30 +575,50 @@ __global__ void __launch_bounds__(BLOCK) k_flag_write(uint8_t* __restrict__ flag
   }
 }
 
-// ============================================================================= host wrappers
+// ============================================================================= host side
 static inline uint64_t cdiv(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
-// Kernel timing: an event pair around each launch on the workspace stream, resolved at the
-// next host synchronisation point.
+#define HIP_TRY(x)                         \
+  do {                                     \
+    hipError_t e_ = (x);                   \
+    if (e_ != hipSuccess) return e_;       \
+  } while (0)
+
+// Kernel timing: an event pair around each launch on the workspace stream, resolved after the
+// query's single host synchronisation (byte counts need the device-side sizes).
 static hipEvent_t prof_begin(Workspace* w) {
   if (!w->prof.on) return nullptr;
   hipEvent_t a = w->prof.get();
   (void)hipEventRecord(a, w->stream);
   return a;
 }
-static void prof_end(Workspace* w, hipEvent_t a, int kid, double bytes) {
+static void prof_end(Workspace* w, hipEvent_t a, int kid, int step, int tix, double cols = 0, double kout = 0) {
   if (!a) return;
   hipEvent_t b = w->prof.get();
   (void)hipEventRecord(b, w->stream);
-  w->prof.pending.push_back({kid, a, b, bytes});
+  w->prof.pending.push_back({kid, step, tix, a, b, cols, kout});
 }
-static void prof_flush(Workspace* w) {
+// algorithmic bytes per kernel (SURVEY.md §8(d) B_GO terms)
+static double prof_bytes(const Prof::Rec& r, const QState& q) {
+  switch (r.kid) {
+    case K_DEGREE: return 12.0 * (double)q.step_n[r.step];                 // 4|F| ids + 8|F| row_ptr
+    case K_EXPAND_MARK: return 4.0 * (double)q.e_st[r.step][r.tix];        // 4 E_s neighbour ids
+    case K_FLAG_WRITE: return 4.0 * (double)q.step_n[r.step + 1];          // write F_{s+1}
+    case K_EXPAND_FINAL: {
+      double rows = 0;
+      for (int s = 0; s < NSHARD; ++s) rows += (double)q.rows[r.tix][s];
+      return 8.0 * (double)q.e_st[r.step][r.tix] * r.cols + 8.0 * rows * r.kout;
+    }
+    default: return 0.0;
+  }
+}
+static void prof_flush(Workspace* w, const QState* q) {
   for (auto& r : w->prof.pending) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
       w->prof.launches[r.kid]++;
       w->prof.ms[r.kid] += ms;
-      w->prof.bytes[r.kid] += r.bytes;
+      if (q) w->prof.bytes[r.kid] += prof_bytes(r, *q);
     }
     w->prof.pool.push_back(r.a);
     w->prof.pool.push_back(r.b);
@@ -499,7 +628,7 @@ static void prof_flush(Workspace* w) {
 
 void ws_profile(Workspace* w, bool on) {
   if (!w) return;
-  prof_flush(w);
+  prof_flush(w, nullptr);
   w->prof.on = on;
   if (on) {
     for (int k = 0; k < K_COUNT; ++k) { w->prof.launches[k] = 0; w->prof.ms[k] = 0; w->prof.bytes[k] = 0; }
@@ -537,12 +666,13 @@ Workspace* ws_create(uint64_t max_frontier, uint64_t nv, hipStream_t s, std::str
   M((void**)&w->block_sum, w->cap_blocks * 4);
   M((void**)&w->flags, w->flag_bytes);
   M((void**)&w->flag_blocks, w->cap_blocks * 4);
-  M((void**)&w->counters, 8 * sizeof(uint64_t));
-  M((void**)&w->d_prog, MAX_PROGRAM * sizeof(Ins));
+  M((void**)&w->q, sizeof(QState));
+  M((void**)&w->d_prog, (size_t)MAX_TYPES_Q * MAX_PROGRAM * sizeof(Ins));
   M((void**)&w->d_row_cols, MAX_YIELDS * sizeof(int64_t*));
-  if (e == hipSuccess) e = hipHostMalloc((void**)&w->h_pinned, 64, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipHostMalloc((void**)&w->h_q, sizeof(QState), hipHostMallocDefault);
+  if (e == hipSuccess) e = hipHostMalloc((void**)&w->h_prog, (size_t)MAX_TYPES_Q * MAX_PROGRAM * sizeof(Ins),
+                                         hipHostMallocDefault);
   if (e == hipSuccess) e = hipMemsetAsync(w->flags, 0, w->flag_bytes, s);
-  if (e == hipSuccess) e = hipMemsetAsync(w->counters, 0, 8 * sizeof(uint64_t), s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
     if (err) *err = std::string("workspace allocation failed: ") + hipGetErrorString(e);
@@ -555,102 +685,114 @@ Workspace* ws_create(uint64_t max_frontier, uint64_t nv, hipStream_t s, std::str
 void ws_destroy(Workspace* w) {
   if (!w) return;
   for (void* p : {(void*)w->frontier[0], (void*)w->frontier[1], (void*)w->seg_end, (void*)w->seg_rs,
-                  (void*)w->block_sum, (void*)w->part, (void*)w->flags, (void*)w->flag_blocks,
-                  (void*)w->counters, (void*)w->rows, (void*)w->d_row_cols, (void*)w->d_prog})
+                  (void*)w->block_sum, (void*)w->flags, (void*)w->flag_blocks, (void*)w->q, (void*)w->rows,
+                  (void*)w->d_row_cols, (void*)w->d_prog})
     if (p) (void)hipFree(p);
-  if (w->h_pinned) (void)hipHostFree(w->h_pinned);
+  for (void* p : {(void*)w->h_q, (void*)w->h_starts, (void*)w->h_prog})
+    if (p) (void)hipHostFree(p);
+  for (auto& r : w->prof.pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+  for (auto e : w->prof.pool) (void)hipEventDestroy(e);
   delete w;
 }
 
-uint32_t* ws_frontier(Workspace* w, int which) { return w->frontier[which]; }
-int64_t** ws_row_cols(Workspace* w) { return w->d_row_cols; }
+uint64_t ws_cap_frontier(Workspace* w) { return w->cap_frontier; }
 int64_t* ws_row_col(Workspace* w, int c) { return w->rows + (uint64_t)c * w->cap_rows; }
-Ins* ws_program(Workspace* w) { return w->d_prog; }
+const QState* ws_host_state(Workspace* w) { return w->h_q; }
+const uint32_t* ws_current_frontier(Workspace* w) { return w->frontier[w->cur]; }
 
 hipError_t ws_reserve_rows(Workspace* w, uint64_t rows, int ncols) {
   if (rows <= w->cap_rows && ncols <= w->ncols_alloc) return hipSuccess;
+  HIP_TRY(hipStreamSynchronize(w->stream));
   if (w->rows) HIP_TRY(hipFree(w->rows));
   w->rows = nullptr;
-  uint64_t cap = rows < 1024 ? 1024 : rows + rows / 8;
+  uint64_t cap = rows < 1024 ? 1024 : rows;
+  if (cap < w->cap_rows) cap = w->cap_rows;
   int nc = ncols < 1 ? 1 : ncols;
+  if (nc < w->ncols_alloc) nc = w->ncols_alloc;
   HIP_TRY(hipMalloc((void**)&w->rows, cap * nc * sizeof(int64_t)));
   w->cap_rows = cap;
   w->ncols_alloc = nc;
   int64_t* cols[MAX_YIELDS];
   for (int c = 0; c < MAX_YIELDS; ++c) cols[c] = w->rows + (uint64_t)(c < nc ? c : 0) * cap;
-  HIP_TRY(hipMemcpyAsync(w->d_row_cols, cols, sizeof(cols), hipMemcpyHostToDevice, w->stream));
-  return hipStreamSynchronize(w->stream);
-}
-
-static hipError_t ensure_tiles(Workspace* w, uint64_t ntiles) {
-  if (ntiles + 2 <= w->cap_tiles) return hipSuccess;
-  if (w->part) HIP_TRY(hipFree(w->part));
-  w->cap_tiles = ntiles + 2 + ntiles / 4;
-  return hipMalloc((void**)&w->part, w->cap_tiles * sizeof(uint32_t));
-}
-
-hipError_t k_degree_scan(Workspace* w, const ExpandArgs& a, uint64_t* total) {
-  if (a.n == 0) { *total = 0; return hipSuccess; }
-  if (a.n > w->cap_frontier) return hipErrorInvalidValue;
-  uint64_t nb = cdiv(a.n, SCAN_TILE);
-  hipEvent_t p = prof_begin(w);
-  hipLaunchKernelGGL(k_degree, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, a.frontier, a.n, a.row_ptr,
-                     a.visible, a.cap, w->seg_end, w->seg_rs, w->block_sum);
-  prof_end(w, p, K_DEGREE, 12.0 * (double)a.n);   // 4|F| ids + 8|F| row_ptr pairs
-  p = prof_begin(w);
-  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, w->stream, w->block_sum, nb, w->counters);
-  prof_end(w, p, K_SCAN, 0.0);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(w->h_pinned, w->counters, 8, hipMemcpyDeviceToHost, w->stream));
-  HIP_TRY(hipStreamSynchronize(w->stream));
-  prof_flush(w);
-  *total = w->h_pinned[0];
+  HIP_TRY(hipMemcpy(w->d_row_cols, cols, sizeof(cols), hipMemcpyHostToDevice));
   return hipSuccess;
 }
 
-static hipError_t launch_partition(Workspace* w, const ExpandArgs& a, uint64_t total, uint64_t* ntiles_out) {
-  uint64_t ntiles = cdiv(a.n + total, TILE);
-  HIP_TRY(ensure_tiles(w, ntiles));
+hipError_t ws_begin_query(Workspace* w, const uint32_t* starts, uint64_t n, const std::vector<TypeProgram>* progs) {
+  if (n > w->cap_frontier) return hipErrorInvalidValue;
+  if (n > w->cap_starts) {
+    if (w->h_starts) HIP_TRY(hipHostFree(w->h_starts));
+    w->cap_starts = n + n / 2 + 1024;
+    HIP_TRY(hipHostMalloc((void**)&w->h_starts, w->cap_starts * 4, hipHostMallocDefault));
+  }
+  // the previous query on this workspace has completed (its end synchronised the stream)
+  memcpy(w->h_starts, starts, n * 4);
+  memset(w->h_q, 0, sizeof(QState));
+  w->h_q->n = n;
+  w->h_q->step_n[1] = n;
+  w->cur = 0;
+  HIP_TRY(hipMemcpyAsync(w->frontier[0], w->h_starts, n * 4, hipMemcpyHostToDevice, w->stream));
+  HIP_TRY(hipMemcpyAsync(w->q, w->h_q, sizeof(QState), hipMemcpyHostToDevice, w->stream));
+  if (progs && !progs->empty()) {
+    size_t k = 0;
+    for (auto& p : *progs) {
+      memcpy(w->h_prog + k * MAX_PROGRAM, p.code.data(), p.code.size() * sizeof(Ins));
+      ++k;
+    }
+    HIP_TRY(hipMemcpyAsync(w->d_prog, w->h_prog, k * MAX_PROGRAM * sizeof(Ins), hipMemcpyHostToDevice, w->stream));
+  }
+  return hipSuccess;
+}
+
+// Enqueue k_degree + k_scan_blocks for the current frontier (n <= n_bound) over one type.
+static hipError_t enqueue_scan(Workspace* w, const ExpandArgs& a, uint64_t n_bound, int step, int tix) {
+  uint64_t nb = cdiv(n_bound ? n_bound : 1, SCAN_TILE);
   hipEvent_t p = prof_begin(w);
-  hipLaunchKernelGGL(k_partition, dim3((unsigned)cdiv(ntiles + 1, 256)), dim3(256), 0, w->stream, w->seg_end,
-                     w->block_sum, a.n, total, ntiles, w->part);
-  prof_end(w, p, K_PARTITION, 0.0);
-  *ntiles_out = ntiles;
+  hipLaunchKernelGGL(k_degree, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->frontier[w->cur], w->q, a.row_ptr,
+                     a.visible, a.cap, w->seg_end, w->seg_rs, w->block_sum);
+  prof_end(w, p, K_DEGREE, step, tix);
+  p = prof_begin(w);
+  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, w->stream, w->block_sum, w->q, (uint64_t)0,
+                     &w->q->total, &w->q->e_st[step][tix]);
+  prof_end(w, p, K_SCAN, step, tix);
   return hipGetLastError();
 }
 
-hipError_t k_expand_mark(Workspace* w, const ExpandArgs& a, uint64_t total) {
-  if (total == 0) return hipSuccess;
-  uint64_t ntiles;
-  HIP_TRY(launch_partition(w, a, total, &ntiles));
+static unsigned expand_grid(uint64_t n_bound, uint64_t e_bound) {
+  uint64_t tiles = cdiv(n_bound + e_bound + 1, TILE);
+  return (unsigned)(tiles < EXPAND_GRID ? (tiles ? tiles : 1) : EXPAND_GRID);
+}
+
+hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, uint64_t e_bound, int step, int tix) {
+  if (step > MAX_STEPS || tix >= MAX_TYPES_Q) return hipErrorInvalidValue;
+  HIP_TRY(enqueue_scan(w, a0, n_bound, step, tix));
+  ExpandArgs a = a0;
+  a.frontier = w->frontier[w->cur];
   FinalParams fp{};
   hipEvent_t p = prof_begin(w);
-  hipLaunchKernelGGL(k_expand<MARK>, dim3((unsigned)ntiles), dim3(BLOCK), 0, w->stream, a, w->seg_end,
-                     w->block_sum, w->seg_rs, w->part, total, w->flags, fp);
-  prof_end(w, p, K_EXPAND_MARK, 4.0 * (double)total);   // 4 E_s neighbour ids
+  hipLaunchKernelGGL(k_expand<MARK>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, w->q,
+                     w->seg_end, w->block_sum, w->seg_rs, w->flags, fp);
+  prof_end(w, p, K_EXPAND_MARK, step, tix);
   return hipGetLastError();
 }
 
-hipError_t k_compact(Workspace* w, uint64_t nv, uint32_t* next, uint64_t* count) {
+hipError_t ws_compact(Workspace* w, int step) {
   uint64_t nb = w->flag_bytes / FLAG_BYTES;
+  uint32_t* next = w->frontier[w->cur ^ 1];
   hipEvent_t p = prof_begin(w);
   hipLaunchKernelGGL(k_flag_count, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->flags, w->flag_bytes,
                      w->flag_blocks);
-  prof_end(w, p, K_FLAG_COUNT, 0.0);
+  prof_end(w, p, K_FLAG_COUNT, step, 0);
   p = prof_begin(w);
-  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, w->stream, w->flag_blocks, nb, w->counters);
-  prof_end(w, p, K_SCAN, 0.0);
+  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, w->stream, w->flag_blocks, w->q, nb, &w->q->n,
+                     &w->q->step_n[step + 1]);
+  prof_end(w, p, K_SCAN, step, 0);
   p = prof_begin(w);
-  hipLaunchKernelGGL(k_flag_write, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->flags, w->flag_bytes, nv,
+  hipLaunchKernelGGL(k_flag_write, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->flags, w->flag_bytes, w->nv,
                      w->flag_blocks, next);
-  prof_end(w, p, K_FLAG_WRITE, 0.0);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(w->h_pinned, w->counters, 8, hipMemcpyDeviceToHost, w->stream));
-  HIP_TRY(hipStreamSynchronize(w->stream));
-  *count = w->h_pinned[0];
-  if (!w->prof.pending.empty()) w->prof.pending.back().bytes = 4.0 * (double)*count;   // write F_{s+1}
-  prof_flush(w);
-  return hipSuccess;
+  prof_end(w, p, K_FLAG_WRITE, step, 0);
+  w->cur ^= 1;
+  return hipGetLastError();
 }
 
 // distinct 8-byte edge columns a program reads per edge (props, _dst, _rank)
@@ -667,43 +809,96 @@ static int edge_columns_read(const TypeProgram& prog) {
   return n;
 }
 
-hipError_t k_expand_final(Workspace* w, const ExpandArgs& a, uint64_t total, const TypeProgram& prog,
-                          const Ins* d_prog, int64_t** d_out_cols, uint64_t row_base, uint64_t* rows_out,
-                          int* err_out) {
-  *rows_out = 0;
-  *err_out = 0;
-  if (total == 0) return hipSuccess;
-  uint64_t ntiles;
-  HIP_TRY(launch_partition(w, a, total, &ntiles));
+// Recognise the FastProg shapes in the compiled bytecode (see FastProg).
+static FastProg detect_fast(const TypeProgram& prog, const ExpandArgs& a) {
+  FastProg f{};
+  f.enabled = 0;
+  f.where_col = -1;
+  auto leaf_col = [&](const Ins& i) {
+    return i.op == OP_COL || (i.op == OP_COLV && a.valid == nullptr);
+  };
+  if (prog.where_reg >= 0) {
+    if (prog.where_len != 3) return f;
+    const Ins &i0 = prog.code[0], &i1 = prog.code[1], &c = prog.code[2];
+    static const int kOps[6] = {OP_LT_I, OP_LE_I, OP_GT_I, OP_GE_I, OP_EQ_I, OP_NE_I};
+    static const int kSwap[6] = {2, 3, 0, 1, 4, 5};   // const <op> col  ==  col <swap(op)> const
+    int op = -1;
+    for (int k = 0; k < 6; ++k)
+      if (c.op == kOps[k]) op = k;
+    if (op < 0 || c.d != prog.where_reg) return f;
+    const Ins* colI = nullptr;
+    const Ins* constI = nullptr;
+    if (leaf_col(i0) && i1.op == OP_CONST) { colI = &i0; constI = &i1; }
+    else if (i0.op == OP_CONST && leaf_col(i1)) { colI = &i1; constI = &i0; }
+    else return f;
+    if (c.a == colI->d && c.b == constI->d) f.where_op = op;
+    else if (c.a == constI->d && c.b == colI->d) f.where_op = kSwap[op];
+    else return f;
+    f.where_col = colI->aux;
+    f.where_const = constI->imm;
+  }
+  const int ny = (int)prog.yield_reg.size();
+  int pc = prog.where_len;
+  for (int y = 0; y < ny; ++y) {
+    if (prog.yield_reg[y] < 0) { f.ykind[y] = 4; continue; }
+    if (pc >= (int)prog.code.size()) return f;
+    const Ins& i = prog.code[pc++];
+    if (i.d != prog.yield_reg[y]) return f;
+    if (i.op == OP_DST) f.ykind[y] = 0;
+    else if (i.op == OP_SRC) f.ykind[y] = 1;
+    else if (i.op == OP_RANK) f.ykind[y] = 2;
+    else if (leaf_col(i)) { f.ykind[y] = 3; f.ycol[y] = i.aux; }
+    else return f;
+  }
+  if (pc != (int)prog.code.size()) return f;
+  f.enabled = 1;
+  return f;
+}
+
+uint64_t ws_shard_cap(uint64_t n_bound, uint64_t e_bound) {
+  uint64_t tiles = cdiv(n_bound + e_bound + 1, TILE);
+  return cdiv(tiles, NSHARD) * TILE;
+}
+
+hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, uint64_t e_bound, int step, int tix,
+                           const TypeProgram& prog, uint64_t region_base, uint64_t shard_cap) {
+  if (step > MAX_STEPS || tix >= MAX_TYPES_Q) return hipErrorInvalidValue;
+  HIP_TRY(enqueue_scan(w, a0, n_bound, step, tix));
+  ExpandArgs a = a0;
+  a.frontier = w->frontier[w->cur];
   FinalParams fp{};
-  fp.prog = d_prog;
+  fp.prog = w->d_prog + (size_t)tix * MAX_PROGRAM;
   fp.where_len = prog.where_len;
   fp.where_reg = prog.where_reg;
   fp.prog_len = (int)prog.code.size();
   fp.nyields = (int)prog.yield_reg.size();
-  int kout = 0;
   for (int y = 0; y < fp.nyields; ++y) {
     fp.yield_reg[y] = prog.yield_reg[y];
     fp.yield_const[y] = prog.yield_const[y];
-    kout += 1;
   }
-  fp.out_cols = d_out_cols;
-  fp.row_base = row_base;
-  fp.row_counter = w->counters + 1;
-  fp.err_flag = w->counters + 2;
-  HIP_TRY(hipMemsetAsync(w->counters + 1, 0, 2 * sizeof(uint64_t), w->stream));
-  size_t lds = (size_t)(prog.nregs > 0 ? prog.nregs : 1) * BLOCK * sizeof(int64_t);
+  fp.out_cols = w->d_row_cols;
+  fp.region_base = region_base;
+  fp.shard_cap = shard_cap;
+  fp.shard_rows = &w->q->rows[tix][0];
+  fp.err_flag = &w->q->err;
+  fp.fast = detect_fast(prog, a);
+  size_t lds = fp.fast.enabled ? 0 : (size_t)(prog.nregs > 0 ? prog.nregs : 1) * BLOCK * sizeof(int64_t);
   hipEvent_t p = prof_begin(w);
-  hipLaunchKernelGGL(k_expand<FINAL>, dim3((unsigned)ntiles), dim3(BLOCK), lds, w->stream, a, w->seg_end,
-                     w->block_sum, w->seg_rs, w->part, total, w->flags, fp);
-  prof_end(w, p, K_EXPAND_FINAL, 8.0 * (double)total * edge_columns_read(prog));
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(w->h_pinned, w->counters, 24, hipMemcpyDeviceToHost, w->stream));
+  hipLaunchKernelGGL(k_expand<FINAL>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), lds, w->stream, a, w->q,
+                     w->seg_end, w->block_sum, w->seg_rs, w->flags, fp);
+  prof_end(w, p, K_EXPAND_FINAL, step, tix, (double)edge_columns_read(prog), (double)fp.nyields);
+  return hipGetLastError();
+}
+
+// Scan-only expansion (final step whose WHERE folded to false still counts E_N).
+hipError_t ws_scan_only(Workspace* w, const ExpandArgs& a, uint64_t n_bound, int step, int tix) {
+  return enqueue_scan(w, a, n_bound, step, tix);
+}
+
+hipError_t ws_end_query(Workspace* w) {
+  HIP_TRY(hipMemcpyAsync(w->h_q, w->q, sizeof(QState), hipMemcpyDeviceToHost, w->stream));
   HIP_TRY(hipStreamSynchronize(w->stream));
-  *rows_out = w->h_pinned[1];
-  *err_out = w->h_pinned[2] != 0;
-  if (!w->prof.pending.empty()) w->prof.pending.back().bytes += 8.0 * (double)*rows_out * kout;   // R * 8k
-  prof_flush(w);
+  prof_flush(w, w->h_q);
   return hipSuccess;
 }
 

@@ -146,9 +146,26 @@ struct TypeProgram {
 };
 
 // ----------------------------------------------------------------------------- kernel interface
+constexpr int VT = 4;                  // k_expand: path items per thread
+constexpr int TILE = 256 * VT;         // path items (frontier segments + edges) per tile
+constexpr int NSHARD = 64;             // row-output shards (one counter + region each)
+constexpr int MAX_STEPS = 32;          // GO N STEPS upper bound
+constexpr int MAX_TYPES_Q = 16;        // OVER types per query
+
+// Device-resident state of one query: every size the kernels need, so a query is enqueued
+// without host synchronisation; the host reads it back once at the end.
+struct QState {
+  unsigned long long n;                // current frontier size
+  unsigned long long total;            // edges of the current (step, type) expansion
+  unsigned long long err;              // WHERE/YIELD evaluation error
+  unsigned long long pad;
+  unsigned long long step_n[MAX_STEPS + 2];              // frontier size entering step s
+  unsigned long long e_st[MAX_STEPS + 2][MAX_TYPES_Q];   // edges per (step, type)
+  unsigned long long rows[MAX_TYPES_Q][NSHARD];          // rows per (type, shard) at step N
+};
+
 struct ExpandArgs {                // one (step, edge type) expansion
-  const uint32_t* frontier;        // [n] dense ids
-  uint64_t n;
+  const uint32_t* frontier;        // filled in by the workspace (current buffer)
   const uint32_t* row_ptr;
   const uint32_t* col;
   const int64_t* dst_vid;
@@ -166,26 +183,23 @@ Workspace* ws_create(uint64_t max_frontier, uint64_t nv, hipStream_t s, std::str
 void ws_destroy(Workspace* w);
 void ws_profile(Workspace* w, bool on);
 int ws_profile_read(Workspace* w, nbg_kernel_stat* out, int cap);
+uint64_t ws_cap_frontier(Workspace* w);
 hipError_t ws_reserve_rows(Workspace* w, uint64_t rows, int ncols);
+int64_t* ws_row_col(Workspace* w, int c);       // device pointer of output column c
+uint64_t ws_shard_cap(uint64_t n_bound, uint64_t e_bound);
+const QState* ws_host_state(Workspace* w);       // valid after ws_end_query
+const uint32_t* ws_current_frontier(Workspace* w);
 
-// Returns total edges of this expansion (host sync inside).
-hipError_t k_degree_scan(Workspace* w, const ExpandArgs& a, uint64_t* total);
-// Intermediate step: mark next-frontier flags for every scanned edge.
-hipError_t k_expand_mark(Workspace* w, const ExpandArgs& a, uint64_t total);
-// Compact flags into the next frontier (sorted), clearing flags.  Returns the new size.
-hipError_t k_compact(Workspace* w, uint64_t nv, uint32_t* next, uint64_t* count);
-// Final step: evaluate program, emit rows at w->row_count.  err_out != 0 if any lane errored.
-hipError_t k_expand_final(Workspace* w, const ExpandArgs& a, uint64_t total, const TypeProgram& prog,
-                          const Ins* d_prog, int64_t** d_out_cols, uint64_t row_base,
-                          uint64_t* rows_out, int* err_out);
-
-// Frontier double buffers and other workspace accessors.
-uint32_t* ws_frontier(Workspace* w, int which);
-int64_t** ws_row_cols(Workspace* w);        // device array of output column pointers
-int64_t* ws_row_col(Workspace* w, int c);   // device pointer of output column c
-Ins* ws_program(Workspace* w);
-
-// Path kernels (FIND PATH) — kernels.hip
-struct BfsSide;
+// Query pipeline (all asynchronous on the workspace stream until ws_end_query):
+hipError_t ws_begin_query(Workspace* w, const uint32_t* starts, uint64_t n, const std::vector<TypeProgram>* progs);
+// steps 1..N-1, per OVER type: scan + expand into next-frontier flags
+hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a, uint64_t n_bound, uint64_t e_bound, int step, int tix);
+// after all types of a step: flags -> next frontier
+hipError_t ws_compact(Workspace* w, int step);
+// step N, per OVER type: scan + WHERE/YIELD + sharded row emission into [region_base, +NSHARD*shard_cap)
+hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a, uint64_t n_bound, uint64_t e_bound, int step, int tix,
+                           const TypeProgram& prog, uint64_t region_base, uint64_t shard_cap);
+hipError_t ws_scan_only(Workspace* w, const ExpandArgs& a, uint64_t n_bound, int step, int tix);
+hipError_t ws_end_query(Workspace* w);
 
 }  // namespace nbg
