@@ -180,6 +180,8 @@ int32_t nbg_find_path(nbg_engine* e, const nbg_path_request* req, nbg_paths** ou
 int64_t nbg_paths_count(const nbg_paths* p);
 int64_t nbg_path_len(const nbg_paths* p, int64_t i);
 const int64_t* nbg_path_entries(const nbg_paths* p, int64_t i);
+/* Adjacency entries the search scanned (both directions; TEPS numerator). */
+uint64_t nbg_paths_edges_scanned(const nbg_paths* p);
 void nbg_paths_free(nbg_paths* p);
 
 /* ---- in-library kernel timing (HIP events on the engine's stream) ----------------------- */

@@ -87,6 +87,7 @@ SIGNATURES = [
     ("nbg_paths_count", i64, [vp]),
     ("nbg_path_len", i64, [vp, i64]),
     ("nbg_path_entries", P(i64), [vp, i64]),
+    ("nbg_paths_edges_scanned", u64, [vp]),
     ("nbg_paths_free", None, [vp]),
     ("nbg_profile", i32, [vp, i32]),
     ("nbg_profile_read", i32, [vp, vp, i32]),

@@ -47,10 +47,6 @@ struct nbg_rows {
   std::vector<uint64_t> step_frontier, step_edges;
 };
 
-struct nbg_paths {
-  std::vector<std::vector<int64_t>> paths;
-};
-
 namespace {
 
 int32_t materialize_rows(nbg_rows* r) {
@@ -500,6 +496,7 @@ int64_t nbg_path_len(const nbg_paths* p, int64_t i) {
 const int64_t* nbg_path_entries(const nbg_paths* p, int64_t i) {
   return (p && i >= 0 && i < (int64_t)p->paths.size()) ? p->paths[i].data() : nullptr;
 }
+uint64_t nbg_paths_edges_scanned(const nbg_paths* p) { return p ? p->edges : 0; }
 void nbg_paths_free(nbg_paths* p) { delete p; }
 
 }  // extern "C"

@@ -50,3 +50,8 @@ struct Engine {
 struct nbg_engine {
   nbg::Engine e;
 };
+
+struct nbg_paths {
+  std::vector<std::vector<int64_t>> paths;
+  uint64_t edges = 0;   // BFS adjacency entries scanned, both directions
+};

@@ -41,13 +41,14 @@ constexpr int FLAG_BYTES = BLOCK * 16;           // k_flag_*: bytes per block
 constexpr int EXPAND_GRID = 2048;                // persistent k_expand grid (8 blocks / CU)
 
 enum KernelId { K_DEGREE = 0, K_SCAN, K_EXPAND_MARK, K_FLAG_COUNT, K_FLAG_WRITE, K_EXPAND_FINAL, K_BFS,
-                K_COUNT };
+                K_GATHER, K_DEGSUM, K_GREEDY, K_STAMP, K_COUNT };
 static const char* const kKernelNames[K_COUNT] = {"k_degree", "k_scan_blocks", "k_expand<MARK>", "k_flag_count",
-                                                  "k_flag_write", "k_expand<FINAL>", "k_expand<BFS>"};
+                                                  "k_flag_write", "k_expand<FINAL>", "k_expand<BFS>", "k_gather",
+                                                  "k_degsum", "k_path_greedy", "k_stamp"};
 
 struct Prof {
   bool on = false;
-  struct Rec { int kid, step, tix; hipEvent_t a, b; double cols, kout; };
+  struct Rec { int kid, step, tix; hipEvent_t a, b; double cols, kout; bool path; };
   std::vector<Rec> pending;
   std::vector<hipEvent_t> pool;
   uint64_t launches[K_COUNT] = {};
@@ -85,6 +86,19 @@ struct Workspace {
   int ncols_alloc = 0;
   int64_t** d_row_cols = nullptr; // device array of column pointers
   Ins* d_prog = nullptr;          // [MAX_TYPES_Q][MAX_PROGRAM]
+  // FIND PATH (allocated on first use)
+  PState* ps = nullptr;
+  PState* h_ps = nullptr;         // pinned mirror
+  uint32_t* lab[NUM_LABS] = {};   // [nv] epoch-stamped labels
+  uint32_t epoch[NUM_LABS] = {};
+  uint32_t* slot[PSLOTS] = {};    // frontier / B-set / meet lists
+  uint64_t slot_cap = 0;
+  uint32_t* pscratch = nullptr;   // claim shards
+  uint64_t pscratch_cap = 0;
+  int64_t* d_path = nullptr;      // [1 + 3 MAX_PATH_LEN]
+  int64_t* h_path = nullptr;
+  uint32_t* h_stage = nullptr;    // pinned [PSLOTS][STAGE] upload staging (one upload per slot per query)
+  int rec = 0;                    // next PState expansion record
 };
 
 // ----------------------------------------------------------------------------- helpers
@@ -117,13 +131,21 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* total,
 }
 
 // ----------------------------------------------------------------------------- k_degree
-__global__ void __launch_bounds__(BLOCK) k_degree(const uint32_t* __restrict__ frontier, const QState* __restrict__ q,
+// `reset` (nullable): NSHARD counters zeroed by block 0 (the BFS claim shards of the previous
+// expansion, consumed by k_gather before this launch in stream order).
+__global__ void __launch_bounds__(BLOCK) k_degree(const uint32_t* __restrict__ frontier,
+                                                  const unsigned long long* __restrict__ np,
                                                   const uint32_t* __restrict__ row_ptr,
                                                   const uint8_t* __restrict__ visible, uint32_t cap,
                                                   uint32_t* __restrict__ seg_end, uint32_t* __restrict__ seg_rs,
-                                                  uint32_t* __restrict__ block_sum) {
+                                                  uint32_t* __restrict__ block_sum, unsigned long long* reset,
+                                                  unsigned long long* n_rec) {
   __shared__ uint32_t lds[WAVES];
-  const uint64_t n = q->n;
+  const uint64_t n = *np;
+  if (blockIdx.x == 0) {
+    if (reset && threadIdx.x < NSHARD) reset[threadIdx.x] = 0;
+    if (n_rec && threadIdx.x == 0) *n_rec = n;
+  }
   if ((uint64_t)blockIdx.x * SCAN_TILE >= n) return;
   const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
   uint32_t deg[SCAN_ITEMS], rs[SCAN_ITEMS];
@@ -158,13 +180,14 @@ __global__ void __launch_bounds__(BLOCK) k_degree(const uint32_t* __restrict__ f
   if (threadIdx.x == 0) block_sum[blockIdx.x] = total;
 }
 
-// One workgroup: exclusive scan of nb uint32 in place.  nb = fixed_nb, or ceil(q->n / 2048) when
-// fixed_nb == 0.  The grand total goes to *total_out and is added to *accum (stats).
-__global__ void __launch_bounds__(1024) k_scan_blocks(uint32_t* __restrict__ v, const QState* qn, uint64_t fixed_nb,
-                                                      unsigned long long* total_out, unsigned long long* accum) {
+// One workgroup: exclusive scan of nb uint32 in place.  nb = fixed_nb, or ceil(*np / 2048) when
+// fixed_nb == 0.  The grand total goes to *total_out and is added to *accum (stats, nullable).
+__global__ void __launch_bounds__(1024) k_scan_blocks(uint32_t* __restrict__ v, const unsigned long long* np,
+                                                      uint64_t fixed_nb, unsigned long long* total_out,
+                                                      unsigned long long* accum) {
   __shared__ uint64_t lds[16];
   __shared__ uint64_t carry;
-  const uint64_t nb = fixed_nb ? fixed_nb : (qn->n + SCAN_TILE - 1) / SCAN_TILE;
+  const uint64_t nb = fixed_nb ? fixed_nb : (*np + SCAN_TILE - 1) / SCAN_TILE;
   if (threadIdx.x == 0) carry = 0;
   __syncthreads();
   for (uint64_t base = 0; base < nb; base += 1024) {
@@ -329,7 +352,30 @@ __device__ __forceinline__ void run_program(const Ins* __restrict__ prog, int pc
 }
 
 // ----------------------------------------------------------------------------- k_expand
-enum Mode { MARK = 0, FINAL = 1 };
+enum Mode { MARK = 0, FINAL = 1, BFS = 2 };
+
+// BFS-mode expansion (FIND SHORTEST PATH): every neighbour w is claimed at most once per epoch by
+// a CAS on its label (epoch << LVL_BITS | level); winners are appended, one atomic per tile on a
+// sharded counter, to NSHARD regions of `out` that k_gather then packs into the next frontier.
+struct BfsParams {
+  uint32_t* lab;                  // claim labels
+  uint32_t stamp;                 // claimed label value
+  uint32_t epoch;                 // a label is live when (lab >> LVL_BITS) == epoch
+  const uint32_t* rlab;           // restriction (nullable): claim w only if rlab[w] == rstamp
+  uint32_t rstamp;
+  const uint32_t* mlab;           // meet test (nullable): a claimed w with a live mlab label met
+  uint32_t mepoch;                //   the other search side
+  uint32_t* mout;                 // meets: mout[w] = mstamp, w appended to meet_list
+  uint32_t mstamp;
+  uint32_t* meet_list;
+  unsigned long long* meet_n;
+  const uint32_t* tlab;           // targets (nullable): claimed w with tlab[w] == tstamp counts
+  uint32_t tstamp;
+  unsigned long long* found;
+  uint32_t* out;                  // shard regions [NSHARD][shard_cap]
+  uint64_t shard_cap;
+  unsigned long long* shard_cnt;  // [NSHARD]
+};
 
 struct FinalParams {
   const Ins* prog;
@@ -348,11 +394,12 @@ struct FinalParams {
 };
 
 template <int M>
-__global__ void __launch_bounds__(BLOCK) k_expand(ExpandArgs a, const QState* __restrict__ q,
+__global__ void __launch_bounds__(BLOCK) k_expand(ExpandArgs a, const unsigned long long* __restrict__ np,
+                                                  const unsigned long long* __restrict__ totp,
                                                   const uint32_t* __restrict__ seg_end,
                                                   const uint32_t* __restrict__ block_pre,
                                                   const uint32_t* __restrict__ seg_rs, uint8_t* __restrict__ flags,
-                                                  FinalParams fp) {
+                                                  FinalParams fp, BfsParams bp) {
   __shared__ uint32_t sEnd[TILE + 2];   // seg_end for i in [a0-1, a1]
   __shared__ uint32_t sRs[TILE + 1];    // seg_rs for i in [a0, a1]
   __shared__ uint32_t sSeg[TILE];       // segment of each edge item in this tile
@@ -361,8 +408,8 @@ __global__ void __launch_bounds__(BLOCK) k_expand(ExpandArgs a, const QState* __
   __shared__ uint64_t sBase;
   extern __shared__ int64_t regs[];     // FINAL generic path: [nregs][BLOCK]
 
-  const uint64_t n = q->n;
-  const uint64_t total = q->total;
+  const uint64_t n = *np;
+  const uint64_t total = *totp;
   const uint64_t npath = n + total;
   const uint64_t ntiles = (npath + TILE - 1) / TILE;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -426,6 +473,64 @@ __global__ void __launch_bounds__(BLOCK) k_expand(ExpandArgs a, const QState* __
         uint64_t j = (uint64_t)sRs[s] + (e - (uint64_t)sEnd[s]);   // sEnd[s] = start of segment a0+s
         uint32_t u = a.col[j];
         if (u != NO_ROW) flags[u] = 1;
+      }
+    } else if (M == BFS) {
+      uint32_t wv[VT];
+      uint32_t cmask = 0, mmask = 0;
+#pragma unroll
+      for (int i = 0; i < VT; ++i) {
+        const int k = i * BLOCK + threadIdx.x;
+        wv[i] = NO_ROW;
+        if (k < nb) {
+          uint32_t s = sSeg[k];
+          wv[i] = a.col[(uint64_t)sRs[s] + (b0 + k - (uint64_t)sEnd[s])];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < VT; ++i) {
+        const uint32_t x = wv[i];
+        if (x == NO_ROW) continue;
+        if (bp.rlab && bp.rlab[x] != bp.rstamp) continue;
+        const uint32_t old = bp.lab[x];
+        if ((old >> LVL_BITS) == bp.epoch) continue;
+        if (atomicCAS(bp.lab + x, old, bp.stamp) != old) continue;
+        cmask |= 1u << i;
+        if (bp.mlab && (bp.mlab[x] >> LVL_BITS) == bp.mepoch) mmask |= 1u << i;
+        if (bp.tlab && bp.tlab[x] == bp.tstamp) atomicAdd(bp.found, 1ull);
+      }
+#pragma unroll
+      for (int i = 0; i < VT; ++i) {
+        unsigned long long bal = __ballot((cmask >> i) & 1u);
+        if (lane == 0) sCnt[i * WAVES + w] = (uint32_t)__popcll(bal);
+      }
+      __syncthreads();
+      const uint64_t shard = t % NSHARD;
+      if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int k = 0; k < VT * WAVES; ++k) {
+          uint32_t c = sCnt[k];
+          sCnt[k] = run;
+          run += c;
+        }
+        sBase = run ? atomicAdd(bp.shard_cnt + shard, (unsigned long long)run) : 0ull;
+      }
+      __syncthreads();
+      uint32_t* const region = bp.out + shard * bp.shard_cap + sBase;
+      for (int i = 0; i < VT; ++i) {
+        const bool c = (cmask >> i) & 1u;
+        unsigned long long bal = __ballot(c);
+        if (c) region[sCnt[i * WAVES + w] + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = wv[i];
+        const bool m = (mmask >> i) & 1u;
+        unsigned long long mb = __ballot(m);
+        if (mb) {
+          unsigned long long base = 0;
+          if (lane == 0) base = atomicAdd(bp.meet_n, (unsigned long long)__popcll(mb));
+          base = __shfl(base, 0, 64);
+          if (m) {
+            bp.meet_list[base + (uint32_t)__popcll(mb & ((1ull << lane) - 1ull))] = wv[i];
+            bp.mout[wv[i]] = bp.mstamp;
+          }
+        }
       }
     } else {
       // phase A: WHERE for every item of the tile (VT items per thread, striped)
@@ -596,7 +701,7 @@ static void prof_end(Workspace* w, hipEvent_t a, int kid, int step, int tix, dou
   if (!a) return;
   hipEvent_t b = w->prof.get();
   (void)hipEventRecord(b, w->stream);
-  w->prof.pending.push_back({kid, step, tix, a, b, cols, kout});
+  w->prof.pending.push_back({kid, step, tix, a, b, cols, kout, false});
 }
 // algorithmic bytes per kernel (SURVEY.md §8(d) B_GO terms)
 static double prof_bytes(const Prof::Rec& r, const QState& q) {
@@ -607,18 +712,36 @@ static double prof_bytes(const Prof::Rec& r, const QState& q) {
     case K_EXPAND_FINAL: {
       double rows = 0;
       for (int s = 0; s < NSHARD; ++s) rows += (double)q.rows[r.tix][s];
-      return 8.0 * (double)q.e_st[r.step][r.tix] * r.cols + 8.0 * rows * r.kout;
+      // SURVEY §8(d) B_GO final-step terms: 4 E_N neighbour ids + 8 E_N per WHERE/YIELD edge
+      // property column + 8 k per emitted row
+      return (double)q.e_st[r.step][r.tix] * (4.0 + 8.0 * r.cols) + 8.0 * rows * r.kout;
     }
     default: return 0.0;
   }
 }
-static void prof_flush(Workspace* w, const QState* q) {
+// FIND PATH launches: r.step indexes the per-query expansion records of PState (B_SP terms:
+// 4|F| ids + 8|F| row_ptr, 4 E neighbour ids, 4 per claimed vertex written)
+static double prof_bytes_path(const Prof::Rec& r, const PState& p) {
+  const int i = r.step < PATH_REC ? r.step : PATH_REC - 1;
+  switch (r.kid) {
+    case K_DEGREE: return 12.0 * (double)p.ln[i];
+    case K_BFS: return 4.0 * (double)p.le[i];
+    case K_GATHER: return 8.0 * (double)p.lc[i];
+    case K_DEGSUM: return 12.0 * (double)p.ln[i];
+    default: return 0.0;
+  }
+}
+static void prof_flush(Workspace* w, const QState* q, const PState* ps = nullptr) {
   for (auto& r : w->prof.pending) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
       w->prof.launches[r.kid]++;
       w->prof.ms[r.kid] += ms;
-      if (q) w->prof.bytes[r.kid] += prof_bytes(r, *q);
+      if (r.path) {
+        if (ps) w->prof.bytes[r.kid] += prof_bytes_path(r, *ps);
+      } else if (q) {
+        w->prof.bytes[r.kid] += prof_bytes(r, *q);
+      }
     }
     w->prof.pool.push_back(r.a);
     w->prof.pool.push_back(r.b);
@@ -688,8 +811,15 @@ void ws_destroy(Workspace* w) {
                   (void*)w->block_sum, (void*)w->flags, (void*)w->flag_blocks, (void*)w->q, (void*)w->rows,
                   (void*)w->d_row_cols, (void*)w->d_prog})
     if (p) (void)hipFree(p);
-  for (void* p : {(void*)w->h_q, (void*)w->h_starts, (void*)w->h_prog})
+  for (void* p : {(void*)w->h_q, (void*)w->h_starts, (void*)w->h_prog, (void*)w->h_ps, (void*)w->h_path,
+                  (void*)w->h_stage})
     if (p) (void)hipHostFree(p);
+  for (void* p : {(void*)w->ps, (void*)w->pscratch, (void*)w->d_path})
+    if (p) (void)hipFree(p);
+  for (auto* p : w->lab)
+    if (p) (void)hipFree(p);
+  for (auto* p : w->slot)
+    if (p) (void)hipFree(p);
   for (auto& r : w->prof.pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
   for (auto e : w->prof.pool) (void)hipEventDestroy(e);
   delete w;
@@ -748,11 +878,12 @@ hipError_t ws_begin_query(Workspace* w, const uint32_t* starts, uint64_t n, cons
 static hipError_t enqueue_scan(Workspace* w, const ExpandArgs& a, uint64_t n_bound, int step, int tix) {
   uint64_t nb = cdiv(n_bound ? n_bound : 1, SCAN_TILE);
   hipEvent_t p = prof_begin(w);
-  hipLaunchKernelGGL(k_degree, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->frontier[w->cur], w->q, a.row_ptr,
-                     a.visible, a.cap, w->seg_end, w->seg_rs, w->block_sum);
+  hipLaunchKernelGGL(k_degree, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->frontier[w->cur], &w->q->n,
+                     a.row_ptr, a.visible, a.cap, w->seg_end, w->seg_rs, w->block_sum,
+                     (unsigned long long*)nullptr, (unsigned long long*)nullptr);
   prof_end(w, p, K_DEGREE, step, tix);
   p = prof_begin(w);
-  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, w->stream, w->block_sum, w->q, (uint64_t)0,
+  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, w->stream, w->block_sum, &w->q->n, (uint64_t)0,
                      &w->q->total, &w->q->e_st[step][tix]);
   prof_end(w, p, K_SCAN, step, tix);
   return hipGetLastError();
@@ -770,8 +901,8 @@ hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, 
   a.frontier = w->frontier[w->cur];
   FinalParams fp{};
   hipEvent_t p = prof_begin(w);
-  hipLaunchKernelGGL(k_expand<MARK>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, w->q,
-                     w->seg_end, w->block_sum, w->seg_rs, w->flags, fp);
+  hipLaunchKernelGGL(k_expand<MARK>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, &w->q->n,
+                     &w->q->total, w->seg_end, w->block_sum, w->seg_rs, w->flags, fp, BfsParams{});
   prof_end(w, p, K_EXPAND_MARK, step, tix);
   return hipGetLastError();
 }
@@ -784,7 +915,7 @@ hipError_t ws_compact(Workspace* w, int step) {
                      w->flag_blocks);
   prof_end(w, p, K_FLAG_COUNT, step, 0);
   p = prof_begin(w);
-  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, w->stream, w->flag_blocks, w->q, nb, &w->q->n,
+  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, w->stream, w->flag_blocks, &w->q->n, nb, &w->q->n,
                      &w->q->step_n[step + 1]);
   prof_end(w, p, K_SCAN, step, 0);
   p = prof_begin(w);
@@ -795,16 +926,14 @@ hipError_t ws_compact(Workspace* w, int step) {
   return hipGetLastError();
 }
 
-// distinct 8-byte edge columns a program reads per edge (props, _dst, _rank)
+// distinct 8-byte edge property columns a program reads per edge (WHERE + YIELD)
 static int edge_columns_read(const TypeProgram& prog) {
   uint64_t seen = 0;
   int n = 0;
   for (auto& ins : prog.code) {
-    int key = -1;
-    if (ins.op == OP_COL || ins.op == OP_COLV) key = 2 + (ins.aux & 31);
-    else if (ins.op == OP_DST) key = 0;
-    else if (ins.op == OP_RANK) key = 1;
-    if (key >= 0 && !(seen & (1ull << key))) { seen |= 1ull << key; ++n; }
+    if (ins.op != OP_COL && ins.op != OP_COLV) continue;
+    const uint64_t bit = 1ull << (ins.aux & 63);
+    if (!(seen & bit)) { seen |= bit; ++n; }
   }
   return n;
 }
@@ -884,8 +1013,8 @@ hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound,
   fp.fast = detect_fast(prog, a);
   size_t lds = fp.fast.enabled ? 0 : (size_t)(prog.nregs > 0 ? prog.nregs : 1) * BLOCK * sizeof(int64_t);
   hipEvent_t p = prof_begin(w);
-  hipLaunchKernelGGL(k_expand<FINAL>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), lds, w->stream, a, w->q,
-                     w->seg_end, w->block_sum, w->seg_rs, w->flags, fp);
+  hipLaunchKernelGGL(k_expand<FINAL>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), lds, w->stream, a, &w->q->n,
+                     &w->q->total, w->seg_end, w->block_sum, w->seg_rs, w->flags, fp, BfsParams{});
   prof_end(w, p, K_EXPAND_FINAL, step, tix, (double)edge_columns_read(prog), (double)fp.nyields);
   return hipGetLastError();
 }
@@ -899,6 +1028,418 @@ hipError_t ws_end_query(Workspace* w) {
   HIP_TRY(hipMemcpyAsync(w->h_q, w->q, sizeof(QState), hipMemcpyDeviceToHost, w->stream));
   HIP_TRY(hipStreamSynchronize(w->stream));
   prof_flush(w, w->h_q);
+  return hipSuccess;
+}
+
+
+// ============================================================================= FIND SHORTEST PATH
+// Bidirectional BFS over epoch-stamped labels (path.cpp drives it level by level):
+//   k_expand<BFS>  claims neighbours (CAS on the label), detects meets, appends to claim shards
+//   k_gather       packs the NSHARD claim regions into the next frontier list
+//   k_degsum       degree sum of a frontier (which side to expand next)
+//   k_stamp        label a list (sources, targets, level-0 vertices)
+//   k_path_greedy  lexicographically smallest shortest path through the B-sets (one workgroup)
+
+__global__ void __launch_bounds__(BLOCK) k_stamp(const uint32_t* __restrict__ ids,
+                                                 const unsigned long long* __restrict__ np,
+                                                 uint32_t* __restrict__ lab, uint32_t stamp) {
+  const uint64_t n = *np;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
+    uint32_t v = ids[i];
+    if (v != NO_ROW) lab[v] = stamp;
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_gather(const uint32_t* __restrict__ scratch, uint64_t shard_cap,
+                                                  const unsigned long long* __restrict__ shard_cnt,
+                                                  uint32_t* __restrict__ out, unsigned long long* n_out,
+                                                  unsigned long long* c_rec) {
+  __shared__ unsigned long long pre[NSHARD + 1];
+  if (threadIdx.x == 0) {
+    unsigned long long run = 0;
+    for (int s = 0; s < NSHARD; ++s) {
+      pre[s] = run;
+      run += shard_cnt[s];
+    }
+    pre[NSHARD] = run;
+    if (blockIdx.x == 0) {
+      *n_out = run;
+      if (c_rec) *c_rec = run;
+    }
+  }
+  __syncthreads();
+  for (int s = 0; s < NSHARD; ++s) {
+    const uint64_t cnt = pre[s + 1] - pre[s];
+    const uint32_t* src = scratch + (uint64_t)s * shard_cap;
+    uint32_t* dst = out + pre[s];
+    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * BLOCK)
+      dst[i] = src[i];
+  }
+}
+
+struct DegsumArgs {
+  int ntypes;
+  const uint32_t* row_ptr[MAX_TYPES_Q];
+  const uint8_t* visible;
+  uint32_t cap;
+};
+
+__global__ void __launch_bounds__(BLOCK) k_degsum(const uint32_t* __restrict__ f,
+                                                  const unsigned long long* __restrict__ np, DegsumArgs d,
+                                                  unsigned long long* out, unsigned long long* n_rec) {
+  __shared__ unsigned long long lds[WAVES];
+  const uint64_t n = *np;
+  if (n_rec && blockIdx.x == 0 && threadIdx.x == 0) *n_rec = n;
+  unsigned long long sum = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
+    uint32_t v = f[i];
+    if (v == NO_ROW || (d.visible && !d.visible[v])) continue;
+    for (int t = 0; t < d.ntypes; ++t) {
+      uint32_t deg = d.row_ptr[t][v + 1] - d.row_ptr[t][v];
+      sum += deg < d.cap ? deg : d.cap;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_down(sum, o, 64);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) lds[w] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int i = 0; i < WAVES; ++i) t += lds[i];
+    if (t) atomicAdd(out, t);
+  }
+}
+
+struct GreedyArgs {
+  int ntypes;
+  int32_t type[MAX_TYPES_Q];
+  const uint32_t* row_ptr[MAX_TYPES_Q];
+  const uint32_t* col[MAX_TYPES_Q];
+  const int64_t* dst_vid[MAX_TYPES_Q];
+  const int64_t* rank[MAX_TYPES_Q];
+  const uint8_t* visible;
+  const int64_t* vids;
+  uint32_t cap;
+  int L, kf;
+  const uint32_t* lab_m;
+  uint32_t em;
+  const uint32_t* lab_b;
+  uint32_t eb;
+  const uint32_t* starts;
+  const unsigned long long* nstarts;
+  int64_t* out;                 // [v0, t0, r0, v1, ...]
+  unsigned long long* err;
+};
+
+struct Cand {                   // (type, rank, vid) key + dense id of the vertex
+  int64_t t, r, v;
+  uint32_t d;
+};
+__device__ __forceinline__ bool cand_less(const Cand& x, const Cand& y) {
+  if (x.t != y.t) return x.t < y.t;
+  if (x.r != y.r) return x.r < y.r;
+  return x.v < y.v;
+}
+__device__ __forceinline__ Cand shfl_cand(const Cand& c, int o) {
+  Cand r;
+  r.t = __shfl_down(c.t, o, 64);
+  r.r = __shfl_down(c.r, o, 64);
+  r.v = __shfl_down(c.v, o, 64);
+  r.d = __shfl_down(c.d, o, 64);
+  return r;
+}
+constexpr int GREEDY_BLOCK = 1024;
+
+// Block-wide minimum; every thread gets the result.  INT64_MAX type marks "no candidate".
+__device__ Cand block_min(Cand c, Cand* lds) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Cand x = shfl_cand(c, o);
+    if (cand_less(x, c)) c = x;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) lds[w] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Cand b = lds[0];
+    for (int i = 1; i < GREEDY_BLOCK / 64; ++i)
+      if (cand_less(lds[i], b)) b = lds[i];
+    lds[GREEDY_BLOCK / 64] = b;
+  }
+  __syncthreads();
+  Cand r = lds[GREEDY_BLOCK / 64];
+  __syncthreads();
+  return r;
+}
+
+// Position pos (1..L) of a shortest path is valid for w when w is in B[pos]: positions <= kf
+// carry a LAB_M stamp (the backward B-set passes over the forward levels), positions > kf the
+// backward BFS level L - pos.
+__device__ __forceinline__ bool greedy_valid(const GreedyArgs& g, uint32_t w, int pos) {
+  if (w == NO_ROW) return false;
+  if (pos <= g.kf) return g.lab_m[w] == ((g.em << LVL_BITS) | (uint32_t)pos);
+  return g.lab_b[w] == ((g.eb << LVL_BITS) | (uint32_t)(g.L - pos));
+}
+
+__global__ void __launch_bounds__(GREEDY_BLOCK) k_path_greedy(GreedyArgs g) {
+  __shared__ Cand lds[GREEDY_BLOCK / 64 + 1];
+  const Cand none{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
+  // v0 = smallest vid among the start candidates (dense ids are in vid order)
+  Cand c = none;
+  const uint64_t ns = *g.nstarts;
+  for (uint64_t i = threadIdx.x; i < ns; i += GREEDY_BLOCK) {
+    uint32_t d = g.starts[i];
+    if (d != NO_ROW && (int64_t)d < c.t) c = Cand{(int64_t)d, 0, 0, d};
+  }
+  c = block_min(c, lds);
+  uint32_t v = c.d;
+  if (v == NO_ROW) {
+    if (threadIdx.x == 0) *g.err = 1;
+    return;
+  }
+  if (threadIdx.x == 0) g.out[0] = g.vids[v];
+  for (int pos = 0; pos < g.L; ++pos) {
+    Cand best = none;
+    if (!g.visible || g.visible[v]) {
+      for (int t = 0; t < g.ntypes; ++t) {
+        const uint32_t rs = g.row_ptr[t][v];
+        uint32_t deg = g.row_ptr[t][v + 1] - rs;
+        deg = deg < g.cap ? deg : g.cap;
+        for (uint32_t k = threadIdx.x; k < deg; k += GREEDY_BLOCK) {
+          const uint64_t j = (uint64_t)rs + k;
+          const uint32_t w = g.col[t][j];
+          if (!greedy_valid(g, w, pos + 1)) continue;
+          Cand x{(int64_t)g.type[t], g.rank[t] ? g.rank[t][j] : 0, g.dst_vid[t][j], w};
+          if (cand_less(x, best)) best = x;
+        }
+      }
+    }
+    best = block_min(best, lds);
+    if (best.d == NO_ROW) {
+      if (threadIdx.x == 0) *g.err = 1;
+      return;
+    }
+    if (threadIdx.x == 0) {
+      g.out[1 + 3 * pos] = best.t;
+      g.out[2 + 3 * pos] = best.r;
+      g.out[3 + 3 * pos] = best.v;
+    }
+    v = best.d;
+  }
+}
+
+// ----------------------------------------------------------------------------- path host side
+constexpr uint64_t STAGE = 4096;
+static hipEvent_t prof_begin_p(Workspace* w) { return prof_begin(w); }
+static void prof_end_p(Workspace* w, hipEvent_t a, int kid, int rec) {
+  if (!a) return;
+  hipEvent_t b = w->prof.get();
+  (void)hipEventRecord(b, w->stream);
+  w->prof.pending.push_back({kid, rec, 0, a, b, 0, 0, true});
+}
+
+hipError_t ws_path_begin(Workspace* w, uint64_t scratch_entries, uint64_t list_entries) {
+  if (!w->ps) {
+    HIP_TRY(hipMalloc((void**)&w->ps, sizeof(PState)));
+    HIP_TRY(hipHostMalloc((void**)&w->h_ps, sizeof(PState), hipHostMallocDefault));
+    HIP_TRY(hipMalloc((void**)&w->d_path, (1 + 3 * MAX_PATH_LEN) * sizeof(int64_t)));
+    HIP_TRY(hipHostMalloc((void**)&w->h_path, (1 + 3 * MAX_PATH_LEN) * sizeof(int64_t), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&w->h_stage, (size_t)PSLOTS * STAGE * sizeof(uint32_t), hipHostMallocDefault));
+    for (int l = 0; l < NUM_LABS; ++l) {
+      HIP_TRY(hipMalloc((void**)&w->lab[l], (w->nv + 1) * sizeof(uint32_t)));
+      HIP_TRY(hipMemsetAsync(w->lab[l], 0, (w->nv + 1) * sizeof(uint32_t), w->stream));
+      w->epoch[l] = 0;
+    }
+  }
+  if (list_entries > w->slot_cap) {
+    HIP_TRY(hipStreamSynchronize(w->stream));
+    for (auto*& p : w->slot) {
+      if (p) HIP_TRY(hipFree(p));
+      p = nullptr;
+    }
+    w->slot_cap = list_entries;
+    for (auto*& p : w->slot) HIP_TRY(hipMalloc((void**)&p, w->slot_cap * sizeof(uint32_t)));
+  }
+  if (scratch_entries > w->pscratch_cap) {
+    HIP_TRY(hipStreamSynchronize(w->stream));
+    if (w->pscratch) HIP_TRY(hipFree(w->pscratch));
+    w->pscratch = nullptr;
+    w->pscratch_cap = scratch_entries;
+    HIP_TRY(hipMalloc((void**)&w->pscratch, w->pscratch_cap * sizeof(uint32_t)));
+  }
+  w->rec = 0;
+  return hipMemsetAsync(w->ps, 0, sizeof(PState), w->stream);
+}
+
+uint32_t ws_path_epoch(Workspace* w, int l) {
+  if (++w->epoch[l] >= (1u << (32 - LVL_BITS))) {   // wrap: clear the labels once
+    (void)hipMemsetAsync(w->lab[l], 0, (w->nv + 1) * sizeof(uint32_t), w->stream);
+    w->epoch[l] = 1;
+  }
+  return w->epoch[l];
+}
+
+uint32_t* ws_path_slot(Workspace* w, int s) { return w->slot[s]; }
+
+hipError_t ws_path_upload(Workspace* w, int s, const uint32_t* ids, uint64_t n) {
+  if (n > w->slot_cap) return hipErrorInvalidValue;
+  if (n <= STAGE) {   // common case: no synchronisation
+    uint32_t* st = w->h_stage + (size_t)s * STAGE;
+    memcpy(st, ids, n * 4);
+    w->h_ps->n[s] = n;
+    if (n) HIP_TRY(hipMemcpyAsync(w->slot[s], st, n * 4, hipMemcpyHostToDevice, w->stream));
+    return hipMemcpyAsync(&w->ps->n[s], &w->h_ps->n[s], sizeof(unsigned long long), hipMemcpyHostToDevice,
+                          w->stream);
+  }
+  if (n > w->cap_starts) {
+    HIP_TRY(hipStreamSynchronize(w->stream));
+    if (w->h_starts) HIP_TRY(hipHostFree(w->h_starts));
+    w->cap_starts = n + n / 2 + 1024;
+    HIP_TRY(hipHostMalloc((void**)&w->h_starts, w->cap_starts * 4, hipHostMallocDefault));
+  }
+  // the staging buffer may still feed an earlier copy of this query
+  HIP_TRY(hipStreamSynchronize(w->stream));
+  memcpy(w->h_starts, ids, n * 4);
+  w->h_ps->n[s] = n;
+  HIP_TRY(hipMemcpyAsync(w->slot[s], w->h_starts, n * 4, hipMemcpyHostToDevice, w->stream));
+  return hipMemcpyAsync(&w->ps->n[s], &w->h_ps->n[s], sizeof(unsigned long long), hipMemcpyHostToDevice,
+                        w->stream);
+}
+
+hipError_t ws_path_stamp(Workspace* w, int s, uint64_t n_bound, int l, uint32_t stamp) {
+  unsigned nb = (unsigned)cdiv(n_bound ? n_bound : 1, BLOCK);
+  if (nb > 1024) nb = 1024;
+  hipEvent_t p = prof_begin_p(w);
+  hipLaunchKernelGGL(k_stamp, dim3(nb), dim3(BLOCK), 0, w->stream, w->slot[s], &w->ps->n[s], w->lab[l], stamp);
+  prof_end_p(w, p, K_STAMP, 0);
+  return hipGetLastError();
+}
+
+hipError_t ws_path_degsum(Workspace* w, int s, uint64_t n_bound, const PathTypes& pt, int side) {
+  DegsumArgs d{};
+  d.ntypes = pt.n;
+  for (int t = 0; t < pt.n; ++t) d.row_ptr[t] = pt.a[t].row_ptr;
+  d.visible = pt.n ? pt.a[0].visible : nullptr;
+  d.cap = pt.n ? pt.a[0].cap : 0xFFFFFFFFu;
+  unsigned nb = (unsigned)cdiv(n_bound ? n_bound : 1, BLOCK);
+  if (nb > 2048) nb = 2048;
+  const int rec = w->rec < PATH_REC ? w->rec++ : PATH_REC - 1;
+  HIP_TRY(hipMemsetAsync(&w->ps->dsum[side], 0, sizeof(unsigned long long), w->stream));
+  hipEvent_t p = prof_begin_p(w);
+  hipLaunchKernelGGL(k_degsum, dim3(nb), dim3(BLOCK), 0, w->stream, w->slot[s], &w->ps->n[s], d,
+                     &w->ps->dsum[side], &w->ps->ln[rec]);
+  prof_end_p(w, p, K_DEGSUM, rec);
+  return hipGetLastError();
+}
+
+hipError_t ws_path_level(Workspace* w, const PathTypes& pt, int src, uint64_t n_bound, uint64_t e_bound, int dst,
+                         const PathLevel& lv) {
+  // claim shards: a shard's count is bounded by its tiles over all types of this level
+  uint64_t shard_cap = 0;
+  for (int t = 0; t < pt.n; ++t) shard_cap += ws_shard_cap(n_bound, e_bound);
+  if (shard_cap * NSHARD > w->pscratch_cap) {
+    HIP_TRY(hipStreamSynchronize(w->stream));
+    if (w->pscratch) HIP_TRY(hipFree(w->pscratch));
+    w->pscratch = nullptr;
+    w->pscratch_cap = shard_cap * NSHARD;
+    HIP_TRY(hipMalloc((void**)&w->pscratch, w->pscratch_cap * sizeof(uint32_t)));
+  }
+  BfsParams bp{};
+  bp.lab = w->lab[lv.lab];
+  bp.stamp = lv.stamp;
+  bp.epoch = lv.stamp >> LVL_BITS;
+  if (lv.rlab >= 0) { bp.rlab = w->lab[lv.rlab]; bp.rstamp = lv.rstamp; }
+  if (lv.mlab >= 0) {
+    bp.mlab = w->lab[lv.mlab];
+    bp.mepoch = lv.mepoch;
+    bp.mout = w->lab[LAB_M];
+    bp.mstamp = lv.mstamp;
+    bp.meet_list = w->slot[lv.meet_slot];
+    bp.meet_n = &w->ps->n[lv.meet_slot];
+  }
+  if (lv.tlab >= 0) { bp.tlab = w->lab[lv.tlab]; bp.tstamp = lv.tstamp; bp.found = &w->ps->found; }
+  bp.out = w->pscratch;
+  bp.shard_cap = shard_cap;
+  bp.shard_cnt = w->ps->shard;
+  const int rec = w->rec < PATH_REC ? w->rec++ : PATH_REC - 1;
+  for (int t = 0; t < pt.n; ++t) {
+    ExpandArgs a = pt.a[t];
+    a.frontier = w->slot[src];
+    uint64_t nb = cdiv(n_bound ? n_bound : 1, SCAN_TILE);
+    hipEvent_t p = prof_begin_p(w);
+    hipLaunchKernelGGL(k_degree, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->slot[src], &w->ps->n[src],
+                       a.row_ptr, a.visible, a.cap, w->seg_end, w->seg_rs, w->block_sum,
+                       t == 0 ? w->ps->shard : (unsigned long long*)nullptr, &w->ps->ln[rec]);
+    prof_end_p(w, p, K_DEGREE, rec);
+    p = prof_begin_p(w);
+    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, w->stream, w->block_sum, &w->ps->n[src], (uint64_t)0,
+                       &w->ps->total, &w->ps->le[rec]);
+    prof_end_p(w, p, K_SCAN, rec);
+    p = prof_begin_p(w);
+    hipLaunchKernelGGL(k_expand<BFS>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a,
+                       &w->ps->n[src], &w->ps->total, w->seg_end, w->block_sum, w->seg_rs, (uint8_t*)nullptr,
+                       FinalParams{}, bp);
+    prof_end_p(w, p, K_BFS, rec);
+  }
+  uint64_t gb = cdiv(n_bound + e_bound + 1, (uint64_t)BLOCK * 4);
+  unsigned grid = (unsigned)(gb < 1 ? 1 : (gb > 1024 ? 1024 : gb));
+  hipEvent_t p = prof_begin_p(w);
+  hipLaunchKernelGGL(k_gather, dim3(grid), dim3(BLOCK), 0, w->stream, w->pscratch, shard_cap, w->ps->shard,
+                     w->slot[dst], &w->ps->n[dst], &w->ps->lc[rec]);
+  prof_end_p(w, p, K_GATHER, rec);
+  return hipGetLastError();
+}
+
+int ws_path_last_rec(Workspace* w) { return w->rec - 1; }
+
+hipError_t ws_path_read_label(Workspace* w, int l, uint32_t v, uint32_t* out) {
+  HIP_TRY(hipMemcpyAsync(w->h_stage, w->lab[l] + v, sizeof(uint32_t), hipMemcpyDeviceToHost, w->stream));
+  HIP_TRY(hipStreamSynchronize(w->stream));
+  *out = w->h_stage[0];
+  return hipSuccess;
+}
+
+hipError_t ws_path_greedy(Workspace* w, const PathTypes& pt, const PathGreedy& pg) {
+  if (pg.L < 1 || pg.L > (int)MAX_PATH_LEN) return hipErrorInvalidValue;
+  GreedyArgs g{};
+  g.ntypes = pt.n;
+  for (int t = 0; t < pt.n; ++t) {
+    g.type[t] = pt.type[t];
+    g.row_ptr[t] = pt.a[t].row_ptr;
+    g.col[t] = pt.a[t].col;
+    g.dst_vid[t] = pt.a[t].dst_vid;
+    g.rank[t] = pt.a[t].rank;
+  }
+  g.visible = pt.n ? pt.a[0].visible : nullptr;
+  g.vids = pt.n ? pt.a[0].vids : nullptr;
+  g.cap = pt.n ? pt.a[0].cap : 0xFFFFFFFFu;
+  g.L = pg.L;
+  g.kf = pg.kf;
+  g.lab_m = w->lab[LAB_M];
+  g.em = pg.em;
+  g.lab_b = w->lab[LAB_B];
+  g.eb = pg.eb;
+  g.starts = w->slot[pg.start_slot];
+  g.nstarts = &w->ps->n[pg.start_slot];
+  g.out = w->d_path;
+  g.err = &w->ps->err;
+  hipEvent_t p = prof_begin_p(w);
+  hipLaunchKernelGGL(k_path_greedy, dim3(1), dim3(GREEDY_BLOCK), 0, w->stream, g);
+  prof_end_p(w, p, K_GREEDY, 0);
+  return hipGetLastError();
+}
+
+hipError_t ws_path_sync(Workspace* w, PState* out, int64_t* path, int path_len) {
+  HIP_TRY(hipMemcpyAsync(w->h_ps, w->ps, sizeof(PState), hipMemcpyDeviceToHost, w->stream));
+  if (path && path_len > 0)
+    HIP_TRY(hipMemcpyAsync(w->h_path, w->d_path, (size_t)path_len * sizeof(int64_t), hipMemcpyDeviceToHost,
+                           w->stream));
+  HIP_TRY(hipStreamSynchronize(w->stream));
+  if (out) *out = *w->h_ps;
+  if (path && path_len > 0) memcpy(path, w->h_path, (size_t)path_len * sizeof(int64_t));
+  // resolve timing of the launches since the last sync (record indices stay valid per query)
+  prof_flush(w, nullptr, w->h_ps);
   return hipSuccess;
 }
 

@@ -177,6 +177,35 @@ struct ExpandArgs {                // one (step, edge type) expansion
   uint32_t cap;                    // max_edge_returned_per_vertex
 };
 
+// ----------------------------------------------------------------------------- FIND PATH state
+// Vertex labels are epoch-stamped so no per-query clearing is needed: label = epoch << LVL_BITS |
+// level, live when its epoch is the current one.
+constexpr int LVL_BITS = 6;
+constexpr uint32_t MAX_PATH_LEN = (1u << LVL_BITS) - 1;   // UPTO bound
+constexpr int PSLOTS = 8;           // 0,1 forward / 2,3 backward frontiers, 4 meets, 5 starts, 6,7 B-sets
+enum PathLabel { LAB_F = 0, LAB_B = 1, LAB_S = 2, LAB_M = 3, NUM_LABS = 4 };
+constexpr int PATH_REC = 64;        // per-query expansion records (profiling byte counts)
+
+struct PState {                      // device-resident sizes of one FIND PATH query
+  unsigned long long n[PSLOTS];      // size of each frontier slot
+  unsigned long long total;          // edges of the current expansion
+  unsigned long long edges;          // BFS edges scanned (both sides)
+  unsigned long long meets;          // meet-list length
+  unsigned long long found;          // targets reached (one-sided search)
+  unsigned long long err;            // reconstruction failure
+  unsigned long long dsum[2];        // degree sum of the current forward / backward frontier
+  unsigned long long shard[NSHARD];  // claim counters
+  unsigned long long ln[PATH_REC];   // per expansion record: frontier size, edges, claims
+  unsigned long long le[PATH_REC];
+  unsigned long long lc[PATH_REC];
+};
+
+struct PathTypes {                   // the CSRs one search direction expands (one per OVER type)
+  int n = 0;
+  int32_t type[MAX_TYPES_Q];
+  ExpandArgs a[MAX_TYPES_Q];
+};
+
 struct Workspace;   // kernels.hip
 
 Workspace* ws_create(uint64_t max_frontier, uint64_t nv, hipStream_t s, std::string* err);
@@ -201,5 +230,41 @@ hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a, uint64_t n_bound, 
                            const TypeProgram& prog, uint64_t region_base, uint64_t shard_cap);
 hipError_t ws_scan_only(Workspace* w, const ExpandArgs& a, uint64_t n_bound, int step, int tix);
 hipError_t ws_end_query(Workspace* w);
+
+// FIND SHORTEST PATH (kernels.hip).  Frontier lists live in numbered device slots; PState sizes
+// are read back by ws_path_sync.  All calls enqueue on the workspace stream.
+hipError_t ws_path_begin(Workspace* w, uint64_t scratch_entries, uint64_t list_entries);
+uint32_t ws_path_epoch(Workspace* w, int lab);                    // fresh epoch for one label array
+uint32_t* ws_path_slot(Workspace* w, int slot);
+hipError_t ws_path_upload(Workspace* w, int slot, const uint32_t* ids, uint64_t n);
+// lab[ids of slot] = stamp
+hipError_t ws_path_stamp(Workspace* w, int slot, uint64_t n_bound, int lab, uint32_t stamp);
+// degree sum of a slot's frontier over the given CSRs into PState.dsum[side]
+hipError_t ws_path_degsum(Workspace* w, int slot, uint64_t n_bound, const PathTypes& pt, int side);
+// one BFS level: expand slot `src` over pt, claim into lab `bp` fields, pack claims into `dst`
+struct PathLevel {
+  int lab;                 // label claimed
+  uint32_t stamp;
+  int rlab = -1;           // restriction label (-1 none)
+  uint32_t rstamp = 0;
+  int mlab = -1;           // meet-test label (-1 none)
+  uint32_t mepoch = 0;
+  uint32_t mstamp = 0;     // written into LAB_M for met vertices
+  int meet_slot = -1;
+  int tlab = -1;           // target label (-1 none)
+  uint32_t tstamp = 0;
+};
+hipError_t ws_path_level(Workspace* w, const PathTypes& pt, int src, uint64_t n_bound, uint64_t e_bound, int dst,
+                         const PathLevel& lv);
+// greedy lexicographically smallest reconstruction of one path of length L (see path.cpp)
+struct PathGreedy {
+  int L, kf;
+  uint32_t em, eb;         // epochs of LAB_M (positions <= kf) and LAB_B (positions > kf)
+  int start_slot;          // B[0] candidates (minimum dense id starts the path)
+};
+hipError_t ws_path_greedy(Workspace* w, const PathTypes& out_types, const PathGreedy& g);
+int ws_path_last_rec(Workspace* w);                              // PState record of the last launch
+hipError_t ws_path_read_label(Workspace* w, int lab, uint32_t v, uint32_t* out);   // synchronous
+hipError_t ws_path_sync(Workspace* w, PState* out, int64_t* path, int path_len);
 
 }  // namespace nbg

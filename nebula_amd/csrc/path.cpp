@@ -1,10 +1,312 @@
-// FIND SHORTEST | ALL PATH driver (FindPathExecutor semantics).
+// FIND SHORTEST PATH driver (FindPathExecutor result semantics) over the device snapshot.
+//
+// Reference: src/graph/FindPathExecutor.cpp — rounds of from-side expansion over the OVER types
+// and to-side expansion over their in-edges (-type) (:145-216), odd/even meets (:218-290), one
+// path per target across all sources, minimum hop count (:292-382), UPTO N steps (parser.yy
+// :858-861, default 5), from/to de-duplicated (VerticesClause).  The reference breaks ties
+// between equal-length paths by hash-map iteration order; this engine (and the oracle,
+// oracle/graph.cpp runShortestBfs) returns the lexicographically smallest entry list
+// [v0, t0, r0, v1, ...] instead — a deterministic member of the reference's answer set.
+//
+// Two device strategies, identical results:
+//   * one source, one target (s != t): bidirectional BFS.  Each level expands the side whose
+//     frontier has the smaller degree sum; labels are epoch-stamped (no clearing).  The first
+//     level that claims a vertex labelled by the other side fixes L = kf + kb, and every vertex
+//     met in that level sits at forward position kf (no shorter meet existed).  B-sets over
+//     the forward levels are then recovered backwards from the meet set through in-edges,
+//     restricted to forward level i; positions past kf are the backward BFS levels.
+//   * otherwise: one-sided BFS from all sources (walk length >= 1, as the reference's rounds
+//     never revisit a source at depth 0), stopping once every target is labelled; per target
+//     the B-sets are recovered from the target through in-edges restricted to forward levels.
+// The path is then built greedily (k_path_greedy): v0 = min B[0], each hop the minimum
+// (type, rank, dst) edge into the next B-set.  Lexicographic minimality follows because every
+// B-set member extends to a shortest path.
+//
+// In-edge records mirror out-edges (InsertEdgeExecutor.cpp:180-196 writes both), so the to-side
+// sees exactly the reverse of the from-side; with a non-default max_edge_returned_per_vertex the
+// two caps differ and the device path reports NBG_E_UNSUPPORTED.
+#include <algorithm>
+#include <climits>
+#include <unordered_set>
+
 #include "engine.h"
 
-extern "C" int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* req, nbg_paths** out) {
-  if (!h || !req || !out) return NBG_E_INVALID_ARGUMENT;
+using namespace nbg;
+
+namespace {
+
+constexpr int S_F0 = 0, S_B0 = 2, S_MEET = 4, S_START = 5, S_SET0 = 6;
+
+inline uint32_t stamp(uint32_t epoch, uint32_t level) { return (epoch << LVL_BITS) | level; }
+
+struct PathCtx {
+  Engine& E;
+  Workspace* ws;
+  PathTypes fwd, bwd;
+  uint64_t bwd_edges = 0;   // in-edges over the OVER types (B-set pass bound)
+  uint64_t edges = 0;       // BFS edges scanned (both sides)
+};
+
+int32_t dev_fail(Engine& E, hipError_t e, const char* what) {
+  return E.fail(NBG_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// Recover B[i] for i = top-1 .. lo from B[top] (slot `cur`, <= n_top entries) through in-edges:
+// B[i] = { u : u -> B[i+1], forward label of u == i } (i >= 1) or u in S (i == 0).
+hipError_t bsets(PathCtx& c, int cur, uint64_t n_top, int top, int lo, uint32_t ef, uint32_t em, uint32_t es,
+                 const std::vector<uint64_t>& level_n, int* out_slot) {
+  hipError_t he = hipSuccess;
+  uint64_t nb = n_top;
+  for (int i = top - 1; i >= lo && he == hipSuccess; --i) {
+    PathLevel lv;
+    lv.lab = LAB_M;
+    lv.stamp = stamp(em, (uint32_t)i);
+    if (i >= 1) {
+      lv.rlab = LAB_F;
+      lv.rstamp = stamp(ef, (uint32_t)i);
+    } else {
+      // B[0] (sources) is only the greedy's start list; claim it in a fresh LAB_B epoch, as a
+      // source may also be the target itself, already in B[L] under this LAB_M epoch
+      lv.lab = LAB_B;
+      lv.stamp = stamp(ws_path_epoch(c.ws, LAB_B), 0);
+      lv.rlab = LAB_S;
+      lv.rstamp = stamp(es, 0);
+    }
+    const int dst = cur == S_SET0 ? S_SET0 + 1 : S_SET0;
+    he = ws_path_level(c.ws, c.bwd, cur, nb, c.bwd_edges, dst, lv);
+    cur = dst;
+    nb = (size_t)i < level_n.size() ? level_n[i] : c.E.snap.nv;
+  }
+  *out_slot = cur;
+  return he;
+}
+
+int32_t read_path(PathCtx& c, int L, std::vector<int64_t>* path) {
+  std::vector<int64_t> p(1 + 3 * (size_t)L);
+  PState ps;
+  hipError_t he = ws_path_sync(c.ws, &ps, p.data(), (int)p.size());
+  if (he != hipSuccess) return dev_fail(c.E, he, "path readback");
+  if (ps.err) return c.E.fail(NBG_E_UNKNOWN, "shortest-path reconstruction failed (in/out edges disagree)");
+  *path = std::move(p);
+  return NBG_OK;
+}
+
+int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_paths* out) {
+  Workspace* ws = c.ws;
+  const uint32_t ef = ws_path_epoch(ws, LAB_F), eb = ws_path_epoch(ws, LAB_B), em = ws_path_epoch(ws, LAB_M);
+  hipError_t he = hipSuccess;
+  auto T = [&](hipError_t e) { if (he == hipSuccess) he = e; };
+  T(ws_path_upload(ws, S_F0, &s, 1));
+  T(ws_path_upload(ws, S_B0, &t, 1));
+  T(ws_path_upload(ws, S_START, &s, 1));
+  T(ws_path_stamp(ws, S_F0, 1, LAB_F, stamp(ef, 0)));
+  T(ws_path_stamp(ws, S_B0, 1, LAB_B, stamp(eb, 0)));
+  T(ws_path_degsum(ws, S_F0, 1, c.fwd, 0));
+  T(ws_path_degsum(ws, S_B0, 1, c.bwd, 1));
+  PState ps;
+  T(ws_path_sync(ws, &ps, nullptr, 0));
+  if (he != hipSuccess) return dev_fail(c.E, he, "path setup");
+  int fcur = S_F0, bcur = S_B0, kf = 0, kb = 0;
+  uint64_t nf = 1, nbk = 1, dsf = ps.dsum[0], dsb = ps.dsum[1];
+  std::vector<uint64_t> fn(1, 1);   // forward level sizes
+  bool met = false;
+  while ((uint32_t)(kf + kb) < upto) {
+    const bool forward = dsf <= dsb;
+    PathLevel lv;
+    lv.mlab = forward ? LAB_B : LAB_F;
+    lv.mepoch = forward ? eb : ef;
+    lv.meet_slot = S_MEET;
+    if (forward) {
+      lv.lab = LAB_F;
+      lv.stamp = stamp(ef, (uint32_t)kf + 1);
+      lv.mstamp = stamp(em, (uint32_t)kf + 1);
+      T(ws_path_level(ws, c.fwd, fcur, nf, dsf, fcur ^ 1, lv));
+      fcur ^= 1;
+      ++kf;
+      T(ws_path_degsum(ws, fcur, dsf ? dsf : 1, c.fwd, 0));
+    } else {
+      lv.lab = LAB_B;
+      lv.stamp = stamp(eb, (uint32_t)kb + 1);
+      lv.mstamp = stamp(em, (uint32_t)kf);
+      T(ws_path_level(ws, c.bwd, bcur, nbk, dsb, bcur ^ 1, lv));
+      bcur ^= 1;
+      ++kb;
+      T(ws_path_degsum(ws, bcur, dsb ? dsb : 1, c.bwd, 1));
+    }
+    const int rec = ws_path_last_rec(ws) - 1;   // the level's record (degsum took the next one)
+    T(ws_path_sync(ws, &ps, nullptr, 0));
+    if (he != hipSuccess) return dev_fail(c.E, he, "path level");
+    if (rec >= 0 && rec < PATH_REC) c.edges += ps.le[rec];
+    nf = ps.n[fcur];
+    nbk = ps.n[bcur];
+    dsf = ps.dsum[0];
+    dsb = ps.dsum[1];
+    if (forward) fn.push_back(nf);
+    if (ps.n[S_MEET]) { met = true; break; }
+    if (nf == 0 || nbk == 0) break;
+  }
+  if (!met) return NBG_OK;
+  const int L = kf + kb;
+  int start_slot = S_START;
+  if (kf >= 1) {
+    // B[kf] = the meet list; B[kf-1] .. B[1] through in-edges; B[0] = {s}
+    int slot = S_MEET;
+    T(bsets(c, S_MEET, ps.n[S_MEET], kf, 1, ef, em, 0, fn, &slot));
+  }
+  PathGreedy g{L, kf, em, eb, start_slot};
+  T(ws_path_greedy(ws, c.fwd, g));
+  if (he != hipSuccess) return dev_fail(c.E, he, "path reconstruction");
+  std::vector<int64_t> p;
+  int32_t rc = read_path(c, L, &p);
+  if (rc) return rc;
+  out->paths.push_back(std::move(p));
+  return NBG_OK;
+}
+
+int32_t one_sided(PathCtx& c, const std::vector<uint32_t>& S, const std::vector<uint32_t>& Tg, uint32_t upto,
+                  nbg_paths* out) {
+  Workspace* ws = c.ws;
+  const uint32_t ef = ws_path_epoch(ws, LAB_F), es = ws_path_epoch(ws, LAB_S), et = ws_path_epoch(ws, LAB_B);
+  hipError_t he = hipSuccess;
+  auto T = [&](hipError_t e) { if (he == hipSuccess) he = e; };
+  T(ws_path_upload(ws, S_START, S.data(), S.size()));
+  T(ws_path_stamp(ws, S_START, S.size(), LAB_S, stamp(es, 0)));
+  T(ws_path_upload(ws, S_MEET, Tg.data(), Tg.size()));
+  T(ws_path_stamp(ws, S_MEET, Tg.size(), LAB_B, stamp(et, 0)));
+  T(ws_path_upload(ws, S_F0, S.data(), S.size()));
+  T(ws_path_degsum(ws, S_F0, S.size(), c.fwd, 0));
+  PState ps;
+  T(ws_path_sync(ws, &ps, nullptr, 0));
+  if (he != hipSuccess) return dev_fail(c.E, he, "path setup");
+  std::vector<uint64_t> level_n(1, S.size());
+  int cur = S_F0;
+  uint64_t n = S.size(), ds = ps.dsum[0];
+  for (uint32_t l = 1; l <= upto; ++l) {
+    PathLevel lv;
+    lv.lab = LAB_F;
+    lv.stamp = stamp(ef, l);
+    lv.tlab = LAB_B;
+    lv.tstamp = stamp(et, 0);
+    T(ws_path_level(ws, c.fwd, cur, n, ds, cur ^ 1, lv));
+    const int rec = ws_path_last_rec(ws);
+    cur ^= 1;
+    T(ws_path_degsum(ws, cur, ds ? ds : 1, c.fwd, 0));
+    T(ws_path_sync(ws, &ps, nullptr, 0));
+    if (he != hipSuccess) return dev_fail(c.E, he, "path level");
+    if (rec >= 0 && rec < PATH_REC) c.edges += ps.le[rec];
+    n = ps.n[cur];
+    ds = ps.dsum[0];
+    level_n.push_back(n);
+    if (n == 0 || ps.found >= Tg.size()) break;
+  }
+  // per target: its forward level is its distance
+  std::vector<uint32_t> labels(Tg.size());
+  for (size_t i = 0; i < Tg.size(); ++i) {
+    he = ws_path_read_label(ws, LAB_F, Tg[i], &labels[i]);
+    if (he != hipSuccess) return dev_fail(c.E, he, "label readback");
+  }
+  for (size_t i = 0; i < Tg.size(); ++i) {
+    if ((labels[i] >> LVL_BITS) != ef) continue;
+    const int L = (int)(labels[i] & MAX_PATH_LEN);
+    const uint32_t em = ws_path_epoch(ws, LAB_M);
+    T(ws_path_upload(ws, S_SET0, &Tg[i], 1));
+    T(ws_path_stamp(ws, S_SET0, 1, LAB_M, stamp(em, (uint32_t)L)));
+    int slot = S_SET0;
+    T(bsets(c, S_SET0, 1, L, 0, ef, em, es, level_n, &slot));
+    PathGreedy g{L, L, em, 0, slot};
+    T(ws_path_greedy(ws, c.fwd, g));
+    if (he != hipSuccess) return dev_fail(c.E, he, "path reconstruction");
+    std::vector<int64_t> p;
+    int32_t rc = read_path(c, L, &p);
+    if (rc) return rc;
+    out->paths.push_back(std::move(p));
+  }
+  return NBG_OK;
+}
+
+}  // namespace
+
+extern "C" int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* rq, nbg_paths** out) {
+  if (!h || !rq || !out) return NBG_E_INVALID_ARGUMENT;
   *out = nullptr;
-  return h->e.fail(NBG_E_UNSUPPORTED, "FIND PATH device path not built yet");
+  Engine& E = h->e;
+  std::lock_guard<std::mutex> lg(E.mu);
+  if (!E.finalized) return E.fail(NBG_E_STATE, "engine not finalized");
+  if (!rq->shortest) return E.fail(NBG_E_UNSUPPORTED, "FIND ALL PATH is not supported on the device path yet");
+  if (rq->upto > MAX_PATH_LEN) return E.fail(NBG_E_UNSUPPORTED, "UPTO exceeds the device path limit (63)");
+  if (E.cfg.max_edge_returned_per_vertex > 0 && E.cfg.max_edge_returned_per_vertex != INT_MAX)
+    return E.fail(NBG_E_UNSUPPORTED, "FIND PATH with max_edge_returned_per_vertex is not supported on the device");
+  // OVER (FindPathExecutor::prepareOver)
+  std::vector<int32_t> over;
+  if (rq->over_all) {
+    for (auto& kv : E.edges) over.push_back(kv.first);
+  } else {
+    for (int32_t i = 0; i < rq->num_edge_types; ++i) {
+      int32_t t = rq->edge_types[i];
+      if (t <= 0 || !E.edges.count(t)) return E.fail(NBG_E_EXECUTION_ERROR, "edge type not found");
+      if (std::find(over.begin(), over.end(), t) == over.end()) over.push_back(t);
+    }
+  }
+  if (over.empty()) return E.fail(NBG_E_EXECUTION_ERROR, "empty OVER clause");
+  if ((int)over.size() > MAX_TYPES_Q) return E.fail(NBG_E_UNSUPPORTED, "too many OVER types");
+  auto* res = new nbg_paths();
+  // from / to: de-duplicated; vertices without rows have no edges on either side
+  std::vector<uint32_t> S, Tg;
+  {
+    std::unordered_set<int64_t> seen;
+    for (uint64_t i = 0; i < rq->num_from; ++i)
+      if (seen.insert(rq->from[i]).second) {
+        uint32_t d = E.dense(rq->from[i]);
+        if (d != NO_ROW) S.push_back(d);
+      }
+    seen.clear();
+    for (uint64_t i = 0; i < rq->num_to; ++i)
+      if (seen.insert(rq->to[i]).second) {
+        uint32_t d = E.dense(rq->to[i]);
+        if (d != NO_ROW) Tg.push_back(d);
+      }
+  }
+  if (S.empty() || Tg.empty() || rq->upto == 0) { *out = res; return NBG_OK; }
+  PathCtx c{E, E.ws, {}, {}, 0, 0};
+  const uint32_t cap = 0x7fffffff;
+  auto add = [&](PathTypes& pt, int32_t signed_type) {
+    auto it = E.snap.types.find(signed_type);
+    if (it == E.snap.types.end()) return;
+    const DevEdgeType& dt = it->second;
+    ExpandArgs a{};
+    a.row_ptr = dt.row_ptr;
+    a.col = dt.col;
+    a.dst_vid = dt.dst_vid;
+    a.rank = dt.rank;
+    a.valid = dt.valid;
+    a.visible = E.snap.d_visible;
+    a.vids = E.snap.d_vids;
+    a.props = dt.d_props;
+    a.cap = cap;
+    pt.type[pt.n] = signed_type;
+    pt.a[pt.n++] = a;
+    if (signed_type < 0) c.bwd_edges += dt.num_edges;
+  };
+  for (int32_t t : over) {
+    const bool out_edges = E.snap.types.count(t) > 0, in_edges = E.snap.types.count(-t) > 0;
+    if (out_edges && !in_edges) {
+      delete res;
+      return E.fail(NBG_E_UNSUPPORTED, "FIND PATH needs the in-edge records of every OVER type");
+    }
+    add(c.fwd, t);
+    add(c.bwd, -t);
+  }
+  hipError_t he = ws_path_begin(c.ws, 0, E.snap.nv + S.size() + Tg.size() + 1024);
+  if (he != hipSuccess) { delete res; return dev_fail(E, he, "path workspace"); }
+  int32_t rc;
+  if (c.fwd.n == 0) rc = NBG_OK;
+  else if (S.size() == 1 && Tg.size() == 1 && S[0] != Tg[0]) rc = bidirectional(c, S[0], Tg[0], rq->upto, res);
+  else rc = one_sided(c, S, Tg, rq->upto, res);
+  if (rc) { delete res; return rc; }
+  std::sort(res->paths.begin(), res->paths.end());
+  res->edges = c.edges;
+  *out = res;
+  return NBG_OK;
 }
 
 extern "C" int32_t nbg_comm_unique_id(uint8_t out[NBG_UNIQUE_ID_BYTES]) {

@@ -210,7 +210,9 @@ class Engine:
         return DeviceRows(self, out)
 
     # ------------------------------------------------------------------ FIND PATH
-    def find_path(self, frm, to, etypes, upto=5, shortest=True, over_all=False):
+    def find_path(self, frm, to, etypes, upto=5, shortest=True, over_all=False, stats=None):
+        """FIND SHORTEST PATH: sorted entry lists [v0, t0, r0, v1, ...].  ``stats`` (a dict)
+        receives ``edges`` — adjacency entries scanned by both search directions."""
         f = np.ascontiguousarray(frm, np.int64)
         t = np.ascontiguousarray(to, np.int64)
         e = np.ascontiguousarray(etypes, np.int32)
@@ -226,6 +228,8 @@ class Engine:
                 n = self.lib.nbg_path_len(out, i)
                 ptr = self.lib.nbg_path_entries(out, i)
                 paths.append([int(ptr[k]) for k in range(n)])
+            if stats is not None:
+                stats["edges"] = int(self.lib.nbg_paths_edges_scanned(out))
             return sorted(paths)
         finally:
             self.lib.nbg_paths_free(out)

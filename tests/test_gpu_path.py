@@ -1,0 +1,98 @@
+"""FIND SHORTEST PATH parity on the MI355X: nebula_amd (bidirectional / one-sided BFS kernels,
+B-set recovery, greedy canonical reconstruction) vs the CPU oracle (oracle/graph.cpp
+runShortestBfs, itself pinned by FindPathTest.cpp's golden paths).  Bit-exact entry lists."""
+import numpy as np
+import pytest
+
+from nebula_amd import NbgError, nba_engine
+from nebula_amd import _lib
+from tests.support import golden, graphs
+
+pytestmark = pytest.mark.gpu
+
+FIND = golden.load("findpath_golden.json")
+
+
+@pytest.fixture(scope="module")
+def nba(nba_data):
+    eng = nba_engine(nba_data)
+    yield eng
+    eng.close()
+
+
+@pytest.mark.parametrize("case", FIND, ids=[f"{c['test']}-{i}" for i, c in enumerate(FIND)])
+def test_findpath_golden_on_gpu(nba, case):
+    why = golden.unsupported_reason(case)
+    if why:
+        pytest.skip(why)
+    try:
+        ok, msg = golden.run_path_case(nba, case)
+    except NbgError as ex:
+        if ex.code == _lib.E_UNSUPPORTED:
+            pytest.skip(f"not on the device path yet: {ex}")
+        raise
+    assert ok, msg
+
+
+@pytest.fixture(scope="module")
+def rmat12():
+    src, dst, w = graphs.rmat_graph(12)
+    eng = graphs.rmat_engine(src, dst, w)
+    orc = graphs.rmat_oracle(src, dst, w)
+    yield src, dst, eng, orc
+    eng.close()
+    orc.close()
+
+
+def pairs(src, dst, k, seed=7):
+    """Pairs drawn uniformly from vertices with degree >= 1 (SURVEY §8(d) C4 scheme)."""
+    verts = np.unique(np.concatenate([src, dst]))
+    rng = np.random.default_rng(seed)
+    a = rng.choice(verts, k)
+    b = rng.choice(verts, k)
+    return [(int(x), int(y)) for x, y in zip(a, b)]
+
+
+@pytest.mark.parametrize("upto", [1, 2, 3, 5])
+def test_rmat_shortest_single_pairs(rmat12, upto):
+    """One source, one target: the bidirectional search."""
+    src, dst, eng, orc = rmat12
+    found = 0
+    for s, t in pairs(src, dst, 48, seed=upto):
+        st = {}
+        got = eng.find_path([s], [t], [1], upto, stats=st)
+        exp = orc.find_path([s], [t], [1], upto, True, mode=1)
+        assert got == sorted(exp), (s, t, upto)
+        found += len(got)
+        assert st["edges"] >= 0
+    if upto >= 3:
+        assert found > 0
+
+
+def test_rmat_shortest_self_and_unknown(rmat12):
+    """s == t needs a cycle (walk length >= 1); unknown vids have no rows."""
+    src, dst, eng, orc = rmat12
+    for s, _ in pairs(src, dst, 8, seed=11):
+        assert eng.find_path([s], [s], [1], 5) == sorted(orc.find_path([s], [s], [1], 5, True, mode=1))
+    s = int(src[0])
+    assert eng.find_path([s], [123456789], [1], 5) == []
+    assert eng.find_path([123456789], [s], [1], 5) == []
+
+
+def test_rmat_shortest_multi_source_target(rmat12):
+    """Several sources and targets: one path per target, minimum over sources (one-sided search)."""
+    src, dst, eng, orc = rmat12
+    ps = pairs(src, dst, 24, seed=3)
+    for k in range(0, 24, 6):
+        frm = [p[0] for p in ps[k:k + 3]]
+        to = [p[1] for p in ps[k:k + 6]] + [frm[0]]
+        got = eng.find_path(frm + frm[:1], to, [1], 4)
+        exp = orc.find_path(frm, to, [1], 4, True, mode=1)
+        assert got == sorted(exp), (frm, to)
+
+
+def test_find_all_path_reports_unsupported(rmat12):
+    src, dst, eng, orc = rmat12
+    with pytest.raises(NbgError) as ex:
+        eng.find_path([int(src[0])], [int(dst[0])], [1], 3, shortest=False)
+    assert ex.value.code == _lib.E_UNSUPPORTED
