@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--sp-pairs", type=int, default=10000, help="FIND SHORTEST PATH pairs (0 = skip)")
+    ap.add_argument("--sp-upto", type=int, default=5)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -111,6 +113,12 @@ def main():
     if not args.no_profile:
         eng.profile(False)
 
+    sp = None
+    pairs = []
+    if args.sp_pairs > 0:
+        pairs = rmat.pick_pairs(src, dst, args.sp_pairs, 7)
+        sp = shortest_path_leg(eng, pairs, args, barrier)
+
     tot_scanned, max_elapsed = float(scanned), elapsed
     if dist is not None:
         t = torch.tensor([float(scanned), elapsed], dtype=torch.float64)
@@ -148,11 +156,13 @@ def main():
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(src, dst, w, roots, where, args)
+        cpu, sp_cpu = cpu_baseline(src, dst, w, roots, where, pairs, args)
+        if sp is not None:
+            sp["cpu_baseline"] = sp_cpu
 
     lat_ms = np.array(lats) * 1e3
     out = {
-        "metric": "GO 3 STEPS traversed edges/sec (TEPS)",
+        "metric": "GO 3 STEPS traversed edges/sec (TEPS) at 1/2/4/8 GPU; FIND SHORTEST PATH p50",
         "value": value,
         "unit": "TEPS",
         "n_gpus": world,
@@ -176,6 +186,7 @@ def main():
         "rows_per_step": rows // max(1, args.steps),
         "edges_per_step": scanned // max(1, args.steps),
         "kernels": kernels,
+        "find_shortest_path": sp,
         "load_seconds": round(load_s, 2),
     }
     print(json.dumps(out), flush=True)
@@ -183,13 +194,57 @@ def main():
         dist.barrier()
 
 
-def cpu_baseline(src, dst, w, roots, where, args):
+def shortest_path_leg(eng, pairs, args, barrier):
+    """FIND SHORTEST PATH FROM s TO t OVER e UPTO n STEPS, one query per pair."""
+    for s, t in pairs[:16]:   # warm-up
+        eng.find_path([s], [t], [1], args.sp_upto)
+    if not args.no_profile:
+        eng.profile(True)
+    barrier()
+    lat, edges, found, hops = [], 0, 0, 0
+    t0 = time.perf_counter()
+    for s, t in pairs:
+        st = {}
+        q0 = time.perf_counter()
+        paths = eng.find_path([s], [t], [1], args.sp_upto, stats=st)
+        lat.append(time.perf_counter() - q0)
+        edges += st["edges"]
+        if paths:
+            found += 1
+            hops += (len(paths[0]) - 1) // 3
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kst = eng.profile_read() if not args.no_profile else {}
+    if not args.no_profile:
+        eng.profile(False)
+    lat_ms = np.array(lat) * 1e3
+    out = {"query": f"FIND SHORTEST PATH FROM <s> TO <t> OVER e UPTO {args.sp_upto} STEPS",
+           "pairs": len(pairs), "pairs_seed": 7, "found": found,
+           "mean_hops": round(hops / found, 3) if found else None,
+           "p50_ms": float(np.percentile(lat_ms, 50)), "p90_ms": float(np.percentile(lat_ms, 90)),
+           "p99_ms": float(np.percentile(lat_ms, 99)), "mean_ms": float(lat_ms.mean()),
+           "teps": edges / elapsed if elapsed else None, "edges": edges, "seconds": round(elapsed, 3)}
+    if kst:
+        ks = {k: v for k, v in kst.items() if v["launches"]}
+        out["kernels"] = {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
+                              "algo_GBs": round(v["algo_bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None}
+                          for k, v in ks.items()}
+        name, v = max(ks.items(), key=lambda kv: kv[1]["ms"])
+        ach = v["algo_bytes"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] else 0.0
+        out["roofline"] = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                           "avg_launch_us": round(v["ms"] * 1e3 / v["launches"], 2)}
+        out["kernel_time_frac_of_wall"] = round(sum(x["ms"] for x in ks.values()) * 1e-3 / elapsed, 3)
+    return out
+
+
+def cpu_baseline(src, dst, w, roots, where, pairs, args):
     """oracle/ (storaged+graphd restated, RocksDB/thrift excluded) timed on the host cores."""
     try:
         from tests.support.oracle import Oracle
     except Exception as ex:  # pragma: no cover
         log(f"cpu baseline unavailable: {ex}")
-        return None
+        return None, None
     t0 = time.time()
     handlers = 10   # FLAGS_max_handlers_per_req
     o = Oracle(args.parts, threads=handlers)
@@ -207,11 +262,26 @@ def cpu_baseline(src, dst, w, roots, where, args):
         n += 1
         if secs >= args.cpu_seconds:
             break
+    go = {"value": scanned / secs if secs else None, "unit": "TEPS", "cores": handlers, "kind": "port",
+          "sample": f"first {n} of the {len(roots)} roots (same graph and query), {secs:.1f}s; one storaged "
+                    f"host, {handlers} handler threads (max_handlers_per_req), RowSet encode/decode per hop, "
+                    f"RocksDB/thrift/RPC excluded"}
+    sp = None
+    if pairs:
+        lat = []
+        for s, t in pairs:
+            q0 = time.perf_counter()
+            o.find_path([s], [t], [1], args.sp_upto, True, mode=1)
+            lat.append(time.perf_counter() - q0)
+            if sum(lat) >= args.cpu_seconds:
+                break
+        lat_ms = np.array(lat) * 1e3
+        sp = {"p50_ms": float(np.percentile(lat_ms, 50)), "mean_ms": float(lat_ms.mean()), "cores": 1,
+              "kind": "port", "sample": f"first {len(lat)} of the {len(pairs)} pairs, {sum(lat):.1f}s; oracle "
+                                        f"canonical shortest path (level-synchronous BFS from s over the "
+                                        f"storaged-faithful KV store, then B-set reconstruction), 1 thread"}
     o.close()
-    return {"value": scanned / secs if secs else None, "unit": "TEPS", "cores": handlers, "kind": "port",
-            "sample": f"first {n} of the {len(roots)} roots (same graph and query), {secs:.1f}s; one storaged "
-                      f"host, {handlers} handler threads (max_handlers_per_req), RowSet encode/decode per hop, "
-                      f"RocksDB/thrift/RPC excluded"}
+    return go, sp
 
 
 if __name__ == "__main__":

@@ -90,6 +90,16 @@ def dedup_last(src, dst, w):
     return src[idx], dst[idx], w[idx]
 
 
+def pick_pairs(src, dst, k: int, seed: int = 7):
+    """k (source, target) pairs, each end drawn uniformly (seeded, with replacement) among the
+    vertices with degree >= 1."""
+    verts = np.union1d(np.unique(src), np.unique(dst))
+    rng = np.random.default_rng(seed)
+    a = verts[rng.integers(0, len(verts), size=k)]
+    b = verts[rng.integers(0, len(verts), size=k)]
+    return [(int(x), int(y)) for x, y in zip(a, b)]
+
+
 def pick_roots(src, k: int, seed: int = 42):
     """k roots drawn uniformly (seeded) among vertices with out-degree >= 1."""
     verts = np.unique(src)

@@ -1,10 +1,9 @@
 """FIND SHORTEST PATH parity on the MI355X: nebula_amd (bidirectional / one-sided BFS kernels,
 B-set recovery, greedy canonical reconstruction) vs the CPU oracle (oracle/graph.cpp
 runShortestBfs, itself pinned by FindPathTest.cpp's golden paths).  Bit-exact entry lists."""
-import numpy as np
 import pytest
 
-from nebula_amd import NbgError, nba_engine
+from nebula_amd import NbgError, nba_engine, rmat
 from nebula_amd import _lib
 from tests.support import golden, graphs
 
@@ -45,12 +44,8 @@ def rmat12():
 
 
 def pairs(src, dst, k, seed=7):
-    """Pairs drawn uniformly from vertices with degree >= 1 (SURVEY §8(d) C4 scheme)."""
-    verts = np.unique(np.concatenate([src, dst]))
-    rng = np.random.default_rng(seed)
-    a = rng.choice(verts, k)
-    b = rng.choice(verts, k)
-    return [(int(x), int(y)) for x, y in zip(a, b)]
+    """Pairs drawn uniformly from vertices with degree >= 1 (the bench's C4 scheme)."""
+    return rmat.pick_pairs(src, dst, k, seed)
 
 
 @pytest.mark.parametrize("upto", [1, 2, 3, 5])
