@@ -27,6 +27,21 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+# HBM traffic per launch from the committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
+# bench (tools/gpu_check.sh pmc -> tools/pmc_summary.py; FETCH_SIZE doubled per the gfx950 note).
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_v3_pmc_hbm.json")
+PMC_NAMES = {"k_expand<MARK>": "k_expand<0>", "k_expand<FINAL>": "k_expand<1>", "k_expand<BFS>": "k_expand<2>"}
+
+
+def pmc_traffic(kernel):
+    """Corrected HBM bytes per launch of `kernel` from the committed PMC summary, or None."""
+    try:
+        with open(PMC_FILE) as f:
+            d = json.load(f)
+        k = d[PMC_NAMES.get(kernel, kernel)]
+        return k["read_bytes_per_launch_corrected"] + k["write_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def log(*a):
@@ -145,8 +160,11 @@ def main():
         dom = max(kstats.items(), key=lambda kv: kv[1]["ms"])
         name, v = dom
         achieved = v["algo_bytes"] / (v["ms"] * 1e-3) / 1e9
+        traffic = pmc_traffic(name)
         roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": round(traffic) if traffic else None,
+                    "traffic_source": os.path.relpath(PMC_FILE, ROOT) if traffic else None,
                     "avg_launch_us": round(v["ms"] * 1e3 / v["launches"], 2),
                     "algo_bytes_per_launch": v["algo_bytes"] / v["launches"]}
         total_ms = sum(x["ms"] for x in kstats.values())
