@@ -7,9 +7,14 @@ edge factor 16, seeded), 100 partitions, edge type e(w int); one "step" = the 64
 separate query through the C ABI (nbg_go_device: result rows stay in HBM).
 TEPS = Σ_s E_s (adjacency entries scanned at every step, after version de-dup) / wall time.
 
-Multi-GPU (torch.distributed.run, one rank per GPU): every rank holds a replica of the
-snapshot and runs the same 64-query step ("replicas", weak scaling); value = Σ edges over
-ranks / max time over ranks.  The partitioned all-to-all path is not in this build yet.
+Multi-GPU (torch.distributed.run, one rank per GPU): the engine is
+PARTITIONED — rank r holds the parts p with p % N == r (out-edges at src's part, in-edges at
+dst's part) and every query runs on all ranks; each hop's candidate set is exchanged with one
+bitmap all-to-all over RCCL/xGMI (the owner-side OR is GoExecutor's per-step dst set).  Weak
+scaling: the graph is RMAT-(22 + log2 N) (vertices and edges per GPU held constant; N=8 is
+RMAT-25, --scale overrides).  value = edges scanned by all queries (whole-query counts, summed
+over ranks inside the library) / max time over ranks.  torch.distributed (gloo) only carries the
+RCCL unique id, the barriers and the max-over-ranks timing.
 
 Also reported: the dominant kernel's achieved algorithmic HBM bandwidth (HIP events inside
 the library over the timed region) against the 8 TB/s peak, and the CPU oracle
@@ -53,7 +58,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scale", type=int, default=22)
+    ap.add_argument("--scale", type=int, default=None, help="RMAT scale (default 22 + log2(GPUs))")
     ap.add_argument("--roots", type=int, default=64)
     ap.add_argument("--parts", type=int, default=100)
     ap.add_argument("--go-steps", type=int, default=3)
@@ -67,6 +72,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("NBG_SAME_DEVICE"):
+        # rehearsal on a one-GPU box: every rank on device 0, RCCL over its socket transport
+        # (distinct host ids; see tools/rccl_probe.py).  Timings are then not xGMI numbers.
+        local = 0
+        os.environ["NCCL_HOSTID"] = f"nbg-rank-{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     dist = None
     if world > 1:
         import torch
@@ -74,12 +85,18 @@ def main():
         dist.init_process_group("gloo")
     import torch
 
-    from nebula_amd import Engine, expr as E, rmat
+    from nebula_amd import Engine, comm_unique_id, expr as E, rmat
 
+    if args.scale is None:
+        args.scale = 22 + max(0, int(round(np.log2(world))))
     t0 = time.time()
     src, dst, w = rmat.rmat_edges_fast(args.scale)
     gen_s = time.time() - t0
-    eng = Engine(args.parts, device=local)
+    eng = Engine(args.parts, num_gpus=world, rank=rank, device=local)
+    if world > 1:
+        box = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        eng.comm_init(box[0], world, rank)
     eng.register_edge(1, "e", [("w", 2)])
     t0 = time.time()
     eng.load_edges(1, src, dst, [w])
@@ -130,18 +147,20 @@ def main():
 
     sp = None
     pairs = []
-    if args.sp_pairs > 0:
+    if args.sp_pairs > 0 and world == 1:   # FIND PATH on a partitioned engine: not in this build
         pairs = rmat.pick_pairs(src, dst, args.sp_pairs, 7)
         sp = shortest_path_leg(eng, pairs, args, barrier)
 
-    tot_scanned, max_elapsed = float(scanned), elapsed
+    # edges_scanned is already the whole query's count (summed over ranks in the library);
+    # rows stay on the rank that produced them, so they are summed here
+    tot_scanned, max_elapsed, tot_rows = float(scanned), elapsed, float(rows)
     if dist is not None:
-        t = torch.tensor([float(scanned), elapsed], dtype=torch.float64)
+        t = torch.tensor([float(rows), elapsed], dtype=torch.float64)
         s_ = t.clone()
         dist.all_reduce(s_[:1], op=dist.ReduceOp.SUM)
         m_ = t.clone()
         dist.all_reduce(m_[1:], op=dist.ReduceOp.MAX)
-        tot_scanned, max_elapsed = float(s_[0]), float(m_[1])
+        tot_rows, max_elapsed = float(s_[0]), float(m_[1])
 
     if rank != 0:
         if dist is not None:
@@ -157,7 +176,9 @@ def main():
             if v["launches"]:
                 kernels[k] = {"launches": v["launches"], "ms": round(v["ms"], 3),
                               "algo_GBs": round(v["algo_bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None}
-        dom = max(kstats.items(), key=lambda kv: kv[1]["ms"])
+        # the collective is reported on its own (xGMI link bytes, not HBM)
+        comm = kstats.get("alltoall(xGMI)")
+        dom = max(((k, v) for k, v in kstats.items() if k != "alltoall(xGMI)"), key=lambda kv: kv[1]["ms"])
         name, v = dom
         achieved = v["algo_bytes"] / (v["ms"] * 1e-3) / 1e9
         traffic = pmc_traffic(name)
@@ -167,8 +188,13 @@ def main():
                     "traffic_source": os.path.relpath(PMC_FILE, ROOT) if traffic else None,
                     "avg_launch_us": round(v["ms"] * 1e3 / v["launches"], 2),
                     "algo_bytes_per_launch": v["algo_bytes"] / v["launches"]}
-        total_ms = sum(x["ms"] for x in kstats.values())
-        total_bytes = sum(x["algo_bytes"] for x in kstats.values())
+        if comm and comm["launches"]:
+            roofline["exchange"] = {"launches": comm["launches"], "avg_us": round(comm["ms"] * 1e3 / comm["launches"], 2),
+                                    "bytes_sent_per_launch": comm["algo_bytes"] / comm["launches"],
+                                    "note": "bitmap all-to-all per hop; bytes = (N-1) x npad/8 sent per rank"}
+        kst_hbm = {k: x for k, x in kstats.items() if k != "alltoall(xGMI)"}
+        total_ms = sum(x["ms"] for x in kst_hbm.values())
+        total_bytes = sum(x["algo_bytes"] for x in kst_hbm.values())
         roofline["all_kernels_GBs"] = round(total_bytes / (total_ms * 1e-3) / 1e9, 1) if total_ms else None
         roofline["kernel_time_frac_of_wall"] = round(total_ms * 1e-3 / elapsed, 3)
 
@@ -195,13 +221,14 @@ def main():
         "config": {"workload": f"GO {args.go_steps} STEPS FROM <root> OVER e WHERE e.w < 50 YIELD e._dst, "
                                f"{len(roots)} single-root queries per step",
                    "graph": f"RMAT-{args.scale}", "parts": args.parts, "roots": len(roots),
-                   "parallelism": "single" if world == 1 else f"replicas{world}",
+                   "parallelism": "single" if world == 1 else f"partitioned{world}: part % {world}, bitmap "
+                                                               f"all-to-all per hop over RCCL",
                    "vertices": st["num_vertices"], "live_edges_out_plus_in": st["num_edges"]},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "query_latency_ms": {"p50": float(np.percentile(lat_ms, 50)), "p90": float(np.percentile(lat_ms, 90)),
                              "max": float(lat_ms.max())},
-        "rows_per_step": rows // max(1, args.steps),
+        "rows_per_step": int(tot_rows) // max(1, args.steps),
         "edges_per_step": scanned // max(1, args.steps),
         "kernels": kernels,
         "find_shortest_path": sp,

@@ -145,7 +145,8 @@ int32_t nbg_go_device(nbg_engine* e, const nbg_go_request* req, nbg_rows** out);
 
 int64_t nbg_rows_count(const nbg_rows* r);
 int32_t nbg_rows_num_cols(const nbg_rows* r);
-/* Σ_s E_s: adjacency entries scanned over all steps (the TEPS numerator). */
+/* Σ_s E_s: adjacency entries scanned over all steps (the TEPS numerator); whole query, i.e.
+ * summed over ranks on a partitioned engine. */
 uint64_t nbg_rows_edges_scanned(const nbg_rows* r);
 /* Per-step counters: frontier size |F_s| and edges E_s, s = 1..steps (arrays of length steps). */
 int32_t nbg_rows_step_stats(const nbg_rows* r, uint64_t* frontier, uint64_t* edges, int32_t cap);
@@ -196,10 +197,27 @@ int32_t nbg_profile(nbg_engine* e, int32_t enable);
 /* Copies up to cap kernel records; returns the number of kernels. */
 int32_t nbg_profile_read(const nbg_engine* e, nbg_kernel_stat* out, int32_t cap);
 
-/* ---- multi-GPU (one process per GPU, RCCL over xGMI) ----------------------------------- */
+/* ---- multi-GPU: partitioned engine ------------------------------------
+ * With nbg_config.num_gpus = G > 1 an engine holds only the parts p with p % G == rank
+ * (CreateSpaceProcessor.cpp:84-95, GPUs as storaged hosts) and every query is a collective:
+ * all G engines must run the same nbg_go calls (same arguments, in the same order), the way
+ * StorageClient::getNeighbors fans one request out to every host (StorageClient.cpp:94-124).
+ * Per GO hop each rank expands its local frontier, and the per-step dst SET
+ * (GoExecutor::getDstIdsFromResp, GoExecutor.cpp:501-541) is formed by one bitmap all-to-all:
+ * rank q receives the candidates it owns.  Final-step rows stay on the rank that produced
+ * them (the result is the union over ranks); nbg_rows_step_stats / nbg_rows_edges_scanned
+ * report the whole query (summed over ranks).  The communicator must be attached before
+ * nbg_finalize (the loader exchanges vertex dictionaries to build global neighbour ids).
+ * FIND PATH on a partitioned engine returns NBG_E_UNSUPPORTED in this build. */
 #define NBG_UNIQUE_ID_BYTES 128
+/* RCCL unique id (ncclGetUniqueId); rank 0 creates it and ships it to the others. */
 int32_t nbg_comm_unique_id(uint8_t out[NBG_UNIQUE_ID_BYTES]);
+/* One process per GPU: RCCL communicator over xGMI (ncclCommInitRank); collective per rank. */
 int32_t nbg_comm_init(nbg_engine* e, const uint8_t id[NBG_UNIQUE_ID_BYTES], int32_t world, int32_t rank);
+/* Several engines of ONE process (engine i has rank i, num_gpus == n): an in-process group whose
+ * collectives copy between the engines' buffers.  Each engine is then driven by its own host
+ * thread (finalize and every query), exactly as the RCCL ranks are. */
+int32_t nbg_comm_init_local(nbg_engine* const* engines, int32_t n);
 
 #ifdef __cplusplus
 }

@@ -4,6 +4,6 @@ The product is the C ABI in ``include/nbg.h`` implemented by ``nebula_amd/libnbg
 (host C++ + gfx950 HIP kernels).  This package is the Python host binding plus fixture
 tooling (KV record builders, an nGQL front end for GO / FIND PATH).
 """
-from .engine import Engine, NbgError, DeviceRows, nba_engine  # noqa: F401
+from .engine import DeviceRows, Engine, LocalCluster, NbgError, comm_unique_id, nba_engine  # noqa: F401
 
-__all__ = ["Engine", "NbgError", "DeviceRows", "nba_engine"]
+__all__ = ["Engine", "NbgError", "DeviceRows", "LocalCluster", "comm_unique_id", "nba_engine"]

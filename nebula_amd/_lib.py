@@ -93,6 +93,7 @@ SIGNATURES = [
     ("nbg_profile_read", i32, [vp, vp, i32]),
     ("nbg_comm_unique_id", i32, [P(u8)]),
     ("nbg_comm_init", i32, [vp, P(u8), i32, i32]),
+    ("nbg_comm_init_local", i32, [P(vp), i32]),
 ]
 
 _lib = None

@@ -94,6 +94,7 @@ static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_row
   std::lock_guard<std::mutex> lg(E.mu);
   if (!E.finalized) return E.fail(NBG_E_STATE, "engine not finalized");
   if (rq->steps < 1) return E.fail(NBG_E_INVALID_ARGUMENT, "steps must be >= 1");
+  if (hipSetDevice(E.cfg.device) != hipSuccess) return E.fail(NBG_E_DEVICE, "hipSetDevice failed");
   // OVER (prepareOver / prepareOverAll, GoExecutor.cpp:197-263)
   std::vector<int32_t> over;
   if (rq->over_all) {
@@ -211,7 +212,8 @@ static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_row
   rows->eng = &E;
   rows->ncols = ncols;
   rows->on_device = device;
-  if (f0.empty()) { *out = rows; return NBG_OK; }
+  // (partitioned: every rank runs the same collective sequence, even with no local start)
+  if (f0.empty() && !E.partitioned()) { *out = rows; return NBG_OK; }
   if ((int)over.size() > MAX_TYPES_Q || rq->steps > (uint32_t)MAX_STEPS) {
     delete rows;
     return E.fail(NBG_E_UNSUPPORTED, "too many OVER types or steps");
@@ -220,6 +222,10 @@ static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_row
     ws_destroy(E.ws);
     E.ws = ws_create(f0.size(), E.snap.nv, E.stream, &err);
     if (!E.ws) { delete rows; return E.fail(NBG_E_OUT_OF_MEMORY, err); }
+    if (E.partitioned() && ws_set_partition(E.ws, E.comm.get(), E.npad) != hipSuccess) {
+      delete rows;
+      return E.fail(NBG_E_OUT_OF_MEMORY, "partition buffers");
+    }
   }
   Workspace* ws = E.ws;
   const uint32_t cap = (uint32_t)(E.cfg.max_edge_returned_per_vertex <= 0 ? 0x7fffffff
@@ -281,26 +287,36 @@ static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_row
       }
     }
     if (!final && he == hipSuccess) {
-      he = ws_compact(ws, (int)s);
+      he = E.partitioned() ? ws_exchange(ws, (int)s) : ws_compact(ws, (int)s);
       n_bound = E.snap.nv;
     }
   }
+  if (he == hipSuccess && E.partitioned()) he = ws_global_stats(ws, (int)over.size());
   if (he == hipSuccess) he = ws_end_query(ws);
   if (he != hipSuccess) {
     delete rows;
     return E.fail(NBG_E_DEVICE, std::string("HIP: ") + hipGetErrorString(he));
   }
   const QState& q = *ws_host_state(ws);
-  for (uint32_t s = 1; s <= rq->steps; ++s) {
-    uint64_t es = 0;
-    for (size_t i = 0; i < over.size(); ++i) es += q.e_st[s][i];
-    rows->step_frontier.push_back(q.step_n[s]);
-    rows->step_edges.push_back(es);
-    rows->scanned += es;
+  // statistics of the whole query: this engine's, or summed over all ranks when partitioned
+  unsigned long long g_err = q.err, g_n[MAX_STEPS + 2], g_e[MAX_STEPS + 2];
+  if (E.partitioned()) {
+    ws_host_gstats(ws, &g_err, g_n, g_e);
+  } else {
+    for (int s = 0; s < MAX_STEPS + 2; ++s) {
+      g_n[s] = q.step_n[s];
+      g_e[s] = 0;
+      for (size_t i = 0; i < over.size(); ++i) g_e[s] += q.e_st[s][i];
+    }
   }
-  const bool reached_final = q.step_n[rq->steps] > 0;
+  for (uint32_t s = 1; s <= rq->steps; ++s) {
+    rows->step_frontier.push_back(g_n[s]);
+    rows->step_edges.push_back(g_e[s]);
+    rows->scanned += g_e[s];
+  }
+  const bool reached_final = g_n[rq->steps] > 0;
   if (reached_final && deferred) { delete rows; return E.fail(deferred, deferred_msg); }
-  if (q.err) { delete rows; return E.fail(NBG_E_EXECUTION_ERROR, "WHERE/YIELD evaluation error"); }
+  if (g_err) { delete rows; return E.fail(NBG_E_EXECUTION_ERROR, "WHERE/YIELD evaluation error"); }
   for (size_t i = 0; i < over.size(); ++i) {
     for (int sh = 0; sh < NSHARD; ++sh) {
       uint64_t c = q.rows[i][sh];
@@ -413,6 +429,10 @@ int32_t nbg_finalize(nbg_engine* h) {
   std::string err;
   E.ws = ws_create(E.snap.nv + 1024, E.snap.nv, E.stream, &err);
   if (!E.ws) return E.fail(NBG_E_OUT_OF_MEMORY, err);
+  if (E.partitioned()) {
+    hipError_t he = ws_set_partition(E.ws, E.comm.get(), E.npad);
+    if (he != hipSuccess) return E.fail(NBG_E_OUT_OF_MEMORY, std::string("partition buffers: ") + hipGetErrorString(he));
+  }
   return NBG_OK;
 }
 

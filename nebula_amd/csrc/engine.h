@@ -1,5 +1,6 @@
 // Engine object behind the C ABI.
 #pragma once
+#include <memory>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -27,9 +28,10 @@ struct Engine {
   hipStream_t stream = nullptr;
   Workspace* ws = nullptr;
   std::mutex mu;
-  // multi-GPU
-  void* comm = nullptr;
-  int32_t world = 1;
+  // multi-GPU (partitioned mode when cfg.num_gpus > 1): global id = owner * npad + local id
+  std::unique_ptr<Comm> comm;
+  uint64_t npad = 0;
+  bool partitioned() const { return cfg.num_gpus > 1; }
 
   int32_t fail(int32_t code, const std::string& msg) {
     last_error = msg;
@@ -42,6 +44,8 @@ struct Engine {
   int32_t load_edges(int32_t type, const int64_t* src, const int64_t* dst, const int64_t* rank, uint64_t n,
                      const void* const* cols, int32_t ncols);
   int32_t finalize();
+  int32_t exchange_dictionary(const std::vector<int64_t>& local, std::vector<int64_t>* gdict,
+                              std::vector<uint64_t>* gcount);
   uint32_t dense(int64_t vid) const;
 };
 

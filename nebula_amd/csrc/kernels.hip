@@ -41,10 +41,12 @@ constexpr int FLAG_BYTES = BLOCK * 16;           // k_flag_*: bytes per block
 constexpr int EXPAND_GRID = 2048;                // persistent k_expand grid (8 blocks / CU)
 
 enum KernelId { K_DEGREE = 0, K_SCAN, K_EXPAND_MARK, K_FLAG_COUNT, K_FLAG_WRITE, K_EXPAND_FINAL, K_BFS,
-                K_GATHER, K_DEGSUM, K_GREEDY, K_STAMP, K_COUNT };
+                K_GATHER, K_DEGSUM, K_GREEDY, K_STAMP, K_PACK, K_ALLTOALL, K_BITS_COUNT, K_BITS_WRITE, K_COUNT };
 static const char* const kKernelNames[K_COUNT] = {"k_degree", "k_scan_blocks", "k_expand<MARK>", "k_flag_count",
                                                   "k_flag_write", "k_expand<FINAL>", "k_expand<BFS>", "k_gather",
-                                                  "k_degsum", "k_path_greedy", "k_stamp"};
+                                                  "k_degsum", "k_path_greedy", "k_stamp", "k_pack_bits",
+                                                  "alltoall(xGMI)", "k_bits_count", "k_bits_write"};
+constexpr int BITS_BLOCK = BLOCK * 64;           // k_bits_*: vertices (bits) per block
 
 struct Prof {
   bool on = false;
@@ -99,6 +101,15 @@ struct Workspace {
   int64_t* h_path = nullptr;
   uint32_t* h_stage = nullptr;    // pinned [PSLOTS][STAGE] upload staging (one upload per slot per query)
   int rec = 0;                    // next PState expansion record
+  // partitioned mode: flags cover the global id space [world * npad), one
+  // bitmap segment of npad bits per owner rank is exchanged per hop
+  Comm* comm = nullptr;
+  uint64_t npad = 0;
+  unsigned long long* sendbits = nullptr;   // [world * npad / 64]
+  unsigned long long* recvbits = nullptr;   // [world * npad / 64]
+  unsigned long long* mbits = nullptr;      // [npad / 64] OR of the received segments
+  unsigned long long* gst = nullptr;        // [GST_N] globally reduced query statistics
+  unsigned long long* h_gst = nullptr;
 };
 
 // ----------------------------------------------------------------------------- helpers
@@ -680,6 +691,81 @@ __global__ void __launch_bounds__(BLOCK) k_flag_write(uint8_t* __restrict__ flag
   }
 }
 
+// ----------------------------------------------------------------------------- partitioned exchange
+// Pack the byte flags of the global id space into a bitmap (one 64-bit word per 64 flags) and
+// clear them.  Segment q of the bitmap (npad bits) holds the next-frontier candidates owned by
+// rank q; the all-to-all hands every owner the G segments that concern it.
+__global__ void __launch_bounds__(BLOCK) k_pack_bits(uint8_t* __restrict__ flags, uint64_t nwords,
+                                                     unsigned long long* __restrict__ bits) {
+  const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= nwords) return;
+  uint4* p = reinterpret_cast<uint4*>(flags + i * 64);
+  unsigned long long m = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint4 q = p[k];
+    const uint32_t ws[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {   // flag bytes are 0 or 1
+      const uint32_t x = ws[j];
+      const unsigned long long b = (x & 1u) | ((x >> 7) & 2u) | ((x >> 14) & 4u) | ((x >> 21) & 8u);
+      m |= b << (k * 16 + j * 4);
+    }
+  }
+  bits[i] = m;
+  if (m) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) p[k] = make_uint4(0, 0, 0, 0);
+  }
+}
+
+// Owner side: OR the G received segments (one per sending rank) of this rank's id range; the
+// union is the global per-step dst SET restricted to the owner (getDstIdsFromResp).
+__global__ void __launch_bounds__(BLOCK) k_bits_count(const unsigned long long* __restrict__ recv, int world,
+                                                      uint64_t seg_words, uint64_t nv,
+                                                      unsigned long long* __restrict__ merged,
+                                                      uint32_t* __restrict__ block_cnt) {
+  __shared__ uint32_t lds[WAVES];
+  const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  unsigned long long m = 0;
+  for (int q = 0; q < world; ++q) m |= recv[(uint64_t)q * seg_words + i];
+  const uint64_t lo = i * 64;
+  if (lo >= nv) m = 0;
+  else if (nv - lo < 64) m &= (1ull << (nv - lo)) - 1ull;
+  merged[i] = m;
+  uint32_t tot;
+  block_excl_scan((uint32_t)__popcll(m), &tot, lds);
+  if (threadIdx.x == 0) block_cnt[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_bits_write(const unsigned long long* __restrict__ merged,
+                                                      const uint32_t* __restrict__ block_pre,
+                                                      uint32_t* __restrict__ out) {
+  __shared__ uint32_t lds[WAVES];
+  const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  unsigned long long m = merged[i];
+  uint32_t tot;
+  uint32_t pre = block_excl_scan((uint32_t)__popcll(m), &tot, lds) + block_pre[blockIdx.x];
+  while (m) {
+    const int b = __ffsll((long long)m) - 1;
+    out[pre++] = (uint32_t)(i * 64 + b);
+    m &= m - 1;
+  }
+}
+
+// Query statistics every rank needs globally: [err, step_n[0..MAX_STEPS+1], Σ_types e_st[s]].
+constexpr int GST_N = 1 + 2 * (MAX_STEPS + 2);
+__global__ void k_gstats(const QState* __restrict__ q, int ntypes, unsigned long long* __restrict__ g) {
+  const int s = threadIdx.x;
+  if (s == 0) g[0] = q->err ? 1ull : 0ull;
+  if (s < MAX_STEPS + 2) {
+    g[1 + s] = q->step_n[s];
+    unsigned long long e = 0;
+    for (int t = 0; t < ntypes; ++t) e += q->e_st[s][t];
+    g[1 + (MAX_STEPS + 2) + s] = e;
+  }
+}
+
 // ============================================================================= host side
 static inline uint64_t cdiv(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
@@ -709,6 +795,8 @@ static double prof_bytes(const Prof::Rec& r, const QState& q) {
     case K_DEGREE: return 12.0 * (double)q.step_n[r.step];                 // 4|F| ids + 8|F| row_ptr
     case K_EXPAND_MARK: return 4.0 * (double)q.e_st[r.step][r.tix];        // 4 E_s neighbour ids
     case K_FLAG_WRITE: return 4.0 * (double)q.step_n[r.step + 1];          // write F_{s+1}
+    case K_BITS_WRITE: return 4.0 * (double)q.step_n[r.step + 1];
+    case K_PACK: case K_ALLTOALL: case K_BITS_COUNT: return r.cols;       // fixed sizes (set at launch)
     case K_EXPAND_FINAL: {
       double rows = 0;
       for (int s = 0; s < NSHARD; ++s) rows += (double)q.rows[r.tix][s];
@@ -814,6 +902,9 @@ void ws_destroy(Workspace* w) {
   for (void* p : {(void*)w->h_q, (void*)w->h_starts, (void*)w->h_prog, (void*)w->h_ps, (void*)w->h_path,
                   (void*)w->h_stage})
     if (p) (void)hipHostFree(p);
+  for (void* p : {(void*)w->sendbits, (void*)w->recvbits, (void*)w->mbits, (void*)w->gst})
+    if (p) (void)hipFree(p);
+  if (w->h_gst) (void)hipHostFree(w->h_gst);
   for (void* p : {(void*)w->ps, (void*)w->pscratch, (void*)w->d_path})
     if (p) (void)hipFree(p);
   for (auto* p : w->lab)
@@ -1029,6 +1120,84 @@ hipError_t ws_end_query(Workspace* w) {
   HIP_TRY(hipStreamSynchronize(w->stream));
   prof_flush(w, w->h_q);
   return hipSuccess;
+}
+
+// ----------------------------------------------------------------------------- partitioned mode
+hipError_t ws_set_partition(Workspace* w, Comm* comm, uint64_t npad) {
+  if (!comm || npad % BITS_BLOCK) return hipErrorInvalidValue;
+  const uint64_t G = (uint64_t)comm->world;
+  HIP_TRY(hipStreamSynchronize(w->stream));
+  w->comm = comm;
+  w->npad = npad;
+  if (w->flags) HIP_TRY(hipFree(w->flags));
+  w->flags = nullptr;
+  w->flag_bytes = G * npad;                     // multiple of FLAG_BYTES (npad % BITS_BLOCK == 0)
+  HIP_TRY(hipMalloc((void**)&w->flags, w->flag_bytes));
+  HIP_TRY(hipMemsetAsync(w->flags, 0, w->flag_bytes, w->stream));
+  HIP_TRY(hipMalloc((void**)&w->sendbits, G * npad / 8));
+  HIP_TRY(hipMalloc((void**)&w->recvbits, G * npad / 8));
+  HIP_TRY(hipMalloc((void**)&w->mbits, npad / 8));
+  HIP_TRY(hipMalloc((void**)&w->gst, GST_N * sizeof(unsigned long long)));
+  HIP_TRY(hipHostMalloc((void**)&w->h_gst, GST_N * sizeof(unsigned long long), hipHostMallocDefault));
+  const uint64_t nb = npad / BITS_BLOCK + 1;
+  if (nb > w->cap_blocks) {
+    if (w->flag_blocks) HIP_TRY(hipFree(w->flag_blocks));
+    w->flag_blocks = nullptr;
+    w->cap_blocks = nb;
+    HIP_TRY(hipMalloc((void**)&w->flag_blocks, nb * 4));
+    HIP_TRY(hipFree(w->block_sum));
+    w->block_sum = nullptr;
+    HIP_TRY(hipMalloc((void**)&w->block_sum, nb * 4));
+  }
+  return hipStreamSynchronize(w->stream);
+}
+
+// After all OVER types of a non-final step marked their candidates (global ids) in the flags:
+// pack -> all-to-all of npad-bit segments -> owner OR + compaction into the next local frontier.
+hipError_t ws_exchange(Workspace* w, int step) {
+  if (!w->comm) return hipErrorInvalidValue;
+  const uint64_t G = (uint64_t)w->comm->world;
+  const uint64_t nwords = G * w->npad / 64, seg_words = w->npad / 64, nb = w->npad / BITS_BLOCK;
+  hipEvent_t p = prof_begin(w);
+  hipLaunchKernelGGL(k_pack_bits, dim3((unsigned)cdiv(nwords, BLOCK)), dim3(BLOCK), 0, w->stream, w->flags, nwords,
+                     w->sendbits);
+  prof_end(w, p, K_PACK, step, 0, (double)(G * w->npad) + (double)(G * w->npad / 8));
+  HIP_TRY(hipGetLastError());
+  p = prof_begin(w);
+  if (w->comm->alltoall(w->sendbits, w->recvbits, w->npad / 8, w->stream)) return hipErrorUnknown;
+  prof_end(w, p, K_ALLTOALL, step, 0, (double)((G - 1) * w->npad / 8));
+  p = prof_begin(w);
+  hipLaunchKernelGGL(k_bits_count, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->recvbits, (int)G, seg_words,
+                     w->nv, w->mbits, w->flag_blocks);
+  prof_end(w, p, K_BITS_COUNT, step, 0, (double)(G * w->npad / 8) + (double)(w->npad / 8));
+  p = prof_begin(w);
+  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, w->stream, w->flag_blocks, &w->q->n, nb, &w->q->n,
+                     &w->q->step_n[step + 1]);
+  prof_end(w, p, K_SCAN, step, 0);
+  p = prof_begin(w);
+  hipLaunchKernelGGL(k_bits_write, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->mbits, w->flag_blocks,
+                     w->frontier[w->cur ^ 1]);
+  prof_end(w, p, K_BITS_WRITE, step, 0);
+  w->cur ^= 1;
+  return hipGetLastError();
+}
+
+// Global query statistics (err flag, |F_s|, E_s summed over ranks), synchronised with the query
+// end; valid in ws_host_gstats() after ws_end_query.
+hipError_t ws_global_stats(Workspace* w, int ntypes) {
+  if (!w->comm) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_gstats, dim3(1), dim3(64), 0, w->stream, w->q, ntypes, w->gst);
+  HIP_TRY(hipGetLastError());
+  if (w->comm->allreduce_sum_u64(w->gst, GST_N, w->stream)) return hipErrorUnknown;
+  return hipMemcpyAsync(w->h_gst, w->gst, GST_N * sizeof(unsigned long long), hipMemcpyDeviceToHost, w->stream);
+}
+
+void ws_host_gstats(Workspace* w, unsigned long long* err, unsigned long long* step_n, unsigned long long* esum) {
+  *err = w->h_gst[0];
+  for (int s = 0; s < MAX_STEPS + 2; ++s) {
+    step_n[s] = w->h_gst[1 + s];
+    esum[s] = w->h_gst[1 + (MAX_STEPS + 2) + s];
+  }
 }
 
 

@@ -215,6 +215,44 @@ inline bool rowkey_less(const RowKey& a, const RowKey& b) {
 }
 }  // namespace
 
+// Every rank learns every rank's sorted vertex dictionary (allgather over the communicator):
+// npad = the largest dictionary rounded up to PART_ALIGN.
+int32_t Engine::exchange_dictionary(const std::vector<int64_t>& local, std::vector<int64_t>* gdict,
+                                    std::vector<uint64_t>* gcount) {
+  if (!comm) return fail(NBG_E_STATE, "a partitioned engine (num_gpus > 1) needs nbg_comm_init before nbg_finalize");
+  const uint64_t G = (uint64_t)cfg.num_gpus;
+  uint64_t* d_cnt = nullptr;
+  int64_t *d_loc = nullptr, *d_glob = nullptr;
+  auto done = [&](int32_t rc, const std::string& msg) {
+    for (void* p : {(void*)d_cnt, (void*)d_loc, (void*)d_glob})
+      if (p) (void)hipFree(p);
+    return rc ? fail(rc, msg) : NBG_OK;
+  };
+  const uint64_t nv = local.size();
+  if (hipMalloc((void**)&d_cnt, (G + 1) * 8) != hipSuccess ||
+      hipMemcpy(d_cnt + G, &nv, 8, hipMemcpyHostToDevice) != hipSuccess)
+    return done(NBG_E_OUT_OF_MEMORY, "dictionary exchange: device allocation");
+  if (comm->allgather(d_cnt + G, d_cnt, 8, stream) || hipStreamSynchronize(stream) != hipSuccess)
+    return done(NBG_E_DEVICE, "dictionary exchange (counts): " + comm->last);
+  gcount->assign(G, 0);
+  if (hipMemcpy(gcount->data(), d_cnt, G * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return done(NBG_E_DEVICE, "dictionary exchange: copy");
+  uint64_t mx = 1;
+  for (uint64_t c : *gcount) mx = std::max(mx, c);
+  npad = (mx + PART_ALIGN - 1) / PART_ALIGN * PART_ALIGN;
+  if (G * npad >= (uint64_t)NO_ROW) return done(NBG_E_UNSUPPORTED, "global id space exceeds 2^32-1 vertices");
+  if (hipMalloc((void**)&d_loc, npad * 8) != hipSuccess || hipMalloc((void**)&d_glob, G * npad * 8) != hipSuccess)
+    return done(NBG_E_OUT_OF_MEMORY, "dictionary exchange: device allocation");
+  if (nv && hipMemcpy(d_loc, local.data(), nv * 8, hipMemcpyHostToDevice) != hipSuccess)
+    return done(NBG_E_DEVICE, "dictionary exchange: upload");
+  if (comm->allgather(d_loc, d_glob, npad * 8, stream) || hipStreamSynchronize(stream) != hipSuccess)
+    return done(NBG_E_DEVICE, "dictionary exchange (vids): " + comm->last);
+  gdict->resize(G * npad);
+  if (hipMemcpy(gdict->data(), d_glob, G * npad * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return done(NBG_E_DEVICE, "dictionary exchange: download");
+  return done(NBG_OK, "");
+}
+
 int32_t Engine::finalize() {
   if (finalized) return fail(NBG_E_STATE, "engine already finalized");
   // 1. string dictionary: sorted; device code = 2 * rank
@@ -263,6 +301,23 @@ int32_t Engine::finalize() {
     if (home[d] != hash_part(all[d], cfg.num_parts)) { visible[d] = 0; all_visible = false; }
   }
   snap.h_part = home;
+
+  // 2b. partitioned mode: a global id space [G * npad) — rank q's vertices are q * npad + local
+  // id — so a neighbour id names its owner (the rank serving its hash part) without a lookup.
+  std::vector<int64_t> gdict;
+  std::vector<uint64_t> gcount;
+  if (partitioned()) {
+    int32_t prc = exchange_dictionary(all, &gdict, &gcount);
+    if (prc) return prc;
+  }
+  const int32_t G = cfg.num_gpus;
+  auto gid = [&](int64_t vid) -> uint32_t {
+    if (!partitioned()) return dense(vid);
+    const uint64_t q = (uint64_t)(hash_part(vid, cfg.num_parts) % G);
+    auto b = gdict.begin() + q * npad, e = b + gcount[q];
+    auto it = std::lower_bound(b, e, vid);
+    return (it != e && *it == vid) ? (uint32_t)(q * npad + (uint64_t)(it - b)) : NO_ROW;
+  };
 
   // 3. per signed type: bucket by src, sort rows in key order, keep the live version
   int32_t rc = NBG_OK;
@@ -322,7 +377,7 @@ int32_t Engine::finalize() {
       for (uint32_t m = 0; m < live[d + 1]; ++m) {
         const RowKey& k = keys[cnt[d] + m];
         uint64_t i = k.idx;
-        col[o + m] = dense(st.dst[i]);
+        col[o + m] = gid(st.dst[i]);
         dvid[o + m] = st.dst[i];
         rk[o + m] = st.rank[i];
         if (st.rank[i]) any_rank = true;

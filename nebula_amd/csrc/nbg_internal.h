@@ -206,6 +206,22 @@ struct PathTypes {                   // the CSRs one search direction expands (o
   ExpandArgs a[MAX_TYPES_Q];
 };
 
+// ----------------------------------------------------------------------------- collectives (comm.cpp)
+// Transport of the partitioned engine.  Methods return 0 on success; `last` holds the error.
+struct Comm {
+  int world = 1, rank = 0;
+  std::string last;
+  virtual ~Comm() {}
+  virtual const char* kind() const = 0;
+  // recv[q * bytes ..] <- rank q's send[rank * bytes ..], for every q (stream-ordered)
+  virtual int alltoall(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
+  // recv[q * bytes ..] <- rank q's send[0 .. bytes)
+  virtual int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
+  virtual int allreduce_sum_u64(unsigned long long* buf, size_t n, hipStream_t s) = 0;
+};
+Comm* comm_rccl(const uint8_t id[NBG_UNIQUE_ID_BYTES], int world, int rank, std::string* err);
+std::vector<Comm*> comm_local_group(int world);
+
 struct Workspace;   // kernels.hip
 
 Workspace* ws_create(uint64_t max_frontier, uint64_t nv, hipStream_t s, std::string* err);
@@ -230,6 +246,12 @@ hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a, uint64_t n_bound, 
                            const TypeProgram& prog, uint64_t region_base, uint64_t shard_cap);
 hipError_t ws_scan_only(Workspace* w, const ExpandArgs& a, uint64_t n_bound, int step, int tix);
 hipError_t ws_end_query(Workspace* w);
+// partitioned mode: flags over [world * npad) global ids, per-hop bitmap all-to-all
+constexpr uint64_t PART_ALIGN = 256 * 64;    // npad granularity (k_bits_* block)
+hipError_t ws_set_partition(Workspace* w, Comm* comm, uint64_t npad);
+hipError_t ws_exchange(Workspace* w, int step);            // replaces ws_compact
+hipError_t ws_global_stats(Workspace* w, int ntypes);      // before ws_end_query
+void ws_host_gstats(Workspace* w, unsigned long long* err, unsigned long long* step_n, unsigned long long* esum);
 
 // FIND SHORTEST PATH (kernels.hip).  Frontier lists live in numbered device slots; PState sizes
 // are read back by ws_path_sync.  All calls enqueue on the workspace stream.

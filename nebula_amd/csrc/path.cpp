@@ -232,6 +232,8 @@ extern "C" int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* rq, nbg_
   Engine& E = h->e;
   std::lock_guard<std::mutex> lg(E.mu);
   if (!E.finalized) return E.fail(NBG_E_STATE, "engine not finalized");
+  if (E.partitioned()) return E.fail(NBG_E_UNSUPPORTED, "FIND PATH on a partitioned engine is not built yet");
+  if (hipSetDevice(E.cfg.device) != hipSuccess) return E.fail(NBG_E_DEVICE, "hipSetDevice failed");
   if (!rq->shortest) return E.fail(NBG_E_UNSUPPORTED, "FIND ALL PATH is not supported on the device path yet");
   if (rq->upto > MAX_PATH_LEN) return E.fail(NBG_E_UNSUPPORTED, "UPTO exceeds the device path limit (63)");
   if (E.cfg.max_edge_returned_per_vertex > 0 && E.cfg.max_edge_returned_per_vertex != INT_MAX)
@@ -307,14 +309,4 @@ extern "C" int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* rq, nbg_
   res->edges = c.edges;
   *out = res;
   return NBG_OK;
-}
-
-extern "C" int32_t nbg_comm_unique_id(uint8_t out[NBG_UNIQUE_ID_BYTES]) {
-  (void)out;
-  return NBG_E_UNSUPPORTED;
-}
-
-extern "C" int32_t nbg_comm_init(nbg_engine* h, const uint8_t id[NBG_UNIQUE_ID_BYTES], int32_t world, int32_t rank) {
-  (void)id; (void)world; (void)rank;
-  return h ? h->e.fail(NBG_E_UNSUPPORTED, "multi-GPU not built yet") : NBG_E_INVALID_ARGUMENT;
 }

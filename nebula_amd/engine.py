@@ -235,6 +235,92 @@ class Engine:
             self.lib.nbg_paths_free(out)
 
 
+# ---------------------------------------------------------------------- multi-GPU (partitioned)
+def comm_unique_id() -> bytes:
+    """RCCL unique id (rank 0 creates it and ships it to the other ranks)."""
+    lib = L.load()
+    buf = (C.c_uint8 * 128)()
+    rc = lib.nbg_comm_unique_id(buf)
+    if rc:
+        raise NbgError(rc, "nbg_comm_unique_id failed")
+    return bytes(buf)
+
+
+def _comm_init(self, uid: bytes, world: int, rank: int):
+    """Attach an RCCL communicator (one process per GPU); before ``finalize``."""
+    buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+    self._check(self.lib.nbg_comm_init(self.h, buf, world, rank), "comm_init")
+
+
+Engine.comm_init = _comm_init
+
+
+class LocalCluster:
+    """G partitioned engines in ONE process (nbg_comm_init_local), each driven by its own host
+    thread exactly like one RCCL rank per process.  Used to run the partitioned path on a single
+    GPU (all ranks on ``device``) and by hosts that drive a node's GPUs from one process."""
+
+    def __init__(self, num_parts: int, world: int, devices=None, max_edge_returned_per_vertex: int = 0x7FFFFFFF):
+        from concurrent.futures import ThreadPoolExecutor
+        devices = devices or [0] * world
+        self.engines = [Engine(num_parts, world, r, devices[r], max_edge_returned_per_vertex) for r in range(world)]
+        arr = (C.c_void_p * world)(*[e.h.value for e in self.engines])
+        rc = self.engines[0].lib.nbg_comm_init_local(arr, world)
+        if rc:
+            raise NbgError(rc, "nbg_comm_init_local failed")
+        self.pool = ThreadPoolExecutor(max_workers=world)
+
+    def each(self, fn):
+        """Run fn(engine) on every rank concurrently; returns the per-rank results."""
+        futs = [self.pool.submit(fn, e) for e in self.engines]
+        return [f.result() for f in futs]
+
+    @property
+    def edge_types(self):
+        return self.engines[0].edge_types
+
+    @property
+    def edge_names(self):
+        return self.engines[0].edge_names
+
+    @property
+    def tag_ids(self):
+        return self.engines[0].tag_ids
+
+    def register_edge(self, *a, **k):
+        for e in self.engines:
+            e.register_edge(*a, **k)
+
+    def register_tag(self, *a, **k):
+        for e in self.engines:
+            e.register_tag(*a, **k)
+
+    def load_edges(self, *a, **k):
+        for e in self.engines:
+            e.load_edges(*a, **k)
+
+    def load_builder(self, kb):
+        for e in self.engines:
+            e.load_builder(kb, finalize=False)
+        self.finalize()
+
+    def finalize(self):
+        self.each(lambda e: e.finalize())
+
+    def go(self, *a, **k):
+        """Union of the ranks' rows (each rank keeps the rows its final frontier produced)."""
+        out = []
+        for rows in self.each(lambda e: e.go(*a, **k)):
+            out += rows
+        self.last_step_stats = self.engines[0].last_step_stats
+        return out
+
+    def close(self):
+        self.pool.shutdown()
+        for e in self.engines:
+            e.close()
+
+
 def nba_engine(data, parts=1, device=0):
     """The TraverseTestBase dataset loaded through the KV path."""
     from . import kvgen

@@ -1,0 +1,130 @@
+"""Partitioned GO N STEPS on the MI355X: G engines, each holding the parts
+p % G == rank, exchange each hop's candidate set with a bitmap all-to-all.  The union of the
+ranks' rows must equal the single-engine result bit-exactly (sorted row multisets), and the
+whole-query statistics (|F_s|, E_s) must equal the single engine's.
+
+The ranks run as an in-process group on one GPU (nbg_comm_init_local: one host thread per rank,
+the same engine code as one RCCL rank per process; only the transport differs)."""
+import numpy as np
+import pytest
+
+from nebula_amd import LocalCluster, NbgError, _lib, expr as E, kvgen
+from tests.support import golden, graphs
+from tests.support.oracle import nba_oracle
+
+pytestmark = pytest.mark.gpu
+
+WHERES = {
+    "none": None,
+    "w<50": E.binop("<", E.edge_prop("e", "w"), E.const(50)),
+    "w%7==3||w>=90": E.binop("||", E.binop("==", E.binop("%", E.edge_prop("e", "w"), E.const(7)), E.const(3)),
+                             E.binop(">=", E.edge_prop("e", "w"), E.const(90))),
+}
+
+
+def cluster_for(src, dst, w, world, parts=100, max_edge=0x7FFFFFFF):
+    c = LocalCluster(parts, world, max_edge_returned_per_vertex=max_edge)
+    c.register_edge(graphs.E_TYPE, "e", graphs.E_SCHEMA)
+    c.load_edges(graphs.E_TYPE, src, dst, [w])
+    c.finalize()
+    return c
+
+
+@pytest.fixture(scope="module")
+def rmat11():
+    src, dst, w = graphs.rmat_graph(11)
+    single = graphs.rmat_engine(src, dst, w)
+    orc = graphs.rmat_oracle(src, dst, w)
+    clusters = {g: cluster_for(src, dst, w, g) for g in (2, 3, 4)}
+    yield src, single, orc, clusters
+    for c in clusters.values():
+        c.close()
+    single.close()
+    orc.close()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("steps", [1, 2, 3])
+@pytest.mark.parametrize("where", list(WHERES))
+def test_partitioned_go_matches_single_and_oracle(rmat11, world, steps, where):
+    src, single, orc, clusters = rmat11
+    c = clusters[world]
+    wb = WHERES[where].encode() if WHERES[where] is not None else b""
+    yields = [E.edge_prop("e", "_src").encode(), E.edge_prop("e", "_dst").encode(), E.edge_prop("e", "w").encode()]
+    for r in graphs.roots(src, 3, seed=5):
+        got = graphs.sorted_rows(c.go([r], [1], steps, wb, yields))
+        ref = graphs.sorted_rows(single.go([r], [1], steps, wb, yields))
+        assert got == ref, f"G={world} root {r}: {len(got)} vs {len(ref)} rows"
+        # the whole-query statistics are global on every rank
+        assert c.last_step_stats == single.last_step_stats
+        exp = graphs.sorted_rows(orc.go([r], [1], steps, wb, yields))
+        assert got == exp
+
+
+def test_partitioned_multi_start_duplicates(rmat11):
+    src, single, orc, clusters = rmat11
+    rs = graphs.roots(src, 6, seed=9)
+    starts = rs + rs[:2] + [123456789]          # duplicates kept, unknown vid ignored
+    for world, c in clusters.items():
+        got = graphs.sorted_rows(c.go(starts, [1], 2))
+        assert got == graphs.sorted_rows(orc.go(starts, [1], 2)), world
+
+
+def test_partitioned_eval_error_is_global(rmat11):
+    # WHERE e.w / 0 fails the whole query wherever the failing edge lives
+    src, single, orc, clusters = rmat11
+    bad = E.binop("==", E.binop("/", E.edge_prop("e", "w"), E.const(0)), E.const(1)).encode()
+    r = graphs.roots(src, 1, seed=3)[0]
+    for c in clusters.values():
+        errs = c.each(lambda e: _code_of(lambda: e.go([r], [1], 2, bad)))
+        assert errs == [_lib.E_EXECUTION_ERROR] * len(errs)
+
+
+def _code_of(fn):
+    try:
+        fn()
+        return 0
+    except NbgError as ex:
+        return ex.code
+
+
+def test_partitioned_edge_cap():
+    src, dst, w = graphs.rmat_graph(10)
+    c = cluster_for(src, dst, w, 2, max_edge=3)
+    orc = graphs.rmat_oracle(src, dst, w, max_edge=3)
+    try:
+        for r in graphs.roots(src, 3, seed=11):
+            assert graphs.sorted_rows(c.go([r], [1], 3)) == graphs.sorted_rows(orc.go([r], [1], 3))
+    finally:
+        c.close()
+        orc.close()
+
+
+def test_partitioned_nba_golden(nba_data):
+    """The reference's GoTest golden cases through the KV path on 3 ranks (7 parts)."""
+    parts = 7
+    c = LocalCluster(parts, 3)
+    for (kind, name), cols in kvgen.NBA_SCHEMAS.items():
+        if kind == "edge":
+            c.register_edge(kvgen.NBA_EDGES[name], name, cols)
+        else:
+            c.register_tag(kvgen.NBA_TAGS[name], name, cols)
+    c.load_builder(kvgen.nba_kv(nba_data, parts))
+    orc = nba_oracle(nba_data, parts)
+    try:
+        checked = 0
+        for case in golden.load("go_golden.json"):
+            if golden.unsupported_reason(case):
+                continue
+            try:
+                ok, msg = golden.run_go_case(c, case)
+            except NbgError as ex:
+                if ex.code == _lib.E_UNSUPPORTED:   # same cases the single-engine test skips
+                    continue
+                raise
+            assert ok, msg
+            checked += 1
+        assert checked > 0
+    finally:
+        c.close()
+        orc.close()
