@@ -156,8 +156,12 @@ int32_t nbg_rows_fetch(nbg_rows* r);
 const int64_t* nbg_rows_col_bits(const nbg_rows* r, int32_t col);
 const uint8_t* nbg_rows_col_tags(const nbg_rows* r, int32_t col);
 const char* nbg_rows_string(const nbg_rows* r, int64_t string_id);
-/* Device view of a column's 8-byte payloads (valid for nbg_go_device results). */
+/* Device view of a column's 8-byte payloads (valid for nbg_go_device results).  Rows are not
+ * contiguous: each producing workgroup appends to its own region, so the result is the union of
+ * the row ranges [begin, end) listed by nbg_rows_segment (host fetches pack them in that order). */
 const void* nbg_rows_device_col(const nbg_rows* r, int32_t col);
+int64_t nbg_rows_num_segments(const nbg_rows* r);
+int32_t nbg_rows_segment(const nbg_rows* r, int64_t i, uint64_t* begin, uint64_t* end);
 void nbg_rows_free(nbg_rows* r);
 
 /* ---- FIND SHORTEST | ALL PATH (FindPathExecutor semantics) ----------------------------- */
@@ -192,7 +196,9 @@ typedef struct {
   double total_ms;            /* sum of event-measured launch durations                        */
   double algo_bytes;          /* algorithmic HBM bytes of those launches */
 } nbg_kernel_stat;
-/* enable != 0 starts (and resets) per-kernel timing; 0 stops it. */
+/* enable = 1 starts (and resets) timing of every launch; 2 times only the final-step /
+ * shortest-path expansion kernels (two events per query: minimal perturbation of the timed
+ * region); 0 stops timing. */
 int32_t nbg_profile(nbg_engine* e, int32_t enable);
 /* Copies up to cap kernel records; returns the number of kernels. */
 int32_t nbg_profile_read(const nbg_engine* e, nbg_kernel_stat* out, int32_t cap);

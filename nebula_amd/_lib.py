@@ -82,6 +82,8 @@ SIGNATURES = [
     ("nbg_rows_col_tags", P(u8), [vp, i32]),
     ("nbg_rows_string", C.c_char_p, [vp, i64]),
     ("nbg_rows_device_col", vp, [vp, i32]),
+    ("nbg_rows_num_segments", i64, [vp]),
+    ("nbg_rows_segment", i32, [vp, i64, P(u64), P(u64)]),
     ("nbg_rows_free", None, [vp]),
     ("nbg_find_path", i32, [vp, P(nbg_path_request), P(vp)]),
     ("nbg_paths_count", i64, [vp]),

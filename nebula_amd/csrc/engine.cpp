@@ -30,9 +30,10 @@ uint32_t Engine::dense(int64_t vid) const {
 struct nbg_rows {
   struct Seg {
     uint64_t begin = 0, end = 0;
-    std::vector<VKind> kinds;
-    std::vector<std::string> const_str;   // string constants absent from the dictionary
+    int type = 0;                          // index into kinds / const_str (OVER position)
   };
+  std::vector<std::vector<VKind>> kinds;              // per OVER type: value kind of each column
+  std::vector<std::vector<std::string>> const_str;    // per OVER type: string constants absent from the dictionary
   Engine* eng = nullptr;
   int ncols = 0;
   uint64_t count = 0;
@@ -54,14 +55,19 @@ int32_t materialize_rows(nbg_rows* r) {
   const auto& dict = r->eng->snap.strings;
   r->bits.assign(r->ncols, std::vector<int64_t>(r->count));
   r->tags.assign(r->ncols, std::vector<uint8_t>(r->count));
+  {
+    std::vector<std::pair<uint64_t, uint64_t>> segs;
+    for (auto& s : r->segs) segs.emplace_back(s.begin, s.end - s.begin);
+    std::vector<int64_t*> hc;
+    for (auto& b : r->bits) hc.push_back(b.data());
+    if (ws_fetch_rows(r->eng->ws, segs, r->ncols, r->count, hc.data()) != hipSuccess) return NBG_E_DEVICE;
+  }
   std::unordered_map<int64_t, int64_t> sidx;
   uint64_t o = 0;
   for (auto& s : r->segs) {
     uint64_t len = s.end - s.begin;
     for (int c = 0; c < r->ncols; ++c) {
-      if (hipMemcpy(r->bits[c].data() + o, r->dcols[c] + s.begin, len * 8, hipMemcpyDeviceToHost) != hipSuccess)
-        return NBG_E_DEVICE;
-      VKind k = s.kinds[c];
+      VKind k = r->kinds[s.type][c];
       for (uint64_t i = o; i < o + len; ++i) {
         r->tags[c][i] = (uint8_t)k;
         if (k == VK_STRING) {
@@ -69,7 +75,7 @@ int32_t materialize_rows(nbg_rows* r) {
           auto it = sidx.find(code);
           if (it == sidx.end()) {
             std::string txt = (code >= 0 && (code & 1) == 0 && (uint64_t)(code / 2) < dict.size())
-                                  ? dict[code / 2] : s.const_str[c];
+                                  ? dict[code / 2] : r->const_str[s.type][c];
             it = sidx.emplace(code, (int64_t)r->strings.size()).first;
             r->strings.push_back(txt);
           }
@@ -220,7 +226,7 @@ static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_row
   }
   if (f0.size() > ws_cap_frontier(E.ws)) {   // room for a duplicated start list
     ws_destroy(E.ws);
-    E.ws = ws_create(f0.size(), E.snap.nv, E.stream, &err);
+    E.ws = ws_create(f0.size(), E.snap.nv, E.snap.max_edges(), E.stream, &err);
     if (!E.ws) { delete rows; return E.fail(NBG_E_OUT_OF_MEMORY, err); }
     if (E.partitioned() && ws_set_partition(E.ws, E.comm.get(), E.npad) != hipSuccess) {
       delete rows;
@@ -249,10 +255,22 @@ static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_row
     auto it = progs.find(over[i]);
     if (it != progs.end()) plist[i] = it->second;
   }
+  // the start list keeps duplicates, so its edge space is the one frontier not bounded by E:
+  // the device lists carry it in 32 bits
+  for (int32_t t : over) {
+    auto it = E.snap.types.find(t);
+    if (it == E.snap.types.end()) continue;
+    uint64_t sum = 0;
+    for (uint32_t d : f0) sum += std::min<uint64_t>(it->second.h_row_ptr[d + 1] - it->second.h_row_ptr[d], cap);
+    if (sum >= 0xFFFFFFFFull) {
+      delete rows;
+      return E.fail(NBG_E_UNSUPPORTED, "the start list's edges exceed 2^32-1 (duplicated hub starts)");
+    }
+  }
   // final-step row regions: the frontier entering step N is a set (N >= 2) or the start list
   // (N == 1, exact edge count known on the host)
   const uint64_t n_final = rq->steps == 1 ? f0.size() : E.snap.nv;
-  std::vector<uint64_t> region(over.size()), shard_cap(over.size()), ebound(over.size());
+  std::vector<uint64_t> region(over.size()), blk_cap(over.size()), ebound(over.size());
   uint64_t cap_rows = 0;
   for (size_t i = 0; i < over.size(); ++i) {
     auto it = E.snap.types.find(over[i]);
@@ -265,9 +283,9 @@ static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_row
       }
     }
     ebound[i] = eb;
-    shard_cap[i] = ws_shard_cap(n_final, eb);
+    blk_cap[i] = ws_final_blk_cap(n_final, eb);
     region[i] = cap_rows;
-    cap_rows += shard_cap[i] * NSHARD;
+    cap_rows += blk_cap[i] * ws_final_grid(n_final, eb);
   }
   hipError_t he = ws_reserve_rows(ws, cap_rows, ncols);
   if (he == hipSuccess) he = ws_begin_query(ws, f0.data(), f0.size(), &plist);
@@ -283,11 +301,19 @@ static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_row
       } else if (deferred || (plist[i].where_const && !plist[i].where_const_val)) {
         he = ws_scan_only(ws, a, n_bound, (int)s, (int)i);
       } else {
-        he = ws_expand_final(ws, a, n_bound, ebound[i], (int)s, (int)i, plist[i], region[i], shard_cap[i]);
+        he = ws_expand_final(ws, a, n_bound, ebound[i], (int)s, (int)i, plist[i], region[i], blk_cap[i]);
       }
     }
     if (!final && he == hipSuccess) {
-      he = E.partitioned() ? ws_exchange(ws, (int)s) : ws_compact(ws, (int)s);
+      // the next step's first OVER type gets its degree pass fused into the compaction
+      auto it0 = E.snap.types.find(over[0]);
+      ExpandArgs next0{};
+      const ExpandArgs* np0 = nullptr;
+      if (it0 != E.snap.types.end()) {
+        next0 = args_for(it0->second);
+        np0 = &next0;
+      }
+      he = E.partitioned() ? ws_exchange(ws, (int)s, np0) : ws_compact(ws, (int)s, np0);
       n_bound = E.snap.nv;
     }
   }
@@ -318,15 +344,18 @@ static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_row
   if (reached_final && deferred) { delete rows; return E.fail(deferred, deferred_msg); }
   if (g_err) { delete rows; return E.fail(NBG_E_EXECUTION_ERROR, "WHERE/YIELD evaluation error"); }
   for (size_t i = 0; i < over.size(); ++i) {
-    for (int sh = 0; sh < NSHARD; ++sh) {
-      uint64_t c = q.rows[i][sh];
+    rows->kinds.push_back(plist[i].yield_kind);
+    rows->const_str.push_back(plist[i].yield_const_str);
+    const unsigned grid = ws_final_grid_of(ws, (int)i);   // 0: the final expansion did not run
+    const uint32_t* per_block = ws_host_blk_rows(ws, (int)i);
+    for (unsigned b = 0; b < grid; ++b) {
+      uint64_t c = per_block[b];
       if (!c) continue;
       nbg_rows::Seg seg;
-      seg.begin = region[i] + (uint64_t)sh * shard_cap[i];
+      seg.begin = region[i] + (uint64_t)b * blk_cap[i];
       seg.end = seg.begin + c;
-      seg.kinds = plist[i].yield_kind;
-      seg.const_str = plist[i].yield_const_str;
-      rows->segs.push_back(std::move(seg));
+      seg.type = (int)i;
+      rows->segs.push_back(seg);
       rows->count += c;
     }
   }
@@ -427,7 +456,7 @@ int32_t nbg_finalize(nbg_engine* h) {
   int32_t rc = E.finalize();
   if (rc) return rc;
   std::string err;
-  E.ws = ws_create(E.snap.nv + 1024, E.snap.nv, E.stream, &err);
+  E.ws = ws_create(E.snap.nv + 1024, E.snap.nv, E.snap.max_edges(), E.stream, &err);
   if (!E.ws) return E.fail(NBG_E_OUT_OF_MEMORY, err);
   if (E.partitioned()) {
     hipError_t he = ws_set_partition(E.ws, E.comm.get(), E.npad);
@@ -488,6 +517,13 @@ const char* nbg_rows_string(const nbg_rows* r, int64_t id) {
   if (!r || id < 0 || id >= (int64_t)r->strings.size()) return nullptr;
   return r->strings[id].c_str();
 }
+int64_t nbg_rows_num_segments(const nbg_rows* r) { return r ? (int64_t)r->segs.size() : -1; }
+int32_t nbg_rows_segment(const nbg_rows* r, int64_t i, uint64_t* begin, uint64_t* end) {
+  if (!r || i < 0 || i >= (int64_t)r->segs.size() || !begin || !end) return NBG_E_INVALID_ARGUMENT;
+  *begin = r->segs[i].begin;
+  *end = r->segs[i].end;
+  return NBG_OK;
+}
 const void* nbg_rows_device_col(const nbg_rows* r, int32_t col) {
   if (!r || col < 0 || col >= (int32_t)r->dcols.size()) return nullptr;
   return r->dcols[col];
@@ -498,7 +534,7 @@ int32_t nbg_profile(nbg_engine* h, int32_t enable) {
   if (!h) return NBG_E_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> lg(h->e.mu);
   if (!h->e.ws) return h->e.fail(NBG_E_STATE, "engine not finalized");
-  ws_profile(h->e.ws, enable != 0);
+  ws_profile(h->e.ws, enable == 2 ? 2 : (enable != 0 ? 1 : 0));
   return NBG_OK;
 }
 

@@ -5,20 +5,20 @@
 // size) lives in a device-resident QState and grids are sized from host-known upper bounds.
 //
 // Per hop over one edge type (CSR):
-//   k_degree      frontier degrees (row_ptr gathers, capped by max_edge_returned_per_vertex)
-//                 + block-local inclusive scan                       (wave64 shuffles + LDS)
-//   k_scan_blocks exclusive scan of the per-block totals (one workgroup); publishes the total
+//   k_relist      the frontier's entries with edges, their degree prefix, row starts and the
+//                 merge-path split of every tile (one packed atomic per workgroup: no scan pass)
 //   k_expand<M>   persistent, load-balanced expansion over merge-path tiles: a tile owns TILE
-//                 path items (frontier segments + edges) whatever the degree skew, its split is
-//                 found by a wave-wide 64-ary search over the global scan; items are processed striped
-//                 across the block so neighbour / property reads are coalesced.
+//                 path items (frontier entries + edges) whatever the degree skew; its split is
+//                 read from the list, items are processed striped across the workgroup so
+//                 neighbour / property reads are coalesced.
 //                 M = MARK  (steps 1..N-1: set next-frontier byte flags, idempotent plain stores)
 //                 M = FINAL (step N: WHERE/YIELD bytecode per edge, wave-ballot compaction, rows
-//                           appended to one of NSHARD per-shard regions: one atomic per
-//                           tile on a sharded counter, never a single hot word; simple
+//                           appended to the workgroup's own region: no atomics; simple
 //                           `col <cmp> const` / leaf-yield programs skip the interpreter)
-//   k_flag_count / k_scan_blocks / k_flag_write  dense compaction of the byte flags into the
-//                 next (sorted) frontier, clearing the flags in the same pass.
+//   k_compact     the byte flags -> the next frontier list (with the first OVER type's degrees
+//                 and splits, so that type needs no k_relist), clearing the flags.
+// A GO 3 STEPS query over one edge type is 6 launches: relist, MARK, compact, MARK, compact,
+// FINAL.
 // Semantics follow QueryBaseProcessor::collectEdgeProps (version de-dup is done at load,
 // neighbours are in memcmp key order, the cap counts edges in that order) and
 // GoExecutor::getDstIdsFromResp (per-step dst SET, no global visited set).
@@ -34,22 +34,19 @@ namespace nbg {
 
 constexpr int BLOCK = 256;
 constexpr int WAVES = BLOCK / 64;
-constexpr int SCAN_ITEMS = 8;                    // k_degree: items per thread
-constexpr int SCAN_TILE = BLOCK * SCAN_ITEMS;    // 2048 frontier entries per block
-constexpr int SCAN_SHIFT = 11;
-constexpr int FLAG_BYTES = BLOCK * 16;           // k_flag_*: bytes per block
+constexpr int FLAG_ALIGN = 1024 * 16;           // flag array granularity (k_compact workgroup)
 constexpr int EXPAND_GRID = 2048;                // persistent k_expand grid (8 blocks / CU)
 
-enum KernelId { K_DEGREE = 0, K_SCAN, K_EXPAND_MARK, K_FLAG_COUNT, K_FLAG_WRITE, K_EXPAND_FINAL, K_BFS,
-                K_GATHER, K_DEGSUM, K_GREEDY, K_STAMP, K_PACK, K_ALLTOALL, K_BITS_COUNT, K_BITS_WRITE, K_COUNT };
-static const char* const kKernelNames[K_COUNT] = {"k_degree", "k_scan_blocks", "k_expand<MARK>", "k_flag_count",
-                                                  "k_flag_write", "k_expand<FINAL>", "k_expand<BFS>", "k_gather",
-                                                  "k_degsum", "k_path_greedy", "k_stamp", "k_pack_bits",
-                                                  "alltoall(xGMI)", "k_bits_count", "k_bits_write"};
-constexpr int BITS_BLOCK = BLOCK * 64;           // k_bits_*: vertices (bits) per block
+enum KernelId { K_RELIST = 0, K_EXPAND_MARK, K_COMPACT, K_EXPAND_FINAL, K_BFS, K_GATHER, K_DEGSUM, K_GREEDY,
+                K_STAMP, K_PACK, K_ALLTOALL, K_BITS_COMPACT, K_COUNT };
+static const char* const kKernelNames[K_COUNT] = {"k_relist", "k_expand<MARK>", "k_compact", "k_expand<FINAL>",
+                                                  "k_expand<BFS>", "k_gather", "k_degsum", "k_path_greedy",
+                                                  "k_stamp", "k_pack_bits", "alltoall(xGMI)", "k_bits_compact"};
+constexpr int BITS_BLOCK = BLOCK * 16;           // k_bits_compact: vertices (bits) per block
 
 struct Prof {
   bool on = false;
+  uint32_t mask = ~0u;     // kernels timed (bit per KernelId)
   struct Rec { int kid, step, tix; hipEvent_t a, b; double cols, kout; bool path; };
   std::vector<Rec> pending;
   std::vector<hipEvent_t> pool;
@@ -73,11 +70,17 @@ struct Workspace {
   int cur = 0;
   uint32_t* seg_end = nullptr;    // block-local inclusive scan of degrees
   uint32_t* seg_rs = nullptr;     // row start per frontier entry
-  uint32_t* block_sum = nullptr;  // per-block totals -> exclusive prefix (in place)
-  uint64_t cap_blocks = 0;
-  uint8_t* flags = nullptr;       // [nv rounded up to FLAG_BYTES], kept all-zero between steps
+  uint32_t* rlist = nullptr;      // k_relist output list
+  uint8_t* flags = nullptr;       // [nv rounded up to FLAG_ALIGN], kept all-zero between steps
   uint64_t flag_bytes = 0;
-  uint32_t* flag_blocks = nullptr;
+  uint32_t* tsplit = nullptr;      // [cap_tiles] merge-path split per tile (compaction-produced frontiers)
+  uint32_t* blk_rows = nullptr;    // [MAX_TYPES_Q][EXPAND_GRID] final-step rows per workgroup
+  uint32_t* h_blk_rows = nullptr;  // pinned mirror (valid after ws_end_query)
+  unsigned final_grid[MAX_TYPES_Q] = {};
+  uint64_t cap_tiles = 0;
+  bool seg_ready = false;          // the compaction list carries the first OVER type's edge space
+  const unsigned long long* list_acc = nullptr;   // packed size of frontier[cur] (null: q->n, plain)
+  int pr = 0, pc = 0;              // ping-pong parity of the relist / compaction accumulators
   QState* q = nullptr;            // device query state
   QState* h_q = nullptr;          // pinned host mirror
   uint32_t* h_starts = nullptr;   // pinned staging for start ids
@@ -101,13 +104,13 @@ struct Workspace {
   int64_t* h_path = nullptr;
   uint32_t* h_stage = nullptr;    // pinned [PSLOTS][STAGE] upload staging (one upload per slot per query)
   int rec = 0;                    // next PState expansion record
+  int ppr = 0;                    // ping-pong parity of the path relist accumulators
   // partitioned mode: flags cover the global id space [world * npad), one
   // bitmap segment of npad bits per owner rank is exchanged per hop
   Comm* comm = nullptr;
   uint64_t npad = 0;
   unsigned long long* sendbits = nullptr;   // [world * npad / 64]
   unsigned long long* recvbits = nullptr;   // [world * npad / 64]
-  unsigned long long* mbits = nullptr;      // [npad / 64] OR of the received segments
   unsigned long long* gst = nullptr;        // [GST_N] globally reduced query statistics
   unsigned long long* h_gst = nullptr;
 };
@@ -123,7 +126,8 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
-// Exclusive block scan of one value per thread; *total gets the block sum.
+// Exclusive scan of one value per thread over an NT-thread block; *total gets the block sum.
+template <int NT = BLOCK>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* total, uint32_t* lds) {
   uint32_t inc = wave_incl_scan(v);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -131,7 +135,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* total,
   __syncthreads();
   uint32_t pre = 0, tot = 0;
 #pragma unroll
-  for (int i = 0; i < WAVES; ++i) {
+  for (int i = 0; i < NT / 64; ++i) {
     uint32_t s = lds[i];
     pre += (i < w) ? s : 0u;
     tot += s;
@@ -141,122 +145,134 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* total,
   return pre + inc - v;
 }
 
-// ----------------------------------------------------------------------------- k_degree
-// `reset` (nullable): NSHARD counters zeroed by block 0 (the BFS claim shards of the previous
-// expansion, consumed by k_gather before this launch in stream order).
-__global__ void __launch_bounds__(BLOCK) k_degree(const uint32_t* __restrict__ frontier,
-                                                  const unsigned long long* __restrict__ np,
-                                                  const uint32_t* __restrict__ row_ptr,
-                                                  const uint8_t* __restrict__ visible, uint32_t cap,
-                                                  uint32_t* __restrict__ seg_end, uint32_t* __restrict__ seg_rs,
-                                                  uint32_t* __restrict__ block_sum, unsigned long long* reset,
-                                                  unsigned long long* n_rec) {
-  __shared__ uint32_t lds[WAVES];
-  const uint64_t n = *np;
-  if (blockIdx.x == 0) {
-    if (reset && threadIdx.x < NSHARD) reset[threadIdx.x] = 0;
-    if (n_rec && threadIdx.x == 0) *n_rec = n;
-  }
-  if ((uint64_t)blockIdx.x * SCAN_TILE >= n) return;
-  const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
-  uint32_t deg[SCAN_ITEMS], rs[SCAN_ITEMS];
-  uint32_t sum = 0;
-#pragma unroll
-  for (int k = 0; k < SCAN_ITEMS; ++k) {
-    uint64_t i = base + k;
-    uint32_t d = 0, r = 0;
-    if (i < n) {
-      uint32_t v = frontier[i];
-      if (v != NO_ROW && (!visible || visible[v])) {
-        r = row_ptr[v];
-        d = row_ptr[v + 1] - r;
-        d = d < cap ? d : cap;
-      }
-    }
-    deg[k] = d;
-    rs[k] = r;
-    sum += d;
-  }
-  uint32_t total;
-  uint32_t pre = block_excl_scan(sum, &total, lds);
-#pragma unroll
-  for (int k = 0; k < SCAN_ITEMS; ++k) {
-    uint64_t i = base + k;
-    pre += deg[k];
-    if (i < n) {
-      seg_end[i] = pre;   // inclusive, block-local
-      seg_rs[i] = rs[k];
-    }
-  }
-  if (threadIdx.x == 0) block_sum[blockIdx.x] = total;
+// ----------------------------------------------------------------------------- frontier lists
+// Every frontier list an expansion consumes is produced together with its edge space: entry i
+// owns edges [seg_end[i] - deg_i, seg_end[i]) (deg capped by max_edge_returned_per_vertex), row
+// start seg_rs[i], and the merge-path split of every TILE boundary it covers (tsplit).  List
+// positions and edge offsets are handed out per workgroup by ONE 64-bit atomicAdd on a packed
+// accumulator (count << 32 | degree sum): no separate scan pass, no fences, no grid barrier.
+// Lists are therefore in workgroup-arrival order (id order inside a workgroup); frontier order
+// is irrelevant to GoExecutor's semantics (a per-step SET, GoExecutor.cpp:501-541).
+// The degree sum fits the low word: a step's frontier is a set (Σ deg <= E < 2^32 per type) and
+// the host checks the start list (which keeps duplicates) before launching.
+struct DegSrc {                    // the CSR whose degrees the list carries (row_ptr null: none)
+  const uint32_t* row_ptr;
+  const uint8_t* visible;
+  uint32_t cap;
+};
+
+struct ListOut {
+  uint32_t* ids;
+  uint32_t* seg_end;               // inclusive degree prefix (global)
+  uint32_t* seg_rs;                // row start
+  uint32_t* tsplit;                // merge-path split per tile
+  unsigned long long* acc;         // packed (entries << 32 | edges); zero before the launch
+  unsigned long long* zero_next;   // the other accumulator of the ping-pong pair, zeroed here
+  unsigned long long* stat_n;      // frontier size of this step (input count), nullable
+};
+
+__device__ __forceinline__ uint32_t vdeg(const DegSrc& ds, uint32_t v, uint32_t* rs) {
+  if (!ds.row_ptr || v == NO_ROW || (ds.visible && !ds.visible[v])) { *rs = 0; return 0; }
+  const uint32_t r = ds.row_ptr[v];
+  const uint32_t d = ds.row_ptr[v + 1] - r;
+  *rs = r;
+  return d < ds.cap ? d : ds.cap;
 }
 
-// One workgroup: exclusive scan of nb uint32 in place.  nb = fixed_nb, or ceil(*np / 2048) when
-// fixed_nb == 0.  The grand total goes to *total_out and is added to *accum (stats, nullable).
-__global__ void __launch_bounds__(1024) k_scan_blocks(uint32_t* __restrict__ v, const unsigned long long* np,
-                                                      uint64_t fixed_nb, unsigned long long* total_out,
-                                                      unsigned long long* accum) {
-  __shared__ uint64_t lds[16];
-  __shared__ uint64_t carry;
-  const uint64_t nb = fixed_nb ? fixed_nb : (*np + SCAN_TILE - 1) / SCAN_TILE;
-  if (threadIdx.x == 0) carry = 0;
+// Entry i owns merge-path positions [i + start_i, i + end_i] (its edges, then its terminator);
+// the split of tile t (entries consumed before position t * TILE) is the entry whose range holds
+// t * TILE, so each entry records the tile boundaries it covers and k_expand reads its split.
+__device__ __forceinline__ void record_splits(uint32_t* tsplit, uint32_t i, uint32_t end_incl, uint32_t deg) {
+  const uint64_t lo = (uint64_t)i + end_incl - deg, hi = (uint64_t)i + end_incl;
+  for (uint64_t t = (lo + TILE - 1) / TILE; t * TILE <= hi; ++t) tsplit[t] = i;
+}
+
+// Block-wide reservation: exclusive per-thread offsets (*pc list position, *pd edge offset).
+template <int NT>
+__device__ __forceinline__ void reserve(uint32_t c, uint32_t d, unsigned long long* acc, uint32_t* pc, uint32_t* pd) {
+  __shared__ uint32_t lds[NT / 64];
+  __shared__ unsigned long long s_old;
+  uint32_t tc, td;
+  const uint32_t xc = block_excl_scan<NT>(c, &tc, lds);
+  const uint32_t xd = block_excl_scan<NT>(d, &td, lds);
+  if (threadIdx.x == 0) s_old = (tc | td) ? atomicAdd(acc, ((unsigned long long)tc << 32) | td) : 0ull;
   __syncthreads();
-  for (uint64_t base = 0; base < nb; base += 1024) {
-    uint64_t i = base + threadIdx.x;
-    uint64_t x = i < nb ? v[i] : 0;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint64_t inc = x;
-    for (int o = 1; o < 64; o <<= 1) {
-      uint64_t t = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += t;
-    }
-    if (lane == 63) lds[w] = inc;
-    __syncthreads();
-    uint64_t pre = 0, tot = 0;
-    for (int k = 0; k < 16; ++k) {
-      pre += (k < w) ? lds[k] : 0;
-      tot += lds[k];
-    }
-    uint64_t c = carry;
-    if (i < nb) v[i] = (uint32_t)(c + pre + inc - x);
-    __syncthreads();
-    if (threadIdx.x == 0) carry = c + tot;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    *total_out = carry;
-    if (accum) *accum += carry;
+  *pc = (uint32_t)(s_old >> 32) + xc;
+  *pd = (uint32_t)s_old + xd;
+}
+
+__device__ __forceinline__ void list_put(const ListOut& o, const DegSrc& ds, uint32_t pos, uint32_t v, uint32_t* pd,
+                                         uint32_t dg, uint32_t rs) {
+  o.ids[pos] = v;
+  if (ds.row_ptr) {
+    *pd += dg;
+    o.seg_end[pos] = *pd;
+    o.seg_rs[pos] = rs;
+    record_splits(o.tsplit, pos, *pd, dg);
   }
 }
 
-__device__ __forceinline__ uint32_t seg_end_at(const uint32_t* __restrict__ seg_end,
-                                               const uint32_t* __restrict__ block_pre, uint64_t i) {
-  return seg_end[i] + block_pre[i >> SCAN_SHIFT];
+// k_relist: a list (start ids, an earlier list, a FIND PATH frontier) -> the list of its entries
+// with edges over one CSR.  Entries without edges are dropped (they expand to nothing).
+constexpr int RL_ITEMS = 8;
+constexpr int RL_TILE = BLOCK * RL_ITEMS;
+__global__ void __launch_bounds__(BLOCK) k_relist(const uint32_t* __restrict__ in, const unsigned long long* in_n,
+                                                  int in_packed, DegSrc ds, ListOut o, unsigned long long* reset) {
+  const uint64_t n = in_packed ? (*in_n >> 32) : *in_n;
+  if (blockIdx.x == 0) {
+    if (threadIdx.x == 0) {
+      *o.zero_next = 0;
+      if (o.stat_n) *o.stat_n = n;
+    }
+    if (reset && threadIdx.x < NSHARD) reset[threadIdx.x] = 0;   // BFS claim counters of the last level
+  }
+  const uint64_t base = (uint64_t)blockIdx.x * RL_TILE + (uint64_t)threadIdx.x * RL_ITEMS;
+  if ((uint64_t)blockIdx.x * RL_TILE >= n) return;
+  uint32_t v[RL_ITEMS], dg[RL_ITEMS], rs[RL_ITEMS];
+  uint32_t c = 0, d = 0;
+#pragma unroll
+  for (int k = 0; k < RL_ITEMS; ++k) {
+    v[k] = base + k < n ? in[base + k] : NO_ROW;
+    dg[k] = vdeg(ds, v[k], &rs[k]);
+    c += dg[k] ? 1u : 0u;
+    d += dg[k];
+  }
+  uint32_t pc, pd;
+  reserve<BLOCK>(c, d, o.acc, &pc, &pd);
+#pragma unroll
+  for (int k = 0; k < RL_ITEMS; ++k)
+    if (dg[k]) list_put(o, ds, pc++, v[k], &pd, dg[k], rs[k]);
 }
 
-// Merge-path split: number of frontier segments fully consumed in the first d path items, i.e.
-// the smallest i with NOT(end(i) <= d-1-i).  Computed by one whole wave as a 64-ary search:
-// each round the 64 lanes probe 64 evenly spaced candidates in parallel (one memory round trip)
-// and a ballot narrows the range 64x, so a split costs ceil(log64(n)) <= 5 round trips instead
-// of ~25 dependent loads of a binary search.
-__device__ __forceinline__ uint64_t wave_merge_split(const uint32_t* __restrict__ seg_end,
-                                                     const uint32_t* __restrict__ block_pre, uint64_t n,
-                                                     uint64_t total, uint64_t d) {
-  const int lane = threadIdx.x & 63;
-  uint64_t lo = d > total ? d - total : 0;
-  uint64_t hi = d < n ? d : n;
-  while (lo < hi) {
-    const uint64_t step = (hi - lo + 63) >> 6;
-    const uint64_t p = lo + (uint64_t)lane * step;
-    bool t = p < hi && (uint64_t)seg_end_at(seg_end, block_pre, p) <= d - 1 - p;
-    const int c = __popcll(__ballot(t));
-    const uint64_t nlo = c > 0 ? lo + (uint64_t)(c - 1) * step + 1 : lo;
-    uint64_t nhi = lo + (uint64_t)c * step;
-    if (nhi > hi) nhi = hi;
-    lo = nlo;
-    hi = nhi;
+// k_compact: next frontier = the byte flags set by k_expand<MARK> (the per-step dst SET),
+// listed with the degrees of the next step's first OVER type; clears the flags.  Every flagged
+// vertex is kept (this list is the frontier for every OVER type).  16 flag bytes per thread,
+// their degree gathers all in flight at once.
+constexpr int CP_THREADS = 1024;
+constexpr int CP_BYTES = CP_THREADS * 16;        // flag bytes per workgroup
+__global__ void __launch_bounds__(CP_THREADS) k_compact(uint8_t* __restrict__ flags, DegSrc ds, ListOut o) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *o.zero_next = 0;
+  const uint64_t off = (uint64_t)blockIdx.x * CP_BYTES + (uint64_t)threadIdx.x * 16;
+  uint4* p = reinterpret_cast<uint4*>(flags + off);
+  const uint4 q = *p;
+  const uint32_t ws[4] = {q.x, q.y, q.z, q.w};
+  uint32_t c = 0, d = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) c += __popc(ws[j] & 0x01010101u);
+  uint32_t dg[16], rs[16];
+#pragma unroll
+  for (int b = 0; b < 16; ++b) {
+    const bool set = (ws[b >> 2] >> ((b & 3) * 8)) & 1u;
+    dg[b] = set ? vdeg(ds, (uint32_t)(off + b), &rs[b]) : 0u;
+    d += dg[b];
   }
-  return lo;
+  uint32_t pc, pd;
+  reserve<CP_THREADS>(c, d, o.acc, &pc, &pd);
+  if (!c) return;
+#pragma unroll
+  for (int b = 0; b < 16; ++b)
+    if ((ws[b >> 2] >> ((b & 3) * 8)) & 1u) list_put(o, ds, pc++, (uint32_t)(off + b), &pd, dg[b], rs[b]);
+  *p = make_uint4(0, 0, 0, 0);
 }
 
 // Fast path for the common final-step program shape: WHERE absent or `col <cmp> const` on an
@@ -269,6 +285,7 @@ struct FastProg {
   int64_t where_const;
   int ykind[MAX_YIELDS];   // 0 DST, 1 SRC, 2 RANK, 3 COL, 4 CONST
   int ycol[MAX_YIELDS];
+  int dst_yield;           // some YIELD is _dst
 };
 
 __device__ __forceinline__ bool cmp_i(int op, int64_t x, int64_t y) {
@@ -363,7 +380,8 @@ __device__ __forceinline__ void run_program(const Ins* __restrict__ prog, int pc
 }
 
 // ----------------------------------------------------------------------------- k_expand
-enum Mode { MARK = 0, FINAL = 1, BFS = 2 };
+// FINALF: the final step with a FastProg program (no interpreter: fewer registers, 8 waves/SIMD)
+enum Mode { MARK = 0, FINAL = 1, BFS = 2, FINALF = 3 };
 
 // BFS-mode expansion (FIND SHORTEST PATH): every neighbour w is claimed at most once per epoch by
 // a CAS on its label (epoch << LVL_BITS | level); winners are appended, one atomic per tile on a
@@ -398,41 +416,46 @@ struct FinalParams {
   int64_t yield_const[MAX_YIELDS];
   int64_t** out_cols;
   uint64_t region_base;   // first row of this type's region
-  uint64_t shard_cap;     // rows per shard region
-  unsigned long long* shard_rows;   // [NSHARD] counters of this type
+  uint64_t blk_cap;       // rows per workgroup region (each workgroup appends to its own region)
+  uint32_t* blk_rows;     // [gridDim.x] rows written per workgroup
   unsigned long long* err_flag;
   FastProg fast;
 };
 
 template <int M>
-__global__ void __launch_bounds__(BLOCK) k_expand(ExpandArgs a, const unsigned long long* __restrict__ np,
-                                                  const unsigned long long* __restrict__ totp,
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M == FINAL ? 4 : 8))) k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc,
                                                   const uint32_t* __restrict__ seg_end,
-                                                  const uint32_t* __restrict__ block_pre,
                                                   const uint32_t* __restrict__ seg_rs, uint8_t* __restrict__ flags,
-                                                  FinalParams fp, BfsParams bp) {
+                                                  FinalParams fp, BfsParams bp, unsigned long long* stat_e,
+                                                  unsigned long long* stat_n) {
   __shared__ uint32_t sEnd[TILE + 2];   // seg_end for i in [a0-1, a1]
   __shared__ uint32_t sRs[TILE + 1];    // seg_rs for i in [a0, a1]
   __shared__ uint32_t sSeg[TILE];       // segment of each edge item in this tile
   __shared__ uint32_t sCnt[VT * WAVES]; // FINAL: passing items per (iteration, wave) -> offsets
   __shared__ uint64_t sSplit[2];
-  __shared__ uint64_t sBase;
+  __shared__ uint64_t sBase;            // BFS: claim base; FINAL: rows this workgroup wrote so far
+  __shared__ uint64_t sTileBase;        // FINAL: first row of the current tile in the region
   extern __shared__ int64_t regs[];     // FINAL generic path: [nregs][BLOCK]
 
-  const uint64_t n = *np;
-  const uint64_t total = *totp;
+  const unsigned long long packed = *acc;  // (list entries << 32 | edges) of the list a.frontier
+  const uint64_t n = packed >> 32;
+  const uint64_t total = packed & 0xFFFFFFFFull;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (stat_e) *stat_e += total;
+    if (stat_n) *stat_n = n;
+  }
   const uint64_t npath = n + total;
   const uint64_t ntiles = (npath + TILE - 1) / TILE;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   bool anyErr = false;
+  constexpr bool kFinal = M == FINAL || M == FINALF;
+  constexpr bool kFast = M == FINALF;
+  if (kFinal && threadIdx.x == 0) sBase = 0;
 
   for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const uint64_t d0 = t * TILE;
     const uint64_t d1 = (d0 + TILE < npath) ? d0 + TILE : npath;
-    if (w < 2) {
-      uint64_t sp = wave_merge_split(seg_end, block_pre, n, total, w ? d1 : d0);
-      if (lane == 0) sSplit[w] = sp;
-    }
+    if (threadIdx.x < 2) sSplit[threadIdx.x] = threadIdx.x == 0 ? a.tsplit[t] : (d1 == npath ? n : a.tsplit[t + 1]);
     __syncthreads();
     const uint64_t a0 = sSplit[0], a1 = sSplit[1];
     const uint64_t b0 = d0 - a0, b1 = d1 - a1;
@@ -441,7 +464,7 @@ __global__ void __launch_bounds__(BLOCK) k_expand(ExpandArgs a, const unsigned l
     // stage the tile's segment ends / row starts in LDS
     for (int k = threadIdx.x; k <= na + 1; k += BLOCK) {
       int64_t i = (int64_t)a0 - 1 + k;
-      sEnd[k] = (i < 0) ? 0u : (i < (int64_t)n ? seg_end_at(seg_end, block_pre, (uint64_t)i) : 0xFFFFFFFFu);
+      sEnd[k] = (i < 0) ? 0u : (i < (int64_t)n ? seg_end[i] : 0xFFFFFFFFu);
     }
     for (int k = threadIdx.x; k <= na; k += BLOCK) {
       uint64_t i = a0 + k;
@@ -547,6 +570,7 @@ __global__ void __launch_bounds__(BLOCK) k_expand(ExpandArgs a, const unsigned l
       // phase A: WHERE for every item of the tile (VT items per thread, striped)
       uint64_t jj[VT];
       uint32_t vv[VT];
+      int64_t dv[VT];       // fast path: _dst prefetched with the WHERE column (one round trip)
       uint32_t pmask = 0;
 #pragma unroll
       for (int i = 0; i < VT; ++i) {
@@ -559,7 +583,11 @@ __global__ void __launch_bounds__(BLOCK) k_expand(ExpandArgs a, const unsigned l
           vv[i] = s;
         }
       }
-      if (fp.fast.enabled) {
+      if (kFast) {
+        if (fp.fast.dst_yield) {
+#pragma unroll
+          for (int i = 0; i < VT; ++i) dv[i] = (i * BLOCK + (int)threadIdx.x < nb) ? a.dst_vid[jj[i]] : 0;
+        }
         if (fp.fast.where_col < 0) {
 #pragma unroll
           for (int i = 0; i < VT; ++i) pmask |= (uint32_t)(i * BLOCK + (int)threadIdx.x < nb) << i;
@@ -588,14 +616,14 @@ __global__ void __launch_bounds__(BLOCK) k_expand(ExpandArgs a, const unsigned l
           pmask |= (uint32_t)pass << i;
         }
       }
-      // one atomic per tile on a sharded counter: offsets for (iteration, wave) in item order
+      // offsets for (iteration, wave) in item order; rows are appended to this workgroup's own
+      // region (no atomics: a cursor in LDS), so a tile never waits on a global round trip
 #pragma unroll
       for (int i = 0; i < VT; ++i) {
         unsigned long long bal = __ballot((pmask >> i) & 1u);
         if (lane == 0) sCnt[i * WAVES + w] = (uint32_t)__popcll(bal);
       }
       __syncthreads();
-      const uint64_t shard = t % NSHARD;
       if (threadIdx.x == 0) {
         uint32_t run = 0;
         for (int k = 0; k < VT * WAVES; ++k) {
@@ -603,29 +631,34 @@ __global__ void __launch_bounds__(BLOCK) k_expand(ExpandArgs a, const unsigned l
           sCnt[k] = run;
           run += c;
         }
-        sBase = run ? atomicAdd(fp.shard_rows + shard, (unsigned long long)run) : 0ull;
+        sTileBase = sBase;
+        sBase += run;
       }
       __syncthreads();
       // phase B: YIELD for the passing items, written at their final rows
-      const uint64_t region = fp.region_base + shard * fp.shard_cap + sBase;
+      const uint64_t region = fp.region_base + (uint64_t)blockIdx.x * fp.blk_cap + sTileBase;
       int64_t* const* cols = fp.out_cols;
       for (int i = 0; i < VT; ++i) {
         const bool pass = (pmask >> i) & 1u;
         unsigned long long bal = __ballot(pass);
         if (!bal) continue;
         const uint64_t row = region + sCnt[i * WAVES + w] + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-        if (fp.fast.enabled) {
+        if (kFast) {
           if (pass) {
             for (int y = 0; y < fp.nyields; ++y) {
               int64_t val;
               switch (fp.fast.ykind[y]) {
-                case 0: val = a.dst_vid[jj[i]]; break;
+                case 0: val = dv[i]; break;
                 case 1: val = a.vids[a.frontier[a0 + vv[i]]]; break;
                 case 2: val = a.rank ? a.rank[jj[i]] : 0; break;
                 case 3: val = a.props[fp.fast.ycol[y]][jj[i]]; break;
                 default: val = fp.yield_const[y]; break;
               }
+#ifndef NBG_EXP_NOSTORE   // timing experiment only
               cols[y][row] = val;
+#else
+              if (val == 0x7eadbeefLL) cols[y][row] = val;
+#endif
             }
           }
         } else {
@@ -644,50 +677,9 @@ __global__ void __launch_bounds__(BLOCK) k_expand(ExpandArgs a, const unsigned l
     }
     __syncthreads();   // LDS reuse by the next tile
   }
-  if (M == FINAL && anyErr) atomicOr(fp.err_flag, 1ull);
-}
-
-// ----------------------------------------------------------------------------- flag compaction
-__global__ void __launch_bounds__(BLOCK) k_flag_count(const uint8_t* __restrict__ flags, uint64_t nbytes,
-                                                      uint32_t* __restrict__ block_cnt) {
-  __shared__ uint32_t lds[WAVES];
-  uint64_t off = (uint64_t)blockIdx.x * FLAG_BYTES + threadIdx.x * 16;
-  uint32_t c = 0;
-  if (off < nbytes) {
-    uint4 q = *reinterpret_cast<const uint4*>(flags + off);
-    uint32_t ws[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) c += __popc(ws[i] & 0x01010101u);
-  }
-  uint32_t tot;
-  block_excl_scan(c, &tot, lds);
-  if (threadIdx.x == 0) block_cnt[blockIdx.x] = tot;
-}
-
-__global__ void __launch_bounds__(BLOCK) k_flag_write(uint8_t* __restrict__ flags, uint64_t nbytes, uint64_t nv,
-                                                      const uint32_t* __restrict__ block_pre,
-                                                      uint32_t* __restrict__ out) {
-  __shared__ uint32_t lds[WAVES];
-  uint64_t off = (uint64_t)blockIdx.x * FLAG_BYTES + threadIdx.x * 16;
-  uint32_t ws[4] = {0, 0, 0, 0};
-  uint32_t c = 0;
-  if (off < nbytes) {
-    uint4 q = *reinterpret_cast<const uint4*>(flags + off);
-    ws[0] = q.x; ws[1] = q.y; ws[2] = q.z; ws[3] = q.w;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) c += __popc(ws[i] & 0x01010101u);
-  }
-  uint32_t tot;
-  uint32_t pre = block_excl_scan(c, &tot, lds) + block_pre[blockIdx.x];
-  if (c) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      if ((ws[i >> 2] >> ((i & 3) * 8)) & 1u) {
-        uint64_t v = off + i;
-        if (v < nv) out[pre++] = (uint32_t)v;
-      }
-    }
-    *reinterpret_cast<uint4*>(flags + off) = make_uint4(0, 0, 0, 0);
+  if (kFinal) {
+    if (threadIdx.x == 0) fp.blk_rows[blockIdx.x] = (uint32_t)sBase;
+    if (anyErr) atomicOr(fp.err_flag, 1ull);
   }
 }
 
@@ -720,37 +712,39 @@ __global__ void __launch_bounds__(BLOCK) k_pack_bits(uint8_t* __restrict__ flags
 }
 
 // Owner side: OR the G received segments (one per sending rank) of this rank's id range; the
-// union is the global per-step dst SET restricted to the owner (getDstIdsFromResp).
-__global__ void __launch_bounds__(BLOCK) k_bits_count(const unsigned long long* __restrict__ recv, int world,
-                                                      uint64_t seg_words, uint64_t nv,
-                                                      unsigned long long* __restrict__ merged,
-                                                      uint32_t* __restrict__ block_cnt) {
-  __shared__ uint32_t lds[WAVES];
-  const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-  unsigned long long m = 0;
-  for (int q = 0; q < world; ++q) m |= recv[(uint64_t)q * seg_words + i];
-  const uint64_t lo = i * 64;
+// union is the global per-step dst SET restricted to the owner (getDstIdsFromResp).  Listed as
+// k_compact does: 16 vertices (bits) per thread.
+__global__ void __launch_bounds__(BLOCK) k_bits_compact(const unsigned long long* __restrict__ recv, int world,
+                                                        uint64_t seg_words, uint64_t nv, DegSrc ds, ListOut o) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *o.zero_next = 0;
+  const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;   // 16-bit slice index
+  const uint64_t word = i >> 2;
+  const int sh = (int)(i & 3) * 16;
+  unsigned long long m64 = 0;
+  for (int q = 0; q < world; ++q) m64 |= recv[(uint64_t)q * seg_words + word];
+  uint32_t m = (uint32_t)(m64 >> sh) & 0xFFFFu;
+  const uint64_t lo = i * 16;
   if (lo >= nv) m = 0;
-  else if (nv - lo < 64) m &= (1ull << (nv - lo)) - 1ull;
-  merged[i] = m;
-  uint32_t tot;
-  block_excl_scan((uint32_t)__popcll(m), &tot, lds);
-  if (threadIdx.x == 0) block_cnt[blockIdx.x] = tot;
+  else if (nv - lo < 16) m &= (1u << (nv - lo)) - 1u;
+  uint32_t dg[16], rs[16], d = 0;
+#pragma unroll
+  for (int b = 0; b < 16; ++b) {
+    dg[b] = ((m >> b) & 1u) ? vdeg(ds, (uint32_t)(lo + b), &rs[b]) : 0u;
+    d += dg[b];
+  }
+  uint32_t pc, pd;
+  reserve<BLOCK>((uint32_t)__popc(m), d, o.acc, &pc, &pd);
+#pragma unroll
+  for (int b = 0; b < 16; ++b)
+    if ((m >> b) & 1u) list_put(o, ds, pc++, (uint32_t)(lo + b), &pd, dg[b], rs[b]);
 }
 
-__global__ void __launch_bounds__(BLOCK) k_bits_write(const unsigned long long* __restrict__ merged,
-                                                      const uint32_t* __restrict__ block_pre,
-                                                      uint32_t* __restrict__ out) {
-  __shared__ uint32_t lds[WAVES];
-  const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-  unsigned long long m = merged[i];
-  uint32_t tot;
-  uint32_t pre = block_excl_scan((uint32_t)__popcll(m), &tot, lds) + block_pre[blockIdx.x];
-  while (m) {
-    const int b = __ffsll((long long)m) - 1;
-    out[pre++] = (uint32_t)(i * 64 + b);
-    m &= m - 1;
-  }
+// Stats of an expansion that is not launched (final step whose WHERE folded to false).
+__global__ void k_note(const unsigned long long* __restrict__ acc, unsigned long long* stat_e,
+                       unsigned long long* stat_n) {
+  const unsigned long long v = *acc;
+  *stat_e += v & 0xFFFFFFFFull;
+  if (stat_n) *stat_n = v >> 32;
 }
 
 // Query statistics every rank needs globally: [err, step_n[0..MAX_STEPS+1], Σ_types e_st[s]].
@@ -766,6 +760,19 @@ __global__ void k_gstats(const QState* __restrict__ q, int ntypes, unsigned long
   }
 }
 
+// ----------------------------------------------------------------------------- row packing
+// Gathers the segments of a GO result (one per producing workgroup and type) into contiguous
+// columns: segment k = rows [seg[3k], seg[3k] + seg[3k+1]) of every column, written at seg[3k+2].
+__global__ void __launch_bounds__(BLOCK) k_pack_rows(const uint64_t* __restrict__ seg, int nseg,
+                                                     int64_t* const* __restrict__ cols, int ncols,
+                                                     int64_t* __restrict__ out, uint64_t total) {
+  for (int k = blockIdx.x; k < nseg; k += gridDim.x) {
+    const uint64_t b = seg[3 * k], len = seg[3 * k + 1], o = seg[3 * k + 2];
+    for (int c = 0; c < ncols; ++c)
+      for (uint64_t i = threadIdx.x; i < len; i += BLOCK) out[(uint64_t)c * total + o + i] = cols[c][b + i];
+  }
+}
+
 // ============================================================================= host side
 static inline uint64_t cdiv(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
@@ -777,8 +784,8 @@ static inline uint64_t cdiv(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
 // Kernel timing: an event pair around each launch on the workspace stream, resolved after the
 // query's single host synchronisation (byte counts need the device-side sizes).
-static hipEvent_t prof_begin(Workspace* w) {
-  if (!w->prof.on) return nullptr;
+static hipEvent_t prof_begin(Workspace* w, int kid) {
+  if (!w->prof.on || !((w->prof.mask >> kid) & 1u)) return nullptr;
   hipEvent_t a = w->prof.get();
   (void)hipEventRecord(a, w->stream);
   return a;
@@ -790,16 +797,16 @@ static void prof_end(Workspace* w, hipEvent_t a, int kid, int step, int tix, dou
   w->prof.pending.push_back({kid, step, tix, a, b, cols, kout, false});
 }
 // algorithmic bytes per kernel (SURVEY.md §8(d) B_GO terms)
-static double prof_bytes(const Prof::Rec& r, const QState& q) {
+static double prof_bytes(const Workspace* w, const Prof::Rec& r, const QState& q) {
   switch (r.kid) {
-    case K_DEGREE: return 12.0 * (double)q.step_n[r.step];                 // 4|F| ids + 8|F| row_ptr
+    case K_RELIST: return 12.0 * (double)q.step_n[r.step];                 // 4|F| ids + 8|F| row_ptr
     case K_EXPAND_MARK: return 4.0 * (double)q.e_st[r.step][r.tix];        // 4 E_s neighbour ids
-    case K_FLAG_WRITE: return 4.0 * (double)q.step_n[r.step + 1];          // write F_{s+1}
-    case K_BITS_WRITE: return 4.0 * (double)q.step_n[r.step + 1];
-    case K_PACK: case K_ALLTOALL: case K_BITS_COUNT: return r.cols;       // fixed sizes (set at launch)
+    // next frontier: 4|F_{s+1}| ids written + the fused degree pass of the next step (12|F_{s+1}|)
+    case K_COMPACT: case K_BITS_COMPACT: return 16.0 * (double)q.step_n[r.step + 1];
+    case K_PACK: case K_ALLTOALL: return r.cols;                           // fixed sizes (set at launch)
     case K_EXPAND_FINAL: {
       double rows = 0;
-      for (int s = 0; s < NSHARD; ++s) rows += (double)q.rows[r.tix][s];
+      for (unsigned b = 0; b < w->final_grid[r.tix]; ++b) rows += (double)w->h_blk_rows[(size_t)r.tix * EXPAND_GRID + b];
       // SURVEY §8(d) B_GO final-step terms: 4 E_N neighbour ids + 8 E_N per WHERE/YIELD edge
       // property column + 8 k per emitted row
       return (double)q.e_st[r.step][r.tix] * (4.0 + 8.0 * r.cols) + 8.0 * rows * r.kout;
@@ -812,7 +819,7 @@ static double prof_bytes(const Prof::Rec& r, const QState& q) {
 static double prof_bytes_path(const Prof::Rec& r, const PState& p) {
   const int i = r.step < PATH_REC ? r.step : PATH_REC - 1;
   switch (r.kid) {
-    case K_DEGREE: return 12.0 * (double)p.ln[i];
+    case K_RELIST: return 12.0 * (double)p.ln[i];
     case K_BFS: return 4.0 * (double)p.le[i];
     case K_GATHER: return 8.0 * (double)p.lc[i];
     case K_DEGSUM: return 12.0 * (double)p.ln[i];
@@ -828,7 +835,7 @@ static void prof_flush(Workspace* w, const QState* q, const PState* ps = nullptr
       if (r.path) {
         if (ps) w->prof.bytes[r.kid] += prof_bytes_path(r, *ps);
       } else if (q) {
-        w->prof.bytes[r.kid] += prof_bytes(r, *q);
+        w->prof.bytes[r.kid] += prof_bytes(w, r, *q);
       }
     }
     w->prof.pool.push_back(r.a);
@@ -837,10 +844,12 @@ static void prof_flush(Workspace* w, const QState* q, const PState* ps = nullptr
   w->prof.pending.clear();
 }
 
-void ws_profile(Workspace* w, bool on) {
+void ws_profile(Workspace* w, int mode) {
   if (!w) return;
   prof_flush(w, nullptr);
-  w->prof.on = on;
+  w->prof.on = mode != 0;
+  w->prof.mask = mode == 2 ? ((1u << K_EXPAND_FINAL) | (1u << K_BFS)) : ~0u;
+  const bool on = w->prof.on;
   if (on) {
     for (int k = 0; k < K_COUNT; ++k) { w->prof.launches[k] = 0; w->prof.ms[k] = 0; w->prof.bytes[k] = 0; }
   }
@@ -859,28 +868,29 @@ int ws_profile_read(Workspace* w, nbg_kernel_stat* out, int cap) {
   return n;
 }
 
-Workspace* ws_create(uint64_t max_frontier, uint64_t nv, hipStream_t s, std::string* err) {
+Workspace* ws_create(uint64_t max_frontier, uint64_t nv, uint64_t e_max, hipStream_t s, std::string* err) {
   auto* w = new Workspace();
   w->stream = s;
   w->nv = nv;
   w->cap_frontier = max_frontier < 1024 ? 1024 : max_frontier;
-  w->cap_blocks = cdiv(w->cap_frontier, SCAN_TILE) + 1;
-  w->flag_bytes = cdiv(nv + 1, FLAG_BYTES) * FLAG_BYTES;
-  uint64_t fblocks = w->flag_bytes / FLAG_BYTES + 1;
-  if (fblocks > w->cap_blocks) w->cap_blocks = fblocks;
+  w->flag_bytes = cdiv(nv + 1, FLAG_ALIGN) * FLAG_ALIGN;
   hipError_t e = hipSuccess;
   auto M = [&](void** p, size_t b) { if (e == hipSuccess) e = hipMalloc(p, b); };
   M((void**)&w->frontier[0], w->cap_frontier * 4);
   M((void**)&w->frontier[1], w->cap_frontier * 4);
   M((void**)&w->seg_end, w->cap_frontier * 4);
   M((void**)&w->seg_rs, w->cap_frontier * 4);
-  M((void**)&w->block_sum, w->cap_blocks * 4);
+  M((void**)&w->rlist, w->cap_frontier * 4);
   M((void**)&w->flags, w->flag_bytes);
-  M((void**)&w->flag_blocks, w->cap_blocks * 4);
+  w->cap_tiles = cdiv(w->cap_frontier + e_max + 1, TILE) + 2;
+  M((void**)&w->tsplit, w->cap_tiles * 4);
+  M((void**)&w->blk_rows, (size_t)MAX_TYPES_Q * EXPAND_GRID * 4);
   M((void**)&w->q, sizeof(QState));
   M((void**)&w->d_prog, (size_t)MAX_TYPES_Q * MAX_PROGRAM * sizeof(Ins));
   M((void**)&w->d_row_cols, MAX_YIELDS * sizeof(int64_t*));
   if (e == hipSuccess) e = hipHostMalloc((void**)&w->h_q, sizeof(QState), hipHostMallocDefault);
+  if (e == hipSuccess)
+    e = hipHostMalloc((void**)&w->h_blk_rows, (size_t)MAX_TYPES_Q * EXPAND_GRID * 4, hipHostMallocDefault);
   if (e == hipSuccess) e = hipHostMalloc((void**)&w->h_prog, (size_t)MAX_TYPES_Q * MAX_PROGRAM * sizeof(Ins),
                                          hipHostMallocDefault);
   if (e == hipSuccess) e = hipMemsetAsync(w->flags, 0, w->flag_bytes, s);
@@ -896,13 +906,14 @@ Workspace* ws_create(uint64_t max_frontier, uint64_t nv, hipStream_t s, std::str
 void ws_destroy(Workspace* w) {
   if (!w) return;
   for (void* p : {(void*)w->frontier[0], (void*)w->frontier[1], (void*)w->seg_end, (void*)w->seg_rs,
-                  (void*)w->block_sum, (void*)w->flags, (void*)w->flag_blocks, (void*)w->q, (void*)w->rows,
+                  (void*)w->rlist, (void*)w->flags, (void*)w->tsplit, (void*)w->blk_rows,
+                  (void*)w->q, (void*)w->rows,
                   (void*)w->d_row_cols, (void*)w->d_prog})
     if (p) (void)hipFree(p);
-  for (void* p : {(void*)w->h_q, (void*)w->h_starts, (void*)w->h_prog, (void*)w->h_ps, (void*)w->h_path,
+  for (void* p : {(void*)w->h_q, (void*)w->h_blk_rows, (void*)w->h_starts, (void*)w->h_prog, (void*)w->h_ps, (void*)w->h_path,
                   (void*)w->h_stage})
     if (p) (void)hipHostFree(p);
-  for (void* p : {(void*)w->sendbits, (void*)w->recvbits, (void*)w->mbits, (void*)w->gst})
+  for (void* p : {(void*)w->sendbits, (void*)w->recvbits, (void*)w->gst})
     if (p) (void)hipFree(p);
   if (w->h_gst) (void)hipHostFree(w->h_gst);
   for (void* p : {(void*)w->ps, (void*)w->pscratch, (void*)w->d_path})
@@ -917,6 +928,8 @@ void ws_destroy(Workspace* w) {
 }
 
 uint64_t ws_cap_frontier(Workspace* w) { return w->cap_frontier; }
+unsigned ws_final_grid_of(Workspace* w, int tix) { return w->final_grid[tix]; }
+const uint32_t* ws_host_blk_rows(Workspace* w, int tix) { return w->h_blk_rows + (size_t)tix * EXPAND_GRID; }
 int64_t* ws_row_col(Workspace* w, int c) { return w->rows + (uint64_t)c * w->cap_rows; }
 const QState* ws_host_state(Workspace* w) { return w->h_q; }
 const uint32_t* ws_current_frontier(Workspace* w) { return w->frontier[w->cur]; }
@@ -952,6 +965,10 @@ hipError_t ws_begin_query(Workspace* w, const uint32_t* starts, uint64_t n, cons
   w->h_q->n = n;
   w->h_q->step_n[1] = n;
   w->cur = 0;
+  w->seg_ready = false;
+  w->list_acc = nullptr;
+  w->pr = w->pc = 0;
+  for (auto& g : w->final_grid) g = 0;
   HIP_TRY(hipMemcpyAsync(w->frontier[0], w->h_starts, n * 4, hipMemcpyHostToDevice, w->stream));
   HIP_TRY(hipMemcpyAsync(w->q, w->h_q, sizeof(QState), hipMemcpyHostToDevice, w->stream));
   if (progs && !progs->empty()) {
@@ -965,19 +982,52 @@ hipError_t ws_begin_query(Workspace* w, const uint32_t* starts, uint64_t n, cons
   return hipSuccess;
 }
 
-// Enqueue k_degree + k_scan_blocks for the current frontier (n <= n_bound) over one type.
-static hipError_t enqueue_scan(Workspace* w, const ExpandArgs& a, uint64_t n_bound, int step, int tix) {
-  uint64_t nb = cdiv(n_bound ? n_bound : 1, SCAN_TILE);
-  hipEvent_t p = prof_begin(w);
-  hipLaunchKernelGGL(k_degree, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->frontier[w->cur], &w->q->n,
-                     a.row_ptr, a.visible, a.cap, w->seg_end, w->seg_rs, w->block_sum,
-                     (unsigned long long*)nullptr, (unsigned long long*)nullptr);
-  prof_end(w, p, K_DEGREE, step, tix);
-  p = prof_begin(w);
-  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, w->stream, w->block_sum, &w->q->n, (uint64_t)0,
-                     &w->q->total, &w->q->e_st[step][tix]);
-  prof_end(w, p, K_SCAN, step, tix);
-  return hipGetLastError();
+// The list one expansion consumes: the compaction's list when it already carries this (first)
+// type's edge space, otherwise a k_relist of the current frontier over this type's CSR.
+struct ListRef {
+  const uint32_t* ids;
+  const unsigned long long* acc;
+  unsigned long long* stat_n;      // the expansion records |F_s| (its list is the whole frontier)
+};
+
+static DegSrc deg_of(const ExpandArgs& a) {
+  DegSrc ds{};
+  ds.row_ptr = a.row_ptr;
+  ds.visible = a.visible;
+  ds.cap = a.cap;
+  return ds;
+}
+
+static ListOut list_out(Workspace* w, uint32_t* ids, unsigned long long* acc, unsigned long long* zero_next,
+                        unsigned long long* stat_n) {
+  ListOut o{};
+  o.ids = ids;
+  o.seg_end = w->seg_end;
+  o.seg_rs = w->seg_rs;
+  o.tsplit = w->tsplit;
+  o.acc = acc;
+  o.zero_next = zero_next;
+  o.stat_n = stat_n;
+  return o;
+}
+
+static ListRef prepare_list(Workspace* w, const ExpandArgs& a, uint64_t n_bound, int step, int tix) {
+  if (tix == 0 && w->seg_ready) {
+    w->seg_ready = false;
+    return ListRef{w->frontier[w->cur], w->list_acc, &w->q->step_n[step]};
+  }
+  unsigned long long* acc = &w->q->acc[w->pr];
+  unsigned long long* other = &w->q->acc[w->pr ^ 1];
+  w->pr ^= 1;
+  const bool packed = w->list_acc != nullptr;
+  const unsigned long long* in_n = packed ? w->list_acc : &w->q->n;
+  hipEvent_t p = prof_begin(w, K_RELIST);
+  hipLaunchKernelGGL(k_relist, dim3((unsigned)cdiv(n_bound ? n_bound : 1, RL_TILE)), dim3(BLOCK), 0, w->stream,
+                     w->frontier[w->cur], in_n, (int)packed, deg_of(a),
+                     list_out(w, w->rlist, acc, other, step > 1 ? &w->q->step_n[step] : nullptr),
+                     (unsigned long long*)nullptr);
+  prof_end(w, p, K_RELIST, step, tix);
+  return ListRef{w->rlist, acc, nullptr};
 }
 
 static unsigned expand_grid(uint64_t n_bound, uint64_t e_bound) {
@@ -987,33 +1037,32 @@ static unsigned expand_grid(uint64_t n_bound, uint64_t e_bound) {
 
 hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, uint64_t e_bound, int step, int tix) {
   if (step > MAX_STEPS || tix >= MAX_TYPES_Q) return hipErrorInvalidValue;
-  HIP_TRY(enqueue_scan(w, a0, n_bound, step, tix));
+  const ListRef L = prepare_list(w, a0, n_bound, step, tix);
   ExpandArgs a = a0;
-  a.frontier = w->frontier[w->cur];
+  a.frontier = L.ids;
+  a.tsplit = w->tsplit;
   FinalParams fp{};
-  hipEvent_t p = prof_begin(w);
-  hipLaunchKernelGGL(k_expand<MARK>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, &w->q->n,
-                     &w->q->total, w->seg_end, w->block_sum, w->seg_rs, w->flags, fp, BfsParams{});
+  hipEvent_t p = prof_begin(w, K_EXPAND_MARK);
+  hipLaunchKernelGGL(k_expand<MARK>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, L.acc,
+                     w->seg_end, w->seg_rs, w->flags, fp, BfsParams{}, &w->q->e_st[step][tix], L.stat_n);
   prof_end(w, p, K_EXPAND_MARK, step, tix);
   return hipGetLastError();
 }
 
-hipError_t ws_compact(Workspace* w, int step) {
-  uint64_t nb = w->flag_bytes / FLAG_BYTES;
+static DegSrc deg_src(const ExpandArgs* next0) { return next0 ? deg_of(*next0) : DegSrc{}; }
+
+hipError_t ws_compact(Workspace* w, int step, const ExpandArgs* next0) {
+  unsigned long long* acc = &w->q->acc[2 + w->pc];
+  unsigned long long* other = &w->q->acc[2 + (w->pc ^ 1)];
+  w->pc ^= 1;
   uint32_t* next = w->frontier[w->cur ^ 1];
-  hipEvent_t p = prof_begin(w);
-  hipLaunchKernelGGL(k_flag_count, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->flags, w->flag_bytes,
-                     w->flag_blocks);
-  prof_end(w, p, K_FLAG_COUNT, step, 0);
-  p = prof_begin(w);
-  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, w->stream, w->flag_blocks, &w->q->n, nb, &w->q->n,
-                     &w->q->step_n[step + 1]);
-  prof_end(w, p, K_SCAN, step, 0);
-  p = prof_begin(w);
-  hipLaunchKernelGGL(k_flag_write, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->flags, w->flag_bytes, w->nv,
-                     w->flag_blocks, next);
-  prof_end(w, p, K_FLAG_WRITE, step, 0);
+  hipEvent_t p = prof_begin(w, K_COMPACT);
+  hipLaunchKernelGGL(k_compact, dim3((unsigned)(w->flag_bytes / CP_BYTES)), dim3(CP_THREADS), 0, w->stream, w->flags,
+                     deg_src(next0), list_out(w, next, acc, other, nullptr));
+  prof_end(w, p, K_COMPACT, step, 0);
   w->cur ^= 1;
+  w->list_acc = acc;
+  w->seg_ready = next0 != nullptr;
   return hipGetLastError();
 }
 
@@ -1064,7 +1113,7 @@ static FastProg detect_fast(const TypeProgram& prog, const ExpandArgs& a) {
     if (pc >= (int)prog.code.size()) return f;
     const Ins& i = prog.code[pc++];
     if (i.d != prog.yield_reg[y]) return f;
-    if (i.op == OP_DST) f.ykind[y] = 0;
+    if (i.op == OP_DST) { f.ykind[y] = 0; f.dst_yield = 1; }
     else if (i.op == OP_SRC) f.ykind[y] = 1;
     else if (i.op == OP_RANK) f.ykind[y] = 2;
     else if (leaf_col(i)) { f.ykind[y] = 3; f.ycol[y] = i.aux; }
@@ -1075,17 +1124,25 @@ static FastProg detect_fast(const TypeProgram& prog, const ExpandArgs& a) {
   return f;
 }
 
+unsigned ws_final_grid(uint64_t n_bound, uint64_t e_bound) { return expand_grid(n_bound, e_bound); }
+
+uint64_t ws_final_blk_cap(uint64_t n_bound, uint64_t e_bound) {
+  const uint64_t tiles = cdiv(n_bound + e_bound + 1, TILE);
+  return cdiv(tiles, expand_grid(n_bound, e_bound)) * TILE;
+}
+
 uint64_t ws_shard_cap(uint64_t n_bound, uint64_t e_bound) {
   uint64_t tiles = cdiv(n_bound + e_bound + 1, TILE);
   return cdiv(tiles, NSHARD) * TILE;
 }
 
 hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, uint64_t e_bound, int step, int tix,
-                           const TypeProgram& prog, uint64_t region_base, uint64_t shard_cap) {
+                           const TypeProgram& prog, uint64_t region_base, uint64_t blk_cap) {
   if (step > MAX_STEPS || tix >= MAX_TYPES_Q) return hipErrorInvalidValue;
-  HIP_TRY(enqueue_scan(w, a0, n_bound, step, tix));
+  const ListRef L = prepare_list(w, a0, n_bound, step, tix);
   ExpandArgs a = a0;
-  a.frontier = w->frontier[w->cur];
+  a.frontier = L.ids;
+  a.tsplit = w->tsplit;
   FinalParams fp{};
   fp.prog = w->d_prog + (size_t)tix * MAX_PROGRAM;
   fp.where_len = prog.where_len;
@@ -1098,25 +1155,71 @@ hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound,
   }
   fp.out_cols = w->d_row_cols;
   fp.region_base = region_base;
-  fp.shard_cap = shard_cap;
-  fp.shard_rows = &w->q->rows[tix][0];
+  fp.blk_cap = blk_cap;
+  fp.blk_rows = w->blk_rows + (size_t)tix * EXPAND_GRID;
   fp.err_flag = &w->q->err;
   fp.fast = detect_fast(prog, a);
   size_t lds = fp.fast.enabled ? 0 : (size_t)(prog.nregs > 0 ? prog.nregs : 1) * BLOCK * sizeof(int64_t);
-  hipEvent_t p = prof_begin(w);
-  hipLaunchKernelGGL(k_expand<FINAL>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), lds, w->stream, a, &w->q->n,
-                     &w->q->total, w->seg_end, w->block_sum, w->seg_rs, w->flags, fp, BfsParams{});
+  hipEvent_t p = prof_begin(w, K_EXPAND_FINAL);
+  if (fp.fast.enabled)
+    hipLaunchKernelGGL(k_expand<FINALF>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, L.acc,
+                       w->seg_end, w->seg_rs, w->flags, fp, BfsParams{}, &w->q->e_st[step][tix], L.stat_n);
+  else
+    hipLaunchKernelGGL(k_expand<FINAL>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), lds, w->stream, a, L.acc,
+                       w->seg_end, w->seg_rs, w->flags, fp, BfsParams{}, &w->q->e_st[step][tix], L.stat_n);
   prof_end(w, p, K_EXPAND_FINAL, step, tix, (double)edge_columns_read(prog), (double)fp.nyields);
+  w->final_grid[tix] = expand_grid(n_bound, e_bound);
   return hipGetLastError();
 }
 
 // Scan-only expansion (final step whose WHERE folded to false still counts E_N).
 hipError_t ws_scan_only(Workspace* w, const ExpandArgs& a, uint64_t n_bound, int step, int tix) {
-  return enqueue_scan(w, a, n_bound, step, tix);
+  const ListRef L = prepare_list(w, a, n_bound, step, tix);
+  hipLaunchKernelGGL(k_note, dim3(1), dim3(1), 0, w->stream, L.acc, &w->q->e_st[step][tix], L.stat_n);
+  return hipGetLastError();
+}
+
+// Synchronous: packs `segs` (begin, len) of the workspace's row columns into host columns.
+hipError_t ws_fetch_rows(Workspace* w, const std::vector<std::pair<uint64_t, uint64_t>>& segs, int ncols,
+                         uint64_t total, int64_t* const* host_cols) {
+  if (!total || !ncols) return hipSuccess;
+  std::vector<uint64_t> meta;
+  uint64_t o = 0;
+  for (auto& sg : segs) {
+    if (!sg.second) continue;
+    meta.push_back(sg.first);
+    meta.push_back(sg.second);
+    meta.push_back(o);
+    o += sg.second;
+  }
+  if (o != total) return hipErrorInvalidValue;
+  uint64_t* d_meta = nullptr;
+  int64_t* d_out = nullptr;
+  hipError_t e = hipMalloc((void**)&d_meta, meta.size() * 8);
+  if (e == hipSuccess) e = hipMalloc((void**)&d_out, total * ncols * 8);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_meta, meta.data(), meta.size() * 8, hipMemcpyHostToDevice, w->stream);
+  if (e == hipSuccess) {
+    const int nseg = (int)(meta.size() / 3);
+    hipLaunchKernelGGL(k_pack_rows, dim3((unsigned)(nseg < 4096 ? nseg : 4096)), dim3(BLOCK), 0, w->stream, d_meta,
+                       nseg, (int64_t* const*)w->d_row_cols, ncols, d_out, total);
+    e = hipGetLastError();
+  }
+  for (int c = 0; e == hipSuccess && c < ncols; ++c)
+    e = hipMemcpyAsync(host_cols[c], d_out + (uint64_t)c * total, total * 8, hipMemcpyDeviceToHost, w->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(w->stream);
+  if (d_meta) (void)hipFree(d_meta);
+  if (d_out) (void)hipFree(d_out);
+  return e;
 }
 
 hipError_t ws_end_query(Workspace* w) {
   HIP_TRY(hipMemcpyAsync(w->h_q, w->q, sizeof(QState), hipMemcpyDeviceToHost, w->stream));
+  int nt = 0;
+  for (int t = 0; t < MAX_TYPES_Q; ++t)
+    if (w->final_grid[t]) nt = t + 1;
+  if (nt)
+    HIP_TRY(hipMemcpyAsync(w->h_blk_rows, w->blk_rows, (size_t)nt * EXPAND_GRID * 4, hipMemcpyDeviceToHost,
+                           w->stream));
   HIP_TRY(hipStreamSynchronize(w->stream));
   prof_flush(w, w->h_q);
   return hipSuccess;
@@ -1124,61 +1227,47 @@ hipError_t ws_end_query(Workspace* w) {
 
 // ----------------------------------------------------------------------------- partitioned mode
 hipError_t ws_set_partition(Workspace* w, Comm* comm, uint64_t npad) {
-  if (!comm || npad % BITS_BLOCK) return hipErrorInvalidValue;
+  if (!comm || npad % PART_ALIGN || PART_ALIGN % BITS_BLOCK || PART_ALIGN % FLAG_ALIGN) return hipErrorInvalidValue;
   const uint64_t G = (uint64_t)comm->world;
   HIP_TRY(hipStreamSynchronize(w->stream));
   w->comm = comm;
   w->npad = npad;
   if (w->flags) HIP_TRY(hipFree(w->flags));
   w->flags = nullptr;
-  w->flag_bytes = G * npad;                     // multiple of FLAG_BYTES (npad % BITS_BLOCK == 0)
+  w->flag_bytes = G * npad;                     // multiple of FLAG_ALIGN (PART_ALIGN is)
   HIP_TRY(hipMalloc((void**)&w->flags, w->flag_bytes));
   HIP_TRY(hipMemsetAsync(w->flags, 0, w->flag_bytes, w->stream));
   HIP_TRY(hipMalloc((void**)&w->sendbits, G * npad / 8));
   HIP_TRY(hipMalloc((void**)&w->recvbits, G * npad / 8));
-  HIP_TRY(hipMalloc((void**)&w->mbits, npad / 8));
   HIP_TRY(hipMalloc((void**)&w->gst, GST_N * sizeof(unsigned long long)));
   HIP_TRY(hipHostMalloc((void**)&w->h_gst, GST_N * sizeof(unsigned long long), hipHostMallocDefault));
-  const uint64_t nb = npad / BITS_BLOCK + 1;
-  if (nb > w->cap_blocks) {
-    if (w->flag_blocks) HIP_TRY(hipFree(w->flag_blocks));
-    w->flag_blocks = nullptr;
-    w->cap_blocks = nb;
-    HIP_TRY(hipMalloc((void**)&w->flag_blocks, nb * 4));
-    HIP_TRY(hipFree(w->block_sum));
-    w->block_sum = nullptr;
-    HIP_TRY(hipMalloc((void**)&w->block_sum, nb * 4));
-  }
   return hipStreamSynchronize(w->stream);
 }
 
 // After all OVER types of a non-final step marked their candidates (global ids) in the flags:
 // pack -> all-to-all of npad-bit segments -> owner OR + compaction into the next local frontier.
-hipError_t ws_exchange(Workspace* w, int step) {
+hipError_t ws_exchange(Workspace* w, int step, const ExpandArgs* next0) {
   if (!w->comm) return hipErrorInvalidValue;
   const uint64_t G = (uint64_t)w->comm->world;
   const uint64_t nwords = G * w->npad / 64, seg_words = w->npad / 64, nb = w->npad / BITS_BLOCK;
-  hipEvent_t p = prof_begin(w);
+  hipEvent_t p = prof_begin(w, K_PACK);
   hipLaunchKernelGGL(k_pack_bits, dim3((unsigned)cdiv(nwords, BLOCK)), dim3(BLOCK), 0, w->stream, w->flags, nwords,
                      w->sendbits);
   prof_end(w, p, K_PACK, step, 0, (double)(G * w->npad) + (double)(G * w->npad / 8));
   HIP_TRY(hipGetLastError());
-  p = prof_begin(w);
+  p = prof_begin(w, K_ALLTOALL);
   if (w->comm->alltoall(w->sendbits, w->recvbits, w->npad / 8, w->stream)) return hipErrorUnknown;
   prof_end(w, p, K_ALLTOALL, step, 0, (double)((G - 1) * w->npad / 8));
-  p = prof_begin(w);
-  hipLaunchKernelGGL(k_bits_count, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->recvbits, (int)G, seg_words,
-                     w->nv, w->mbits, w->flag_blocks);
-  prof_end(w, p, K_BITS_COUNT, step, 0, (double)(G * w->npad / 8) + (double)(w->npad / 8));
-  p = prof_begin(w);
-  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, w->stream, w->flag_blocks, &w->q->n, nb, &w->q->n,
-                     &w->q->step_n[step + 1]);
-  prof_end(w, p, K_SCAN, step, 0);
-  p = prof_begin(w);
-  hipLaunchKernelGGL(k_bits_write, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->mbits, w->flag_blocks,
-                     w->frontier[w->cur ^ 1]);
-  prof_end(w, p, K_BITS_WRITE, step, 0);
+  unsigned long long* acc = &w->q->acc[2 + w->pc];
+  unsigned long long* other = &w->q->acc[2 + (w->pc ^ 1)];
+  w->pc ^= 1;
+  p = prof_begin(w, K_BITS_COMPACT);
+  hipLaunchKernelGGL(k_bits_compact, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->recvbits, (int)G, seg_words,
+                     w->nv, deg_src(next0), list_out(w, w->frontier[w->cur ^ 1], acc, other, nullptr));
+  prof_end(w, p, K_BITS_COMPACT, step, 0);
   w->cur ^= 1;
+  w->list_acc = acc;
+  w->seg_ready = next0 != nullptr;
   return hipGetLastError();
 }
 
@@ -1400,7 +1489,7 @@ __global__ void __launch_bounds__(GREEDY_BLOCK) k_path_greedy(GreedyArgs g) {
 
 // ----------------------------------------------------------------------------- path host side
 constexpr uint64_t STAGE = 4096;
-static hipEvent_t prof_begin_p(Workspace* w) { return prof_begin(w); }
+static hipEvent_t prof_begin_p(Workspace* w, int kid) { return prof_begin(w, kid); }
 static void prof_end_p(Workspace* w, hipEvent_t a, int kid, int rec) {
   if (!a) return;
   hipEvent_t b = w->prof.get();
@@ -1438,6 +1527,7 @@ hipError_t ws_path_begin(Workspace* w, uint64_t scratch_entries, uint64_t list_e
     HIP_TRY(hipMalloc((void**)&w->pscratch, w->pscratch_cap * sizeof(uint32_t)));
   }
   w->rec = 0;
+  w->ppr = 0;
   return hipMemsetAsync(w->ps, 0, sizeof(PState), w->stream);
 }
 
@@ -1479,7 +1569,7 @@ hipError_t ws_path_upload(Workspace* w, int s, const uint32_t* ids, uint64_t n) 
 hipError_t ws_path_stamp(Workspace* w, int s, uint64_t n_bound, int l, uint32_t stamp) {
   unsigned nb = (unsigned)cdiv(n_bound ? n_bound : 1, BLOCK);
   if (nb > 1024) nb = 1024;
-  hipEvent_t p = prof_begin_p(w);
+  hipEvent_t p = prof_begin_p(w, K_STAMP);
   hipLaunchKernelGGL(k_stamp, dim3(nb), dim3(BLOCK), 0, w->stream, w->slot[s], &w->ps->n[s], w->lab[l], stamp);
   prof_end_p(w, p, K_STAMP, 0);
   return hipGetLastError();
@@ -1495,7 +1585,7 @@ hipError_t ws_path_degsum(Workspace* w, int s, uint64_t n_bound, const PathTypes
   if (nb > 2048) nb = 2048;
   const int rec = w->rec < PATH_REC ? w->rec++ : PATH_REC - 1;
   HIP_TRY(hipMemsetAsync(&w->ps->dsum[side], 0, sizeof(unsigned long long), w->stream));
-  hipEvent_t p = prof_begin_p(w);
+  hipEvent_t p = prof_begin_p(w, K_DEGSUM);
   hipLaunchKernelGGL(k_degsum, dim3(nb), dim3(BLOCK), 0, w->stream, w->slot[s], &w->ps->n[s], d,
                      &w->ps->dsum[side], &w->ps->ln[rec]);
   prof_end_p(w, p, K_DEGSUM, rec);
@@ -1534,26 +1624,26 @@ hipError_t ws_path_level(Workspace* w, const PathTypes& pt, int src, uint64_t n_
   const int rec = w->rec < PATH_REC ? w->rec++ : PATH_REC - 1;
   for (int t = 0; t < pt.n; ++t) {
     ExpandArgs a = pt.a[t];
-    a.frontier = w->slot[src];
-    uint64_t nb = cdiv(n_bound ? n_bound : 1, SCAN_TILE);
-    hipEvent_t p = prof_begin_p(w);
-    hipLaunchKernelGGL(k_degree, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->slot[src], &w->ps->n[src],
-                       a.row_ptr, a.visible, a.cap, w->seg_end, w->seg_rs, w->block_sum,
-                       t == 0 ? w->ps->shard : (unsigned long long*)nullptr, &w->ps->ln[rec]);
-    prof_end_p(w, p, K_DEGREE, rec);
-    p = prof_begin_p(w);
-    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, w->stream, w->block_sum, &w->ps->n[src], (uint64_t)0,
-                       &w->ps->total, &w->ps->le[rec]);
-    prof_end_p(w, p, K_SCAN, rec);
-    p = prof_begin_p(w);
-    hipLaunchKernelGGL(k_expand<BFS>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a,
-                       &w->ps->n[src], &w->ps->total, w->seg_end, w->block_sum, w->seg_rs, (uint8_t*)nullptr,
-                       FinalParams{}, bp);
+    unsigned long long* acc = &w->ps->acc[w->ppr];
+    unsigned long long* other = &w->ps->acc[w->ppr ^ 1];
+    w->ppr ^= 1;
+    hipEvent_t p = prof_begin_p(w, K_RELIST);
+    hipLaunchKernelGGL(k_relist, dim3((unsigned)cdiv(n_bound ? n_bound : 1, RL_TILE)), dim3(BLOCK), 0, w->stream,
+                       w->slot[src], &w->ps->n[src], 0, deg_of(a),
+                       list_out(w, w->rlist, acc, other, t == 0 ? &w->ps->ln[rec] : nullptr),
+                       t == 0 ? w->ps->shard : (unsigned long long*)nullptr);
+    prof_end_p(w, p, K_RELIST, rec);
+    a.frontier = w->rlist;
+    a.tsplit = w->tsplit;
+    p = prof_begin_p(w, K_BFS);
+    hipLaunchKernelGGL(k_expand<BFS>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, acc,
+                       w->seg_end, w->seg_rs, (uint8_t*)nullptr, FinalParams{}, bp, &w->ps->le[rec],
+                       (unsigned long long*)nullptr);
     prof_end_p(w, p, K_BFS, rec);
   }
   uint64_t gb = cdiv(n_bound + e_bound + 1, (uint64_t)BLOCK * 4);
   unsigned grid = (unsigned)(gb < 1 ? 1 : (gb > 1024 ? 1024 : gb));
-  hipEvent_t p = prof_begin_p(w);
+  hipEvent_t p = prof_begin_p(w, K_GATHER);
   hipLaunchKernelGGL(k_gather, dim3(grid), dim3(BLOCK), 0, w->stream, w->pscratch, shard_cap, w->ps->shard,
                      w->slot[dst], &w->ps->n[dst], &w->ps->lc[rec]);
   prof_end_p(w, p, K_GATHER, rec);
@@ -1593,7 +1683,7 @@ hipError_t ws_path_greedy(Workspace* w, const PathTypes& pt, const PathGreedy& p
   g.nstarts = &w->ps->n[pg.start_slot];
   g.out = w->d_path;
   g.err = &w->ps->err;
-  hipEvent_t p = prof_begin_p(w);
+  hipEvent_t p = prof_begin_p(w, K_GREEDY);
   hipLaunchKernelGGL(k_path_greedy, dim3(1), dim3(GREEDY_BLOCK), 0, w->stream, g);
   prof_end_p(w, p, K_GREEDY, 0);
   return hipGetLastError();

@@ -90,6 +90,11 @@ struct Snapshot {
   std::map<int32_t, DevEdgeType> types; // signed type -> CSR
   std::vector<std::string> strings;     // sorted dictionary; device code = 2 * index
   uint64_t device_bytes = 0;
+  uint64_t max_edges() const {
+    uint64_t m = 0;
+    for (auto& kv : types) m = kv.second.num_edges > m ? kv.second.num_edges : m;
+    return m;
+  }
 };
 
 // ----------------------------------------------------------------------------- bytecode
@@ -146,7 +151,10 @@ struct TypeProgram {
 };
 
 // ----------------------------------------------------------------------------- kernel interface
-constexpr int VT = 4;                  // k_expand: path items per thread
+#ifndef NBG_VT
+#define NBG_VT 4
+#endif
+constexpr int VT = NBG_VT;             // k_expand: path items per thread
 constexpr int TILE = 256 * VT;         // path items (frontier segments + edges) per tile
 constexpr int NSHARD = 64;             // row-output shards (one counter + region each)
 constexpr int MAX_STEPS = 32;          // GO N STEPS upper bound
@@ -158,10 +166,9 @@ struct QState {
   unsigned long long n;                // current frontier size
   unsigned long long total;            // edges of the current (step, type) expansion
   unsigned long long err;              // WHERE/YIELD evaluation error
-  unsigned long long pad;
+  unsigned long long acc[4];           // packed list sizes (entries << 32 | edges): relist 0/1, compaction 2/3
   unsigned long long step_n[MAX_STEPS + 2];              // frontier size entering step s
   unsigned long long e_st[MAX_STEPS + 2][MAX_TYPES_Q];   // edges per (step, type)
-  unsigned long long rows[MAX_TYPES_Q][NSHARD];          // rows per (type, shard) at step N
 };
 
 struct ExpandArgs {                // one (step, edge type) expansion
@@ -175,6 +182,7 @@ struct ExpandArgs {                // one (step, edge type) expansion
   const int64_t* vids;             // dense id -> vid (for _src)
   const int64_t* const* props;     // device array of column pointers
   uint32_t cap;                    // max_edge_returned_per_vertex
+  const uint32_t* tsplit;          // per-tile merge-path splits (set by the workspace; null: search)
 };
 
 // ----------------------------------------------------------------------------- FIND PATH state
@@ -193,6 +201,7 @@ struct PState {                      // device-resident sizes of one FIND PATH q
   unsigned long long meets;          // meet-list length
   unsigned long long found;          // targets reached (one-sided search)
   unsigned long long err;            // reconstruction failure
+  unsigned long long acc[2];         // packed relist sizes (ping-pong)
   unsigned long long dsum[2];        // degree sum of the current forward / backward frontier
   unsigned long long shard[NSHARD];  // claim counters
   unsigned long long ln[PATH_REC];   // per expansion record: frontier size, edges, claims
@@ -224,14 +233,22 @@ std::vector<Comm*> comm_local_group(int world);
 
 struct Workspace;   // kernels.hip
 
-Workspace* ws_create(uint64_t max_frontier, uint64_t nv, hipStream_t s, std::string* err);
+// e_max: the largest edge count of one signed type (sizes the per-tile split array)
+Workspace* ws_create(uint64_t max_frontier, uint64_t nv, uint64_t e_max, hipStream_t s, std::string* err);
 void ws_destroy(Workspace* w);
-void ws_profile(Workspace* w, bool on);
+void ws_profile(Workspace* w, int mode);   // 0 off, 1 every launch, 2 final/BFS expansions only
 int ws_profile_read(Workspace* w, nbg_kernel_stat* out, int cap);
 uint64_t ws_cap_frontier(Workspace* w);
 hipError_t ws_reserve_rows(Workspace* w, uint64_t rows, int ncols);
 int64_t* ws_row_col(Workspace* w, int c);       // device pointer of output column c
 uint64_t ws_shard_cap(uint64_t n_bound, uint64_t e_bound);
+// final-step row layout: ws_final_grid workgroups, each appending to its own blk_cap rows
+unsigned ws_final_grid(uint64_t n_bound, uint64_t e_bound);
+uint64_t ws_final_blk_cap(uint64_t n_bound, uint64_t e_bound);
+unsigned ws_final_grid_of(Workspace* w, int tix);          // grid of the last final expansion (0: none)
+const uint32_t* ws_host_blk_rows(Workspace* w, int tix);    // rows per workgroup (after ws_end_query)
+hipError_t ws_fetch_rows(Workspace* w, const std::vector<std::pair<uint64_t, uint64_t>>& segs, int ncols,
+                         uint64_t total, int64_t* const* host_cols);
 const QState* ws_host_state(Workspace* w);       // valid after ws_end_query
 const uint32_t* ws_current_frontier(Workspace* w);
 
@@ -240,16 +257,17 @@ hipError_t ws_begin_query(Workspace* w, const uint32_t* starts, uint64_t n, cons
 // steps 1..N-1, per OVER type: scan + expand into next-frontier flags
 hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a, uint64_t n_bound, uint64_t e_bound, int step, int tix);
 // after all types of a step: flags -> next frontier
-hipError_t ws_compact(Workspace* w, int step);
+// next0: the first OVER type's CSR of step + 1 (its degree pass is fused into the compaction)
+hipError_t ws_compact(Workspace* w, int step, const ExpandArgs* next0);
 // step N, per OVER type: scan + WHERE/YIELD + sharded row emission into [region_base, +NSHARD*shard_cap)
 hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a, uint64_t n_bound, uint64_t e_bound, int step, int tix,
-                           const TypeProgram& prog, uint64_t region_base, uint64_t shard_cap);
+                           const TypeProgram& prog, uint64_t region_base, uint64_t blk_cap);
 hipError_t ws_scan_only(Workspace* w, const ExpandArgs& a, uint64_t n_bound, int step, int tix);
 hipError_t ws_end_query(Workspace* w);
 // partitioned mode: flags over [world * npad) global ids, per-hop bitmap all-to-all
-constexpr uint64_t PART_ALIGN = 256 * 64;    // npad granularity (k_bits_* block)
+constexpr uint64_t PART_ALIGN = 16384 * 4;   // npad granularity (flag / bit workgroups divide it)
 hipError_t ws_set_partition(Workspace* w, Comm* comm, uint64_t npad);
-hipError_t ws_exchange(Workspace* w, int step);            // replaces ws_compact
+hipError_t ws_exchange(Workspace* w, int step, const ExpandArgs* next0);   // replaces ws_compact
 hipError_t ws_global_stats(Workspace* w, int ntypes);      // before ws_end_query
 void ws_host_gstats(Workspace* w, unsigned long long* err, unsigned long long* step_n, unsigned long long* esum);
 

@@ -143,7 +143,8 @@ class Engine:
                 "num_edge_types": s.num_edge_types}
 
     # ------------------------------------------------------------------ profiling
-    def profile(self, enable: bool = True):
+    def profile(self, enable=True):
+        """True/1: time every launch; 2: only the final-step / BFS expansion kernels; False/0: off."""
         self._check(self.lib.nbg_profile(self.h, int(enable)), "profile")
 
     def profile_read(self):
