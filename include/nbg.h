@@ -143,6 +143,17 @@ int32_t nbg_go(nbg_engine* e, const nbg_go_request* req, nbg_rows** out);
  * nbg_rows_free); nbg_rows_fetch() copies them to the host on demand. */
 int32_t nbg_go_device(nbg_engine* e, const nbg_go_request* req, nbg_rows** out);
 
+/* Prepared GO statement: GoExecutor::prepare() once (OVER / WHERE / YIELD validated and compiled
+ * per OVER type, GoExecutor.cpp:136-263), then execute() from any number of start lists — the
+ * request's starts are ignored by prepare.  Name-resolution errors stay deferred to the final step
+ * as in nbg_go.  A statement belongs to its engine and must be freed before it. */
+typedef struct nbg_go_stmt nbg_go_stmt;
+int32_t nbg_go_prepare(nbg_engine* e, const nbg_go_request* req, nbg_go_stmt** out);
+/* device != 0: rows stay in HBM as with nbg_go_device; otherwise as nbg_go. */
+int32_t nbg_go_execute(nbg_go_stmt* stmt, const int64_t* starts, uint64_t num_starts, int32_t device,
+                       nbg_rows** out);
+void nbg_go_stmt_free(nbg_go_stmt* stmt);
+
 int64_t nbg_rows_count(const nbg_rows* r);
 int32_t nbg_rows_num_cols(const nbg_rows* r);
 /* Σ_s E_s: adjacency entries scanned over all steps (the TEPS numerator); whole query, i.e.

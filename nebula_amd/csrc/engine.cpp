@@ -10,6 +10,7 @@
 // Each hop runs on the device: degree scan -> merge-path partition -> expand (+ byte-flag
 // dedup and compaction, or the final-step bytecode + row compaction).
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 
 #include "engine.h"
@@ -94,13 +95,24 @@ const char* kGoUnsupportedDistinct = "YIELD DISTINCT is not supported on the dev
 }  // namespace
 
 // ============================================================================= GO driver
-static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_rows** out) {
+// A prepared GO statement: GoExecutor::prepare() (OVER / WHERE / YIELD validated, compiled once
+// per OVER type, GoExecutor.cpp:136-263); execute() runs it from a start list.
+struct nbg_go_stmt {
+  Engine* eng = nullptr;
+  uint64_t id = 0;                   // device program cache key
+  std::vector<int32_t> over;
+  std::vector<TypeProgram> plist;    // OVER order (default program where compilation deferred)
+  int ncols = 0;
+  uint32_t steps = 1;
+  int32_t deferred = NBG_OK;         // name-resolution error, reported only if the final step runs
+  std::string deferred_msg;
+};
+
+static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out) {
   if (!rq || !out) return E.fail(NBG_E_INVALID_ARGUMENT, "null argument");
   *out = nullptr;
-  std::lock_guard<std::mutex> lg(E.mu);
   if (!E.finalized) return E.fail(NBG_E_STATE, "engine not finalized");
   if (rq->steps < 1) return E.fail(NBG_E_INVALID_ARGUMENT, "steps must be >= 1");
-  if (hipSetDevice(E.cfg.device) != hipSuccess) return E.fail(NBG_E_DEVICE, "hipSetDevice failed");
   // OVER (prepareOver / prepareOverAll, GoExecutor.cpp:197-263)
   std::vector<int32_t> over;
   if (rq->over_all) {
@@ -207,11 +219,42 @@ static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_row
     if ((int)tp.code.size() > MAX_PROGRAM) return E.fail(NBG_E_UNSUPPORTED, "program too long");
     progs[t] = std::move(tp);
   }
+  if ((int)over.size() > MAX_TYPES_Q || rq->steps > (uint32_t)MAX_STEPS)
+    return E.fail(NBG_E_UNSUPPORTED, "too many OVER types or steps");
+  static std::atomic<uint64_t> next_id{1};
+  auto* st = new nbg_go_stmt();
+  st->eng = &E;
+  st->id = next_id++;
+  st->over = over;
+  st->plist.resize(over.size());
+  for (size_t i = 0; i < over.size(); ++i) {
+    auto it = progs.find(over[i]);
+    if (it != progs.end()) st->plist[i] = std::move(it->second);
+  }
+  st->ncols = ncols;
+  st->steps = rq->steps;
+  st->deferred = deferred;
+  st->deferred_msg = deferred_msg;
+  *out = st;
+  return NBG_OK;
+}
+
+static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* starts, uint64_t num_starts, bool device,
+                          nbg_rows** out) {
+  if (!out || (num_starts && !starts)) return E.fail(NBG_E_INVALID_ARGUMENT, "null argument");
+  *out = nullptr;
+  if (hipSetDevice(E.cfg.device) != hipSuccess) return E.fail(NBG_E_DEVICE, "hipSetDevice failed");
+  const std::vector<int32_t>& over = st->over;
+  const std::vector<TypeProgram>& plist = st->plist;
+  const int ncols = st->ncols;
+  const uint32_t steps = st->steps;
+  const int32_t deferred = st->deferred;
+  std::string err;
   // starts -> dense ids (duplicates kept)
   std::vector<uint32_t> f0;
-  f0.reserve(rq->num_starts);
-  for (uint64_t i = 0; i < rq->num_starts; ++i) {
-    uint32_t d = E.dense(rq->starts[i]);
+  f0.reserve(num_starts);
+  for (uint64_t i = 0; i < num_starts; ++i) {
+    uint32_t d = E.dense(starts[i]);
     if (d != NO_ROW) f0.push_back(d);
   }
   auto* rows = new nbg_rows();
@@ -220,10 +263,6 @@ static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_row
   rows->on_device = device;
   // (partitioned: every rank runs the same collective sequence, even with no local start)
   if (f0.empty() && !E.partitioned()) { *out = rows; return NBG_OK; }
-  if ((int)over.size() > MAX_TYPES_Q || rq->steps > (uint32_t)MAX_STEPS) {
-    delete rows;
-    return E.fail(NBG_E_UNSUPPORTED, "too many OVER types or steps");
-  }
   if (f0.size() > ws_cap_frontier(E.ws)) {   // room for a duplicated start list
     ws_destroy(E.ws);
     E.ws = ws_create(f0.size(), E.snap.nv, E.snap.max_edges(), E.stream, &err);
@@ -249,12 +288,6 @@ static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_row
     a.cap = cap;
     return a;
   };
-  // programs in OVER order (slot = index in `over`)
-  std::vector<TypeProgram> plist(over.size());
-  for (size_t i = 0; i < over.size(); ++i) {
-    auto it = progs.find(over[i]);
-    if (it != progs.end()) plist[i] = it->second;
-  }
   // the start list keeps duplicates, so its edge space is the one frontier not bounded by E:
   // the device lists carry it in 32 bits
   for (int32_t t : over) {
@@ -269,14 +302,14 @@ static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_row
   }
   // final-step row regions: the frontier entering step N is a set (N >= 2) or the start list
   // (N == 1, exact edge count known on the host)
-  const uint64_t n_final = rq->steps == 1 ? f0.size() : E.snap.nv;
+  const uint64_t n_final = steps == 1 ? f0.size() : E.snap.nv;
   std::vector<uint64_t> region(over.size()), blk_cap(over.size()), ebound(over.size());
   uint64_t cap_rows = 0;
   for (size_t i = 0; i < over.size(); ++i) {
     auto it = E.snap.types.find(over[i]);
     uint64_t eb = 0;
     if (it != E.snap.types.end()) {
-      if (rq->steps == 1) {
+      if (steps == 1) {
         for (uint32_t d : f0) eb += std::min<uint64_t>(it->second.h_row_ptr[d + 1] - it->second.h_row_ptr[d], cap);
       } else {
         eb = it->second.num_edges;
@@ -288,10 +321,10 @@ static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_row
     cap_rows += blk_cap[i] * ws_final_grid(n_final, eb);
   }
   hipError_t he = ws_reserve_rows(ws, cap_rows, ncols);
-  if (he == hipSuccess) he = ws_begin_query(ws, f0.data(), f0.size(), &plist);
+  if (he == hipSuccess) he = ws_begin_query(ws, f0.data(), f0.size(), &plist, st->id);
   uint64_t n_bound = f0.size();
-  for (uint32_t s = 1; he == hipSuccess && s <= rq->steps; ++s) {
-    const bool final = s == rq->steps;
+  for (uint32_t s = 1; he == hipSuccess && s <= steps; ++s) {
+    const bool final = s == steps;
     for (size_t i = 0; he == hipSuccess && i < over.size(); ++i) {
       auto it = E.snap.types.find(over[i]);
       if (it == E.snap.types.end()) continue;
@@ -335,13 +368,13 @@ static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_row
       for (size_t i = 0; i < over.size(); ++i) g_e[s] += q.e_st[s][i];
     }
   }
-  for (uint32_t s = 1; s <= rq->steps; ++s) {
+  for (uint32_t s = 1; s <= steps; ++s) {
     rows->step_frontier.push_back(g_n[s]);
     rows->step_edges.push_back(g_e[s]);
     rows->scanned += g_e[s];
   }
-  const bool reached_final = g_n[rq->steps] > 0;
-  if (reached_final && deferred) { delete rows; return E.fail(deferred, deferred_msg); }
+  const bool reached_final = g_n[steps] > 0;
+  if (reached_final && deferred) { delete rows; return E.fail(deferred, st->deferred_msg); }
   if (g_err) { delete rows; return E.fail(NBG_E_EXECUTION_ERROR, "WHERE/YIELD evaluation error"); }
   for (size_t i = 0; i < over.size(); ++i) {
     rows->kinds.push_back(plist[i].yield_kind);
@@ -366,6 +399,16 @@ static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_row
   }
   *out = rows;
   return NBG_OK;
+}
+
+static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_rows** out) {
+  std::lock_guard<std::mutex> lg(E.mu);
+  nbg_go_stmt* st = nullptr;
+  int32_t rc = go_prepare(E, rq, &st);
+  if (rc) return rc;
+  rc = go_execute(E, st, rq->starts, rq->num_starts, device, out);
+  delete st;
+  return rc;
 }
 
 // ============================================================================= C ABI
@@ -485,6 +528,20 @@ int32_t nbg_go_device(nbg_engine* h, const nbg_go_request* req, nbg_rows** out) 
   if (!h) return NBG_E_INVALID_ARGUMENT;
   return go_impl(h->e, req, true, out);
 }
+
+int32_t nbg_go_prepare(nbg_engine* h, const nbg_go_request* req, nbg_go_stmt** out) {
+  if (!h) return NBG_E_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lg(h->e.mu);
+  return go_prepare(h->e, req, out);
+}
+
+int32_t nbg_go_execute(nbg_go_stmt* st, const int64_t* starts, uint64_t num_starts, int32_t device, nbg_rows** out) {
+  if (!st || !st->eng) return NBG_E_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lg(st->eng->mu);
+  return go_execute(*st->eng, st, starts, num_starts, device != 0, out);
+}
+
+void nbg_go_stmt_free(nbg_go_stmt* st) { delete st; }
 
 int64_t nbg_rows_count(const nbg_rows* r) { return r ? (int64_t)r->count : -1; }
 int32_t nbg_rows_num_cols(const nbg_rows* r) { return r ? r->ncols : -1; }

@@ -44,6 +44,12 @@ static const char* const kKernelNames[K_COUNT] = {"k_relist", "k_expand<MARK>", 
                                                   "k_stamp", "k_pack_bits", "alltoall(xGMI)", "k_bits_compact"};
 constexpr int BITS_BLOCK = BLOCK * 16;           // k_bits_compact: vertices (bits) per block
 
+constexpr int INLINE_STARTS = 32;
+struct InlineIds {                 // a short start list passed by value in the kernel arguments
+  uint32_t n;
+  uint32_t id[INLINE_STARTS];
+};
+
 struct Prof {
   bool on = false;
   uint32_t mask = ~0u;     // kernels timed (bit per KernelId)
@@ -81,6 +87,10 @@ struct Workspace {
   bool seg_ready = false;          // the compaction list carries the first OVER type's edge space
   const unsigned long long* list_acc = nullptr;   // packed size of frontier[cur] (null: q->n, plain)
   int pr = 0, pc = 0;              // ping-pong parity of the relist / compaction accumulators
+  uint64_t start_n = 0;            // step-1 list: start ids (inline in the kernel arguments when short)
+  bool start_inline = false;
+  InlineIds inl{};
+  uint64_t prog_stmt = 0;          // statement whose programs d_prog holds
   QState* q = nullptr;            // device query state
   QState* h_q = nullptr;          // pinned host mirror
   uint32_t* h_starts = nullptr;   // pinned staging for start ids
@@ -216,9 +226,19 @@ __device__ __forceinline__ void list_put(const ListOut& o, const DegSrc& ds, uin
 // with edges over one CSR.  Entries without edges are dropped (they expand to nothing).
 constexpr int RL_ITEMS = 8;
 constexpr int RL_TILE = BLOCK * RL_ITEMS;
+// Input count: *in_n (packed when in_packed), or n_val when in_n is null; ids: in[], or the
+// start ids inside the kernel arguments when in is null (n_val <= INLINE_STARTS).
 __global__ void __launch_bounds__(BLOCK) k_relist(const uint32_t* __restrict__ in, const unsigned long long* in_n,
-                                                  int in_packed, DegSrc ds, ListOut o, unsigned long long* reset) {
-  const uint64_t n = in_packed ? (*in_n >> 32) : *in_n;
+                                                  int in_packed, uint32_t n_val, InlineIds inl, DegSrc ds, ListOut o,
+                                                  unsigned long long* reset) {
+  __shared__ uint32_t sIn[INLINE_STARTS];
+  const uint64_t n = in_n ? (in_packed ? (*in_n >> 32) : *in_n) : n_val;
+  if (!in) {   // uniform: stage the inline ids (constant indices only, no scratch)
+#pragma unroll
+    for (int k = 0; k < INLINE_STARTS; ++k)
+      if (threadIdx.x == k) sIn[k] = inl.id[k];
+    __syncthreads();
+  }
   if (blockIdx.x == 0) {
     if (threadIdx.x == 0) {
       *o.zero_next = 0;
@@ -232,7 +252,7 @@ __global__ void __launch_bounds__(BLOCK) k_relist(const uint32_t* __restrict__ i
   uint32_t c = 0, d = 0;
 #pragma unroll
   for (int k = 0; k < RL_ITEMS; ++k) {
-    v[k] = base + k < n ? in[base + k] : NO_ROW;
+    v[k] = base + k < n ? (in ? in[base + k] : sIn[base + k]) : NO_ROW;
     dg[k] = vdeg(ds, v[k], &rs[k]);
     c += dg[k] ? 1u : 0u;
     d += dg[k];
@@ -884,13 +904,17 @@ Workspace* ws_create(uint64_t max_frontier, uint64_t nv, uint64_t e_max, hipStre
   M((void**)&w->flags, w->flag_bytes);
   w->cap_tiles = cdiv(w->cap_frontier + e_max + 1, TILE) + 2;
   M((void**)&w->tsplit, w->cap_tiles * 4);
-  M((void**)&w->blk_rows, (size_t)MAX_TYPES_Q * EXPAND_GRID * 4);
-  M((void**)&w->q, sizeof(QState));
+  // QState and the per-workgroup row counts are one allocation: one copy ends a query
+  M((void**)&w->q, sizeof(QState) + (size_t)MAX_TYPES_Q * EXPAND_GRID * 4);
   M((void**)&w->d_prog, (size_t)MAX_TYPES_Q * MAX_PROGRAM * sizeof(Ins));
   M((void**)&w->d_row_cols, MAX_YIELDS * sizeof(int64_t*));
-  if (e == hipSuccess) e = hipHostMalloc((void**)&w->h_q, sizeof(QState), hipHostMallocDefault);
   if (e == hipSuccess)
-    e = hipHostMalloc((void**)&w->h_blk_rows, (size_t)MAX_TYPES_Q * EXPAND_GRID * 4, hipHostMallocDefault);
+    e = hipHostMalloc((void**)&w->h_q, sizeof(QState) + (size_t)MAX_TYPES_Q * EXPAND_GRID * 4, hipHostMallocDefault);
+  if (e == hipSuccess) {
+    w->blk_rows = reinterpret_cast<uint32_t*>(w->q + 1);
+    w->h_blk_rows = reinterpret_cast<uint32_t*>(w->h_q + 1);
+    e = hipMemsetAsync(w->q, 0, sizeof(QState), s);
+  }
   if (e == hipSuccess) e = hipHostMalloc((void**)&w->h_prog, (size_t)MAX_TYPES_Q * MAX_PROGRAM * sizeof(Ins),
                                          hipHostMallocDefault);
   if (e == hipSuccess) e = hipMemsetAsync(w->flags, 0, w->flag_bytes, s);
@@ -906,11 +930,11 @@ Workspace* ws_create(uint64_t max_frontier, uint64_t nv, uint64_t e_max, hipStre
 void ws_destroy(Workspace* w) {
   if (!w) return;
   for (void* p : {(void*)w->frontier[0], (void*)w->frontier[1], (void*)w->seg_end, (void*)w->seg_rs,
-                  (void*)w->rlist, (void*)w->flags, (void*)w->tsplit, (void*)w->blk_rows,
+                  (void*)w->rlist, (void*)w->flags, (void*)w->tsplit,
                   (void*)w->q, (void*)w->rows,
                   (void*)w->d_row_cols, (void*)w->d_prog})
     if (p) (void)hipFree(p);
-  for (void* p : {(void*)w->h_q, (void*)w->h_blk_rows, (void*)w->h_starts, (void*)w->h_prog, (void*)w->h_ps, (void*)w->h_path,
+  for (void* p : {(void*)w->h_q, (void*)w->h_starts, (void*)w->h_prog, (void*)w->h_ps, (void*)w->h_path,
                   (void*)w->h_stage})
     if (p) (void)hipHostFree(p);
   for (void* p : {(void*)w->sendbits, (void*)w->recvbits, (void*)w->gst})
@@ -952,26 +976,34 @@ hipError_t ws_reserve_rows(Workspace* w, uint64_t rows, int ncols) {
   return hipSuccess;
 }
 
-hipError_t ws_begin_query(Workspace* w, const uint32_t* starts, uint64_t n, const std::vector<TypeProgram>* progs) {
+// The device QState is already zero (reset behind the previous query's final copy).  A short
+// start list travels inside the first kernel's arguments: a query then begins with a launch, not
+// a copy.  Programs are uploaded when the statement changes.
+hipError_t ws_begin_query(Workspace* w, const uint32_t* starts, uint64_t n, const std::vector<TypeProgram>* progs,
+                          uint64_t stmt_id) {
   if (n > w->cap_frontier) return hipErrorInvalidValue;
-  if (n > w->cap_starts) {
-    if (w->h_starts) HIP_TRY(hipHostFree(w->h_starts));
-    w->cap_starts = n + n / 2 + 1024;
-    HIP_TRY(hipHostMalloc((void**)&w->h_starts, w->cap_starts * 4, hipHostMallocDefault));
-  }
-  // the previous query on this workspace has completed (its end synchronised the stream)
-  memcpy(w->h_starts, starts, n * 4);
-  memset(w->h_q, 0, sizeof(QState));
-  w->h_q->n = n;
-  w->h_q->step_n[1] = n;
   w->cur = 0;
   w->seg_ready = false;
   w->list_acc = nullptr;
   w->pr = w->pc = 0;
   for (auto& g : w->final_grid) g = 0;
-  HIP_TRY(hipMemcpyAsync(w->frontier[0], w->h_starts, n * 4, hipMemcpyHostToDevice, w->stream));
-  HIP_TRY(hipMemcpyAsync(w->q, w->h_q, sizeof(QState), hipMemcpyHostToDevice, w->stream));
-  if (progs && !progs->empty()) {
+  w->start_n = n;
+  w->start_inline = n <= INLINE_STARTS;
+  if (w->start_inline) {
+    w->inl.n = (uint32_t)n;
+    for (uint64_t i = 0; i < n; ++i) w->inl.id[i] = starts[i];
+  } else {
+    if (n > w->cap_starts) {
+      if (w->h_starts) HIP_TRY(hipHostFree(w->h_starts));
+      w->cap_starts = n + n / 2 + 1024;
+      HIP_TRY(hipHostMalloc((void**)&w->h_starts, w->cap_starts * 4, hipHostMallocDefault));
+    }
+    // the previous query on this workspace has completed (its end synchronised the stream)
+    memcpy(w->h_starts, starts, n * 4);
+    HIP_TRY(hipMemcpyAsync(w->frontier[0], w->h_starts, n * 4, hipMemcpyHostToDevice, w->stream));
+  }
+  if (progs && !progs->empty() && stmt_id != w->prog_stmt) {
+    w->prog_stmt = stmt_id;
     size_t k = 0;
     for (auto& p : *progs) {
       memcpy(w->h_prog + k * MAX_PROGRAM, p.code.data(), p.code.size() * sizeof(Ins));
@@ -1019,13 +1051,12 @@ static ListRef prepare_list(Workspace* w, const ExpandArgs& a, uint64_t n_bound,
   unsigned long long* acc = &w->q->acc[w->pr];
   unsigned long long* other = &w->q->acc[w->pr ^ 1];
   w->pr ^= 1;
-  const bool packed = w->list_acc != nullptr;
-  const unsigned long long* in_n = packed ? w->list_acc : &w->q->n;
+  const bool first = w->list_acc == nullptr;   // the start list
+  const uint32_t* in = first && w->start_inline ? nullptr : w->frontier[w->cur];
   hipEvent_t p = prof_begin(w, K_RELIST);
-  hipLaunchKernelGGL(k_relist, dim3((unsigned)cdiv(n_bound ? n_bound : 1, RL_TILE)), dim3(BLOCK), 0, w->stream,
-                     w->frontier[w->cur], in_n, (int)packed, deg_of(a),
-                     list_out(w, w->rlist, acc, other, step > 1 ? &w->q->step_n[step] : nullptr),
-                     (unsigned long long*)nullptr);
+  hipLaunchKernelGGL(k_relist, dim3((unsigned)cdiv(n_bound ? n_bound : 1, RL_TILE)), dim3(BLOCK), 0, w->stream, in,
+                     w->list_acc, 1, (uint32_t)w->start_n, w->inl, deg_of(a),
+                     list_out(w, w->rlist, acc, other, &w->q->step_n[step]), (unsigned long long*)nullptr);
   prof_end(w, p, K_RELIST, step, tix);
   return ListRef{w->rlist, acc, nullptr};
 }
@@ -1213,14 +1244,14 @@ hipError_t ws_fetch_rows(Workspace* w, const std::vector<std::pair<uint64_t, uin
 }
 
 hipError_t ws_end_query(Workspace* w) {
-  HIP_TRY(hipMemcpyAsync(w->h_q, w->q, sizeof(QState), hipMemcpyDeviceToHost, w->stream));
   int nt = 0;
   for (int t = 0; t < MAX_TYPES_Q; ++t)
     if (w->final_grid[t]) nt = t + 1;
-  if (nt)
-    HIP_TRY(hipMemcpyAsync(w->h_blk_rows, w->blk_rows, (size_t)nt * EXPAND_GRID * 4, hipMemcpyDeviceToHost,
-                           w->stream));
+  HIP_TRY(hipMemcpyAsync(w->h_q, w->q, sizeof(QState) + (size_t)nt * EXPAND_GRID * 4, hipMemcpyDeviceToHost,
+                         w->stream));
   HIP_TRY(hipStreamSynchronize(w->stream));
+  // reset for the next query; runs while the host reads the results
+  HIP_TRY(hipMemsetAsync(w->q, 0, sizeof(QState), w->stream));
   prof_flush(w, w->h_q);
   return hipSuccess;
 }
@@ -1629,7 +1660,7 @@ hipError_t ws_path_level(Workspace* w, const PathTypes& pt, int src, uint64_t n_
     w->ppr ^= 1;
     hipEvent_t p = prof_begin_p(w, K_RELIST);
     hipLaunchKernelGGL(k_relist, dim3((unsigned)cdiv(n_bound ? n_bound : 1, RL_TILE)), dim3(BLOCK), 0, w->stream,
-                       w->slot[src], &w->ps->n[src], 0, deg_of(a),
+                       w->slot[src], &w->ps->n[src], 0, 0u, InlineIds{}, deg_of(a),
                        list_out(w, w->rlist, acc, other, t == 0 ? &w->ps->ln[rec] : nullptr),
                        t == 0 ? w->ps->shard : (unsigned long long*)nullptr);
     prof_end_p(w, p, K_RELIST, rec);

@@ -253,7 +253,8 @@ const QState* ws_host_state(Workspace* w);       // valid after ws_end_query
 const uint32_t* ws_current_frontier(Workspace* w);
 
 // Query pipeline (all asynchronous on the workspace stream until ws_end_query):
-hipError_t ws_begin_query(Workspace* w, const uint32_t* starts, uint64_t n, const std::vector<TypeProgram>* progs);
+hipError_t ws_begin_query(Workspace* w, const uint32_t* starts, uint64_t n, const std::vector<TypeProgram>* progs,
+                          uint64_t stmt_id);
 // steps 1..N-1, per OVER type: scan + expand into next-frontier flags
 hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a, uint64_t n_bound, uint64_t e_bound, int step, int tix);
 // after all types of a step: flags -> next frontier

@@ -67,6 +67,48 @@ class DeviceRows:
         self.free()
 
 
+class GoStatement:
+    """A prepared GO statement (nbg_go_prepare / nbg_go_execute)."""
+
+    def __init__(self, eng, h):
+        self.eng, self.h = eng, h
+        self._buf = (C.c_int64 * 64)()
+
+    def _starts(self, starts):
+        n = len(starts)
+        if n <= len(self._buf):
+            for i, v in enumerate(starts):
+                self._buf[i] = v
+            return self._buf, n
+        a = np.ascontiguousarray(starts, np.int64)
+        self._keep = a
+        return a.ctypes.data_as(C.POINTER(C.c_int64)), n
+
+    def run_device(self, starts) -> DeviceRows:
+        ptr, n = self._starts(starts)
+        out = C.c_void_p()
+        self.eng._check(self.eng.lib.nbg_go_execute(self.h, ptr, n, 1, C.byref(out)), "go_execute")
+        return DeviceRows(self.eng, out)
+
+    def run(self, starts):
+        ptr, n = self._starts(starts)
+        out = C.c_void_p()
+        self.eng._check(self.eng.lib.nbg_go_execute(self.h, ptr, n, 0, C.byref(out)), "go_execute")
+        try:
+            return self.eng._host_rows(out)
+        finally:
+            self.eng.lib.nbg_rows_free(out)
+
+    def free(self):
+        if self.h:
+            self.eng.lib.nbg_go_stmt_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        if getattr(self, "eng", None) is not None and getattr(self.eng, "h", None):
+            self.free()
+
+
 class Engine:
     def __init__(self, num_parts: int, num_gpus: int = 1, rank: int = 0, device: int = 0,
                  max_edge_returned_per_vertex: int = 0x7FFFFFFF):
@@ -209,6 +251,13 @@ class Engine:
         rc = self.lib.nbg_go_device(self.h, C.byref(req), C.byref(out))
         self._check(rc, "go_device")
         return DeviceRows(self, out)
+
+    def prepare_go(self, etypes, steps=1, where=b"", yields=(), distinct=False, over_all=False) -> "GoStatement":
+        """GoExecutor::prepare() once; ``GoStatement.run*`` executes it from start lists."""
+        req, keep = self._go_request([], etypes, steps, where, yields, distinct, over_all)
+        out = C.c_void_p()
+        self._check(self.lib.nbg_go_prepare(self.h, C.byref(req), C.byref(out)), "go_prepare")
+        return GoStatement(self, out)
 
     # ------------------------------------------------------------------ FIND PATH
     def find_path(self, frm, to, etypes, upto=5, shortest=True, over_all=False, stats=None):

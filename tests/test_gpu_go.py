@@ -129,3 +129,42 @@ def test_device_rows_stay_in_hbm(rmat12):
     assert len(rows) == n
     assert graphs.sorted_rows(rows) == graphs.sorted_rows(orc.go(r, [1], 3, WHERES["w<50"].encode()))
     dev.free()
+
+
+def test_prepared_statements_interleaved(rmat12):
+    """GoExecutor prepare/execute split: two prepared statements with interpreter (generic)
+    programs run alternately from inline (<= 32) and long start lists; rows equal the oracle's."""
+    src, eng, orc = rmat12
+    w1 = WHERES["w*1.5>=60.0"].encode()
+    w2 = WHERES["w%7==3||w>=90"].encode()
+    ys = [E.edge_prop("e", "_src").encode(), E.binop("+", E.edge_prop("e", "w"), E.const(1)).encode()]
+    s1 = eng.prepare_go([1], 2, w1, ys)
+    s2 = eng.prepare_go([1], 3, w2)
+    roots = graphs.roots(src, 40, seed=21)
+    for k in range(3):
+        starts = roots[: 1 + 19 * k]          # 1, 20, 39 starts: inline and copied start lists
+        got1 = graphs.sorted_rows(s1.run(starts))
+        got2 = graphs.sorted_rows(s2.run(starts))
+        assert got1 == graphs.sorted_rows(orc.go(starts, [1], 2, w1, ys))
+        assert got2 == graphs.sorted_rows(orc.go(starts, [1], 3, w2))
+    s1.free()
+    s2.free()
+
+
+def test_device_rows_segments_cover_count(rmat12):
+    src, eng, orc = rmat12
+    stmt = eng.prepare_go([1], 3, WHERES["w<50"].encode())
+    r = graphs.roots(src, 1, seed=2)[0]
+    res = stmt.run_device([r])
+    n = eng.lib.nbg_rows_num_segments(res.h)
+    spans = []
+    for i in range(n):
+        b, e = _lib.u64(), _lib.u64()
+        assert eng.lib.nbg_rows_segment(res.h, i, b, e) == 0
+        spans.append((b.value, e.value))
+    spans.sort()
+    assert sum(e - b for b, e in spans) == res.count
+    assert all(spans[i][1] <= spans[i + 1][0] for i in range(len(spans) - 1))
+    assert len(res.fetch()) == res.count
+    res.free()
+    stmt.free()
