@@ -285,6 +285,7 @@ static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* start
     a.visible = E.snap.d_visible;
     a.vids = E.snap.d_vids;
     a.props = dt.d_props;
+    a.hprops = dt.props.data();
     a.cap = cap;
     return a;
   };

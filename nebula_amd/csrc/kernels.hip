@@ -300,24 +300,14 @@ __global__ void __launch_bounds__(CP_THREADS) k_compact(uint8_t* __restrict__ fl
 // interpreter, no LDS registers; the generic bytecode path handles everything else.
 struct FastProg {
   int enabled;
-  int where_col;           // -1: no WHERE
-  int where_op;            // 0 LT 1 LE 2 GT 3 GE 4 EQ 5 NE (int64)
-  int64_t where_const;
+  int has_where;
+  int where_neg;           // pass = (lo <= x && x <= hi) != where_neg   (branch-free `col <op> const`)
+  int64_t lo, hi;
+  const int64_t* wcol;     // WHERE column (device pointer, resolved on the host)
   int ykind[MAX_YIELDS];   // 0 DST, 1 SRC, 2 RANK, 3 COL, 4 CONST
-  int ycol[MAX_YIELDS];
+  const int64_t* ycol[MAX_YIELDS];
   int dst_yield;           // some YIELD is _dst
 };
-
-__device__ __forceinline__ bool cmp_i(int op, int64_t x, int64_t y) {
-  switch (op) {
-    case 0: return x < y;
-    case 1: return x <= y;
-    case 2: return x > y;
-    case 3: return x >= y;
-    case 4: return x == y;
-    default: return x != y;
-  }
-}
 
 // ----------------------------------------------------------------------------- bytecode
 struct EdgeCtx {
@@ -434,13 +424,35 @@ struct FinalParams {
   int nyields;
   int yield_reg[MAX_YIELDS];
   int64_t yield_const[MAX_YIELDS];
-  int64_t** out_cols;
+  int64_t* out_cols[MAX_YIELDS];   // by value: global stores, no pointer loads per row
   uint64_t region_base;   // first row of this type's region
   uint64_t blk_cap;       // rows per workgroup region (each workgroup appends to its own region)
   uint32_t* blk_rows;     // [gridDim.x] rows written per workgroup
   unsigned long long* err_flag;
   FastProg fast;
 };
+
+// Merge-path split of tile t: entries consumed before position t * TILE (which 0) or before the
+// tile's end (which 1).
+__device__ __forceinline__ uint64_t tile_split(const uint32_t* __restrict__ tsplit, uint64_t t, int which,
+                                               uint64_t npath, uint64_t n) {
+  if (which == 0) return tsplit[t];
+  return (t + 1) * TILE >= npath ? n : tsplit[t + 1];
+}
+
+// Entry threadIdx.x of a tile's window: seg_end[a0 - 1 + k] (k <= na + 1) and seg_rs[a0 + k].
+__device__ __forceinline__ void stage_pre(const uint32_t* __restrict__ seg_end, const uint32_t* __restrict__ seg_rs,
+                                          uint64_t n, uint64_t a0, uint64_t a1, uint32_t* e, uint32_t* r) {
+  const int k = threadIdx.x, na = (int)(a1 - a0);
+  if (k <= na + 1) {
+    const int64_t i = (int64_t)a0 - 1 + k;
+    *e = i < 0 ? 0u : (i < (int64_t)n ? seg_end[i] : 0xFFFFFFFFu);
+  }
+  if (k <= na) {
+    const uint64_t i = a0 + k;
+    *r = i < n ? seg_rs[i] : 0u;
+  }
+}
 
 template <int M>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M == FINAL ? 4 : 8))) k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc,
@@ -472,25 +484,50 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M ==
   constexpr bool kFast = M == FINALF;
   if (kFinal && threadIdx.x == 0) sBase = 0;
 
-  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  // Software pipeline over this workgroup's tiles t, t + g, t + 2g, ...: while tile t is
+  // processed, the split of tile t + 2g and the first BLOCK segment ends / row starts of tile
+  // t + g are already in flight (registers), so a tile starts with an LDS fill instead of two
+  // dependent global round trips.
+  const uint64_t g = gridDim.x;
+  uint64_t t = blockIdx.x;
+  uint64_t sp_next = 0;            // threads 0, 1: split (start, end) of tile t + g
+  uint64_t a0 = 0, a1 = 0;         // split of tile t
+  uint32_t e_pre = 0, r_pre = 0;   // entry threadIdx.x of tile t's segment-end window / row starts
+  if (t < ntiles) {
+    if (threadIdx.x < 2) {
+      sSplit[threadIdx.x] = tile_split(a.tsplit, t, threadIdx.x, npath, n);
+      if (t + g < ntiles) sp_next = tile_split(a.tsplit, t + g, threadIdx.x, npath, n);
+    }
+    __syncthreads();
+    a0 = sSplit[0];
+    a1 = sSplit[1];
+    stage_pre(seg_end, seg_rs, n, a0, a1, &e_pre, &r_pre);
+    __syncthreads();   // sSplit is rewritten in the loop
+  }
+  for (; t < ntiles; t += g) {
     const uint64_t d0 = t * TILE;
     const uint64_t d1 = (d0 + TILE < npath) ? d0 + TILE : npath;
-    if (threadIdx.x < 2) sSplit[threadIdx.x] = threadIdx.x == 0 ? a.tsplit[t] : (d1 == npath ? n : a.tsplit[t + 1]);
-    __syncthreads();
-    const uint64_t a0 = sSplit[0], a1 = sSplit[1];
     const uint64_t b0 = d0 - a0, b1 = d1 - a1;
     const int na = (int)(a1 - a0), nb = (int)(b1 - b0);
 
-    // stage the tile's segment ends / row starts in LDS
-    for (int k = threadIdx.x; k <= na + 1; k += BLOCK) {
-      int64_t i = (int64_t)a0 - 1 + k;
-      sEnd[k] = (i < 0) ? 0u : (i < (int64_t)n ? seg_end[i] : 0xFFFFFFFFu);
+    // stage the tile's segment ends / row starts in LDS (entries past the prefetch directly)
+    if ((int)threadIdx.x <= na + 1) sEnd[threadIdx.x] = e_pre;
+    if ((int)threadIdx.x <= na) sRs[threadIdx.x] = r_pre;
+    for (int k = threadIdx.x + BLOCK; k <= na + 1; k += BLOCK) {
+      const uint64_t i = a0 - 1 + (uint64_t)k;
+      sEnd[k] = i < n ? seg_end[i] : 0xFFFFFFFFu;
+      if (k <= na) sRs[k] = i + 1 < n ? seg_rs[i + 1] : 0u;
     }
-    for (int k = threadIdx.x; k <= na; k += BLOCK) {
-      uint64_t i = a0 + k;
-      sRs[k] = i < n ? seg_rs[i] : 0u;
-    }
+    if (threadIdx.x < 2) sSplit[threadIdx.x] = sp_next;
     __syncthreads();
+    // prefetch tile t + g's window and tile t + 2g's split
+    uint64_t na0 = 0, na1 = 0;
+    if (t + g < ntiles) {
+      na0 = sSplit[0];
+      na1 = sSplit[1];
+      stage_pre(seg_end, seg_rs, n, na0, na1, &e_pre, &r_pre);
+      if (threadIdx.x < 2 && t + 2 * g < ntiles) sp_next = tile_split(a.tsplit, t + 2 * g, threadIdx.x, npath, n);
+    }
     const uint32_t* A = sEnd + 1;   // A[k] = end of segment a0 + k
 
     // thread-level merge path over this tile: assign a segment to every edge item
@@ -521,13 +558,19 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M ==
     __syncthreads();
 
     if (M == MARK) {
-      for (int k = threadIdx.x; k < nb; k += BLOCK) {
-        uint32_t s = sSeg[k];
-        uint64_t e = b0 + k;
-        uint64_t j = (uint64_t)sRs[s] + (e - (uint64_t)sEnd[s]);   // sEnd[s] = start of segment a0+s
-        uint32_t u = a.col[j];
-        if (u != NO_ROW) flags[u] = 1;
+      uint32_t u[VT];   // all neighbour loads in flight before the flag stores
+#pragma unroll
+      for (int i = 0; i < VT; ++i) {
+        const int k = i * BLOCK + threadIdx.x;
+        u[i] = NO_ROW;
+        if (k < nb) {
+          const uint32_t s = sSeg[k];
+          u[i] = a.col[(uint64_t)sRs[s] + (b0 + k - (uint64_t)sEnd[s])];   // sEnd[s] = start of a0+s
+        }
       }
+#pragma unroll
+      for (int i = 0; i < VT; ++i)
+        if (u[i] != NO_ROW) flags[u[i]] = 1;
     } else if (M == BFS) {
       uint32_t wv[VT];
       uint32_t cmask = 0, mmask = 0;
@@ -588,7 +631,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M ==
       }
     } else {
       // phase A: WHERE for every item of the tile (VT items per thread, striped)
-      uint64_t jj[VT];
+      uint32_t jj[VT];      // edge index in the CSR (< 2^32 per type)
       uint32_t vv[VT];
       int64_t dv[VT];       // fast path: _dst prefetched with the WHERE column (one round trip)
       uint32_t pmask = 0;
@@ -599,27 +642,25 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M ==
         vv[i] = 0;
         if (k < nb) {
           uint32_t s = sSeg[k];
-          jj[i] = (uint64_t)sRs[s] + (b0 + k - (uint64_t)sEnd[s]);
+          jj[i] = sRs[s] + (uint32_t)(b0 + k - (uint64_t)sEnd[s]);
           vv[i] = s;
         }
       }
       if (kFast) {
-        if (fp.fast.dst_yield) {
+        // all loads of the tile in flight at once; the comparison is branch-free
+        int64_t x[VT];
 #pragma unroll
-          for (int i = 0; i < VT; ++i) dv[i] = (i * BLOCK + (int)threadIdx.x < nb) ? a.dst_vid[jj[i]] : 0;
+        for (int i = 0; i < VT; ++i) {
+          const bool act = i * BLOCK + (int)threadIdx.x < nb;
+          dv[i] = (act && fp.fast.dst_yield) ? a.dst_vid[jj[i]] : 0;
+          x[i] = (act && fp.fast.has_where) ? fp.fast.wcol[jj[i]] : 0;
         }
-        if (fp.fast.where_col < 0) {
 #pragma unroll
-          for (int i = 0; i < VT; ++i) pmask |= (uint32_t)(i * BLOCK + (int)threadIdx.x < nb) << i;
-        } else {
-          const int64_t* __restrict__ wc = a.props[fp.fast.where_col];
-          int64_t x[VT];
-#pragma unroll
-          for (int i = 0; i < VT; ++i) x[i] = (i * BLOCK + (int)threadIdx.x < nb) ? wc[jj[i]] : 0;
-#pragma unroll
-          for (int i = 0; i < VT; ++i)
-            pmask |= (uint32_t)((i * BLOCK + (int)threadIdx.x < nb) && cmp_i(fp.fast.where_op, x[i],
-                                                                               fp.fast.where_const)) << i;
+        for (int i = 0; i < VT; ++i) {
+          const bool act = i * BLOCK + (int)threadIdx.x < nb;
+          const bool in = (x[i] >= fp.fast.lo) & (x[i] <= fp.fast.hi);
+          const bool pass = act & (!fp.fast.has_where | (in != (fp.fast.where_neg != 0)));
+          pmask |= (uint32_t)pass << i;
         }
       } else {
         for (int i = 0; i < VT; ++i) {
@@ -657,7 +698,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M ==
       __syncthreads();
       // phase B: YIELD for the passing items, written at their final rows
       const uint64_t region = fp.region_base + (uint64_t)blockIdx.x * fp.blk_cap + sTileBase;
-      int64_t* const* cols = fp.out_cols;
+      int64_t* const* cols = fp.out_cols;   // kernel-argument array (constant indices after unroll)
       for (int i = 0; i < VT; ++i) {
         const bool pass = (pmask >> i) & 1u;
         unsigned long long bal = __ballot(pass);
@@ -671,7 +712,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M ==
                 case 0: val = dv[i]; break;
                 case 1: val = a.vids[a.frontier[a0 + vv[i]]]; break;
                 case 2: val = a.rank ? a.rank[jj[i]] : 0; break;
-                case 3: val = a.props[fp.fast.ycol[y]][jj[i]]; break;
+                case 3: val = fp.fast.ycol[y][jj[i]]; break;
                 default: val = fp.yield_const[y]; break;
               }
 #ifndef NBG_EXP_NOSTORE   // timing experiment only
@@ -696,6 +737,8 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M ==
       }
     }
     __syncthreads();   // LDS reuse by the next tile
+    a0 = na0;
+    a1 = na1;
   }
   if (kFinal) {
     if (threadIdx.x == 0) fp.blk_rows[blockIdx.x] = (uint32_t)sBase;
@@ -1113,9 +1156,8 @@ static int edge_columns_read(const TypeProgram& prog) {
 static FastProg detect_fast(const TypeProgram& prog, const ExpandArgs& a) {
   FastProg f{};
   f.enabled = 0;
-  f.where_col = -1;
   auto leaf_col = [&](const Ins& i) {
-    return i.op == OP_COL || (i.op == OP_COLV && a.valid == nullptr);
+    return (i.op == OP_COL || (i.op == OP_COLV && a.valid == nullptr)) && a.hprops != nullptr;
   };
   if (prog.where_reg >= 0) {
     if (prog.where_len != 3) return f;
@@ -1131,11 +1173,26 @@ static FastProg detect_fast(const TypeProgram& prog, const ExpandArgs& a) {
     if (leaf_col(i0) && i1.op == OP_CONST) { colI = &i0; constI = &i1; }
     else if (i0.op == OP_CONST && leaf_col(i1)) { colI = &i1; constI = &i0; }
     else return f;
-    if (c.a == colI->d && c.b == constI->d) f.where_op = op;
-    else if (c.a == constI->d && c.b == colI->d) f.where_op = kSwap[op];
-    else return f;
-    f.where_col = colI->aux;
-    f.where_const = constI->imm;
+    if (c.a == colI->d && c.b == constI->d) {
+    } else if (c.a == constI->d && c.b == colI->d) {
+      op = kSwap[op];
+    } else {
+      return f;
+    }
+    // col <op> k  as the range test lo <= x <= hi (negated for !=)
+    const int64_t k = constI->imm;
+    f.lo = INT64_MIN;
+    f.hi = INT64_MAX;
+    switch (op) {
+      case 0: if (k == INT64_MIN) { f.lo = 1; f.hi = 0; } else f.hi = k - 1; break;   // <
+      case 1: f.hi = k; break;                                                        // <=
+      case 2: if (k == INT64_MAX) { f.lo = 1; f.hi = 0; } else f.lo = k + 1; break;   // >
+      case 3: f.lo = k; break;                                                        // >=
+      case 4: f.lo = f.hi = k; break;                                                 // ==
+      default: f.lo = f.hi = k; f.where_neg = 1; break;                               // !=
+    }
+    f.has_where = 1;
+    f.wcol = a.hprops[colI->aux];
   }
   const int ny = (int)prog.yield_reg.size();
   int pc = prog.where_len;
@@ -1147,7 +1204,7 @@ static FastProg detect_fast(const TypeProgram& prog, const ExpandArgs& a) {
     if (i.op == OP_DST) { f.ykind[y] = 0; f.dst_yield = 1; }
     else if (i.op == OP_SRC) f.ykind[y] = 1;
     else if (i.op == OP_RANK) f.ykind[y] = 2;
-    else if (leaf_col(i)) { f.ykind[y] = 3; f.ycol[y] = i.aux; }
+    else if (leaf_col(i)) { f.ykind[y] = 3; f.ycol[y] = a.hprops[i.aux]; }
     else return f;
   }
   if (pc != (int)prog.code.size()) return f;
@@ -1184,7 +1241,7 @@ hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound,
     fp.yield_reg[y] = prog.yield_reg[y];
     fp.yield_const[y] = prog.yield_const[y];
   }
-  fp.out_cols = w->d_row_cols;
+  for (int y = 0; y < MAX_YIELDS; ++y) fp.out_cols[y] = ws_row_col(w, y < w->ncols_alloc ? y : 0);
   fp.region_base = region_base;
   fp.blk_cap = blk_cap;
   fp.blk_rows = w->blk_rows + (size_t)tix * EXPAND_GRID;

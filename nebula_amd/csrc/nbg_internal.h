@@ -182,7 +182,8 @@ struct ExpandArgs {                // one (step, edge type) expansion
   const int64_t* vids;             // dense id -> vid (for _src)
   const int64_t* const* props;     // device array of column pointers
   uint32_t cap;                    // max_edge_returned_per_vertex
-  const uint32_t* tsplit;          // per-tile merge-path splits (set by the workspace; null: search)
+  const uint32_t* tsplit;          // per-tile merge-path splits (set by the workspace)
+  const int64_t* const* hprops;    // host array of the same column pointers (host-side planning)
 };
 
 // ----------------------------------------------------------------------------- FIND PATH state
