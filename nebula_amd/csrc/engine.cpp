@@ -286,6 +286,8 @@ static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* start
     a.vids = E.snap.d_vids;
     a.props = dt.d_props;
     a.hprops = dt.props.data();
+    a.hnarrow = dt.narrow.empty() ? nullptr : dt.narrow.data();
+    a.hnarrow_bytes = dt.narrow_bytes.empty() ? nullptr : dt.narrow_bytes.data();
     a.cap = cap;
     return a;
   };
@@ -436,6 +438,8 @@ void nbg_destroy(nbg_engine* h) {
                     (void*)d.d_props})
       if (p) (void)hipFree(p);
     for (auto* p : d.props)
+      if (p) (void)hipFree(p);
+    for (auto* p : d.narrow)
       if (p) (void)hipFree(p);
   }
   if (E.snap.d_vids) (void)hipFree(E.snap.d_vids);

@@ -298,14 +298,33 @@ __global__ void __launch_bounds__(CP_THREADS) k_compact(uint8_t* __restrict__ fl
 // Fast path for the common final-step program shape: WHERE absent or `col <cmp> const` on an
 // INT column, YIELD columns that are plain edge fields / key props / constants.  No
 // interpreter, no LDS registers; the generic bytecode path handles everything else.
+__device__ __forceinline__ int64_t load_col(const void* p, int bytes, uint32_t j) {
+  switch (bytes) {   // uniform
+    case 1: return reinterpret_cast<const int8_t*>(p)[j];
+    case 2: return reinterpret_cast<const int16_t*>(p)[j];
+    case 4: return reinterpret_cast<const int32_t*>(p)[j];
+    default: return reinterpret_cast<const int64_t*>(p)[j];
+  }
+}
+
+// VT loads of a column of type T (sign-extended), all in flight at once
+template <typename T>
+__device__ __forceinline__ void load_narrow(const void* p, const uint32_t* jj, int nb, int lane, int64_t* x) {
+  const T* c = reinterpret_cast<const T*>(p);
+#pragma unroll
+  for (int i = 0; i < VT; ++i) x[i] = (i * 64 + lane < nb) ? (int64_t)c[jj[i]] : 0;
+}
+
 struct FastProg {
   int enabled;
   int has_where;
   int where_neg;           // pass = (lo <= x && x <= hi) != where_neg   (branch-free `col <op> const`)
   int64_t lo, hi;
-  const int64_t* wcol;     // WHERE column (device pointer, resolved on the host)
+  const void* wcol;        // WHERE column (device pointer, resolved on the host) ...
+  int wbytes;              // ... at this width (1/2/4: narrow copy of an INT column; 8)
   int ykind[MAX_YIELDS];   // 0 DST, 1 SRC, 2 RANK, 3 COL, 4 CONST
-  const int64_t* ycol[MAX_YIELDS];
+  const void* ycol[MAX_YIELDS];
+  int ybytes[MAX_YIELDS];
   int dst_yield;           // some YIELD is _dst
 };
 
@@ -440,10 +459,10 @@ __device__ __forceinline__ uint64_t tile_split(const uint32_t* __restrict__ tspl
   return (t + 1) * TILE >= npath ? n : tsplit[t + 1];
 }
 
-// Entry threadIdx.x of a tile's window: seg_end[a0 - 1 + k] (k <= na + 1) and seg_rs[a0 + k].
+// Lane k's entry of a tile's window: seg_end[a0 - 1 + k] (k <= na + 1) and seg_rs[a0 + k].
 __device__ __forceinline__ void stage_pre(const uint32_t* __restrict__ seg_end, const uint32_t* __restrict__ seg_rs,
-                                          uint64_t n, uint64_t a0, uint64_t a1, uint32_t* e, uint32_t* r) {
-  const int k = threadIdx.x, na = (int)(a1 - a0);
+                                          uint64_t n, uint64_t a0, uint64_t a1, int k, uint32_t* e, uint32_t* r) {
+  const int na = (int)(a1 - a0);
   if (k <= na + 1) {
     const int64_t i = (int64_t)a0 - 1 + k;
     *e = i < 0 ? 0u : (i < (int64_t)n ? seg_end[i] : 0xFFFFFFFFu);
@@ -454,20 +473,36 @@ __device__ __forceinline__ void stage_pre(const uint32_t* __restrict__ seg_end, 
   }
 }
 
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {   // a wave-uniform value, in SGPRs
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// LDS written by some lanes of a wave and read by others: complete the wave's LDS operations.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Wave-tiled, load-balanced expansion.  Every WAVE owns whole tiles of TILE = 64 * VT merge-path
+// items (frontier entries + edges) and runs them without workgroup barriers: its segment window,
+// merge-path assignment and row offsets live in its own LDS slice and registers, so the 32 waves
+// of a CU progress independently and the memory latency of one is hidden by the others.  While
+// a wave processes tile t, the split of tile t + 2g and the window of tile t + g are in flight
+// (software pipeline, registers).  Items are processed striped across the wave's lanes so
+// neighbour / property reads are coalesced.
 template <int M>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M == FINAL ? 4 : 8))) k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc,
-                                                  const uint32_t* __restrict__ seg_end,
-                                                  const uint32_t* __restrict__ seg_rs, uint8_t* __restrict__ flags,
-                                                  FinalParams fp, BfsParams bp, unsigned long long* stat_e,
-                                                  unsigned long long* stat_n) {
-  __shared__ uint32_t sEnd[TILE + 2];   // seg_end for i in [a0-1, a1]
-  __shared__ uint32_t sRs[TILE + 1];    // seg_rs for i in [a0, a1]
-  __shared__ uint32_t sSeg[TILE];       // segment of each edge item in this tile
-  __shared__ uint32_t sCnt[VT * WAVES]; // FINAL: passing items per (iteration, wave) -> offsets
-  __shared__ uint64_t sSplit[2];
-  __shared__ uint64_t sBase;            // BFS: claim base; FINAL: rows this workgroup wrote so far
-  __shared__ uint64_t sTileBase;        // FINAL: first row of the current tile in the region
-  extern __shared__ int64_t regs[];     // FINAL generic path: [nregs][BLOCK]
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M == FINAL ? 4 : 8)))
+k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_t* __restrict__ seg_end,
+         const uint32_t* __restrict__ seg_rs, uint8_t* __restrict__ flags, FinalParams fp, BfsParams bp,
+         unsigned long long* stat_e, unsigned long long* stat_n) {
+  __shared__ uint32_t sEndAll[WAVES][TILE + 2];   // per wave: seg_end for i in [a0-1, a1]
+  __shared__ uint32_t sRsAll[WAVES][TILE + 1];    // per wave: seg_rs for i in [a0, a1]
+  __shared__ uint16_t sSegAll[WAVES][TILE];       // per wave: segment of each edge item
+  __shared__ unsigned long long sBase;            // FINAL: rows this workgroup wrote (LDS cursor)
+  extern __shared__ int64_t regs[];               // FINAL generic path: [nregs][BLOCK]
 
   const unsigned long long packed = *acc;  // (list entries << 32 | edges) of the list a.frontier
   const uint64_t n = packed >> 32;
@@ -478,31 +513,43 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M ==
   }
   const uint64_t npath = n + total;
   const uint64_t ntiles = (npath + TILE - 1) / TILE;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar registers
+  uint32_t* const sEnd = sEndAll[w];
+  uint32_t* const sRs = sRsAll[w];
+  uint16_t* const sSeg = sSegAll[w];
   bool anyErr = false;
   constexpr bool kFinal = M == FINAL || M == FINALF;
   constexpr bool kFast = M == FINALF;
-  if (kFinal && threadIdx.x == 0) sBase = 0;
-
-  // Software pipeline over this workgroup's tiles t, t + g, t + 2g, ...: while tile t is
-  // processed, the split of tile t + 2g and the first BLOCK segment ends / row starts of tile
-  // t + g are already in flight (registers), so a tile starts with an LDS fill instead of two
-  // dependent global round trips.
-  const uint64_t g = gridDim.x;
-  uint64_t t = blockIdx.x;
-  uint64_t sp_next = 0;            // threads 0, 1: split (start, end) of tile t + g
-  uint64_t a0 = 0, a1 = 0;         // split of tile t
-  uint32_t e_pre = 0, r_pre = 0;   // entry threadIdx.x of tile t's segment-end window / row starts
-  if (t < ntiles) {
-    if (threadIdx.x < 2) {
-      sSplit[threadIdx.x] = tile_split(a.tsplit, t, threadIdx.x, npath, n);
-      if (t + g < ntiles) sp_next = tile_split(a.tsplit, t + g, threadIdx.x, npath, n);
-    }
+  if (kFinal) {
+    if (threadIdx.x == 0) sBase = 0;
     __syncthreads();
-    a0 = sSplit[0];
-    a1 = sSplit[1];
-    stage_pre(seg_end, seg_rs, n, a0, a1, &e_pre, &r_pre);
-    __syncthreads();   // sSplit is rewritten in the loop
+  }
+#ifdef NBG_PHASE_TIMING   // experiment builds only: cycles per tile phase (lane 0 of wave 0), printed
+  unsigned long long ph[5] = {0, 0, 0, 0, 0}, ph_prev = clock64();
+#define NBG_PH(k)                                        \
+  if (threadIdx.x == 0) {                                \
+    const unsigned long long c_ = clock64();             \
+    ph[k] += c_ - ph_prev;                               \
+    ph_prev = c_;                                        \
+  }
+#else
+#define NBG_PH(k)
+#endif
+  const uint64_t g = (uint64_t)gridDim.x * WAVES;
+  uint64_t t = (uint64_t)blockIdx.x * WAVES + w;
+  uint64_t sp_next = 0;            // lanes 0, 1: split (start, end) of tile t + g
+  uint64_t a0 = 0, a1 = 0;         // split of tile t
+  uint32_t e_pre = 0, r_pre = 0;   // lane's entry of tile t's segment-end window / row starts
+  if (t < ntiles) {
+    uint64_t sp = 0;
+    if (lane < 2) {
+      sp = tile_split(a.tsplit, t, lane, npath, n);
+      if (t + g < ntiles) sp_next = tile_split(a.tsplit, t + g, lane, npath, n);
+    }
+    a0 = uniform64(__shfl(sp, 0, 64));
+    a1 = uniform64(__shfl(sp, 1, 64));
+    stage_pre(seg_end, seg_rs, n, a0, a1, lane, &e_pre, &r_pre);
   }
   for (; t < ntiles; t += g) {
     const uint64_t d0 = t * TILE;
@@ -510,30 +557,30 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M ==
     const uint64_t b0 = d0 - a0, b1 = d1 - a1;
     const int na = (int)(a1 - a0), nb = (int)(b1 - b0);
 
-    // stage the tile's segment ends / row starts in LDS (entries past the prefetch directly)
-    if ((int)threadIdx.x <= na + 1) sEnd[threadIdx.x] = e_pre;
-    if ((int)threadIdx.x <= na) sRs[threadIdx.x] = r_pre;
-    for (int k = threadIdx.x + BLOCK; k <= na + 1; k += BLOCK) {
+    // the wave's window in LDS (entries past the prefetch loaded directly)
+    if (lane <= na + 1) sEnd[lane] = e_pre;
+    if (lane <= na) sRs[lane] = r_pre;
+    for (int k = lane + 64; k <= na + 1; k += 64) {
       const uint64_t i = a0 - 1 + (uint64_t)k;
       sEnd[k] = i < n ? seg_end[i] : 0xFFFFFFFFu;
       if (k <= na) sRs[k] = i + 1 < n ? seg_rs[i + 1] : 0u;
     }
-    if (threadIdx.x < 2) sSplit[threadIdx.x] = sp_next;
-    __syncthreads();
     // prefetch tile t + g's window and tile t + 2g's split
     uint64_t na0 = 0, na1 = 0;
     if (t + g < ntiles) {
-      na0 = sSplit[0];
-      na1 = sSplit[1];
-      stage_pre(seg_end, seg_rs, n, na0, na1, &e_pre, &r_pre);
-      if (threadIdx.x < 2 && t + 2 * g < ntiles) sp_next = tile_split(a.tsplit, t + 2 * g, threadIdx.x, npath, n);
+      na0 = uniform64(__shfl(sp_next, 0, 64));
+      na1 = uniform64(__shfl(sp_next, 1, 64));
+      stage_pre(seg_end, seg_rs, n, na0, na1, lane, &e_pre, &r_pre);
+      if (lane < 2 && t + 2 * g < ntiles) sp_next = tile_split(a.tsplit, t + 2 * g, lane, npath, n);
     }
+    wave_lds_sync();
+    NBG_PH(0)
     const uint32_t* A = sEnd + 1;   // A[k] = end of segment a0 + k
 
-    // thread-level merge path over this tile: assign a segment to every edge item
+    // lane-level merge path over this tile: assign a segment to every edge item
     {
-      int diag = threadIdx.x * VT;
-      int dmax = na + nb;
+      const int diag = lane * VT;
+      const int dmax = na + nb;
       if (diag < dmax) {
         int lo = diag > nb ? diag - nb : 0;
         int hi = diag < na ? diag : na;
@@ -549,19 +596,20 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M ==
           if (ai < na && (bi >= nb || (uint64_t)A[ai] <= b0 + (uint64_t)bi)) {
             ++ai;
           } else {
-            sSeg[bi] = (uint32_t)ai;
+            sSeg[bi] = (uint16_t)ai;
             ++bi;
           }
         }
       }
     }
-    __syncthreads();
+    wave_lds_sync();
+    NBG_PH(1)
 
     if (M == MARK) {
       uint32_t u[VT];   // all neighbour loads in flight before the flag stores
 #pragma unroll
       for (int i = 0; i < VT; ++i) {
-        const int k = i * BLOCK + threadIdx.x;
+        const int k = i * 64 + lane;
         u[i] = NO_ROW;
         if (k < nb) {
           const uint32_t s = sSeg[k];
@@ -576,10 +624,10 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M ==
       uint32_t cmask = 0, mmask = 0;
 #pragma unroll
       for (int i = 0; i < VT; ++i) {
-        const int k = i * BLOCK + threadIdx.x;
+        const int k = i * 64 + lane;
         wv[i] = NO_ROW;
         if (k < nb) {
-          uint32_t s = sSeg[k];
+          const uint32_t s = sSeg[k];
           wv[i] = a.col[(uint64_t)sRs[s] + (b0 + k - (uint64_t)sEnd[s])];
         }
       }
@@ -595,53 +643,48 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M ==
         if (bp.mlab && (bp.mlab[x] >> LVL_BITS) == bp.mepoch) mmask |= 1u << i;
         if (bp.tlab && bp.tlab[x] == bp.tstamp) atomicAdd(bp.found, 1ull);
       }
+      // one atomic per wave tile on a sharded claim counter
+      uint32_t pre[VT], run = 0;
 #pragma unroll
       for (int i = 0; i < VT; ++i) {
-        unsigned long long bal = __ballot((cmask >> i) & 1u);
-        if (lane == 0) sCnt[i * WAVES + w] = (uint32_t)__popcll(bal);
+        pre[i] = run;
+        run += (uint32_t)__popcll(__ballot((cmask >> i) & 1u));
       }
-      __syncthreads();
       const uint64_t shard = t % NSHARD;
-      if (threadIdx.x == 0) {
-        uint32_t run = 0;
-        for (int k = 0; k < VT * WAVES; ++k) {
-          uint32_t c = sCnt[k];
-          sCnt[k] = run;
-          run += c;
-        }
-        sBase = run ? atomicAdd(bp.shard_cnt + shard, (unsigned long long)run) : 0ull;
-      }
-      __syncthreads();
-      uint32_t* const region = bp.out + shard * bp.shard_cap + sBase;
+      unsigned long long base = 0;
+      if (lane == 0 && run) base = atomicAdd(bp.shard_cnt + shard, (unsigned long long)run);
+      base = __shfl(base, 0, 64);
+      uint32_t* const region = bp.out + shard * bp.shard_cap + base;
+#pragma unroll
       for (int i = 0; i < VT; ++i) {
         const bool c = (cmask >> i) & 1u;
-        unsigned long long bal = __ballot(c);
-        if (c) region[sCnt[i * WAVES + w] + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = wv[i];
+        const unsigned long long bal = __ballot(c);
+        if (c) region[pre[i] + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = wv[i];
         const bool m = (mmask >> i) & 1u;
-        unsigned long long mb = __ballot(m);
+        const unsigned long long mb = __ballot(m);
         if (mb) {
-          unsigned long long base = 0;
-          if (lane == 0) base = atomicAdd(bp.meet_n, (unsigned long long)__popcll(mb));
-          base = __shfl(base, 0, 64);
+          unsigned long long mbase = 0;
+          if (lane == 0) mbase = atomicAdd(bp.meet_n, (unsigned long long)__popcll(mb));
+          mbase = __shfl(mbase, 0, 64);
           if (m) {
-            bp.meet_list[base + (uint32_t)__popcll(mb & ((1ull << lane) - 1ull))] = wv[i];
+            bp.meet_list[mbase + (uint32_t)__popcll(mb & ((1ull << lane) - 1ull))] = wv[i];
             bp.mout[wv[i]] = bp.mstamp;
           }
         }
       }
     } else {
-      // phase A: WHERE for every item of the tile (VT items per thread, striped)
+      // phase A: WHERE for every item of the tile (VT items per lane, striped)
       uint32_t jj[VT];      // edge index in the CSR (< 2^32 per type)
       uint32_t vv[VT];
       int64_t dv[VT];       // fast path: _dst prefetched with the WHERE column (one round trip)
       uint32_t pmask = 0;
 #pragma unroll
       for (int i = 0; i < VT; ++i) {
-        const int k = i * BLOCK + threadIdx.x;
+        const int k = i * 64 + lane;
         jj[i] = 0;
         vv[i] = 0;
         if (k < nb) {
-          uint32_t s = sSeg[k];
+          const uint32_t s = sSeg[k];
           jj[i] = sRs[s] + (uint32_t)(b0 + k - (uint64_t)sEnd[s]);
           vv[i] = s;
         }
@@ -651,20 +694,29 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M ==
         int64_t x[VT];
 #pragma unroll
         for (int i = 0; i < VT; ++i) {
-          const bool act = i * BLOCK + (int)threadIdx.x < nb;
+          const bool act = i * 64 + lane < nb;
           dv[i] = (act && fp.fast.dst_yield) ? a.dst_vid[jj[i]] : 0;
-          x[i] = (act && fp.fast.has_where) ? fp.fast.wcol[jj[i]] : 0;
+        }
+        // the WHERE column at its stored width (narrow copy of an INT column when it fits)
+        switch (fp.fast.has_where ? fp.fast.wbytes : 0) {
+          case 1: load_narrow<int8_t>(fp.fast.wcol, jj, nb, lane, x); break;
+          case 2: load_narrow<int16_t>(fp.fast.wcol, jj, nb, lane, x); break;
+          case 4: load_narrow<int32_t>(fp.fast.wcol, jj, nb, lane, x); break;
+          case 8: load_narrow<int64_t>(fp.fast.wcol, jj, nb, lane, x); break;
+          default:
+#pragma unroll
+            for (int i = 0; i < VT; ++i) x[i] = 0;
         }
 #pragma unroll
         for (int i = 0; i < VT; ++i) {
-          const bool act = i * BLOCK + (int)threadIdx.x < nb;
+          const bool act = i * 64 + lane < nb;
           const bool in = (x[i] >= fp.fast.lo) & (x[i] <= fp.fast.hi);
           const bool pass = act & (!fp.fast.has_where | (in != (fp.fast.where_neg != 0)));
           pmask |= (uint32_t)pass << i;
         }
       } else {
         for (int i = 0; i < VT; ++i) {
-          const int k = i * BLOCK + threadIdx.x;
+          const int k = i * 64 + lane;
           const bool active = k < nb;
           bool pass = active;
           if (fp.where_reg >= 0) {
@@ -677,33 +729,27 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M ==
           pmask |= (uint32_t)pass << i;
         }
       }
-      // offsets for (iteration, wave) in item order; rows are appended to this workgroup's own
-      // region (no atomics: a cursor in LDS), so a tile never waits on a global round trip
+      NBG_PH(2)
+      // row offsets in item order: wave-uniform prefix over the VT ballots, then one LDS atomic
+      // on the workgroup's cursor (rows go to the workgroup's own region: no global atomics)
+      uint32_t run = 0;
+#pragma unroll
+      for (int i = 0; i < VT; ++i) run += (uint32_t)__popcll(__ballot((pmask >> i) & 1u));
+      unsigned long long base = 0;
+      if (lane == 0 && run) base = atomicAdd(&sBase, (unsigned long long)run);
+      base = __shfl(base, 0, 64);
+      NBG_PH(3)
+      // phase B: YIELD for the passing items, written at their final rows
+      const uint64_t region = fp.region_base + (uint64_t)blockIdx.x * fp.blk_cap + base;
+      int64_t* const* cols = fp.out_cols;   // kernel-argument array
+      uint32_t off = 0;                     // rows of the earlier items of this tile
 #pragma unroll
       for (int i = 0; i < VT; ++i) {
-        unsigned long long bal = __ballot((pmask >> i) & 1u);
-        if (lane == 0) sCnt[i * WAVES + w] = (uint32_t)__popcll(bal);
-      }
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        uint32_t run = 0;
-        for (int k = 0; k < VT * WAVES; ++k) {
-          uint32_t c = sCnt[k];
-          sCnt[k] = run;
-          run += c;
-        }
-        sTileBase = sBase;
-        sBase += run;
-      }
-      __syncthreads();
-      // phase B: YIELD for the passing items, written at their final rows
-      const uint64_t region = fp.region_base + (uint64_t)blockIdx.x * fp.blk_cap + sTileBase;
-      int64_t* const* cols = fp.out_cols;   // kernel-argument array (constant indices after unroll)
-      for (int i = 0; i < VT; ++i) {
         const bool pass = (pmask >> i) & 1u;
-        unsigned long long bal = __ballot(pass);
+        const unsigned long long bal = __ballot(pass);
         if (!bal) continue;
-        const uint64_t row = region + sCnt[i * WAVES + w] + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+        const uint64_t row = region + off + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+        off += (uint32_t)__popcll(bal);
         if (kFast) {
           if (pass) {
             for (int y = 0; y < fp.nyields; ++y) {
@@ -712,14 +758,10 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M ==
                 case 0: val = dv[i]; break;
                 case 1: val = a.vids[a.frontier[a0 + vv[i]]]; break;
                 case 2: val = a.rank ? a.rank[jj[i]] : 0; break;
-                case 3: val = fp.fast.ycol[y][jj[i]]; break;
+                case 3: val = load_col(fp.fast.ycol[y], fp.fast.ybytes[y], jj[i]); break;
                 default: val = fp.yield_const[y]; break;
               }
-#ifndef NBG_EXP_NOSTORE   // timing experiment only
               cols[y][row] = val;
-#else
-              if (val == 0x7eadbeefLL) cols[y][row] = val;
-#endif
             }
           }
         } else {
@@ -735,12 +777,18 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M ==
           }
         }
       }
+      NBG_PH(4)
     }
-    __syncthreads();   // LDS reuse by the next tile
     a0 = na0;
     a1 = na1;
   }
+#ifdef NBG_PHASE_TIMING
+  if (kFinal && threadIdx.x == 0 && blockIdx.x % 256 == 0 && ntiles > 8192)
+    printf("PH blk %u tiles %llu fill %llu merge %llu loadA %llu scan %llu storeB %llu\n", blockIdx.x,
+           (unsigned long long)ntiles, ph[0], ph[1], ph[2], ph[3], ph[4]);
+#endif
   if (kFinal) {
+    __syncthreads();   // every wave of the workgroup has reserved its rows
     if (threadIdx.x == 0) fp.blk_rows[blockIdx.x] = (uint32_t)sBase;
     if (anyErr) atomicOr(fp.err_flag, 1ull);
   }
@@ -1104,9 +1152,10 @@ static ListRef prepare_list(Workspace* w, const ExpandArgs& a, uint64_t n_bound,
   return ListRef{w->rlist, acc, nullptr};
 }
 
+// workgroups of a k_expand launch: one wave per tile up to EXPAND_GRID workgroups (persistent)
 static unsigned expand_grid(uint64_t n_bound, uint64_t e_bound) {
-  uint64_t tiles = cdiv(n_bound + e_bound + 1, TILE);
-  return (unsigned)(tiles < EXPAND_GRID ? (tiles ? tiles : 1) : EXPAND_GRID);
+  const uint64_t blocks = cdiv(cdiv(n_bound + e_bound + 1, TILE), WAVES);
+  return (unsigned)(blocks < EXPAND_GRID ? (blocks ? blocks : 1) : EXPAND_GRID);
 }
 
 hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, uint64_t e_bound, int step, int tix) {
@@ -1153,6 +1202,16 @@ static int edge_columns_read(const TypeProgram& prog) {
 }
 
 // Recognise the FastProg shapes in the compiled bytecode (see FastProg).
+// A column as the fast path reads it: the narrow copy when the loader made one.
+static const void* col_ptr(const ExpandArgs& a, int c, int* bytes) {
+  if (a.hnarrow && a.hnarrow[c]) {
+    *bytes = a.hnarrow_bytes[c];
+    return a.hnarrow[c];
+  }
+  *bytes = 8;
+  return a.hprops[c];
+}
+
 static FastProg detect_fast(const TypeProgram& prog, const ExpandArgs& a) {
   FastProg f{};
   f.enabled = 0;
@@ -1192,7 +1251,7 @@ static FastProg detect_fast(const TypeProgram& prog, const ExpandArgs& a) {
       default: f.lo = f.hi = k; f.where_neg = 1; break;                               // !=
     }
     f.has_where = 1;
-    f.wcol = a.hprops[colI->aux];
+    f.wcol = col_ptr(a, colI->aux, &f.wbytes);
   }
   const int ny = (int)prog.yield_reg.size();
   int pc = prog.where_len;
@@ -1204,7 +1263,7 @@ static FastProg detect_fast(const TypeProgram& prog, const ExpandArgs& a) {
     if (i.op == OP_DST) { f.ykind[y] = 0; f.dst_yield = 1; }
     else if (i.op == OP_SRC) f.ykind[y] = 1;
     else if (i.op == OP_RANK) f.ykind[y] = 2;
-    else if (leaf_col(i)) { f.ykind[y] = 3; f.ycol[y] = a.hprops[i.aux]; }
+    else if (leaf_col(i)) { f.ykind[y] = 3; f.ycol[y] = col_ptr(a, i.aux, &f.ybytes[y]); }
     else return f;
   }
   if (pc != (int)prog.code.size()) return f;
@@ -1215,8 +1274,10 @@ static FastProg detect_fast(const TypeProgram& prog, const ExpandArgs& a) {
 unsigned ws_final_grid(uint64_t n_bound, uint64_t e_bound) { return expand_grid(n_bound, e_bound); }
 
 uint64_t ws_final_blk_cap(uint64_t n_bound, uint64_t e_bound) {
+  // a workgroup's waves each take tiles w, w + g, ... (g = grid * WAVES waves)
   const uint64_t tiles = cdiv(n_bound + e_bound + 1, TILE);
-  return cdiv(tiles, expand_grid(n_bound, e_bound)) * TILE;
+  const uint64_t waves = (uint64_t)expand_grid(n_bound, e_bound) * WAVES;
+  return cdiv(tiles, waves) * WAVES * TILE;
 }
 
 uint64_t ws_shard_cap(uint64_t n_bound, uint64_t e_bound) {

@@ -406,6 +406,34 @@ int32_t Engine::finalize() {
     dt.prop_kind = kinds;
     dt.props.assign(nc, nullptr);
     for (size_t c = 0; ok && c < nc; ++c) ok = up((void**)&dt.props[c], pc[c].data(), E * 8);
+    // narrow copy of INT columns whose values fit 1 / 2 / 4 bytes (sign-extended on load): the
+    // final-step fast path reads it instead of the 8-byte column
+    dt.narrow.assign(nc, nullptr);
+    dt.narrow_bytes.assign(nc, 0);
+    for (size_t c = 0; ok && c < nc && E; ++c) {
+      if (kinds[c] != VK_INT) continue;
+      int64_t lo = INT64_MAX, hi = INT64_MIN;
+#pragma omp parallel for reduction(min : lo) reduction(max : hi)
+      for (int64_t i = 0; i < (int64_t)E; ++i) {
+        lo = std::min(lo, pc[c][i]);
+        hi = std::max(hi, pc[c][i]);
+      }
+      int bytes = 8;
+      if (lo >= INT8_MIN && hi <= INT8_MAX) bytes = 1;
+      else if (lo >= INT16_MIN && hi <= INT16_MAX) bytes = 2;
+      else if (lo >= INT32_MIN && hi <= INT32_MAX) bytes = 4;
+      if (bytes == 8) continue;
+      std::vector<uint8_t> buf(E * (size_t)bytes);
+#pragma omp parallel for schedule(static)
+      for (int64_t i = 0; i < (int64_t)E; ++i) {
+        const int64_t v = pc[c][i];
+        if (bytes == 1) reinterpret_cast<int8_t*>(buf.data())[i] = (int8_t)v;
+        else if (bytes == 2) reinterpret_cast<int16_t*>(buf.data())[i] = (int16_t)v;
+        else reinterpret_cast<int32_t*>(buf.data())[i] = (int32_t)v;
+      }
+      ok = up(&dt.narrow[c], buf.data(), buf.size());
+      dt.narrow_bytes[c] = bytes;
+    }
     if (ok && any_invalid) ok = up((void**)&dt.valid, valid.data(), E);
     if (ok && nc) {
       ok = up((void**)&dt.d_props, dt.props.data(), nc * sizeof(int64_t*));

@@ -75,6 +75,8 @@ struct DevEdgeType {            // CSR for one signed edge type over this rank's
   int64_t* rank = nullptr;      // [E] or nullptr when every rank is 0
   std::vector<int64_t*> props;  // [ncols][E] (positive types)
   int64_t** d_props = nullptr;  // device copy of `props`
+  std::vector<void*> narrow;    // [ncols] INT column at narrow_bytes width (nullptr: none)
+  std::vector<int> narrow_bytes;
   std::vector<VKind> prop_kind;
   uint8_t* valid = nullptr;     // [E] or nullptr when every value decoded
   int max_degree = 0;
@@ -155,7 +157,7 @@ struct TypeProgram {
 #define NBG_VT 4
 #endif
 constexpr int VT = NBG_VT;             // k_expand: path items per thread
-constexpr int TILE = 256 * VT;         // path items (frontier segments + edges) per tile
+constexpr int TILE = 64 * VT;          // path items (frontier entries + edges) per wave tile
 constexpr int NSHARD = 64;             // row-output shards (one counter + region each)
 constexpr int MAX_STEPS = 32;          // GO N STEPS upper bound
 constexpr int MAX_TYPES_Q = 16;        // OVER types per query
@@ -184,6 +186,8 @@ struct ExpandArgs {                // one (step, edge type) expansion
   uint32_t cap;                    // max_edge_returned_per_vertex
   const uint32_t* tsplit;          // per-tile merge-path splits (set by the workspace)
   const int64_t* const* hprops;    // host array of the same column pointers (host-side planning)
+  void* const* hnarrow;            // host array: narrow copies of INT columns (nullptr: none)
+  const int* hnarrow_bytes;
 };
 
 // ----------------------------------------------------------------------------- FIND PATH state

@@ -168,3 +168,25 @@ def test_device_rows_segments_cover_count(rmat12):
     assert len(res.fetch()) == res.count
     res.free()
     stmt.free()
+
+
+@pytest.mark.parametrize("scale_w", [(-1, -50), (300, 0), (70000, 0), (10 ** 12, -7)])
+def test_narrow_int_columns(scale_w):
+    """The final-step fast path reads INT columns at their narrowest width (1/2/4/8 bytes,
+    sign-extended): values spanning each width, WHERE range tests and YIELD of the column."""
+    mul, add = scale_w
+    src, dst, w = graphs.rmat_graph(10)
+    w2 = w * mul + add
+    eng = graphs.rmat_engine(src, dst, w2)
+    orc = graphs.rmat_oracle(src, dst, w2)
+    try:
+        mid = int(np.median(w2))
+        ys = [E.edge_prop("e", "_dst").encode(), E.edge_prop("e", "w").encode()]
+        for op in ("<", "<=", ">", ">=", "==", "!="):
+            wh = E.binop(op, E.edge_prop("e", "w"), E.const(mid)).encode()
+            for r in graphs.roots(src, 2, seed=13):
+                got = graphs.sorted_rows(eng.go([r], [1], 2, wh, ys))
+                assert got == graphs.sorted_rows(orc.go([r], [1], 2, wh, ys)), (op, mul, add)
+    finally:
+        eng.close()
+        orc.close()

@@ -1,7 +1,3 @@
-cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/var2
-for v in base vt8 nostore; do
-  if [ $v = base ]; then L=nebula_amd/libnbg.so; else L=build/variants/libnbg_$v.so; fi
-  NBG_LIB=$L timeout -k 10 200 python -u bench.py --steps 2 --sp-pairs 0 --no-cpu-baseline > gpurun_out/var2/$v.json 2>gpurun_out/var2/$v.log || exit 1
-  NBG_LIB=$L timeout -k 10 200 python -u bench.py --steps 2 --sp-pairs 0 --no-cpu-baseline --no-profile > gpurun_out/var2/${v}_np.json 2>>gpurun_out/var2/$v.log || exit 1
-  echo "$v done"
-done
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/ph
+NBG_LIB=build/variants/libnbg_vt8ph.so timeout -k 10 200 python -u bench.py --steps 1 --warmup 0 --sp-pairs 0 --no-cpu-baseline --no-profile --roots 8 > gpurun_out/ph/out8.txt 2>gpurun_out/ph/err8.txt &&
+NBG_LIB=build/variants/libnbg_vt8.so timeout -k 10 200 python -u bench.py --steps 2 --sp-pairs 0 --no-cpu-baseline > gpurun_out/ph/vt8.json 2>gpurun_out/ph/vt8.log
