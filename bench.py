@@ -104,7 +104,8 @@ def main():
     load_s = time.time() - t0
     st = eng.stats()
     log(f"[rank {rank}] RMAT-{args.scale}: {len(src)} samples, snapshot {st}, gen {gen_s:.1f}s load {load_s:.1f}s")
-    roots = [int(x) for x in rmat.pick_roots(src, args.roots, 42)]
+    src_verts, all_verts = rmat.vertex_sets(args.scale)
+    roots = [int(x) for x in rmat.pick_roots(src, args.roots, 42, verts=src_verts)]
     where = E.binop("<", E.edge_prop("e", "w"), E.const(50)).encode()
 
     # GoExecutor::prepare() once, execute() per root (rows stay in HBM)
@@ -163,7 +164,7 @@ def main():
     sp = None
     pairs = []
     if args.sp_pairs > 0 and world == 1:   # FIND PATH on a partitioned engine: not in this build
-        pairs = rmat.pick_pairs(src, dst, args.sp_pairs, 7)
+        pairs = rmat.pick_pairs(src, dst, args.sp_pairs, 7, verts=all_verts)
         sp = shortest_path_leg(eng, pairs, args, barrier)
 
     # edges_scanned is already the whole query's count (summed over ranks in the library);

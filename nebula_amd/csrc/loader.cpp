@@ -285,17 +285,27 @@ int32_t Engine::finalize() {
     auto it = std::lower_bound(all.begin(), all.end(), vid);
     return (it != all.end() && *it == vid) ? (uint32_t)(it - all.begin()) : NO_ROW;
   };
-  // home part per vertex; a vid whose rows sit in two parts is not representable
+  // dense id of every record's source (reused by the CSR build); home part per vertex — a vid
+  // whose rows sit in two parts is not representable
+  std::map<int32_t, std::vector<uint32_t>> src_dense;
   std::vector<int32_t> home(nv, 0);
   bool all_visible = true;
+  bool split = false;
   for (auto& kv : stage) {
     auto& st = kv.second;
-    for (size_t i = 0; i < st.src.size(); ++i) {
-      uint32_t d = dense(st.src[i]);
-      if (home[d] == 0) home[d] = st.part[i];
-      else if (home[d] != st.part[i]) return fail(NBG_E_UNSUPPORTED, "vertex rows split across partitions");
+    auto& sd = src_dense[kv.first];
+    sd.resize(st.src.size());
+#pragma omp parallel for schedule(static) reduction(|| : split)
+    for (int64_t i = 0; i < (int64_t)st.src.size(); ++i) {
+      const uint32_t d = dense(st.src[i]);
+      sd[i] = d;
+      int32_t expected = 0;
+      if (!__atomic_compare_exchange_n(&home[d], &expected, st.part[i], false, __ATOMIC_RELAXED, __ATOMIC_RELAXED) &&
+          expected != st.part[i])
+        split = true;
     }
   }
+  if (split) return fail(NBG_E_UNSUPPORTED, "vertex rows split across partitions");
   std::vector<uint8_t> visible(nv, 1);
   for (uint64_t d = 0; d < nv; ++d) {
     if (home[d] != hash_part(all[d], cfg.num_parts)) { visible[d] = 0; all_visible = false; }
@@ -325,18 +335,21 @@ int32_t Engine::finalize() {
     const int32_t type = kv.first;
     EdgeStage& st = kv.second;
     const uint64_t n = st.src.size();
-    std::vector<uint32_t> sd(n);
-#pragma omp parallel for schedule(static)
-    for (int64_t i = 0; i < (int64_t)n; ++i) sd[i] = dense(st.src[i]);
+    std::vector<uint32_t> sd = std::move(src_dense[type]);
     std::vector<uint64_t> cnt(nv + 1, 0);
-    for (uint64_t i = 0; i < n; ++i) cnt[sd[i] + 1]++;
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < (int64_t)n; ++i) __atomic_fetch_add(&cnt[sd[i] + 1], 1ull, __ATOMIC_RELAXED);
     for (uint64_t d = 0; d < nv; ++d) cnt[d + 1] += cnt[d];
     std::vector<RowKey> keys(n);
     {
+      // bucket order inside a vertex does not matter: each bucket is sorted by rowkey_less
+      // (a total order: load sequence breaks ties)
       std::vector<uint64_t> cur(cnt.begin(), cnt.end() - 1);
-      for (uint64_t i = 0; i < n; ++i) {
-        uint64_t p = cur[sd[i]]++;
-        keys[p] = RowKey{bswap64((uint64_t)st.rank[i]), bswap64((uint64_t)st.dst[i]), st.verkey[i], st.seq[i], i};
+#pragma omp parallel for schedule(static)
+      for (int64_t i = 0; i < (int64_t)n; ++i) {
+        const uint64_t p = __atomic_fetch_add(&cur[sd[i]], 1ull, __ATOMIC_RELAXED);
+        keys[p] = RowKey{bswap64((uint64_t)st.rank[i]), bswap64((uint64_t)st.dst[i]), st.verkey[i], st.seq[i],
+                         (uint64_t)i};
       }
     }
     std::vector<uint32_t> live(nv + 1, 0);

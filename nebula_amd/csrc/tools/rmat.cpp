@@ -35,3 +35,35 @@ extern "C" int nbgtool_rmat(int scale, int edge_factor, uint64_t seed, int64_t* 
   }
   return 0;
 }
+
+// Vertex sets of the same graph without sorting the sample arrays: marks src_seen[u] / any_seen[u]
+// over the RMAT id space (u < 2^scale; the vid is mix(u + seed) masked, as above).  Byte stores
+// of the same value from several threads are benign.
+extern "C" int nbgtool_rmat_vertices(int scale, int edge_factor, uint64_t seed, uint8_t* src_seen, uint8_t* any_seen) {
+  const uint64_t n = (uint64_t)edge_factor << scale;
+  const uint64_t ta = (uint64_t)(0.57 * 9007199254740992.0);
+  const uint64_t tab = (uint64_t)((0.57 + 0.19) * 9007199254740992.0);
+  const uint64_t tabc = (uint64_t)((0.57 + 0.19 + 0.19) * 9007199254740992.0);
+#pragma omp parallel for schedule(static, 65536)
+  for (int64_t ii = 0; ii < (int64_t)n; ++ii) {
+    uint64_t i = (uint64_t)ii, u = 0, v = 0, base = i * 64;
+    for (int l = 0; l < scale; ++l) {
+      uint64_t r = splitmix64(seed ^ (base + (uint64_t)l)) >> 11;
+      uint64_t bu = r >= tab;
+      uint64_t bv = ((r >= ta) && (r < tab)) || (r >= tabc);
+      u |= bu << l;
+      v |= bv << l;
+    }
+    src_seen[u] = 1;
+    any_seen[u] = 1;
+    any_seen[v] = 1;
+  }
+  return 0;
+}
+
+// vid of RMAT id u (the scramble above), for ids u[0..n)
+extern "C" int nbgtool_rmat_vids(uint64_t seed, const uint64_t* u, uint64_t n, int64_t* out) {
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < (int64_t)n; ++i) out[i] = (int64_t)(mix(u[i] + seed) & 0x7FFFFFFFFFFFFFFFull);
+  return 0;
+}

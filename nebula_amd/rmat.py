@@ -90,18 +90,47 @@ def dedup_last(src, dst, w):
     return src[idx], dst[idx], w[idx]
 
 
-def pick_pairs(src, dst, k: int, seed: int = 7):
+def vertex_sets(scale: int, edge_factor: int = 16, seed: int | None = None):
+    """(sorted vids with out-degree >= 1, sorted vids with degree >= 1) of rmat_edges(scale) —
+    equal to np.unique(src) and np.union1d(src, dst), without sorting the sample arrays."""
+    import ctypes as C
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libnbgtools.so")
+    seed = (SEED_BASE ^ scale) if seed is None else seed
+    if not os.path.exists(path):
+        src, dst, _ = rmat_edges(scale, edge_factor, seed)
+        return np.unique(src), np.union1d(src, dst)
+    lib = C.CDLL(path)
+    lib.nbgtool_rmat_vertices.argtypes = [C.c_int, C.c_int, C.c_uint64, C.c_void_p, C.c_void_p]
+    lib.nbgtool_rmat_vids.argtypes = [C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p]
+    s_seen = np.zeros(1 << scale, np.uint8)
+    a_seen = np.zeros(1 << scale, np.uint8)
+    lib.nbgtool_rmat_vertices(scale, edge_factor, seed & 0xFFFFFFFFFFFFFFFF, s_seen.ctypes.data, a_seen.ctypes.data)
+    out = []
+    for seen in (s_seen, a_seen):
+        u = np.flatnonzero(seen).astype(np.uint64)
+        v = np.empty(len(u), np.int64)
+        lib.nbgtool_rmat_vids(seed & 0xFFFFFFFFFFFFFFFF, u.ctypes.data, len(u), v.ctypes.data)
+        v.sort()
+        out.append(v)
+    return out[0], out[1]
+
+
+def pick_pairs(src, dst, k: int, seed: int = 7, verts=None):
     """k (source, target) pairs, each end drawn uniformly (seeded, with replacement) among the
     vertices with degree >= 1."""
-    verts = np.union1d(np.unique(src), np.unique(dst))
+    if verts is None:
+        verts = np.union1d(np.unique(src), np.unique(dst))
     rng = np.random.default_rng(seed)
     a = verts[rng.integers(0, len(verts), size=k)]
     b = verts[rng.integers(0, len(verts), size=k)]
     return [(int(x), int(y)) for x, y in zip(a, b)]
 
 
-def pick_roots(src, k: int, seed: int = 42):
-    """k roots drawn uniformly (seeded) among vertices with out-degree >= 1."""
-    verts = np.unique(src)
+def pick_roots(src, k: int, seed: int = 42, verts=None):
+    """k roots drawn uniformly (seeded) among vertices with out-degree >= 1 (``verts``: the
+    precomputed sorted set, see vertex_sets)."""
+    if verts is None:
+        verts = np.unique(src)
     rng = np.random.default_rng(seed)
     return verts[rng.choice(len(verts), size=min(k, len(verts)), replace=False)]
