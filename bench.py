@@ -163,7 +163,7 @@ def main():
 
     sp = None
     pairs = []
-    if args.sp_pairs > 0 and world == 1:   # FIND PATH on a partitioned engine: not in this build
+    if args.sp_pairs > 0:   # partitioned: every rank runs each query collectively
         pairs = rmat.pick_pairs(src, dst, args.sp_pairs, 7, verts=all_verts)
         sp = shortest_path_leg(eng, pairs, args, barrier)
 
@@ -289,8 +289,8 @@ def shortest_path_leg(eng, pairs, args, barrier):
            "p50_ms": float(np.percentile(lat_ms, 50)), "p90_ms": float(np.percentile(lat_ms, 90)),
            "p99_ms": float(np.percentile(lat_ms, 99)), "mean_ms": float(lat_ms.mean()),
            "teps": edges / elapsed if elapsed else None, "edges": edges, "seconds": round(elapsed, 3)}
-    if kst:
-        ks = {k: v for k, v in kst.items() if v["launches"]}
+    ks = {k: v for k, v in kst.items() if v["launches"]} if kst else {}
+    if ks:
         out["kernels"] = {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
                               "algo_GBs": round(v["algo_bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None}
                           for k, v in ks.items()}

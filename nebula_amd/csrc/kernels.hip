@@ -122,6 +122,8 @@ struct Workspace {
   unsigned long long* sendbits = nullptr;   // [world * npad / 64]
   unsigned long long* recvbits = nullptr;   // [world * npad / 64]
   unsigned long long* gst = nullptr;        // [GST_N] globally reduced query statistics
+  unsigned long long* pgst = nullptr;       // [PG_N] globally reduced FIND PATH sizes
+  unsigned long long* h_pgst = nullptr;
   unsigned long long* h_gst = nullptr;
 };
 
@@ -1028,7 +1030,8 @@ void ws_destroy(Workspace* w) {
   for (void* p : {(void*)w->h_q, (void*)w->h_starts, (void*)w->h_prog, (void*)w->h_ps, (void*)w->h_path,
                   (void*)w->h_stage})
     if (p) (void)hipHostFree(p);
-  for (void* p : {(void*)w->sendbits, (void*)w->recvbits, (void*)w->gst})
+  if (w->h_pgst) (void)hipHostFree(w->h_pgst);
+  for (void* p : {(void*)w->sendbits, (void*)w->recvbits, (void*)w->gst, (void*)w->pgst})
     if (p) (void)hipFree(p);
   if (w->h_gst) (void)hipHostFree(w->h_gst);
   for (void* p : {(void*)w->ps, (void*)w->pscratch, (void*)w->d_path})
@@ -1849,6 +1852,364 @@ hipError_t ws_path_sync(Workspace* w, PState* out, int64_t* path, int path_len) 
   // resolve timing of the launches since the last sync (record indices stay valid per query)
   prof_flush(w, nullptr, w->h_ps);
   return hipSuccess;
+}
+
+// ============================================================================= partitioned FIND PATH
+// The BFS of a partitioned engine: a level expands the rank's own frontier
+// over its CSRs into byte flags over the global id space (k_expand<MARK>), the flags travel to
+// their owners in the per-hop bitmap all-to-all, and the OWNER claims its vertices (label test
+// and set — each vertex is handled by exactly one thread, no CAS), detects meets against its
+// own labels of the other side and counts reached targets.  Sizes every rank needs (frontier
+// sizes, degree sums, meets, targets found) are summed over ranks at each synchronisation.
+struct ClaimParams {
+  uint32_t* lab;                  // claim labels
+  uint32_t stamp;
+  uint32_t epoch;
+  const uint32_t* rlab;           // restriction (nullable): claim v only if rlab[v] == rstamp
+  uint32_t rstamp;
+  const uint32_t* mlab;           // meet test (nullable)
+  uint32_t mepoch;
+  uint32_t* mout;
+  uint32_t mstamp;
+  uint32_t* meet_list;
+  unsigned long long* meet_n;
+  const uint32_t* tlab;           // targets (nullable)
+  uint32_t tstamp;
+  unsigned long long* found;
+  uint32_t* out;                  // claimed vertices (next frontier, local ids)
+  unsigned long long* out_n;
+};
+
+// Block-wide append of c items per thread to a list with counter *n: returns this thread's slot.
+__device__ __forceinline__ uint32_t block_append(uint32_t c, unsigned long long* n) {
+  __shared__ uint32_t lds[WAVES];
+  __shared__ unsigned long long s_base;
+  uint32_t tot;
+  const uint32_t x = block_excl_scan(c, &tot, lds);
+  if (threadIdx.x == 0) s_base = tot ? atomicAdd(n, (unsigned long long)tot) : 0ull;
+  __syncthreads();
+  return (uint32_t)s_base + x;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_bits_claim(const unsigned long long* __restrict__ recv, int world,
+                                                      uint64_t seg_words, uint64_t nv, ClaimParams cp) {
+  const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;   // 16-bit slice index
+  const uint64_t word = i >> 2;
+  const int sh = (int)(i & 3) * 16;
+  unsigned long long m64 = 0;
+  for (int q = 0; q < world; ++q) m64 |= recv[(uint64_t)q * seg_words + word];
+  uint32_t m = (uint32_t)(m64 >> sh) & 0xFFFFu;
+  const uint64_t lo = i * 16;
+  if (lo >= nv) m = 0;
+  else if (nv - lo < 16) m &= (1u << (nv - lo)) - 1u;
+  uint32_t cm = 0, mm = 0;
+  for (uint32_t x = m; x; x &= x - 1) {
+    const int b = __ffs(x) - 1;
+    const uint32_t v = (uint32_t)(lo + b);
+    if (cp.rlab && cp.rlab[v] != cp.rstamp) continue;
+    if ((cp.lab[v] >> LVL_BITS) == cp.epoch) continue;
+    cp.lab[v] = cp.stamp;
+    cm |= 1u << b;
+    if (cp.mlab && (cp.mlab[v] >> LVL_BITS) == cp.mepoch) mm |= 1u << b;
+    if (cp.tlab && cp.tlab[v] == cp.tstamp) atomicAdd(cp.found, 1ull);
+  }
+  uint32_t pos = block_append((uint32_t)__popc(cm), cp.out_n);
+  for (uint32_t x = cm; x; x &= x - 1) cp.out[pos++] = (uint32_t)(lo + __ffs(x) - 1);
+  if (cp.meet_list) {
+    uint32_t mp = block_append((uint32_t)__popc(mm), cp.meet_n);
+    for (uint32_t x = mm; x; x &= x - 1) {
+      const uint32_t v = (uint32_t)(lo + __ffs(x) - 1);
+      cp.meet_list[mp++] = v;
+      cp.mout[v] = cp.mstamp;
+    }
+  }
+}
+
+// Greedy reconstruction, one hop of a partitioned engine: among this rank's vertices u in the
+// next B-set, the minimum (type, rank, vid) in-edge u <- v (the out-edge v -> u) from the current
+// vertex v (global id); per-block minima, then one block reduces them to this rank's candidate.
+struct GreedyPart {
+  int ntypes;
+  int32_t type[MAX_TYPES_Q];            // OVER types (positive)
+  const uint32_t* row_ptr[MAX_TYPES_Q]; // in-edge CSRs (-type)
+  const uint32_t* col[MAX_TYPES_Q];     // global id of the in-edge's source
+  const int64_t* rank[MAX_TYPES_Q];
+  const uint8_t* visible;               // reported per candidate: an invisible vertex has no out-edges
+  const int64_t* vids;
+  uint64_t nv;
+  uint32_t gbase;                       // this rank's first global id
+  uint32_t v;                           // current vertex (global id)
+  int pos;                              // B-set position of the candidates
+  int L, kf;
+  const uint32_t* lab_m;
+  uint32_t em;
+  const uint32_t* lab_b;
+  uint32_t eb;
+  Cand* part;                           // [gridDim.x] per-block minima
+};
+constexpr int GREC = 6;                 // rank record: type, rank, vid, global id (-1: none), visible, 0
+
+__device__ __forceinline__ bool part_valid(const GreedyPart& g, uint32_t u) {
+  if (g.pos <= g.kf) return g.lab_m[u] == ((g.em << LVL_BITS) | (uint32_t)g.pos);
+  return g.lab_b[u] == ((g.eb << LVL_BITS) | (uint32_t)(g.L - g.pos));
+}
+
+__global__ void __launch_bounds__(BLOCK) k_greedy_part(GreedyPart g) {
+  __shared__ Cand lds[WAVES + 1];
+  Cand best{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
+  for (uint64_t u = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; u < g.nv; u += (uint64_t)gridDim.x * BLOCK) {
+    if (!part_valid(g, (uint32_t)u)) continue;
+    for (int t = 0; t < g.ntypes; ++t) {
+      const uint32_t rs = g.row_ptr[t][u], re = g.row_ptr[t][u + 1];
+      for (uint32_t j = rs; j < re; ++j) {
+        if (g.col[t][j] != g.v) continue;
+        Cand x{(int64_t)g.type[t], g.rank[t] ? g.rank[t][j] : 0, g.vids[u], (uint32_t)u};
+        if (cand_less(x, best)) best = x;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Cand x = shfl_cand(best, o);
+    if (cand_less(x, best)) best = x;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) lds[w] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Cand b = lds[0];
+    for (int k = 1; k < WAVES; ++k)
+      if (cand_less(lds[k], b)) b = lds[k];
+    g.part[blockIdx.x] = b;
+  }
+}
+
+__device__ __forceinline__ void put_record(const Cand& b, uint32_t gbase, const uint8_t* visible, int64_t* out) {
+  out[0] = b.t;
+  out[1] = b.r;
+  out[2] = b.v;
+  out[3] = b.d == NO_ROW ? -1 : (int64_t)(gbase + b.d);
+  out[4] = b.d == NO_ROW ? 0 : (visible ? visible[b.d] : 1);
+  out[5] = 0;
+}
+
+__global__ void k_greedy_part_reduce(const Cand* __restrict__ part, int nparts, uint32_t gbase,
+                                     const uint8_t* __restrict__ visible, int64_t* out) {
+  if (threadIdx.x != 0) return;
+  Cand b{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
+  for (int k = 0; k < nparts; ++k)
+    if (cand_less(part[k], b)) b = part[k];
+  put_record(b, gbase, visible, out);
+}
+
+// Minimum vid among a list's entries (B[0] of the greedy) as a rank record (type = rank = 0).
+__global__ void k_min_vid(const uint32_t* __restrict__ ids, const unsigned long long* __restrict__ np,
+                          const int64_t* __restrict__ vids, uint32_t gbase, const uint8_t* __restrict__ visible,
+                          int64_t* out) {
+  if (threadIdx.x != 0) return;
+  Cand b{0, 0, INT64_MAX, NO_ROW};
+  const uint64_t n = *np;
+  for (uint64_t k = 0; k < n; ++k) {
+    const uint32_t d = ids[k];
+    if (d != NO_ROW && vids[d] < b.v) b = Cand{0, 0, vids[d], d};
+  }
+  put_record(b, gbase, visible, out);
+}
+
+hipError_t ws_path_level_part(Workspace* w, const PathTypes& pt, int src, uint64_t n_bound, uint64_t e_bound, int dst,
+                              const PathLevel& lv) {
+  if (!w->comm) return hipErrorInvalidValue;
+  const int rec = w->rec < PATH_REC ? w->rec++ : PATH_REC - 1;
+  HIP_TRY(hipMemsetAsync(&w->ps->n[dst], 0, sizeof(unsigned long long), w->stream));
+  for (int t = 0; t < pt.n; ++t) {
+    ExpandArgs a = pt.a[t];
+    unsigned long long* acc = &w->ps->acc[w->ppr];
+    unsigned long long* other = &w->ps->acc[w->ppr ^ 1];
+    w->ppr ^= 1;
+    hipEvent_t p = prof_begin_p(w, K_RELIST);
+    hipLaunchKernelGGL(k_relist, dim3((unsigned)cdiv(n_bound ? n_bound : 1, RL_TILE)), dim3(BLOCK), 0, w->stream,
+                       w->slot[src], &w->ps->n[src], 0, 0u, InlineIds{}, deg_of(a),
+                       list_out(w, w->rlist, acc, other, t == 0 ? &w->ps->ln[rec] : nullptr),
+                       (unsigned long long*)nullptr);
+    prof_end_p(w, p, K_RELIST, rec);
+    a.frontier = w->rlist;
+    a.tsplit = w->tsplit;
+    p = prof_begin_p(w, K_EXPAND_MARK);
+    hipLaunchKernelGGL(k_expand<MARK>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, acc,
+                       w->seg_end, w->seg_rs, w->flags, FinalParams{}, BfsParams{}, &w->ps->le[rec],
+                       (unsigned long long*)nullptr);
+    prof_end_p(w, p, K_EXPAND_MARK, rec);
+  }
+  const uint64_t G = (uint64_t)w->comm->world;
+  const uint64_t nwords = G * w->npad / 64, seg_words = w->npad / 64, nb = w->npad / BITS_BLOCK;
+  hipEvent_t p = prof_begin_p(w, K_PACK);
+  hipLaunchKernelGGL(k_pack_bits, dim3((unsigned)cdiv(nwords, BLOCK)), dim3(BLOCK), 0, w->stream, w->flags, nwords,
+                     w->sendbits);
+  prof_end_p(w, p, K_PACK, rec);
+  HIP_TRY(hipGetLastError());
+  if (w->comm->alltoall(w->sendbits, w->recvbits, w->npad / 8, w->stream)) return hipErrorUnknown;
+  ClaimParams cp{};
+  cp.lab = w->lab[lv.lab];
+  cp.stamp = lv.stamp;
+  cp.epoch = lv.stamp >> LVL_BITS;
+  if (lv.rlab >= 0) { cp.rlab = w->lab[lv.rlab]; cp.rstamp = lv.rstamp; }
+  if (lv.mlab >= 0) {
+    cp.mlab = w->lab[lv.mlab];
+    cp.mepoch = lv.mepoch;
+    cp.mout = w->lab[LAB_M];
+    cp.mstamp = lv.mstamp;
+    cp.meet_list = w->slot[lv.meet_slot];
+    cp.meet_n = &w->ps->n[lv.meet_slot];
+  }
+  if (lv.tlab >= 0) { cp.tlab = w->lab[lv.tlab]; cp.tstamp = lv.tstamp; cp.found = &w->ps->found; }
+  cp.out = w->slot[dst];
+  cp.out_n = &w->ps->n[dst];
+  p = prof_begin_p(w, K_BITS_COMPACT);
+  hipLaunchKernelGGL(k_bits_claim, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->recvbits, (int)G, seg_words,
+                     w->nv, cp);
+  prof_end_p(w, p, K_BITS_COMPACT, rec);
+  return hipGetLastError();
+}
+
+// The PState fields every rank needs, summed over ranks (n[], dsum[], found, err, le[]).
+constexpr int PG_N = PSLOTS + 2 + 2 + PATH_REC;
+__global__ void k_pgstats(const PState* __restrict__ ps, unsigned long long* __restrict__ g) {
+  const int k = threadIdx.x;
+  if (k < PSLOTS) g[k] = ps->n[k];
+  if (k < 2) g[PSLOTS + k] = ps->dsum[k];
+  if (k == 0) {
+    g[PSLOTS + 2] = ps->found;
+    g[PSLOTS + 3] = ps->err;
+  }
+  if (k < PATH_REC) g[PSLOTS + 4 + k] = ps->le[k];
+}
+
+// Synchronous: like ws_path_sync, with the per-rank sizes summed over ranks.
+hipError_t ws_path_sync_part(Workspace* w, PState* out) {
+  if (!w->comm) return hipErrorInvalidValue;
+  if (!w->pgst) {
+    HIP_TRY(hipMalloc((void**)&w->pgst, PG_N * sizeof(unsigned long long)));
+    HIP_TRY(hipHostMalloc((void**)&w->h_pgst, PG_N * sizeof(unsigned long long), hipHostMallocDefault));
+  }
+  hipLaunchKernelGGL(k_pgstats, dim3(1), dim3(64), 0, w->stream, w->ps, w->pgst);
+  HIP_TRY(hipGetLastError());
+  if (w->comm->allreduce_sum_u64(w->pgst, PG_N, w->stream)) return hipErrorUnknown;
+  HIP_TRY(hipMemcpyAsync(w->h_pgst, w->pgst, PG_N * sizeof(unsigned long long), hipMemcpyDeviceToHost, w->stream));
+  HIP_TRY(hipMemcpyAsync(w->h_ps, w->ps, sizeof(PState), hipMemcpyDeviceToHost, w->stream));
+  HIP_TRY(hipStreamSynchronize(w->stream));
+  PState g = *w->h_ps;
+  for (int k = 0; k < PSLOTS; ++k) g.n[k] = w->h_pgst[k];
+  for (int k = 0; k < 2; ++k) g.dsum[k] = w->h_pgst[PSLOTS + k];
+  g.found = w->h_pgst[PSLOTS + 2];
+  g.err = w->h_pgst[PSLOTS + 3];
+  for (int k = 0; k < PATH_REC; ++k) g.le[k] = w->h_pgst[PSLOTS + 4 + k];
+  if (out) *out = g;
+  prof_flush(w, nullptr, w->h_ps);
+  return hipSuccess;
+}
+
+// Sum a host vector over ranks (small control data: label values, presence flags).
+hipError_t ws_allreduce_host(Workspace* w, std::vector<unsigned long long>& v) {
+  if (!w->comm || v.empty()) return hipSuccess;
+  unsigned long long* d = nullptr;
+  hipError_t e = hipMalloc((void**)&d, v.size() * 8);
+  if (e == hipSuccess) e = hipMemcpyAsync(d, v.data(), v.size() * 8, hipMemcpyHostToDevice, w->stream);
+  if (e == hipSuccess && w->comm->allreduce_sum_u64(d, v.size(), w->stream)) e = hipErrorUnknown;
+  if (e == hipSuccess) e = hipMemcpyAsync(v.data(), d, v.size() * 8, hipMemcpyDeviceToHost, w->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(w->stream);
+  if (d) (void)hipFree(d);
+  return e;
+}
+
+// Gather one GREC x int64 record per rank (rank order) from a device buffer.
+static hipError_t gather_records(Workspace* w, const int64_t* d_rec, std::vector<int64_t>* out) {
+  const int G = w->comm->world;
+  int64_t* d_all = nullptr;
+  hipError_t e = hipMalloc((void**)&d_all, (size_t)G * GREC * 8);
+  if (e == hipSuccess && w->comm->allgather(d_rec, d_all, GREC * 8, w->stream)) e = hipErrorUnknown;
+  out->assign((size_t)G * GREC, 0);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(out->data(), d_all, (size_t)G * GREC * 8, hipMemcpyDeviceToHost, w->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(w->stream);
+  if (d_all) (void)hipFree(d_all);
+  return e;
+}
+
+// Lexicographically smallest shortest path through the B-sets on a partitioned engine; the path
+// entries are written to `path` (1 + 3L).  Returns hipErrorNotFound when a hop has no candidate.
+hipError_t ws_path_greedy_part(Workspace* w, const PathTypes& bwd, const PathGreedy& pg, const int64_t* vids,
+                               const uint8_t* visible, int64_t* path) {
+  if (!w->comm) return hipErrorInvalidValue;
+  if (pg.L < 1 || pg.L > (int)MAX_PATH_LEN) return hipErrorInvalidValue;
+  const uint32_t gbase = (uint32_t)((uint64_t)w->comm->rank * w->npad);
+  const uint64_t nblk = cdiv(w->nv ? w->nv : 1, BLOCK);
+  const unsigned grid = (unsigned)(nblk < 1024 ? nblk : 1024);
+  Cand* d_part = nullptr;
+  int64_t* d_rec = nullptr;
+  hipError_t e = hipMalloc((void**)&d_part, (size_t)grid * sizeof(Cand));
+  if (e == hipSuccess) e = hipMalloc((void**)&d_rec, GREC * 8);
+  std::vector<int64_t> all;
+  // the rank records' minimum (type, rank, vid); distinct ranks never tie (vids are unique)
+  auto pick = [&]() -> const int64_t* {
+    const int64_t* b = nullptr;
+    for (int q = 0; q < w->comm->world; ++q) {
+      const int64_t* x = &all[(size_t)q * GREC];
+      if (x[3] < 0) continue;
+      if (!b || x[0] < b[0] || (x[0] == b[0] && (x[1] < b[1] || (x[1] == b[1] && x[2] < b[2])))) b = x;
+    }
+    return b;
+  };
+  // v0: the smallest vid of B[0]
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_min_vid, dim3(1), dim3(64), 0, w->stream, w->slot[pg.start_slot], &w->ps->n[pg.start_slot],
+                       vids, gbase, visible, d_rec);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = gather_records(w, d_rec, &all);
+  const int64_t* b = e == hipSuccess ? pick() : nullptr;
+  if (e == hipSuccess && !b) e = hipErrorNotFound;
+  if (e == hipSuccess) path[0] = b[2];
+  for (int pos = 1; e == hipSuccess && pos <= pg.L; ++pos) {
+    if (!b[4]) { e = hipErrorNotFound; break; }   // an invisible vertex has no out-edges
+    GreedyPart g{};
+    g.ntypes = bwd.n;
+    for (int t = 0; t < bwd.n; ++t) {
+      g.type[t] = -bwd.type[t];
+      g.row_ptr[t] = bwd.a[t].row_ptr;
+      g.col[t] = bwd.a[t].col;
+      g.rank[t] = bwd.a[t].rank;
+    }
+    g.visible = visible;
+    g.vids = vids;
+    g.nv = w->nv;
+    g.gbase = gbase;
+    g.v = (uint32_t)b[3];
+    g.pos = pos;
+    g.L = pg.L;
+    g.kf = pg.kf;
+    g.lab_m = w->lab[LAB_M];
+    g.em = pg.em;
+    g.lab_b = w->lab[LAB_B];
+    g.eb = pg.eb;
+    g.part = d_part;
+    hipEvent_t p = prof_begin_p(w, K_GREEDY);
+    hipLaunchKernelGGL(k_greedy_part, dim3(grid), dim3(BLOCK), 0, w->stream, g);
+    hipLaunchKernelGGL(k_greedy_part_reduce, dim3(1), dim3(64), 0, w->stream, d_part, (int)grid, gbase, visible,
+                       d_rec);
+    prof_end_p(w, p, K_GREEDY, 0);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = gather_records(w, d_rec, &all);
+    b = e == hipSuccess ? pick() : nullptr;
+    if (e == hipSuccess && !b) e = hipErrorNotFound;
+    if (e == hipSuccess) {
+      path[1 + 3 * (pos - 1)] = b[0];
+      path[2 + 3 * (pos - 1)] = b[1];
+      path[3 + 3 * (pos - 1)] = b[2];
+    }
+  }
+  if (d_part) (void)hipFree(d_part);
+  if (d_rec) (void)hipFree(d_rec);
+  return e;
 }
 
 }  // namespace nbg

@@ -312,5 +312,13 @@ hipError_t ws_path_greedy(Workspace* w, const PathTypes& out_types, const PathGr
 int ws_path_last_rec(Workspace* w);                              // PState record of the last launch
 hipError_t ws_path_read_label(Workspace* w, int lab, uint32_t v, uint32_t* out);   // synchronous
 hipError_t ws_path_sync(Workspace* w, PState* out, int64_t* path, int path_len);
+// partitioned engine (collective: every rank calls these in the same order)
+hipError_t ws_path_level_part(Workspace* w, const PathTypes& pt, int src, uint64_t n_bound, uint64_t e_bound, int dst,
+                              const PathLevel& lv);
+hipError_t ws_path_sync_part(Workspace* w, PState* out);                 // sizes summed over ranks
+hipError_t ws_allreduce_host(Workspace* w, std::vector<unsigned long long>& v);
+// greedy over the in-edges (bwd) of the rank's B-set members; writes the 1 + 3L path entries
+hipError_t ws_path_greedy_part(Workspace* w, const PathTypes& bwd, const PathGreedy& pg, const int64_t* vids,
+                               const uint8_t* visible, int64_t* path);
 
 }  // namespace nbg

@@ -22,6 +22,14 @@
 // (type, rank, dst) edge into the next B-set.  Lexicographic minimality follows because every
 // B-set member extends to a shortest path.
 //
+// Partitioned engine: every rank runs the same sequence collectively.  A level
+// marks next-frontier candidates by global id, the bitmap all-to-all hands them to their owners,
+// and the owner claims them against its own labels (ws_path_level_part) — the meet test and the
+// target count are local at the owner; sizes and "all targets found" are summed over ranks at
+// each synchronisation.  The greedy walks the in-edges of each rank's B-set members (the
+// out-edge v -> u is stored at v's owner, its mirror at u's owner where u's labels are) and
+// takes the minimum of the ranks' candidates, one small all-gather per hop.
+//
 // In-edge records mirror out-edges (InsertEdgeExecutor.cpp:180-196 writes both), so the to-side
 // sees exactly the reverse of the from-side; with a non-default max_edge_returned_per_vertex the
 // two caps differ and the device path reports NBG_E_UNSUPPORTED.
@@ -45,11 +53,26 @@ struct PathCtx {
   PathTypes fwd, bwd;
   uint64_t bwd_edges = 0;   // in-edges over the OVER types (B-set pass bound)
   uint64_t edges = 0;       // BFS edges scanned (both sides)
+  bool part = false;        // partitioned engine: collective levels and greedy
 };
 
 int32_t dev_fail(Engine& E, hipError_t e, const char* what) {
   return E.fail(NBG_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }
+
+hipError_t level(PathCtx& c, const PathTypes& pt, int src, uint64_t n_bound, uint64_t e_bound, int dst,
+                 const PathLevel& lv) {
+  return c.part ? ws_path_level_part(c.ws, pt, src, n_bound, e_bound, dst, lv)
+                : ws_path_level(c.ws, pt, src, n_bound, e_bound, dst, lv);
+}
+
+// sizes of the whole graph (summed over ranks when partitioned)
+hipError_t sync(PathCtx& c, PState* ps) {
+  return c.part ? ws_path_sync_part(c.ws, ps) : ws_path_sync(c.ws, ps, nullptr, 0);
+}
+
+// one id (or none: NO_ROW, a vertex owned by another rank) into a slot
+hipError_t upload1(Workspace* ws, int slot, uint32_t id) { return ws_path_upload(ws, slot, &id, id != NO_ROW); }
 
 // Recover B[i] for i = top-1 .. lo from B[top] (slot `cur`, <= n_top entries) through in-edges:
 // B[i] = { u : u -> B[i+1], forward label of u == i } (i >= 1) or u in S (i == 0).
@@ -73,7 +96,7 @@ hipError_t bsets(PathCtx& c, int cur, uint64_t n_top, int top, int lo, uint32_t 
       lv.rstamp = stamp(es, 0);
     }
     const int dst = cur == S_SET0 ? S_SET0 + 1 : S_SET0;
-    he = ws_path_level(c.ws, c.bwd, cur, nb, c.bwd_edges, dst, lv);
+    he = level(c, c.bwd, cur, nb, c.bwd_edges, dst, lv);
     cur = dst;
     nb = (size_t)i < level_n.size() ? level_n[i] : c.E.snap.nv;
   }
@@ -81,30 +104,43 @@ hipError_t bsets(PathCtx& c, int cur, uint64_t n_top, int top, int lo, uint32_t 
   return he;
 }
 
-int32_t read_path(PathCtx& c, int L, std::vector<int64_t>* path) {
+// Greedy reconstruction of one path of length L and its readback.
+int32_t greedy_path(PathCtx& c, const PathGreedy& g, std::vector<int64_t>* path) {
+  const int L = g.L;
   std::vector<int64_t> p(1 + 3 * (size_t)L);
+  if (c.part) {
+    hipError_t he = ws_path_greedy_part(c.ws, c.bwd, g, c.E.snap.d_vids, c.E.snap.d_visible, p.data());
+    if (he == hipErrorNotFound)
+      return c.E.fail(NBG_E_UNKNOWN, "shortest-path reconstruction failed (in/out edges disagree)");
+    if (he != hipSuccess) return dev_fail(c.E, he, "path reconstruction");
+    *path = std::move(p);
+    return NBG_OK;
+  }
+  hipError_t he = ws_path_greedy(c.ws, c.fwd, g);
+  if (he != hipSuccess) return dev_fail(c.E, he, "path reconstruction");
   PState ps;
-  hipError_t he = ws_path_sync(c.ws, &ps, p.data(), (int)p.size());
+  he = ws_path_sync(c.ws, &ps, p.data(), (int)p.size());
   if (he != hipSuccess) return dev_fail(c.E, he, "path readback");
   if (ps.err) return c.E.fail(NBG_E_UNKNOWN, "shortest-path reconstruction failed (in/out edges disagree)");
   *path = std::move(p);
   return NBG_OK;
 }
 
+// s, t: local ids (NO_ROW on a rank that does not own them)
 int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_paths* out) {
   Workspace* ws = c.ws;
   const uint32_t ef = ws_path_epoch(ws, LAB_F), eb = ws_path_epoch(ws, LAB_B), em = ws_path_epoch(ws, LAB_M);
   hipError_t he = hipSuccess;
   auto T = [&](hipError_t e) { if (he == hipSuccess) he = e; };
-  T(ws_path_upload(ws, S_F0, &s, 1));
-  T(ws_path_upload(ws, S_B0, &t, 1));
-  T(ws_path_upload(ws, S_START, &s, 1));
+  T(upload1(ws, S_F0, s));
+  T(upload1(ws, S_B0, t));
+  T(upload1(ws, S_START, s));
   T(ws_path_stamp(ws, S_F0, 1, LAB_F, stamp(ef, 0)));
   T(ws_path_stamp(ws, S_B0, 1, LAB_B, stamp(eb, 0)));
   T(ws_path_degsum(ws, S_F0, 1, c.fwd, 0));
   T(ws_path_degsum(ws, S_B0, 1, c.bwd, 1));
   PState ps;
-  T(ws_path_sync(ws, &ps, nullptr, 0));
+  T(sync(c, &ps));
   if (he != hipSuccess) return dev_fail(c.E, he, "path setup");
   int fcur = S_F0, bcur = S_B0, kf = 0, kb = 0;
   uint64_t nf = 1, nbk = 1, dsf = ps.dsum[0], dsb = ps.dsum[1];
@@ -120,7 +156,7 @@ int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_pat
       lv.lab = LAB_F;
       lv.stamp = stamp(ef, (uint32_t)kf + 1);
       lv.mstamp = stamp(em, (uint32_t)kf + 1);
-      T(ws_path_level(ws, c.fwd, fcur, nf, dsf, fcur ^ 1, lv));
+      T(level(c, c.fwd, fcur, nf, dsf, fcur ^ 1, lv));
       fcur ^= 1;
       ++kf;
       T(ws_path_degsum(ws, fcur, dsf ? dsf : 1, c.fwd, 0));
@@ -128,13 +164,13 @@ int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_pat
       lv.lab = LAB_B;
       lv.stamp = stamp(eb, (uint32_t)kb + 1);
       lv.mstamp = stamp(em, (uint32_t)kf);
-      T(ws_path_level(ws, c.bwd, bcur, nbk, dsb, bcur ^ 1, lv));
+      T(level(c, c.bwd, bcur, nbk, dsb, bcur ^ 1, lv));
       bcur ^= 1;
       ++kb;
       T(ws_path_degsum(ws, bcur, dsb ? dsb : 1, c.bwd, 1));
     }
     const int rec = ws_path_last_rec(ws) - 1;   // the level's record (degsum took the next one)
-    T(ws_path_sync(ws, &ps, nullptr, 0));
+    T(sync(c, &ps));
     if (he != hipSuccess) return dev_fail(c.E, he, "path level");
     if (rec >= 0 && rec < PATH_REC) c.edges += ps.le[rec];
     nf = ps.n[fcur];
@@ -153,45 +189,49 @@ int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_pat
     int slot = S_MEET;
     T(bsets(c, S_MEET, ps.n[S_MEET], kf, 1, ef, em, 0, fn, &slot));
   }
+  if (he != hipSuccess) return dev_fail(c.E, he, "path B-sets");
   PathGreedy g{L, kf, em, eb, start_slot};
-  T(ws_path_greedy(ws, c.fwd, g));
-  if (he != hipSuccess) return dev_fail(c.E, he, "path reconstruction");
   std::vector<int64_t> p;
-  int32_t rc = read_path(c, L, &p);
+  int32_t rc = greedy_path(c, g, &p);
   if (rc) return rc;
   out->paths.push_back(std::move(p));
   return NBG_OK;
 }
 
-int32_t one_sided(PathCtx& c, const std::vector<uint32_t>& S, const std::vector<uint32_t>& Tg, uint32_t upto,
-                  nbg_paths* out) {
+// S: this rank's sources (local ids); Tg: every target, by global position, as a local id
+// (NO_ROW where another rank owns it); nS: the number of sources over all ranks.
+int32_t one_sided(PathCtx& c, const std::vector<uint32_t>& S, const std::vector<uint32_t>& Tg, uint64_t nS,
+                  uint32_t upto, nbg_paths* out) {
   Workspace* ws = c.ws;
   const uint32_t ef = ws_path_epoch(ws, LAB_F), es = ws_path_epoch(ws, LAB_S), et = ws_path_epoch(ws, LAB_B);
   hipError_t he = hipSuccess;
   auto T = [&](hipError_t e) { if (he == hipSuccess) he = e; };
+  std::vector<uint32_t> Tl;
+  for (uint32_t d : Tg)
+    if (d != NO_ROW) Tl.push_back(d);
   T(ws_path_upload(ws, S_START, S.data(), S.size()));
   T(ws_path_stamp(ws, S_START, S.size(), LAB_S, stamp(es, 0)));
-  T(ws_path_upload(ws, S_MEET, Tg.data(), Tg.size()));
-  T(ws_path_stamp(ws, S_MEET, Tg.size(), LAB_B, stamp(et, 0)));
+  T(ws_path_upload(ws, S_MEET, Tl.data(), Tl.size()));
+  T(ws_path_stamp(ws, S_MEET, Tl.size(), LAB_B, stamp(et, 0)));
   T(ws_path_upload(ws, S_F0, S.data(), S.size()));
   T(ws_path_degsum(ws, S_F0, S.size(), c.fwd, 0));
   PState ps;
-  T(ws_path_sync(ws, &ps, nullptr, 0));
+  T(sync(c, &ps));
   if (he != hipSuccess) return dev_fail(c.E, he, "path setup");
-  std::vector<uint64_t> level_n(1, S.size());
+  std::vector<uint64_t> level_n(1, nS);
   int cur = S_F0;
-  uint64_t n = S.size(), ds = ps.dsum[0];
+  uint64_t n = nS, ds = ps.dsum[0];
   for (uint32_t l = 1; l <= upto; ++l) {
     PathLevel lv;
     lv.lab = LAB_F;
     lv.stamp = stamp(ef, l);
     lv.tlab = LAB_B;
     lv.tstamp = stamp(et, 0);
-    T(ws_path_level(ws, c.fwd, cur, n, ds, cur ^ 1, lv));
+    T(level(c, c.fwd, cur, n, ds, cur ^ 1, lv));
     const int rec = ws_path_last_rec(ws);
     cur ^= 1;
     T(ws_path_degsum(ws, cur, ds ? ds : 1, c.fwd, 0));
-    T(ws_path_sync(ws, &ps, nullptr, 0));
+    T(sync(c, &ps));
     if (he != hipSuccess) return dev_fail(c.E, he, "path level");
     if (rec >= 0 && rec < PATH_REC) c.edges += ps.le[rec];
     n = ps.n[cur];
@@ -199,25 +239,31 @@ int32_t one_sided(PathCtx& c, const std::vector<uint32_t>& S, const std::vector<
     level_n.push_back(n);
     if (n == 0 || ps.found >= Tg.size()) break;
   }
-  // per target: its forward level is its distance
-  std::vector<uint32_t> labels(Tg.size());
+  // per target: its forward level is its distance (read at the owner, summed over ranks)
+  std::vector<unsigned long long> labels(Tg.size(), 0);
   for (size_t i = 0; i < Tg.size(); ++i) {
-    he = ws_path_read_label(ws, LAB_F, Tg[i], &labels[i]);
+    if (Tg[i] == NO_ROW) continue;
+    uint32_t x = 0;
+    he = ws_path_read_label(ws, LAB_F, Tg[i], &x);
     if (he != hipSuccess) return dev_fail(c.E, he, "label readback");
+    labels[i] = x;
+  }
+  if (c.part) {
+    he = ws_allreduce_host(ws, labels);
+    if (he != hipSuccess) return dev_fail(c.E, he, "label exchange");
   }
   for (size_t i = 0; i < Tg.size(); ++i) {
-    if ((labels[i] >> LVL_BITS) != ef) continue;
+    if ((uint32_t)(labels[i] >> LVL_BITS) != ef) continue;
     const int L = (int)(labels[i] & MAX_PATH_LEN);
     const uint32_t em = ws_path_epoch(ws, LAB_M);
-    T(ws_path_upload(ws, S_SET0, &Tg[i], 1));
+    T(upload1(ws, S_SET0, Tg[i]));
     T(ws_path_stamp(ws, S_SET0, 1, LAB_M, stamp(em, (uint32_t)L)));
     int slot = S_SET0;
     T(bsets(c, S_SET0, 1, L, 0, ef, em, es, level_n, &slot));
+    if (he != hipSuccess) return dev_fail(c.E, he, "path B-sets");
     PathGreedy g{L, L, em, 0, slot};
-    T(ws_path_greedy(ws, c.fwd, g));
-    if (he != hipSuccess) return dev_fail(c.E, he, "path reconstruction");
     std::vector<int64_t> p;
-    int32_t rc = read_path(c, L, &p);
+    int32_t rc = greedy_path(c, g, &p);
     if (rc) return rc;
     out->paths.push_back(std::move(p));
   }
@@ -232,7 +278,6 @@ extern "C" int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* rq, nbg_
   Engine& E = h->e;
   std::lock_guard<std::mutex> lg(E.mu);
   if (!E.finalized) return E.fail(NBG_E_STATE, "engine not finalized");
-  if (E.partitioned()) return E.fail(NBG_E_UNSUPPORTED, "FIND PATH on a partitioned engine is not built yet");
   if (hipSetDevice(E.cfg.device) != hipSuccess) return E.fail(NBG_E_DEVICE, "hipSetDevice failed");
   if (!rq->shortest) return E.fail(NBG_E_UNSUPPORTED, "FIND ALL PATH is not supported on the device path yet");
   if (rq->upto > MAX_PATH_LEN) return E.fail(NBG_E_UNSUPPORTED, "UPTO exceeds the device path limit (63)");
@@ -252,24 +297,52 @@ extern "C" int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* rq, nbg_
   if (over.empty()) return E.fail(NBG_E_EXECUTION_ERROR, "empty OVER clause");
   if ((int)over.size() > MAX_TYPES_Q) return E.fail(NBG_E_UNSUPPORTED, "too many OVER types");
   auto* res = new nbg_paths();
-  // from / to: de-duplicated; vertices without rows have no edges on either side
-  std::vector<uint32_t> S, Tg;
+  // from / to: de-duplicated; vertices without rows have no edges on either side.  Partitioned:
+  // each rank resolves the ids it owns, and presence is summed over ranks so that every rank
+  // takes the same branches (all collective calls below happen in the same order everywhere).
+  std::vector<int64_t> fv, tv;
   {
     std::unordered_set<int64_t> seen;
     for (uint64_t i = 0; i < rq->num_from; ++i)
-      if (seen.insert(rq->from[i]).second) {
-        uint32_t d = E.dense(rq->from[i]);
-        if (d != NO_ROW) S.push_back(d);
-      }
+      if (seen.insert(rq->from[i]).second) fv.push_back(rq->from[i]);
     seen.clear();
     for (uint64_t i = 0; i < rq->num_to; ++i)
-      if (seen.insert(rq->to[i]).second) {
-        uint32_t d = E.dense(rq->to[i]);
-        if (d != NO_ROW) Tg.push_back(d);
-      }
+      if (seen.insert(rq->to[i]).second) tv.push_back(rq->to[i]);
   }
-  if (S.empty() || Tg.empty() || rq->upto == 0) { *out = res; return NBG_OK; }
-  PathCtx c{E, E.ws, {}, {}, 0, 0};
+  std::vector<uint32_t> fd(fv.size()), td(tv.size());
+  for (size_t i = 0; i < fv.size(); ++i) fd[i] = E.dense(fv[i]);
+  for (size_t i = 0; i < tv.size(); ++i) td[i] = E.dense(tv[i]);
+  // presence per from / to id, then: rank has OVER out-edges, rank lacks an OVER type's in-edges
+  std::vector<unsigned long long> pres(fv.size() + tv.size() + 2, 0);
+  for (size_t i = 0; i < fv.size(); ++i) pres[i] = fd[i] != NO_ROW;
+  for (size_t i = 0; i < tv.size(); ++i) pres[fv.size() + i] = td[i] != NO_ROW;
+  for (int32_t t : over) {
+    const bool out_edges = E.snap.types.count(t) > 0, in_edges = E.snap.types.count(-t) > 0;
+    if (out_edges) pres[pres.size() - 2] = 1;
+    if (out_edges && !in_edges) pres[pres.size() - 1] = 1;
+  }
+  if (E.partitioned()) {
+    hipError_t he = ws_allreduce_host(E.ws, pres);
+    if (he != hipSuccess) { delete res; return dev_fail(E, he, "path request exchange"); }
+  }
+  if (pres[pres.size() - 1]) {
+    delete res;
+    return E.fail(NBG_E_UNSUPPORTED, "FIND PATH needs the in-edge records of every OVER type");
+  }
+  std::vector<uint32_t> S, Tg;        // local sources; targets by global position (NO_ROW: not here)
+  std::vector<int64_t> Sv, Tv;        // their vids
+  for (size_t i = 0; i < fv.size(); ++i)
+    if (pres[i]) {
+      Sv.push_back(fv[i]);
+      if (fd[i] != NO_ROW) S.push_back(fd[i]);
+    }
+  for (size_t i = 0; i < tv.size(); ++i)
+    if (pres[fv.size() + i]) {
+      Tv.push_back(tv[i]);
+      Tg.push_back(td[i]);
+    }
+  if (Sv.empty() || Tv.empty() || rq->upto == 0 || !pres[pres.size() - 2]) { *out = res; return NBG_OK; }
+  PathCtx c{E, E.ws, {}, {}, 0, 0, E.partitioned()};
   const uint32_t cap = 0x7fffffff;
   auto add = [&](PathTypes& pt, int32_t signed_type) {
     auto it = E.snap.types.find(signed_type);
@@ -290,20 +363,16 @@ extern "C" int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* rq, nbg_
     if (signed_type < 0) c.bwd_edges += dt.num_edges;
   };
   for (int32_t t : over) {
-    const bool out_edges = E.snap.types.count(t) > 0, in_edges = E.snap.types.count(-t) > 0;
-    if (out_edges && !in_edges) {
-      delete res;
-      return E.fail(NBG_E_UNSUPPORTED, "FIND PATH needs the in-edge records of every OVER type");
-    }
     add(c.fwd, t);
     add(c.bwd, -t);
   }
   hipError_t he = ws_path_begin(c.ws, 0, E.snap.nv + S.size() + Tg.size() + 1024);
   if (he != hipSuccess) { delete res; return dev_fail(E, he, "path workspace"); }
   int32_t rc;
-  if (c.fwd.n == 0) rc = NBG_OK;
-  else if (S.size() == 1 && Tg.size() == 1 && S[0] != Tg[0]) rc = bidirectional(c, S[0], Tg[0], rq->upto, res);
-  else rc = one_sided(c, S, Tg, rq->upto, res);
+  if (Sv.size() == 1 && Tv.size() == 1 && Sv[0] != Tv[0])
+    rc = bidirectional(c, S.empty() ? NO_ROW : S[0], Tg[0], rq->upto, res);
+  else
+    rc = one_sided(c, S, Tg, Sv.size(), rq->upto, res);
   if (rc) { delete res; return rc; }
   std::sort(res->paths.begin(), res->paths.end());
   res->edges = c.edges;

@@ -325,6 +325,11 @@ class LocalCluster:
         futs = [self.pool.submit(fn, e) for e in self.engines]
         return [f.result() for f in futs]
 
+    def each_indexed(self, fn):
+        """Run fn(rank, engine) on every rank concurrently."""
+        futs = [self.pool.submit(fn, i, e) for i, e in enumerate(self.engines)]
+        return [f.result() for f in futs]
+
     @property
     def edge_types(self):
         return self.engines[0].edge_types
@@ -364,6 +369,17 @@ class LocalCluster:
             out += rows
         self.last_step_stats = self.engines[0].last_step_stats
         return out
+
+    def find_path(self, *a, stats=None, **k):
+        """FIND SHORTEST PATH, run collectively; every rank reconstructs the same paths."""
+        sts = [dict() for _ in self.engines]
+        res = self.each_indexed(lambda i, e: e.find_path(*a, stats=sts[i], **k))
+        for r in res[1:]:
+            if r != res[0]:
+                raise NbgError(L.E_UNKNOWN, "ranks disagree on the FIND PATH result")
+        if stats is not None:
+            stats.update(sts[0])
+        return res[0]
 
     def close(self):
         self.pool.shutdown()

@@ -128,3 +128,79 @@ def test_partitioned_nba_golden(nba_data):
     finally:
         c.close()
         orc.close()
+
+
+# --------------------------------------------------------------------------- FIND SHORTEST PATH
+# The partitioned BFS claims at the owner after the bitmap all-to-all; B-sets and the greedy are
+# collective.  Every rank returns the same paths, equal to the single engine's and the oracle's.
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_partitioned_shortest_single_pairs(rmat11, world):
+    from nebula_amd import rmat
+    src, single, orc, clusters = rmat11
+    c = clusters[world]
+    found = 0
+    for s, t in rmat.pick_pairs(src, _dst_of(src), 24, seed=world):
+        for upto in (2, 5):
+            st, st1 = {}, {}
+            got = c.find_path([s], [t], [1], upto, stats=st)
+            ref = single.find_path([s], [t], [1], upto, stats=st1)
+            assert got == ref, (world, s, t, upto)
+            assert st["edges"] == st1["edges"]
+            assert got == sorted(orc.find_path([s], [t], [1], upto, True, mode=1))
+            found += len(got)
+    assert found > 0
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_partitioned_shortest_multi_and_self(rmat11, world):
+    from nebula_amd import rmat
+    src, single, orc, clusters = rmat11
+    c = clusters[world]
+    ps = rmat.pick_pairs(src, _dst_of(src), 18, seed=13)
+    for k in range(0, 18, 6):
+        frm = [p[0] for p in ps[k:k + 3]]
+        to = [p[1] for p in ps[k:k + 6]] + [frm[0], 123456789]
+        got = c.find_path(frm + frm[:1], to, [1], 4)
+        assert got == single.find_path(frm + frm[:1], to, [1], 4), (frm, to)
+        assert got == sorted(orc.find_path(frm, to, [1], 4, True, mode=1))
+    s = ps[0][0]
+    assert c.find_path([s], [s], [1], 5) == single.find_path([s], [s], [1], 5)
+    assert c.find_path([s], [123456789], [1], 5) == []
+    assert c.find_path([123456789], [s], [1], 5) == []
+
+
+def test_partitioned_shortest_nba_golden(nba_data):
+    """The reference's FindPathTest golden cases on 3 ranks (7 parts)."""
+    c = LocalCluster(7, 3)
+    for (kind, name), cols in kvgen.NBA_SCHEMAS.items():
+        if kind == "edge":
+            c.register_edge(kvgen.NBA_EDGES[name], name, cols)
+        else:
+            c.register_tag(kvgen.NBA_TAGS[name], name, cols)
+    c.load_builder(kvgen.nba_kv(nba_data, 7))
+    try:
+        checked = 0
+        for case in golden.load("findpath_golden.json"):
+            if golden.unsupported_reason(case):
+                continue
+            try:
+                ok, msg = golden.run_path_case(c, case)
+            except NbgError as ex:
+                if ex.code == _lib.E_UNSUPPORTED:
+                    continue
+                raise
+            assert ok, msg
+            checked += 1
+        assert checked > 0
+    finally:
+        c.close()
+
+
+_DST = {}
+
+
+def _dst_of(src):
+    """The dst array of the module's RMAT-11 graph (pick_pairs draws from both ends)."""
+    if "d" not in _DST:
+        _DST["d"] = graphs.rmat_graph(11)[1]
+    return _DST["d"]

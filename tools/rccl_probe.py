@@ -55,6 +55,17 @@ def main():
                 good = got == ref and stats == single.last_step_stats
                 ok &= good
                 print(f"root {r} steps {steps}: {len(got)} rows {'OK' if good else 'MISMATCH'}", flush=True)
+    # FIND SHORTEST PATH: every rank reconstructs the same paths (collective BFS + greedy)
+    from nebula_amd import rmat
+    for s, t in rmat.pick_pairs(src, dst, 8, seed=17):
+        mine = eng.find_path([s], [t], [1], 5)
+        parts = [None] * world
+        dist.all_gather_object(parts, mine)
+        if rank == 0:
+            ref = single.find_path([s], [t], [1], 5)
+            good = all(p == ref for p in parts)
+            ok &= good
+            print(f"path {s}->{t}: {ref[0] if ref else []} {'OK' if good else 'MISMATCH'}", flush=True)
     dist.barrier()
     if rank == 0:
         print("RCCL partitioned probe:", "PASS" if ok else "FAIL", flush=True)
