@@ -34,8 +34,11 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 # HBM traffic per launch from the committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
 # bench (tools/gpu_check.sh pmc -> tools/pmc_summary.py; FETCH_SIZE doubled per the gfx950 note).
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_v3_pmc_hbm.json")
-PMC_NAMES = {"k_expand<MARK>": "k_expand<0>", "k_expand<FINAL>": "k_expand<1>", "k_expand<BFS>": "k_expand<2>"}
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_v4_pmc_hbm.json")
+# library kernel id -> instantiations in the rocprof names (FINAL: the fast-path instantiation
+# k_expand<3> runs this bench's range WHERE; k_expand<1> is the general interpreter)
+PMC_NAMES = {"k_expand<MARK>": ["k_expand<0>"], "k_expand<FINAL>": ["k_expand<3>", "k_expand<1>"],
+             "k_expand<BFS>": ["k_expand<2>"]}
 
 
 def pmc_traffic(kernel):
@@ -43,10 +46,12 @@ def pmc_traffic(kernel):
     try:
         with open(PMC_FILE) as f:
             d = json.load(f)
-        k = d[PMC_NAMES.get(kernel, kernel)]
-        return k["read_bytes_per_launch_corrected"] + k["write_bytes_per_launch"]
+        for name in PMC_NAMES.get(kernel, [kernel]):
+            if name in d:
+                return d[name]["read_bytes_per_launch_corrected"] + d[name]["write_bytes_per_launch"]
     except (OSError, KeyError, ValueError):
-        return None
+        pass
+    return None
 
 
 def log(*a):
