@@ -13,9 +13,8 @@
  *   nbg_create/…/nbg_finalize  ≙ the storaged data a kvstore part holds: NebulaStore parts
  *       filled through AddEdgesProcessor / AddVerticesProcessor
  *       (src/storage/AddEdgesProcessor.cpp:15-37, src/kvstore/NebulaStore.cpp:326-336)
- *   nbg_get_neighbors          ≙ StorageServiceHandler::future_getBound → QueryBoundProcessor
- *       (src/storage/StorageServiceHandler.cpp:33-40, src/storage/QueryBoundProcessor.cpp:16-220)
  *   nbg_go / nbg_go_device     ≙ GoExecutor result semantics (src/graph/GoExecutor.cpp:83-984)
+ *   nbg_go_prepare / _execute  ≙ GoExecutor::prepare() / execute() (GoExecutor.cpp:28-110)
  *   nbg_find_path              ≙ FindPathExecutor result semantics
  *       (src/graph/FindPathExecutor.cpp:145-715)
  */
@@ -225,7 +224,9 @@ int32_t nbg_profile_read(const nbg_engine* e, nbg_kernel_stat* out, int32_t cap)
  * them (the result is the union over ranks); nbg_rows_step_stats / nbg_rows_edges_scanned
  * report the whole query (summed over ranks).  The communicator must be attached before
  * nbg_finalize (the loader exchanges vertex dictionaries to build global neighbour ids).
- * FIND PATH on a partitioned engine returns NBG_E_UNSUPPORTED in this build. */
+ * nbg_find_path is collective too: each BFS level exchanges its candidate bitmap and the owner
+ * claims (meet / target tests local at the owner, FindPathExecutor.cpp:218-290), sizes are summed
+ * over ranks, and every rank returns the same paths. */
 #define NBG_UNIQUE_ID_BYTES 128
 /* RCCL unique id (ncclGetUniqueId); rank 0 creates it and ships it to the others. */
 int32_t nbg_comm_unique_id(uint8_t out[NBG_UNIQUE_ID_BYTES]);
