@@ -9,6 +9,7 @@
 //     errors fail the query (processFinalResult :948-969).
 // Each hop runs on the device: degree scan -> merge-path partition -> expand (+ byte-flag
 // dedup and compaction, or the final-step bytecode + row compaction).
+#include <chrono>
 #include <algorithm>
 #include <atomic>
 #include <cstring>
@@ -44,7 +45,32 @@ struct nbg_rows {
   std::vector<std::vector<int64_t>> bits;
   std::vector<std::vector<uint8_t>> tags;
   std::vector<std::string> strings;
-  std::vector<Seg> segs;
+  std::vector<Seg> segs;                 // built on first use from the per-workgroup counts
+  struct TypeBlocks {
+    uint64_t region = 0, blk_cap = 0;
+    std::vector<uint32_t> counts;        // rows per workgroup of the final expansion
+  };
+  std::vector<TypeBlocks> blocks;
+  bool segs_built = false;
+  void build_segs() {
+    if (segs_built) return;
+    segs_built = true;
+    size_t n = 0;
+    for (auto& tb : blocks)
+      for (uint32_t c : tb.counts) n += c != 0;
+    segs.reserve(n);
+    for (size_t i = 0; i < blocks.size(); ++i) {
+      const TypeBlocks& tb = blocks[i];
+      for (size_t b = 0; b < tb.counts.size(); ++b) {
+        if (!tb.counts[b]) continue;
+        Seg seg;
+        seg.begin = tb.region + (uint64_t)b * tb.blk_cap;
+        seg.end = seg.begin + tb.counts[b];
+        seg.type = (int)i;
+        segs.push_back(seg);
+      }
+    }
+  }
   uint64_t scanned = 0;
   std::vector<uint64_t> step_frontier, step_edges;
 };
@@ -53,6 +79,7 @@ namespace {
 
 int32_t materialize_rows(nbg_rows* r) {
   if (r->fetched) return NBG_OK;
+  r->build_segs();
   const auto& dict = r->eng->snap.strings;
   r->bits.assign(r->ncols, std::vector<int64_t>(r->count));
   r->tags.assign(r->ncols, std::vector<uint8_t>(r->count));
@@ -239,9 +266,21 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
   return NBG_OK;
 }
 
+// host-side phase timing of go_execute (NBG_HOST_TIMING=1: averages printed by nbg_destroy)
+static struct HostTiming {
+  bool on = getenv("NBG_HOST_TIMING") != nullptr;
+  double t[4] = {0, 0, 0, 0};
+  uint64_t n = 0;
+} g_ht;
+static inline double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* starts, uint64_t num_starts, bool device,
                           nbg_rows** out) {
   if (!out || (num_starts && !starts)) return E.fail(NBG_E_INVALID_ARGUMENT, "null argument");
+  const double ht0 = g_ht.on ? now_us() : 0;
+  double ht1 = 0, ht2 = 0, ht3 = 0;
   *out = nullptr;
   if (hipSetDevice(E.cfg.device) != hipSuccess) return E.fail(NBG_E_DEVICE, "hipSetDevice failed");
   const std::vector<int32_t>& over = st->over;
@@ -323,7 +362,33 @@ static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* start
     region[i] = cap_rows;
     cap_rows += blk_cap[i] * ws_final_grid(n_final, eb);
   }
+  // a short start list travels to the first expansion in its kernel arguments, with its edge
+  // space over each OVER type computed here from the host CSR offsets (no k_relist launch)
+  std::vector<InlineList> inl;
+  if (f0.size() <= (size_t)INLINE_STARTS) {
+    inl.resize(over.size());
+    for (size_t i = 0; i < over.size(); ++i) {
+      InlineList& il = inl[i];
+      il = InlineList{};
+      il.n_in = (uint32_t)f0.size();
+      auto it = E.snap.types.find(over[i]);
+      if (it == E.snap.types.end()) continue;
+      const std::vector<uint32_t>& rp = it->second.h_row_ptr;
+      for (uint32_t d : f0) {
+        if (!E.snap.h_visible.empty() && !E.snap.h_visible[d]) continue;
+        const uint32_t deg = std::min<uint32_t>(rp[d + 1] - rp[d], cap);
+        if (!deg) continue;
+        il.total += deg;
+        il.id[il.n] = d;
+        il.end[il.n] = il.total;
+        il.rs[il.n] = rp[d];
+        ++il.n;
+      }
+    }
+  }
+  auto inl_of = [&](size_t i, uint32_t s) -> const InlineList* { return s == 1 && !inl.empty() ? &inl[i] : nullptr; };
   hipError_t he = ws_reserve_rows(ws, cap_rows, ncols);
+  if (g_ht.on) ht1 = now_us();
   if (he == hipSuccess) he = ws_begin_query(ws, f0.data(), f0.size(), &plist, st->id);
   uint64_t n_bound = f0.size();
   for (uint32_t s = 1; he == hipSuccess && s <= steps; ++s) {
@@ -333,11 +398,12 @@ static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* start
       if (it == E.snap.types.end()) continue;
       ExpandArgs a = args_for(it->second);
       if (!final) {
-        he = ws_expand_mark(ws, a, n_bound, it->second.num_edges, (int)s, (int)i);
+        he = ws_expand_mark(ws, a, n_bound, it->second.num_edges, (int)s, (int)i, inl_of(i, s));
       } else if (deferred || (plist[i].where_const && !plist[i].where_const_val)) {
         he = ws_scan_only(ws, a, n_bound, (int)s, (int)i);
       } else {
-        he = ws_expand_final(ws, a, n_bound, ebound[i], (int)s, (int)i, plist[i], region[i], blk_cap[i]);
+        he = ws_expand_final(ws, a, n_bound, ebound[i], (int)s, (int)i, plist[i], region[i], blk_cap[i],
+                             inl_of(i, s));
       }
     }
     if (!final && he == hipSuccess) {
@@ -354,7 +420,9 @@ static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* start
     }
   }
   if (he == hipSuccess && E.partitioned()) he = ws_global_stats(ws, (int)over.size());
+  if (g_ht.on) ht2 = now_us();
   if (he == hipSuccess) he = ws_end_query(ws);
+  if (g_ht.on) ht3 = now_us();
   if (he != hipSuccess) {
     delete rows;
     return E.fail(NBG_E_DEVICE, std::string("HIP: ") + hipGetErrorString(he));
@@ -384,16 +452,14 @@ static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* start
     rows->const_str.push_back(plist[i].yield_const_str);
     const unsigned grid = ws_final_grid_of(ws, (int)i);   // 0: the final expansion did not run
     const uint32_t* per_block = ws_host_blk_rows(ws, (int)i);
-    for (unsigned b = 0; b < grid; ++b) {
-      uint64_t c = per_block[b];
-      if (!c) continue;
-      nbg_rows::Seg seg;
-      seg.begin = region[i] + (uint64_t)b * blk_cap[i];
-      seg.end = seg.begin + c;
-      seg.type = (int)i;
-      rows->segs.push_back(seg);
-      rows->count += c;
-    }
+    nbg_rows::TypeBlocks tb;
+    tb.region = region[i];
+    tb.blk_cap = blk_cap[i];
+    tb.counts.assign(per_block, per_block + grid);
+    uint64_t c = 0;
+    for (uint32_t x : tb.counts) c += x;
+    rows->count += c;
+    rows->blocks.push_back(std::move(tb));
   }
   for (int c = 0; c < ncols; ++c) rows->dcols.push_back(ws_row_col(ws, c));
   if (!device) {
@@ -401,6 +467,14 @@ static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* start
     if (rc) { delete rows; return E.fail(rc, "row fetch failed"); }
   }
   *out = rows;
+  if (g_ht.on) {
+    const double ht4 = now_us();
+    g_ht.t[0] += ht1 - ht0;   // setup
+    g_ht.t[1] += ht2 - ht1;   // enqueue
+    g_ht.t[2] += ht3 - ht2;   // wait + readback
+    g_ht.t[3] += ht4 - ht3;   // result object
+    g_ht.n++;
+  }
   return NBG_OK;
 }
 
@@ -441,6 +515,11 @@ void nbg_destroy(nbg_engine* h) {
       if (p) (void)hipFree(p);
     for (auto* p : d.narrow)
       if (p) (void)hipFree(p);
+  }
+  if (g_ht.on && g_ht.n) {
+    fprintf(stderr, "[nbg host timing] %llu queries, us/query: setup %.1f enqueue %.1f wait %.1f result %.1f\n",
+            (unsigned long long)g_ht.n, g_ht.t[0] / g_ht.n, g_ht.t[1] / g_ht.n, g_ht.t[2] / g_ht.n, g_ht.t[3] / g_ht.n);
+    g_ht = HostTiming{};
   }
   if (E.snap.d_vids) (void)hipFree(E.snap.d_vids);
   if (E.snap.d_visible) (void)hipFree(E.snap.d_visible);
@@ -579,8 +658,13 @@ const char* nbg_rows_string(const nbg_rows* r, int64_t id) {
   if (!r || id < 0 || id >= (int64_t)r->strings.size()) return nullptr;
   return r->strings[id].c_str();
 }
-int64_t nbg_rows_num_segments(const nbg_rows* r) { return r ? (int64_t)r->segs.size() : -1; }
+int64_t nbg_rows_num_segments(const nbg_rows* r) {
+  if (!r) return -1;
+  const_cast<nbg_rows*>(r)->build_segs();
+  return (int64_t)r->segs.size();
+}
 int32_t nbg_rows_segment(const nbg_rows* r, int64_t i, uint64_t* begin, uint64_t* end) {
+  if (r) const_cast<nbg_rows*>(r)->build_segs();
   if (!r || i < 0 || i >= (int64_t)r->segs.size() || !begin || !end) return NBG_E_INVALID_ARGUMENT;
   *begin = r->segs[i].begin;
   *end = r->segs[i].end;

@@ -44,7 +44,6 @@ static const char* const kKernelNames[K_COUNT] = {"k_relist", "k_expand<MARK>", 
                                                   "k_stamp", "k_pack_bits", "alltoall(xGMI)", "k_bits_compact"};
 constexpr int BITS_BLOCK = BLOCK * 16;           // k_bits_compact: vertices (bits) per block
 
-constexpr int INLINE_STARTS = 32;
 struct InlineIds {                 // a short start list passed by value in the kernel arguments
   uint32_t n;
   uint32_t id[INLINE_STARTS];
@@ -122,6 +121,7 @@ struct Workspace {
   unsigned long long* sendbits = nullptr;   // [world * npad / 64]
   unsigned long long* recvbits = nullptr;   // [world * npad / 64]
   unsigned long long* gst = nullptr;        // [GST_N] globally reduced query statistics
+  hipEvent_t done_ev = nullptr;             // ws_wait's completion event
   unsigned long long* pgst = nullptr;       // [PG_N] globally reduced FIND PATH sizes
   unsigned long long* h_pgst = nullptr;
   unsigned long long* h_gst = nullptr;
@@ -412,7 +412,10 @@ __device__ __forceinline__ void run_program(const Ins* __restrict__ prog, int pc
 
 // ----------------------------------------------------------------------------- k_expand
 // FINALF: the final step with a FastProg program (no interpreter: fewer registers, 8 waves/SIMD)
-enum Mode { MARK = 0, FINAL = 1, BFS = 2, FINALF = 3 };
+// FINALD: FINALF whose YIELDs are only _dst / constants; a tile's rows are stored after the NEXT
+// tile's loads are issued, so waiting for those loads never waits for this tile's stores (on
+// CDNA one counter, vmcnt, retires loads and stores in issue order)
+enum Mode { MARK = 0, FINAL = 1, BFS = 2, FINALF = 3, FINALD = 4 };
 
 // BFS-mode expansion (FIND SHORTEST PATH): every neighbour w is claimed at most once per epoch by
 // a CAS on its label (epoch << LVL_BITS | level); winners are appended, one atomic per tile on a
@@ -495,23 +498,47 @@ __device__ __forceinline__ void wave_lds_sync() {
 // a wave processes tile t, the split of tile t + 2g and the window of tile t + g are in flight
 // (software pipeline, registers).  Items are processed striped across the wave's lanes so
 // neighbour / property reads are coalesced.
-template <int M>
+struct NoInline {};
+template <bool INL>
+using InlineArg = typename std::conditional<INL, InlineList, NoInline>::type;
+
+// INL: the list is the query's start list, passed in the kernel arguments (InlineList) and
+// staged in LDS; its tile splits are counted directly (<= INLINE_STARTS entries).
+template <int M, bool INL = false>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M == FINAL ? 4 : 8)))
 k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_t* __restrict__ seg_end,
          const uint32_t* __restrict__ seg_rs, uint8_t* __restrict__ flags, FinalParams fp, BfsParams bp,
-         unsigned long long* stat_e, unsigned long long* stat_n) {
+         unsigned long long* stat_e, unsigned long long* stat_n, InlineArg<INL> il) {
   __shared__ uint32_t sEndAll[WAVES][TILE + 2];   // per wave: seg_end for i in [a0-1, a1]
   __shared__ uint32_t sRsAll[WAVES][TILE + 1];    // per wave: seg_rs for i in [a0, a1]
   __shared__ uint16_t sSegAll[WAVES][TILE];       // per wave: segment of each edge item
   __shared__ unsigned long long sBase;            // FINAL: rows this workgroup wrote (LDS cursor)
   extern __shared__ int64_t regs[];               // FINAL generic path: [nregs][BLOCK]
 
-  const unsigned long long packed = *acc;  // (list entries << 32 | edges) of the list a.frontier
-  const uint64_t n = packed >> 32;
-  const uint64_t total = packed & 0xFFFFFFFFull;
+  __shared__ uint32_t sIl[INL ? 3 * INLINE_STARTS : 1];   // INL: end[], rs[], id[] of the start list
+  uint64_t n, total;   // list entries, edges
+  if constexpr (INL) {
+    n = il.n;
+    total = il.total;
+#pragma unroll
+    for (int k = 0; k < INLINE_STARTS; ++k)   // constant kernel-argument offsets (no scratch copy)
+      if (threadIdx.x == k) {
+        sIl[k] = il.end[k];
+        sIl[INLINE_STARTS + k] = il.rs[k];
+        sIl[2 * INLINE_STARTS + k] = il.id[k];
+      }
+    __syncthreads();
+  } else {
+    const unsigned long long packed = *acc;   // (list entries << 32 | edges) of the list a.frontier
+    n = packed >> 32;
+    total = packed & 0xFFFFFFFFull;
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (stat_e) *stat_e += total;
-    if (stat_n) *stat_n = n;
+    if (stat_n) {
+      if constexpr (INL) *stat_n = il.n_in;
+      else *stat_n = n;
+    }
   }
   const uint64_t npath = n + total;
   const uint64_t ntiles = (npath + TILE - 1) / TILE;
@@ -521,8 +548,62 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
   uint32_t* const sRs = sRsAll[w];
   uint16_t* const sSeg = sSegAll[w];
   bool anyErr = false;
-  constexpr bool kFinal = M == FINAL || M == FINALF;
-  constexpr bool kFast = M == FINALF;
+  // merge-path split of tile tt (which 0: entries before its start; 1: before its end)
+  auto split_of = [&](uint64_t tt, int which) -> uint64_t {
+    if constexpr (INL) {
+      const uint64_t p = (tt + (uint64_t)which) * TILE;
+      if (which == 1 && p >= npath) return n;
+      uint64_t c = 0;   // entries whose span [j + start_j, j + end_j] ends before p
+      for (uint32_t j = 0; j < (uint32_t)n; ++j) c += (uint64_t)j + sIl[j] < p;
+      return c;
+    } else {
+      return tile_split(a.tsplit, tt, which, npath, n);
+    }
+  };
+  // lane k's entry of a tile's segment-end window (seg_end[a0 - 1 + k]) and row starts (seg_rs[a0 + k])
+  auto stage = [&](uint64_t s0, uint64_t s1, uint32_t* e, uint32_t* r) {
+    if constexpr (INL) {
+      const int na_ = (int)(s1 - s0);
+      if (lane <= na_ + 1) {
+        const int64_t i = (int64_t)s0 - 1 + lane;
+        *e = i < 0 ? 0u : (i < (int64_t)n ? sIl[i] : 0xFFFFFFFFu);
+      }
+      if (lane <= na_) *r = s0 + lane < n ? sIl[INLINE_STARTS + s0 + lane] : 0u;
+    } else {
+      stage_pre(seg_end, seg_rs, n, s0, s1, lane, e, r);
+    }
+  };
+  // the list's vertex at position i
+  auto list_id = [&](uint64_t i) -> uint32_t {
+    if constexpr (INL) return sIl[2 * INLINE_STARTS + i];
+    else return a.frontier[i];
+  };
+  constexpr bool kFinal = M == FINAL || M == FINALF || M == FINALD;
+  constexpr bool kFast = M == FINALF || M == FINALD;
+  constexpr bool kDefer = M == FINALD;
+  int64_t pdv[VT];                 // FINALD: the previous tile's _dst values, pass mask, first row
+  uint32_t ppm = 0;
+  uint64_t preg = 0;
+#pragma unroll
+  for (int i = 0; i < VT; ++i) pdv[i] = 0;
+  uint32_t pu[VT];                 // MARK: the previous tile's neighbours (flags not yet set)
+#pragma unroll
+  for (int i = 0; i < VT; ++i) pu[i] = NO_ROW;
+  int64_t* const* ycols = fp.out_cols;
+  // rows of one tile: ballot-ordered positions from `region`, YIELD y = _dst or a constant
+  auto store_dst_rows = [&](const int64_t* vdv, uint32_t pm, uint64_t region) {
+    uint32_t off = 0;
+#pragma unroll
+    for (int i = 0; i < VT; ++i) {
+      const bool pass = (pm >> i) & 1u;
+      const unsigned long long bal = __ballot(pass);
+      if (!bal) continue;
+      const uint64_t row = region + off + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+      off += (uint32_t)__popcll(bal);
+      if (pass)
+        for (int y = 0; y < fp.nyields; ++y) ycols[y][row] = fp.fast.ykind[y] == 0 ? vdv[i] : fp.yield_const[y];
+    }
+  };
   if (kFinal) {
     if (threadIdx.x == 0) sBase = 0;
     __syncthreads();
@@ -546,12 +627,12 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
   if (t < ntiles) {
     uint64_t sp = 0;
     if (lane < 2) {
-      sp = tile_split(a.tsplit, t, lane, npath, n);
-      if (t + g < ntiles) sp_next = tile_split(a.tsplit, t + g, lane, npath, n);
+      sp = split_of(t, lane);
+      if (t + g < ntiles) sp_next = split_of(t + g, lane);
     }
     a0 = uniform64(__shfl(sp, 0, 64));
     a1 = uniform64(__shfl(sp, 1, 64));
-    stage_pre(seg_end, seg_rs, n, a0, a1, lane, &e_pre, &r_pre);
+    stage(a0, a1, &e_pre, &r_pre);
   }
   for (; t < ntiles; t += g) {
     const uint64_t d0 = t * TILE;
@@ -562,18 +643,20 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
     // the wave's window in LDS (entries past the prefetch loaded directly)
     if (lane <= na + 1) sEnd[lane] = e_pre;
     if (lane <= na) sRs[lane] = r_pre;
-    for (int k = lane + 64; k <= na + 1; k += 64) {
-      const uint64_t i = a0 - 1 + (uint64_t)k;
-      sEnd[k] = i < n ? seg_end[i] : 0xFFFFFFFFu;
-      if (k <= na) sRs[k] = i + 1 < n ? seg_rs[i + 1] : 0u;
+    if constexpr (!INL) {   // (an inline list has <= INLINE_STARTS entries: the prefetch covers it)
+      for (int k = lane + 64; k <= na + 1; k += 64) {
+        const uint64_t i = a0 - 1 + (uint64_t)k;
+        sEnd[k] = i < n ? seg_end[i] : 0xFFFFFFFFu;
+        if (k <= na) sRs[k] = i + 1 < n ? seg_rs[i + 1] : 0u;
+      }
     }
     // prefetch tile t + g's window and tile t + 2g's split
     uint64_t na0 = 0, na1 = 0;
     if (t + g < ntiles) {
       na0 = uniform64(__shfl(sp_next, 0, 64));
       na1 = uniform64(__shfl(sp_next, 1, 64));
-      stage_pre(seg_end, seg_rs, n, na0, na1, lane, &e_pre, &r_pre);
-      if (lane < 2 && t + 2 * g < ntiles) sp_next = tile_split(a.tsplit, t + 2 * g, lane, npath, n);
+      stage(na0, na1, &e_pre, &r_pre);
+      if (lane < 2 && t + 2 * g < ntiles) sp_next = split_of(t + 2 * g, lane);
     }
     wave_lds_sync();
     NBG_PH(0)
@@ -618,9 +701,12 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
           u[i] = a.col[(uint64_t)sRs[s] + (b0 + k - (uint64_t)sEnd[s])];   // sEnd[s] = start of a0+s
         }
       }
+      // the previous tile's flags behind this tile's loads (see FINALD)
 #pragma unroll
-      for (int i = 0; i < VT; ++i)
-        if (u[i] != NO_ROW) flags[u[i]] = 1;
+      for (int i = 0; i < VT; ++i) {
+        if (pu[i] != NO_ROW) flags[pu[i]] = 1;
+        pu[i] = u[i];
+      }
     } else if (M == BFS) {
       uint32_t wv[VT];
       uint32_t cmask = 0, mmask = 0;
@@ -709,6 +795,10 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
 #pragma unroll
             for (int i = 0; i < VT; ++i) x[i] = 0;
         }
+        if (kDefer) {   // the previous tile's rows, behind this tile's loads
+          store_dst_rows(pdv, ppm, preg);
+          ppm = 0;
+        }
 #pragma unroll
         for (int i = 0; i < VT; ++i) {
           const bool act = i * 64 + lane < nb;
@@ -723,7 +813,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
           bool pass = active;
           if (fp.where_reg >= 0) {
             bool werr = false;
-            EdgeCtx c{jj[i], active ? a.frontier[a0 + vv[i]] : 0u};
+            EdgeCtx c{jj[i], active ? list_id(a0 + vv[i]) : 0u};
             run_program(fp.prog, 0, fp.where_len, c, a, regs, active, werr);
             pass = active && !werr && regs[fp.where_reg * BLOCK + threadIdx.x] != 0;
             if (active && werr) anyErr = true;
@@ -743,10 +833,16 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
       NBG_PH(3)
       // phase B: YIELD for the passing items, written at their final rows
       const uint64_t region = fp.region_base + (uint64_t)blockIdx.x * fp.blk_cap + base;
+      if (kDefer) {   // stored behind the next tile's loads (or after the loop)
+#pragma unroll
+        for (int i = 0; i < VT; ++i) pdv[i] = dv[i];
+        ppm = pmask;
+        preg = region;
+      }
       int64_t* const* cols = fp.out_cols;   // kernel-argument array
       uint32_t off = 0;                     // rows of the earlier items of this tile
 #pragma unroll
-      for (int i = 0; i < VT; ++i) {
+      for (int i = 0; i < VT && !kDefer; ++i) {
         const bool pass = (pmask >> i) & 1u;
         const unsigned long long bal = __ballot(pass);
         if (!bal) continue;
@@ -758,7 +854,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
               int64_t val;
               switch (fp.fast.ykind[y]) {
                 case 0: val = dv[i]; break;
-                case 1: val = a.vids[a.frontier[a0 + vv[i]]]; break;
+                case 1: val = a.vids[list_id(a0 + vv[i])]; break;
                 case 2: val = a.rank ? a.rank[jj[i]] : 0; break;
                 case 3: val = load_col(fp.fast.ycol[y], fp.fast.ybytes[y], jj[i]); break;
                 default: val = fp.yield_const[y]; break;
@@ -768,7 +864,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
           }
         } else {
           bool yerr = false;
-          EdgeCtx c{jj[i], pass ? a.frontier[a0 + vv[i]] : 0u};
+          EdgeCtx c{jj[i], pass ? list_id(a0 + vv[i]) : 0u};
           run_program(fp.prog, fp.where_len, fp.prog_len, c, a, regs, pass, yerr);
           if (pass && yerr) anyErr = true;
           if (pass) {
@@ -783,6 +879,12 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
     }
     a0 = na0;
     a1 = na1;
+  }
+  if (kDefer) store_dst_rows(pdv, ppm, preg);   // the wave's last tile
+  if (M == MARK) {
+#pragma unroll
+    for (int i = 0; i < VT; ++i)
+      if (pu[i] != NO_ROW) flags[pu[i]] = 1;
   }
 #ifdef NBG_PHASE_TIMING
   if (kFinal && threadIdx.x == 0 && blockIdx.x % 256 == 0 && ntiles > 8192)
@@ -1031,6 +1133,7 @@ void ws_destroy(Workspace* w) {
                   (void*)w->h_stage})
     if (p) (void)hipHostFree(p);
   if (w->h_pgst) (void)hipHostFree(w->h_pgst);
+  if (w->done_ev) (void)hipEventDestroy(w->done_ev);
   for (void* p : {(void*)w->sendbits, (void*)w->recvbits, (void*)w->gst, (void*)w->pgst})
     if (p) (void)hipFree(p);
   if (w->h_gst) (void)hipHostFree(w->h_gst);
@@ -1073,6 +1176,20 @@ hipError_t ws_reserve_rows(Workspace* w, uint64_t rows, int ncols) {
 // The device QState is already zero (reset behind the previous query's final copy).  A short
 // start list travels inside the first kernel's arguments: a query then begins with a launch, not
 // a copy.  Programs are uploaded when the statement changes.
+// Wait for the engine's stream.  A query's latency ends with this wait, so it polls an event
+// (a host core spins for the few tens of microseconds a query takes) instead of the blocking
+// hipStreamSynchronize; NBG_BLOCKING_SYNC=1 restores the blocking wait.
+hipError_t ws_wait(Workspace* w) {
+  static const bool blocking = getenv("NBG_BLOCKING_SYNC") != nullptr;
+  if (blocking) return hipStreamSynchronize(w->stream);
+  if (!w->done_ev) HIP_TRY(hipEventCreateWithFlags(&w->done_ev, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(w->done_ev, w->stream));
+  hipError_t e;
+  while ((e = hipEventQuery(w->done_ev)) == hipErrorNotReady) {
+  }
+  return e;
+}
+
 hipError_t ws_begin_query(Workspace* w, const uint32_t* starts, uint64_t n, const std::vector<TypeProgram>* progs,
                           uint64_t stmt_id) {
   if (n > w->cap_frontier) return hipErrorInvalidValue;
@@ -1161,8 +1278,25 @@ static unsigned expand_grid(uint64_t n_bound, uint64_t e_bound) {
   return (unsigned)(blocks < EXPAND_GRID ? (blocks ? blocks : 1) : EXPAND_GRID);
 }
 
-hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, uint64_t e_bound, int step, int tix) {
+// The expansion's list is the query's start list, available in inline form.
+static bool inline_start_list(const Workspace* w, int tix, const InlineList* il) {
+  return il && !(tix == 0 && w->seg_ready) && w->list_acc == nullptr && w->start_inline;
+}
+
+hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, uint64_t e_bound, int step, int tix,
+                          const InlineList* il) {
   if (step > MAX_STEPS || tix >= MAX_TYPES_Q) return hipErrorInvalidValue;
+  if (inline_start_list(w, tix, il)) {   // no k_relist: the list travels in the kernel arguments
+    ExpandArgs a = a0;
+    a.frontier = nullptr;
+    a.tsplit = nullptr;
+    hipEvent_t p = prof_begin(w, K_EXPAND_MARK);
+    hipLaunchKernelGGL((k_expand<MARK, true>), dim3(expand_grid(il->n, il->total)), dim3(BLOCK), 0, w->stream, a,
+                       (const unsigned long long*)nullptr, w->seg_end, w->seg_rs, w->flags, FinalParams{},
+                       BfsParams{}, &w->q->e_st[step][tix], &w->q->step_n[step], *il);
+    prof_end(w, p, K_EXPAND_MARK, step, tix);
+    return hipGetLastError();
+  }
   const ListRef L = prepare_list(w, a0, n_bound, step, tix);
   ExpandArgs a = a0;
   a.frontier = L.ids;
@@ -1170,7 +1304,7 @@ hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, 
   FinalParams fp{};
   hipEvent_t p = prof_begin(w, K_EXPAND_MARK);
   hipLaunchKernelGGL(k_expand<MARK>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, L.acc,
-                     w->seg_end, w->seg_rs, w->flags, fp, BfsParams{}, &w->q->e_st[step][tix], L.stat_n);
+                     w->seg_end, w->seg_rs, w->flags, fp, BfsParams{}, &w->q->e_st[step][tix], L.stat_n, NoInline{});
   prof_end(w, p, K_EXPAND_MARK, step, tix);
   return hipGetLastError();
 }
@@ -1289,12 +1423,13 @@ uint64_t ws_shard_cap(uint64_t n_bound, uint64_t e_bound) {
 }
 
 hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, uint64_t e_bound, int step, int tix,
-                           const TypeProgram& prog, uint64_t region_base, uint64_t blk_cap) {
+                           const TypeProgram& prog, uint64_t region_base, uint64_t blk_cap, const InlineList* il) {
   if (step > MAX_STEPS || tix >= MAX_TYPES_Q) return hipErrorInvalidValue;
-  const ListRef L = prepare_list(w, a0, n_bound, step, tix);
+  const bool inl = inline_start_list(w, tix, il);
+  const ListRef L = inl ? ListRef{nullptr, nullptr, &w->q->step_n[step]} : prepare_list(w, a0, n_bound, step, tix);
   ExpandArgs a = a0;
   a.frontier = L.ids;
-  a.tsplit = w->tsplit;
+  a.tsplit = inl ? nullptr : w->tsplit;
   FinalParams fp{};
   fp.prog = w->d_prog + (size_t)tix * MAX_PROGRAM;
   fp.where_len = prog.where_len;
@@ -1312,13 +1447,31 @@ hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound,
   fp.err_flag = &w->q->err;
   fp.fast = detect_fast(prog, a);
   size_t lds = fp.fast.enabled ? 0 : (size_t)(prog.nregs > 0 ? prog.nregs : 1) * BLOCK * sizeof(int64_t);
+  bool dst_only = fp.fast.enabled;   // YIELDs are _dst / constants: the deferred-store instantiation
+  for (int y = 0; y < fp.nyields; ++y) dst_only = dst_only && (fp.fast.ykind[y] == 0 || fp.fast.ykind[y] == 4);
   hipEvent_t p = prof_begin(w, K_EXPAND_FINAL);
-  if (fp.fast.enabled)
-    hipLaunchKernelGGL(k_expand<FINALF>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, L.acc,
-                       w->seg_end, w->seg_rs, w->flags, fp, BfsParams{}, &w->q->e_st[step][tix], L.stat_n);
-  else
-    hipLaunchKernelGGL(k_expand<FINAL>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), lds, w->stream, a, L.acc,
-                       w->seg_end, w->seg_rs, w->flags, fp, BfsParams{}, &w->q->e_st[step][tix], L.stat_n);
+  const dim3 grid(expand_grid(n_bound, e_bound));
+  unsigned long long* e_st = &w->q->e_st[step][tix];
+  if (inl) {
+    if (dst_only)
+      hipLaunchKernelGGL((k_expand<FINALD, true>), grid, dim3(BLOCK), 0, w->stream, a, L.acc, w->seg_end, w->seg_rs,
+                         w->flags, fp, BfsParams{}, e_st, L.stat_n, *il);
+    else if (fp.fast.enabled)
+      hipLaunchKernelGGL((k_expand<FINALF, true>), grid, dim3(BLOCK), 0, w->stream, a, L.acc, w->seg_end, w->seg_rs,
+                         w->flags, fp, BfsParams{}, e_st, L.stat_n, *il);
+    else
+      hipLaunchKernelGGL((k_expand<FINAL, true>), grid, dim3(BLOCK), lds, w->stream, a, L.acc, w->seg_end, w->seg_rs,
+                         w->flags, fp, BfsParams{}, e_st, L.stat_n, *il);
+  } else if (dst_only) {
+    hipLaunchKernelGGL(k_expand<FINALD>, grid, dim3(BLOCK), 0, w->stream, a, L.acc, w->seg_end, w->seg_rs, w->flags,
+                       fp, BfsParams{}, e_st, L.stat_n, NoInline{});
+  } else if (fp.fast.enabled) {
+    hipLaunchKernelGGL(k_expand<FINALF>, grid, dim3(BLOCK), 0, w->stream, a, L.acc, w->seg_end, w->seg_rs, w->flags,
+                       fp, BfsParams{}, e_st, L.stat_n, NoInline{});
+  } else {
+    hipLaunchKernelGGL(k_expand<FINAL>, grid, dim3(BLOCK), lds, w->stream, a, L.acc, w->seg_end, w->seg_rs, w->flags,
+                       fp, BfsParams{}, e_st, L.stat_n, NoInline{});
+  }
   prof_end(w, p, K_EXPAND_FINAL, step, tix, (double)edge_columns_read(prog), (double)fp.nyields);
   w->final_grid[tix] = expand_grid(n_bound, e_bound);
   return hipGetLastError();
@@ -1370,7 +1523,7 @@ hipError_t ws_end_query(Workspace* w) {
     if (w->final_grid[t]) nt = t + 1;
   HIP_TRY(hipMemcpyAsync(w->h_q, w->q, sizeof(QState) + (size_t)nt * EXPAND_GRID * 4, hipMemcpyDeviceToHost,
                          w->stream));
-  HIP_TRY(hipStreamSynchronize(w->stream));
+  HIP_TRY(ws_wait(w));
   // reset for the next query; runs while the host reads the results
   HIP_TRY(hipMemsetAsync(w->q, 0, sizeof(QState), w->stream));
   prof_flush(w, w->h_q);
@@ -1790,7 +1943,7 @@ hipError_t ws_path_level(Workspace* w, const PathTypes& pt, int src, uint64_t n_
     p = prof_begin_p(w, K_BFS);
     hipLaunchKernelGGL(k_expand<BFS>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, acc,
                        w->seg_end, w->seg_rs, (uint8_t*)nullptr, FinalParams{}, bp, &w->ps->le[rec],
-                       (unsigned long long*)nullptr);
+                       (unsigned long long*)nullptr, NoInline{});
     prof_end_p(w, p, K_BFS, rec);
   }
   uint64_t gb = cdiv(n_bound + e_bound + 1, (uint64_t)BLOCK * 4);
@@ -1806,7 +1959,7 @@ int ws_path_last_rec(Workspace* w) { return w->rec - 1; }
 
 hipError_t ws_path_read_label(Workspace* w, int l, uint32_t v, uint32_t* out) {
   HIP_TRY(hipMemcpyAsync(w->h_stage, w->lab[l] + v, sizeof(uint32_t), hipMemcpyDeviceToHost, w->stream));
-  HIP_TRY(hipStreamSynchronize(w->stream));
+  HIP_TRY(ws_wait(w));
   *out = w->h_stage[0];
   return hipSuccess;
 }
@@ -1846,7 +1999,7 @@ hipError_t ws_path_sync(Workspace* w, PState* out, int64_t* path, int path_len) 
   if (path && path_len > 0)
     HIP_TRY(hipMemcpyAsync(w->h_path, w->d_path, (size_t)path_len * sizeof(int64_t), hipMemcpyDeviceToHost,
                            w->stream));
-  HIP_TRY(hipStreamSynchronize(w->stream));
+  HIP_TRY(ws_wait(w));
   if (out) *out = *w->h_ps;
   if (path && path_len > 0) memcpy(path, w->h_path, (size_t)path_len * sizeof(int64_t));
   // resolve timing of the launches since the last sync (record indices stay valid per query)
@@ -2037,7 +2190,7 @@ hipError_t ws_path_level_part(Workspace* w, const PathTypes& pt, int src, uint64
     p = prof_begin_p(w, K_EXPAND_MARK);
     hipLaunchKernelGGL(k_expand<MARK>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, acc,
                        w->seg_end, w->seg_rs, w->flags, FinalParams{}, BfsParams{}, &w->ps->le[rec],
-                       (unsigned long long*)nullptr);
+                       (unsigned long long*)nullptr, NoInline{});
     prof_end_p(w, p, K_EXPAND_MARK, rec);
   }
   const uint64_t G = (uint64_t)w->comm->world;
@@ -2096,7 +2249,7 @@ hipError_t ws_path_sync_part(Workspace* w, PState* out) {
   if (w->comm->allreduce_sum_u64(w->pgst, PG_N, w->stream)) return hipErrorUnknown;
   HIP_TRY(hipMemcpyAsync(w->h_pgst, w->pgst, PG_N * sizeof(unsigned long long), hipMemcpyDeviceToHost, w->stream));
   HIP_TRY(hipMemcpyAsync(w->h_ps, w->ps, sizeof(PState), hipMemcpyDeviceToHost, w->stream));
-  HIP_TRY(hipStreamSynchronize(w->stream));
+  HIP_TRY(ws_wait(w));
   PState g = *w->h_ps;
   for (int k = 0; k < PSLOTS; ++k) g.n[k] = w->h_pgst[k];
   for (int k = 0; k < 2; ++k) g.dsum[k] = w->h_pgst[PSLOTS + k];

@@ -463,6 +463,7 @@ int32_t Engine::finalize() {
             hipMemcpy(snap.d_vids, all.data(), nv * 8, hipMemcpyHostToDevice) == hipSuccess;
   snap.device_bytes += nv * 8;
   if (ok && !all_visible) {
+    snap.h_visible = visible;
     ok = hipMalloc((void**)&snap.d_visible, nv) == hipSuccess &&
          hipMemcpy(snap.d_visible, visible.data(), nv, hipMemcpyHostToDevice) == hipSuccess;
     snap.device_bytes += nv;

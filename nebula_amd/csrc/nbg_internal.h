@@ -88,6 +88,7 @@ struct Snapshot {
   int64_t* d_vids = nullptr;            // dense id -> vid (sorted ascending, signed)
   std::vector<int64_t> h_vids;
   uint8_t* d_visible = nullptr;         // home part == hash part; nullptr when all visible
+  std::vector<uint8_t> h_visible;       // host copy (empty when all visible)
   std::vector<int32_t> h_part;          // home part per dense id
   std::map<int32_t, DevEdgeType> types; // signed type -> CSR
   std::vector<std::string> strings;     // sorted dictionary; device code = 2 * index
@@ -161,6 +162,19 @@ constexpr int TILE = 64 * VT;          // path items (frontier entries + edges) 
 constexpr int NSHARD = 64;             // row-output shards (one counter + region each)
 constexpr int MAX_STEPS = 32;          // GO N STEPS upper bound
 constexpr int MAX_TYPES_Q = 16;        // OVER types per query
+constexpr int INLINE_STARTS = 32;      // start lists up to this size travel in kernel arguments
+
+// A short start list with its edge space over one CSR, built on the host from the CSR offsets
+// (the host copy of row_ptr) and passed by value to the first expansion: the query's first
+// list needs no device pass (no k_relist launch).
+struct InlineList {
+  uint32_t n;                     // entries: the starts with edges
+  uint32_t n_in;                  // starts given (|F_1|: duplicates and edgeless starts included)
+  uint32_t total;                 // edges of the entries (capped degrees)
+  uint32_t id[INLINE_STARTS];
+  uint32_t end[INLINE_STARTS];    // inclusive prefix sums of the degrees
+  uint32_t rs[INLINE_STARTS];     // row starts
+};
 
 // Device-resident state of one query: every size the kernels need, so a query is enqueued
 // without host synchronisation; the host reads it back once at the end.
@@ -261,13 +275,15 @@ const uint32_t* ws_current_frontier(Workspace* w);
 hipError_t ws_begin_query(Workspace* w, const uint32_t* starts, uint64_t n, const std::vector<TypeProgram>* progs,
                           uint64_t stmt_id);
 // steps 1..N-1, per OVER type: scan + expand into next-frontier flags
-hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a, uint64_t n_bound, uint64_t e_bound, int step, int tix);
+// il: the start list's inline form for this type (used when the list is the query's start list)
+hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a, uint64_t n_bound, uint64_t e_bound, int step, int tix,
+                          const InlineList* il = nullptr);
 // after all types of a step: flags -> next frontier
 // next0: the first OVER type's CSR of step + 1 (its degree pass is fused into the compaction)
 hipError_t ws_compact(Workspace* w, int step, const ExpandArgs* next0);
 // step N, per OVER type: scan + WHERE/YIELD + sharded row emission into [region_base, +NSHARD*shard_cap)
 hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a, uint64_t n_bound, uint64_t e_bound, int step, int tix,
-                           const TypeProgram& prog, uint64_t region_base, uint64_t blk_cap);
+                           const TypeProgram& prog, uint64_t region_base, uint64_t blk_cap, const InlineList* il = nullptr);
 hipError_t ws_scan_only(Workspace* w, const ExpandArgs& a, uint64_t n_bound, int step, int tix);
 hipError_t ws_end_query(Workspace* w);
 // partitioned mode: flags over [world * npad) global ids, per-hop bitmap all-to-all

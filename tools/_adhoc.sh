@@ -1,2 +1,5 @@
-cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/ld
-timeout -k 10 400 python -u bench.py --scale 24 --steps 1 --warmup 1 --sp-pairs 0 --no-cpu-baseline --no-profile --roots 16 > gpurun_out/ld/s24.json 2>gpurun_out/ld/s24.log
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/ht
+for v in base spin base2 spin2; do
+  if [ "${v:0:4}" = spin ]; then export NBG_SPIN_SYNC=1; else unset NBG_SPIN_SYNC; fi
+  NBG_HOST_TIMING=1 timeout -k 10 200 python -u bench.py --steps 3 --sp-pairs 0 --no-cpu-baseline --no-profile > gpurun_out/ht/$v.json 2>gpurun_out/ht/$v.log || exit 1
+done
