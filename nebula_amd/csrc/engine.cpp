@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstring>
+#include <set>
 
 #include "engine.h"
 
@@ -117,7 +118,7 @@ int32_t materialize_rows(nbg_rows* r) {
   return NBG_OK;
 }
 
-const char* kGoUnsupportedDistinct = "YIELD DISTINCT is not supported on the device path yet";
+const char* kGoUnsupportedDistinct = "YIELD DISTINCT is not supported on a partitioned engine yet";
 
 }  // namespace
 
@@ -133,7 +134,21 @@ struct nbg_go_stmt {
   uint32_t steps = 1;
   int32_t deferred = NBG_OK;         // name-resolution error, reported only if the final step runs
   std::string deferred_msg;
+  std::string dst_unknown;           // a $$ tag name is unknown: fails once the final step has edges
+  bool distinct = false;             // YIELD DISTINCT: distinct starts and rows
 };
+
+// Props a query names on each edge alias (Expression::prepare's alias set, Expressions.cpp:314-400)
+static void alias_props(const Node* n, std::map<std::string, std::set<std::string>>& out) {
+  if (!n) return;
+  switch (n->kind) {
+    case EK_ALIAS: case EK_DST: case EK_SRCID: case EK_RANK: case EK_TYPE:
+      out[n->alias].insert(n->prop);
+      break;
+    default: break;
+  }
+  for (auto& k : n->kids) alias_props(k.get(), out);
+}
 
 static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out) {
   if (!rq || !out) return E.fail(NBG_E_INVALID_ARGUMENT, "null argument");
@@ -153,7 +168,7 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
     }
   }
   if (over.empty()) return E.fail(NBG_E_EXECUTION_ERROR, "empty OVER clause");
-  if (rq->distinct) return E.fail(NBG_E_UNSUPPORTED, kGoUnsupportedDistinct);
+  if (rq->distinct && E.partitioned()) return E.fail(NBG_E_UNSUPPORTED, kGoUnsupportedDistinct);
   // WHERE / YIELD
   std::string err;
   std::unique_ptr<Node> where;
@@ -181,12 +196,32 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
   // compile per OVER type; name-resolution errors are reported only if the final step runs
   std::map<int32_t, TypeProgram> progs;
   int32_t deferred = NBG_OK;
-  std::string deferred_msg;
+  std::string deferred_msg, dst_unknown;
+  std::map<std::string, std::set<std::string>> named;
+  alias_props(where.get(), named);
+  for (auto& y : yields) alias_props(y.get(), named);
   for (int32_t t : over) {
     auto it = E.snap.types.find(t);
     CompileEnv env{t, &over, &E.edges, &E.snap.strings,
                    it != E.snap.types.end() && it->second.valid != nullptr,
                    it != E.snap.types.end() && it->second.rank != nullptr};
+    // the response edge row schema of type t: _dst, then the props named on t (getStepOutProps,
+    // GoExecutor.cpp:587-630)
+    std::map<std::string, VKind> row_cols{{"_dst", VK_INT}};
+    const SchemaSet& es = E.edges[t];
+    for (auto& p : named[es.name]) {
+      if (p == "_src" || p == "_dst" || p == "_type" || p == "_rank") { row_cols.emplace(p, VK_INT); continue; }
+      const Schema* sc = es.latest();
+      const int c = sc ? sc->find(p) : -1;
+      if (c >= 0) row_cols.emplace(p, kindOfType(sc->cols[c].type));
+    }
+    uint32_t probe = 0;
+    env.tags = &E.tags;
+    env.dtags = &E.snap.tags;
+    env.row_cols = &row_cols;
+    env.partitioned = E.partitioned();
+    env.dst_unknown = &dst_unknown;
+    env.probe_mask = &probe;
     ProgramBuilder pb;
     TypeProgram tp;
     tp.etype = t;
@@ -242,6 +277,7 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
       continue;
     }
     tp.code = pb.code;
+    tp.probe_mask = probe;
     tp.nregs = std::max(1, pb.max_reg);
     if ((int)tp.code.size() > MAX_PROGRAM) return E.fail(NBG_E_UNSUPPORTED, "program too long");
     progs[t] = std::move(tp);
@@ -262,6 +298,8 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
   st->steps = rq->steps;
   st->deferred = deferred;
   st->deferred_msg = deferred_msg;
+  st->dst_unknown = dst_unknown;
+  st->distinct = rq->distinct != 0;
   *out = st;
   return NBG_OK;
 }
@@ -296,6 +334,10 @@ static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* start
     uint32_t d = E.dense(starts[i]);
     if (d != NO_ROW) f0.push_back(d);
   }
+  if (st->distinct) {   // DISTINCT de-duplicates the starts too (GoExecutor.cpp:101-107)
+    std::sort(f0.begin(), f0.end());
+    f0.erase(std::unique(f0.begin(), f0.end()), f0.end());
+  }
   auto* rows = new nbg_rows();
   rows->eng = &E;
   rows->ncols = ncols;
@@ -328,6 +370,9 @@ static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* start
     a.hnarrow = dt.narrow.empty() ? nullptr : dt.narrow.data();
     a.hnarrow_bytes = dt.narrow_bytes.empty() ? nullptr : dt.narrow_bytes.data();
     a.cap = cap;
+    a.tcols = E.snap.d_tcols;
+    a.tpres = E.snap.d_tpres;
+    a.gbase = E.partitioned() ? (uint32_t)((uint64_t)E.cfg.rank * E.npad) : 0u;
     return a;
   };
   // the start list keeps duplicates, so its edge space is the one frontier not bounded by E:
@@ -429,9 +474,9 @@ static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* start
   }
   const QState& q = *ws_host_state(ws);
   // statistics of the whole query: this engine's, or summed over all ranks when partitioned
-  unsigned long long g_err = q.err, g_n[MAX_STEPS + 2], g_e[MAX_STEPS + 2];
+  unsigned long long g_err = q.err, g_n[MAX_STEPS + 2], g_e[MAX_STEPS + 2], g_tb = q.tagbits;
   if (E.partitioned()) {
-    ws_host_gstats(ws, &g_err, g_n, g_e);
+    ws_host_gstats(ws, &g_err, g_n, g_e, &g_tb);
   } else {
     for (int s = 0; s < MAX_STEPS + 2; ++s) {
       g_n[s] = q.step_n[s];
@@ -446,7 +491,16 @@ static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* start
   }
   const bool reached_final = g_n[steps] > 0;
   if (reached_final && deferred) { delete rows; return E.fail(deferred, st->deferred_msg); }
+  if (reached_final && g_e[steps] > 0 && !st->dst_unknown.empty()) {
+    delete rows;
+    return E.fail(NBG_E_EXECUTION_ERROR, st->dst_unknown);
+  }
   if (g_err) { delete rows; return E.fail(NBG_E_EXECUTION_ERROR, "WHERE/YIELD evaluation error"); }
+  // a $$ default read for a tag no final destination has: VertexHolder::defaultFor fails
+  if ((g_tb >> MAX_TAG_BITS) & ~g_tb & ((1ull << MAX_TAG_BITS) - 1)) {
+    delete rows;
+    return E.fail(NBG_E_EXECUTION_ERROR, "Unknown Vertex");
+  }
   for (size_t i = 0; i < over.size(); ++i) {
     rows->kinds.push_back(plist[i].yield_kind);
     rows->const_str.push_back(plist[i].yield_const_str);
@@ -460,6 +514,30 @@ static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* start
     for (uint32_t x : tb.counts) c += x;
     rows->count += c;
     rows->blocks.push_back(std::move(tb));
+  }
+  if (st->distinct && rows->count) {
+    // YIELD DISTINCT on the device: segments deduplicated and compacted in place
+    std::vector<std::array<uint64_t, 3>> segs;
+    std::vector<std::pair<size_t, size_t>> where;   // (type, block) of each segment
+    for (size_t i = 0; i < rows->blocks.size(); ++i) {
+      const auto& tb = rows->blocks[i];
+      for (size_t b = 0; b < tb.counts.size(); ++b) {
+        if (!tb.counts[b]) continue;
+        segs.push_back({tb.region + (uint64_t)b * tb.blk_cap, tb.counts[b], (uint64_t)i});
+        where.emplace_back(i, b);
+      }
+    }
+    std::vector<uint32_t> kept;
+    hipError_t de = ws_distinct(ws, segs, ncols, rows->kinds, &kept);
+    if (de != hipSuccess) {
+      delete rows;
+      return E.fail(NBG_E_DEVICE, std::string("HIP (distinct): ") + hipGetErrorString(de));
+    }
+    rows->count = 0;
+    for (size_t k = 0; k < segs.size(); ++k) {
+      rows->blocks[where[k].first].counts[where[k].second] = kept[k];
+      rows->count += kept[k];
+    }
   }
   for (int c = 0; c < ncols; ++c) rows->dcols.push_back(ws_row_col(ws, c));
   if (!device) {
@@ -521,6 +599,13 @@ void nbg_destroy(nbg_engine* h) {
             (unsigned long long)g_ht.n, g_ht.t[0] / g_ht.n, g_ht.t[1] / g_ht.n, g_ht.t[2] / g_ht.n, g_ht.t[3] / g_ht.n);
     g_ht = HostTiming{};
   }
+  for (auto& kv : E.snap.tags) {
+    if (kv.second.present) (void)hipFree(kv.second.present);
+    for (auto* p : kv.second.cols)
+      if (p) (void)hipFree(p);
+  }
+  if (E.snap.d_tcols) (void)hipFree(E.snap.d_tcols);
+  if (E.snap.d_tpres) (void)hipFree(E.snap.d_tpres);
   if (E.snap.d_vids) (void)hipFree(E.snap.d_vids);
   if (E.snap.d_visible) (void)hipFree(E.snap.d_visible);
   if (E.stream) (void)hipStreamDestroy(E.stream);

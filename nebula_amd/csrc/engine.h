@@ -18,7 +18,7 @@ struct Engine {
   std::map<int32_t, SchemaSet> tags;
   // staging (until finalize)
   std::map<int32_t, EdgeStage> stage;   // signed type -> records
-  std::vector<std::pair<int64_t, int32_t>> tag_vertices;
+  std::map<int32_t, TagStage> tstage;   // tag id -> vertex records
   std::vector<std::string> pool;        // string props, load order
   std::unordered_map<std::string, int64_t> pool_index;
   uint64_t seq = 0;
@@ -44,6 +44,7 @@ struct Engine {
   int32_t load_edges(int32_t type, const int64_t* src, const int64_t* dst, const int64_t* rank, uint64_t n,
                      const void* const* cols, int32_t ncols);
   int32_t finalize();
+  int32_t build_tags(const std::vector<int64_t>& dict, const std::vector<int64_t>& remap);
   int32_t exchange_dictionary(const std::vector<int64_t>& local, std::vector<int64_t>* gdict,
                               std::vector<uint64_t>* gcount);
   uint32_t dense(int64_t vid) const;

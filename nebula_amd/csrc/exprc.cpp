@@ -390,6 +390,100 @@ struct Ctx {
     return NBG_OK;
   }
 
+  const SchemaSet* tag_by_name(const std::string& name, int32_t* tag) {
+    if (!env.tags) return nullptr;
+    for (auto& kv : *env.tags) {
+      if (kv.second.name == name) { *tag = kv.first; return &kv.second; }
+    }
+    return nullptr;
+  }
+  int64_t default_bits(VKind k) {   // RowReader::getDefaultProp: 0, 0.0, false, ""
+    return k == VK_STRING ? string_code(*env.strings, "") : 0;
+  }
+  // the tag column `e.prop` of tag `e.alias`: NBG_OK with *col < 0 when the prop is unknown
+  int32_t tag_column(const Node& e, const DevTag** dt, int* col) {
+    int32_t tid;
+    const SchemaSet* ts = tag_by_name(e.alias, &tid);
+    *col = -1;
+    *dt = nullptr;
+    if (!ts) return NBG_E_TAG_PROP_NOT_FOUND;
+    if (!env.dtags || !env.dtags->count(tid)) {
+      *err = "tag tables missing";
+      return NBG_E_UNSUPPORTED;
+    }
+    *dt = &env.dtags->at(tid);
+    const Schema* sc = ts->latest();
+    *col = sc ? sc->find(e.prop) : -1;
+    return NBG_OK;
+  }
+
+  // $^.tag.prop: GoExecutor's source getter over the getNeighbors tag data
+  // (GoExecutor.cpp:888-905); the tag / prop name checks are the storage request's
+  // (getStepOutProps :603-612, QueryBaseProcessor.inl:77-100) and fail the final step.
+  int32_t leaf_src_tag(const Node& e, Compiled* out) {
+    const DevTag* dt;
+    int col;
+    int32_t rc = tag_column(e, &dt, &col);
+    if (rc == NBG_E_TAG_PROP_NOT_FOUND) {
+      *err = "No schema found for '" + e.alias + "'";
+      return NBG_E_EXECUTION_ERROR;   // deferred to the final step
+    }
+    if (rc) return rc;
+    if (col < 0) {
+      *err = "Get neighbors failed: prop `" + e.alias + "." + e.prop + "' not found";
+      return NBG_E_IMPROPER_DATA_TYPE;   // deferred to the final step
+    }
+    Compiled c;
+    c.kind = dt->kind[col];
+    const int32_t aux = (dt->index << 16) | (dt->col_base + col);
+    const bool has_default = env.row_cols && env.row_cols->count(e.prop);
+    c.reg = push();
+    if (!has_default) {
+      emit(OP_TAGS_E, c.reg, 0, 0, aux, 0);   // no such column in the row schema: "Unknown type"
+    } else {
+      if (env.row_cols->at(e.prop) != c.kind) {
+        *err = "$^ prop whose missing-tag default has another type";
+        return NBG_E_UNSUPPORTED;
+      }
+      emit(OP_TAGS, c.reg, 0, 0, aux, default_bits(c.kind));
+    }
+    *out = c;
+    return NBG_OK;
+  }
+
+  // $$.tag.prop: VertexHolder::get over the final destinations' tag data (GoExecutor.cpp:986-1064)
+  int32_t leaf_dst_tag(const Node& e, Compiled* out) {
+    const DevTag* dt;
+    int col;
+    int32_t rc = tag_column(e, &dt, &col);
+    if (rc == NBG_E_TAG_PROP_NOT_FOUND) {
+      // fetchVertexProps fails the query once the final step returned edges (GoExecutor.cpp:652-690)
+      if (env.dst_unknown && env.dst_unknown->empty()) *env.dst_unknown = "No schema found for '" + e.alias + "'";
+      *out = make_error();
+      return NBG_OK;
+    }
+    if (rc) return rc;
+    if (col < 0) {   // getVertexProps rejects the request: the holder is empty -> "Unknown Vertex"
+      *out = make_error();
+      return NBG_OK;
+    }
+    if (dt->index >= MAX_TAG_BITS) {
+      *err = "$$ over more than 16 tags";
+      return NBG_E_UNSUPPORTED;
+    }
+    Compiled c;
+    c.kind = dt->kind[col];
+    if (env.partitioned && c.kind == VK_STRING) {
+      *err = "$$ STRING props on a partitioned engine";
+      return NBG_E_UNSUPPORTED;
+    }
+    c.reg = push();
+    emit(OP_TAGD, c.reg, 0, 0, (dt->index << 16) | (dt->col_base + col), default_bits(c.kind));
+    if (env.probe_mask) *env.probe_mask |= 1u << dt->index;
+    *out = c;
+    return NBG_OK;
+  }
+
   int32_t compile(const Node& e, Compiled* out) {
     // constant subtrees fold on the host with the reference's exact rules
     {
@@ -412,8 +506,8 @@ struct Ctx {
         *out = make_const(CVal(e.alias));
         return NBG_OK;
       }
-      case EK_SRCPROP: *err = "$^ tag props are not supported on the device path yet"; return NBG_E_UNSUPPORTED;
-      case EK_DSTPROP: *err = "$$ tag props are not supported on the device path yet"; return NBG_E_UNSUPPORTED;
+      case EK_SRCPROP: return leaf_src_tag(e, out);
+      case EK_DSTPROP: return leaf_dst_tag(e, out);
       case EK_INPUT: case EK_VAR: *err = "input/variable props are not supported"; return NBG_E_UNSUPPORTED;
       case EK_FUNC: *err = "function calls are not supported"; return NBG_E_UNSUPPORTED;
       case EK_UNARY: {

@@ -35,6 +35,15 @@ struct CompileEnv {
   const std::vector<std::string>* strings;         // sorted string dictionary
   bool has_valid;                                  // the type has edges without a decoded value
   bool has_rank;
+  // tag props ($^ / $$)
+  const std::map<int32_t, SchemaSet>* tags = nullptr;   // registered tag schemas
+  const std::map<int32_t, DevTag>* dtags = nullptr;     // device tag tables (index, columns, kinds)
+  // $^ of a source without the tag reads RowReader::getDefaultProp of the RESPONSE edge row
+  // schema (GoExecutor.cpp:896-898): `_dst` plus every prop the query names on this edge type
+  const std::map<std::string, VKind>* row_cols = nullptr;
+  bool partitioned = false;
+  std::string* dst_unknown = nullptr;   // set when a $$ tag name is unknown (fails iff E_N > 0)
+  uint32_t* probe_mask = nullptr;       // tags read through $$
 };
 
 // Result of compiling one expression for one edge type.

@@ -23,6 +23,7 @@
 // neighbours are in memcmp key order, the cap counts edges in that order) and
 // GoExecutor::getDstIdsFromResp (per-step dst SET, no global visited set).
 #include <hip/hip_runtime.h>
+#include <array>
 
 #include <cstdio>
 #include <cstring>
@@ -99,6 +100,15 @@ struct Workspace {
   uint64_t cap_rows = 0;
   int ncols_alloc = 0;
   int64_t** d_row_cols = nullptr; // device array of column pointers
+  // YIELD DISTINCT scratch (grown on demand): open-addressing row table, keep flags, segments
+  unsigned long long* dtab = nullptr;
+  uint64_t dtab_cap = 0;
+  uint8_t* dkeep = nullptr;
+  uint64_t dkeep_cap = 0;
+  uint64_t* dseg = nullptr;
+  uint64_t dseg_cap = 0;
+  uint32_t* dcnt = nullptr;
+  uint8_t* dkinds = nullptr;
   Ins* d_prog = nullptr;          // [MAX_TYPES_Q][MAX_PROGRAM]
   // FIND PATH (allocated on first use)
   PState* ps = nullptr;
@@ -343,7 +353,7 @@ __device__ __forceinline__ int64_t fbits(double d) { return __double_as_longlong
 // lane per register ([reg][BLOCK]); instruction fetch is wave-uniform (scalar loads).
 __device__ __forceinline__ void run_program(const Ins* __restrict__ prog, int pc0, int pc1, const EdgeCtx& c,
                                             const ExpandArgs& a, int64_t* __restrict__ regs, bool active,
-                                            bool& err) {
+                                            bool& err, uint32_t& tbits) {
   const int tid = threadIdx.x;
   for (int pc = pc0; pc < pc1; ++pc) {
     const Ins ins = prog[pc];
@@ -363,6 +373,26 @@ __device__ __forceinline__ void run_program(const Ins* __restrict__ prog, int pc
       case OP_SRC: r = active ? a.vids[c.v] : 0; break;
       case OP_RANK: r = (active && a.rank) ? a.rank[c.j] : 0; break;
       case OP_ERR: err = true; break;
+      case OP_TAGS:
+      case OP_TAGS_E:
+        if (active) {
+          const uint32_t v = a.gbase + c.v;
+          if (a.tpres[ins.aux >> 16][v]) r = a.tcols[ins.aux & 0xFFFF][v];
+          else if (ins.op == OP_TAGS) r = ins.imm;
+          else err = true;
+        }
+        break;
+      case OP_TAGD:
+        if (active) {
+          const uint32_t v = a.col[c.j];
+          if (v != NO_ROW && a.tpres[ins.aux >> 16][v]) {
+            r = a.tcols[ins.aux & 0xFFFF][v];
+          } else {
+            r = ins.imm;
+            tbits |= 1u << (MAX_TAG_BITS + (ins.aux >> 16));
+          }
+        }
+        break;
       case OP_ADD_I: r = (int64_t)((uint64_t)x + (uint64_t)y); break;
       case OP_SUB_I: r = (int64_t)((uint64_t)x - (uint64_t)y); break;
       case OP_MUL_I: r = (int64_t)((uint64_t)x * (uint64_t)y); break;
@@ -453,6 +483,8 @@ struct FinalParams {
   uint64_t blk_cap;       // rows per workgroup region (each workgroup appends to its own region)
   uint32_t* blk_rows;     // [gridDim.x] rows written per workgroup
   unsigned long long* err_flag;
+  uint32_t probe_mask;             // tags read through $$ (presence probed for every final edge)
+  unsigned long long* tag_bits;    // QState::tagbits
   FastProg fast;
 };
 
@@ -548,6 +580,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
   uint32_t* const sRs = sRsAll[w];
   uint16_t* const sSeg = sSegAll[w];
   bool anyErr = false;
+  uint32_t tbits = 0;              // FINAL: $$ holder bits (QState::tagbits)
   // merge-path split of tile tt (which 0: entries before its start; 1: before its end)
   auto split_of = [&](uint64_t tt, int which) -> uint64_t {
     if constexpr (INL) {
@@ -811,10 +844,18 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
           const int k = i * 64 + lane;
           const bool active = k < nb;
           bool pass = active;
+          if (fp.probe_mask && active) {   // the holder: every final destination's tags
+            const uint32_t d = a.col[jj[i]];
+            if (d != NO_ROW)
+              for (uint32_t m = fp.probe_mask; m; m &= m - 1) {
+                const int t = __builtin_ctz(m);
+                if (a.tpres[t][d]) tbits |= 1u << t;
+              }
+          }
           if (fp.where_reg >= 0) {
             bool werr = false;
             EdgeCtx c{jj[i], active ? list_id(a0 + vv[i]) : 0u};
-            run_program(fp.prog, 0, fp.where_len, c, a, regs, active, werr);
+            run_program(fp.prog, 0, fp.where_len, c, a, regs, active, werr, tbits);
             pass = active && !werr && regs[fp.where_reg * BLOCK + threadIdx.x] != 0;
             if (active && werr) anyErr = true;
           }
@@ -865,7 +906,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
         } else {
           bool yerr = false;
           EdgeCtx c{jj[i], pass ? list_id(a0 + vv[i]) : 0u};
-          run_program(fp.prog, fp.where_len, fp.prog_len, c, a, regs, pass, yerr);
+          run_program(fp.prog, fp.where_len, fp.prog_len, c, a, regs, pass, yerr, tbits);
           if (pass && yerr) anyErr = true;
           if (pass) {
             for (int y = 0; y < fp.nyields; ++y) {
@@ -895,6 +936,12 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
     __syncthreads();   // every wave of the workgroup has reserved its rows
     if (threadIdx.x == 0) fp.blk_rows[blockIdx.x] = (uint32_t)sBase;
     if (anyErr) atomicOr(fp.err_flag, 1ull);
+    if (M == FINAL && fp.probe_mask) {
+      // OR over the wave, one atomic per wave with bits
+      uint32_t x = tbits;
+      for (int o = 32; o; o >>= 1) x |= (uint32_t)__shfl_xor((int)x, o, 64);
+      if (lane == 0 && x) atomicOr(fp.tag_bits, (unsigned long long)x);
+    }
   }
 }
 
@@ -963,10 +1010,13 @@ __global__ void k_note(const unsigned long long* __restrict__ acc, unsigned long
 }
 
 // Query statistics every rank needs globally: [err, step_n[0..MAX_STEPS+1], Σ_types e_st[s]].
-constexpr int GST_N = 1 + 2 * (MAX_STEPS + 2);
+// Then one counter per QState::tagbits bit (summed: > 0 is the OR over ranks).
+constexpr int GST_N0 = 1 + 2 * (MAX_STEPS + 2);
+constexpr int GST_N = GST_N0 + 2 * MAX_TAG_BITS;
 __global__ void k_gstats(const QState* __restrict__ q, int ntypes, unsigned long long* __restrict__ g) {
   const int s = threadIdx.x;
   if (s == 0) g[0] = q->err ? 1ull : 0ull;
+  if (s < 2 * MAX_TAG_BITS) g[GST_N0 + s] = (q->tagbits >> s) & 1ull;
   if (s < MAX_STEPS + 2) {
     g[1 + s] = q->step_n[s];
     unsigned long long e = 0;
@@ -985,6 +1035,92 @@ __global__ void __launch_bounds__(BLOCK) k_pack_rows(const uint64_t* __restrict_
     const uint64_t b = seg[3 * k], len = seg[3 * k + 1], o = seg[3 * k + 2];
     for (int c = 0; c < ncols; ++c)
       for (uint64_t i = threadIdx.x; i < len; i += BLOCK) out[(uint64_t)c * total + o + i] = cols[c][b + i];
+  }
+}
+
+// ----------------------------------------------------------------------------- YIELD DISTINCT
+// GoExecutor::setupInterimResult keeps the first row of each distinct encoded row
+// (GoExecutor.cpp:771-778).  A row's identity here is its value kinds (per OVER type) plus its
+// 8-byte payloads — the encoded row up to the RowWriter framing.  k_distinct_mark inserts every
+// row into an open-addressing table (CAS on an empty slot; a lost race re-compares), flagging the
+// winners; k_distinct_compact then compacts each result segment in place, stably.
+// seg[4k..4k+3] = (first row, rows, flag offset, OVER type index); kinds[type * MAX_YIELDS + c].
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_distinct_mark(const uint64_t* __restrict__ seg, int nseg,
+                                                         int64_t* const* __restrict__ cols, int ncols,
+                                                         const uint8_t* __restrict__ kinds,
+                                                         unsigned long long* __restrict__ tab, uint64_t tmask,
+                                                         uint8_t* __restrict__ keep) {
+  for (int k = blockIdx.x; k < nseg; k += gridDim.x) {
+    const uint64_t b = seg[4 * k], len = seg[4 * k + 1], fo = seg[4 * k + 2];
+    const uint32_t ty = (uint32_t)seg[4 * k + 3];
+    for (uint64_t i = threadIdx.x; i < len; i += BLOCK) {
+      const uint64_t row = b + i;
+      uint64_t h = 0x6E6562756C61ull;
+      for (int c = 0; c < ncols; ++c)
+        h = mix64(h ^ (uint64_t)cols[c][row] ^ ((uint64_t)kinds[ty * MAX_YIELDS + c] << 61) ^ (uint64_t)c);
+      const unsigned long long me = ((unsigned long long)ty << 48) | (row + 1);
+      bool kept = false;
+      for (uint64_t p = h & tmask;; p = (p + 1) & tmask) {
+        unsigned long long cur = tab[p];
+        if (cur == 0ull) {
+          cur = atomicCAS(tab + p, 0ull, me);
+          if (cur == 0ull) { kept = true; break; }
+        }
+        const uint64_t orow = (cur & ((1ull << 48) - 1)) - 1;
+        const uint32_t oty = (uint32_t)(cur >> 48);
+        bool eq = true;
+        for (int c = 0; c < ncols && eq; ++c)
+          eq = cols[c][orow] == cols[c][row] && kinds[oty * MAX_YIELDS + c] == kinds[ty * MAX_YIELDS + c];
+        if (eq) break;
+      }
+      keep[fo + i] = kept ? 1 : 0;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_distinct_compact(const uint64_t* __restrict__ seg, int nseg,
+                                                            int64_t* const* __restrict__ cols, int ncols,
+                                                            const uint8_t* __restrict__ keep,
+                                                            uint32_t* __restrict__ counts) {
+  __shared__ uint32_t wsum[WAVES];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int k = blockIdx.x; k < nseg; k += gridDim.x) {
+    const uint64_t b = seg[4 * k], len = seg[4 * k + 1], fo = seg[4 * k + 2];
+    uint64_t out = 0;
+    for (uint64_t c0 = 0; c0 < len; c0 += BLOCK) {
+      const uint64_t i = c0 + threadIdx.x;
+      const bool kp = i < len && keep[fo + i];
+      int64_t v[MAX_YIELDS];
+#pragma unroll
+      for (int c = 0; c < MAX_YIELDS; ++c)
+        if (c < ncols && kp) v[c] = cols[c][b + i];
+      const unsigned long long bal = __ballot(kp);
+      if (lane == 0) wsum[wv] = (uint32_t)__popcll(bal);
+      __syncthreads();   // every read of this chunk precedes its writes (positions <= reads)
+      uint32_t before = 0, tot = 0;
+      for (int x = 0; x < WAVES; ++x) {
+        if (x < wv) before += wsum[x];
+        tot += wsum[x];
+      }
+      if (kp) {
+        const uint64_t dst = b + out + before + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+#pragma unroll
+        for (int c = 0; c < MAX_YIELDS; ++c)
+          if (c < ncols) cols[c][dst] = v[c];
+      }
+      out += tot;
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) counts[k] = (uint32_t)out;
   }
 }
 
@@ -1127,7 +1263,8 @@ void ws_destroy(Workspace* w) {
   for (void* p : {(void*)w->frontier[0], (void*)w->frontier[1], (void*)w->seg_end, (void*)w->seg_rs,
                   (void*)w->rlist, (void*)w->flags, (void*)w->tsplit,
                   (void*)w->q, (void*)w->rows,
-                  (void*)w->d_row_cols, (void*)w->d_prog})
+                  (void*)w->d_row_cols, (void*)w->d_prog, (void*)w->dtab, (void*)w->dkeep, (void*)w->dseg,
+                  (void*)w->dcnt, (void*)w->dkinds})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)w->h_q, (void*)w->h_starts, (void*)w->h_prog, (void*)w->h_ps, (void*)w->h_path,
                   (void*)w->h_stage})
@@ -1445,6 +1582,8 @@ hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound,
   fp.blk_cap = blk_cap;
   fp.blk_rows = w->blk_rows + (size_t)tix * EXPAND_GRID;
   fp.err_flag = &w->q->err;
+  fp.probe_mask = prog.probe_mask;
+  fp.tag_bits = &w->q->tagbits;
   fp.fast = detect_fast(prog, a);
   size_t lds = fp.fast.enabled ? 0 : (size_t)(prog.nregs > 0 ? prog.nregs : 1) * BLOCK * sizeof(int64_t);
   bool dst_only = fp.fast.enabled;   // YIELDs are _dst / constants: the deferred-store instantiation
@@ -1475,6 +1614,62 @@ hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound,
   prof_end(w, p, K_EXPAND_FINAL, step, tix, (double)edge_columns_read(prog), (double)fp.nyields);
   w->final_grid[tix] = expand_grid(n_bound, e_bound);
   return hipGetLastError();
+}
+
+// YIELD DISTINCT over the result segments (synchronous): rows of each segment compacted in place,
+// new row counts per segment in `counts`.  segs: (first row, rows, OVER type index).
+hipError_t ws_distinct(Workspace* w, const std::vector<std::array<uint64_t, 3>>& segs, int ncols,
+                       const std::vector<std::vector<VKind>>& kinds, std::vector<uint32_t>* counts) {
+  counts->assign(segs.size(), 0);
+  if (segs.empty() || !ncols) return hipSuccess;
+  if (kinds.size() > (size_t)MAX_TYPES_Q) return hipErrorInvalidValue;
+  uint64_t total = 0;
+  std::vector<uint64_t> meta;
+  for (auto& sg : segs) {
+    meta.insert(meta.end(), {sg[0], sg[1], total, sg[2]});
+    total += sg[1];
+  }
+  if (!total) return hipSuccess;
+  uint64_t tcap = 1024;
+  while (tcap < 2 * total) tcap <<= 1;
+  HIP_TRY(hipStreamSynchronize(w->stream));
+  if (tcap > w->dtab_cap) {
+    if (w->dtab) HIP_TRY(hipFree(w->dtab));
+    w->dtab = nullptr;
+    HIP_TRY(hipMalloc((void**)&w->dtab, tcap * 8));
+    w->dtab_cap = tcap;
+  }
+  if (total > w->dkeep_cap) {
+    if (w->dkeep) HIP_TRY(hipFree(w->dkeep));
+    w->dkeep = nullptr;
+    HIP_TRY(hipMalloc((void**)&w->dkeep, total));
+    w->dkeep_cap = total;
+  }
+  if (segs.size() > w->dseg_cap) {
+    if (w->dseg) HIP_TRY(hipFree(w->dseg));
+    if (w->dcnt) HIP_TRY(hipFree(w->dcnt));
+    w->dseg = nullptr;
+    w->dcnt = nullptr;
+    HIP_TRY(hipMalloc((void**)&w->dseg, segs.size() * 32));
+    HIP_TRY(hipMalloc((void**)&w->dcnt, segs.size() * 4));
+    w->dseg_cap = segs.size();
+  }
+  if (!w->dkinds) HIP_TRY(hipMalloc((void**)&w->dkinds, MAX_TYPES_Q * MAX_YIELDS));
+  uint8_t hk[MAX_TYPES_Q * MAX_YIELDS] = {};
+  for (size_t t = 0; t < kinds.size(); ++t)
+    for (size_t c = 0; c < kinds[t].size() && c < (size_t)MAX_YIELDS; ++c) hk[t * MAX_YIELDS + c] = (uint8_t)kinds[t][c];
+  HIP_TRY(hipMemcpy(w->dkinds, hk, sizeof(hk), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(w->dseg, meta.data(), meta.size() * 8, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemsetAsync(w->dtab, 0, tcap * 8, w->stream));
+  const unsigned grid = (unsigned)std::min<uint64_t>(segs.size(), 8192);
+  hipLaunchKernelGGL(k_distinct_mark, dim3(grid), dim3(BLOCK), 0, w->stream, w->dseg, (int)segs.size(), w->d_row_cols,
+                     ncols, w->dkinds, w->dtab, tcap - 1, w->dkeep);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_distinct_compact, dim3(grid), dim3(BLOCK), 0, w->stream, w->dseg, (int)segs.size(),
+                     w->d_row_cols, ncols, w->dkeep, w->dcnt);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(counts->data(), w->dcnt, segs.size() * 4, hipMemcpyDeviceToHost, w->stream));
+  return hipStreamSynchronize(w->stream);
 }
 
 // Scan-only expansion (final step whose WHERE folded to false still counts E_N).
@@ -1586,8 +1781,12 @@ hipError_t ws_global_stats(Workspace* w, int ntypes) {
   return hipMemcpyAsync(w->h_gst, w->gst, GST_N * sizeof(unsigned long long), hipMemcpyDeviceToHost, w->stream);
 }
 
-void ws_host_gstats(Workspace* w, unsigned long long* err, unsigned long long* step_n, unsigned long long* esum) {
+void ws_host_gstats(Workspace* w, unsigned long long* err, unsigned long long* step_n, unsigned long long* esum,
+                    unsigned long long* tagbits) {
   *err = w->h_gst[0];
+  *tagbits = 0;
+  for (int b = 0; b < 2 * MAX_TAG_BITS; ++b)
+    if (w->h_gst[GST_N0 + b]) *tagbits |= 1ull << b;
   for (int s = 0; s < MAX_STEPS + 2; ++s) {
     step_n[s] = w->h_gst[1 + s];
     esum[s] = w->h_gst[1 + (MAX_STEPS + 2) + s];

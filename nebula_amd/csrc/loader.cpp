@@ -144,9 +144,27 @@ int32_t Engine::load_part_kv(int32_t part, const uint8_t* kd, const uint64_t* ko
         st.valid.push_back(ok ? 1 : 0);
       }
     } else if (klen == 24) {
+      // vertex key (NebulaKeyUtils::vertexKey, NebulaKeyUtils.cpp:12-26): part | vid | tag | version
+      int32_t tag;
       int64_t vid;
+      uint64_t ver;
       memcpy(&vid, k + 4, 8);
-      tag_vertices.emplace_back(vid, item >> 8);   // tag records (props: §8(f) next)
+      memcpy(&tag, k + 12, 4);
+      memcpy(&ver, k + 16, 8);
+      if (tag & 0x40000000) continue;
+      TagStage& ts = tstage[tag];
+      ts.vid.push_back(vid);
+      ts.verkey.push_back(bswap64(ver));
+      ts.seq.push_back(seq++);
+      ts.part.push_back(item >> 8);
+      auto sit = tags.find(tag);
+      const Schema* latest = sit == tags.end() ? nullptr : sit->second.latest();
+      size_t nc = latest ? latest->cols.size() : 0;
+      if (ts.props.size() < nc) ts.props.resize(nc);
+      props.assign(nc, 0);
+      bool ok = latest && decode_row(sit->second, v, vlen, props.data());
+      for (size_t c = 0; c < nc; ++c) ts.props[c].push_back(ok ? props[c] : 0);
+      ts.valid.push_back(ok ? 1 : 0);
     }
   }
   return NBG_OK;
@@ -253,6 +271,82 @@ int32_t Engine::exchange_dictionary(const std::vector<int64_t>& local, std::vect
   return done(NBG_OK, "");
 }
 
+// Tag records -> per-vertex columns (the live record of each (vid, tag) is the newest version,
+// i.e. the first key of the vertex prefix, QueryBaseProcessor::collectVertexProps,
+// QueryBaseProcessor.inl:354-378).  Partitioned engines gather every rank's columns into the
+// global id space, so a `$$` read of a remote destination stays a local load.
+int32_t Engine::build_tags(const std::vector<int64_t>& dict, const std::vector<int64_t>& remap) {
+  const uint64_t nv = dict.size();
+  const uint64_t G = (uint64_t)cfg.num_gpus;
+  const uint64_t local = partitioned() ? npad : nv;          // rows of the local arrays
+  const uint64_t space = partitioned() ? G * npad : nv;      // rows of the device arrays
+  std::vector<int64_t*> all_cols;
+  std::vector<uint8_t*> all_pres;
+  void* d_stage = nullptr;
+  auto up = [&](void** dst, const void* src, size_t bytes) -> bool {
+    if (hipMalloc(dst, std::max<size_t>(bytes, 8)) != hipSuccess) return false;
+    snap.device_bytes += bytes;
+    if (!bytes) return true;
+    if (!partitioned()) return !src || hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess;
+    // local rows -> staging -> all-gather into the global id space
+    const size_t lb = bytes / G;
+    if (hipMemcpy(d_stage, src, lb, hipMemcpyHostToDevice) != hipSuccess) return false;
+    return comm->allgather(d_stage, *dst, lb, stream) == 0 && hipStreamSynchronize(stream) == hipSuccess;
+  };
+  if (partitioned() && hipMalloc(&d_stage, std::max<uint64_t>(local, 1) * 8) != hipSuccess)
+    return fail(NBG_E_OUT_OF_MEMORY, "tag staging");
+  int32_t rc = NBG_OK;
+  for (auto& kv : tags) {
+    const int32_t tag = kv.first;
+    const Schema* latest = kv.second.latest();
+    const size_t nc = latest ? latest->cols.size() : 0;
+    DevTag& dt = snap.tags[tag];
+    dt.tag = tag;
+    dt.index = (int)all_pres.size();
+    dt.col_base = (int)all_cols.size();
+    for (size_t c = 0; c < nc; ++c) dt.kind.push_back(kindOfType(latest->cols[c].type));
+    std::vector<uint8_t> pres(local, 0);
+    std::vector<std::vector<int64_t>> cols(nc, std::vector<int64_t>(local, 0));
+    auto it = tstage.find(tag);
+    if (it != tstage.end()) {
+      const TagStage& ts = it->second;
+      std::vector<int64_t> best(local, -1);   // record index of the live version per vertex
+      for (size_t i = 0; i < ts.vid.size(); ++i) {
+        auto p = std::lower_bound(dict.begin(), dict.end(), ts.vid[i]);
+        const uint64_t d = (uint64_t)(p - dict.begin());
+        const int64_t b = best[d];
+        if (b < 0 || ts.verkey[i] < ts.verkey[b] || (ts.verkey[i] == ts.verkey[b] && ts.seq[i] > ts.seq[b]))
+          best[d] = (int64_t)i;
+      }
+      for (uint64_t d = 0; d < nv; ++d) {
+        const int64_t b = best[d];
+        if (b < 0) continue;
+        pres[d] = 1;
+        for (size_t c = 0; c < nc && c < ts.props.size(); ++c) {
+          int64_t x = ts.props[c][b];
+          if (dt.kind[c] == VK_STRING && ts.valid[b]) x = remap[x];
+          cols[c][d] = x;
+        }
+      }
+    }
+    bool ok = up((void**)&dt.present, pres.data(), space);
+    dt.cols.assign(nc, nullptr);
+    for (size_t c = 0; ok && c < nc; ++c) ok = up((void**)&dt.cols[c], cols[c].data(), space * 8);
+    if (!ok) { rc = fail(NBG_E_OUT_OF_MEMORY, "device allocation failed for tag columns"); break; }
+    all_pres.push_back(dt.present);
+    for (auto* p : dt.cols) all_cols.push_back(p);
+  }
+  if (d_stage) (void)hipFree(d_stage);
+  if (rc) return rc;
+  bool ok = hipMalloc((void**)&snap.d_tcols, std::max<size_t>(all_cols.size(), 1) * 8) == hipSuccess &&
+            hipMalloc((void**)&snap.d_tpres, std::max<size_t>(all_pres.size(), 1) * 8) == hipSuccess;
+  if (ok && !all_cols.empty())
+    ok = hipMemcpy(snap.d_tcols, all_cols.data(), all_cols.size() * 8, hipMemcpyHostToDevice) == hipSuccess;
+  if (ok && !all_pres.empty())
+    ok = hipMemcpy(snap.d_tpres, all_pres.data(), all_pres.size() * 8, hipMemcpyHostToDevice) == hipSuccess;
+  return ok ? NBG_OK : fail(NBG_E_OUT_OF_MEMORY, "device allocation failed for the tag tables");
+}
+
 int32_t Engine::finalize() {
   if (finalized) return fail(NBG_E_STATE, "engine already finalized");
   // 1. string dictionary: sorted; device code = 2 * rank
@@ -274,6 +368,7 @@ int32_t Engine::finalize() {
     for (auto& kv : stage) tot += kv.second.src.size();
     all.reserve(tot);
     for (auto& kv : stage) all.insert(all.end(), kv.second.src.begin(), kv.second.src.end());
+    for (auto& kv : tstage) all.insert(all.end(), kv.second.vid.begin(), kv.second.vid.end());
     __gnu_parallel::sort(all.begin(), all.end());
     all.erase(std::unique(all.begin(), all.end()), all.end());
   }
@@ -303,6 +398,14 @@ int32_t Engine::finalize() {
       if (!__atomic_compare_exchange_n(&home[d], &expected, st.part[i], false, __ATOMIC_RELAXED, __ATOMIC_RELAXED) &&
           expected != st.part[i])
         split = true;
+    }
+  }
+  for (auto& kv : tstage) {
+    const TagStage& ts = kv.second;
+    for (size_t i = 0; i < ts.vid.size(); ++i) {
+      const uint32_t d = dense(ts.vid[i]);
+      if (home[d] == 0) home[d] = ts.part[i];
+      else if (home[d] != ts.part[i]) split = true;
     }
   }
   if (split) return fail(NBG_E_UNSUPPORTED, "vertex rows split across partitions");
@@ -459,6 +562,8 @@ int32_t Engine::finalize() {
     st = EdgeStage();
   }
   if (rc) return rc;
+  rc = build_tags(all, remap);
+  if (rc) return rc;
   bool ok = hipMalloc((void**)&snap.d_vids, std::max<uint64_t>(nv, 1) * 8) == hipSuccess &&
             hipMemcpy(snap.d_vids, all.data(), nv * 8, hipMemcpyHostToDevice) == hipSuccess;
   snap.device_bytes += nv * 8;
@@ -470,6 +575,7 @@ int32_t Engine::finalize() {
   }
   if (!ok) return fail(NBG_E_OUT_OF_MEMORY, "device allocation failed for the vertex table");
   stage.clear();
+  tstage.clear();
   pool.clear();
   pool_index.clear();
   finalized = true;

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime_api.h>
 
+#include <array>
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -60,6 +61,15 @@ struct EdgeStage {              // one signed edge type, before finalize
   std::vector<uint8_t> valid;                // value decoded (positive types)
 };
 
+struct TagStage {               // one tag's vertex records, before finalize
+  std::vector<int64_t> vid;
+  std::vector<uint64_t> verkey; // version bytes read big-endian (memcmp order: newest first)
+  std::vector<uint64_t> seq;
+  std::vector<int32_t> part;
+  std::vector<std::vector<int64_t>> props;   // [col][i] 8-byte payload (latest schema order)
+  std::vector<uint8_t> valid;
+};
+
 // ----------------------------------------------------------------------------- device snapshot
 struct DevBuf {
   void* p = nullptr;
@@ -83,6 +93,17 @@ struct DevEdgeType {            // CSR for one signed edge type over this rank's
   std::vector<uint32_t> h_row_ptr;   // host copy (path reconstruction, host planning)
 };
 
+// Tag properties of one tag, indexed by vertex id (single GPU: dense id; partitioned: global id,
+// gathered from every rank at finalize so `$$` reads a remote destination's props locally).
+struct DevTag {
+  int32_t tag = 0;
+  int index = 0;                // position in Snapshot::d_tpres
+  int col_base = 0;             // first column in Snapshot::d_tcols
+  uint8_t* present = nullptr;   // [tag_space] the vertex has a record of this tag
+  std::vector<int64_t*> cols;   // [ncols][tag_space] latest-schema columns
+  std::vector<VKind> kind;
+};
+
 struct Snapshot {
   uint64_t nv = 0;
   int64_t* d_vids = nullptr;            // dense id -> vid (sorted ascending, signed)
@@ -92,6 +113,9 @@ struct Snapshot {
   std::vector<int32_t> h_part;          // home part per dense id
   std::map<int32_t, DevEdgeType> types; // signed type -> CSR
   std::vector<std::string> strings;     // sorted dictionary; device code = 2 * index
+  std::map<int32_t, DevTag> tags;       // tag id -> per-vertex columns
+  int64_t** d_tcols = nullptr;          // device array: every tag column (DevTag::col_base + c)
+  uint8_t** d_tpres = nullptr;          // device array: presence per tag (DevTag::index)
   uint64_t device_bytes = 0;
   uint64_t max_edges() const {
     uint64_t m = 0;
@@ -111,6 +135,10 @@ enum Op : uint8_t {
   OP_SRC,        // r[d] = vid of the source vertex
   OP_RANK,       // r[d] = rank[j] (0 when no rank column)
   OP_ERR,        // error flag := 1 (statically ill-typed node, still evaluated)
+  // tag props; aux = tag index << 16 | tag column (Snapshot::d_tpres / d_tcols)
+  OP_TAGS,       // r[d] = $^ prop of the source vertex; imm when the vertex lacks the tag
+  OP_TAGS_E,     // same, but a vertex without the tag is an evaluation error
+  OP_TAGD,       // r[d] = $$ prop of the destination; imm (+ the tag's "default used" bit) when absent
   // int64
   OP_ADD_I, OP_SUB_I, OP_MUL_I, OP_DIV_I, OP_MOD_I, OP_XOR_I, OP_NEG_I,
   OP_LT_I, OP_LE_I, OP_GT_I, OP_GE_I, OP_EQ_I, OP_NE_I,
@@ -150,6 +178,7 @@ struct TypeProgram {
   std::vector<int64_t> yield_const;   // constant payload when yield_reg == -1
   std::vector<std::string> yield_const_str;   // string constants (may be absent from the dictionary)
   bool needs_error_check = false;  // any op can raise an error
+  uint32_t probe_mask = 0;         // tags read through $$: presence probed for every final edge
   int nregs = 0;
 };
 
@@ -163,6 +192,7 @@ constexpr int NSHARD = 64;             // row-output shards (one counter + regio
 constexpr int MAX_STEPS = 32;          // GO N STEPS upper bound
 constexpr int MAX_TYPES_Q = 16;        // OVER types per query
 constexpr int INLINE_STARTS = 32;      // start lists up to this size travel in kernel arguments
+constexpr int MAX_TAG_BITS = 16;       // tags addressable by $$ (QState::tagbits: has | used << 16)
 
 // A short start list with its edge space over one CSR, built on the host from the CSR offsets
 // (the host copy of row_ptr) and passed by value to the first expansion: the query's first
@@ -185,6 +215,9 @@ struct QState {
   unsigned long long acc[4];           // packed list sizes (entries << 32 | edges): relist 0/1, compaction 2/3
   unsigned long long step_n[MAX_STEPS + 2];              // frontier size entering step s
   unsigned long long e_st[MAX_STEPS + 2][MAX_TYPES_Q];   // edges per (step, type)
+  // $$ holder semantics (GoExecutor::VertexHolder, GoExecutor.cpp:986-1064): bit t = some final
+  // destination has tag t; bit 16 + t = a row read tag t's default for a destination without it
+  unsigned long long tagbits;
 };
 
 struct ExpandArgs {                // one (step, edge type) expansion
@@ -202,6 +235,9 @@ struct ExpandArgs {                // one (step, edge type) expansion
   const int64_t* const* hprops;    // host array of the same column pointers (host-side planning)
   void* const* hnarrow;            // host array: narrow copies of INT columns (nullptr: none)
   const int* hnarrow_bytes;
+  const int64_t* const* tcols;     // tag columns (Snapshot::d_tcols), indexed by vertex id
+  const uint8_t* const* tpres;     // tag presence (Snapshot::d_tpres)
+  uint32_t gbase;                  // id of local vertex 0 in the tag index space (rank * npad)
 };
 
 // ----------------------------------------------------------------------------- FIND PATH state
@@ -269,6 +305,9 @@ const uint32_t* ws_host_blk_rows(Workspace* w, int tix);    // rows per workgrou
 hipError_t ws_fetch_rows(Workspace* w, const std::vector<std::pair<uint64_t, uint64_t>>& segs, int ncols,
                          uint64_t total, int64_t* const* host_cols);
 const QState* ws_host_state(Workspace* w);       // valid after ws_end_query
+// YIELD DISTINCT: dedup + in-place compaction of result segments (first row, rows, OVER index)
+hipError_t ws_distinct(Workspace* w, const std::vector<std::array<uint64_t, 3>>& segs, int ncols,
+                       const std::vector<std::vector<VKind>>& kinds, std::vector<uint32_t>* counts);
 const uint32_t* ws_current_frontier(Workspace* w);
 
 // Query pipeline (all asynchronous on the workspace stream until ws_end_query):
@@ -291,7 +330,8 @@ constexpr uint64_t PART_ALIGN = 16384 * 4;   // npad granularity (flag / bit wor
 hipError_t ws_set_partition(Workspace* w, Comm* comm, uint64_t npad);
 hipError_t ws_exchange(Workspace* w, int step, const ExpandArgs* next0);   // replaces ws_compact
 hipError_t ws_global_stats(Workspace* w, int ntypes);      // before ws_end_query
-void ws_host_gstats(Workspace* w, unsigned long long* err, unsigned long long* step_n, unsigned long long* esum);
+void ws_host_gstats(Workspace* w, unsigned long long* err, unsigned long long* step_n, unsigned long long* esum,
+                    unsigned long long* tagbits);
 
 // FIND SHORTEST PATH (kernels.hip).  Frontier lists live in numbered device slots; PState sizes
 // are read back by ws_path_sync.  All calls enqueue on the workspace stream.

@@ -55,3 +55,67 @@ def multiset_digest(cols: list[np.ndarray]) -> tuple:
         for c in cols:
             h = rmat.splitmix64(h ^ c.astype(np.uint64))
     return (len(h), int(np.bitwise_xor.reduce(h)), int(h.sum(dtype=np.uint64)))
+
+
+# ---------------------------------------------------------------------------- tagged two-type graph
+# Vertices carry tag `person(age INT, score DOUBLE, name STRING)` (about 85 %) and/or `city(pop INT)`
+# (about 20 %); tag `ghost(g INT)` is registered with no records.  Edge types e(w INT), f(k INT).
+# Loaded through the KV path on both sides, so tag records, versions and in-edge mirrors follow
+# the reference's AddVerticesProcessor / AddEdgesProcessor key layout.
+T_PERSON, T_CITY, T_GHOST, E_F = 11, 12, 13, 2
+PERSON = [("age", kvgen.INT), ("score", kvgen.DOUBLE), ("name", kvgen.STRING)]
+CITY = [("pop", kvgen.INT)]
+GHOST = [("g", kvgen.INT)]
+F_SCHEMA = [("k", kvgen.INT)]
+
+
+def tagged_kv(scale, parts=7, seed=5):
+    """(src, persons, kb): edge sources, vids with a person tag, the KV records."""
+    src, dst, w = rmat.rmat_edges(scale, seed=seed)
+    rng = np.random.default_rng(seed)
+    kb = kvgen.KVBuilder(parts)
+    now = 1_600_000_000_000_000
+    verts = np.unique(np.concatenate([src, dst]))
+    persons = []
+    for v in verts.tolist():
+        r = rng.random()
+        if r < 0.85:
+            age = int(rng.integers(10, 60))
+            kb.insert_vertex(v, T_PERSON, PERSON, [age, float(rng.random() * 10), f"p{age % 13}"], now)
+            persons.append(v)
+            if r < 0.05:   # a newer version of the same tag record wins
+                kb.insert_vertex(v, T_PERSON, PERSON, [age + 1, 0.5, "renamed"], now + 9)
+        if 0.7 < r < 0.9:
+            kb.insert_vertex(v, T_CITY, CITY, [int(rng.integers(0, 1000))], now + 1)
+    for i, (s, d, x) in enumerate(zip(src.tolist(), dst.tolist(), w.tolist())):
+        if i % 3:
+            kb.insert_edge(s, d, E_TYPE, 0, E_SCHEMA, [x], now + 2)
+        else:
+            kb.insert_edge(s, d, E_F, 0, F_SCHEMA, [x % 7], now + 3)
+    return src, persons, kb
+
+
+def tagged_register(be, is_engine):
+    regs = [(True, E_TYPE, "e", E_SCHEMA), (True, E_F, "f", F_SCHEMA), (False, T_PERSON, "person", PERSON),
+            (False, T_CITY, "city", CITY), (False, T_GHOST, "ghost", GHOST)]
+    for is_edge, ident, name, cols in regs:
+        if not is_engine:
+            be.register(is_edge, ident, name, cols)
+        elif is_edge:
+            be.register_edge(ident, name, cols)
+        else:
+            be.register_tag(ident, name, cols)
+
+
+def tagged_pair(scale, parts=7, seed=5):
+    """(src, persons, engine, oracle) over the same tagged KV records."""
+    from nebula_amd import Engine
+    from tests.support.oracle import Oracle
+    src, persons, kb = tagged_kv(scale, parts, seed)
+    eng = Engine(parts)
+    tagged_register(eng, True)
+    eng.load_builder(kb)
+    orc = Oracle(parts)
+    tagged_register(orc, False)
+    orc.load_builder(kb)
+    return src, persons, eng, orc
