@@ -17,6 +17,8 @@
  *   nbg_go_prepare / _execute  ≙ GoExecutor::prepare() / execute() (GoExecutor.cpp:28-110)
  *   nbg_find_path              ≙ FindPathExecutor result semantics
  *       (src/graph/FindPathExecutor.cpp:145-715)
+ *   nbg_get_neighbors          ≙ StorageServiceHandler::future_getBound → QueryBoundProcessor
+ *       (src/storage/StorageServiceHandler.cpp:33-40, src/storage/QueryBoundProcessor.cpp:16-220)
  */
 #ifndef NEBULA_AMD_NBG_H_
 #define NEBULA_AMD_NBG_H_
@@ -198,6 +200,63 @@ const int64_t* nbg_path_entries(const nbg_paths* p, int64_t i);
 /* Adjacency entries the search scanned (both directions; TEPS numerator). */
 uint64_t nbg_paths_edges_scanned(const nbg_paths* p);
 void nbg_paths_free(nbg_paths* p);
+
+/* ---- GetNeighbors (storage boundary: StorageServiceHandler::future_getBound) -------------
+ * Columnar mirror of GetNeighborsRequest / QueryResponse (src/interface/storage.thrift:47-106,
+ * 153-161) served by QueryBoundProcessor (src/storage/QueryBoundProcessor.cpp:16-220,
+ * QueryBaseProcessor.inl:60-562): per requested (part, vid), tag rows of the SOURCE columns and,
+ * per requested edge type that has return columns, the RowSet of its edges in key order
+ * (latest version, storage-side filter with keep-on-error, first max_edge_returned_per_vertex
+ * accepted edges).  Rows are the exact RowWriter / RowSetWriter bytes storaged would send
+ * (src/dataman/RowWriter.cpp:26-95, RowSetWriter.cpp:21-43), so a thrift adapter copies them
+ * into QueryResponse unchanged.  Request-level errors (unknown schema / prop, an invalid filter)
+ * are reported as one failed code per requested part, like QueryBaseProcessor.inl:529-535;
+ * parts this engine does not serve fail with NBG_E_PART_NOT_FOUND.  The edge walk and filter
+ * run on the device (one expansion over the requested vertices per edge type). */
+#define NBG_PROP_SOURCE 1
+#define NBG_PROP_DEST   2
+#define NBG_PROP_EDGE   3
+typedef struct {
+  int32_t owner;                  /* NBG_PROP_SOURCE / _DEST (tag prop) or _EDGE               */
+  int32_t id;                     /* tag id, or signed edge type                               */
+  const char* name;               /* prop name; _src / _dst / _type / _rank for edge keys      */
+} nbg_prop_def;
+
+typedef struct {
+  const int32_t* parts;           /* part of each vid: the map<PartitionID, list<VertexID>>   */
+  const int64_t* vids;            /*   flattened (one entry per requested vid)                 */
+  uint64_t num_vids;
+  const int32_t* edge_types;      /* signed: negative = in-edges                               */
+  int32_t num_edge_types;
+  const uint8_t* filter;          /* Expression::encode bytes; NULL/0 = none                   */
+  uint32_t filter_len;
+  const nbg_prop_def* return_columns;
+  int32_t num_return_columns;
+} nbg_gn_request;
+
+typedef struct nbg_gn_response nbg_gn_response;
+int32_t nbg_get_neighbors(nbg_engine* e, const nbg_gn_request* req, nbg_gn_response** out);
+/* result.failed_codes: (code, part) pairs; latency_in_us */
+int32_t nbg_gn_num_failed(const nbg_gn_response* r);
+int32_t nbg_gn_failed(const nbg_gn_response* r, int32_t i, int32_t* code, int32_t* part);
+int32_t nbg_gn_latency_us(const nbg_gn_response* r);
+/* vertex_schema (is_edge = 0) / edge_schema (is_edge = 1): entries, then columns of entry i */
+int32_t nbg_gn_num_schemas(const nbg_gn_response* r, int32_t is_edge);
+int32_t nbg_gn_schema(const nbg_gn_response* r, int32_t is_edge, int32_t i, int32_t* id, int32_t* ncols);
+int32_t nbg_gn_schema_col(const nbg_gn_response* r, int32_t is_edge, int32_t i, int32_t c, const char** name,
+                          int32_t* type);
+/* vertices[i]: vid, tag_data[k] = (tag, row bytes), edge_data[k] = (type, RowSet bytes) */
+int64_t nbg_gn_num_vertices(const nbg_gn_response* r);
+int64_t nbg_gn_vertex_id(const nbg_gn_response* r, int64_t i);
+int32_t nbg_gn_vertex_num_tags(const nbg_gn_response* r, int64_t i);
+int32_t nbg_gn_vertex_tag(const nbg_gn_response* r, int64_t i, int32_t k, int32_t* tag, const uint8_t** data,
+                          uint64_t* len);
+int32_t nbg_gn_vertex_num_edges(const nbg_gn_response* r, int64_t i);
+int32_t nbg_gn_vertex_edges(const nbg_gn_response* r, int64_t i, int32_t k, int32_t* type, const uint8_t** data,
+                            uint64_t* len);
+/* Adjacency entries the device walk returned (after the filter and cap). */
+uint64_t nbg_gn_edges(const nbg_gn_response* r);
+void nbg_gn_free(nbg_gn_response* r);
 
 /* ---- in-library kernel timing (HIP events on the engine's stream) ----------------------- */
 typedef struct {

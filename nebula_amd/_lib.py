@@ -60,6 +60,16 @@ class nbg_path_request(C.Structure):
                 ("over_all", i32), ("to", P(i64)), ("num_to", u64), ("upto", u32), ("shortest", i32)]
 
 
+class nbg_prop_def(C.Structure):
+    _fields_ = [("owner", i32), ("id", i32), ("name", C.c_char_p)]
+
+
+class nbg_gn_request(C.Structure):
+    _fields_ = [("parts", P(i32)), ("vids", P(i64)), ("num_vids", u64), ("edge_types", P(i32)),
+                ("num_edge_types", i32), ("filter", P(u8)), ("filter_len", u32),
+                ("return_columns", P(nbg_prop_def)), ("num_return_columns", i32)]
+
+
 # (name, restype, argtypes) for every symbol include/nbg.h declares
 SIGNATURES = [
     ("nbg_create", i32, [P(nbg_config), P(vp)]),
@@ -94,6 +104,21 @@ SIGNATURES = [
     ("nbg_path_entries", P(i64), [vp, i64]),
     ("nbg_paths_edges_scanned", u64, [vp]),
     ("nbg_paths_free", None, [vp]),
+    ("nbg_get_neighbors", i32, [vp, P(nbg_gn_request), P(vp)]),
+    ("nbg_gn_num_failed", i32, [vp]),
+    ("nbg_gn_failed", i32, [vp, i32, P(i32), P(i32)]),
+    ("nbg_gn_latency_us", i32, [vp]),
+    ("nbg_gn_num_schemas", i32, [vp, i32]),
+    ("nbg_gn_schema", i32, [vp, i32, i32, P(i32), P(i32)]),
+    ("nbg_gn_schema_col", i32, [vp, i32, i32, i32, P(C.c_char_p), P(i32)]),
+    ("nbg_gn_num_vertices", i64, [vp]),
+    ("nbg_gn_vertex_id", i64, [vp, i64]),
+    ("nbg_gn_vertex_num_tags", i32, [vp, i64]),
+    ("nbg_gn_vertex_tag", i32, [vp, i64, i32, P(i32), P(P(u8)), P(u64)]),
+    ("nbg_gn_vertex_num_edges", i32, [vp, i64]),
+    ("nbg_gn_vertex_edges", i32, [vp, i64, i32, P(i32), P(P(u8)), P(u64)]),
+    ("nbg_gn_edges", u64, [vp]),
+    ("nbg_gn_free", None, [vp]),
     ("nbg_profile", i32, [vp, i32]),
     ("nbg_profile_read", i32, [vp, vp, i32]),
     ("nbg_comm_unique_id", i32, [P(u8)]),

@@ -353,11 +353,15 @@ struct Ctx {
     // GoExecutor::processFinalResult getAliasProp (GoExecutor.cpp:851-878)
     int32_t et;
     const SchemaSet* ss = edge_by_name(e.alias, &et);
-    if (!ss || std::find(env.over->begin(), env.over->end(), et) == env.over->end()) {
+    if (!ss || (!env.storage && std::find(env.over->begin(), env.over->end(), et) == env.over->end())) {
       *err = "the edge was not found '" + e.alias + "'";
       return NBG_E_EXECUTION_ERROR;   // deferred to the final step (getStepOutProps)
     }
     bool key = e.prop == "_dst" || e.prop == "_src" || e.prop == "_rank" || e.prop == "_type";
+    if (env.storage && (et != env.etype || key)) {   // "ignore this edge" / "Invalid Prop"
+      *out = make_error();
+      return NBG_OK;
+    }
     const Schema* sc = ss->latest();
     int col = (!key && sc) ? sc->find(e.prop) : -1;
     if (!key && col < 0) {
@@ -436,7 +440,7 @@ struct Ctx {
     Compiled c;
     c.kind = dt->kind[col];
     const int32_t aux = (dt->index << 16) | (dt->col_base + col);
-    const bool has_default = env.row_cols && env.row_cols->count(e.prop);
+    const bool has_default = !env.storage && env.row_cols && env.row_cols->count(e.prop);
     c.reg = push();
     if (!has_default) {
       emit(OP_TAGS_E, c.reg, 0, 0, aux, 0);   // no such column in the row schema: "Unknown type"
@@ -499,7 +503,7 @@ struct Ctx {
       case EK_TYPE: {
         int32_t et;
         const SchemaSet* ss = edge_by_name(e.alias, &et);
-        if (!ss || std::find(env.over->begin(), env.over->end(), et) == env.over->end()) {
+        if (!env.storage && (!ss || std::find(env.over->begin(), env.over->end(), et) == env.over->end())) {
           *err = "the edge was not found '" + e.alias + "'";
           return NBG_E_EXECUTION_ERROR;
         }

@@ -44,6 +44,9 @@ struct CompileEnv {
   bool partitioned = false;
   std::string* dst_unknown = nullptr;   // set when a $$ tag name is unknown (fails iff E_N > 0)
   uint32_t* probe_mask = nullptr;       // tags read through $$
+  // storage-side filter (QueryBaseProcessor.inl:580-606 getters): another edge's alias and the
+  // key props `_src/_dst/_rank` read from the value row fail, $^ without the tag fails
+  bool storage = false;
 };
 
 // Result of compiling one expression for one edge type.

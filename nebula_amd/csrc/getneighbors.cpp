@@ -1,0 +1,547 @@
+// GetNeighbors — the storage boundary (StorageServiceHandler::future_getBound,
+// src/storage/StorageServiceHandler.cpp:33-40) served from the device snapshot.
+//
+// QueryBoundProcessor (src/storage/QueryBoundProcessor.cpp:16-220) over QueryBaseProcessor
+// (src/storage/QueryBaseProcessor.inl:60-562):
+//   * checkAndBuildContexts (:60-169): tag contexts for SOURCE/DEST columns, one edge context per
+//     requested type (plus types named only by return columns), key props from the key, in-edge
+//     value props skipped; the filter is decoded and checked (checkExp, :172-290).  A request-level
+//     error is one failed code per requested part (:529-535).
+//   * processVertex (QueryBoundProcessor.cpp:64-111): the tag rows first, then one RowSet per edge
+//     context with props; a vertex is returned only if some RowSet is non-empty.
+//   * collectEdgeProps (:381-458): key order, latest version, the filter on out-edges with
+//     keep-on-error, at most max_edge_returned_per_vertex accepted edges.
+// The edge walk and the filter run on the device (k_expand<FINAL> with a keep-on-error WHERE and
+// the edge index / source vid / return columns as YIELDs); the host regroups the rows in key order
+// and writes the RowWriter / RowSetWriter bytes (RowWriter.cpp:26-95, RowSetWriter.cpp:21-43).
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <unordered_map>
+
+#include "engine.h"
+
+using namespace nbg;
+
+struct nbg_gn_response {
+  struct Sch {
+    int32_t id;
+    std::vector<std::pair<std::string, int32_t>> cols;
+  };
+  struct Vertex {
+    int64_t vid;
+    std::vector<std::pair<int32_t, std::string>> tags, edges;
+  };
+  std::vector<std::pair<int32_t, int32_t>> failed;   // (code, part)
+  int32_t latency_us = 0;
+  std::vector<Sch> vschema, eschema;
+  std::vector<Vertex> vertices;
+  uint64_t edges = 0;
+};
+
+namespace {
+
+// ------------------------------------------------------------------ RowWriter (schema-less mode)
+// QueryBaseProcessor writes rows with RowWriter(nullptr): a SchemaWriter records the columns, the
+// header carries no schema version (RowWriter.cpp:49-75); a block offset every 16 columns.
+struct RowBytes {
+  std::string cord;
+  std::vector<uint64_t> blocks;
+  int64_t cols = 0;
+  void varint(uint64_t v) {
+    while (v >= 0x80) {
+      cord.push_back((char)(v | 0x80));
+      v >>= 7;
+    }
+    cord.push_back((char)v);
+  }
+  void done() {
+    ++cols;
+    if ((cols & 15) == 0) blocks.push_back(cord.size());
+  }
+  void put_int(int64_t v) { varint((uint64_t)v); done(); }
+  void put_vid(int64_t v) { cord.append(reinterpret_cast<const char*>(&v), 8); done(); }
+  void put_double(int64_t bits) { cord.append(reinterpret_cast<const char*>(&bits), 8); done(); }
+  void put_bool(int64_t v) { cord.push_back(v ? 1 : 0); done(); }
+  void put_string(const std::string& s) { varint(s.size()); cord += s; done(); }
+  std::string encode() const {
+    int off = 0;
+    uint64_t n = cord.size();
+    do { ++off; n >>= 8; } while (n);
+    std::string out(1, (char)(off - 1));
+    for (uint64_t b : blocks) out.append(reinterpret_cast<const char*>(&b), off);
+    return out + cord;
+  }
+};
+
+void rowset_add(std::string& rs, const std::string& row) {   // RowSetWriter::addRow
+  uint64_t v = row.size();
+  while (v >= 0x80) {
+    rs.push_back((char)(v | 0x80));
+    v >>= 7;
+  }
+  rs.push_back((char)v);
+  rs += row;
+}
+
+struct PropCtx {
+  std::string name;
+  int32_t type = 0;     // NBG_T_* of the response schema column
+  int pik = 0;          // key prop: 1 _src, 2 _dst, 3 _type, 4 _rank
+  int col = -1;         // value column (edge or tag schema)
+};
+struct TagCtx {
+  int32_t tag;
+  std::vector<PropCtx> props;   // returned props
+};
+struct EdgeCtx {
+  int32_t type;
+  std::vector<PropCtx> props;
+};
+
+int32_t key_type(const std::string& n) {
+  return (n == "_src" || n == "_dst") ? NBG_T_VID : NBG_T_INT;
+}
+int key_pik(const std::string& n) {
+  return n == "_src" ? 1 : n == "_dst" ? 2 : n == "_type" ? 3 : n == "_rank" ? 4 : 0;
+}
+
+// QueryBaseProcessor::checkExp (QueryBaseProcessor.inl:172-290): true if the storage can run it
+bool check_exp(const Engine& E, const Node& e, bool have_edges) {
+  switch (e.kind) {
+    case EK_PRIMARY: return true;
+    case EK_FUNC: return false;
+    case EK_UNARY: case EK_CAST: return check_exp(E, *e.kids[0], have_edges);
+    case EK_ARITH: case EK_REL: case EK_LOGIC:
+      return check_exp(E, *e.kids[0], have_edges) && check_exp(E, *e.kids[1], have_edges);
+    case EK_SRCPROP: {
+      for (auto& kv : E.tags)
+        if (kv.second.name == e.alias) {
+          const Schema* s = kv.second.latest();
+          return s && s->find(e.prop) >= 0;
+        }
+      return false;
+    }
+    case EK_RANK: case EK_DST: case EK_SRCID: case EK_TYPE: return true;
+    case EK_ALIAS: {
+      if (!have_edges) return false;
+      for (auto& kv : E.edges)
+        if (kv.second.name == e.alias) {
+          const Schema* s = kv.second.latest();
+          return s && s->find(e.prop) >= 0;
+        }
+      return false;
+    }
+    default: return false;
+  }
+}
+
+bool part_served(const Engine& E, int32_t part) {
+  if (part < 1 || part > E.cfg.num_parts) return false;
+  return E.cfg.num_gpus <= 1 || part % E.cfg.num_gpus == E.cfg.rank;
+}
+
+}  // namespace
+
+static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_response* resp) {
+  // --- checkAndBuildContexts
+  std::vector<TagCtx> tctx;
+  std::vector<EdgeCtx> ectx;
+  auto edge_ctx = [&](int32_t t) -> EdgeCtx* {
+    for (auto& c : ectx)
+      if (c.type == t) return &c;
+    return nullptr;
+  };
+  for (int32_t i = 0; i < rq->num_edge_types; ++i)
+    if (!edge_ctx(rq->edge_types[i])) ectx.push_back(EdgeCtx{rq->edge_types[i], {}});
+  int32_t code = NBG_OK;
+  for (int32_t i = 0; i < rq->num_return_columns && !code; ++i) {
+    const nbg_prop_def& pd = rq->return_columns[i];
+    const std::string name = pd.name ? pd.name : "";
+    PropCtx pc;
+    pc.name = name;
+    if (pd.owner == NBG_PROP_SOURCE || pd.owner == NBG_PROP_DEST) {
+      auto it = E.tags.find(pd.id);
+      const Schema* s = it == E.tags.end() ? nullptr : it->second.latest();
+      if (!s) { code = NBG_E_TAG_PROP_NOT_FOUND; break; }
+      pc.col = s->find(name);
+      if (pc.col < 0) { code = NBG_E_IMPROPER_DATA_TYPE; break; }
+      pc.type = s->cols[pc.col].type;
+      TagCtx* tc = nullptr;
+      for (auto& c : tctx)
+        if (c.tag == pd.id) tc = &c;
+      if (!tc) { tctx.push_back(TagCtx{pd.id, {}}); tc = &tctx.back(); }
+      tc->props.push_back(pc);
+    } else {
+      if ((pc.pik = key_pik(name))) {
+        pc.type = key_type(name);
+      } else if (pd.id > 0) {
+        auto it = E.edges.find(pd.id);
+        const Schema* s = it == E.edges.end() ? nullptr : it->second.latest();
+        if (!s) { code = NBG_E_EDGE_PROP_NOT_FOUND; break; }
+        pc.col = s->find(name);
+        if (pc.col < 0) { code = NBG_E_IMPROPER_DATA_TYPE; break; }
+        pc.type = s->cols[pc.col].type;
+      } else {
+        continue;   // "InBound has none props, skip it!"
+      }
+      EdgeCtx* ec = edge_ctx(pd.id);
+      if (!ec) { ectx.push_back(EdgeCtx{pd.id, {}}); ec = &ectx.back(); }
+      ec->props.push_back(pc);
+    }
+  }
+  std::unique_ptr<Node> filter;
+  if (!code && rq->filter && rq->filter_len) {
+    std::string err;
+    filter = decode_expr(rq->filter, rq->filter_len, &err);
+    if (!filter || !check_exp(E, *filter, !ectx.empty())) code = NBG_E_INVALID_FILTER;
+  }
+  // requested parts, ascending (the processor's part order)
+  std::vector<int32_t> parts(rq->parts, rq->parts + rq->num_vids);
+  std::sort(parts.begin(), parts.end());
+  parts.erase(std::unique(parts.begin(), parts.end()), parts.end());
+  if (code) {
+    for (int32_t p : parts) resp->failed.emplace_back(code, p);
+    return NBG_OK;
+  }
+  // --- vertices: dense ids of the requested (part, vid) with rows in that part
+  std::vector<uint8_t> part_bad(parts.size(), 0);
+  for (size_t k = 0; k < parts.size(); ++k)
+    if (!part_served(E, parts[k])) {
+      part_bad[k] = 1;
+      resp->failed.emplace_back(NBG_E_PART_NOT_FOUND, parts[k]);
+    }
+  auto part_ok = [&](int32_t p) { return !part_bad[std::lower_bound(parts.begin(), parts.end(), p) - parts.begin()]; };
+  std::vector<uint32_t> dense(rq->num_vids, NO_ROW);
+  std::vector<uint32_t> starts;
+  for (uint64_t i = 0; i < rq->num_vids; ++i) {
+    if (!part_ok(rq->parts[i])) continue;
+    const uint32_t d = E.dense(rq->vids[i]);
+    if (d == NO_ROW || E.snap.h_part[d] != rq->parts[i]) continue;   // prefix scan of another part
+    dense[i] = d;
+    starts.push_back(d);
+  }
+  std::sort(starts.begin(), starts.end());
+  starts.erase(std::unique(starts.begin(), starts.end()), starts.end());
+
+  // --- device walk: one final-step expansion per edge context with props
+  struct TypeRows {
+    std::vector<int64_t> vid, eidx;
+    std::vector<std::vector<int64_t>> vals;   // [prop][row]
+    std::unordered_map<int64_t, std::pair<uint64_t, uint64_t>> range;   // vid -> [lo, hi) in key order
+  };
+  std::vector<TypeRows> trows(ectx.size());
+  std::vector<size_t> active;   // ectx indices walked on the device
+  std::vector<std::vector<int>> yield_of(ectx.size());   // returned prop -> YIELD column
+  for (size_t k = 0; k < ectx.size(); ++k)
+    if (!ectx[k].props.empty() && E.snap.types.count(ectx[k].type)) active.push_back(k);
+  if (!starts.empty() && !active.empty()) {
+    if (active.size() > (size_t)MAX_TYPES_Q) return E.fail(NBG_E_UNSUPPORTED, "too many edge types");
+    std::vector<TypeProgram> plist;
+    std::vector<uint64_t> region, blk_cap, ebound;
+    uint64_t cap_rows = 0;
+    int ncols = 0;
+    std::string err;
+    for (size_t k : active) {
+      const EdgeCtx& ec = ectx[k];
+      const DevEdgeType& dt = E.snap.types.at(ec.type);
+      TypeProgram tp;
+      tp.etype = ec.type;
+      tp.keep_on_error = true;
+      ProgramBuilder pb;
+      if (filter && ec.type > 0) {   // in-edges carry no value: the filter is not evaluated (inl:410)
+        std::vector<int32_t> over{ec.type};
+        CompileEnv env{ec.type, &over, &E.edges, &E.snap.strings, dt.valid != nullptr, dt.rank != nullptr};
+        env.tags = &E.tags;
+        env.dtags = &E.snap.tags;
+        env.partitioned = E.partitioned();
+        env.storage = true;
+        Compiled c;
+        int32_t rc = compile_expr(*filter, env, pb, &c, &err);
+        if (rc) return E.fail(rc == NBG_E_UNSUPPORTED ? rc : NBG_E_INVALID_FILTER, "filter: " + err);
+        if (c.is_const) {
+          bool tv;
+          switch (c.kind) {
+            case VK_STRING: tv = c.const_str.empty(); break;
+            case VK_DOUBLE: { double d; memcpy(&d, &c.const_bits, 8); tv = d != 0.0; break; }
+            default: tv = c.const_bits != 0;
+          }
+          pb.code.clear();
+          pb.code.push_back(Ins{OP_CONST, 0, 0, 0, 0, tv ? 1 : 0});
+          c.reg = 0;
+          c.kind = VK_BOOL;
+          pb.max_reg = std::max(pb.max_reg, 1);
+        }
+        const uint8_t r = (uint8_t)c.reg;
+        if (c.kind == VK_INT) pb.code.push_back(Ins{OP_TRUTHY_I, r, r, 0, 0, 0});
+        else if (c.kind == VK_DOUBLE) pb.code.push_back(Ins{OP_TRUTHY_F, r, r, 0, 0, 0});
+        else if (c.kind == VK_STRING) pb.code.push_back(Ins{OP_TRUTHY_S, r, r, 0, 0, string_code(E.snap.strings, "")});
+        tp.where_len = (int)pb.code.size();
+        tp.where_reg = c.reg;
+      }
+      // YIELDs: source vid, edge index, then one payload per returned prop
+      auto yield_op = [&](uint8_t op, int32_t aux = 0) {
+        const int reg = (int)tp.yield_reg.size() % MAX_REGS;
+        pb.code.push_back(Ins{op, (uint8_t)reg, 0, 0, aux, 0});
+        tp.yield_reg.push_back(reg);
+        tp.yield_kind.push_back(VK_INT);
+        tp.yield_const.push_back(0);
+        tp.yield_const_str.emplace_back();
+        pb.max_reg = std::max(pb.max_reg, reg + 1);
+      };
+      yield_op(OP_SRC);
+      yield_op(OP_EIDX);
+      // one YIELD per distinct source of the returned props (a prop may be asked for repeatedly)
+      std::vector<std::pair<int, int>> srcs;   // (pik, col)
+      std::vector<int>& map = yield_of[k];
+      for (auto& pc : ec.props) {
+        const std::pair<int, int> key{pc.pik, pc.pik ? -1 : pc.col};
+        auto f = std::find(srcs.begin(), srcs.end(), key);
+        map.push_back(2 + (int)(f - srcs.begin()));
+        if (f != srcs.end()) continue;
+        srcs.push_back(key);
+        if (pc.pik == 1) yield_op(OP_SRC);
+        else if (pc.pik == 2) yield_op(OP_DST);
+        else if (pc.pik == 4) yield_op(OP_RANK);
+        else if (pc.pik == 3) {   // constant: the key's type
+          tp.yield_reg.push_back(-1);
+          tp.yield_kind.push_back(VK_INT);
+          tp.yield_const.push_back(ec.type);
+          tp.yield_const_str.emplace_back();
+        } else {
+          yield_op(OP_COL, pc.col);
+        }
+      }
+      if ((int)tp.yield_reg.size() > MAX_YIELDS) return E.fail(NBG_E_UNSUPPORTED, "too many return columns");
+      tp.code = pb.code;
+      tp.nregs = std::max(1, pb.max_reg);
+      if ((int)tp.code.size() > MAX_PROGRAM) return E.fail(NBG_E_UNSUPPORTED, "program too long");
+      ncols = std::max(ncols, (int)tp.yield_reg.size());
+      uint64_t eb = 0;
+      for (uint32_t d : starts) eb += dt.h_row_ptr[d + 1] - dt.h_row_ptr[d];
+      ebound.push_back(eb);
+      blk_cap.push_back(ws_final_blk_cap(starts.size(), eb));
+      region.push_back(cap_rows);
+      cap_rows += blk_cap.back() * ws_final_grid(starts.size(), eb);
+      plist.push_back(std::move(tp));
+    }
+    if (starts.size() > ws_cap_frontier(E.ws)) return E.fail(NBG_E_UNSUPPORTED, "too many vertices in one request");
+    static std::atomic<uint64_t> gn_id{1ull << 62};   // program cache keys disjoint from GO statements
+    Workspace* ws = E.ws;
+    hipError_t he = ws_reserve_rows(ws, cap_rows, ncols);
+    if (he == hipSuccess) he = ws_begin_query(ws, starts.data(), starts.size(), &plist, gn_id++);
+    for (size_t i = 0; he == hipSuccess && i < active.size(); ++i) {
+      const DevEdgeType& dt = E.snap.types.at(ectx[active[i]].type);
+      ExpandArgs a{};
+      a.row_ptr = dt.row_ptr;
+      a.col = dt.col;
+      a.dst_vid = dt.dst_vid;
+      a.rank = dt.rank;
+      a.valid = dt.valid;
+      a.visible = nullptr;   // the part check above replaces the visibility test
+      a.vids = E.snap.d_vids;
+      a.props = dt.d_props;
+      a.hprops = dt.props.data();
+      a.hnarrow = nullptr;
+      a.hnarrow_bytes = nullptr;
+      a.cap = 0x7fffffff;    // the cap counts ACCEPTED edges: applied on the host below
+      a.tcols = E.snap.d_tcols;
+      a.tpres = E.snap.d_tpres;
+      a.gbase = E.partitioned() ? (uint32_t)((uint64_t)E.cfg.rank * E.npad) : 0u;
+      he = ws_expand_final(ws, a, starts.size(), ebound[i], 1, (int)i, plist[i], region[i], blk_cap[i], nullptr);
+    }
+    if (he == hipSuccess) he = ws_end_query(ws);
+    if (he != hipSuccess) return E.fail(NBG_E_DEVICE, std::string("HIP: ") + hipGetErrorString(he));
+    for (size_t i = 0; i < active.size(); ++i) {
+      const int nc = (int)plist[i].yield_reg.size();
+      const unsigned grid = ws_final_grid_of(ws, (int)i);
+      const uint32_t* per = ws_host_blk_rows(ws, (int)i);
+      std::vector<std::pair<uint64_t, uint64_t>> segs;
+      uint64_t total = 0;
+      for (unsigned b = 0; b < grid; ++b)
+        if (per[b]) {
+          segs.emplace_back(region[i] + (uint64_t)b * blk_cap[i], per[b]);
+          total += per[b];
+        }
+      std::vector<std::vector<int64_t>> cols(nc, std::vector<int64_t>(total));
+      std::vector<int64_t*> hc;
+      for (auto& c : cols) hc.push_back(c.data());
+      if (total && ws_fetch_rows(ws, segs, nc, total, hc.data()) != hipSuccess)
+        return E.fail(NBG_E_DEVICE, "row fetch failed");
+      // key order: CSR index order (rows of one source are contiguous and sorted)
+      std::vector<uint64_t> ord(total);
+      for (uint64_t r = 0; r < total; ++r) ord[r] = r;
+      std::sort(ord.begin(), ord.end(), [&](uint64_t x, uint64_t y) { return cols[1][x] < cols[1][y]; });
+      TypeRows& tr = trows[active[i]];
+      tr.vid.resize(total);
+      tr.eidx.resize(total);
+      const std::vector<int>& ymap = yield_of[active[i]];
+      tr.vals.assign(ymap.size(), std::vector<int64_t>(total));
+      for (uint64_t r = 0; r < total; ++r) {
+        tr.vid[r] = cols[0][ord[r]];
+        tr.eidx[r] = cols[1][ord[r]];
+        for (size_t p = 0; p < ymap.size(); ++p) tr.vals[p][r] = cols[ymap[p]][ord[r]];
+      }
+      for (uint64_t r = 0; r < total;) {
+        uint64_t e = r;
+        while (e < total && tr.vid[e] == tr.vid[r]) ++e;
+        tr.range[tr.vid[r]] = {r, e};
+        r = e;
+      }
+    }
+  }
+
+  // --- responses per requested vertex, in part order (QueryBaseProcessor::genBuckets order)
+  const uint64_t cap = (uint64_t)(E.cfg.max_edge_returned_per_vertex <= 0 ? 0x7fffffff : E.cfg.max_edge_returned_per_vertex);
+  const auto& dict = E.snap.strings;
+  auto str_of = [&](int64_t code) -> std::string {
+    return (code >= 0 && (code & 1) == 0 && (uint64_t)(code / 2) < dict.size()) ? dict[code / 2] : std::string();
+  };
+  auto put_value = [&](RowBytes& w, int32_t type, int64_t bits) {
+    switch (kindOfType(type)) {   // RowReader::getPropByName -> VariantType -> PropsCollector
+      case VK_INT: w.put_int(bits); break;
+      case VK_DOUBLE: w.put_double(bits); break;
+      case VK_BOOL: w.put_bool(bits); break;
+      case VK_STRING: w.put_string(str_of(bits)); break;
+    }
+  };
+  std::vector<uint64_t> order(rq->num_vids);
+  for (uint64_t i = 0; i < rq->num_vids; ++i) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return rq->parts[a] < rq->parts[b]; });
+  for (uint64_t i : order) {
+    if (!part_ok(rq->parts[i])) continue;
+    nbg_gn_response::Vertex v;
+    v.vid = rq->vids[i];
+    const uint32_t d = dense[i];
+    if (d == NO_ROW) continue;   // no keys in this part: no edges, not returned
+    for (auto& tc : tctx) {      // collectVertexProps: the tag's live record, returned props
+      const DevTag& dtg = E.snap.tags.at(tc.tag);
+      if (!dtg.h_present[d]) continue;
+      RowBytes w;
+      if (dtg.h_present[d] == 1)
+        for (auto& pc : tc.props) put_value(w, pc.type, dtg.h_cols[pc.col][d]);
+      if (w.cols > 0) v.tags.emplace_back(tc.tag, w.encode());
+    }
+    for (size_t k = 0; k < ectx.size(); ++k) {
+      const EdgeCtx& ec = ectx[k];
+      if (ec.props.empty()) continue;
+      const TypeRows& tr = trows[k];
+      auto it = tr.range.find(v.vid);
+      if (it == tr.range.end()) continue;
+      std::string rs;
+      const uint64_t lo = it->second.first, hi = std::min(it->second.second, it->second.first + cap);
+      for (uint64_t r = lo; r < hi; ++r) {
+        RowBytes w;
+        for (size_t p = 0; p < ec.props.size(); ++p) {
+          const PropCtx& pc = ec.props[p];
+          const int64_t x = tr.vals[p][r];
+          switch (pc.pik) {
+            case 1: case 2: w.put_vid(x); break;
+            case 3: case 4: w.put_int(x); break;
+            default: put_value(w, pc.type, x);
+          }
+        }
+        rowset_add(rs, w.encode());
+        ++resp->edges;
+      }
+      if (!rs.empty()) v.edges.emplace_back(ec.type, std::move(rs));
+    }
+    if (v.edges.empty()) continue;   // only vertices with edges (QueryBoundProcessor.cpp:104-107)
+    resp->vertices.push_back(std::move(v));
+  }
+  // --- onProcessFinished: schemas of the returned columns
+  for (auto& tc : tctx) {
+    nbg_gn_response::Sch s{tc.tag, {}};
+    for (auto& pc : tc.props) s.cols.emplace_back(pc.name, pc.type);
+    if (!s.cols.empty()) resp->vschema.push_back(std::move(s));
+  }
+  for (auto& ec : ectx) {
+    nbg_gn_response::Sch s{ec.type, {}};
+    for (auto& pc : ec.props) s.cols.emplace_back(pc.name, pc.type);
+    if (!s.cols.empty()) resp->eschema.push_back(std::move(s));
+  }
+  return NBG_OK;
+}
+
+extern "C" {
+
+int32_t nbg_get_neighbors(nbg_engine* h, const nbg_gn_request* rq, nbg_gn_response** out) {
+  if (!h || !rq || !out || (rq->num_vids && (!rq->vids || !rq->parts)) ||
+      (rq->num_edge_types && !rq->edge_types) || (rq->num_return_columns && !rq->return_columns))
+    return NBG_E_INVALID_ARGUMENT;
+  *out = nullptr;
+  Engine& E = h->e;
+  std::lock_guard<std::mutex> lg(E.mu);
+  if (!E.finalized) return E.fail(NBG_E_STATE, "engine not finalized");
+  if (hipSetDevice(E.cfg.device) != hipSuccess) return E.fail(NBG_E_DEVICE, "hipSetDevice failed");
+  const auto t0 = std::chrono::steady_clock::now();
+  auto* r = new nbg_gn_response();
+  int32_t rc = get_neighbors(E, rq, r);
+  if (rc) { delete r; return rc; }
+  r->latency_us = (int32_t)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0)
+                      .count();
+  *out = r;
+  return NBG_OK;
+}
+
+int32_t nbg_gn_num_failed(const nbg_gn_response* r) { return r ? (int32_t)r->failed.size() : -1; }
+int32_t nbg_gn_failed(const nbg_gn_response* r, int32_t i, int32_t* code, int32_t* part) {
+  if (!r || i < 0 || i >= (int32_t)r->failed.size() || !code || !part) return NBG_E_INVALID_ARGUMENT;
+  *code = r->failed[i].first;
+  *part = r->failed[i].second;
+  return NBG_OK;
+}
+int32_t nbg_gn_latency_us(const nbg_gn_response* r) { return r ? r->latency_us : -1; }
+int32_t nbg_gn_num_schemas(const nbg_gn_response* r, int32_t is_edge) {
+  return r ? (int32_t)(is_edge ? r->eschema : r->vschema).size() : -1;
+}
+int32_t nbg_gn_schema(const nbg_gn_response* r, int32_t is_edge, int32_t i, int32_t* id, int32_t* ncols) {
+  if (!r || !id || !ncols) return NBG_E_INVALID_ARGUMENT;
+  const auto& v = is_edge ? r->eschema : r->vschema;
+  if (i < 0 || i >= (int32_t)v.size()) return NBG_E_INVALID_ARGUMENT;
+  *id = v[i].id;
+  *ncols = (int32_t)v[i].cols.size();
+  return NBG_OK;
+}
+int32_t nbg_gn_schema_col(const nbg_gn_response* r, int32_t is_edge, int32_t i, int32_t c, const char** name,
+                          int32_t* type) {
+  if (!r || !name || !type) return NBG_E_INVALID_ARGUMENT;
+  const auto& v = is_edge ? r->eschema : r->vschema;
+  if (i < 0 || i >= (int32_t)v.size() || c < 0 || c >= (int32_t)v[i].cols.size()) return NBG_E_INVALID_ARGUMENT;
+  *name = v[i].cols[c].first.c_str();
+  *type = v[i].cols[c].second;
+  return NBG_OK;
+}
+int64_t nbg_gn_num_vertices(const nbg_gn_response* r) { return r ? (int64_t)r->vertices.size() : -1; }
+int64_t nbg_gn_vertex_id(const nbg_gn_response* r, int64_t i) {
+  return (r && i >= 0 && i < (int64_t)r->vertices.size()) ? r->vertices[i].vid : 0;
+}
+int32_t nbg_gn_vertex_num_tags(const nbg_gn_response* r, int64_t i) {
+  return (r && i >= 0 && i < (int64_t)r->vertices.size()) ? (int32_t)r->vertices[i].tags.size() : -1;
+}
+int32_t nbg_gn_vertex_num_edges(const nbg_gn_response* r, int64_t i) {
+  return (r && i >= 0 && i < (int64_t)r->vertices.size()) ? (int32_t)r->vertices[i].edges.size() : -1;
+}
+static int32_t gn_item(const nbg_gn_response* r, int64_t i, int32_t k, bool edges, int32_t* id, const uint8_t** data,
+                       uint64_t* len) {
+  if (!r || i < 0 || i >= (int64_t)r->vertices.size() || !id || !data || !len) return NBG_E_INVALID_ARGUMENT;
+  const auto& v = edges ? r->vertices[i].edges : r->vertices[i].tags;
+  if (k < 0 || k >= (int32_t)v.size()) return NBG_E_INVALID_ARGUMENT;
+  *id = v[k].first;
+  *data = reinterpret_cast<const uint8_t*>(v[k].second.data());
+  *len = v[k].second.size();
+  return NBG_OK;
+}
+int32_t nbg_gn_vertex_tag(const nbg_gn_response* r, int64_t i, int32_t k, int32_t* tag, const uint8_t** data,
+                          uint64_t* len) {
+  return gn_item(r, i, k, false, tag, data, len);
+}
+int32_t nbg_gn_vertex_edges(const nbg_gn_response* r, int64_t i, int32_t k, int32_t* type, const uint8_t** data,
+                            uint64_t* len) {
+  return gn_item(r, i, k, true, type, data, len);
+}
+uint64_t nbg_gn_edges(const nbg_gn_response* r) { return r ? r->edges : 0; }
+void nbg_gn_free(nbg_gn_response* r) { delete r; }
+
+}  // extern "C"

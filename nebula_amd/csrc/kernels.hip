@@ -393,6 +393,7 @@ __device__ __forceinline__ void run_program(const Ins* __restrict__ prog, int pc
           }
         }
         break;
+      case OP_EIDX: r = (int64_t)c.j; break;
       case OP_ADD_I: r = (int64_t)((uint64_t)x + (uint64_t)y); break;
       case OP_SUB_I: r = (int64_t)((uint64_t)x - (uint64_t)y); break;
       case OP_MUL_I: r = (int64_t)((uint64_t)x * (uint64_t)y); break;
@@ -484,6 +485,7 @@ struct FinalParams {
   uint32_t* blk_rows;     // [gridDim.x] rows written per workgroup
   unsigned long long* err_flag;
   uint32_t probe_mask;             // tags read through $$ (presence probed for every final edge)
+  int keep_on_error;               // storage-side filter: an evaluation error keeps the edge
   unsigned long long* tag_bits;    // QState::tagbits
   FastProg fast;
 };
@@ -856,8 +858,12 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
             bool werr = false;
             EdgeCtx c{jj[i], active ? list_id(a0 + vv[i]) : 0u};
             run_program(fp.prog, 0, fp.where_len, c, a, regs, active, werr, tbits);
-            pass = active && !werr && regs[fp.where_reg * BLOCK + threadIdx.x] != 0;
-            if (active && werr) anyErr = true;
+            if (fp.keep_on_error) {
+              pass = active && (werr || regs[fp.where_reg * BLOCK + threadIdx.x] != 0);
+            } else {
+              pass = active && !werr && regs[fp.where_reg * BLOCK + threadIdx.x] != 0;
+              if (active && werr) anyErr = true;
+            }
           }
           pmask |= (uint32_t)pass << i;
         }
@@ -1583,6 +1589,7 @@ hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound,
   fp.blk_rows = w->blk_rows + (size_t)tix * EXPAND_GRID;
   fp.err_flag = &w->q->err;
   fp.probe_mask = prog.probe_mask;
+  fp.keep_on_error = prog.keep_on_error ? 1 : 0;
   fp.tag_bits = &w->q->tagbits;
   fp.fast = detect_fast(prog, a);
   size_t lds = fp.fast.enabled ? 0 : (size_t)(prog.nregs > 0 ? prog.nregs : 1) * BLOCK * sizeof(int64_t);

@@ -307,10 +307,11 @@ int32_t Engine::build_tags(const std::vector<int64_t>& dict, const std::vector<i
     for (size_t c = 0; c < nc; ++c) dt.kind.push_back(kindOfType(latest->cols[c].type));
     std::vector<uint8_t> pres(local, 0);
     std::vector<std::vector<int64_t>> cols(nc, std::vector<int64_t>(local, 0));
+    dt.h_present.assign(nv, 0);
     auto it = tstage.find(tag);
     if (it != tstage.end()) {
       const TagStage& ts = it->second;
-      std::vector<int64_t> best(local, -1);   // record index of the live version per vertex
+      std::vector<int64_t> best(nv, -1);   // record index of the live version per vertex
       for (size_t i = 0; i < ts.vid.size(); ++i) {
         auto p = std::lower_bound(dict.begin(), dict.end(), ts.vid[i]);
         const uint64_t d = (uint64_t)(p - dict.begin());
@@ -322,6 +323,7 @@ int32_t Engine::build_tags(const std::vector<int64_t>& dict, const std::vector<i
         const int64_t b = best[d];
         if (b < 0) continue;
         pres[d] = 1;
+        dt.h_present[d] = ts.valid[b] ? 1 : 2;   // 2: record present, value undecodable
         for (size_t c = 0; c < nc && c < ts.props.size(); ++c) {
           int64_t x = ts.props[c][b];
           if (dt.kind[c] == VK_STRING && ts.valid[b]) x = remap[x];
@@ -329,6 +331,8 @@ int32_t Engine::build_tags(const std::vector<int64_t>& dict, const std::vector<i
         }
       }
     }
+    dt.h_cols.resize(nc);
+    for (size_t c = 0; c < nc; ++c) dt.h_cols[c].assign(cols[c].begin(), cols[c].begin() + (ptrdiff_t)nv);
     bool ok = up((void**)&dt.present, pres.data(), space);
     dt.cols.assign(nc, nullptr);
     for (size_t c = 0; ok && c < nc; ++c) ok = up((void**)&dt.cols[c], cols[c].data(), space * 8);

@@ -102,6 +102,9 @@ struct DevTag {
   uint8_t* present = nullptr;   // [tag_space] the vertex has a record of this tag
   std::vector<int64_t*> cols;   // [ncols][tag_space] latest-schema columns
   std::vector<VKind> kind;
+  // host copies over this engine's local dense ids (GetNeighbors tag rows are built on the host)
+  std::vector<uint8_t> h_present;   // 0 none, 1 decoded, 2 record present but undecodable
+  std::vector<std::vector<int64_t>> h_cols;
 };
 
 struct Snapshot {
@@ -139,6 +142,7 @@ enum Op : uint8_t {
   OP_TAGS,       // r[d] = $^ prop of the source vertex; imm when the vertex lacks the tag
   OP_TAGS_E,     // same, but a vertex without the tag is an evaluation error
   OP_TAGD,       // r[d] = $$ prop of the destination; imm (+ the tag's "default used" bit) when absent
+  OP_EIDX,       // r[d] = the edge's CSR index (GetNeighbors: rows regrouped in key order on the host)
   // int64
   OP_ADD_I, OP_SUB_I, OP_MUL_I, OP_DIV_I, OP_MOD_I, OP_XOR_I, OP_NEG_I,
   OP_LT_I, OP_LE_I, OP_GT_I, OP_GE_I, OP_EQ_I, OP_NE_I,
@@ -179,6 +183,7 @@ struct TypeProgram {
   std::vector<std::string> yield_const_str;   // string constants (may be absent from the dictionary)
   bool needs_error_check = false;  // any op can raise an error
   uint32_t probe_mask = 0;         // tags read through $$: presence probed for every final edge
+  bool keep_on_error = false;      // storage filter: an evaluation error keeps the edge (inl:444-448)
   int nregs = 0;
 };
 

@@ -285,6 +285,67 @@ class Engine:
             self.lib.nbg_paths_free(out)
 
 
+    # ------------------------------------------------------------------ GetNeighbors (storage)
+    def get_neighbors(self, part_vids, edge_types, filter=b"", returns=()):
+        """StorageServiceHandler::future_getBound: ``part_vids`` = [(part, vid), ...], ``returns`` =
+        [(owner, id, name), ...] (owner 1 SOURCE, 2 DEST, 3 EDGE).  Returns a canonical dict of the
+        QueryResponse (see :func:`gn_canonical`)."""
+        parts = np.ascontiguousarray([p for p, _ in part_vids], np.int32)
+        vids = np.ascontiguousarray([v for _, v in part_vids], np.int64)
+        et = np.ascontiguousarray(edge_types, np.int32)
+        rets = (L.nbg_prop_def * max(1, len(returns)))(
+            *[L.nbg_prop_def(o, i, n.encode()) for o, i, n in returns])
+        fb = (C.c_uint8 * max(1, len(filter))).from_buffer_copy(filter or b"\0")
+        req = L.nbg_gn_request(
+            parts.ctypes.data_as(C.POINTER(C.c_int32)) if len(parts) else None,
+            vids.ctypes.data_as(C.POINTER(C.c_int64)) if len(vids) else None, len(vids),
+            et.ctypes.data_as(C.POINTER(C.c_int32)) if len(et) else None, len(et),
+            C.cast(fb, C.POINTER(C.c_uint8)) if filter else None, len(filter), rets, len(returns))
+        out = C.c_void_p()
+        self._check(self.lib.nbg_get_neighbors(self.h, C.byref(req), C.byref(out)), "get_neighbors")
+        lib = self.lib
+        try:
+            code, part = C.c_int32(), C.c_int32()
+            failed = []
+            for i in range(lib.nbg_gn_num_failed(out)):
+                lib.nbg_gn_failed(out, i, C.byref(code), C.byref(part))
+                failed.append((code.value, part.value))
+            schemas = []
+            for is_edge in (0, 1):
+                d = {}
+                ident, ncols = C.c_int32(), C.c_int32()
+                name, typ = C.c_char_p(), C.c_int32()
+                for i in range(lib.nbg_gn_num_schemas(out, is_edge)):
+                    lib.nbg_gn_schema(out, is_edge, i, C.byref(ident), C.byref(ncols))
+                    cols = []
+                    for c in range(ncols.value):
+                        lib.nbg_gn_schema_col(out, is_edge, i, c, C.byref(name), C.byref(typ))
+                        cols.append((name.value.decode(), typ.value))
+                    d[ident.value] = cols
+                schemas.append(d)
+            verts = []
+            ident, ptr, ln = C.c_int32(), C.POINTER(C.c_uint8)(), C.c_uint64()
+            for i in range(lib.nbg_gn_num_vertices(out)):
+                tags, edges = [], []
+                for k in range(lib.nbg_gn_vertex_num_tags(out, i)):
+                    lib.nbg_gn_vertex_tag(out, i, k, C.byref(ident), C.byref(ptr), C.byref(ln))
+                    tags.append((ident.value, C.string_at(ptr, ln.value)))
+                for k in range(lib.nbg_gn_vertex_num_edges(out, i)):
+                    lib.nbg_gn_vertex_edges(out, i, k, C.byref(ident), C.byref(ptr), C.byref(ln))
+                    edges.append((ident.value, C.string_at(ptr, ln.value)))
+                verts.append((int(lib.nbg_gn_vertex_id(out, i)), tuple(sorted(tags)), tuple(sorted(edges))))
+            return gn_canonical(failed, schemas[0], schemas[1], verts)
+        finally:
+            lib.nbg_gn_free(out)
+
+
+def gn_canonical(failed, vschema, eschema, vertices):
+    """Order-free form of a QueryResponse: failed codes, schemas, vertices as a sorted list of
+    (vid, tag_data, edge_data) with byte-exact rows (the reference's containers are unordered)."""
+    return {"failed": sorted(failed), "vertex_schema": dict(vschema), "edge_schema": dict(eschema),
+            "vertices": sorted(vertices)}
+
+
 # ---------------------------------------------------------------------- multi-GPU (partitioned)
 def comm_unique_id() -> bytes:
     """RCCL unique id (rank 0 creates it and ships it to the other ranks)."""

@@ -189,4 +189,59 @@ double orc_go_timed(void* h, const int64_t* starts, uint64_t nstarts, const int3
   return std::chrono::duration<double>(t1 - t0).count();
 }
 
+// ---- getBound (QueryBoundProcessor restated), response accessors mirror nbg_gn_*
+struct OrcGN { QueryResponse r; std::vector<std::pair<int32_t, Schema>> vs, es; };
+
+void* orc_get_bound(void* h, const int32_t* parts, const int64_t* vids, uint64_t n, const int32_t* etypes,
+                    int32_t ne, const uint8_t* filter, uint32_t flen, const int32_t* owners, const int32_t* ids,
+                    const char* const* names, int32_t nret) {
+  const Store& st = *static_cast<Store*>(h);
+  GNRequest req;
+  for (uint64_t i = 0; i < n; ++i) req.parts[parts[i]].push_back(vids[i]);
+  req.edgeTypes.assign(etypes, etypes + ne);
+  if (filter && flen) req.filter.assign(reinterpret_cast<const char*>(filter), flen);
+  for (int32_t i = 0; i < nret; ++i) req.returns.push_back(PropDef{owners[i], ids[i], names[i]});
+  auto* g = new OrcGN();
+  g->r = getBound(st, req);
+  for (auto& kv : g->r.vertexSchema) g->vs.emplace_back(kv.first, kv.second);
+  for (auto& kv : g->r.edgeSchema) g->es.emplace_back(kv.first, kv.second);
+  return g;
+}
+int32_t orc_gn_num_failed(void* r) { return (int32_t)static_cast<OrcGN*>(r)->r.failed.size(); }
+void orc_gn_failed(void* r, int32_t i, int32_t* code, int32_t* part) {
+  auto& f = static_cast<OrcGN*>(r)->r.failed[i];
+  *code = f.first;
+  *part = f.second;
+}
+int32_t orc_gn_num_schemas(void* r, int32_t is_edge) {
+  auto* g = static_cast<OrcGN*>(r);
+  return (int32_t)(is_edge ? g->es : g->vs).size();
+}
+int32_t orc_gn_schema(void* r, int32_t is_edge, int32_t i, int32_t c, const char** name, int32_t* type) {
+  auto* g = static_cast<OrcGN*>(r);
+  auto& e = (is_edge ? g->es : g->vs)[i];
+  if (c < 0) return (int32_t)e.second.cols.size() * 0 + e.first;   // c < 0: the id
+  *name = e.second.cols[c].name.c_str();
+  *type = e.second.cols[c].type;
+  return (int32_t)e.second.cols.size();
+}
+int64_t orc_gn_num_vertices(void* r) { return (int64_t)static_cast<OrcGN*>(r)->r.vertices.size(); }
+int64_t orc_gn_vertex_id(void* r, int64_t i) { return static_cast<OrcGN*>(r)->r.vertices[i].vid; }
+int32_t orc_gn_vertex_count(void* r, int64_t i, int32_t edges) {
+  auto& v = static_cast<OrcGN*>(r)->r.vertices[i];
+  return (int32_t)(edges ? v.edges.size() : v.tags.size());
+}
+int32_t orc_gn_vertex_item(void* r, int64_t i, int32_t edges, int32_t k, const uint8_t** data, uint64_t* len) {
+  auto& v = static_cast<OrcGN*>(r)->r.vertices[i];
+  if (edges) {
+    *data = reinterpret_cast<const uint8_t*>(v.edges[k].data.data());
+    *len = v.edges[k].data.size();
+    return v.edges[k].type;
+  }
+  *data = reinterpret_cast<const uint8_t*>(v.tags[k].data.data());
+  *len = v.tags[k].data.size();
+  return v.tags[k].tag;
+}
+void orc_gn_free(void* r) { delete static_cast<OrcGN*>(r); }
+
 }  // extern "C"

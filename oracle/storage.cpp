@@ -227,6 +227,7 @@ struct Processor {
                            TagFilters* tf, std::string& rowset) {
     auto prefix = edgePrefix(part, vid, et);
     auto rng = st.prefixRange(part, prefix);
+    if (rng.first == rng.second) return E_SUCCEEDED;
     const auto& kvs = st.parts.at(part);
     int64_t lastRank = -1, lastDst = 0;
     bool firstLoop = true;
@@ -269,7 +270,8 @@ struct Processor {
 
   // QueryBoundProcessor::processVertex (QueryBoundProcessor.cpp:64-111)
   int32_t processVertex(int32_t part, int64_t vid, bool onlyVertexProps, std::vector<VertexData>& out) {
-    if (st.parts.find(part) == st.parts.end()) return E_PART_NOT_FOUND;
+    // every part 1..numParts of the space exists (possibly empty) on its host
+    if (part < 1 || part > st.numParts) return E_PART_NOT_FOUND;
     VertexData vd; vd.vid = vid;
     TagFilters tf;
     for (auto& tc : tagCtx) {

@@ -107,15 +107,15 @@ def tagged_register(be, is_engine):
             be.register_tag(ident, name, cols)
 
 
-def tagged_pair(scale, parts=7, seed=5):
+def tagged_pair(scale, parts=7, seed=5, max_edge=0x7FFFFFFF):
     """(src, persons, engine, oracle) over the same tagged KV records."""
     from nebula_amd import Engine
     from tests.support.oracle import Oracle
     src, persons, kb = tagged_kv(scale, parts, seed)
-    eng = Engine(parts)
+    eng = Engine(parts, max_edge_returned_per_vertex=max_edge)
     tagged_register(eng, True)
     eng.load_builder(kb)
-    orc = Oracle(parts)
+    orc = Oracle(parts, max_edge_per_vertex=max_edge)
     tagged_register(orc, False)
     orc.load_builder(kb)
     return src, persons, eng, orc

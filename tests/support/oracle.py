@@ -52,6 +52,19 @@ def lib():
         L.orc_load_edges.argtypes = [vp, i32, vp, vp, u64, P(vp), i32]
         L.orc_load_edges.restype = i32
         L.orc_set_hosts.argtypes = [vp, i32]
+        L.orc_get_bound.restype = vp
+        L.orc_get_bound.argtypes = [vp, vp, vp, u64, vp, i32, vp, u32, vp, vp, vp, i32]
+        L.orc_gn_num_failed.argtypes = [vp]
+        L.orc_gn_failed.argtypes = [vp, i32, P(i32), P(i32)]
+        L.orc_gn_num_schemas.argtypes = [vp, i32]
+        L.orc_gn_schema.argtypes = [vp, i32, i32, i32, P(C.c_char_p), P(i32)]
+        L.orc_gn_num_vertices.argtypes = [vp]
+        L.orc_gn_num_vertices.restype = i64
+        L.orc_gn_vertex_id.argtypes = [vp, i64]
+        L.orc_gn_vertex_id.restype = i64
+        L.orc_gn_vertex_count.argtypes = [vp, i64, i32]
+        L.orc_gn_vertex_item.argtypes = [vp, i64, i32, i32, P(P(C.c_uint8)), P(u64)]
+        L.orc_gn_free.argtypes = [vp]
         _lib = L
     return _lib
 
@@ -171,6 +184,53 @@ class Oracle:
             return paths
         finally:
             self.L.orc_result_free(out)
+
+    def get_neighbors(self, part_vids, edge_types, filter=b"", returns=()):
+        """QueryBoundProcessor restated; same canonical dict as Engine.get_neighbors."""
+        from nebula_amd.engine import gn_canonical
+        L = self.L
+        parts = np.asarray([p for p, _ in part_vids], np.int32)
+        vids = np.asarray([v for _, v in part_vids], np.int64)
+        et = np.asarray(edge_types, np.int32)
+        owners = np.asarray([o for o, _, _ in returns], np.int32)
+        ids = np.asarray([i for _, i, _ in returns], np.int32)
+        names = (C.c_char_p * max(1, len(returns)))(*[n.encode() for _, _, n in returns])
+        fb = np.frombuffer(filter, np.uint8) if filter else None
+        r = L.orc_get_bound(self.h, _ptr(parts), _ptr(vids), len(vids), _ptr(et), len(et), _ptr(fb), len(filter),
+                            _ptr(owners), _ptr(ids), names, len(returns))
+        try:
+            code, part = C.c_int32(), C.c_int32()
+            failed = []
+            for i in range(L.orc_gn_num_failed(r)):
+                L.orc_gn_failed(r, i, C.byref(code), C.byref(part))
+                failed.append((code.value, part.value))
+            schemas = []
+            name, typ = C.c_char_p(), C.c_int32()
+            for is_edge in (0, 1):
+                d = {}
+                for i in range(L.orc_gn_num_schemas(r, is_edge)):
+                    ident = L.orc_gn_schema(r, is_edge, i, -1, C.byref(name), C.byref(typ))
+                    n = L.orc_gn_schema(r, is_edge, i, 0, C.byref(name), C.byref(typ))   # schemas are non-empty
+                    cols = [(name.value.decode(), typ.value)]
+                    for c in range(1, n):
+                        L.orc_gn_schema(r, is_edge, i, c, C.byref(name), C.byref(typ))
+                        cols.append((name.value.decode(), typ.value))
+                    d[ident] = cols
+                schemas.append(d)
+            verts = []
+            ptr, ln = C.POINTER(C.c_uint8)(), C.c_uint64()
+            for i in range(L.orc_gn_num_vertices(r)):
+                items = []
+                for edges in (0, 1):
+                    lst = []
+                    for k in range(L.orc_gn_vertex_count(r, i, edges)):
+                        ident = L.orc_gn_vertex_item(r, i, edges, k, C.byref(ptr), C.byref(ln))
+                        lst.append((ident, C.string_at(ptr, ln.value)))
+                    items.append(tuple(sorted(lst)))
+                verts.append((int(L.orc_gn_vertex_id(r, i)), items[0], items[1]))
+            return gn_canonical(failed, schemas[0], schemas[1], verts)
+        finally:
+            L.orc_gn_free(r)
 
     def go_timed(self, starts, etypes, steps, where=b""):
         s = np.asarray(starts, np.int64)
