@@ -2572,3 +2572,222 @@ hipError_t ws_path_greedy_part(Workspace* w, const PathTypes& bwd, const PathGre
 }
 
 }  // namespace nbg
+
+// ============================================================================= FIND ALL PATH
+// FindPathExecutor with ALL returns every walk of 1..N hops from a source to a target over the
+// OVER types, cycles included, each once (its odd/even meets decompose a walk uniquely,
+// FindPathExecutor.cpp:218-411).  The device enumerates the walks forward, level by level, and
+// prunes with the backward BFS distance to the targets (LAB label, computed by path.cpp): a walk
+// of i hops is extended to d only if dist(d) <= N - i - 1, so every stored walk completes and the
+// work is proportional to the output.  Level l holds, per walk, its last vertex, its parent walk
+// in level l - 1, the edge (CSR index, OVER position); a walk ending on a target is also listed as
+// a completion.  Each level is a count pass then a fill pass (exact allocation).
+namespace nbg {
+namespace {
+constexpr int WALK_MAX = 32;   // UPTO bound of FIND ALL PATH on the device
+
+struct WalkArgs {
+  int ntypes;
+  const uint32_t* row_ptr[MAX_TYPES_Q];
+  const uint32_t* col[MAX_TYPES_Q];
+  const uint8_t* visible;
+  const uint32_t* lab;
+  uint32_t epoch;
+  uint32_t budget;                 // largest admissible distance to a target for the next vertex
+  const uint32_t* vtx;             // level i: last vertex per walk
+  uint64_t n;
+  int fill;
+  uint32_t* nvtx;                  // level i + 1 (fill pass)
+  uint32_t* npar;
+  uint32_t* neid;
+  uint8_t* ntix;
+  uint32_t* comp;                  // completions of level i + 1 (walk index)
+  unsigned long long* cnt;         // [0] walks, [1] completions, [2] adjacency entries scanned
+};
+
+__global__ void __launch_bounds__(BLOCK) k_walk(WalkArgs a) {
+  unsigned long long nw = 0, nc = 0, ns = 0;
+  for (uint64_t w = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; w < a.n; w += (uint64_t)gridDim.x * BLOCK) {
+    const uint32_t v = a.vtx[w];
+    if (a.visible && !a.visible[v]) continue;
+    for (int t = 0; t < a.ntypes; ++t) {
+      const uint32_t b = a.row_ptr[t][v], e = a.row_ptr[t][v + 1];
+      ns += e - b;
+      for (uint32_t j = b; j < e; ++j) {
+        const uint32_t d = a.col[t][j];
+        if (d == NO_ROW) continue;
+        const uint32_t lb = a.lab[d];
+        if ((lb >> LVL_BITS) != a.epoch || (lb & MAX_PATH_LEN) > a.budget) continue;
+        const bool done = (lb & MAX_PATH_LEN) == 0;
+        if (!a.fill) {
+          ++nw;
+          nc += done;
+          continue;
+        }
+        const unsigned long long pos = atomicAdd(&a.cnt[0], 1ull);
+        a.nvtx[pos] = d;
+        a.npar[pos] = (uint32_t)w;
+        a.neid[pos] = j;
+        a.ntix[pos] = (uint8_t)t;
+        if (done) a.comp[atomicAdd(&a.cnt[1], 1ull)] = (uint32_t)pos;
+      }
+    }
+  }
+  if (!a.fill) {
+    for (int o = 32; o; o >>= 1) {
+      nw += __shfl_xor(nw, o, 64);
+      nc += __shfl_xor(nc, o, 64);
+      ns += __shfl_xor(ns, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0 && (nw | nc | ns)) {
+      atomicAdd(&a.cnt[0], nw);
+      atomicAdd(&a.cnt[1], nc);
+      atomicAdd(&a.cnt[2], ns);
+    }
+  }
+}
+
+struct WalkLevels {
+  const uint32_t* vtx[WALK_MAX + 1];
+  const uint32_t* par[WALK_MAX + 1];
+  const uint32_t* eid[WALK_MAX + 1];
+  const uint8_t* tix[WALK_MAX + 1];
+};
+struct WalkTypes {
+  const int64_t* rank[MAX_TYPES_Q];
+  int32_t type[MAX_TYPES_Q];
+};
+
+// entry list [v0, t0, r0, v1, ..., vL] of every completion of level L
+__global__ void __launch_bounds__(BLOCK) k_walk_emit(WalkLevels lv, WalkTypes wt, const uint32_t* __restrict__ comp,
+                                                     uint64_t ncomp, int L, const int64_t* __restrict__ vids,
+                                                     int64_t* __restrict__ out) {
+  for (uint64_t c = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; c < ncomp; c += (uint64_t)gridDim.x * BLOCK) {
+    uint32_t k = comp[c];
+    int64_t* o = out + c * (uint64_t)(1 + 3 * L);
+    for (int l = L; l >= 1; --l) {
+      const int t = lv.tix[l][k];
+      o[3 * l] = vids[lv.vtx[l][k]];
+      o[3 * l - 2] = wt.type[t];
+      o[3 * l - 1] = wt.rank[t] ? wt.rank[t][lv.eid[l][k]] : 0;
+      k = lv.par[l][k];
+    }
+    o[0] = vids[lv.vtx[0][k]];
+  }
+}
+}  // namespace
+
+hipError_t ws_all_paths(Workspace* w, const PathTypes& fwd, int lab, uint32_t epoch, const uint32_t* S, uint64_t nS,
+                        uint32_t upto, const int64_t* d_vids, const uint8_t* visible, uint64_t max_walks,
+                        std::vector<std::vector<int64_t>>* out, uint64_t* scanned) {
+  if (upto > (uint32_t)WALK_MAX || fwd.n > MAX_TYPES_Q) return hipErrorInvalidValue;
+  std::vector<void*> owned;
+  auto cleanup = [&]() {
+    (void)hipStreamSynchronize(w->stream);
+    for (void* p : owned) (void)hipFree(p);
+  };
+  auto alloc = [&](void** p, size_t b) -> hipError_t {
+    hipError_t e = hipMalloc(p, b < 8 ? 8 : b);
+    if (e == hipSuccess) owned.push_back(*p);
+    return e;
+  };
+#define WALK_TRY(x)                      \
+  do {                                   \
+    hipError_t e_ = (x);                 \
+    if (e_ != hipSuccess) {              \
+      cleanup();                         \
+      return e_;                         \
+    }                                    \
+  } while (0)
+  WalkLevels lv{};
+  std::vector<uint64_t> nlev(upto + 1, 0), ncomp(upto + 1, 0);
+  std::vector<uint32_t*> comp(upto + 1, nullptr);
+  uint32_t* v0 = nullptr;
+  WALK_TRY(alloc((void**)&v0, nS * 4));
+  WALK_TRY(hipMemcpy(v0, S, nS * 4, hipMemcpyHostToDevice));
+  lv.vtx[0] = v0;
+  nlev[0] = nS;
+  unsigned long long* cnt = nullptr;
+  WALK_TRY(alloc((void**)&cnt, 3 * 8));
+  unsigned long long h[3];
+  uint64_t total = nS;
+  *scanned = 0;
+  WalkArgs a{};
+  a.ntypes = fwd.n;
+  for (int t = 0; t < fwd.n; ++t) {
+    a.row_ptr[t] = fwd.a[t].row_ptr;
+    a.col[t] = fwd.a[t].col;
+  }
+  a.visible = visible;
+  a.cnt = cnt;
+  a.lab = w->lab[lab];
+  a.epoch = epoch;
+  uint32_t L = 0;
+  for (uint32_t i = 0; i < upto && nlev[i]; ++i) {
+    a.budget = upto - i - 1;
+    a.vtx = lv.vtx[i];
+    a.n = nlev[i];
+    const unsigned grid = (unsigned)std::min<uint64_t>(cdiv(a.n, BLOCK), 4096);
+    a.fill = 0;
+    WALK_TRY(hipMemsetAsync(cnt, 0, 3 * 8, w->stream));
+    hipLaunchKernelGGL(k_walk, dim3(grid), dim3(BLOCK), 0, w->stream, a);
+    WALK_TRY(hipGetLastError());
+    WALK_TRY(hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, w->stream));
+    WALK_TRY(hipStreamSynchronize(w->stream));
+    *scanned += h[2];
+    if (!h[0]) break;
+    total += h[0];
+    if (total > max_walks || h[0] >= 0xFFFFFFFFull) {
+      cleanup();
+      return hipErrorOutOfMemory;   // reported as "too many paths"
+    }
+    uint32_t *nv, *np, *ne, *cp;
+    uint8_t* nt;
+    WALK_TRY(alloc((void**)&nv, h[0] * 4));
+    WALK_TRY(alloc((void**)&np, h[0] * 4));
+    WALK_TRY(alloc((void**)&ne, h[0] * 4));
+    WALK_TRY(alloc((void**)&nt, h[0]));
+    WALK_TRY(alloc((void**)&cp, h[1] * 4));
+    a.fill = 1;
+    a.nvtx = nv;
+    a.npar = np;
+    a.neid = ne;
+    a.ntix = nt;
+    a.comp = cp;
+    a.cnt = cnt;
+    WALK_TRY(hipMemsetAsync(cnt, 0, 3 * 8, w->stream));
+    hipLaunchKernelGGL(k_walk, dim3(grid), dim3(BLOCK), 0, w->stream, a);
+    WALK_TRY(hipGetLastError());
+    lv.vtx[i + 1] = nv;
+    lv.par[i + 1] = np;
+    lv.eid[i + 1] = ne;
+    lv.tix[i + 1] = nt;
+    comp[i + 1] = cp;
+    nlev[i + 1] = h[0];
+    ncomp[i + 1] = h[1];
+    L = i + 1;
+  }
+  WalkTypes wt{};
+  for (int t = 0; t < fwd.n; ++t) {
+    wt.rank[t] = fwd.a[t].rank;
+    wt.type[t] = fwd.type[t];
+  }
+  for (uint32_t l = 1; l <= L; ++l) {
+    if (!ncomp[l]) continue;
+    const uint64_t width = 1 + 3 * (uint64_t)l;
+    int64_t* o = nullptr;
+    WALK_TRY(alloc((void**)&o, ncomp[l] * width * 8));
+    hipLaunchKernelGGL(k_walk_emit, dim3((unsigned)std::min<uint64_t>(cdiv(ncomp[l], BLOCK), 4096)), dim3(BLOCK), 0,
+                       w->stream, lv, wt, comp[l], ncomp[l], (int)l, d_vids, o);
+    WALK_TRY(hipGetLastError());
+    std::vector<int64_t> host(ncomp[l] * width);
+    WALK_TRY(hipMemcpyAsync(host.data(), o, host.size() * 8, hipMemcpyDeviceToHost, w->stream));
+    WALK_TRY(hipStreamSynchronize(w->stream));
+    for (uint64_t c = 0; c < ncomp[l]; ++c)
+      out->emplace_back(host.begin() + (ptrdiff_t)(c * width), host.begin() + (ptrdiff_t)((c + 1) * width));
+  }
+#undef WALK_TRY
+  cleanup();
+  return hipSuccess;
+}
+}  // namespace nbg

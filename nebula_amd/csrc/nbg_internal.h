@@ -373,6 +373,13 @@ hipError_t ws_path_greedy(Workspace* w, const PathTypes& out_types, const PathGr
 int ws_path_last_rec(Workspace* w);                              // PState record of the last launch
 hipError_t ws_path_read_label(Workspace* w, int lab, uint32_t v, uint32_t* out);   // synchronous
 hipError_t ws_path_sync(Workspace* w, PState* out, int64_t* path, int path_len);
+// FIND ALL PATH (single engine): every walk of 1..upto hops from the sources S (host, local ids)
+// whose hops keep the label distance (lab, epoch: backward BFS level from the targets) within
+// budget; entry lists appended to *out.  hipErrorOutOfMemory when more than max_walks partial
+// walks would be stored.
+hipError_t ws_all_paths(Workspace* w, const PathTypes& fwd, int lab, uint32_t epoch, const uint32_t* S, uint64_t nS,
+                        uint32_t upto, const int64_t* d_vids, const uint8_t* visible, uint64_t max_walks,
+                        std::vector<std::vector<int64_t>>* out, uint64_t* scanned);
 // partitioned engine (collective: every rank calls these in the same order)
 hipError_t ws_path_level_part(Workspace* w, const PathTypes& pt, int src, uint64_t n_bound, uint64_t e_bound, int dst,
                               const PathLevel& lv);

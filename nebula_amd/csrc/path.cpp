@@ -35,6 +35,7 @@
 // two caps differ and the device path reports NBG_E_UNSUPPORTED.
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <unordered_set>
 
 #include "engine.h"
@@ -270,6 +271,45 @@ int32_t one_sided(PathCtx& c, const std::vector<uint32_t>& S, const std::vector<
   return NBG_OK;
 }
 
+// FIND ALL PATH: backward BFS distances from the targets over in-edges (LAB_B, levels
+// 0..upto-1), then the pruned forward walk enumeration (ws_all_paths).
+int32_t all_paths(PathCtx& c, const std::vector<uint32_t>& S, const std::vector<uint32_t>& T, uint32_t upto,
+                  nbg_paths* out) {
+  Workspace* ws = c.ws;
+  const uint32_t eb = ws_path_epoch(ws, LAB_B);
+  hipError_t he = hipSuccess;
+  auto Tr = [&](hipError_t e) { if (he == hipSuccess) he = e; };
+  Tr(ws_path_upload(ws, S_B0, T.data(), T.size()));
+  Tr(ws_path_stamp(ws, S_B0, T.size(), LAB_B, stamp(eb, 0)));
+  Tr(ws_path_degsum(ws, S_B0, T.size(), c.bwd, 1));
+  PState ps;
+  Tr(sync(c, &ps));
+  if (he != hipSuccess) return dev_fail(c.E, he, "path setup");
+  int cur = S_B0;
+  uint64_t n = T.size(), ds = ps.dsum[1];
+  for (uint32_t l = 1; l < upto && n; ++l) {
+    PathLevel lv;
+    lv.lab = LAB_B;
+    lv.stamp = stamp(eb, l);
+    Tr(level(c, c.bwd, cur, n, ds, cur ^ 1, lv));
+    cur ^= 1;
+    Tr(ws_path_degsum(ws, cur, ds ? ds : 1, c.bwd, 1));
+    Tr(sync(c, &ps));
+    if (he != hipSuccess) return dev_fail(c.E, he, "path level");
+    n = ps.n[cur];
+    ds = ps.dsum[1];
+  }
+  uint64_t scanned = 0;
+  static const uint64_t max_walks = getenv("NBG_MAX_WALKS") ? strtoull(getenv("NBG_MAX_WALKS"), nullptr, 10)
+                                                            : (1ull << 28);
+  he = ws_all_paths(ws, c.fwd, LAB_B, eb, S.data(), S.size(), upto, c.E.snap.d_vids, c.E.snap.d_visible, max_walks,
+                    &out->paths, &scanned);
+  if (he == hipErrorOutOfMemory) return c.E.fail(NBG_E_OUT_OF_MEMORY, "FIND ALL PATH: too many paths");
+  if (he != hipSuccess) return dev_fail(c.E, he, "path enumeration");
+  c.edges += scanned;
+  return NBG_OK;
+}
+
 }  // namespace
 
 extern "C" int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* rq, nbg_paths** out) {
@@ -279,7 +319,9 @@ extern "C" int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* rq, nbg_
   std::lock_guard<std::mutex> lg(E.mu);
   if (!E.finalized) return E.fail(NBG_E_STATE, "engine not finalized");
   if (hipSetDevice(E.cfg.device) != hipSuccess) return E.fail(NBG_E_DEVICE, "hipSetDevice failed");
-  if (!rq->shortest) return E.fail(NBG_E_UNSUPPORTED, "FIND ALL PATH is not supported on the device path yet");
+  if (!rq->shortest && E.partitioned())
+    return E.fail(NBG_E_UNSUPPORTED, "FIND ALL PATH on a partitioned engine is not supported yet");
+  if (!rq->shortest && rq->upto > 32) return E.fail(NBG_E_UNSUPPORTED, "FIND ALL PATH UPTO exceeds 32");
   if (rq->upto > MAX_PATH_LEN) return E.fail(NBG_E_UNSUPPORTED, "UPTO exceeds the device path limit (63)");
   if (E.cfg.max_edge_returned_per_vertex > 0 && E.cfg.max_edge_returned_per_vertex != INT_MAX)
     return E.fail(NBG_E_UNSUPPORTED, "FIND PATH with max_edge_returned_per_vertex is not supported on the device");
@@ -369,7 +411,12 @@ extern "C" int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* rq, nbg_
   hipError_t he = ws_path_begin(c.ws, 0, E.snap.nv + S.size() + Tg.size() + 1024);
   if (he != hipSuccess) { delete res; return dev_fail(E, he, "path workspace"); }
   int32_t rc;
-  if (Sv.size() == 1 && Tv.size() == 1 && Sv[0] != Tv[0])
+  if (!rq->shortest) {
+    std::vector<uint32_t> Tl;
+    for (uint32_t d : Tg)
+      if (d != NO_ROW) Tl.push_back(d);
+    rc = all_paths(c, S, Tl, rq->upto, res);
+  } else if (Sv.size() == 1 && Tv.size() == 1 && Sv[0] != Tv[0])
     rc = bidirectional(c, S.empty() ? NO_ROW : S[0], Tg[0], rq->upto, res);
   else
     rc = one_sided(c, S, Tg, Sv.size(), rq->upto, res);

@@ -91,7 +91,7 @@ def tagged_kv(scale, parts=7, seed=5):
         if i % 3:
             kb.insert_edge(s, d, E_TYPE, 0, E_SCHEMA, [x], now + 2)
         else:
-            kb.insert_edge(s, d, E_F, 0, F_SCHEMA, [x % 7], now + 3)
+            kb.insert_edge(s, d, E_F, i % 3, F_SCHEMA, [x % 7], now + 3)   # ranks 0..2
     return src, persons, kb
 
 

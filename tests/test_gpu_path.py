@@ -1,6 +1,7 @@
 """FIND SHORTEST PATH parity on the MI355X: nebula_amd (bidirectional / one-sided BFS kernels,
 B-set recovery, greedy canonical reconstruction) vs the CPU oracle (oracle/graph.cpp
 runShortestBfs, itself pinned by FindPathTest.cpp's golden paths).  Bit-exact entry lists."""
+import numpy as np
 import pytest
 
 from nebula_amd import NbgError, nba_engine, rmat
@@ -86,8 +87,61 @@ def test_rmat_shortest_multi_source_target(rmat12):
         assert got == sorted(exp), (frm, to)
 
 
-def test_find_all_path_reports_unsupported(rmat12):
+@pytest.fixture(scope="module")
+def rmat10():
+    src, dst, w = graphs.rmat_graph(10)
+    eng = graphs.rmat_engine(src, dst, w)
+    orc = graphs.rmat_oracle(src, dst, w)
+    yield src, dst, eng, orc
+    eng.close()
+    orc.close()
+
+
+@pytest.mark.parametrize("upto", [1, 2, 3, 4])
+def test_rmat_all_paths_single_pairs(rmat10, upto):
+    """FIND ALL PATH: every walk of 1..N hops, cycles included, vs the faithful FindPathExecutor
+    restatement (odd/even meets over path multimaps, oracle/graph.cpp runFindPath)."""
+    src, dst, eng, orc = rmat10
+    total = 0
+    for s, t in pairs(src, dst, 12, seed=upto):
+        got = eng.find_path([s], [t], [1], upto, shortest=False)
+        exp = sorted(orc.find_path([s], [t], [1], upto, False))
+        assert got == exp, (s, t, upto, len(got), len(exp))
+        total += len(got)
+    if upto >= 3:
+        assert total > 0
+
+
+def test_rmat_all_paths_sets(rmat10):
+    """Several sources and targets (a source may be a target: cycles back to it count)."""
+    src, dst, eng, orc = rmat10
+    ps = pairs(src, dst, 12, seed=5)
+    frm = [p[0] for p in ps[:3]]
+    to = [p[1] for p in ps[:5]] + [frm[0]]
+    got = eng.find_path(frm + frm[:1], to, [1], 3, shortest=False)
+    exp = sorted(orc.find_path(frm, to, [1], 3, False))
+    assert got == exp and got
+
+
+def test_tagged_all_paths_multi_edge_ranks():
+    """Two OVER types with ranks (multi-edges between the same pair are distinct walks)."""
+    src, persons, eng, orc = graphs.tagged_pair(9)
+    try:
+        for s, t in pairs(src, src[::-1].copy(), 8, seed=2):
+            got = eng.find_path([s], [t], [graphs.E_TYPE, graphs.E_F], 3, shortest=False)
+            exp = sorted(orc.find_path([s], [t], [graphs.E_TYPE, graphs.E_F], 3, False))
+            assert got == exp, (s, t)
+    finally:
+        eng.close()
+        orc.close()
+
+
+def test_all_paths_too_many_is_an_error(rmat12):
+    """A walk explosion past the device budget fails loudly (NBG_E_OUT_OF_MEMORY)."""
+    import os
     src, dst, eng, orc = rmat12
+    hub = int(np.bincount(np.searchsorted(np.unique(src), src)).argmax())
+    h = int(np.unique(src)[hub])
     with pytest.raises(NbgError) as ex:
-        eng.find_path([int(src[0])], [int(dst[0])], [1], 3, shortest=False)
-    assert ex.value.code == _lib.E_UNSUPPORTED
+        eng.find_path([h], [h], [1], 12, shortest=False)
+    assert ex.value.code == _lib.E_OUT_OF_MEMORY
