@@ -75,6 +75,7 @@ def main():
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--sp-pairs", type=int, default=10000, help="FIND SHORTEST PATH pairs (0 = skip)")
     ap.add_argument("--sp-upto", type=int, default=5)
+    ap.add_argument("--sync", action="store_true", help="one query at a time (no query slots)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -119,7 +120,11 @@ def main():
     # GoExecutor::prepare() once, execute() per root (rows stay in HBM)
     stmt = eng.prepare_go([1], args.go_steps, where)
 
-    def one_step():
+    # queries in flight (nbg_go_submit query slots: concurrent queries, each on its own stream
+    # and workspace); a partitioned engine runs its collective queries one at a time
+    inflight = 0 if (world > 1 or args.sync) else int(os.environ.get("NBG_QUERY_SLOTS", "4"))
+
+    def one_step_sync():
         scanned = rows = 0
         lat = []
         for r in roots:
@@ -131,6 +136,25 @@ def main():
             res.free()
         return scanned, rows, lat
 
+    def one_step():
+        if not inflight:
+            return one_step_sync()
+        scanned = rows = 0
+        pending = []
+        for r in roots:
+            if len(pending) == inflight:
+                res = stmt.wait(pending.pop(0))
+                scanned += res.edges_scanned
+                rows += res.count
+                res.free()
+            pending.append(stmt.submit([r]))
+        for tk in pending:
+            res = stmt.wait(tk)
+            scanned += res.edges_scanned
+            rows += res.count
+            res.free()
+        return scanned, rows, []
+
     for _ in range(args.warmup):
         one_step()
 
@@ -140,13 +164,14 @@ def main():
         if torch.cuda.is_available():
             torch.cuda.synchronize()
 
-    def timed_pass():
+    def timed_pass(step=None):
+        step = step or one_step
         barrier()
         t0 = time.perf_counter()
         scanned = rows = 0
         lats = []
         for _ in range(args.steps):
-            s, r, lat = one_step()
+            s, r, lat = step()
             scanned += s
             rows += r
             lats += lat
@@ -155,17 +180,19 @@ def main():
 
     # the measured pass: no instrumentation inside the timed region
     scanned, rows, lats, elapsed = timed_pass()
+    # per-query latency: one more step with the queries run one at a time
+    _, _, lats = one_step_sync()
     kstats, breakdown, ev_elapsed = {}, {}, None
     if not args.no_profile:
         # roofline pass: the same K steps again with HIP events around every launch of the
         # dominant (final-step) kernel on the engine's stream (the events cost ~10% of the wall
         # time, which is why `value` comes from the pass above)
         eng.profile(2)
-        _, _, _, ev_elapsed = timed_pass()
+        _, _, _, ev_elapsed = timed_pass(one_step_sync)
         kstats = eng.profile_read()
         # per-kernel breakdown: one more step with events around every launch
         eng.profile(True)
-        one_step()
+        one_step_sync()
         breakdown = eng.profile_read()
         eng.profile(False)
 
@@ -249,6 +276,7 @@ def main():
         "config": {"workload": f"GO {args.go_steps} STEPS FROM <root> OVER e WHERE e.w < 50 YIELD e._dst, "
                                f"{len(roots)} single-root queries per step",
                    "graph": f"RMAT-{args.scale}", "parts": args.parts, "roots": len(roots),
+                   "queries_in_flight": inflight or 1,
                    "parallelism": "single" if world == 1 else f"partitioned{world}: part % {world}, bitmap "
                                                                f"all-to-all per hop over RCCL",
                    "vertices": st["num_vertices"], "live_edges_out_plus_in": st["num_edges"]},

@@ -155,6 +155,20 @@ int32_t nbg_go_execute(nbg_go_stmt* stmt, const int64_t* starts, uint64_t num_st
                        nbg_rows** out);
 void nbg_go_stmt_free(nbg_go_stmt* stmt);
 
+/* Asynchronous execution (the way graphd runs concurrent queries): up to NBG_QUERY_SLOTS
+ * (environment, default 4) queries of one engine in flight, each on its own workspace and HIP
+ * stream.  nbg_go_submit enqueues the query and returns a ticket (when every slot is busy it first
+ * completes the oldest query, whose result stays in its ticket); nbg_go_wait completes the ticket
+ * (and every older one), returns its rows with nbg_go_execute's semantics and frees the ticket.
+ * Device rows (device != 0) stay valid until the slot's next query, i.e. until NBG_QUERY_SLOTS
+ * further submissions.  A ticket never waited for is reclaimed by nbg_destroy; tickets must be
+ * waited for before their statement is freed.  Not available on partitioned engines (queries
+ * there are collectives). */
+typedef struct nbg_go_ticket nbg_go_ticket;
+int32_t nbg_go_submit(nbg_go_stmt* stmt, const int64_t* starts, uint64_t num_starts, int32_t device,
+                      nbg_go_ticket** out);
+int32_t nbg_go_wait(nbg_go_ticket* ticket, nbg_rows** out);
+
 int64_t nbg_rows_count(const nbg_rows* r);
 int32_t nbg_rows_num_cols(const nbg_rows* r);
 /* Σ_s E_s: adjacency entries scanned over all steps (the TEPS numerator); whole query, i.e.

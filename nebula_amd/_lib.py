@@ -86,6 +86,8 @@ SIGNATURES = [
     ("nbg_go_prepare", i32, [vp, P(nbg_go_request), P(vp)]),
     ("nbg_go_execute", i32, [vp, P(i64), u64, i32, P(vp)]),
     ("nbg_go_stmt_free", None, [vp]),
+    ("nbg_go_submit", i32, [vp, P(i64), u64, i32, P(vp)]),
+    ("nbg_go_wait", i32, [vp, P(vp)]),
     ("nbg_rows_count", i64, [vp]),
     ("nbg_rows_num_cols", i32, [vp]),
     ("nbg_rows_edges_scanned", u64, [vp]),

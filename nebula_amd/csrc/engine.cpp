@@ -38,6 +38,7 @@ struct nbg_rows {
   std::vector<std::vector<VKind>> kinds;              // per OVER type: value kind of each column
   std::vector<std::vector<std::string>> const_str;    // per OVER type: string constants absent from the dictionary
   Engine* eng = nullptr;
+  Workspace* ws = nullptr;               // the workspace holding the rows (device results)
   int ncols = 0;
   uint64_t count = 0;
   bool on_device = false;
@@ -89,7 +90,8 @@ int32_t materialize_rows(nbg_rows* r) {
     for (auto& s : r->segs) segs.emplace_back(s.begin, s.end - s.begin);
     std::vector<int64_t*> hc;
     for (auto& b : r->bits) hc.push_back(b.data());
-    if (ws_fetch_rows(r->eng->ws, segs, r->ncols, r->count, hc.data()) != hipSuccess) return NBG_E_DEVICE;
+    if (ws_fetch_rows(r->ws ? r->ws : r->eng->ws, segs, r->ncols, r->count, hc.data()) != hipSuccess)
+      return NBG_E_DEVICE;
   }
   std::unordered_map<int64_t, int64_t> sidx;
   uint64_t o = 0;
@@ -304,22 +306,20 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
   return NBG_OK;
 }
 
-// host-side phase timing of go_execute (NBG_HOST_TIMING=1: averages printed by nbg_destroy)
-static struct HostTiming {
-  bool on = getenv("NBG_HOST_TIMING") != nullptr;
-  double t[4] = {0, 0, 0, 0};
-  uint64_t n = 0;
-} g_ht;
-static inline double now_us() {
-  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
+// A GO query enqueued on a workspace, completed by go_collect.
+struct GoPending {
+  nbg_rows* rows = nullptr;
+  Workspace* ws = nullptr;
+  bool device = false;
+  bool finished = false;                 // nothing was enqueued (no start has rows)
+  std::vector<uint64_t> region, blk_cap;
+};
 
-static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* starts, uint64_t num_starts, bool device,
-                          nbg_rows** out) {
-  if (!out || (num_starts && !starts)) return E.fail(NBG_E_INVALID_ARGUMENT, "null argument");
-  const double ht0 = g_ht.on ? now_us() : 0;
-  double ht1 = 0, ht2 = 0, ht3 = 0;
-  *out = nullptr;
+// Enqueue the whole query (every step, the final-step rows and the end-of-query copy) on the
+// workspace *wsp (its stream `stream`); no host synchronisation.
+static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts, uint64_t num_starts, bool device,
+                         Workspace** wsp, hipStream_t stream, GoPending* p) {
+  if (num_starts && !starts) return E.fail(NBG_E_INVALID_ARGUMENT, "null argument");
   if (hipSetDevice(E.cfg.device) != hipSuccess) return E.fail(NBG_E_DEVICE, "hipSetDevice failed");
   const std::vector<int32_t>& over = st->over;
   const std::vector<TypeProgram>& plist = st->plist;
@@ -342,18 +342,23 @@ static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* start
   rows->eng = &E;
   rows->ncols = ncols;
   rows->on_device = device;
+  p->rows = rows;
+  p->device = device;
   // (partitioned: every rank runs the same collective sequence, even with no local start)
-  if (f0.empty() && !E.partitioned()) { *out = rows; return NBG_OK; }
-  if (f0.size() > ws_cap_frontier(E.ws)) {   // room for a duplicated start list
-    ws_destroy(E.ws);
-    E.ws = ws_create(f0.size(), E.snap.nv, E.snap.max_edges(), E.stream, &err);
-    if (!E.ws) { delete rows; return E.fail(NBG_E_OUT_OF_MEMORY, err); }
-    if (E.partitioned() && ws_set_partition(E.ws, E.comm.get(), E.npad) != hipSuccess) {
+  if (f0.empty() && !E.partitioned()) { p->finished = true; return NBG_OK; }
+  if (f0.size() > ws_cap_frontier(*wsp)) {   // room for a duplicated start list
+    ws_destroy(*wsp);
+    *wsp = ws_create(f0.size(), E.snap.nv, E.snap.max_edges(), stream, &err);
+    if (!*wsp) { delete rows; p->rows = nullptr; return E.fail(NBG_E_OUT_OF_MEMORY, err); }
+    if (E.partitioned() && ws_set_partition(*wsp, E.comm.get(), E.npad) != hipSuccess) {
       delete rows;
+      p->rows = nullptr;
       return E.fail(NBG_E_OUT_OF_MEMORY, "partition buffers");
     }
   }
-  Workspace* ws = E.ws;
+  Workspace* ws = *wsp;
+  p->ws = ws;
+  rows->ws = ws;
   const uint32_t cap = (uint32_t)(E.cfg.max_edge_returned_per_vertex <= 0 ? 0x7fffffff
                                                                           : E.cfg.max_edge_returned_per_vertex);
   auto args_for = [&](const DevEdgeType& dt) {
@@ -433,7 +438,6 @@ static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* start
   }
   auto inl_of = [&](size_t i, uint32_t s) -> const InlineList* { return s == 1 && !inl.empty() ? &inl[i] : nullptr; };
   hipError_t he = ws_reserve_rows(ws, cap_rows, ncols);
-  if (g_ht.on) ht1 = now_us();
   if (he == hipSuccess) he = ws_begin_query(ws, f0.data(), f0.size(), &plist, st->id);
   uint64_t n_bound = f0.size();
   for (uint32_t s = 1; he == hipSuccess && s <= steps; ++s) {
@@ -465,9 +469,32 @@ static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* start
     }
   }
   if (he == hipSuccess && E.partitioned()) he = ws_global_stats(ws, (int)over.size());
-  if (g_ht.on) ht2 = now_us();
-  if (he == hipSuccess) he = ws_end_query(ws);
-  if (g_ht.on) ht3 = now_us();
+  if (he == hipSuccess) he = ws_end_query_async(ws);
+  if (he != hipSuccess) {
+    delete rows;
+    p->rows = nullptr;
+    return E.fail(NBG_E_DEVICE, std::string("HIP: ") + hipGetErrorString(he));
+  }
+  p->region = std::move(region);
+  p->blk_cap = std::move(blk_cap);
+  return NBG_OK;
+}
+
+// Wait for a launched query and build its result.
+static int32_t go_collect(Engine& E, const nbg_go_stmt* st, GoPending* p, nbg_rows** out) {
+  nbg_rows* rows = p->rows;
+  p->rows = nullptr;
+  if (p->finished) { *out = rows; return NBG_OK; }
+  Workspace* ws = p->ws;
+  const std::vector<int32_t>& over = st->over;
+  const std::vector<TypeProgram>& plist = st->plist;
+  const int ncols = st->ncols;
+  const uint32_t steps = st->steps;
+  const int32_t deferred = st->deferred;
+  const std::vector<uint64_t>& region = p->region;
+  const std::vector<uint64_t>& blk_cap = p->blk_cap;
+  const bool device = p->device;
+  hipError_t he = ws_end_query_wait(ws);
   if (he != hipSuccess) {
     delete rows;
     return E.fail(NBG_E_DEVICE, std::string("HIP: ") + hipGetErrorString(he));
@@ -545,15 +572,17 @@ static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* start
     if (rc) { delete rows; return E.fail(rc, "row fetch failed"); }
   }
   *out = rows;
-  if (g_ht.on) {
-    const double ht4 = now_us();
-    g_ht.t[0] += ht1 - ht0;   // setup
-    g_ht.t[1] += ht2 - ht1;   // enqueue
-    g_ht.t[2] += ht3 - ht2;   // wait + readback
-    g_ht.t[3] += ht4 - ht3;   // result object
-    g_ht.n++;
-  }
   return NBG_OK;
+}
+
+static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* starts, uint64_t num_starts, bool device,
+                          nbg_rows** out) {
+  if (!out) return E.fail(NBG_E_INVALID_ARGUMENT, "null argument");
+  *out = nullptr;
+  GoPending p;
+  int32_t rc = go_launch(E, st, starts, num_starts, device, &E.ws, E.stream, &p);
+  if (rc) return rc;
+  return go_collect(E, st, &p, out);
 }
 
 static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_rows** out) {
@@ -566,8 +595,92 @@ static int32_t go_impl(Engine& E, const nbg_go_request* rq, bool device, nbg_row
   return rc;
 }
 
+// ============================================================================= asynchronous GO
+// Up to NBG_QUERY_SLOTS queries of one engine in flight: each on its own workspace and HIP
+// stream, so the device overlaps one query's latency-bound small launches with another's
+// expansion (graphd serves concurrent queries the same way, one executor per query).
+struct nbg_go_ticket {
+  nbg_go_stmt* st = nullptr;
+  int slot = -1;
+  GoPending p;
+  bool done = false;
+  int32_t rc = NBG_OK;
+  nbg_rows* result = nullptr;
+};
+
+static int query_slots() {
+  static const int n = [] {
+    const char* v = getenv("NBG_QUERY_SLOTS");
+    const int k = v ? atoi(v) : 4;
+    return k < 1 ? 1 : (k > 16 ? 16 : k);
+  }();
+  return n;
+}
+
+// complete the oldest submitted ticket (its result stays in the ticket until nbg_go_wait)
+static void complete_oldest(Engine& E) {
+  auto* t = static_cast<nbg_go_ticket*>(E.inflight.front());
+  E.inflight.erase(E.inflight.begin());
+  t->rc = go_collect(E, t->st, &t->p, &t->result);
+  t->done = true;
+  E.slots[t->slot].ticket = nullptr;
+}
+
 // ============================================================================= C ABI
 extern "C" {
+
+int32_t nbg_go_submit(nbg_go_stmt* st, const int64_t* starts, uint64_t num_starts, int32_t device,
+                      nbg_go_ticket** out) {
+  if (!st || !st->eng || !out) return NBG_E_INVALID_ARGUMENT;
+  Engine& E = *st->eng;
+  std::lock_guard<std::mutex> lg(E.mu);
+  *out = nullptr;
+  if (E.partitioned()) return E.fail(NBG_E_UNSUPPORTED, "asynchronous GO on a partitioned engine (queries are collectives)");
+  if (hipSetDevice(E.cfg.device) != hipSuccess) return E.fail(NBG_E_DEVICE, "hipSetDevice failed");
+  if (E.slots.empty()) E.slots.resize(query_slots());
+  int slot = -1;
+  for (size_t i = 0; i < E.slots.size() && slot < 0; ++i)
+    if (!E.slots[i].ticket) slot = (int)i;
+  if (slot < 0) {   // every slot busy: finish the oldest query first
+    const int s0 = static_cast<nbg_go_ticket*>(E.inflight.front())->slot;
+    complete_oldest(E);
+    slot = s0;
+  }
+  Engine::QuerySlot& q = E.slots[slot];
+  if (!q.stream && hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking) != hipSuccess)
+    return E.fail(NBG_E_DEVICE, "hipStreamCreate failed");
+  if (!q.ws) {
+    std::string err;
+    q.ws = ws_create(E.snap.nv + 1024, E.snap.nv, E.snap.max_edges(), q.stream, &err);
+    if (!q.ws) return E.fail(NBG_E_OUT_OF_MEMORY, err);
+  }
+  auto* t = new nbg_go_ticket();
+  t->st = st;
+  t->slot = slot;
+  int32_t rc = go_launch(E, st, starts, num_starts, device != 0, &q.ws, q.stream, &t->p);
+  if (rc) { delete t; return rc; }
+  q.ticket = t;
+  E.inflight.push_back(t);
+  *out = t;
+  return NBG_OK;
+}
+
+int32_t nbg_go_wait(nbg_go_ticket* t, nbg_rows** out) {
+  if (!t || !out) return NBG_E_INVALID_ARGUMENT;
+  Engine& E = *t->st->eng;
+  std::lock_guard<std::mutex> lg(E.mu);
+  *out = nullptr;
+  if (!t->done) {
+    // complete every older ticket first (their results stay in their tickets)
+    while (!E.inflight.empty() && E.inflight.front() != t) complete_oldest(E);
+    complete_oldest(E);
+  }
+  const int32_t rc = t->rc;
+  *out = t->result;
+  delete t;
+  return rc;
+}
+
 
 int32_t nbg_create(const nbg_config* cfg, nbg_engine** out) {
   if (!cfg || !out) return NBG_E_INVALID_ARGUMENT;
@@ -583,6 +696,16 @@ int32_t nbg_create(const nbg_config* cfg, nbg_engine** out) {
 void nbg_destroy(nbg_engine* h) {
   if (!h) return;
   Engine& E = h->e;
+  while (!E.inflight.empty()) {   // tickets never waited for
+    auto* t = static_cast<nbg_go_ticket*>(E.inflight.front());
+    complete_oldest(E);
+    if (t->result) nbg_rows_free(t->result);
+    t->result = nullptr;
+  }
+  for (auto& q : E.slots) {
+    if (q.ws) ws_destroy(q.ws);
+    if (q.stream) (void)hipStreamDestroy(q.stream);
+  }
   if (E.ws) ws_destroy(E.ws);
   for (auto& kv : E.snap.types) {
     auto& d = kv.second;
@@ -593,11 +716,6 @@ void nbg_destroy(nbg_engine* h) {
       if (p) (void)hipFree(p);
     for (auto* p : d.narrow)
       if (p) (void)hipFree(p);
-  }
-  if (g_ht.on && g_ht.n) {
-    fprintf(stderr, "[nbg host timing] %llu queries, us/query: setup %.1f enqueue %.1f wait %.1f result %.1f\n",
-            (unsigned long long)g_ht.n, g_ht.t[0] / g_ht.n, g_ht.t[1] / g_ht.n, g_ht.t[2] / g_ht.n, g_ht.t[3] / g_ht.n);
-    g_ht = HostTiming{};
   }
   for (auto& kv : E.snap.tags) {
     if (kv.second.present) (void)hipFree(kv.second.present);

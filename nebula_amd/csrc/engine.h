@@ -28,6 +28,14 @@ struct Engine {
   hipStream_t stream = nullptr;
   Workspace* ws = nullptr;
   std::mutex mu;
+  // asynchronous GO (nbg_go_submit / nbg_go_wait): query slots, each a workspace on its own stream
+  struct QuerySlot {
+    Workspace* ws = nullptr;
+    hipStream_t stream = nullptr;
+    void* ticket = nullptr;   // the ticket running on this slot (nullptr: free)
+  };
+  std::vector<QuerySlot> slots;
+  std::vector<void*> inflight;          // submitted tickets, oldest first
   // multi-GPU (partitioned mode when cfg.num_gpus > 1): global id = owner * npad + local id
   std::unique_ptr<Comm> comm;
   uint64_t npad = 0;

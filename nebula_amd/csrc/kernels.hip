@@ -1719,17 +1719,37 @@ hipError_t ws_fetch_rows(Workspace* w, const std::vector<std::pair<uint64_t, uin
   return e;
 }
 
-hipError_t ws_end_query(Workspace* w) {
+// The end of a query in two halves: the QState / row-count copy and an event behind it (async),
+// then the wait for that event and the reset of QState for the next query on this workspace.
+hipError_t ws_end_query_async(Workspace* w) {
   int nt = 0;
   for (int t = 0; t < MAX_TYPES_Q; ++t)
     if (w->final_grid[t]) nt = t + 1;
   HIP_TRY(hipMemcpyAsync(w->h_q, w->q, sizeof(QState) + (size_t)nt * EXPAND_GRID * 4, hipMemcpyDeviceToHost,
                          w->stream));
-  HIP_TRY(ws_wait(w));
+  if (!w->done_ev) HIP_TRY(hipEventCreateWithFlags(&w->done_ev, hipEventDisableTiming));
+  return hipEventRecord(w->done_ev, w->stream);
+}
+
+hipError_t ws_end_query_wait(Workspace* w) {
+  static const bool blocking = getenv("NBG_BLOCKING_SYNC") != nullptr;
+  if (blocking) {
+    HIP_TRY(hipEventSynchronize(w->done_ev));
+  } else {
+    hipError_t e;
+    while ((e = hipEventQuery(w->done_ev)) == hipErrorNotReady) {
+    }
+    HIP_TRY(e);
+  }
   // reset for the next query; runs while the host reads the results
   HIP_TRY(hipMemsetAsync(w->q, 0, sizeof(QState), w->stream));
   prof_flush(w, w->h_q);
   return hipSuccess;
+}
+
+hipError_t ws_end_query(Workspace* w) {
+  HIP_TRY(ws_end_query_async(w));
+  return ws_end_query_wait(w);
 }
 
 // ----------------------------------------------------------------------------- partitioned mode

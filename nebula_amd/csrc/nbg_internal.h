@@ -330,6 +330,8 @@ hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a, uint64_t n_bound, 
                            const TypeProgram& prog, uint64_t region_base, uint64_t blk_cap, const InlineList* il = nullptr);
 hipError_t ws_scan_only(Workspace* w, const ExpandArgs& a, uint64_t n_bound, int step, int tix);
 hipError_t ws_end_query(Workspace* w);
+hipError_t ws_end_query_async(Workspace* w);   // enqueue the end-of-query copy + event
+hipError_t ws_end_query_wait(Workspace* w);    // wait for it (then as ws_end_query)
 // partitioned mode: flags over [world * npad) global ids, per-hop bitmap all-to-all
 constexpr uint64_t PART_ALIGN = 16384 * 4;   // npad granularity (flag / bit workgroups divide it)
 hipError_t ws_set_partition(Workspace* w, Comm* comm, uint64_t npad);

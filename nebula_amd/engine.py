@@ -90,6 +90,19 @@ class GoStatement:
         self.eng._check(self.eng.lib.nbg_go_execute(self.h, ptr, n, 1, C.byref(out)), "go_execute")
         return DeviceRows(self.eng, out)
 
+    def submit(self, starts, device=True):
+        """nbg_go_submit: enqueue on a free query slot; returns a ticket for :meth:`wait`."""
+        a = np.ascontiguousarray(starts, np.int64)
+        out = C.c_void_p()
+        self.eng._check(self.eng.lib.nbg_go_submit(self.h, a.ctypes.data_as(C.POINTER(C.c_int64)) if len(a) else None,
+                                                   len(a), int(device), C.byref(out)), "go_submit")
+        return out
+
+    def wait(self, ticket) -> DeviceRows:
+        out = C.c_void_p()
+        self.eng._check(self.eng.lib.nbg_go_wait(ticket, C.byref(out)), "go_wait")
+        return DeviceRows(self.eng, out)
+
     def run(self, starts):
         ptr, n = self._starts(starts)
         out = C.c_void_p()

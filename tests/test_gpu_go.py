@@ -190,3 +190,26 @@ def test_narrow_int_columns(scale_w):
     finally:
         eng.close()
         orc.close()
+
+
+def test_async_submit_wait_parity(rmat12):
+    """nbg_go_submit / nbg_go_wait: queries in flight on the query slots (more than there are
+    slots, waited for out of order) return exactly the synchronous results."""
+    src, eng, orc = rmat12
+    wb = WHERES["w<50"].encode()
+    stmt = eng.prepare_go([1], 3, wb)
+    roots = graphs.roots(src, 11, seed=9)
+    try:
+        tickets = [stmt.submit([r], device=False) for r in roots]
+        order = list(range(len(roots)))[::-1]   # newest first: older tickets complete inside
+        got = {}
+        for i in order:
+            res = stmt.wait(tickets[i])
+            got[i] = (res.count, res.edges_scanned, graphs.sorted_rows(res.fetch()))
+            res.free()
+        for i, r in enumerate(roots):
+            exp = graphs.sorted_rows(orc.go([r], [1], 3, wb))
+            assert got[i][2] == exp, r
+            assert got[i][0] == len(exp)
+    finally:
+        stmt.free()
