@@ -122,7 +122,7 @@ def main():
 
     # queries in flight (nbg_go_submit query slots: concurrent queries, each on its own stream
     # and workspace); a partitioned engine runs its collective queries one at a time
-    inflight = 0 if (world > 1 or args.sync) else int(os.environ.get("NBG_QUERY_SLOTS", "4"))
+    inflight = 0 if (world > 1 or args.sync) else int(os.environ.get("NBG_QUERY_SLOTS", "6"))
 
     def one_step_sync():
         scanned = rows = 0

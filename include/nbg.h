@@ -156,7 +156,7 @@ int32_t nbg_go_execute(nbg_go_stmt* stmt, const int64_t* starts, uint64_t num_st
 void nbg_go_stmt_free(nbg_go_stmt* stmt);
 
 /* Asynchronous execution (the way graphd runs concurrent queries): up to NBG_QUERY_SLOTS
- * (environment, default 4) queries of one engine in flight, each on its own workspace and HIP
+ * (environment, default 6) queries of one engine in flight, each on its own workspace and HIP
  * stream.  nbg_go_submit enqueues the query and returns a ticket (when every slot is busy it first
  * completes the oldest query, whose result stays in its ticket); nbg_go_wait completes the ticket
  * (and every older one), returns its rows with nbg_go_execute's semantics and frees the ticket.

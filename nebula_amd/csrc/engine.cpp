@@ -611,7 +611,7 @@ struct nbg_go_ticket {
 static int query_slots() {
   static const int n = [] {
     const char* v = getenv("NBG_QUERY_SLOTS");
-    const int k = v ? atoi(v) : 4;
+    const int k = v ? atoi(v) : 6;
     return k < 1 ? 1 : (k > 16 ? 16 : k);
   }();
   return n;
