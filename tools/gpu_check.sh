@@ -18,7 +18,7 @@ for step in "$@"; do
       timeout -k 10 600 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.log" || { tail -30 "$OUT/bench.log"; exit 1; } ;;
     prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-        python3 -u bench.py --sp-pairs 2000 --no-cpu-baseline > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.log" \
+        python3 -u bench.py --sp-pairs 2000 --no-cpu-baseline --sync > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.log" \
         || { tail -30 "$OUT/bench_prof.log"; exit 1; } ;;
     probe)
       timeout -k 10 180 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
