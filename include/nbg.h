@@ -272,6 +272,25 @@ int32_t nbg_gn_vertex_edges(const nbg_gn_response* r, int64_t i, int32_t k, int3
 uint64_t nbg_gn_edges(const nbg_gn_response* r);
 void nbg_gn_free(nbg_gn_response* r);
 
+/* ---- boundStats (StorageServiceHandler::future_boundStats -> QueryStatsProcessor) ---------
+ * The GetNeighbors request with a StatType per return column (storage.thrift PropDef.stat):
+ * one row of SUM / COUNT / AVG over the collected values (QueryStatsProcessor.cpp:16-130,
+ * StatsCollector in Collector.h:76-109): tag props of the requested vertices, edge props of the
+ * accepted edges; _src/_dst are not collected, bool/string only count; SUM/AVG need a numeric
+ * column (else NBG_E_IMPROPER_DATA_TYPE per part).  `data` is the encoded row. */
+#define NBG_STAT_SUM   1
+#define NBG_STAT_COUNT 2
+#define NBG_STAT_AVG   3
+typedef struct nbg_stats_response nbg_stats_response;
+int32_t nbg_bound_stats(nbg_engine* e, const nbg_gn_request* req, const int32_t* stats, nbg_stats_response** out);
+int32_t nbg_stats_num_failed(const nbg_stats_response* r);
+int32_t nbg_stats_failed(const nbg_stats_response* r, int32_t i, int32_t* code, int32_t* part);
+int32_t nbg_stats_num_cols(const nbg_stats_response* r);
+/* column c: name, NBG_T_INT / NBG_T_DOUBLE, value (int64 or double bits) */
+int32_t nbg_stats_col(const nbg_stats_response* r, int32_t c, const char** name, int32_t* type, int64_t* bits);
+int32_t nbg_stats_data(const nbg_stats_response* r, const uint8_t** data, uint64_t* len);
+void nbg_stats_free(nbg_stats_response* r);
+
 /* ---- in-library kernel timing (HIP events on the engine's stream) ----------------------- */
 typedef struct {
   const char* name;           /* kernel name (static string)                                  */

@@ -121,6 +121,13 @@ SIGNATURES = [
     ("nbg_gn_vertex_edges", i32, [vp, i64, i32, P(i32), P(P(u8)), P(u64)]),
     ("nbg_gn_edges", u64, [vp]),
     ("nbg_gn_free", None, [vp]),
+    ("nbg_bound_stats", i32, [vp, P(nbg_gn_request), P(i32), P(vp)]),
+    ("nbg_stats_num_failed", i32, [vp]),
+    ("nbg_stats_failed", i32, [vp, i32, P(i32), P(i32)]),
+    ("nbg_stats_num_cols", i32, [vp]),
+    ("nbg_stats_col", i32, [vp, i32, P(C.c_char_p), P(i32), P(i64)]),
+    ("nbg_stats_data", i32, [vp, P(P(u8)), P(u64)]),
+    ("nbg_stats_free", None, [vp]),
     ("nbg_profile", i32, [vp, i32]),
     ("nbg_profile_read", i32, [vp, vp, i32]),
     ("nbg_comm_unique_id", i32, [P(u8)]),

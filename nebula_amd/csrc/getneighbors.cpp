@@ -90,6 +90,23 @@ struct PropCtx {
   int32_t type = 0;     // NBG_T_* of the response schema column
   int pik = 0;          // key prop: 1 _src, 2 _dst, 3 _type, 4 _rank
   int col = -1;         // value column (edge or tag schema)
+  int ret = 0;          // retIndex_: position among the returned columns
+  int32_t stat = 0;     // boundStats: NBG_STAT_* (0: none)
+};
+
+// QueryStatsProcessor / StatsCollector (src/storage/QueryStatsProcessor.cpp:16-130,
+// src/storage/Collector.h:76-109): one SUM / COUNT / AVG per returned column over every collected
+// value; vids (_src/_dst) are not collected at all, bool and string only count.
+struct StatAcc {
+  std::string name;
+  int32_t stat = 0;
+  bool dbl = false;     // the column's values are doubles (sum kept as double)
+  int64_t isum = 0;
+  double dsum = 0;
+  int32_t count = 0;
+};
+struct StatsSink {
+  std::vector<StatAcc> acc;   // by retIndex_
 };
 struct TagCtx {
   int32_t tag;
@@ -144,7 +161,16 @@ bool part_served(const Engine& E, int32_t part) {
 
 }  // namespace
 
-static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_response* resp) {
+// stats != nullptr: boundStats — accumulate per returned column (stat_types[i] per request column)
+static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_response* resp,
+                             const int32_t* stat_types = nullptr, StatsSink* stats = nullptr) {
+  int ret_index = 0;
+  // QueryBaseProcessor::validOperation (QueryBaseProcessor.inl:18-35)
+  auto valid_op = [](int32_t type, int32_t stat) {
+    if (stat != NBG_STAT_SUM && stat != NBG_STAT_AVG) return true;
+    return type == NBG_T_INT || type == NBG_T_VID || type == NBG_T_TIMESTAMP || type == NBG_T_FLOAT ||
+           type == NBG_T_DOUBLE;
+  };
   // --- checkAndBuildContexts
   std::vector<TagCtx> tctx;
   std::vector<EdgeCtx> ectx;
@@ -168,6 +194,9 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
       pc.col = s->find(name);
       if (pc.col < 0) { code = NBG_E_IMPROPER_DATA_TYPE; break; }
       pc.type = s->cols[pc.col].type;
+      pc.stat = stat_types ? stat_types[i] : 0;
+      if (!valid_op(pc.type, pc.stat)) { code = NBG_E_IMPROPER_DATA_TYPE; break; }
+      pc.ret = ret_index++;
       TagCtx* tc = nullptr;
       for (auto& c : tctx)
         if (c.tag == pd.id) tc = &c;
@@ -186,6 +215,9 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
       } else {
         continue;   // "InBound has none props, skip it!"
       }
+      pc.stat = stat_types ? stat_types[i] : 0;
+      if (!valid_op(pc.type, pc.stat)) { code = NBG_E_IMPROPER_DATA_TYPE; break; }
+      pc.ret = ret_index++;
       EdgeCtx* ec = edge_ctx(pd.id);
       if (!ec) { ectx.push_back(EdgeCtx{pd.id, {}}); ec = &ectx.back(); }
       ec->props.push_back(pc);
@@ -406,18 +438,56 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
       case VK_STRING: w.put_string(str_of(bits)); break;
     }
   };
+  if (stats) {
+    stats->acc.assign(ret_index, StatAcc{});
+    for (auto& tc : tctx)
+      for (auto& pc : tc.props) stats->acc[pc.ret] = StatAcc{pc.name, pc.stat, kindOfType(pc.type) == VK_DOUBLE};
+    for (auto& ec : ectx)
+      for (auto& pc : ec.props)
+        stats->acc[pc.ret] = StatAcc{pc.name, pc.stat, !pc.pik && kindOfType(pc.type) == VK_DOUBLE};
+  }
+  auto collect = [&](const PropCtx& pc, int64_t bits) {   // StatsCollector::collect*
+    StatAcc& a = stats->acc[pc.ret];
+    if (pc.pik == 1 || pc.pik == 2) return;                // collectVid: nothing
+    if (pc.pik) { a.isum += bits; ++a.count; return; }    // _type / _rank: collectInt64
+    switch (kindOfType(pc.type)) {
+      case VK_INT: a.isum += bits; break;
+      case VK_DOUBLE: { double d; memcpy(&d, &bits, 8); a.dsum += d; break; }
+      default: break;                                      // bool / string: count only
+    }
+    ++a.count;
+  };
   std::vector<uint64_t> order(rq->num_vids);
   for (uint64_t i = 0; i < rq->num_vids; ++i) order[i] = i;
   std::stable_sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return rq->parts[a] < rq->parts[b]; });
+  std::vector<int32_t> stat_failed;   // parts with a failed vertex (boundStats)
   for (uint64_t i : order) {
     if (!part_ok(rq->parts[i])) continue;
     nbg_gn_response::Vertex v;
     v.vid = rq->vids[i];
     const uint32_t d = dense[i];
+    if (stats) {
+      // QueryStatsProcessor::processVertex: a requested tag the vertex lacks fails the vertex
+      // (ERR_KEY_NOT_FOUND -> E_UNKNOWN, BaseProcessor.inl:14-29), first failure per part
+      bool missing = false;
+      for (auto& tc : tctx) missing = missing || d == NO_ROW || !E.snap.tags.at(tc.tag).h_present[d];
+      if (missing) {
+        if (std::find(stat_failed.begin(), stat_failed.end(), rq->parts[i]) == stat_failed.end()) {
+          stat_failed.push_back(rq->parts[i]);
+          resp->failed.emplace_back(NBG_E_UNKNOWN, rq->parts[i]);
+        }
+        continue;
+      }
+    }
     if (d == NO_ROW) continue;   // no keys in this part: no edges, not returned
     for (auto& tc : tctx) {      // collectVertexProps: the tag's live record, returned props
       const DevTag& dtg = E.snap.tags.at(tc.tag);
       if (!dtg.h_present[d]) continue;
+      if (stats) {
+        if (dtg.h_present[d] == 1)
+          for (auto& pc : tc.props) collect(pc, dtg.h_cols[pc.col][d]);
+        continue;
+      }
       RowBytes w;
       if (dtg.h_present[d] == 1)
         for (auto& pc : tc.props) put_value(w, pc.type, dtg.h_cols[pc.col][d]);
@@ -431,6 +501,12 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
       if (it == tr.range.end()) continue;
       std::string rs;
       const uint64_t lo = it->second.first, hi = std::min(it->second.second, it->second.first + cap);
+      if (stats) {
+        for (uint64_t r = lo; r < hi; ++r)
+          for (size_t p = 0; p < ec.props.size(); ++p) collect(ec.props[p], tr.vals[p][r]);
+        resp->edges += hi - lo;
+        continue;
+      }
       for (uint64_t r = lo; r < hi; ++r) {
         RowBytes w;
         for (size_t p = 0; p < ec.props.size(); ++p) {
@@ -484,6 +560,85 @@ int32_t nbg_get_neighbors(nbg_engine* h, const nbg_gn_request* rq, nbg_gn_respon
   *out = r;
   return NBG_OK;
 }
+
+// ---- boundStats (StorageServiceHandler::future_boundStats -> QueryStatsProcessor)
+struct nbg_stats_response {
+  std::vector<std::pair<int32_t, int32_t>> failed;
+  std::vector<std::pair<std::string, int32_t>> schema;   // (name, NBG_T_INT / NBG_T_DOUBLE)
+  std::vector<int64_t> bits;                            // value per column (int64 or double bits)
+  std::string data;                                     // the encoded row (RowWriter, schema-less)
+  uint64_t edges = 0;
+};
+
+int32_t nbg_bound_stats(nbg_engine* h, const nbg_gn_request* rq, const int32_t* stats, nbg_stats_response** out) {
+  if (!h || !rq || !out || (rq->num_return_columns && !stats) || (rq->num_vids && (!rq->vids || !rq->parts)) ||
+      (rq->num_edge_types && !rq->edge_types) || (rq->num_return_columns && !rq->return_columns))
+    return NBG_E_INVALID_ARGUMENT;
+  *out = nullptr;
+  Engine& E = h->e;
+  std::lock_guard<std::mutex> lg(E.mu);
+  if (!E.finalized) return E.fail(NBG_E_STATE, "engine not finalized");
+  if (hipSetDevice(E.cfg.device) != hipSuccess) return E.fail(NBG_E_DEVICE, "hipSetDevice failed");
+  nbg_gn_response tmp;
+  StatsSink sink;
+  int32_t rc = get_neighbors(E, rq, &tmp, stats, &sink);
+  if (rc) return rc;
+  auto* r = new nbg_stats_response();
+  r->failed = tmp.failed;
+  r->edges = tmp.edges;
+  if (!sink.acc.empty() || r->failed.empty()) {   // not a request-level error
+    // QueryStatsProcessor::calcResult (QueryStatsProcessor.cpp:16-63)
+    RowBytes w;
+    for (auto& a : sink.acc) {
+      int64_t bits = 0;
+      switch (a.stat) {
+        case NBG_STAT_SUM:
+          if (a.dbl) { memcpy(&bits, &a.dsum, 8); w.put_double(bits); r->schema.emplace_back(a.name, NBG_T_DOUBLE); }
+          else { bits = a.isum; w.put_int(bits); r->schema.emplace_back(a.name, NBG_T_INT); }
+          break;
+        case NBG_STAT_COUNT:
+          bits = a.count;
+          w.put_int(bits);
+          r->schema.emplace_back(a.name, NBG_T_INT);
+          break;
+        case NBG_STAT_AVG: {
+          const double v = a.dbl ? a.dsum / a.count : (double)a.isum / a.count;
+          memcpy(&bits, &v, 8);
+          w.put_double(bits);
+          r->schema.emplace_back(a.name, NBG_T_DOUBLE);
+          break;
+        }
+        default: continue;   // no stat set: no column
+      }
+      r->bits.push_back(bits);
+    }
+    r->data = w.encode();
+  }
+  *out = r;
+  return NBG_OK;
+}
+int32_t nbg_stats_num_failed(const nbg_stats_response* r) { return r ? (int32_t)r->failed.size() : -1; }
+int32_t nbg_stats_failed(const nbg_stats_response* r, int32_t i, int32_t* code, int32_t* part) {
+  if (!r || i < 0 || i >= (int32_t)r->failed.size() || !code || !part) return NBG_E_INVALID_ARGUMENT;
+  *code = r->failed[i].first;
+  *part = r->failed[i].second;
+  return NBG_OK;
+}
+int32_t nbg_stats_num_cols(const nbg_stats_response* r) { return r ? (int32_t)r->schema.size() : -1; }
+int32_t nbg_stats_col(const nbg_stats_response* r, int32_t c, const char** name, int32_t* type, int64_t* bits) {
+  if (!r || c < 0 || c >= (int32_t)r->schema.size() || !name || !type || !bits) return NBG_E_INVALID_ARGUMENT;
+  *name = r->schema[c].first.c_str();
+  *type = r->schema[c].second;
+  *bits = r->bits[c];
+  return NBG_OK;
+}
+int32_t nbg_stats_data(const nbg_stats_response* r, const uint8_t** data, uint64_t* len) {
+  if (!r || !data || !len) return NBG_E_INVALID_ARGUMENT;
+  *data = reinterpret_cast<const uint8_t*>(r->data.data());
+  *len = r->data.size();
+  return NBG_OK;
+}
+void nbg_stats_free(nbg_stats_response* r) { delete r; }
 
 int32_t nbg_gn_num_failed(const nbg_gn_response* r) { return r ? (int32_t)r->failed.size() : -1; }
 int32_t nbg_gn_failed(const nbg_gn_response* r, int32_t i, int32_t* code, int32_t* part) {

@@ -298,6 +298,33 @@ class Engine:
             self.lib.nbg_paths_free(out)
 
 
+    # ------------------------------------------------------------------ boundStats (storage)
+    def bound_stats(self, part_vids, edge_types, filter=b"", returns=(), stats=()):
+        """StorageServiceHandler::future_boundStats: (failed, [(name, type, bits)], data bytes)."""
+        keep = []
+        req = _gn_request(part_vids, edge_types, filter, returns, keep)
+        st = np.ascontiguousarray(stats, np.int32)
+        out = C.c_void_p()
+        self._check(self.lib.nbg_bound_stats(self.h, C.byref(req), st.ctypes.data_as(C.POINTER(C.c_int32)),
+                                             C.byref(out)), "bound_stats")
+        lib = self.lib
+        try:
+            code, part = C.c_int32(), C.c_int32()
+            failed = []
+            for i in range(lib.nbg_stats_num_failed(out)):
+                lib.nbg_stats_failed(out, i, C.byref(code), C.byref(part))
+                failed.append((code.value, part.value))
+            cols = []
+            name, typ, bits = C.c_char_p(), C.c_int32(), C.c_int64()
+            for c in range(lib.nbg_stats_num_cols(out)):
+                lib.nbg_stats_col(out, c, C.byref(name), C.byref(typ), C.byref(bits))
+                cols.append((name.value.decode(), typ.value, bits.value))
+            ptr, ln = C.POINTER(C.c_uint8)(), C.c_uint64()
+            lib.nbg_stats_data(out, C.byref(ptr), C.byref(ln))
+            return sorted(failed), cols, C.string_at(ptr, ln.value)
+        finally:
+            lib.nbg_stats_free(out)
+
     # ------------------------------------------------------------------ GetNeighbors (storage)
     def get_neighbors(self, part_vids, edge_types, filter=b"", returns=()):
         """StorageServiceHandler::future_getBound: ``part_vids`` = [(part, vid), ...], ``returns`` =
@@ -350,6 +377,20 @@ class Engine:
             return gn_canonical(failed, schemas[0], schemas[1], verts)
         finally:
             lib.nbg_gn_free(out)
+
+
+def _gn_request(part_vids, edge_types, filter, returns, keep):
+    parts = np.ascontiguousarray([p for p, _ in part_vids], np.int32)
+    vids = np.ascontiguousarray([v for _, v in part_vids], np.int64)
+    et = np.ascontiguousarray(edge_types, np.int32)
+    rets = (L.nbg_prop_def * max(1, len(returns)))(*[L.nbg_prop_def(o, i, n.encode()) for o, i, n in returns])
+    fb = (C.c_uint8 * max(1, len(filter))).from_buffer_copy(filter or b"\0")
+    keep.extend([parts, vids, et, rets, fb])
+    return L.nbg_gn_request(
+        parts.ctypes.data_as(C.POINTER(C.c_int32)) if len(parts) else None,
+        vids.ctypes.data_as(C.POINTER(C.c_int64)) if len(vids) else None, len(vids),
+        et.ctypes.data_as(C.POINTER(C.c_int32)) if len(et) else None, len(et),
+        C.cast(fb, C.POINTER(C.c_uint8)) if filter else None, len(filter), rets, len(returns))
 
 
 def gn_canonical(failed, vschema, eschema, vertices):

@@ -2,6 +2,7 @@
 // cpu_baseline leg.  Not linked by the product.
 #include <algorithm>
 #include <chrono>
+#include <cstring>
 #include "orc.h"
 
 using namespace orc;
@@ -243,5 +244,39 @@ int32_t orc_gn_vertex_item(void* r, int64_t i, int32_t edges, int32_t k, const u
   return v.tags[k].tag;
 }
 void orc_gn_free(void* r) { delete static_cast<OrcGN*>(r); }
+
+// ---- boundStats (QueryStatsProcessor restated)
+void* orc_bound_stats(void* h, const int32_t* parts, const int64_t* vids, uint64_t n, const int32_t* etypes,
+                      int32_t ne, const uint8_t* filter, uint32_t flen, const int32_t* owners, const int32_t* ids,
+                      const char* const* names, const int32_t* stats, int32_t nret) {
+  const Store& st = *static_cast<Store*>(h);
+  GNRequest req;
+  for (uint64_t i = 0; i < n; ++i) req.parts[parts[i]].push_back(vids[i]);
+  req.edgeTypes.assign(etypes, etypes + ne);
+  if (filter && flen) req.filter.assign(reinterpret_cast<const char*>(filter), flen);
+  for (int32_t i = 0; i < nret; ++i) req.returns.push_back(PropDef{owners[i], ids[i], names[i], stats[i]});
+  return new StatsResult(boundStats(st, req));
+}
+int32_t orc_stats_num_failed(void* r) { return (int32_t)static_cast<StatsResult*>(r)->failed.size(); }
+void orc_stats_failed(void* r, int32_t i, int32_t* code, int32_t* part) {
+  auto& f = static_cast<StatsResult*>(r)->failed[i];
+  *code = f.first;
+  *part = f.second;
+}
+int32_t orc_stats_num_cols(void* r) { return (int32_t)static_cast<StatsResult*>(r)->schema.cols.size(); }
+void orc_stats_col(void* r, int32_t c, const char** name, int32_t* type, int64_t* bits) {
+  auto* s = static_cast<StatsResult*>(r);
+  *name = s->schema.cols[c].name.c_str();
+  *type = s->schema.cols[c].type;
+  const Value& v = s->values[c];
+  if (v.index() == 1) { double d = std::get<1>(v); memcpy(bits, &d, 8); }
+  else *bits = std::get<0>(v);
+}
+void orc_stats_data(void* r, const uint8_t** data, uint64_t* len) {
+  auto* s = static_cast<StatsResult*>(r);
+  *data = reinterpret_cast<const uint8_t*>(s->data.data());
+  *len = s->data.size();
+}
+void orc_stats_free(void* r) { delete static_cast<StatsResult*>(r); }
 
 }  // extern "C"

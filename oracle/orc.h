@@ -216,7 +216,9 @@ struct Store {
 };
 
 // ---------------------------------------------------------------- getBound (K3-K8)
-struct PropDef { int32_t owner; int32_t id; std::string name; };   // owner 1 SRC 2 DST 3 EDGE
+struct PropDef {   // owner 1 SRC 2 DST 3 EDGE; stat 0 none, 1 SUM, 2 COUNT, 3 AVG
+  int32_t owner; int32_t id; std::string name; int32_t stat = 0;
+};
 struct GNRequest {
   std::unordered_map<int32_t, std::vector<int64_t>> parts;
   std::vector<int32_t> edgeTypes;
@@ -235,6 +237,14 @@ struct QueryResponse {
 QueryResponse getBound(const Store& st, const GNRequest& req);
 // QueryVertexPropsProcessor (src/storage/QueryVertexPropsProcessor.cpp:14-27)
 QueryResponse getVertexProps(const Store& st, const GNRequest& req);
+// QueryStatsProcessor (src/storage/QueryStatsProcessor.cpp:16-130): one row of SUM/COUNT/AVG
+struct StatsResult {
+  std::vector<std::pair<int32_t, int32_t>> failed;
+  Schema schema;
+  std::vector<Value> values;
+  std::string data;
+};
+StatsResult boundStats(const Store& st, const GNRequest& req);
 // StorageClient::getNeighbors: group vids by part and issue one request (one host).
 QueryResponse getNeighbors(const Store& st, const std::vector<int64_t>& vids,
                            const std::vector<int32_t>& etypes, const std::string& filter,

@@ -65,6 +65,12 @@ struct PropCtx {
   int pik = 0;            // 0 none, 1 src, 2 dst, 3 type, 4 rank
   bool returned = false;
   bool filtered = false;  // from a $^ filter
+  int retIndex = -1;
+  // StatsCollector state (Collector.h:76-109); the reference's sum_ starts as int64 0 and a
+  // double value would hit boost::bad_get — restated here as a double sum
+  int64_t isum = 0;
+  double dsum = 0;
+  int32_t count = 0;
   std::string tagName;
 };
 struct TagCtx { int32_t tag; std::vector<PropCtx> props; std::vector<std::string> filterNames; };
@@ -78,6 +84,22 @@ struct Processor {
   std::vector<std::pair<int32_t, std::vector<PropCtx>>> edgeCtx;
   std::unique_ptr<Expr> exp;
   std::mutex lock;
+  bool stats = false;     // QueryStatsProcessor: collect into the PropCtx accumulators
+  int retIndex = 0;
+  // QueryBaseProcessor::validOperation (QueryBaseProcessor.inl:18-35)
+  static bool validOp(SType t, int32_t stat) {
+    if (stat != 1 && stat != 3) return true;
+    return t == ST_INT || t == ST_VID || t == ST_TIMESTAMP || t == ST_FLOAT || t == ST_DOUBLE;
+  }
+  static void statCollect(const PropCtx& p, const Value& v) {
+    auto& q = const_cast<PropCtx&>(p);
+    switch (v.index()) {
+      case 0: q.isum += std::get<0>(v); break;
+      case 1: q.dsum += std::get<1>(v); break;
+      default: break;
+    }
+    q.count++;
+  }
 
   explicit Processor(const Store& s) : st(s) {}
 
@@ -140,7 +162,8 @@ struct Processor {
         if (!s) return E_TAG_PROP_NOT_FOUND;
         SType ft = s->typeOf(col.name);
         if (ft == ST_UNKNOWN) return E_IMPROPER_DATA_TYPE;
-        pc.type = ft; pc.prop = col; pc.returned = true;
+        if (!validOp(ft, col.stat)) return E_IMPROPER_DATA_TYPE;
+        pc.type = ft; pc.prop = col; pc.returned = true; pc.retIndex = retIndex++;
         bool found = false;
         for (auto& tc : tagCtx) if (tc.tag == col.id) { tc.props.push_back(pc); found = true; break; }
         if (!found) { TagCtx tc; tc.tag = col.id; tc.props.push_back(pc); tagCtx.push_back(std::move(tc)); }
@@ -158,7 +181,8 @@ struct Processor {
         } else {
           continue;   // "InBound has none props, skip it!"
         }
-        pc.prop = col; pc.returned = true;
+        if (!validOp(pc.type, col.stat)) return E_IMPROPER_DATA_TYPE;
+        pc.prop = col; pc.returned = true; pc.retIndex = retIndex++;
         auto* v = edgeProps(et);
         if (!v) { edgeCtx.emplace_back(et, std::vector<PropCtx>{pc}); }
         else v->push_back(pc);
@@ -177,6 +201,14 @@ struct Processor {
   void collectProps(RowReader* reader, const char* key, const std::vector<PropCtx>& props,
                     TagFilters* tf, RowWriter& w) {
     for (const auto& p : props) {
+      if (stats) {   // StatsCollector: collectVid does nothing; _type/_rank collectInt64
+        switch (p.pik) {
+          case 1: case 2: continue;
+          case 3: statCollect(p, Value((int64_t)keyType(key))); continue;
+          case 4: statCollect(p, Value(keyRank(key))); continue;
+          default: break;
+        }
+      }
       switch (p.pik) {
         case 1: w.putVid(keySrc(key)); continue;
         case 2: w.putVid(keyDst(key)); continue;
@@ -188,6 +220,7 @@ struct Processor {
       auto v = reader->get(p.prop.name);
       if (!v.ok()) continue;   // "Skip the bad value"
       if (p.filtered && tf) (*tf)[{p.tagName, p.prop.name}] = v.v;
+      if (p.returned && stats) { statCollect(p, v.v); continue; }
       if (p.returned) {
         switch (v.v.index()) {
           case 0: w.putInt(std::get<0>(v.v)); break;
@@ -370,6 +403,74 @@ QueryResponse process(const Store& st, const GNRequest& req, bool onlyVertexProp
 QueryResponse getBound(const Store& st, const GNRequest& req) { return process(st, req, false); }
 
 QueryResponse getVertexProps(const Store& st, const GNRequest& req) { return process(st, req, true); }
+
+// QueryStatsProcessor::processVertex / onProcessFinished / calcResult
+// (src/storage/QueryStatsProcessor.cpp:16-130): tag props of every requested vertex, edge props
+// of every accepted edge, one row in retIndex order.
+StatsResult boundStats(const Store& st, const GNRequest& req) {
+  StatsResult res;
+  Processor proc(st);
+  proc.stats = true;
+  std::vector<int32_t> partOrder;
+  for (auto& p : req.parts) partOrder.push_back(p.first);
+  std::sort(partOrder.begin(), partOrder.end());
+  int32_t rc = proc.build(req);
+  if (rc != E_SUCCEEDED) {
+    for (auto p : partOrder) res.failed.emplace_back(rc, p);
+    return res;
+  }
+  std::unordered_set<int32_t> failedParts;
+  for (auto part : partOrder) {
+    for (auto vid : req.parts.at(part)) {
+      if (part < 1 || part > st.numParts) {
+        if (failedParts.insert(part).second) res.failed.emplace_back(E_PART_NOT_FOUND, part);
+        continue;
+      }
+      TagFilters tf;
+      bool missing = false;   // QueryStatsProcessor::processVertex returns the tag's failure
+      for (auto& tc : proc.tagCtx) {
+        RowWriter w(nullptr);
+        if (proc.collectVertexProps(part, vid, tc.tag, tc.props, &tf, w) != E_SUCCEEDED) { missing = true; break; }
+      }
+      if (missing) {   // ERR_KEY_NOT_FOUND -> E_UNKNOWN (BaseProcessor.inl:14-29), first per part
+        if (failedParts.insert(part).second) res.failed.emplace_back(E_UNKNOWN, part);
+        continue;
+      }
+      for (auto& ec : proc.edgeCtx) {
+        if (ec.second.empty()) continue;
+        std::string rs;
+        proc.collectEdgeProps(part, vid, ec.first, ec.second, &tf, rs);
+      }
+    }
+  }
+  std::vector<const PropCtx*> props;
+  for (auto& tc : proc.tagCtx)
+    for (auto& p : tc.props) if (p.returned) props.push_back(&p);
+  for (auto& ec : proc.edgeCtx)
+    for (auto& p : ec.second) props.push_back(&p);
+  std::sort(props.begin(), props.end(), [](const PropCtx* a, const PropCtx* b) { return a->retIndex < b->retIndex; });
+  RowWriter w(nullptr);
+  for (auto* p : props) {
+    const bool dbl = p->type == ST_DOUBLE || p->type == ST_FLOAT;
+    switch (p->prop.stat) {
+      case 1:
+        if (dbl) { w.putDouble(p->dsum); res.schema.cols.push_back({p->prop.name, ST_DOUBLE}); res.values.push_back(p->dsum); }
+        else { w.putInt(p->isum); res.schema.cols.push_back({p->prop.name, ST_INT}); res.values.push_back(p->isum); }
+        break;
+      case 2:
+        w.putInt(p->count); res.schema.cols.push_back({p->prop.name, ST_INT}); res.values.push_back((int64_t)p->count);
+        break;
+      case 3: {
+        const double v = dbl ? p->dsum / p->count : static_cast<double>(p->isum) / p->count;
+        w.putDouble(v); res.schema.cols.push_back({p->prop.name, ST_DOUBLE}); res.values.push_back(v);
+        break;
+      }
+      default: break;
+    }
+  }
+  res.data = w.encode();
+  return res;
+}
 
 QueryResponse getNeighbors(const Store& st, const std::vector<int64_t>& vids,
                            const std::vector<int32_t>& etypes, const std::string& filter,

@@ -65,6 +65,14 @@ def lib():
         L.orc_gn_vertex_count.argtypes = [vp, i64, i32]
         L.orc_gn_vertex_item.argtypes = [vp, i64, i32, i32, P(P(C.c_uint8)), P(u64)]
         L.orc_gn_free.argtypes = [vp]
+        L.orc_bound_stats.restype = vp
+        L.orc_bound_stats.argtypes = [vp, vp, vp, u64, vp, i32, vp, u32, vp, vp, vp, vp, i32]
+        L.orc_stats_num_failed.argtypes = [vp]
+        L.orc_stats_failed.argtypes = [vp, i32, P(i32), P(i32)]
+        L.orc_stats_num_cols.argtypes = [vp]
+        L.orc_stats_col.argtypes = [vp, i32, P(C.c_char_p), P(i32), P(i64)]
+        L.orc_stats_data.argtypes = [vp, P(P(C.c_uint8)), P(u64)]
+        L.orc_stats_free.argtypes = [vp]
         _lib = L
     return _lib
 
@@ -231,6 +239,36 @@ class Oracle:
             return gn_canonical(failed, schemas[0], schemas[1], verts)
         finally:
             L.orc_gn_free(r)
+
+    def bound_stats(self, part_vids, edge_types, filter=b"", returns=(), stats=()):
+        """QueryStatsProcessor restated: (failed, [(name, type, bits)], data bytes)."""
+        L = self.L
+        parts = np.asarray([p for p, _ in part_vids], np.int32)
+        vids = np.asarray([v for _, v in part_vids], np.int64)
+        et = np.asarray(edge_types, np.int32)
+        owners = np.asarray([o for o, _, _ in returns], np.int32)
+        ids = np.asarray([i for _, i, _ in returns], np.int32)
+        st = np.asarray(stats, np.int32)
+        names = (C.c_char_p * max(1, len(returns)))(*[n.encode() for _, _, n in returns])
+        fb = np.frombuffer(filter, np.uint8) if filter else None
+        r = L.orc_bound_stats(self.h, _ptr(parts), _ptr(vids), len(vids), _ptr(et), len(et), _ptr(fb), len(filter),
+                              _ptr(owners), _ptr(ids), names, _ptr(st), len(returns))
+        try:
+            code, part = C.c_int32(), C.c_int32()
+            failed = []
+            for i in range(L.orc_stats_num_failed(r)):
+                L.orc_stats_failed(r, i, C.byref(code), C.byref(part))
+                failed.append((code.value, part.value))
+            cols = []
+            name, typ, bits = C.c_char_p(), C.c_int32(), C.c_int64()
+            for c in range(L.orc_stats_num_cols(r)):
+                L.orc_stats_col(r, c, C.byref(name), C.byref(typ), C.byref(bits))
+                cols.append((name.value.decode(), typ.value, bits.value))
+            ptr, ln = C.POINTER(C.c_uint8)(), C.c_uint64()
+            L.orc_stats_data(r, C.byref(ptr), C.byref(ln))
+            return sorted(failed), cols, C.string_at(ptr, ln.value)
+        finally:
+            L.orc_stats_free(r)
 
     def go_timed(self, starts, etypes, steps, where=b""):
         s = np.asarray(starts, np.int64)

@@ -115,3 +115,44 @@ def test_nba_get_neighbors(nba_data):
     finally:
         eng.close()
         orc.close()
+
+
+# ---------------------------------------------------------------------------- boundStats
+SUM, COUNT, AVG = 1, 2, 3
+STAT_CASES = {
+    "edge_props": ([ET, EF], b"", [(EDGE, ET, "w"), (EDGE, ET, "w"), (EDGE, ET, "w"), (EDGE, EF, "k"),
+                                   (EDGE, EF, "_rank"), (EDGE, ET, "_type"), (EDGE, ET, "_dst")],
+                   [SUM, COUNT, AVG, AVG, SUM, SUM, COUNT]),
+    "tag_props": ([ET], b"", [(SRC, TP, "age"), (SRC, TP, "score"), (SRC, TP, "score"), (SRC, TP, "name"),
+                              (EDGE, ET, "w")], [SUM, SUM, AVG, COUNT, AVG]),
+    "filtered": ([ET, -ET], W50, [(EDGE, ET, "w"), (EDGE, -ET, "_rank"), (EDGE, ET, "_dst")], [SUM, COUNT, AVG]),
+    "string_sum_rejected": ([ET], b"", [(SRC, TP, "name")], [SUM]),
+}
+
+
+@pytest.mark.parametrize("name", list(STAT_CASES))
+def test_bound_stats_parity(tg, name):
+    """QueryStatsProcessor: one row of SUM/COUNT/AVG, byte-exact, vs the oracle restatement."""
+    src, persons, eng, orc = tg
+    types, filt, rets, stats = STAT_CASES[name]
+    ps = set(persons)
+    vids = [v for v in graphs.roots(src, 64, seed=len(name)) if v in ps][:20]
+    got = eng.bound_stats(pv(vids), types, filt, rets, stats)
+    exp = orc.bound_stats(pv(vids), types, filt, rets, stats)
+    assert got == exp
+    if name == "string_sum_rejected":
+        assert exp[0] and all(c == -23 for c, _ in exp[0])
+    else:
+        assert not exp[0] and exp[1]
+
+
+def test_bound_stats_missing_tag_fails_vertex(tg):
+    """A requested vertex without the requested tag fails its part (E_UNKNOWN) and adds nothing."""
+    src, persons, eng, orc = tg
+    ps = set(persons)
+    vids = graphs.roots(src, 40, seed=4)
+    assert any(v not in ps for v in vids)
+    rets, stats = [(SRC, TP, "age"), (EDGE, ET, "w")], [SUM, SUM]
+    got = eng.bound_stats(pv(vids), [ET], b"", rets, stats)
+    exp = orc.bound_stats(pv(vids), [ET], b"", rets, stats)
+    assert got == exp and exp[0]
