@@ -121,8 +121,9 @@ def main():
     stmt = eng.prepare_go([1], args.go_steps, where)
 
     # queries in flight (nbg_go_submit query slots: concurrent queries, each on its own stream
-    # and workspace); a partitioned engine runs its collective queries one at a time
-    inflight = 0 if (world > 1 or args.sync) else int(os.environ.get("NBG_QUERY_SLOTS", "6"))
+    # and workspace; on a partitioned engine the slots share one stream, so each rank's
+    # collectives stay in submission order)
+    inflight = 0 if args.sync else int(os.environ.get("NBG_QUERY_SLOTS", "6"))
 
     def one_step_sync():
         scanned = rows = 0

@@ -162,8 +162,9 @@ void nbg_go_stmt_free(nbg_go_stmt* stmt);
  * (and every older one), returns its rows with nbg_go_execute's semantics and frees the ticket.
  * Device rows (device != 0) stay valid until the slot's next query, i.e. until NBG_QUERY_SLOTS
  * further submissions.  A ticket never waited for is reclaimed by nbg_destroy; tickets must be
- * waited for before their statement is freed.  Not available on partitioned engines (queries
- * there are collectives). */
+ * waited for before their statement is freed.  On a partitioned engine every rank must submit
+ * the same queries in the same order (they are collectives); its slots share the engine's stream
+ * and communicator, so the device runs them in that order while the host work overlaps. */
 typedef struct nbg_go_ticket nbg_go_ticket;
 int32_t nbg_go_submit(nbg_go_stmt* stmt, const int64_t* starts, uint64_t num_starts, int32_t device,
                       nbg_go_ticket** out);

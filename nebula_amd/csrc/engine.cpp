@@ -635,7 +635,6 @@ int32_t nbg_go_submit(nbg_go_stmt* st, const int64_t* starts, uint64_t num_start
   Engine& E = *st->eng;
   std::lock_guard<std::mutex> lg(E.mu);
   *out = nullptr;
-  if (E.partitioned()) return E.fail(NBG_E_UNSUPPORTED, "asynchronous GO on a partitioned engine (queries are collectives)");
   if (hipSetDevice(E.cfg.device) != hipSuccess) return E.fail(NBG_E_DEVICE, "hipSetDevice failed");
   if (E.slots.empty()) E.slots.resize(query_slots());
   int slot = -1;
@@ -647,17 +646,23 @@ int32_t nbg_go_submit(nbg_go_stmt* st, const int64_t* starts, uint64_t num_start
     slot = s0;
   }
   Engine::QuerySlot& q = E.slots[slot];
-  if (!q.stream && hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking) != hipSuccess)
+  // a partitioned engine's queries are collectives: its slots share the engine's stream (and
+  // communicator), so every rank's collectives stay in submission order — the host work of one
+  // query overlaps the device work of the next, the device runs them one after another
+  const hipStream_t qs = E.partitioned() ? E.stream : q.stream;
+  if (!E.partitioned() && !q.stream && hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking) != hipSuccess)
     return E.fail(NBG_E_DEVICE, "hipStreamCreate failed");
   if (!q.ws) {
     std::string err;
-    q.ws = ws_create(E.snap.nv + 1024, E.snap.nv, E.snap.max_edges(), q.stream, &err);
+    q.ws = ws_create(E.snap.nv + 1024, E.snap.nv, E.snap.max_edges(), E.partitioned() ? E.stream : q.stream, &err);
     if (!q.ws) return E.fail(NBG_E_OUT_OF_MEMORY, err);
+    if (E.partitioned() && ws_set_partition(q.ws, E.comm.get(), E.npad) != hipSuccess)
+      return E.fail(NBG_E_OUT_OF_MEMORY, "partition buffers");
   }
   auto* t = new nbg_go_ticket();
   t->st = st;
   t->slot = slot;
-  int32_t rc = go_launch(E, st, starts, num_starts, device != 0, &q.ws, q.stream, &t->p);
+  int32_t rc = go_launch(E, st, starts, num_starts, device != 0, &q.ws, qs, &t->p);
   if (rc) { delete t; return rc; }
   q.ticket = t;
   E.inflight.push_back(t);

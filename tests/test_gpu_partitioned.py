@@ -204,3 +204,36 @@ def _dst_of(src):
     if "d" not in _DST:
         _DST["d"] = graphs.rmat_graph(11)[1]
     return _DST["d"]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_partitioned_async_slots(rmat11, world):
+    """nbg_go_submit on a partitioned engine: more queries than slots in flight per rank (the
+    slots share the rank's stream, so the collectives stay in submission order); the union of
+    the ranks' rows equals the single engine's for every query."""
+    src, single, orc, clusters = rmat11
+    c = clusters[world]
+    wb = WHERES["w<50"].encode()
+    roots = graphs.roots(src, 9, seed=13)
+
+    def run(e):
+        stmt = e.prepare_go([graphs.E_TYPE], 3, wb)
+        try:
+            tickets = [stmt.submit([r], device=False) for r in roots]
+            out = []
+            for t in tickets:
+                res = stmt.wait(t)
+                out.append((res.fetch(), res.edges_scanned))
+                res.free()
+            return out
+        finally:
+            stmt.free()
+
+    per_rank = c.each(run)
+    for i, r in enumerate(roots):
+        rows = []
+        for rk in per_rank:
+            rows += rk[i][0]
+        exp = single.go([r], [graphs.E_TYPE], 3, wb)
+        assert graphs.sorted_rows(rows) == graphs.sorted_rows(exp), r
+        assert all(rk[i][1] == per_rank[0][i][1] for rk in per_rank)
