@@ -136,6 +136,18 @@ typedef struct {
   const uint32_t* yield_lens;     /*   (<edge>._dst per OVER edge, parser.yy:518-531)          */
   int32_t num_yields;
   int32_t distinct;               /* YIELD DISTINCT                                            */
+  /* Piped / variable input for $-.col / $var.col in WHERE / YIELD: the rows the FROM $-.col or
+   * $var.col came from, as columns.  GoExecutor::setupStarts indexes them by the FROM column
+   * (input_vid_col; the last row of a vid wins, InterimResult.cpp:158-250) and a final-step row
+   * reads the row of its source's root (VertexBackTracker, GoExecutor.h:169-188).  Column c holds
+   * num_input_rows int64 payloads (int, double bits, bool 0/1) or, when input_kinds[c] is
+   * NBG_V_STRING, a const char* const* of row strings.  num_input_cols = 0: no input. */
+  int32_t num_input_cols;
+  const char* const* input_names;
+  const uint8_t* input_kinds;
+  const void* const* input_cols;
+  uint64_t num_input_rows;
+  int32_t input_vid_col;
 } nbg_go_request;
 
 /* Rows are copied to host memory. */

@@ -52,7 +52,9 @@ class nbg_kernel_stat(C.Structure):
 class nbg_go_request(C.Structure):
     _fields_ = [("starts", P(i64)), ("num_starts", u64), ("edge_types", P(i32)), ("num_edge_types", i32),
                 ("over_all", i32), ("steps", u32), ("where", P(u8)), ("where_len", u32),
-                ("yields", P(P(u8))), ("yield_lens", P(u32)), ("num_yields", i32), ("distinct", i32)]
+                ("yields", P(P(u8))), ("yield_lens", P(u32)), ("num_yields", i32), ("distinct", i32),
+                ("num_input_cols", i32), ("input_names", P(C.c_char_p)), ("input_kinds", P(u8)),
+                ("input_cols", P(vp)), ("num_input_rows", u64), ("input_vid_col", i32)]
 
 
 class nbg_path_request(C.Structure):

@@ -138,7 +138,29 @@ struct nbg_go_stmt {
   std::string deferred_msg;
   std::string dst_unknown;           // a $$ tag name is unknown: fails once the final step has edges
   bool distinct = false;             // YIELD DISTINCT: distinct starts and rows
+  // $- / $var input: index rows (dense id of the FROM vid, ascending; last row per vid) and
+  // their columns, uploaded on first execution
+  bool uses_input = false;
+  std::vector<uint32_t> in_ids;
+  std::vector<std::vector<int64_t>> in_cols;
+  uint32_t* d_in_ids = nullptr;
+  int64_t** d_in_cols = nullptr;
+  std::vector<int64_t*> d_in_col_ptrs;
+  ~nbg_go_stmt() {
+    if (d_in_ids) (void)hipFree(d_in_ids);
+    for (auto* p : d_in_col_ptrs)
+      if (p) (void)hipFree(p);
+    if (d_in_cols) (void)hipFree(d_in_cols);
+  }
 };
+
+static bool has_input_prop(const Node* n) {
+  if (!n) return false;
+  if (n->kind == EK_INPUT || n->kind == EK_VAR) return true;
+  for (auto& k : n->kids)
+    if (has_input_prop(k.get())) return true;
+  return false;
+}
 
 // Props a query names on each edge alias (Expression::prepare's alias set, Expressions.cpp:314-400)
 static void alias_props(const Node* n, std::map<std::string, std::set<std::string>>& out) {
@@ -195,6 +217,52 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
   }
   if ((int)yields.size() > MAX_YIELDS) return E.fail(NBG_E_UNSUPPORTED, "too many YIELD columns");
   const int ncols = (int)yields.size();
+  // $- / $var input: the index GoExecutor::setupStarts builds on the FROM column
+  bool uses_input = has_input_prop(where.get());
+  for (auto& y : yields) uses_input = uses_input || has_input_prop(y.get());
+  std::vector<std::string> in_names;
+  std::vector<VKind> in_kinds;
+  std::vector<uint32_t> in_ids;
+  std::vector<std::vector<int64_t>> in_cols;
+  if (uses_input && rq->num_input_cols > 0) {
+    if (E.partitioned()) return E.fail(NBG_E_UNSUPPORTED, "$- / $var props on a partitioned engine");
+    if (rq->num_input_cols > MAX_INPUT_COLS || !rq->input_names || !rq->input_kinds || !rq->input_cols ||
+        rq->input_vid_col < 0 || rq->input_vid_col >= rq->num_input_cols)
+      return E.fail(NBG_E_INVALID_ARGUMENT, "input table");
+    const uint64_t n = rq->num_input_rows;
+    for (int32_t c = 0; c < rq->num_input_cols; ++c) {
+      in_names.emplace_back(rq->input_names[c] ? rq->input_names[c] : "");
+      in_kinds.push_back((VKind)rq->input_kinds[c]);
+    }
+    const int64_t* vidc = static_cast<const int64_t*>(rq->input_cols[rq->input_vid_col]);
+    std::vector<std::pair<uint32_t, uint64_t>> rowof;   // (dense id, last row)
+    {
+      std::unordered_map<int64_t, uint64_t> last;
+      for (uint64_t r = 0; r < n; ++r) last[vidc[r]] = r;   // vidToRowIndex_[v] = row: the last wins
+      for (auto& kv : last) {
+        const uint32_t d = E.dense(kv.first);
+        if (d != NO_ROW) rowof.emplace_back(d, kv.second);
+      }
+      std::sort(rowof.begin(), rowof.end());
+    }
+    in_cols.assign(rq->num_input_cols, std::vector<int64_t>(rowof.size()));
+    for (auto& pr : rowof) in_ids.push_back(pr.first);
+    for (int32_t c = 0; c < rq->num_input_cols; ++c) {
+      for (size_t k = 0; k < rowof.size(); ++k) {
+        const uint64_t r = rowof[k].second;
+        if (in_kinds[c] == VK_STRING) {
+          const char* str = static_cast<const char* const*>(rq->input_cols[c])[r];
+          const int64_t code = string_code(E.snap.strings, str ? str : "");
+          if (code & 1) return E.fail(NBG_E_UNSUPPORTED, "an input string absent from the snapshot's dictionary");
+          in_cols[c][k] = code;
+        } else {
+          in_cols[c][k] = static_cast<const int64_t*>(rq->input_cols[c])[r];
+        }
+      }
+    }
+  } else if (uses_input) {
+    return E.fail(NBG_E_EXECUTION_ERROR, "$- / $var props need the piped or variable input");
+  }
   // compile per OVER type; name-resolution errors are reported only if the final step runs
   std::map<int32_t, TypeProgram> progs;
   int32_t deferred = NBG_OK;
@@ -224,6 +292,10 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
     env.partitioned = E.partitioned();
     env.dst_unknown = &dst_unknown;
     env.probe_mask = &probe;
+    if (uses_input) {
+      env.input_names = &in_names;
+      env.input_kinds = &in_kinds;
+    }
     ProgramBuilder pb;
     TypeProgram tp;
     tp.etype = t;
@@ -302,6 +374,9 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
   st->deferred_msg = deferred_msg;
   st->dst_unknown = dst_unknown;
   st->distinct = rq->distinct != 0;
+  st->uses_input = uses_input;
+  st->in_ids = std::move(in_ids);
+  st->in_cols = std::move(in_cols);
   *out = st;
   return NBG_OK;
 }
@@ -359,6 +434,29 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
   Workspace* ws = *wsp;
   p->ws = ws;
   rows->ws = ws;
+  uint32_t* bt = nullptr;   // VertexBackTracker roots, when $- / $var props are read after >= 2 steps
+  if (st->uses_input) {
+    auto* ms = const_cast<nbg_go_stmt*>(st);
+    if (!ms->d_in_ids) {
+      const size_t n = std::max<size_t>(ms->in_ids.size(), 1);
+      bool ok = hipMalloc((void**)&ms->d_in_ids, n * 4) == hipSuccess &&
+                hipMemcpy(ms->d_in_ids, ms->in_ids.data(), ms->in_ids.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
+      ms->d_in_col_ptrs.assign(ms->in_cols.size(), nullptr);
+      for (size_t c = 0; ok && c < ms->in_cols.size(); ++c)
+        ok = hipMalloc((void**)&ms->d_in_col_ptrs[c], n * 8) == hipSuccess &&
+             hipMemcpy(ms->d_in_col_ptrs[c], ms->in_cols[c].data(), ms->in_cols[c].size() * 8, hipMemcpyHostToDevice) ==
+                 hipSuccess;
+      ok = ok && hipMalloc((void**)&ms->d_in_cols, std::max<size_t>(ms->in_cols.size(), 1) * 8) == hipSuccess &&
+           hipMemcpy(ms->d_in_cols, ms->d_in_col_ptrs.data(), ms->in_cols.size() * 8, hipMemcpyHostToDevice) ==
+               hipSuccess;
+      if (!ok) { delete rows; p->rows = nullptr; return E.fail(NBG_E_OUT_OF_MEMORY, "input index upload"); }
+    }
+    if (steps > 1 && !(bt = ws_backtracker(ws))) {
+      delete rows;
+      p->rows = nullptr;
+      return E.fail(NBG_E_OUT_OF_MEMORY, "backtracker");
+    }
+  }
   const uint32_t cap = (uint32_t)(E.cfg.max_edge_returned_per_vertex <= 0 ? 0x7fffffff
                                                                           : E.cfg.max_edge_returned_per_vertex);
   auto args_for = [&](const DevEdgeType& dt) {
@@ -378,6 +476,12 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
     a.tcols = E.snap.d_tcols;
     a.tpres = E.snap.d_tpres;
     a.gbase = E.partitioned() ? (uint32_t)((uint64_t)E.cfg.rank * E.npad) : 0u;
+    a.bt = bt;
+    if (st->uses_input) {
+      a.in_ids = st->d_in_ids;
+      a.in_n = st->in_ids.size();
+      a.in_cols = st->d_in_cols;
+    }
     return a;
   };
   // the start list keeps duplicates, so its edge space is the one frontier not bounded by E:
@@ -446,6 +550,7 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
       auto it = E.snap.types.find(over[i]);
       if (it == E.snap.types.end()) continue;
       ExpandArgs a = args_for(it->second);
+      a.bt_first = s == 1;
       if (!final) {
         he = ws_expand_mark(ws, a, n_bound, it->second.num_edges, (int)s, (int)i, inl_of(i, s));
       } else if (deferred || (plist[i].where_const && !plist[i].where_const_val)) {

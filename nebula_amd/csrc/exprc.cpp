@@ -512,7 +512,26 @@ struct Ctx {
       }
       case EK_SRCPROP: return leaf_src_tag(e, out);
       case EK_DSTPROP: return leaf_dst_tag(e, out);
-      case EK_INPUT: case EK_VAR: *err = "input/variable props are not supported"; return NBG_E_UNSUPPORTED;
+      case EK_INPUT: case EK_VAR: {
+        // GoExecutor getInputProp / getVariableProp -> InterimResultIndex::getColumnWithVID
+        // (GoExecutor.cpp:932-945, InterimResult.cpp:252-270): the column of the root's input row
+        if (!env.input_names) {
+          *err = "input/variable props without an input";
+          return NBG_E_EXECUTION_ERROR;
+        }
+        auto it = std::find(env.input_names->begin(), env.input_names->end(), e.prop);
+        if (it == env.input_names->end()) {   // "Prop `x' not found": an evaluation error
+          *out = make_error();
+          return NBG_OK;
+        }
+        const int col = (int)(it - env.input_names->begin());
+        Compiled c;
+        c.kind = (*env.input_kinds)[col];
+        c.reg = push();
+        emit(OP_INPUT, c.reg, 0, 0, col);
+        *out = c;
+        return NBG_OK;
+      }
       case EK_FUNC: *err = "function calls are not supported"; return NBG_E_UNSUPPORTED;
       case EK_UNARY: {
         Compiled a;

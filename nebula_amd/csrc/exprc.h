@@ -47,6 +47,9 @@ struct CompileEnv {
   // storage-side filter (QueryBaseProcessor.inl:580-606 getters): another edge's alias and the
   // key props `_src/_dst/_rank` read from the value row fail, $^ without the tag fails
   bool storage = false;
+  // $-.col / $var.col: the input rows' columns (names, kinds); nullptr: the query has no input
+  const std::vector<std::string>* input_names = nullptr;
+  const std::vector<VKind>* input_kinds = nullptr;
 };
 
 // Result of compiling one expression for one edge type.

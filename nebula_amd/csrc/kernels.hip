@@ -109,6 +109,7 @@ struct Workspace {
   uint64_t dseg_cap = 0;
   uint32_t* dcnt = nullptr;
   uint8_t* dkinds = nullptr;
+  uint32_t* bt = nullptr;         // VertexBackTracker roots [nv] (queries with $- / $var props)
   Ins* d_prog = nullptr;          // [MAX_TYPES_Q][MAX_PROGRAM]
   // FIND PATH (allocated on first use)
   PState* ps = nullptr;
@@ -394,6 +395,19 @@ __device__ __forceinline__ void run_program(const Ins* __restrict__ prog, int pc
         }
         break;
       case OP_EIDX: r = (int64_t)c.j; break;
+      case OP_INPUT:
+        if (active) {
+          const uint32_t root = a.bt ? a.bt[c.v] : c.v;   // getPropFromInterim (GoExecutor.cpp:1066-1075)
+          uint64_t lo = 0, hi = a.in_n;
+          while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (a.in_ids[mid] < root) lo = mid + 1;
+            else hi = mid;
+          }
+          if (lo < a.in_n && a.in_ids[lo] == root) r = a.in_cols[ins.aux][lo];
+          else err = true;
+        }
+        break;
       case OP_ADD_I: r = (int64_t)((uint64_t)x + (uint64_t)y); break;
       case OP_SUB_I: r = (int64_t)((uint64_t)x - (uint64_t)y); break;
       case OP_MUL_I: r = (int64_t)((uint64_t)x * (uint64_t)y); break;
@@ -446,7 +460,9 @@ __device__ __forceinline__ void run_program(const Ins* __restrict__ prog, int pc
 // FINALD: FINALF whose YIELDs are only _dst / constants; a tile's rows are stored after the NEXT
 // tile's loads are issued, so waiting for those loads never waits for this tile's stores (on
 // CDNA one counter, vmcnt, retires loads and stores in issue order)
-enum Mode { MARK = 0, FINAL = 1, BFS = 2, FINALF = 3, FINALD = 4 };
+// MARKB: MARK that also records each reached vertex's root (VertexBackTracker::add, last write
+// wins as in the reference's unordered iteration) for queries that read $- / $var props
+enum Mode { MARK = 0, FINAL = 1, BFS = 2, FINALF = 3, FINALD = 4, MARKB = 5 };
 
 // BFS-mode expansion (FIND SHORTEST PATH): every neighbour w is claimed at most once per epoch by
 // a CAS on its label (epoch << LVL_BITS | level); winners are appended, one atomic per tile on a
@@ -725,7 +741,20 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
     wave_lds_sync();
     NBG_PH(1)
 
-    if (M == MARK) {
+    if (M == MARKB) {
+#pragma unroll
+      for (int i = 0; i < VT; ++i) {
+        const int k = i * 64 + lane;
+        if (k < nb) {
+          const uint32_t s = sSeg[k];
+          const uint32_t u = a.col[(uint64_t)sRs[s] + (b0 + k - (uint64_t)sEnd[s])];
+          if (u == NO_ROW) continue;
+          const uint32_t src = list_id(a0 + s);
+          a.bt[u] = a.bt_first ? src : a.bt[src];
+          flags[u] = 1;
+        }
+      }
+    } else if (M == MARK) {
       uint32_t u[VT];   // all neighbour loads in flight before the flag stores
 #pragma unroll
       for (int i = 0; i < VT; ++i) {
@@ -1270,7 +1299,7 @@ void ws_destroy(Workspace* w) {
                   (void*)w->rlist, (void*)w->flags, (void*)w->tsplit,
                   (void*)w->q, (void*)w->rows,
                   (void*)w->d_row_cols, (void*)w->d_prog, (void*)w->dtab, (void*)w->dkeep, (void*)w->dseg,
-                  (void*)w->dcnt, (void*)w->dkinds})
+                  (void*)w->dcnt, (void*)w->dkinds, (void*)w->bt})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)w->h_q, (void*)w->h_starts, (void*)w->h_prog, (void*)w->h_ps, (void*)w->h_path,
                   (void*)w->h_stage})
@@ -1434,9 +1463,14 @@ hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, 
     a.frontier = nullptr;
     a.tsplit = nullptr;
     hipEvent_t p = prof_begin(w, K_EXPAND_MARK);
-    hipLaunchKernelGGL((k_expand<MARK, true>), dim3(expand_grid(il->n, il->total)), dim3(BLOCK), 0, w->stream, a,
-                       (const unsigned long long*)nullptr, w->seg_end, w->seg_rs, w->flags, FinalParams{},
-                       BfsParams{}, &w->q->e_st[step][tix], &w->q->step_n[step], *il);
+    if (a.bt)
+      hipLaunchKernelGGL((k_expand<MARKB, true>), dim3(expand_grid(il->n, il->total)), dim3(BLOCK), 0, w->stream, a,
+                         (const unsigned long long*)nullptr, w->seg_end, w->seg_rs, w->flags, FinalParams{},
+                         BfsParams{}, &w->q->e_st[step][tix], &w->q->step_n[step], *il);
+    else
+      hipLaunchKernelGGL((k_expand<MARK, true>), dim3(expand_grid(il->n, il->total)), dim3(BLOCK), 0, w->stream, a,
+                         (const unsigned long long*)nullptr, w->seg_end, w->seg_rs, w->flags, FinalParams{},
+                         BfsParams{}, &w->q->e_st[step][tix], &w->q->step_n[step], *il);
     prof_end(w, p, K_EXPAND_MARK, step, tix);
     return hipGetLastError();
   }
@@ -1446,8 +1480,12 @@ hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, 
   a.tsplit = w->tsplit;
   FinalParams fp{};
   hipEvent_t p = prof_begin(w, K_EXPAND_MARK);
-  hipLaunchKernelGGL(k_expand<MARK>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, L.acc,
-                     w->seg_end, w->seg_rs, w->flags, fp, BfsParams{}, &w->q->e_st[step][tix], L.stat_n, NoInline{});
+  if (a.bt)
+    hipLaunchKernelGGL(k_expand<MARKB>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, L.acc,
+                       w->seg_end, w->seg_rs, w->flags, fp, BfsParams{}, &w->q->e_st[step][tix], L.stat_n, NoInline{});
+  else
+    hipLaunchKernelGGL(k_expand<MARK>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, L.acc,
+                       w->seg_end, w->seg_rs, w->flags, fp, BfsParams{}, &w->q->e_st[step][tix], L.stat_n, NoInline{});
   prof_end(w, p, K_EXPAND_MARK, step, tix);
   return hipGetLastError();
 }
@@ -1677,6 +1715,11 @@ hipError_t ws_distinct(Workspace* w, const std::vector<std::array<uint64_t, 3>>&
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(counts->data(), w->dcnt, segs.size() * 4, hipMemcpyDeviceToHost, w->stream));
   return hipStreamSynchronize(w->stream);
+}
+
+uint32_t* ws_backtracker(Workspace* w) {
+  if (!w->bt && hipMalloc((void**)&w->bt, (w->nv + 1) * 4) != hipSuccess) w->bt = nullptr;
+  return w->bt;
 }
 
 // Scan-only expansion (final step whose WHERE folded to false still counts E_N).

@@ -143,6 +143,7 @@ enum Op : uint8_t {
   OP_TAGS_E,     // same, but a vertex without the tag is an evaluation error
   OP_TAGD,       // r[d] = $$ prop of the destination; imm (+ the tag's "default used" bit) when absent
   OP_EIDX,       // r[d] = the edge's CSR index (GetNeighbors: rows regrouped in key order on the host)
+  OP_INPUT,      // r[d] = column aux of the input row of the source's root ($-.col / $var.col)
   // int64
   OP_ADD_I, OP_SUB_I, OP_MUL_I, OP_DIV_I, OP_MOD_I, OP_XOR_I, OP_NEG_I,
   OP_LT_I, OP_LE_I, OP_GT_I, OP_GE_I, OP_EQ_I, OP_NE_I,
@@ -198,6 +199,7 @@ constexpr int MAX_STEPS = 32;          // GO N STEPS upper bound
 constexpr int MAX_TYPES_Q = 16;        // OVER types per query
 constexpr int INLINE_STARTS = 32;      // start lists up to this size travel in kernel arguments
 constexpr int MAX_TAG_BITS = 16;       // tags addressable by $$ (QState::tagbits: has | used << 16)
+constexpr int MAX_INPUT_COLS = 32;     // columns of a piped / variable input
 
 // A short start list with its edge space over one CSR, built on the host from the CSR offsets
 // (the host copy of row_ptr) and passed by value to the first expansion: the query's first
@@ -243,6 +245,12 @@ struct ExpandArgs {                // one (step, edge type) expansion
   const int64_t* const* tcols;     // tag columns (Snapshot::d_tcols), indexed by vertex id
   const uint8_t* const* tpres;     // tag presence (Snapshot::d_tpres)
   uint32_t gbase;                  // id of local vertex 0 in the tag index space (rank * npad)
+  // piped / variable input (GoExecutor::setupStarts index + VertexBackTracker, GoExecutor.h:169-188)
+  uint32_t* bt;                    // [nv] root (dense id) of every vertex reached (nullptr: not tracked)
+  int bt_first;                    // MARK: this is step 1 (the root of a start is itself)
+  const uint32_t* in_ids;          // input index: dense ids of the rows' vids, ascending (last row wins)
+  uint64_t in_n;
+  const int64_t* const* in_cols;   // [col][k] 8-byte payloads of the indexed rows
 };
 
 // ----------------------------------------------------------------------------- FIND PATH state
@@ -329,6 +337,7 @@ hipError_t ws_compact(Workspace* w, int step, const ExpandArgs* next0);
 hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a, uint64_t n_bound, uint64_t e_bound, int step, int tix,
                            const TypeProgram& prog, uint64_t region_base, uint64_t blk_cap, const InlineList* il = nullptr);
 hipError_t ws_scan_only(Workspace* w, const ExpandArgs& a, uint64_t n_bound, int step, int tix);
+uint32_t* ws_backtracker(Workspace* w);          // [nv] roots (allocated on first use)
 hipError_t ws_end_query(Workspace* w);
 hipError_t ws_end_query_async(Workspace* w);   // enqueue the end-of-query copy + event
 hipError_t ws_end_query_wait(Workspace* w);    // wait for it (then as ws_end_query)

@@ -209,7 +209,34 @@ class Engine:
                                        "algo_bytes": arr[i].algo_bytes} for i in range(n)}
 
     # ------------------------------------------------------------------ GO
-    def _go_request(self, starts, etypes, steps, where, yields, distinct, over_all):
+    @staticmethod
+    def _input_table(inputs, keep):
+        """(names, rows, vid column name) -> the nbg_go_request input fields (kinds from the
+        first row's values, as the InterimResult schema is fixed by its first row)."""
+        names, rows, vid_col = inputs
+        nc, nr = len(names), len(rows)
+        kinds, cols = [], []
+        for c in range(nc):
+            v = rows[0][c] if nr else 0
+            if isinstance(v, bool):
+                k, arr = 2, np.ascontiguousarray([int(bool(r[c])) for r in rows], np.int64)
+            elif isinstance(v, float):
+                k, arr = 1, np.ascontiguousarray([float(r[c]) for r in rows], np.float64).view(np.int64)
+            elif isinstance(v, str):
+                k, arr = 3, (C.c_char_p * max(1, nr))(*[str(r[c]).encode() for r in rows])
+            else:
+                k, arr = 0, np.ascontiguousarray([int(r[c]) for r in rows], np.int64)
+            kinds.append(k)
+            cols.append(arr)
+        keep.extend(cols)
+        cname = (C.c_char_p * max(1, nc))(*[n.encode() for n in names])
+        ckind = (C.c_uint8 * max(1, nc))(*kinds)
+        cptr = (C.c_void_p * max(1, nc))(*[
+            (a.ctypes.data if isinstance(a, np.ndarray) else C.cast(a, C.c_void_p).value) for a in cols])
+        keep.extend([cname, ckind, cptr])
+        return nc, cname, ckind, cptr, nr, names.index(vid_col)
+
+    def _go_request(self, starts, etypes, steps, where, yields, distinct, over_all, inputs=None):
         s = np.ascontiguousarray(starts, np.int64)
         t = np.ascontiguousarray(etypes, np.int32)
         wb = np.frombuffer(where, np.uint8).copy() if where else None
@@ -222,7 +249,12 @@ class Engine:
             t.ctypes.data_as(C.POINTER(C.c_int32)) if len(t) else None, len(t), int(over_all), steps,
             wb.ctypes.data_as(C.POINTER(C.c_uint8)) if wb is not None else None, len(where or b""),
             yptrs, ylens, len(ybufs), int(distinct))
-        return req, (s, t, wb, ybufs, yptrs, ylens)
+        keep = [s, t, wb, ybufs, yptrs, ylens]
+        if inputs is not None:
+            nc, cname, ckind, cptr, nr, vc = self._input_table(inputs, keep)
+            req.num_input_cols, req.input_names, req.input_kinds = nc, cname, ckind
+            req.input_cols, req.num_input_rows, req.input_vid_col = cptr, nr, vc
+        return req, keep
 
     def _host_rows(self, h):
         n, nc = self.lib.nbg_rows_count(h), self.lib.nbg_rows_num_cols(h)
@@ -243,8 +275,9 @@ class Engine:
             cols.append(col)
         return [list(r) for r in zip(*cols)] if nc else [[] for _ in range(n)]
 
-    def go(self, starts, etypes, steps=1, where=b"", yields=(), distinct=False, over_all=False):
-        req, keep = self._go_request(starts, etypes, steps, where, yields, distinct, over_all)
+    def go(self, starts, etypes, steps=1, where=b"", yields=(), distinct=False, over_all=False, inputs=None):
+        """GO N STEPS; ``inputs`` = (column names, rows, FROM column) for $-.x / $var.x props."""
+        req, keep = self._go_request(starts, etypes, steps, where, yields, distinct, over_all, inputs)
         out = C.c_void_p()
         rc = self.lib.nbg_go(self.h, C.byref(req), C.byref(out))
         self._check(rc, "go")

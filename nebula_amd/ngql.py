@@ -489,6 +489,20 @@ class Session:
             cols = g.yields
         if g.over_all and not cols:
             cols = [YieldCol(E.edge_prop(self.b.edge_names[t], "_dst")) for t in etypes]
+        # `$-.*` / `$var.*`: every column of the input (YieldClause expansion)
+        if any(c.expr.kind in (E.K_INPUT, E.K_VAR) and c.expr.prop == "*" for c in cols):
+            if g.from_ref is None:
+                raise ExecError("`*' input props need a piped or variable FROM")
+            src = self._source(g.from_ref, inp)
+            expanded = []
+            for c in cols:
+                if c.expr.kind in (E.K_INPUT, E.K_VAR) and c.expr.prop == "*":
+                    for n in (src.columns if src is not None else []):
+                        expanded.append(YieldCol(E.input_prop(n) if c.expr.kind == E.K_INPUT
+                                                 else E.var_prop(c.expr.alias, n)))
+                else:
+                    expanded.append(c)
+            cols = expanded
         names = [c.name() for c in cols]
         if g.from_ref is not None:
             src = self._source(g.from_ref, inp)
@@ -497,13 +511,18 @@ class Session:
             starts = [int(v) for v in src.col(g.from_ref[1])]
         else:
             starts = list(g.from_vids)
-        for c in cols + ([YieldCol(g.where)] if g.where else []):
-            for n in c.expr.walk():
-                if n.kind in (E.K_INPUT, E.K_VAR):
-                    raise ExecError("input/variable props in WHERE/YIELD are not supported", -23)
+        uses_input = any(n.kind in (E.K_INPUT, E.K_VAR)
+                         for c in cols + ([YieldCol(g.where)] if g.where else []) for n in c.expr.walk())
+        kw = {}
+        if uses_input:
+            # $-.x / $var.x read the FROM source's rows (GoExecutor::setupStarts index)
+            if g.from_ref is None:
+                raise ExecError("input/variable props need a piped or variable FROM")
+            src = self._source(g.from_ref, inp)
+            kw["inputs"] = (src.columns, src.rows, g.from_ref[1])
         rows = self.b.go(starts=starts, etypes=etypes, steps=g.steps,
                          where=g.where.encode() if g.where else b"",
-                         yields=[c.expr.encode() for c in cols], distinct=g.distinct)
+                         yields=[c.expr.encode() for c in cols], distinct=g.distinct, **kw)
         return Interim(names, rows)
 
     def _find(self, s: FindPathSentence, inp):

@@ -96,6 +96,25 @@ int32_t orc_finalize(void* h) {
   return 0;
 }
 
+// The next orc_go's piped / variable input (consumed by that call).
+static thread_local GoQuery g_input;
+void orc_set_input(int32_t ncols, const char* const* names, const uint8_t* kinds, const void* const* cols,
+                   uint64_t nrows, int32_t vid_col) {
+  g_input = GoQuery();
+  g_input.inputVidCol = vid_col;
+  for (int32_t c = 0; c < ncols; ++c) g_input.inputNames.emplace_back(names[c]);
+  g_input.inputRows.assign(nrows, std::vector<Value>(ncols));
+  for (uint64_t r = 0; r < nrows; ++r)
+    for (int32_t c = 0; c < ncols; ++c) {
+      switch (kinds[c]) {
+        case 1: { double d; memcpy(&d, static_cast<const int64_t*>(cols[c]) + r, 8); g_input.inputRows[r][c] = d; break; }
+        case 2: g_input.inputRows[r][c] = static_cast<const int64_t*>(cols[c])[r] != 0; break;
+        case 3: g_input.inputRows[r][c] = std::string(static_cast<const char* const*>(cols[c])[r]); break;
+        default: g_input.inputRows[r][c] = static_cast<const int64_t*>(cols[c])[r];
+      }
+    }
+}
+
 int32_t orc_go(void* h, const int64_t* starts, uint64_t nstarts, const int32_t* etypes, int32_t ntypes,
                int32_t over_all, uint32_t steps, const uint8_t* where, uint32_t where_len,
                const uint8_t* yields_blob, const uint32_t* yield_lens, int32_t nyields, int32_t distinct,
@@ -113,6 +132,10 @@ int32_t orc_go(void* h, const int64_t* starts, uint64_t nstarts, const int32_t* 
     off += yield_lens[i];
   }
   q.distinct = distinct != 0;
+  q.inputNames = std::move(g_input.inputNames);
+  q.inputRows = std::move(g_input.inputRows);
+  q.inputVidCol = g_input.inputVidCol;
+  g_input = GoQuery();
   auto* r = new OrcResult();
   r->rs = runGo(*s, q);
   *result = r;

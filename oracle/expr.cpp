@@ -179,8 +179,7 @@ OptValue Expr::eval(Getters& g) const {
     case kEdgeType: return Value(alias);                        // Expressions.cpp:310-312
     case kSourceProp: return g.srcTagProp(alias, prop);         // :429-431
     case kDestProp: return g.dstTagProp(alias, prop);           // :217-219
-    case kInputProp: case kVariableProp:
-      return Status::Err("input/variable props are not supported by this oracle");
+    case kInputProp: case kVariableProp: return g.inputProp(prop);   // GoExecutor.cpp:932-945
     case kFunctionCall: return Status::Err("function calls are not supported by this oracle");
     case kUnary: {        // UnaryExpression::eval (:698-716)
       auto v = a->eval(g);

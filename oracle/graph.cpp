@@ -85,7 +85,27 @@ struct GoGetters : Getters {
   const VertexHolder* holder = nullptr;
   bool saveType = false;
   SType* colType = nullptr;
+  // InterimResultIndex (InterimResult.cpp:158-270) + VertexBackTracker (GoExecutor.h:169-188)
+  const GoQuery* q = nullptr;
+  const std::unordered_map<int64_t, size_t>* index = nullptr;
+  const std::unordered_map<int64_t, int64_t>* tracker = nullptr;   // null when steps == 1
+  int64_t srcVid = 0;
   explicit GoGetters(const Store& s) : st(s) {}
+
+  OptValue inputProp(const std::string& prop) override {
+    if (!index) return Status::Err("no input");
+    int64_t root = srcVid;
+    if (tracker) {
+      auto t = tracker->find(srcVid);
+      if (t == tracker->end()) return Status::Err("no root");
+      root = t->second;
+    }
+    auto r = index->find(root);
+    if (r == index->end()) return Status::Err("no input row");
+    for (size_t c = 0; c < q->inputNames.size(); ++c)
+      if (q->inputNames[c] == prop) return q->inputRows[r->second][c];
+    return Status::Err("Prop `" + prop + "' not found");
+  }
 
   OptValue aliasProp(const std::string& edge, const std::string& prop) override {
     auto et = st.edgeByName.find(edge);
@@ -190,6 +210,11 @@ ResultSet runGo(const Store& st, const GoQuery& q) {
     starts.assign(u.begin(), u.end());
   }
   uint32_t steps = q.steps;
+  std::unordered_map<int64_t, size_t> index;   // vidToRowIndex_: the last row of each vid wins
+  const bool hasInput = q.inputVidCol >= 0;
+  if (hasInput)
+    for (size_t r = 0; r < q.inputRows.size(); ++r) index[std::get<0>(q.inputRows[r][q.inputVidCol])] = r;
+  std::unordered_map<int64_t, int64_t> tracker;
   for (uint32_t cur = 1;; ++cur) {
     bool final = cur >= steps;
     // getStepOutProps (GoExecutor.cpp:587-630)
@@ -228,6 +253,12 @@ ResultSet runGo(const Store& st, const GoQuery& q) {
             RowReader r(row, &s);
             auto d = r.get("_dst");
             if (d.ok()) set.insert(std::get<0>(d.v));
+            if (!final && d.ok()) {   // VertexBackTracker::add (GoExecutor.cpp:531-533)
+              int64_t value = vd.vid;
+              auto it = tracker.find(vd.vid);
+              if (it != tracker.end()) value = it->second;
+              tracker[std::get<0>(d.v)] = value;
+            }
           }
         }
       }
@@ -248,6 +279,9 @@ ResultSet runGo(const Store& st, const GoQuery& q) {
       // fallthrough to finish with holder
       GoGetters g(st);
       g.holder = &holder;
+      g.q = &q;
+      g.index = hasInput ? &index : nullptr;
+      g.tracker = steps > 1 ? &tracker : nullptr;
       // processFinalResult + setupInterimResult
       std::unique_ptr<Schema> outSchema;
       std::unordered_set<std::string> uniq;
@@ -256,7 +290,7 @@ ResultSet runGo(const Store& st, const GoQuery& q) {
           const Schema& s = resp.edgeSchema.at(ed.type);
           for (auto& row : rowSetSplit(ed.data)) {
             RowReader r(row, &s);
-            g.edgeType = ed.type; g.row = &r; g.rowSchema = &s;
+            g.edgeType = ed.type; g.row = &r; g.rowSchema = &s; g.srcVid = vd.vid;
             g.edgeSchema = &resp.edgeSchema; g.tagSchema = &resp.vertexSchema; g.tagData = &vd.tags;
             g.saveType = false;
             if (filter) {
@@ -308,6 +342,9 @@ ResultSet runGo(const Store& st, const GoQuery& q) {
     VertexHolder holder;
     GoGetters g(st);
     g.holder = &holder;
+    g.q = &q;
+    g.index = hasInput ? &index : nullptr;
+    g.tracker = steps > 1 ? &tracker : nullptr;
     std::unique_ptr<Schema> outSchema;
     std::unordered_set<std::string> uniq;
     for (auto& vd : resp.vertices) {
@@ -315,7 +352,7 @@ ResultSet runGo(const Store& st, const GoQuery& q) {
         const Schema& s = resp.edgeSchema.at(ed.type);
         for (auto& row : rowSetSplit(ed.data)) {
           RowReader r(row, &s);
-          g.edgeType = ed.type; g.row = &r; g.rowSchema = &s;
+          g.edgeType = ed.type; g.row = &r; g.rowSchema = &s; g.srcVid = vd.vid;
           g.edgeSchema = &resp.edgeSchema; g.tagSchema = &resp.vertexSchema; g.tagData = &vd.tags;
           g.saveType = false;
           if (filter) {

@@ -172,6 +172,7 @@ struct Getters {
   virtual OptValue srcTagProp(const std::string& tag, const std::string& prop) = 0;
   virtual OptValue dstTagProp(const std::string& tag, const std::string& prop) = 0;
   virtual OptValue edgeRank() { return Status::Err("no rank getter"); }
+  virtual OptValue inputProp(const std::string&) { return Status::Err("no input"); }
 };
 
 // Expression::decode / encode (src/common/filter/Expressions.cpp:93-116 and per-class codecs)
@@ -268,6 +269,10 @@ struct GoQuery {
   std::vector<std::string> yields; // encoded yield expressions; empty = default
   std::vector<std::string> yieldNames;
   bool distinct = false;
+  // piped / variable input ($-.col, $var.col): the FROM source's rows (InterimResult)
+  std::vector<std::string> inputNames;
+  std::vector<std::vector<Value>> inputRows;
+  int inputVidCol = -1;
 };
 ResultSet runGo(const Store& st, const GoQuery& q);
 

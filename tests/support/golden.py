@@ -11,9 +11,6 @@ GOLDEN = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))
 
 # Cases whose features are outside the hot path this build covers (documented in DESIGN.md).
 UNSUPPORTED = (
-    ("$-.", "input props in YIELD/WHERE ($-.name) need graphd's InterimResult index"),
-    ("$var.name", "variable props in YIELD/WHERE need graphd's InterimResult index"),
-    ("$var.*", "variable props in YIELD/WHERE need graphd's InterimResult index"),
     ("udf_is_in", "function calls (FunctionManager) are rejected by the storage filter and out of scope"),
     ("REVERSELY", "REVERSELY is rejected by the reference GoExecutor (GoExecutor.cpp:243-246)"),
 )

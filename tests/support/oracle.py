@@ -30,6 +30,7 @@ def lib():
         L.orc_load_part_kv.argtypes = [vp, i32, vp, vp, vp, vp, u64]
         L.orc_finalize.argtypes = [vp]
         L.orc_go.argtypes = [vp, vp, u64, vp, i32, i32, u32, vp, u32, vp, vp, i32, i32, P(vp)]
+        L.orc_set_input.argtypes = [i32, vp, vp, vp, u64, i32]
         L.orc_go.restype = i32
         L.orc_result_code.argtypes = [vp]
         L.orc_result_error.argtypes = [vp]
@@ -135,7 +136,13 @@ class Oracle:
         self.L.orc_finalize(self.h)
 
     # ---------------------------------------------------------------- ngql backend API
-    def go(self, starts, etypes, steps, where=b"", yields=(), distinct=False, over_all=False):
+    def go(self, starts, etypes, steps, where=b"", yields=(), distinct=False, over_all=False, inputs=None):
+        if inputs is not None:
+            from nebula_amd.engine import Engine
+            keep = []
+            nc, cname, ckind, cptr, nr, vc = Engine._input_table(inputs, keep)
+            self.L.orc_set_input(nc, C.cast(cname, C.c_void_p), C.cast(ckind, C.c_void_p), C.cast(cptr, C.c_void_p),
+                                 nr, vc)
         s = np.asarray(starts, np.int64)
         t = np.asarray(etypes, np.int32)
         blob = b"".join(yields)

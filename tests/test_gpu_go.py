@@ -213,3 +213,49 @@ def test_async_submit_wait_parity(rmat12):
             assert got[i][0] == len(exp)
     finally:
         stmt.free()
+
+
+def _forest(seed=3, roots=6, depth=4, fan=4):
+    """A forest (every vertex has one parent): a final row's root is unique, so the reference's
+    VertexBackTracker (last write wins over unordered responses) is deterministic on it."""
+    rng = np.random.default_rng(seed)
+    src, dst = [], []
+    level = [int(x) for x in rng.choice(1 << 40, roots, replace=False)]
+    all_roots = list(level)
+    nxt = 1 << 41
+    for _ in range(depth):
+        new = []
+        for v in level:
+            for _ in range(int(rng.integers(1, fan + 1))):
+                nxt += int(rng.integers(1, 1000))
+                src.append(v)
+                dst.append(nxt)
+                new.append(nxt)
+        level = new
+    w = rng.integers(0, 100, len(src))
+    return all_roots, np.array(src, np.int64), np.array(dst, np.int64), w.astype(np.int64)
+
+
+@pytest.mark.parametrize("steps", [1, 2, 3])
+def test_input_props_backtracker(steps):
+    """$-.col in YIELD / WHERE after N steps: the root's input row (GoExecutor::getPropFromInterim,
+    VertexBackTracker) — device MARKB roots vs the oracle."""
+    roots, src, dst, w = _forest()
+    eng = graphs.rmat_engine(src, dst, w, parts=7)
+    orc = graphs.rmat_oracle(src, dst, w, parts=7)
+    try:
+        # input rows: (id, name-like int, score) with a duplicated id (the last row wins)
+        rows = [[r, 1000 + i, 0.5 * i] for i, r in enumerate(roots)] + [[roots[0], 7, 9.25]]
+        inputs = (["id", "tag", "score"], rows, "id")
+        yields = [E.input_prop("tag").encode(), E.input_prop("score").encode(), E.edge_prop("e", "_dst").encode()]
+        where = E.binop(">", E.input_prop("tag"), E.const(1001)).encode()
+        for wb in (b"", where):
+            got = eng.go(roots, [1], steps, wb, yields, inputs=inputs)
+            exp = orc.go(roots, [1], steps, wb, yields, inputs=inputs)
+            assert graphs.sorted_rows(got) == graphs.sorted_rows(exp) and got
+        bad = [E.input_prop("nosuch").encode()]
+        with pytest.raises(NbgError):
+            eng.go(roots, [1], steps, b"", bad, inputs=inputs)
+    finally:
+        eng.close()
+        orc.close()
