@@ -113,6 +113,14 @@ int32_t nbg_load_edges(nbg_engine* e, int32_t edge_type, const int64_t* src, con
  * it to HBM.  Host-side staging is released afterwards. */
 int32_t nbg_finalize(nbg_engine* e);
 
+/* Snapshot files (restart without re-ingesting the kvstore): nbg_snapshot_save writes a finalized
+ * engine's snapshot (schemas, dictionaries, CSR/CSC, columns, tag columns) to `path`;
+ * nbg_snapshot_load replaces registration + loading + nbg_finalize on a fresh engine created with
+ * the same num_parts / num_gpus / rank (a partitioned engine attaches its communicator first;
+ * the load is then collective).  Schemas come from the file. */
+int32_t nbg_snapshot_save(nbg_engine* e, const char* path);
+int32_t nbg_snapshot_load(nbg_engine* e, const char* path);
+
 typedef struct {
   uint64_t num_vertices;      /* vertices with at least one record in this rank's parts        */
   uint64_t num_edges;         /* live (latest-version) edge records, all signed types          */

@@ -82,6 +82,8 @@ SIGNATURES = [
     ("nbg_load_part_kv", i32, [vp, i32, vp, vp, vp, vp, u64]),
     ("nbg_load_edges", i32, [vp, i32, vp, vp, vp, u64, P(vp), i32]),
     ("nbg_finalize", i32, [vp]),
+    ("nbg_snapshot_save", i32, [vp, C.c_char_p]),
+    ("nbg_snapshot_load", i32, [vp, C.c_char_p]),
     ("nbg_get_stats", i32, [vp, P(nbg_stats)]),
     ("nbg_go", i32, [vp, P(nbg_go_request), P(vp)]),
     ("nbg_go_device", i32, [vp, P(nbg_go_request), P(vp)]),

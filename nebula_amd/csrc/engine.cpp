@@ -731,6 +731,18 @@ static void complete_oldest(Engine& E) {
   E.slots[t->slot].ticket = nullptr;
 }
 
+// The query workspace of a finalized (or snapshot-loaded) engine.
+int32_t nbg::engine_ready(Engine& E) {
+  std::string err;
+  E.ws = ws_create(E.snap.nv + 1024, E.snap.nv, E.snap.max_edges(), E.stream, &err);
+  if (!E.ws) return E.fail(NBG_E_OUT_OF_MEMORY, err);
+  if (E.partitioned()) {
+    hipError_t he = ws_set_partition(E.ws, E.comm.get(), E.npad);
+    if (he != hipSuccess) return E.fail(NBG_E_OUT_OF_MEMORY, std::string("partition buffers: ") + hipGetErrorString(he));
+  }
+  return NBG_OK;
+}
+
 // ============================================================================= C ABI
 extern "C" {
 
@@ -895,14 +907,7 @@ int32_t nbg_finalize(nbg_engine* h) {
     return E.fail(NBG_E_DEVICE, "hipStreamCreate failed");
   int32_t rc = E.finalize();
   if (rc) return rc;
-  std::string err;
-  E.ws = ws_create(E.snap.nv + 1024, E.snap.nv, E.snap.max_edges(), E.stream, &err);
-  if (!E.ws) return E.fail(NBG_E_OUT_OF_MEMORY, err);
-  if (E.partitioned()) {
-    hipError_t he = ws_set_partition(E.ws, E.comm.get(), E.npad);
-    if (he != hipSuccess) return E.fail(NBG_E_OUT_OF_MEMORY, std::string("partition buffers: ") + hipGetErrorString(he));
-  }
-  return NBG_OK;
+  return engine_ready(E);
 }
 
 int32_t nbg_get_stats(const nbg_engine* h, nbg_stats* out) {

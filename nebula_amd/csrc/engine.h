@@ -53,10 +53,19 @@ struct Engine {
                      const void* const* cols, int32_t ncols);
   int32_t finalize();
   int32_t build_tags(const std::vector<int64_t>& dict, const std::vector<int64_t>& remap);
+  int32_t upload_tags();   // DevTag host arrays -> device (+ all-gather when partitioned)
+  bool upload_type(DevEdgeType& dt, uint64_t nv, const std::vector<uint32_t>& col, const std::vector<int64_t>& dvid,
+                   const std::vector<int64_t>* rk, const std::vector<std::vector<int64_t>>& pc,
+                   const std::vector<uint8_t>* valid, const std::vector<VKind>& kinds);
+  int32_t upload_vertices(const std::vector<uint8_t>& visible, bool all_visible);
+  int32_t save_snapshot(const char* path);
+  int32_t load_snapshot(const char* path);
   int32_t exchange_dictionary(const std::vector<int64_t>& local, std::vector<int64_t>* gdict,
                               std::vector<uint64_t>* gcount);
   uint32_t dense(int64_t vid) const;
 };
+
+int32_t engine_ready(Engine& E);   // workspace (+ partition buffers) after finalize / snapshot load
 
 }  // namespace nbg
 

@@ -277,6 +277,49 @@ int32_t Engine::exchange_dictionary(const std::vector<int64_t>& local, std::vect
 // global id space, so a `$$` read of a remote destination stays a local load.
 int32_t Engine::build_tags(const std::vector<int64_t>& dict, const std::vector<int64_t>& remap) {
   const uint64_t nv = dict.size();
+  int index = 0, col_base = 0;
+  for (auto& kv : tags) {
+    const int32_t tag = kv.first;
+    const Schema* latest = kv.second.latest();
+    const size_t nc = latest ? latest->cols.size() : 0;
+    DevTag& dt = snap.tags[tag];
+    dt.tag = tag;
+    dt.index = index++;
+    dt.col_base = col_base;
+    col_base += (int)nc;
+    dt.kind.clear();
+    for (size_t c = 0; c < nc; ++c) dt.kind.push_back(kindOfType(latest->cols[c].type));
+    dt.h_present.assign(nv, 0);
+    dt.h_cols.assign(nc, std::vector<int64_t>(nv, 0));
+    auto it = tstage.find(tag);
+    if (it == tstage.end()) continue;
+    const TagStage& ts = it->second;
+    std::vector<int64_t> best(nv, -1);   // record index of the live version per vertex
+    for (size_t i = 0; i < ts.vid.size(); ++i) {
+      auto p = std::lower_bound(dict.begin(), dict.end(), ts.vid[i]);
+      const uint64_t d = (uint64_t)(p - dict.begin());
+      const int64_t b = best[d];
+      if (b < 0 || ts.verkey[i] < ts.verkey[b] || (ts.verkey[i] == ts.verkey[b] && ts.seq[i] > ts.seq[b]))
+        best[d] = (int64_t)i;
+    }
+    for (uint64_t d = 0; d < nv; ++d) {
+      const int64_t b = best[d];
+      if (b < 0) continue;
+      dt.h_present[d] = ts.valid[b] ? 1 : 2;   // 2: record present, value undecodable
+      for (size_t c = 0; c < nc && c < ts.props.size(); ++c) {
+        int64_t x = ts.props[c][b];
+        if (dt.kind[c] == VK_STRING && ts.valid[b]) x = remap[x];
+        dt.h_cols[c][d] = x;
+      }
+    }
+  }
+  return upload_tags();
+}
+
+// DevTag host arrays (local dense ids) -> device arrays over the tag index space (single GPU: the
+// dense ids; partitioned: all ranks' local rows gathered into the global id space).
+int32_t Engine::upload_tags() {
+  const uint64_t nv = snap.nv;
   const uint64_t G = (uint64_t)cfg.num_gpus;
   const uint64_t local = partitioned() ? npad : nv;          // rows of the local arrays
   const uint64_t space = partitioned() ? G * npad : nv;      // rows of the device arrays
@@ -288,7 +331,6 @@ int32_t Engine::build_tags(const std::vector<int64_t>& dict, const std::vector<i
     snap.device_bytes += bytes;
     if (!bytes) return true;
     if (!partitioned()) return !src || hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess;
-    // local rows -> staging -> all-gather into the global id space
     const size_t lb = bytes / G;
     if (hipMemcpy(d_stage, src, lb, hipMemcpyHostToDevice) != hipSuccess) return false;
     return comm->allgather(d_stage, *dst, lb, stream) == 0 && hipStreamSynchronize(stream) == hipSuccess;
@@ -296,46 +338,19 @@ int32_t Engine::build_tags(const std::vector<int64_t>& dict, const std::vector<i
   if (partitioned() && hipMalloc(&d_stage, std::max<uint64_t>(local, 1) * 8) != hipSuccess)
     return fail(NBG_E_OUT_OF_MEMORY, "tag staging");
   int32_t rc = NBG_OK;
-  for (auto& kv : tags) {
-    const int32_t tag = kv.first;
-    const Schema* latest = kv.second.latest();
-    const size_t nc = latest ? latest->cols.size() : 0;
-    DevTag& dt = snap.tags[tag];
-    dt.tag = tag;
-    dt.index = (int)all_pres.size();
-    dt.col_base = (int)all_cols.size();
-    for (size_t c = 0; c < nc; ++c) dt.kind.push_back(kindOfType(latest->cols[c].type));
+  std::vector<DevTag*> order(snap.tags.size(), nullptr);
+  for (auto& kv : snap.tags) order[kv.second.index] = &kv.second;
+  for (DevTag* dtp : order) {
+    DevTag& dt = *dtp;
     std::vector<uint8_t> pres(local, 0);
-    std::vector<std::vector<int64_t>> cols(nc, std::vector<int64_t>(local, 0));
-    dt.h_present.assign(nv, 0);
-    auto it = tstage.find(tag);
-    if (it != tstage.end()) {
-      const TagStage& ts = it->second;
-      std::vector<int64_t> best(nv, -1);   // record index of the live version per vertex
-      for (size_t i = 0; i < ts.vid.size(); ++i) {
-        auto p = std::lower_bound(dict.begin(), dict.end(), ts.vid[i]);
-        const uint64_t d = (uint64_t)(p - dict.begin());
-        const int64_t b = best[d];
-        if (b < 0 || ts.verkey[i] < ts.verkey[b] || (ts.verkey[i] == ts.verkey[b] && ts.seq[i] > ts.seq[b]))
-          best[d] = (int64_t)i;
-      }
-      for (uint64_t d = 0; d < nv; ++d) {
-        const int64_t b = best[d];
-        if (b < 0) continue;
-        pres[d] = 1;
-        dt.h_present[d] = ts.valid[b] ? 1 : 2;   // 2: record present, value undecodable
-        for (size_t c = 0; c < nc && c < ts.props.size(); ++c) {
-          int64_t x = ts.props[c][b];
-          if (dt.kind[c] == VK_STRING && ts.valid[b]) x = remap[x];
-          cols[c][d] = x;
-        }
-      }
-    }
-    dt.h_cols.resize(nc);
-    for (size_t c = 0; c < nc; ++c) dt.h_cols[c].assign(cols[c].begin(), cols[c].begin() + (ptrdiff_t)nv);
+    for (uint64_t d = 0; d < nv; ++d) pres[d] = dt.h_present[d] != 0;
     bool ok = up((void**)&dt.present, pres.data(), space);
-    dt.cols.assign(nc, nullptr);
-    for (size_t c = 0; ok && c < nc; ++c) ok = up((void**)&dt.cols[c], cols[c].data(), space * 8);
+    dt.cols.assign(dt.h_cols.size(), nullptr);
+    std::vector<int64_t> buf(local, 0);
+    for (size_t c = 0; ok && c < dt.h_cols.size(); ++c) {
+      std::copy(dt.h_cols[c].begin(), dt.h_cols[c].end(), buf.begin());
+      ok = up((void**)&dt.cols[c], buf.data(), space * 8);
+    }
     if (!ok) { rc = fail(NBG_E_OUT_OF_MEMORY, "device allocation failed for tag columns"); break; }
     all_pres.push_back(dt.present);
     for (auto* p : dt.cols) all_cols.push_back(p);
@@ -349,6 +364,76 @@ int32_t Engine::build_tags(const std::vector<int64_t>& dict, const std::vector<i
   if (ok && !all_pres.empty())
     ok = hipMemcpy(snap.d_tpres, all_pres.data(), all_pres.size() * 8, hipMemcpyHostToDevice) == hipSuccess;
   return ok ? NBG_OK : fail(NBG_E_OUT_OF_MEMORY, "device allocation failed for the tag tables");
+}
+
+// dense id -> vid table and the visibility flags
+int32_t Engine::upload_vertices(const std::vector<uint8_t>& visible, bool all_visible) {
+  const uint64_t nv = snap.nv;
+  bool ok = hipMalloc((void**)&snap.d_vids, std::max<uint64_t>(nv, 1) * 8) == hipSuccess &&
+            hipMemcpy(snap.d_vids, snap.h_vids.data(), nv * 8, hipMemcpyHostToDevice) == hipSuccess;
+  snap.device_bytes += nv * 8;
+  if (ok && !all_visible) {
+    snap.h_visible = visible;
+    ok = hipMalloc((void**)&snap.d_visible, nv) == hipSuccess &&
+         hipMemcpy(snap.d_visible, visible.data(), nv, hipMemcpyHostToDevice) == hipSuccess;
+    snap.device_bytes += nv;
+  }
+  return ok ? NBG_OK : fail(NBG_E_OUT_OF_MEMORY, "device allocation failed for the vertex table");
+}
+
+// Upload one signed type's CSR and columns (plus narrow copies of INT columns whose values fit
+// 1 / 2 / 4 bytes, sign-extended on load: the final-step fast path reads those).  rank / valid:
+// nullptr when every rank is 0 / every value decoded.
+bool Engine::upload_type(DevEdgeType& dt, uint64_t nv, const std::vector<uint32_t>& col, const std::vector<int64_t>& dvid,
+                         const std::vector<int64_t>* rk, const std::vector<std::vector<int64_t>>& pc,
+                         const std::vector<uint8_t>* valid, const std::vector<VKind>& kinds) {
+  const uint64_t E = dt.num_edges;
+  const size_t nc = pc.size();
+  auto up = [&](void** dst, const void* src, size_t bytes) -> bool {
+    if (!bytes) bytes = 8;
+    if (hipMalloc(dst, bytes) != hipSuccess) return false;
+    snap.device_bytes += bytes;
+    if (src && hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice) != hipSuccess) return false;
+    return true;
+  };
+  bool ok = up((void**)&dt.row_ptr, dt.h_row_ptr.data(), (nv + 1) * 4) && up((void**)&dt.col, col.data(), E * 4) &&
+            up((void**)&dt.dst_vid, dvid.data(), E * 8);
+  if (ok && rk) ok = up((void**)&dt.rank, rk->data(), E * 8);
+  dt.prop_kind = kinds;
+  dt.props.assign(nc, nullptr);
+  for (size_t c = 0; ok && c < nc; ++c) ok = up((void**)&dt.props[c], pc[c].data(), E * 8);
+  dt.narrow.assign(nc, nullptr);
+  dt.narrow_bytes.assign(nc, 0);
+  for (size_t c = 0; ok && c < nc && E; ++c) {
+    if (kinds[c] != VK_INT) continue;
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+#pragma omp parallel for reduction(min : lo) reduction(max : hi)
+    for (int64_t i = 0; i < (int64_t)E; ++i) {
+      lo = std::min(lo, pc[c][i]);
+      hi = std::max(hi, pc[c][i]);
+    }
+    int bytes = 8;
+    if (lo >= INT8_MIN && hi <= INT8_MAX) bytes = 1;
+    else if (lo >= INT16_MIN && hi <= INT16_MAX) bytes = 2;
+    else if (lo >= INT32_MIN && hi <= INT32_MAX) bytes = 4;
+    if (bytes == 8) continue;
+    std::vector<uint8_t> buf(E * (size_t)bytes);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < (int64_t)E; ++i) {
+      const int64_t v = pc[c][i];
+      if (bytes == 1) reinterpret_cast<int8_t*>(buf.data())[i] = (int8_t)v;
+      else if (bytes == 2) reinterpret_cast<int16_t*>(buf.data())[i] = (int16_t)v;
+      else reinterpret_cast<int32_t*>(buf.data())[i] = (int32_t)v;
+    }
+    ok = up(&dt.narrow[c], buf.data(), buf.size());
+    dt.narrow_bytes[c] = bytes;
+  }
+  if (ok && valid) ok = up((void**)&dt.valid, valid->data(), E);
+  if (ok && nc) ok = up((void**)&dt.d_props, dt.props.data(), nc * sizeof(int64_t*));
+  uint32_t md = 0;
+  for (uint64_t d = 0; d < nv; ++d) md = std::max(md, dt.h_row_ptr[d + 1] - dt.h_row_ptr[d]);
+  dt.max_degree = (int)md;
+  return ok;
 }
 
 int32_t Engine::finalize() {
@@ -512,72 +597,17 @@ int32_t Engine::finalize() {
         }
       }
     }
-    // upload
-    auto up = [&](void** dst, const void* src, size_t bytes) -> bool {
-      if (!bytes) bytes = 8;
-      if (hipMalloc(dst, bytes) != hipSuccess) return false;
-      snap.device_bytes += bytes;
-      if (src && hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice) != hipSuccess) return false;
-      return true;
-    };
-    bool ok = up((void**)&dt.row_ptr, dt.h_row_ptr.data(), (nv + 1) * 4) &&
-              up((void**)&dt.col, col.data(), E * 4) && up((void**)&dt.dst_vid, dvid.data(), E * 8);
-    if (ok && any_rank) ok = up((void**)&dt.rank, rk.data(), E * 8);
-    dt.prop_kind = kinds;
-    dt.props.assign(nc, nullptr);
-    for (size_t c = 0; ok && c < nc; ++c) ok = up((void**)&dt.props[c], pc[c].data(), E * 8);
-    // narrow copy of INT columns whose values fit 1 / 2 / 4 bytes (sign-extended on load): the
-    // final-step fast path reads it instead of the 8-byte column
-    dt.narrow.assign(nc, nullptr);
-    dt.narrow_bytes.assign(nc, 0);
-    for (size_t c = 0; ok && c < nc && E; ++c) {
-      if (kinds[c] != VK_INT) continue;
-      int64_t lo = INT64_MAX, hi = INT64_MIN;
-#pragma omp parallel for reduction(min : lo) reduction(max : hi)
-      for (int64_t i = 0; i < (int64_t)E; ++i) {
-        lo = std::min(lo, pc[c][i]);
-        hi = std::max(hi, pc[c][i]);
-      }
-      int bytes = 8;
-      if (lo >= INT8_MIN && hi <= INT8_MAX) bytes = 1;
-      else if (lo >= INT16_MIN && hi <= INT16_MAX) bytes = 2;
-      else if (lo >= INT32_MIN && hi <= INT32_MAX) bytes = 4;
-      if (bytes == 8) continue;
-      std::vector<uint8_t> buf(E * (size_t)bytes);
-#pragma omp parallel for schedule(static)
-      for (int64_t i = 0; i < (int64_t)E; ++i) {
-        const int64_t v = pc[c][i];
-        if (bytes == 1) reinterpret_cast<int8_t*>(buf.data())[i] = (int8_t)v;
-        else if (bytes == 2) reinterpret_cast<int16_t*>(buf.data())[i] = (int16_t)v;
-        else reinterpret_cast<int32_t*>(buf.data())[i] = (int32_t)v;
-      }
-      ok = up(&dt.narrow[c], buf.data(), buf.size());
-      dt.narrow_bytes[c] = bytes;
-    }
-    if (ok && any_invalid) ok = up((void**)&dt.valid, valid.data(), E);
-    if (ok && nc) {
-      ok = up((void**)&dt.d_props, dt.props.data(), nc * sizeof(int64_t*));
-    }
+    bool ok = upload_type(dt, nv, col, dvid, any_rank ? &rk : nullptr, pc, any_invalid ? &valid : nullptr, kinds);
     if (!ok) { rc = fail(NBG_E_OUT_OF_MEMORY, "device allocation failed for the snapshot"); break; }
-    uint32_t md = 0;
-    for (uint64_t d = 0; d < nv; ++d) md = std::max(md, live[d + 1]);
-    dt.max_degree = (int)md;
+
     EdgeStage().src.swap(st.src);   // release staging as we go
     st = EdgeStage();
   }
   if (rc) return rc;
   rc = build_tags(all, remap);
   if (rc) return rc;
-  bool ok = hipMalloc((void**)&snap.d_vids, std::max<uint64_t>(nv, 1) * 8) == hipSuccess &&
-            hipMemcpy(snap.d_vids, all.data(), nv * 8, hipMemcpyHostToDevice) == hipSuccess;
-  snap.device_bytes += nv * 8;
-  if (ok && !all_visible) {
-    snap.h_visible = visible;
-    ok = hipMalloc((void**)&snap.d_visible, nv) == hipSuccess &&
-         hipMemcpy(snap.d_visible, visible.data(), nv, hipMemcpyHostToDevice) == hipSuccess;
-    snap.device_bytes += nv;
-  }
-  if (!ok) return fail(NBG_E_OUT_OF_MEMORY, "device allocation failed for the vertex table");
+  rc = upload_vertices(visible, all_visible);
+  if (rc) return rc;
   stage.clear();
   tstage.clear();
   pool.clear();

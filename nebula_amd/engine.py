@@ -191,6 +191,15 @@ class Engine:
     def finalize(self):
         self._check(self.lib.nbg_finalize(self.h), "finalize")
 
+    def snapshot_save(self, path: str):
+        """nbg_snapshot_save: the finalized snapshot to a file (restart without re-ingest)."""
+        self._check(self.lib.nbg_snapshot_save(self.h, path.encode()), "snapshot_save")
+
+    def snapshot_load(self, path: str):
+        """nbg_snapshot_load: instead of register / load / finalize; schemas come from the file."""
+        self._check(self.lib.nbg_snapshot_load(self.h, path.encode()), "snapshot_load")
+        self._schemas_from_engine = True
+
     def stats(self):
         s = L.nbg_stats()
         self._check(self.lib.nbg_get_stats(self.h, C.byref(s)), "stats")

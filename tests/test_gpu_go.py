@@ -4,7 +4,7 @@ rows are compared as sorted multisets (TestBase::verifyResult semantics)."""
 import numpy as np
 import pytest
 
-from nebula_amd import NbgError, expr as E, nba_engine
+from nebula_amd import NbgError, expr as E, kvgen, nba_engine
 from nebula_amd import _lib
 from tests.support import golden, graphs
 from tests.support.oracle import nba_oracle
@@ -256,6 +256,43 @@ def test_input_props_backtracker(steps):
         bad = [E.input_prop("nosuch").encode()]
         with pytest.raises(NbgError):
             eng.go(roots, [1], steps, b"", bad, inputs=inputs)
+    finally:
+        eng.close()
+        orc.close()
+
+
+def test_snapshot_save_load_roundtrip(tmp_path):
+    """nbg_snapshot_save / nbg_snapshot_load: a reloaded engine answers GO (tag props, ranks,
+    two types), GetNeighbors and FIND PATH exactly like the engine that built the snapshot."""
+    from nebula_amd import Engine
+    src, persons, eng, orc = graphs.tagged_pair(9)
+    path = str(tmp_path / "snap.nbg")
+    try:
+        eng.snapshot_save(path)
+        re = Engine(7)
+        re.snapshot_load(path)
+        ps = set(persons)
+        starts = [r for r in graphs.roots(src, 40, seed=2) if r in ps][:5]
+        ys = [E.edge_prop("e", "_dst").encode(), E.dst_prop("person", "name").encode(),
+              E.edge_prop("f", "_rank").encode()]
+        for steps in (1, 2, 3):
+            if steps == 1:   # the starts are persons: $^ is defined
+                ys = ys + [E.src_prop("person", "age").encode()]
+            a = graphs.sorted_rows(eng.go(starts, [1, 2], steps, b"", ys))
+            b = graphs.sorted_rows(re.go(starts, [1, 2], steps, b"", ys))
+            assert a == b and a
+            ys = ys[:3]
+        assert eng.find_path(starts[:2], starts[2:], [1, 2], 4) == re.find_path(starts[:2], starts[2:], [1, 2], 4)
+        pvs = [(kvgen.part_of(v, 7), v) for v in starts]
+        rets = [(3, 1, "_dst"), (3, 1, "w"), (1, graphs.T_PERSON, "name")]
+        assert eng.get_neighbors(pvs, [1, 2], b"", rets) == re.get_neighbors(pvs, [1, 2], b"", rets)
+        assert eng.stats()["num_edges"] == re.stats()["num_edges"]
+        re.close()
+        # a snapshot of another partitioning is rejected
+        other = Engine(5)
+        with pytest.raises(NbgError):
+            other.snapshot_load(path)
+        other.close()
     finally:
         eng.close()
         orc.close()
