@@ -76,6 +76,8 @@ def main():
     ap.add_argument("--sp-pairs", type=int, default=10000, help="FIND SHORTEST PATH pairs (0 = skip)")
     ap.add_argument("--sp-upto", type=int, default=5)
     ap.add_argument("--sync", action="store_true", help="one query at a time (no query slots)")
+    ap.add_argument("--c5-scale", type=int, default=20,
+                    help="C5 substitute (knows RMAT + likes bipartite): knows scale, 0 = skip")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -203,6 +205,10 @@ def main():
         pairs = rmat.pick_pairs(src, dst, args.sp_pairs, 7, verts=all_verts)
         sp = shortest_path_leg(eng, pairs, args, barrier)
 
+    c5 = None
+    if world == 1 and args.c5_scale > 0:
+        c5 = c5_leg(args, barrier)
+
     # edges_scanned is already the whole query's count (summed over ranks in the library);
     # rows stay on the rank that produced them, so they are summed here
     tot_scanned, max_elapsed, tot_rows = float(scanned), elapsed, float(rows)
@@ -289,6 +295,7 @@ def main():
         "edges_per_step": scanned // max(1, args.steps),
         "kernels": kernels,
         "find_shortest_path": sp,
+        "c5_substitute": c5,
         "load_seconds": round(load_s, 2),
     }
     print(json.dumps(out), flush=True)
@@ -338,6 +345,77 @@ def shortest_path_leg(eng, pairs, args, barrier):
                            "avg_launch_us": round(v["ms"] * 1e3 / v["launches"], 2)}
         out["kernel_time_frac_of_wall"] = round(sum(x["ms"] for x in ks.values()) * 1e-3 / elapsed, 3)
     return out
+
+
+def c5_leg(args, barrier):
+    """SURVEY §8(d) C5 substitute (LDBC SNB SF100 is not available offline): `knows` = RMAT-k
+    over persons, `likes` = a bipartite RMAT from persons to posts (same seed scheme, post vids in a
+    disjoint range).  GO 4 STEPS OVER knows, likes (16 roots, queries in flight) and FIND ALL PATH
+    UPTO 4 STEPS OVER knows (64 pairs)."""
+    from nebula_amd import Engine, rmat
+    k = args.c5_scale
+    t0 = time.time()
+    ks, kd, kw = rmat.rmat_edges_fast(k)
+    ls, ld, lw = rmat.rmat_edges_fast(k - 1, seed=rmat.SEED_BASE ^ 0x6C696B6573)
+    persons = np.union1d(np.unique(ks), np.unique(kd))
+    ls = persons[(ls.astype(np.uint64) % np.uint64(len(persons))).astype(np.int64)]
+    ld = ld ^ (1 << 61)                       # posts: a vid range disjoint from the persons
+    eng = Engine(args.parts)
+    eng.register_edge(1, "knows", [("w", 2)])
+    eng.register_edge(2, "likes", [("w", 2)])
+    eng.load_edges(1, ks, kd, [kw])
+    eng.load_edges(2, ls, ld, [lw])
+    eng.finalize()
+    load_s = time.time() - t0
+    roots = [int(x) for x in rmat.pick_roots(ks, 16, 42)]
+    stmt = eng.prepare_go([1, 2], 4)
+    for r in roots[:4]:
+        stmt.run_device([r]).free()
+    inflight = 0 if args.sync else int(os.environ.get("NBG_QUERY_SLOTS", "6"))
+    barrier()
+    t1 = time.perf_counter()
+    scanned = rows = 0
+    pending = []
+    for r in roots:
+        if inflight and len(pending) == inflight:
+            res = stmt.wait(pending.pop(0))
+            scanned += res.edges_scanned
+            rows += res.count
+            res.free()
+        if inflight:
+            pending.append(stmt.submit([r]))
+        else:
+            res = stmt.run_device([r])
+            scanned += res.edges_scanned
+            rows += res.count
+            res.free()
+    for tk in pending:
+        res = stmt.wait(tk)
+        scanned += res.edges_scanned
+        rows += res.count
+        res.free()
+    barrier()
+    go_s = time.perf_counter() - t1
+    stmt.free()
+    pairs = rmat.pick_pairs(ks, kd, 64, 7, verts=persons)
+    lat, paths = [], 0
+    for s_, t_ in pairs[:4]:
+        eng.find_path([s_], [t_], [1], 4, shortest=False)
+    for s_, t_ in pairs:
+        q0 = time.perf_counter()
+        paths += len(eng.find_path([s_], [t_], [1], 4, shortest=False))
+        lat.append(time.perf_counter() - q0)
+    eng.close()
+    lat_ms = np.array(lat) * 1e3
+    return {"graph": f"knows RMAT-{k} ({len(ks)} samples) + likes bipartite RMAT-{k - 1} to posts ({len(ls)} samples)",
+            "note": "synthetic substitute for LDBC SNB SF100 (no datagen or files offline)",
+            "load_seconds": round(load_s, 2),
+            "go4": {"query": "GO 4 STEPS FROM <root> OVER knows, likes", "roots": len(roots),
+                    "teps": scanned / go_s if go_s else None, "edges": scanned, "rows": rows,
+                    "seconds": round(go_s, 4)},
+            "find_all_path": {"query": "FIND ALL PATH FROM <s> TO <t> OVER knows UPTO 4 STEPS", "pairs": len(pairs),
+                              "paths": paths, "p50_ms": float(np.percentile(lat_ms, 50)),
+                              "p90_ms": float(np.percentile(lat_ms, 90)), "max_ms": float(lat_ms.max())}}
 
 
 def cpu_baseline(src, dst, w, roots, where, pairs, args):
