@@ -110,6 +110,8 @@ struct Workspace {
   uint32_t* dcnt = nullptr;
   uint8_t* dkinds = nullptr;
   uint32_t* bt = nullptr;         // VertexBackTracker roots [nv] (queries with $- / $var props)
+  uint8_t* walk_arena = nullptr;  // FIND ALL PATH level arrays (grow-only)
+  size_t walk_cap = 0;
   Ins* d_prog = nullptr;          // [MAX_TYPES_Q][MAX_PROGRAM]
   // FIND PATH (allocated on first use)
   PState* ps = nullptr;
@@ -1299,7 +1301,7 @@ void ws_destroy(Workspace* w) {
                   (void*)w->rlist, (void*)w->flags, (void*)w->tsplit,
                   (void*)w->q, (void*)w->rows,
                   (void*)w->d_row_cols, (void*)w->d_prog, (void*)w->dtab, (void*)w->dkeep, (void*)w->dseg,
-                  (void*)w->dcnt, (void*)w->dkinds, (void*)w->bt})
+                  (void*)w->dcnt, (void*)w->dkinds, (void*)w->bt, (void*)w->walk_arena})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)w->h_q, (void*)w->h_starts, (void*)w->h_prog, (void*)w->h_ps, (void*)w->h_path,
                   (void*)w->h_stage})
@@ -2744,15 +2746,31 @@ hipError_t ws_all_paths(Workspace* w, const PathTypes& fwd, int lab, uint32_t ep
                         uint32_t upto, const int64_t* d_vids, const uint8_t* visible, uint64_t max_walks,
                         std::vector<std::vector<int64_t>>* out, uint64_t* scanned) {
   if (upto > (uint32_t)WALK_MAX || fwd.n > MAX_TYPES_Q) return hipErrorInvalidValue;
+  // bump allocation from the workspace's walk arena (kept across queries, grown by doubling; an
+  // outgrown arena stays alive until this call ends, earlier levels still live in it)
   std::vector<void*> owned;
+  size_t used = 0;
   auto cleanup = [&]() {
     (void)hipStreamSynchronize(w->stream);
     for (void* p : owned) (void)hipFree(p);
   };
   auto alloc = [&](void** p, size_t b) -> hipError_t {
-    hipError_t e = hipMalloc(p, b < 8 ? 8 : b);
-    if (e == hipSuccess) owned.push_back(*p);
-    return e;
+    b = ((b ? b : 1) + 255) & ~(size_t)255;   // 256-byte aligned, never empty
+    if (used + b > w->walk_cap || !w->walk_arena) {
+      if (w->walk_arena) owned.push_back(w->walk_arena);
+      size_t cap = w->walk_cap ? w->walk_cap : ((size_t)1 << 24);
+      while (cap < b) cap *= 2;
+      cap *= 2;
+      w->walk_arena = nullptr;
+      w->walk_cap = 0;
+      hipError_t e = hipMalloc((void**)&w->walk_arena, cap);
+      if (e != hipSuccess) return e;
+      w->walk_cap = cap;
+      used = 0;
+    }
+    *p = w->walk_arena + used;
+    used += b;
+    return hipSuccess;
   };
 #define WALK_TRY(x)                      \
   do {                                   \
