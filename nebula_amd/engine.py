@@ -372,17 +372,8 @@ class Engine:
         """StorageServiceHandler::future_getBound: ``part_vids`` = [(part, vid), ...], ``returns`` =
         [(owner, id, name), ...] (owner 1 SOURCE, 2 DEST, 3 EDGE).  Returns a canonical dict of the
         QueryResponse (see :func:`gn_canonical`)."""
-        parts = np.ascontiguousarray([p for p, _ in part_vids], np.int32)
-        vids = np.ascontiguousarray([v for _, v in part_vids], np.int64)
-        et = np.ascontiguousarray(edge_types, np.int32)
-        rets = (L.nbg_prop_def * max(1, len(returns)))(
-            *[L.nbg_prop_def(o, i, n.encode()) for o, i, n in returns])
-        fb = (C.c_uint8 * max(1, len(filter))).from_buffer_copy(filter or b"\0")
-        req = L.nbg_gn_request(
-            parts.ctypes.data_as(C.POINTER(C.c_int32)) if len(parts) else None,
-            vids.ctypes.data_as(C.POINTER(C.c_int64)) if len(vids) else None, len(vids),
-            et.ctypes.data_as(C.POINTER(C.c_int32)) if len(et) else None, len(et),
-            C.cast(fb, C.POINTER(C.c_uint8)) if filter else None, len(filter), rets, len(returns))
+        keep = []
+        req = _gn_request(part_vids, edge_types, filter, returns, keep)
         out = C.c_void_p()
         self._check(self.lib.nbg_get_neighbors(self.h, C.byref(req), C.byref(out)), "get_neighbors")
         lib = self.lib
