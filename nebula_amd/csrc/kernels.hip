@@ -1209,7 +1209,7 @@ static double prof_bytes_path(const Prof::Rec& r, const PState& p) {
   switch (r.kid) {
     case K_RELIST: return 12.0 * (double)p.ln[i];
     case K_BFS: return 4.0 * (double)p.le[i];
-    case K_GATHER: return 8.0 * (double)p.lc[i];
+    case K_GATHER: return 8.0 * (double)p.lc[i];   // (+8 B per packed vertex when it sums degrees)
     case K_DEGSUM: return 12.0 * (double)p.ln[i];
     default: return 0.0;
   }
@@ -1884,11 +1884,23 @@ __global__ void __launch_bounds__(BLOCK) k_stamp(const uint32_t* __restrict__ id
   }
 }
 
+struct DegsumArgs {
+  int ntypes;
+  const uint32_t* row_ptr[MAX_TYPES_Q];
+  const uint8_t* visible;
+  uint32_t cap;
+};
+
+// Packs the NSHARD claim regions into the next frontier list; with a non-null `dsum` it also sums
+// the packed vertices' degrees (the next level's direction choice and grid bound), so a level
+// ends with one launch instead of gather + memset + degsum.
 __global__ void __launch_bounds__(BLOCK) k_gather(const uint32_t* __restrict__ scratch, uint64_t shard_cap,
                                                   const unsigned long long* __restrict__ shard_cnt,
                                                   uint32_t* __restrict__ out, unsigned long long* n_out,
-                                                  unsigned long long* c_rec) {
+                                                  unsigned long long* c_rec, DegsumArgs d,
+                                                  unsigned long long* dsum) {
   __shared__ unsigned long long pre[NSHARD + 1];
+  __shared__ unsigned long long red[WAVES];
   if (threadIdx.x == 0) {
     unsigned long long run = 0;
     for (int s = 0; s < NSHARD; ++s) {
@@ -1902,21 +1914,34 @@ __global__ void __launch_bounds__(BLOCK) k_gather(const uint32_t* __restrict__ s
     }
   }
   __syncthreads();
+  unsigned long long sum = 0;
   for (int s = 0; s < NSHARD; ++s) {
     const uint64_t cnt = pre[s + 1] - pre[s];
     const uint32_t* src = scratch + (uint64_t)s * shard_cap;
     uint32_t* dst = out + pre[s];
-    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * BLOCK)
-      dst[i] = src[i];
+    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * BLOCK) {
+      const uint32_t v = src[i];
+      dst[i] = v;
+      if (dsum && v != NO_ROW && (!d.visible || d.visible[v])) {
+        for (int t = 0; t < d.ntypes; ++t) {
+          const uint32_t deg = d.row_ptr[t][v + 1] - d.row_ptr[t][v];
+          sum += deg < d.cap ? deg : d.cap;
+        }
+      }
+    }
+  }
+  if (!dsum) return;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_down(sum, o, 64);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int i = 0; i < WAVES; ++i) t += red[i];
+    if (t) atomicAdd(dsum, t);
   }
 }
-
-struct DegsumArgs {
-  int ntypes;
-  const uint32_t* row_ptr[MAX_TYPES_Q];
-  const uint8_t* visible;
-  uint32_t cap;
-};
 
 __global__ void __launch_bounds__(BLOCK) k_degsum(const uint32_t* __restrict__ f,
                                                   const unsigned long long* __restrict__ np, DegsumArgs d,
@@ -1984,6 +2009,7 @@ __device__ __forceinline__ Cand shfl_cand(const Cand& c, int o) {
   return r;
 }
 constexpr int GREEDY_BLOCK = 1024;
+constexpr int GREEDY_U = 8;
 
 // Block-wide minimum; every thread gets the result.  INT64_MAX type marks "no candidate".
 __device__ Cand block_min(Cand c, Cand* lds) {
@@ -2040,12 +2066,26 @@ __global__ void __launch_bounds__(GREEDY_BLOCK) k_path_greedy(GreedyArgs g) {
         const uint32_t rs = g.row_ptr[t][v];
         uint32_t deg = g.row_ptr[t][v + 1] - rs;
         deg = deg < g.cap ? deg : g.cap;
-        for (uint32_t k = threadIdx.x; k < deg; k += GREEDY_BLOCK) {
-          const uint64_t j = (uint64_t)rs + k;
-          const uint32_t w = g.col[t][j];
-          if (!greedy_valid(g, w, pos + 1)) continue;
-          Cand x{(int64_t)g.type[t], g.rank[t] ? g.rank[t][j] : 0, g.dst_vid[t][j], w};
-          if (cand_less(x, best)) best = x;
+        // GREEDY_U neighbours per thread per pass: their column loads, then their label loads,
+        // are issued back to back (a hub's adjacency is otherwise one dependent load pair per
+        // neighbour per thread)
+        for (uint32_t k0 = 0; k0 < deg; k0 += GREEDY_BLOCK * GREEDY_U) {
+          uint32_t wv[GREEDY_U];
+#pragma unroll
+          for (int u = 0; u < GREEDY_U; ++u) {
+            const uint32_t k = k0 + (uint32_t)u * GREEDY_BLOCK + threadIdx.x;
+            wv[u] = k < deg ? g.col[t][(uint64_t)rs + k] : NO_ROW;
+          }
+          bool ok[GREEDY_U];
+#pragma unroll
+          for (int u = 0; u < GREEDY_U; ++u) ok[u] = greedy_valid(g, wv[u], pos + 1);
+#pragma unroll
+          for (int u = 0; u < GREEDY_U; ++u) {
+            if (!ok[u]) continue;
+            const uint64_t j = (uint64_t)rs + k0 + (uint32_t)u * GREEDY_BLOCK + threadIdx.x;
+            Cand x{(int64_t)g.type[t], g.rank[t] ? g.rank[t][j] : 0, g.dst_vid[t][j], wv[u]};
+            if (cand_less(x, best)) best = x;
+          }
         }
       }
     }
@@ -2073,7 +2113,16 @@ static void prof_end_p(Workspace* w, hipEvent_t a, int kid, int rec) {
   w->prof.pending.push_back({kid, rec, 0, a, b, 0, 0, true});
 }
 
-hipError_t ws_path_begin(Workspace* w, uint64_t scratch_entries, uint64_t list_entries) {
+static DegsumArgs degsum_args(const PathTypes& pt) {
+  DegsumArgs d{};
+  d.ntypes = pt.n;
+  for (int t = 0; t < pt.n; ++t) d.row_ptr[t] = pt.a[t].row_ptr;
+  d.visible = pt.n ? pt.a[0].visible : nullptr;
+  d.cap = pt.n ? pt.a[0].cap : 0xFFFFFFFFu;
+  return d;
+}
+
+hipError_t ws_path_begin(Workspace* w, uint64_t scratch_entries, uint64_t list_entries, bool zero_state) {
   if (!w->ps) {
     HIP_TRY(hipMalloc((void**)&w->ps, sizeof(PState)));
     HIP_TRY(hipHostMalloc((void**)&w->h_ps, sizeof(PState), hipHostMallocDefault));
@@ -2104,7 +2153,70 @@ hipError_t ws_path_begin(Workspace* w, uint64_t scratch_entries, uint64_t list_e
   }
   w->rec = 0;
   w->ppr = 0;
-  return hipMemsetAsync(w->ps, 0, sizeof(PState), w->stream);
+  return zero_state ? hipMemsetAsync(w->ps, 0, sizeof(PState), w->stream) : hipSuccess;
+}
+
+struct PairSetup {
+  uint32_t s, t;
+  uint32_t *slot_f, *slot_b, *slot_start;
+  int sf, sb, sst;
+  uint32_t *lab_f, *lab_b;
+  uint32_t stamp_f, stamp_b;
+  DegsumArgs df, db;
+  PState* ps;
+};
+
+__device__ unsigned long long degree_of(const DegsumArgs& d, uint32_t v) {
+  if (v == NO_ROW || (d.visible && !d.visible[v])) return 0;
+  unsigned long long sum = 0;
+  for (int t = 0; t < d.ntypes; ++t) {
+    const uint32_t deg = d.row_ptr[t][v + 1] - d.row_ptr[t][v];
+    sum += deg < d.cap ? deg : d.cap;
+  }
+  return sum;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_path_setup(PairSetup a) {
+  unsigned long long* p = reinterpret_cast<unsigned long long*>(a.ps);
+  for (unsigned i = threadIdx.x; i < sizeof(PState) / 8; i += BLOCK) p[i] = 0;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const bool hs = a.s != NO_ROW, ht = a.t != NO_ROW;
+  a.slot_f[0] = a.s;
+  a.slot_start[0] = a.s;
+  a.slot_b[0] = a.t;
+  a.ps->n[a.sf] = hs;
+  a.ps->n[a.sst] = hs;
+  a.ps->n[a.sb] = ht;
+  if (hs) a.lab_f[a.s] = a.stamp_f;
+  if (ht) a.lab_b[a.t] = a.stamp_b;
+  a.ps->dsum[0] = degree_of(a.df, a.s);
+  a.ps->dsum[1] = degree_of(a.db, a.t);
+}
+
+hipError_t ws_path_setup_pair(Workspace* w, const PathTypes& fwd, const PathTypes& bwd, uint32_t s, uint32_t t,
+                              int slot_f, int slot_b, int slot_start, int lab_f, uint32_t stamp_f, int lab_b,
+                              uint32_t stamp_b) {
+  static_assert(sizeof(PState) % 8 == 0, "PState is cleared in 8-byte words");
+  if (w->slot_cap < 1) return hipErrorInvalidValue;
+  PairSetup a{};
+  a.s = s;
+  a.t = t;
+  a.slot_f = w->slot[slot_f];
+  a.slot_b = w->slot[slot_b];
+  a.slot_start = w->slot[slot_start];
+  a.sf = slot_f;
+  a.sb = slot_b;
+  a.sst = slot_start;
+  a.lab_f = w->lab[lab_f];
+  a.lab_b = w->lab[lab_b];
+  a.stamp_f = stamp_f;
+  a.stamp_b = stamp_b;
+  a.df = degsum_args(fwd);
+  a.db = degsum_args(bwd);
+  a.ps = w->ps;
+  hipLaunchKernelGGL(k_path_setup, dim3(1), dim3(BLOCK), 0, w->stream, a);
+  return hipGetLastError();
 }
 
 uint32_t ws_path_epoch(Workspace* w, int l) {
@@ -2152,11 +2264,7 @@ hipError_t ws_path_stamp(Workspace* w, int s, uint64_t n_bound, int l, uint32_t 
 }
 
 hipError_t ws_path_degsum(Workspace* w, int s, uint64_t n_bound, const PathTypes& pt, int side) {
-  DegsumArgs d{};
-  d.ntypes = pt.n;
-  for (int t = 0; t < pt.n; ++t) d.row_ptr[t] = pt.a[t].row_ptr;
-  d.visible = pt.n ? pt.a[0].visible : nullptr;
-  d.cap = pt.n ? pt.a[0].cap : 0xFFFFFFFFu;
+  const DegsumArgs d = degsum_args(pt);
   unsigned nb = (unsigned)cdiv(n_bound ? n_bound : 1, BLOCK);
   if (nb > 2048) nb = 2048;
   const int rec = w->rec < PATH_REC ? w->rec++ : PATH_REC - 1;
@@ -2220,8 +2328,10 @@ hipError_t ws_path_level(Workspace* w, const PathTypes& pt, int src, uint64_t n_
   uint64_t gb = cdiv(n_bound + e_bound + 1, (uint64_t)BLOCK * 4);
   unsigned grid = (unsigned)(gb < 1 ? 1 : (gb > 1024 ? 1024 : gb));
   hipEvent_t p = prof_begin_p(w, K_GATHER);
+  // a clamped record (rec == PATH_REC - 1 reused) accumulates: the degree sum then only over-bounds
   hipLaunchKernelGGL(k_gather, dim3(grid), dim3(BLOCK), 0, w->stream, w->pscratch, shard_cap, w->ps->shard,
-                     w->slot[dst], &w->ps->n[dst], &w->ps->lc[rec]);
+                     w->slot[dst], &w->ps->n[dst], &w->ps->lc[rec],
+                     lv.deg ? degsum_args(*lv.deg) : DegsumArgs{}, lv.deg ? &w->ps->ld[rec] : nullptr);
   prof_end_p(w, p, K_GATHER, rec);
   return hipGetLastError();
 }

@@ -275,6 +275,7 @@ struct PState {                      // device-resident sizes of one FIND PATH q
   unsigned long long ln[PATH_REC];   // per expansion record: frontier size, edges, claims
   unsigned long long le[PATH_REC];
   unsigned long long lc[PATH_REC];
+  unsigned long long ld[PATH_REC];   // degree sum of the level's output list (fused into k_gather)
 };
 
 struct PathTypes {                   // the CSRs one search direction expands (one per OVER type)
@@ -351,7 +352,13 @@ void ws_host_gstats(Workspace* w, unsigned long long* err, unsigned long long* s
 
 // FIND SHORTEST PATH (kernels.hip).  Frontier lists live in numbered device slots; PState sizes
 // are read back by ws_path_sync.  All calls enqueue on the workspace stream.
-hipError_t ws_path_begin(Workspace* w, uint64_t scratch_entries, uint64_t list_entries);
+hipError_t ws_path_begin(Workspace* w, uint64_t scratch_entries, uint64_t list_entries, bool zero_state = true);
+// One-pair set-up in one launch (replaces the PState clear, three single-id uploads, two stamps
+// and two degree sums): slots f/b/start = {s}, {t}, {s}; labels lab_f[s], lab_b[t] stamped;
+// PState.dsum[0] = out-degree of s over fwd, dsum[1] = in-degree of t over bwd.
+hipError_t ws_path_setup_pair(Workspace* w, const PathTypes& fwd, const PathTypes& bwd, uint32_t s, uint32_t t,
+                              int slot_f, int slot_b, int slot_start, int lab_f, uint32_t stamp_f, int lab_b,
+                              uint32_t stamp_b);
 uint32_t ws_path_epoch(Workspace* w, int lab);                    // fresh epoch for one label array
 uint32_t* ws_path_slot(Workspace* w, int slot);
 hipError_t ws_path_upload(Workspace* w, int slot, const uint32_t* ids, uint64_t n);
@@ -371,6 +378,8 @@ struct PathLevel {
   int meet_slot = -1;
   int tlab = -1;           // target label (-1 none)
   uint32_t tstamp = 0;
+  const PathTypes* deg = nullptr;   // non-null: k_gather also sums the output list's degrees over
+                                    // these CSRs into PState.ld[rec] (replaces a k_degsum launch)
 };
 hipError_t ws_path_level(Workspace* w, const PathTypes& pt, int src, uint64_t n_bound, uint64_t e_bound, int dst,
                          const PathLevel& lv);

@@ -67,6 +67,23 @@ hipError_t level(PathCtx& c, const PathTypes& pt, int src, uint64_t n_bound, uin
                 : ws_path_level(c.ws, pt, src, n_bound, e_bound, dst, lv);
 }
 
+// One level plus the degree sum of its output list over the same CSRs (the next level's bound
+// and, bidirectionally, its direction).  Single engine: summed by the level's k_gather into
+// PState.ld[rec]; partitioned: a collective k_degsum into PState.dsum[side].  *rec = the level's
+// PState record.
+hipError_t level_ds(PathCtx& c, const PathTypes& pt, int src, uint64_t n_bound, uint64_t e_bound, int dst,
+                    PathLevel lv, int side, int* rec) {
+  if (!c.part) lv.deg = &pt;
+  hipError_t he = level(c, pt, src, n_bound, e_bound, dst, lv);
+  *rec = ws_path_last_rec(c.ws);
+  if (he == hipSuccess && c.part) he = ws_path_degsum(c.ws, dst, e_bound ? e_bound : 1, pt, side);
+  return he;
+}
+
+uint64_t level_dsum(const PathCtx& c, const PState& ps, int rec, int side) {
+  return c.part ? ps.dsum[side] : ps.ld[rec >= 0 && rec < PATH_REC ? rec : PATH_REC - 1];
+}
+
 // sizes of the whole graph (summed over ranks when partitioned)
 hipError_t sync(PathCtx& c, PState* ps) {
   return c.part ? ws_path_sync_part(c.ws, ps) : ws_path_sync(c.ws, ps, nullptr, 0);
@@ -133,13 +150,17 @@ int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_pat
   const uint32_t ef = ws_path_epoch(ws, LAB_F), eb = ws_path_epoch(ws, LAB_B), em = ws_path_epoch(ws, LAB_M);
   hipError_t he = hipSuccess;
   auto T = [&](hipError_t e) { if (he == hipSuccess) he = e; };
-  T(upload1(ws, S_F0, s));
-  T(upload1(ws, S_B0, t));
-  T(upload1(ws, S_START, s));
-  T(ws_path_stamp(ws, S_F0, 1, LAB_F, stamp(ef, 0)));
-  T(ws_path_stamp(ws, S_B0, 1, LAB_B, stamp(eb, 0)));
-  T(ws_path_degsum(ws, S_F0, 1, c.fwd, 0));
-  T(ws_path_degsum(ws, S_B0, 1, c.bwd, 1));
+  if (!c.part) {   // the PState clear was left to this launch (ws_path_begin zero_state=false)
+    T(ws_path_setup_pair(ws, c.fwd, c.bwd, s, t, S_F0, S_B0, S_START, LAB_F, stamp(ef, 0), LAB_B, stamp(eb, 0)));
+  } else {
+    T(upload1(ws, S_F0, s));
+    T(upload1(ws, S_B0, t));
+    T(upload1(ws, S_START, s));
+    T(ws_path_stamp(ws, S_F0, 1, LAB_F, stamp(ef, 0)));
+    T(ws_path_stamp(ws, S_B0, 1, LAB_B, stamp(eb, 0)));
+    T(ws_path_degsum(ws, S_F0, 1, c.fwd, 0));
+    T(ws_path_degsum(ws, S_B0, 1, c.bwd, 1));
+  }
   PState ps;
   T(sync(c, &ps));
   if (he != hipSuccess) return dev_fail(c.E, he, "path setup");
@@ -153,31 +174,31 @@ int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_pat
     lv.mlab = forward ? LAB_B : LAB_F;
     lv.mepoch = forward ? eb : ef;
     lv.meet_slot = S_MEET;
+    int rec = -1;
     if (forward) {
       lv.lab = LAB_F;
       lv.stamp = stamp(ef, (uint32_t)kf + 1);
       lv.mstamp = stamp(em, (uint32_t)kf + 1);
-      T(level(c, c.fwd, fcur, nf, dsf, fcur ^ 1, lv));
+      T(level_ds(c, c.fwd, fcur, nf, dsf, fcur ^ 1, lv, 0, &rec));
       fcur ^= 1;
       ++kf;
-      T(ws_path_degsum(ws, fcur, dsf ? dsf : 1, c.fwd, 0));
     } else {
       lv.lab = LAB_B;
       lv.stamp = stamp(eb, (uint32_t)kb + 1);
       lv.mstamp = stamp(em, (uint32_t)kf);
-      T(level(c, c.bwd, bcur, nbk, dsb, bcur ^ 1, lv));
+      T(level_ds(c, c.bwd, bcur, nbk, dsb, bcur ^ 1, lv, 1, &rec));
       bcur ^= 1;
       ++kb;
-      T(ws_path_degsum(ws, bcur, dsb ? dsb : 1, c.bwd, 1));
     }
-    const int rec = ws_path_last_rec(ws) - 1;   // the level's record (degsum took the next one)
     T(sync(c, &ps));
     if (he != hipSuccess) return dev_fail(c.E, he, "path level");
     if (rec >= 0 && rec < PATH_REC) c.edges += ps.le[rec];
     nf = ps.n[fcur];
     nbk = ps.n[bcur];
-    dsf = ps.dsum[0];
-    dsb = ps.dsum[1];
+    if (forward)
+      dsf = level_dsum(c, ps, rec, 0);
+    else
+      dsb = level_dsum(c, ps, rec, 1);
     if (forward) fn.push_back(nf);
     if (ps.n[S_MEET]) { met = true; break; }
     if (nf == 0 || nbk == 0) break;
@@ -228,15 +249,14 @@ int32_t one_sided(PathCtx& c, const std::vector<uint32_t>& S, const std::vector<
     lv.stamp = stamp(ef, l);
     lv.tlab = LAB_B;
     lv.tstamp = stamp(et, 0);
-    T(level(c, c.fwd, cur, n, ds, cur ^ 1, lv));
-    const int rec = ws_path_last_rec(ws);
+    int rec = -1;
+    T(level_ds(c, c.fwd, cur, n, ds, cur ^ 1, lv, 0, &rec));
     cur ^= 1;
-    T(ws_path_degsum(ws, cur, ds ? ds : 1, c.fwd, 0));
     T(sync(c, &ps));
     if (he != hipSuccess) return dev_fail(c.E, he, "path level");
     if (rec >= 0 && rec < PATH_REC) c.edges += ps.le[rec];
     n = ps.n[cur];
-    ds = ps.dsum[0];
+    ds = level_dsum(c, ps, rec, 0);
     level_n.push_back(n);
     if (n == 0 || ps.found >= Tg.size()) break;
   }
@@ -291,13 +311,13 @@ int32_t all_paths(PathCtx& c, const std::vector<uint32_t>& S, const std::vector<
     PathLevel lv;
     lv.lab = LAB_B;
     lv.stamp = stamp(eb, l);
-    Tr(level(c, c.bwd, cur, n, ds, cur ^ 1, lv));
+    int rec = -1;
+    Tr(level_ds(c, c.bwd, cur, n, ds, cur ^ 1, lv, 1, &rec));
     cur ^= 1;
-    Tr(ws_path_degsum(ws, cur, ds ? ds : 1, c.bwd, 1));
     Tr(sync(c, &ps));
     if (he != hipSuccess) return dev_fail(c.E, he, "path level");
     n = ps.n[cur];
-    ds = ps.dsum[1];
+    ds = level_dsum(c, ps, rec, 1);
   }
   uint64_t scanned = 0;
   static const uint64_t max_walks = getenv("NBG_MAX_WALKS") ? strtoull(getenv("NBG_MAX_WALKS"), nullptr, 10)
@@ -408,7 +428,8 @@ extern "C" int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* rq, nbg_
     add(c.fwd, t);
     add(c.bwd, -t);
   }
-  hipError_t he = ws_path_begin(c.ws, 0, E.snap.nv + S.size() + Tg.size() + 1024);
+  const bool pair = rq->shortest && Sv.size() == 1 && Tv.size() == 1 && Sv[0] != Tv[0];
+  hipError_t he = ws_path_begin(c.ws, 0, E.snap.nv + S.size() + Tg.size() + 1024, !(pair && !c.part));
   if (he != hipSuccess) { delete res; return dev_fail(E, he, "path workspace"); }
   int32_t rc;
   if (!rq->shortest) {
@@ -416,7 +437,7 @@ extern "C" int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* rq, nbg_
     for (uint32_t d : Tg)
       if (d != NO_ROW) Tl.push_back(d);
     rc = all_paths(c, S, Tl, rq->upto, res);
-  } else if (Sv.size() == 1 && Tv.size() == 1 && Sv[0] != Tv[0])
+  } else if (pair)
     rc = bidirectional(c, S.empty() ? NO_ROW : S[0], Tg[0], rq->upto, res);
   else
     rc = one_sided(c, S, Tg, Sv.size(), rq->upto, res);
