@@ -41,7 +41,7 @@ constexpr int EXPAND_GRID = 2048;                // persistent k_expand grid (8 
 enum KernelId { K_RELIST = 0, K_EXPAND_MARK, K_COMPACT, K_EXPAND_FINAL, K_BFS, K_GATHER, K_DEGSUM, K_GREEDY,
                 K_STAMP, K_PACK, K_ALLTOALL, K_BITS_COMPACT, K_COUNT };
 static const char* const kKernelNames[K_COUNT] = {"k_relist", "k_expand<MARK>", "k_compact", "k_expand<FINAL>",
-                                                  "k_expand<BFS>", "k_gather", "k_degsum", "k_path_greedy",
+                                                  "k_expand<BFS>", "k_gather", "k_degsum", "k_greedy",
                                                   "k_stamp", "k_pack_bits", "alltoall(xGMI)", "k_bits_compact"};
 constexpr int BITS_BLOCK = BLOCK * 16;           // k_bits_compact: vertices (bits) per block
 
@@ -259,7 +259,7 @@ __global__ void __launch_bounds__(BLOCK) k_relist(const uint32_t* __restrict__ i
       *o.zero_next = 0;
       if (o.stat_n) *o.stat_n = n;
     }
-    if (reset && threadIdx.x < NSHARD) reset[threadIdx.x] = 0;   // BFS claim counters of the last level
+    if (reset && threadIdx.x == 0) *reset = 0;   // the length of the list the expansion appends to
   }
   const uint64_t base = (uint64_t)blockIdx.x * RL_TILE + (uint64_t)threadIdx.x * RL_ITEMS;
   if ((uint64_t)blockIdx.x * RL_TILE >= n) return;
@@ -466,9 +466,28 @@ __device__ __forceinline__ void run_program(const Ins* __restrict__ prog, int pc
 // wins as in the reference's unordered iteration) for queries that read $- / $var props
 enum Mode { MARK = 0, FINAL = 1, BFS = 2, FINALF = 3, FINALD = 4, MARKB = 5 };
 
+struct DegsumArgs {
+  int ntypes;
+  const uint32_t* row_ptr[MAX_TYPES_Q];
+  const uint8_t* visible;
+  uint32_t cap;
+};
+
+__device__ unsigned long long degree_of(const DegsumArgs& d, uint32_t v) {
+  if (v == NO_ROW || (d.visible && !d.visible[v])) return 0;
+  unsigned long long sum = 0;
+  for (int t = 0; t < d.ntypes; ++t) {
+    const uint32_t deg = d.row_ptr[t][v + 1] - d.row_ptr[t][v];
+    sum += deg < d.cap ? deg : d.cap;
+  }
+  return sum;
+}
+
 // BFS-mode expansion (FIND SHORTEST PATH): every neighbour w is claimed at most once per epoch by
-// a CAS on its label (epoch << LVL_BITS | level); winners are appended, one atomic per tile on a
-// sharded counter, to NSHARD regions of `out` that k_gather then packs into the next frontier.
+// a CAS on its label (epoch << LVL_BITS | level); winners are appended, one atomic per wave tile,
+// straight to the next frontier list (`out`, count `*out_n`).  With `dsum` set, each tile also
+// adds its claimed vertices' degrees over `deg` (the next level's bound and direction) with one
+// atomic.
 struct BfsParams {
   uint32_t* lab;                  // claim labels
   uint32_t stamp;                 // claimed label value
@@ -484,9 +503,10 @@ struct BfsParams {
   const uint32_t* tlab;           // targets (nullable): claimed w with tlab[w] == tstamp counts
   uint32_t tstamp;
   unsigned long long* found;
-  uint32_t* out;                  // shard regions [NSHARD][shard_cap]
-  uint64_t shard_cap;
-  unsigned long long* shard_cnt;  // [NSHARD]
+  uint32_t* out;                  // next frontier list (a level claims <= nv vertices)
+  unsigned long long* out_n;      // its length, zero before the level
+  DegsumArgs deg;
+  unsigned long long* dsum;       // nullable
 };
 
 struct FinalParams {
@@ -797,18 +817,17 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
         if (bp.mlab && (bp.mlab[x] >> LVL_BITS) == bp.mepoch) mmask |= 1u << i;
         if (bp.tlab && bp.tlab[x] == bp.tstamp) atomicAdd(bp.found, 1ull);
       }
-      // one atomic per wave tile on a sharded claim counter
+      // one atomic per wave tile on the list length
       uint32_t pre[VT], run = 0;
 #pragma unroll
       for (int i = 0; i < VT; ++i) {
         pre[i] = run;
         run += (uint32_t)__popcll(__ballot((cmask >> i) & 1u));
       }
-      const uint64_t shard = t % NSHARD;
       unsigned long long base = 0;
-      if (lane == 0 && run) base = atomicAdd(bp.shard_cnt + shard, (unsigned long long)run);
+      if (lane == 0 && run) base = atomicAdd(bp.out_n, (unsigned long long)run);
       base = __shfl(base, 0, 64);
-      uint32_t* const region = bp.out + shard * bp.shard_cap + base;
+      uint32_t* const region = bp.out + base;
 #pragma unroll
       for (int i = 0; i < VT; ++i) {
         const bool c = (cmask >> i) & 1u;
@@ -825,6 +844,15 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
             bp.mout[wv[i]] = bp.mstamp;
           }
         }
+      }
+      if (bp.dsum && run) {
+        unsigned long long ds = 0;
+#pragma unroll
+        for (int i = 0; i < VT; ++i)
+          if ((cmask >> i) & 1u) ds += degree_of(bp.deg, wv[i]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) ds += __shfl_down(ds, o, 64);
+        if (lane == 0 && ds) atomicAdd(bp.dsum, ds);
       }
     } else {
       // phase A: WHERE for every item of the tile (VT items per lane, striped)
@@ -1869,10 +1897,11 @@ void ws_host_gstats(Workspace* w, unsigned long long* err, unsigned long long* s
 // ============================================================================= FIND SHORTEST PATH
 // Bidirectional BFS over epoch-stamped labels (path.cpp drives it level by level):
 //   k_expand<BFS>  claims neighbours (CAS on the label), detects meets, appends to claim shards
-//   k_gather       packs the NSHARD claim regions into the next frontier list
+//   (claims append straight to the next frontier slot, one atomic per wave tile)
 //   k_degsum       degree sum of a frontier (which side to expand next)
 //   k_stamp        label a list (sources, targets, level-0 vertices)
-//   k_path_greedy  lexicographically smallest shortest path through the B-sets (one workgroup)
+//   k_greedy_start / k_greedy_hop  lexicographically smallest shortest path through the B-sets
+//                  (one launch per hop; a hop's adjacency is scanned by GREEDY_HOP_BLOCKS workgroups)
 
 __global__ void __launch_bounds__(BLOCK) k_stamp(const uint32_t* __restrict__ ids,
                                                  const unsigned long long* __restrict__ np,
@@ -1881,65 +1910,6 @@ __global__ void __launch_bounds__(BLOCK) k_stamp(const uint32_t* __restrict__ id
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (uint64_t)gridDim.x * BLOCK) {
     uint32_t v = ids[i];
     if (v != NO_ROW) lab[v] = stamp;
-  }
-}
-
-struct DegsumArgs {
-  int ntypes;
-  const uint32_t* row_ptr[MAX_TYPES_Q];
-  const uint8_t* visible;
-  uint32_t cap;
-};
-
-// Packs the NSHARD claim regions into the next frontier list; with a non-null `dsum` it also sums
-// the packed vertices' degrees (the next level's direction choice and grid bound), so a level
-// ends with one launch instead of gather + memset + degsum.
-__global__ void __launch_bounds__(BLOCK) k_gather(const uint32_t* __restrict__ scratch, uint64_t shard_cap,
-                                                  const unsigned long long* __restrict__ shard_cnt,
-                                                  uint32_t* __restrict__ out, unsigned long long* n_out,
-                                                  unsigned long long* c_rec, DegsumArgs d,
-                                                  unsigned long long* dsum) {
-  __shared__ unsigned long long pre[NSHARD + 1];
-  __shared__ unsigned long long red[WAVES];
-  if (threadIdx.x == 0) {
-    unsigned long long run = 0;
-    for (int s = 0; s < NSHARD; ++s) {
-      pre[s] = run;
-      run += shard_cnt[s];
-    }
-    pre[NSHARD] = run;
-    if (blockIdx.x == 0) {
-      *n_out = run;
-      if (c_rec) *c_rec = run;
-    }
-  }
-  __syncthreads();
-  unsigned long long sum = 0;
-  for (int s = 0; s < NSHARD; ++s) {
-    const uint64_t cnt = pre[s + 1] - pre[s];
-    const uint32_t* src = scratch + (uint64_t)s * shard_cap;
-    uint32_t* dst = out + pre[s];
-    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * BLOCK) {
-      const uint32_t v = src[i];
-      dst[i] = v;
-      if (dsum && v != NO_ROW && (!d.visible || d.visible[v])) {
-        for (int t = 0; t < d.ntypes; ++t) {
-          const uint32_t deg = d.row_ptr[t][v + 1] - d.row_ptr[t][v];
-          sum += deg < d.cap ? deg : d.cap;
-        }
-      }
-    }
-  }
-  if (!dsum) return;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) sum += __shfl_down(sum, o, 64);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (lane == 0) red[w] = sum;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long t = 0;
-    for (int i = 0; i < WAVES; ++i) t += red[i];
-    if (t) atomicAdd(dsum, t);
   }
 }
 
@@ -1989,6 +1959,9 @@ struct GreedyArgs {
   const unsigned long long* nstarts;
   int64_t* out;                 // [v0, t0, r0, v1, ...]
   unsigned long long* err;
+  unsigned long long* gticket;  // PState::gticket / gv / gpart
+  unsigned long long* gv;
+  unsigned long long* gpart;
 };
 
 struct Cand {                   // (type, rank, vid) key + dense id of the vertex
@@ -2008,10 +1981,12 @@ __device__ __forceinline__ Cand shfl_cand(const Cand& c, int o) {
   r.d = __shfl_down(c.d, o, 64);
   return r;
 }
-constexpr int GREEDY_BLOCK = 1024;
-constexpr int GREEDY_U = 8;
+constexpr int GH_THREADS = 256;
+constexpr int GH_U = 4;          // neighbours per thread per pass (loads issued back to back)
+static_assert(sizeof(Cand) == 32, "Cand travels through PState::gpart as 4 words");
 
 // Block-wide minimum; every thread gets the result.  INT64_MAX type marks "no candidate".
+template <int NT>
 __device__ Cand block_min(Cand c, Cand* lds) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -2023,12 +1998,12 @@ __device__ Cand block_min(Cand c, Cand* lds) {
   __syncthreads();
   if (threadIdx.x == 0) {
     Cand b = lds[0];
-    for (int i = 1; i < GREEDY_BLOCK / 64; ++i)
+    for (int i = 1; i < NT / 64; ++i)
       if (cand_less(lds[i], b)) b = lds[i];
-    lds[GREEDY_BLOCK / 64] = b;
+    lds[NT / 64] = b;
   }
   __syncthreads();
-  Cand r = lds[GREEDY_BLOCK / 64];
+  Cand r = lds[NT / 64];
   __syncthreads();
   return r;
 }
@@ -2042,65 +2017,98 @@ __device__ __forceinline__ bool greedy_valid(const GreedyArgs& g, uint32_t w, in
   return g.lab_b[w] == ((g.eb << LVL_BITS) | (uint32_t)(g.L - pos));
 }
 
-__global__ void __launch_bounds__(GREEDY_BLOCK) k_path_greedy(GreedyArgs g) {
-  __shared__ Cand lds[GREEDY_BLOCK / 64 + 1];
+__device__ __forceinline__ uint64_t ld_agent(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Greedy reconstruction, step 0 (one workgroup): v0 = the smallest vid among the start
+// candidates (dense ids are in vid order).
+__global__ void __launch_bounds__(GH_THREADS) k_greedy_start(GreedyArgs g) {
+  __shared__ Cand lds[GH_THREADS / 64 + 1];
   const Cand none{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
-  // v0 = smallest vid among the start candidates (dense ids are in vid order)
   Cand c = none;
   const uint64_t ns = *g.nstarts;
-  for (uint64_t i = threadIdx.x; i < ns; i += GREEDY_BLOCK) {
-    uint32_t d = g.starts[i];
+  for (uint64_t i = threadIdx.x; i < ns; i += GH_THREADS) {
+    const uint32_t d = g.starts[i];
     if (d != NO_ROW && (int64_t)d < c.t) c = Cand{(int64_t)d, 0, 0, d};
   }
-  c = block_min(c, lds);
-  uint32_t v = c.d;
-  if (v == NO_ROW) {
-    if (threadIdx.x == 0) *g.err = 1;
-    return;
-  }
-  if (threadIdx.x == 0) g.out[0] = g.vids[v];
-  for (int pos = 0; pos < g.L; ++pos) {
-    Cand best = none;
-    if (!g.visible || g.visible[v]) {
-      for (int t = 0; t < g.ntypes; ++t) {
-        const uint32_t rs = g.row_ptr[t][v];
-        uint32_t deg = g.row_ptr[t][v + 1] - rs;
-        deg = deg < g.cap ? deg : g.cap;
-        // GREEDY_U neighbours per thread per pass: their column loads, then their label loads,
-        // are issued back to back (a hub's adjacency is otherwise one dependent load pair per
-        // neighbour per thread)
-        for (uint32_t k0 = 0; k0 < deg; k0 += GREEDY_BLOCK * GREEDY_U) {
-          uint32_t wv[GREEDY_U];
+  c = block_min<GH_THREADS>(c, lds);
+  if (threadIdx.x != 0) return;
+  *g.gticket = 0;
+  *g.gv = c.d;
+  if (c.d == NO_ROW)
+    *g.err = 1;
+  else
+    g.out[0] = g.vids[c.d];
+}
+
+// Greedy reconstruction, hop pos (GREEDY_HOP_BLOCKS workgroups): the minimum (type, rank, dst)
+// edge from the current vertex into B[pos + 1].  The current vertex may be a hub, so its
+// adjacency is scanned by many CUs; each workgroup leaves its minimum in PState::gpart and the
+// last one to finish (ticket) reduces them, records the hop and moves the current vertex.
+__global__ void __launch_bounds__(GH_THREADS) k_greedy_hop(GreedyArgs g, int pos) {
+  __shared__ Cand lds[GH_THREADS / 64 + 1];
+  __shared__ int s_last;
+  const Cand none{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
+  const uint32_t v = (uint32_t)*g.gv;
+  if (v == NO_ROW) return;   // an earlier step failed (err is set)
+  Cand best = none;
+  if (!g.visible || g.visible[v]) {
+    for (int t = 0; t < g.ntypes; ++t) {
+      const uint32_t rs = g.row_ptr[t][v];
+      uint32_t deg = g.row_ptr[t][v + 1] - rs;
+      deg = deg < g.cap ? deg : g.cap;
+      const uint32_t stride = gridDim.x * GH_THREADS * GH_U;
+      for (uint32_t k0 = blockIdx.x * GH_THREADS * GH_U; k0 < deg; k0 += stride) {
+        uint32_t wv[GH_U];
 #pragma unroll
-          for (int u = 0; u < GREEDY_U; ++u) {
-            const uint32_t k = k0 + (uint32_t)u * GREEDY_BLOCK + threadIdx.x;
-            wv[u] = k < deg ? g.col[t][(uint64_t)rs + k] : NO_ROW;
-          }
-          bool ok[GREEDY_U];
+        for (int u = 0; u < GH_U; ++u) {
+          const uint32_t k = k0 + (uint32_t)u * GH_THREADS + threadIdx.x;
+          wv[u] = k < deg ? g.col[t][(uint64_t)rs + k] : NO_ROW;
+        }
+        bool ok[GH_U];
 #pragma unroll
-          for (int u = 0; u < GREEDY_U; ++u) ok[u] = greedy_valid(g, wv[u], pos + 1);
+        for (int u = 0; u < GH_U; ++u) ok[u] = greedy_valid(g, wv[u], pos + 1);
 #pragma unroll
-          for (int u = 0; u < GREEDY_U; ++u) {
-            if (!ok[u]) continue;
-            const uint64_t j = (uint64_t)rs + k0 + (uint32_t)u * GREEDY_BLOCK + threadIdx.x;
-            Cand x{(int64_t)g.type[t], g.rank[t] ? g.rank[t][j] : 0, g.dst_vid[t][j], wv[u]};
-            if (cand_less(x, best)) best = x;
-          }
+        for (int u = 0; u < GH_U; ++u) {
+          if (!ok[u]) continue;
+          const uint64_t j = (uint64_t)rs + k0 + (uint32_t)u * GH_THREADS + threadIdx.x;
+          Cand x{(int64_t)g.type[t], g.rank[t] ? g.rank[t][j] : 0, g.dst_vid[t][j], wv[u]};
+          if (cand_less(x, best)) best = x;
         }
       }
     }
-    best = block_min(best, lds);
-    if (best.d == NO_ROW) {
-      if (threadIdx.x == 0) *g.err = 1;
-      return;
-    }
-    if (threadIdx.x == 0) {
-      g.out[1 + 3 * pos] = best.t;
-      g.out[2 + 3 * pos] = best.r;
-      g.out[3 + 3 * pos] = best.v;
-    }
-    v = best.d;
   }
+  best = block_min<GH_THREADS>(best, lds);
+  unsigned long long* part = g.gpart + 4 * blockIdx.x;
+  if (threadIdx.x == 0) {
+    part[0] = (unsigned long long)best.t;
+    part[1] = (unsigned long long)best.r;
+    part[2] = (unsigned long long)best.v;
+    part[3] = best.d;
+    __threadfence();
+    s_last = atomicAdd(g.gticket, 1ull) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  Cand c = none;
+  if (threadIdx.x < gridDim.x) {
+    const unsigned long long* q = g.gpart + 4 * threadIdx.x;
+    c = Cand{(int64_t)ld_agent(q), (int64_t)ld_agent(q + 1), (int64_t)ld_agent(q + 2), (uint32_t)ld_agent(q + 3)};
+  }
+  c = block_min<GH_THREADS>(c, lds);
+  if (threadIdx.x != 0) return;
+  *g.gticket = 0;
+  if (c.d == NO_ROW) {
+    *g.err = 1;
+    *g.gv = NO_ROW;
+    return;
+  }
+  g.out[1 + 3 * pos] = c.t;
+  g.out[2 + 3 * pos] = c.r;
+  g.out[3 + 3 * pos] = c.v;
+  *g.gv = c.d;
 }
 
 // ----------------------------------------------------------------------------- path host side
@@ -2165,16 +2173,6 @@ struct PairSetup {
   DegsumArgs df, db;
   PState* ps;
 };
-
-__device__ unsigned long long degree_of(const DegsumArgs& d, uint32_t v) {
-  if (v == NO_ROW || (d.visible && !d.visible[v])) return 0;
-  unsigned long long sum = 0;
-  for (int t = 0; t < d.ntypes; ++t) {
-    const uint32_t deg = d.row_ptr[t][v + 1] - d.row_ptr[t][v];
-    sum += deg < d.cap ? deg : d.cap;
-  }
-  return sum;
-}
 
 __global__ void __launch_bounds__(BLOCK) k_path_setup(PairSetup a) {
   unsigned long long* p = reinterpret_cast<unsigned long long*>(a.ps);
@@ -2278,16 +2276,7 @@ hipError_t ws_path_degsum(Workspace* w, int s, uint64_t n_bound, const PathTypes
 
 hipError_t ws_path_level(Workspace* w, const PathTypes& pt, int src, uint64_t n_bound, uint64_t e_bound, int dst,
                          const PathLevel& lv) {
-  // claim shards: a shard's count is bounded by its tiles over all types of this level
-  uint64_t shard_cap = 0;
-  for (int t = 0; t < pt.n; ++t) shard_cap += ws_shard_cap(n_bound, e_bound);
-  if (shard_cap * NSHARD > w->pscratch_cap) {
-    HIP_TRY(hipStreamSynchronize(w->stream));
-    if (w->pscratch) HIP_TRY(hipFree(w->pscratch));
-    w->pscratch = nullptr;
-    w->pscratch_cap = shard_cap * NSHARD;
-    HIP_TRY(hipMalloc((void**)&w->pscratch, w->pscratch_cap * sizeof(uint32_t)));
-  }
+  // claims append straight to slot dst (a level claims each vertex at most once: <= nv entries)
   BfsParams bp{};
   bp.lab = w->lab[lv.lab];
   bp.stamp = lv.stamp;
@@ -2302,10 +2291,11 @@ hipError_t ws_path_level(Workspace* w, const PathTypes& pt, int src, uint64_t n_
     bp.meet_n = &w->ps->n[lv.meet_slot];
   }
   if (lv.tlab >= 0) { bp.tlab = w->lab[lv.tlab]; bp.tstamp = lv.tstamp; bp.found = &w->ps->found; }
-  bp.out = w->pscratch;
-  bp.shard_cap = shard_cap;
-  bp.shard_cnt = w->ps->shard;
   const int rec = w->rec < PATH_REC ? w->rec++ : PATH_REC - 1;
+  bp.out = w->slot[dst];
+  bp.out_n = &w->ps->n[dst];
+  // a clamped record (rec == PATH_REC - 1 reused) accumulates: the degree sum then only over-bounds
+  if (lv.deg) { bp.deg = degsum_args(*lv.deg); bp.dsum = &w->ps->ld[rec]; }
   for (int t = 0; t < pt.n; ++t) {
     ExpandArgs a = pt.a[t];
     unsigned long long* acc = &w->ps->acc[w->ppr];
@@ -2315,7 +2305,7 @@ hipError_t ws_path_level(Workspace* w, const PathTypes& pt, int src, uint64_t n_
     hipLaunchKernelGGL(k_relist, dim3((unsigned)cdiv(n_bound ? n_bound : 1, RL_TILE)), dim3(BLOCK), 0, w->stream,
                        w->slot[src], &w->ps->n[src], 0, 0u, InlineIds{}, deg_of(a),
                        list_out(w, w->rlist, acc, other, t == 0 ? &w->ps->ln[rec] : nullptr),
-                       t == 0 ? w->ps->shard : (unsigned long long*)nullptr);
+                       t == 0 ? &w->ps->n[dst] : (unsigned long long*)nullptr);   // zeroed before the claims
     prof_end_p(w, p, K_RELIST, rec);
     a.frontier = w->rlist;
     a.tsplit = w->tsplit;
@@ -2325,14 +2315,6 @@ hipError_t ws_path_level(Workspace* w, const PathTypes& pt, int src, uint64_t n_
                        (unsigned long long*)nullptr, NoInline{});
     prof_end_p(w, p, K_BFS, rec);
   }
-  uint64_t gb = cdiv(n_bound + e_bound + 1, (uint64_t)BLOCK * 4);
-  unsigned grid = (unsigned)(gb < 1 ? 1 : (gb > 1024 ? 1024 : gb));
-  hipEvent_t p = prof_begin_p(w, K_GATHER);
-  // a clamped record (rec == PATH_REC - 1 reused) accumulates: the degree sum then only over-bounds
-  hipLaunchKernelGGL(k_gather, dim3(grid), dim3(BLOCK), 0, w->stream, w->pscratch, shard_cap, w->ps->shard,
-                     w->slot[dst], &w->ps->n[dst], &w->ps->lc[rec],
-                     lv.deg ? degsum_args(*lv.deg) : DegsumArgs{}, lv.deg ? &w->ps->ld[rec] : nullptr);
-  prof_end_p(w, p, K_GATHER, rec);
   return hipGetLastError();
 }
 
@@ -2369,8 +2351,13 @@ hipError_t ws_path_greedy(Workspace* w, const PathTypes& pt, const PathGreedy& p
   g.nstarts = &w->ps->n[pg.start_slot];
   g.out = w->d_path;
   g.err = &w->ps->err;
+  g.gticket = &w->ps->gticket;
+  g.gv = &w->ps->gv;
+  g.gpart = w->ps->gpart;
   hipEvent_t p = prof_begin_p(w, K_GREEDY);
-  hipLaunchKernelGGL(k_path_greedy, dim3(1), dim3(GREEDY_BLOCK), 0, w->stream, g);
+  hipLaunchKernelGGL(k_greedy_start, dim3(1), dim3(GH_THREADS), 0, w->stream, g);
+  for (int pos = 0; pos < pg.L; ++pos)
+    hipLaunchKernelGGL(k_greedy_hop, dim3(GREEDY_HOP_BLOCKS), dim3(GH_THREADS), 0, w->stream, g, pos);
   prof_end_p(w, p, K_GREEDY, 0);
   return hipGetLastError();
 }

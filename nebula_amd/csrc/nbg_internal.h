@@ -260,6 +260,7 @@ constexpr int LVL_BITS = 6;
 constexpr uint32_t MAX_PATH_LEN = (1u << LVL_BITS) - 1;   // UPTO bound
 constexpr int PSLOTS = 8;           // 0,1 forward / 2,3 backward frontiers, 4 meets, 5 starts, 6,7 B-sets
 enum PathLabel { LAB_F = 0, LAB_B = 1, LAB_S = 2, LAB_M = 3, NUM_LABS = 4 };
+constexpr int GREEDY_HOP_BLOCKS = 64;   // workgroups scanning one reconstruction hop
 constexpr int PATH_REC = 64;        // per-query expansion records (profiling byte counts)
 
 struct PState {                      // device-resident sizes of one FIND PATH query
@@ -275,7 +276,10 @@ struct PState {                      // device-resident sizes of one FIND PATH q
   unsigned long long ln[PATH_REC];   // per expansion record: frontier size, edges, claims
   unsigned long long le[PATH_REC];
   unsigned long long lc[PATH_REC];
-  unsigned long long ld[PATH_REC];   // degree sum of the level's output list (fused into k_gather)
+  unsigned long long gticket;         // greedy hop: workgroups done (the last one reduces)
+  unsigned long long gv;              // greedy hop: the current path vertex (dense id)
+  unsigned long long gpart[4 * GREEDY_HOP_BLOCKS];   // greedy hop: per-workgroup minimum candidate
+  unsigned long long ld[PATH_REC];   // degree sum of the level's output list (summed by k_expand<BFS>)
 };
 
 struct PathTypes {                   // the CSRs one search direction expands (one per OVER type)
@@ -378,7 +382,7 @@ struct PathLevel {
   int meet_slot = -1;
   int tlab = -1;           // target label (-1 none)
   uint32_t tstamp = 0;
-  const PathTypes* deg = nullptr;   // non-null: k_gather also sums the output list's degrees over
+  const PathTypes* deg = nullptr;   // non-null: k_expand<BFS> also sums the output list's degrees over
                                     // these CSRs into PState.ld[rec] (replaces a k_degsum launch)
 };
 hipError_t ws_path_level(Workspace* w, const PathTypes& pt, int src, uint64_t n_bound, uint64_t e_bound, int dst,

@@ -68,7 +68,7 @@ hipError_t level(PathCtx& c, const PathTypes& pt, int src, uint64_t n_bound, uin
 }
 
 // One level plus the degree sum of its output list over the same CSRs (the next level's bound
-// and, bidirectionally, its direction).  Single engine: summed by the level's k_gather into
+// and, bidirectionally, its direction).  Single engine: summed by the level's k_expand<BFS> into
 // PState.ld[rec]; partitioned: a collective k_degsum into PState.dsum[side].  *rec = the level's
 // PState record.
 hipError_t level_ds(PathCtx& c, const PathTypes& pt, int src, uint64_t n_bound, uint64_t e_bound, int dst,
