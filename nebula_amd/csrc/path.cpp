@@ -84,6 +84,20 @@ uint64_t level_dsum(const PathCtx& c, const PState& ps, int rec, int side) {
   return c.part ? ps.dsum[side] : ps.ld[rec >= 0 && rec < PATH_REC ? rec : PATH_REC - 1];
 }
 
+// Degree of local vertex v over a direction's CSRs, from the host copy of the offsets (single
+// engine), capped like k_degsum.
+uint64_t host_degree(const PathCtx& c, const PathTypes& pt, uint32_t v) {
+  if (v == NO_ROW || (!c.E.snap.h_visible.empty() && !c.E.snap.h_visible[v])) return 0;
+  uint64_t sum = 0;
+  for (int k = 0; k < pt.n; ++k) {
+    auto it = c.E.snap.types.find(pt.type[k]);
+    if (it == c.E.snap.types.end() || it->second.h_row_ptr.size() <= (size_t)v + 1) continue;
+    const std::vector<uint32_t>& rp = it->second.h_row_ptr;
+    sum += std::min<uint64_t>(rp[v + 1] - rp[v], pt.a[k].cap);
+  }
+  return sum;
+}
+
 // sizes of the whole graph (summed over ranks when partitioned)
 hipError_t sync(PathCtx& c, PState* ps) {
   return c.part ? ws_path_sync_part(c.ws, ps) : ws_path_sync(c.ws, ps, nullptr, 0);
@@ -150,8 +164,17 @@ int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_pat
   const uint32_t ef = ws_path_epoch(ws, LAB_F), eb = ws_path_epoch(ws, LAB_B), em = ws_path_epoch(ws, LAB_M);
   hipError_t he = hipSuccess;
   auto T = [&](hipError_t e) { if (he == hipSuccess) he = e; };
-  if (!c.part) {   // the PState clear was left to this launch (ws_path_begin zero_state=false)
+  PState ps;
+  uint64_t dsf = 0, dsb = 0;
+  if (!c.part) {
+    // the first level's bounds and direction come from the host copy of the CSR offsets, so the
+    // set-up needs no round trip; an endpoint without edges has no path at all
+    dsf = host_degree(c, c.fwd, s);
+    dsb = host_degree(c, c.bwd, t);
+    if (!dsf || !dsb) return NBG_OK;
+    // the PState clear was left to this launch (ws_path_begin zero_state=false)
     T(ws_path_setup_pair(ws, c.fwd, c.bwd, s, t, S_F0, S_B0, S_START, LAB_F, stamp(ef, 0), LAB_B, stamp(eb, 0)));
+    if (he != hipSuccess) return dev_fail(c.E, he, "path setup");
   } else {
     T(upload1(ws, S_F0, s));
     T(upload1(ws, S_B0, t));
@@ -160,12 +183,13 @@ int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_pat
     T(ws_path_stamp(ws, S_B0, 1, LAB_B, stamp(eb, 0)));
     T(ws_path_degsum(ws, S_F0, 1, c.fwd, 0));
     T(ws_path_degsum(ws, S_B0, 1, c.bwd, 1));
+    T(sync(c, &ps));
+    if (he != hipSuccess) return dev_fail(c.E, he, "path setup");
+    dsf = ps.dsum[0];
+    dsb = ps.dsum[1];
   }
-  PState ps;
-  T(sync(c, &ps));
-  if (he != hipSuccess) return dev_fail(c.E, he, "path setup");
   int fcur = S_F0, bcur = S_B0, kf = 0, kb = 0;
-  uint64_t nf = 1, nbk = 1, dsf = ps.dsum[0], dsb = ps.dsum[1];
+  uint64_t nf = 1, nbk = 1;
   std::vector<uint64_t> fn(1, 1);   // forward level sizes
   bool met = false;
   while ((uint32_t)(kf + kb) < upto) {
