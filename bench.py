@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 # HBM traffic per launch from the committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
 # bench (tools/gpu_check.sh pmc -> tools/pmc_summary.py; FETCH_SIZE doubled per the gfx950 note).
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_v8_pmc_hbm.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_v13_pmc_hbm.json")
 # library kernel id -> instantiations in the rocprof names, first match wins (FINAL: this bench's
 # range WHERE with a _dst YIELD runs k_expand<4> = FINALD; <3> FINALF; <1> the general interpreter;
 # the bool is the inline-start-list variant)
