@@ -2767,31 +2767,59 @@ struct WalkArgs {
   unsigned long long* cnt;         // [0] walks, [1] completions, [2] adjacency entries scanned
 };
 
+// One WAVE per walk: the lanes stride the last vertex's adjacency (coalesced `col` reads, 64
+// label probes in flight), and the fill pass places a wave's admissible extensions with one
+// atomic per 64 neighbours (ballot prefix).  A hub's adjacency is therefore 1/64 of the serial
+// chain it was with a thread per walk.  Walk order inside a level is irrelevant (paths are
+// sorted at the end), but the count and fill passes test the same predicate.
 __global__ void __launch_bounds__(BLOCK) k_walk(WalkArgs a) {
   unsigned long long nw = 0, nc = 0, ns = 0;
-  for (uint64_t w = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; w < a.n; w += (uint64_t)gridDim.x * BLOCK) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  const uint64_t wave0 = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
+  const uint64_t nwaves = ((uint64_t)gridDim.x * BLOCK) >> 6;
+  for (uint64_t w = wave0; w < a.n; w += nwaves) {
     const uint32_t v = a.vtx[w];
     if (a.visible && !a.visible[v]) continue;
     for (int t = 0; t < a.ntypes; ++t) {
       const uint32_t b = a.row_ptr[t][v], e = a.row_ptr[t][v + 1];
-      ns += e - b;
-      for (uint32_t j = b; j < e; ++j) {
-        const uint32_t d = a.col[t][j];
-        if (d == NO_ROW) continue;
-        const uint32_t lb = a.lab[d];
-        if ((lb >> LVL_BITS) != a.epoch || (lb & MAX_PATH_LEN) > a.budget) continue;
-        const bool done = (lb & MAX_PATH_LEN) == 0;
+      if (lane == 0) ns += e - b;
+      for (uint32_t j0 = b; j0 < e; j0 += 64) {
+        const uint32_t j = j0 + (uint32_t)lane;
+        uint32_t d = NO_ROW;
+        bool ok = false, done = false;
+        if (j < e) {
+          d = a.col[t][j];
+          if (d != NO_ROW) {
+            const uint32_t lb = a.lab[d];
+            ok = (lb >> LVL_BITS) == a.epoch && (lb & MAX_PATH_LEN) <= a.budget;
+            done = ok && (lb & MAX_PATH_LEN) == 0;
+          }
+        }
         if (!a.fill) {
-          ++nw;
+          nw += ok;
           nc += done;
           continue;
         }
-        const unsigned long long pos = atomicAdd(&a.cnt[0], 1ull);
-        a.nvtx[pos] = d;
-        a.npar[pos] = (uint32_t)w;
-        a.neid[pos] = j;
-        a.ntix[pos] = (uint8_t)t;
-        if (done) a.comp[atomicAdd(&a.cnt[1], 1ull)] = (uint32_t)pos;
+        const unsigned long long ob = __ballot(ok);
+        if (!ob) continue;
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(&a.cnt[0], (unsigned long long)__popcll(ob));
+        base = __shfl(base, 0, 64);
+        const unsigned long long pos = base + (unsigned long long)__popcll(ob & lt);
+        if (ok) {
+          a.nvtx[pos] = d;
+          a.npar[pos] = (uint32_t)w;
+          a.neid[pos] = j;
+          a.ntix[pos] = (uint8_t)t;
+        }
+        const unsigned long long cb = __ballot(done);
+        if (cb) {
+          unsigned long long cbase = 0;
+          if (lane == 0) cbase = atomicAdd(&a.cnt[1], (unsigned long long)__popcll(cb));
+          cbase = __shfl(cbase, 0, 64);
+          if (done) a.comp[cbase + (unsigned long long)__popcll(cb & lt)] = (uint32_t)pos;
+        }
       }
     }
   }
@@ -2801,7 +2829,7 @@ __global__ void __launch_bounds__(BLOCK) k_walk(WalkArgs a) {
       nc += __shfl_xor(nc, o, 64);
       ns += __shfl_xor(ns, o, 64);
     }
-    if ((threadIdx.x & 63) == 0 && (nw | nc | ns)) {
+    if (lane == 0 && (nw | nc | ns)) {
       atomicAdd(&a.cnt[0], nw);
       atomicAdd(&a.cnt[1], nc);
       atomicAdd(&a.cnt[2], ns);
@@ -2905,7 +2933,7 @@ hipError_t ws_all_paths(Workspace* w, const PathTypes& fwd, int lab, uint32_t ep
     a.budget = upto - i - 1;
     a.vtx = lv.vtx[i];
     a.n = nlev[i];
-    const unsigned grid = (unsigned)std::min<uint64_t>(cdiv(a.n, BLOCK), 4096);
+    const unsigned grid = (unsigned)std::min<uint64_t>(cdiv(a.n, WAVES), 8192);   // a wave per walk
     a.fill = 0;
     WALK_TRY(hipMemsetAsync(cnt, 0, 3 * 8, w->stream));
     hipLaunchKernelGGL(k_walk, dim3(grid), dim3(BLOCK), 0, w->stream, a);

@@ -332,7 +332,7 @@ class Engine:
             for i in range(self.lib.nbg_paths_count(out)):
                 n = self.lib.nbg_path_len(out, i)
                 ptr = self.lib.nbg_path_entries(out, i)
-                paths.append([int(ptr[k]) for k in range(n)])
+                paths.append(ptr[:n])   # one C-level slice per path
             if stats is not None:
                 stats["edges"] = int(self.lib.nbg_paths_edges_scanned(out))
             return sorted(paths)
