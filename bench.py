@@ -382,30 +382,36 @@ def c5_leg(args, barrier):
     for r in roots[:4]:
         stmt.run_device([r]).free()
     inflight = 0 if args.sync else int(os.environ.get("NBG_QUERY_SLOTS", "6"))
-    barrier()
-    t1 = time.perf_counter()
-    scanned = rows = 0
-    pending = []
-    for r in roots:
-        if inflight and len(pending) == inflight:
-            res = stmt.wait(pending.pop(0))
+
+    def go4_pass():
+        scanned = rows = 0
+        pending = []
+        t1 = time.perf_counter()
+        for r in roots:
+            if inflight and len(pending) == inflight:
+                res = stmt.wait(pending.pop(0))
+                scanned += res.edges_scanned
+                rows += res.count
+                res.free()
+            if inflight:
+                pending.append(stmt.submit([r]))
+            else:
+                res = stmt.run_device([r])
+                scanned += res.edges_scanned
+                rows += res.count
+                res.free()
+        for tk in pending:
+            res = stmt.wait(tk)
             scanned += res.edges_scanned
             rows += res.count
             res.free()
-        if inflight:
-            pending.append(stmt.submit([r]))
-        else:
-            res = stmt.run_device([r])
-            scanned += res.edges_scanned
-            rows += res.count
-            res.free()
-    for tk in pending:
-        res = stmt.wait(tk)
-        scanned += res.edges_scanned
-        rows += res.count
-        res.free()
+        return scanned, rows, time.perf_counter() - t1
+
+    # one pass is ~10 ms of work: report the median of 5 passes
     barrier()
-    go_s = time.perf_counter() - t1
+    passes = [go4_pass() for _ in range(5)]
+    barrier()
+    scanned, rows, go_s = sorted(passes, key=lambda p: p[2])[len(passes) // 2]
     stmt.free()
     pairs = rmat.pick_pairs(ks, kd, 64, 7, verts=persons)
     lat, paths = [], 0
@@ -422,7 +428,7 @@ def c5_leg(args, barrier):
             "load_seconds": round(load_s, 2),
             "go4": {"query": "GO 4 STEPS FROM <root> OVER knows, likes", "roots": len(roots),
                     "teps": scanned / go_s if go_s else None, "edges": scanned, "rows": rows,
-                    "seconds": round(go_s, 4)},
+                    "seconds": round(go_s, 4), "timing": "median of 5 passes over the 16 roots"},
             "find_all_path": {"query": "FIND ALL PATH FROM <s> TO <t> OVER knows UPTO 4 STEPS", "pairs": len(pairs),
                               "paths": paths, "p50_ms": float(np.percentile(lat_ms, 50)),
                               "p90_ms": float(np.percentile(lat_ms, 90)), "max_ms": float(lat_ms.max())}}
