@@ -78,6 +78,8 @@ def main():
     ap.add_argument("--sync", action="store_true", help="one query at a time (no query slots)")
     ap.add_argument("--c5-scale", type=int, default=20,
                     help="C5 substitute (knows RMAT + likes bipartite): knows scale, 0 = skip")
+    ap.add_argument("--getbound-reqs", type=int, default=200,
+                    help="QueryBoundBenchmark-shaped GetNeighbors requests (0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -208,6 +210,9 @@ def main():
     c5 = None
     if world == 1 and args.c5_scale > 0:
         c5 = c5_leg(args, barrier)
+    getbound = None
+    if world == 1 and args.getbound_reqs > 0:
+        getbound = getbound_leg(args)
 
     # edges_scanned is already the whole query's count (summed over ranks in the library);
     # rows stay on the rank that produced them, so they are summed here
@@ -298,6 +303,7 @@ def main():
         "kernels": kernels,
         "find_shortest_path": sp,
         "c5_substitute": c5,
+        "getbound": getbound,
         "load_seconds": round(load_s, 2),
     }
     print(json.dumps(out), flush=True)
@@ -354,6 +360,97 @@ def shortest_path_leg(eng, pairs, args, barrier):
                            "avg_launch_us": round(v["ms"] * 1e3 / v["launches"], 2)}
         out["roofline"]["timing"] = (f"HIP events around every k_expand<BFS> launch in a second pass over the "
                                      f"first {prof_pairs} pairs; latencies come from the uninstrumented pass")
+    return out
+
+
+def getbound_leg(args):
+    """Boundary 1 (StorageServiceHandler::future_getBound) on the shape of the reference's only
+    published storage measurement, src/storage/test/QueryBoundBenchmark.cpp:33-168,178-189: one
+    part, 100 vertices per request, each with 7 out-edges of type 101 written in 3 versions (the
+    latest is returned), edge schema 10 INT + 10 STRING columns, tags 3001-3009 with 3 INT + 3
+    STRING columns; the request returns 3 tag props, _dst, _rank and 10 edge props (700 rows).
+    The published figure is 13.69 ms/req (10 handlers, Xeon E5-2690 v2); the oracle's
+    QueryBoundProcessor restatement is timed here on the same request, and the device response
+    is checked byte-for-byte against it."""
+    from nebula_amd import Engine, kvgen
+    parts, nv = 6, 999
+    now = 1_600_000_000_000_000
+    kb = kvgen.KVBuilder(parts)
+    I, S = kvgen.INT, kvgen.STRING
+    eschema = [(f"col_{i}", I) for i in range(10)] + [(f"col_{i}", S) for i in range(10, 20)]
+    tschema = {t: [(f"tag_{t}_col_{i}", I) for i in range(3)] + [(f"tag_{t}_col_{i}", S) for i in range(3, 6)]
+               for t in range(3001, 3010)}
+    part1 = [k * parts for k in range(1, nv + 1)]   # vids of hash part 1 ((uint64)vid % 6 + 1)
+    for v in part1:
+        for t in range(3001, 3010):
+            kb.insert_vertex(v, t, tschema[t], [0, 1, 2] + [f"tag_string_col_{i}" for i in range(3, 6)], now)
+        for d in range(10001, 10008):
+            for ver in range(3):
+                kb.insert_edge(v, d, 101, d - 10001, eschema,
+                               list(range(10)) + [f"string_col_{i}_{ver}" for i in range(10, 20)], now + ver)
+    eng = Engine(parts)
+    eng.register_edge(101, "e101", eschema)
+    for t in range(3001, 3010):
+        eng.register_tag(t, f"tag_{t}", tschema[t])
+    eng.load_builder(kb)
+    req_vids = [(1, v) for v in part1[:100]]
+    rets = [(1, 3001 + 2 * i, f"tag_{3001 + 2 * i}_col_{2 * i}") for i in range(3)]
+    rets += [(3, 101, "_dst"), (3, 101, "_rank")] + [(3, 101, f"col_{2 * i}") for i in range(10)]
+    import ctypes as C
+    from nebula_amd.engine import _gn_request
+    for _ in range(5):
+        got = eng.get_neighbors(req_vids, [101], b"", rets)
+    # the C ABI call alone (request in, encoded QueryResponse rows and schemas out in host memory);
+    # the Python mirror's decoding of the response into dicts is not part of the boundary
+    keep = []
+    req = _gn_request(req_vids, [101], b"", rets, keep)
+    lat = []
+    for _ in range(args.getbound_reqs):
+        resp = C.c_void_p()
+        q0 = time.perf_counter()
+        rc = eng.lib.nbg_get_neighbors(eng.h, C.byref(req), C.byref(resp))
+        lat.append(time.perf_counter() - q0)
+        assert rc == 0, rc
+        eng.lib.nbg_gn_free(resp)
+    eng.close()
+    out = {"request": "1 part x 100 vertices x 7 out-edges (latest of 3 versions), 3 tag props + _dst, _rank "
+                      "+ 10 edge props (QueryBoundBenchmark shape)",
+           "requests": args.getbound_reqs, "timing": "nbg_get_neighbors C ABI call, response decoding excluded",
+           "p50_ms": float(np.percentile(np.array(lat) * 1e3, 50)),
+           "p90_ms": float(np.percentile(np.array(lat) * 1e3, 90)),
+           "reference_published": {"ms_per_req": 13.69, "handlers": 10,
+                                   "hardware": "40 procs, Xeon E5-2690 v2 (QueryBoundBenchmark.cpp:178-189)"}}
+    if not args.no_cpu_baseline:
+        try:
+            from tests.support.oracle import Oracle
+            o = Oracle(parts, threads=10)
+            o.register(True, 101, "e101", eschema)
+            for t in range(3001, 3010):
+                o.register(False, t, f"tag_{t}", tschema[t])
+            o.load_builder(kb)
+            exp = o.get_neighbors(req_vids, [101], b"", rets)
+            out["parity_vs_oracle"] = exp == got
+            from tests.support.oracle import _ptr
+            a_parts = np.asarray([p for p, _ in req_vids], np.int32)
+            a_vids = np.asarray([v for _, v in req_vids], np.int64)
+            a_et = np.asarray([101], np.int32)
+            a_own = np.asarray([x for x, _, _ in rets], np.int32)
+            a_ids = np.asarray([i for _, i, _ in rets], np.int32)
+            a_names = (C.c_char_p * len(rets))(*[n.encode() for _, _, n in rets])
+            olat = []
+            t0 = time.perf_counter()
+            while time.perf_counter() - t0 < 5.0 and len(olat) < args.getbound_reqs:
+                q0 = time.perf_counter()
+                r = o.L.orc_get_bound(o.h, _ptr(a_parts), _ptr(a_vids), len(a_vids), _ptr(a_et), 1, None, 0,
+                                      _ptr(a_own), _ptr(a_ids), a_names, len(rets))
+                olat.append(time.perf_counter() - q0)
+                o.L.orc_gn_free(r)
+            o.close()
+            out["cpu_baseline"] = {"p50_ms": float(np.percentile(np.array(olat) * 1e3, 50)), "cores": 10,
+                                   "kind": "port", "sample": f"{len(olat)} requests, 10 handler threads",
+                                   "timing": "orc_get_bound C call (QueryBoundProcessor restated), decoding excluded"}
+        except Exception as ex:  # pragma: no cover
+            log(f"getbound cpu baseline unavailable: {ex}")
     return out
 
 
