@@ -160,9 +160,19 @@ typedef struct {
 
 /* Rows are copied to host memory. */
 int32_t nbg_go(nbg_engine* e, const nbg_go_request* req, nbg_rows** out);
-/* Rows stay in HBM (engine-owned buffers, valid until the next query on this engine or
- * nbg_rows_free); nbg_rows_fetch() copies them to the host on demand. */
+/* Rows stay in HBM in the query workspace; nbg_rows_fetch() copies them to the host on demand.
+ * They stay valid until nbg_rows_free: a later query that needs the workspace hands it over to
+ * the live result (released by nbg_rows_free) and continues on a fresh one.  Every result must
+ * be freed before nbg_destroy. */
 int32_t nbg_go_device(nbg_engine* e, const nbg_go_request* req, nbg_rows** out);
+
+/* Default YIELD of a GO without YIELD: the edge types whose `<edge>._dst` columns it returns, in
+ * column order.  OVER e1, e2: the OVER order (parser.yy:518-531).  OVER * (over_all = 1, `over` =
+ * every edge type as graphd requests them): the iteration order of the response's edge_schema map
+ * (GoExecutor::getEdgeNamesFromResp, GoExecutor.cpp:481-499,546-561).  Returns the column count
+ * (writes up to cap types) or a negative status. */
+int32_t nbg_go_default_columns(nbg_engine* e, const int32_t* over, int32_t n, int32_t over_all, int32_t* out,
+                               int32_t cap);
 
 /* Prepared GO statement: GoExecutor::prepare() once (OVER / WHERE / YIELD validated and compiled
  * per OVER type, GoExecutor.cpp:136-263), then execute() from any number of start lists — the
@@ -180,8 +190,9 @@ void nbg_go_stmt_free(nbg_go_stmt* stmt);
  * stream.  nbg_go_submit enqueues the query and returns a ticket (when every slot is busy it first
  * completes the oldest query, whose result stays in its ticket); nbg_go_wait completes the ticket
  * (and every older one), returns its rows with nbg_go_execute's semantics and frees the ticket.
- * Device rows (device != 0) stay valid until the slot's next query, i.e. until NBG_QUERY_SLOTS
- * further submissions.  A ticket never waited for is reclaimed by nbg_destroy; tickets must be
+ * Device rows (device != 0) stay valid until nbg_rows_free, as with nbg_go_device (a slot whose
+ * workspace still holds live rows gives it to them and takes a fresh one).  A ticket never
+ * waited for is reclaimed by nbg_destroy; tickets must be
  * waited for before their statement is freed.  On a partitioned engine every rank must submit
  * the same queries in the same order (they are collectives); its slots share the engine's stream
  * and communicator, so the device runs them in that order while the host work overlaps. */

@@ -87,6 +87,7 @@ SIGNATURES = [
     ("nbg_get_stats", i32, [vp, P(nbg_stats)]),
     ("nbg_go", i32, [vp, P(nbg_go_request), P(vp)]),
     ("nbg_go_device", i32, [vp, P(nbg_go_request), P(vp)]),
+    ("nbg_go_default_columns", i32, [vp, vp, i32, i32, vp, i32]),
     ("nbg_go_prepare", i32, [vp, P(nbg_go_request), P(vp)]),
     ("nbg_go_execute", i32, [vp, P(i64), u64, i32, P(vp)]),
     ("nbg_go_stmt_free", None, [vp]),

@@ -14,12 +14,35 @@
 #include <atomic>
 #include <cstring>
 #include <set>
+#include <iterator>
+#include <unordered_map>
 
 #include "engine.h"
 
 using namespace nbg;
 
 namespace nbg {
+
+void Engine::free_snapshot() {
+  for (auto& kv : snap.types) {
+    auto& d = kv.second;
+    for (void* p : {(void*)d.row_ptr, (void*)d.col, (void*)d.dst_vid, (void*)d.rank, (void*)d.valid,
+                    (void*)d.d_props})
+      if (p) (void)hipFree(p);
+    for (auto* p : d.props)
+      if (p) (void)hipFree(p);
+    for (auto* p : d.narrow)
+      if (p) (void)hipFree(p);
+  }
+  for (auto& kv : snap.tags) {
+    if (kv.second.present) (void)hipFree(kv.second.present);
+    for (auto* p : kv.second.cols)
+      if (p) (void)hipFree(p);
+  }
+  for (void* p : {(void*)snap.d_tcols, (void*)snap.d_tpres, (void*)snap.d_vids, (void*)snap.d_visible})
+    if (p) (void)hipFree(p);
+  snap = Snapshot();
+}
 
 uint32_t Engine::dense(int64_t vid) const {
   auto& v = snap.h_vids;
@@ -39,6 +62,7 @@ struct nbg_rows {
   std::vector<std::vector<std::string>> const_str;    // per OVER type: string constants absent from the dictionary
   Engine* eng = nullptr;
   Workspace* ws = nullptr;               // the workspace holding the rows (device results)
+  Workspace* owned_ws = nullptr;         // set when the engine handed that workspace over (ws_release)
   int ncols = 0;
   uint64_t count = 0;
   bool on_device = false;
@@ -174,6 +198,27 @@ static void alias_props(const Node* n, std::map<std::string, std::set<std::strin
   for (auto& k : n->kids) alias_props(k.get(), out);
 }
 
+// OVER * without YIELD: GoExecutor::finishExecution names one `<edge>._dst` column per entry of
+// the first response's edge_schema, in that map's iteration order (GoExecutor.cpp:481-499,
+// 546-561).  The order is libstdc++'s: storaged fills edgeContexts_ (an unordered_map, from the
+// request's edge types, QueryBaseProcessor.inl:46-57, QueryBaseProcessor.h:114), copies it into
+// the response's edge_schema (an unordered_map, QueryBoundProcessor.cpp:139-158), and graphd
+// decodes that into another unordered_map (storage.thrift:104).  The same three containers, keyed
+// the same way, reproduce it.
+static std::vector<int32_t> response_schema_order(const std::vector<int32_t>& req) {
+  std::unordered_map<int32_t, int> contexts;
+  std::transform(req.begin(), req.end(), std::inserter(contexts, contexts.end()),
+                 [](int32_t t) { return std::make_pair(t, 0); });
+  std::unordered_map<int32_t, int> schema;
+  for (const auto& kv : contexts)
+    if (schema.find(kv.first) == schema.end()) schema.emplace(kv.first, 0);
+  std::unordered_map<int32_t, int> decoded;
+  for (const auto& kv : schema) decoded.emplace(kv.first, 0);
+  std::vector<int32_t> order;
+  for (const auto& kv : decoded) order.push_back(kv.first);
+  return order;
+}
+
 static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out) {
   if (!rq || !out) return E.fail(NBG_E_INVALID_ARGUMENT, "null argument");
   *out = nullptr;
@@ -207,7 +252,7 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
     yields.push_back(std::move(y));
   }
   if (yields.empty()) {   // default YIELD <edge>._dst per OVER edge (parser.yy:518-531)
-    for (int32_t t : over) {
+    for (int32_t t : rq->over_all ? response_schema_order(over) : over) {
       auto n = std::make_unique<Node>();
       n->kind = EK_DST;
       n->alias = E.edges[t].name;
@@ -675,6 +720,8 @@ static int32_t go_collect(Engine& E, const nbg_go_stmt* st, GoPending* p, nbg_ro
   if (!device) {
     int32_t rc = materialize_rows(rows);
     if (rc) { delete rows; return E.fail(rc, "row fetch failed"); }
+  } else if (rows->count) {
+    E.holders[ws] = rows;   // the rows stay valid until nbg_rows_free (ws_release)
   }
   *out = rows;
   return NBG_OK;
@@ -685,7 +732,9 @@ static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* start
   if (!out) return E.fail(NBG_E_INVALID_ARGUMENT, "null argument");
   *out = nullptr;
   GoPending p;
-  int32_t rc = go_launch(E, st, starts, num_starts, device, &E.ws, E.stream, &p);
+  int32_t rc = ws_release(E, &E.ws, E.stream);
+  if (rc) return rc;
+  rc = go_launch(E, st, starts, num_starts, device, &E.ws, E.stream, &p);
   if (rc) return rc;
   return go_collect(E, st, &p, out);
 }
@@ -731,6 +780,25 @@ static void complete_oldest(Engine& E) {
   E.slots[t->slot].ticket = nullptr;
 }
 
+int32_t nbg::ws_release(Engine& E, Workspace** wsp, hipStream_t stream) {
+  auto it = E.holders.find(*wsp);
+  if (it == E.holders.end()) return NBG_OK;
+  nbg_rows* r = it->second;
+  E.holders.erase(it);
+  r->owned_ws = *wsp;
+  std::string err;
+  Workspace* fresh = ws_create(E.snap.nv + 1024, E.snap.nv, E.snap.max_edges(), stream, &err);
+  if (!fresh) { *wsp = nullptr; return E.fail(NBG_E_OUT_OF_MEMORY, err); }
+  if (E.partitioned() && ws_set_partition(fresh, E.comm.get(), E.npad) != hipSuccess) {
+    ws_destroy(fresh);
+    *wsp = nullptr;
+    return E.fail(NBG_E_OUT_OF_MEMORY, "partition buffers");
+  }
+  ws_profile_inherit(fresh, *wsp);
+  *wsp = fresh;
+  return NBG_OK;
+}
+
 // The query workspace of a finalized (or snapshot-loaded) engine.
 int32_t nbg::engine_ready(Engine& E) {
   std::string err;
@@ -769,6 +837,10 @@ int32_t nbg_go_submit(nbg_go_stmt* st, const int64_t* starts, uint64_t num_start
   const hipStream_t qs = E.partitioned() ? E.stream : q.stream;
   if (!E.partitioned() && !q.stream && hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking) != hipSuccess)
     return E.fail(NBG_E_DEVICE, "hipStreamCreate failed");
+  if (q.ws) {   // rows of an earlier device result still there: hand the workspace to them
+    int32_t rc = ws_release(E, &q.ws, qs);
+    if (rc) return rc;
+  }
   if (!q.ws) {
     std::string err;
     q.ws = ws_create(E.snap.nv + 1024, E.snap.nv, E.snap.max_edges(), E.partitioned() ? E.stream : q.stream, &err);
@@ -823,31 +895,15 @@ void nbg_destroy(nbg_engine* h) {
     complete_oldest(E);
     if (t->result) nbg_rows_free(t->result);
     t->result = nullptr;
+    delete t;
   }
+  E.holders.clear();   // results must be freed before nbg_destroy (nbg.h)
   for (auto& q : E.slots) {
     if (q.ws) ws_destroy(q.ws);
     if (q.stream) (void)hipStreamDestroy(q.stream);
   }
   if (E.ws) ws_destroy(E.ws);
-  for (auto& kv : E.snap.types) {
-    auto& d = kv.second;
-    for (void* p : {(void*)d.row_ptr, (void*)d.col, (void*)d.dst_vid, (void*)d.rank, (void*)d.valid,
-                    (void*)d.d_props})
-      if (p) (void)hipFree(p);
-    for (auto* p : d.props)
-      if (p) (void)hipFree(p);
-    for (auto* p : d.narrow)
-      if (p) (void)hipFree(p);
-  }
-  for (auto& kv : E.snap.tags) {
-    if (kv.second.present) (void)hipFree(kv.second.present);
-    for (auto* p : kv.second.cols)
-      if (p) (void)hipFree(p);
-  }
-  if (E.snap.d_tcols) (void)hipFree(E.snap.d_tcols);
-  if (E.snap.d_tpres) (void)hipFree(E.snap.d_tpres);
-  if (E.snap.d_vids) (void)hipFree(E.snap.d_vids);
-  if (E.snap.d_visible) (void)hipFree(E.snap.d_visible);
+  E.free_snapshot();
   if (E.stream) (void)hipStreamDestroy(E.stream);
   delete h;
 }
@@ -931,6 +987,15 @@ int32_t nbg_go_device(nbg_engine* h, const nbg_go_request* req, nbg_rows** out) 
   return go_impl(h->e, req, true, out);
 }
 
+int32_t nbg_go_default_columns(nbg_engine* h, const int32_t* over, int32_t n, int32_t over_all, int32_t* out,
+                               int32_t cap) {
+  if (!h || n < 0 || (n && !over) || (cap && !out)) return NBG_E_INVALID_ARGUMENT;
+  std::vector<int32_t> req(over, over + n);
+  if (over_all) req = response_schema_order(req);
+  for (int32_t i = 0; i < cap && i < (int32_t)req.size(); ++i) out[i] = req[i];
+  return (int32_t)req.size();
+}
+
 int32_t nbg_go_prepare(nbg_engine* h, const nbg_go_request* req, nbg_go_stmt** out) {
   if (!h) return NBG_E_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> lg(h->e.mu);
@@ -992,7 +1057,20 @@ const void* nbg_rows_device_col(const nbg_rows* r, int32_t col) {
   if (!r || col < 0 || col >= (int32_t)r->dcols.size()) return nullptr;
   return r->dcols[col];
 }
-void nbg_rows_free(nbg_rows* r) { delete r; }
+void nbg_rows_free(nbg_rows* r) {
+  if (!r) return;
+  if (r->eng && (r->owned_ws || r->ws)) {
+    Engine& E = *r->eng;
+    std::lock_guard<std::mutex> lg(E.mu);
+    auto it = E.holders.find(r->ws);
+    if (it != E.holders.end() && it->second == r) E.holders.erase(it);
+    if (r->owned_ws) {
+      (void)hipSetDevice(E.cfg.device);
+      ws_destroy(r->owned_ws);
+    }
+  }
+  delete r;
+}
 
 int32_t nbg_profile(nbg_engine* h, int32_t enable) {
   if (!h) return NBG_E_INVALID_ARGUMENT;

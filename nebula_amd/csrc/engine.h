@@ -36,6 +36,9 @@ struct Engine {
   };
   std::vector<QuerySlot> slots;
   std::vector<void*> inflight;          // submitted tickets, oldest first
+  // device GO results (rows left in HBM) and the workspace their rows live in: before that
+  // workspace runs another query it is handed to the result (freed with it) and replaced
+  std::unordered_map<Workspace*, ::nbg_rows*> holders;
   // multi-GPU (partitioned mode when cfg.num_gpus > 1): global id = owner * npad + local id
   std::unique_ptr<Comm> comm;
   uint64_t npad = 0;
@@ -63,9 +66,13 @@ struct Engine {
   int32_t exchange_dictionary(const std::vector<int64_t>& local, std::vector<int64_t>* gdict,
                               std::vector<uint64_t>* gcount);
   uint32_t dense(int64_t vid) const;
+  void free_snapshot();   // release every device array of `snap` and reset it
 };
 
 int32_t engine_ready(Engine& E);   // workspace (+ partition buffers) after finalize / snapshot load
+// Make *wsp free for a new query: if live device rows still sit in it, the rows take the
+// workspace over and *wsp becomes a fresh one on `stream` (profiling state carried over).
+int32_t ws_release(Engine& E, Workspace** wsp, hipStream_t stream);
 
 }  // namespace nbg
 

@@ -358,6 +358,7 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
       cap_rows += blk_cap.back() * ws_final_grid(starts.size(), eb);
       plist.push_back(std::move(tp));
     }
+    if (int32_t rrc = ws_release(E, &E.ws, E.stream)) return rrc;   // a held device GO result keeps its rows
     if (starts.size() > ws_cap_frontier(E.ws)) return E.fail(NBG_E_UNSUPPORTED, "too many vertices in one request");
     static std::atomic<uint64_t> gn_id{1ull << 62};   // program cache keys disjoint from GO statements
     Workspace* ws = E.ws;

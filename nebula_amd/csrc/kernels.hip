@@ -1271,6 +1271,18 @@ void ws_profile(Workspace* w, int mode) {
   }
 }
 
+void ws_profile_inherit(Workspace* to, Workspace* from) {
+  if (!to || !from) return;
+  prof_flush(from, nullptr);
+  to->prof.on = from->prof.on;
+  to->prof.mask = from->prof.mask;
+  for (int k = 0; k < K_COUNT; ++k) {
+    to->prof.launches[k] = from->prof.launches[k];
+    to->prof.ms[k] = from->prof.ms[k];
+    to->prof.bytes[k] = from->prof.bytes[k];
+  }
+}
+
 int ws_profile_read(Workspace* w, nbg_kernel_stat* out, int cap) {
   if (!w) return 0;
   int n = 0;

@@ -311,6 +311,7 @@ Workspace* ws_create(uint64_t max_frontier, uint64_t nv, uint64_t e_max, hipStre
 void ws_destroy(Workspace* w);
 void ws_profile(Workspace* w, int mode);   // 0 off, 1 every launch, 2 final/BFS expansions only
 int ws_profile_read(Workspace* w, nbg_kernel_stat* out, int cap);
+void ws_profile_inherit(Workspace* to, Workspace* from);   // profiling mode and counters
 uint64_t ws_cap_frontier(Workspace* w);
 hipError_t ws_reserve_rows(Workspace* w, uint64_t rows, int ncols);
 int64_t* ws_row_col(Workspace* w, int c);       // device pointer of output column c

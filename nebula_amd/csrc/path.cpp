@@ -428,6 +428,10 @@ extern "C" int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* rq, nbg_
       Tg.push_back(td[i]);
     }
   if (Sv.empty() || Tv.empty() || rq->upto == 0 || !pres[pres.size() - 2]) { *out = res; return NBG_OK; }
+  {
+    const int32_t rrc = ws_release(E, &E.ws, E.stream);   // a held device GO result keeps its rows
+    if (rrc) { delete res; return rrc; }
+  }
   PathCtx c{E, E.ws, {}, {}, 0, 0, E.partitioned()};
   const uint32_t cap = 0x7fffffff;
   auto add = [&](PathTypes& pt, int32_t signed_type) {

@@ -192,6 +192,7 @@ int32_t Engine::load_snapshot(const char* path) {
   In in{f};
   auto bad = [&](const std::string& why) {
     fclose(f);
+    free_snapshot();   // no partial device state survives a rejected file
     return fail(NBG_E_INVALID_ARGUMENT, "snapshot " + std::string(path) + ": " + why);
   };
   char magic[8];
@@ -212,6 +213,13 @@ int32_t Engine::load_snapshot(const char* path) {
   const uint64_t nv = snap.nv;
   if (!in.ok || snap.h_part.size() != nv || (!snap.h_visible.empty() && snap.h_visible.size() != nv))
     return bad("vertex tables");
+  // dense() binary-searches the dictionary: strictly ascending vids
+  for (uint64_t d = 1; d < nv; ++d)
+    if (snap.h_vids[d - 1] >= snap.h_vids[d]) return bad("vertex dictionary not sorted");
+  if (nv >= NO_ROW || (partitioned() && ((npad % PART_ALIGN) || nv > npad || (uint64_t)cfg.num_gpus * npad >= NO_ROW)))
+    return bad("vertex id space");
+  // neighbour ids index [nv) on one GPU, the global id space [G * npad) when partitioned
+  const uint64_t id_space = partitioned() ? (uint64_t)cfg.num_gpus * npad : nv;
   const uint32_t nt = in.get<uint32_t>();
   for (uint32_t k = 0; in.ok && k < nt; ++k) {
     const int32_t type = in.get<int32_t>();
@@ -238,8 +246,16 @@ int32_t Engine::load_snapshot(const char* path) {
                  (!has_valid || valid.size() == E) && dt.h_row_ptr[nv] == E;
     for (auto& c : pc) sizes = sizes && c.size() == E;
     if (!in.ok || !sizes) return bad("edge type " + std::to_string(type));
+    if (dt.h_row_ptr[0] != 0) return bad("edge type " + std::to_string(type) + ": row offsets");
+    for (uint64_t d = 0; d < nv; ++d)
+      if (dt.h_row_ptr[d] > dt.h_row_ptr[d + 1]) return bad("edge type " + std::to_string(type) + ": row offsets");
+    for (uint32_t c : col)
+      if (c != NO_ROW && c >= id_space) return bad("edge type " + std::to_string(type) + ": neighbour id");
+    for (VKind k : kinds)
+      if (k > VK_STRING) return bad("edge type " + std::to_string(type) + ": column kind");
     if (!upload_type(dt, nv, col, dvid, has_rank ? &rk : nullptr, pc, has_valid ? &valid : nullptr, kinds)) {
       fclose(f);
+      free_snapshot();
       return fail(NBG_E_OUT_OF_MEMORY, "device allocation failed for the snapshot");
     }
   }
@@ -259,14 +275,35 @@ int32_t Engine::load_snapshot(const char* path) {
     if (!in.ok || t.h_present.size() != nv) return bad("tag " + std::to_string(tag));
     for (auto& c : t.h_cols)
       if (c.size() != nv) return bad("tag " + std::to_string(tag));
+    for (uint8_t k : kinds)
+      if (k > VK_STRING) return bad("tag " + std::to_string(tag) + ": column kind");
+  }
+  {   // tag slots index Snapshot::d_tpres / d_tcols: a permutation / disjoint column ranges
+    std::vector<int> seen(snap.tags.size(), 0);
+    int cols = 0;
+    for (auto& kv : snap.tags) {
+      const DevTag& t = kv.second;
+      if (t.index < 0 || t.index >= (int)seen.size() || seen[t.index]++) return bad("tag table");
+      cols += (int)t.kind.size();
+    }
+    std::vector<int> used(cols, 0);
+    for (auto& kv : snap.tags) {
+      const DevTag& t = kv.second;
+      if (t.col_base < 0 || t.col_base + (int)t.kind.size() > cols) return bad("tag table");
+      for (size_t c = 0; c < t.kind.size(); ++c)
+        if (used[t.col_base + c]++) return bad("tag table");
+    }
   }
   in.raw(magic, sizeof magic);
   if (!in.ok || memcmp(magic, kMagic, sizeof kMagic)) return bad("truncated");
   fclose(f);
   int32_t rc = upload_tags();
-  if (rc) return rc;
-  rc = upload_vertices(snap.h_visible, snap.h_visible.empty());
-  if (rc) return rc;
+  if (!rc) rc = upload_vertices(snap.h_visible, snap.h_visible.empty());
+  if (rc) {
+    const std::string msg = last_error;
+    free_snapshot();
+    return fail(rc, msg);
+  }
   finalized = true;
   return NBG_OK;
 }

@@ -11,6 +11,7 @@ The engine also implements the backend interface of ``nebula_amd.ngql.Session`` 
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 import struct
 from typing import List, Optional, Sequence
 
@@ -30,10 +31,13 @@ def _ptr(a):
 
 
 class DeviceRows:
-    """Rows of a ``go_device`` call, resident in HBM until freed or the next query."""
+    """Rows of a ``go_device`` / device ``submit`` call, resident in HBM until freed (a later
+    query on the same workspace leaves them in place, nbg.h).  The engine frees the ones still
+    alive when it is closed."""
 
     def __init__(self, eng, h):
         self.eng, self.h = eng, h
+        eng._live.add(self)
 
     @property
     def count(self) -> int:
@@ -134,10 +138,13 @@ class Engine:
         self.h = h
         self.edge_types, self.edge_names, self.tag_ids = {}, {}, {}
         self.last_step_stats = None
+        self._live = weakref.WeakSet()   # DeviceRows not freed yet
 
     # ------------------------------------------------------------------ lifecycle
     def close(self):
         if getattr(self, "h", None):
+            for r in list(getattr(self, "_live", ())):
+                r.free()
             self.lib.nbg_destroy(self.h)
             self.h = None
 
@@ -306,6 +313,16 @@ class Engine:
         rc = self.lib.nbg_go_device(self.h, C.byref(req), C.byref(out))
         self._check(rc, "go_device")
         return DeviceRows(self, out)
+
+    def default_columns(self, etypes, over_all=False):
+        """Edge types of a YIELD-less GO's `<edge>._dst` columns, in column order (OVER order;
+        for OVER *, the response edge_schema's iteration order, GoExecutor.cpp:481-499)."""
+        t = np.asarray(etypes, np.int32)
+        out = np.zeros(max(1, len(t)), np.int32)
+        n = self.lib.nbg_go_default_columns(self.h, _ptr(t) if len(t) else None, len(t), int(over_all),
+                                            _ptr(out), len(out))
+        self._check(n if n < 0 else 0, "go_default_columns")
+        return [int(x) for x in out[:n]]
 
     def prepare_go(self, etypes, steps=1, where=b"", yields=(), distinct=False, over_all=False) -> "GoStatement":
         """GoExecutor::prepare() once; ``GoStatement.run*`` executes it from start lists."""
@@ -489,6 +506,9 @@ class LocalCluster:
     @property
     def tag_ids(self):
         return self.engines[0].tag_ids
+
+    def default_columns(self, *a, **k):
+        return self.engines[0].default_columns(*a, **k)
 
     def register_edge(self, *a, **k):
         for e in self.engines:

@@ -488,7 +488,10 @@ class Session:
         else:
             cols = g.yields
         if g.over_all and not cols:
-            cols = [YieldCol(E.edge_prop(self.b.edge_names[t], "_dst")) for t in etypes]
+            # one `<edge>._dst` column per entry of the response's edge_schema, in that map's
+            # order (GoExecutor::finishExecution, GoExecutor.cpp:546-561)
+            cols = [YieldCol(E.edge_prop(self.b.edge_names[t], "_dst"))
+                    for t in self.b.default_columns(etypes, over_all=True)]
         # `$-.*` / `$var.*`: every column of the input (YieldClause expansion)
         if any(c.expr.kind in (E.K_INPUT, E.K_VAR) and c.expr.prop == "*" for c in cols):
             if g.from_ref is None:

@@ -142,6 +142,13 @@ int32_t orc_go(void* h, const int64_t* starts, uint64_t nstarts, const int32_t* 
   return r->rs.code;
 }
 
+int32_t orc_go_default_columns(const int32_t* over, int32_t n, int32_t over_all, int32_t* out, int32_t cap) {
+  std::vector<int32_t> t(over, over + n);
+  if (over_all) t = responseEdgeSchemaOrder(t);
+  for (int32_t i = 0; i < cap && i < (int32_t)t.size(); ++i) out[i] = t[i];
+  return (int32_t)t.size();
+}
+
 int32_t orc_result_code(void* r) { return static_cast<OrcResult*>(r)->rs.code; }
 const char* orc_result_error(void* r) { return static_cast<OrcResult*>(r)->rs.err.c_str(); }
 int64_t orc_result_rows(void* r) { return (int64_t) static_cast<OrcResult*>(r)->rs.rows.size(); }

@@ -150,6 +150,26 @@ ResultSet goError(const std::string& m) { ResultSet r; r.code = E_EXECUTION_ERRO
 }  // namespace
 
 // ---------------------------------------------------------------- GO
+// GoExecutor::getEdgeNamesFromResp (GoExecutor.cpp:481-499) walks resp[0].edge_schema, a
+// std::unordered_map (storage.thrift:104) that graphd decoded from storaged's own
+// unordered_map (QueryBoundProcessor.cpp:139-158), which was filled by walking
+// edgeContexts_ (unordered_map, QueryBaseProcessor.h:114) built from the request's types
+// with std::inserter (QueryBaseProcessor.inl:46-57).  Restated hop by hop with the same
+// libstdc++ containers.
+std::vector<int32_t> responseEdgeSchemaOrder(const std::vector<int32_t>& reqTypes) {
+  std::unordered_map<int32_t, std::vector<int>> edgeContexts;
+  for (int32_t t : reqTypes) edgeContexts.insert(edgeContexts.end(), {t, std::vector<int>{}});
+  std::unordered_map<int32_t, std::string> storagedSchema;
+  for (const auto& ec : edgeContexts) {
+    if (storagedSchema.find(ec.first) == storagedSchema.end()) storagedSchema.emplace(ec.first, "_dst");
+  }
+  std::unordered_map<int32_t, std::string> graphdSchema;   // thrift map decode
+  for (const auto& kv : storagedSchema) graphdSchema.emplace(kv.first, kv.second);
+  std::vector<int32_t> names;
+  for (const auto& kv : graphdSchema) names.push_back(kv.first);
+  return names;
+}
+
 ResultSet runGo(const Store& st, const GoQuery& q) {
   ResultSet out;
   // prepareOver (GoExecutor.cpp:197-263)
@@ -189,7 +209,7 @@ ResultSet runGo(const Store& st, const GoQuery& q) {
     }
   }
   if (defaultOverAllYield) {
-    for (auto et : etypes) {
+    for (auto et : responseEdgeSchemaOrder(etypes)) {
       auto e = std::make_unique<Expr>();
       e->kind = kEdgeDstId; e->alias = st.edgeNames.at(et); e->prop = "_dst";
       yields.push_back(std::move(e));

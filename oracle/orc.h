@@ -275,6 +275,8 @@ struct GoQuery {
   int inputVidCol = -1;
 };
 ResultSet runGo(const Store& st, const GoQuery& q);
+// OVER * without YIELD: edge types of the default `_dst` columns, in column order
+std::vector<int32_t> responseEdgeSchemaOrder(const std::vector<int32_t>& reqTypes);
 
 struct PathStep { int64_t id; int32_t type; int64_t rank; };
 using Path = std::vector<PathStep>;

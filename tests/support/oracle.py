@@ -31,6 +31,8 @@ def lib():
         L.orc_finalize.argtypes = [vp]
         L.orc_go.argtypes = [vp, vp, u64, vp, i32, i32, u32, vp, u32, vp, vp, i32, i32, P(vp)]
         L.orc_set_input.argtypes = [i32, vp, vp, vp, u64, i32]
+        L.orc_go_default_columns.argtypes = [vp, i32, i32, vp, i32]
+        L.orc_go_default_columns.restype = i32
         L.orc_go.restype = i32
         L.orc_result_code.argtypes = [vp]
         L.orc_result_error.argtypes = [vp]
@@ -136,6 +138,12 @@ class Oracle:
         self.L.orc_finalize(self.h)
 
     # ---------------------------------------------------------------- ngql backend API
+    def default_columns(self, etypes, over_all=False):
+        t = np.asarray(etypes, np.int32)
+        out = np.zeros(max(1, len(t)), np.int32)
+        n = self.L.orc_go_default_columns(_ptr(t) if len(t) else None, len(t), int(over_all), _ptr(out), len(out))
+        return [int(x) for x in out[:n]]
+
     def go(self, starts, etypes, steps, where=b"", yields=(), distinct=False, over_all=False, inputs=None):
         if inputs is not None:
             from nebula_amd.engine import Engine

@@ -59,3 +59,20 @@ def test_bulk_load_rejects_unknown_type():
     with pytest.raises(NbgError) as ex:
         e.load_edges(9, np.array([1]), np.array([2]))
     assert ex.value.code == _lib.E_EDGE_PROP_NOT_FOUND
+
+
+def test_over_all_default_column_order():
+    """OVER * without YIELD: columns follow the response edge_schema map's iteration order
+    (GoExecutor.cpp:481-499); for the nba types serve=4, like=5 that is like, serve — what
+    GoTest.cpp:437-448 expects ({0, team} rows).  Engine (host-only ABI) and oracle agree."""
+    from tests.support.oracle import Oracle
+    e = Engine(num_parts=1)
+    o = Oracle(1)
+    try:
+        assert e.default_columns([4, 5], over_all=True) == [5, 4]
+        assert e.default_columns([4, 5], over_all=False) == [4, 5]
+        for types in ([1], [1, 2, 3], [2, 7, 9, 30], list(range(1, 20))):
+            assert e.default_columns(types, True) == o.default_columns(types, True), types
+    finally:
+        e.close()
+        o.close()

@@ -215,6 +215,55 @@ def test_async_submit_wait_parity(rmat12):
         stmt.free()
 
 
+def test_async_device_rows_outlive_slot_reuse(rmat12):
+    """Device tickets: more submissions than query slots, every result held (not freed) while
+    later queries reuse the slots; each result's rows stay intact (the slot's workspace is handed
+    to the live result) and equal the oracle's.  Also the synchronous device path: a held
+    nbg_go_device result survives later queries on the engine's own workspace."""
+    src, eng, orc = rmat12
+    wb = WHERES["w<50"].encode()
+    stmt = eng.prepare_go([1], 2, wb)
+    roots = graphs.roots(src, 14, seed=19)
+    held = []
+    try:
+        tickets = [stmt.submit([r], device=True) for r in roots]
+        held = [stmt.wait(t) for t in tickets]
+        sync = [stmt.run_device([r]) for r in roots[:3]]
+        for r, res in zip(roots, held):
+            exp = graphs.sorted_rows(orc.go([r], [1], 2, wb))
+            assert res.count == len(exp)
+            assert graphs.sorted_rows(res.fetch()) == exp, r
+        for r, res in zip(roots[:3], sync):
+            assert graphs.sorted_rows(res.fetch()) == graphs.sorted_rows(orc.go([r], [1], 2, wb)), r
+        held += sync
+    finally:
+        for res in held:
+            res.free()
+        stmt.free()
+
+
+def test_c1_go_2_steps_nba(nba, nba_data):
+    """BASELINE configs[0] (C1): GO 2 STEPS FROM "Tim Duncan" OVER like (the `follow` edge of
+    later releases is this reference's `like`) — device vs the oracle, plus
+    YIELD variants on the same hop pattern."""
+    from nebula_amd import ngql
+    from nebula_amd.vidhash import std_hash
+    orc = nba_oracle(nba_data)
+    try:
+        tim = std_hash("Tim Duncan")
+        for q in (f"GO 2 STEPS FROM {tim} OVER like",
+                  f"GO 2 STEPS FROM {tim} OVER like YIELD like._dst, like.likeness, $$.player.name",
+                  f"GO 2 STEPS FROM {tim} OVER like WHERE like.likeness >= 90 YIELD like._src, like._dst",
+                  f"GO 2 STEPS FROM {tim} OVER *"):
+            got = ngql.Session(nba).execute(q)
+            exp = ngql.Session(orc).execute(q)
+            assert got.columns == exp.columns, q
+            assert golden.rows_match(got.rows, exp.rows), q
+            assert got.rows, q
+    finally:
+        orc.close()
+
+
 def _forest(seed=3, roots=6, depth=4, fan=4):
     """A forest (every vertex has one parent): a final row's root is unique, so the reference's
     VertexBackTracker (last write wins over unordered responses) is deterministic on it."""
