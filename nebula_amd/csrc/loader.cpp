@@ -101,6 +101,25 @@ bool Engine::decode_row(const SchemaSet& ss, const uint8_t* v, size_t n, int64_t
 }
 
 // ----------------------------------------------------------------------------- ingest
+// One staged record (KV path).  The optional columns of EdgeStage materialise on the first
+// record that needs them, so bulk loads keep only src / dst / props.
+static void stage_push(EdgeStage& st, int64_t src, int64_t dst, int64_t rank, uint64_t verkey, int32_t part,
+                       int32_t parts) {
+  const uint64_t n = st.size();
+  if (n == 0 && st.verkey.empty()) st.ver0 = verkey;
+  if (st.rank.empty() && rank != 0) st.rank.assign(n, 0);
+  if (st.verkey.empty() && verkey != st.ver0) st.verkey.assign(n, st.ver0);
+  if (st.part.empty() && part != hash_part(src, parts)) {
+    st.part.resize(n);
+    for (uint64_t i = 0; i < n; ++i) st.part[i] = hash_part(st.src[i], parts);
+  }
+  st.src.push_back(src);
+  st.dst.push_back(dst);
+  if (!st.rank.empty()) st.rank.push_back(rank);
+  if (!st.verkey.empty()) st.verkey.push_back(verkey);
+  if (!st.part.empty()) st.part.push_back(part);
+}
+
 int32_t Engine::load_part_kv(int32_t part, const uint8_t* kd, const uint64_t* ko, const uint8_t* vd,
                              const uint64_t* vo, uint64_t n) {
   if (finalized) return fail(NBG_E_STATE, "engine already finalized");
@@ -127,21 +146,20 @@ int32_t Engine::load_part_kv(int32_t part, const uint8_t* kd, const uint64_t* ko
       memcpy(&dst, k + 24, 8);
       memcpy(&ver, k + 32, 8);
       EdgeStage& st = stage[type];
-      st.src.push_back(src);
-      st.dst.push_back(dst);
-      st.rank.push_back(rank);
-      st.verkey.push_back(bswap64(ver));
-      st.seq.push_back(seq++);
-      st.part.push_back(item >> 8);
+      const uint64_t at = st.size();
+      stage_push(st, src, dst, rank, bswap64(ver), item >> 8, cfg.num_parts);
+      ++seq;
       if (type > 0) {
         auto es = edges.find(type);
         const Schema* latest = es == edges.end() ? nullptr : es->second.latest();
         size_t nc = latest ? latest->cols.size() : 0;
-        if (st.props.size() < nc) st.props.resize(nc);
+        if (st.props.size() < nc) st.props.resize(nc, std::vector<int64_t>(at, 0));
         props.assign(nc, 0);
         bool ok = latest && decode_row(es->second, v, vlen, props.data());
         for (size_t c = 0; c < nc; ++c) st.props[c].push_back(ok ? props[c] : 0);
-        st.valid.push_back(ok ? 1 : 0);
+        for (size_t c = nc; c < st.props.size(); ++c) st.props[c].push_back(0);
+        if (!ok && st.valid.empty()) st.valid.assign(at, 1);
+        if (!st.valid.empty()) st.valid.push_back(ok ? 1 : 0);
       }
     } else if (klen == 24) {
       // vertex key (NebulaKeyUtils::vertexKey, NebulaKeyUtils.cpp:12-26): part | vid | tag | version
@@ -170,6 +188,32 @@ int32_t Engine::load_part_kv(int32_t part, const uint8_t* kd, const uint64_t* ko
   return NBG_OK;
 }
 
+// The indices i in [0, n) with keep(i), ascending (parallel, two passes).
+template <typename Keep>
+static std::vector<uint64_t> kept_indices(uint64_t n, Keep keep) {
+  const int T = omp_get_max_threads();
+  std::vector<uint64_t> cnt(T + 1, 0);
+#pragma omp parallel num_threads(T)
+  {
+    const int t = omp_get_thread_num();
+    const uint64_t b = n * t / T, e = n * (t + 1) / T;
+    uint64_t c = 0;
+    for (uint64_t i = b; i < e; ++i) c += keep(i) ? 1 : 0;
+    cnt[t + 1] = c;
+  }
+  for (int t = 0; t < T; ++t) cnt[t + 1] += cnt[t];
+  std::vector<uint64_t> idx(cnt[T]);
+#pragma omp parallel num_threads(T)
+  {
+    const int t = omp_get_thread_num();
+    const uint64_t b = n * t / T, e = n * (t + 1) / T;
+    uint64_t o = cnt[t];
+    for (uint64_t i = b; i < e; ++i)
+      if (keep(i)) idx[o++] = i;
+  }
+  return idx;
+}
+
 int32_t Engine::load_edges(int32_t type, const int64_t* src, const int64_t* dst, const int64_t* rank, uint64_t n,
                            const void* const* cols, int32_t ncols) {
   if (finalized) return fail(NBG_E_STATE, "engine already finalized");
@@ -179,60 +223,64 @@ int32_t Engine::load_edges(int32_t type, const int64_t* src, const int64_t* dst,
   if ((int32_t)latest->cols.size() != ncols) return fail(NBG_E_INVALID_ARGUMENT, "column count mismatch");
   for (auto& c : latest->cols)
     if (c.type == NBG_T_STRING) return fail(NBG_E_UNSUPPORTED, "bulk load of STRING columns");
-  EdgeStage& out = stage[type];
-  EdgeStage& in = stage[-type];
-  if (out.props.size() < (size_t)ncols) out.props.resize(ncols);
   const uint64_t ver = bswap64((uint64_t)(INT64_MAX - 1));   // one version for the whole batch
-  const int32_t P = cfg.num_parts, G = cfg.num_gpus;
-  for (uint64_t i = 0; i < n; ++i) {
-    int64_t r = rank ? rank[i] : 0;
-    int32_t ps = hash_part(src[i], P), pd = hash_part(dst[i], P);
-    if (G <= 1 || ps % G == cfg.rank) {
-      out.src.push_back(src[i]);
-      out.dst.push_back(dst[i]);
-      out.rank.push_back(r);
-      out.verkey.push_back(ver);
-      out.seq.push_back(seq + i);
-      out.part.push_back(ps);
-      for (int32_t c = 0; c < ncols; ++c) {
-        int64_t b = 0;
-        switch (latest->cols[c].type) {
-          case NBG_T_BOOL: b = static_cast<const uint8_t*>(cols[c])[i] != 0; break;
-          case NBG_T_FLOAT: case NBG_T_DOUBLE: memcpy(&b, static_cast<const double*>(cols[c]) + i, 8); break;
-          default: b = static_cast<const int64_t*>(cols[c])[i]; break;
+  const int32_t P = cfg.num_parts, G = cfg.num_gpus, R = cfg.rank;
+  bool any_rank = false;
+  if (rank) {
+#pragma omp parallel for reduction(|| : any_rank)
+    for (int64_t i = 0; i < (int64_t)n; ++i) any_rank = any_rank || rank[i] != 0;
+  }
+  // out-edges at src's part, in-edges (dst, -type, rank, src) with no props at dst's part
+  for (int side = 0; side < 2; ++side) {
+    EdgeStage& st = stage[side ? -type : type];
+    const int64_t* a = side ? dst : src;
+    const int64_t* b = side ? src : dst;
+    const uint64_t at = st.size();
+    if (at == 0 && st.verkey.empty()) st.ver0 = ver;
+    if (st.verkey.empty() && ver != st.ver0) st.verkey.assign(at, st.ver0);
+    if (any_rank && st.rank.empty()) st.rank.assign(at, 0);
+    const bool with_props = side == 0;
+    if (with_props && st.props.size() < (size_t)ncols) st.props.resize(ncols, std::vector<int64_t>(at, 0));
+    // a partitioned rank keeps the records of the parts it serves (part % G == rank)
+    std::vector<uint64_t> idx;
+    if (G > 1) idx = kept_indices(n, [&](uint64_t i) { return hash_part(a[i], P) % G == R; });
+    const uint64_t m = G > 1 ? idx.size() : n;
+    // grow every column to its final size first (the parallel writes below index into them)
+    st.src.resize(at + m);
+    st.dst.resize(at + m);
+    if (!st.rank.empty()) st.rank.resize(at + m);
+    if (!st.verkey.empty()) st.verkey.resize(at + m);
+    if (!st.part.empty()) st.part.resize(at + m);
+    if (!st.valid.empty()) st.valid.resize(at + m);
+    if (with_props)
+      for (int32_t c = 0; c < ncols; ++c) st.props[c].resize(at + m);
+    auto put = [&](uint64_t o, uint64_t i) {
+      st.src[o] = a[i];
+      st.dst[o] = b[i];
+      if (!st.rank.empty()) st.rank[o] = rank ? rank[i] : 0;
+      if (!st.verkey.empty()) st.verkey[o] = ver;
+      if (!st.part.empty()) st.part[o] = hash_part(a[i], P);
+      if (!st.valid.empty()) st.valid[o] = 1;
+      if (with_props) {
+        for (int32_t c = 0; c < ncols; ++c) {
+          int64_t x = 0;
+          switch (latest->cols[c].type) {
+            case NBG_T_BOOL: x = static_cast<const uint8_t*>(cols[c])[i] != 0; break;
+            case NBG_T_FLOAT: case NBG_T_DOUBLE: memcpy(&x, static_cast<const double*>(cols[c]) + i, 8); break;
+            default: x = static_cast<const int64_t*>(cols[c])[i]; break;
+          }
+          st.props[c][o] = x;
         }
-        out.props[c].push_back(b);
       }
-      out.valid.push_back(1);
-    }
-    if (G <= 1 || pd % G == cfg.rank) {
-      in.src.push_back(dst[i]);
-      in.dst.push_back(src[i]);
-      in.rank.push_back(r);
-      in.verkey.push_back(ver);
-      in.seq.push_back(seq + i);
-      in.part.push_back(pd);
-    }
+    };
+#pragma omp parallel for schedule(static)
+    for (int64_t k = 0; k < (int64_t)m; ++k) put(at + (uint64_t)k, G > 1 ? idx[k] : (uint64_t)k);
   }
   seq += n;
   return NBG_OK;
 }
 
 // ----------------------------------------------------------------------------- finalize
-namespace {
-struct RowKey {   // memcmp order of (rank | dst | version) then newest load first
-  uint64_t rank_be, dst_be, ver;
-  uint64_t seq;
-  uint64_t idx;
-};
-inline bool rowkey_less(const RowKey& a, const RowKey& b) {
-  if (a.rank_be != b.rank_be) return a.rank_be < b.rank_be;
-  if (a.dst_be != b.dst_be) return a.dst_be < b.dst_be;
-  if (a.ver != b.ver) return a.ver < b.ver;
-  return a.seq > b.seq;
-}
-}  // namespace
-
 // Every rank learns every rank's sorted vertex dictionary (allgather over the communicator):
 // npad = the largest dictionary rounded up to PART_ALIGN.
 int32_t Engine::exchange_dictionary(const std::vector<int64_t>& local, std::vector<int64_t>* gdict,
@@ -369,9 +417,12 @@ int32_t Engine::upload_tags() {
 // dense id -> vid table and the visibility flags
 int32_t Engine::upload_vertices(const std::vector<uint8_t>& visible, bool all_visible) {
   const uint64_t nv = snap.nv;
-  bool ok = hipMalloc((void**)&snap.d_vids, std::max<uint64_t>(nv, 1) * 8) == hipSuccess &&
-            hipMemcpy(snap.d_vids, snap.h_vids.data(), nv * 8, hipMemcpyHostToDevice) == hipSuccess;
-  snap.device_bytes += nv * 8;
+  bool ok = true;
+  if (!snap.d_vids) {   // (finalize builds the table on the device; a snapshot file uploads it)
+    ok = hipMalloc((void**)&snap.d_vids, std::max<uint64_t>(nv, 1) * 8) == hipSuccess &&
+         hipMemcpy(snap.d_vids, snap.h_vids.data(), nv * 8, hipMemcpyHostToDevice) == hipSuccess;
+    snap.device_bytes += nv * 8;
+  }
   if (ok && !all_visible) {
     snap.h_visible = visible;
     ok = hipMalloc((void**)&snap.d_visible, nv) == hipSuccess &&
@@ -438,6 +489,28 @@ bool Engine::upload_type(DevEdgeType& dt, uint64_t nv, const std::vector<uint32_
 
 int32_t Engine::finalize() {
   if (finalized) return fail(NBG_E_STATE, "engine already finalized");
+  const hipStream_t s = stream;
+  // device temporaries of the build, released on every exit
+  std::map<int32_t, int64_t*> d_src;
+  std::vector<void*> tmp;
+  auto cleanup = [&]() {
+    for (auto& kv : d_src)
+      if (kv.second) (void)hipFree(kv.second);
+    d_src.clear();
+    for (void* p : tmp)
+      if (p) (void)hipFree(p);
+    tmp.clear();
+  };
+  auto bail = [&](int32_t code, const std::string& msg) {
+    cleanup();
+    free_snapshot();
+    return fail(code, msg);
+  };
+  auto hip = [&](hipError_t e, const char* what) -> bool {
+    if (e == hipSuccess) return true;
+    last_error = std::string(what) + ": " + hipGetErrorString(e);
+    return false;
+  };
   // 1. string dictionary: sorted; device code = 2 * rank
   std::vector<int64_t> remap(pool.size());
   {
@@ -450,164 +523,191 @@ int32_t Engine::finalize() {
       remap[id] = 2 * (int64_t)(snap.strings.size() - 1);
     }
   }
-  // 2. vertex dictionary: every vid that owns a row (src of any signed type)
-  std::vector<int64_t> all;
+  // 2. vertex dictionary on the device: every vid that owns a row (the source of any signed
+  // type's record, or a tag record): per-type sorted sets, then their union
+  std::vector<int64_t> tag_vids;
+  for (auto& kv : tstage) tag_vids.insert(tag_vids.end(), kv.second.vid.begin(), kv.second.vid.end());
+  int64_t* d_dict = nullptr;
+  uint64_t nv = 0;
   {
-    size_t tot = 0;
-    for (auto& kv : stage) tot += kv.second.src.size();
-    all.reserve(tot);
-    for (auto& kv : stage) all.insert(all.end(), kv.second.src.begin(), kv.second.src.end());
-    for (auto& kv : tstage) all.insert(all.end(), kv.second.vid.begin(), kv.second.vid.end());
-    __gnu_parallel::sort(all.begin(), all.end());
-    all.erase(std::unique(all.begin(), all.end()), all.end());
+    std::vector<std::pair<int64_t*, uint64_t>> sets;
+    uint64_t tot = tag_vids.size();
+    for (auto& kv : stage) {
+      const uint64_t n = kv.second.size();
+      int64_t* d = nullptr;
+      if (!hip(hipMalloc((void**)&d, std::max<uint64_t>(n, 1) * 8), "device allocation (sources)"))
+        return bail(NBG_E_OUT_OF_MEMORY, last_error);
+      d_src[kv.first] = d;
+      if (n && !hip(hipMemcpyAsync(d, kv.second.src.data(), n * 8, hipMemcpyHostToDevice, s), "upload"))
+        return bail(NBG_E_DEVICE, last_error);
+      int64_t* u = nullptr;
+      uint64_t nu = 0;
+      if (!hip(bd_sort_unique(d, n, &u, &nu, s), "vertex dictionary")) return bail(NBG_E_DEVICE, last_error);
+      tmp.push_back(u);
+      sets.emplace_back(u, nu);
+      tot += nu;
+    }
+    int64_t* cat = nullptr;
+    if (!hip(hipMalloc((void**)&cat, std::max<uint64_t>(tot, 1) * 8), "device allocation (dictionary)"))
+      return bail(NBG_E_OUT_OF_MEMORY, last_error);
+    tmp.push_back(cat);
+    uint64_t o = 0;
+    for (auto& u : sets) {
+      if (u.second && !hip(hipMemcpyAsync(cat + o, u.first, u.second * 8, hipMemcpyDeviceToDevice, s), "copy"))
+        return bail(NBG_E_DEVICE, last_error);
+      o += u.second;
+    }
+    if (!tag_vids.empty() &&
+        !hip(hipMemcpyAsync(cat + o, tag_vids.data(), tag_vids.size() * 8, hipMemcpyHostToDevice, s), "upload"))
+      return bail(NBG_E_DEVICE, last_error);
+    if (!hip(bd_sort_unique(cat, tot, &d_dict, &nv, s), "vertex dictionary")) return bail(NBG_E_DEVICE, last_error);
+    snap.d_vids = d_dict;   // the snapshot's dense id -> vid table
+    snap.device_bytes += std::max<uint64_t>(nv, 1) * 8;
   }
-  const uint64_t nv = all.size();
-  if (nv >= NO_ROW) return fail(NBG_E_UNSUPPORTED, "more than 2^32-1 vertices on one GPU");
+  if (nv >= NO_ROW) return bail(NBG_E_UNSUPPORTED, "more than 2^32-1 vertices on one GPU");
   snap.nv = nv;
+  std::vector<int64_t> all(nv);
+  if (nv && !hip(hipMemcpy(all.data(), d_dict, nv * 8, hipMemcpyDeviceToHost), "download"))
+    return bail(NBG_E_DEVICE, last_error);
   snap.h_vids = all;
   auto dense = [&](int64_t vid) -> uint32_t {
     auto it = std::lower_bound(all.begin(), all.end(), vid);
     return (it != all.end() && *it == vid) ? (uint32_t)(it - all.begin()) : NO_ROW;
   };
-  // dense id of every record's source (reused by the CSR build); home part per vertex — a vid
-  // whose rows sit in two parts is not representable
-  std::map<int32_t, std::vector<uint32_t>> src_dense;
+  // 2a. home part per vertex; a vid whose rows sit in two parts is not representable.  Records
+  // loaded without an explicit part sit in their source's hash part.
   std::vector<int32_t> home(nv, 0);
-  bool all_visible = true;
+  bool explicit_parts = false;
+  for (auto& kv : stage) explicit_parts = explicit_parts || !kv.second.part.empty();
+  for (auto& kv : tstage)
+    for (size_t i = 0; i < kv.second.vid.size() && !explicit_parts; ++i)
+      explicit_parts = kv.second.part[i] != hash_part(kv.second.vid[i], cfg.num_parts);
   bool split = false;
-  for (auto& kv : stage) {
-    auto& st = kv.second;
-    auto& sd = src_dense[kv.first];
-    sd.resize(st.src.size());
-#pragma omp parallel for schedule(static) reduction(|| : split)
-    for (int64_t i = 0; i < (int64_t)st.src.size(); ++i) {
-      const uint32_t d = dense(st.src[i]);
-      sd[i] = d;
-      int32_t expected = 0;
-      if (!__atomic_compare_exchange_n(&home[d], &expected, st.part[i], false, __ATOMIC_RELAXED, __ATOMIC_RELAXED) &&
-          expected != st.part[i])
-        split = true;
+  if (explicit_parts) {
+    int32_t* d_home = nullptr;
+    if (!hip(hipMalloc((void**)&d_home, std::max<uint64_t>(nv, 1) * 4), "device allocation (home)"))
+      return bail(NBG_E_OUT_OF_MEMORY, last_error);
+    tmp.push_back(d_home);
+    if (!hip(hipMemsetAsync(d_home, 0, std::max<uint64_t>(nv, 1) * 4, s), "memset"))
+      return bail(NBG_E_DEVICE, last_error);
+    for (auto& kv : stage) {
+      bool sp = false;
+      const EdgeStage& st = kv.second;
+      if (!hip(bd_home(d_home, d_src[kv.first], st.part.empty() ? nullptr : st.part.data(), st.size(), d_dict, nv,
+                       cfg.num_parts, &sp, s),
+               "home parts"))
+        return bail(NBG_E_DEVICE, last_error);
+      split = split || sp;
     }
-  }
-  for (auto& kv : tstage) {
-    const TagStage& ts = kv.second;
-    for (size_t i = 0; i < ts.vid.size(); ++i) {
-      const uint32_t d = dense(ts.vid[i]);
-      if (home[d] == 0) home[d] = ts.part[i];
-      else if (home[d] != ts.part[i]) split = true;
+    if (nv && !hip(hipMemcpy(home.data(), d_home, nv * 4, hipMemcpyDeviceToHost), "download"))
+      return bail(NBG_E_DEVICE, last_error);
+    for (auto& kv : tstage) {
+      const TagStage& ts = kv.second;
+      for (size_t i = 0; i < ts.vid.size(); ++i) {
+        const uint32_t d = dense(ts.vid[i]);
+        if (home[d] == 0) home[d] = ts.part[i];
+        else if (home[d] != ts.part[i]) split = true;
+      }
     }
+  } else {
+#pragma omp parallel for schedule(static)
+    for (int64_t d = 0; d < (int64_t)nv; ++d) home[d] = hash_part(all[d], cfg.num_parts);
   }
-  if (split) return fail(NBG_E_UNSUPPORTED, "vertex rows split across partitions");
+  if (split) return bail(NBG_E_UNSUPPORTED, "vertex rows split across partitions");
+  bool all_visible = true;
   std::vector<uint8_t> visible(nv, 1);
-  for (uint64_t d = 0; d < nv; ++d) {
-    if (home[d] != hash_part(all[d], cfg.num_parts)) { visible[d] = 0; all_visible = false; }
+  if (explicit_parts) {
+    for (uint64_t d = 0; d < nv; ++d) {
+      if (home[d] != hash_part(all[d], cfg.num_parts)) { visible[d] = 0; all_visible = false; }
+    }
   }
   snap.h_part = home;
 
   // 2b. partitioned mode: a global id space [G * npad) — rank q's vertices are q * npad + local
   // id — so a neighbour id names its owner (the rank serving its hash part) without a lookup.
-  std::vector<int64_t> gdict;
-  std::vector<uint64_t> gcount;
+  GidMap gm;
+  gm.dict = d_dict;
+  gm.nv = nv;
+  gm.parts = cfg.num_parts;
+  gm.gpus = cfg.num_gpus;
   if (partitioned()) {
+    std::vector<int64_t> gdict;
+    std::vector<uint64_t> gcount;
     int32_t prc = exchange_dictionary(all, &gdict, &gcount);
-    if (prc) return prc;
+    if (prc) {
+      const std::string msg = last_error;
+      return bail(prc, msg);
+    }
+    int64_t* d_g = nullptr;
+    uint64_t* d_c = nullptr;
+    if (!hip(hipMalloc((void**)&d_g, std::max<size_t>(gdict.size(), 1) * 8), "device allocation") ||
+        !hip(hipMalloc((void**)&d_c, std::max<size_t>(gcount.size(), 1) * 8), "device allocation"))
+      return bail(NBG_E_OUT_OF_MEMORY, last_error);
+    tmp.push_back(d_g);
+    tmp.push_back(d_c);
+    if (!hip(hipMemcpy(d_g, gdict.data(), gdict.size() * 8, hipMemcpyHostToDevice), "upload") ||
+        !hip(hipMemcpy(d_c, gcount.data(), gcount.size() * 8, hipMemcpyHostToDevice), "upload"))
+      return bail(NBG_E_DEVICE, last_error);
+    gm.gdict = d_g;
+    gm.gcount = d_c;
+    gm.npad = npad;
   }
-  const int32_t G = cfg.num_gpus;
-  auto gid = [&](int64_t vid) -> uint32_t {
-    if (!partitioned()) return dense(vid);
-    const uint64_t q = (uint64_t)(hash_part(vid, cfg.num_parts) % G);
-    auto b = gdict.begin() + q * npad, e = b + gcount[q];
-    auto it = std::lower_bound(b, e, vid);
-    return (it != e && *it == vid) ? (uint32_t)(q * npad + (uint64_t)(it - b)) : NO_ROW;
-  };
 
-  // 3. per signed type: bucket by src, sort rows in key order, keep the live version
-  int32_t rc = NBG_OK;
+  // 3. per signed type: CSR on the device (records sorted in key order, the live version kept)
   for (auto& kv : stage) {
     const int32_t type = kv.first;
     EdgeStage& st = kv.second;
-    const uint64_t n = st.src.size();
-    std::vector<uint32_t> sd = std::move(src_dense[type]);
-    std::vector<uint64_t> cnt(nv + 1, 0);
-#pragma omp parallel for schedule(static)
-    for (int64_t i = 0; i < (int64_t)n; ++i) __atomic_fetch_add(&cnt[sd[i] + 1], 1ull, __ATOMIC_RELAXED);
-    for (uint64_t d = 0; d < nv; ++d) cnt[d + 1] += cnt[d];
-    std::vector<RowKey> keys(n);
-    {
-      // bucket order inside a vertex does not matter: each bucket is sorted by rowkey_less
-      // (a total order: load sequence breaks ties)
-      std::vector<uint64_t> cur(cnt.begin(), cnt.end() - 1);
-#pragma omp parallel for schedule(static)
-      for (int64_t i = 0; i < (int64_t)n; ++i) {
-        const uint64_t p = __atomic_fetch_add(&cur[sd[i]], 1ull, __ATOMIC_RELAXED);
-        keys[p] = RowKey{bswap64((uint64_t)st.rank[i]), bswap64((uint64_t)st.dst[i]), st.verkey[i], st.seq[i],
-                         (uint64_t)i};
-      }
-    }
-    std::vector<uint32_t> live(nv + 1, 0);
-#pragma omp parallel for schedule(dynamic, 4096)
-    for (int64_t d = 0; d < (int64_t)nv; ++d) {
-      auto b = keys.begin() + cnt[d], e = keys.begin() + cnt[d + 1];
-      if (e - b > 1) std::sort(b, e, rowkey_less);
-      uint32_t m = 0;
-      for (auto it = b; it != e; ++it) {
-        if (it != b && it->rank_be == (it - 1)->rank_be && it->dst_be == (it - 1)->dst_be) continue;
-        b[m++] = *it;   // compact in place (m <= position)
-      }
-      live[d + 1] = m;
-    }
-    std::vector<uint64_t> rp(nv + 1, 0);
-    for (uint64_t d = 0; d < nv; ++d) rp[d + 1] = rp[d] + live[d + 1];
-    const uint64_t E = rp[nv];
-    if (E >= 0xFFFFFFFFull) return fail(NBG_E_UNSUPPORTED, "more than 2^32-1 edges of one type on one GPU");
-    DevEdgeType& dt = snap.types[type];
-    dt.type = type;
-    dt.num_edges = E;
-    dt.h_row_ptr.resize(nv + 1);
-    for (uint64_t d = 0; d <= nv; ++d) dt.h_row_ptr[d] = (uint32_t)rp[d];
-    std::vector<uint32_t> col(E);
-    std::vector<int64_t> dvid(E), rk(E);
     const size_t nc = type > 0 ? st.props.size() : 0;
-    std::vector<std::vector<int64_t>> pc(nc, std::vector<int64_t>(E));
-    std::vector<uint8_t> valid(type > 0 ? E : 0);
-    bool any_rank = false, any_invalid = false;
     std::vector<VKind> kinds(nc, VK_INT);
     if (nc) {
       const Schema* latest = edges[type].latest();
       for (size_t c = 0; c < nc; ++c) kinds[c] = kindOfType(latest->cols[c].type);
     }
-#pragma omp parallel for schedule(dynamic, 4096) reduction(|| : any_rank, any_invalid)
-    for (int64_t d = 0; d < (int64_t)nv; ++d) {
-      uint64_t o = rp[d];
-      for (uint32_t m = 0; m < live[d + 1]; ++m) {
-        const RowKey& k = keys[cnt[d] + m];
-        uint64_t i = k.idx;
-        col[o + m] = gid(st.dst[i]);
-        dvid[o + m] = st.dst[i];
-        rk[o + m] = st.rank[i];
-        if (st.rank[i]) any_rank = true;
-        for (size_t c = 0; c < nc; ++c) {
-          int64_t b = st.props[c][i];
-          if (kinds[c] == VK_STRING && st.valid[i]) b = remap[b];
-          pc[c][o + m] = b;
-        }
-        if (type > 0) {
-          valid[o + m] = st.valid[i];
-          if (!st.valid[i]) any_invalid = true;
-        }
-      }
+    for (size_t c = 0; c < nc; ++c) {   // string ids -> dictionary codes
+      if (kinds[c] != VK_STRING) continue;
+      std::vector<int64_t>& col = st.props[c];
+#pragma omp parallel for schedule(static)
+      for (int64_t i = 0; i < (int64_t)col.size(); ++i)
+        if (st.valid.empty() || st.valid[i]) col[i] = remap[col[i]];
     }
-    bool ok = upload_type(dt, nv, col, dvid, any_rank ? &rk : nullptr, pc, any_invalid ? &valid : nullptr, kinds);
-    if (!ok) { rc = fail(NBG_E_OUT_OF_MEMORY, "device allocation failed for the snapshot"); break; }
-
-    EdgeStage().src.swap(st.src);   // release staging as we go
+    std::vector<const int64_t*> pcols(nc);
+    for (size_t c = 0; c < nc; ++c) pcols[c] = st.props[c].data();
+    TypeBuildIn in;
+    in.n = st.size();
+    in.d_src = d_src[type];
+    in.dst = st.dst.data();
+    in.rank = st.rank.empty() ? nullptr : st.rank.data();
+    in.verkey = st.verkey.empty() ? nullptr : st.verkey.data();
+    in.nprops = (int)nc;
+    in.props = pcols.data();
+    in.kinds = kinds.data();
+    in.valid = (type > 0 && !st.valid.empty()) ? st.valid.data() : nullptr;
+    DevEdgeType& dt = snap.types[type];
+    dt.type = type;
+    dt.prop_kind = kinds;
+    uint64_t bytes = 0;
+    std::string err;
+    hipError_t he = bd_build_type(in, gm, s, &dt, &bytes, &err);
+    if (he != hipSuccess) {
+      if (err.empty()) err = std::string("snapshot build: ") + hipGetErrorString(he);
+      return bail(he == hipErrorOutOfMemory ? NBG_E_OUT_OF_MEMORY
+                                            : (he == hipErrorInvalidValue ? NBG_E_UNSUPPORTED : NBG_E_DEVICE),
+                  err);
+    }
+    if (dt.num_edges >= 0xFFFFFFFFull) return bail(NBG_E_UNSUPPORTED, "more than 2^32-1 edges of one type on one GPU");
+    snap.device_bytes += bytes;
+    (void)hipFree(d_src[type]);   // release as we go
+    d_src[type] = nullptr;
     st = EdgeStage();
   }
-  if (rc) return rc;
-  rc = build_tags(all, remap);
-  if (rc) return rc;
-  rc = upload_vertices(visible, all_visible);
-  if (rc) return rc;
+  cleanup();
+  int32_t rc = build_tags(all, remap);
+  if (!rc) rc = upload_vertices(visible, all_visible);
+  if (rc) {
+    const std::string msg = last_error;
+    free_snapshot();
+    return fail(rc, msg);
+  }
   stage.clear();
   tstage.clear();
   pool.clear();

@@ -52,13 +52,15 @@ inline VKind kindOfType(int32_t t) {
 }
 
 // ----------------------------------------------------------------------------- host staging
-struct EdgeStage {              // one signed edge type, before finalize
-  std::vector<int64_t> src, dst, rank;
-  std::vector<uint64_t> verkey; // version bytes read big-endian (memcmp order)
-  std::vector<uint64_t> seq;    // load order (identical keys: later wins)
-  std::vector<int32_t> part;
+struct EdgeStage {              // one signed edge type, before finalize: records in load order
+  std::vector<int64_t> src, dst;                 // (identical keys: the later record wins)
+  std::vector<int64_t> rank;    // empty: every rank so far is 0
+  std::vector<uint64_t> verkey; // version bytes read big-endian (memcmp order); empty: all == ver0
+  uint64_t ver0 = 0;
+  std::vector<int32_t> part;    // empty: every record so far sits in its source's hash part
   std::vector<std::vector<int64_t>> props;   // [col][i] 8-byte payload (positive types)
-  std::vector<uint8_t> valid;                // value decoded (positive types)
+  std::vector<uint8_t> valid;   // value decoded (positive types); empty: all decoded
+  uint64_t size() const { return src.size(); }
 };
 
 struct TagStage {               // one tag's vertex records, before finalize
@@ -303,6 +305,38 @@ struct Comm {
 };
 Comm* comm_rccl(const uint8_t id[NBG_UNIQUE_ID_BYTES], int world, int rank, std::string* err);
 std::vector<Comm*> comm_local_group(int world);
+
+// ----------------------------------------------------------------------------- snapshot build (build.hip)
+// Neighbour id of a vid: single GPU = its dense id in `dict`; partitioned = owner * npad + its
+// index in the owner's dictionary (gdict = every rank's dictionary, npad apart).
+struct GidMap {
+  const int64_t* dict = nullptr;    // device, sorted local dictionary
+  uint64_t nv = 0;
+  const int64_t* gdict = nullptr;   // device [G * npad] (partitioned) or nullptr
+  const uint64_t* gcount = nullptr; // device [G]
+  uint64_t npad = 0;
+  int32_t gpus = 1, parts = 1;
+};
+struct TypeBuildIn {                // one signed type's staged records, load order
+  uint64_t n = 0;
+  const int64_t* d_src = nullptr;   // device copy of the sources
+  const int64_t* dst = nullptr;     // host arrays from here on
+  const int64_t* rank = nullptr;    // nullptr: every rank is 0
+  const uint64_t* verkey = nullptr; // nullptr: one version for every record
+  int nprops = 0;
+  const int64_t* const* props = nullptr;   // [nprops][n] (string ids already dictionary codes)
+  const VKind* kinds = nullptr;
+  const uint8_t* valid = nullptr;   // nullptr: every value decoded
+};
+// sorted unique values of n device int64s -> *out (hipMalloc'd, *n_out entries)
+hipError_t bd_sort_unique(const int64_t* d_in, uint64_t n, int64_t** out, uint64_t* n_out, hipStream_t s);
+// home part per dense id (d_home zeroed by the caller): part[i] or, when null, the source's hash part
+hipError_t bd_home(int32_t* d_home, const int64_t* d_src, const int32_t* part, uint64_t n, const int64_t* d_dict,
+                   uint64_t nv, int32_t parts, bool* split, hipStream_t s);
+// CSR of one signed type over the dictionary's vertices (row_ptr, col, dst_vid, rank, props,
+// narrow INT copies, valid, h_row_ptr, max_degree); *bytes = device bytes kept
+hipError_t bd_build_type(const TypeBuildIn& in, const GidMap& gm, hipStream_t s, DevEdgeType* out, uint64_t* bytes,
+                         std::string* err);
 
 struct Workspace;   // kernels.hip
 

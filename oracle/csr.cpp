@@ -1,0 +1,467 @@
+// SPDX: test infrastructure — NOT product code.
+//
+// CSR ORACLE: a second CPU restatement of the same semantics, over an in-memory CSR instead of
+// the storaged-faithful KV store (storage.cpp / graph.cpp).  Two jobs:
+//   * the checker at sizes the faithful restatement cannot reach in seconds (RMAT-22 full row
+//     compares, RMAT-26 order-independent digests);
+//   * CPU baseline mode (ii) of SURVEY.md §8(d): an OpenMP CSR GO / bidirectional BFS, the
+//     honest "good CPU" denominator next to the storaged-faithful mode (i).
+// It is pinned to the faithful restatement on RMAT <= 12 (tests/test_oracle_csr.py).  Only
+// tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use it.
+//
+// Semantics restated (paths relative to the reference checkout):
+//   * one live edge per (src, dst) — rank 0, the last sample wins (AddEdgesProcessor.cpp:15-37
+//     same-key overwrite); in-edges mirror out-edges (InsertEdgeExecutor.cpp:180-196);
+//   * GO N STEPS: starts keep duplicates; frontier_{s+1} = SET of _dst over the step's edges, no
+//     global visited set (GoExecutor.cpp:501-541); final step: one row per (frontier entry, live
+//     edge) passing WHERE (GoExecutor.cpp:803-984);
+//   * FIND SHORTEST PATH s -> t UPTO n: minimal hop count, one path, ties broken by the
+//     lexicographically smallest vid sequence (the build's canonical rule), length
+//     >= 1 (s == t asks for the shortest cycle through s, FindPathExecutor.cpp:218-290).
+#include <omp.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+namespace {
+
+inline uint64_t mix64(uint64_t z) {   // splitmix64 finaliser
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+inline uint64_t splitmix64(uint64_t x) { return mix64(x + 0x9E3779B97F4A7C15ull); }
+
+struct Csr {
+  uint64_t nv = 0, ne = 0;
+  std::vector<int64_t> vid;                 // dense id -> vid (bucket-major; not sorted)
+  std::vector<uint64_t> off, ioff;          // out / in row offsets [nv + 1]
+  std::vector<uint32_t> nbr, inbr;          // out / in neighbour dense ids
+  std::vector<int64_t> w;                   // out-edge weight column
+  // vid -> dense id: hash bucket, then binary search inside the bucket's sorted vids
+  int bbits = 0;
+  std::vector<uint64_t> bstart;             // [B + 1] first dense id of each bucket
+  int threads = 1;
+  // per-query labels (epoch-stamped: no clearing between queries)
+  std::vector<uint32_t> labf, labb;
+  uint32_t epoch = 0;
+
+  uint64_t bucket_of(int64_t v) const { return mix64((uint64_t)v) >> (64 - bbits); }
+  int64_t dense(int64_t v) const {
+    const uint64_t b = bucket_of(v);
+    auto lo = vid.begin() + bstart[b], hi = vid.begin() + bstart[b + 1];
+    auto it = std::lower_bound(lo, hi, v);
+    return (it != hi && *it == v) ? (int64_t)(it - vid.begin()) : -1;
+  }
+};
+
+// Stable bucketing of `keys` by key -> bucket id (parallel counting sort); returns the bucket
+// offsets and the permutation (order[i] = index into keys).
+template <typename BucketFn>
+void bucket_sort(uint64_t n, uint64_t nb, BucketFn bucket, int T, std::vector<uint64_t>& start,
+                 std::vector<uint64_t>& order) {
+  std::vector<uint64_t> cnt((uint64_t)T * nb, 0);
+#pragma omp parallel num_threads(T)
+  {
+    const int t = omp_get_thread_num();
+    const uint64_t b = n * t / T, e = n * (t + 1) / T;
+    uint64_t* c = cnt.data() + (uint64_t)t * nb;
+    for (uint64_t i = b; i < e; ++i) ++c[bucket(i)];
+  }
+  start.assign(nb + 1, 0);
+  // bucket-major, thread-minor prefix: stable
+  uint64_t run = 0;
+  for (uint64_t k = 0; k < nb; ++k) {
+    start[k] = run;
+    for (int t = 0; t < T; ++t) {
+      const uint64_t x = cnt[(uint64_t)t * nb + k];
+      cnt[(uint64_t)t * nb + k] = run;
+      run += x;
+    }
+  }
+  start[nb] = run;
+  order.resize(n);
+#pragma omp parallel num_threads(T)
+  {
+    const int t = omp_get_thread_num();
+    const uint64_t b = n * t / T, e = n * (t + 1) / T;
+    uint64_t* c = cnt.data() + (uint64_t)t * nb;
+    for (uint64_t i = b; i < e; ++i) order[c[bucket(i)]++] = i;
+  }
+}
+
+Csr* build(const int64_t* src, const int64_t* dst, const int64_t* w, uint64_t n, int T) {
+  auto* g = new Csr();
+  g->threads = T;
+  // ---- vertex dictionary: every endpoint, hashed into buckets, sorted and de-duplicated
+  g->bbits = 8;
+  while (g->bbits < 24 && (1ull << g->bbits) * 4096 < 2 * n) ++g->bbits;
+  const uint64_t B = 1ull << g->bbits;
+  std::vector<uint64_t> bst, order;
+  bucket_sort(2 * n, B, [&](uint64_t i) { return g->bucket_of(i < n ? src[i] : dst[i - n]); }, T, bst, order);
+  std::vector<uint32_t> dense_of(2 * n);
+  std::vector<uint64_t> bu(B + 1, 0);   // unique vids per bucket
+  std::vector<std::vector<int64_t>> uniq(B);
+#pragma omp parallel for schedule(dynamic, 64) num_threads(T)
+  for (int64_t b = 0; b < (int64_t)B; ++b) {
+    std::vector<int64_t>& u = uniq[b];
+    for (uint64_t k = bst[b]; k < bst[b + 1]; ++k) {
+      const uint64_t i = order[k];
+      u.push_back(i < n ? src[i] : dst[i - n]);
+    }
+    std::sort(u.begin(), u.end());
+    u.erase(std::unique(u.begin(), u.end()), u.end());
+    bu[b + 1] = u.size();
+  }
+  for (uint64_t b = 0; b < B; ++b) bu[b + 1] += bu[b];
+  g->nv = bu[B];
+  g->bstart = bu;
+  g->vid.resize(g->nv);
+#pragma omp parallel for schedule(dynamic, 64) num_threads(T)
+  for (int64_t b = 0; b < (int64_t)B; ++b) {
+    std::copy(uniq[b].begin(), uniq[b].end(), g->vid.begin() + bu[b]);
+    const std::vector<int64_t>& u = uniq[b];
+    for (uint64_t k = bst[b]; k < bst[b + 1]; ++k) {
+      const uint64_t i = order[k];
+      const int64_t v = i < n ? src[i] : dst[i - n];
+      dense_of[i] = (uint32_t)(bu[b] + (std::lower_bound(u.begin(), u.end(), v) - u.begin()));
+    }
+    std::vector<int64_t>().swap(uniq[b]);
+  }
+  std::vector<uint64_t>().swap(order);
+  const uint64_t nv = g->nv;
+  // ---- out CSR: edges by dense source (stable: load order inside a row), then per row by
+  // (dst, load order descending) — the first of each dst is the live edge (last sample wins)
+  std::vector<uint64_t> rs, eo;
+  bucket_sort(n, nv, [&](uint64_t i) { return dense_of[i]; }, T, rs, eo);
+  std::vector<uint32_t> live_cnt(nv, 0);
+#pragma omp parallel for schedule(dynamic, 1024) num_threads(T)
+  for (int64_t d = 0; d < (int64_t)nv; ++d) {
+    auto b = eo.begin() + rs[d], e = eo.begin() + rs[d + 1];
+    std::sort(b, e, [&](uint64_t x, uint64_t y) {
+      const uint32_t dx = dense_of[n + x], dy = dense_of[n + y];
+      return dx != dy ? dx < dy : x > y;
+    });
+    uint64_t m = 0;
+    for (auto it = b; it != e; ++it)
+      if (it == b || dense_of[n + *it] != dense_of[n + *(it - 1)]) b[m++] = *it;
+    live_cnt[d] = (uint32_t)m;
+  }
+  g->off.assign(nv + 1, 0);
+  for (uint64_t d = 0; d < nv; ++d) g->off[d + 1] = g->off[d] + live_cnt[d];
+  g->ne = g->off[nv];
+  g->nbr.resize(g->ne);
+  g->w.resize(g->ne);
+#pragma omp parallel for schedule(dynamic, 1024) num_threads(T)
+  for (int64_t d = 0; d < (int64_t)nv; ++d) {
+    for (uint32_t k = 0; k < live_cnt[d]; ++k) {
+      const uint64_t i = eo[rs[d] + k];
+      g->nbr[g->off[d] + k] = dense_of[n + i];
+      g->w[g->off[d] + k] = w ? w[i] : 0;
+    }
+  }
+  // ---- in CSR: the mirror of every live out-edge, grouped by destination
+  std::vector<uint32_t> icnt(nv + 1, 0);
+  for (uint64_t j = 0; j < g->ne; ++j) ++icnt[g->nbr[j] + 1];
+  g->ioff.assign(nv + 1, 0);
+  for (uint64_t d = 0; d < nv; ++d) g->ioff[d + 1] = g->ioff[d] + icnt[d + 1];
+  g->inbr.resize(g->ne);
+  std::vector<uint64_t> cur(g->ioff.begin(), g->ioff.end() - 1);
+  for (uint64_t d = 0; d < nv; ++d)
+    for (uint64_t j = g->off[d]; j < g->off[d + 1]; ++j) g->inbr[cur[g->nbr[j]]++] = (uint32_t)d;
+  g->labf.assign(nv, 0);
+  g->labb.assign(nv, 0);
+  return g;
+}
+
+// ---------------------------------------------------------------- GO N STEPS
+struct GoOut {
+  uint64_t rows = 0, x = 0, sum = 0, scanned = 0;
+};
+
+enum { Y_DST = 1, Y_SRC = 2, Y_W = 4 };
+
+inline bool where_ok(int op, int64_t w, int64_t c) {
+  switch (op) {
+    case 0: return true;
+    case 1: return w < c;
+    case 2: return w <= c;
+    case 3: return w > c;
+    case 4: return w >= c;
+    case 5: return w == c;
+    default: return w != c;
+  }
+}
+
+// rows_out (nullable, cap rows x ncols int64, row-major): the first `cap` rows, any order
+GoOut go(Csr& g, const int64_t* starts, uint64_t ns, uint32_t steps, int op, int64_t c, int ymask, int64_t* rows_out,
+         uint64_t cap) {
+  GoOut out;
+  const int T = g.threads;
+  std::vector<uint32_t> f;
+  for (uint64_t i = 0; i < ns; ++i) {
+    const int64_t d = g.dense(starts[i]);
+    if (d >= 0) f.push_back((uint32_t)d);
+  }
+  std::vector<uint64_t> bits;
+  for (uint32_t s = 1; s < steps && !f.empty(); ++s) {
+    bits.assign((g.nv + 63) / 64, 0);
+    uint64_t sc = 0;
+#pragma omp parallel for schedule(dynamic, 64) reduction(+ : sc) num_threads(T)
+    for (int64_t k = 0; k < (int64_t)f.size(); ++k) {
+      const uint32_t v = f[k];
+      sc += g.off[v + 1] - g.off[v];
+      for (uint64_t j = g.off[v]; j < g.off[v + 1]; ++j) {
+        const uint32_t u = g.nbr[j];
+        const uint64_t m = 1ull << (u & 63);
+        if (!(__atomic_load_n(&bits[u >> 6], __ATOMIC_RELAXED) & m)) __atomic_fetch_or(&bits[u >> 6], m, __ATOMIC_RELAXED);
+      }
+    }
+    out.scanned += sc;
+    f.clear();
+    for (uint64_t wd = 0; wd < bits.size(); ++wd)
+      for (uint64_t b = bits[wd]; b; b &= b - 1) f.push_back((uint32_t)(wd * 64 + __builtin_ctzll(b)));
+  }
+  if (f.empty()) return out;
+  const int ncols = __builtin_popcount(ymask);
+  std::atomic<uint64_t> wr{0};
+  uint64_t rows = 0, x = 0, sum = 0, sc = 0;
+#pragma omp parallel for schedule(dynamic, 64) reduction(+ : rows, sum, sc) reduction(^ : x) num_threads(T)
+  for (int64_t k = 0; k < (int64_t)f.size(); ++k) {
+    const uint32_t v = f[k];
+    sc += g.off[v + 1] - g.off[v];
+    for (uint64_t j = g.off[v]; j < g.off[v + 1]; ++j) {
+      if (!where_ok(op, g.w[j], c)) continue;
+      int64_t cols[3];
+      int n = 0;
+      if (ymask & Y_DST) cols[n++] = g.vid[g.nbr[j]];
+      if (ymask & Y_SRC) cols[n++] = g.vid[v];
+      if (ymask & Y_W) cols[n++] = g.w[j];
+      uint64_t h = 0;
+      for (int q = 0; q < n; ++q) h = splitmix64(h ^ (uint64_t)cols[q]);
+      ++rows;
+      x ^= h;
+      sum += h;
+      if (rows_out) {
+        const uint64_t r = wr.fetch_add(1, std::memory_order_relaxed);
+        if (r < cap)
+          for (int q = 0; q < ncols; ++q) rows_out[r * ncols + q] = cols[q];
+      }
+    }
+  }
+  out.rows = rows;
+  out.x = x;
+  out.sum = sum;
+  out.scanned += sc;
+  return out;
+}
+
+// ---------------------------------------------------------------- FIND SHORTEST PATH
+// Labels: epoch << 6 | level, live when the epoch matches.
+constexpr int LB = 6;
+
+struct Level {
+  std::vector<uint32_t> v;
+};
+
+// Expands `f` over (off, nbr) claiming unlabelled neighbours at `level` in `lab`; returns the
+// new frontier and the edges scanned; `meet` collects claimed (or already-claimed) vertices
+// carrying a live label of the other side.
+uint64_t expand(const Csr& g, const std::vector<uint64_t>& off, const std::vector<uint32_t>& nbr,
+                const std::vector<uint32_t>& f, std::vector<uint32_t>& lab, const std::vector<uint32_t>& other,
+                uint32_t ep, uint32_t level, std::vector<uint32_t>& next, std::vector<uint32_t>& meet, int T) {
+  uint64_t sc = 0;
+  std::vector<std::vector<uint32_t>> nx(T), mt(T);
+  const uint32_t stamp = ep << LB | level;
+#pragma omp parallel num_threads(T) reduction(+ : sc)
+  {
+    const int t = omp_get_thread_num();
+#pragma omp for schedule(dynamic, 64)
+    for (int64_t k = 0; k < (int64_t)f.size(); ++k) {
+      const uint32_t v = f[k];
+      sc += off[v + 1] - off[v];
+      for (uint64_t j = off[v]; j < off[v + 1]; ++j) {
+        const uint32_t u = nbr[j];
+        uint32_t cur = __atomic_load_n(&lab[u], __ATOMIC_RELAXED);
+        if ((cur >> LB) == ep) continue;
+        if (__atomic_compare_exchange_n(&lab[u], &cur, stamp, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+          nx[t].push_back(u);
+          if ((other[u] >> LB) == ep) mt[t].push_back(u);
+        }
+      }
+    }
+  }
+  next.clear();
+  meet.clear();
+  for (int t = 0; t < T; ++t) {
+    next.insert(next.end(), nx[t].begin(), nx[t].end());
+    meet.insert(meet.end(), mt[t].begin(), mt[t].end());
+  }
+  return sc;
+}
+
+// returns the path length L (0: none within upto); path = [vid0, vid1, ..., vidL]
+int shortest(Csr& g, int64_t sv, int64_t tv, uint32_t upto, std::vector<int64_t>& path, uint64_t* scanned) {
+  path.clear();
+  *scanned = 0;
+  const int64_t s64 = g.dense(sv), t64 = g.dense(tv);
+  if (s64 < 0 || t64 < 0 || upto == 0) return 0;
+  const uint32_t s = (uint32_t)s64, t = (uint32_t)t64;
+  const int T = g.threads;
+  if (++g.epoch >= (1u << (32 - LB))) {
+    std::fill(g.labf.begin(), g.labf.end(), 0);
+    std::fill(g.labb.begin(), g.labb.end(), 0);
+    g.epoch = 1;
+  }
+  const uint32_t ep = g.epoch;
+  auto lev = [&](const std::vector<uint32_t>& lab, uint32_t v) -> int {
+    return (lab[v] >> LB) == ep ? (int)(lab[v] & ((1u << LB) - 1)) : -1;
+  };
+  std::vector<std::vector<uint32_t>> F{{s}}, Bk{{t}};
+  g.labf[s] = ep << LB;
+  uint32_t kf = 0, kb = 0, L = 0;
+  std::vector<uint32_t> meet, next;
+  if (s == t) {
+    // shortest cycle through s: forward BFS; position L = the first level whose frontier has an
+    // edge into s.  dist_t(v) = distance from v to s over out-edges = backward BFS from s.
+    for (kf = 0; kf < upto && !F[kf].empty(); ++kf) {
+      bool hit = false;
+      for (uint32_t v : F[kf]) {
+        *scanned += 0;
+        for (uint64_t j = g.off[v]; j < g.off[v + 1] && !hit; ++j) hit = g.nbr[j] == s;
+      }
+      if (hit) { L = kf + 1; break; }
+      std::vector<uint32_t> m;
+      *scanned += expand(g, g.off, g.nbr, F[kf], g.labf, g.labb, ep, kf + 1, next, m, T);
+      F.push_back(next);
+    }
+    if (!L) return 0;
+    // backward levels from t over in-edges up to L - 1 (t = s stamped at 0 on the b side)
+    g.labb[t] = ep << LB;
+    for (kb = 0; kb + 1 < L; ++kb) {
+      std::vector<uint32_t> m;
+      *scanned += expand(g, g.ioff, g.inbr, Bk[kb], g.labb, g.labf, ep, kb + 1, next, m, T);
+      Bk.push_back(next);
+    }
+    path.push_back(g.vid[s]);
+    uint32_t c = s;
+    for (uint32_t i = 0; i + 1 < L; ++i) {
+      int64_t best = -1;
+      uint32_t bu = 0;
+      for (uint64_t j = g.off[c]; j < g.off[c + 1]; ++j) {
+        const uint32_t u = g.nbr[j];
+        if (u == s || lev(g.labf, u) != (int)(i + 1) || lev(g.labb, u) != (int)(L - i - 1)) continue;
+        if (best < 0 || g.vid[u] < best) { best = g.vid[u]; bu = u; }
+      }
+      if (best < 0) return 0;
+      path.push_back(best);
+      c = bu;
+    }
+    path.push_back(g.vid[s]);
+    return (int)L;
+  }
+  g.labb[t] = ep << LB;
+  // bidirectional level-synchronous BFS: expand the side whose frontier has the smaller degree
+  // sum; the first level that claims a vertex labelled by the other side fixes L = kf + kb
+  auto dsum = [&](const std::vector<uint32_t>& fr, const std::vector<uint64_t>& off) {
+    uint64_t x = 0;
+    for (uint32_t v : fr) x += off[v + 1] - off[v];
+    return x;
+  };
+  bool fwd_last = true;
+  while (kf + kb < upto) {
+    if (F[kf].empty() || Bk[kb].empty()) return 0;
+    const bool fwd = dsum(F[kf], g.off) <= dsum(Bk[kb], g.ioff);
+    if (fwd) {
+      *scanned += expand(g, g.off, g.nbr, F[kf], g.labf, g.labb, ep, kf + 1, next, meet, T);
+      F.push_back(next);
+      ++kf;
+    } else {
+      *scanned += expand(g, g.ioff, g.inbr, Bk[kb], g.labb, g.labf, ep, kb + 1, next, meet, T);
+      Bk.push_back(next);
+      ++kb;
+    }
+    fwd_last = fwd;
+    if (!meet.empty()) break;
+  }
+  if (meet.empty()) return 0;
+  L = kf + kb;
+  // positions: the meet set sits at forward position kf; B[i] for i < kf = vertices of forward
+  // level i with an out-edge into B[i + 1]; positions > kf are backward levels L - i
+  (void)fwd_last;
+  std::vector<std::vector<uint8_t>> inB;   // membership by position (only positions <= kf)
+  std::vector<uint32_t> cur(meet);
+  std::vector<uint32_t> mark(g.nv, 0);     // position + 1 of B-set membership for <= kf
+  for (uint32_t v : cur) mark[v] = kf + 1;
+  for (int i = (int)kf - 1; i >= 0; --i) {
+    std::vector<uint32_t> prev;
+    for (uint32_t v : cur)
+      for (uint64_t j = g.ioff[v]; j < g.ioff[v + 1]; ++j) {
+        const uint32_t u = g.inbr[j];
+        if (lev(g.labf, u) == i && mark[u] != (uint32_t)i + 1) {
+          mark[u] = (uint32_t)i + 1;
+          prev.push_back(u);
+        }
+      }
+    cur.swap(prev);
+  }
+  path.push_back(g.vid[s]);
+  uint32_t c = s;
+  for (uint32_t i = 0; i < L; ++i) {
+    int64_t best = -1;
+    uint32_t bu = 0;
+    for (uint64_t j = g.off[c]; j < g.off[c + 1]; ++j) {
+      const uint32_t u = g.nbr[j];
+      const bool ok = (i + 1 <= kf) ? mark[u] == i + 2 : lev(g.labb, u) == (int)(L - i - 1);
+      if (!ok) continue;
+      if (best < 0 || g.vid[u] < best) { best = g.vid[u]; bu = u; }
+    }
+    if (best < 0) return 0;
+    path.push_back(best);
+    c = bu;
+  }
+  return (int)L;
+}
+
+}  // namespace
+
+extern "C" {
+
+void* orc_csr_build(const int64_t* src, const int64_t* dst, const int64_t* w, uint64_t n, int32_t threads) {
+  return build(src, dst, w, n, threads > 0 ? threads : omp_get_max_threads());
+}
+void orc_csr_free(void* h) { delete static_cast<Csr*>(h); }
+uint64_t orc_csr_nv(void* h) { return static_cast<Csr*>(h)->nv; }
+uint64_t orc_csr_ne(void* h) { return static_cast<Csr*>(h)->ne; }
+void orc_csr_threads(void* h, int32_t threads) { static_cast<Csr*>(h)->threads = threads > 0 ? threads : 1; }
+
+// GO `steps` STEPS FROM starts OVER e [WHERE e.w <op> c] YIELD (e._dst | e._src | e.w per ymask
+// bit, in that order).  out4 = {rows, xor of row hashes, sum of row hashes, edges scanned}.
+// op: 0 none, 1 <, 2 <=, 3 >, 4 >=, 5 ==, 6 !=.  Returns seconds (steady clock).
+double orc_csr_go(void* h, const int64_t* starts, uint64_t ns, uint32_t steps, int32_t op, int64_t c, int32_t ymask,
+                  uint64_t* out4, int64_t* rows_out, uint64_t cap) {
+  auto t0 = std::chrono::steady_clock::now();
+  GoOut r = go(*static_cast<Csr*>(h), starts, ns, steps, op, c, ymask, rows_out, cap);
+  auto t1 = std::chrono::steady_clock::now();
+  out4[0] = r.rows;
+  out4[1] = r.x;
+  out4[2] = r.sum;
+  out4[3] = r.scanned;
+  return std::chrono::duration<double>(t1 - t0).count();
+}
+
+// FIND SHORTEST PATH s -> t UPTO upto over e: writes L + 1 vids into path (cap >= upto + 1);
+// returns L (0: no path); *scanned = adjacency entries scanned (both directions).
+int32_t orc_csr_shortest(void* h, int64_t s, int64_t t, uint32_t upto, int64_t* path, uint64_t* scanned) {
+  std::vector<int64_t> p;
+  const int L = shortest(*static_cast<Csr*>(h), s, t, upto, p, scanned);
+  for (size_t i = 0; L && i < p.size(); ++i) path[i] = p[i];
+  return L;
+}
+
+}  // extern "C"

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round-2 GPU-box steps (from the repo root, via gpurun): bash tools/gpu_r02.sh <tag> <step>...
+#   tests  — pytest -m gpu;  load26 — RMAT-26 generate + load + GO leg only (load time);
+#   bench  — default bench.py
+set -u
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+TAG=$1; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+for step in "$@"; do
+  case $step in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        > "$OUT/pytest_gpu.log" 2>&1 || { tail -40 "$OUT/pytest_gpu.log"; exit 1; } ;;
+    load26)
+      timeout -k 10 900 python -u bench.py --scale 26 --roots 16 --steps 2 --sp-pairs 0 --no-cpu-baseline \
+        --c5-scale 0 --getbound-reqs 0 --no-profile > "$OUT/load26.json" 2> "$OUT/load26.log" \
+        || { tail -30 "$OUT/load26.log"; exit 1; } ;;
+    bench)
+      timeout -k 10 900 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.log" || { tail -30 "$OUT/bench.log"; exit 1; } ;;
+  esac
+  echo "step $step done"
+done
