@@ -220,6 +220,12 @@ const char* nbg_rows_string(const nbg_rows* r, int64_t string_id);
 const void* nbg_rows_device_col(const nbg_rows* r, int32_t col);
 int64_t nbg_rows_num_segments(const nbg_rows* r);
 int32_t nbg_rows_segment(const nbg_rows* r, int64_t i, uint64_t* begin, uint64_t* end);
+/* Order-independent digest of a result's rows, computed where the rows are (HBM for device
+ * results): per row h = splitmix64(... splitmix64(0 ^ cell_0) ... ^ cell_{k-1}) over its 8-byte
+ * cell payloads in column order; out[0] = rows, out[1] = XOR of h, out[2] = sum of h (mod 2^64).
+ * Verifies results at sizes too large to fetch.  String cells hash their payload: the snapshot's
+ * dictionary code for device rows, the result's string index (nbg_rows_string) for host rows. */
+int32_t nbg_rows_digest(const nbg_rows* r, uint64_t* out);
 void nbg_rows_free(nbg_rows* r);
 
 /* ---- FIND SHORTEST | ALL PATH (FindPathExecutor semantics) ----------------------------- */

@@ -104,6 +104,7 @@ SIGNATURES = [
     ("nbg_rows_device_col", vp, [vp, i32]),
     ("nbg_rows_num_segments", i64, [vp]),
     ("nbg_rows_segment", i32, [vp, i64, P(u64), P(u64)]),
+    ("nbg_rows_digest", i32, [vp, P(u64)]),
     ("nbg_rows_free", None, [vp]),
     ("nbg_find_path", i32, [vp, P(nbg_path_request), P(vp)]),
     ("nbg_paths_count", i64, [vp]),

@@ -1057,6 +1057,36 @@ const void* nbg_rows_device_col(const nbg_rows* r, int32_t col) {
   if (!r || col < 0 || col >= (int32_t)r->dcols.size()) return nullptr;
   return r->dcols[col];
 }
+int32_t nbg_rows_digest(const nbg_rows* r, uint64_t* out) {
+  if (!r || !out) return NBG_E_INVALID_ARGUMENT;
+  out[0] = out[1] = out[2] = 0;
+  if (!r->count) return NBG_OK;
+  if (r->fetched && !r->on_device) {   // host rows: the same chain on the host
+    for (uint64_t i = 0; i < r->count; ++i) {
+      uint64_t h = 0;
+      for (int c = 0; c < r->ncols; ++c) {
+        uint64_t z = (h ^ (uint64_t)r->bits[c][i]) + 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        h = z ^ (z >> 31);
+      }
+      ++out[0];
+      out[1] ^= h;
+      out[2] += h;
+    }
+    return NBG_OK;
+  }
+  Engine& E = *r->eng;
+  std::lock_guard<std::mutex> lg(E.mu);
+  if (hipSetDevice(E.cfg.device) != hipSuccess) return E.fail(NBG_E_DEVICE, "hipSetDevice failed");
+  auto* m = const_cast<nbg_rows*>(r);
+  m->build_segs();
+  std::vector<std::pair<uint64_t, uint64_t>> segs;
+  for (auto& sg : m->segs) segs.emplace_back(sg.begin, sg.end - sg.begin);
+  const hipError_t he = ws_rows_digest(r->owned_ws ? r->owned_ws : r->ws, segs, r->ncols, out);
+  return he == hipSuccess ? NBG_OK : E.fail(NBG_E_DEVICE, std::string("digest: ") + hipGetErrorString(he));
+}
+
 void nbg_rows_free(nbg_rows* r) {
   if (!r) return;
   if (r->eng && (r->owned_ws || r->ws)) {

@@ -1103,6 +1103,41 @@ __global__ void __launch_bounds__(BLOCK) k_pack_rows(const uint64_t* __restrict_
   }
 }
 
+// Order-independent digest of a result: per row h = splitmix64-chain of its 8-byte cell
+// payloads (column order), summed and xor-ed over the rows (out = {rows, xor, sum}).
+__device__ __forceinline__ uint64_t splitmix64_d(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void __launch_bounds__(BLOCK) k_rows_digest(const uint64_t* __restrict__ seg, int nseg,
+                                                       int64_t* const* __restrict__ cols, int ncols,
+                                                       unsigned long long* __restrict__ out) {
+  unsigned long long n = 0, x = 0, sum = 0;
+  for (int k = blockIdx.x; k < nseg; k += gridDim.x) {
+    const uint64_t b = seg[3 * k], len = seg[3 * k + 1];
+    for (uint64_t i = threadIdx.x; i < len; i += BLOCK) {
+      uint64_t h = 0;
+      for (int c = 0; c < ncols; ++c) h = splitmix64_d(h ^ (uint64_t)cols[c][b + i]);
+      ++n;
+      x ^= h;
+      sum += h;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {   // wave64 reduction
+    n += __shfl_xor(n, o);
+    x ^= __shfl_xor(x, o);
+    sum += __shfl_xor(sum, o);
+  }
+  if ((threadIdx.x & 63) == 0 && n) {
+    atomicAdd(&out[0], n);
+    atomicXor(&out[1], x);
+    atomicAdd(&out[2], sum);
+  }
+}
+
 // ----------------------------------------------------------------------------- YIELD DISTINCT
 // GoExecutor::setupInterimResult keeps the first row of each distinct encoded row
 // (GoExecutor.cpp:771-778).  A row's identity here is its value kinds (per OVER type) plus its
@@ -1798,6 +1833,36 @@ hipError_t ws_fetch_rows(Workspace* w, const std::vector<std::pair<uint64_t, uin
   }
   for (int c = 0; e == hipSuccess && c < ncols; ++c)
     e = hipMemcpyAsync(host_cols[c], d_out + (uint64_t)c * total, total * 8, hipMemcpyDeviceToHost, w->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(w->stream);
+  if (d_meta) (void)hipFree(d_meta);
+  if (d_out) (void)hipFree(d_out);
+  return e;
+}
+
+hipError_t ws_rows_digest(Workspace* w, const std::vector<std::pair<uint64_t, uint64_t>>& segs, int ncols,
+                          uint64_t out[3]) {
+  out[0] = out[1] = out[2] = 0;
+  std::vector<uint64_t> meta;
+  for (auto& sg : segs) {
+    if (!sg.second) continue;
+    meta.push_back(sg.first);
+    meta.push_back(sg.second);
+    meta.push_back(0);
+  }
+  if (meta.empty() || !ncols) return hipSuccess;
+  uint64_t* d_meta = nullptr;
+  unsigned long long* d_out = nullptr;
+  hipError_t e = hipMalloc((void**)&d_meta, meta.size() * 8);
+  if (e == hipSuccess) e = hipMalloc((void**)&d_out, 3 * 8);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_meta, meta.data(), meta.size() * 8, hipMemcpyHostToDevice, w->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(d_out, 0, 3 * 8, w->stream);
+  if (e == hipSuccess) {
+    const int nseg = (int)(meta.size() / 3);
+    hipLaunchKernelGGL(k_rows_digest, dim3((unsigned)(nseg < 8192 ? nseg : 8192)), dim3(BLOCK), 0, w->stream, d_meta,
+                       nseg, (int64_t* const*)w->d_row_cols, ncols, d_out);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, 3 * 8, hipMemcpyDeviceToHost, w->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(w->stream);
   if (d_meta) (void)hipFree(d_meta);
   if (d_out) (void)hipFree(d_out);

@@ -357,6 +357,9 @@ unsigned ws_final_grid_of(Workspace* w, int tix);          // grid of the last f
 const uint32_t* ws_host_blk_rows(Workspace* w, int tix);    // rows per workgroup (after ws_end_query)
 hipError_t ws_fetch_rows(Workspace* w, const std::vector<std::pair<uint64_t, uint64_t>>& segs, int ncols,
                          uint64_t total, int64_t* const* host_cols);
+// order-independent digest {rows, xor, sum} of the rows in segs (splitmix64 chain per row)
+hipError_t ws_rows_digest(Workspace* w, const std::vector<std::pair<uint64_t, uint64_t>>& segs, int ncols,
+                          uint64_t out[3]);
 const QState* ws_host_state(Workspace* w);       // valid after ws_end_query
 // YIELD DISTINCT: dedup + in-place compaction of result segments (first row, rows, OVER index)
 hipError_t ws_distinct(Workspace* w, const std::vector<std::array<uint64_t, 3>>& segs, int ncols,

@@ -62,6 +62,24 @@ class DeviceRows:
             raise NbgError(rc, "fetch failed")
         return self.eng._host_rows(self.h)
 
+    def fetch_bits(self) -> List[np.ndarray]:
+        """The rows as one int64 payload array per column (nbg_rows_col_bits; no per-cell
+        decoding — for large integer results)."""
+        rc = self.eng.lib.nbg_rows_fetch(self.h)
+        if rc:
+            raise NbgError(rc, "fetch failed")
+        n, nc = self.count, self.eng.lib.nbg_rows_num_cols(self.h)
+        return [np.ctypeslib.as_array(self.eng.lib.nbg_rows_col_bits(self.h, c), shape=(n,)).copy() if n
+                else np.zeros(0, np.int64) for c in range(nc)]
+
+    def digest(self):
+        """(rows, xor, sum) of the rows' splitmix64 chains, computed in HBM (nbg_rows_digest)."""
+        out = (C.c_uint64 * 3)()
+        rc = self.eng.lib.nbg_rows_digest(self.h, out)
+        if rc:
+            raise NbgError(rc, "digest failed")
+        return (int(out[0]), int(out[1]), int(out[2]))
+
     def free(self):
         if self.h:
             self.eng.lib.nbg_rows_free(self.h)

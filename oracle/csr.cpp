@@ -24,6 +24,8 @@
 #include <atomic>
 #include <chrono>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <vector>
@@ -48,7 +50,7 @@ struct Csr {
   std::vector<uint64_t> bstart;             // [B + 1] first dense id of each bucket
   int threads = 1;
   // per-query labels (epoch-stamped: no clearing between queries)
-  std::vector<uint32_t> labf, labb;
+  std::vector<uint32_t> labf, labb, mark;   // mark: B-set position, epoch-stamped like the labels
   uint32_t epoch = 0;
 
   uint64_t bucket_of(int64_t v) const { return mix64((uint64_t)v) >> (64 - bbits); }
@@ -96,6 +98,13 @@ void bucket_sort(uint64_t n, uint64_t nb, BucketFn bucket, int T, std::vector<ui
 }
 
 Csr* build(const int64_t* src, const int64_t* dst, const int64_t* w, uint64_t n, int T) {
+  const bool verbose = getenv("ORC_CSR_VERBOSE") != nullptr;
+  auto t_last = std::chrono::steady_clock::now();
+  auto phase = [&](const char* what) {
+    auto now = std::chrono::steady_clock::now();
+    if (verbose) fprintf(stderr, "csr build %s %.3fs\n", what, std::chrono::duration<double>(now - t_last).count());
+    t_last = now;
+  };
   auto* g = new Csr();
   g->threads = T;
   // ---- vertex dictionary: every endpoint, hashed into buckets, sorted and de-duplicated
@@ -104,6 +113,7 @@ Csr* build(const int64_t* src, const int64_t* dst, const int64_t* w, uint64_t n,
   const uint64_t B = 1ull << g->bbits;
   std::vector<uint64_t> bst, order;
   bucket_sort(2 * n, B, [&](uint64_t i) { return g->bucket_of(i < n ? src[i] : dst[i - n]); }, T, bst, order);
+  phase("bucket");
   std::vector<uint32_t> dense_of(2 * n);
   std::vector<uint64_t> bu(B + 1, 0);   // unique vids per bucket
   std::vector<std::vector<int64_t>> uniq(B);
@@ -134,11 +144,21 @@ Csr* build(const int64_t* src, const int64_t* dst, const int64_t* w, uint64_t n,
     std::vector<int64_t>().swap(uniq[b]);
   }
   std::vector<uint64_t>().swap(order);
+  phase("dictionary");
   const uint64_t nv = g->nv;
-  // ---- out CSR: edges by dense source (stable: load order inside a row), then per row by
+  // ---- out CSR: edges grouped by dense source (atomic counting scatter), then per row sorted by
   // (dst, load order descending) — the first of each dst is the live edge (last sample wins)
-  std::vector<uint64_t> rs, eo;
-  bucket_sort(n, nv, [&](uint64_t i) { return dense_of[i]; }, T, rs, eo);
+  std::vector<uint64_t> rs(nv + 1, 0), eo(n);
+  {
+    std::vector<uint64_t> cnt(nv + 1, 0);
+#pragma omp parallel for schedule(static) num_threads(T)
+    for (int64_t i = 0; i < (int64_t)n; ++i) __atomic_fetch_add(&cnt[dense_of[i] + 1], 1ull, __ATOMIC_RELAXED);
+    for (uint64_t d = 0; d < nv; ++d) cnt[d + 1] += cnt[d];
+    rs = cnt;
+#pragma omp parallel for schedule(static) num_threads(T)
+    for (int64_t i = 0; i < (int64_t)n; ++i) eo[__atomic_fetch_add(&cnt[dense_of[i]], 1ull, __ATOMIC_RELAXED)] = i;
+  }
+  phase("group");
   std::vector<uint32_t> live_cnt(nv, 0);
 #pragma omp parallel for schedule(dynamic, 1024) num_threads(T)
   for (int64_t d = 0; d < (int64_t)nv; ++d) {
@@ -152,6 +172,7 @@ Csr* build(const int64_t* src, const int64_t* dst, const int64_t* w, uint64_t n,
       if (it == b || dense_of[n + *it] != dense_of[n + *(it - 1)]) b[m++] = *it;
     live_cnt[d] = (uint32_t)m;
   }
+  phase("row sort");
   g->off.assign(nv + 1, 0);
   for (uint64_t d = 0; d < nv; ++d) g->off[d + 1] = g->off[d] + live_cnt[d];
   g->ne = g->off[nv];
@@ -166,16 +187,20 @@ Csr* build(const int64_t* src, const int64_t* dst, const int64_t* w, uint64_t n,
     }
   }
   // ---- in CSR: the mirror of every live out-edge, grouped by destination
-  std::vector<uint32_t> icnt(nv + 1, 0);
-  for (uint64_t j = 0; j < g->ne; ++j) ++icnt[g->nbr[j] + 1];
-  g->ioff.assign(nv + 1, 0);
-  for (uint64_t d = 0; d < nv; ++d) g->ioff[d + 1] = g->ioff[d] + icnt[d + 1];
+  std::vector<uint64_t> icnt(nv + 1, 0);
+#pragma omp parallel for schedule(static) num_threads(T)
+  for (int64_t j = 0; j < (int64_t)g->ne; ++j) __atomic_fetch_add(&icnt[g->nbr[j] + 1], 1ull, __ATOMIC_RELAXED);
+  for (uint64_t d = 0; d < nv; ++d) icnt[d + 1] += icnt[d];
+  g->ioff = icnt;
   g->inbr.resize(g->ne);
-  std::vector<uint64_t> cur(g->ioff.begin(), g->ioff.end() - 1);
-  for (uint64_t d = 0; d < nv; ++d)
-    for (uint64_t j = g->off[d]; j < g->off[d + 1]; ++j) g->inbr[cur[g->nbr[j]]++] = (uint32_t)d;
+#pragma omp parallel for schedule(dynamic, 1024) num_threads(T)
+  for (int64_t d = 0; d < (int64_t)nv; ++d)
+    for (uint64_t j = g->off[d]; j < g->off[d + 1]; ++j)
+      g->inbr[__atomic_fetch_add(&icnt[g->nbr[j]], 1ull, __ATOMIC_RELAXED)] = (uint32_t)d;
   g->labf.assign(nv, 0);
   g->labb.assign(nv, 0);
+  g->mark.assign(nv, 0);
+  phase("csr");
   return g;
 }
 
@@ -276,6 +301,9 @@ uint64_t expand(const Csr& g, const std::vector<uint64_t>& off, const std::vecto
                 const std::vector<uint32_t>& f, std::vector<uint32_t>& lab, const std::vector<uint32_t>& other,
                 uint32_t ep, uint32_t level, std::vector<uint32_t>& next, std::vector<uint32_t>& meet, int T) {
   uint64_t sc = 0;
+  uint64_t work = 0;
+  for (size_t k = 0; k < f.size() && work < 65536; ++k) work += off[f[k] + 1] - off[f[k]] + 1;
+  if (work < 65536) T = 1;   // a small level: no thread fan-out
   std::vector<std::vector<uint32_t>> nx(T), mt(T);
   const uint32_t stamp = ep << LB | level;
 #pragma omp parallel num_threads(T) reduction(+ : sc)
@@ -316,6 +344,7 @@ int shortest(Csr& g, int64_t sv, int64_t tv, uint32_t upto, std::vector<int64_t>
   if (++g.epoch >= (1u << (32 - LB))) {
     std::fill(g.labf.begin(), g.labf.end(), 0);
     std::fill(g.labb.begin(), g.labb.end(), 0);
+    std::fill(g.mark.begin(), g.mark.end(), 0);
     g.epoch = 1;
   }
   const uint32_t ep = g.epoch;
@@ -394,17 +423,17 @@ int shortest(Csr& g, int64_t sv, int64_t tv, uint32_t upto, std::vector<int64_t>
   // positions: the meet set sits at forward position kf; B[i] for i < kf = vertices of forward
   // level i with an out-edge into B[i + 1]; positions > kf are backward levels L - i
   (void)fwd_last;
-  std::vector<std::vector<uint8_t>> inB;   // membership by position (only positions <= kf)
   std::vector<uint32_t> cur(meet);
-  std::vector<uint32_t> mark(g.nv, 0);     // position + 1 of B-set membership for <= kf
-  for (uint32_t v : cur) mark[v] = kf + 1;
+  std::vector<uint32_t>& mark = g.mark;    // ep << LB | position, for B-set members at positions <= kf
+  for (uint32_t v : cur) mark[v] = ep << LB | kf;
   for (int i = (int)kf - 1; i >= 0; --i) {
     std::vector<uint32_t> prev;
+    const uint32_t st = ep << LB | (uint32_t)i;
     for (uint32_t v : cur)
       for (uint64_t j = g.ioff[v]; j < g.ioff[v + 1]; ++j) {
         const uint32_t u = g.inbr[j];
-        if (lev(g.labf, u) == i && mark[u] != (uint32_t)i + 1) {
-          mark[u] = (uint32_t)i + 1;
+        if (lev(g.labf, u) == i && mark[u] != st) {
+          mark[u] = st;
           prev.push_back(u);
         }
       }
@@ -417,7 +446,7 @@ int shortest(Csr& g, int64_t sv, int64_t tv, uint32_t upto, std::vector<int64_t>
     uint32_t bu = 0;
     for (uint64_t j = g.off[c]; j < g.off[c + 1]; ++j) {
       const uint32_t u = g.nbr[j];
-      const bool ok = (i + 1 <= kf) ? mark[u] == i + 2 : lev(g.labb, u) == (int)(L - i - 1);
+      const bool ok = (i + 1 <= kf) ? mark[u] == (ep << LB | (i + 1)) : lev(g.labb, u) == (int)(L - i - 1);
       if (!ok) continue;
       if (best < 0 || g.vid[u] < best) { best = g.vid[u]; bu = u; }
     }

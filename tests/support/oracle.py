@@ -303,3 +303,100 @@ def nba_oracle(data, parts=1):
         o.register(kind == "edge", ident, name, cols)
     o.load_builder(kvgen.nba_kv(data, parts))
     return o
+
+
+WHERE_OPS = {None: 0, "<": 1, "<=": 2, ">": 3, ">=": 4, "==": 5, "!=": 6}
+Y_DST, Y_SRC, Y_W = 1, 2, 4
+
+
+class CsrOracle:
+    """oracle/csr.cpp: the same GO / SHORTEST semantics over an in-memory CSR (OpenMP), for
+    sizes the faithful restatement cannot reach and as CPU baseline mode (ii).  One edge type
+    `e(w int)` loaded from bulk (src, dst, w) samples (last sample wins)."""
+
+    def __init__(self, src, dst, w, threads=0):
+        L = lib()
+        vp, i32, i64, u32, u64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_uint64
+        L.orc_csr_build.restype = vp
+        L.orc_csr_build.argtypes = [vp, vp, vp, u64, i32]
+        L.orc_csr_free.argtypes = [vp]
+        L.orc_csr_nv.argtypes = [vp]
+        L.orc_csr_nv.restype = u64
+        L.orc_csr_ne.argtypes = [vp]
+        L.orc_csr_ne.restype = u64
+        L.orc_csr_threads.argtypes = [vp, i32]
+        L.orc_csr_go.restype = C.c_double
+        L.orc_csr_go.argtypes = [vp, vp, u64, u32, i32, i64, i32, vp, vp, u64]
+        L.orc_csr_shortest.restype = i32
+        L.orc_csr_shortest.argtypes = [vp, i64, i64, u32, vp, C.POINTER(u64)]
+        self.L = L
+        src = np.ascontiguousarray(src, np.int64)
+        dst = np.ascontiguousarray(dst, np.int64)
+        w = np.ascontiguousarray(w, np.int64)
+        self.h = L.orc_csr_build(_ptr(src), _ptr(dst), _ptr(w), len(src), threads)
+
+    @property
+    def num_vertices(self):
+        return self.L.orc_csr_nv(self.h)
+
+    @property
+    def num_edges(self):
+        return self.L.orc_csr_ne(self.h)
+
+    def set_threads(self, n):
+        self.L.orc_csr_threads(self.h, n)
+
+    def go(self, starts, steps, op=None, c=0, ymask=Y_DST, rows=False, cap=None):
+        """-> (digest (rows, xor, sum), edges scanned, seconds, rows as an int64 [n, ncols] array
+        or None)."""
+        s = np.asarray(starts, np.int64)
+        out = np.zeros(4, np.uint64)
+        ncols = bin(ymask).count("1")
+        buf = None
+        if rows:
+            if cap is None:
+                out0 = np.zeros(4, np.uint64)
+                self.L.orc_csr_go(self.h, _ptr(s), len(s), steps, WHERE_OPS[op], c, ymask, _ptr(out0), None, 0)
+                cap = int(out0[0])
+            buf = np.zeros((max(cap, 1), ncols), np.int64)
+        sec = self.L.orc_csr_go(self.h, _ptr(s), len(s), steps, WHERE_OPS[op], c, ymask, _ptr(out),
+                                buf.ctypes.data_as(C.c_void_p) if buf is not None else None, cap or 0)
+        digest = (int(out[0]), int(out[1]), int(out[2]))
+        got = buf[:min(cap, digest[0])] if buf is not None else None   # [rows, ncols] int64
+        return digest, int(out[3]), sec, got
+
+    def shortest(self, s, t, upto=5):
+        """-> (vid path [s, ..., t] or [], edges scanned)."""
+        buf = np.zeros(upto + 2, np.int64)
+        sc = C.c_uint64()
+        n = self.L.orc_csr_shortest(self.h, int(s), int(t), upto, _ptr(buf), C.byref(sc))
+        return ([int(x) for x in buf[:n + 1]] if n else []), sc.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.orc_csr_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+def row_digest(rows):
+    """(rows, xor, sum) of splitmix64-chained row hashes — the digest orc_csr_go and
+    nbg_rows_digest compute."""
+    M = (1 << 64) - 1
+
+    def mix(z):
+        z = (z + 0x9E3779B97F4A7C15) & M
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        return z ^ (z >> 31)
+
+    x = s = 0
+    for r in rows:
+        h = 0
+        for v in r:
+            h = mix(h ^ (int(v) & M))
+        x ^= h
+        s = (s + h) & M
+    return (len(rows), x, s)

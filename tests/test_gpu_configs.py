@@ -1,0 +1,137 @@
+"""GPU parity at the sizes BASELINE.json's configs are quoted on:
+
+  C2  RMAT-22, GO 3 STEPS FROM <r> OVER e WHERE e.w < 50 YIELD e._dst (the bench's query):
+      full sorted row compare for 4 roots, device digest + edges scanned for all 64 bench roots
+  C4  FIND SHORTEST PATH UPTO 5 on RMAT-22: 256 pairs (seed 7), canonical paths
+  C3  RMAT-26 (1.07 G samples, the headline graph): device digest (nbg_rows_digest) vs the CSR
+      oracle's digest for the bench's 16 roots, a sampled full compare for 2 roots, and 64
+      SHORTEST pairs
+
+The checker is oracle/csr.cpp (CSR restatement, pinned to the storaged-faithful oracle on
+RMAT <= 12 by tests/test_oracle_csr.py).  Graphs are the bench's own (nebula_amd.rmat)."""
+import os
+
+import numpy as np
+import pytest
+
+from nebula_amd import Engine, expr as E, rmat
+from tests.support.oracle import CsrOracle, Y_DST
+
+pytestmark = pytest.mark.gpu
+
+WHERE = E.binop("<", E.edge_prop("e", "w"), E.const(50)).encode()
+
+
+def _load(scale):
+    src, dst, w = rmat.rmat_edges_fast(scale)
+    eng = Engine(100)
+    eng.register_edge(1, "e", [("w", 2)])
+    eng.load_edges(1, src, dst, [w])
+    eng.finalize()
+    csr = CsrOracle(src, dst, w, threads=min(16, os.cpu_count() or 8))
+    src_verts, all_verts = rmat.vertex_sets(scale)
+    return src, dst, eng, csr, src_verts, all_verts
+
+
+@pytest.fixture(scope="module")
+def rmat22():
+    src, dst, eng, csr, sv, av = _load(22)
+    yield src, dst, eng, csr, sv, av
+    eng.close()
+    csr.close()
+
+
+def _sorted_col(a):
+    return np.sort(np.asarray(a, np.int64))
+
+
+@pytest.mark.timeout(600)
+def test_c2_go3_full_compare(rmat22):
+    src, dst, eng, csr, sv, _ = rmat22
+    roots = [int(x) for x in rmat.pick_roots(src, 64, 42, verts=sv)]
+    stmt = eng.prepare_go([1], 3, WHERE)
+    try:
+        for r in roots[:4]:
+            res = stmt.run_device([r])
+            got = res.fetch_bits()[0]
+            _, scanned, _, rows = csr.go([r], 3, "<", 50, Y_DST, rows=True)
+            exp = rows[:, 0]
+            assert res.count == len(exp) > 0
+            assert np.array_equal(_sorted_col(got), _sorted_col(exp)), r
+            assert res.edges_scanned == scanned
+            res.free()
+    finally:
+        stmt.free()
+
+
+def test_c2_go3_digest_all_bench_roots(rmat22):
+    src, dst, eng, csr, sv, _ = rmat22
+    roots = [int(x) for x in rmat.pick_roots(src, 64, 42, verts=sv)]
+    stmt = eng.prepare_go([1], 3, WHERE)
+    try:
+        for r in roots:
+            res = stmt.run_device([r])
+            digest, scanned, _, _ = csr.go([r], 3, "<", 50, Y_DST)
+            assert res.digest() == digest, r
+            assert res.edges_scanned == scanned, r
+            res.free()
+    finally:
+        stmt.free()
+
+
+def _check_pairs(eng, csr, pairs, upto=5):
+    found = 0
+    for s, t in pairs:
+        got = eng.find_path([s], [t], [1], upto)
+        exp, _ = csr.shortest(s, t, upto)
+        got_vids = got[0][0::3] if got else []
+        assert len(got) <= 1
+        assert got_vids == exp, (s, t)
+        if got:
+            assert all(x == 1 for x in got[0][1::3]) and all(x == 0 for x in got[0][2::3])
+            found += 1
+    return found
+
+
+def test_c4_shortest_pairs_rmat22(rmat22):
+    src, dst, eng, csr, _, av = rmat22
+    pairs = rmat.pick_pairs(src, dst, 256, 7, verts=av)
+    found = _check_pairs(eng, csr, pairs)
+    assert found > 100
+
+
+@pytest.fixture(scope="module")
+def rmat26():
+    if os.environ.get("NBG_SKIP_RMAT26"):
+        pytest.skip("NBG_SKIP_RMAT26 set")
+    src, dst, eng, csr, sv, av = _load(26)
+    yield src, dst, eng, csr, sv, av
+    eng.close()
+    csr.close()
+
+
+@pytest.mark.timeout(1200)
+def test_c3_rmat26_digests(rmat26):
+    src, dst, eng, csr, sv, _ = rmat26
+    assert eng.stats()["num_edges"] == 2 * csr.num_edges
+    roots = [int(x) for x in rmat.pick_roots(src, 16, 42, verts=sv)]
+    stmt = eng.prepare_go([1], 3, WHERE)
+    try:
+        for k, r in enumerate(roots):
+            res = stmt.run_device([r])
+            digest, scanned, _, rows = csr.go([r], 3, "<", 50, Y_DST, rows=k < 2)
+            assert res.digest() == digest, r
+            assert res.edges_scanned == scanned, r
+            if rows is not None:   # sampled full compare
+                got = res.fetch_bits()[0]
+                assert np.array_equal(_sorted_col(got), _sorted_col(rows[:, 0])), r
+            res.free()
+    finally:
+        stmt.free()
+
+
+@pytest.mark.timeout(600)
+def test_c4_shortest_pairs_rmat26(rmat26):
+    src, dst, eng, csr, _, av = rmat26
+    pairs = rmat.pick_pairs(src, dst, 64, 7, verts=av)
+    assert _check_pairs(eng, csr, pairs) > 20
