@@ -1,28 +1,32 @@
 #!/usr/bin/env python3
-"""nebula_amd benchmark — GO 3 STEPS traversed edges/sec (TEPS) on MI355X.
+"""nebula_amd benchmark — GO 3 STEPS traversed edges/sec (TEPS) and FIND SHORTEST PATH on MI355X.
 
-Workload (BASELINE.json configs[1]): RMAT scale-22 (A .57/B .19/C .19,
-edge factor 16, seeded), 100 partitions, edge type e(w int); one "step" = the 64 queries
-``GO 3 STEPS FROM <root> OVER e WHERE e.w < 50`` (roots: seed 42, out-degree >= 1), each a
-separate query through the C ABI (nbg_go_device: result rows stay in HBM).
-TEPS = Σ_s E_s (adjacency entries scanned at every step, after version de-dup) / wall time.
+Headline workload (BASELINE.json configs[2]/[3]): RMAT scale-26 (A .57 /
+B .19 / C .19, edge factor 16, seeded: 1.07 G samples, 2.12 G live out+in edges), 100 partitions,
+edge type e(w int).  One "step" = the 16 queries ``GO 3 STEPS FROM <root> OVER e WHERE e.w < 50
+YIELD e._dst`` (roots: seed 42, out-degree >= 1), each a separate query through the C ABI
+(nbg_go_submit / nbg_go_wait, result rows left in HBM).  TEPS = Σ_s E_s (adjacency entries
+scanned at every step, after version de-dup) / wall time.  The same graph runs at every GPU count
+(strong scaling, P = 100 at every N; --weak runs RMAT-(22 + log2 N) instead).
 
-Multi-GPU (torch.distributed.run, one rank per GPU): the engine is
-PARTITIONED — rank r holds the parts p with p % N == r (out-edges at src's part, in-edges at
-dst's part) and every query runs on all ranks; each hop's candidate set is exchanged with one
-bitmap all-to-all over RCCL/xGMI (the owner-side OR is GoExecutor's per-step dst set).  Weak
-scaling: the graph is RMAT-(22 + log2 N) (vertices and edges per GPU held constant; N=8 is
-RMAT-25, --scale overrides).  value = edges scanned by all queries (whole-query counts, summed
-over ranks inside the library) / max time over ranks.  torch.distributed (gloo) only carries the
-RCCL unique id, the barriers and the max-over-ranks timing.
+Multi-GPU: ``bench.py --gpus N`` starts N ranks itself (torch.distributed.run as a child process;
+this parent never touches the GPU), or runs as one of them when launched by torch.distributed.run.
+The engine is PARTITIONED: rank r holds the parts p with p % N == r (out-edges at src's part,
+in-edges at dst's part) and every query runs on all ranks; each hop's candidate set is exchanged
+with one bitmap all-to-all over RCCL/xGMI (the owner-side OR is GoExecutor's per-step dst set).
+value = edges scanned by all queries (whole-query counts, summed over ranks in the library) / max
+time over ranks.  torch.distributed (gloo) only carries the RCCL unique id, barriers and timings.
 
-Also reported: the dominant kernel's achieved algorithmic HBM bandwidth (HIP events inside
-the library over the timed region) against the 8 TB/s peak, and the CPU oracle
-(storaged+graphd restatement, oracle/) on a bounded sample of the same queries.
+Also reported, outside the timed region: the dominant kernel's algorithmic HBM bandwidth (HIP
+events inside the library) against the 8 TB/s peak, the end-to-end algorithmic fraction, the
+host-delivered result rate (nbg_go: rows copied to the host), a device-digest check of the
+headline queries against the CPU CSR oracle, FIND SHORTEST PATH latency (C4), the C2 RMAT-22 leg,
+the C5 substitute, boundary-1 getBound, and the CPU baselines (oracle/, on the box's host cores).
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -32,9 +36,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+METRIC = "GO 3 STEPS traversed edges/sec (TEPS) at 1/2/4/8 GPU; FIND SHORTEST PATH p50"
 # HBM traffic per launch from the committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
-# bench (tools/gpu_check.sh pmc -> tools/pmc_summary.py; FETCH_SIZE doubled per the gfx950 note).
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_v13_pmc_hbm.json")
+# bench's default workload (tools/gpu_r02.sh pmc -> tools/pmc_summary.py; FETCH_SIZE doubled per
+# the gfx950 note), keyed by workload
+PMC_FILES = {("RMAT-26", 16): os.path.join(ROOT, "profiles", "r02_pmc_hbm_rmat26.json"),
+             ("RMAT-22", 64): os.path.join(ROOT, "profiles", "r02_pmc_hbm_rmat22.json")}
 # library kernel id -> instantiations in the rocprof names, first match wins (FINAL: this bench's
 # range WHERE with a _dst YIELD runs k_expand<4> = FINALD; <3> FINALF; <1> the general interpreter;
 # the bool is the inline-start-list variant)
@@ -44,278 +51,191 @@ PMC_NAMES = {"k_expand<MARK>": ["k_expand<0, false>", "k_expand<0, true>"],
              "k_expand<BFS>": ["k_expand<2, false>", "k_expand<2, true>"]}
 
 
-def pmc_traffic(kernel):
-    """Corrected HBM bytes per launch of `kernel` from the committed PMC summary, or None."""
-    try:
-        with open(PMC_FILE) as f:
-            d = json.load(f)
-        for name in PMC_NAMES.get(kernel, [kernel]):
-            if name in d:
-                return d[name]["read_bytes_per_launch_corrected"] + d[name]["write_bytes_per_launch"]
-    except (OSError, KeyError, ValueError):
-        pass
-    return None
-
-
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scale", type=int, default=None, help="RMAT scale (default 22 + log2(GPUs))")
-    ap.add_argument("--roots", type=int, default=64)
-    ap.add_argument("--parts", type=int, default=100)
-    ap.add_argument("--go-steps", type=int, default=3)
-    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline sample budget")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-profile", action="store_true")
-    ap.add_argument("--sp-pairs", type=int, default=10000, help="FIND SHORTEST PATH pairs (0 = skip)")
-    ap.add_argument("--sp-upto", type=int, default=5)
-    ap.add_argument("--sync", action="store_true", help="one query at a time (no query slots)")
-    ap.add_argument("--c5-scale", type=int, default=20,
-                    help="C5 substitute (knows RMAT + likes bipartite): knows scale, 0 = skip")
-    ap.add_argument("--getbound-reqs", type=int, default=200,
-                    help="QueryBoundBenchmark-shaped GetNeighbors requests (0 = skip)")
-    args = ap.parse_args()
+def pmc_traffic(kernel, workload):
+    """Corrected HBM bytes per launch of `kernel` from the committed PMC summary of `workload`."""
+    path = PMC_FILES.get(workload)
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        for name in PMC_NAMES.get(kernel, [kernel]):
+            if name in d:
+                return d[name]["read_bytes_per_launch_corrected"] + d[name]["write_bytes_per_launch"], path
+    except (OSError, KeyError, ValueError, TypeError):
+        pass
+    return None, None
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if os.environ.get("NBG_SAME_DEVICE"):
-        # rehearsal on a one-GPU box: every rank on device 0, RCCL over its socket transport
-        # (distinct host ids; see tools/rccl_probe.py).  Timings are then not xGMI numbers.
-        local = 0
-        os.environ["NCCL_HOSTID"] = f"nbg-rank-{rank}"
-        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
-    import torch
 
-    from nebula_amd import Engine, comm_unique_id, expr as E, rmat
+def cpu_info():
+    """Host CPU model and the threads this process may use (the box's share, OMP_NUM_THREADS)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = min(avail, int(omp)) if omp and omp.isdigit() else avail
+    return model, max(1, threads), os.cpu_count()
 
-    if args.scale is None:
-        args.scale = 22 + max(0, int(round(np.log2(world))))
-    t0 = time.time()
-    src, dst, w = rmat.rmat_edges_fast(args.scale)
-    gen_s = time.time() - t0
-    eng = Engine(args.parts, num_gpus=world, rank=rank, device=local)
-    if world > 1:
-        box = [comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(box, src=0)
-        eng.comm_init(box[0], world, rank)
-    eng.register_edge(1, "e", [("w", 2)])
-    t0 = time.time()
-    eng.load_edges(1, src, dst, [w])
-    eng.finalize()
-    load_s = time.time() - t0
-    st = eng.stats()
-    log(f"[rank {rank}] RMAT-{args.scale}: {len(src)} samples, snapshot {st}, gen {gen_s:.1f}s load {load_s:.1f}s")
-    src_verts, all_verts = rmat.vertex_sets(args.scale)
-    roots = [int(x) for x in rmat.pick_roots(src, args.roots, 42, verts=src_verts)]
-    where = E.binop("<", E.edge_prop("e", "w"), E.const(50)).encode()
 
-    # GoExecutor::prepare() once, execute() per root (rows stay in HBM)
-    stmt = eng.prepare_go([1], args.go_steps, where)
+def spawn_ranks(args):
+    """--gpus N without a launcher: run torch.distributed.run as a child (this process never
+    initialises the GPU, so nothing is exec'd from a GPU process) and exit with its code."""
+    port = str(29500 + (os.getpid() % 2000))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", port, os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    log(f"starting {args.gpus} ranks: {' '.join(cmd)}")
+    return subprocess.call(cmd, env=env)
 
-    # queries in flight (nbg_go_submit query slots: concurrent queries, each on its own stream
-    # and workspace; on a partitioned engine the slots share one stream, so each rank's
-    # collectives stay in submission order)
-    inflight = 0 if args.sync else int(os.environ.get("NBG_QUERY_SLOTS", "6"))
 
-    def one_step_sync():
-        scanned = rows = 0
-        lat = []
-        for r in roots:
-            q0 = time.perf_counter()
-            res = stmt.run_device([r])
-            lat.append(time.perf_counter() - q0)
+# ------------------------------------------------------------------------------------ GO legs
+def run_queries(stmt, roots, inflight):
+    """One step: every root as its own query, `inflight` queries on the query slots."""
+    scanned = rows = 0
+    pending = []
+    for r in roots:
+        if inflight and len(pending) == inflight:
+            res = stmt.wait(pending.pop(0))
             scanned += res.edges_scanned
             rows += res.count
             res.free()
-        return scanned, rows, lat
-
-    def one_step():
-        if not inflight:
-            return one_step_sync()
-        scanned = rows = 0
-        pending = []
-        for r in roots:
-            if len(pending) == inflight:
-                res = stmt.wait(pending.pop(0))
-                scanned += res.edges_scanned
-                rows += res.count
-                res.free()
+        if inflight:
             pending.append(stmt.submit([r]))
-        for tk in pending:
-            res = stmt.wait(tk)
+        else:
+            res = stmt.run_device([r])
             scanned += res.edges_scanned
             rows += res.count
             res.free()
-        return scanned, rows, []
+    for tk in pending:
+        res = stmt.wait(tk)
+        scanned += res.edges_scanned
+        rows += res.count
+        res.free()
+    return scanned, rows
 
+
+def go_leg(eng, stmt, roots, args, barrier, inflight, profile=True):
+    """Warm-up, the timed K steps, per-query latency, then the instrumented roofline passes."""
     for _ in range(args.warmup):
-        one_step()
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-        if torch.cuda.is_available():
-            torch.cuda.synchronize()
-
-    def timed_pass(step=None):
-        step = step or one_step
-        barrier()
-        t0 = time.perf_counter()
-        scanned = rows = 0
-        lats = []
-        for _ in range(args.steps):
-            s, r, lat = step()
-            scanned += s
-            rows += r
-            lats += lat
-        barrier()
-        return scanned, rows, lats, time.perf_counter() - t0
-
-    # the measured pass: no instrumentation inside the timed region
-    scanned, rows, lats, elapsed = timed_pass()
-    # per-query latency: one more step with the queries run one at a time
-    _, _, lats = one_step_sync()
-    kstats, breakdown, ev_elapsed = {}, {}, None
-    if not args.no_profile:
-        # roofline pass: the same K steps again with HIP events around every launch of the
-        # dominant (final-step) kernel on the engine's stream (the events cost ~10% of the wall
-        # time, which is why `value` comes from the pass above)
+        run_queries(stmt, roots, inflight)
+    barrier()
+    t0 = time.perf_counter()
+    scanned = rows = 0
+    for _ in range(args.steps):
+        s, r = run_queries(stmt, roots, inflight)
+        scanned += s
+        rows += r
+    barrier()
+    elapsed = time.perf_counter() - t0
+    lats = []
+    for r in roots:   # per-query latency: one query at a time
+        q0 = time.perf_counter()
+        stmt.run_device([r]).free()
+        lats.append(time.perf_counter() - q0)
+    out = {"scanned": scanned, "rows": rows, "elapsed": elapsed, "lat": lats}
+    if profile and not args.no_profile:
+        # roofline pass: the same K steps with HIP events around every launch of the dominant
+        # (final-step) kernel on the engine's stream; the events cost ~10% of the wall time,
+        # which is why `value` comes from the pass above
         eng.profile(2)
-        _, _, _, ev_elapsed = timed_pass(one_step_sync)
-        kstats = eng.profile_read()
+        barrier()
+        e0 = time.perf_counter()
+        for _ in range(args.steps):
+            run_queries(stmt, roots, 0)
+        barrier()
+        out["ev_elapsed"] = time.perf_counter() - e0
+        out["kstats"] = eng.profile_read()
         # per-kernel breakdown: one more step with events around every launch
         eng.profile(True)
-        one_step_sync()
-        breakdown = eng.profile_read()
+        barrier()
+        b0 = time.perf_counter()
+        run_queries(stmt, roots, 0)
+        barrier()
+        out["bd_elapsed"] = time.perf_counter() - b0
+        out["breakdown"] = eng.profile_read()
         eng.profile(False)
+    return out
 
-    sp = None
-    pairs = []
-    if args.sp_pairs > 0:   # partitioned: every rank runs each query collectively
-        pairs = rmat.pick_pairs(src, dst, args.sp_pairs, 7, verts=all_verts)
-        sp = shortest_path_leg(eng, pairs, args, barrier)
 
-    c5 = None
-    if world == 1 and args.c5_scale > 0:
-        c5 = c5_leg(args, barrier)
-    getbound = None
-    if world == 1 and args.getbound_reqs > 0:
-        getbound = getbound_leg(args)
-
-    # edges_scanned is already the whole query's count (summed over ranks in the library);
-    # rows stay on the rank that produced them, so they are summed here
-    tot_scanned, max_elapsed, tot_rows = float(scanned), elapsed, float(rows)
-    if dist is not None:
-        t = torch.tensor([float(rows), elapsed], dtype=torch.float64)
-        s_ = t.clone()
-        dist.all_reduce(s_[:1], op=dist.ReduceOp.SUM)
-        m_ = t.clone()
-        dist.all_reduce(m_[1:], op=dist.ReduceOp.MAX)
-        tot_rows, max_elapsed = float(s_[0]), float(m_[1])
-
-    if rank != 0:
-        if dist is not None:
-            dist.barrier()
-        return
-
-    value = tot_scanned / max_elapsed
-    # dominant kernel roofline (HIP events over the timed region, inside the library)
-    roofline = None
+def roofline_of(g, workload, steps):
+    """Dominant-kernel roofline + end-to-end algorithmic fraction from go_leg's profile passes."""
+    kstats, breakdown = g.get("kstats"), g.get("breakdown")
+    if not kstats:
+        return None, {}
     kernels = {}
-    if kstats:
-        for k, v in breakdown.items():
-            if v["launches"]:
-                kernels[k] = {"launches": v["launches"], "ms": round(v["ms"], 3),
-                              "algo_GBs": round(v["algo_bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None}
-        # the collective is reported on its own (xGMI link bytes, not HBM)
-        comm = breakdown.get("alltoall(xGMI)")
-        dom = max(((k, v) for k, v in kstats.items() if k != "alltoall(xGMI)"), key=lambda kv: kv[1]["ms"])
-        name, v = dom
-        achieved = v["algo_bytes"] / (v["ms"] * 1e-3) / 1e9
-        # the committed PMC summary was taken on the default workload (RMAT-22, one GPU, 64 roots)
-        default_workload = (args.scale, world, args.roots, args.go_steps) == (22, 1, 64, 3)
-        traffic = pmc_traffic(name) if default_workload else None
-        roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": round(traffic) if traffic else None,
-                    "traffic_source": os.path.relpath(PMC_FILE, ROOT) if traffic else None,
-                    "avg_launch_us": round(v["ms"] * 1e3 / v["launches"], 2),
-                    "algo_bytes_per_launch": v["algo_bytes"] / v["launches"]}
-        if comm and comm["launches"]:
-            roofline["exchange"] = {"launches": comm["launches"], "avg_us": round(comm["ms"] * 1e3 / comm["launches"], 2),
-                                    "bytes_sent_per_launch": comm["algo_bytes"] / comm["launches"],
-                                    "note": "bitmap all-to-all per hop; bytes = (N-1) x npad/8 sent per rank"}
-        kst_hbm = {k: x for k, x in breakdown.items() if k != "alltoall(xGMI)"}
-        total_ms = sum(x["ms"] for x in kst_hbm.values())
-        total_bytes = sum(x["algo_bytes"] for x in kst_hbm.values())
-        roofline["all_kernels_GBs"] = round(total_bytes / (total_ms * 1e-3) / 1e9, 1) if total_ms else None
-        roofline["timing"] = ("HIP events around every launch of this kernel on its stream during a second "
-                              "timed pass of the same K steps (profile mode 2); per-kernel table from a "
-                              "third, fully instrumented step")
-        roofline["events_pass_ms_per_step"] = round(ev_elapsed / args.steps * 1e3, 3) if ev_elapsed else None
-        roofline["kernel_time_frac_of_wall"] = round(v["ms"] * 1e-3 / ev_elapsed, 3) if ev_elapsed else None
+    for k, v in breakdown.items():
+        if v["launches"]:
+            kernels[k] = {"launches": v["launches"], "ms": round(v["ms"], 3),
+                          "algo_GBs": round(v["algo_bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None}
+    comm = breakdown.get("alltoall(xGMI)")
+    name, v = max(((k, x) for k, x in kstats.items() if k != "alltoall(xGMI)"), key=lambda kv: kv[1]["ms"])
+    achieved = v["algo_bytes"] / (v["ms"] * 1e-3) / 1e9
+    traffic, tsrc = pmc_traffic(name, workload)
+    roof = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": round(traffic) if traffic else None,
+            "traffic_source": os.path.relpath(tsrc, ROOT) if tsrc else None,
+            "avg_launch_us": round(v["ms"] * 1e3 / v["launches"], 2),
+            "algo_bytes_per_launch": v["algo_bytes"] / v["launches"]}
+    if comm and comm["launches"]:
+        roof["exchange"] = {"launches": comm["launches"], "avg_us": round(comm["ms"] * 1e3 / comm["launches"], 2),
+                            "bytes_sent_per_launch": comm["algo_bytes"] / comm["launches"],
+                            "note": "bitmap all-to-all per hop; bytes = (N-1) x npad/8 sent per rank"}
+    hbm = {k: x for k, x in breakdown.items() if k != "alltoall(xGMI)"}
+    total_ms = sum(x["ms"] for x in hbm.values())
+    total_bytes = sum(x["algo_bytes"] for x in hbm.values())
+    roof["all_kernels_GBs"] = round(total_bytes / (total_ms * 1e-3) / 1e9, 1) if total_ms else None
+    # end to end: every GO kernel's algorithmic bytes of one step / the wall time of a step
+    step_s = g["elapsed"] / steps
+    bd = g.get("bd_elapsed")
+    roof["end_to_end"] = {"algo_bytes_per_step": total_bytes,
+                          "GBs_vs_timed_step": round(total_bytes / step_s / 1e9, 1),
+                          "frac_vs_timed_step": round(total_bytes / step_s / 1e9 / HBM_PEAK_GBS, 4),
+                          "note": "all GO kernels' algorithmic bytes of one step (instrumented pass) / "
+                                  "ms_per_step of the timed pass"}
+    if bd:
+        roof["end_to_end"]["frac_vs_instrumented_step"] = round(total_bytes / bd / 1e9 / HBM_PEAK_GBS, 4)
+    roof["timing"] = ("HIP events around every launch of this kernel on its stream during a second timed pass of "
+                      "the same K steps (profile mode 2); per-kernel table from a third, fully instrumented step")
+    ev = g.get("ev_elapsed")
+    roof["events_pass_ms_per_step"] = round(ev / steps * 1e3, 3) if ev else None
+    roof["kernel_time_frac_of_wall"] = round(v["ms"] * 1e-3 / ev, 3) if ev else None
+    return roof, kernels
 
-    cpu = None
-    if world == 1 and not args.no_cpu_baseline:
-        cpu, sp_cpu = cpu_baseline(src, dst, w, roots, where, pairs, args)
-        if sp is not None:
-            sp["cpu_baseline"] = sp_cpu
 
-    lat_ms = np.array(lats) * 1e3
-    out = {
-        "metric": "GO 3 STEPS traversed edges/sec (TEPS) at 1/2/4/8 GPU; FIND SHORTEST PATH p50",
-        "value": value,
-        "unit": "TEPS",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": max_elapsed / args.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "int64",
-        "data": f"synthetic RMAT-{args.scale} (seeded Graph500 Kronecker, edge factor 16, w uniform 0-99)",
-        "config": {"workload": f"GO {args.go_steps} STEPS FROM <root> OVER e WHERE e.w < 50 YIELD e._dst, "
-                               f"{len(roots)} single-root queries per step",
-                   "graph": f"RMAT-{args.scale}", "parts": args.parts, "roots": len(roots),
-                   "queries_in_flight": inflight or 1,
-                   "parallelism": "single" if world == 1 else f"partitioned{world}: part % {world}, bitmap "
-                                                               f"all-to-all per hop over RCCL",
-                   "vertices": st["num_vertices"], "live_edges_out_plus_in": st["num_edges"]},
-        "roofline": roofline,
-        "cpu_baseline": cpu,
-        "query_latency_ms": {"p50": float(np.percentile(lat_ms, 50)), "p90": float(np.percentile(lat_ms, 90)),
-                             "max": float(lat_ms.max())},
-        "rows_per_step": int(tot_rows) // max(1, args.steps),
-        "edges_per_step": scanned // max(1, args.steps),
-        "kernels": kernels,
-        "find_shortest_path": sp,
-        "c5_substitute": c5,
-        "getbound": getbound,
-        "load_seconds": round(load_s, 2),
-    }
-    print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.barrier()
+def host_delivered(stmt, roots):
+    """nbg_go semantics (rows copied to host memory, what ExecutionResponse carries): rows/s and
+    the device-to-host GB/s of the 8-byte cells."""
+    rows = cells = 0
+    t0 = time.perf_counter()
+    for r in roots:
+        res = stmt.run_device([r])
+        cols = res.fetch_bits()
+        rows += res.count
+        cells += sum(len(c) for c in cols)
+        res.free()
+    el = time.perf_counter() - t0
+    return {"queries": len(roots), "rows": rows, "seconds": round(el, 4), "rows_per_s": rows / el if el else None,
+            "d2h_GBs": cells * 8 / el / 1e9 if el else None,
+            "timing": "nbg_go_execute (device) + nbg_rows_fetch of every row, one query at a time"}
 
 
 def shortest_path_leg(eng, pairs, args, barrier):
-    """FIND SHORTEST PATH FROM s TO t OVER e UPTO n STEPS, one query per pair."""
+    """FIND SHORTEST PATH FROM s TO t OVER e UPTO n STEPS, one query per pair (C4)."""
     for s, t in pairs[:16]:   # warm-up
         eng.find_path([s], [t], [1], args.sp_upto)
-    # latency pass: uninstrumented (no HIP events around the launches)
     barrier()
     lat, edges, found, hops = [], 0, 0, 0
     t0 = time.perf_counter()
@@ -330,9 +250,8 @@ def shortest_path_leg(eng, pairs, args, barrier):
             hops += (len(paths[0]) - 1) // 3
     barrier()
     elapsed = time.perf_counter() - t0
-    # roofline pass: HIP events around k_expand<BFS> over the first pairs (same queries)
     kst, prof_pairs = {}, 0
-    if not args.no_profile:
+    if not args.no_profile:   # roofline pass: HIP events around k_expand<BFS> over the first pairs
         eng.profile(2)
         barrier()
         for s, t in pairs[:2000]:
@@ -357,10 +276,349 @@ def shortest_path_leg(eng, pairs, args, barrier):
         ach = v["algo_bytes"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] else 0.0
         out["roofline"] = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                           "avg_launch_us": round(v["ms"] * 1e3 / v["launches"], 2)}
-        out["roofline"]["timing"] = (f"HIP events around every k_expand<BFS> launch in a second pass over the "
-                                     f"first {prof_pairs} pairs; latencies come from the uninstrumented pass")
+                           "avg_launch_us": round(v["ms"] * 1e3 / v["launches"], 2),
+                           "timing": f"HIP events around every k_expand<BFS> launch in a second pass over the "
+                                     f"first {prof_pairs} pairs; latencies come from the uninstrumented pass"}
     return out
+
+
+def load_engine(scale, args, world, rank, local, comm_init):
+    from nebula_amd import Engine, rmat
+    t0 = time.time()
+    src, dst, w = rmat.rmat_edges_fast(scale)
+    gen_s = time.time() - t0
+    eng = Engine(args.parts, num_gpus=world, rank=rank, device=local)
+    if world > 1:
+        comm_init(eng)
+    eng.register_edge(1, "e", [("w", 2)])
+    t0 = time.time()
+    eng.load_edges(1, src, dst, [w])
+    eng.finalize()
+    load_s = time.time() - t0
+    log(f"[rank {rank}] RMAT-{scale}: {len(src)} samples, snapshot {eng.stats()}, gen {gen_s:.1f}s load {load_s:.1f}s")
+    return src, dst, w, eng, gen_s, load_s
+
+
+# ------------------------------------------------------------------------------------ main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scale", type=int, default=None, help="RMAT scale (default 26; --weak: 22 + log2 N)")
+    ap.add_argument("--weak", action="store_true", help="weak scaling: RMAT-(22 + log2 N), 64 roots")
+    ap.add_argument("--roots", type=int, default=None, help="queries per step (default 16 at RMAT-26, else 64)")
+    ap.add_argument("--parts", type=int, default=100)
+    ap.add_argument("--go-steps", type=int, default=3)
+    ap.add_argument("--verify", type=int, default=4, help="headline roots checked by device digest vs the CSR oracle")
+    ap.add_argument("--cpu-seconds", type=float, default=30.0, help="storaged-faithful CPU baseline budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--sp-pairs", type=int, default=10000, help="FIND SHORTEST PATH pairs (0 = skip)")
+    ap.add_argument("--sp-upto", type=int, default=5)
+    ap.add_argument("--sync", action="store_true", help="one query at a time (no query slots)")
+    ap.add_argument("--c2", type=int, default=1, help="C2 leg (RMAT-22, 64 roots) when the headline is larger")
+    ap.add_argument("--c5-scale", type=int, default=20,
+                    help="C5 substitute (knows RMAT + likes bipartite): knows scale, 0 = skip")
+    ap.add_argument("--getbound-reqs", type=int, default=200,
+                    help="QueryBoundBenchmark-shaped GetNeighbors requests (0 = skip)")
+    args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"WORLD_SIZE={world} but --gpus {args.gpus}")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("NBG_SAME_DEVICE"):
+        # rehearsal on a one-GPU box: every rank on device 0, RCCL over its socket transport
+        # (distinct host ids; see tools/rccl_probe.py).  Timings are then not xGMI numbers.
+        local = 0
+        os.environ["NCCL_HOSTID"] = f"nbg-rank-{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    from nebula_amd import comm_unique_id, expr as E, rmat
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    def comm_init(eng):
+        box = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        eng.comm_init(box[0], world, rank)
+
+    scaling = "weak" if args.weak else "strong"
+    if args.scale is None:
+        args.scale = 22 + max(0, int(round(np.log2(world)))) if args.weak else 26
+    if args.roots is None:
+        args.roots = 16 if args.scale >= 26 else 64
+    where = E.binop("<", E.edge_prop("e", "w"), E.const(50)).encode()
+    inflight = 0 if args.sync else int(os.environ.get("NBG_QUERY_SLOTS", "6"))
+    model, threads, ncpu = cpu_info()
+
+    # ---------------- headline: GO 3 STEPS on RMAT-scale (C3 at N GPUs), FIND SHORTEST PATH (C4)
+    src, dst, w, eng, gen_s, load_s = load_engine(args.scale, args, world, rank, local, comm_init)
+    st = eng.stats()
+    src_verts, all_verts = rmat.vertex_sets(args.scale)
+    roots = [int(x) for x in rmat.pick_roots(src, args.roots, 42, verts=src_verts)]
+    pairs = rmat.pick_pairs(src, dst, args.sp_pairs, 7, verts=all_verts) if args.sp_pairs > 0 else []
+    del src_verts, all_verts
+    if rank != 0:   # only rank 0 keeps the samples (CSR oracle / CPU baselines)
+        del src, dst, w
+        src = dst = w = None
+    stmt = eng.prepare_go([1], args.go_steps, where)
+    g = go_leg(eng, stmt, roots, args, barrier, inflight)
+    workload = (f"RMAT-{args.scale}", len(roots)) if world == 1 and args.go_steps == 3 else None
+    roofline, kernels = roofline_of(g, workload, args.steps)
+    delivered = host_delivered(stmt, roots[:4]) if world == 1 else None
+    # device digests of the first headline queries (summed over ranks: rows stay where produced)
+    dig = []
+    for r in roots[:args.verify]:
+        res = stmt.run_device([r])
+        dig.append(list(res.digest()) + [res.edges_scanned])
+        res.free()
+    stmt.free()
+    sp = shortest_path_leg(eng, pairs, args, barrier) if pairs else None
+    sp_sample = []
+    if pairs and args.verify:   # device paths for the verification sample
+        sp_sample = [eng.find_path([s], [t], [1], args.sp_upto) for s, t in pairs[:64]]
+    eng.close()
+
+    tot_scanned, max_elapsed, tot_rows = float(g["scanned"]), g["elapsed"], float(g["rows"])
+    if dist is not None:
+        t = torch.tensor([float(g["rows"]), g["elapsed"]], dtype=torch.float64)
+        s_, m_ = t.clone(), t.clone()
+        dist.all_reduce(s_[:1], op=dist.ReduceOp.SUM)
+        dist.all_reduce(m_[1:], op=dist.ReduceOp.MAX)
+        tot_rows, max_elapsed = float(s_[0]), float(m_[1])
+        # digests are additive over ranks: rows +, xor ^, sum + (mod 2^64)
+        parts = [None] * world
+        dist.all_gather_object(parts, dig)
+        if rank == 0:
+            M = (1 << 64) - 1
+            dig = [[sum(p[i][0] for p in parts), 0, sum(p[i][2] for p in parts) & M, parts[0][i][3]]
+                   for i in range(len(dig))]
+            for i in range(len(dig)):
+                for p in parts:
+                    dig[i][1] ^= p[i][1]
+
+    if rank != 0:
+        dist.barrier()
+        return
+
+    # ---------------- verification + CPU baseline mode (ii): the CSR oracle on the same graph
+    verify = None
+    cpu_csr = None
+    if (args.verify or not args.no_cpu_baseline) and world >= 1:
+        try:
+            from tests.support.oracle import CsrOracle, Y_DST
+            t0 = time.time()
+            csr = CsrOracle(src, dst, w, threads=threads)
+            build_s = time.time() - t0
+            log(f"CSR oracle built in {build_s:.1f}s ({threads} threads)")
+            ok = True
+            checked = []
+            for r, d in zip(roots, dig):
+                exp, scanned, _, _ = csr.go([r], args.go_steps, "<", 50, Y_DST)
+                match = list(exp) == d[:3] and scanned == d[3]
+                ok = ok and match
+                checked.append({"root": r, "rows": d[0], "match": match})
+            sp_ok, sp_found = True, 0
+            for (s, t), got in zip(pairs[:64], sp_sample):
+                exp, _ = csr.shortest(s, t, args.sp_upto)
+                gv = got[0][0::3] if got else []
+                sp_ok = sp_ok and gv == exp
+                sp_found += bool(exp)
+            verify = {"go_roots_checked": len(checked), "go_match": ok, "sp_pairs_checked": len(sp_sample),
+                      "sp_match": sp_ok, "sp_found": sp_found,
+                      "method": "device nbg_rows_digest (rows, xor, sum of splitmix64 row chains; summed over ranks) "
+                                "and edges scanned vs oracle/csr.cpp on the same graph; SHORTEST paths compared "
+                                "entry by entry", "oracle_build_s": round(build_s, 1)}
+            if not args.no_cpu_baseline and world == 1:
+                cpu_csr = csr_baseline(csr, roots, pairs, args, threads, model, ncpu)
+            csr.close()
+        except Exception as ex:  # pragma: no cover
+            log(f"verification / CSR baseline unavailable: {ex}")
+    del src, dst, w
+
+    # ---------------- secondary legs (one GPU)
+    c2 = None
+    if world == 1 and args.c2 and args.scale != 22:
+        c2 = c2_leg(args, barrier, inflight)
+    c5 = c5_leg(args, barrier) if world == 1 and args.c5_scale > 0 else None
+    getbound = getbound_leg(args) if world == 1 and args.getbound_reqs > 0 else None
+
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = faithful_baseline(args, where, threads, model, ncpu)
+        if cpu is not None:
+            cpu["csr_openmp"] = cpu_csr
+        elif cpu_csr is not None:
+            cpu = cpu_csr
+    if sp is not None and cpu_csr is not None:
+        sp["cpu_baseline"] = cpu_csr.get("shortest")
+
+    lat_ms = np.array(g["lat"]) * 1e3
+    out = {
+        "metric": METRIC,
+        "value": tot_scanned / max_elapsed,
+        "unit": "TEPS",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": max_elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": scaling,
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": f"synthetic RMAT-{args.scale} (seeded Graph500 Kronecker, edge factor 16, w uniform 0-99)",
+        "config": {"workload": f"GO {args.go_steps} STEPS FROM <root> OVER e WHERE e.w < 50 YIELD e._dst, "
+                               f"{len(roots)} single-root queries per step",
+                   "graph": f"RMAT-{args.scale}", "parts": args.parts, "roots": len(roots),
+                   "queries_in_flight": inflight or 1, "result_residency": "rows left in HBM (nbg_go_submit "
+                                                                          "device=1); host-delivered rate below",
+                   "parallelism": "single" if world == 1 else f"partitioned{world}: part % {world}, bitmap "
+                                                               f"all-to-all per hop over RCCL",
+                   "vertices_rank0": st["num_vertices"], "live_edges_out_plus_in_rank0": st["num_edges"]},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "verification": verify,
+        "query_latency_ms": {"p50": float(np.percentile(lat_ms, 50)), "p90": float(np.percentile(lat_ms, 90)),
+                             "max": float(lat_ms.max())},
+        "rows_per_step": int(tot_rows) // max(1, args.steps),
+        "edges_per_step": int(tot_scanned) // max(1, args.steps),
+        "host_delivered": delivered,
+        "kernels": kernels,
+        "find_shortest_path": sp,
+        "c2_rmat22": c2,
+        "c5_substitute": c5,
+        "getbound": getbound,
+        "gen_seconds": round(gen_s, 2),
+        "load_seconds": round(load_s, 2),
+    }
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+
+
+def c2_leg(args, barrier, inflight):
+    """RMAT-22 on one GPU, 64 roots, the same GO 3 STEPS query; FIND SHORTEST
+    PATH over 10k pairs on the same graph."""
+    from nebula_amd import expr as E, rmat
+    src, dst, w, eng, gen_s, load_s = load_engine(22, args, 1, 0, 0, None)
+    sv, av = rmat.vertex_sets(22)
+    roots = [int(x) for x in rmat.pick_roots(src, 64, 42, verts=sv)]
+    where = E.binop("<", E.edge_prop("e", "w"), E.const(50)).encode()
+    stmt = eng.prepare_go([1], 3, where)
+    g = go_leg(eng, stmt, roots, args, barrier, inflight)
+    roof, kernels = roofline_of(g, ("RMAT-22", 64), args.steps)
+    stmt.free()
+    sp = None
+    if args.sp_pairs > 0:
+        a2 = argparse.Namespace(**vars(args))
+        sp = shortest_path_leg(eng, rmat.pick_pairs(src, dst, args.sp_pairs, 7, verts=av), a2, barrier)
+    eng.close()
+    lat_ms = np.array(g["lat"]) * 1e3
+    return {"graph": "RMAT-22", "roots": 64, "teps": g["scanned"] / g["elapsed"],
+            "ms_per_step": g["elapsed"] / args.steps * 1e3, "rows_per_step": g["rows"] // args.steps,
+            "edges_per_step": g["scanned"] // args.steps, "query_latency_ms": {"p50": float(np.percentile(lat_ms, 50)),
+                                                                             "p90": float(np.percentile(lat_ms, 90))},
+            "roofline": roof, "kernels": kernels, "find_shortest_path": sp, "load_seconds": round(load_s, 2)}
+
+
+def csr_baseline(csr, roots, pairs, args, threads, model, ncpu):
+    """CPU baseline mode (ii): oracle/csr.cpp — OpenMP GO over a CSR and a
+    bidirectional BFS — on the headline graph, median of 5 runs after one warm-up."""
+    from tests.support.oracle import Y_DST
+    csr.set_threads(threads)
+    runs = []
+    for k in range(6):
+        secs = scanned = 0.0
+        for r in roots:
+            _, sc, sec, _ = csr.go([r], args.go_steps, "<", 50, Y_DST)
+            secs += sec
+            scanned += sc
+        if k:
+            runs.append((scanned / secs, secs))
+    runs.sort()
+    teps, secs = runs[len(runs) // 2]
+    sp = None
+    if pairs:
+        sample = pairs[:200]
+        med = []
+        for k in range(6):
+            lat = []
+            for s, t in sample:
+                q0 = time.perf_counter()
+                csr.shortest(s, t, args.sp_upto)
+                lat.append(time.perf_counter() - q0)
+            if k:
+                med.append(float(np.percentile(np.array(lat) * 1e3, 50)))
+        sp = {"p50_ms": sorted(med)[len(med) // 2], "cores": threads, "kind": "port",
+              "sample": f"first {len(sample)} of the {len(pairs)} pairs, median of 5 runs of the p50",
+              "model": model}
+    return {"value": teps, "unit": "TEPS", "cores": threads, "kind": "port", "mode": "csr_openmp",
+            "sample": f"all {len(roots)} headline roots (same graph and query), median of 5 runs after 1 warm-up "
+                      f"({secs:.2f}s per run); oracle/csr.cpp OpenMP CSR GO, {threads} threads",
+            "model": model, "host_cpus": ncpu, "shortest": sp}
+
+
+def faithful_baseline(args, where, threads, model, ncpu):
+    """CPU baseline mode (i): oracle/ storaged+graphd restatement (per-edge RowReader decode,
+    RowSet encode/decode per hop, unordered_set frontiers, bucket fan-out of 10 handlers; RocksDB /
+    thrift / RPC excluded) on the C2 graph (RMAT-22: the KV store of RMAT-26 needs ~90 GB of host
+    RAM), sampled within --cpu-seconds."""
+    try:
+        from tests.support.oracle import Oracle
+        from nebula_amd import rmat
+    except Exception as ex:  # pragma: no cover
+        log(f"cpu baseline unavailable: {ex}")
+        return None
+    src, dst, w = rmat.rmat_edges_fast(22)
+    sv, av = rmat.vertex_sets(22)
+    roots = [int(x) for x in rmat.pick_roots(src, 64, 42, verts=sv)]
+    t0 = time.time()
+    handlers = 10   # FLAGS_max_handlers_per_req
+    o = Oracle(args.parts, threads=handlers)
+    o.L.orc_set_hosts(o.h, 1)
+    o.register(True, 1, "e", [("w", 2)])
+    o.load_edges(1, src, dst, [w])
+    o.finalize()
+    log(f"cpu baseline store built in {time.time() - t0:.1f}s")
+    secs = scanned = 0.0
+    n = 0
+    for r in roots[:16]:
+        s, rows, sc = o.go_timed([r], [1], args.go_steps, where)
+        secs += s
+        scanned += sc
+        n += 1
+        if secs >= args.cpu_seconds:
+            break
+    pairs = rmat.pick_pairs(src, dst, 20, 7, verts=av)
+    lat = []
+    for s_, t_ in pairs:
+        q0 = time.perf_counter()
+        o.find_path([s_], [t_], [1], args.sp_upto, True, mode=1)
+        lat.append(time.perf_counter() - q0)
+        if sum(lat) >= args.cpu_seconds / 2:
+            break
+    o.close()
+    return {"value": scanned / secs if secs else None, "unit": "TEPS", "cores": handlers, "kind": "port",
+            "mode": "storaged_faithful",
+            "sample": f"RMAT-22 (C2), first {n} of 64 roots, {secs:.1f}s; one storaged host, {handlers} handler "
+                      f"threads (max_handlers_per_req), RowSet encode/decode per hop, RocksDB/thrift/RPC excluded",
+            "model": model, "host_cpus": ncpu,
+            "shortest": {"p50_ms": float(np.percentile(np.array(lat) * 1e3, 50)), "pairs": len(lat), "cores": 1,
+                         "sample": "RMAT-22 pairs (seed 7); canonical BFS over the storaged-faithful KV store"}}
 
 
 def getbound_leg(args):
@@ -400,8 +658,6 @@ def getbound_leg(args):
     from nebula_amd.engine import _gn_request
     for _ in range(5):
         got = eng.get_neighbors(req_vids, [101], b"", rets)
-    # the C ABI call alone (request in, encoded QueryResponse rows and schemas out in host memory);
-    # the Python mirror's decoding of the response into dicts is not part of the boundary
     keep = []
     req = _gn_request(req_vids, [101], b"", rets, keep)
     lat = []
@@ -422,7 +678,7 @@ def getbound_leg(args):
                                    "hardware": "40 procs, Xeon E5-2690 v2 (QueryBoundBenchmark.cpp:178-189)"}}
     if not args.no_cpu_baseline:
         try:
-            from tests.support.oracle import Oracle
+            from tests.support.oracle import Oracle, _ptr
             o = Oracle(parts, threads=10)
             o.register(True, 101, "e101", eschema)
             for t in range(3001, 3010):
@@ -430,7 +686,6 @@ def getbound_leg(args):
             o.load_builder(kb)
             exp = o.get_neighbors(req_vids, [101], b"", rets)
             out["parity_vs_oracle"] = exp == got
-            from tests.support.oracle import _ptr
             a_parts = np.asarray([p for p, _ in req_vids], np.int32)
             a_vids = np.asarray([v for _, v in req_vids], np.int64)
             a_et = np.asarray([101], np.int32)
@@ -481,27 +736,8 @@ def c5_leg(args, barrier):
     inflight = 0 if args.sync else int(os.environ.get("NBG_QUERY_SLOTS", "6"))
 
     def go4_pass():
-        scanned = rows = 0
-        pending = []
         t1 = time.perf_counter()
-        for r in roots:
-            if inflight and len(pending) == inflight:
-                res = stmt.wait(pending.pop(0))
-                scanned += res.edges_scanned
-                rows += res.count
-                res.free()
-            if inflight:
-                pending.append(stmt.submit([r]))
-            else:
-                res = stmt.run_device([r])
-                scanned += res.edges_scanned
-                rows += res.count
-                res.free()
-        for tk in pending:
-            res = stmt.wait(tk)
-            scanned += res.edges_scanned
-            rows += res.count
-            res.free()
+        scanned, rows = run_queries(stmt, roots, inflight)
         return scanned, rows, time.perf_counter() - t1
 
     # one pass is ~10 ms of work: report the median of 5 passes
@@ -529,52 +765,6 @@ def c5_leg(args, barrier):
             "find_all_path": {"query": "FIND ALL PATH FROM <s> TO <t> OVER knows UPTO 4 STEPS", "pairs": len(pairs),
                               "paths": paths, "p50_ms": float(np.percentile(lat_ms, 50)),
                               "p90_ms": float(np.percentile(lat_ms, 90)), "max_ms": float(lat_ms.max())}}
-
-
-def cpu_baseline(src, dst, w, roots, where, pairs, args):
-    """oracle/ (storaged+graphd restated, RocksDB/thrift excluded) timed on the host cores."""
-    try:
-        from tests.support.oracle import Oracle
-    except Exception as ex:  # pragma: no cover
-        log(f"cpu baseline unavailable: {ex}")
-        return None, None
-    t0 = time.time()
-    handlers = 10   # FLAGS_max_handlers_per_req
-    o = Oracle(args.parts, threads=handlers)
-    o.L.orc_set_hosts(o.h, 1)
-    o.register(True, 1, "e", [("w", 2)])
-    o.load_edges(1, src, dst, [w])
-    o.finalize()
-    log(f"cpu baseline store built in {time.time() - t0:.1f}s")
-    secs = scanned = 0.0
-    n = 0
-    for r in roots:
-        s, rows, sc = o.go_timed([r], [1], args.go_steps, where)
-        secs += s
-        scanned += sc
-        n += 1
-        if secs >= args.cpu_seconds:
-            break
-    go = {"value": scanned / secs if secs else None, "unit": "TEPS", "cores": handlers, "kind": "port",
-          "sample": f"first {n} of the {len(roots)} roots (same graph and query), {secs:.1f}s; one storaged "
-                    f"host, {handlers} handler threads (max_handlers_per_req), RowSet encode/decode per hop, "
-                    f"RocksDB/thrift/RPC excluded"}
-    sp = None
-    if pairs:
-        lat = []
-        for s, t in pairs:
-            q0 = time.perf_counter()
-            o.find_path([s], [t], [1], args.sp_upto, True, mode=1)
-            lat.append(time.perf_counter() - q0)
-            if sum(lat) >= args.cpu_seconds:
-                break
-        lat_ms = np.array(lat) * 1e3
-        sp = {"p50_ms": float(np.percentile(lat_ms, 50)), "mean_ms": float(lat_ms.mean()), "cores": 1,
-              "kind": "port", "sample": f"first {len(lat)} of the {len(pairs)} pairs, {sum(lat):.1f}s; oracle "
-                                        f"canonical shortest path (level-synchronous BFS from s over the "
-                                        f"storaged-faithful KV store, then B-set reconstruction), 1 thread"}
-    o.close()
-    return go, sp
 
 
 if __name__ == "__main__":

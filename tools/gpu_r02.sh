@@ -12,10 +12,27 @@ for step in "$@"; do
     tests)
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
         > "$OUT/pytest_gpu.log" 2>&1 || { tail -40 "$OUT/pytest_gpu.log"; exit 1; } ;;
+    configs)
+      timeout -k 10 1100 python -u -m pytest tests/test_gpu_configs.py -x -v --timeout 1200 --timeout-method thread \
+        > "$OUT/pytest_configs.log" 2>&1 || { tail -40 "$OUT/pytest_configs.log"; exit 1; } ;;
     load26)
       timeout -k 10 900 python -u bench.py --scale 26 --roots 16 --steps 2 --sp-pairs 0 --no-cpu-baseline \
         --c5-scale 0 --getbound-reqs 0 --no-profile > "$OUT/load26.json" 2> "$OUT/load26.log" \
         || { tail -30 "$OUT/load26.log"; exit 1; } ;;
+    pmc26|pmc22)
+      sc=${step#pmc}
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 400 rocprofv3 --pmc $c -d "$OUT/pmc${sc}_$c" -o run --output-format csv -- \
+          python3 -u bench.py --scale $sc --steps 1 --warmup 1 --sp-pairs 0 --no-cpu-baseline --no-profile \
+          --verify 0 --c2 0 --c5-scale 0 --getbound-reqs 0 > "$OUT/pmc${sc}_$c.json" 2> "$OUT/pmc${sc}_$c.log" \
+          || { tail -30 "$OUT/pmc${sc}_$c.log"; exit 1; }
+      done
+      python3 tools/pmc_summary.py $(find "$OUT/pmc${sc}_FETCH_SIZE" "$OUT/pmc${sc}_WRITE_SIZE" -name '*counter_collection.csv') \
+        > "$OUT/pmc_hbm_rmat${sc}.json" ;;
+    prof26)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof26" -o run --output-format csv -- \
+        python3 -u bench.py --sp-pairs 2000 --no-cpu-baseline --verify 0 --c2 0 --c5-scale 0 --getbound-reqs 0 \
+        > "$OUT/bench_prof26.json" 2> "$OUT/bench_prof26.log" || { tail -30 "$OUT/bench_prof26.log"; exit 1; } ;;
     bench)
       timeout -k 10 900 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.log" || { tail -30 "$OUT/bench.log"; exit 1; } ;;
   esac
