@@ -44,6 +44,16 @@ void Engine::free_snapshot() {
   snap = Snapshot();
 }
 
+uint64_t Engine::sp_item_cap() const {
+  // a level claims each vertex once; its items are its 64-entry runs over the side's types
+  uint64_t pos_types = 0, e_out = 0, e_in = 0;
+  for (auto& kv : snap.types) {
+    if (kv.first > 0) { ++pos_types; e_out += kv.second.num_edges; }
+    else e_in += kv.second.num_edges;
+  }
+  return snap.nv * std::max<uint64_t>(pos_types, 1) + std::max(e_out, e_in) / 64 + 1024;
+}
+
 uint32_t Engine::dense(int64_t vid) const {
   auto& v = snap.h_vids;
   auto it = std::lower_bound(v.begin(), v.end(), vid);
@@ -591,13 +601,23 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
   uint64_t n_bound = f0.size();
   for (uint32_t s = 1; he == hipSuccess && s <= steps; ++s) {
     const bool final = s == steps;
+    // the next step's first OVER type: the next frontier list carries its edge space
+    ExpandArgs next0{};
+    const ExpandArgs* np0 = nullptr;
+    if (!final) {
+      auto it0 = E.snap.types.find(over[0]);
+      if (it0 != E.snap.types.end()) {
+        next0 = args_for(it0->second);
+        np0 = &next0;
+      }
+    }
     for (size_t i = 0; he == hipSuccess && i < over.size(); ++i) {
       auto it = E.snap.types.find(over[i]);
       if (it == E.snap.types.end()) continue;
       ExpandArgs a = args_for(it->second);
       a.bt_first = s == 1;
       if (!final) {
-        he = ws_expand_mark(ws, a, n_bound, it->second.num_edges, (int)s, (int)i, inl_of(i, s));
+        he = ws_expand_mark(ws, a, n_bound, it->second.num_edges, (int)s, (int)i, inl_of(i, s), np0);
       } else if (deferred || (plist[i].where_const && !plist[i].where_const_val)) {
         he = ws_scan_only(ws, a, n_bound, (int)s, (int)i);
       } else {
@@ -606,15 +626,7 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
       }
     }
     if (!final && he == hipSuccess) {
-      // the next step's first OVER type gets its degree pass fused into the compaction
-      auto it0 = E.snap.types.find(over[0]);
-      ExpandArgs next0{};
-      const ExpandArgs* np0 = nullptr;
-      if (it0 != E.snap.types.end()) {
-        next0 = args_for(it0->second);
-        np0 = &next0;
-      }
-      he = E.partitioned() ? ws_exchange(ws, (int)s, np0) : ws_compact(ws, (int)s, np0);
+      he = E.partitioned() ? ws_exchange(ws, (int)s, np0) : ws_finish_step(ws, (int)s, np0);
       n_bound = E.snap.nv;
     }
   }
@@ -903,6 +915,7 @@ void nbg_destroy(nbg_engine* h) {
     if (q.stream) (void)hipStreamDestroy(q.stream);
   }
   if (E.ws) ws_destroy(E.ws);
+  if (E.sp) sp_destroy(E.sp);
   E.free_snapshot();
   if (E.stream) (void)hipStreamDestroy(E.stream);
   delete h;

@@ -35,6 +35,8 @@ struct Engine {
     void* ticket = nullptr;   // the ticket running on this slot (nullptr: free)
   };
   std::vector<QuerySlot> slots;
+  SpCtx* sp = nullptr;                  // one-pair FIND SHORTEST PATH workspace (sp.hip), on `stream`
+  uint64_t sp_item_cap() const;         // items a shortest-path list may hold
   std::vector<void*> inflight;          // submitted tickets, oldest first
   // device GO results (rows left in HBM) and the workspace their rows live in: before that
   // workspace runs another query it is handed to the result (freed with it) and replaced

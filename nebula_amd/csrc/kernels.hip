@@ -74,8 +74,17 @@ struct Workspace {
   uint64_t nv = 0;
   uint32_t* frontier[2] = {nullptr, nullptr};
   int cur = 0;
-  uint32_t* seg_end = nullptr;    // block-local inclusive scan of degrees
-  uint32_t* seg_rs = nullptr;     // row start per frontier entry
+  // edge space of a list, two sets: frontier[i]'s list carries set i; k_relist writes into the
+  // set of the current frontier (free by then); claim-mode MARK builds the next list in the other
+  uint32_t* seg_end = nullptr;    // set 0: inclusive scan of degrees
+  uint32_t* seg_rs = nullptr;     // set 0: row start per frontier entry
+  uint32_t* seg_end1 = nullptr;   // set 1
+  uint32_t* seg_rs1 = nullptr;
+  uint32_t* tsplit1 = nullptr;
+  uint32_t* seen = nullptr;       // [nv + 1] claim stamps of the per-step dst SET (single engine)
+  uint32_t seen_stamp = 0;        // last stamp handed out
+  uint32_t step_stamp = 0;        // stamp of the current step (all its OVER types)
+  bool mark_flags = false;        // NBG_MARK_FLAGS=1: byte flags + k_compact instead of claims
   uint32_t* rlist = nullptr;      // k_relist output list
   uint8_t* flags = nullptr;       // [nv rounded up to FLAG_ALIGN], kept all-zero between steps
   uint64_t flag_bytes = 0;
@@ -507,6 +516,10 @@ struct BfsParams {
   unsigned long long* out_n;      // its length, zero before the level
   DegsumArgs deg;
   unsigned long long* dsum;       // nullable
+  // MARK claim mode (lab != nullptr): claimed neighbours go to this list with their edge space
+  // over nds (the next step's first OVER type); nlist.zero_next is zeroed by workgroup 0
+  ListOut nlist;
+  DegSrc nds;
 };
 
 struct FinalParams {
@@ -527,6 +540,41 @@ struct FinalParams {
   unsigned long long* tag_bits;    // QState::tagbits
   FastProg fast;
 };
+
+// MARK claim mode: the per-step dst SET (GoExecutor::getDstIdsFromResp, GoExecutor.cpp:501-541)
+// as claims — the first expansion of the step to CAS a neighbour's stamp to the step's stamp
+// owns it — and the owners appended to the next frontier list together with their edge space
+// over the next step's first OVER type: one packed atomic per wave for list positions and edge
+// offsets.  A vertex without edges there is kept (the list is the frontier of every OVER type).
+__device__ __forceinline__ void claim_append(const uint32_t (&u)[VT], const BfsParams& bp, int lane) {
+  uint32_t dg[VT], rs[VT], cmask = 0;
+#pragma unroll
+  for (int i = 0; i < VT; ++i) {
+    dg[i] = 0;
+    rs[i] = 0;
+    const uint32_t x = u[i];
+    if (x == NO_ROW) continue;
+    const uint32_t old = bp.lab[x];
+    if (old == bp.stamp) continue;
+    if (atomicCAS(bp.lab + x, old, bp.stamp) != old) continue;
+    cmask |= 1u << i;
+    dg[i] = vdeg(bp.nds, x, &rs[i]);
+  }
+  uint32_t c = (uint32_t)__popc(cmask), d = 0;
+#pragma unroll
+  for (int i = 0; i < VT; ++i) d += dg[i];
+  const uint32_t ic = wave_incl_scan(c), id = wave_incl_scan(d);
+  const uint32_t tc = __shfl(ic, 63, 64), td = __shfl(id, 63, 64);
+  if (!tc) return;   // wave-uniform
+  unsigned long long old = 0;
+  if (lane == 0) old = atomicAdd(bp.nlist.acc, ((unsigned long long)tc << 32) | td);
+  old = __shfl(old, 0, 64);
+  uint32_t pos = (uint32_t)(old >> 32) + ic - c;
+  uint32_t pd = (uint32_t)old + id - d;
+#pragma unroll
+  for (int i = 0; i < VT; ++i)
+    if ((cmask >> i) & 1u) list_put(bp.nlist, bp.nds, pos++, u[i], &pd, dg[i], rs[i]);
+}
 
 // Merge-path split of tile t: entries consumed before position t * TILE (which 0) or before the
 // tile's end (which 1).
@@ -681,6 +729,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
     if (threadIdx.x == 0) sBase = 0;
     __syncthreads();
   }
+  if ((M == MARK || M == MARKB) && bp.nlist.zero_next && blockIdx.x == 0 && threadIdx.x == 0) *bp.nlist.zero_next = 0;
 #ifdef NBG_PHASE_TIMING   // experiment builds only: cycles per tile phase (lane 0 of wave 0), printed
   unsigned long long ph[5] = {0, 0, 0, 0, 0}, ph_prev = clock64();
 #define NBG_PH(k)                                        \
@@ -764,20 +813,23 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
     NBG_PH(1)
 
     if (M == MARKB) {
+      uint32_t u[VT];
 #pragma unroll
       for (int i = 0; i < VT; ++i) {
         const int k = i * 64 + lane;
+        u[i] = NO_ROW;
         if (k < nb) {
           const uint32_t s = sSeg[k];
-          const uint32_t u = a.col[(uint64_t)sRs[s] + (b0 + k - (uint64_t)sEnd[s])];
-          if (u == NO_ROW) continue;
+          u[i] = a.col[(uint64_t)sRs[s] + (b0 + k - (uint64_t)sEnd[s])];
+          if (u[i] == NO_ROW) continue;
           const uint32_t src = list_id(a0 + s);
-          a.bt[u] = a.bt_first ? src : a.bt[src];
-          flags[u] = 1;
+          a.bt[u[i]] = a.bt_first ? src : a.bt[src];
+          if (!bp.lab) flags[u[i]] = 1;
         }
       }
+      if (bp.lab) claim_append(u, bp, lane);
     } else if (M == MARK) {
-      uint32_t u[VT];   // all neighbour loads in flight before the flag stores
+      uint32_t u[VT];   // all neighbour loads in flight before the flag stores / claims
 #pragma unroll
       for (int i = 0; i < VT; ++i) {
         const int k = i * 64 + lane;
@@ -787,11 +839,15 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
           u[i] = a.col[(uint64_t)sRs[s] + (b0 + k - (uint64_t)sEnd[s])];   // sEnd[s] = start of a0+s
         }
       }
-      // the previous tile's flags behind this tile's loads (see FINALD)
+      if (bp.lab) {
+        claim_append(u, bp, lane);
+      } else {
+        // the previous tile's flags behind this tile's loads (see FINALD)
 #pragma unroll
-      for (int i = 0; i < VT; ++i) {
-        if (pu[i] != NO_ROW) flags[pu[i]] = 1;
-        pu[i] = u[i];
+        for (int i = 0; i < VT; ++i) {
+          if (pu[i] != NO_ROW) flags[pu[i]] = 1;
+          pu[i] = u[i];
+        }
       }
     } else if (M == BFS) {
       uint32_t wv[VT];
@@ -1343,10 +1399,15 @@ Workspace* ws_create(uint64_t max_frontier, uint64_t nv, uint64_t e_max, hipStre
   M((void**)&w->frontier[1], w->cap_frontier * 4);
   M((void**)&w->seg_end, w->cap_frontier * 4);
   M((void**)&w->seg_rs, w->cap_frontier * 4);
+  M((void**)&w->seg_end1, w->cap_frontier * 4);
+  M((void**)&w->seg_rs1, w->cap_frontier * 4);
   M((void**)&w->rlist, w->cap_frontier * 4);
   M((void**)&w->flags, w->flag_bytes);
+  M((void**)&w->seen, (nv + 1) * 4);
   w->cap_tiles = cdiv(w->cap_frontier + e_max + 1, TILE) + 2;
   M((void**)&w->tsplit, w->cap_tiles * 4);
+  M((void**)&w->tsplit1, w->cap_tiles * 4);
+  w->mark_flags = getenv("NBG_MARK_FLAGS") && atoi(getenv("NBG_MARK_FLAGS")) != 0;
   // QState and the per-workgroup row counts are one allocation: one copy ends a query
   M((void**)&w->q, sizeof(QState) + (size_t)MAX_TYPES_Q * EXPAND_GRID * 4);
   M((void**)&w->d_prog, (size_t)MAX_TYPES_Q * MAX_PROGRAM * sizeof(Ins));
@@ -1361,6 +1422,7 @@ Workspace* ws_create(uint64_t max_frontier, uint64_t nv, uint64_t e_max, hipStre
   if (e == hipSuccess) e = hipHostMalloc((void**)&w->h_prog, (size_t)MAX_TYPES_Q * MAX_PROGRAM * sizeof(Ins),
                                          hipHostMallocDefault);
   if (e == hipSuccess) e = hipMemsetAsync(w->flags, 0, w->flag_bytes, s);
+  if (e == hipSuccess) e = hipMemsetAsync(w->seen, 0, (nv + 1) * 4, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
     if (err) *err = std::string("workspace allocation failed: ") + hipGetErrorString(e);
@@ -1373,6 +1435,7 @@ Workspace* ws_create(uint64_t max_frontier, uint64_t nv, uint64_t e_max, hipStre
 void ws_destroy(Workspace* w) {
   if (!w) return;
   for (void* p : {(void*)w->frontier[0], (void*)w->frontier[1], (void*)w->seg_end, (void*)w->seg_rs,
+                  (void*)w->seg_end1, (void*)w->seg_rs1, (void*)w->tsplit1, (void*)w->seen,
                   (void*)w->rlist, (void*)w->flags, (void*)w->tsplit,
                   (void*)w->q, (void*)w->rows,
                   (void*)w->d_row_cols, (void*)w->d_prog, (void*)w->dtab, (void*)w->dkeep, (void*)w->dseg,
@@ -1480,7 +1543,12 @@ struct ListRef {
   const uint32_t* ids;
   const unsigned long long* acc;
   unsigned long long* stat_n;      // the expansion records |F_s| (its list is the whole frontier)
+  int set;                         // edge-space set the list's seg_end / seg_rs / tsplit live in
 };
+
+static uint32_t* set_end(Workspace* w, int set) { return set ? w->seg_end1 : w->seg_end; }
+static uint32_t* set_rs(Workspace* w, int set) { return set ? w->seg_rs1 : w->seg_rs; }
+static uint32_t* set_split(Workspace* w, int set) { return set ? w->tsplit1 : w->tsplit; }
 
 static DegSrc deg_of(const ExpandArgs& a) {
   DegSrc ds{};
@@ -1491,12 +1559,12 @@ static DegSrc deg_of(const ExpandArgs& a) {
 }
 
 static ListOut list_out(Workspace* w, uint32_t* ids, unsigned long long* acc, unsigned long long* zero_next,
-                        unsigned long long* stat_n) {
+                        unsigned long long* stat_n, int set = 0) {
   ListOut o{};
   o.ids = ids;
-  o.seg_end = w->seg_end;
-  o.seg_rs = w->seg_rs;
-  o.tsplit = w->tsplit;
+  o.seg_end = set_end(w, set);
+  o.seg_rs = set_rs(w, set);
+  o.tsplit = set_split(w, set);
   o.acc = acc;
   o.zero_next = zero_next;
   o.stat_n = stat_n;
@@ -1506,7 +1574,7 @@ static ListOut list_out(Workspace* w, uint32_t* ids, unsigned long long* acc, un
 static ListRef prepare_list(Workspace* w, const ExpandArgs& a, uint64_t n_bound, int step, int tix) {
   if (tix == 0 && w->seg_ready) {
     w->seg_ready = false;
-    return ListRef{w->frontier[w->cur], w->list_acc, &w->q->step_n[step]};
+    return ListRef{w->frontier[w->cur], w->list_acc, &w->q->step_n[step], w->cur};
   }
   unsigned long long* acc = &w->q->acc[w->pr];
   unsigned long long* other = &w->q->acc[w->pr ^ 1];
@@ -1516,9 +1584,9 @@ static ListRef prepare_list(Workspace* w, const ExpandArgs& a, uint64_t n_bound,
   hipEvent_t p = prof_begin(w, K_RELIST);
   hipLaunchKernelGGL(k_relist, dim3((unsigned)cdiv(n_bound ? n_bound : 1, RL_TILE)), dim3(BLOCK), 0, w->stream, in,
                      w->list_acc, 1, (uint32_t)w->start_n, w->inl, deg_of(a),
-                     list_out(w, w->rlist, acc, other, &w->q->step_n[step]), (unsigned long long*)nullptr);
+                     list_out(w, w->rlist, acc, other, &w->q->step_n[step], w->cur), (unsigned long long*)nullptr);
   prof_end(w, p, K_RELIST, step, tix);
-  return ListRef{w->rlist, acc, nullptr};
+  return ListRef{w->rlist, acc, nullptr, w->cur};
 }
 
 // workgroups of a k_expand launch: one wave per tile up to EXPAND_GRID workgroups (persistent)
@@ -1532,9 +1600,33 @@ static bool inline_start_list(const Workspace* w, int tix, const InlineList* il)
   return il && !(tix == 0 && w->seg_ready) && w->list_acc == nullptr && w->start_inline;
 }
 
+static DegSrc deg_src(const ExpandArgs* next0) { return next0 ? deg_of(*next0) : DegSrc{}; }
+
+hipError_t ws_compact(Workspace* w, int step, const ExpandArgs* next0);
+
 hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, uint64_t e_bound, int step, int tix,
-                          const InlineList* il) {
+                          const InlineList* il, const ExpandArgs* next0) {
   if (step > MAX_STEPS || tix >= MAX_TYPES_Q) return hipErrorInvalidValue;
+  // claim mode (single engine): the step's dst SET is claimed against a per-step stamp and the
+  // winners are appended, with their edge space over next0, straight to the next list (set
+  // cur ^ 1, accumulator slot 2 + (step + 1) % 3; this step's first launch zeroes the slot of
+  // step + 2, whose list (step - 1) nobody reads any more)
+  BfsParams bp{};
+  if (!w->comm && !w->mark_flags) {
+    if (tix == 0) {
+      if (++w->seen_stamp == 0) {   // wrap: clear the stamps once
+        HIP_TRY(hipMemsetAsync(w->seen, 0, (w->nv + 1) * 4, w->stream));
+        w->seen_stamp = 1;
+      }
+      w->step_stamp = w->seen_stamp;
+    }
+    bp.lab = w->seen;
+    bp.stamp = w->step_stamp;
+    const int nset = w->cur ^ 1;
+    bp.nds = deg_src(next0);
+    bp.nlist = list_out(w, w->frontier[nset], &w->q->acc[2 + (step + 1) % 3],
+                        tix == 0 ? &w->q->acc[2 + (step + 2) % 3] : nullptr, nullptr, nset);
+  }
   if (inline_start_list(w, tix, il)) {   // no k_relist: the list travels in the kernel arguments
     ExpandArgs a = a0;
     a.frontier = nullptr;
@@ -1543,31 +1635,39 @@ hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, 
     if (a.bt)
       hipLaunchKernelGGL((k_expand<MARKB, true>), dim3(expand_grid(il->n, il->total)), dim3(BLOCK), 0, w->stream, a,
                          (const unsigned long long*)nullptr, w->seg_end, w->seg_rs, w->flags, FinalParams{},
-                         BfsParams{}, &w->q->e_st[step][tix], &w->q->step_n[step], *il);
+                         bp, &w->q->e_st[step][tix], &w->q->step_n[step], *il);
     else
       hipLaunchKernelGGL((k_expand<MARK, true>), dim3(expand_grid(il->n, il->total)), dim3(BLOCK), 0, w->stream, a,
                          (const unsigned long long*)nullptr, w->seg_end, w->seg_rs, w->flags, FinalParams{},
-                         BfsParams{}, &w->q->e_st[step][tix], &w->q->step_n[step], *il);
+                         bp, &w->q->e_st[step][tix], &w->q->step_n[step], *il);
     prof_end(w, p, K_EXPAND_MARK, step, tix);
     return hipGetLastError();
   }
   const ListRef L = prepare_list(w, a0, n_bound, step, tix);
   ExpandArgs a = a0;
   a.frontier = L.ids;
-  a.tsplit = w->tsplit;
+  a.tsplit = set_split(w, L.set);
   FinalParams fp{};
   hipEvent_t p = prof_begin(w, K_EXPAND_MARK);
   if (a.bt)
     hipLaunchKernelGGL(k_expand<MARKB>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, L.acc,
-                       w->seg_end, w->seg_rs, w->flags, fp, BfsParams{}, &w->q->e_st[step][tix], L.stat_n, NoInline{});
+                       set_end(w, L.set), set_rs(w, L.set), w->flags, fp, bp, &w->q->e_st[step][tix], L.stat_n,
+                       NoInline{});
   else
     hipLaunchKernelGGL(k_expand<MARK>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, L.acc,
-                       w->seg_end, w->seg_rs, w->flags, fp, BfsParams{}, &w->q->e_st[step][tix], L.stat_n, NoInline{});
+                       set_end(w, L.set), set_rs(w, L.set), w->flags, fp, bp, &w->q->e_st[step][tix], L.stat_n,
+                       NoInline{});
   prof_end(w, p, K_EXPAND_MARK, step, tix);
   return hipGetLastError();
 }
 
-static DegSrc deg_src(const ExpandArgs* next0) { return next0 ? deg_of(*next0) : DegSrc{}; }
+hipError_t ws_finish_step(Workspace* w, int step, const ExpandArgs* next0) {
+  if (w->mark_flags) return ws_compact(w, step, next0);
+  w->cur ^= 1;
+  w->list_acc = &w->q->acc[2 + (step + 1) % 3];
+  w->seg_ready = next0 != nullptr;
+  return hipSuccess;
+}
 
 hipError_t ws_compact(Workspace* w, int step, const ExpandArgs* next0) {
   unsigned long long* acc = &w->q->acc[2 + w->pc];
@@ -1576,7 +1676,7 @@ hipError_t ws_compact(Workspace* w, int step, const ExpandArgs* next0) {
   uint32_t* next = w->frontier[w->cur ^ 1];
   hipEvent_t p = prof_begin(w, K_COMPACT);
   hipLaunchKernelGGL(k_compact, dim3((unsigned)(w->flag_bytes / CP_BYTES)), dim3(CP_THREADS), 0, w->stream, w->flags,
-                     deg_src(next0), list_out(w, next, acc, other, nullptr));
+                     deg_src(next0), list_out(w, next, acc, other, nullptr, w->cur ^ 1));
   prof_end(w, p, K_COMPACT, step, 0);
   w->cur ^= 1;
   w->list_acc = acc;
@@ -1684,10 +1784,12 @@ hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound,
                            const TypeProgram& prog, uint64_t region_base, uint64_t blk_cap, const InlineList* il) {
   if (step > MAX_STEPS || tix >= MAX_TYPES_Q) return hipErrorInvalidValue;
   const bool inl = inline_start_list(w, tix, il);
-  const ListRef L = inl ? ListRef{nullptr, nullptr, &w->q->step_n[step]} : prepare_list(w, a0, n_bound, step, tix);
+  const ListRef L = inl ? ListRef{nullptr, nullptr, &w->q->step_n[step], 0} : prepare_list(w, a0, n_bound, step, tix);
   ExpandArgs a = a0;
   a.frontier = L.ids;
-  a.tsplit = inl ? nullptr : w->tsplit;
+  a.tsplit = inl ? nullptr : set_split(w, L.set);
+  uint32_t* const l_end = set_end(w, L.set);
+  uint32_t* const l_rs = set_rs(w, L.set);
   FinalParams fp{};
   fp.prog = w->d_prog + (size_t)tix * MAX_PROGRAM;
   fp.where_len = prog.where_len;
@@ -1715,22 +1817,22 @@ hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound,
   unsigned long long* e_st = &w->q->e_st[step][tix];
   if (inl) {
     if (dst_only)
-      hipLaunchKernelGGL((k_expand<FINALD, true>), grid, dim3(BLOCK), 0, w->stream, a, L.acc, w->seg_end, w->seg_rs,
+      hipLaunchKernelGGL((k_expand<FINALD, true>), grid, dim3(BLOCK), 0, w->stream, a, L.acc, l_end, l_rs,
                          w->flags, fp, BfsParams{}, e_st, L.stat_n, *il);
     else if (fp.fast.enabled)
-      hipLaunchKernelGGL((k_expand<FINALF, true>), grid, dim3(BLOCK), 0, w->stream, a, L.acc, w->seg_end, w->seg_rs,
+      hipLaunchKernelGGL((k_expand<FINALF, true>), grid, dim3(BLOCK), 0, w->stream, a, L.acc, l_end, l_rs,
                          w->flags, fp, BfsParams{}, e_st, L.stat_n, *il);
     else
-      hipLaunchKernelGGL((k_expand<FINAL, true>), grid, dim3(BLOCK), lds, w->stream, a, L.acc, w->seg_end, w->seg_rs,
+      hipLaunchKernelGGL((k_expand<FINAL, true>), grid, dim3(BLOCK), lds, w->stream, a, L.acc, l_end, l_rs,
                          w->flags, fp, BfsParams{}, e_st, L.stat_n, *il);
   } else if (dst_only) {
-    hipLaunchKernelGGL(k_expand<FINALD>, grid, dim3(BLOCK), 0, w->stream, a, L.acc, w->seg_end, w->seg_rs, w->flags,
+    hipLaunchKernelGGL(k_expand<FINALD>, grid, dim3(BLOCK), 0, w->stream, a, L.acc, l_end, l_rs, w->flags,
                        fp, BfsParams{}, e_st, L.stat_n, NoInline{});
   } else if (fp.fast.enabled) {
-    hipLaunchKernelGGL(k_expand<FINALF>, grid, dim3(BLOCK), 0, w->stream, a, L.acc, w->seg_end, w->seg_rs, w->flags,
+    hipLaunchKernelGGL(k_expand<FINALF>, grid, dim3(BLOCK), 0, w->stream, a, L.acc, l_end, l_rs, w->flags,
                        fp, BfsParams{}, e_st, L.stat_n, NoInline{});
   } else {
-    hipLaunchKernelGGL(k_expand<FINAL>, grid, dim3(BLOCK), lds, w->stream, a, L.acc, w->seg_end, w->seg_rs, w->flags,
+    hipLaunchKernelGGL(k_expand<FINAL>, grid, dim3(BLOCK), lds, w->stream, a, L.acc, l_end, l_rs, w->flags,
                        fp, BfsParams{}, e_st, L.stat_n, NoInline{});
   }
   prof_end(w, p, K_EXPAND_FINAL, step, tix, (double)edge_columns_read(prog), (double)fp.nyields);
@@ -1940,7 +2042,7 @@ hipError_t ws_exchange(Workspace* w, int step, const ExpandArgs* next0) {
   w->pc ^= 1;
   p = prof_begin(w, K_BITS_COMPACT);
   hipLaunchKernelGGL(k_bits_compact, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->recvbits, (int)G, seg_words,
-                     w->nv, deg_src(next0), list_out(w, w->frontier[w->cur ^ 1], acc, other, nullptr));
+                     w->nv, deg_src(next0), list_out(w, w->frontier[w->cur ^ 1], acc, other, nullptr, w->cur ^ 1));
   prof_end(w, p, K_BITS_COMPACT, step, 0);
   w->cur ^= 1;
   w->list_acc = acc;

@@ -221,7 +221,8 @@ struct QState {
   unsigned long long n;                // current frontier size
   unsigned long long total;            // edges of the current (step, type) expansion
   unsigned long long err;              // WHERE/YIELD evaluation error
-  unsigned long long acc[4];           // packed list sizes (entries << 32 | edges): relist 0/1, compaction 2/3
+  unsigned long long acc[5];           // packed list sizes (entries << 32 | edges): relist 0/1,
+                                       // step lists 2..4 (compaction ping-pong 2/3, claim lists rotate 2..4)
   unsigned long long step_n[MAX_STEPS + 2];              // frontier size entering step s
   unsigned long long e_st[MAX_STEPS + 2][MAX_TYPES_Q];   // edges per (step, type)
   // $$ holder semantics (GoExecutor::VertexHolder, GoExecutor.cpp:986-1064): bit t = some final
@@ -289,6 +290,32 @@ struct PathTypes {                   // the CSRs one search direction expands (o
   int32_t type[MAX_TYPES_Q];
   ExpandArgs a[MAX_TYPES_Q];
 };
+
+// ----------------------------------------------------------------------------- one-pair FIND SHORTEST PATH (sp.hip)
+struct SpTypes {                     // the CSRs one search direction expands (OVER order)
+  int n = 0;
+  int32_t type[MAX_TYPES_Q];
+  const uint32_t* row_ptr[MAX_TYPES_Q];
+  const uint32_t* col[MAX_TYPES_Q];
+  const int64_t* dst_vid[MAX_TYPES_Q];
+  const int64_t* rank[MAX_TYPES_Q];
+};
+struct SpResult {                    // one query's result block (device, copied to pinned memory)
+  unsigned long long L;              // path length, 0 = no path within UPTO
+  unsigned long long edges;          // BFS adjacency entries scanned (both sides)
+  unsigned long long err;            // 1 reconstruction failure, 2 spin bound, 3 list overflow
+  unsigned long long levels;         // BFS levels run
+  long long path[1 + 3 * MAX_PATH_LEN];   // [v0, t0, r0, v1, ...]
+};
+struct SpCtx;                        // labels, item lists, control block, result block of one slot
+// item_cap: items a list may hold = sum over a side's types of (nv + E_t / 64), plus slack
+SpCtx* sp_create(uint64_t nv, uint64_t item_cap, hipStream_t s, std::string* err);
+void sp_destroy(SpCtx* c);
+// enqueue the persistent search for s -> t (local dense ids, s != t) and its result copy
+hipError_t sp_launch(SpCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible, const int64_t* vids,
+                     uint32_t s, uint32_t t, uint32_t upto);
+bool sp_ready(SpCtx* c);
+hipError_t sp_wait(SpCtx* c, SpResult* out);
 
 // ----------------------------------------------------------------------------- collectives (comm.cpp)
 // Transport of the partitioned engine.  Methods return 0 on success; `last` holds the error.
@@ -369,13 +396,14 @@ const uint32_t* ws_current_frontier(Workspace* w);
 // Query pipeline (all asynchronous on the workspace stream until ws_end_query):
 hipError_t ws_begin_query(Workspace* w, const uint32_t* starts, uint64_t n, const std::vector<TypeProgram>* progs,
                           uint64_t stmt_id);
-// steps 1..N-1, per OVER type: scan + expand into next-frontier flags
-// il: the start list's inline form for this type (used when the list is the query's start list)
+// steps 1..N-1, per OVER type: scan + expand into the next frontier.  Single engine: every new
+// neighbour is CLAIMED against a per-step stamp and appended to the next list (with its edge
+// space over next0 = the first OVER type's CSR of step + 1); partitioned: byte flags over the
+// global id space for ws_exchange.  il: the start list's inline form for this type.
 hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a, uint64_t n_bound, uint64_t e_bound, int step, int tix,
-                          const InlineList* il = nullptr);
-// after all types of a step: flags -> next frontier
-// next0: the first OVER type's CSR of step + 1 (its degree pass is fused into the compaction)
-hipError_t ws_compact(Workspace* w, int step, const ExpandArgs* next0);
+                          const InlineList* il, const ExpandArgs* next0);
+// after all types of a non-final step (single engine): the claimed list becomes the frontier
+hipError_t ws_finish_step(Workspace* w, int step, const ExpandArgs* next0);
 // step N, per OVER type: scan + WHERE/YIELD + sharded row emission into [region_base, +NSHARD*shard_cap)
 hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a, uint64_t n_bound, uint64_t e_bound, int step, int tix,
                            const TypeProgram& prog, uint64_t region_base, uint64_t blk_cap, const InlineList* il = nullptr);

@@ -36,6 +36,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
+#include <string>
 #include <unordered_set>
 
 #include "engine.h"
@@ -242,6 +243,45 @@ int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_pat
   if (rc) return rc;
   out->paths.push_back(std::move(p));
   return NBG_OK;
+}
+
+// One (s, t) pair on a single engine: the persistent device search (sp.hip) — one launch, one
+// result copy, one host wait.
+SpTypes sp_types(const PathTypes& pt) {
+  SpTypes T{};
+  T.n = pt.n;
+  for (int k = 0; k < pt.n; ++k) {
+    T.type[k] = pt.type[k];
+    T.row_ptr[k] = pt.a[k].row_ptr;
+    T.col[k] = pt.a[k].col;
+    T.dst_vid[k] = pt.a[k].dst_vid;
+    T.rank[k] = pt.a[k].rank;
+  }
+  return T;
+}
+
+int32_t device_pair(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_paths* out) {
+  Engine& E = c.E;
+  if (!E.sp) {
+    std::string err;
+    E.sp = sp_create(E.snap.nv, E.sp_item_cap(), E.stream, &err);
+    if (!E.sp) return E.fail(NBG_E_OUT_OF_MEMORY, err);
+  }
+  if (!host_degree(c, c.fwd, s) || !host_degree(c, c.bwd, t)) return NBG_OK;   // an endpoint without edges
+  hipError_t he = sp_launch(E.sp, sp_types(c.fwd), sp_types(c.bwd), E.snap.d_visible, E.snap.d_vids, s, t, upto);
+  SpResult r;
+  if (he == hipSuccess) he = sp_wait(E.sp, &r);
+  if (he != hipSuccess) return dev_fail(E, he, "shortest path");
+  if (r.err == 1) return E.fail(NBG_E_UNKNOWN, "shortest-path reconstruction failed (in/out edges disagree)");
+  if (r.err) return E.fail(NBG_E_DEVICE, "shortest path: device search aborted (code " + std::to_string(r.err) + ")");
+  c.edges += r.edges;
+  if (r.L) out->paths.emplace_back(r.path, r.path + 1 + 3 * r.L);
+  return NBG_OK;
+}
+
+bool sp_legacy() {
+  static const bool v = getenv("NBG_SP_LEGACY") && atoi(getenv("NBG_SP_LEGACY")) != 0;
+  return v;
 }
 
 // S: this rank's sources (local ids); Tg: every target, by global position, as a local id
@@ -457,6 +497,13 @@ extern "C" int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* rq, nbg_
     add(c.bwd, -t);
   }
   const bool pair = rq->shortest && Sv.size() == 1 && Tv.size() == 1 && Sv[0] != Tv[0];
+  if (pair && !c.part && !sp_legacy()) {
+    int32_t rc = device_pair(c, S.empty() ? NO_ROW : S[0], Tg[0], rq->upto, res);
+    if (rc) { delete res; return rc; }
+    res->edges = c.edges;
+    *out = res;
+    return NBG_OK;
+  }
   hipError_t he = ws_path_begin(c.ws, 0, E.snap.nv + S.size() + Tg.size() + 1024, !(pair && !c.part));
   if (he != hipSuccess) { delete res; return dev_fail(E, he, "path workspace"); }
   int32_t rc;

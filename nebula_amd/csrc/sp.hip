@@ -1,0 +1,703 @@
+// FIND SHORTEST PATH for one (source, target) pair in ONE persistent launch (single engine).
+//
+// Same semantics and result as path.cpp's bidirectional search (FindPathExecutor.cpp:145-411
+// restated: minimal hop count, UPTO N, one path per target, ties broken by the lexicographically
+// smallest entry list [v0, t0, r0, v1, ...]), but the level loop, the direction choice, the
+// meet / termination tests, the B-set recovery and the greedy reconstruction all run on the
+// device: the host enqueues one launch and one copy of the result block per pair, and waits once.
+//
+// Work is cut into ITEMS — runs of <= 64 consecutive CSR entries of one OVER type — produced
+// when a vertex is claimed (its edges over the side's CSRs, split into 64-entry runs), so every
+// level is a flat list of equal-sized items: a wave takes SP_U items per iteration, lane l owns
+// entry l of each, and hubs spread over all waves with no merge-path pass and no degree scan.
+//
+// Workgroup 0 is the leader: it runs every small phase (<= SP_SMALL items) alone, and for a big
+// phase publishes the phase parameters (agent-scope release, then the generation word) so that
+// every workgroup takes its share; followers poll the generation word (sc1 loads + s_sleep),
+// acquire, work, release and arrive on a counter the leader waits for.  Every spin is bounded
+// (SpCtl::err = 2 and all workgroups leave).  Labels are epoch-stamped (epoch << LVL_BITS |
+// level) like path.cpp's, read with agent-scope loads (sc1: the L1 may hold a stale line of a
+// label another workgroup or an earlier phase claimed) and claimed with CAS.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+
+#include "nbg_internal.h"
+
+#define HIP_TRY_SP(x)                     \
+  do {                                    \
+    hipError_t e_ = (x);                  \
+    if (e_ != hipSuccess) return e_;      \
+  } while (0)
+
+namespace nbg {
+namespace {
+
+constexpr int SP_THREADS = 256;
+constexpr int SP_WAVES = SP_THREADS / 64;
+constexpr int SP_U = 4;                 // items per wave iteration (their loads in flight together)
+constexpr uint32_t SP_CH = 64;          // CSR entries per item
+constexpr uint64_t SP_SMALL = 96;       // a phase with at most this many items runs on the leader alone
+constexpr uint32_t SP_GREEDY_SMALL = 4096;   // greedy hop: adjacency the leader scans alone
+constexpr int SP_MAX_WGS = 256;
+
+enum SpOp : uint32_t { OP_LEVEL = 1, OP_BSET = 2, OP_GREEDY = 3, OP_EXIT = 4 };
+enum SpList : int { L_F0 = 0, L_F1 = 1, L_B0 = 2, L_B1 = 3, L_M0 = 4, L_M1 = 5, SP_NLISTS = 6 };
+
+}  // namespace
+
+// Device control block of one persistent query (zeroed once; per-query words reset by the leader).
+struct SpCtl {
+  unsigned long long gen;          // released phase: (q << 24) | phase
+  unsigned long long arrive;       // follower arrivals (reset at query start)
+  unsigned long long err;          // 1 reconstruction failure, 2 spin bound hit, 3 list overflow
+  // phase parameters (leader writes, releases, bumps gen)
+  unsigned long long op, side, src, n, dst, pos, cur, stamp, mstamp;
+  // phase accumulators (leader zeroes before the phase)
+  unsigned long long out_n, dsum, meet_n, meet_items, edges;
+  unsigned long long gpart[4 * SP_MAX_WGS];   // greedy: per-workgroup minimum (type, rank, vid, dense)
+};
+
+struct SpArgs {
+  SpTypes fwd, bwd;
+  const uint8_t* visible;
+  const int64_t* vids;
+  uint32_t s, t, upto;
+  uint32_t* lab_f;
+  uint32_t* lab_b;
+  uint32_t* lab_m;
+  uint32_t ef, eb, em;             // this query's epochs
+  uint64_t* list[SP_NLISTS];
+  uint64_t list_cap;
+  SpCtl* ctl;
+  SpResult* res;
+  unsigned long long q;            // query sequence number (generation encoding)
+  unsigned long long spin_limit;
+};
+
+namespace {
+
+__device__ __forceinline__ uint32_t ld1(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld1(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st1(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st1(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint32_t stamp_of(uint32_t epoch, uint32_t level) { return (epoch << LVL_BITS) | level; }
+__device__ __forceinline__ bool live(uint32_t lab, uint32_t epoch) { return (lab >> LVL_BITS) == epoch; }
+
+// item: [j0:32][len-1:8][type index:8]
+__device__ __forceinline__ uint64_t item_make(uint32_t j0, uint32_t len, uint32_t t) {
+  return ((uint64_t)j0 << 32) | ((uint64_t)(len - 1) << 8) | t;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+// Items of vertex x over a side's CSRs (visible vertices only): count and edge total.
+__device__ __forceinline__ void vertex_items(const SpTypes& T, const uint8_t* visible, uint32_t x, uint32_t* nitems,
+                                             uint32_t* nedges) {
+  uint32_t ni = 0, ne = 0;
+  if (x != NO_ROW && (!visible || visible[x])) {
+    for (int t = 0; t < T.n; ++t) {
+      const uint32_t d = T.row_ptr[t][x + 1] - T.row_ptr[t][x];
+      ni += (d + SP_CH - 1) / SP_CH;
+      ne += d;
+    }
+  }
+  *nitems = ni;
+  *nedges = ne;
+}
+
+// Writes items [first, total) step `stride` of vertex x over T at out[base + k]: item k is the
+// k-th 64-entry run of x's rows, types in OVER order.
+__device__ __forceinline__ void write_items(const SpTypes& T, uint32_t x, uint64_t* out, uint64_t base, uint32_t first,
+                                            uint32_t stride, uint32_t total) {
+  for (uint32_t k = first; k < total; k += stride) {
+    uint32_t kk = k, rs = 0, re = 0;
+    int t = 0;
+    for (; t < T.n; ++t) {
+      rs = T.row_ptr[t][x];
+      re = T.row_ptr[t][x + 1];
+      const uint32_t ni = (re - rs + SP_CH - 1) / SP_CH;
+      if (kk < ni) break;
+      kk -= ni;
+    }
+    const uint32_t j0 = rs + kk * SP_CH;
+    const uint32_t len = re - j0 < SP_CH ? re - j0 : SP_CH;
+    out[base + k] = item_make(j0, len, (uint32_t)t);
+  }
+}
+
+// Appends, for every lane with want != 0, vertex x's items over T to list `out` (counter *n):
+// one returning atomic per wave; vertices with many items are written by the whole wave.
+__device__ __forceinline__ void wave_append(const SpTypes& T, uint32_t x, bool want, uint32_t nitems, uint64_t* out,
+                                            unsigned long long* n, uint64_t cap, unsigned long long* err) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t c = want ? nitems : 0;
+  const uint32_t inc = wave_incl_scan32(c);
+  const uint32_t tot = __shfl(inc, 63, 64);
+  if (!tot) return;
+  unsigned long long base = 0;
+  if (lane == 0) base = atomicAdd(n, (unsigned long long)tot);
+  base = __shfl(base, 0, 64);
+  if (base + tot > cap) {
+    if (lane == 0) atomicOr(err, 3ull);
+    return;
+  }
+  const uint64_t mine = base + inc - c;
+  const bool big = c > 8;
+  if (c && !big) write_items(T, x, out, mine, 0, 1, c);
+  unsigned long long bm = __ballot(big);
+  while (bm) {   // hubs: the whole wave writes their items
+    const int l = __ffsll((long long)bm) - 1;
+    bm &= bm - 1;
+    const uint32_t hx = __shfl(x, l, 64);
+    const uint64_t hb = __shfl(mine, l, 64);
+    const uint32_t hc = __shfl(c, l, 64);
+    write_items(T, hx, out, hb, (uint32_t)lane, 64, hc);
+  }
+}
+
+struct LevelCfg {
+  const SpTypes* T;          // CSRs expanded (side's direction)
+  const SpTypes* N;          // CSRs of the claimed vertices' items (next level of the same side)
+  const SpTypes* M;          // CSRs of a meet vertex's B-set items (in-edges)
+  uint32_t* lab;             // claimed label
+  uint32_t epoch, stamp;
+  bool exact;                // already claimed = lab == stamp (B-sets: one LAB_M epoch, many positions)
+  const uint32_t* rlab;      // restriction (B-set): claim u only if rlab[u] == rstamp
+  uint32_t rstamp;
+  const uint32_t* olab;      // other side's labels (meet test), nullable
+  uint32_t oepoch;
+  uint32_t mstamp;           // LAB_M stamp of a meet vertex
+  bool append;               // append the claimed vertices' items (N) to dst
+};
+
+// One phase over the items of list `src` (n items): this workgroup's share of the waves
+// [wg * SP_WAVES, (wg + 1) * SP_WAVES) out of nwg * SP_WAVES.
+__device__ void run_level(const SpArgs& A, const LevelCfg& C, const uint64_t* src, uint64_t n, uint64_t* dst,
+                          int wg, int nwg) {
+  SpCtl* ctl = A.ctl;
+  const int lane = threadIdx.x & 63;
+  const uint64_t gw = (uint64_t)wg * SP_WAVES + (threadIdx.x >> 6);
+  const uint64_t NW = (uint64_t)nwg * SP_WAVES;
+  unsigned long long edges = 0, dsum = 0;
+  for (uint64_t i0 = gw * SP_U; i0 < n; i0 += NW * SP_U) {
+    uint64_t it = 0;
+    if (lane < SP_U && i0 + lane < n) it = src[i0 + lane];
+    uint32_t x[SP_U];
+#pragma unroll
+    for (int u = 0; u < SP_U; ++u) {
+      const uint64_t iu = __shfl(it, u, 64);
+      x[u] = NO_ROW;
+      if (i0 + u < n) {
+        const uint32_t j0 = (uint32_t)(iu >> 32), len = (uint32_t)((iu >> 8) & 0xFF) + 1, t = (uint32_t)(iu & 0xFF);
+        if ((uint32_t)lane < len) {
+          x[u] = C.T->col[t][(uint64_t)j0 + lane];
+          ++edges;
+        }
+      }
+    }
+    uint32_t claimed = 0, meet = 0;
+#pragma unroll
+    for (int u = 0; u < SP_U; ++u) {
+      const uint32_t w = x[u];
+      if (w == NO_ROW) continue;
+      if (C.rlab && ld1(C.rlab + w) != C.rstamp) continue;
+      const uint32_t old = ld1(C.lab + w);
+      if (C.exact ? old == C.stamp : live(old, C.epoch)) continue;
+      if (atomicCAS(C.lab + w, old, C.stamp) != old) continue;
+      claimed |= 1u << u;
+      if (C.olab && live(ld1(C.olab + w), C.oepoch)) meet |= 1u << u;
+    }
+#pragma unroll
+    for (int u = 0; u < SP_U; ++u) {
+      const bool cl = (claimed >> u) & 1u, mt = (meet >> u) & 1u;
+      uint32_t ni = 0, ne = 0;
+      if (cl && C.append) vertex_items(*C.N, A.visible, x[u], &ni, &ne);
+      dsum += ne;
+      if (C.append) wave_append(*C.N, x[u], cl, ni, dst, &ctl->out_n, A.list_cap, &ctl->err);
+      if (C.olab && __ballot(mt)) {
+        uint32_t mi = 0, me = 0;
+        if (mt) {
+          st1(A.lab_m + x[u], C.mstamp);
+          vertex_items(*C.M, A.visible, x[u], &mi, &me);
+        }
+        const unsigned long long mb = __ballot(mt);
+        if (lane == 0) atomicAdd(&ctl->meet_n, (unsigned long long)__popcll(mb));
+        wave_append(*C.M, x[u], mt, mi, A.list[L_M0], &ctl->meet_items, A.list_cap, &ctl->err);
+      }
+    }
+  }
+  // wave totals: one atomic each
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    edges += __shfl_xor(edges, o, 64);
+    dsum += __shfl_xor(dsum, o, 64);
+  }
+  if (lane == 0) {
+    if (edges) atomicAdd(&ctl->edges, edges);
+    if (dsum) atomicAdd(&ctl->dsum, dsum);
+  }
+}
+
+struct Cand {
+  int64_t t, r, v;
+  uint32_t d;
+};
+__device__ __forceinline__ bool cand_less(const Cand& a, const Cand& b) {
+  if (a.t != b.t) return a.t < b.t;
+  if (a.r != b.r) return a.r < b.r;
+  return a.v < b.v;
+}
+
+// Greedy hop `pos` from vertex c: the minimum (type, rank, dst vid) out-edge into B[pos + 1].
+__device__ Cand greedy_scan(const SpArgs& A, uint32_t c, int pos, int L, int kf, int wg, int nwg, Cand* lds) {
+  const Cand none{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
+  Cand best = none;
+  const uint32_t want_m = stamp_of(A.em, (uint32_t)(pos + 1));
+  const uint32_t want_b = stamp_of(A.eb, (uint32_t)(L - pos - 1));
+  const bool by_m = pos + 1 <= kf;
+  if (c != NO_ROW && (!A.visible || A.visible[c])) {
+    const uint64_t g = (uint64_t)wg * SP_THREADS + threadIdx.x, G = (uint64_t)nwg * SP_THREADS;
+    for (int t = 0; t < A.fwd.n; ++t) {
+      const uint32_t rs = A.fwd.row_ptr[t][c], re = A.fwd.row_ptr[t][c + 1];
+      for (uint64_t j = rs + g; j < re; j += G) {
+        const uint32_t w = A.fwd.col[t][j];
+        if (w == NO_ROW) continue;
+        const bool ok = by_m ? ld1(A.lab_m + w) == want_m : ld1(A.lab_b + w) == want_b;
+        if (!ok) continue;
+        Cand x{(int64_t)A.fwd.type[t], A.fwd.rank[t] ? A.fwd.rank[t][j] : 0, A.fwd.dst_vid[t][j], w};
+        if (cand_less(x, best)) best = x;
+      }
+    }
+  }
+  // block minimum
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Cand x;
+    x.t = __shfl_down(best.t, o, 64);
+    x.r = __shfl_down(best.r, o, 64);
+    x.v = __shfl_down(best.v, o, 64);
+    x.d = __shfl_down(best.d, o, 64);
+    if ((threadIdx.x & 63) + o < 64 && cand_less(x, best)) best = x;
+  }
+  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < SP_WAVES; ++i)
+      if (cand_less(lds[i], best)) best = lds[i];
+    lds[SP_WAVES] = best;
+  }
+  __syncthreads();
+  best = lds[SP_WAVES];
+  __syncthreads();
+  return best;
+}
+
+// ---------------------------------------------------------------- leader / follower protocol
+// every storing wave drained, the workgroup joined, then one lane's agent release
+__device__ __forceinline__ void wg_release() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+__device__ __forceinline__ void wg_acquire() {
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+struct PhaseView {   // the leader's phase parameters, as every workgroup reads them
+  uint32_t op, side, src, dst, pos, cur;
+  uint64_t n;
+  uint32_t stamp, mstamp;
+  uint32_t L, kf;
+};
+
+__device__ void run_phase(const SpArgs& A, const PhaseView& P, int wg, int nwg, Cand* lds) {
+  if (P.op == OP_LEVEL) {
+    LevelCfg C{};
+    const bool fw = P.side == 0;
+    C.T = fw ? &A.fwd : &A.bwd;
+    C.N = C.T;
+    C.M = &A.bwd;
+    C.lab = fw ? A.lab_f : A.lab_b;
+    C.epoch = fw ? A.ef : A.eb;
+    C.stamp = P.stamp;
+    C.olab = fw ? A.lab_b : A.lab_f;
+    C.oepoch = fw ? A.eb : A.ef;
+    C.mstamp = P.mstamp;
+    C.append = true;
+    run_level(A, C, A.list[P.src], P.n, A.list[P.dst], wg, nwg);
+  } else if (P.op == OP_BSET) {
+    // B[pos] from B[pos + 1] through in-edges, restricted to forward level pos, claimed in LAB_M
+    LevelCfg C{};
+    C.T = &A.bwd;
+    C.N = &A.bwd;
+    C.lab = A.lab_m;
+    C.exact = true;
+    C.stamp = P.stamp;
+    C.rlab = A.lab_f;
+    C.rstamp = stamp_of(A.ef, P.pos);
+    C.append = P.pos >= 2;   // B[1]'s in-edges are not needed (B[0] = {s})
+    run_level(A, C, A.list[P.src], P.n, A.list[P.dst], wg, nwg);
+  } else if (P.op == OP_GREEDY) {
+    Cand b = greedy_scan(A, P.cur, (int)P.pos, (int)P.L, (int)P.kf, wg, nwg, lds);
+    if (threadIdx.x == 0) {
+      unsigned long long* part = A.ctl->gpart + 4 * wg;
+      part[0] = (unsigned long long)b.t;
+      part[1] = (unsigned long long)b.r;
+      part[2] = (unsigned long long)b.v;
+      part[3] = b.d;
+    }
+  }
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(SP_THREADS) k_sp_pair(SpArgs A) {
+  __shared__ PhaseView sP;
+  __shared__ Cand lds[SP_WAVES + 1];
+  __shared__ int sQuit;
+  SpCtl* ctl = A.ctl;
+  const unsigned long long g0 = A.q << 24;
+  const int nwg = gridDim.x;
+  if (blockIdx.x != 0) {
+    // ------------------------------------------------ follower
+    unsigned long long seen = g0;
+    for (;;) {
+      if (threadIdx.x == 0) {
+        unsigned long long g = ld1(&ctl->gen);
+        unsigned long long spins = 0;
+        while (g == seen || g < g0) {   // (< g0: a generation of an earlier query)
+          if (++spins > A.spin_limit) { atomicOr(&ctl->err, 2ull); g = 0; break; }
+          __builtin_amdgcn_s_sleep(2);
+          g = ld1(&ctl->gen);
+        }
+        sQuit = g == 0;
+        seen = g;
+      }
+      __syncthreads();
+      if (sQuit) return;
+      wg_acquire();
+      if (threadIdx.x == 0) {
+        sP.op = (uint32_t)ctl->op;
+        sP.side = (uint32_t)ctl->side;
+        sP.src = (uint32_t)ctl->src;
+        sP.n = ctl->n;
+        sP.dst = (uint32_t)ctl->dst;
+        sP.pos = (uint32_t)ctl->pos;
+        sP.cur = (uint32_t)ctl->cur;
+        sP.stamp = (uint32_t)ctl->stamp;
+        sP.mstamp = (uint32_t)ctl->mstamp;
+        sP.L = (uint32_t)(ctl->mstamp >> 32);
+        sP.kf = (uint32_t)(ctl->stamp >> 32);
+      }
+      __syncthreads();
+      const PhaseView P = sP;
+      if (P.op == OP_EXIT) return;
+      run_phase(A, P, (int)blockIdx.x, nwg, lds);
+      wg_release();
+      if (threadIdx.x == 0) atomicAdd(&ctl->arrive, 1ull);
+      __syncthreads();
+    }
+  }
+  // -------------------------------------------------- leader
+  __shared__ unsigned long long sAcc[6];
+  unsigned long long phase = 0, big_phases = 0;
+  bool failed = false;
+  // run one phase: alone when small, else published to every workgroup
+  auto phase_run = [&](PhaseView P, bool big) {
+    if (threadIdx.x == 0) {
+      st1(&ctl->out_n, 0ull);
+      st1(&ctl->dsum, 0ull);
+      st1(&ctl->meet_n, 0ull);
+      st1(&ctl->meet_items, 0ull);
+      st1(&ctl->edges, 0ull);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (big && nwg > 1 && !failed) {
+      if (threadIdx.x == 0) {
+        ctl->op = P.op;
+        ctl->side = P.side;
+        ctl->src = P.src;
+        ctl->n = P.n;
+        ctl->dst = P.dst;
+        ctl->pos = P.pos;
+        ctl->cur = P.cur;
+        ctl->stamp = ((unsigned long long)P.kf << 32) | P.stamp;
+        ctl->mstamp = ((unsigned long long)P.L << 32) | P.mstamp;
+      }
+      wg_release();
+      if (threadIdx.x == 0) st1(&ctl->gen, g0 | ++phase);
+      __syncthreads();
+      run_phase(A, P, 0, nwg, lds);
+      ++big_phases;
+      if (threadIdx.x == 0) {
+        const unsigned long long want = big_phases * (unsigned long long)(nwg - 1);
+        unsigned long long spins = 0;
+        while (ld1(&ctl->arrive) < want) {
+          if (++spins > A.spin_limit) { atomicOr(&ctl->err, 2ull); break; }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __syncthreads();
+      wg_acquire();
+    } else {
+      run_phase(A, P, 0, 1, lds);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      sAcc[0] = ld1(&ctl->out_n);
+      sAcc[1] = ld1(&ctl->dsum);
+      sAcc[2] = ld1(&ctl->meet_n);
+      sAcc[3] = ld1(&ctl->meet_items);
+      sAcc[4] = ld1(&ctl->edges);
+      sAcc[5] = ld1(&ctl->err);
+    }
+    __syncthreads();
+    failed = failed || sAcc[5] != 0;
+  };
+
+  // ---- set-up: labels of s and t, their items
+  if (threadIdx.x == 0) {
+    st1(&ctl->arrive, 0ull);
+    st1(&ctl->err, 0ull);
+    st1(&ctl->out_n, 0ull);
+    st1(&ctl->meet_items, 0ull);
+    A.res->L = 0;
+    A.res->edges = 0;
+    A.res->err = 0;
+    A.res->levels = 0;
+  }
+  __syncthreads();
+  uint32_t nis = 0, nes = 0, nit = 0, net = 0;
+  if (threadIdx.x == 0) {
+    st1(A.lab_f + A.s, stamp_of(A.ef, 0));
+    st1(A.lab_b + A.t, stamp_of(A.eb, 0));
+  }
+  vertex_items(A.fwd, A.visible, A.s, &nis, &nes);
+  vertex_items(A.bwd, A.visible, A.t, &nit, &net);
+  if (threadIdx.x < 64) {   // wave 0 writes both item lists
+    write_items(A.fwd, A.s, A.list[L_F0], 0, (uint32_t)threadIdx.x, 64, nis);
+    write_items(A.bwd, A.t, A.list[L_B0], 0, (uint32_t)threadIdx.x, 64, nit);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  uint64_t nF = nis, nB = nit, dsf = nes, dsb = net, edges = 0;
+  int fcur = L_F0, bcur = L_B0, kf = 0, kb = 0;
+  bool met = false;
+  uint64_t n_meet_items = 0;
+  int levels = 0;
+  if (dsf && dsb) {
+    while ((uint32_t)(kf + kb) < A.upto && !failed) {
+      const bool fw = dsf <= dsb;
+      PhaseView P{};
+      P.op = OP_LEVEL;
+      P.side = fw ? 0 : 1;
+      P.src = (uint32_t)(fw ? fcur : bcur);
+      P.dst = P.src ^ 1u;
+      P.n = fw ? nF : nB;
+      P.stamp = fw ? stamp_of(A.ef, (uint32_t)kf + 1) : stamp_of(A.eb, (uint32_t)kb + 1);
+      P.mstamp = stamp_of(A.em, fw ? (uint32_t)kf + 1 : (uint32_t)kf);
+      phase_run(P, P.n > SP_SMALL);
+      ++levels;
+      edges += sAcc[4];
+      if (fw) { fcur ^= 1; nF = sAcc[0]; dsf = sAcc[1]; ++kf; }
+      else { bcur ^= 1; nB = sAcc[0]; dsb = sAcc[1]; ++kb; }
+      if (sAcc[2]) { met = true; n_meet_items = sAcc[3]; break; }
+      if (sAcc[0] == 0) break;   // a side has no further edges: no path
+    }
+  }
+  const int L = kf + kb;
+  bool ok = met && !failed;
+  // ---- B-sets over the forward positions kf - 1 .. 1 (B[kf] = the meet set, stamped at meet)
+  int mcur = L_M0;
+  uint64_t nM = n_meet_items;
+  for (int i = kf - 1; ok && i >= 1; --i) {
+    PhaseView P{};
+    P.op = OP_BSET;
+    P.src = (uint32_t)mcur;
+    P.dst = (uint32_t)(mcur == L_M0 ? L_M1 : L_M0);
+    P.n = nM;
+    P.pos = (uint32_t)i;
+    P.stamp = stamp_of(A.em, (uint32_t)i);
+    phase_run(P, P.n > SP_SMALL);
+    mcur = (int)P.dst;
+    nM = sAcc[0];
+    ok = !failed;
+  }
+  // ---- greedy reconstruction from s
+  uint32_t c = A.s;
+  if (ok && threadIdx.x == 0) A.res->path[0] = A.vids[A.s];
+  for (int pos = 0; ok && pos < L; ++pos) {
+    uint32_t deg = 0;
+    if (!A.visible || A.visible[c])
+      for (int t = 0; t < A.fwd.n; ++t) deg += A.fwd.row_ptr[t][c + 1] - A.fwd.row_ptr[t][c];
+    PhaseView P{};
+    P.op = OP_GREEDY;
+    P.pos = (uint32_t)pos;
+    P.cur = c;
+    P.L = (uint32_t)L;
+    P.kf = (uint32_t)kf;
+    const bool big = deg > SP_GREEDY_SMALL && nwg > 1;
+    phase_run(P, big);
+    if (threadIdx.x == 0) {
+      Cand best{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
+      const int parts = big ? nwg : 1;
+      for (int k = 0; k < parts; ++k) {
+        const unsigned long long* q = ctl->gpart + 4 * k;
+        Cand x{(int64_t)ld1(q), (int64_t)ld1(q + 1), (int64_t)ld1(q + 2), (uint32_t)ld1(q + 3)};
+        if (cand_less(x, best)) best = x;
+      }
+      lds[0] = best;
+      if (best.d != NO_ROW) {
+        A.res->path[1 + 3 * pos] = best.t;
+        A.res->path[2 + 3 * pos] = best.r;
+        A.res->path[3 + 3 * pos] = best.v;
+      }
+    }
+    __syncthreads();
+    c = lds[0].d;
+    __syncthreads();
+    if (c == NO_ROW) {
+      ok = false;
+      if (threadIdx.x == 0) atomicOr(&ctl->err, 1ull);
+    }
+  }
+  // ---- result, release the followers
+  if (threadIdx.x == 0) {
+    A.res->L = ok ? (unsigned long long)L : 0ull;
+    A.res->edges = edges;
+    A.res->err = ld1(&ctl->err);
+    A.res->levels = (unsigned long long)levels;
+    ctl->op = OP_EXIT;
+  }
+  wg_release();
+  if (threadIdx.x == 0 && nwg > 1) st1(&ctl->gen, g0 | ++phase);
+}
+
+// ---------------------------------------------------------------------------- host side
+struct SpCtx {
+  hipStream_t stream = nullptr;
+  uint64_t nv = 0, cap = 0;
+  uint32_t* lab[3] = {};
+  uint32_t epoch = 0;
+  uint64_t* list[SP_NLISTS] = {};
+  SpCtl* ctl = nullptr;
+  SpResult* d_res = nullptr;
+  SpResult* h_res = nullptr;
+  hipEvent_t done = nullptr;
+  unsigned long long q = 0;
+  int wgs = 64;
+};
+
+SpCtx* sp_create(uint64_t nv, uint64_t item_cap, hipStream_t s, std::string* err) {
+  auto* c = new SpCtx();
+  c->stream = s;
+  c->nv = nv;
+  c->cap = item_cap;
+  const char* e = getenv("NBG_SP_WGS");
+  c->wgs = e ? std::max(1, std::min(SP_MAX_WGS, atoi(e))) : 64;
+  hipError_t he = hipSuccess;
+  auto M = [&](void** p, size_t b) { if (he == hipSuccess) he = hipMalloc(p, b); };
+  for (auto& l : c->lab) M((void**)&l, (nv + 1) * 4);
+  for (auto& l : c->list) M((void**)&l, std::max<uint64_t>(item_cap, 1) * 8);
+  M((void**)&c->ctl, sizeof(SpCtl));
+  M((void**)&c->d_res, sizeof(SpResult));
+  if (he == hipSuccess) he = hipHostMalloc((void**)&c->h_res, sizeof(SpResult), hipHostMallocDefault);
+  if (he == hipSuccess) he = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
+  for (auto& l : c->lab)
+    if (he == hipSuccess) he = hipMemsetAsync(l, 0, (nv + 1) * 4, s);
+  if (he == hipSuccess) he = hipMemsetAsync(c->ctl, 0, sizeof(SpCtl), s);
+  if (he == hipSuccess) he = hipStreamSynchronize(s);
+  if (he != hipSuccess) {
+    if (err) *err = std::string("shortest-path workspace: ") + hipGetErrorString(he);
+    sp_destroy(c);
+    return nullptr;
+  }
+  return c;
+}
+
+void sp_destroy(SpCtx* c) {
+  if (!c) return;
+  for (auto* l : c->lab)
+    if (l) (void)hipFree(l);
+  for (auto* l : c->list)
+    if (l) (void)hipFree(l);
+  if (c->ctl) (void)hipFree(c->ctl);
+  if (c->d_res) (void)hipFree(c->d_res);
+  if (c->h_res) (void)hipHostFree(c->h_res);
+  if (c->done) (void)hipEventDestroy(c->done);
+  delete c;
+}
+
+hipError_t sp_launch(SpCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible, const int64_t* vids,
+                     uint32_t s, uint32_t t, uint32_t upto) {
+  if (upto > MAX_PATH_LEN || s == NO_ROW || t == NO_ROW) return hipErrorInvalidValue;
+  if (++c->epoch >= (1u << (32 - LVL_BITS))) {   // wrap: clear the labels once
+    for (auto* l : c->lab) HIP_TRY_SP(hipMemsetAsync(l, 0, (c->nv + 1) * 4, c->stream));
+    c->epoch = 1;
+  }
+  SpArgs a{};
+  a.fwd = fwd;
+  a.bwd = bwd;
+  a.visible = visible;
+  a.vids = vids;
+  a.s = s;
+  a.t = t;
+  a.upto = upto;
+  a.lab_f = c->lab[0];
+  a.lab_b = c->lab[1];
+  a.lab_m = c->lab[2];
+  a.ef = a.eb = a.em = c->epoch;
+  for (int i = 0; i < SP_NLISTS; ++i) a.list[i] = c->list[i];
+  a.list_cap = c->cap;
+  a.ctl = c->ctl;
+  a.res = c->d_res;
+  a.q = ++c->q;
+  a.spin_limit = 1ull << 24;   // ~10 s of polling: a stuck phase ends the query with err = 2
+  hipLaunchKernelGGL(k_sp_pair, dim3((unsigned)c->wgs), dim3(SP_THREADS), 0, c->stream, a);
+  HIP_TRY_SP(hipGetLastError());
+  HIP_TRY_SP(hipMemcpyAsync(c->h_res, c->d_res, sizeof(SpResult), hipMemcpyDeviceToHost, c->stream));
+  return hipEventRecord(c->done, c->stream);
+}
+
+bool sp_ready(SpCtx* c) { return hipEventQuery(c->done) == hipSuccess; }
+
+hipError_t sp_wait(SpCtx* c, SpResult* out) {
+  hipError_t e;
+  while ((e = hipEventQuery(c->done)) == hipErrorNotReady) {
+  }
+  if (e != hipSuccess) return e;
+  memcpy(out, c->h_res, sizeof(SpResult));
+  return hipSuccess;
+}
+
+}  // namespace nbg

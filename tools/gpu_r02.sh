@@ -33,6 +33,11 @@ for step in "$@"; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof26" -o run --output-format csv -- \
         python3 -u bench.py --sp-pairs 2000 --no-cpu-baseline --verify 0 --c2 0 --c5-scale 0 --getbound-reqs 0 \
         > "$OUT/bench_prof26.json" 2> "$OUT/bench_prof26.log" || { tail -30 "$OUT/bench_prof26.log"; exit 1; } ;;
+    go26|go26flags)
+      [ "$step" = go26flags ] && export NBG_MARK_FLAGS=1
+      timeout -k 10 600 python -u bench.py --sp-pairs 0 --no-cpu-baseline --verify 4 --c2 0 --c5-scale 0 \
+        --getbound-reqs 0 > "$OUT/$step.json" 2> "$OUT/$step.log" || { tail -30 "$OUT/$step.log"; exit 1; }
+      unset NBG_MARK_FLAGS ;;
     bench)
       timeout -k 10 900 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.log" || { tail -30 "$OUT/bench.log"; exit 1; } ;;
   esac
