@@ -250,6 +250,34 @@ def shortest_path_leg(eng, pairs, args, barrier):
             hops += (len(paths[0]) - 1) // 3
     barrier()
     elapsed = time.perf_counter() - t0
+    # throughput pass: the same pairs with queries in flight on the query slots
+    # (nbg_find_path_submit / _wait; on a partitioned engine each query still runs collectively)
+    inflight = 0 if args.sync else int(os.environ.get("NBG_QUERY_SLOTS", "6"))
+    conc = None
+    if inflight:
+        barrier()
+        c0 = time.perf_counter()
+        c_edges, c_found, pending = 0, 0, []
+
+        def drain_one():
+            st = {}
+            got = eng.find_path_wait(pending.pop(0), stats=st)
+            return st["edges"], bool(got)
+
+        for s, t in pairs:
+            if len(pending) == inflight:
+                e_, f_ = drain_one()
+                c_edges += e_
+                c_found += f_
+            pending.append(eng.find_path_submit([s], [t], [1], args.sp_upto))
+        while pending:
+            e_, f_ = drain_one()
+            c_edges += e_
+            c_found += f_
+        barrier()
+        c_el = time.perf_counter() - c0
+        conc = {"queries_in_flight": inflight, "pairs_per_s": len(pairs) / c_el if c_el else None,
+                "teps": c_edges / c_el if c_el else None, "seconds": round(c_el, 3), "found": c_found}
     kst, prof_pairs = {}, 0
     if not args.no_profile:   # roofline pass: HIP events around k_expand<BFS> over the first pairs
         eng.profile(2)
@@ -266,7 +294,8 @@ def shortest_path_leg(eng, pairs, args, barrier):
            "mean_hops": round(hops / found, 3) if found else None,
            "p50_ms": float(np.percentile(lat_ms, 50)), "p90_ms": float(np.percentile(lat_ms, 90)),
            "p99_ms": float(np.percentile(lat_ms, 99)), "mean_ms": float(lat_ms.mean()),
-           "teps": edges / elapsed if elapsed else None, "edges": edges, "seconds": round(elapsed, 3)}
+           "teps": edges / elapsed if elapsed else None, "edges": edges, "seconds": round(elapsed, 3),
+           "timing": "latency pass: one query at a time, uninstrumented", "concurrent": conc}
     ks = {k: v for k, v in kst.items() if v["launches"]} if kst else {}
     if ks:
         out["kernels"] = {k: {"launches": v["launches"], "ms": round(v["ms"], 3),

@@ -246,6 +246,15 @@ typedef struct {
  * SHORTEST returns at most one path per target: the minimum hop count, ties broken by the
  * lexicographically smallest entry list (the reference's tie-break is iteration order). */
 int32_t nbg_find_path(nbg_engine* e, const nbg_path_request* req, nbg_paths** out);
+/* Asynchronous FIND PATH: up to NBG_QUERY_SLOTS (default 6) one-pair SHORTEST queries of a
+ * single (non-partitioned) engine in flight, each on its own device workspace and HIP stream;
+ * every other request runs inside nbg_find_path_submit.  When every slot is busy the oldest query
+ * is completed first (its result stays in its ticket).  nbg_find_path_wait returns the result with
+ * nbg_find_path's semantics (and status) and frees the ticket; tickets must be waited for before
+ * nbg_destroy (outstanding ones are reclaimed there). */
+typedef struct nbg_path_ticket nbg_path_ticket;
+int32_t nbg_find_path_submit(nbg_engine* e, const nbg_path_request* req, nbg_path_ticket** out);
+int32_t nbg_find_path_wait(nbg_path_ticket* ticket, nbg_paths** out);
 int64_t nbg_paths_count(const nbg_paths* p);
 int64_t nbg_path_len(const nbg_paths* p, int64_t i);
 const int64_t* nbg_path_entries(const nbg_paths* p, int64_t i);

@@ -914,6 +914,7 @@ void nbg_destroy(nbg_engine* h) {
     if (q.ws) ws_destroy(q.ws);
     if (q.stream) (void)hipStreamDestroy(q.stream);
   }
+  path_slots_release(E);
   if (E.ws) ws_destroy(E.ws);
   if (E.sp) sp_destroy(E.sp);
   E.free_snapshot();

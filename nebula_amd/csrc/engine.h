@@ -36,6 +36,13 @@ struct Engine {
   };
   std::vector<QuerySlot> slots;
   SpCtx* sp = nullptr;                  // one-pair FIND SHORTEST PATH workspace (sp.hip), on `stream`
+  struct PathSlot {                     // asynchronous FIND SHORTEST PATH (nbg_find_path_submit)
+    SpCtx* sp = nullptr;
+    hipStream_t stream = nullptr;
+    void* ticket = nullptr;
+  };
+  std::vector<PathSlot> path_slots;
+  std::vector<void*> path_inflight;
   uint64_t sp_item_cap() const;         // items a shortest-path list may hold
   std::vector<void*> inflight;          // submitted tickets, oldest first
   // device GO results (rows left in HBM) and the workspace their rows live in: before that
@@ -72,6 +79,7 @@ struct Engine {
 };
 
 int32_t engine_ready(Engine& E);   // workspace (+ partition buffers) after finalize / snapshot load
+void path_slots_release(Engine& E); // completes outstanding path tickets, frees the path slots
 // Make *wsp free for a new query: if live device rows still sit in it, the rows take the
 // workspace over and *wsp becomes a fresh one on `stream` (profiling state carried over).
 int32_t ws_release(Engine& E, Workspace** wsp, hipStream_t stream);

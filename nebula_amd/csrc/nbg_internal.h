@@ -306,6 +306,9 @@ struct SpResult {                    // one query's result block (device, copied
   unsigned long long err;            // 1 reconstruction failure, 2 spin bound, 3 list overflow
   unsigned long long levels;         // BFS levels run
   long long path[1 + 3 * MAX_PATH_LEN];   // [v0, t0, r0, v1, ...]
+  // phase trace (wall_clock64 ticks): trace[0] = launch start, then (kind << 56 | tick) per phase
+  unsigned long long ntrace;
+  unsigned long long trace[40];
 };
 struct SpCtx;                        // labels, item lists, control block, result block of one slot
 // item_cap: items a list may hold = sum over a side's types of (nv + E_t / 64), plus slack

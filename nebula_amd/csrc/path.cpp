@@ -394,13 +394,17 @@ int32_t all_paths(PathCtx& c, const std::vector<uint32_t>& S, const std::vector<
   return NBG_OK;
 }
 
-}  // namespace
 
-extern "C" int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* rq, nbg_paths** out) {
-  if (!h || !rq || !out) return NBG_E_INVALID_ARGUMENT;
-  *out = nullptr;
-  Engine& E = h->e;
-  std::lock_guard<std::mutex> lg(E.mu);
+// A one-pair SHORTEST request handed to a query slot instead of being run here.
+struct PairLaunch {
+  SpTypes fwd, bwd;
+  uint32_t s = NO_ROW, t = NO_ROW, upto = 0;
+};
+constexpr int32_t PAIR_DEFERRED = 1;
+
+// nbg_find_path under the engine lock.  With `pl`, a single-engine one-pair SHORTEST request
+// whose endpoints have edges is not run: *pl describes it and PAIR_DEFERRED is returned.
+int32_t find_path_locked(Engine& E, const nbg_path_request* rq, nbg_paths** out, PairLaunch* pl) {
   if (!E.finalized) return E.fail(NBG_E_STATE, "engine not finalized");
   if (hipSetDevice(E.cfg.device) != hipSuccess) return E.fail(NBG_E_DEVICE, "hipSetDevice failed");
   if (!rq->shortest && E.partitioned())
@@ -498,7 +502,17 @@ extern "C" int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* rq, nbg_
   }
   const bool pair = rq->shortest && Sv.size() == 1 && Tv.size() == 1 && Sv[0] != Tv[0];
   if (pair && !c.part && !sp_legacy()) {
-    int32_t rc = device_pair(c, S.empty() ? NO_ROW : S[0], Tg[0], rq->upto, res);
+    const uint32_t s0 = S.empty() ? NO_ROW : S[0];
+    if (pl && host_degree(c, c.fwd, s0) && host_degree(c, c.bwd, Tg[0])) {
+      pl->fwd = sp_types(c.fwd);
+      pl->bwd = sp_types(c.bwd);
+      pl->s = s0;
+      pl->t = Tg[0];
+      pl->upto = rq->upto;
+      delete res;
+      return PAIR_DEFERRED;
+    }
+    int32_t rc = device_pair(c, s0, Tg[0], rq->upto, res);
     if (rc) { delete res; return rc; }
     res->edges = c.edges;
     *out = res;
@@ -522,3 +536,137 @@ extern "C" int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* rq, nbg_
   *out = res;
   return NBG_OK;
 }
+
+int sp_query_slots() {
+  static const int n = [] {
+    const char* v = getenv("NBG_QUERY_SLOTS");
+    const int k = v ? atoi(v) : 6;
+    return k < 1 ? 1 : (k > 16 ? 16 : k);
+  }();
+  return n;
+}
+
+}  // namespace
+
+// ============================================================================= asynchronous FIND PATH
+// Up to NBG_QUERY_SLOTS one-pair SHORTEST queries in flight, each on its own shortest-path
+// workspace and HIP stream (the way graphd runs concurrent FindPathExecutors); every other request
+// runs at submission.
+struct nbg_path_ticket {
+  Engine* eng = nullptr;
+  int slot = -1;
+  bool done = false;
+  int32_t rc = NBG_OK;
+  nbg_paths* result = nullptr;
+};
+
+namespace {
+
+void path_complete_oldest(Engine& E) {
+  auto* t = static_cast<nbg_path_ticket*>(E.path_inflight.front());
+  E.path_inflight.erase(E.path_inflight.begin());
+  Engine::PathSlot& ps = E.path_slots[t->slot];
+  SpResult r;
+  hipError_t he = sp_wait(ps.sp, &r);
+  if (he != hipSuccess) {
+    t->rc = E.fail(NBG_E_DEVICE, std::string("shortest path: ") + hipGetErrorString(he));
+  } else if (r.err == 1) {
+    t->rc = E.fail(NBG_E_UNKNOWN, "shortest-path reconstruction failed (in/out edges disagree)");
+  } else if (r.err) {
+    t->rc = E.fail(NBG_E_DEVICE, "shortest path: device search aborted (code " + std::to_string(r.err) + ")");
+  } else {
+    auto* res = new nbg_paths();
+    res->edges = r.edges;
+    if (r.L) res->paths.emplace_back(r.path, r.path + 1 + 3 * r.L);
+    t->result = res;
+  }
+  t->done = true;
+  ps.ticket = nullptr;
+}
+
+}  // namespace
+
+void nbg::path_slots_release(Engine& E) {
+  while (!E.path_inflight.empty()) {
+    auto* t = static_cast<nbg_path_ticket*>(E.path_inflight.front());
+    path_complete_oldest(E);
+    if (t->result) delete t->result;
+    delete t;
+  }
+  for (auto& ps : E.path_slots) {
+    if (ps.sp) sp_destroy(ps.sp);
+    if (ps.stream) (void)hipStreamDestroy(ps.stream);
+  }
+  E.path_slots.clear();
+}
+
+extern "C" {
+
+int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* rq, nbg_paths** out) {
+  if (!h || !rq || !out) return NBG_E_INVALID_ARGUMENT;
+  *out = nullptr;
+  Engine& E = h->e;
+  std::lock_guard<std::mutex> lg(E.mu);
+  return find_path_locked(E, rq, out, nullptr);
+}
+
+int32_t nbg_find_path_submit(nbg_engine* h, const nbg_path_request* rq, nbg_path_ticket** out) {
+  if (!h || !rq || !out) return NBG_E_INVALID_ARGUMENT;
+  *out = nullptr;
+  Engine& E = h->e;
+  std::lock_guard<std::mutex> lg(E.mu);
+  auto* t = new nbg_path_ticket();
+  t->eng = &E;
+  PairLaunch pl;
+  nbg_paths* res = nullptr;
+  const int32_t rc = find_path_locked(E, rq, &res, E.partitioned() ? nullptr : &pl);
+  if (rc != PAIR_DEFERRED) {   // ran here (or failed): the ticket carries the outcome
+    t->done = true;
+    t->rc = rc;
+    t->result = res;
+    *out = t;
+    return NBG_OK;
+  }
+  if (E.path_slots.empty()) E.path_slots.resize(sp_query_slots());
+  int slot = -1;
+  for (size_t i = 0; i < E.path_slots.size() && slot < 0; ++i)
+    if (!E.path_slots[i].ticket) slot = (int)i;
+  if (slot < 0) {   // every slot busy: finish the oldest query first
+    slot = static_cast<nbg_path_ticket*>(E.path_inflight.front())->slot;
+    path_complete_oldest(E);
+  }
+  Engine::PathSlot& ps = E.path_slots[slot];
+  if (!ps.stream && hipStreamCreateWithFlags(&ps.stream, hipStreamNonBlocking) != hipSuccess) {
+    delete t;
+    return E.fail(NBG_E_DEVICE, "hipStreamCreate failed");
+  }
+  if (!ps.sp) {
+    std::string err;
+    ps.sp = sp_create(E.snap.nv, E.sp_item_cap(), ps.stream, &err);
+    if (!ps.sp) { delete t; return E.fail(NBG_E_OUT_OF_MEMORY, err); }
+  }
+  hipError_t he = sp_launch(ps.sp, pl.fwd, pl.bwd, E.snap.d_visible, E.snap.d_vids, pl.s, pl.t, pl.upto);
+  if (he != hipSuccess) { delete t; return dev_fail(E, he, "shortest path"); }
+  t->slot = slot;
+  ps.ticket = t;
+  E.path_inflight.push_back(t);
+  *out = t;
+  return NBG_OK;
+}
+
+int32_t nbg_find_path_wait(nbg_path_ticket* t, nbg_paths** out) {
+  if (!t || !out) return NBG_E_INVALID_ARGUMENT;
+  Engine& E = *t->eng;
+  std::lock_guard<std::mutex> lg(E.mu);
+  *out = nullptr;
+  if (!t->done) {
+    while (!E.path_inflight.empty() && E.path_inflight.front() != t) path_complete_oldest(E);
+    path_complete_oldest(E);
+  }
+  const int32_t rc = t->rc;
+  *out = t->result;
+  delete t;
+  return rc;
+}
+
+}  // extern "C"

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <string>
 
@@ -35,11 +36,12 @@
 namespace nbg {
 namespace {
 
-constexpr int SP_THREADS = 256;
+constexpr int SP_THREADS = 512;
 constexpr int SP_WAVES = SP_THREADS / 64;
-constexpr int SP_U = 4;                 // items per wave iteration (their loads in flight together)
+constexpr int SP_U = 8;                 // items per wave pass (their loads in flight together)
+constexpr int SP_PASS = SP_WAVES * SP_U;   // items per workgroup pass
 constexpr uint32_t SP_CH = 64;          // CSR entries per item
-constexpr uint64_t SP_SMALL = 96;       // a phase with at most this many items runs on the leader alone
+constexpr uint64_t SP_SMALL = 2 * SP_PASS;   // a phase with at most this many items runs on the leader alone
 constexpr uint32_t SP_GREEDY_SMALL = 4096;   // greedy hop: adjacency the leader scans alone
 constexpr int SP_MAX_WGS = 256;
 
@@ -49,15 +51,20 @@ enum SpList : int { L_F0 = 0, L_F1 = 1, L_B0 = 2, L_B1 = 3, L_M0 = 4, L_M1 = 5, 
 }  // namespace
 
 // Device control block of one persistent query (zeroed once; per-query words reset by the leader).
+// The polled generation word, the arrival counter and each accumulator sit on cache lines of
+// their own: 63 pollers on the line that the level's atomics hit would serialise both.
+struct alignas(128) SpWord {
+  unsigned long long v;
+  unsigned long long pad[15];
+};
 struct SpCtl {
-  unsigned long long gen;          // released phase: (q << 24) | phase
-  unsigned long long arrive;       // follower arrivals (reset at query start)
-  unsigned long long err;          // 1 reconstruction failure, 2 spin bound hit, 3 list overflow
+  SpWord gen;                      // released phase: (q << 24) | phase
+  SpWord arrive;                   // follower arrivals (reset at query start)
+  SpWord err;                      // 1 reconstruction failure, 2 spin bound hit, 3 list overflow
+  SpWord out_n, dsum, meet_n, meet_items, edges;   // phase accumulators (leader zeroes them)
   // phase parameters (leader writes, releases, bumps gen)
-  unsigned long long op, side, src, n, dst, pos, cur, stamp, mstamp;
-  // phase accumulators (leader zeroes before the phase)
-  unsigned long long out_n, dsum, meet_n, meet_items, edges;
-  unsigned long long gpart[4 * SP_MAX_WGS];   // greedy: per-workgroup minimum (type, rank, vid, dense)
+  alignas(128) unsigned long long op, side, src, n, dst, pos, cur, stamp, mstamp;
+  alignas(128) unsigned long long gpart[4 * SP_MAX_WGS];   // greedy: per-workgroup minimum
 };
 
 struct SpArgs {
@@ -190,16 +197,52 @@ struct LevelCfg {
   bool append;               // append the claimed vertices' items (N) to dst
 };
 
-// One phase over the items of list `src` (n items): this workgroup's share of the waves
-// [wg * SP_WAVES, (wg + 1) * SP_WAVES) out of nwg * SP_WAVES.
+// Per-workgroup scratch of run_level's aggregated append.
+struct LevelLds {
+  uint32_t wave_tot[SP_WAVES];
+  unsigned long long base;
+  uint32_t total;
+};
+
+// Items of the claimed vertices of one lane (up to SP_U of them) over T, from their row ranges.
+__device__ __forceinline__ uint32_t lane_items(const SpTypes& T, const uint32_t (&x)[SP_U], uint32_t cmask,
+                                               const uint8_t* visible, uint32_t (&ni)[SP_U], unsigned long long* dsum) {
+  uint32_t vis[SP_U];
+#pragma unroll
+  for (int u = 0; u < SP_U; ++u) vis[u] = ((cmask >> u) & 1u) && (!visible || visible[x[u]]);
+  uint32_t c = 0;
+#pragma unroll
+  for (int u = 0; u < SP_U; ++u) ni[u] = 0;
+  for (int t = 0; t < T.n; ++t) {
+    uint32_t rs[SP_U], re[SP_U];
+#pragma unroll
+    for (int u = 0; u < SP_U; ++u) {   // every row range of this type in flight at once
+      rs[u] = vis[u] ? T.row_ptr[t][x[u]] : 0u;
+      re[u] = vis[u] ? T.row_ptr[t][x[u] + 1] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < SP_U; ++u) {
+      const uint32_t d = re[u] - rs[u];
+      ni[u] += (d + SP_CH - 1) / SP_CH;
+      *dsum += d;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < SP_U; ++u) c += ni[u];
+  return c;
+}
+
+// One phase over the items of list `src` (n items): workgroup wg of nwg takes passes of SP_PASS
+// items (SP_U per wave; lane l owns entry l of each item).  Per pass: every neighbour's labels in
+// flight at once, the CAS claims, the claimed vertices' row ranges, then ONE atomic per workgroup
+// reserves the pass's output items (block scan in LDS).
 __device__ void run_level(const SpArgs& A, const LevelCfg& C, const uint64_t* src, uint64_t n, uint64_t* dst,
-                          int wg, int nwg) {
+                          int wg, int nwg, LevelLds* L) {
   SpCtl* ctl = A.ctl;
-  const int lane = threadIdx.x & 63;
-  const uint64_t gw = (uint64_t)wg * SP_WAVES + (threadIdx.x >> 6);
-  const uint64_t NW = (uint64_t)nwg * SP_WAVES;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   unsigned long long edges = 0, dsum = 0;
-  for (uint64_t i0 = gw * SP_U; i0 < n; i0 += NW * SP_U) {
+  for (uint64_t p0 = (uint64_t)wg * SP_PASS; p0 < n; p0 += (uint64_t)nwg * SP_PASS) {   // uniform per workgroup
+    const uint64_t i0 = p0 + (uint64_t)wv * SP_U;
     uint64_t it = 0;
     if (lane < SP_U && i0 + lane < n) it = src[i0 + lane];
     uint32_t x[SP_U];
@@ -215,34 +258,101 @@ __device__ void run_level(const SpArgs& A, const LevelCfg& C, const uint64_t* sr
         }
       }
     }
+    // labels (claim, restriction, other side) of every neighbour in flight together
+    uint32_t old[SP_U], rl[SP_U], ol[SP_U];
+#pragma unroll
+    for (int u = 0; u < SP_U; ++u) {
+      const bool v = x[u] != NO_ROW;
+      old[u] = v ? ld1(C.lab + x[u]) : 0u;
+      rl[u] = (v && C.rlab) ? ld1(C.rlab + x[u]) : C.rstamp;
+      ol[u] = (v && C.olab) ? ld1(C.olab + x[u]) : 0u;
+    }
     uint32_t claimed = 0, meet = 0;
 #pragma unroll
     for (int u = 0; u < SP_U; ++u) {
-      const uint32_t w = x[u];
-      if (w == NO_ROW) continue;
-      if (C.rlab && ld1(C.rlab + w) != C.rstamp) continue;
-      const uint32_t old = ld1(C.lab + w);
-      if (C.exact ? old == C.stamp : live(old, C.epoch)) continue;
-      if (atomicCAS(C.lab + w, old, C.stamp) != old) continue;
+      if (x[u] == NO_ROW || rl[u] != C.rstamp) continue;
+      if (C.exact ? old[u] == C.stamp : live(old[u], C.epoch)) continue;
+      if (atomicCAS(C.lab + x[u], old[u], C.stamp) != old[u]) continue;
       claimed |= 1u << u;
-      if (C.olab && live(ld1(C.olab + w), C.oepoch)) meet |= 1u << u;
+      if (C.olab && live(ol[u], C.oepoch)) meet |= 1u << u;
     }
+    // output items of the claimed vertices: one reservation per workgroup pass
+    uint32_t ni[SP_U];
 #pragma unroll
-    for (int u = 0; u < SP_U; ++u) {
-      const bool cl = (claimed >> u) & 1u, mt = (meet >> u) & 1u;
-      uint32_t ni = 0, ne = 0;
-      if (cl && C.append) vertex_items(*C.N, A.visible, x[u], &ni, &ne);
-      dsum += ne;
-      if (C.append) wave_append(*C.N, x[u], cl, ni, dst, &ctl->out_n, A.list_cap, &ctl->err);
-      if (C.olab && __ballot(mt)) {
-        uint32_t mi = 0, me = 0;
-        if (mt) {
-          st1(A.lab_m + x[u], C.mstamp);
-          vertex_items(*C.M, A.visible, x[u], &mi, &me);
+    for (int u = 0; u < SP_U; ++u) ni[u] = 0;
+    const uint32_t c = C.append ? lane_items(*C.N, x, claimed, A.visible, ni, &dsum) : 0u;
+    const uint32_t incl = wave_incl_scan32(c);
+    if (lane == 63) L->wave_tot[wv] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t run = 0;
+      for (int k = 0; k < SP_WAVES; ++k) {
+        const uint32_t w_ = L->wave_tot[k];
+        L->wave_tot[k] = run;
+        run += w_;
+      }
+      L->total = run;
+      L->base = run ? atomicAdd(&ctl->out_n.v, (unsigned long long)run) : 0ull;
+      if (run && L->base + run > A.list_cap) atomicOr(&ctl->err.v, 3ull);
+    }
+    __syncthreads();
+    const bool room = L->base + L->total <= A.list_cap;
+    uint64_t mine = L->base + L->wave_tot[wv] + incl - c;
+    __syncthreads();   // wave_tot / base are rewritten by the next pass
+    if (room) {
+      bool big = false;
+#pragma unroll
+      for (int u = 0; u < SP_U; ++u) big |= ni[u] > 8;
+      if (!big) {
+#pragma unroll
+        for (int u = 0; u < SP_U; ++u)
+          if (ni[u]) {
+            write_items(*C.N, x[u], dst, mine, 0, 1, ni[u]);
+            mine += ni[u];
+          }
+      }
+      unsigned long long bm = __ballot(big);
+      while (bm) {   // lanes with a hub among their vertices: the whole wave writes their items
+        const int l = __ffsll((long long)bm) - 1;
+        bm &= bm - 1;
+        uint64_t b = __shfl(mine, l, 64);
+#pragma unroll
+        for (int u = 0; u < SP_U; ++u) {
+          const uint32_t hx = __shfl(x[u], l, 64), hc = __shfl(ni[u], l, 64);
+          if (hc) write_items(*C.N, hx, dst, b, (uint32_t)lane, 64, hc);
+          b += hc;
         }
-        const unsigned long long mb = __ballot(mt);
-        if (lane == 0) atomicAdd(&ctl->meet_n, (unsigned long long)__popcll(mb));
-        wave_append(*C.M, x[u], mt, mi, A.list[L_M0], &ctl->meet_items, A.list_cap, &ctl->err);
+      }
+    }
+    if (C.olab && __ballot(meet != 0)) {   // rare: a meet vertex gets LAB_M and its in-edge items
+      uint32_t mi[SP_U];
+      unsigned long long md = 0;
+#pragma unroll
+      for (int u = 0; u < SP_U; ++u)
+        if ((meet >> u) & 1u) st1(A.lab_m + x[u], C.mstamp);
+      const uint32_t mc = lane_items(*C.M, x, meet, A.visible, mi, &md);
+      const uint32_t minc = wave_incl_scan32(mc);
+      const uint32_t mtot = __shfl(minc, 63, 64);
+      const uint32_t nmeet = (uint32_t)__popc(meet);
+      uint32_t mcount = nmeet;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) mcount += __shfl_xor(mcount, o, 64);
+      unsigned long long mb = 0;
+      if (lane == 0) {
+        atomicAdd(&ctl->meet_n.v, (unsigned long long)mcount);
+        if (mtot) mb = atomicAdd(&ctl->meet_items.v, (unsigned long long)mtot);
+      }
+      mb = __shfl(mb, 0, 64);
+      if (mb + mtot <= A.list_cap) {
+        uint64_t m = mb + minc - mc;
+#pragma unroll
+        for (int u = 0; u < SP_U; ++u)
+          if (mi[u]) {
+            write_items(*C.M, x[u], A.list[L_M0], m, 0, 1, mi[u]);
+            m += mi[u];
+          }
+      } else if (lane == 0) {
+        atomicOr(&ctl->err.v, 3ull);
       }
     }
   }
@@ -253,8 +363,8 @@ __device__ void run_level(const SpArgs& A, const LevelCfg& C, const uint64_t* sr
     dsum += __shfl_xor(dsum, o, 64);
   }
   if (lane == 0) {
-    if (edges) atomicAdd(&ctl->edges, edges);
-    if (dsum) atomicAdd(&ctl->dsum, dsum);
+    if (edges) atomicAdd(&ctl->edges.v, edges);
+    if (dsum) atomicAdd(&ctl->dsum.v, dsum);
   }
 }
 
@@ -277,15 +387,24 @@ __device__ Cand greedy_scan(const SpArgs& A, uint32_t c, int pos, int L, int kf,
   const bool by_m = pos + 1 <= kf;
   if (c != NO_ROW && (!A.visible || A.visible[c])) {
     const uint64_t g = (uint64_t)wg * SP_THREADS + threadIdx.x, G = (uint64_t)nwg * SP_THREADS;
+    const uint32_t* lab = by_m ? A.lab_m : A.lab_b;
+    const uint32_t want = by_m ? want_m : want_b;
     for (int t = 0; t < A.fwd.n; ++t) {
       const uint32_t rs = A.fwd.row_ptr[t][c], re = A.fwd.row_ptr[t][c + 1];
-      for (uint64_t j = rs + g; j < re; j += G) {
-        const uint32_t w = A.fwd.col[t][j];
-        if (w == NO_ROW) continue;
-        const bool ok = by_m ? ld1(A.lab_m + w) == want_m : ld1(A.lab_b + w) == want_b;
-        if (!ok) continue;
-        Cand x{(int64_t)A.fwd.type[t], A.fwd.rank[t] ? A.fwd.rank[t][j] : 0, A.fwd.dst_vid[t][j], w};
-        if (cand_less(x, best)) best = x;
+      for (uint64_t j0 = rs + g; j0 < re; j0 += 4 * G) {   // 4 edges per thread in flight
+        uint32_t w[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[k] = j0 + k * G < re ? A.fwd.col[t][j0 + k * G] : NO_ROW;
+        uint32_t l[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) l[k] = w[k] != NO_ROW ? ld1(lab + w[k]) : 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (w[k] == NO_ROW || l[k] != want) continue;
+          const uint64_t j = j0 + k * G;
+          Cand x{(int64_t)A.fwd.type[t], A.fwd.rank[t] ? A.fwd.rank[t][j] : 0, A.fwd.dst_vid[t][j], w[k]};
+          if (cand_less(x, best)) best = x;
+        }
       }
     }
   }
@@ -338,7 +457,7 @@ struct PhaseView {   // the leader's phase parameters, as every workgroup reads 
   uint32_t L, kf;
 };
 
-__device__ void run_phase(const SpArgs& A, const PhaseView& P, int wg, int nwg, Cand* lds) {
+__device__ void run_phase(const SpArgs& A, const PhaseView& P, int wg, int nwg, Cand* lds, LevelLds* L) {
   if (P.op == OP_LEVEL) {
     LevelCfg C{};
     const bool fw = P.side == 0;
@@ -352,7 +471,7 @@ __device__ void run_phase(const SpArgs& A, const PhaseView& P, int wg, int nwg, 
     C.oepoch = fw ? A.eb : A.ef;
     C.mstamp = P.mstamp;
     C.append = true;
-    run_level(A, C, A.list[P.src], P.n, A.list[P.dst], wg, nwg);
+    run_level(A, C, A.list[P.src], P.n, A.list[P.dst], wg, nwg, L);
   } else if (P.op == OP_BSET) {
     // B[pos] from B[pos + 1] through in-edges, restricted to forward level pos, claimed in LAB_M
     LevelCfg C{};
@@ -364,7 +483,7 @@ __device__ void run_phase(const SpArgs& A, const PhaseView& P, int wg, int nwg, 
     C.rlab = A.lab_f;
     C.rstamp = stamp_of(A.ef, P.pos);
     C.append = P.pos >= 2;   // B[1]'s in-edges are not needed (B[0] = {s})
-    run_level(A, C, A.list[P.src], P.n, A.list[P.dst], wg, nwg);
+    run_level(A, C, A.list[P.src], P.n, A.list[P.dst], wg, nwg, L);
   } else if (P.op == OP_GREEDY) {
     Cand b = greedy_scan(A, P.cur, (int)P.pos, (int)P.L, (int)P.kf, wg, nwg, lds);
     if (threadIdx.x == 0) {
@@ -382,6 +501,7 @@ __device__ void run_phase(const SpArgs& A, const PhaseView& P, int wg, int nwg, 
 __global__ void __launch_bounds__(SP_THREADS) k_sp_pair(SpArgs A) {
   __shared__ PhaseView sP;
   __shared__ Cand lds[SP_WAVES + 1];
+  __shared__ LevelLds sL;
   __shared__ int sQuit;
   SpCtl* ctl = A.ctl;
   const unsigned long long g0 = A.q << 24;
@@ -391,12 +511,12 @@ __global__ void __launch_bounds__(SP_THREADS) k_sp_pair(SpArgs A) {
     unsigned long long seen = g0;
     for (;;) {
       if (threadIdx.x == 0) {
-        unsigned long long g = ld1(&ctl->gen);
+        unsigned long long g = ld1(&ctl->gen.v);
         unsigned long long spins = 0;
         while (g == seen || g < g0) {   // (< g0: a generation of an earlier query)
-          if (++spins > A.spin_limit) { atomicOr(&ctl->err, 2ull); g = 0; break; }
+          if (++spins > A.spin_limit) { atomicOr(&ctl->err.v, 2ull); g = 0; break; }
           __builtin_amdgcn_s_sleep(2);
-          g = ld1(&ctl->gen);
+          g = ld1(&ctl->gen.v);
         }
         sQuit = g == 0;
         seen = g;
@@ -420,9 +540,9 @@ __global__ void __launch_bounds__(SP_THREADS) k_sp_pair(SpArgs A) {
       __syncthreads();
       const PhaseView P = sP;
       if (P.op == OP_EXIT) return;
-      run_phase(A, P, (int)blockIdx.x, nwg, lds);
+      run_phase(A, P, (int)blockIdx.x, nwg, lds, &sL);
       wg_release();
-      if (threadIdx.x == 0) atomicAdd(&ctl->arrive, 1ull);
+      if (threadIdx.x == 0) atomicAdd(&ctl->arrive.v, 1ull);
       __syncthreads();
     }
   }
@@ -430,14 +550,19 @@ __global__ void __launch_bounds__(SP_THREADS) k_sp_pair(SpArgs A) {
   __shared__ unsigned long long sAcc[6];
   unsigned long long phase = 0, big_phases = 0;
   bool failed = false;
+  unsigned ntr = 0;
+  auto trace = [&](unsigned long long kind) {   // thread 0
+    if (ntr < 40) A.res->trace[ntr++] = (kind << 56) | ((unsigned long long)wall_clock64() & ((1ull << 56) - 1));
+  };
+  if (threadIdx.x == 0) trace(0);
   // run one phase: alone when small, else published to every workgroup
   auto phase_run = [&](PhaseView P, bool big) {
     if (threadIdx.x == 0) {
-      st1(&ctl->out_n, 0ull);
-      st1(&ctl->dsum, 0ull);
-      st1(&ctl->meet_n, 0ull);
-      st1(&ctl->meet_items, 0ull);
-      st1(&ctl->edges, 0ull);
+      st1(&ctl->out_n.v, 0ull);
+      st1(&ctl->dsum.v, 0ull);
+      st1(&ctl->meet_n.v, 0ull);
+      st1(&ctl->meet_items.v, 0ull);
+      st1(&ctl->edges.v, 0ull);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -454,32 +579,33 @@ __global__ void __launch_bounds__(SP_THREADS) k_sp_pair(SpArgs A) {
         ctl->mstamp = ((unsigned long long)P.L << 32) | P.mstamp;
       }
       wg_release();
-      if (threadIdx.x == 0) st1(&ctl->gen, g0 | ++phase);
+      if (threadIdx.x == 0) st1(&ctl->gen.v, g0 | ++phase);
       __syncthreads();
-      run_phase(A, P, 0, nwg, lds);
+      run_phase(A, P, 0, nwg, lds, &sL);
       ++big_phases;
       if (threadIdx.x == 0) {
         const unsigned long long want = big_phases * (unsigned long long)(nwg - 1);
         unsigned long long spins = 0;
-        while (ld1(&ctl->arrive) < want) {
-          if (++spins > A.spin_limit) { atomicOr(&ctl->err, 2ull); break; }
+        while (ld1(&ctl->arrive.v) < want) {
+          if (++spins > A.spin_limit) { atomicOr(&ctl->err.v, 2ull); break; }
           __builtin_amdgcn_s_sleep(1);
         }
       }
       __syncthreads();
       wg_acquire();
     } else {
-      run_phase(A, P, 0, 1, lds);
+      run_phase(A, P, 0, 1, lds, &sL);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
     if (threadIdx.x == 0) {
-      sAcc[0] = ld1(&ctl->out_n);
-      sAcc[1] = ld1(&ctl->dsum);
-      sAcc[2] = ld1(&ctl->meet_n);
-      sAcc[3] = ld1(&ctl->meet_items);
-      sAcc[4] = ld1(&ctl->edges);
-      sAcc[5] = ld1(&ctl->err);
+      trace((unsigned long long)P.op * 2 + (big && nwg > 1 ? 1 : 0));
+      sAcc[0] = ld1(&ctl->out_n.v);
+      sAcc[1] = ld1(&ctl->dsum.v);
+      sAcc[2] = ld1(&ctl->meet_n.v);
+      sAcc[3] = ld1(&ctl->meet_items.v);
+      sAcc[4] = ld1(&ctl->edges.v);
+      sAcc[5] = ld1(&ctl->err.v);
     }
     __syncthreads();
     failed = failed || sAcc[5] != 0;
@@ -487,10 +613,10 @@ __global__ void __launch_bounds__(SP_THREADS) k_sp_pair(SpArgs A) {
 
   // ---- set-up: labels of s and t, their items
   if (threadIdx.x == 0) {
-    st1(&ctl->arrive, 0ull);
-    st1(&ctl->err, 0ull);
-    st1(&ctl->out_n, 0ull);
-    st1(&ctl->meet_items, 0ull);
+    st1(&ctl->arrive.v, 0ull);
+    st1(&ctl->err.v, 0ull);
+    st1(&ctl->out_n.v, 0ull);
+    st1(&ctl->meet_items.v, 0ull);
     A.res->L = 0;
     A.res->edges = 0;
     A.res->err = 0;
@@ -510,6 +636,7 @@ __global__ void __launch_bounds__(SP_THREADS) k_sp_pair(SpArgs A) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (threadIdx.x == 0) trace(1);
   uint64_t nF = nis, nB = nit, dsf = nes, dsb = net, edges = 0;
   int fcur = L_F0, bcur = L_B0, kf = 0, kb = 0;
   bool met = false;
@@ -566,12 +693,17 @@ __global__ void __launch_bounds__(SP_THREADS) k_sp_pair(SpArgs A) {
     P.cur = c;
     P.L = (uint32_t)L;
     P.kf = (uint32_t)kf;
-    const bool big = deg > SP_GREEDY_SMALL && nwg > 1;
-    phase_run(P, big);
+    const bool big = deg > SP_GREEDY_SMALL && nwg > 1 && !failed;
+    Cand mine{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
+    if (big) {
+      phase_run(P, true);
+    } else {   // the leader alone: its block minimum is the answer
+      mine = greedy_scan(A, c, pos, L, kf, 0, 1, lds);
+      if (threadIdx.x == 0) trace((unsigned long long)OP_GREEDY * 2);
+    }
     if (threadIdx.x == 0) {
-      Cand best{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
-      const int parts = big ? nwg : 1;
-      for (int k = 0; k < parts; ++k) {
+      Cand best = mine;
+      for (int k = 0; big && k < nwg; ++k) {
         const unsigned long long* q = ctl->gpart + 4 * k;
         Cand x{(int64_t)ld1(q), (int64_t)ld1(q + 1), (int64_t)ld1(q + 2), (uint32_t)ld1(q + 3)};
         if (cand_less(x, best)) best = x;
@@ -588,19 +720,23 @@ __global__ void __launch_bounds__(SP_THREADS) k_sp_pair(SpArgs A) {
     __syncthreads();
     if (c == NO_ROW) {
       ok = false;
-      if (threadIdx.x == 0) atomicOr(&ctl->err, 1ull);
+      if (threadIdx.x == 0) atomicOr(&ctl->err.v, 1ull);
     }
   }
   // ---- result, release the followers
   if (threadIdx.x == 0) {
     A.res->L = ok ? (unsigned long long)L : 0ull;
     A.res->edges = edges;
-    A.res->err = ld1(&ctl->err);
+    A.res->err = ld1(&ctl->err.v);
     A.res->levels = (unsigned long long)levels;
-    ctl->op = OP_EXIT;
+    trace(15);
+    A.res->ntrace = ntr;
+    if (nwg > 1) {   // EXIT: written through (sc1) and drained before the generation word
+      st1(&ctl->op, (unsigned long long)OP_EXIT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      st1(&ctl->gen.v, g0 | ++phase);
+    }
   }
-  wg_release();
-  if (threadIdx.x == 0 && nwg > 1) st1(&ctl->gen, g0 | ++phase);
 }
 
 // ---------------------------------------------------------------------------- host side
@@ -616,6 +752,10 @@ struct SpCtx {
   hipEvent_t done = nullptr;
   unsigned long long q = 0;
   int wgs = 64;
+  // NBG_SP_TRACE=1: per phase kind, launches and device ticks (printed by sp_destroy)
+  bool tracing = false;
+  double tick_us = 0.01;
+  unsigned long long tr_n[16] = {}, tr_ticks[16] = {}, queries = 0, total_ticks = 0;
 };
 
 SpCtx* sp_create(uint64_t nv, uint64_t item_cap, hipStream_t s, std::string* err) {
@@ -625,6 +765,13 @@ SpCtx* sp_create(uint64_t nv, uint64_t item_cap, hipStream_t s, std::string* err
   c->cap = item_cap;
   const char* e = getenv("NBG_SP_WGS");
   c->wgs = e ? std::max(1, std::min(SP_MAX_WGS, atoi(e))) : 64;
+  c->tracing = getenv("NBG_SP_TRACE") && atoi(getenv("NBG_SP_TRACE")) != 0;
+  {
+    int dev = 0, khz = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0)
+      c->tick_us = 1000.0 / khz;
+  }
   hipError_t he = hipSuccess;
   auto M = [&](void** p, size_t b) { if (he == hipSuccess) he = hipMalloc(p, b); };
   for (auto& l : c->lab) M((void**)&l, (nv + 1) * 4);
@@ -647,6 +794,16 @@ SpCtx* sp_create(uint64_t nv, uint64_t item_cap, hipStream_t s, std::string* err
 
 void sp_destroy(SpCtx* c) {
   if (!c) return;
+  if (c->tracing && c->queries) {
+    static const char* names[16] = {"launch", "setup", "level", "level*", "bset", "bset*", "greedy", "greedy*",
+                                    "", "", "", "", "", "", "", "end"};
+    fprintf(stderr, "[sp trace] %llu queries, %.2f us per query on the device (* = all workgroups)\n",
+            c->queries, c->total_ticks * c->tick_us / c->queries);
+    for (int k = 1; k < 16; ++k)
+      if (c->tr_n[k])
+        fprintf(stderr, "[sp trace]   %-8s %8llu phases  %8.2f us each  %8.2f us per query\n", names[k], c->tr_n[k],
+                c->tr_ticks[k] * c->tick_us / c->tr_n[k], c->tr_ticks[k] * c->tick_us / c->queries);
+  }
   for (auto* l : c->lab)
     if (l) (void)hipFree(l);
   for (auto* l : c->list)
@@ -697,6 +854,18 @@ hipError_t sp_wait(SpCtx* c, SpResult* out) {
   }
   if (e != hipSuccess) return e;
   memcpy(out, c->h_res, sizeof(SpResult));
+  if (c->tracing && out->ntrace >= 2) {
+    const unsigned long long mask = (1ull << 56) - 1;
+    unsigned long long prev = out->trace[0] & mask;
+    for (unsigned long long i = 1; i < out->ntrace && i < 40; ++i) {
+      const unsigned long long k = out->trace[i] >> 56, t = out->trace[i] & mask;
+      c->tr_n[k & 15] += 1;
+      c->tr_ticks[k & 15] += t - prev;
+      prev = t;
+    }
+    c->total_ticks += prev - (out->trace[0] & mask);
+    ++c->queries;
+  }
   return hipSuccess;
 }
 

@@ -350,9 +350,8 @@ class Engine:
         return GoStatement(self, out)
 
     # ------------------------------------------------------------------ FIND PATH
-    def find_path(self, frm, to, etypes, upto=5, shortest=True, over_all=False, stats=None):
-        """FIND SHORTEST PATH: sorted entry lists [v0, t0, r0, v1, ...].  ``stats`` (a dict)
-        receives ``edges`` — adjacency entries scanned by both search directions."""
+    @staticmethod
+    def _path_request(frm, to, etypes, upto, shortest, over_all):
         f = np.ascontiguousarray(frm, np.int64)
         t = np.ascontiguousarray(to, np.int64)
         e = np.ascontiguousarray(etypes, np.int32)
@@ -360,8 +359,30 @@ class Engine:
             f.ctypes.data_as(C.POINTER(C.c_int64)) if len(f) else None, len(f),
             e.ctypes.data_as(C.POINTER(C.c_int32)) if len(e) else None, len(e), int(over_all),
             t.ctypes.data_as(C.POINTER(C.c_int64)) if len(t) else None, len(t), upto, int(shortest))
+        return req, (f, t, e)
+
+    def find_path_submit(self, frm, to, etypes, upto=5, shortest=True, over_all=False):
+        """nbg_find_path_submit: a one-pair SHORTEST query on a free query slot (others run now);
+        returns a ticket for :meth:`find_path_wait`."""
+        req, keep = self._path_request(frm, to, etypes, upto, shortest, over_all)
+        out = C.c_void_p()
+        self._check(self.lib.nbg_find_path_submit(self.h, C.byref(req), C.byref(out)), "find_path_submit")
+        return out
+
+    def find_path_wait(self, ticket, stats=None):
+        out = C.c_void_p()
+        self._check(self.lib.nbg_find_path_wait(ticket, C.byref(out)), "find_path_wait")
+        return self._paths(out, stats)
+
+    def find_path(self, frm, to, etypes, upto=5, shortest=True, over_all=False, stats=None):
+        """FIND SHORTEST PATH: sorted entry lists [v0, t0, r0, v1, ...].  ``stats`` (a dict)
+        receives ``edges`` — adjacency entries scanned by both search directions."""
+        req, keep = self._path_request(frm, to, etypes, upto, shortest, over_all)
         out = C.c_void_p()
         self._check(self.lib.nbg_find_path(self.h, C.byref(req), C.byref(out)), "find_path")
+        return self._paths(out, stats)
+
+    def _paths(self, out, stats):
         try:
             paths = []
             for i in range(self.lib.nbg_paths_count(out)):

@@ -145,3 +145,32 @@ def test_all_paths_too_many_is_an_error(rmat12):
     with pytest.raises(NbgError) as ex:
         eng.find_path([h], [h], [1], 12, shortest=False)
     assert ex.value.code == _lib.E_OUT_OF_MEMORY
+
+
+def test_async_path_submit_wait_parity():
+    """nbg_find_path_submit / nbg_find_path_wait: one-pair SHORTEST queries on the query slots (more
+    than there are slots, waited for out of order), plus requests that run at submission
+    (multi-source, s == t, ALL PATH); results equal the synchronous ones and the oracle's."""
+    src, dst, w = graphs.rmat_graph(11)
+    eng = graphs.rmat_engine(src, dst, w)
+    orc = graphs.rmat_oracle(src, dst, w)
+    try:
+        verts = np.union1d(src, dst)
+        rng = np.random.default_rng(17)
+        reqs = [([int(a)], [int(b)]) for a, b in zip(rng.choice(verts, 20), rng.choice(verts, 20))]
+        reqs.append((reqs[0][0] + reqs[1][0], reqs[2][1]))   # two sources
+        reqs.append((reqs[3][0], reqs[3][0]))                 # s == t
+        tickets = [eng.find_path_submit(f, t, [1], 4) for f, t in reqs]
+        got = {}
+        for i in list(range(len(reqs)))[::-1]:
+            st = {}
+            got[i] = (eng.find_path_wait(tickets[i], stats=st), st["edges"])
+        for i, (f, t) in enumerate(reqs):
+            exp = sorted(orc.find_path(f, t, [1], 4, True, mode=1))
+            assert got[i][0] == exp, (f, t)
+            assert got[i][0] == eng.find_path(f, t, [1], 4)
+        all_t = eng.find_path_submit(reqs[4][0], reqs[4][1], [1], 3, shortest=False)
+        assert eng.find_path_wait(all_t) == eng.find_path(reqs[4][0], reqs[4][1], [1], 3, shortest=False)
+    finally:
+        eng.close()
+        orc.close()
