@@ -309,6 +309,7 @@ struct SpResult {                    // one query's result block (device, copied
   // phase trace (wall_clock64 ticks): trace[0] = launch start, then (kind << 56 | tick) per phase
   unsigned long long ntrace;
   unsigned long long trace[40];
+  unsigned long long sub[8];         // ticks of run_level's sub-steps on the leader (NBG_SP_TRACE)
 };
 struct SpCtx;                        // labels, item lists, control block, result block of one slot
 // item_cap: items a list may hold = sum over a side's types of (nv + E_t / 64), plus slack

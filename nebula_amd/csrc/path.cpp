@@ -279,9 +279,12 @@ int32_t device_pair(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_paths
   return NBG_OK;
 }
 
+// The multi-launch path (bidirectional above) is the default for one pair: measured faster than
+// the persistent search at RMAT-26 so far (profiles/r02_*_probe*).  NBG_SP_PERSISTENT=1 selects
+// the persistent kernel.
 bool sp_legacy() {
-  static const bool v = getenv("NBG_SP_LEGACY") && atoi(getenv("NBG_SP_LEGACY")) != 0;
-  return v;
+  const char* e = getenv("NBG_SP_PERSISTENT");   // (read per query: tests switch it)
+  return !(e && atoi(e) != 0);
 }
 
 // S: this rank's sources (local ids); Tg: every target, by global position, as a local id

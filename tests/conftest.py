@@ -23,3 +23,14 @@ def nba_data():
     import json
     with open(os.path.join(ROOT, "tests", "golden", "nba.json")) as f:
         return json.load(f)
+
+
+@pytest.fixture(params=["multi-launch", "persistent"])
+def sp_mode(request, monkeypatch):
+    """Both one-pair FIND SHORTEST PATH device paths: the multi-launch level loop (default) and
+    the persistent one-launch search (NBG_SP_PERSISTENT=1, read per query)."""
+    if request.param == "persistent":
+        monkeypatch.setenv("NBG_SP_PERSISTENT", "1")
+    else:
+        monkeypatch.delenv("NBG_SP_PERSISTENT", raising=False)
+    return request.param

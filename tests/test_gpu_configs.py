@@ -93,7 +93,7 @@ def _check_pairs(eng, csr, pairs, upto=5):
     return found
 
 
-def test_c4_shortest_pairs_rmat22(rmat22):
+def test_c4_shortest_pairs_rmat22(rmat22, sp_mode):
     src, dst, eng, csr, _, av = rmat22
     pairs = rmat.pick_pairs(src, dst, 256, 7, verts=av)
     found = _check_pairs(eng, csr, pairs)
@@ -131,7 +131,7 @@ def test_c3_rmat26_digests(rmat26):
 
 
 @pytest.mark.timeout(600)
-def test_c4_shortest_pairs_rmat26(rmat26):
+def test_c4_shortest_pairs_rmat26(rmat26, sp_mode):
     src, dst, eng, csr, _, av = rmat26
     pairs = rmat.pick_pairs(src, dst, 64, 7, verts=av)
     assert _check_pairs(eng, csr, pairs) > 20

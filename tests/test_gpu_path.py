@@ -50,7 +50,7 @@ def pairs(src, dst, k, seed=7):
 
 
 @pytest.mark.parametrize("upto", [1, 2, 3, 5])
-def test_rmat_shortest_single_pairs(rmat12, upto):
+def test_rmat_shortest_single_pairs(rmat12, upto, sp_mode):
     """One source, one target: the bidirectional search."""
     src, dst, eng, orc = rmat12
     found = 0
@@ -65,7 +65,7 @@ def test_rmat_shortest_single_pairs(rmat12, upto):
         assert found > 0
 
 
-def test_rmat_shortest_self_and_unknown(rmat12):
+def test_rmat_shortest_self_and_unknown(rmat12, sp_mode):
     """s == t needs a cycle (walk length >= 1); unknown vids have no rows."""
     src, dst, eng, orc = rmat12
     for s, _ in pairs(src, dst, 8, seed=11):
@@ -147,7 +147,7 @@ def test_all_paths_too_many_is_an_error(rmat12):
     assert ex.value.code == _lib.E_OUT_OF_MEMORY
 
 
-def test_async_path_submit_wait_parity():
+def test_async_path_submit_wait_parity(sp_mode):
     """nbg_find_path_submit / nbg_find_path_wait: one-pair SHORTEST queries on the query slots (more
     than there are slots, waited for out of order), plus requests that run at submission
     (multi-source, s == t, ALL PATH); results equal the synchronous ones and the oracle's."""

@@ -41,17 +41,22 @@ for step in "$@"; do
     ptest)
       timeout -k 10 400 python -u -m pytest tests/test_gpu_path.py tests/test_gpu_configs.py -x -v --timeout 300 \
         --timeout-method thread > "$OUT/pytest_path.log" 2>&1 || { tail -40 "$OUT/pytest_path.log"; exit 1; } ;;
-    sp26|sp26legacy)
-      [ "$step" = sp26legacy ] && export NBG_SP_LEGACY=1
+    sp26|sp26persistent)
+      [ "$step" = sp26persistent ] && export NBG_SP_PERSISTENT=1
       timeout -k 10 600 python -u bench.py --steps 1 --warmup 1 --no-profile --no-cpu-baseline --verify 4 --c2 0 \
         --c5-scale 0 --getbound-reqs 0 > "$OUT/$step.json" 2> "$OUT/$step.log" || { tail -30 "$OUT/$step.log"; exit 1; }
-      unset NBG_SP_LEGACY ;;
+      unset NBG_SP_PERSISTENT ;;
     probe22|probe26)
       sc=${step#probe}
-      NBG_SP_TRACE=1 timeout -k 10 300 python -u tools/sp_probe.py $sc 4000 > "$OUT/$step.txt" 2>&1 \
+      NBG_SP_PERSISTENT=1 NBG_SP_TRACE=1 timeout -k 10 300 python -u tools/sp_probe.py $sc 4000 > "$OUT/$step.txt" 2>&1 \
         || { tail -30 "$OUT/$step.txt"; exit 1; }
-      NBG_SP_LEGACY=1 timeout -k 10 300 python -u tools/sp_probe.py $sc 4000 > "$OUT/${step}_legacy.txt" 2>&1 \
+      timeout -k 10 300 python -u tools/sp_probe.py $sc 4000 > "$OUT/${step}_legacy.txt" 2>&1 \
         || { tail -30 "$OUT/${step}_legacy.txt"; exit 1; } ;;
+    wgs26)   # persistent SP: workgroup-count sweep
+      for w in 1 8 32 64 128; do
+        NBG_SP_PERSISTENT=1 NBG_SP_WGS=$w NBG_SP_TRACE=1 timeout -k 10 300 python -u tools/sp_probe.py 26 1500 > "$OUT/wgs26_$w.txt" 2>&1 \
+          || { tail -30 "$OUT/wgs26_$w.txt"; exit 1; }
+      done ;;
     bench)
       timeout -k 10 900 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.log" || { tail -30 "$OUT/bench.log"; exit 1; } ;;
   esac
