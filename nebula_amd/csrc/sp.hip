@@ -251,7 +251,7 @@ __device__ __forceinline__ uint32_t lane_items(const SpTypes& T, const uint32_t 
 // items (SP_U per wave; lane l owns entry l of each item).  Per pass: every neighbour's labels in
 // flight at once, the CAS claims, the claimed vertices' row ranges, then ONE atomic per workgroup
 // reserves the pass's output items (block scan in LDS).
-__device__ void run_level(const SpArgs& A, const LevelCfg& C, const uint64_t* src, uint64_t n, uint64_t* dst,
+__device__ __forceinline__ void run_level(const SpArgs& A, const LevelCfg& C, const uint64_t* src, uint64_t n, uint64_t* dst,
                           int wg, int nwg, LevelLds* L) {
   SpCtl* ctl = A.ctl;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -441,7 +441,7 @@ __device__ __forceinline__ bool cand_less(const Cand& a, const Cand& b) {
 }
 
 // Greedy hop `pos` from vertex c: the minimum (type, rank, dst vid) out-edge into B[pos + 1].
-__device__ Cand greedy_scan(const SpArgs& A, const SpQ& Q, uint32_t c, int pos, int L, int kf, int wg, int nwg,
+__device__ __forceinline__ Cand greedy_scan(const SpArgs& A, const SpQ& Q, uint32_t c, int pos, int L, int kf, int wg, int nwg,
                             Cand* lds) {
   const Cand none{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
   Cand best = none;
@@ -520,10 +520,22 @@ struct PhaseView {   // the leader's phase parameters, as every workgroup reads 
   uint32_t L, kf;
 };
 
-__device__ void run_phase(const SpArgs& A, const SpQ& Q, const PhaseView& P, int wg, int nwg, Cand* lds,
-                          LevelLds* L) {
+__device__ __forceinline__ void run_phase(const SpArgs& A, const SpQ& Q, const PhaseView& P, int wg, int nwg,
+                                          Cand* lds, LevelLds* L) {
+  if (P.op == OP_GREEDY) {
+    Cand b = greedy_scan(A, Q, P.cur, (int)P.pos, (int)P.L, (int)P.kf, wg, nwg, lds);
+    if (threadIdx.x == 0) {
+      unsigned long long* part = A.ctl->gpart + 4 * wg;
+      part[0] = (unsigned long long)b.t;
+      part[1] = (unsigned long long)b.r;
+      part[2] = (unsigned long long)b.v;
+      part[3] = b.d;
+    }
+    return;
+  }
+  if (P.op != OP_LEVEL && P.op != OP_BSET) return;
+  LevelCfg C{};
   if (P.op == OP_LEVEL) {
-    LevelCfg C{};
     const bool fw = P.side == 0;
     C.T = fw ? &A.fwd : &A.bwd;
     C.N = C.T;
@@ -535,10 +547,8 @@ __device__ void run_phase(const SpArgs& A, const SpQ& Q, const PhaseView& P, int
     C.oepoch = fw ? Q.eb : Q.ef;
     C.mstamp = P.mstamp;
     C.append = true;
-    run_level(A, C, A.list[P.src], P.n, A.list[P.dst], wg, nwg, L);
-  } else if (P.op == OP_BSET) {
+  } else {
     // B[pos] from B[pos + 1] through in-edges, restricted to forward level pos, claimed in LAB_M
-    LevelCfg C{};
     C.T = &A.bwd;
     C.N = &A.bwd;
     C.lab = A.lab_m;
@@ -547,17 +557,8 @@ __device__ void run_phase(const SpArgs& A, const SpQ& Q, const PhaseView& P, int
     C.rlab = A.lab_f;
     C.rstamp = stamp_of(Q.ef, P.pos);
     C.append = P.pos >= 2;   // B[1]'s in-edges are not needed (B[0] = {s})
-    run_level(A, C, A.list[P.src], P.n, A.list[P.dst], wg, nwg, L);
-  } else if (P.op == OP_GREEDY) {
-    Cand b = greedy_scan(A, Q, P.cur, (int)P.pos, (int)P.L, (int)P.kf, wg, nwg, lds);
-    if (threadIdx.x == 0) {
-      unsigned long long* part = A.ctl->gpart + 4 * wg;
-      part[0] = (unsigned long long)b.t;
-      part[1] = (unsigned long long)b.r;
-      part[2] = (unsigned long long)b.v;
-      part[3] = b.d;
-    }
   }
+  run_level(A, C, A.list[P.src], P.n, A.list[P.dst], wg, nwg, L);
 }
 
 }  // namespace

@@ -52,6 +52,9 @@ for step in "$@"; do
         || { tail -30 "$OUT/$step.txt"; exit 1; }
       timeout -k 10 300 python -u tools/sp_probe.py $sc 4000 > "$OUT/${step}_legacy.txt" 2>&1 \
         || { tail -30 "$OUT/${step}_legacy.txt"; exit 1; } ;;
+    spprof26)   # kernel trace of the one-pair SP queries (default path)
+      timeout -k 10 600 rocprofv3 --kernel-trace -d "$OUT/spprof26" -o run --output-format csv -- \
+        python3 -u tools/sp_probe.py 26 400 > "$OUT/spprof26.txt" 2>&1 || { tail -30 "$OUT/spprof26.txt"; exit 1; } ;;
     wgs26)   # persistent SP: workgroup-count sweep
       for w in 1 8 32 64 128; do
         NBG_SP_PERSISTENT=1 NBG_SP_WGS=$w NBG_SP_TRACE=1 timeout -k 10 300 python -u tools/sp_probe.py 26 1500 > "$OUT/wgs26_$w.txt" 2>&1 \
