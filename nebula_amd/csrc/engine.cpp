@@ -54,6 +54,12 @@ uint64_t Engine::sp_item_cap() const {
   return snap.nv * std::max<uint64_t>(pos_types, 1) + std::max(e_out, e_in) / 64 + 1024;
 }
 
+uint64_t Engine::sp_edge_cap() const {
+  uint64_t e_out = 0, e_in = 0;
+  for (auto& kv : snap.types) (kv.first > 0 ? e_out : e_in) += kv.second.num_edges;
+  return std::max(e_out, e_in) + 1;
+}
+
 uint32_t Engine::dense(int64_t vid) const {
   auto& v = snap.h_vids;
   auto it = std::lower_bound(v.begin(), v.end(), vid);

@@ -44,6 +44,7 @@ struct Engine {
   std::vector<PathSlot> path_slots;
   std::vector<void*> path_inflight;
   uint64_t sp_item_cap() const;         // items a shortest-path list may hold
+  uint64_t sp_edge_cap() const;         // edges of the larger direction (a level's edge space)
   std::vector<void*> inflight;          // submitted tickets, oldest first
   // device GO results (rows left in HBM) and the workspace their rows live in: before that
   // workspace runs another query it is handed to the result (freed with it) and replaced

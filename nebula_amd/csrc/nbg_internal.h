@@ -313,12 +313,22 @@ struct SpResult {                    // one query's result block (device, copied
 };
 struct SpCtx;                        // labels, item lists, control block, result block of one slot
 // item_cap: items a list may hold = sum over a side's types of (nv + E_t / 64), plus slack
-SpCtx* sp_create(uint64_t nv, uint64_t item_cap, hipStream_t s, std::string* err);
+// One query at a time per context; the device buffers of each mode are allocated on its first use.
+enum SpMode : int { SP_PERSISTENT = 0, SP_CHAIN = 1 };
+SpCtx* sp_create(uint64_t nv, uint64_t item_cap, uint64_t edge_cap, hipStream_t s, std::string* err);
 void sp_destroy(SpCtx* c);
-// enqueue the persistent search for s -> t (local dense ids, s != t) and its result copy
-hipError_t sp_launch(SpCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible, const int64_t* vids,
-                     uint32_t s, uint32_t t, uint32_t upto);
+// enqueue the search for s -> t (local dense ids, s != t) and its result copy: SP_PERSISTENT = one
+// persistent launch (sp.hip), SP_CHAIN = the device-driven level loop (spchain.hip, one OVER type)
+hipError_t sp_launch(SpCtx* c, int mode, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible,
+                     const int64_t* vids, uint32_t s, uint32_t t, uint32_t upto);
 bool sp_ready(SpCtx* c);
+struct ChainCtx;
+ChainCtx* chain_create(uint64_t nv, uint64_t edge_cap, hipStream_t s, std::string* err);
+void chain_destroy(ChainCtx* c);
+hipError_t chain_launch(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible,
+                        const int64_t* vids, uint32_t* const lab[3], uint32_t epoch, uint32_t s, uint32_t t,
+                        uint32_t upto);
+void chain_result(const ChainCtx* c, SpResult* out);
 hipError_t sp_wait(SpCtx* c, SpResult* out);
 
 // ----------------------------------------------------------------------------- collectives (comm.cpp)

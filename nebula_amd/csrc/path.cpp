@@ -36,6 +36,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <unordered_set>
 
@@ -260,15 +261,15 @@ SpTypes sp_types(const PathTypes& pt) {
   return T;
 }
 
-int32_t device_pair(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_paths* out) {
+int32_t device_pair(PathCtx& c, int mode, uint32_t s, uint32_t t, uint32_t upto, nbg_paths* out) {
   Engine& E = c.E;
   if (!E.sp) {
     std::string err;
-    E.sp = sp_create(E.snap.nv, E.sp_item_cap(), E.stream, &err);
+    E.sp = sp_create(E.snap.nv, E.sp_item_cap(), E.sp_edge_cap(), E.stream, &err);
     if (!E.sp) return E.fail(NBG_E_OUT_OF_MEMORY, err);
   }
   if (!host_degree(c, c.fwd, s) || !host_degree(c, c.bwd, t)) return NBG_OK;   // an endpoint without edges
-  hipError_t he = sp_launch(E.sp, sp_types(c.fwd), sp_types(c.bwd), E.snap.d_visible, E.snap.d_vids, s, t, upto);
+  hipError_t he = sp_launch(E.sp, mode, sp_types(c.fwd), sp_types(c.bwd), E.snap.d_visible, E.snap.d_vids, s, t, upto);
   SpResult r;
   if (he == hipSuccess) he = sp_wait(E.sp, &r);
   if (he != hipSuccess) return dev_fail(E, he, "shortest path");
@@ -279,12 +280,19 @@ int32_t device_pair(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_paths
   return NBG_OK;
 }
 
-// The multi-launch path (bidirectional above) is the default for one pair: measured faster than
-// the persistent search at RMAT-26 so far (profiles/r02_*_probe*).  NBG_SP_PERSISTENT=1 selects
-// the persistent kernel.
-bool sp_legacy() {
-  const char* e = getenv("NBG_SP_PERSISTENT");   // (read per query: tests switch it)
-  return !(e && atoi(e) != 0);
+// One-pair SHORTEST on a single engine.  NBG_SP_MODE (read per query: tests switch it):
+//   chain (default) - the device-driven level loop (spchain.hip): one host round trip per pair;
+//                     one OVER type per direction, other requests take the host loop
+//   persistent      - one persistent launch (sp.hip); NBG_SP_PERSISTENT=1 means the same
+//   host            - the host-driven level loop (bidirectional above), one round trip per level
+enum PairMode { PM_HOST = -1 };
+int sp_mode(const PathCtx& c) {
+  const char* p = getenv("NBG_SP_PERSISTENT");
+  if (p && atoi(p) != 0) return SP_PERSISTENT;
+  const char* m = getenv("NBG_SP_MODE");
+  if (m && !strcmp(m, "host")) return PM_HOST;
+  if (m && !strcmp(m, "persistent")) return SP_PERSISTENT;
+  return c.fwd.n == 1 && c.bwd.n == 1 ? SP_CHAIN : PM_HOST;
 }
 
 // S: this rank's sources (local ids); Tg: every target, by global position, as a local id
@@ -400,6 +408,7 @@ int32_t all_paths(PathCtx& c, const std::vector<uint32_t>& S, const std::vector<
 
 // A one-pair SHORTEST request handed to a query slot instead of being run here.
 struct PairLaunch {
+  int mode = SP_CHAIN;
   SpTypes fwd, bwd;
   uint32_t s = NO_ROW, t = NO_ROW, upto = 0;
 };
@@ -504,9 +513,11 @@ int32_t find_path_locked(Engine& E, const nbg_path_request* rq, nbg_paths** out,
     add(c.bwd, -t);
   }
   const bool pair = rq->shortest && Sv.size() == 1 && Tv.size() == 1 && Sv[0] != Tv[0];
-  if (pair && !c.part && !sp_legacy()) {
+  const int pmode = pair && !c.part ? sp_mode(c) : PM_HOST;
+  if (pmode != PM_HOST) {
     const uint32_t s0 = S.empty() ? NO_ROW : S[0];
     if (pl && host_degree(c, c.fwd, s0) && host_degree(c, c.bwd, Tg[0])) {
+      pl->mode = pmode;
       pl->fwd = sp_types(c.fwd);
       pl->bwd = sp_types(c.bwd);
       pl->s = s0;
@@ -515,7 +526,7 @@ int32_t find_path_locked(Engine& E, const nbg_path_request* rq, nbg_paths** out,
       delete res;
       return PAIR_DEFERRED;
     }
-    int32_t rc = device_pair(c, s0, Tg[0], rq->upto, res);
+    int32_t rc = device_pair(c, pmode, s0, Tg[0], rq->upto, res);
     if (rc) { delete res; return rc; }
     res->edges = c.edges;
     *out = res;
@@ -645,10 +656,10 @@ int32_t nbg_find_path_submit(nbg_engine* h, const nbg_path_request* rq, nbg_path
   }
   if (!ps.sp) {
     std::string err;
-    ps.sp = sp_create(E.snap.nv, E.sp_item_cap(), ps.stream, &err);
+    ps.sp = sp_create(E.snap.nv, E.sp_item_cap(), E.sp_edge_cap(), ps.stream, &err);
     if (!ps.sp) { delete t; return E.fail(NBG_E_OUT_OF_MEMORY, err); }
   }
-  hipError_t he = sp_launch(ps.sp, pl.fwd, pl.bwd, E.snap.d_visible, E.snap.d_vids, pl.s, pl.t, pl.upto);
+  hipError_t he = sp_launch(ps.sp, pl.mode, pl.fwd, pl.bwd, E.snap.d_visible, E.snap.d_vids, pl.s, pl.t, pl.upto);
   if (he != hipSuccess) { delete t; return dev_fail(E, he, "shortest path"); }
   t->slot = slot;
   ps.ticket = t;

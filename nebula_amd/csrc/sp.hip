@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -812,7 +813,9 @@ __global__ void __launch_bounds__(SP_THREADS) k_sp_pair(const SpArgs* __restrict
 // ---------------------------------------------------------------------------- host side
 struct SpCtx {
   hipStream_t stream = nullptr;
-  uint64_t nv = 0, cap = 0;
+  uint64_t nv = 0, cap = 0, edge_cap = 0;
+  ChainCtx* chain = nullptr;       // the level-loop buffers (first SP_CHAIN query)
+  int mode = SP_PERSISTENT;        // of the query in flight
   uint32_t* lab[3] = {};
   uint32_t epoch = 0;
   uint64_t* list[SP_NLISTS] = {};
@@ -830,13 +833,16 @@ struct SpCtx {
   bool tracing = false;
   double tick_us = 0.01;
   unsigned long long tr_n[16] = {}, tr_ticks[16] = {}, queries = 0, total_ticks = 0, sub[8] = {};
+  double host_us = 0;              // level loop: host time enqueueing a query's chain
+  unsigned long long host_n = 0;
 };
 
-SpCtx* sp_create(uint64_t nv, uint64_t item_cap, hipStream_t s, std::string* err) {
+SpCtx* sp_create(uint64_t nv, uint64_t item_cap, uint64_t edge_cap, hipStream_t s, std::string* err) {
   auto* c = new SpCtx();
   c->stream = s;
   c->nv = nv;
   c->cap = item_cap;
+  c->edge_cap = edge_cap;
   const char* e = getenv("NBG_SP_WGS");
   c->wgs = e ? std::max(1, std::min(SP_MAX_WGS, atoi(e))) : 64;
   c->tracing = getenv("NBG_SP_TRACE") && atoi(getenv("NBG_SP_TRACE")) != 0;
@@ -849,7 +855,6 @@ SpCtx* sp_create(uint64_t nv, uint64_t item_cap, hipStream_t s, std::string* err
   hipError_t he = hipSuccess;
   auto M = [&](void** p, size_t b) { if (he == hipSuccess) he = hipMalloc(p, b); };
   for (auto& l : c->lab) M((void**)&l, (nv + 1) * 4);
-  for (auto& l : c->list) M((void**)&l, std::max<uint64_t>(item_cap, 1) * 8);
   M((void**)&c->ctl, sizeof(SpCtl));
   M((void**)&c->d_res, sizeof(SpResult));
   M((void**)&c->d_args, sizeof(SpArgs));
@@ -870,6 +875,9 @@ SpCtx* sp_create(uint64_t nv, uint64_t item_cap, hipStream_t s, std::string* err
 
 void sp_destroy(SpCtx* c) {
   if (!c) return;
+  if (c->tracing && c->host_n)
+    fprintf(stderr, "[sp trace] level loop: %llu queries, %.2f us host enqueue each\n", c->host_n,
+            c->host_us / c->host_n);
   if (c->tracing && c->queries) {
     static const char* names[16] = {"launch", "setup", "level", "level*", "bset", "bset*", "greedy", "greedy*",
                                     "", "", "", "", "", "", "", "end"};
@@ -890,6 +898,7 @@ void sp_destroy(SpCtx* c) {
     if (l) (void)hipFree(l);
   for (auto* l : c->list)
     if (l) (void)hipFree(l);
+  chain_destroy(c->chain);
   if (c->ctl) (void)hipFree(c->ctl);
   if (c->d_args) (void)hipFree(c->d_args);
   if (c->h_args) (void)hipHostFree(c->h_args);
@@ -899,12 +908,32 @@ void sp_destroy(SpCtx* c) {
   delete c;
 }
 
-hipError_t sp_launch(SpCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible, const int64_t* vids,
-                     uint32_t s, uint32_t t, uint32_t upto) {
+hipError_t sp_launch(SpCtx* c, int mode, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible,
+                     const int64_t* vids, uint32_t s, uint32_t t, uint32_t upto) {
   if (upto > MAX_PATH_LEN || s == NO_ROW || t == NO_ROW) return hipErrorInvalidValue;
   if (++c->epoch >= (1u << (32 - LVL_BITS))) {   // wrap: clear the labels once
     for (auto* l : c->lab) HIP_TRY_SP(hipMemsetAsync(l, 0, (c->nv + 1) * 4, c->stream));
     c->epoch = 1;
+  }
+  c->mode = mode;
+  if (mode == SP_CHAIN) {
+    if (!c->chain) {
+      std::string err;
+      c->chain = chain_create(c->nv, c->edge_cap, c->stream, &err);
+      if (!c->chain) return hipErrorOutOfMemory;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    HIP_TRY_SP(chain_launch(c->chain, fwd, bwd, visible, vids, c->lab, c->epoch, s, t, upto));
+    const hipError_t e = hipEventRecord(c->done, c->stream);
+    if (c->tracing) {
+      c->host_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+      ++c->host_n;
+    }
+    return e;
+  }
+  if (!c->list[0]) {
+    HIP_TRY_SP(hipStreamSynchronize(c->stream));
+    for (auto& l : c->list) HIP_TRY_SP(hipMalloc((void**)&l, std::max<uint64_t>(c->cap, 1) * 8));
   }
   SpArgs a;
   memset(&a, 0, sizeof(a));   // compared bytewise: no indeterminate padding
@@ -947,6 +976,10 @@ hipError_t sp_wait(SpCtx* c, SpResult* out) {
   while ((e = hipEventQuery(c->done)) == hipErrorNotReady) {
   }
   if (e != hipSuccess) return e;
+  if (c->mode == SP_CHAIN) {
+    chain_result(c->chain, out);
+    return hipSuccess;
+  }
   memcpy(out, c->h_res, sizeof(SpResult));
   if (c->tracing && out->ntrace >= 2) {
     const unsigned long long mask = (1ull << 56) - 1;

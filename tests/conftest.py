@@ -25,12 +25,10 @@ def nba_data():
         return json.load(f)
 
 
-@pytest.fixture(params=["multi-launch", "persistent"])
+@pytest.fixture(params=["chain", "host", "persistent"])
 def sp_mode(request, monkeypatch):
-    """Both one-pair FIND SHORTEST PATH device paths: the multi-launch level loop (default) and
-    the persistent one-launch search (NBG_SP_PERSISTENT=1, read per query)."""
-    if request.param == "persistent":
-        monkeypatch.setenv("NBG_SP_PERSISTENT", "1")
-    else:
-        monkeypatch.delenv("NBG_SP_PERSISTENT", raising=False)
+    """Every one-pair FIND SHORTEST PATH device path (NBG_SP_MODE, read per query): the
+    device-driven level loop (default), the host-driven level loop and the persistent search."""
+    monkeypatch.delenv("NBG_SP_PERSISTENT", raising=False)
+    monkeypatch.setenv("NBG_SP_MODE", request.param)
     return request.param

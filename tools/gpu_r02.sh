@@ -41,16 +41,16 @@ for step in "$@"; do
     ptest)
       timeout -k 10 400 python -u -m pytest tests/test_gpu_path.py tests/test_gpu_configs.py -x -v --timeout 300 \
         --timeout-method thread > "$OUT/pytest_path.log" 2>&1 || { tail -40 "$OUT/pytest_path.log"; exit 1; } ;;
-    sp26|sp26persistent)
-      [ "$step" = sp26persistent ] && export NBG_SP_PERSISTENT=1
+    sp26|sp26host)
+      [ "$step" = sp26host ] && export NBG_SP_MODE=host
       timeout -k 10 600 python -u bench.py --steps 1 --warmup 1 --no-profile --no-cpu-baseline --verify 4 --c2 0 \
         --c5-scale 0 --getbound-reqs 0 > "$OUT/$step.json" 2> "$OUT/$step.log" || { tail -30 "$OUT/$step.log"; exit 1; }
-      unset NBG_SP_PERSISTENT ;;
+      unset NBG_SP_MODE ;;
     probe22|probe26)
       sc=${step#probe}
-      NBG_SP_PERSISTENT=1 NBG_SP_TRACE=1 timeout -k 10 300 python -u tools/sp_probe.py $sc 4000 > "$OUT/$step.txt" 2>&1 \
+      timeout -k 10 300 python -u tools/sp_probe.py $sc 4000 > "$OUT/$step.txt" 2>&1 \
         || { tail -30 "$OUT/$step.txt"; exit 1; }
-      timeout -k 10 300 python -u tools/sp_probe.py $sc 4000 > "$OUT/${step}_legacy.txt" 2>&1 \
+      NBG_SP_MODE=host timeout -k 10 300 python -u tools/sp_probe.py $sc 4000 > "$OUT/${step}_legacy.txt" 2>&1 \
         || { tail -30 "$OUT/${step}_legacy.txt"; exit 1; } ;;
     spprof26)   # kernel trace of the one-pair SP queries (default path)
       timeout -k 10 600 rocprofv3 --kernel-trace -d "$OUT/spprof26" -o run --output-format csv -- \
