@@ -328,6 +328,7 @@ void chain_destroy(ChainCtx* c);
 hipError_t chain_launch(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible,
                         const int64_t* vids, uint32_t* const lab[3], uint32_t epoch, uint32_t s, uint32_t t,
                         uint32_t upto);
+bool chain_more(ChainCtx* c, hipError_t* he);   // false: a continuation batch was enqueued
 void chain_result(const ChainCtx* c, SpResult* out);
 hipError_t sp_wait(SpCtx* c, SpResult* out);
 

@@ -285,14 +285,14 @@ int32_t device_pair(PathCtx& c, int mode, uint32_t s, uint32_t t, uint32_t upto,
 //                     one OVER type per direction, other requests take the host loop
 //   persistent      - one persistent launch (sp.hip); NBG_SP_PERSISTENT=1 means the same
 //   host            - the host-driven level loop (bidirectional above), one round trip per level
-enum PairMode { PM_HOST = -1 };
+constexpr int PM_HOST = -1;
 int sp_mode(const PathCtx& c) {
   const char* p = getenv("NBG_SP_PERSISTENT");
   if (p && atoi(p) != 0) return SP_PERSISTENT;
   const char* m = getenv("NBG_SP_MODE");
   if (m && !strcmp(m, "host")) return PM_HOST;
   if (m && !strcmp(m, "persistent")) return SP_PERSISTENT;
-  return c.fwd.n == 1 && c.bwd.n == 1 ? SP_CHAIN : PM_HOST;
+  return c.fwd.n == 1 && c.bwd.n == 1 ? (int)SP_CHAIN : PM_HOST;
 }
 
 // S: this rank's sources (local ids); Tg: every target, by global position, as a local id

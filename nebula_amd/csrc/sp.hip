@@ -977,6 +977,13 @@ hipError_t sp_wait(SpCtx* c, SpResult* out) {
   }
   if (e != hipSuccess) return e;
   if (c->mode == SP_CHAIN) {
+    while (!chain_more(c->chain, &e)) {   // a continuation batch: wait for it too
+      if (e == hipSuccess) e = hipEventRecord(c->done, c->stream);
+      if (e != hipSuccess) return e;
+      while ((e = hipEventQuery(c->done)) == hipErrorNotReady) {
+      }
+      if (e != hipSuccess) return e;
+    }
     chain_result(c->chain, out);
     return hipSuccess;
   }

@@ -2,21 +2,29 @@
 //
 // Same semantics and result as path.cpp's bidirectional() (FindPathExecutor.cpp:173-290
 // restated: minimal hop count, UPTO N, one path per target, ties broken by the lexicographically
-// smallest entry list [v0, t0, r0, v1, ...]).  The host enqueues a FIXED chain per pair —
-//   k_ch_setup, UPTO x k_ch_level(BFS), UPTO-1 x k_ch_level(B-set), UPTO x k_ch_hop, one copy —
-// and waits once.  Every launch reads what it has to do (the direction, the frontier list, its
-// stamps, whether the search is over) from a device state block (ChState) that the LAST
-// workgroup of the previous launch wrote (ticket counter), so no launch waits for the host and
-// launches past the end of the search return at once.
+// smallest entry list [v0, t0, r0, v1, ...]).  The host enqueues a chain per pair —
+//   k_ch_setup, K x k_ch_step, H x k_ch_hop, one copy of the state —
+// and waits once.  Step launch i derives what it does from the state snapshot of launch i - 1
+// (snap[i - 1]) and that launch's results (its output-list and meet counters, lacc / lmeet[i - 1]),
+// which are final at the launch boundary: the BFS level loop (direction = the side with the
+// smaller edge total, meet / empty / UPTO tests), then the B-set steps, then nothing (a launch
+// past the end returns at once).  Workgroup 0 stores the derived snapshot for launch i + 1, so no
+// launch waits for the host or for a last-workgroup ticket.  K and H follow the recent queries
+// (steps and path lengths seen); a query that needs more gets a continuation batch.
 //
 // Frontier lists carry their edge space (the packed-atomic protocol of kernels.hip's lists):
 // entry i = vertex ids[i], its edges at positions [seg_end[i] - deg, seg_end[i]) of the list's
 // edge space starting at CSR row seg_rs[i], plus the merge-path split of every TILE boundary
 // (tsplit).  A vertex is appended with its edge space when it is CLAIMED (CAS on its label), so
 // a level is one launch: merge-path tiles over (entries + edges), neighbour gather, claims,
-// appends.  One OVER type per direction (path.cpp sends other requests to the host loop).
+// appends.  The first B-set step (B[kf - 1] from the meet set B[kf]) runs either way round:
+// push = the in-edges of B[kf] into forward level kf - 1, pull = the out-edges of forward level
+// kf - 1 into B[kf], whichever edge total is smaller (same set).  One OVER type per direction
+// (path.cpp sends other requests to the host loop).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
 #include <cstddef>
 #include <cstring>
 #include <string>
@@ -38,10 +46,10 @@ constexpr int CH_VT = 8;                  // merge-path items per lane per tile
 constexpr int CH_TILE = 64 * CH_VT;       // items (entries + edges) per wave tile
 constexpr int CH_HOP_WGS = 64;            // workgroups scanning one greedy hop
 constexpr int CH_HOP_U = 4;               // neighbours per thread in flight (greedy)
+constexpr int CH_MAXS = 2 * MAX_PATH_LEN + 2;   // step launches of one query, at most
 
 enum ChListId : int { CL_F0 = 0, CL_F1 = 1, CL_B0 = 2, CL_B1 = 3, CL_M = 4, CH_NLISTS = 5 };
-// B-set lists reuse the forward lists (the forward frontier is dead once the sides met)
-constexpr int CL_S0 = CL_F0;
+enum ChPhase : uint32_t { PH_BFS = 0, PH_BSET = 1, PH_DONE = 2 };
 
 }  // namespace
 
@@ -52,16 +60,24 @@ struct ChList {
   uint32_t* tsplit;     // merge-path split per tile
 };
 
-struct ChState {        // device; the prefix up to gpart is copied back per query
-  unsigned long long acc[CH_NLISTS];   // packed (entries << 32 | edges) per list
-  unsigned long long meets;            // meet vertices of the meeting level
-  unsigned long long ticket;           // workgroups done (the last one does the bookkeeping)
-  unsigned long long edges;            // BFS edges expanded
-  unsigned long long err;              // 1 reconstruction failure, 3 list overflow
+struct ChSnap {         // the search state before one step launch
+  uint32_t phase, kf, kb, dir, met, L, bstep, err;
+  uint32_t cur[2];                     // current list of each side (F0/F1, B0/B1)
+  unsigned long long cnt[2];           // packed (entries << 32 | edges) of each side's current list
+  unsigned long long fprev;            // ... of the forward list one level back
+  unsigned long long bcnt;             // ... of the B-set step's source list
+  unsigned long long edges;            // BFS edges expanded so far
   unsigned long long levels;
-  unsigned long long gticket, gv;      // greedy hop: workgroups done, current vertex
-  unsigned long long ds[2];            // edge totals of the current forward / backward frontier
-  uint32_t cur[2], kf, kb, done, met, L, dir;
+};
+
+struct ChState {        // device; copied back per batch up to gpart
+  unsigned long long lacc[CH_MAXS];    // packed output list of step launch i
+  unsigned long long lmeet[CH_MAXS];   // meet vertices found by step launch i
+  unsigned long long macc;             // packed meet list (over in-edges)
+  unsigned long long err;              // 1 reconstruction failure, 3 list overflow
+  unsigned long long hpos, gticket, gv;   // greedy: next hop, workgroups done, current vertex
+  unsigned long long hlaunch;          // greedy launches that did work
+  ChSnap snap[CH_MAXS];
   long long path[1 + 3 * MAX_PATH_LEN];
   unsigned long long gpart[4 * CH_HOP_WGS];
 };
@@ -84,6 +100,47 @@ struct ChQ {
   uint32_t s, t, upto;
   uint32_t ef, eb, em;
 };
+
+// The state after step launch `i` (snapshot p before it, its results from st): every step launch
+// and the host derive it the same way.
+__host__ __device__ inline ChSnap ch_advance(const ChSnap& p, unsigned long long out, unsigned long long meets,
+                                              unsigned long long macc, unsigned long long err, uint32_t upto) {
+  ChSnap s = p;
+  if (p.phase == PH_BFS) {
+    const int side = (int)p.dir;
+    if (side == 0) s.fprev = p.cnt[0];
+    s.edges += p.cnt[side] & 0xFFFFFFFFull;
+    s.levels += 1;
+    s.cnt[side] = out;
+    s.cur[side] ^= 1u;
+    if (side == 0) ++s.kf;
+    else ++s.kb;
+    if (err) {
+      s.phase = PH_DONE;
+      s.err = 1;
+    } else if (meets) {
+      s.met = 1;
+      s.L = s.kf + s.kb;
+      s.bstep = 0;
+      s.bcnt = macc;
+      s.phase = s.kf >= 2 ? PH_BSET : PH_DONE;
+    } else if ((out >> 32) == 0 || s.kf + s.kb >= upto) {
+      s.phase = PH_DONE;   // a side has no further edges, or UPTO reached: no path
+    } else {
+      s.dir = (s.cnt[0] & 0xFFFFFFFFull) <= (s.cnt[1] & 0xFFFFFFFFull) ? 0u : 1u;
+    }
+  } else if (p.phase == PH_BSET) {
+    s.bcnt = out;
+    s.bstep += 1;
+    if (err) {
+      s.phase = PH_DONE;
+      s.err = 1;
+    } else if (s.bstep + 1 >= s.kf) {
+      s.phase = PH_DONE;   // B[kf - 1] .. B[1] are there
+    }
+  }
+  return s;
+}
 
 namespace {
 
@@ -138,9 +195,10 @@ __device__ __forceinline__ void list_put(const ChArgs& A, const ChList& L, uint3
 }
 
 // Appends, per lane, the vertices x[i] with bit i of `m` and a nonzero degree (dg[i], rs[i]) to
-// list `li`: one packed atomic per wave for positions and edge offsets.
-__device__ __forceinline__ void wave_append(const ChArgs& A, int li, const uint32_t (&x)[CH_VT], uint32_t m,
-                                            const uint32_t (&dg)[CH_VT], const uint32_t (&rs)[CH_VT]) {
+// list L (counter *acc): one packed atomic per wave for positions and edge offsets.
+__device__ __forceinline__ void wave_append(const ChArgs& A, const ChList& L, unsigned long long* acc,
+                                            const uint32_t (&x)[CH_VT], uint32_t m, const uint32_t (&dg)[CH_VT],
+                                            const uint32_t (&rs)[CH_VT]) {
   const int lane = threadIdx.x & 63;
   uint32_t c = 0, d = 0;
 #pragma unroll
@@ -153,7 +211,7 @@ __device__ __forceinline__ void wave_append(const ChArgs& A, int li, const uint3
   const uint32_t tc = __shfl(ic, 63, 64), td = __shfl(id, 63, 64);
   if (!tc) return;   // wave-uniform
   unsigned long long old = 0;
-  if (lane == 0) old = atomicAdd(&A.st->acc[li], ((unsigned long long)tc << 32) | td);
+  if (lane == 0) old = atomicAdd(acc, ((unsigned long long)tc << 32) | td);
   old = __shfl(old, 0, 64);
   if ((old >> 32) + tc > A.list_cap) {
     if (lane == 0) atomicOr(&A.st->err, 3ull);
@@ -161,7 +219,6 @@ __device__ __forceinline__ void wave_append(const ChArgs& A, int li, const uint3
   }
   uint32_t pos = (uint32_t)(old >> 32) + ic - c;
   uint32_t end = (uint32_t)old + id - d;
-  const ChList L = A.list[li];
 #pragma unroll
   for (int i = 0; i < CH_VT; ++i)
     if (((m >> i) & 1u) && dg[i]) {
@@ -170,19 +227,10 @@ __device__ __forceinline__ void wave_append(const ChArgs& A, int li, const uint3
     }
 }
 
-// The last workgroup of a launch to finish (ticket) gets true, with the other workgroups'
-// writes visible.
-__device__ __forceinline__ bool last_workgroup(unsigned long long* ticket) {
-  __shared__ int s_last;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    s_last = atomicAdd(ticket, 1ull) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!s_last) return false;
-  __threadfence();
-  return true;
+// The snapshot step launch i runs under: snap[0] (set-up) or derived from launch i - 1.
+__device__ __forceinline__ ChSnap snap_for(const ChState* st, int i, uint32_t upto) {
+  if (i == 0) return st->snap[0];
+  return ch_advance(st->snap[i - 1], st->lacc[i - 1], st->lmeet[i - 1], st->macc, st->err, upto);
 }
 
 }  // namespace
@@ -195,79 +243,101 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_setup(const ChArgs* __restrict_
   const uint32_t dsf = vdeg(A, 0, q.s, &rsf), dsb = vdeg(A, 1, q.t, &rsb);
   for (uint64_t t = threadIdx.x; t * CH_TILE <= dsf && t < A.tsplit_cap; t += CH_BLOCK) A.list[CL_F0].tsplit[t] = 0;
   for (uint64_t t = threadIdx.x; t * CH_TILE <= dsb && t < A.tsplit_cap; t += CH_BLOCK) A.list[CL_B0].tsplit[t] = 0;
+  for (int i = threadIdx.x; i < CH_MAXS; i += CH_BLOCK) {
+    st->lacc[i] = 0;
+    st->lmeet[i] = 0;
+  }
   if (threadIdx.x != 0) return;
-  for (int i = 0; i < CH_NLISTS; ++i) st->acc[i] = 0;
-  st->meets = st->ticket = st->edges = st->err = st->levels = st->gticket = 0;
-  st->cur[0] = st->cur[1] = 0;
-  st->kf = st->kb = st->met = st->L = 0;
-  st->ds[0] = dsf;
-  st->ds[1] = dsb;
-  st->dir = dsf <= dsb ? 0u : 1u;
-  st->done = !dsf || !dsb;
+  st->macc = st->err = st->hpos = st->gticket = st->hlaunch = 0;
+  ChSnap s;
+  memset(&s, 0, sizeof(s));
+  s.phase = dsf && dsb ? PH_BFS : PH_DONE;
+  s.dir = dsf <= dsb ? 0u : 1u;
+  s.cnt[0] = (1ull << 32) | dsf;
+  s.cnt[1] = (1ull << 32) | dsb;
+  st->snap[0] = s;
   A.lab[0][q.s] = stamp_of(q.ef, 0);
   A.lab[1][q.t] = stamp_of(q.eb, 0);
-  if (dsf) {
-    const ChList& F = A.list[CL_F0];
-    F.ids[0] = q.s;
-    F.seg_end[0] = dsf;
-    F.seg_rs[0] = rsf;
-    st->acc[CL_F0] = (1ull << 32) | dsf;
-  }
-  if (dsb) {
-    const ChList& B = A.list[CL_B0];
-    B.ids[0] = q.t;
-    B.seg_end[0] = dsb;
-    B.seg_rs[0] = rsb;
-    st->acc[CL_B0] = (1ull << 32) | dsb;
-  }
+  const ChList& F = A.list[CL_F0];
+  F.ids[0] = q.s;
+  F.seg_end[0] = dsf;
+  F.seg_rs[0] = rsf;
+  const ChList& B = A.list[CL_B0];
+  B.ids[0] = q.t;
+  B.seg_end[0] = dsb;
+  B.seg_rs[0] = rsb;
   st->gv = q.s;
   st->path[0] = A.vids[q.s];
 }
 
-// One level: mode 0 = the next BFS level (side from ChState::dir), mode 1 = B-set step k
-// (B[kf - 1 - k] from B[kf - k] through in-edges, restricted to forward level kf - 1 - k).
-__global__ void __launch_bounds__(CH_BLOCK) k_ch_level(const ChArgs* __restrict__ Ap, ChQ q, int mode, int k) {
+// Step launch i: a BFS level, a B-set step or nothing, as its snapshot says.
+//   BFS, side d: expand side d's current list over d's CSR; claim unlabelled neighbours with the
+//     side's next level stamp, append them to d's other list, and record meets (claimed vertices
+//     the other side already labelled: LAB_M stamp, meet list over in-edges).
+//   B-set step k: B[kf - 1 - k] = vertices of forward level kf - 1 - k with an edge into
+//     B[kf - k], claimed in LAB_M (push: in-edges of B[kf - k]; pull, k == 0 only: out-edges of
+//     forward level kf - 1).
+__global__ void __launch_bounds__(CH_BLOCK) k_ch_step(const ChArgs* __restrict__ Ap, ChQ q, int i) {
   __shared__ uint32_t sEndAll[CH_WAVES][CH_TILE + 2];
   __shared__ uint32_t sRsAll[CH_WAVES][CH_TILE + 1];
   __shared__ uint16_t sSegAll[CH_WAVES][CH_TILE];
   const ChArgs& A = *Ap;
   ChState* st = A.st;
-  const bool bfs = mode == 0;
-  // ---- what this launch does (every workgroup reads the same state: uniform)
-  const uint32_t kf = st->kf, kb = st->kb;
-  int side, src, dst;
-  uint32_t* lab;
-  uint32_t epoch = 0, stamp, oepoch = 0, mstamp = 0, rstamp = 0;
-  const uint32_t* olab = nullptr;
-  const uint32_t* rlab = nullptr;
+  const ChSnap P = snap_for(st, i, q.upto);
+  if (i > 0 && blockIdx.x == 0 && threadIdx.x == 0) st->snap[i] = P;   // for launch i + 1
+  if (P.phase == PH_DONE) return;
+  const bool bfs = P.phase == PH_BFS;
+  // ---- this launch's lists, labels and stamps (uniform)
+  int side;              // CSR expanded
+  ChList S, D;           // source list, output list
+  unsigned long long scnt;
+  uint32_t* lab;         // claimed label
+  uint32_t epoch, stamp, oepoch = 0, mstamp = 0, rstamp = 0;
+  const uint32_t* olab = nullptr;   // BFS: meet test
+  const uint32_t* rlab = nullptr;   // push B-set: restriction to a forward level
+  const uint32_t* tlab = nullptr;   // pull B-set: the neighbour must be in B[kf] (LAB_M == tstamp)
+  uint32_t tstamp = 0;
+  int oside;             // CSR of the output list's edge space
   bool append = true;
   if (bfs) {
-    if (st->done) return;
-    side = (int)st->dir;
-    src = side * 2 + (int)st->cur[side];
-    dst = src ^ 1;
+    side = (int)P.dir;
+    const int src = side * 2 + (int)P.cur[side];
+    S = A.list[src];
+    D = A.list[src ^ 1];
+    scnt = P.cnt[side];
     lab = A.lab[side];
     epoch = side ? q.eb : q.ef;
-    stamp = stamp_of(epoch, (side ? kb : kf) + 1);
+    stamp = stamp_of(epoch, (side ? P.kb : P.kf) + 1);
     olab = A.lab[side ^ 1];
     oepoch = side ? q.ef : q.eb;
-    mstamp = stamp_of(q.em, side ? kf : kf + 1);
+    mstamp = stamp_of(q.em, side ? P.kf : P.kf + 1);
+    oside = side;
   } else {
-    if (!st->met || kf < 2u + (uint32_t)k) return;
-    const uint32_t pos = kf - 1 - (uint32_t)k;
-    side = 1;
-    src = k == 0 ? CL_M : CL_S0 + ((k - 1) & 1);
-    dst = CL_S0 + (k & 1);
+    const uint32_t k = P.bstep, pos = P.kf - 1 - k;
     lab = A.lab[2];
     epoch = q.em;   // (as the host loop: a vertex with any B-set stamp of this query is taken)
     stamp = stamp_of(q.em, pos);
-    rlab = A.lab[0];
-    rstamp = stamp_of(q.ef, pos);
     append = pos >= 2;   // B[1]'s in-edges are not needed (B[0] = {s})
+    oside = 1;
+    D = A.list[CL_B0 + (int)(k & 1)];   // the backward lists are free once the sides met
+    const bool pull = k == 0 && (P.fprev & 0xFFFFFFFFull) < (P.bcnt & 0xFFFFFFFFull);
+    if (pull) {   // forward level kf - 1 is the forward side's other list
+      side = 0;
+      S = A.list[CL_F0 + (int)(P.cur[0] ^ 1u)];
+      scnt = P.fprev;
+      tlab = A.lab[2];
+      tstamp = stamp_of(q.em, P.kf);
+    } else {
+      side = 1;
+      S = A.list[k == 0 ? CL_M : CL_B0 + (int)((k - 1) & 1)];
+      scnt = P.bcnt;
+      rlab = A.lab[0];
+      rstamp = stamp_of(q.ef, pos);
+    }
   }
-  const unsigned long long packed = st->acc[src];
-  const uint64_t n = packed >> 32, total = packed & 0xFFFFFFFFull;
-  const ChList S = A.list[src];
+  const bool pull = tlab != nullptr;
+  unsigned long long* const out_acc = &st->lacc[i];
+  const uint64_t n = scnt >> 32, total = scnt & 0xFFFFFFFFull;
   const uint32_t* __restrict__ col = A.col[side];
   const uint64_t npath = n + total, ntiles = (npath + CH_TILE - 1) / CH_TILE;
   const int lane = threadIdx.x & 63;
@@ -277,17 +347,21 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_level(const ChArgs* __restrict_
   uint16_t* const sSeg = sSegAll[w];
   for (uint64_t t = (uint64_t)blockIdx.x * CH_WAVES + w; t < ntiles; t += (uint64_t)gridDim.x * CH_WAVES) {
     uint64_t sp = 0;
-    if (lane == 0) sp = S.tsplit[t];
-    if (lane == 1) sp = (t + 1) * CH_TILE >= npath ? n : S.tsplit[t + 1];
+    if (ntiles > 1) {
+      if (lane == 0) sp = S.tsplit[t];
+      if (lane == 1) sp = (t + 1) * CH_TILE >= npath ? n : S.tsplit[t + 1];
+    } else {
+      sp = lane == 1 ? n : 0;   // one tile: no split to read
+    }
     const uint64_t a0 = uniform64(__shfl(sp, 0, 64)), a1 = uniform64(__shfl(sp, 1, 64));
     const uint64_t d0 = t * CH_TILE, d1 = d0 + CH_TILE < npath ? d0 + CH_TILE : npath;
     const uint64_t b0 = d0 - a0, b1 = d1 - a1;
     const int na = (int)(a1 - a0), nb = (int)(b1 - b0);
     // the tile's window: sEnd[k] = seg_end[a0 - 1 + k], sRs[k] = seg_rs[a0 + k]
     for (int kk = lane; kk <= na + 1; kk += 64) {
-      const int64_t i = (int64_t)a0 - 1 + kk;
-      sEnd[kk] = i < 0 ? 0u : (i < (int64_t)n ? S.seg_end[i] : 0xFFFFFFFFu);
-      if (kk <= na) sRs[kk] = (uint64_t)(i + 1) < n ? S.seg_rs[i + 1] : 0u;
+      const int64_t e = (int64_t)a0 - 1 + kk;
+      sEnd[kk] = e < 0 ? 0u : (e < (int64_t)n ? S.seg_end[e] : 0xFFFFFFFFu);
+      if (kk <= na) sRs[kk] = (uint64_t)(e + 1) < n ? S.seg_rs[e + 1] : 0u;
     }
     wave_lds_sync();
     const uint32_t* Aend = sEnd + 1;   // Aend[j] = end of entry a0 + j
@@ -314,186 +388,247 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_level(const ChArgs* __restrict_
       }
     }
     wave_lds_sync();
-    // neighbours, all loads in flight together
-    uint32_t x[CH_VT];
+    // neighbours (and, pulling, the list entry each edge belongs to), all loads in flight
+    uint32_t x[CH_VT], seg[CH_VT];
 #pragma unroll
-    for (int i = 0; i < CH_VT; ++i) {
-      const int kk = i * 64 + lane;
-      x[i] = NO_ROW;
+    for (int j = 0; j < CH_VT; ++j) {
+      const int kk = j * 64 + lane;
+      x[j] = NO_ROW;
+      seg[j] = 0;
       if (kk < nb) {
         const uint32_t s = sSeg[kk];
-        x[i] = col[(uint64_t)sRs[s] + (b0 + kk - (uint64_t)sEnd[s])];
+        seg[j] = s;
+        x[j] = col[(uint64_t)sRs[s] + (b0 + kk - (uint64_t)sEnd[s])];
       }
+    }
+    wave_lds_sync();   // (the next tile rewrites the window)
+    uint32_t c[CH_VT];   // the vertex a claim is about: the neighbour, or (pull) the list entry
+    if (pull) {
+      uint32_t tl[CH_VT], vis[CH_VT];
+#pragma unroll
+      for (int j = 0; j < CH_VT; ++j) {
+        tl[j] = x[j] != NO_ROW ? tlab[x[j]] : 0u;
+        vis[j] = x[j] != NO_ROW && A.visible ? A.visible[x[j]] : 1u;
+      }
+#pragma unroll
+      for (int j = 0; j < CH_VT; ++j)
+        c[j] = (x[j] != NO_ROW && tl[j] == tstamp && vis[j]) ? S.ids[a0 + seg[j]] : NO_ROW;
+    } else {
+#pragma unroll
+      for (int j = 0; j < CH_VT; ++j) c[j] = x[j];
     }
     uint32_t old[CH_VT], gate[CH_VT];
 #pragma unroll
-    for (int i = 0; i < CH_VT; ++i) {
-      old[i] = x[i] != NO_ROW ? lab[x[i]] : 0u;
-      gate[i] = (x[i] != NO_ROW && rlab) ? rlab[x[i]] : rstamp;
+    for (int j = 0; j < CH_VT; ++j) {
+      old[j] = c[j] != NO_ROW ? lab[c[j]] : 0u;
+      gate[j] = (c[j] != NO_ROW && rlab) ? rlab[c[j]] : rstamp;
     }
-    wave_lds_sync();   // (the next tile rewrites the window)
     uint32_t cm = 0;
 #pragma unroll
-    for (int i = 0; i < CH_VT; ++i) {
-      if (x[i] == NO_ROW || gate[i] != rstamp) continue;
-      if (live(old[i], epoch)) continue;
-      if (atomicCAS(lab + x[i], old[i], stamp) != old[i]) continue;
-      cm |= 1u << i;
+    for (int j = 0; j < CH_VT; ++j) {
+      if (c[j] == NO_ROW || gate[j] != rstamp || live(old[j], epoch)) continue;
+      if (atomicCAS(lab + c[j], old[j], stamp) != old[j]) continue;
+      cm |= 1u << j;
     }
     if (!__ballot(cm != 0)) continue;
     uint32_t mm = 0;
-    if (bfs) {
+    if (bfs) {   // meet test: claimed vertices only (most neighbours of a big level are not)
       uint32_t ol[CH_VT];
 #pragma unroll
-      for (int i = 0; i < CH_VT; ++i) ol[i] = ((cm >> i) & 1u) ? olab[x[i]] : 0u;
+      for (int j = 0; j < CH_VT; ++j) ol[j] = ((cm >> j) & 1u) ? olab[c[j]] : 0u;
 #pragma unroll
-      for (int i = 0; i < CH_VT; ++i)
-        if (((cm >> i) & 1u) && live(ol[i], oepoch)) mm |= 1u << i;
+      for (int j = 0; j < CH_VT; ++j)
+        if (((cm >> j) & 1u) && live(ol[j], oepoch)) mm |= 1u << j;
     }
     if (append) {
       uint32_t dg[CH_VT], rs[CH_VT];
 #pragma unroll
-      for (int i = 0; i < CH_VT; ++i) dg[i] = ((cm >> i) & 1u) ? vdeg(A, side, x[i], &rs[i]) : (rs[i] = 0, 0u);
-      wave_append(A, dst, x, cm, dg, rs);
+      for (int j = 0; j < CH_VT; ++j) {
+        dg[j] = 0;
+        rs[j] = 0;
+        if ((cm >> j) & 1u) dg[j] = vdeg(A, oside, c[j], &rs[j]);
+      }
+      wave_append(A, D, out_acc, c, cm, dg, rs);
     }
     if (__ballot(mm != 0)) {   // the sides met: LAB_M stamps, the meet list over in-edges
       uint32_t dg[CH_VT], rs[CH_VT];
       uint32_t nm = 0;
 #pragma unroll
-      for (int i = 0; i < CH_VT; ++i) {
-        dg[i] = 0;
-        rs[i] = 0;
-        if ((mm >> i) & 1u) {
-          A.lab[2][x[i]] = mstamp;
-          dg[i] = vdeg(A, 1, x[i], &rs[i]);
+      for (int j = 0; j < CH_VT; ++j) {
+        dg[j] = 0;
+        rs[j] = 0;
+        if ((mm >> j) & 1u) {
+          A.lab[2][c[j]] = mstamp;
+          dg[j] = vdeg(A, 1, c[j], &rs[j]);
           ++nm;
         }
       }
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) nm += __shfl_xor(nm, o, 64);
-      if (lane == 0) atomicAdd(&st->meets, (unsigned long long)nm);
-      wave_append(A, CL_M, x, mm, dg, rs);
+      if (lane == 0) atomicAdd(&st->lmeet[i], (unsigned long long)nm);
+      wave_append(A, A.list[CL_M], &st->macc, c, mm, dg, rs);
     }
   }
-  // ---- bookkeeping by the last workgroup: the next launch's parameters
-  if (!last_workgroup(&st->ticket) || threadIdx.x != 0) return;
-  st->ticket = 0;
-  if (!bfs) {
-    if (k >= 1) st->acc[src] = 0;   // the list the next B-set step appends to
-    return;
-  }
-  const unsigned long long nn = ld_agent(&st->acc[dst]);
-  const uint32_t nkf = kf + (side == 0), nkb = kb + (side == 1);
-  st->cur[side] ^= 1u;
-  st->acc[src] = 0;   // this side's next level appends here
-  st->kf = nkf;
-  st->kb = nkb;
-  const unsigned long long ds = nn & 0xFFFFFFFFull, dso = st->ds[side ^ 1];
-  st->ds[side] = ds;
-  st->edges += total;
-  st->levels += 1;
-  const unsigned long long err = ld_agent(&st->err);
-  if (err) {
-    st->done = 1;
-  } else if (ld_agent(&st->meets)) {
-    st->met = 1;
-    st->L = nkf + nkb;
-    st->done = 1;
-    st->acc[CL_F0] = st->acc[CL_F1] = 0;   // the B-set lists
-  } else if ((nn >> 32) == 0 || nkf + nkb >= q.upto) {
-    st->done = 1;   // a side has no further edges, or UPTO reached: no path
-  }
-  st->dir = (side == 0 ? ds <= dso : dso <= ds) ? 0u : 1u;
 }
 
-// Greedy hop pos (CH_HOP_WGS workgroups): the minimum (type, rank, dst vid) out-edge of the
-// current vertex into B[pos + 1]; the last workgroup reduces, records the hop, moves on.
-__global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ Ap, ChQ q, int pos) {
-  struct Cand {
-    int64_t t, r, v;
-    uint32_t d;
-  };
+namespace {
+
+struct Cand {
+  int64_t t, r, v;
+  uint32_t d;
+};
+__device__ __forceinline__ bool cand_less(const Cand& a, const Cand& b) {
+  if (a.t != b.t) return a.t < b.t;
+  if (a.r != b.r) return a.r < b.r;
+  return a.v < b.v;
+}
+constexpr uint32_t CH_SOLO_DEG = 4 * CH_BLOCK * CH_HOP_U;   // a hop one workgroup takes alone
+
+// Workgroup-wide minimum (every thread gets it).
+__device__ __forceinline__ Cand block_min(Cand b, Cand* lds) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Cand y;
+    y.t = __shfl_down(b.t, o, 64);
+    y.r = __shfl_down(b.r, o, 64);
+    y.v = __shfl_down(b.v, o, 64);
+    y.d = __shfl_down(b.d, o, 64);
+    if ((threadIdx.x & 63) + o < 64 && cand_less(y, b)) b = y;
+  }
+  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = b;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < CH_WAVES; ++k)
+      if (cand_less(lds[k], b)) b = lds[k];
+    lds[CH_WAVES] = b;
+  }
+  __syncthreads();
+  b = lds[CH_WAVES];
+  __syncthreads();
+  return b;
+}
+
+// This thread's best candidate among c's out-edges [rs + g, re) step G into B[pos + 1].
+__device__ __forceinline__ Cand hop_scan(const ChArgs& A, const uint32_t* vlab, uint32_t want, uint32_t rs,
+                                         uint32_t re, uint64_t g, uint64_t G) {
+  Cand best{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
+  for (uint64_t j0 = rs + g; j0 < re; j0 += CH_HOP_U * G) {
+    uint32_t wv[CH_HOP_U], lv[CH_HOP_U];
+#pragma unroll
+    for (int u = 0; u < CH_HOP_U; ++u) wv[u] = j0 + u * G < re ? A.col[0][j0 + u * G] : NO_ROW;
+#pragma unroll
+    for (int u = 0; u < CH_HOP_U; ++u) lv[u] = wv[u] != NO_ROW ? vlab[wv[u]] : 0u;
+#pragma unroll
+    for (int u = 0; u < CH_HOP_U; ++u) {
+      if (wv[u] == NO_ROW || lv[u] != want) continue;
+      const uint64_t j = j0 + u * G;
+      const Cand x{A.type, A.rank ? A.rank[j] : 0, A.dst_vid[j], wv[u]};
+      if (cand_less(x, best)) best = x;
+    }
+  }
+  return best;
+}
+
+}  // namespace
+
+// Greedy hops (CH_HOP_WGS workgroups).  The state after step launch `last` says whether the
+// sides met and the path length L; hop pos = st->hpos (< L) takes the minimum (type, rank, dst
+// vid) out-edge of the current vertex c into B[pos + 1] (B[pos + 1] = LAB_M stamp pos + 1 for
+// positions <= kf, backward level L - pos - 1 beyond).  A hub's hop is scanned by every
+// workgroup and reduced by the last one to finish; small hops are taken by one workgroup alone
+// (workgroup 0, or the reducing one after a hub), which walks on until the path is complete or
+// the next vertex is a hub — left to the next launch.
+__global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ Ap, ChQ q, int last) {
   __shared__ Cand lds[CH_WAVES + 1];
+  __shared__ int s_last;
   const ChArgs& A = *Ap;
   ChState* st = A.st;
-  if (!st->met || (uint32_t)pos >= st->L || st->err) return;
-  const uint32_t c = (uint32_t)st->gv, L = st->L, kf = st->kf;
-  auto less = [](const Cand& a, const Cand& b) {
-    if (a.t != b.t) return a.t < b.t;
-    if (a.r != b.r) return a.r < b.r;
-    return a.v < b.v;
-  };
+  const ChSnap F = ch_advance(st->snap[last], st->lacc[last], st->lmeet[last], st->macc, st->err, q.upto);
+  uint32_t pos = (uint32_t)st->hpos;
+  if (!F.met || F.phase != PH_DONE || F.err || pos >= F.L || st->err) return;
+  const uint32_t L = F.L, kf = F.kf;
+  uint32_t c = (uint32_t)st->gv;
   const Cand none{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
-  Cand best = none;
-  const bool by_m = (uint32_t)pos + 1 <= kf;
-  const uint32_t* vlab = by_m ? A.lab[2] : A.lab[1];
-  const uint32_t want = by_m ? stamp_of(q.em, (uint32_t)pos + 1) : stamp_of(q.eb, L - (uint32_t)pos - 1);
-  if (c != NO_ROW && (!A.visible || A.visible[c])) {
-    const uint32_t rs = A.row_ptr[0][c], re = A.row_ptr[0][c + 1];
-    const uint64_t g = (uint64_t)blockIdx.x * CH_BLOCK + threadIdx.x, G = (uint64_t)gridDim.x * CH_BLOCK;
-    for (uint64_t j0 = rs + g; j0 < re; j0 += CH_HOP_U * G) {
-      uint32_t wv[CH_HOP_U], lv[CH_HOP_U];
-#pragma unroll
-      for (int u = 0; u < CH_HOP_U; ++u) wv[u] = j0 + u * G < re ? A.col[0][j0 + u * G] : NO_ROW;
-#pragma unroll
-      for (int u = 0; u < CH_HOP_U; ++u) lv[u] = wv[u] != NO_ROW ? vlab[wv[u]] : 0u;
-#pragma unroll
-      for (int u = 0; u < CH_HOP_U; ++u) {
-        if (wv[u] == NO_ROW || lv[u] != want) continue;
-        const uint64_t j = j0 + u * G;
-        const Cand x{A.type, A.rank ? A.rank[j] : 0, A.dst_vid[j], wv[u]};
-        if (less(x, best)) best = x;
-      }
+  auto range = [&](uint32_t v, uint32_t* rs, uint32_t* re) {
+    *rs = *re = 0;
+    if (v != NO_ROW && (!A.visible || A.visible[v])) {
+      *rs = A.row_ptr[0][v];
+      *re = A.row_ptr[0][v + 1];
     }
-  }
-  auto block_min = [&](Cand b) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      Cand y;
-      y.t = __shfl_down(b.t, o, 64);
-      y.r = __shfl_down(b.r, o, 64);
-      y.v = __shfl_down(b.v, o, 64);
-      y.d = __shfl_down(b.d, o, 64);
-      if ((threadIdx.x & 63) + o < 64 && less(y, b)) b = y;
-    }
-    if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = b;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      for (int i = 1; i < CH_WAVES; ++i)
-        if (less(lds[i], b)) b = lds[i];
-      lds[CH_WAVES] = b;
-    }
-    __syncthreads();
-    b = lds[CH_WAVES];
-    __syncthreads();
-    return b;
   };
-  best = block_min(best);
-  if (threadIdx.x == 0) {
-    unsigned long long* part = st->gpart + 4 * blockIdx.x;
-    part[0] = (unsigned long long)best.t;
-    part[1] = (unsigned long long)best.r;
-    part[2] = (unsigned long long)best.v;
-    part[3] = best.d;
+  auto want_of = [&](uint32_t p, const uint32_t** vlab) {
+    const bool by_m = p + 1 <= kf;
+    *vlab = by_m ? A.lab[2] : A.lab[1];
+    return by_m ? stamp_of(q.em, p + 1) : stamp_of(q.eb, L - p - 1);
+  };
+  // record hop p (thread 0): false when it has no candidate (reconstruction failure)
+  auto record = [&](uint32_t p, const Cand& r) {
+    if (r.d == NO_ROW) {
+      st->err |= 1ull;
+      st->gv = NO_ROW;
+      return false;
+    }
+    st->path[1 + 3 * p] = r.t;
+    st->path[2 + 3 * p] = r.r;
+    st->path[3 + 3 * p] = r.v;
+    st->gv = r.d;
+    st->hpos = p + 1;
+    return true;
+  };
+  uint32_t rs, re;
+  range(c, &rs, &re);
+  bool solo;   // this workgroup walks on alone
+  if (re - rs > CH_SOLO_DEG) {   // a hub: every workgroup scans a share
+    const uint32_t* vlab;
+    const uint32_t want = want_of(pos, &vlab);
+    Cand best = hop_scan(A, vlab, want, rs, re, (uint64_t)blockIdx.x * CH_BLOCK + threadIdx.x,
+                         (uint64_t)gridDim.x * CH_BLOCK);
+    best = block_min(best, lds);
+    if (threadIdx.x == 0) {
+      unsigned long long* part = st->gpart + 4 * blockIdx.x;
+      part[0] = (unsigned long long)best.t;
+      part[1] = (unsigned long long)best.r;
+      part[2] = (unsigned long long)best.v;
+      part[3] = best.d;
+      __threadfence();
+      s_last = atomicAdd(&st->gticket, 1ull) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    Cand r = none;
+    if (threadIdx.x < gridDim.x) {
+      const unsigned long long* p = st->gpart + 4 * threadIdx.x;
+      r = Cand{(int64_t)ld_agent(p), (int64_t)ld_agent(p + 1), (int64_t)ld_agent(p + 2), (uint32_t)ld_agent(p + 3)};
+    }
+    r = block_min(r, lds);
+    if (threadIdx.x == 0) {
+      st->gticket = 0;
+      s_last = record(pos, r);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    c = r.d;
+    ++pos;
+    solo = true;
+  } else {
+    solo = blockIdx.x == 0;
   }
-  if (!last_workgroup(&st->gticket)) return;
-  Cand r = none;
-  if (threadIdx.x < gridDim.x) {
-    const unsigned long long* p = st->gpart + 4 * threadIdx.x;
-    r = Cand{(int64_t)ld_agent(p), (int64_t)ld_agent(p + 1), (int64_t)ld_agent(p + 2), (uint32_t)ld_agent(p + 3)};
+  if (!solo) return;
+  if (threadIdx.x == 0) st->hlaunch += 1;
+  // one workgroup, small hops
+  while (pos < L) {
+    range(c, &rs, &re);
+    if (re - rs > CH_SOLO_DEG) return;   // a hub: the next launch spreads it
+    const uint32_t* vlab;
+    const uint32_t want = want_of(pos, &vlab);
+    const Cand r = block_min(hop_scan(A, vlab, want, rs, re, threadIdx.x, CH_BLOCK), lds);
+    if (threadIdx.x == 0) s_last = record(pos, r);
+    __syncthreads();
+    if (!s_last) return;
+    c = r.d;
+    ++pos;
   }
-  r = block_min(r);
-  if (threadIdx.x != 0) return;
-  st->gticket = 0;
-  if (r.d == NO_ROW) {
-    st->err |= 1ull;
-    st->gv = NO_ROW;
-    return;
-  }
-  st->path[1 + 3 * pos] = r.t;
-  st->path[2 + 3 * pos] = r.r;
-  st->path[3 + 3 * pos] = r.v;
-  st->gv = r.d;
 }
 
 // ---------------------------------------------------------------------------- host side
@@ -508,6 +643,12 @@ struct ChainCtx {
   ChArgs cached{};
   bool args_valid = false;
   unsigned grid = 512;
+  // the query in flight: what has been enqueued
+  ChQ q{};
+  int steps = 0, hops = 0;
+  // recent queries: step launches and path lengths used (sizes the next chain)
+  double ema_steps = 6, ema_hops = 2;
+  unsigned long long batches = 0, queries = 0;
 };
 
 static constexpr size_t CH_COPY = offsetof(ChState, gpart);
@@ -544,6 +685,9 @@ ChainCtx* chain_create(uint64_t nv, uint64_t edge_cap, hipStream_t s, std::strin
 
 void chain_destroy(ChainCtx* c) {
   if (!c) return;
+  if (getenv("NBG_SP_TRACE") && c->queries)
+    fprintf(stderr, "[sp trace] level loop: %llu queries, %.3f batches each, chain sized for %.2f steps, %.2f hops\n",
+            c->queries, (double)c->batches / c->queries, c->ema_steps, c->ema_hops);
   for (auto& L : c->list)
     for (uint32_t* p : {L.ids, L.seg_end, L.seg_rs, L.tsplit})
       if (p) (void)hipFree(p);
@@ -552,6 +696,18 @@ void chain_destroy(ChainCtx* c) {
   if (c->h_st) (void)hipHostFree(c->h_st);
   if (c->h_args) (void)hipHostFree(c->h_args);
   delete c;
+}
+
+// Enqueue step launches [steps, steps + k) and h hop launches, then the state copy.
+static hipError_t chain_batch(ChainCtx* c, int k, int h) {
+  const ChArgs* A = c->d_args;
+  for (int j = 0; j < k; ++j, ++c->steps)
+    hipLaunchKernelGGL(k_ch_step, dim3(c->grid), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps);
+  for (int j = 0; j < h; ++j, ++c->hops)
+    hipLaunchKernelGGL(k_ch_hop, dim3(CH_HOP_WGS), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps - 1);
+  HIP_TRY_CH(hipGetLastError());
+  ++c->batches;
+  return hipMemcpyAsync(c->h_st, c->d_st, CH_COPY, hipMemcpyDeviceToHost, c->stream);
 }
 
 hipError_t chain_launch(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible,
@@ -581,26 +737,50 @@ hipError_t chain_launch(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, con
     c->cached = a;
     c->args_valid = true;
   }
-  const ChArgs* A = c->d_args;
-  const ChQ q{s, t, upto, epoch, epoch, epoch};
-  hipLaunchKernelGGL(k_ch_setup, dim3(1), dim3(CH_BLOCK), 0, c->stream, A, q);
-  for (uint32_t i = 0; i < upto; ++i)
-    hipLaunchKernelGGL(k_ch_level, dim3(c->grid), dim3(CH_BLOCK), 0, c->stream, A, q, 0, (int)i);
-  for (uint32_t k = 0; k + 2 <= upto; ++k)   // B-set steps: kf - 1 - k >= 1 needs kf >= k + 2
-    hipLaunchKernelGGL(k_ch_level, dim3(c->grid), dim3(CH_BLOCK), 0, c->stream, A, q, 1, (int)k);
-  for (uint32_t p = 0; p < upto; ++p)
-    hipLaunchKernelGGL(k_ch_hop, dim3(CH_HOP_WGS), dim3(CH_BLOCK), 0, c->stream, A, q, (int)p);
-  HIP_TRY_CH(hipGetLastError());
-  return hipMemcpyAsync(c->h_st, c->d_st, CH_COPY, hipMemcpyDeviceToHost, c->stream);
+  c->q = ChQ{s, t, upto, epoch, epoch, epoch};
+  c->steps = c->hops = 0;
+  ++c->queries;
+  hipLaunchKernelGGL(k_ch_setup, dim3(1), dim3(CH_BLOCK), 0, c->stream, (const ChArgs*)c->d_args, c->q);
+  // sized by the recent queries; a longer one gets a continuation batch (chain_more)
+  const int max_steps = 2 * (int)upto - 1;
+  const int k = std::min(max_steps, std::max(1, (int)std::ceil(c->ema_steps)));
+  const int h = std::min((int)upto, std::max(1, (int)std::ceil(c->ema_hops)));
+  return chain_batch(c, k, h);
 }
 
-// the copied state -> SpResult (after the stream reached the copy)
+// After a batch's copy completed: the query's final state, or false with a continuation batch
+// enqueued (the caller waits again).
+bool chain_more(ChainCtx* c, hipError_t* he) {
+  *he = hipSuccess;
+  const ChState& h = *c->h_st;
+  const ChSnap F = ch_advance(h.snap[c->steps - 1], h.lacc[c->steps - 1], h.lmeet[c->steps - 1], h.macc, h.err,
+                              c->q.upto);
+  const int max_steps = 2 * (int)c->q.upto - 1;
+  if (F.phase != PH_DONE && c->steps < max_steps) {
+    *he = chain_batch(c, max_steps - c->steps, (int)c->q.upto);   // the rest, at once
+    return false;
+  }
+  if (F.met && !F.err && !h.err && h.hpos < F.L && c->hops < (int)c->q.upto) {
+    *he = chain_batch(c, 0, (int)F.L - (int)h.hpos);
+    return false;
+  }
+  // steps used: the BFS levels and B-set steps; decay toward this query's needs
+  const double used = (double)F.levels + (F.met && F.kf >= 2 ? F.kf - 1 : 0);
+  c->ema_steps = 0.9 * c->ema_steps + 0.1 * (used + 0.5);
+  if (F.met) c->ema_hops = 0.9 * c->ema_hops + 0.1 * ((double)h.hlaunch + 0.3);
+  return true;
+}
+
+// the final state -> SpResult
 void chain_result(const ChainCtx* c, SpResult* out) {
   const ChState& h = *c->h_st;
+  const ChSnap F = ch_advance(h.snap[c->steps - 1], h.lacc[c->steps - 1], h.lmeet[c->steps - 1], h.macc, h.err,
+                              c->q.upto);
   out->err = h.err;
-  out->edges = h.edges;
-  out->levels = h.levels;
-  out->L = (h.met && !h.err) ? h.L : 0;
+  out->edges = F.edges;
+  out->levels = F.levels;
+  out->L = (F.met && !h.err && h.hpos == F.L) ? F.L : 0;
+  if (F.met && !h.err && h.hpos != F.L) out->err = 2;   // (cannot happen: the hops were enqueued)
   out->ntrace = 0;
   if (out->L) memcpy(out->path, h.path, (1 + 3 * (size_t)out->L) * sizeof(long long));
 }
