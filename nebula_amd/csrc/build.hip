@@ -109,6 +109,12 @@ __global__ void k_live(uint32_t* live, const uint32_t* sd_sorted, const uint32_t
   }
 }
 
+// superseded versions: a record that is not its group's live edge but the first of its own
+// (src, rank, dst, version) run (identical keys: only the last write exists)
+__global__ void k_old(uint32_t* old, const uint32_t* live, const uint32_t* perm, const uint64_t* ver, uint64_t n) {
+  GRID_STRIDE(i, n) old[i] = !live[i] && ver[perm[i]] != ver[perm[i - 1]];
+}
+
 __global__ void k_row_ptr(uint32_t* row_ptr, const uint32_t* sd_sorted, const uint32_t* pos, uint64_t n, uint64_t nv,
                           uint32_t E) {
   GRID_STRIDE(d, nv + 1) {
@@ -133,6 +139,8 @@ struct EmitArgs {
   uint8_t* valid_out;
   GidMap g;
   unsigned* flags;              // bit 0: a live rank != 0, bit 1: a live undecodable value
+  const uint32_t* gpos;         // superseded versions: the live edges' positions (grp = gpos - 1)
+  uint32_t* grp;
 };
 
 __global__ void k_emit(EmitArgs a, uint64_t n) {
@@ -144,6 +152,7 @@ __global__ void k_emit(EmitArgs a, uint64_t n) {
     const int64_t v = a.dst[j];
     a.col[o] = gid_of(a.g, v);
     a.dvid[o] = v;
+    if (a.grp) a.grp[o] = a.gpos[i] - 1;
     if (a.rank) {
       const int64_t r = a.rank[j];
       a.rank_out[o] = r;
@@ -301,13 +310,14 @@ hipError_t bd_build_type(const TypeBuildIn& in, const GidMap& gm, hipStream_t s,
   }
   rocprim::double_buffer<uint32_t> perm(perm0, perm1);
   rocprim::double_buffer<uint64_t> keys(key0, key1);
+  uint64_t* ver_keep = nullptr;
   if (n && in.verkey) {   // version bytes (BE), ascending = newest first
     uint64_t* ver = sc.alloc<uint64_t>(n);
     BD_TRY(sc.err);
     BD_TRY(hipMemcpyAsync(ver, in.verkey, n * 8, hipMemcpyHostToDevice, s));
     k_gather_key<false><<<grid_for(n), BT, 0, s>>>(keys.current(), ver, perm.current(), n);
     BD_TRY(sort_pairs(sc, keys, perm, n, 64, s));
-    sc.release(ver);
+    ver_keep = ver;   // (the superseded versions are told apart by it below)
   }
   if (n) {   // dst bytes LE, compared as memcmp = bswap64 as unsigned
     k_gather_key<true><<<grid_for(n), BT, 0, s>>>(keys.current(), reinterpret_cast<const uint64_t*>(dst),
@@ -416,6 +426,76 @@ hipError_t bd_build_type(const TypeBuildIn& in, const GidMap& gm, hipStream_t s,
     (void)hipFree(dt.valid);
     dt.valid = nullptr;
     dev -= std::max<uint64_t>(E, 8);
+  }
+  // ---- 3b. superseded versions (multi-version data): their own CSR, each tagged with its group
+  if (ver_keep && n > 1) {
+    uint32_t* oflag = sc.alloc<uint32_t>(n);
+    uint32_t* opos = sc.alloc<uint32_t>(n);
+    BD_TRY(sc.err);
+    BD_TRY(hipMemsetAsync(oflag, 0, 4, s));
+    k_old<<<grid_for(n - 1), BT, 0, s>>>(oflag + 1, live + 1, perm.current() + 1, ver_keep, n - 1);
+    BD_TRY(hipGetLastError());
+    size_t bytes = 0;
+    BD_TRY(rocprim::exclusive_scan(nullptr, bytes, oflag, opos, 0u, n, rocprim::plus<uint32_t>(), s));
+    void* tmp = sc.alloc<uint8_t>(bytes);
+    BD_TRY(sc.err);
+    BD_TRY(rocprim::exclusive_scan(tmp, bytes, oflag, opos, 0u, n, rocprim::plus<uint32_t>(), s));
+    uint32_t tail[2];
+    BD_TRY(hipMemcpyAsync(&tail[0], opos + n - 1, 4, hipMemcpyDeviceToHost, s));
+    BD_TRY(hipMemcpyAsync(&tail[1], oflag + n - 1, 4, hipMemcpyDeviceToHost, s));
+    BD_TRY(hipStreamSynchronize(s));
+    sc.release(tmp);
+    const uint32_t NO = tail[0] + tail[1];
+    if (NO) {
+      auto* od = new DevEdgeType();
+      dt.old = od;
+      od->type = dt.type;
+      od->num_edges = NO;
+      BD_TRY(keep((void**)&od->row_ptr, (nv + 1) * 4));
+      BD_TRY(keep((void**)&od->col, (uint64_t)NO * 4));
+      BD_TRY(keep((void**)&od->dst_vid, (uint64_t)NO * 8));
+      if (dt.rank) BD_TRY(keep((void**)&od->rank, (uint64_t)NO * 8));
+      if (in.valid) BD_TRY(keep((void**)&od->valid, NO));
+      od->props.assign(in.nprops, nullptr);
+      for (int c = 0; c < in.nprops; ++c) BD_TRY(keep((void**)&od->props[c], (uint64_t)NO * 8));
+      uint32_t* grp = sc.alloc<uint32_t>(NO);
+      BD_TRY(sc.err);
+      k_row_ptr<<<grid_for(nv + 1), BT, 0, s>>>(od->row_ptr, sd_sorted, opos, n, nv, NO);
+      if (in.nprops) BD_TRY(hipMemcpyAsync(d_pout, od->props.data(), in.nprops * 8, hipMemcpyHostToDevice, s));
+      EmitArgs a{};
+      a.perm = perm.current();
+      a.live = oflag;
+      a.pos = opos;
+      a.dst = dst;
+      a.rank = dt.rank ? rank : nullptr;
+      a.valid = valid;
+      a.pin = d_pin;
+      a.pout = d_pout;
+      a.nprops = in.nprops;
+      a.col = od->col;
+      a.dvid = od->dst_vid;
+      a.rank_out = od->rank;
+      a.valid_out = od->valid;
+      a.g = gm;
+      a.flags = flags;
+      a.gpos = pos;
+      a.grp = grp;
+      k_emit<<<grid_for(n), BT, 0, s>>>(a, n);
+      BD_TRY(hipGetLastError());
+      od->h_row_ptr.resize(nv + 1);
+      od->h_grp.resize(NO);
+      BD_TRY(hipMemcpyAsync(od->h_row_ptr.data(), od->row_ptr, (nv + 1) * 4, hipMemcpyDeviceToHost, s));
+      BD_TRY(hipMemcpyAsync(od->h_grp.data(), grp, (uint64_t)NO * 4, hipMemcpyDeviceToHost, s));
+      od->narrow.assign(in.nprops, nullptr);
+      od->narrow_bytes.assign(in.nprops, 0);
+      od->prop_kind = dt.prop_kind;
+      if (in.nprops) BD_TRY(keep((void**)&od->d_props, (uint64_t)in.nprops * 8));
+      if (in.nprops) BD_TRY(hipMemcpyAsync(od->d_props, od->props.data(), in.nprops * 8, hipMemcpyHostToDevice, s));
+      BD_TRY(hipStreamSynchronize(s));
+      uint32_t md = 0;
+      for (uint64_t d = 0; d < nv; ++d) md = std::max(md, od->h_row_ptr[d + 1] - od->h_row_ptr[d]);
+      od->max_degree = (int)md;
+    }
   }
   // ---- 4. narrow copies of INT columns (read by the final-step fast path)
   dt.narrow.assign(in.nprops, nullptr);

@@ -23,17 +23,22 @@ using namespace nbg;
 
 namespace nbg {
 
-void Engine::free_snapshot() {
-  for (auto& kv : snap.types) {
-    auto& d = kv.second;
-    for (void* p : {(void*)d.row_ptr, (void*)d.col, (void*)d.dst_vid, (void*)d.rank, (void*)d.valid,
-                    (void*)d.d_props})
-      if (p) (void)hipFree(p);
-    for (auto* p : d.props)
-      if (p) (void)hipFree(p);
-    for (auto* p : d.narrow)
-      if (p) (void)hipFree(p);
+static void free_edge_type(DevEdgeType& d) {
+  for (void* p : {(void*)d.row_ptr, (void*)d.col, (void*)d.dst_vid, (void*)d.rank, (void*)d.valid, (void*)d.d_props})
+    if (p) (void)hipFree(p);
+  for (auto* p : d.props)
+    if (p) (void)hipFree(p);
+  for (auto* p : d.narrow)
+    if (p) (void)hipFree(p);
+  if (d.old) {
+    free_edge_type(*d.old);
+    delete d.old;
+    d.old = nullptr;
   }
+}
+
+void Engine::free_snapshot() {
+  for (auto& kv : snap.types) free_edge_type(kv.second);
   for (auto& kv : snap.tags) {
     if (kv.second.present) (void)hipFree(kv.second.present);
     for (auto* p : kv.second.cols)

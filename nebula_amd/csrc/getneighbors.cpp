@@ -264,6 +264,11 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
     std::unordered_map<int64_t, std::pair<uint64_t, uint64_t>> range;   // vid -> [lo, hi) in key order
   };
   std::vector<TypeRows> trows(ectx.size());
+  // superseded versions of a filtered type: rows of its older versions that pass (vid -> (grp, values))
+  struct OldRows {
+    std::unordered_map<int64_t, std::vector<std::pair<uint32_t, std::vector<int64_t>>>> by_vid;
+  };
+  std::vector<OldRows> orows(ectx.size());
   std::vector<size_t> active;   // ectx indices walked on the device
   std::vector<std::vector<int>> yield_of(ectx.size());   // returned prop -> YIELD column
   for (size_t k = 0; k < ectx.size(); ++k)
@@ -358,14 +363,32 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
       cap_rows += blk_cap.back() * ws_final_grid(starts.size(), eb);
       plist.push_back(std::move(tp));
     }
+    // the older versions of filtered out-edge types: walked with the same program (the filtered
+    // walk reads them until an edge is accepted, QueryBaseProcessor.inl:394-456)
+    std::vector<size_t> olds;   // positions in `active`
+    for (size_t i = 0; filter && i < active.size(); ++i) {
+      const DevEdgeType& dt = E.snap.types.at(ectx[active[i]].type);
+      if (ectx[active[i]].type < 0 || !dt.old || !dt.old->num_edges) continue;
+      uint64_t eb = 0;
+      for (uint32_t d : starts) eb += dt.old->h_row_ptr[d + 1] - dt.old->h_row_ptr[d];
+      if (!eb) continue;
+      olds.push_back(i);
+      ebound.push_back(eb);
+      blk_cap.push_back(ws_final_blk_cap(starts.size(), eb));
+      region.push_back(cap_rows);
+      cap_rows += blk_cap.back() * ws_final_grid(starts.size(), eb);
+      plist.push_back(plist[i]);
+    }
+    if (plist.size() > (size_t)MAX_TYPES_Q) return E.fail(NBG_E_UNSUPPORTED, "too many edge types");
     if (int32_t rrc = ws_release(E, &E.ws, E.stream)) return rrc;   // a held device GO result keeps its rows
     if (starts.size() > ws_cap_frontier(E.ws)) return E.fail(NBG_E_UNSUPPORTED, "too many vertices in one request");
     static std::atomic<uint64_t> gn_id{1ull << 62};   // program cache keys disjoint from GO statements
     Workspace* ws = E.ws;
     hipError_t he = ws_reserve_rows(ws, cap_rows, ncols);
     if (he == hipSuccess) he = ws_begin_query(ws, starts.data(), starts.size(), &plist, gn_id++);
-    for (size_t i = 0; he == hipSuccess && i < active.size(); ++i) {
-      const DevEdgeType& dt = E.snap.types.at(ectx[active[i]].type);
+    for (size_t i = 0; he == hipSuccess && i < plist.size(); ++i) {
+      const DevEdgeType& top = E.snap.types.at(ectx[active[i < active.size() ? i : olds[i - active.size()]]].type);
+      const DevEdgeType& dt = i < active.size() ? top : *top.old;
       ExpandArgs a{};
       a.row_ptr = dt.row_ptr;
       a.col = dt.col;
@@ -386,7 +409,7 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
     }
     if (he == hipSuccess) he = ws_end_query(ws);
     if (he != hipSuccess) return E.fail(NBG_E_DEVICE, std::string("HIP: ") + hipGetErrorString(he));
-    for (size_t i = 0; i < active.size(); ++i) {
+    for (size_t i = 0; i < plist.size(); ++i) {
       const int nc = (int)plist[i].yield_reg.size();
       const unsigned grid = ws_final_grid_of(ws, (int)i);
       const uint32_t* per = ws_host_blk_rows(ws, (int)i);
@@ -406,6 +429,18 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
       std::vector<uint64_t> ord(total);
       for (uint64_t r = 0; r < total; ++r) ord[r] = r;
       std::sort(ord.begin(), ord.end(), [&](uint64_t x, uint64_t y) { return cols[1][x] < cols[1][y]; });
+      if (i >= active.size()) {   // older versions: per vid in key order, tagged with their live edge
+        const size_t k = active[olds[i - active.size()]];
+        const DevEdgeType& od = *E.snap.types.at(ectx[k].type).old;
+        const std::vector<int>& ymap = yield_of[k];
+        for (uint64_t r = 0; r < total; ++r) {
+          const uint64_t q = ord[r];
+          std::vector<int64_t> vals(ymap.size());
+          for (size_t p = 0; p < ymap.size(); ++p) vals[p] = cols[ymap[p]][q];
+          orows[k].by_vid[cols[0][q]].emplace_back(od.h_grp[(size_t)cols[1][q]], std::move(vals));
+        }
+        continue;
+      }
       TypeRows& tr = trows[active[i]];
       tr.vid.resize(total);
       tr.eidx.resize(total);
@@ -499,20 +534,24 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
       if (ec.props.empty()) continue;
       const TypeRows& tr = trows[k];
       auto it = tr.range.find(v.vid);
-      if (it == tr.range.end()) continue;
-      std::string rs;
-      const uint64_t lo = it->second.first, hi = std::min(it->second.second, it->second.first + cap);
-      if (stats) {
-        for (uint64_t r = lo; r < hi; ++r)
-          for (size_t p = 0; p < ec.props.size(); ++p) collect(ec.props[p], tr.vals[p][r]);
-        resp->edges += hi - lo;
-        continue;
+      // an older version passing before the first accepted live edge comes first (firstLoop)
+      const std::vector<int64_t>* first_old = nullptr;
+      if (auto ot = orows[k].by_vid.find(v.vid); ot != orows[k].by_vid.end()) {
+        const int64_t j1 = it == tr.range.end() ? INT64_MAX : tr.eidx[it->second.first];
+        if ((int64_t)ot->second.front().first < j1) first_old = &ot->second.front().second;
       }
-      for (uint64_t r = lo; r < hi; ++r) {
+      if (it == tr.range.end() && !first_old) continue;
+      std::string rs;
+      uint64_t lo = 0, hi = 0;
+      if (it != tr.range.end()) {
+        lo = it->second.first;
+        hi = std::min(it->second.second, it->second.first + cap - (first_old ? 1 : 0));
+      }
+      auto put_row = [&](const std::vector<int64_t>* row, uint64_t r) {
         RowBytes w;
         for (size_t p = 0; p < ec.props.size(); ++p) {
           const PropCtx& pc = ec.props[p];
-          const int64_t x = tr.vals[p][r];
+          const int64_t x = row ? (*row)[p] : tr.vals[p][r];
           switch (pc.pik) {
             case 1: case 2: w.put_vid(x); break;
             case 3: case 4: w.put_int(x); break;
@@ -521,7 +560,17 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
         }
         rowset_add(rs, w.encode());
         ++resp->edges;
+      };
+      if (stats) {
+        if (first_old)
+          for (size_t p = 0; p < ec.props.size(); ++p) collect(ec.props[p], (*first_old)[p]);
+        for (uint64_t r = lo; r < hi; ++r)
+          for (size_t p = 0; p < ec.props.size(); ++p) collect(ec.props[p], tr.vals[p][r]);
+        resp->edges += hi - lo + (first_old ? 1 : 0);
+        continue;
       }
+      if (first_old) put_row(first_old, 0);
+      for (uint64_t r = lo; r < hi; ++r) put_row(nullptr, r);
       if (!rs.empty()) v.edges.emplace_back(ec.type, std::move(rs));
     }
     if (v.edges.empty()) continue;   // only vertices with edges (QueryBoundProcessor.cpp:104-107)

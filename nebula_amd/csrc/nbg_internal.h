@@ -93,6 +93,12 @@ struct DevEdgeType {            // CSR for one signed edge type over this rank's
   uint8_t* valid = nullptr;     // [E] or nullptr when every value decoded
   int max_degree = 0;
   std::vector<uint32_t> h_row_ptr;   // host copy (path reconstruction, host planning)
+  // Superseded versions (multi-version data only): a CSR of the older versions of every edge, in
+  // key order, with h_grp[i] = the live edge (index into this CSR's parent) of version i.  Read
+  // by GetNeighbors' filtered walk, which sees older versions until an edge is accepted
+  // (QueryBaseProcessor.inl:394-456).  Owned by the parent; not persisted by snapshot_save.
+  DevEdgeType* old = nullptr;
+  std::vector<uint32_t> h_grp;
 };
 
 // Tag properties of one tag, indexed by vertex id (single GPU: dense id; partitioned: global id,

@@ -22,7 +22,7 @@ from .vidhash import std_hash
 
 _TOK = re.compile(r"""\s*(?:
     (?P<double>\d+\.\d*(?:[eE][+-]?\d+)?|\.\d+(?:[eE][+-]?\d+)?)
-   |(?P<int>\d+)
+   |(?P<int>0[xX][0-9a-fA-F]+|0[0-7]+|\d+)
    |(?P<str>"(?:[^"\\]|\\.)*"|'(?:[^'\\]|\\.)*')
    |(?P<var>\$[A-Za-z_]\w*)
    |(?P<sym>\$\^|\$\$|\$-|<=|>=|==|!=|&&|\|\||[<>+\-*/%^!(),.;|=])
@@ -345,8 +345,19 @@ class Parser:
 
     def primary(self):
         kind, text = self.take()
-        if kind == "int":
-            return E.const(int(text))
+        if kind == "int":   # scanner.lex:328-368: hex (%lx), octal (%lo), decimal
+            if text[:2] in ("0x", "0X"):
+                v = int(text, 16)
+            elif len(text) > 1 and text[0] == "0":
+                v = int(text, 8)
+            else:
+                v = int(text)
+            if v >= 1 << 63:
+                if text[:2] in ("0x", "0X") or text[0] == "0":
+                    v -= 1 << 64   # the sscanf into int64_t wraps
+                else:
+                    raise ParseError(f"integer out of range: {text}")
+            return E.const(v)
         if kind == "double":
             return E.const(float(text))
         if kind == "str":

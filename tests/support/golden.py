@@ -73,3 +73,52 @@ def run_path_case(backend, case):
     got = sorted(ngql.path_string(r[0], names) for r in res.rows)
     exp = sorted(case["expected"])
     return got == exp, "" if got == exp else f"{got} != {exp}"
+
+
+# ------------------------------------------------------------------- ExpressionTest.cpp vectors
+EXPR_ROOT = 'hash("Tim Duncan")'   # two `like` edges: every case yields two equal rows
+
+
+def expr_queries(case):
+    """The GO statements one ExpressionTest vector runs as (WHERE and YIELD)."""
+    e = case["expr"]
+    return (f"GO FROM {EXPR_ROOT} OVER like WHERE {e} YIELD like._dst AS d",
+            f"GO FROM {EXPR_ROOT} OVER like YIELD {e} AS v")
+
+
+def run_expr_case(backend, case):
+    """(ok, message): the WHERE keeps both edges iff the value is true; the YIELD value equals
+    the test's expected value (ASSERT_DOUBLE_EQ: within 4 ulps); invalid expressions fail."""
+    import math
+    s = ngql.Session(backend)
+    where_q, yield_q = expr_queries(case)
+    if case.get("error"):
+        for q in (where_q, yield_q):
+            try:
+                s.execute(q)
+            except Exception:
+                continue
+            return False, f"{q!r} did not fail"
+        return True, "failed as expected"
+    rows = s.execute(where_q).rows
+    exp = case["expect"]
+    # Expression::asBool (Expressions.h:228-242): a string is "true" when it is EMPTY
+    truthy = bool(exp) if case["kind"] != "String" else exp == ""
+    if len(rows) != (2 if truthy else 0):
+        return False, f"WHERE kept {len(rows)} rows"
+    vals = [r[0] for r in s.execute(yield_q).rows]
+    if len(vals) != 2:
+        return False, f"YIELD gave {vals}"
+    for v in vals:
+        if case["kind"] == "Double":
+            if not isinstance(v, float) or not math.isclose(v, exp, rel_tol=4 * 2.0 ** -52, abs_tol=0.0):
+                return False, f"YIELD {v!r} != {exp!r}"
+        elif case["kind"] == "Bool":
+            if not isinstance(v, bool) or v != exp:
+                return False, f"YIELD {v!r} != {exp!r}"
+        elif case["kind"] == "Int":
+            if isinstance(v, bool) or not isinstance(v, int) or v != exp:
+                return False, f"YIELD {v!r} != {exp!r}"
+        elif v != exp:
+            return False, f"YIELD {v!r} != {exp!r}"
+    return True, "ok"
