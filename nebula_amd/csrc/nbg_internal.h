@@ -305,6 +305,7 @@ struct SpTypes {                     // the CSRs one search direction expands (O
   const uint32_t* col[MAX_TYPES_Q];
   const int64_t* dst_vid[MAX_TYPES_Q];
   const int64_t* rank[MAX_TYPES_Q];
+  uint64_t ne[MAX_TYPES_Q];          // edges of each CSR (bounds of the checked build)
 };
 struct SpResult {                    // one query's result block (device, copied to pinned memory)
   unsigned long long L;              // path length, 0 = no path within UPTO

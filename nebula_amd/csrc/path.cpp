@@ -248,11 +248,12 @@ int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_pat
 
 // One (s, t) pair on a single engine: the persistent device search (sp.hip) — one launch, one
 // result copy, one host wait.
-SpTypes sp_types(const PathTypes& pt) {
+SpTypes sp_types(const Engine& E, const PathTypes& pt) {
   SpTypes T{};
   T.n = pt.n;
   for (int k = 0; k < pt.n; ++k) {
     T.type[k] = pt.type[k];
+    T.ne[k] = E.snap.types.at(pt.type[k]).num_edges;
     T.row_ptr[k] = pt.a[k].row_ptr;
     T.col[k] = pt.a[k].col;
     T.dst_vid[k] = pt.a[k].dst_vid;
@@ -269,7 +270,7 @@ int32_t device_pair(PathCtx& c, int mode, uint32_t s, uint32_t t, uint32_t upto,
     if (!E.sp) return E.fail(NBG_E_OUT_OF_MEMORY, err);
   }
   if (!host_degree(c, c.fwd, s) || !host_degree(c, c.bwd, t)) return NBG_OK;   // an endpoint without edges
-  hipError_t he = sp_launch(E.sp, mode, sp_types(c.fwd), sp_types(c.bwd), E.snap.d_visible, E.snap.d_vids, s, t, upto);
+  hipError_t he = sp_launch(E.sp, mode, sp_types(c.E, c.fwd), sp_types(c.E, c.bwd), E.snap.d_visible, E.snap.d_vids, s, t, upto);
   SpResult r;
   if (he == hipSuccess) he = sp_wait(E.sp, &r);
   if (he != hipSuccess) return dev_fail(E, he, "shortest path");
@@ -518,8 +519,8 @@ int32_t find_path_locked(Engine& E, const nbg_path_request* rq, nbg_paths** out,
     const uint32_t s0 = S.empty() ? NO_ROW : S[0];
     if (pl && host_degree(c, c.fwd, s0) && host_degree(c, c.bwd, Tg[0])) {
       pl->mode = pmode;
-      pl->fwd = sp_types(c.fwd);
-      pl->bwd = sp_types(c.bwd);
+      pl->fwd = sp_types(c.E, c.fwd);
+      pl->bwd = sp_types(c.E, c.bwd);
       pl->s = s0;
       pl->t = Tg[0];
       pl->upto = rq->upto;

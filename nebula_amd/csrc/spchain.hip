@@ -75,8 +75,12 @@ struct ChState {        // device; copied back per batch up to gpart
   unsigned long long lmeet[CH_MAXS];   // meet vertices found by step launch i
   unsigned long long macc;             // packed meet list (over in-edges)
   unsigned long long err;              // 1 reconstruction failure, 3 list overflow
-  unsigned long long hpos, gticket, gv;   // greedy: next hop, workgroups done, current vertex
+  unsigned long long gticket;          // greedy hop: workgroups done (the last one reduces)
   unsigned long long hlaunch;          // greedy launches that did work
+  // greedy launch h starts from hstart[h] = (position << 32 | current vertex) and exactly one of
+  // its workgroups writes hstart[h + 1]: state that no launch mutates while its own workgroups
+  // may still read it (workgroups of one launch start at different times)
+  unsigned long long hstart[CH_MAXS + 1];
   ChSnap snap[CH_MAXS];
   long long path[1 + 3 * MAX_PATH_LEN];
   unsigned long long gpart[4 * CH_HOP_WGS];
@@ -93,6 +97,7 @@ struct ChArgs {         // device memory (indexed at run time: never a by-value 
   uint32_t* lab[3];                    // forward, backward, B-set (LAB_M)
   ChList list[CH_NLISTS];
   uint64_t list_cap, tsplit_cap;
+  uint64_t nv, ne[2];                  // vertices, edges per direction (bounds of the checked build)
   ChState* st;
 };
 
@@ -144,6 +149,29 @@ __host__ __device__ inline ChSnap ch_advance(const ChSnap& p, unsigned long long
 
 namespace {
 
+// CH_GUARD=1 (a debugging build, `make EXTRA=-DCH_GUARD=1`): every indexed access is checked
+// against its array's size; a violation sets bit 8 + site of ChState::err instead of touching
+// memory, and the query fails with that code.
+#ifndef CH_GUARD
+#define CH_GUARD 0
+#endif
+template <typename T>
+__device__ __forceinline__ T gld(const T* p, uint64_t i, uint64_t n, int site, ChState* st) {
+  if (CH_GUARD && i >= n) {
+    atomicOr(&st->err, 1ull << (8 + site));
+    return T(0);
+  }
+  return p[i];
+}
+template <typename T>
+__device__ __forceinline__ void gst(T* p, uint64_t i, uint64_t n, T v, int site, ChState* st) {
+  if (CH_GUARD && i >= n) {
+    atomicOr(&st->err, 1ull << (8 + site));
+    return;
+  }
+  p[i] = v;
+}
+
 __device__ __forceinline__ uint32_t stamp_of(uint32_t epoch, uint32_t level) { return (epoch << LVL_BITS) | level; }
 __device__ __forceinline__ bool live(uint32_t lab, uint32_t epoch) { return (lab >> LVL_BITS) == epoch; }
 __device__ __forceinline__ unsigned long long ld_agent(const unsigned long long* p) {
@@ -174,22 +202,22 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
 
 // degree of v over direction `side` (0 for an invisible vertex), *rs its row start
 __device__ __forceinline__ uint32_t vdeg(const ChArgs& A, int side, uint32_t v, uint32_t* rs) {
-  if (v == NO_ROW || (A.visible && !A.visible[v])) {
+  if (v == NO_ROW || (A.visible && !gld(A.visible, v, A.nv, 0, A.st))) {
     *rs = 0;
     return 0;
   }
-  const uint32_t r = A.row_ptr[side][v];
+  const uint32_t r = gld(A.row_ptr[side], v, A.nv + 1, 1, A.st);
   *rs = r;
-  return A.row_ptr[side][v + 1] - r;
+  return gld(A.row_ptr[side], (uint64_t)v + 1, A.nv + 1, 1, A.st) - r;
 }
 
 // Entry pos of list L: vertex v, its deg edges ending at edge offset end, from row rs; the tile
 // boundaries its merge-path range [pos + end - deg, pos + end] covers get their split.
 __device__ __forceinline__ void list_put(const ChArgs& A, const ChList& L, uint32_t pos, uint32_t v, uint32_t end,
                                          uint32_t deg, uint32_t rs) {
-  L.ids[pos] = v;
-  L.seg_end[pos] = end;
-  L.seg_rs[pos] = rs;
+  gst(L.ids, pos, A.list_cap, v, 2, A.st);
+  gst(L.seg_end, pos, A.list_cap, end, 2, A.st);
+  gst(L.seg_rs, pos, A.list_cap, rs, 2, A.st);
   const uint64_t lo = (uint64_t)pos + end - deg, hi = (uint64_t)pos + end;
   for (uint64_t t = (lo + CH_TILE - 1) / CH_TILE; t * CH_TILE <= hi && t < A.tsplit_cap; ++t) L.tsplit[t] = pos;
 }
@@ -248,7 +276,7 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_setup(const ChArgs* __restrict_
     st->lmeet[i] = 0;
   }
   if (threadIdx.x != 0) return;
-  st->macc = st->err = st->hpos = st->gticket = st->hlaunch = 0;
+  st->macc = st->err = st->gticket = st->hlaunch = 0;
   ChSnap s;
   memset(&s, 0, sizeof(s));
   s.phase = dsf && dsb ? PH_BFS : PH_DONE;
@@ -266,8 +294,8 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_setup(const ChArgs* __restrict_
   B.ids[0] = q.t;
   B.seg_end[0] = dsb;
   B.seg_rs[0] = rsb;
-  st->gv = q.s;
-  st->path[0] = A.vids[q.s];
+  st->hstart[0] = q.s;   // position 0, vertex s
+  st->path[0] = gld(A.vids, q.s, A.nv, 16, st);
 }
 
 // Step launch i: a BFS level, a B-set step or nothing, as its snapshot says.
@@ -348,8 +376,8 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_step(const ChArgs* __restrict__
   for (uint64_t t = (uint64_t)blockIdx.x * CH_WAVES + w; t < ntiles; t += (uint64_t)gridDim.x * CH_WAVES) {
     uint64_t sp = 0;
     if (ntiles > 1) {
-      if (lane == 0) sp = S.tsplit[t];
-      if (lane == 1) sp = (t + 1) * CH_TILE >= npath ? n : S.tsplit[t + 1];
+      if (lane == 0) sp = gld(S.tsplit, t, A.tsplit_cap, 3, st);
+      if (lane == 1) sp = (t + 1) * CH_TILE >= npath ? n : gld(S.tsplit, t + 1, A.tsplit_cap, 3, st);
     } else {
       sp = lane == 1 ? n : 0;   // one tile: no split to read
     }
@@ -360,8 +388,8 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_step(const ChArgs* __restrict__
     // the tile's window: sEnd[k] = seg_end[a0 - 1 + k], sRs[k] = seg_rs[a0 + k]
     for (int kk = lane; kk <= na + 1; kk += 64) {
       const int64_t e = (int64_t)a0 - 1 + kk;
-      sEnd[kk] = e < 0 ? 0u : (e < (int64_t)n ? S.seg_end[e] : 0xFFFFFFFFu);
-      if (kk <= na) sRs[kk] = (uint64_t)(e + 1) < n ? S.seg_rs[e + 1] : 0u;
+      sEnd[kk] = e < 0 ? 0u : (e < (int64_t)n ? gld(S.seg_end, (uint64_t)e, A.list_cap, 4, st) : 0xFFFFFFFFu);
+      if (kk <= na) sRs[kk] = (uint64_t)(e + 1) < n ? gld(S.seg_rs, (uint64_t)(e + 1), A.list_cap, 4, st) : 0u;
     }
     wave_lds_sync();
     const uint32_t* Aend = sEnd + 1;   // Aend[j] = end of entry a0 + j
@@ -398,7 +426,7 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_step(const ChArgs* __restrict__
       if (kk < nb) {
         const uint32_t s = sSeg[kk];
         seg[j] = s;
-        x[j] = col[(uint64_t)sRs[s] + (b0 + kk - (uint64_t)sEnd[s])];
+        x[j] = gld(col, (uint64_t)sRs[s] + (b0 + kk - (uint64_t)sEnd[s]), A.ne[side], 5, st);
       }
     }
     wave_lds_sync();   // (the next tile rewrites the window)
@@ -407,12 +435,12 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_step(const ChArgs* __restrict__
       uint32_t tl[CH_VT], vis[CH_VT];
 #pragma unroll
       for (int j = 0; j < CH_VT; ++j) {
-        tl[j] = x[j] != NO_ROW ? tlab[x[j]] : 0u;
-        vis[j] = x[j] != NO_ROW && A.visible ? A.visible[x[j]] : 1u;
+        tl[j] = x[j] != NO_ROW ? gld(tlab, x[j], A.nv, 6, st) : 0u;
+        vis[j] = x[j] != NO_ROW && A.visible ? gld(A.visible, x[j], A.nv, 6, st) : 1u;
       }
 #pragma unroll
       for (int j = 0; j < CH_VT; ++j)
-        c[j] = (x[j] != NO_ROW && tl[j] == tstamp && vis[j]) ? S.ids[a0 + seg[j]] : NO_ROW;
+        c[j] = (x[j] != NO_ROW && tl[j] == tstamp && vis[j]) ? gld(S.ids, a0 + seg[j], A.list_cap, 7, st) : NO_ROW;
     } else {
 #pragma unroll
       for (int j = 0; j < CH_VT; ++j) c[j] = x[j];
@@ -420,13 +448,14 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_step(const ChArgs* __restrict__
     uint32_t old[CH_VT], gate[CH_VT];
 #pragma unroll
     for (int j = 0; j < CH_VT; ++j) {
-      old[j] = c[j] != NO_ROW ? lab[c[j]] : 0u;
-      gate[j] = (c[j] != NO_ROW && rlab) ? rlab[c[j]] : rstamp;
+      old[j] = c[j] != NO_ROW ? gld(lab, c[j], A.nv, 8, st) : 0u;
+      gate[j] = (c[j] != NO_ROW && rlab) ? gld(rlab, c[j], A.nv, 8, st) : rstamp;
     }
     uint32_t cm = 0;
 #pragma unroll
     for (int j = 0; j < CH_VT; ++j) {
       if (c[j] == NO_ROW || gate[j] != rstamp || live(old[j], epoch)) continue;
+      if (CH_GUARD && c[j] >= A.nv) continue;
       if (atomicCAS(lab + c[j], old[j], stamp) != old[j]) continue;
       cm |= 1u << j;
     }
@@ -435,7 +464,7 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_step(const ChArgs* __restrict__
     if (bfs) {   // meet test: claimed vertices only (most neighbours of a big level are not)
       uint32_t ol[CH_VT];
 #pragma unroll
-      for (int j = 0; j < CH_VT; ++j) ol[j] = ((cm >> j) & 1u) ? olab[c[j]] : 0u;
+      for (int j = 0; j < CH_VT; ++j) ol[j] = ((cm >> j) & 1u) ? gld(olab, c[j], A.nv, 9, st) : 0u;
 #pragma unroll
       for (int j = 0; j < CH_VT; ++j)
         if (((cm >> j) & 1u) && live(ol[j], oepoch)) mm |= 1u << j;
@@ -458,7 +487,7 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_step(const ChArgs* __restrict__
         dg[j] = 0;
         rs[j] = 0;
         if ((mm >> j) & 1u) {
-          A.lab[2][c[j]] = mstamp;
+          gst(A.lab[2], c[j], A.nv, mstamp, 10, st);
           dg[j] = vdeg(A, 1, c[j], &rs[j]);
           ++nm;
         }
@@ -515,14 +544,14 @@ __device__ __forceinline__ Cand hop_scan(const ChArgs& A, const uint32_t* vlab, 
   for (uint64_t j0 = rs + g; j0 < re; j0 += CH_HOP_U * G) {
     uint32_t wv[CH_HOP_U], lv[CH_HOP_U];
 #pragma unroll
-    for (int u = 0; u < CH_HOP_U; ++u) wv[u] = j0 + u * G < re ? A.col[0][j0 + u * G] : NO_ROW;
+    for (int u = 0; u < CH_HOP_U; ++u) wv[u] = j0 + u * G < re ? gld(A.col[0], j0 + u * G, A.ne[0], 11, A.st) : NO_ROW;
 #pragma unroll
-    for (int u = 0; u < CH_HOP_U; ++u) lv[u] = wv[u] != NO_ROW ? vlab[wv[u]] : 0u;
+    for (int u = 0; u < CH_HOP_U; ++u) lv[u] = wv[u] != NO_ROW ? gld(vlab, wv[u], A.nv, 12, A.st) : 0u;
 #pragma unroll
     for (int u = 0; u < CH_HOP_U; ++u) {
       if (wv[u] == NO_ROW || lv[u] != want) continue;
       const uint64_t j = j0 + u * G;
-      const Cand x{A.type, A.rank ? A.rank[j] : 0, A.dst_vid[j], wv[u]};
+      const Cand x{A.type, A.rank ? gld(A.rank, j, A.ne[0], 13, A.st) : 0, gld(A.dst_vid, j, A.ne[0], 13, A.st), wv[u]};
       if (cand_less(x, best)) best = x;
     }
   }
@@ -531,29 +560,36 @@ __device__ __forceinline__ Cand hop_scan(const ChArgs& A, const uint32_t* vlab, 
 
 }  // namespace
 
-// Greedy hops (CH_HOP_WGS workgroups).  The state after step launch `last` says whether the
-// sides met and the path length L; hop pos = st->hpos (< L) takes the minimum (type, rank, dst
-// vid) out-edge of the current vertex c into B[pos + 1] (B[pos + 1] = LAB_M stamp pos + 1 for
-// positions <= kf, backward level L - pos - 1 beyond).  A hub's hop is scanned by every
-// workgroup and reduced by the last one to finish; small hops are taken by one workgroup alone
-// (workgroup 0, or the reducing one after a hub), which walks on until the path is complete or
-// the next vertex is a hub — left to the next launch.
-__global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ Ap, ChQ q, int last) {
+// Greedy hops (CH_HOP_WGS workgroups), launch h of the query.  The state after step launch
+// `last` says whether the sides met and the path length L; the launch starts from hstart[h] =
+// (pos, c): hop pos (< L) takes the minimum (type, rank, dst vid) out-edge of the current vertex c
+// into B[pos + 1] (B[pos + 1] = LAB_M stamp pos + 1 for positions <= kf, backward level
+// L - pos - 1 beyond).  A hub's hop is scanned by every workgroup and reduced by the last one to
+// finish; small hops are taken by one workgroup alone (workgroup 0, or the reducing one after a
+// hub), which walks on until the path is complete or the next vertex is a hub — left to the next
+// launch — and writes hstart[h + 1].
+__global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ Ap, ChQ q, int last, int h) {
   __shared__ Cand lds[CH_WAVES + 1];
   __shared__ int s_last;
   const ChArgs& A = *Ap;
   ChState* st = A.st;
   const ChSnap F = ch_advance(st->snap[last], st->lacc[last], st->lmeet[last], st->macc, st->err, q.upto);
-  uint32_t pos = (uint32_t)st->hpos;
-  if (!F.met || F.phase != PH_DONE || F.err || pos >= F.L || st->err) return;
+  const unsigned long long H = st->hstart[h];
+  uint32_t pos = (uint32_t)(H >> 32), c = (uint32_t)H;
+  auto finish = [&](uint32_t p, uint32_t v) {   // (thread 0 of the one writer)
+    st->hstart[h + 1] = ((unsigned long long)p << 32) | v;
+  };
+  if (!F.met || F.phase != PH_DONE || F.err || pos >= F.L || c == NO_ROW) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) finish(pos, c);
+    return;
+  }
   const uint32_t L = F.L, kf = F.kf;
-  uint32_t c = (uint32_t)st->gv;
   const Cand none{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
   auto range = [&](uint32_t v, uint32_t* rs, uint32_t* re) {
     *rs = *re = 0;
-    if (v != NO_ROW && (!A.visible || A.visible[v])) {
-      *rs = A.row_ptr[0][v];
-      *re = A.row_ptr[0][v + 1];
+    if (v != NO_ROW && (!A.visible || gld(A.visible, v, A.nv, 14, st))) {
+      *rs = gld(A.row_ptr[0], v, A.nv + 1, 14, st);
+      *re = gld(A.row_ptr[0], (uint64_t)v + 1, A.nv + 1, 14, st);
     }
   };
   auto want_of = [&](uint32_t p, const uint32_t** vlab) {
@@ -564,20 +600,17 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ 
   // record hop p (thread 0): false when it has no candidate (reconstruction failure)
   auto record = [&](uint32_t p, const Cand& r) {
     if (r.d == NO_ROW) {
-      st->err |= 1ull;
-      st->gv = NO_ROW;
+      atomicOr(&st->err, 1ull);
+      finish(p, NO_ROW);
       return false;
     }
-    st->path[1 + 3 * p] = r.t;
-    st->path[2 + 3 * p] = r.r;
-    st->path[3 + 3 * p] = r.v;
-    st->gv = r.d;
-    st->hpos = p + 1;
+    gst(st->path, 1 + 3 * (uint64_t)p, 1 + 3 * (uint64_t)MAX_PATH_LEN, (long long)r.t, 15, st);
+    gst(st->path, 2 + 3 * (uint64_t)p, 1 + 3 * (uint64_t)MAX_PATH_LEN, (long long)r.r, 15, st);
+    gst(st->path, 3 + 3 * (uint64_t)p, 1 + 3 * (uint64_t)MAX_PATH_LEN, (long long)r.v, 15, st);
     return true;
   };
   uint32_t rs, re;
   range(c, &rs, &re);
-  bool solo;   // this workgroup walks on alone
   if (re - rs > CH_SOLO_DEG) {   // a hub: every workgroup scans a share
     const uint32_t* vlab;
     const uint32_t want = want_of(pos, &vlab);
@@ -610,16 +643,14 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ 
     if (!s_last) return;
     c = r.d;
     ++pos;
-    solo = true;
-  } else {
-    solo = blockIdx.x == 0;
+  } else if (blockIdx.x != 0) {
+    return;
   }
-  if (!solo) return;
+  // this workgroup alone: small hops
   if (threadIdx.x == 0) st->hlaunch += 1;
-  // one workgroup, small hops
   while (pos < L) {
     range(c, &rs, &re);
-    if (re - rs > CH_SOLO_DEG) return;   // a hub: the next launch spreads it
+    if (re - rs > CH_SOLO_DEG) break;   // a hub: the next launch spreads it
     const uint32_t* vlab;
     const uint32_t want = want_of(pos, &vlab);
     const Cand r = block_min(hop_scan(A, vlab, want, rs, re, threadIdx.x, CH_BLOCK), lds);
@@ -629,6 +660,7 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ 
     c = r.d;
     ++pos;
   }
+  if (threadIdx.x == 0) finish(pos, c);
 }
 
 // ---------------------------------------------------------------------------- host side
@@ -703,8 +735,8 @@ static hipError_t chain_batch(ChainCtx* c, int k, int h) {
   const ChArgs* A = c->d_args;
   for (int j = 0; j < k; ++j, ++c->steps)
     hipLaunchKernelGGL(k_ch_step, dim3(c->grid), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps);
-  for (int j = 0; j < h; ++j, ++c->hops)
-    hipLaunchKernelGGL(k_ch_hop, dim3(CH_HOP_WGS), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps - 1);
+  for (int j = 0; j < h && c->hops < CH_MAXS; ++j, ++c->hops)
+    hipLaunchKernelGGL(k_ch_hop, dim3(CH_HOP_WGS), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps - 1, c->hops);
   HIP_TRY_CH(hipGetLastError());
   ++c->batches;
   return hipMemcpyAsync(c->h_st, c->d_st, CH_COPY, hipMemcpyDeviceToHost, c->stream);
@@ -729,6 +761,9 @@ hipError_t chain_launch(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, con
   for (int i = 0; i < CH_NLISTS; ++i) a.list[i] = c->list[i];
   a.list_cap = c->list_cap;
   a.tsplit_cap = c->tsplit_cap;
+  a.nv = c->nv;
+  a.ne[0] = fwd.ne[0];
+  a.ne[1] = bwd.ne[0];
   a.st = c->d_st;
   if (!c->args_valid || memcmp(&a, &c->cached, sizeof(a)) != 0) {
     HIP_TRY_CH(hipStreamSynchronize(c->stream));   // the staging buffer may still feed an earlier upload
@@ -760,8 +795,9 @@ bool chain_more(ChainCtx* c, hipError_t* he) {
     *he = chain_batch(c, max_steps - c->steps, (int)c->q.upto);   // the rest, at once
     return false;
   }
-  if (F.met && !F.err && !h.err && h.hpos < F.L && c->hops < (int)c->q.upto) {
-    *he = chain_batch(c, 0, (int)F.L - (int)h.hpos);
+  const uint32_t hpos = (uint32_t)(h.hstart[c->hops] >> 32);
+  if (F.met && !F.err && !h.err && hpos < F.L && c->hops < CH_MAXS) {
+    *he = chain_batch(c, 0, (int)F.L - (int)hpos);
     return false;
   }
   // steps used: the BFS levels and B-set steps; decay toward this query's needs
@@ -779,8 +815,9 @@ void chain_result(const ChainCtx* c, SpResult* out) {
   out->err = h.err;
   out->edges = F.edges;
   out->levels = F.levels;
-  out->L = (F.met && !h.err && h.hpos == F.L) ? F.L : 0;
-  if (F.met && !h.err && h.hpos != F.L) out->err = 2;   // (cannot happen: the hops were enqueued)
+  const uint32_t hpos = (uint32_t)(h.hstart[c->hops] >> 32);
+  out->L = (F.met && !h.err && hpos == F.L) ? F.L : 0;
+  if (F.met && !h.err && hpos != F.L) out->err = 2;   // (cannot happen: the hops were enqueued)
   out->ntrace = 0;
   if (out->L) memcpy(out->path, h.path, (1 + 3 * (size_t)out->L) * sizeof(long long));
 }
