@@ -213,17 +213,30 @@ __device__ __forceinline__ uint32_t vdeg(const ChArgs& A, int side, uint32_t v, 
 
 // Entry pos of list L: vertex v, its deg edges ending at edge offset end, from row rs; the tile
 // boundaries its merge-path range [pos + end - deg, pos + end] covers get their split.
+constexpr uint32_t CH_SPLITS_SOLO = 4;   // an entry covering more tile boundaries: the wave writes them
+
+// Entry pos of list L: vertex v, its deg edges ending at edge offset end, from row rs.  The tile
+// boundaries its merge-path range [pos + end - deg, pos + end] covers, [*t0, *t1), get the entry
+// as their split; up to CH_SPLITS_SOLO of them are written here, the caller spreads the rest.
 __device__ __forceinline__ void list_put(const ChArgs& A, const ChList& L, uint32_t pos, uint32_t v, uint32_t end,
-                                         uint32_t deg, uint32_t rs) {
+                                         uint32_t deg, uint32_t rs, uint64_t* t0, uint64_t* t1) {
   gst(L.ids, pos, A.list_cap, v, 2, A.st);
   gst(L.seg_end, pos, A.list_cap, end, 2, A.st);
   gst(L.seg_rs, pos, A.list_cap, rs, 2, A.st);
   const uint64_t lo = (uint64_t)pos + end - deg, hi = (uint64_t)pos + end;
-  for (uint64_t t = (lo + CH_TILE - 1) / CH_TILE; t * CH_TILE <= hi && t < A.tsplit_cap; ++t) L.tsplit[t] = pos;
+  const uint64_t a = (lo + CH_TILE - 1) / CH_TILE;
+  const uint64_t b = hi / CH_TILE + 1 < A.tsplit_cap ? hi / CH_TILE + 1 : A.tsplit_cap;
+  *t0 = a;
+  *t1 = a < b ? b : a;
+  if (*t1 - *t0 <= CH_SPLITS_SOLO) {
+    for (uint64_t t = a; t < b; ++t) L.tsplit[t] = pos;
+    *t1 = *t0;
+  }
 }
 
 // Appends, per lane, the vertices x[i] with bit i of `m` and a nonzero degree (dg[i], rs[i]) to
-// list L (counter *acc): one packed atomic per wave for positions and edge offsets.
+// list L (counter *acc): one packed atomic per wave for positions and edge offsets; the tile
+// splits of hubs (entries spanning many tiles) are written by the whole wave, lane-strided.
 __device__ __forceinline__ void wave_append(const ChArgs& A, const ChList& L, unsigned long long* acc,
                                             const uint32_t (&x)[CH_VT], uint32_t m, const uint32_t (&dg)[CH_VT],
                                             const uint32_t (&rs)[CH_VT]) {
@@ -248,11 +261,22 @@ __device__ __forceinline__ void wave_append(const ChArgs& A, const ChList& L, un
   uint32_t pos = (uint32_t)(old >> 32) + ic - c;
   uint32_t end = (uint32_t)old + id - d;
 #pragma unroll
-  for (int i = 0; i < CH_VT; ++i)
+  for (int i = 0; i < CH_VT; ++i) {
+    uint64_t t0 = 0, t1 = 0;
+    uint32_t p = pos;
     if (((m >> i) & 1u) && dg[i]) {
       end += dg[i];
-      list_put(A, L, pos++, x[i], end, dg[i], rs[i]);
+      list_put(A, L, pos++, x[i], end, dg[i], rs[i], &t0, &t1);
     }
+    unsigned long long bm = __ballot(t1 > t0);
+    while (bm) {   // hubs of this round: the wave writes their tile splits
+      const int l = __ffsll((long long)bm) - 1;
+      bm &= bm - 1;
+      const uint64_t a = __shfl(t0, l, 64), b = __shfl(t1, l, 64);
+      const uint32_t hp = __shfl(p, l, 64);
+      for (uint64_t t = a + (uint64_t)lane; t < b; t += 64) L.tsplit[t] = hp;
+    }
+  }
 }
 
 // The snapshot step launch i runs under: snap[0] (set-up) or derived from launch i - 1.
@@ -374,6 +398,9 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_step(const ChArgs* __restrict__
   uint32_t* const sRs = sRsAll[w];
   uint16_t* const sSeg = sSegAll[w];
   for (uint64_t t = (uint64_t)blockIdx.x * CH_WAVES + w; t < ntiles; t += (uint64_t)gridDim.x * CH_WAVES) {
+    // once this level has met, its claims are not expanded again: their appends are skipped
+    // (read now, used after the claims: the load is off the critical path)
+    const unsigned long long met_now = bfs ? ld_agent(&st->lmeet[i]) : 0ull;
     uint64_t sp = 0;
     if (ntiles > 1) {
       if (lane == 0) sp = gld(S.tsplit, t, A.tsplit_cap, 3, st);
@@ -469,7 +496,7 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_step(const ChArgs* __restrict__
       for (int j = 0; j < CH_VT; ++j)
         if (((cm >> j) & 1u) && live(ol[j], oepoch)) mm |= 1u << j;
     }
-    if (append) {
+    if (append && !met_now) {
       uint32_t dg[CH_VT], rs[CH_VT];
 #pragma unroll
       for (int j = 0; j < CH_VT; ++j) {
