@@ -478,17 +478,32 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_step(const ChArgs* __restrict__
       old[j] = c[j] != NO_ROW ? gld(lab, c[j], A.nv, 8, st) : 0u;
       gate[j] = (c[j] != NO_ROW && rlab) ? gld(rlab, c[j], A.nv, 8, st) : rstamp;
     }
-    uint32_t cm = 0;
+    uint32_t cm = 0, mm = 0;
+    if (met_now) {
+      // the level has met: only meet vertices matter now (B[kf] is the met set; this level's other
+      // labels are read by nothing), so the other side's label is tested before claiming
+      uint32_t ol[CH_VT];
 #pragma unroll
-    for (int j = 0; j < CH_VT; ++j) {
-      if (c[j] == NO_ROW || gate[j] != rstamp || live(old[j], epoch)) continue;
-      if (CH_GUARD && c[j] >= A.nv) continue;
-      if (atomicCAS(lab + c[j], old[j], stamp) != old[j]) continue;
-      cm |= 1u << j;
+      for (int j = 0; j < CH_VT; ++j)
+        ol[j] = (c[j] != NO_ROW && !live(old[j], epoch)) ? gld(olab, c[j], A.nv, 9, st) : 0u;
+#pragma unroll
+      for (int j = 0; j < CH_VT; ++j) {
+        if (c[j] == NO_ROW || live(old[j], epoch) || !live(ol[j], oepoch)) continue;
+        if (CH_GUARD && c[j] >= A.nv) continue;
+        if (atomicCAS(lab + c[j], old[j], stamp) != old[j]) continue;
+        mm |= 1u << j;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < CH_VT; ++j) {
+        if (c[j] == NO_ROW || gate[j] != rstamp || live(old[j], epoch)) continue;
+        if (CH_GUARD && c[j] >= A.nv) continue;
+        if (atomicCAS(lab + c[j], old[j], stamp) != old[j]) continue;
+        cm |= 1u << j;
+      }
     }
-    if (!__ballot(cm != 0)) continue;
-    uint32_t mm = 0;
-    if (bfs) {   // meet test: claimed vertices only (most neighbours of a big level are not)
+    if (!__ballot((cm | mm) != 0)) continue;
+    if (bfs && !met_now) {   // meet test: claimed vertices only (most neighbours of a big level are not)
       uint32_t ol[CH_VT];
 #pragma unroll
       for (int j = 0; j < CH_VT; ++j) ol[j] = ((cm >> j) & 1u) ? gld(olab, c[j], A.nv, 9, st) : 0u;
