@@ -610,6 +610,7 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
   hipError_t he = ws_reserve_rows(ws, cap_rows, ncols);
   if (he == hipSuccess) he = ws_begin_query(ws, f0.data(), f0.size(), &plist, st->id);
   uint64_t n_bound = f0.size();
+  ws_set_mark_claims(ws, over.size() == 1);
   for (uint32_t s = 1; he == hipSuccess && s <= steps; ++s) {
     const bool final = s == steps;
     // the next step's first OVER type: the next frontier list carries its edge space

@@ -84,7 +84,8 @@ struct Workspace {
   uint32_t* seen = nullptr;       // [nv + 1] claim stamps of the per-step dst SET (single engine)
   uint32_t seen_stamp = 0;        // last stamp handed out
   uint32_t step_stamp = 0;        // stamp of the current step (all its OVER types)
-  bool mark_flags = false;        // NBG_MARK_FLAGS=1: byte flags + k_compact instead of claims
+  bool mark_flags = false;        // this query: byte flags + k_compact instead of claims
+  bool env_flags = false;         // NBG_MARK_FLAGS=1: always flags
   uint32_t* rlist = nullptr;      // k_relist output list
   uint8_t* flags = nullptr;       // [nv rounded up to FLAG_ALIGN], kept all-zero between steps
   uint64_t flag_bytes = 0;
@@ -1407,7 +1408,8 @@ Workspace* ws_create(uint64_t max_frontier, uint64_t nv, uint64_t e_max, hipStre
   w->cap_tiles = cdiv(w->cap_frontier + e_max + 1, TILE) + 2;
   M((void**)&w->tsplit, w->cap_tiles * 4);
   M((void**)&w->tsplit1, w->cap_tiles * 4);
-  w->mark_flags = getenv("NBG_MARK_FLAGS") && atoi(getenv("NBG_MARK_FLAGS")) != 0;
+  w->env_flags = getenv("NBG_MARK_FLAGS") && atoi(getenv("NBG_MARK_FLAGS")) != 0;
+  w->mark_flags = w->env_flags;
   // QState and the per-workgroup row counts are one allocation: one copy ends a query
   M((void**)&w->q, sizeof(QState) + (size_t)MAX_TYPES_Q * EXPAND_GRID * 4);
   M((void**)&w->d_prog, (size_t)MAX_TYPES_Q * MAX_PROGRAM * sizeof(Ins));
@@ -1659,6 +1661,18 @@ hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, 
                        NoInline{});
   prof_end(w, p, K_EXPAND_MARK, step, tix);
   return hipGetLastError();
+}
+
+// Claims suit one OVER type (one claim per distinct neighbour); with several types the same
+// vertices are reached through each, and the claim CAS on hot vertices costs more than plain
+// byte flags plus one compaction (C5's knows + likes: 61.9 vs 126.8 G edges/s).
+// The two modes keep different accumulator-slot invariants (claims: slot 2 + (step + 1) % 3, its
+// successor zeroed by the step's first launch; flags: a ping-pong pair zeroed by k_compact), so a
+// switch clears the slots first.
+void ws_set_mark_claims(Workspace* w, bool claims) {
+  const bool flags = w->env_flags || !claims;
+  if (flags != w->mark_flags) (void)hipMemsetAsync(&w->q->acc[2], 0, 3 * sizeof(unsigned long long), w->stream);
+  w->mark_flags = flags;
 }
 
 hipError_t ws_finish_step(Workspace* w, int step, const ExpandArgs* next0) {
