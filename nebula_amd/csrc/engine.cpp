@@ -165,7 +165,6 @@ int32_t materialize_rows(nbg_rows* r) {
   return NBG_OK;
 }
 
-const char* kGoUnsupportedDistinct = "YIELD DISTINCT is not supported on a partitioned engine yet";
 
 }  // namespace
 
@@ -258,7 +257,6 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
     }
   }
   if (over.empty()) return E.fail(NBG_E_EXECUTION_ERROR, "empty OVER clause");
-  if (rq->distinct && E.partitioned()) return E.fail(NBG_E_UNSUPPORTED, kGoUnsupportedDistinct);
   // WHERE / YIELD
   std::string err;
   std::unique_ptr<Node> where;
@@ -716,28 +714,45 @@ static int32_t go_collect(Engine& E, const nbg_go_stmt* st, GoPending* p, nbg_ro
     rows->count += c;
     rows->blocks.push_back(std::move(tb));
   }
-  if (st->distinct && rows->count) {
-    // YIELD DISTINCT on the device: segments deduplicated and compacted in place
-    std::vector<std::array<uint64_t, 3>> segs;
-    std::vector<std::pair<size_t, size_t>> where;   // (type, block) of each segment
-    for (size_t i = 0; i < rows->blocks.size(); ++i) {
-      const auto& tb = rows->blocks[i];
-      for (size_t b = 0; b < tb.counts.size(); ++b) {
-        if (!tb.counts[b]) continue;
-        segs.push_back({tb.region + (uint64_t)b * tb.blk_cap, tb.counts[b], (uint64_t)i});
-        where.emplace_back(i, b);
+  if (st->distinct && (rows->count || E.partitioned())) {
+    // YIELD DISTINCT on the device: segments deduplicated and compacted in place; partitioned,
+    // the survivors then travel to the rank their identity hashes to, which deduplicates again
+    // (every rank takes part: the exchange is collective)
+    auto segments = [&](std::vector<std::pair<size_t, size_t>>* where) {
+      std::vector<std::array<uint64_t, 3>> segs;
+      for (size_t i = 0; i < rows->blocks.size(); ++i) {
+        const auto& tb = rows->blocks[i];
+        for (size_t b = 0; b < tb.counts.size(); ++b) {
+          if (!tb.counts[b]) continue;
+          segs.push_back({tb.region + (uint64_t)b * tb.blk_cap, tb.counts[b], (uint64_t)i});
+          if (where) where->emplace_back(i, b);
+        }
       }
-    }
+      return segs;
+    };
+    std::vector<std::pair<size_t, size_t>> where;   // (type, block) of each segment
+    std::vector<std::array<uint64_t, 3>> segs = segments(&where);
     std::vector<uint32_t> kept;
     hipError_t de = ws_distinct(ws, segs, ncols, rows->kinds, &kept);
+    rows->count = 0;
+    for (size_t k = 0; de == hipSuccess && k < segs.size(); ++k) {
+      rows->blocks[where[k].first].counts[where[k].second] = kept[k];
+      rows->count += kept[k];
+    }
+    if (de == hipSuccess && E.partitioned()) {
+      std::vector<DistinctBlock> db;
+      de = ws_distinct_exchange(ws, segments(nullptr), ncols, rows->kinds, &db);
+      rows->count = 0;
+      for (size_t i = 0; de == hipSuccess && i < rows->blocks.size() && i < db.size(); ++i) {
+        rows->blocks[i].region = db[i].region;
+        rows->blocks[i].blk_cap = db[i].blk_cap;
+        rows->blocks[i].counts = db[i].counts;
+        for (uint32_t c : db[i].counts) rows->count += c;
+      }
+    }
     if (de != hipSuccess) {
       delete rows;
       return E.fail(NBG_E_DEVICE, std::string("HIP (distinct): ") + hipGetErrorString(de));
-    }
-    rows->count = 0;
-    for (size_t k = 0; k < segs.size(); ++k) {
-      rows->blocks[where[k].first].counts[where[k].second] = kept[k];
-      rows->count += kept[k];
     }
   }
   for (int c = 0; c < ncols; ++c) rows->dcols.push_back(ws_row_col(ws, c));

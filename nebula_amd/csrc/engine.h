@@ -73,6 +73,9 @@ struct Engine {
   int32_t upload_vertices(const std::vector<uint8_t>& visible, bool all_visible);
   int32_t save_snapshot(const char* path);
   int32_t load_snapshot(const char* path);
+  // partitioned: the union of every rank's sorted string set (one dictionary, so string codes
+  // mean the same on every rank: gathered $$ columns, rows exchanged for DISTINCT)
+  int32_t exchange_strings(std::vector<std::string>* strings);
   int32_t exchange_dictionary(const std::vector<int64_t>& local, std::vector<int64_t>* gdict,
                               std::vector<uint64_t>* gcount);
   uint32_t dense(int64_t vid) const;

@@ -477,10 +477,6 @@ struct Ctx {
     }
     Compiled c;
     c.kind = dt->kind[col];
-    if (env.partitioned && c.kind == VK_STRING) {
-      *err = "$$ STRING props on a partitioned engine";
-      return NBG_E_UNSUPPORTED;
-    }
     c.reg = push();
     emit(OP_TAGD, c.reg, 0, 0, (dt->index << 16) | (dt->col_base + col), default_bits(c.kind));
     if (env.probe_mask) *env.probe_mask |= 1u << dt->index;

@@ -84,6 +84,14 @@ struct Workspace {
   uint32_t* seen = nullptr;       // [nv + 1] claim stamps of the per-step dst SET (single engine)
   uint32_t seen_stamp = 0;        // last stamp handed out
   uint32_t step_stamp = 0;        // stamp of the current step (all its OVER types)
+  // partitioned DISTINCT exchange scratch (row owners, counts, send / receive buffers)
+  uint32_t* xown = nullptr;
+  uint64_t xown_cap = 0;
+  unsigned long long* xcnt = nullptr;
+  uint64_t xcnt_cap = 0;
+  int64_t* xsend = nullptr;
+  int64_t* xrecv = nullptr;
+  uint64_t xsend_cap = 0, xrecv_cap = 0;
   bool mark_flags = false;        // this query: byte flags + k_compact instead of claims
   bool env_flags = false;         // NBG_MARK_FLAGS=1: always flags
   uint32_t* rlist = nullptr;      // k_relist output list
@@ -1281,6 +1289,73 @@ __global__ void __launch_bounds__(BLOCK) k_distinct_compact(const uint64_t* __re
   }
 }
 
+// Partitioned DISTINCT: every row goes to the rank its identity hashes to (equal rows meet at one
+// owner, whatever rank produced them); the owners then deduplicate locally.
+// seg as for k_distinct_mark, with seg[4k + 2] = the segment's first row in the global row order.
+__device__ __forceinline__ uint64_t row_hash(int64_t* const* cols, int ncols, const uint8_t* kinds, uint32_t ty,
+                                            uint64_t row) {
+  uint64_t h = 0x6E6562756C61ull;
+  for (int c = 0; c < ncols; ++c)
+    h = mix64(h ^ (uint64_t)cols[c][row] ^ ((uint64_t)kinds[ty * MAX_YIELDS + c] << 61) ^ (uint64_t)c);
+  return h;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_row_route(const uint64_t* __restrict__ seg, int nseg,
+                                                     int64_t* const* __restrict__ cols, int ncols,
+                                                     const uint8_t* __restrict__ kinds, int world, int ntypes,
+                                                     uint32_t* __restrict__ owner,
+                                                     unsigned long long* __restrict__ cnt) {
+  for (int k = blockIdx.x; k < nseg; k += gridDim.x) {
+    const uint64_t b = seg[4 * k], len = seg[4 * k + 1], go = seg[4 * k + 2];
+    const uint32_t ty = (uint32_t)seg[4 * k + 3];
+    for (uint64_t i = threadIdx.x; i < len; i += BLOCK) {
+      const uint32_t q = (uint32_t)(row_hash(cols, ncols, kinds, ty, b + i) >> 33) % (uint32_t)world;
+      owner[go + i] = q;
+      atomicAdd(&cnt[(uint64_t)q * ntypes + ty], 1ull);
+    }
+  }
+}
+
+// send[(q * maxc + base[q][ty] + cursor) * ncols + c] <- row; rows of one (owner, type) contiguous
+__global__ void __launch_bounds__(BLOCK) k_row_pack(const uint64_t* __restrict__ seg, int nseg,
+                                                    int64_t* const* __restrict__ cols, int ncols,
+                                                    const uint32_t* __restrict__ owner, int ntypes,
+                                                    const unsigned long long* __restrict__ base,
+                                                    unsigned long long* __restrict__ cursor, uint64_t maxc,
+                                                    int64_t* __restrict__ send) {
+  for (int k = blockIdx.x; k < nseg; k += gridDim.x) {
+    const uint64_t b = seg[4 * k], len = seg[4 * k + 1], go = seg[4 * k + 2];
+    const uint32_t ty = (uint32_t)seg[4 * k + 3];
+    for (uint64_t i = threadIdx.x; i < len; i += BLOCK) {
+      const uint32_t q = owner[go + i];
+      const uint64_t slot = (uint64_t)q * ntypes + ty;
+      const uint64_t pos = base[slot] + atomicAdd(&cursor[slot], 1ull);
+      int64_t* o = send + ((uint64_t)q * maxc + pos) * ncols;
+      for (int c = 0; c < ncols; ++c) o[c] = cols[c][b + i];
+    }
+  }
+}
+
+// received rows of rank r (recv[(r * maxc + j) * ncols ..], j < n_r, type-major) -> the result
+// columns at place[r * ntypes + ty] + (j - first row of that type)
+__global__ void __launch_bounds__(BLOCK) k_row_unpack(const int64_t* __restrict__ recv, int world, int ntypes,
+                                                      uint64_t maxc, int ncols,
+                                                      const unsigned long long* __restrict__ rcnt,
+                                                      const unsigned long long* __restrict__ place,
+                                                      int64_t* const* __restrict__ cols) {
+  const int r = blockIdx.y;
+  uint64_t n = 0;
+  for (int t = 0; t < ntypes; ++t) n += rcnt[(uint64_t)r * ntypes + t];
+  for (uint64_t j = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < n; j += (uint64_t)gridDim.x * BLOCK) {
+    uint64_t k = j;
+    int t = 0;
+    while (k >= rcnt[(uint64_t)r * ntypes + t]) k -= rcnt[(uint64_t)r * ntypes + t++];
+    const uint64_t dst = place[(uint64_t)r * ntypes + t] + k;
+    const int64_t* in = recv + ((uint64_t)r * maxc + j) * ncols;
+    for (int c = 0; c < ncols; ++c) cols[c][dst] = in[c];
+  }
+}
+
 // ============================================================================= host side
 static inline uint64_t cdiv(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
@@ -1441,7 +1516,8 @@ void ws_destroy(Workspace* w) {
                   (void*)w->rlist, (void*)w->flags, (void*)w->tsplit,
                   (void*)w->q, (void*)w->rows,
                   (void*)w->d_row_cols, (void*)w->d_prog, (void*)w->dtab, (void*)w->dkeep, (void*)w->dseg,
-                  (void*)w->dcnt, (void*)w->dkinds, (void*)w->bt, (void*)w->walk_arena})
+                  (void*)w->dcnt, (void*)w->dkinds, (void*)w->bt, (void*)w->walk_arena, (void*)w->xown,
+                  (void*)w->xcnt, (void*)w->xsend, (void*)w->xrecv})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)w->h_q, (void*)w->h_starts, (void*)w->h_prog, (void*)w->h_ps, (void*)w->h_path,
                   (void*)w->h_stage})
@@ -1908,6 +1984,128 @@ hipError_t ws_distinct(Workspace* w, const std::vector<std::array<uint64_t, 3>>&
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(counts->data(), w->dcnt, segs.size() * 4, hipMemcpyDeviceToHost, w->stream));
   return hipStreamSynchronize(w->stream);
+}
+
+hipError_t ws_distinct_exchange(Workspace* w, const std::vector<std::array<uint64_t, 3>>& segs, int ncols,
+                                const std::vector<std::vector<VKind>>& kinds, std::vector<DistinctBlock>* out) {
+  Comm* comm = w->comm;
+  const int G = comm ? comm->world : 1, me = comm ? comm->rank : 0;
+  const int T = (int)kinds.size();
+  if (!comm || T < 1 || T > MAX_TYPES_Q || ncols < 1) return hipErrorInvalidValue;
+  uint64_t total = 0;
+  std::vector<uint64_t> meta;
+  for (auto& sg : segs) {
+    meta.insert(meta.end(), {sg[0], sg[1], total, sg[2]});
+    total += sg[1];
+  }
+  HIP_TRY(hipStreamSynchronize(w->stream));
+  // scratch: owners, counts [G][T] local and gathered, bases, cursors
+  auto grow = [&](void** p, uint64_t* cap, uint64_t need) -> hipError_t {
+    if (need <= *cap) return hipSuccess;
+    if (*p) HIP_TRY(hipFree(*p));
+    *p = nullptr;
+    *cap = need + need / 2 + 4096;
+    return hipMalloc(p, *cap);
+  };
+  const uint64_t GT = (uint64_t)G * T;
+  HIP_TRY(grow((void**)&w->xown, &w->xown_cap, std::max<uint64_t>(total, 1) * 4));
+  HIP_TRY(grow((void**)&w->xcnt, &w->xcnt_cap, (GT + (uint64_t)G * GT + 2 * GT) * 8));
+  unsigned long long* cnt = w->xcnt;            // [G][T] this rank's rows per (owner, type)
+  unsigned long long* all = cnt + GT;           // [G ranks][G][T]
+  unsigned long long* base = all + (uint64_t)G * GT;
+  unsigned long long* cursor = base + GT;
+  if (!w->dkinds) HIP_TRY(hipMalloc((void**)&w->dkinds, MAX_TYPES_Q * MAX_YIELDS));
+  uint8_t hk[MAX_TYPES_Q * MAX_YIELDS] = {};
+  for (int t = 0; t < T; ++t)
+    for (size_t c = 0; c < kinds[t].size() && c < (size_t)MAX_YIELDS; ++c) hk[t * MAX_YIELDS + c] = (uint8_t)kinds[t][c];
+  HIP_TRY(hipMemcpy(w->dkinds, hk, sizeof(hk), hipMemcpyHostToDevice));
+  if (segs.size() > w->dseg_cap) {
+    if (w->dseg) HIP_TRY(hipFree(w->dseg));
+    if (w->dcnt) HIP_TRY(hipFree(w->dcnt));
+    w->dseg = nullptr;
+    w->dcnt = nullptr;
+    HIP_TRY(hipMalloc((void**)&w->dseg, segs.size() * 32));
+    HIP_TRY(hipMalloc((void**)&w->dcnt, segs.size() * 4));
+    w->dseg_cap = segs.size();
+  }
+  if (!meta.empty()) HIP_TRY(hipMemcpy(w->dseg, meta.data(), meta.size() * 8, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemsetAsync(cnt, 0, GT * 8, w->stream));
+  const unsigned grid = (unsigned)std::min<uint64_t>(std::max<size_t>(segs.size(), 1), 8192);
+  if (!segs.empty()) {
+    hipLaunchKernelGGL(k_row_route, dim3(grid), dim3(BLOCK), 0, w->stream, w->dseg, (int)segs.size(), w->d_row_cols,
+                       ncols, w->dkinds, G, T, w->xown, cnt);
+    HIP_TRY(hipGetLastError());
+  }
+  if (comm->allgather(cnt, all, GT * 8, w->stream)) return hipErrorUnknown;
+  HIP_TRY(hipStreamSynchronize(w->stream));
+  std::vector<unsigned long long> h_all((uint64_t)G * GT);
+  HIP_TRY(hipMemcpy(h_all.data(), all, h_all.size() * 8, hipMemcpyDeviceToHost));
+  auto at = [&](int r, int q, int t) { return h_all[(uint64_t)r * GT + (uint64_t)q * T + t]; };
+  uint64_t maxc = 1;
+  for (int r = 0; r < G; ++r)
+    for (int q = 0; q < G; ++q) {
+      uint64_t n = 0;
+      for (int t = 0; t < T; ++t) n += at(r, q, t);
+      maxc = std::max(maxc, n);
+    }
+  std::vector<unsigned long long> h_base(GT);
+  for (int q = 0; q < G; ++q) {
+    uint64_t o = 0;
+    for (int t = 0; t < T; ++t) {
+      h_base[(uint64_t)q * T + t] = o;
+      o += at(me, q, t);
+    }
+  }
+  HIP_TRY(hipMemcpy(base, h_base.data(), GT * 8, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemsetAsync(cursor, 0, GT * 8, w->stream));
+  const uint64_t xbytes = (uint64_t)G * maxc * ncols * 8;
+  HIP_TRY(grow((void**)&w->xsend, &w->xsend_cap, xbytes));
+  HIP_TRY(grow((void**)&w->xrecv, &w->xrecv_cap, xbytes));
+  if (!segs.empty()) {
+    hipLaunchKernelGGL(k_row_pack, dim3(grid), dim3(BLOCK), 0, w->stream, w->dseg, (int)segs.size(), w->d_row_cols,
+                       ncols, w->xown, T, base, cursor, maxc, w->xsend);
+    HIP_TRY(hipGetLastError());
+  }
+  if (comm->alltoall(w->xsend, w->xrecv, maxc * ncols * 8, w->stream)) return hipErrorUnknown;
+  HIP_TRY(hipStreamSynchronize(w->stream));
+  // this rank's rows by type: type t's block b = rows received from rank b
+  out->assign(T, DistinctBlock{});
+  std::vector<unsigned long long> h_rcnt(GT), h_place(GT);
+  uint64_t region = 0;
+  for (int t = 0; t < T; ++t) {
+    uint64_t cap = 0;
+    for (int r = 0; r < G; ++r) cap = std::max<uint64_t>(cap, at(r, me, t));
+    (*out)[t].region = region;
+    (*out)[t].blk_cap = cap;
+    (*out)[t].counts.assign(G, 0);
+    for (int r = 0; r < G; ++r) {
+      h_rcnt[(uint64_t)r * T + t] = at(r, me, t);
+      h_place[(uint64_t)r * T + t] = region + (uint64_t)r * cap;
+    }
+    region += (uint64_t)G * cap;
+  }
+  HIP_TRY(ws_reserve_rows(w, std::max<uint64_t>(region, 1), ncols));
+  HIP_TRY(hipMemcpy(base, h_rcnt.data(), GT * 8, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(cursor, h_place.data(), GT * 8, hipMemcpyHostToDevice));
+  if (region) {
+    hipLaunchKernelGGL(k_row_unpack, dim3((unsigned)std::min<uint64_t>((maxc + BLOCK - 1) / BLOCK, 4096), (unsigned)G),
+                       dim3(BLOCK), 0, w->stream, w->xrecv, G, T, maxc, ncols, base, cursor, w->d_row_cols);
+    HIP_TRY(hipGetLastError());
+  }
+  // the owner's deduplication over what it received
+  std::vector<std::array<uint64_t, 3>> rsegs;
+  std::vector<std::pair<int, int>> where;
+  for (int t = 0; t < T; ++t)
+    for (int r = 0; r < G; ++r) {
+      const uint64_t n = at(r, me, t);
+      if (!n) continue;
+      rsegs.push_back({(*out)[t].region + (uint64_t)r * (*out)[t].blk_cap, n, (uint64_t)t});
+      where.emplace_back(t, r);
+    }
+  std::vector<uint32_t> kept;
+  HIP_TRY(ws_distinct(w, rsegs, ncols, kinds, &kept));
+  for (size_t k = 0; k < rsegs.size(); ++k) (*out)[where[k].first].counts[where[k].second] = kept[k];
+  return hipSuccess;
 }
 
 uint32_t* ws_backtracker(Workspace* w) {

@@ -283,6 +283,57 @@ int32_t Engine::load_edges(int32_t type, const int64_t* src, const int64_t* dst,
 // ----------------------------------------------------------------------------- finalize
 // Every rank learns every rank's sorted vertex dictionary (allgather over the communicator):
 // npad = the largest dictionary rounded up to PART_ALIGN.
+int32_t Engine::exchange_strings(std::vector<std::string>* strings) {
+  if (!comm) return fail(NBG_E_STATE, "a partitioned engine (num_gpus > 1) needs nbg_comm_init before nbg_finalize");
+  const uint64_t G = (uint64_t)cfg.num_gpus;
+  std::string blob;   // [u32 length][bytes] per string
+  for (const std::string& x : *strings) {
+    const uint32_t n = (uint32_t)x.size();
+    blob.append(reinterpret_cast<const char*>(&n), 4);
+    blob += x;
+  }
+  uint64_t* d_cnt = nullptr;
+  char *d_loc = nullptr, *d_glob = nullptr;
+  auto done = [&](int32_t rc, const std::string& msg) {
+    for (void* p : {(void*)d_cnt, (void*)d_loc, (void*)d_glob})
+      if (p) (void)hipFree(p);
+    return rc ? fail(rc, msg) : NBG_OK;
+  };
+  const uint64_t nb = blob.size();
+  if (hipMalloc((void**)&d_cnt, (G + 1) * 8) != hipSuccess || hipMemcpy(d_cnt + G, &nb, 8, hipMemcpyHostToDevice) != hipSuccess)
+    return done(NBG_E_OUT_OF_MEMORY, "string dictionary exchange: device allocation");
+  if (comm->allgather(d_cnt + G, d_cnt, 8, stream) || hipStreamSynchronize(stream) != hipSuccess)
+    return done(NBG_E_DEVICE, "string dictionary exchange (sizes): " + comm->last);
+  std::vector<uint64_t> sizes(G);
+  if (hipMemcpy(sizes.data(), d_cnt, G * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return done(NBG_E_DEVICE, "string dictionary exchange: copy");
+  uint64_t mx = 8;
+  for (uint64_t c : sizes) mx = std::max(mx, (c + 7) / 8 * 8);
+  if (hipMalloc((void**)&d_loc, mx) != hipSuccess || hipMalloc((void**)&d_glob, G * mx) != hipSuccess)
+    return done(NBG_E_OUT_OF_MEMORY, "string dictionary exchange: device allocation");
+  if (nb && hipMemcpy(d_loc, blob.data(), nb, hipMemcpyHostToDevice) != hipSuccess)
+    return done(NBG_E_DEVICE, "string dictionary exchange: upload");
+  if (comm->allgather(d_loc, d_glob, mx, stream) || hipStreamSynchronize(stream) != hipSuccess)
+    return done(NBG_E_DEVICE, "string dictionary exchange (bytes): " + comm->last);
+  std::string all(G * mx, '\0');
+  if (hipMemcpy(&all[0], d_glob, G * mx, hipMemcpyDeviceToHost) != hipSuccess)
+    return done(NBG_E_DEVICE, "string dictionary exchange: download");
+  std::vector<std::string> u;
+  for (uint64_t q = 0; q < G; ++q) {
+    const char* p = all.data() + q * mx;
+    for (uint64_t o = 0; o + 4 <= sizes[q];) {
+      uint32_t n;
+      memcpy(&n, p + o, 4);
+      u.emplace_back(p + o + 4, n);
+      o += 4 + n;
+    }
+  }
+  std::sort(u.begin(), u.end());
+  u.erase(std::unique(u.begin(), u.end()), u.end());
+  *strings = std::move(u);
+  return done(NBG_OK, "");
+}
+
 int32_t Engine::exchange_dictionary(const std::vector<int64_t>& local, std::vector<int64_t>* gdict,
                                     std::vector<uint64_t>* gcount) {
   if (!comm) return fail(NBG_E_STATE, "a partitioned engine (num_gpus > 1) needs nbg_comm_init before nbg_finalize");
@@ -521,6 +572,14 @@ int32_t Engine::finalize() {
     for (auto id : order) {
       if (snap.strings.empty() || snap.strings.back() != pool[id]) snap.strings.push_back(pool[id]);
       remap[id] = 2 * (int64_t)(snap.strings.size() - 1);
+    }
+    if (partitioned()) {   // one dictionary over all ranks: codes are rank-independent
+      if (int32_t rc = exchange_strings(&snap.strings)) {
+        const std::string msg = last_error;
+        return bail(rc, msg);
+      }
+      for (size_t id = 0; id < pool.size(); ++id)
+        remap[id] = 2 * (int64_t)(std::lower_bound(snap.strings.begin(), snap.strings.end(), pool[id]) - snap.strings.begin());
     }
   }
   // 2. vertex dictionary on the device: every vid that owns a row (the source of any signed

@@ -411,6 +411,16 @@ hipError_t ws_rows_digest(Workspace* w, const std::vector<std::pair<uint64_t, ui
                           uint64_t out[3]);
 const QState* ws_host_state(Workspace* w);       // valid after ws_end_query
 // YIELD DISTINCT: dedup + in-place compaction of result segments (first row, rows, OVER index)
+// Partitioned YIELD DISTINCT: rows hashed to their owner rank (all-to-all), deduplicated there.
+// Collective: every rank calls it, with its own (already locally deduplicated) segments.  The
+// rank's rows are then, per OVER type t, blocks r = 0..G-1 at out[t].region + r * out[t].blk_cap
+// holding out[t].counts[r] rows (the rows received from rank r).
+struct DistinctBlock {
+  uint64_t region = 0, blk_cap = 0;
+  std::vector<uint32_t> counts;
+};
+hipError_t ws_distinct_exchange(Workspace* w, const std::vector<std::array<uint64_t, 3>>& segs, int ncols,
+                                const std::vector<std::vector<VKind>>& kinds, std::vector<DistinctBlock>* out);
 hipError_t ws_distinct(Workspace* w, const std::vector<std::array<uint64_t, 3>>& segs, int ncols,
                        const std::vector<std::vector<VKind>>& kinds, std::vector<uint32_t>* counts);
 const uint32_t* ws_current_frontier(Workspace* w);

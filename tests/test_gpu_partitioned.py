@@ -237,3 +237,50 @@ def test_partitioned_async_slots(rmat11, world):
         exp = single.go([r], [graphs.E_TYPE], 3, wb)
         assert graphs.sorted_rows(rows) == graphs.sorted_rows(exp), r
         assert all(rk[i][1] == per_rank[0][i][1] for rk in per_rank)
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("steps", [1, 2, 3])
+def test_partitioned_distinct_matches_single(rmat11, world, steps):
+    """YIELD DISTINCT on a partitioned engine: each rank deduplicates its rows, the survivors go to
+    the rank their identity hashes to (all-to-all) and are deduplicated there, so the union of the
+    ranks' rows has every distinct row exactly once — the single engine's DISTINCT result."""
+    src, single, orc, clusters = rmat11
+    c = clusters[world]
+    wb = WHERES["w<50"].encode()
+    for yields in ([E.edge_prop("e", "_dst").encode()],
+                   [E.edge_prop("e", "w").encode(), E.binop("%", E.edge_prop("e", "_dst"), E.const(7)).encode()]):
+        for r in graphs.roots(src, 2, seed=steps):
+            got = graphs.sorted_rows(c.go([r], [1], steps, wb, yields, distinct=True))
+            ref = graphs.sorted_rows(single.go([r], [1], steps, wb, yields, distinct=True))
+            assert got == ref, (world, steps, r, len(got), len(ref))
+            assert len(set(map(tuple, got))) == len(got)
+            assert got == graphs.sorted_rows(orc.go([r], [1], steps, wb, yields, distinct=True))
+
+
+def test_partitioned_nba_golden_needs_no_skips(nba_data):
+    """Every GO golden case the single engine runs also runs on 3 ranks (DISTINCT, $$ STRING):
+    only $- / $var props in YIELD / WHERE after several steps are still single-engine."""
+    c = LocalCluster(7, 3)
+    for (kind, name), cols in kvgen.NBA_SCHEMAS.items():
+        if kind == "edge":
+            c.register_edge(kvgen.NBA_EDGES[name], name, cols)
+        else:
+            c.register_tag(kvgen.NBA_TAGS[name], name, cols)
+    c.load_builder(kvgen.nba_kv(nba_data, 7))
+    try:
+        skipped = []
+        for case in golden.load("go_golden.json"):
+            if golden.unsupported_reason(case):
+                continue
+            try:
+                ok, msg = golden.run_go_case(c, case)
+            except NbgError as ex:
+                if ex.code == _lib.E_UNSUPPORTED:
+                    skipped.append((case["query"], str(ex)))
+                    continue
+                raise
+            assert ok, msg
+        assert all("$-" in m or "$var" in m for _, m in skipped), skipped
+    finally:
+        c.close()
