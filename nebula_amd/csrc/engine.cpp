@@ -182,12 +182,12 @@ struct nbg_go_stmt {
   std::string deferred_msg;
   std::string dst_unknown;           // a $$ tag name is unknown: fails once the final step has edges
   bool distinct = false;             // YIELD DISTINCT: distinct starts and rows
-  // $- / $var input: index rows (dense id of the FROM vid, ascending; last row per vid) and
-  // their columns, uploaded on first execution
+  // $- / $var input: index rows (the FROM vid, ascending; last row per vid) and their columns,
+  // uploaded on first execution (the same index on every rank of a partitioned engine)
   bool uses_input = false;
-  std::vector<uint32_t> in_ids;
+  std::vector<int64_t> in_ids;
   std::vector<std::vector<int64_t>> in_cols;
-  uint32_t* d_in_ids = nullptr;
+  int64_t* d_in_ids = nullptr;
   int64_t** d_in_cols = nullptr;
   std::vector<int64_t*> d_in_col_ptrs;
   ~nbg_go_stmt() {
@@ -286,10 +286,9 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
   for (auto& y : yields) uses_input = uses_input || has_input_prop(y.get());
   std::vector<std::string> in_names;
   std::vector<VKind> in_kinds;
-  std::vector<uint32_t> in_ids;
+  std::vector<int64_t> in_ids;
   std::vector<std::vector<int64_t>> in_cols;
   if (uses_input && rq->num_input_cols > 0) {
-    if (E.partitioned()) return E.fail(NBG_E_UNSUPPORTED, "$- / $var props on a partitioned engine");
     if (rq->num_input_cols > MAX_INPUT_COLS || !rq->input_names || !rq->input_kinds || !rq->input_cols ||
         rq->input_vid_col < 0 || rq->input_vid_col >= rq->num_input_cols)
       return E.fail(NBG_E_INVALID_ARGUMENT, "input table");
@@ -299,14 +298,11 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
       in_kinds.push_back((VKind)rq->input_kinds[c]);
     }
     const int64_t* vidc = static_cast<const int64_t*>(rq->input_cols[rq->input_vid_col]);
-    std::vector<std::pair<uint32_t, uint64_t>> rowof;   // (dense id, last row)
+    std::vector<std::pair<int64_t, uint64_t>> rowof;   // (vid, last row)
     {
       std::unordered_map<int64_t, uint64_t> last;
       for (uint64_t r = 0; r < n; ++r) last[vidc[r]] = r;   // vidToRowIndex_[v] = row: the last wins
-      for (auto& kv : last) {
-        const uint32_t d = E.dense(kv.first);
-        if (d != NO_ROW) rowof.emplace_back(d, kv.second);
-      }
+      for (auto& kv : last) rowof.emplace_back(kv.first, kv.second);
       std::sort(rowof.begin(), rowof.end());
     }
     in_cols.assign(rq->num_input_cols, std::vector<int64_t>(rowof.size()));
@@ -498,13 +494,14 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
   Workspace* ws = *wsp;
   p->ws = ws;
   rows->ws = ws;
-  uint32_t* bt = nullptr;   // VertexBackTracker roots, when $- / $var props are read after >= 2 steps
+  int64_t *bt = nullptr, *bt_in = nullptr;   // VertexBackTracker roots ($- / $var props after >= 2 steps)
+  ws_backtracker_off(ws);
   if (st->uses_input) {
     auto* ms = const_cast<nbg_go_stmt*>(st);
     if (!ms->d_in_ids) {
       const size_t n = std::max<size_t>(ms->in_ids.size(), 1);
-      bool ok = hipMalloc((void**)&ms->d_in_ids, n * 4) == hipSuccess &&
-                hipMemcpy(ms->d_in_ids, ms->in_ids.data(), ms->in_ids.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
+      bool ok = hipMalloc((void**)&ms->d_in_ids, n * 8) == hipSuccess &&
+                hipMemcpy(ms->d_in_ids, ms->in_ids.data(), ms->in_ids.size() * 8, hipMemcpyHostToDevice) == hipSuccess;
       ms->d_in_col_ptrs.assign(ms->in_cols.size(), nullptr);
       for (size_t c = 0; ok && c < ms->in_cols.size(); ++c)
         ok = hipMalloc((void**)&ms->d_in_col_ptrs[c], n * 8) == hipSuccess &&
@@ -515,7 +512,7 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
                hipSuccess;
       if (!ok) { delete rows; p->rows = nullptr; return E.fail(NBG_E_OUT_OF_MEMORY, "input index upload"); }
     }
-    if (steps > 1 && !(bt = ws_backtracker(ws))) {
+    if (steps > 1 && ws_backtracker(ws, &bt, &bt_in) != hipSuccess) {
       delete rows;
       p->rows = nullptr;
       return E.fail(NBG_E_OUT_OF_MEMORY, "backtracker");
@@ -541,6 +538,7 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
     a.tpres = E.snap.d_tpres;
     a.gbase = E.partitioned() ? (uint32_t)((uint64_t)E.cfg.rank * E.npad) : 0u;
     a.bt = bt;
+    a.bt_in = bt_in;
     if (st->uses_input) {
       a.in_ids = st->d_in_ids;
       a.in_n = st->in_ids.size();

@@ -85,6 +85,9 @@ struct Workspace {
   uint32_t seen_stamp = 0;        // last stamp handed out
   uint32_t step_stamp = 0;        // stamp of the current step (all its OVER types)
   // partitioned DISTINCT exchange scratch (row owners, counts, send / receive buffers)
+  int64_t* bt_out = nullptr;      // partitioned roots: written over the global id space,
+  int64_t* bt_recv = nullptr;     // received per rank segment (G * npad each)
+  bool bt_active = false;         // this query tracks roots: the hop exchange carries them
   uint32_t* xown = nullptr;
   uint64_t xown_cap = 0;
   unsigned long long* xcnt = nullptr;
@@ -127,7 +130,7 @@ struct Workspace {
   uint64_t dseg_cap = 0;
   uint32_t* dcnt = nullptr;
   uint8_t* dkinds = nullptr;
-  uint32_t* bt = nullptr;         // VertexBackTracker roots [nv] (queries with $- / $var props)
+  int64_t* bt = nullptr;         // VertexBackTracker roots [nv] (queries with $- / $var props)
   uint8_t* walk_arena = nullptr;  // FIND ALL PATH level arrays (grow-only)
   size_t walk_cap = 0;
   Ins* d_prog = nullptr;          // [MAX_TYPES_Q][MAX_PROGRAM]
@@ -417,7 +420,8 @@ __device__ __forceinline__ void run_program(const Ins* __restrict__ prog, int pc
       case OP_EIDX: r = (int64_t)c.j; break;
       case OP_INPUT:
         if (active) {
-          const uint32_t root = a.bt ? a.bt[c.v] : c.v;   // getPropFromInterim (GoExecutor.cpp:1066-1075)
+          // getPropFromInterim (GoExecutor.cpp:1066-1075): the row of the source's root
+          const int64_t root = a.bt_in ? a.bt_in[c.v] : a.vids[c.v];
           uint64_t lo = 0, hi = a.in_n;
           while (lo < hi) {
             const uint64_t mid = (lo + hi) >> 1;
@@ -832,7 +836,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
           u[i] = a.col[(uint64_t)sRs[s] + (b0 + k - (uint64_t)sEnd[s])];
           if (u[i] == NO_ROW) continue;
           const uint32_t src = list_id(a0 + s);
-          a.bt[u[i]] = a.bt_first ? src : a.bt[src];
+          a.bt[u[i]] = a.bt_first ? a.vids[src] : a.bt_in[src];
           if (!bp.lab) flags[u[i]] = 1;
         }
       }
@@ -1106,8 +1110,12 @@ __global__ void __launch_bounds__(BLOCK) k_pack_bits(uint8_t* __restrict__ flags
 // Owner side: OR the G received segments (one per sending rank) of this rank's id range; the
 // union is the global per-step dst SET restricted to the owner (getDstIdsFromResp).  Listed as
 // k_compact does: 16 vertices (bits) per thread.
+// bt_recv (nullable): the roots each rank wrote for this rank's vertices; a vertex reached from
+// several ranks takes the highest such rank's (the reference's last write is arbitrary as well)
 __global__ void __launch_bounds__(BLOCK) k_bits_compact(const unsigned long long* __restrict__ recv, int world,
-                                                        uint64_t seg_words, uint64_t nv, DegSrc ds, ListOut o) {
+                                                        uint64_t seg_words, uint64_t nv, DegSrc ds, ListOut o,
+                                                        const int64_t* __restrict__ bt_recv, int64_t* __restrict__ bt_in,
+                                                        uint64_t npad) {
   if (blockIdx.x == 0 && threadIdx.x == 0) *o.zero_next = 0;
   const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;   // 16-bit slice index
   const uint64_t word = i >> 2;
@@ -1129,6 +1137,16 @@ __global__ void __launch_bounds__(BLOCK) k_bits_compact(const unsigned long long
 #pragma unroll
   for (int b = 0; b < 16; ++b)
     if ((m >> b) & 1u) list_put(o, ds, pc++, (uint32_t)(lo + b), &pd, dg[b], rs[b]);
+  if (bt_recv && m) {
+    for (int b = 0; b < 16; ++b) {
+      if (!((m >> b) & 1u)) continue;
+      for (int q = world - 1; q >= 0; --q)
+        if ((recv[(uint64_t)q * seg_words + word] >> (sh + b)) & 1ull) {
+          bt_in[lo + b] = bt_recv[(uint64_t)q * npad + lo + b];
+          break;
+        }
+    }
+  }
 }
 
 // Stats of an expansion that is not launched (final step whose WHERE folded to false).
@@ -1517,7 +1535,7 @@ void ws_destroy(Workspace* w) {
                   (void*)w->q, (void*)w->rows,
                   (void*)w->d_row_cols, (void*)w->d_prog, (void*)w->dtab, (void*)w->dkeep, (void*)w->dseg,
                   (void*)w->dcnt, (void*)w->dkinds, (void*)w->bt, (void*)w->walk_arena, (void*)w->xown,
-                  (void*)w->xcnt, (void*)w->xsend, (void*)w->xrecv})
+                  (void*)w->xcnt, (void*)w->xsend, (void*)w->xrecv, (void*)w->bt_out, (void*)w->bt_recv})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)w->h_q, (void*)w->h_starts, (void*)w->h_prog, (void*)w->h_ps, (void*)w->h_path,
                   (void*)w->h_stage})
@@ -2108,10 +2126,20 @@ hipError_t ws_distinct_exchange(Workspace* w, const std::vector<std::array<uint6
   return hipSuccess;
 }
 
-uint32_t* ws_backtracker(Workspace* w) {
-  if (!w->bt && hipMalloc((void**)&w->bt, (w->nv + 1) * 4) != hipSuccess) w->bt = nullptr;
-  return w->bt;
+hipError_t ws_backtracker(Workspace* w, int64_t** out, int64_t** in) {
+  if (!w->bt) HIP_TRY(hipMalloc((void**)&w->bt, (w->nv + 1) * 8));
+  if (w->comm && !w->bt_out) {
+    const uint64_t G = (uint64_t)w->comm->world;
+    HIP_TRY(hipMalloc((void**)&w->bt_out, G * w->npad * 8));
+    HIP_TRY(hipMalloc((void**)&w->bt_recv, G * w->npad * 8));
+  }
+  w->bt_active = true;
+  *in = w->bt;
+  *out = w->comm ? w->bt_out : w->bt;
+  return hipSuccess;
 }
+
+void ws_backtracker_off(Workspace* w) { w->bt_active = false; }
 
 // Scan-only expansion (final step whose WHERE folded to false still counts E_N).
 hipError_t ws_scan_only(Workspace* w, const ExpandArgs& a, uint64_t n_bound, int step, int tix) {
@@ -2249,12 +2277,14 @@ hipError_t ws_exchange(Workspace* w, int step, const ExpandArgs* next0) {
   p = prof_begin(w, K_ALLTOALL);
   if (w->comm->alltoall(w->sendbits, w->recvbits, w->npad / 8, w->stream)) return hipErrorUnknown;
   prof_end(w, p, K_ALLTOALL, step, 0, (double)((G - 1) * w->npad / 8));
+  if (w->bt_active && w->comm->alltoall(w->bt_out, w->bt_recv, w->npad * 8, w->stream)) return hipErrorUnknown;
   unsigned long long* acc = &w->q->acc[2 + w->pc];
   unsigned long long* other = &w->q->acc[2 + (w->pc ^ 1)];
   w->pc ^= 1;
   p = prof_begin(w, K_BITS_COMPACT);
   hipLaunchKernelGGL(k_bits_compact, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->recvbits, (int)G, seg_words,
-                     w->nv, deg_src(next0), list_out(w, w->frontier[w->cur ^ 1], acc, other, nullptr, w->cur ^ 1));
+                     w->nv, deg_src(next0), list_out(w, w->frontier[w->cur ^ 1], acc, other, nullptr, w->cur ^ 1),
+                     w->bt_active ? (const int64_t*)w->bt_recv : nullptr, w->bt, w->npad);
   prof_end(w, p, K_BITS_COMPACT, step, 0);
   w->cur ^= 1;
   w->list_acc = acc;

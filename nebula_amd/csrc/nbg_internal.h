@@ -255,9 +255,13 @@ struct ExpandArgs {                // one (step, edge type) expansion
   const uint8_t* const* tpres;     // tag presence (Snapshot::d_tpres)
   uint32_t gbase;                  // id of local vertex 0 in the tag index space (rank * npad)
   // piped / variable input (GoExecutor::setupStarts index + VertexBackTracker, GoExecutor.h:169-188)
-  uint32_t* bt;                    // [nv] root (dense id) of every vertex reached (nullptr: not tracked)
+  // Roots travel as vids, so a root means the same on every rank.  MARKB writes bt[u] for each
+  // neighbour u (single engine: dense ids; partitioned: global ids, exchanged to u's owner with
+  // the hop) and reads bt_in[src] for a frontier vertex src (the owner's local view).
+  int64_t* bt;                     // (nullptr: not tracked)
+  const int64_t* bt_in;
   int bt_first;                    // MARK: this is step 1 (the root of a start is itself)
-  const uint32_t* in_ids;          // input index: dense ids of the rows' vids, ascending (last row wins)
+  const int64_t* in_ids;           // input index: the rows' vids, ascending (last row wins)
   uint64_t in_n;
   const int64_t* const* in_cols;   // [col][k] 8-byte payloads of the indexed rows
 };
@@ -441,7 +445,11 @@ void ws_set_mark_claims(Workspace* w, bool claims);   // per query, before its f
 hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a, uint64_t n_bound, uint64_t e_bound, int step, int tix,
                            const TypeProgram& prog, uint64_t region_base, uint64_t blk_cap, const InlineList* il = nullptr);
 hipError_t ws_scan_only(Workspace* w, const ExpandArgs& a, uint64_t n_bound, int step, int tix);
-uint32_t* ws_backtracker(Workspace* w);          // [nv] roots (allocated on first use)
+// roots (allocated on first use): *out written by MARKB, *in read (the same array on a single
+// engine; partitioned, out spans the global id space and in is the owner's local view, merged by
+// the hop exchange).  Enables the root exchange for the workspace's queries until reset.
+hipError_t ws_backtracker(Workspace* w, int64_t** out, int64_t** in);
+void ws_backtracker_off(Workspace* w);
 hipError_t ws_end_query(Workspace* w);
 hipError_t ws_end_query_async(Workspace* w);   // enqueue the end-of-query copy + event
 hipError_t ws_end_query_wait(Workspace* w);    // wait for it (then as ws_end_query)

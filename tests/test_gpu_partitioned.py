@@ -259,8 +259,8 @@ def test_partitioned_distinct_matches_single(rmat11, world, steps):
 
 
 def test_partitioned_nba_golden_needs_no_skips(nba_data):
-    """Every GO golden case the single engine runs also runs on 3 ranks (DISTINCT, $$ STRING):
-    only $- / $var props in YIELD / WHERE after several steps are still single-engine."""
+    """Every GO golden case the single engine runs also runs on 3 ranks (DISTINCT, $$ STRING,
+    $- / $var props): no NBG_E_UNSUPPORTED left on the partitioned path."""
     c = LocalCluster(7, 3)
     for (kind, name), cols in kvgen.NBA_SCHEMAS.items():
         if kind == "edge":
@@ -281,6 +281,33 @@ def test_partitioned_nba_golden_needs_no_skips(nba_data):
                     continue
                 raise
             assert ok, msg
-        assert all("$-" in m or "$var" in m for _, m in skipped), skipped
+        assert not skipped, skipped
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("steps", [1, 2, 3])
+def test_partitioned_input_props_backtracker(world, steps):
+    """$-.col in YIELD / WHERE after N steps on a partitioned engine: the roots travel with each
+    hop's exchange (as vids, to the neighbour's owner) — vs the oracle, on the forest whose roots
+    reach disjoint vertex sets (so the reference's last-write-wins back tracker is unambiguous)."""
+    from tests.test_gpu_go import _forest
+    roots, src, dst, w = _forest()
+    c = LocalCluster(7, world)
+    c.register_edge(graphs.E_TYPE, "e", graphs.E_SCHEMA)
+    c.load_edges(graphs.E_TYPE, src, dst, [w])
+    c.finalize()
+    orc = graphs.rmat_oracle(src, dst, w, parts=7)
+    try:
+        rows = [[r, 1000 + i, 0.5 * i] for i, r in enumerate(roots)] + [[roots[0], 7, 9.25]]
+        inputs = (["id", "tag", "score"], rows, "id")
+        yields = [E.input_prop("tag").encode(), E.input_prop("score").encode(), E.edge_prop("e", "_dst").encode()]
+        where = E.binop(">", E.input_prop("tag"), E.const(1001)).encode()
+        for wb in (b"", where):
+            got = c.go(roots, [1], steps, wb, yields, inputs=inputs)
+            exp = orc.go(roots, [1], steps, wb, yields, inputs=inputs)
+            assert graphs.sorted_rows(got) == graphs.sorted_rows(exp) and got
+    finally:
+        c.close()
+        orc.close()
