@@ -100,6 +100,21 @@ int32_t nbg_load_part_kv(nbg_engine* e, int32_t part,
                          const uint8_t* key_data, const uint64_t* key_offs,
                          const uint8_t* val_data, const uint64_t* val_offs, uint64_t n);
 
+/* SST-file ingest: RocksDB BlockBasedTable files as rocksdb::SstFileWriter writes them for the
+ * Spark generator (src/tools/spark-sstfile-generator/.../SstFileOutputFormat.scala:150-202),
+ * replacing StorageHttpIngestHandler -> NebulaStore::ingest -> RocksEngine::ingest
+ * (src/storage/StorageHttpIngestHandler.cpp:94-100, src/kvstore/NebulaStore.cpp:436-466,
+ * src/kvstore/RocksEngine.cpp:360-370).  Every Put record is loaded as by nbg_load_part_kv (a key
+ * already loaded is overwritten: the ingested file is newer).  Before nbg_finalize.
+ *   nbg_ingest_sst: one file into `part`;
+ *   nbg_ingest_dir: every "*.sst" under <download_dir>/<part>/ (recursively, in name order) for
+ *                   every part this engine serves; a missing part directory is skipped.
+ * Block compression none / Snappy; NBG_E_UNSUPPORTED for other codecs, record types other than
+ * Put and format_version > 3; NBG_E_INVALID_ARGUMENT for unreadable or corrupt files (checksums
+ * are verified). */
+int32_t nbg_ingest_sst(nbg_engine* e, int32_t part, const char* path);
+int32_t nbg_ingest_dir(nbg_engine* e, const char* download_dir);
+
 /* Bulk loader (SST-ingest analogue): n edges of one positive edge type, inserted the way
  * InsertEdgeExecutor does (out-edge with props + in-edge (dst,-type,rank,src) with no props,
  * src/graph/InsertEdgeExecutor.cpp:180-196), all with one version; a later duplicate

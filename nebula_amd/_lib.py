@@ -81,6 +81,8 @@ SIGNATURES = [
     ("nbg_register_edge", i32, [vp, i32, C.c_char_p, i64, P(nbg_column_def), i32]),
     ("nbg_load_part_kv", i32, [vp, i32, vp, vp, vp, vp, u64]),
     ("nbg_load_edges", i32, [vp, i32, vp, vp, vp, u64, P(vp), i32]),
+    ("nbg_ingest_sst", i32, [vp, i32, C.c_char_p]),
+    ("nbg_ingest_dir", i32, [vp, C.c_char_p]),
     ("nbg_finalize", i32, [vp]),
     ("nbg_snapshot_save", i32, [vp, C.c_char_p]),
     ("nbg_snapshot_load", i32, [vp, C.c_char_p]),

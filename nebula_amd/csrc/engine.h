@@ -62,6 +62,9 @@ struct Engine {
   bool decode_row(const SchemaSet& ss, const uint8_t* v, size_t n, int64_t* out);
   int32_t load_part_kv(int32_t part, const uint8_t* kd, const uint64_t* ko, const uint8_t* vd, const uint64_t* vo,
                        uint64_t n);
+  // SST-file ingest (sst.cpp): one file into one part / NebulaStore::ingest over download/<part>
+  int32_t ingest_sst(int32_t part, const std::string& path);
+  int32_t ingest_dir(const std::string& download);
   int32_t load_edges(int32_t type, const int64_t* src, const int64_t* dst, const int64_t* rank, uint64_t n,
                      const void* const* cols, int32_t ncols);
   int32_t finalize();

@@ -512,6 +512,12 @@ hipError_t ws_all_paths(Workspace* w, const PathTypes& fwd, int lab, uint32_t ep
                         uint32_t upto, const int64_t* d_vids, const uint8_t* visible, uint64_t max_walks,
                         std::vector<std::vector<int64_t>>* out, uint64_t* scanned);
 // partitioned engine (collective: every rank calls these in the same order)
+// FIND ALL PATH: the walks of a level are extended by the owner of their last vertex and the level
+// is all-gathered (every rank holds every level); Sgid / Svid: every source (global id, vid), the
+// same on every rank.  Every rank appends the same entry lists.
+hipError_t ws_all_paths_part(Workspace* w, const PathTypes& fwd, int lab, uint32_t epoch, const uint32_t* Sgid,
+                             const int64_t* Svid, uint64_t nS, uint32_t upto, uint64_t nv, const uint8_t* visible,
+                             uint64_t max_walks, std::vector<std::vector<int64_t>>* out, uint64_t* scanned);
 hipError_t ws_path_level_part(Workspace* w, const PathTypes& pt, int src, uint64_t n_bound, uint64_t e_bound, int dst,
                               const PathLevel& lv);
 hipError_t ws_path_sync_part(Workspace* w, PState* out);                 // sizes summed over ranks

@@ -368,9 +368,11 @@ int32_t one_sided(PathCtx& c, const std::vector<uint32_t>& S, const std::vector<
 }
 
 // FIND ALL PATH: backward BFS distances from the targets over in-edges (LAB_B, levels
-// 0..upto-1), then the pruned forward walk enumeration (ws_all_paths).
+// 0..upto-1), then the pruned forward walk enumeration (ws_all_paths; partitioned:
+// ws_all_paths_part, walks extended at their last vertex's owner, levels all-gathered).
+// Partitioned: Sgid / Svid are every source (global id, vid), the same on every rank.
 int32_t all_paths(PathCtx& c, const std::vector<uint32_t>& S, const std::vector<uint32_t>& T, uint32_t upto,
-                  nbg_paths* out) {
+                  const std::vector<uint32_t>& Sgid, const std::vector<int64_t>& Svid, nbg_paths* out) {
   Workspace* ws = c.ws;
   const uint32_t eb = ws_path_epoch(ws, LAB_B);
   hipError_t he = hipSuccess;
@@ -382,7 +384,8 @@ int32_t all_paths(PathCtx& c, const std::vector<uint32_t>& S, const std::vector<
   Tr(sync(c, &ps));
   if (he != hipSuccess) return dev_fail(c.E, he, "path setup");
   int cur = S_B0;
-  uint64_t n = T.size(), ds = ps.dsum[1];
+  // partitioned: the targets over all ranks (every rank must run the same levels)
+  uint64_t n = c.part ? ps.n[S_B0] : T.size(), ds = ps.dsum[1];
   for (uint32_t l = 1; l < upto && n; ++l) {
     PathLevel lv;
     lv.lab = LAB_B;
@@ -398,8 +401,12 @@ int32_t all_paths(PathCtx& c, const std::vector<uint32_t>& S, const std::vector<
   uint64_t scanned = 0;
   static const uint64_t max_walks = getenv("NBG_MAX_WALKS") ? strtoull(getenv("NBG_MAX_WALKS"), nullptr, 10)
                                                             : (1ull << 28);
-  he = ws_all_paths(ws, c.fwd, LAB_B, eb, S.data(), S.size(), upto, c.E.snap.d_vids, c.E.snap.d_visible, max_walks,
-                    &out->paths, &scanned);
+  if (c.part)
+    he = ws_all_paths_part(ws, c.fwd, LAB_B, eb, Sgid.data(), Svid.data(), Sgid.size(), upto, c.E.snap.nv,
+                           c.E.snap.d_visible, max_walks, &out->paths, &scanned);
+  else
+    he = ws_all_paths(ws, c.fwd, LAB_B, eb, S.data(), S.size(), upto, c.E.snap.d_vids, c.E.snap.d_visible, max_walks,
+                      &out->paths, &scanned);
   if (he == hipErrorOutOfMemory) return c.E.fail(NBG_E_OUT_OF_MEMORY, "FIND ALL PATH: too many paths");
   if (he != hipSuccess) return dev_fail(c.E, he, "path enumeration");
   c.edges += scanned;
@@ -420,8 +427,6 @@ constexpr int32_t PAIR_DEFERRED = 1;
 int32_t find_path_locked(Engine& E, const nbg_path_request* rq, nbg_paths** out, PairLaunch* pl) {
   if (!E.finalized) return E.fail(NBG_E_STATE, "engine not finalized");
   if (hipSetDevice(E.cfg.device) != hipSuccess) return E.fail(NBG_E_DEVICE, "hipSetDevice failed");
-  if (!rq->shortest && E.partitioned())
-    return E.fail(NBG_E_UNSUPPORTED, "FIND ALL PATH on a partitioned engine is not supported yet");
   if (!rq->shortest && rq->upto > 32) return E.fail(NBG_E_UNSUPPORTED, "FIND ALL PATH UPTO exceeds 32");
   if (rq->upto > MAX_PATH_LEN) return E.fail(NBG_E_UNSUPPORTED, "UPTO exceeds the device path limit (63)");
   if (E.cfg.max_edge_returned_per_vertex > 0 && E.cfg.max_edge_returned_per_vertex != INT_MAX)
@@ -540,7 +545,22 @@ int32_t find_path_locked(Engine& E, const nbg_path_request* rq, nbg_paths** out,
     std::vector<uint32_t> Tl;
     for (uint32_t d : Tg)
       if (d != NO_ROW) Tl.push_back(d);
-    rc = all_paths(c, S, Tl, rq->upto, res);
+    // partitioned: every source's global id (owner * npad + its local id), summed over ranks
+    std::vector<uint32_t> Sgid;
+    std::vector<int64_t> Svid;
+    if (c.part) {
+      std::vector<unsigned long long> g(fv.size(), 0);
+      for (size_t i = 0; i < fv.size(); ++i)
+        if (pres[i] && fd[i] != NO_ROW) g[i] = (unsigned long long)E.cfg.rank * E.npad + fd[i] + 1;
+      he = ws_allreduce_host(E.ws, g);
+      if (he != hipSuccess) { delete res; return dev_fail(E, he, "path source exchange"); }
+      for (size_t i = 0; i < fv.size(); ++i)
+        if (g[i]) {
+          Sgid.push_back((uint32_t)(g[i] - 1));
+          Svid.push_back(fv[i]);
+        }
+    }
+    rc = all_paths(c, S, Tl, rq->upto, Sgid, Svid, res);
   } else if (pair)
     rc = bidirectional(c, S.empty() ? NO_ROW : S[0], Tg[0], rq->upto, res);
   else

@@ -11,6 +11,7 @@ The engine also implements the backend interface of ``nebula_amd.ngql.Session`` 
 from __future__ import annotations
 
 import ctypes as C
+import os
 import weakref
 import struct
 from typing import List, Optional, Sequence
@@ -196,6 +197,14 @@ class Engine:
     def load_part(self, part, kd, ko, vd, vo, n):
         self._check(self.lib.nbg_load_part_kv(self.h, part, _ptr(kd), _ptr(ko), _ptr(vd), _ptr(vo), n),
                     "load_part_kv")
+
+    def ingest_sst(self, part: int, path: str):
+        """One RocksDB SST file into one part (RocksEngine::ingest)."""
+        self._check(self.lib.nbg_ingest_sst(self.h, part, os.fsencode(path)), "ingest_sst")
+
+    def ingest_dir(self, download_dir: str):
+        """NebulaStore::ingest: every *.sst under <download_dir>/<part>/ of the parts served here."""
+        self._check(self.lib.nbg_ingest_dir(self.h, os.fsencode(download_dir)), "ingest_dir")
 
     def load_builder(self, kb, finalize=True):
         for p in sorted(kb.recs):
@@ -565,6 +574,11 @@ class LocalCluster:
         for e in self.engines:
             e.load_builder(kb, finalize=False)
         self.finalize()
+
+    def ingest_dir(self, download_dir: str):
+        """Every rank ingests the parts it serves (part % world == rank); finalize() afterwards."""
+        for e in self.engines:
+            e.ingest_dir(download_dir)
 
     def finalize(self):
         self.each(lambda e: e.finalize())

@@ -107,6 +107,16 @@ def tagged_register(be, is_engine):
             be.register_tag(ident, name, cols)
 
 
+def tagged_pair_cluster(scale, world, parts=7, seed=5):
+    """The tagged_pair records on a partitioned in-process cluster of `world` ranks."""
+    from nebula_amd import LocalCluster
+    _, _, kb = tagged_kv(scale, parts, seed)
+    c = LocalCluster(parts, world)
+    tagged_register(c, True)
+    c.load_builder(kb)
+    return c
+
+
 def tagged_pair(scale, parts=7, seed=5, max_edge=0x7FFFFFFF):
     """(src, persons, engine, oracle) over the same tagged KV records."""
     from nebula_amd import Engine
