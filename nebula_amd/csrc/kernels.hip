@@ -343,12 +343,25 @@ __device__ __forceinline__ int64_t load_col(const void* p, int bytes, uint32_t j
   }
 }
 
+// Final-step streams that are read or written once per query (the WHERE column, _dst, the rows):
+// non-temporal when built with NBG_NT_LD / NBG_NT_ST (an A/B switch of the build).
+#ifdef NBG_NT_LD
+#define NBG_LD_STREAM(p) __builtin_nontemporal_load(p)
+#else
+#define NBG_LD_STREAM(p) (*(p))
+#endif
+#ifdef NBG_NT_ST
+#define NBG_ST_STREAM(v, p) __builtin_nontemporal_store((v), (p))
+#else
+#define NBG_ST_STREAM(v, p) (*(p) = (v))
+#endif
+
 // VT loads of a column of type T (sign-extended), all in flight at once
 template <typename T>
 __device__ __forceinline__ void load_narrow(const void* p, const uint32_t* jj, int nb, int lane, int64_t* x) {
   const T* c = reinterpret_cast<const T*>(p);
 #pragma unroll
-  for (int i = 0; i < VT; ++i) x[i] = (i * 64 + lane < nb) ? (int64_t)c[jj[i]] : 0;
+  for (int i = 0; i < VT; ++i) x[i] = (i * 64 + lane < nb) ? (int64_t)NBG_LD_STREAM(c + jj[i]) : 0;
 }
 
 struct FastProg {
@@ -735,7 +748,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
       const uint64_t row = region + off + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
       off += (uint32_t)__popcll(bal);
       if (pass)
-        for (int y = 0; y < fp.nyields; ++y) ycols[y][row] = fp.fast.ykind[y] == 0 ? vdv[i] : fp.yield_const[y];
+        for (int y = 0; y < fp.nyields; ++y) NBG_ST_STREAM(fp.fast.ykind[y] == 0 ? vdv[i] : fp.yield_const[y], ycols[y] + row);
     }
   };
   if (kFinal) {
@@ -946,7 +959,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
 #pragma unroll
         for (int i = 0; i < VT; ++i) {
           const bool act = i * 64 + lane < nb;
-          dv[i] = (act && fp.fast.dst_yield) ? a.dst_vid[jj[i]] : 0;
+          dv[i] = (act && fp.fast.dst_yield) ? NBG_LD_STREAM(a.dst_vid + jj[i]) : 0;
         }
         // the WHERE column at its stored width (narrow copy of an INT column when it fits)
         switch (fp.fast.has_where ? fp.fast.wbytes : 0) {
