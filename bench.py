@@ -349,6 +349,7 @@ def main():
     ap.add_argument("--c2", type=int, default=1, help="C2 leg (RMAT-22, 64 roots) when the headline is larger")
     ap.add_argument("--c5-scale", type=int, default=20,
                     help="C5 substitute (knows RMAT + likes bipartite): knows scale, 0 = skip")
+    ap.add_argument("--c1-reqs", type=int, default=200, help="C1 nba GO 2 STEPS latency queries (0 = skip)")
     ap.add_argument("--getbound-reqs", type=int, default=200,
                     help="QueryBoundBenchmark-shaped GetNeighbors requests (0 = skip)")
     args = ap.parse_args()
@@ -485,6 +486,7 @@ def main():
         c2 = c2_leg(args, barrier, inflight)
     c5 = c5_leg(args, barrier) if world == 1 and args.c5_scale > 0 else None
     getbound = getbound_leg(args) if world == 1 and args.getbound_reqs > 0 else None
+    c1 = c1_leg(args) if world == 1 and args.c1_reqs > 0 else None
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
@@ -531,6 +533,7 @@ def main():
         "c2_rmat22": c2,
         "c5_substitute": c5,
         "getbound": getbound,
+        "c1_nba": c1,
         "gen_seconds": round(gen_s, 2),
         "load_seconds": round(load_s, 2),
     }
@@ -648,6 +651,50 @@ def faithful_baseline(args, where, threads, model, ncpu):
             "model": model, "host_cpus": ncpu,
             "shortest": {"p50_ms": float(np.percentile(np.array(lat) * 1e3, 50)), "pairs": len(lat), "cores": 1,
                          "sample": "RMAT-22 pairs (seed 7); canonical BFS over the storaged-faithful KV store"}}
+
+
+def c1_leg(args):
+    """SURVEY §8(d) C1 (BASELINE configs[0]): the TraverseTestBase player/team space, one part,
+    GO 2 STEPS FROM "Tim Duncan" OVER like (this reference's `follow`), latency only: the device
+    (prepared statement, rows fetched to the host) and the oracle's storaged + graphd restatement on
+    the same KV records; rows checked equal."""
+    from nebula_amd import kvgen
+    from nebula_amd.engine import nba_engine
+    from nebula_amd.vidhash import std_hash
+    from tests.support import graphs
+    from tests.support.oracle import nba_oracle
+    data = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden", "nba.json")))
+    eng = nba_engine(data, 1)
+    like = kvgen.NBA_EDGES["like"]
+    tim = std_hash("Tim Duncan")
+    stmt = eng.prepare_go([like], 2)
+    rows = None
+    for _ in range(10):
+        rows = stmt.run([tim])
+    lat = []
+    for _ in range(args.c1_reqs):
+        q0 = time.perf_counter()
+        stmt.run([tim])
+        lat.append(time.perf_counter() - q0)
+    stmt.free()
+    eng.close()
+    out = {"query": "GO 2 STEPS FROM \"Tim Duncan\" OVER like", "rows": len(rows), "queries": args.c1_reqs,
+           "p50_ms": float(np.percentile(np.array(lat) * 1e3, 50)),
+           "timing": "prepared statement executed on the device, rows fetched to the host (nbg_go_execute + nbg_rows_fetch)"}
+    try:
+        orc = nba_oracle(data, 1)
+        olat, orows = [], None
+        for _ in range(args.c1_reqs):
+            q0 = time.perf_counter()
+            orows = orc.go([tim], [like], 2)
+            olat.append(time.perf_counter() - q0)
+        orc.close()
+        out["parity_vs_oracle"] = graphs.sorted_rows(orows) == graphs.sorted_rows(rows)
+        out["cpu_baseline"] = {"p50_ms": float(np.percentile(np.array(olat) * 1e3, 50)), "cores": 1, "kind": "port",
+                               "sample": f"{args.c1_reqs} queries, storaged-faithful oracle (RowSet encode/decode per hop)"}
+    except Exception as ex:   # the oracle library is test infrastructure: the leg reports without it
+        log(f"c1 cpu baseline unavailable: {ex}")
+    return out
 
 
 def getbound_leg(args):
