@@ -232,7 +232,7 @@ def host_delivered(stmt, roots):
             "timing": "nbg_go_execute (device) + nbg_rows_fetch of every row, one query at a time"}
 
 
-def shortest_path_leg(eng, pairs, args, barrier):
+def shortest_path_leg(eng, pairs, args, barrier, batch=True):
     """FIND SHORTEST PATH FROM s TO t OVER e UPTO n STEPS, one query per pair (C4)."""
     for s, t in pairs[:16]:   # warm-up
         eng.find_path([s], [t], [1], args.sp_upto)
@@ -278,6 +278,29 @@ def shortest_path_leg(eng, pairs, args, barrier):
         c_el = time.perf_counter() - c0
         conc = {"queries_in_flight": inflight, "pairs_per_s": len(pairs) / c_el if c_el else None,
                 "teps": c_edges / c_el if c_el else None, "seconds": round(c_el, 3), "found": c_found}
+    # batched pass: nbg_find_path_batch, one-pair queries NBG_SP_BATCH at a time per device chain
+    batched = None
+    if batch and not args.sync:
+        chunk = 2000
+        preps = [eng.path_batch_prepare([([s], [t], [1], args.sp_upto, True) for s, t in pairs[k:k + chunk]])
+                 for k in range(0, len(pairs), chunk)]   # the requests: input, built before the clock
+        barrier()
+        b0 = time.perf_counter()
+        results = [eng.path_batch_run(p) for p in preps]
+        barrier()
+        b_el = time.perf_counter() - b0
+        b_edges, b_found = 0, 0
+        for (outs, rcs), p in zip(results, preps):
+            for i in range(p[1]):
+                if rcs[i]:
+                    raise RuntimeError(f"find_path_batch request failed: {rcs[i]}")
+                b_edges += int(eng.lib.nbg_paths_edges_scanned(outs[i]))
+                b_found += eng.lib.nbg_paths_count(outs[i]) > 0
+                eng.lib.nbg_paths_free(outs[i])
+        batched = {"batch": int(os.environ.get("NBG_SP_BATCH", "32")), "pairs_per_s": len(pairs) / b_el if b_el else None,
+                   "teps": b_edges / b_el if b_el else None, "seconds": round(b_el, 3), "found": b_found,
+                   "timing": f"nbg_find_path_batch over the same pairs, {chunk} requests per call (request "
+                             f"arrays built before the clock; results left in their nbg_paths)"}
     kst, prof_pairs = {}, 0
     if not args.no_profile:   # roofline pass: HIP events around k_expand<BFS> over the first pairs
         eng.profile(2)
@@ -295,7 +318,7 @@ def shortest_path_leg(eng, pairs, args, barrier):
            "p50_ms": float(np.percentile(lat_ms, 50)), "p90_ms": float(np.percentile(lat_ms, 90)),
            "p99_ms": float(np.percentile(lat_ms, 99)), "mean_ms": float(lat_ms.mean()),
            "teps": edges / elapsed if elapsed else None, "edges": edges, "seconds": round(elapsed, 3),
-           "timing": "latency pass: one query at a time, uninstrumented", "concurrent": conc}
+           "timing": "latency pass: one query at a time, uninstrumented", "concurrent": conc, "batched": batched}
     ks = {k: v for k, v in kst.items() if v["launches"]} if kst else {}
     if ks:
         out["kernels"] = {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
@@ -417,7 +440,7 @@ def main():
         dig.append(list(res.digest()) + [res.edges_scanned])
         res.free()
     stmt.free()
-    sp = shortest_path_leg(eng, pairs, args, barrier) if pairs else None
+    sp = shortest_path_leg(eng, pairs, args, barrier, batch=world == 1) if pairs else None
     sp_sample = []
     if pairs and args.verify:   # device paths for the verification sample
         sp_sample = [eng.find_path([s], [t], [1], args.sp_upto) for s, t in pairs[:64]]

@@ -270,6 +270,17 @@ int32_t nbg_find_path(nbg_engine* e, const nbg_path_request* req, nbg_paths** ou
 typedef struct nbg_path_ticket nbg_path_ticket;
 int32_t nbg_find_path_submit(nbg_engine* e, const nbg_path_request* req, nbg_path_ticket** out);
 int32_t nbg_find_path_wait(nbg_path_ticket* ticket, nbg_paths** out);
+
+/* n independent FIND PATH requests at once (a graphd serving many FindPathExecutor queries,
+ * src/graph/FindPathExecutor.cpp:145-411, each with its own result): out[i] / rcs[i] receive
+ * request i's paths (free each with nbg_paths_free; NULL when rcs[i] != NBG_OK) and status.
+ * One-pair SHORTEST requests on a single engine run NBG_SP_BATCH (default 32, at most 32) at a
+ * time as one batched device level loop (every launch serves the whole batch; each of the batch's
+ * workspaces holds 3 label arrays and 5 list buffers of nv entries); other requests run as
+ * nbg_find_path would.  Results equal nbg_find_path's.  Returns NBG_OK unless the batch itself
+ * could not run (arguments, device set-up). */
+int32_t nbg_find_path_batch(nbg_engine* e, const nbg_path_request* reqs, uint64_t n, nbg_paths** out,
+                            int32_t* rcs);
 int64_t nbg_paths_count(const nbg_paths* p);
 int64_t nbg_path_len(const nbg_paths* p, int64_t i);
 const int64_t* nbg_path_entries(const nbg_paths* p, int64_t i);

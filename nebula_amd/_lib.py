@@ -111,6 +111,7 @@ SIGNATURES = [
     ("nbg_find_path", i32, [vp, P(nbg_path_request), P(vp)]),
     ("nbg_find_path_submit", i32, [vp, P(nbg_path_request), P(vp)]),
     ("nbg_find_path_wait", i32, [vp, P(vp)]),
+    ("nbg_find_path_batch", i32, [vp, P(nbg_path_request), u64, P(vp), P(i32)]),
     ("nbg_paths_count", i64, [vp]),
     ("nbg_path_len", i64, [vp, i64]),
     ("nbg_path_entries", P(i64), [vp, i64]),

@@ -43,6 +43,10 @@ struct Engine {
   };
   std::vector<PathSlot> path_slots;
   std::vector<void*> path_inflight;
+  // nbg_find_path_batch: one-pair SHORTEST queries run NBG_SP_BATCH at a time as one batched
+  // launch chain, on workspaces sharing one stream
+  std::vector<SpCtx*> batch_sp;
+  hipStream_t batch_stream = nullptr;
   uint64_t sp_item_cap() const;         // items a shortest-path list may hold
   uint64_t sp_edge_cap() const;         // edges of the larger direction (a level's edge space)
   std::vector<void*> inflight;          // submitted tickets, oldest first

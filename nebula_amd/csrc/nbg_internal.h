@@ -333,6 +333,14 @@ void sp_destroy(SpCtx* c);
 hipError_t sp_launch(SpCtx* c, int mode, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible,
                      const int64_t* vids, uint32_t s, uint32_t t, uint32_t upto);
 bool sp_ready(SpCtx* c);
+struct SpPair {                 // one query of sp_launch_batch
+  const SpTypes* fwd;
+  const SpTypes* bwd;
+  const uint8_t* visible;
+  const int64_t* vids;
+  uint32_t s, t, upto;
+};
+hipError_t sp_launch_batch(SpCtx* const* cs, int n, const SpPair* pairs);
 struct ChainCtx;
 ChainCtx* chain_create(uint64_t nv, uint64_t edge_cap, hipStream_t s, std::string* err);
 void chain_destroy(ChainCtx* c);
@@ -340,6 +348,16 @@ hipError_t chain_launch(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, con
                         const int64_t* vids, uint32_t* const lab[3], uint32_t epoch, uint32_t s, uint32_t t,
                         uint32_t upto);
 bool chain_more(ChainCtx* c, hipError_t* he);   // false: a continuation batch was enqueued
+// one query of a batched chain (spchain.hip, chain_launch_batch)
+struct ChainQuery {
+  const SpTypes* fwd;
+  const SpTypes* bwd;
+  const uint8_t* visible;
+  const int64_t* vids;
+  uint32_t* const* lab;   // [3]
+  uint32_t epoch, s, t, upto;
+};
+hipError_t chain_launch_batch(ChainCtx* const* cs, int n, const ChainQuery* qs);
 void chain_result(const ChainCtx* c, SpResult* out);
 hipError_t sp_wait(SpCtx* c, SpResult* out);
 

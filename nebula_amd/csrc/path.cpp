@@ -621,6 +621,24 @@ void path_complete_oldest(Engine& E) {
 
 }  // namespace
 
+namespace {
+nbg_paths* paths_of(const SpResult& r) {
+  auto* res = new nbg_paths();
+  res->edges = r.edges;
+  if (r.L) res->paths.emplace_back(r.path, r.path + 1 + 3 * r.L);
+  return res;
+}
+
+int sp_batch_size() {
+  static const int n = [] {
+    const char* v = getenv("NBG_SP_BATCH");
+    const int k = v ? atoi(v) : 32;   // RMAT-22: 16 -> 35.6 k, 32 -> 44.8 k pairs/s
+    return k < 1 ? 1 : (k > 32 ? 32 : k);
+  }();
+  return n;
+}
+}  // namespace
+
 void nbg::path_slots_release(Engine& E) {
   while (!E.path_inflight.empty()) {
     auto* t = static_cast<nbg_path_ticket*>(E.path_inflight.front());
@@ -633,6 +651,10 @@ void nbg::path_slots_release(Engine& E) {
     if (ps.stream) (void)hipStreamDestroy(ps.stream);
   }
   E.path_slots.clear();
+  for (SpCtx* c : E.batch_sp) sp_destroy(c);
+  E.batch_sp.clear();
+  if (E.batch_stream) (void)hipStreamDestroy(E.batch_stream);
+  E.batch_stream = nullptr;
 }
 
 extern "C" {
@@ -686,6 +708,95 @@ int32_t nbg_find_path_submit(nbg_engine* h, const nbg_path_request* rq, nbg_path
   ps.ticket = t;
   E.path_inflight.push_back(t);
   *out = t;
+  return NBG_OK;
+}
+
+int32_t nbg_find_path_batch(nbg_engine* h, const nbg_path_request* reqs, uint64_t n, nbg_paths** out, int32_t* rcs) {
+  if (!h || (n && (!reqs || !out || !rcs))) return NBG_E_INVALID_ARGUMENT;
+  Engine& E = h->e;
+  std::lock_guard<std::mutex> lg(E.mu);
+  for (uint64_t i = 0; i < n; ++i) {
+    out[i] = nullptr;
+    rcs[i] = NBG_OK;
+  }
+  // every request is classified as nbg_find_path_submit would; the one-pair SHORTEST ones of the
+  // device level loop are deferred and run as batched chains, the rest run here
+  std::vector<PairLaunch> pl;
+  std::vector<uint64_t> at;
+  for (uint64_t i = 0; i < n; ++i) {
+    PairLaunch x;
+    nbg_paths* res = nullptr;
+    const int32_t rc = find_path_locked(E, &reqs[i], &res, E.partitioned() ? nullptr : &x);
+    if (rc == PAIR_DEFERRED && x.mode == SP_CHAIN) {
+      pl.push_back(x);
+      at.push_back(i);
+      continue;
+    }
+    if (rc == PAIR_DEFERRED) {   // another device mode: one pair at a time on the engine's workspace
+      res = new nbg_paths();
+      if (!E.sp) {
+        std::string err;
+        E.sp = sp_create(E.snap.nv, E.sp_item_cap(), E.sp_edge_cap(), E.stream, &err);
+        if (!E.sp) {
+          delete res;
+          rcs[i] = E.fail(NBG_E_OUT_OF_MEMORY, err);
+          continue;
+        }
+      }
+      SpResult r;
+      hipError_t he = sp_launch(E.sp, x.mode, x.fwd, x.bwd, E.snap.d_visible, E.snap.d_vids, x.s, x.t, x.upto);
+      if (he == hipSuccess) he = sp_wait(E.sp, &r);
+      delete res;
+      if (he != hipSuccess) {
+        rcs[i] = dev_fail(E, he, "shortest path");
+        continue;
+      }
+      if (r.err) {
+        rcs[i] = E.fail(r.err == 1 ? NBG_E_UNKNOWN : NBG_E_DEVICE, "shortest path: device search failed");
+        continue;
+      }
+      out[i] = paths_of(r);
+      continue;
+    }
+    rcs[i] = rc;
+    out[i] = res;
+  }
+  if (pl.empty()) return NBG_OK;
+  const int B = sp_batch_size();
+  if (!E.batch_stream && hipStreamCreateWithFlags(&E.batch_stream, hipStreamNonBlocking) != hipSuccess)
+    return E.fail(NBG_E_DEVICE, "hipStreamCreate failed");
+  while ((int)E.batch_sp.size() < std::min<int>(B, (int)pl.size())) {
+    std::string err;
+    SpCtx* c = sp_create(E.snap.nv, E.sp_item_cap(), E.sp_edge_cap(), E.batch_stream, &err);
+    if (!c) return E.fail(NBG_E_OUT_OF_MEMORY, err);
+    E.batch_sp.push_back(c);
+  }
+  for (size_t b0 = 0; b0 < pl.size(); b0 += (size_t)B) {
+    const int nb = (int)std::min<size_t>((size_t)B, pl.size() - b0);
+    std::vector<SpPair> sp(nb);
+    for (int p = 0; p < nb; ++p) {
+      const PairLaunch& x = pl[b0 + p];
+      sp[p] = SpPair{&x.fwd, &x.bwd, E.snap.d_visible, E.snap.d_vids, x.s, x.t, x.upto};
+    }
+    hipError_t he = sp_launch_batch(E.batch_sp.data(), nb, sp.data());
+    for (int p = 0; p < nb; ++p) {
+      const uint64_t i = at[b0 + p];
+      SpResult r;
+      if (he == hipSuccess) he = sp_wait(E.batch_sp[p], &r);
+      if (he != hipSuccess) {
+        rcs[i] = dev_fail(E, he, "shortest path");
+        continue;
+      }
+      if (r.err == 1) {
+        rcs[i] = E.fail(NBG_E_UNKNOWN, "shortest-path reconstruction failed (in/out edges disagree)");
+      } else if (r.err) {
+        rcs[i] = E.fail(NBG_E_DEVICE, "shortest path: device search aborted (code " + std::to_string(r.err) + ")");
+      } else {
+        out[i] = paths_of(r);
+      }
+    }
+    if (he != hipSuccess) return dev_fail(E, he, "shortest path batch");
+  }
   return NBG_OK;
 }
 

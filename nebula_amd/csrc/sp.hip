@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "nbg_internal.h"
 
@@ -967,6 +968,34 @@ hipError_t sp_launch(SpCtx* c, int mode, const SpTypes& fwd, const SpTypes& bwd,
   HIP_TRY_SP(hipGetLastError());
   HIP_TRY_SP(hipMemcpyAsync(c->h_res, c->d_res, sizeof(SpResult), hipMemcpyDeviceToHost, c->stream));
   return hipEventRecord(c->done, c->stream);
+}
+
+// n one-pair queries on n slots that share one stream, as one batched chain (spchain.hip); each
+// slot's sp_wait then completes its own query.
+hipError_t sp_launch_batch(SpCtx* const* cs, int n, const SpPair* pairs) {
+  if (n < 1) return hipSuccess;
+  std::vector<ChainCtx*> chains(n);
+  std::vector<ChainQuery> qs(n);
+  for (int p = 0; p < n; ++p) {
+    SpCtx* c = cs[p];
+    const SpPair& x = pairs[p];
+    if (x.upto > MAX_PATH_LEN || x.s == NO_ROW || x.t == NO_ROW || c->stream != cs[0]->stream) return hipErrorInvalidValue;
+    if (++c->epoch >= (1u << (32 - LVL_BITS))) {
+      for (auto* l : c->lab) HIP_TRY_SP(hipMemsetAsync(l, 0, (c->nv + 1) * 4, c->stream));
+      c->epoch = 1;
+    }
+    c->mode = SP_CHAIN;
+    if (!c->chain) {
+      std::string err;
+      c->chain = chain_create(c->nv, c->edge_cap, c->stream, &err);
+      if (!c->chain) return hipErrorOutOfMemory;
+    }
+    chains[p] = c->chain;
+    qs[p] = ChainQuery{x.fwd, x.bwd, x.visible, x.vids, c->lab, c->epoch, x.s, x.t, x.upto};
+  }
+  HIP_TRY_SP(chain_launch_batch(chains.data(), n, qs.data()));
+  for (int p = 0; p < n; ++p) HIP_TRY_SP(hipEventRecord(cs[p]->done, cs[p]->stream));
+  return hipSuccess;
 }
 
 bool sp_ready(SpCtx* c) { return hipEventQuery(c->done) == hipSuccess; }

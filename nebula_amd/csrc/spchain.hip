@@ -288,8 +288,7 @@ __device__ __forceinline__ ChSnap snap_for(const ChState* st, int i, uint32_t up
 }  // namespace
 
 // Set-up (one workgroup): the state block, the labels of s and t, the one-entry lists {s}, {t}.
-__global__ void __launch_bounds__(CH_BLOCK) k_ch_setup(const ChArgs* __restrict__ Ap, ChQ q) {
-  const ChArgs& A = *Ap;
+__device__ __forceinline__ void ch_setup(const ChArgs& A, const ChQ& q) {
   ChState* st = A.st;
   uint32_t rsf, rsb;
   const uint32_t dsf = vdeg(A, 0, q.s, &rsf), dsb = vdeg(A, 1, q.t, &rsb);
@@ -329,14 +328,14 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_setup(const ChArgs* __restrict_
 //   B-set step k: B[kf - 1 - k] = vertices of forward level kf - 1 - k with an edge into
 //     B[kf - k], claimed in LAB_M (push: in-edges of B[kf - k]; pull, k == 0 only: out-edges of
 //     forward level kf - 1).
-__global__ void __launch_bounds__(CH_BLOCK) k_ch_step(const ChArgs* __restrict__ Ap, ChQ q, int i) {
+// (bid, nblk: this workgroup among the query's workgroups of the launch)
+__device__ __forceinline__ void ch_step(const ChArgs& A, const ChQ& q, int i, uint32_t bid, uint32_t nblk) {
   __shared__ uint32_t sEndAll[CH_WAVES][CH_TILE + 2];
   __shared__ uint32_t sRsAll[CH_WAVES][CH_TILE + 1];
   __shared__ uint16_t sSegAll[CH_WAVES][CH_TILE];
-  const ChArgs& A = *Ap;
   ChState* st = A.st;
   const ChSnap P = snap_for(st, i, q.upto);
-  if (i > 0 && blockIdx.x == 0 && threadIdx.x == 0) st->snap[i] = P;   // for launch i + 1
+  if (i > 0 && bid == 0 && threadIdx.x == 0) st->snap[i] = P;   // for launch i + 1
   if (P.phase == PH_DONE) return;
   const bool bfs = P.phase == PH_BFS;
   // ---- this launch's lists, labels and stamps (uniform)
@@ -397,7 +396,7 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_step(const ChArgs* __restrict__
   uint32_t* const sEnd = sEndAll[w];
   uint32_t* const sRs = sRsAll[w];
   uint16_t* const sSeg = sSegAll[w];
-  for (uint64_t t = (uint64_t)blockIdx.x * CH_WAVES + w; t < ntiles; t += (uint64_t)gridDim.x * CH_WAVES) {
+  for (uint64_t t = (uint64_t)bid * CH_WAVES + w; t < ntiles; t += (uint64_t)nblk * CH_WAVES) {
     // once this level has met, its claims are not expanded again: their appends are skipped
     // (read now, used after the claims: the load is off the critical path)
     const unsigned long long met_now = bfs ? ld_agent(&st->lmeet[i]) : 0ull;
@@ -610,10 +609,10 @@ __device__ __forceinline__ Cand hop_scan(const ChArgs& A, const uint32_t* vlab, 
 // finish; small hops are taken by one workgroup alone (workgroup 0, or the reducing one after a
 // hub), which walks on until the path is complete or the next vertex is a hub — left to the next
 // launch — and writes hstart[h + 1].
-__global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ Ap, ChQ q, int last, int h) {
+// (bid, nblk: this workgroup among the query's nblk <= CH_HOP_WGS workgroups of the launch)
+__device__ __forceinline__ void ch_hop(const ChArgs& A, const ChQ& q, int last, int h, uint32_t bid, uint32_t nblk) {
   __shared__ Cand lds[CH_WAVES + 1];
   __shared__ int s_last;
-  const ChArgs& A = *Ap;
   ChState* st = A.st;
   const ChSnap F = ch_advance(st->snap[last], st->lacc[last], st->lmeet[last], st->macc, st->err, q.upto);
   const unsigned long long H = st->hstart[h];
@@ -622,7 +621,7 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ 
     st->hstart[h + 1] = ((unsigned long long)p << 32) | v;
   };
   if (!F.met || F.phase != PH_DONE || F.err || pos >= F.L || c == NO_ROW) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) finish(pos, c);
+    if (bid == 0 && threadIdx.x == 0) finish(pos, c);
     return;
   }
   const uint32_t L = F.L, kf = F.kf;
@@ -656,23 +655,22 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ 
   if (re - rs > CH_SOLO_DEG) {   // a hub: every workgroup scans a share
     const uint32_t* vlab;
     const uint32_t want = want_of(pos, &vlab);
-    Cand best = hop_scan(A, vlab, want, rs, re, (uint64_t)blockIdx.x * CH_BLOCK + threadIdx.x,
-                         (uint64_t)gridDim.x * CH_BLOCK);
+    Cand best = hop_scan(A, vlab, want, rs, re, (uint64_t)bid * CH_BLOCK + threadIdx.x, (uint64_t)nblk * CH_BLOCK);
     best = block_min(best, lds);
     if (threadIdx.x == 0) {
-      unsigned long long* part = st->gpart + 4 * blockIdx.x;
+      unsigned long long* part = st->gpart + 4 * bid;
       part[0] = (unsigned long long)best.t;
       part[1] = (unsigned long long)best.r;
       part[2] = (unsigned long long)best.v;
       part[3] = best.d;
       __threadfence();
-      s_last = atomicAdd(&st->gticket, 1ull) == gridDim.x - 1;
+      s_last = atomicAdd(&st->gticket, 1ull) == nblk - 1;
     }
     __syncthreads();
     if (!s_last) return;
     __threadfence();
     Cand r = none;
-    if (threadIdx.x < gridDim.x) {
+    if (threadIdx.x < nblk) {
       const unsigned long long* p = st->gpart + 4 * threadIdx.x;
       r = Cand{(int64_t)ld_agent(p), (int64_t)ld_agent(p + 1), (int64_t)ld_agent(p + 2), (uint32_t)ld_agent(p + 3)};
     }
@@ -685,7 +683,7 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ 
     if (!s_last) return;
     c = r.d;
     ++pos;
-  } else if (blockIdx.x != 0) {
+  } else if (bid != 0) {
     return;
   }
   // this workgroup alone: small hops
@@ -703,6 +701,39 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ 
     ++pos;
   }
   if (threadIdx.x == 0) finish(pos, c);
+}
+
+// ---------------------------------------------------------------------------- kernels
+// One query per launch (the chain of one pair) ...
+__global__ void __launch_bounds__(CH_BLOCK) k_ch_setup(const ChArgs* __restrict__ Ap, ChQ q) { ch_setup(*Ap, q); }
+// (4 waves per SIMD, as the kernel had before it served batches: at most 128 VGPRs)
+__global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) k_ch_step(const ChArgs* __restrict__ Ap, ChQ q, int i) {
+  ch_step(*Ap, q, i, blockIdx.x, gridDim.x);
+}
+__global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ Ap, ChQ q, int last, int h) {
+  ch_hop(*Ap, q, last, h, blockIdx.x, gridDim.x);
+}
+
+// ... or up to CH_BMAX queries per launch (a batch of pairs, each with its own workspace, state and
+// labels): query p takes workgroups [p * per, (p + 1) * per) of every launch of the chain, so one
+// launch latency serves the whole batch.
+constexpr int CH_BMAX = 32;
+struct ChBatch {
+  const ChArgs* A[CH_BMAX];
+  ChQ q[CH_BMAX];
+  int n;
+  uint32_t per;
+};
+__global__ void __launch_bounds__(CH_BLOCK) k_ch_setup_b(ChBatch b) {
+  if ((int)blockIdx.x < b.n) ch_setup(*b.A[blockIdx.x], b.q[blockIdx.x]);
+}
+__global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) k_ch_step_b(ChBatch b, int i) {
+  const uint32_t p = blockIdx.x / b.per;
+  if ((int)p < b.n) ch_step(*b.A[p], b.q[p], i, blockIdx.x % b.per, b.per);
+}
+__global__ void __launch_bounds__(CH_BLOCK) k_ch_hop_b(ChBatch b, int last, int h) {
+  const uint32_t p = blockIdx.x / CH_HOP_WGS;
+  if ((int)p < b.n) ch_hop(*b.A[p], b.q[p], last, h, blockIdx.x % CH_HOP_WGS, CH_HOP_WGS);
 }
 
 // ---------------------------------------------------------------------------- host side
@@ -784,9 +815,10 @@ static hipError_t chain_batch(ChainCtx* c, int k, int h) {
   return hipMemcpyAsync(c->h_st, c->d_st, CH_COPY, hipMemcpyDeviceToHost, c->stream);
 }
 
-hipError_t chain_launch(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible,
-                        const int64_t* vids, uint32_t* const lab[3], uint32_t epoch, uint32_t s, uint32_t t,
-                        uint32_t upto) {
+// The query's arguments into c (uploaded when they changed) and its ChQ; nothing launched.
+static hipError_t chain_prepare(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible,
+                                const int64_t* vids, uint32_t* const lab[3], uint32_t epoch, uint32_t s, uint32_t t,
+                                uint32_t upto) {
   if (fwd.n != 1 || bwd.n != 1 || upto < 1 || upto > MAX_PATH_LEN) return hipErrorInvalidValue;
   ChArgs a;
   memset(&a, 0, sizeof(a));   // compared bytewise: no indeterminate padding
@@ -817,12 +849,65 @@ hipError_t chain_launch(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, con
   c->q = ChQ{s, t, upto, epoch, epoch, epoch};
   c->steps = c->hops = 0;
   ++c->queries;
+  return hipSuccess;
+}
+
+// chain length for c's query: sized by the recent queries; a longer one gets a continuation
+// batch (chain_more)
+static void chain_length(const ChainCtx* c, int* k, int* h) {
+  const int max_steps = 2 * (int)c->q.upto - 1;
+  *k = std::min(max_steps, std::max(1, (int)std::ceil(c->ema_steps)));
+  *h = std::min((int)c->q.upto, std::max(1, (int)std::ceil(c->ema_hops)));
+}
+
+hipError_t chain_launch(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible,
+                        const int64_t* vids, uint32_t* const lab[3], uint32_t epoch, uint32_t s, uint32_t t,
+                        uint32_t upto) {
+  HIP_TRY_CH(chain_prepare(c, fwd, bwd, visible, vids, lab, epoch, s, t, upto));
   hipLaunchKernelGGL(k_ch_setup, dim3(1), dim3(CH_BLOCK), 0, c->stream, (const ChArgs*)c->d_args, c->q);
-  // sized by the recent queries; a longer one gets a continuation batch (chain_more)
-  const int max_steps = 2 * (int)upto - 1;
-  const int k = std::min(max_steps, std::max(1, (int)std::ceil(c->ema_steps)));
-  const int h = std::min((int)upto, std::max(1, (int)std::ceil(c->ema_hops)));
+  int k, h;
+  chain_length(c, &k, &h);
   return chain_batch(c, k, h);
+}
+
+// n <= CH_BMAX queries (contexts on one stream) in one chain of batched launches; each context
+// then continues (chain_more) and completes (chain_result) on its own.
+hipError_t chain_launch_batch(ChainCtx* const* cs, int n, const ChainQuery* qs) {
+  if (n < 1 || n > CH_BMAX) return hipErrorInvalidValue;
+  ChBatch b;
+  memset(&b, 0, sizeof(b));
+  b.n = n;
+  static const unsigned per_env = getenv("NBG_SP_BATCH_WGS") ? (unsigned)atoi(getenv("NBG_SP_BATCH_WGS")) : 0u;
+  b.per = per_env ? per_env : std::max(32u, 1024u / (unsigned)n);
+  int k = 1, h = 1;
+  for (int p = 0; p < n; ++p) {
+    ChainCtx* c = cs[p];
+    if (c->stream != cs[0]->stream) return hipErrorInvalidValue;
+    const ChainQuery& x = qs[p];
+    HIP_TRY_CH(chain_prepare(c, *x.fwd, *x.bwd, x.visible, x.vids, x.lab, x.epoch, x.s, x.t, x.upto));
+    b.A[p] = c->d_args;
+    b.q[p] = c->q;
+    // the whole chain at once (every step and hop launch UPTO allows): a continuation would cost
+    // the batch a host round trip per context, while a launch past a query's end returns at once
+    k = std::max(k, 2 * (int)x.upto - 1);
+    h = std::max(h, (int)x.upto);
+  }
+  const hipStream_t st = cs[0]->stream;
+  hipLaunchKernelGGL(k_ch_setup_b, dim3((unsigned)n), dim3(CH_BLOCK), 0, st, b);
+  for (int j = 0; j < k; ++j) hipLaunchKernelGGL(k_ch_step_b, dim3((unsigned)n * b.per), dim3(CH_BLOCK), 0, st, b, j);
+  for (int j = 0; j < h; ++j)
+    hipLaunchKernelGGL(k_ch_hop_b, dim3((unsigned)n * CH_HOP_WGS), dim3(CH_BLOCK), 0, st, b, k - 1, j);
+  HIP_TRY_CH(hipGetLastError());
+  for (int p = 0; p < n; ++p) {
+    ChainCtx* c = cs[p];
+    // a query needing fewer launches than the batch's longest ran past its end: its launches
+    // returned at once (k_ch_step: phase DONE; k_ch_hop: nothing left to walk), as in chain_batch
+    c->steps = k;
+    c->hops = h;
+    ++c->batches;
+    HIP_TRY_CH(hipMemcpyAsync(c->h_st, c->d_st, CH_COPY, hipMemcpyDeviceToHost, st));
+  }
+  return hipSuccess;
 }
 
 // After a batch's copy completed: the query's final state, or false with a continuation batch

@@ -378,6 +378,49 @@ class Engine:
         self._check(self.lib.nbg_find_path_submit(self.h, C.byref(req), C.byref(out)), "find_path_submit")
         return out
 
+    def path_batch_prepare(self, reqs):
+        """The nbg_path_request array of a batch (built once; path_batch_run runs it)."""
+        n = len(reqs)
+        arr = (L.nbg_path_request * max(1, n))()
+        keep = []
+        for i, r in enumerate(reqs):
+            frm, to, etypes, upto, shortest = (tuple(r) + (5, True))[:5]
+            req, k = self._path_request(frm, to, etypes, upto, shortest, False)
+            arr[i] = req
+            keep.append(k)
+        return arr, n, keep
+
+    def path_batch_run(self, prep):
+        """nbg_find_path_batch on a prepared array: (outs, rcs) as the C call left them (the caller
+        frees every non-NULL outs[i] with nbg_paths_free)."""
+        arr, n, _ = prep
+        outs = (C.c_void_p * max(1, n))()
+        rcs = (C.c_int32 * max(1, n))()
+        self._check(self.lib.nbg_find_path_batch(self.h, arr, n, outs, rcs), "find_path_batch")
+        return outs, rcs
+
+    def find_path_batch(self, reqs, stats=None):
+        """nbg_find_path_batch: ``reqs`` = [(frm, to, etypes, upto, shortest)], run at once (one-pair
+        SHORTEST requests as batched device chains).  Returns one result per request: its sorted
+        entry lists, or the NbgError it failed with.  ``stats`` (a list) receives each request's
+        ``edges`` (None for a failed one)."""
+        prep = self.path_batch_prepare(reqs)
+        outs, rcs = self.path_batch_run(prep)
+        n = len(reqs)
+        res = []
+        for i in range(n):
+            st = {}
+            if rcs[i]:
+                msg = self.lib.nbg_last_error(self.h)
+                res.append(NbgError(rcs[i], f"find_path_batch[{i}]: {msg.decode() if msg else ''}"))
+                if outs[i]:
+                    self.lib.nbg_paths_free(outs[i])
+            else:
+                res.append(self._paths(C.c_void_p(outs[i]), st))
+            if stats is not None:
+                stats.append(st.get("edges"))
+        return res
+
     def find_path_wait(self, ticket, stats=None):
         out = C.c_void_p()
         self._check(self.lib.nbg_find_path_wait(ticket, C.byref(out)), "find_path_wait")

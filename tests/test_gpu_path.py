@@ -174,3 +174,37 @@ def test_async_path_submit_wait_parity(sp_mode):
     finally:
         eng.close()
         orc.close()
+
+
+def test_find_path_batch_matches_single(sp_mode):
+    """nbg_find_path_batch: one-pair SHORTEST requests run NBG_SP_BATCH at a time as one batched
+    device level loop; mixed in are requests that run on their own (s == t, several sources,
+    unknown vids, FIND ALL PATH, an endpoint without edges).  Every result equals nbg_find_path's,
+    the edge counts too, and the oracle's paths."""
+    src, dst, w = graphs.rmat_graph(11)
+    eng = graphs.rmat_engine(src, dst, w)
+    orc = graphs.rmat_oracle(src, dst, w)
+    try:
+        from nebula_amd import rmat
+        ps = rmat.pick_pairs(src, dst, 70, seed=23)
+        reqs = [([s], [t], [1], 5, True) for s, t in ps]
+        reqs += [([ps[0][0]], [ps[0][0]], [1], 4, True), ([ps[1][0], ps[2][0]], [ps[3][1]], [1], 4, True),
+                 ([123456789], [ps[4][1]], [1], 5, True), ([ps[5][0]], [ps[6][1]], [1], 3, False),
+                 ([ps[7][0]], [ps[8][1]], [1], 2, True)]
+        st = []
+        got = eng.find_path_batch(reqs, stats=st)
+        assert len(got) == len(reqs)
+        found = 0
+        for (f, t, e, upto, shortest), g, edges in zip(reqs, got, st):
+            s1 = {}
+            exp = eng.find_path(f, t, e, upto, shortest=shortest, stats=s1)
+            assert g == exp, (f, t, upto, shortest)
+            assert edges == s1["edges"], (f, t)
+            if shortest:
+                assert g == sorted(orc.find_path(f, t, e, upto, True, mode=1))
+            found += bool(g)
+        assert found > 20
+        assert eng.find_path_batch([]) == []
+    finally:
+        eng.close()
+        orc.close()
