@@ -516,6 +516,9 @@ def main():
         cpu = faithful_baseline(args, where, threads, model, ncpu)
         if cpu is not None:
             cpu["csr_openmp"] = cpu_csr
+            full = committed_faithful()
+            if full:
+                cpu["storaged_faithful_full_sample"] = full
         elif cpu_csr is not None:
             cpu = cpu_csr
     if sp is not None and cpu_csr is not None:
@@ -625,6 +628,21 @@ def csr_baseline(csr, roots, pairs, args, threads, model, ncpu):
             "sample": f"all {len(roots)} headline roots (same graph and query), median of 5 runs after 1 warm-up "
                       f"({secs:.2f}s per run); oracle/csr.cpp OpenMP CSR GO, {threads} threads",
             "model": model, "host_cpus": ncpu, "shortest": sp}
+
+
+def committed_faithful():
+    """Mode (i) at the full sample (16 roots x 5 runs, 20 pairs): too long for every bench run
+    (~15 min), so measured once on a GPU box's host by tools/cpu_faithful_full.py and committed."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    out = {}
+    for key, name in (("go", "r02_cpu_faithful_go.json"), ("shortest", "r02_cpu_faithful_sp.json")):
+        path = os.path.join(here, "profiles", name)
+        if os.path.exists(path):
+            d = json.load(open(path))
+            d.pop("lat_ms", None)
+            d["source"] = f"profiles/{name} (tools/cpu_faithful_full.py)"
+            out[key] = d
+    return out or None
 
 
 def faithful_baseline(args, where, threads, model, ncpu):

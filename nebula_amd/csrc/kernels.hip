@@ -158,6 +158,16 @@ struct Workspace {
   hipEvent_t done_ev = nullptr;             // ws_wait's completion event
   unsigned long long* pgst = nullptr;       // [PG_N] globally reduced FIND PATH sizes
   unsigned long long* h_pgst = nullptr;
+  // partitioned greedy (allocated on first use): per-block minima, this rank's record, every
+  // rank's records, the path and {current global id, error} — the hops run without host waits
+  void* g_part = nullptr;
+  int64_t* g_rec = nullptr;
+  int64_t* g_all = nullptr;
+  int64_t* g_path = nullptr;
+  unsigned long long* g_cur = nullptr;
+  int64_t* h_gpath = nullptr;               // pinned: path + {cur, err}
+  unsigned long long* ar_buf = nullptr;     // ws_allreduce_host scratch (grow-only)
+  uint64_t ar_cap = 0;
   unsigned long long* h_gst = nullptr;
 };
 
@@ -1555,8 +1565,10 @@ void ws_destroy(Workspace* w) {
     if (p) (void)hipHostFree(p);
   if (w->h_pgst) (void)hipHostFree(w->h_pgst);
   if (w->done_ev) (void)hipEventDestroy(w->done_ev);
-  for (void* p : {(void*)w->sendbits, (void*)w->recvbits, (void*)w->gst, (void*)w->pgst})
+  for (void* p : {(void*)w->sendbits, (void*)w->recvbits, (void*)w->gst, (void*)w->pgst, w->g_part, (void*)w->g_rec,
+                  (void*)w->g_all, (void*)w->g_path, (void*)w->g_cur, (void*)w->ar_buf})
     if (p) (void)hipFree(p);
+  if (w->h_gpath) (void)hipHostFree(w->h_gpath);
   if (w->h_gst) (void)hipHostFree(w->h_gst);
   for (void* p : {(void*)w->ps, (void*)w->pscratch, (void*)w->d_path})
     if (p) (void)hipFree(p);
@@ -2893,7 +2905,8 @@ struct GreedyPart {
   const int64_t* vids;
   uint64_t nv;
   uint32_t gbase;                       // this rank's first global id
-  uint32_t v;                           // current vertex (global id)
+  uint32_t v;                           // current vertex (global id) ...
+  const unsigned long long* vp;         // ... or read here ({gid, err}: nothing to do after an error)
   int pos;                              // B-set position of the candidates
   int L, kf;
   const uint32_t* lab_m;
@@ -2912,6 +2925,10 @@ __device__ __forceinline__ bool part_valid(const GreedyPart& g, uint32_t u) {
 __global__ void __launch_bounds__(BLOCK) k_greedy_part(GreedyPart g) {
   __shared__ Cand lds[WAVES + 1];
   Cand best{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
+  if (g.vp) {
+    if (g.vp[1]) g.nv = 0;   // an earlier hop failed: no candidates
+    g.v = (uint32_t)g.vp[0];
+  }
   for (uint64_t u = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; u < g.nv; u += (uint64_t)gridDim.x * BLOCK) {
     if (!part_valid(g, (uint32_t)u)) continue;
     for (int t = 0; t < g.ntypes; ++t) {
@@ -2969,6 +2986,32 @@ __global__ void k_min_vid(const uint32_t* __restrict__ ids, const unsigned long 
     if (d != NO_ROW && vids[d] < b.v) b = Cand{0, 0, vids[d], d};
   }
   put_record(b, gbase, visible, out);
+}
+
+// Every rank's record (after the all-gather) -> the global minimum (type, rank, vid): path entry
+// `pos` (0: v0 alone) and the next hop's vertex in cur[0]; cur[1] = error (no candidate, or an
+// invisible vertex that a further hop would have to leave).  Every rank computes the same.
+__global__ void k_greedy_pick(const int64_t* __restrict__ all, int G, int pos, int L, int64_t* __restrict__ path,
+                              unsigned long long* __restrict__ cur) {
+  if (threadIdx.x != 0 || cur[1]) return;
+  const int64_t* b = nullptr;
+  for (int q = 0; q < G; ++q) {   // distinct ranks never tie (vids are unique)
+    const int64_t* x = all + (size_t)q * GREC;
+    if (x[3] < 0) continue;
+    if (!b || x[0] < b[0] || (x[0] == b[0] && (x[1] < b[1] || (x[1] == b[1] && x[2] < b[2])))) b = x;
+  }
+  if (!b || (pos < L && !b[4])) {
+    cur[1] = 1;
+    return;
+  }
+  if (pos == 0) {
+    path[0] = b[2];
+  } else {
+    path[1 + 3 * (pos - 1)] = b[0];
+    path[2 + 3 * (pos - 1)] = b[1];
+    path[3 + 3 * (pos - 1)] = b[2];
+  }
+  cur[0] = (unsigned long long)b[3];
 }
 
 hipError_t ws_path_level_part(Workspace* w, const PathTypes& pt, int src, uint64_t n_bound, uint64_t e_bound, int dst,
@@ -3066,105 +3109,95 @@ hipError_t ws_path_sync_part(Workspace* w, PState* out) {
 // Sum a host vector over ranks (small control data: label values, presence flags).
 hipError_t ws_allreduce_host(Workspace* w, std::vector<unsigned long long>& v) {
   if (!w->comm || v.empty()) return hipSuccess;
-  unsigned long long* d = nullptr;
-  hipError_t e = hipMalloc((void**)&d, v.size() * 8);
-  if (e == hipSuccess) e = hipMemcpyAsync(d, v.data(), v.size() * 8, hipMemcpyHostToDevice, w->stream);
+  if (v.size() > w->ar_cap) {   // grow-only scratch (no allocation per query)
+    if (w->ar_buf) {
+      HIP_TRY(hipStreamSynchronize(w->stream));
+      (void)hipFree(w->ar_buf);
+      w->ar_buf = nullptr;
+      w->ar_cap = 0;
+    }
+    const uint64_t cap = std::max<uint64_t>(v.size(), 256);
+    HIP_TRY(hipMalloc((void**)&w->ar_buf, cap * 8));
+    w->ar_cap = cap;
+  }
+  unsigned long long* d = w->ar_buf;
+  hipError_t e = hipMemcpyAsync(d, v.data(), v.size() * 8, hipMemcpyHostToDevice, w->stream);
   if (e == hipSuccess && w->comm->allreduce_sum_u64(d, v.size(), w->stream)) e = hipErrorUnknown;
   if (e == hipSuccess) e = hipMemcpyAsync(v.data(), d, v.size() * 8, hipMemcpyDeviceToHost, w->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(w->stream);
-  if (d) (void)hipFree(d);
-  return e;
-}
-
-// Gather one GREC x int64 record per rank (rank order) from a device buffer.
-static hipError_t gather_records(Workspace* w, const int64_t* d_rec, std::vector<int64_t>* out) {
-  const int G = w->comm->world;
-  int64_t* d_all = nullptr;
-  hipError_t e = hipMalloc((void**)&d_all, (size_t)G * GREC * 8);
-  if (e == hipSuccess && w->comm->allgather(d_rec, d_all, GREC * 8, w->stream)) e = hipErrorUnknown;
-  out->assign((size_t)G * GREC, 0);
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(out->data(), d_all, (size_t)G * GREC * 8, hipMemcpyDeviceToHost, w->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(w->stream);
-  if (d_all) (void)hipFree(d_all);
   return e;
 }
 
 // Lexicographically smallest shortest path through the B-sets on a partitioned engine; the path
 // entries are written to `path` (1 + 3L).  Returns hipErrorNotFound when a hop has no candidate.
+// The hops run back to back on the device: each rank's candidate record, one all-gather, and
+// k_greedy_pick (the same on every rank) hands the next hop its vertex in device memory; the
+// host waits once, for the path.
 hipError_t ws_path_greedy_part(Workspace* w, const PathTypes& bwd, const PathGreedy& pg, const int64_t* vids,
                                const uint8_t* visible, int64_t* path) {
   if (!w->comm) return hipErrorInvalidValue;
   if (pg.L < 1 || pg.L > (int)MAX_PATH_LEN) return hipErrorInvalidValue;
+  const int G = w->comm->world;
   const uint32_t gbase = (uint32_t)((uint64_t)w->comm->rank * w->npad);
   const uint64_t nblk = cdiv(w->nv ? w->nv : 1, BLOCK);
-  const unsigned grid = (unsigned)(nblk < 1024 ? nblk : 1024);
-  Cand* d_part = nullptr;
-  int64_t* d_rec = nullptr;
-  hipError_t e = hipMalloc((void**)&d_part, (size_t)grid * sizeof(Cand));
-  if (e == hipSuccess) e = hipMalloc((void**)&d_rec, GREC * 8);
-  std::vector<int64_t> all;
-  // the rank records' minimum (type, rank, vid); distinct ranks never tie (vids are unique)
-  auto pick = [&]() -> const int64_t* {
-    const int64_t* b = nullptr;
-    for (int q = 0; q < w->comm->world; ++q) {
-      const int64_t* x = &all[(size_t)q * GREC];
-      if (x[3] < 0) continue;
-      if (!b || x[0] < b[0] || (x[0] == b[0] && (x[1] < b[1] || (x[1] == b[1] && x[2] < b[2])))) b = x;
-    }
-    return b;
-  };
-  // v0: the smallest vid of B[0]
-  if (e == hipSuccess) {
-    hipLaunchKernelGGL(k_min_vid, dim3(1), dim3(64), 0, w->stream, w->slot[pg.start_slot], &w->ps->n[pg.start_slot],
-                       vids, gbase, visible, d_rec);
-    e = hipGetLastError();
+  constexpr unsigned kGrid = 1024;
+  const unsigned grid = (unsigned)(nblk < kGrid ? nblk : kGrid);
+  if (!w->g_part) {
+    HIP_TRY(hipMalloc(&w->g_part, (size_t)kGrid * sizeof(Cand)));
+    HIP_TRY(hipMalloc((void**)&w->g_rec, GREC * 8));
+    HIP_TRY(hipMalloc((void**)&w->g_all, (size_t)G * GREC * 8));
+    HIP_TRY(hipMalloc((void**)&w->g_path, (1 + 3 * (size_t)MAX_PATH_LEN) * 8));
+    HIP_TRY(hipMalloc((void**)&w->g_cur, 2 * 8));
+    HIP_TRY(hipHostMalloc((void**)&w->h_gpath, (3 + 3 * (size_t)MAX_PATH_LEN) * 8, hipHostMallocDefault));
   }
-  if (e == hipSuccess) e = gather_records(w, d_rec, &all);
-  const int64_t* b = e == hipSuccess ? pick() : nullptr;
-  if (e == hipSuccess && !b) e = hipErrorNotFound;
-  if (e == hipSuccess) path[0] = b[2];
-  for (int pos = 1; e == hipSuccess && pos <= pg.L; ++pos) {
-    if (!b[4]) { e = hipErrorNotFound; break; }   // an invisible vertex has no out-edges
-    GreedyPart g{};
-    g.ntypes = bwd.n;
-    for (int t = 0; t < bwd.n; ++t) {
-      g.type[t] = -bwd.type[t];
-      g.row_ptr[t] = bwd.a[t].row_ptr;
-      g.col[t] = bwd.a[t].col;
-      g.rank[t] = bwd.a[t].rank;
-    }
-    g.visible = visible;
-    g.vids = vids;
-    g.nv = w->nv;
-    g.gbase = gbase;
-    g.v = (uint32_t)b[3];
+  Cand* d_part = static_cast<Cand*>(w->g_part);
+  HIP_TRY(hipMemsetAsync(w->g_cur, 0, 2 * 8, w->stream));
+  // v0: the smallest vid of B[0]
+  hipLaunchKernelGGL(k_min_vid, dim3(1), dim3(64), 0, w->stream, w->slot[pg.start_slot], &w->ps->n[pg.start_slot],
+                     vids, gbase, visible, w->g_rec);
+  HIP_TRY(hipGetLastError());
+  if (w->comm->allgather(w->g_rec, w->g_all, GREC * 8, w->stream)) return hipErrorUnknown;
+  hipLaunchKernelGGL(k_greedy_pick, dim3(1), dim3(64), 0, w->stream, w->g_all, G, 0, pg.L, w->g_path, w->g_cur);
+  HIP_TRY(hipGetLastError());
+  GreedyPart g{};
+  g.ntypes = bwd.n;
+  for (int t = 0; t < bwd.n; ++t) {
+    g.type[t] = -bwd.type[t];
+    g.row_ptr[t] = bwd.a[t].row_ptr;
+    g.col[t] = bwd.a[t].col;
+    g.rank[t] = bwd.a[t].rank;
+  }
+  g.visible = visible;
+  g.vids = vids;
+  g.nv = w->nv;
+  g.gbase = gbase;
+  g.vp = w->g_cur;
+  g.L = pg.L;
+  g.kf = pg.kf;
+  g.lab_m = w->lab[LAB_M];
+  g.em = pg.em;
+  g.lab_b = w->lab[LAB_B];
+  g.eb = pg.eb;
+  g.part = d_part;
+  for (int pos = 1; pos <= pg.L; ++pos) {
     g.pos = pos;
-    g.L = pg.L;
-    g.kf = pg.kf;
-    g.lab_m = w->lab[LAB_M];
-    g.em = pg.em;
-    g.lab_b = w->lab[LAB_B];
-    g.eb = pg.eb;
-    g.part = d_part;
     hipEvent_t p = prof_begin_p(w, K_GREEDY);
     hipLaunchKernelGGL(k_greedy_part, dim3(grid), dim3(BLOCK), 0, w->stream, g);
     hipLaunchKernelGGL(k_greedy_part_reduce, dim3(1), dim3(64), 0, w->stream, d_part, (int)grid, gbase, visible,
-                       d_rec);
+                       w->g_rec);
     prof_end_p(w, p, K_GREEDY, 0);
-    e = hipGetLastError();
-    if (e == hipSuccess) e = gather_records(w, d_rec, &all);
-    b = e == hipSuccess ? pick() : nullptr;
-    if (e == hipSuccess && !b) e = hipErrorNotFound;
-    if (e == hipSuccess) {
-      path[1 + 3 * (pos - 1)] = b[0];
-      path[2 + 3 * (pos - 1)] = b[1];
-      path[3 + 3 * (pos - 1)] = b[2];
-    }
+    HIP_TRY(hipGetLastError());
+    if (w->comm->allgather(w->g_rec, w->g_all, GREC * 8, w->stream)) return hipErrorUnknown;
+    hipLaunchKernelGGL(k_greedy_pick, dim3(1), dim3(64), 0, w->stream, w->g_all, G, pos, pg.L, w->g_path, w->g_cur);
+    HIP_TRY(hipGetLastError());
   }
-  if (d_part) (void)hipFree(d_part);
-  if (d_rec) (void)hipFree(d_rec);
-  return e;
+  const size_t np = 1 + 3 * (size_t)pg.L;
+  HIP_TRY(hipMemcpyAsync(w->h_gpath, w->g_path, np * 8, hipMemcpyDeviceToHost, w->stream));
+  HIP_TRY(hipMemcpyAsync(w->h_gpath + np, w->g_cur, 2 * 8, hipMemcpyDeviceToHost, w->stream));
+  HIP_TRY(hipStreamSynchronize(w->stream));
+  if (w->h_gpath[np + 1]) return hipErrorNotFound;
+  memcpy(path, w->h_gpath, np * 8);
+  return hipSuccess;
 }
 
 }  // namespace nbg
