@@ -778,7 +778,15 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
 #define NBG_PH(k)
 #endif
   const uint64_t g = (uint64_t)gridDim.x * WAVES;
+#ifdef NBG_XCD_TILES
+  // XCD-aware tile order (A/B switch of the build): workgroups are dealt round-robin to the 8
+  // XCDs, so number them XCD-major and the adjacent tiles (which share cache lines at their
+  // boundaries) stay on one XCD's L2
+  const uint32_t xb = (gridDim.x % 8 == 0) ? (blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8 : blockIdx.x;
+  uint64_t t = (uint64_t)xb * WAVES + w;
+#else
   uint64_t t = (uint64_t)blockIdx.x * WAVES + w;
+#endif
   uint64_t sp_next = 0;            // lanes 0, 1: split (start, end) of tile t + g
   uint64_t a0 = 0, a1 = 0;         // split of tile t
   uint32_t e_pre = 0, r_pre = 0;   // lane's entry of tile t's segment-end window / row starts
