@@ -135,3 +135,48 @@ def test_c4_shortest_pairs_rmat26(rmat26, sp_mode):
     src, dst, eng, csr, _, av = rmat26
     pairs = rmat.pick_pairs(src, dst, 64, 7, verts=av)
     assert _check_pairs(eng, csr, pairs) > 20
+
+
+def _c5_graph(k):
+    """BASELINE C5's synthetic substitute (bench.py c5_leg) at scale k: knows = RMAT-k over persons,
+    likes = a bipartite RMAT-(k-1) from persons to posts (post vids in a disjoint range)."""
+    ks, kd, kw = rmat.rmat_edges_fast(k)
+    ls, ld, lw = rmat.rmat_edges_fast(k - 1, seed=rmat.SEED_BASE ^ 0x6C696B6573)
+    persons = np.union1d(np.unique(ks), np.unique(kd))
+    ls = persons[(ls.astype(np.uint64) % np.uint64(len(persons))).astype(np.int64)]
+    ld = ld ^ (1 << 61)
+    return (ks, kd, kw), (ls, ld, lw)
+
+
+def test_c5_substitute_go4_and_all_paths():
+    """C5 (LDBC SNB SF100 substitute, at RMAT-11): GO 4 STEPS OVER knows, likes (default YIELD:
+    one _dst column per OVER type) and FIND ALL PATH UPTO 4 STEPS OVER knows, against the
+    storaged-faithful oracle (full sorted compare)."""
+    from tests.support import graphs
+    from tests.support.oracle import Oracle
+    (ks, kd, kw), (ls, ld, lw) = _c5_graph(11)
+    eng = Engine(100)
+    orc = Oracle(100)
+    for be, is_eng in ((eng, True), (orc, False)):
+        for t, name in ((1, "knows"), (2, "likes")):
+            if is_eng:
+                be.register_edge(t, name, [("w", 2)])
+            else:
+                be.register(True, t, name, [("w", 2)])
+        be.load_edges(1, ks, kd, [kw])
+        be.load_edges(2, ls, ld, [lw])
+        be.finalize()
+    try:
+        roots = [int(x) for x in rmat.pick_roots(ks, 6, 42)]
+        for r in roots:
+            got = graphs.sorted_rows(eng.go([r], [1, 2], 4))
+            assert got == graphs.sorted_rows(orc.go([r], [1, 2], 4)), r
+        total = 0
+        for s, t in rmat.pick_pairs(ks, kd, 8, 7):
+            got = eng.find_path([s], [t], [1], 4, shortest=False)
+            assert got == sorted(orc.find_path([s], [t], [1], 4, False)), (s, t)
+            total += len(got)
+        assert total > 0
+    finally:
+        eng.close()
+        orc.close()
