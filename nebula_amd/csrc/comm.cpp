@@ -46,6 +46,19 @@ struct RcclComm final : Comm {
   int allreduce_sum_u64(unsigned long long* buf, size_t n, hipStream_t s) override {
     return check(ncclAllReduce(buf, buf, n, ncclUint64, ncclSum, comm, s), "ncclAllReduce");
   }
+  Comm* split(std::string* err) override {
+    ncclComm_t nc = nullptr;
+    const ncclResult_t r = ncclCommSplit(comm, 0, rank, &nc, nullptr);
+    if (r != ncclSuccess || !nc) {
+      if (err) *err = std::string("ncclCommSplit: ") + ncclGetErrorString(r);
+      return nullptr;
+    }
+    auto* c = new RcclComm();
+    c->comm = nc;
+    c->world = world;
+    c->rank = rank;
+    return c;
+  }
 };
 
 // ----------------------------------------------------------------------------- in-process group

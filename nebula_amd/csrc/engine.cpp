@@ -482,10 +482,11 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
   // (partitioned: every rank runs the same collective sequence, even with no local start)
   if (f0.empty() && !E.partitioned()) { p->finished = true; return NBG_OK; }
   if (f0.size() > ws_cap_frontier(*wsp)) {   // room for a duplicated start list
+    Comm* cm = ws_get_comm(*wsp);
     ws_destroy(*wsp);
     *wsp = ws_create(f0.size(), E.snap.nv, E.snap.max_edges(), stream, &err);
     if (!*wsp) { delete rows; p->rows = nullptr; return E.fail(NBG_E_OUT_OF_MEMORY, err); }
-    if (E.partitioned() && ws_set_partition(*wsp, E.comm.get(), E.npad) != hipSuccess) {
+    if (E.partitioned() && ws_set_partition(*wsp, cm ? cm : E.comm.get(), E.npad) != hipSuccess) {
       delete rows;
       p->rows = nullptr;
       return E.fail(NBG_E_OUT_OF_MEMORY, "partition buffers");
@@ -822,11 +823,12 @@ int32_t nbg::ws_release(Engine& E, Workspace** wsp, hipStream_t stream) {
   if (it == E.holders.end()) return NBG_OK;
   nbg_rows* r = it->second;
   E.holders.erase(it);
+  Comm* cm = ws_get_comm(*wsp);   // (the fresh workspace keeps the slot's communicator)
   r->owned_ws = *wsp;
   std::string err;
   Workspace* fresh = ws_create(E.snap.nv + 1024, E.snap.nv, E.snap.max_edges(), stream, &err);
   if (!fresh) { *wsp = nullptr; return E.fail(NBG_E_OUT_OF_MEMORY, err); }
-  if (E.partitioned() && ws_set_partition(fresh, E.comm.get(), E.npad) != hipSuccess) {
+  if (E.partitioned() && ws_set_partition(fresh, cm ? cm : E.comm.get(), E.npad) != hipSuccess) {
     ws_destroy(fresh);
     *wsp = nullptr;
     return E.fail(NBG_E_OUT_OF_MEMORY, "partition buffers");
@@ -868,27 +870,43 @@ int32_t nbg_go_submit(nbg_go_stmt* st, const int64_t* starts, uint64_t num_start
     slot = s0;
   }
   Engine::QuerySlot& q = E.slots[slot];
-  // a partitioned engine's queries are collectives: its slots share the engine's stream (and
-  // communicator), so every rank's collectives stay in submission order — the host work of one
-  // query overlaps the device work of the next, the device runs them one after another
-  const hipStream_t qs = E.partitioned() ? E.stream : q.stream;
-  if (!E.partitioned() && !q.stream && hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking) != hipSuccess)
-    return E.fail(NBG_E_DEVICE, "hipStreamCreate failed");
+  // A partitioned engine's queries are collectives.  Each slot gets its own communicator (a
+  // split of the engine's, made collectively the first time the slot is used: every rank submits
+  // the same queries in the same order, so it picks the same slot at the same call), and so its
+  // own stream: the ranks issue every communicator's collectives in one order, and queries of
+  // different slots overlap on the device.  Without a split (in-process transport, or
+  // NBG_SLOT_COMMS=0) the slots share the engine's stream and communicator, one query after
+  // another on the device.
+  if (E.partitioned() && !q.comm_tried) {
+    q.comm_tried = true;
+    static const bool split_ok = !getenv("NBG_SLOT_COMMS") || atoi(getenv("NBG_SLOT_COMMS")) != 0;
+    if (split_ok) {
+      std::string err;
+      q.comm.reset(E.comm->split(&err));
+    }
+  }
+  const bool own_stream = !E.partitioned() || q.comm != nullptr;
+  Comm* const qcomm = q.comm ? q.comm.get() : E.comm.get();
+  if (own_stream && !q.stream) {
+    if (hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking) != hipSuccess)
+      return E.fail(NBG_E_DEVICE, "hipStreamCreate failed");
+  }
+  const hipStream_t qstream = own_stream ? q.stream : E.stream;
   if (q.ws) {   // rows of an earlier device result still there: hand the workspace to them
-    int32_t rc = ws_release(E, &q.ws, qs);
+    int32_t rc = ws_release(E, &q.ws, qstream);
     if (rc) return rc;
   }
   if (!q.ws) {
     std::string err;
-    q.ws = ws_create(E.snap.nv + 1024, E.snap.nv, E.snap.max_edges(), E.partitioned() ? E.stream : q.stream, &err);
+    q.ws = ws_create(E.snap.nv + 1024, E.snap.nv, E.snap.max_edges(), qstream, &err);
     if (!q.ws) return E.fail(NBG_E_OUT_OF_MEMORY, err);
-    if (E.partitioned() && ws_set_partition(q.ws, E.comm.get(), E.npad) != hipSuccess)
+    if (E.partitioned() && ws_set_partition(q.ws, qcomm, E.npad) != hipSuccess)
       return E.fail(NBG_E_OUT_OF_MEMORY, "partition buffers");
   }
   auto* t = new nbg_go_ticket();
   t->st = st;
   t->slot = slot;
-  int32_t rc = go_launch(E, st, starts, num_starts, device != 0, &q.ws, qs, &t->p);
+  int32_t rc = go_launch(E, st, starts, num_starts, device != 0, &q.ws, qstream, &t->p);
   if (rc) { delete t; return rc; }
   q.ticket = t;
   E.inflight.push_back(t);
@@ -936,7 +954,9 @@ void nbg_destroy(nbg_engine* h) {
   }
   E.holders.clear();   // results must be freed before nbg_destroy (nbg.h)
   for (auto& q : E.slots) {
+    if (q.stream) (void)hipStreamSynchronize(q.stream);
     if (q.ws) ws_destroy(q.ws);
+    q.comm.reset();
     if (q.stream) (void)hipStreamDestroy(q.stream);
   }
   path_slots_release(E);

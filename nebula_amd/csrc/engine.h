@@ -33,6 +33,10 @@ struct Engine {
     Workspace* ws = nullptr;
     hipStream_t stream = nullptr;
     void* ticket = nullptr;   // the ticket running on this slot (nullptr: free)
+    // partitioned engine: the slot's own communicator (split from `comm` when the slot is first
+    // used) lets its queries run on its own stream beside the other slots'
+    std::unique_ptr<Comm> comm;
+    bool comm_tried = false;
   };
   std::vector<QuerySlot> slots;
   SpCtx* sp = nullptr;                  // one-pair FIND SHORTEST PATH workspace (sp.hip), on `stream`

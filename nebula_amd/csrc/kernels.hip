@@ -2298,6 +2298,8 @@ hipError_t ws_set_partition(Workspace* w, Comm* comm, uint64_t npad) {
 
 // After all OVER types of a non-final step marked their candidates (global ids) in the flags:
 // pack -> all-to-all of npad-bit segments -> owner OR + compaction into the next local frontier.
+Comm* ws_get_comm(const Workspace* w) { return w ? w->comm : nullptr; }
+
 hipError_t ws_exchange(Workspace* w, int step, const ExpandArgs* next0) {
   if (!w->comm) return hipErrorInvalidValue;
   const uint64_t G = (uint64_t)w->comm->world;

@@ -373,6 +373,12 @@ struct Comm {
   // recv[q * bytes ..] <- rank q's send[0 .. bytes)
   virtual int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
   virtual int allreduce_sum_u64(unsigned long long* buf, size_t n, hipStream_t s) = 0;
+  // A second communicator over the same ranks (collective: every rank calls it at the same
+  // point), for collectives on another stream; nullptr when the transport has none.
+  virtual Comm* split(std::string* err) {
+    (void)err;
+    return nullptr;
+  }
 };
 Comm* comm_rccl(const uint8_t id[NBG_UNIQUE_ID_BYTES], int world, int rank, std::string* err);
 std::vector<Comm*> comm_local_group(int world);
@@ -474,6 +480,7 @@ hipError_t ws_end_query_wait(Workspace* w);    // wait for it (then as ws_end_qu
 // partitioned mode: flags over [world * npad) global ids, per-hop bitmap all-to-all
 constexpr uint64_t PART_ALIGN = 16384 * 4;   // npad granularity (flag / bit workgroups divide it)
 hipError_t ws_set_partition(Workspace* w, Comm* comm, uint64_t npad);
+Comm* ws_get_comm(const Workspace* w);   // the communicator of a partitioned workspace (else nullptr)
 hipError_t ws_exchange(Workspace* w, int step, const ExpandArgs* next0);   // replaces ws_compact
 hipError_t ws_global_stats(Workspace* w, int ntypes);      // before ws_end_query
 void ws_host_gstats(Workspace* w, unsigned long long* err, unsigned long long* step_n, unsigned long long* esum,

@@ -55,6 +55,27 @@ def main():
                 good = got == ref and stats == single.last_step_stats
                 ok &= good
                 print(f"root {r} steps {steps}: {len(got)} rows {'OK' if good else 'MISMATCH'}", flush=True)
+    # query slots: more queries in flight than slots; each slot has its own split communicator
+    # and stream (NBG_SLOT_COMMS), so queries of different slots overlap on the device
+    stmt = eng.prepare_go([1], 3, where)
+    roots = graphs.roots(src, 9, seed=13)
+    for rnd in range(2):
+        tickets = [stmt.submit([r], device=bool(rnd)) for r in roots]
+        mine = []
+        for t in tickets:
+            res = stmt.wait(t)
+            mine.append(res.fetch())
+            res.free()
+        parts = [None] * world
+        dist.all_gather_object(parts, mine)
+        if rank == 0:
+            for i, r in enumerate(roots):
+                got = graphs.sorted_rows([row for p in parts for row in p[i]])
+                good = got == graphs.sorted_rows(single.go([r], [1], 3, where))
+                ok &= good
+                print(f"slot query {i} (device={bool(rnd)}) root {r}: {len(got)} rows {'OK' if good else 'MISMATCH'}",
+                      flush=True)
+    stmt.free()
     # FIND SHORTEST PATH: every rank reconstructs the same paths (collective BFS + greedy)
     from nebula_amd import rmat
     for s, t in rmat.pick_pairs(src, dst, 8, seed=17):
