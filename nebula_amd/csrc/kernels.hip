@@ -367,11 +367,11 @@ __device__ __forceinline__ int64_t load_col(const void* p, int bytes, uint32_t j
 #endif
 
 // VT loads of a column of type T (sign-extended), all in flight at once
-template <typename T>
+template <typename T, int V = VT>
 __device__ __forceinline__ void load_narrow(const void* p, const uint32_t* jj, int nb, int lane, int64_t* x) {
   const T* c = reinterpret_cast<const T*>(p);
 #pragma unroll
-  for (int i = 0; i < VT; ++i) x[i] = (i * 64 + lane < nb) ? (int64_t)NBG_LD_STREAM(c + jj[i]) : 0;
+  for (int i = 0; i < V; ++i) x[i] = (i * 64 + lane < nb) ? (int64_t)NBG_LD_STREAM(c + jj[i]) : 0;
 }
 
 struct FastProg {
@@ -660,14 +660,21 @@ using InlineArg = typename std::conditional<INL, InlineList, NoInline>::type;
 
 // INL: the list is the query's start list, passed in the kernel arguments (InlineList) and
 // staged in LDS; its tile splits are counted directly (<= INLINE_STARTS entries).
-template <int M, bool INL = false>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M == FINAL ? 4 : 8)))
+// V: merge-path items per lane (the tile is 64 * V items).  Producers split their lists per
+// TILE = 64 * VT; a V = 2 * VT instantiation reads every other split.  (FINALD with V = 8 at 5 or
+// 6 waves per SIMD measured 307-338 us per RMAT-26 launch against 222 us at V = 4 and 8 waves,
+// profiles/r02_q_final_vt8_ab.json: the default V = VT is the only one launched.)
+template <int M, bool INL = false, int V = VT>
+#ifndef NBG_WIDE_WAVES
+#define NBG_WIDE_WAVES 6
+#endif
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M == FINAL ? 4 : (V > VT ? NBG_WIDE_WAVES : 8))))
 k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_t* __restrict__ seg_end,
          const uint32_t* __restrict__ seg_rs, uint8_t* __restrict__ flags, FinalParams fp, BfsParams bp,
          unsigned long long* stat_e, unsigned long long* stat_n, InlineArg<INL> il) {
-  __shared__ uint32_t sEndAll[WAVES][TILE + 2];   // per wave: seg_end for i in [a0-1, a1]
-  __shared__ uint32_t sRsAll[WAVES][TILE + 1];    // per wave: seg_rs for i in [a0, a1]
-  __shared__ uint16_t sSegAll[WAVES][TILE];       // per wave: segment of each edge item
+  __shared__ uint32_t sEndAll[WAVES][64 * V + 2];   // per wave: seg_end for i in [a0-1, a1]
+  __shared__ uint32_t sRsAll[WAVES][64 * V + 1];    // per wave: seg_rs for i in [a0, a1]
+  __shared__ uint16_t sSegAll[WAVES][64 * V];       // per wave: segment of each edge item
   __shared__ unsigned long long sBase;            // FINAL: rows this workgroup wrote (LDS cursor)
   extern __shared__ int64_t regs[];               // FINAL generic path: [nregs][BLOCK]
 
@@ -697,7 +704,9 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
     }
   }
   const uint64_t npath = n + total;
-  const uint64_t ntiles = (npath + TILE - 1) / TILE;
+  constexpr uint64_t TV = 64 * V;   // items per tile
+  static_assert(TV % TILE == 0, "tiles are whole producer tiles");
+  const uint64_t ntiles = (npath + TV - 1) / TV;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar registers
   uint32_t* const sEnd = sEndAll[w];
@@ -708,13 +717,15 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
   // merge-path split of tile tt (which 0: entries before its start; 1: before its end)
   auto split_of = [&](uint64_t tt, int which) -> uint64_t {
     if constexpr (INL) {
-      const uint64_t p = (tt + (uint64_t)which) * TILE;
+      const uint64_t p = (tt + (uint64_t)which) * TV;
       if (which == 1 && p >= npath) return n;
       uint64_t c = 0;   // entries whose span [j + start_j, j + end_j] ends before p
       for (uint32_t j = 0; j < (uint32_t)n; ++j) c += (uint64_t)j + sIl[j] < p;
       return c;
     } else {
-      return tile_split(a.tsplit, tt, which, npath, n);
+      // producer splits every TILE items: this tile's boundaries are every (TV / TILE)-th of them
+      if (which == 0) return a.tsplit[tt * (TV / TILE)];
+      return (tt + 1) * TV >= npath ? n : a.tsplit[(tt + 1) * (TV / TILE)];
     }
   };
   // lane k's entry of a tile's segment-end window (seg_end[a0 - 1 + k]) and row starts (seg_rs[a0 + k])
@@ -738,20 +749,20 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
   constexpr bool kFinal = M == FINAL || M == FINALF || M == FINALD;
   constexpr bool kFast = M == FINALF || M == FINALD;
   constexpr bool kDefer = M == FINALD;
-  int64_t pdv[VT];                 // FINALD: the previous tile's _dst values, pass mask, first row
+  int64_t pdv[V];                 // FINALD: the previous tile's _dst values, pass mask, first row
   uint32_t ppm = 0;
   uint64_t preg = 0;
 #pragma unroll
-  for (int i = 0; i < VT; ++i) pdv[i] = 0;
-  uint32_t pu[VT];                 // MARK: the previous tile's neighbours (flags not yet set)
+  for (int i = 0; i < V; ++i) pdv[i] = 0;
+  uint32_t pu[V];                 // MARK: the previous tile's neighbours (flags not yet set)
 #pragma unroll
-  for (int i = 0; i < VT; ++i) pu[i] = NO_ROW;
+  for (int i = 0; i < V; ++i) pu[i] = NO_ROW;
   int64_t* const* ycols = fp.out_cols;
   // rows of one tile: ballot-ordered positions from `region`, YIELD y = _dst or a constant
   auto store_dst_rows = [&](const int64_t* vdv, uint32_t pm, uint64_t region) {
     uint32_t off = 0;
 #pragma unroll
-    for (int i = 0; i < VT; ++i) {
+    for (int i = 0; i < V; ++i) {
       const bool pass = (pm >> i) & 1u;
       const unsigned long long bal = __ballot(pass);
       if (!bal) continue;
@@ -801,8 +812,8 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
     stage(a0, a1, &e_pre, &r_pre);
   }
   for (; t < ntiles; t += g) {
-    const uint64_t d0 = t * TILE;
-    const uint64_t d1 = (d0 + TILE < npath) ? d0 + TILE : npath;
+    const uint64_t d0 = t * TV;
+    const uint64_t d1 = (d0 + TV < npath) ? d0 + TV : npath;
     const uint64_t b0 = d0 - a0, b1 = d1 - a1;
     const int na = (int)(a1 - a0), nb = (int)(b1 - b0);
 
@@ -830,7 +841,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
 
     // lane-level merge path over this tile: assign a segment to every edge item
     {
-      const int diag = lane * VT;
+      const int diag = lane * V;
       const int dmax = na + nb;
       if (diag < dmax) {
         int lo = diag > nb ? diag - nb : 0;
@@ -842,7 +853,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
         }
         int ai = lo, bi = diag - lo;
 #pragma unroll
-        for (int k = 0; k < VT; ++k) {
+        for (int k = 0; k < V; ++k) {
           if (ai + bi >= dmax) break;
           if (ai < na && (bi >= nb || (uint64_t)A[ai] <= b0 + (uint64_t)bi)) {
             ++ai;
@@ -856,10 +867,10 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
     wave_lds_sync();
     NBG_PH(1)
 
-    if (M == MARKB) {
-      uint32_t u[VT];
+    if constexpr (M == MARKB) {
+      uint32_t u[V];
 #pragma unroll
-      for (int i = 0; i < VT; ++i) {
+      for (int i = 0; i < V; ++i) {
         const int k = i * 64 + lane;
         u[i] = NO_ROW;
         if (k < nb) {
@@ -872,10 +883,10 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
         }
       }
       if (bp.lab) claim_append(u, bp, lane);
-    } else if (M == MARK) {
-      uint32_t u[VT];   // all neighbour loads in flight before the flag stores / claims
+    } else if constexpr (M == MARK) {
+      uint32_t u[V];   // all neighbour loads in flight before the flag stores / claims
 #pragma unroll
-      for (int i = 0; i < VT; ++i) {
+      for (int i = 0; i < V; ++i) {
         const int k = i * 64 + lane;
         u[i] = NO_ROW;
         if (k < nb) {
@@ -888,16 +899,16 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
       } else {
         // the previous tile's flags behind this tile's loads (see FINALD)
 #pragma unroll
-        for (int i = 0; i < VT; ++i) {
+        for (int i = 0; i < V; ++i) {
           if (pu[i] != NO_ROW) flags[pu[i]] = 1;
           pu[i] = u[i];
         }
       }
-    } else if (M == BFS) {
-      uint32_t wv[VT];
+    } else if constexpr (M == BFS) {
+      uint32_t wv[V];
       uint32_t cmask = 0, mmask = 0;
 #pragma unroll
-      for (int i = 0; i < VT; ++i) {
+      for (int i = 0; i < V; ++i) {
         const int k = i * 64 + lane;
         wv[i] = NO_ROW;
         if (k < nb) {
@@ -906,7 +917,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
         }
       }
 #pragma unroll
-      for (int i = 0; i < VT; ++i) {
+      for (int i = 0; i < V; ++i) {
         const uint32_t x = wv[i];
         if (x == NO_ROW) continue;
         if (bp.rlab && bp.rlab[x] != bp.rstamp) continue;
@@ -918,9 +929,9 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
         if (bp.tlab && bp.tlab[x] == bp.tstamp) atomicAdd(bp.found, 1ull);
       }
       // one atomic per wave tile on the list length
-      uint32_t pre[VT], run = 0;
+      uint32_t pre[V], run = 0;
 #pragma unroll
-      for (int i = 0; i < VT; ++i) {
+      for (int i = 0; i < V; ++i) {
         pre[i] = run;
         run += (uint32_t)__popcll(__ballot((cmask >> i) & 1u));
       }
@@ -929,7 +940,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
       base = __shfl(base, 0, 64);
       uint32_t* const region = bp.out + base;
 #pragma unroll
-      for (int i = 0; i < VT; ++i) {
+      for (int i = 0; i < V; ++i) {
         const bool c = (cmask >> i) & 1u;
         const unsigned long long bal = __ballot(c);
         if (c) region[pre[i] + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = wv[i];
@@ -948,20 +959,20 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
       if (bp.dsum && run) {
         unsigned long long ds = 0;
 #pragma unroll
-        for (int i = 0; i < VT; ++i)
+        for (int i = 0; i < V; ++i)
           if ((cmask >> i) & 1u) ds += degree_of(bp.deg, wv[i]);
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) ds += __shfl_down(ds, o, 64);
         if (lane == 0 && ds) atomicAdd(bp.dsum, ds);
       }
     } else {
-      // phase A: WHERE for every item of the tile (VT items per lane, striped)
-      uint32_t jj[VT];      // edge index in the CSR (< 2^32 per type)
-      uint32_t vv[VT];
-      int64_t dv[VT];       // fast path: _dst prefetched with the WHERE column (one round trip)
+      // phase A: WHERE for every item of the tile (V items per lane, striped)
+      uint32_t jj[V];      // edge index in the CSR (< 2^32 per type)
+      uint32_t vv[V];
+      int64_t dv[V];       // fast path: _dst prefetched with the WHERE column (one round trip)
       uint32_t pmask = 0;
 #pragma unroll
-      for (int i = 0; i < VT; ++i) {
+      for (int i = 0; i < V; ++i) {
         const int k = i * 64 + lane;
         jj[i] = 0;
         vv[i] = 0;
@@ -973,35 +984,35 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
       }
       if (kFast) {
         // all loads of the tile in flight at once; the comparison is branch-free
-        int64_t x[VT];
+        int64_t x[V];
 #pragma unroll
-        for (int i = 0; i < VT; ++i) {
+        for (int i = 0; i < V; ++i) {
           const bool act = i * 64 + lane < nb;
           dv[i] = (act && fp.fast.dst_yield) ? NBG_LD_STREAM(a.dst_vid + jj[i]) : 0;
         }
         // the WHERE column at its stored width (narrow copy of an INT column when it fits)
         switch (fp.fast.has_where ? fp.fast.wbytes : 0) {
-          case 1: load_narrow<int8_t>(fp.fast.wcol, jj, nb, lane, x); break;
-          case 2: load_narrow<int16_t>(fp.fast.wcol, jj, nb, lane, x); break;
-          case 4: load_narrow<int32_t>(fp.fast.wcol, jj, nb, lane, x); break;
-          case 8: load_narrow<int64_t>(fp.fast.wcol, jj, nb, lane, x); break;
+          case 1: load_narrow<int8_t, V>(fp.fast.wcol, jj, nb, lane, x); break;
+          case 2: load_narrow<int16_t, V>(fp.fast.wcol, jj, nb, lane, x); break;
+          case 4: load_narrow<int32_t, V>(fp.fast.wcol, jj, nb, lane, x); break;
+          case 8: load_narrow<int64_t, V>(fp.fast.wcol, jj, nb, lane, x); break;
           default:
 #pragma unroll
-            for (int i = 0; i < VT; ++i) x[i] = 0;
+            for (int i = 0; i < V; ++i) x[i] = 0;
         }
         if (kDefer) {   // the previous tile's rows, behind this tile's loads
           store_dst_rows(pdv, ppm, preg);
           ppm = 0;
         }
 #pragma unroll
-        for (int i = 0; i < VT; ++i) {
+        for (int i = 0; i < V; ++i) {
           const bool act = i * 64 + lane < nb;
           const bool in = (x[i] >= fp.fast.lo) & (x[i] <= fp.fast.hi);
           const bool pass = act & (!fp.fast.has_where | (in != (fp.fast.where_neg != 0)));
           pmask |= (uint32_t)pass << i;
         }
       } else {
-        for (int i = 0; i < VT; ++i) {
+        for (int i = 0; i < V; ++i) {
           const int k = i * 64 + lane;
           const bool active = k < nb;
           bool pass = active;
@@ -1028,11 +1039,11 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
         }
       }
       NBG_PH(2)
-      // row offsets in item order: wave-uniform prefix over the VT ballots, then one LDS atomic
+      // row offsets in item order: wave-uniform prefix over the V ballots, then one LDS atomic
       // on the workgroup's cursor (rows go to the workgroup's own region: no global atomics)
       uint32_t run = 0;
 #pragma unroll
-      for (int i = 0; i < VT; ++i) run += (uint32_t)__popcll(__ballot((pmask >> i) & 1u));
+      for (int i = 0; i < V; ++i) run += (uint32_t)__popcll(__ballot((pmask >> i) & 1u));
       unsigned long long base = 0;
       if (lane == 0 && run) base = atomicAdd(&sBase, (unsigned long long)run);
       base = __shfl(base, 0, 64);
@@ -1041,14 +1052,14 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
       const uint64_t region = fp.region_base + (uint64_t)blockIdx.x * fp.blk_cap + base;
       if (kDefer) {   // stored behind the next tile's loads (or after the loop)
 #pragma unroll
-        for (int i = 0; i < VT; ++i) pdv[i] = dv[i];
+        for (int i = 0; i < V; ++i) pdv[i] = dv[i];
         ppm = pmask;
         preg = region;
       }
       int64_t* const* cols = fp.out_cols;   // kernel-argument array
       uint32_t off = 0;                     // rows of the earlier items of this tile
 #pragma unroll
-      for (int i = 0; i < VT && !kDefer; ++i) {
+      for (int i = 0; i < V && !kDefer; ++i) {
         const bool pass = (pmask >> i) & 1u;
         const unsigned long long bal = __ballot(pass);
         if (!bal) continue;
@@ -1089,7 +1100,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
   if (kDefer) store_dst_rows(pdv, ppm, preg);   // the wave's last tile
   if (M == MARK) {
 #pragma unroll
-    for (int i = 0; i < VT; ++i)
+    for (int i = 0; i < V; ++i)
       if (pu[i] != NO_ROW) flags[pu[i]] = 1;
   }
 #ifdef NBG_PHASE_TIMING
@@ -1910,7 +1921,8 @@ static FastProg detect_fast(const TypeProgram& prog, const ExpandArgs& a) {
 unsigned ws_final_grid(uint64_t n_bound, uint64_t e_bound) { return expand_grid(n_bound, e_bound); }
 
 uint64_t ws_final_blk_cap(uint64_t n_bound, uint64_t e_bound) {
-  // a workgroup's waves each take tiles w, w + g, ... (g = grid * WAVES waves)
+  // a workgroup's waves each take tiles w, w + g, ... (g = grid * WAVES waves); a kernel
+  // instantiated with V != VT needs its own tile size here
   const uint64_t tiles = cdiv(n_bound + e_bound + 1, TILE);
   const uint64_t waves = (uint64_t)expand_grid(n_bound, e_bound) * WAVES;
   return cdiv(tiles, waves) * WAVES * TILE;
