@@ -45,10 +45,13 @@ PMC_FILES = {("RMAT-26", 16): os.path.join(ROOT, "profiles", "r02_pmc_hbm_rmat26
 # library kernel id -> instantiations in the rocprof names, first match wins (FINAL: this bench's
 # range WHERE with a _dst YIELD runs k_expand<4> = FINALD; <3> FINALF; <1> the general interpreter;
 # the bool is the inline-start-list variant)
-PMC_NAMES = {"k_expand<MARK>": ["k_expand<0, false>", "k_expand<0, true>"],
-             "k_expand<FINAL>": ["k_expand<4, false>", "k_expand<4, true>", "k_expand<3, false>",
-                                 "k_expand<3, true>", "k_expand<1, false>", "k_expand<1, true>"],
-             "k_expand<BFS>": ["k_expand<2, false>", "k_expand<2, true>"]}
+# (names as rocprofv3 prints them: since k_expand took its items-per-lane parameter the profile
+# names read k_expand<4, false, 4>; summaries written before that read k_expand<4, false>)
+PMC_NAMES = {k: [n for p in v for n in (p[:-1] + ", 4>", p)] for k, v in {
+    "k_expand<MARK>": ["k_expand<0, false>", "k_expand<0, true>"],
+    "k_expand<FINAL>": ["k_expand<4, false>", "k_expand<4, true>", "k_expand<3, false>",
+                        "k_expand<3, true>", "k_expand<1, false>", "k_expand<1, true>"],
+    "k_expand<BFS>": ["k_expand<2, false>", "k_expand<2, true>"]}.items()}
 
 
 def log(*a):
