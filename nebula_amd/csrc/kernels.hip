@@ -1918,13 +1918,24 @@ static FastProg detect_fast(const TypeProgram& prog, const ExpandArgs& a) {
   return f;
 }
 
-unsigned ws_final_grid(uint64_t n_bound, uint64_t e_bound) { return expand_grid(n_bound, e_bound); }
+// The final step's grid: the expansion grid capped at 1920 workgroups (7.5 per CU instead of 8):
+// the room left beside the persistent FINAL workgroups lets the next queries' MARK launches run
+// alongside.  Same-box A/B on RMAT-26 with 6 queries in flight (profiles/r02_t_final_grid_ab.json):
+// 2048 -> 280-282 G edges/s, FINAL 231 us; 1920 -> 289-290, FINAL 226 us; 1792 -> 288-292;
+// 1664 -> 295-298 but FINAL 244 us.  NBG_FINAL_GRID overrides (0 = no cap).
+static unsigned final_grid(uint64_t n_bound, uint64_t e_bound) {
+  static const unsigned cap = getenv("NBG_FINAL_GRID") ? (unsigned)atoi(getenv("NBG_FINAL_GRID")) : 1920u;
+  const unsigned g = expand_grid(n_bound, e_bound);
+  return cap && cap < g ? cap : g;
+}
+
+unsigned ws_final_grid(uint64_t n_bound, uint64_t e_bound) { return final_grid(n_bound, e_bound); }
 
 uint64_t ws_final_blk_cap(uint64_t n_bound, uint64_t e_bound) {
   // a workgroup's waves each take tiles w, w + g, ... (g = grid * WAVES waves); a kernel
   // instantiated with V != VT needs its own tile size here
   const uint64_t tiles = cdiv(n_bound + e_bound + 1, TILE);
-  const uint64_t waves = (uint64_t)expand_grid(n_bound, e_bound) * WAVES;
+  const uint64_t waves = (uint64_t)final_grid(n_bound, e_bound) * WAVES;
   return cdiv(tiles, waves) * WAVES * TILE;
 }
 
@@ -1966,7 +1977,7 @@ hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound,
   bool dst_only = fp.fast.enabled;   // YIELDs are _dst / constants: the deferred-store instantiation
   for (int y = 0; y < fp.nyields; ++y) dst_only = dst_only && (fp.fast.ykind[y] == 0 || fp.fast.ykind[y] == 4);
   hipEvent_t p = prof_begin(w, K_EXPAND_FINAL);
-  const dim3 grid(expand_grid(n_bound, e_bound));
+  const dim3 grid(final_grid(n_bound, e_bound));
   unsigned long long* e_st = &w->q->e_st[step][tix];
   if (inl) {
     if (dst_only)
@@ -1989,7 +2000,7 @@ hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound,
                        fp, BfsParams{}, e_st, L.stat_n, NoInline{});
   }
   prof_end(w, p, K_EXPAND_FINAL, step, tix, (double)edge_columns_read(prog), (double)fp.nyields);
-  w->final_grid[tix] = expand_grid(n_bound, e_bound);
+  w->final_grid[tix] = final_grid(n_bound, e_bound);
   return hipGetLastError();
 }
 
