@@ -1735,6 +1735,13 @@ static unsigned expand_grid(uint64_t n_bound, uint64_t e_bound) {
   return (unsigned)(blocks < EXPAND_GRID ? (blocks ? blocks : 1) : EXPAND_GRID);
 }
 
+// intermediate GO steps' grid (NBG_MARK_GRID caps it, an A/B switch; default: the expansion grid)
+static unsigned mark_grid(uint64_t n_bound, uint64_t e_bound) {
+  static const unsigned cap = getenv("NBG_MARK_GRID") ? (unsigned)atoi(getenv("NBG_MARK_GRID")) : 0u;
+  const unsigned g = expand_grid(n_bound, e_bound);
+  return cap && cap < g ? cap : g;
+}
+
 // The expansion's list is the query's start list, available in inline form.
 static bool inline_start_list(const Workspace* w, int tix, const InlineList* il) {
   return il && !(tix == 0 && w->seg_ready) && w->list_acc == nullptr && w->start_inline;
@@ -1773,11 +1780,11 @@ hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, 
     a.tsplit = nullptr;
     hipEvent_t p = prof_begin(w, K_EXPAND_MARK);
     if (a.bt)
-      hipLaunchKernelGGL((k_expand<MARKB, true>), dim3(expand_grid(il->n, il->total)), dim3(BLOCK), 0, w->stream, a,
+      hipLaunchKernelGGL((k_expand<MARKB, true>), dim3(mark_grid(il->n, il->total)), dim3(BLOCK), 0, w->stream, a,
                          (const unsigned long long*)nullptr, w->seg_end, w->seg_rs, w->flags, FinalParams{},
                          bp, &w->q->e_st[step][tix], &w->q->step_n[step], *il);
     else
-      hipLaunchKernelGGL((k_expand<MARK, true>), dim3(expand_grid(il->n, il->total)), dim3(BLOCK), 0, w->stream, a,
+      hipLaunchKernelGGL((k_expand<MARK, true>), dim3(mark_grid(il->n, il->total)), dim3(BLOCK), 0, w->stream, a,
                          (const unsigned long long*)nullptr, w->seg_end, w->seg_rs, w->flags, FinalParams{},
                          bp, &w->q->e_st[step][tix], &w->q->step_n[step], *il);
     prof_end(w, p, K_EXPAND_MARK, step, tix);
@@ -1790,11 +1797,11 @@ hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, 
   FinalParams fp{};
   hipEvent_t p = prof_begin(w, K_EXPAND_MARK);
   if (a.bt)
-    hipLaunchKernelGGL(k_expand<MARKB>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, L.acc,
+    hipLaunchKernelGGL(k_expand<MARKB>, dim3(mark_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, L.acc,
                        set_end(w, L.set), set_rs(w, L.set), w->flags, fp, bp, &w->q->e_st[step][tix], L.stat_n,
                        NoInline{});
   else
-    hipLaunchKernelGGL(k_expand<MARK>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, L.acc,
+    hipLaunchKernelGGL(k_expand<MARK>, dim3(mark_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, L.acc,
                        set_end(w, L.set), set_rs(w, L.set), w->flags, fp, bp, &w->q->e_st[step][tix], L.stat_n,
                        NoInline{});
   prof_end(w, p, K_EXPAND_MARK, step, tix);
