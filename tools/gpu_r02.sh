@@ -24,14 +24,14 @@ for step in "$@"; do
       for c in FETCH_SIZE WRITE_SIZE; do
         timeout -s KILL 400 rocprofv3 --pmc $c -d "$OUT/pmc${sc}_$c" -o run --output-format csv -- \
           python3 -u bench.py --scale $sc --steps 1 --warmup 1 --sp-pairs 0 --no-cpu-baseline --no-profile \
-          --verify 0 --c2 0 --c5-scale 0 --getbound-reqs 0 > "$OUT/pmc${sc}_$c.json" 2> "$OUT/pmc${sc}_$c.log" \
+          --verify 0 --c2 0 --c5-scale 0 --getbound-reqs 0 --c1-reqs 0 > "$OUT/pmc${sc}_$c.json" 2> "$OUT/pmc${sc}_$c.log" \
           || { tail -30 "$OUT/pmc${sc}_$c.log"; exit 1; }
       done
       python3 tools/pmc_summary.py $(find "$OUT/pmc${sc}_FETCH_SIZE" "$OUT/pmc${sc}_WRITE_SIZE" -name '*counter_collection.csv') \
         > "$OUT/pmc_hbm_rmat${sc}.json" ;;
     prof26)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof26" -o run --output-format csv -- \
-        python3 -u bench.py --sp-pairs 2000 --no-cpu-baseline --verify 0 --c2 0 --c5-scale 0 --getbound-reqs 0 \
+        python3 -u bench.py --sp-pairs 2000 --no-cpu-baseline --verify 0 --c2 0 --c5-scale 0 --getbound-reqs 0 --c1-reqs 0 \
         > "$OUT/bench_prof26.json" 2> "$OUT/bench_prof26.log" || { tail -30 "$OUT/bench_prof26.log"; exit 1; } ;;
     go26|go26flags)
       [ "$step" = go26flags ] && export NBG_MARK_FLAGS=1

@@ -17,13 +17,14 @@ for line in open(bench):
     line = line.strip()
     if line.startswith("{"):
         b = json.loads(line)
-want = {"FINALD k_expand<4,false>": "k_expand<4, false", "k_ch_step": "k_ch_step(", "k_ch_hop": "k_ch_hop(",
-        "k_ch_setup": "k_ch_setup(", "k_expand<MARK> k_expand<0,false>": "k_expand<0, false",
+want = {"FINALD k_expand<4,false>": "k_expand<4, false", "k_ch_step": "::k_ch_step", "k_ch_hop": "::k_ch_hop",
+        "k_ch_setup": "::k_ch_setup", "k_expand<MARK> k_expand<0,false>": "k_expand<0, false",
         "k_expand<MARK> inline k_expand<0,true>": "k_expand<0, true",
-        "k_ch_step_b (batched pairs)": "k_ch_step_b(", "k_ch_hop_b (batched pairs)": "k_ch_hop_b("}
+        "k_ch_step_b (batched pairs)": "::k_ch_step_b", "k_ch_hop_b (batched pairs)": "::k_ch_hop_b"}
 out = {"source": trace.split("/")[-2:], "kernels": {}}
 for label, pat in want.items():
-    idx = [i for i, (_, _, n) in enumerate(iv) if n.endswith(pat) or pat in n]
+    # "::name": that kernel exactly (k_ch_step, not k_ch_step_b); otherwise a name fragment
+    idx = [i for i, (_, _, n) in enumerate(iv) if (n.endswith(pat) if pat.startswith("::") else pat in n)]
     if not idx:
         continue
     dur, solo = [], []
