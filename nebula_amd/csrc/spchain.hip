@@ -747,7 +747,11 @@ struct ChainCtx {
   ChArgs* h_args = nullptr;
   ChArgs cached{};
   bool args_valid = false;
-  unsigned grid = 512;
+  // step launch grid: most levels are a few tiles, so the launch's own cost (workgroups to
+  // dispatch, each reading the state snapshot first) dominates; RMAT-26 10k-pair sweep
+  // (profiles/r02_x_sp_grid_sweep.json): p50 0.159 ms at 512, 0.151 at 256, 0.148 at 128 and 96,
+  // 0.154 at 32.  NBG_SP_GRID overrides.
+  unsigned grid = 128;
   // the query in flight: what has been enqueued
   ChQ q{};
   int steps = 0, hops = 0;
