@@ -44,7 +44,10 @@ constexpr int CH_BLOCK = 256;
 constexpr int CH_WAVES = CH_BLOCK / 64;
 constexpr int CH_VT = 8;                  // merge-path items per lane per tile
 constexpr int CH_TILE = 64 * CH_VT;       // items (entries + edges) per wave tile
-constexpr int CH_HOP_WGS = 64;            // workgroups scanning one greedy hop
+#ifndef NBG_CH_HOP_WGS
+#define NBG_CH_HOP_WGS 64
+#endif
+constexpr int CH_HOP_WGS = NBG_CH_HOP_WGS;   // workgroups scanning one greedy hop
 constexpr int CH_HOP_U = 4;               // neighbours per thread in flight (greedy)
 constexpr int CH_MAXS = 2 * MAX_PATH_LEN + 2;   // step launches of one query, at most
 
@@ -859,9 +862,13 @@ static hipError_t chain_prepare(ChainCtx* c, const SpTypes& fwd, const SpTypes& 
 // chain length for c's query: sized by the recent queries; a longer one gets a continuation
 // batch (chain_more)
 static void chain_length(const ChainCtx* c, int* k, int* h) {
+  // NBG_SP_KPAD / NBG_SP_HPAD: launches added to the sized chain (A/B switches; an empty launch
+  // costs a few us, a continuation a host round trip)
+  static const int kpad = getenv("NBG_SP_KPAD") ? atoi(getenv("NBG_SP_KPAD")) : 0;
+  static const int hpad = getenv("NBG_SP_HPAD") ? atoi(getenv("NBG_SP_HPAD")) : 0;
   const int max_steps = 2 * (int)c->q.upto - 1;
-  *k = std::min(max_steps, std::max(1, (int)std::ceil(c->ema_steps)));
-  *h = std::min((int)c->q.upto, std::max(1, (int)std::ceil(c->ema_hops)));
+  *k = std::min(max_steps, std::max(1, (int)std::ceil(c->ema_steps) + kpad));
+  *h = std::min((int)c->q.upto, std::max(1, (int)std::ceil(c->ema_hops) + hpad));
 }
 
 hipError_t chain_launch(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible,

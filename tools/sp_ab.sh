@@ -1,15 +1,17 @@
 #!/bin/bash
-# Same-box A/B of an SP switch (env var $2, values 0/1 alternating).  Usage: bash tools/sp_ab.sh <tag> <VAR>
+# Same-box A/B of FIND SHORTEST PATH latency on RMAT-26 (10k pairs) across libnbg builds / settings.
+# Usage: bash tools/sp_ab.sh <tag> <spec>...   spec = <lib path>[,VAR=VALUE[,VAR=VALUE]]
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/$1
+OUT=gpurun_out/$1; shift
 mkdir -p "$OUT"
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { tail -20 "$OUT/smoke.log"; exit 1; }
-timeout -k 10 300 python -u -m pytest tests/test_gpu_path.py -x -q --timeout 120 --timeout-method thread > "$OUT/pytest_path.log" 2>&1 \
-  || { tail -20 "$OUT/pytest_path.log"; exit 1; }
-echo "tests done"
-for v in 0 1 0 1; do
-  env "$2=$v" timeout -k 10 300 python -u bench.py --steps 1 --sp-pairs 10000 --no-cpu-baseline --no-profile --c5-scale 0 \
-    > "$OUT/sp_$2_$v.$RANDOM.json" 2>> "$OUT/ab.log" || { tail -20 "$OUT/ab.log"; exit 1; }
-  echo "run $v done"
+for round in 1 2; do
+  for spec in "$@"; do
+    IFS=, read -r lib envs <<< "$spec"
+    n=$(basename "$lib" .so)${envs:+_${envs//[=,]/_}}
+    env NBG_LIB=$PWD/$lib ${envs//,/ } timeout -k 10 300 python -u bench.py --steps 1 --warmup 1 --sp-pairs 10000 \
+      --no-profile --no-cpu-baseline --verify 0 --c2 0 --c5-scale 0 --getbound-reqs 0 --c1-reqs 0 \
+      > "$OUT/${n}_r$round.json" 2>> "$OUT/ab.log" || { tail -20 "$OUT/ab.log"; exit 1; }
+    python3 -c "import json,sys; sp=json.load(open(sys.argv[1]))['find_shortest_path']; print(sys.argv[2], 'p50', round(sp['p50_ms'],4), 'p90', round(sp['p90_ms'],4), 'p99', round(sp['p99_ms'],4), 'mean', round(sp['mean_ms'],4))" "$OUT/${n}_r$round.json" "$n"
+  done
 done
