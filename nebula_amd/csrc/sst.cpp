@@ -33,6 +33,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -106,7 +107,9 @@ inline uint64_t fixed64(const uint8_t* p) {
 bool snappy_decode(const uint8_t* in, size_t n, std::string* out) {
   Cur c{in, in + n};
   uint64_t ulen = 0;
-  if (!c.varint(&ulen) || ulen > ((uint64_t)1 << 32)) return false;
+  // one element (at least 2 bytes, a 1-byte-offset copy) yields at most 64 bytes: a longer claimed
+  // length is a corrupt header (and must not size an allocation)
+  if (!c.varint(&ulen) || ulen > ((uint64_t)1 << 32) || ulen > 32 * (uint64_t)n + 64) return false;
   out->assign(ulen, '\0');
   uint8_t* o = reinterpret_cast<uint8_t*>(&(*out)[0]);
   size_t op = 0;
@@ -313,12 +316,16 @@ void list_sst(const std::string& dir, std::vector<std::string>* out) {
 
 int32_t Engine::ingest_sst(int32_t part, const std::string& path) {
   if (finalized) return fail(NBG_E_STATE, "engine already finalized");
-  Table t;
-  std::vector<uint8_t> kd, vd;
-  std::vector<uint64_t> ko, vo;
-  if (!t.read(path) || !t.records(&kd, &ko, &vd, &vo)) return fail(t.code, path + ": " + t.err);
-  const uint64_t n = ko.size() - 1;
-  return load_part_kv(part, kd.data(), ko.data(), vd.data(), vo.data(), n);
+  try {   // (no exception crosses the C ABI: an allocation failure is a status)
+    Table t;
+    std::vector<uint8_t> kd, vd;
+    std::vector<uint64_t> ko, vo;
+    if (!t.read(path) || !t.records(&kd, &ko, &vd, &vo)) return fail(t.code, path + ": " + t.err);
+    const uint64_t n = ko.size() - 1;
+    return load_part_kv(part, kd.data(), ko.data(), vd.data(), vo.data(), n);
+  } catch (const std::bad_alloc&) {
+    return fail(NBG_E_OUT_OF_MEMORY, path + ": out of host memory");
+  }
 }
 
 // NebulaStore::ingest: every part this engine serves, every *.sst under download/<part>.
