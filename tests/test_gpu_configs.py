@@ -137,6 +137,23 @@ def test_c4_shortest_pairs_rmat26(rmat26, sp_mode):
     assert _check_pairs(eng, csr, pairs) > 20
 
 
+@pytest.mark.timeout(600)
+def test_c4_batched_pairs_rmat26(rmat26):
+    """nbg_find_path_batch at the C4 size: 96 pairs as three device batches of 32 (the bench's
+    throughput pass), every path and edge count equal to the one-at-a-time query's."""
+    src, dst, eng, csr, _, av = rmat26
+    pairs = rmat.pick_pairs(src, dst, 96, 7, verts=av)
+    st = []
+    got = eng.find_path_batch([([s], [t], [1], 5, True) for s, t in pairs], stats=st)
+    found = 0
+    for (s, t), g, edges in zip(pairs, got, st):
+        one = {}
+        assert g == eng.find_path([s], [t], [1], 5, stats=one), (s, t)
+        assert edges == one["edges"], (s, t)
+        found += bool(g)
+    assert found > 30
+
+
 def _c5_graph(k):
     """BASELINE C5's synthetic substitute (bench.py c5_leg) at scale k: knows = RMAT-k over persons,
     likes = a bipartite RMAT-(k-1) from persons to posts (post vids in a disjoint range)."""
