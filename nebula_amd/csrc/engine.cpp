@@ -144,19 +144,18 @@ int32_t materialize_rows(nbg_rows* r) {
     uint64_t len = s.end - s.begin;
     for (int c = 0; c < r->ncols; ++c) {
       VKind k = r->kinds[s.type][c];
+      std::fill(r->tags[c].begin() + (ptrdiff_t)o, r->tags[c].begin() + (ptrdiff_t)(o + len), (uint8_t)k);
+      if (k != VK_STRING) continue;   // payloads are final as copied
       for (uint64_t i = o; i < o + len; ++i) {
-        r->tags[c][i] = (uint8_t)k;
-        if (k == VK_STRING) {
-          int64_t code = r->bits[c][i];
-          auto it = sidx.find(code);
-          if (it == sidx.end()) {
-            std::string txt = (code >= 0 && (code & 1) == 0 && (uint64_t)(code / 2) < dict.size())
-                                  ? dict[code / 2] : r->const_str[s.type][c];
-            it = sidx.emplace(code, (int64_t)r->strings.size()).first;
-            r->strings.push_back(txt);
-          }
-          r->bits[c][i] = it->second;
+        int64_t code = r->bits[c][i];
+        auto it = sidx.find(code);
+        if (it == sidx.end()) {
+          std::string txt = (code >= 0 && (code & 1) == 0 && (uint64_t)(code / 2) < dict.size())
+                                ? dict[code / 2] : r->const_str[s.type][c];
+          it = sidx.emplace(code, (int64_t)r->strings.size()).first;
+          r->strings.push_back(txt);
         }
+        r->bits[c][i] = it->second;
       }
     }
     o += len;

@@ -168,6 +168,10 @@ struct Workspace {
   int64_t* h_gpath = nullptr;               // pinned: path + {cur, err}
   unsigned long long* ar_buf = nullptr;     // ws_allreduce_host scratch (grow-only)
   uint64_t ar_cap = 0;
+  uint64_t* fetch_meta = nullptr;           // ws_fetch_rows staging (grow-only)
+  size_t fetch_meta_cap = 0;
+  int64_t* fetch_out = nullptr;
+  size_t fetch_out_cap = 0;
   unsigned long long* h_gst = nullptr;
 };
 
@@ -1585,7 +1589,8 @@ void ws_destroy(Workspace* w) {
   if (w->h_pgst) (void)hipHostFree(w->h_pgst);
   if (w->done_ev) (void)hipEventDestroy(w->done_ev);
   for (void* p : {(void*)w->sendbits, (void*)w->recvbits, (void*)w->gst, (void*)w->pgst, w->g_part, (void*)w->g_rec,
-                  (void*)w->g_all, (void*)w->g_path, (void*)w->g_cur, (void*)w->ar_buf})
+                  (void*)w->g_all, (void*)w->g_path, (void*)w->g_cur, (void*)w->ar_buf, (void*)w->fetch_meta,
+                  (void*)w->fetch_out})
     if (p) (void)hipFree(p);
   if (w->h_gpath) (void)hipHostFree(w->h_gpath);
   if (w->h_gst) (void)hipHostFree(w->h_gst);
@@ -2225,10 +2230,25 @@ hipError_t ws_fetch_rows(Workspace* w, const std::vector<std::pair<uint64_t, uin
     o += sg.second;
   }
   if (o != total) return hipErrorInvalidValue;
-  uint64_t* d_meta = nullptr;
-  int64_t* d_out = nullptr;
-  hipError_t e = hipMalloc((void**)&d_meta, meta.size() * 8);
-  if (e == hipSuccess) e = hipMalloc((void**)&d_out, total * ncols * 8);
+  // grow-only staging in the workspace (no allocation / free, which would wait for the device, per
+  // fetch)
+  auto grow = [&](void** p, size_t* cap, size_t bytes) -> hipError_t {
+    if (bytes <= *cap) return hipSuccess;
+    if (*p) {
+      hipError_t se = hipStreamSynchronize(w->stream);
+      if (se != hipSuccess) return se;
+      (void)hipFree(*p);
+      *p = nullptr;
+      *cap = 0;
+    }
+    hipError_t ae = hipMalloc(p, bytes);
+    if (ae == hipSuccess) *cap = bytes;
+    return ae;
+  };
+  hipError_t e = grow((void**)&w->fetch_meta, &w->fetch_meta_cap, meta.size() * 8);
+  if (e == hipSuccess) e = grow((void**)&w->fetch_out, &w->fetch_out_cap, total * ncols * 8);
+  uint64_t* d_meta = w->fetch_meta;
+  int64_t* d_out = w->fetch_out;
   if (e == hipSuccess) e = hipMemcpyAsync(d_meta, meta.data(), meta.size() * 8, hipMemcpyHostToDevice, w->stream);
   if (e == hipSuccess) {
     const int nseg = (int)(meta.size() / 3);
@@ -2239,8 +2259,6 @@ hipError_t ws_fetch_rows(Workspace* w, const std::vector<std::pair<uint64_t, uin
   for (int c = 0; e == hipSuccess && c < ncols; ++c)
     e = hipMemcpyAsync(host_cols[c], d_out + (uint64_t)c * total, total * 8, hipMemcpyDeviceToHost, w->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(w->stream);
-  if (d_meta) (void)hipFree(d_meta);
-  if (d_out) (void)hipFree(d_out);
   return e;
 }
 
