@@ -209,8 +209,10 @@ void nbg_go_stmt_free(nbg_go_stmt* stmt);
  * workspace still holds live rows gives it to them and takes a fresh one).  A ticket never
  * waited for is reclaimed by nbg_destroy; tickets must be
  * waited for before their statement is freed.  On a partitioned engine every rank must submit
- * the same queries in the same order (they are collectives); its slots share the engine's stream
- * and communicator, so the device runs them in that order while the host work overlaps. */
+ * the same queries in the same order (they are collectives).  Over RCCL each slot gets its own
+ * communicator (split from the engine's, collectively, at the slot's first use; NBG_SLOT_COMMS=0
+ * keeps one) and stream, so queries of different slots overlap on the device; the in-process
+ * transport's slots share the engine's stream and communicator. */
 typedef struct nbg_go_ticket nbg_go_ticket;
 int32_t nbg_go_submit(nbg_go_stmt* stmt, const int64_t* starts, uint64_t num_starts, int32_t device,
                       nbg_go_ticket** out);
