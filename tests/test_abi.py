@@ -76,3 +76,18 @@ def test_over_all_default_column_order():
     finally:
         e.close()
         o.close()
+
+
+def test_find_path_batch_arguments_without_gpu():
+    """nbg_find_path_batch: an empty batch is a no-op; missing arrays are invalid arguments; every
+    request of a batch on an engine that is not finalized fails with NBG_E_STATE in its own status."""
+    import ctypes as C
+    e = Engine(num_parts=3)
+    e.register_edge(1, "e", [("w", kvgen.INT)])
+    try:
+        assert e.find_path_batch([]) == []
+        assert e.lib.nbg_find_path_batch(e.h, None, 2, None, None) == _lib.E_INVALID_ARGUMENT
+        res = e.find_path_batch([([1], [2], [1], 5, True), ([1], [3], [1], 3, False)])
+        assert [r.code for r in res] == [_lib.E_STATE, _lib.E_STATE]
+    finally:
+        e.close()
