@@ -168,6 +168,7 @@ struct Workspace {
   int64_t* h_gpath = nullptr;               // pinned: path + {cur, err}
   unsigned long long* ar_buf = nullptr;     // ws_allreduce_host scratch (grow-only)
   uint64_t ar_cap = 0;
+  bool hop_bits = false;                    // this hop's MARKs set sendbits directly (no pack)
   uint64_t* fetch_meta = nullptr;           // ws_fetch_rows staging (grow-only)
   size_t fetch_meta_cap = 0;
   int64_t* fetch_out = nullptr;
@@ -560,6 +561,9 @@ struct BfsParams {
   // over nds (the next step's first OVER type); nlist.zero_next is zeroed by workgroup 0
   ListOut nlist;
   DegSrc nds;
+  // MARK on a partitioned engine (non-null): neighbours set their bit of the global id space in
+  // this bitmap (the hop's all-to-all send buffer) instead of a byte flag — no pack pass
+  unsigned long long* bits;
 };
 
 struct FinalParams {
@@ -904,7 +908,10 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
         // the previous tile's flags behind this tile's loads (see FINALD)
 #pragma unroll
         for (int i = 0; i < V; ++i) {
-          if (pu[i] != NO_ROW) flags[pu[i]] = 1;
+          if (pu[i] != NO_ROW) {
+            if (bp.bits) atomicOr(bp.bits + (pu[i] >> 6), 1ull << (pu[i] & 63));
+            else flags[pu[i]] = 1;
+          }
           pu[i] = u[i];
         }
       }
@@ -1105,7 +1112,10 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
   if (M == MARK) {
 #pragma unroll
     for (int i = 0; i < V; ++i)
-      if (pu[i] != NO_ROW) flags[pu[i]] = 1;
+      if (pu[i] != NO_ROW) {
+        if (bp.bits) atomicOr(bp.bits + (pu[i] >> 6), 1ull << (pu[i] & 63));
+        else flags[pu[i]] = 1;
+      }
   }
 #ifdef NBG_PHASE_TIMING
   if (kFinal && threadIdx.x == 0 && blockIdx.x % 256 == 0 && ntiles > 8192)
@@ -1756,6 +1766,12 @@ static DegSrc deg_src(const ExpandArgs* next0) { return next0 ? deg_of(*next0) :
 
 hipError_t ws_compact(Workspace* w, int step, const ExpandArgs* next0);
 
+// NBG_PART_FLAGS=1: partitioned MARK keeps byte flags + k_pack_bits (the A/B baseline)
+static bool bits_off() {
+  static const bool off = getenv("NBG_PART_FLAGS") && atoi(getenv("NBG_PART_FLAGS")) != 0;
+  return off;
+}
+
 hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, uint64_t e_bound, int step, int tix,
                           const InlineList* il, const ExpandArgs* next0) {
   if (step > MAX_STEPS || tix >= MAX_TYPES_Q) return hipErrorInvalidValue;
@@ -1778,6 +1794,12 @@ hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, 
     bp.nds = deg_src(next0);
     bp.nlist = list_out(w, w->frontier[nset], &w->q->acc[2 + (step + 1) % 3],
                         tix == 0 ? &w->q->acc[2 + (step + 2) % 3] : nullptr, nullptr, nset);
+  }
+  // partitioned MARK (not MARKB, whose roots ride with the byte flags): straight into the hop's
+  // send bitmap, which ws_exchange then sends without a pack pass
+  if (w->comm && !a0.bt && !bits_off()) {
+    bp.bits = w->sendbits;
+    w->hop_bits = true;
   }
   if (inline_start_list(w, tix, il)) {   // no k_relist: the list travels in the kernel arguments
     ExpandArgs a = a0;
@@ -2338,6 +2360,7 @@ hipError_t ws_set_partition(Workspace* w, Comm* comm, uint64_t npad) {
   HIP_TRY(hipMalloc((void**)&w->flags, w->flag_bytes));
   HIP_TRY(hipMemsetAsync(w->flags, 0, w->flag_bytes, w->stream));
   HIP_TRY(hipMalloc((void**)&w->sendbits, G * npad / 8));
+  HIP_TRY(hipMemsetAsync(w->sendbits, 0, G * npad / 8, w->stream));   // all-zero between hops
   HIP_TRY(hipMalloc((void**)&w->recvbits, G * npad / 8));
   HIP_TRY(hipMalloc((void**)&w->gst, GST_N * sizeof(unsigned long long)));
   HIP_TRY(hipHostMalloc((void**)&w->h_gst, GST_N * sizeof(unsigned long long), hipHostMallocDefault));
@@ -2352,14 +2375,20 @@ hipError_t ws_exchange(Workspace* w, int step, const ExpandArgs* next0) {
   if (!w->comm) return hipErrorInvalidValue;
   const uint64_t G = (uint64_t)w->comm->world;
   const uint64_t nwords = G * w->npad / 64, seg_words = w->npad / 64, nb = w->npad / BITS_BLOCK;
-  hipEvent_t p = prof_begin(w, K_PACK);
-  hipLaunchKernelGGL(k_pack_bits, dim3((unsigned)cdiv(nwords, BLOCK)), dim3(BLOCK), 0, w->stream, w->flags, nwords,
-                     w->sendbits);
-  prof_end(w, p, K_PACK, step, 0, (double)(G * w->npad) + (double)(G * w->npad / 8));
-  HIP_TRY(hipGetLastError());
+  hipEvent_t p = nullptr;
+  if (!w->hop_bits) {   // byte flags (MARKB): pack them into the send bitmap
+    p = prof_begin(w, K_PACK);
+    hipLaunchKernelGGL(k_pack_bits, dim3((unsigned)cdiv(nwords, BLOCK)), dim3(BLOCK), 0, w->stream, w->flags, nwords,
+                       w->sendbits);
+    prof_end(w, p, K_PACK, step, 0, (double)(G * w->npad) + (double)(G * w->npad / 8));
+    HIP_TRY(hipGetLastError());
+  }
+  w->hop_bits = false;
   p = prof_begin(w, K_ALLTOALL);
   if (w->comm->alltoall(w->sendbits, w->recvbits, w->npad / 8, w->stream)) return hipErrorUnknown;
   prof_end(w, p, K_ALLTOALL, step, 0, (double)((G - 1) * w->npad / 8));
+  // the send bitmap is all-zero between hops (the next hop's MARKs OR into it)
+  HIP_TRY(hipMemsetAsync(w->sendbits, 0, G * w->npad / 8, w->stream));
   if (w->bt_active && w->comm->alltoall(w->bt_out, w->bt_recv, w->npad * 8, w->stream)) return hipErrorUnknown;
   unsigned long long* acc = &w->q->acc[2 + w->pc];
   unsigned long long* other = &w->q->acc[2 + (w->pc ^ 1)];
@@ -3104,6 +3133,7 @@ hipError_t ws_path_level_part(Workspace* w, const PathTypes& pt, int src, uint64
   prof_end_p(w, p, K_PACK, rec);
   HIP_TRY(hipGetLastError());
   if (w->comm->alltoall(w->sendbits, w->recvbits, w->npad / 8, w->stream)) return hipErrorUnknown;
+  HIP_TRY(hipMemsetAsync(w->sendbits, 0, G * w->npad / 8, w->stream));   // all-zero between hops (GO ORs into it)
   ClaimParams cp{};
   cp.lab = w->lab[lv.lab];
   cp.stamp = lv.stamp;
