@@ -3119,19 +3119,24 @@ hipError_t ws_path_level_part(Workspace* w, const PathTypes& pt, int src, uint64
     prof_end_p(w, p, K_RELIST, rec);
     a.frontier = w->rlist;
     a.tsplit = w->tsplit;
+    BfsParams mb{};
+    if (!bits_off()) mb.bits = w->sendbits;   // the level's candidates straight into the send bitmap
     p = prof_begin_p(w, K_EXPAND_MARK);
     hipLaunchKernelGGL(k_expand<MARK>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, acc,
-                       w->seg_end, w->seg_rs, w->flags, FinalParams{}, BfsParams{}, &w->ps->le[rec],
+                       w->seg_end, w->seg_rs, w->flags, FinalParams{}, mb, &w->ps->le[rec],
                        (unsigned long long*)nullptr, NoInline{});
     prof_end_p(w, p, K_EXPAND_MARK, rec);
   }
   const uint64_t G = (uint64_t)w->comm->world;
   const uint64_t nwords = G * w->npad / 64, seg_words = w->npad / 64, nb = w->npad / BITS_BLOCK;
-  hipEvent_t p = prof_begin_p(w, K_PACK);
-  hipLaunchKernelGGL(k_pack_bits, dim3((unsigned)cdiv(nwords, BLOCK)), dim3(BLOCK), 0, w->stream, w->flags, nwords,
-                     w->sendbits);
-  prof_end_p(w, p, K_PACK, rec);
-  HIP_TRY(hipGetLastError());
+  hipEvent_t p = nullptr;
+  if (bits_off()) {
+    p = prof_begin_p(w, K_PACK);
+    hipLaunchKernelGGL(k_pack_bits, dim3((unsigned)cdiv(nwords, BLOCK)), dim3(BLOCK), 0, w->stream, w->flags, nwords,
+                       w->sendbits);
+    prof_end_p(w, p, K_PACK, rec);
+    HIP_TRY(hipGetLastError());
+  }
   if (w->comm->alltoall(w->sendbits, w->recvbits, w->npad / 8, w->stream)) return hipErrorUnknown;
   HIP_TRY(hipMemsetAsync(w->sendbits, 0, G * w->npad / 8, w->stream));   // all-zero between hops (GO ORs into it)
   ClaimParams cp{};
