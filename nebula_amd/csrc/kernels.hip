@@ -564,6 +564,12 @@ struct BfsParams {
   // MARK on a partitioned engine (non-null): neighbours set their bit of the global id space in
   // this bitmap (the hop's all-to-all send buffer) instead of a byte flag — no pack pass
   unsigned long long* bits;
+  // ... or, for a level whose edge total is small (non-null): the neighbour of edge e (its
+  // position in the list's edge space) goes to slot e of its owner's segment, as the owner's
+  // local id — sparse[owner * sp_stride + e]; slots start as NO_ROW.  No atomics.
+  uint32_t* sparse;
+  uint32_t sp_stride;
+  uint32_t sp_npad;
 };
 
 struct FinalParams {
@@ -904,6 +910,13 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
       }
       if (bp.lab) {
         claim_append(u, bp, lane);
+      } else if (bp.sparse) {
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          if (u[i] == NO_ROW) continue;
+          const uint32_t q = u[i] / bp.sp_npad;
+          bp.sparse[(uint64_t)q * bp.sp_stride + b0 + (uint64_t)(i * 64 + lane)] = u[i] - q * bp.sp_npad;
+        }
       } else {
         // the previous tile's flags behind this tile's loads (see FINALD)
 #pragma unroll
@@ -1765,6 +1778,12 @@ static bool inline_start_list(const Workspace* w, int tix, const InlineList* il)
 static DegSrc deg_src(const ExpandArgs* next0) { return next0 ? deg_of(*next0) : DegSrc{}; }
 
 hipError_t ws_compact(Workspace* w, int step, const ExpandArgs* next0);
+
+// NBG_PART_SPARSE=0: partitioned FIND PATH levels always exchange bitmaps (the A/B baseline)
+static bool sparse_on() {
+  static const bool on = !(getenv("NBG_PART_SPARSE") && atoi(getenv("NBG_PART_SPARSE")) == 0);
+  return on;
+}
 
 // NBG_PART_FLAGS=1: partitioned MARK keeps byte flags + k_pack_bits (the A/B baseline)
 static bool bits_off() {
@@ -2979,6 +2998,32 @@ __global__ void __launch_bounds__(BLOCK) k_bits_claim(const unsigned long long* 
   }
 }
 
+// The owner's claim over the sparse exchange: recv = world segments of `stride` slots (local ids
+// or NO_ROW; a vertex may arrive several times, so the claim is a CAS on its label).
+__global__ void __launch_bounds__(BLOCK) k_list_claim(const uint32_t* __restrict__ recv, uint64_t slots, ClaimParams cp) {
+  const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const uint32_t v = i < slots ? recv[i] : NO_ROW;
+  bool claimed = false, met = false;
+  if (v != NO_ROW && !(cp.rlab && cp.rlab[v] != cp.rstamp)) {
+    const uint32_t old = cp.lab[v];
+    if ((old >> LVL_BITS) != cp.epoch && atomicCAS(cp.lab + v, old, cp.stamp) == old) {
+      claimed = true;
+      met = cp.mlab && (cp.mlab[v] >> LVL_BITS) == cp.mepoch;
+      if (cp.tlab && cp.tlab[v] == cp.tstamp) atomicAdd(cp.found, 1ull);
+    }
+  }
+  const uint32_t pos = block_append(claimed ? 1u : 0u, cp.out_n);
+  if (claimed) cp.out[pos] = v;
+  if (cp.meet_list) {
+    __syncthreads();   // block_append's shared scratch is reused
+    const uint32_t mp = block_append(met ? 1u : 0u, cp.meet_n);
+    if (met) {
+      cp.meet_list[mp] = v;
+      cp.mout[v] = cp.mstamp;
+    }
+  }
+}
+
 // Greedy reconstruction, one hop of a partitioned engine: among this rank's vertices u in the
 // next B-set, the minimum (type, rank, vid) in-edge u <- v (the out-edge v -> u) from the current
 // vertex v (global id); per-block minima, then one block reduces them to this rank's candidate.
@@ -3016,14 +3061,23 @@ __global__ void __launch_bounds__(BLOCK) k_greedy_part(GreedyPart g) {
     if (g.vp[1]) g.nv = 0;   // an earlier hop failed: no candidates
     g.v = (uint32_t)g.vp[0];
   }
-  for (uint64_t u = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; u < g.nv; u += (uint64_t)gridDim.x * BLOCK) {
-    if (!part_valid(g, (uint32_t)u)) continue;
-    for (int t = 0; t < g.ntypes; ++t) {
-      const uint32_t rs = g.row_ptr[t][u], re = g.row_ptr[t][u + 1];
-      for (uint32_t j = rs; j < re; ++j) {
-        if (g.col[t][j] != g.v) continue;
-        Cand x{(int64_t)g.type[t], g.rank[t] ? g.rank[t][j] : 0, g.vids[u], (uint32_t)u};
-        if (cand_less(x, best)) best = x;
+  // a wave tests 64 consecutive vertices, then scans each B-set member's in-edge row together
+  // (lane-strided, coalesced): a hub's row is not left to one thread
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (uint64_t base = ((uint64_t)blockIdx.x * WAVES + w) * 64; base < g.nv; base += (uint64_t)gridDim.x * BLOCK) {
+    const uint64_t mine = base + lane;
+    unsigned long long m = __ballot(mine < g.nv && part_valid(g, (uint32_t)mine));
+    while (m) {
+      const uint32_t u = (uint32_t)(base + __builtin_ctzll(m));
+      m &= m - 1;
+      const int64_t uvid = g.vids[u];
+      for (int t = 0; t < g.ntypes; ++t) {
+        const uint32_t rs = g.row_ptr[t][u], re = g.row_ptr[t][u + 1];
+        for (uint32_t j = rs + lane; j < re; j += 64) {
+          if (g.col[t][j] != g.v) continue;
+          Cand x{(int64_t)g.type[t], g.rank[t] ? g.rank[t][j] : 0, uvid, u};
+          if (cand_less(x, best)) best = x;
+        }
       }
     }
   }
@@ -3032,7 +3086,6 @@ __global__ void __launch_bounds__(BLOCK) k_greedy_part(GreedyPart g) {
     Cand x = shfl_cand(best, o);
     if (cand_less(x, best)) best = x;
   }
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (lane == 0) lds[w] = best;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -3054,11 +3107,16 @@ __device__ __forceinline__ void put_record(const Cand& b, uint32_t gbase, const 
 
 __global__ void k_greedy_part_reduce(const Cand* __restrict__ part, int nparts, uint32_t gbase,
                                      const uint8_t* __restrict__ visible, int64_t* out) {
-  if (threadIdx.x != 0) return;
+  // one wave (launched with 64 threads): lane-strided minima, then a wave reduction
   Cand b{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
-  for (int k = 0; k < nparts; ++k)
+  for (int k = threadIdx.x; k < nparts; k += 64)
     if (cand_less(part[k], b)) b = part[k];
-  put_record(b, gbase, visible, out);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Cand x = shfl_cand(b, o);
+    if (cand_less(x, b)) b = x;
+  }
+  if (threadIdx.x == 0) put_record(b, gbase, visible, out);
 }
 
 // Minimum vid among a list's entries (B[0] of the greedy) as a rank record (type = rank = 0).
@@ -3101,11 +3159,27 @@ __global__ void k_greedy_pick(const int64_t* __restrict__ all, int G, int pos, i
   cur[0] = (unsigned long long)b[3];
 }
 
+// the greedy's start when it is known on every rank
+__global__ void k_greedy_v0(int64_t vid, unsigned long long gid, int64_t* __restrict__ path,
+                            unsigned long long* __restrict__ cur) {
+  if (threadIdx.x != 0) return;
+  path[0] = vid;
+  cur[0] = gid;
+  cur[1] = 0;
+}
+
 hipError_t ws_path_level_part(Workspace* w, const PathTypes& pt, int src, uint64_t n_bound, uint64_t e_bound, int dst,
                               const PathLevel& lv) {
   if (!w->comm) return hipErrorInvalidValue;
   const int rec = w->rec < PATH_REC ? w->rec++ : PATH_REC - 1;
+  const uint64_t G = (uint64_t)w->comm->world;
+  // exchange format: a level of one OVER type whose edge total (e_bound: the frontier's degree
+  // sum over every rank, so a bound on each rank's edges) is small sends per-owner slot arrays
+  // of e_bound ids instead of the npad-bit bitmap segments — the same choice on every rank
+  const uint64_t stride = (e_bound + 63) / 64 * 64;
+  const bool sparse = pt.n == 1 && e_bound && stride * 4 * 2 <= w->npad / 8 && !bits_off() && sparse_on();
   HIP_TRY(hipMemsetAsync(&w->ps->n[dst], 0, sizeof(unsigned long long), w->stream));
+  if (sparse) HIP_TRY(hipMemsetAsync(w->sendbits, 0xFF, G * stride * 4, w->stream));
   for (int t = 0; t < pt.n; ++t) {
     ExpandArgs a = pt.a[t];
     unsigned long long* acc = &w->ps->acc[w->ppr];
@@ -3120,14 +3194,19 @@ hipError_t ws_path_level_part(Workspace* w, const PathTypes& pt, int src, uint64
     a.frontier = w->rlist;
     a.tsplit = w->tsplit;
     BfsParams mb{};
-    if (!bits_off()) mb.bits = w->sendbits;   // the level's candidates straight into the send bitmap
+    if (sparse) {
+      mb.sparse = reinterpret_cast<uint32_t*>(w->sendbits);
+      mb.sp_stride = (uint32_t)stride;
+      mb.sp_npad = (uint32_t)w->npad;
+    } else if (!bits_off()) {
+      mb.bits = w->sendbits;   // the level's candidates straight into the send bitmap
+    }
     p = prof_begin_p(w, K_EXPAND_MARK);
     hipLaunchKernelGGL(k_expand<MARK>, dim3(expand_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, acc,
                        w->seg_end, w->seg_rs, w->flags, FinalParams{}, mb, &w->ps->le[rec],
                        (unsigned long long*)nullptr, NoInline{});
     prof_end_p(w, p, K_EXPAND_MARK, rec);
   }
-  const uint64_t G = (uint64_t)w->comm->world;
   const uint64_t nwords = G * w->npad / 64, seg_words = w->npad / 64, nb = w->npad / BITS_BLOCK;
   hipEvent_t p = nullptr;
   if (bits_off()) {
@@ -3137,8 +3216,9 @@ hipError_t ws_path_level_part(Workspace* w, const PathTypes& pt, int src, uint64
     prof_end_p(w, p, K_PACK, rec);
     HIP_TRY(hipGetLastError());
   }
-  if (w->comm->alltoall(w->sendbits, w->recvbits, w->npad / 8, w->stream)) return hipErrorUnknown;
-  HIP_TRY(hipMemsetAsync(w->sendbits, 0, G * w->npad / 8, w->stream));   // all-zero between hops (GO ORs into it)
+  const uint64_t xbytes = sparse ? stride * 4 : w->npad / 8;   // per peer
+  if (w->comm->alltoall(w->sendbits, w->recvbits, xbytes, w->stream)) return hipErrorUnknown;
+  HIP_TRY(hipMemsetAsync(w->sendbits, 0, G * xbytes, w->stream));   // all-zero between hops (GO ORs into it)
   ClaimParams cp{};
   cp.lab = w->lab[lv.lab];
   cp.stamp = lv.stamp;
@@ -3156,8 +3236,12 @@ hipError_t ws_path_level_part(Workspace* w, const PathTypes& pt, int src, uint64
   cp.out = w->slot[dst];
   cp.out_n = &w->ps->n[dst];
   p = prof_begin_p(w, K_BITS_COMPACT);
-  hipLaunchKernelGGL(k_bits_claim, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->recvbits, (int)G, seg_words,
-                     w->nv, cp);
+  if (sparse)
+    hipLaunchKernelGGL(k_list_claim, dim3((unsigned)cdiv(G * stride, BLOCK)), dim3(BLOCK), 0, w->stream,
+                       reinterpret_cast<const uint32_t*>(w->recvbits), G * stride, cp);
+  else
+    hipLaunchKernelGGL(k_bits_claim, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->recvbits, (int)G, seg_words,
+                       w->nv, cp);
   prof_end_p(w, p, K_BITS_COMPACT, rec);
   return hipGetLastError();
 }
@@ -3244,13 +3328,19 @@ hipError_t ws_path_greedy_part(Workspace* w, const PathTypes& bwd, const PathGre
     HIP_TRY(hipHostMalloc((void**)&w->h_gpath, (3 + 3 * (size_t)MAX_PATH_LEN) * 8, hipHostMallocDefault));
   }
   Cand* d_part = static_cast<Cand*>(w->g_part);
-  HIP_TRY(hipMemsetAsync(w->g_cur, 0, 2 * 8, w->stream));
-  // v0: the smallest vid of B[0]
-  hipLaunchKernelGGL(k_min_vid, dim3(1), dim3(64), 0, w->stream, w->slot[pg.start_slot], &w->ps->n[pg.start_slot],
-                     vids, gbase, visible, w->g_rec);
-  HIP_TRY(hipGetLastError());
-  if (w->comm->allgather(w->g_rec, w->g_all, GREC * 8, w->stream)) return hipErrorUnknown;
-  hipLaunchKernelGGL(k_greedy_pick, dim3(1), dim3(64), 0, w->stream, w->g_all, G, 0, pg.L, w->g_path, w->g_cur);
+  if (pg.v0_gid >= 0) {
+    // v0 known on every rank (one source): no exchange
+    hipLaunchKernelGGL(k_greedy_v0, dim3(1), dim3(64), 0, w->stream, pg.v0_vid, (unsigned long long)pg.v0_gid,
+                       w->g_path, w->g_cur);
+  } else {
+    HIP_TRY(hipMemsetAsync(w->g_cur, 0, 2 * 8, w->stream));
+    // v0: the smallest vid of B[0]
+    hipLaunchKernelGGL(k_min_vid, dim3(1), dim3(64), 0, w->stream, w->slot[pg.start_slot], &w->ps->n[pg.start_slot],
+                       vids, gbase, visible, w->g_rec);
+    HIP_TRY(hipGetLastError());
+    if (w->comm->allgather(w->g_rec, w->g_all, GREC * 8, w->stream)) return hipErrorUnknown;
+    hipLaunchKernelGGL(k_greedy_pick, dim3(1), dim3(64), 0, w->stream, w->g_all, G, 0, pg.L, w->g_path, w->g_cur);
+  }
   HIP_TRY(hipGetLastError());
   GreedyPart g{};
   g.ntypes = bwd.n;

@@ -524,6 +524,8 @@ struct PathGreedy {
   int L, kf;
   uint32_t em, eb;         // epochs of LAB_M (positions <= kf) and LAB_B (positions > kf)
   int start_slot;          // B[0] candidates (minimum dense id starts the path)
+  int64_t v0_gid = -1;     // partitioned, B[0] = {one source}: its global id and vid (no exchange)
+  int64_t v0_vid = 0;
 };
 hipError_t ws_path_greedy(Workspace* w, const PathTypes& out_types, const PathGreedy& g);
 int ws_path_last_rec(Workspace* w);                              // PState record of the last launch

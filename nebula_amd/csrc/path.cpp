@@ -34,7 +34,9 @@
 // sees exactly the reverse of the from-side; with a non-default max_edge_returned_per_vertex the
 // two caps differ and the device path reports NBG_E_UNSUPPORTED.
 #include <algorithm>
+#include <chrono>
 #include <climits>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -73,6 +75,7 @@ hipError_t level(PathCtx& c, const PathTypes& pt, int src, uint64_t n_bound, uin
 // and, bidirectionally, its direction).  Single engine: summed by the level's k_expand<BFS> into
 // PState.ld[rec]; partitioned: a collective k_degsum into PState.dsum[side].  *rec = the level's
 // PState record.
+// out_bound: a bound on the output list's length for the partitioned degree sum (0: e_bound).
 hipError_t level_ds(PathCtx& c, const PathTypes& pt, int src, uint64_t n_bound, uint64_t e_bound, int dst,
                     PathLevel lv, int side, int* rec) {
   if (!c.part) lv.deg = &pt;
@@ -160,14 +163,34 @@ int32_t greedy_path(PathCtx& c, const PathGreedy& g, std::vector<int64_t>* path)
   return NBG_OK;
 }
 
-// s, t: local ids (NO_ROW on a rank that does not own them)
-int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_paths* out) {
+// s, t: local ids (NO_ROW on a rank that does not own them); partitioned: s_gid / s_vid = the
+// source's global id and vid on every rank (the greedy's v0 without an exchange), deg = deg(s),
+// deg(t) over ranks when known (null: a set-up exchange)
+int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_paths* out, int64_t s_gid = -1,
+                      int64_t s_vid = 0, const unsigned long long* deg = nullptr) {
   Workspace* ws = c.ws;
   const uint32_t ef = ws_path_epoch(ws, LAB_F), eb = ws_path_epoch(ws, LAB_B), em = ws_path_epoch(ws, LAB_M);
   hipError_t he = hipSuccess;
   auto T = [&](hipError_t e) { if (he == hipSuccess) he = e; };
   PState ps;
   uint64_t dsf = 0, dsb = 0;
+  // NBG_PATH_TRACE=1: one stderr line per pair with the host-side phase times (microseconds)
+  static const bool trace = getenv("NBG_PATH_TRACE") != nullptr;
+  std::string tr;
+  auto t_last = std::chrono::steady_clock::now();
+  auto mark = [&](const char* what) {
+    if (!trace) return;
+    const auto now = std::chrono::steady_clock::now();
+    tr += std::string(" ") + what + "=" +
+          std::to_string(std::chrono::duration_cast<std::chrono::microseconds>(now - t_last).count());
+    t_last = now;
+  };
+  struct Flush {
+    const std::string& s;
+    ~Flush() {
+      if (trace && !s.empty()) fprintf(stderr, "nbg path trace:%s\n", s.c_str());
+    }
+  } flush{tr};
   if (!c.part) {
     // the first level's bounds and direction come from the host copy of the CSR offsets, so the
     // set-up needs no round trip; an endpoint without edges has no path at all
@@ -183,13 +206,22 @@ int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_pat
     T(upload1(ws, S_START, s));
     T(ws_path_stamp(ws, S_F0, 1, LAB_F, stamp(ef, 0)));
     T(ws_path_stamp(ws, S_B0, 1, LAB_B, stamp(eb, 0)));
-    T(ws_path_degsum(ws, S_F0, 1, c.fwd, 0));
-    T(ws_path_degsum(ws, S_B0, 1, c.bwd, 1));
-    T(sync(c, &ps));
-    if (he != hipSuccess) return dev_fail(c.E, he, "path setup");
-    dsf = ps.dsum[0];
-    dsb = ps.dsum[1];
+    if (deg) {
+      // deg(s), deg(t) came with the request's presence exchange: no set-up round trip
+      if (he != hipSuccess) return dev_fail(c.E, he, "path setup");
+      dsf = deg[0];
+      dsb = deg[1];
+      if (!dsf || !dsb) return NBG_OK;
+    } else {
+      T(ws_path_degsum(ws, S_F0, 1, c.fwd, 0));
+      T(ws_path_degsum(ws, S_B0, 1, c.bwd, 1));
+      T(sync(c, &ps));
+      if (he != hipSuccess) return dev_fail(c.E, he, "path setup");
+      dsf = ps.dsum[0];
+      dsb = ps.dsum[1];
+    }
   }
+  mark("setup");
   int fcur = S_F0, bcur = S_B0, kf = 0, kb = 0;
   uint64_t nf = 1, nbk = 1;
   std::vector<uint64_t> fn(1, 1);   // forward level sizes
@@ -216,7 +248,9 @@ int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_pat
       bcur ^= 1;
       ++kb;
     }
+    mark(forward ? "fwd_enq" : "bwd_enq");
     T(sync(c, &ps));
+    mark("sync");
     if (he != hipSuccess) return dev_fail(c.E, he, "path level");
     if (rec >= 0 && rec < PATH_REC) c.edges += ps.le[rec];
     nf = ps.n[fcur];
@@ -238,9 +272,13 @@ int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_pat
     T(bsets(c, S_MEET, ps.n[S_MEET], kf, 1, ef, em, 0, fn, &slot));
   }
   if (he != hipSuccess) return dev_fail(c.E, he, "path B-sets");
+  mark("bsets_enq");
   PathGreedy g{L, kf, em, eb, start_slot};
+  g.v0_gid = s_gid;   // B[0] = {s}
+  g.v0_vid = s_vid;
   std::vector<int64_t> p;
   int32_t rc = greedy_path(c, g, &p);
+  mark("greedy");
   if (rc) return rc;
   out->paths.push_back(std::move(p));
   return NBG_OK;
@@ -460,10 +498,35 @@ int32_t find_path_locked(Engine& E, const nbg_path_request* rq, nbg_paths** out,
   std::vector<uint32_t> fd(fv.size()), td(tv.size());
   for (size_t i = 0; i < fv.size(); ++i) fd[i] = E.dense(fv[i]);
   for (size_t i = 0; i < tv.size(); ++i) td[i] = E.dense(tv[i]);
-  // presence per from / to id, then: rank has OVER out-edges, rank lacks an OVER type's in-edges
-  std::vector<unsigned long long> pres(fv.size() + tv.size() + 2, 0);
-  for (size_t i = 0; i < fv.size(); ++i) pres[i] = fd[i] != NO_ROW;
-  for (size_t i = 0; i < tv.size(); ++i) pres[fv.size() + i] = td[i] != NO_ROW;
+  // presence per from / to id, then: rank has OVER out-edges, rank lacks an OVER type's in-edges.
+  // Partitioned, a present id's entry is its global id + 1 (owner * npad + local id + 1; only the
+  // owner contributes), so the sum also tells every rank where each endpoint lives.  Next: the
+  // OVER out-degree of the first source and in-degree of the first target (a pair's first
+  // direction, summed like the rest: no set-up exchange later).
+  std::vector<unsigned long long> pres(fv.size() + tv.size() + 4, 0);
+  const size_t P_DEG = fv.size() + tv.size();
+  const bool partd = E.partitioned();
+  auto presence = [&](uint32_t d) -> unsigned long long {
+    if (d == NO_ROW) return 0;
+    return partd ? (unsigned long long)E.cfg.rank * E.npad + d + 1 : 1;
+  };
+  for (size_t i = 0; i < fv.size(); ++i) pres[i] = presence(fd[i]);
+  for (size_t i = 0; i < tv.size(); ++i) pres[fv.size() + i] = presence(td[i]);
+  auto degree = [&](uint32_t v, int sign) {   // as host_degree over the OVER types (uncapped)
+    unsigned long long sum = 0;
+    if (v == NO_ROW || (!E.snap.h_visible.empty() && !E.snap.h_visible[v])) return sum;
+    for (int32_t t : over) {
+      auto it = E.snap.types.find(sign * t);
+      if (it == E.snap.types.end() || it->second.h_row_ptr.size() <= (size_t)v + 1) continue;
+      sum += it->second.h_row_ptr[v + 1] - it->second.h_row_ptr[v];
+    }
+    return sum;
+  };
+  const bool one_one = fv.size() == 1 && tv.size() == 1;
+  if (one_one) {
+    pres[P_DEG] = degree(fd[0], 1);
+    pres[P_DEG + 1] = degree(td[0], -1);
+  }
   for (int32_t t : over) {
     const bool out_edges = E.snap.types.count(t) > 0, in_edges = E.snap.types.count(-t) > 0;
     if (out_edges) pres[pres.size() - 2] = 1;
@@ -479,9 +542,11 @@ int32_t find_path_locked(Engine& E, const nbg_path_request* rq, nbg_paths** out,
   }
   std::vector<uint32_t> S, Tg;        // local sources; targets by global position (NO_ROW: not here)
   std::vector<int64_t> Sv, Tv;        // their vids
+  std::vector<uint32_t> Sgid;         // partitioned: every source's global id
   for (size_t i = 0; i < fv.size(); ++i)
     if (pres[i]) {
       Sv.push_back(fv[i]);
+      if (partd) Sgid.push_back((uint32_t)(pres[i] - 1));
       if (fd[i] != NO_ROW) S.push_back(fd[i]);
     }
   for (size_t i = 0; i < tv.size(); ++i)
@@ -545,24 +610,13 @@ int32_t find_path_locked(Engine& E, const nbg_path_request* rq, nbg_paths** out,
     std::vector<uint32_t> Tl;
     for (uint32_t d : Tg)
       if (d != NO_ROW) Tl.push_back(d);
-    // partitioned: every source's global id (owner * npad + its local id), summed over ranks
-    std::vector<uint32_t> Sgid;
+    // partitioned: every source's global id (from the presence exchange) and vid
     std::vector<int64_t> Svid;
-    if (c.part) {
-      std::vector<unsigned long long> g(fv.size(), 0);
-      for (size_t i = 0; i < fv.size(); ++i)
-        if (pres[i] && fd[i] != NO_ROW) g[i] = (unsigned long long)E.cfg.rank * E.npad + fd[i] + 1;
-      he = ws_allreduce_host(E.ws, g);
-      if (he != hipSuccess) { delete res; return dev_fail(E, he, "path source exchange"); }
-      for (size_t i = 0; i < fv.size(); ++i)
-        if (g[i]) {
-          Sgid.push_back((uint32_t)(g[i] - 1));
-          Svid.push_back(fv[i]);
-        }
-    }
+    if (c.part) Svid = Sv;
     rc = all_paths(c, S, Tl, rq->upto, Sgid, Svid, res);
   } else if (pair)
-    rc = bidirectional(c, S.empty() ? NO_ROW : S[0], Tg[0], rq->upto, res);
+    rc = bidirectional(c, S.empty() ? NO_ROW : S[0], Tg[0], rq->upto, res, c.part ? (int64_t)Sgid[0] : -1, Sv[0],
+                       c.part && one_one ? &pres[P_DEG] : nullptr);
   else
     rc = one_sided(c, S, Tg, Sv.size(), rq->upto, res);
   if (rc) { delete res; return rc; }
@@ -664,7 +718,14 @@ int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* rq, nbg_paths** out
   *out = nullptr;
   Engine& E = h->e;
   std::lock_guard<std::mutex> lg(E.mu);
-  return find_path_locked(E, rq, out, nullptr);
+  static const bool trace = getenv("NBG_PATH_TRACE") != nullptr;
+  if (!trace) return find_path_locked(E, rq, out, nullptr);
+  const auto t0 = std::chrono::steady_clock::now();
+  const int32_t rc = find_path_locked(E, rq, out, nullptr);
+  fprintf(stderr, "nbg path total=%lld\n",
+          (long long)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0)
+              .count());
+  return rc;
 }
 
 int32_t nbg_find_path_submit(nbg_engine* h, const nbg_path_request* rq, nbg_path_ticket** out) {
