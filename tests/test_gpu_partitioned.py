@@ -151,6 +151,33 @@ def test_partitioned_shortest_single_pairs(rmat11, world):
     assert found > 0
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_partitioned_shortest_sparse_and_bitmap_levels(world):
+    """RMAT-16: a level whose edge total is at most 1/16 of a bitmap segment's bits exchanges
+    per-owner slot arrays (k_list_claim), a larger one the bitmap (k_bits_claim); the greedy
+    scans hub rows wave-wide.  Paths and scanned-edge counts equal the single engine's, which
+    the oracle pins at RMAT-11 above."""
+    from nebula_amd import rmat
+    src, dst, w = graphs.rmat_graph(16)
+    single = graphs.rmat_engine(src, dst, w)
+    c = cluster_for(src, dst, w, world)
+    try:
+        found = 0
+        for s, t in rmat.pick_pairs(src, dst, 40, seed=31 + world):
+            st, st1 = {}, {}
+            got = c.find_path([s], [t], [1], 5, stats=st)
+            assert got == single.find_path([s], [t], [1], 5, stats=st1), (world, s, t)
+            assert st["edges"] == st1["edges"]
+            found += len(got)
+        assert found > 0
+        ps = rmat.pick_pairs(src, dst, 8, seed=7)
+        frm, to = [p[0] for p in ps[:3]], [p[1] for p in ps]
+        assert c.find_path(frm, to, [1], 4) == single.find_path(frm, to, [1], 4)
+    finally:
+        c.close()
+        single.close()
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_partitioned_shortest_multi_and_self(rmat11, world):
     from nebula_amd import rmat
