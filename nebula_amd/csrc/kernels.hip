@@ -3045,9 +3045,14 @@ struct GreedyPart {
   uint32_t em;
   const uint32_t* lab_b;
   uint32_t eb;
-  Cand* part;                           // [gridDim.x] per-block minima
+  Cand* part;                           // [2 * gridDim.x] per-block minima (row scan, hub scan)
+  uint32_t* hubs;                       // B-set members whose in-edge rows the whole grid scans ...
+  uint32_t* nhub;                       // ... and their count (reset by k_greedy_part_reduce)
+  uint32_t hub_base;                    // k_greedy_hub's minima start at part[hub_base]
 };
-constexpr int GREC = 6;                 // rank record: type, rank, vid, global id (-1: none), visible, 0
+constexpr int GREC = 6;
+constexpr uint32_t GP_HUB_ROW = 4096;   // a longer in-edge row is a hub's: scanned grid-wide
+constexpr uint32_t GP_HUB_CAP = 1024;   // hubs listed per hop (more: scanned wave-wide in place)                 // rank record: type, rank, vid, global id (-1: none), visible, 0
 
 __device__ __forceinline__ bool part_valid(const GreedyPart& g, uint32_t u) {
   if (g.pos <= g.kf) return g.lab_m[u] == ((g.em << LVL_BITS) | (uint32_t)g.pos);
@@ -3070,6 +3075,17 @@ __global__ void __launch_bounds__(BLOCK) k_greedy_part(GreedyPart g) {
     while (m) {
       const uint32_t u = (uint32_t)(base + __builtin_ctzll(m));
       m &= m - 1;
+      uint32_t len = 0;
+      for (int t = 0; t < g.ntypes; ++t) len += g.row_ptr[t][u + 1] - g.row_ptr[t][u];
+      if (len > GP_HUB_ROW) {   // wave-uniform: left to k_greedy_hub unless the list is full
+        uint32_t k = 0;
+        if (lane == 0) k = atomicAdd(g.nhub, 1u);
+        k = __shfl(k, 0, 64);
+        if (k < GP_HUB_CAP) {
+          if (lane == 0) g.hubs[k] = u;
+          continue;
+        }
+      }
       const int64_t uvid = g.vids[u];
       for (int t = 0; t < g.ntypes; ++t) {
         const uint32_t rs = g.row_ptr[t][u], re = g.row_ptr[t][u + 1];
@@ -3096,6 +3112,46 @@ __global__ void __launch_bounds__(BLOCK) k_greedy_part(GreedyPart g) {
   }
 }
 
+// The hubs k_greedy_part listed: each in-edge row is scanned by the whole grid (thread-strided,
+// coalesced); per-block minima go to part[hub_base + block].
+__global__ void __launch_bounds__(BLOCK) k_greedy_hub(GreedyPart g) {
+  __shared__ Cand lds[WAVES];
+  Cand best{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
+  uint32_t nh = *g.nhub;
+  if (nh > GP_HUB_CAP) nh = GP_HUB_CAP;
+  if (g.vp) {
+    if (g.vp[1]) nh = 0;
+    g.v = (uint32_t)g.vp[0];
+  }
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (uint32_t h = 0; h < nh; ++h) {
+    const uint32_t u = g.hubs[h];
+    const int64_t uvid = g.vids[u];
+    for (int t = 0; t < g.ntypes; ++t) {
+      const uint64_t rs = g.row_ptr[t][u], re = g.row_ptr[t][u + 1];
+      for (uint64_t j = rs + (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < re; j += stride) {
+        if (g.col[t][j] != g.v) continue;
+        Cand x{(int64_t)g.type[t], g.rank[t] ? g.rank[t][j] : 0, uvid, u};
+        if (cand_less(x, best)) best = x;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Cand x = shfl_cand(best, o);
+    if (cand_less(x, best)) best = x;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) lds[w] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Cand b = lds[0];
+    for (int k = 1; k < WAVES; ++k)
+      if (cand_less(lds[k], b)) b = lds[k];
+    g.part[g.hub_base + blockIdx.x] = b;
+  }
+}
+
 __device__ __forceinline__ void put_record(const Cand& b, uint32_t gbase, const uint8_t* visible, int64_t* out) {
   out[0] = b.t;
   out[1] = b.r;
@@ -3106,7 +3162,8 @@ __device__ __forceinline__ void put_record(const Cand& b, uint32_t gbase, const 
 }
 
 __global__ void k_greedy_part_reduce(const Cand* __restrict__ part, int nparts, uint32_t gbase,
-                                     const uint8_t* __restrict__ visible, int64_t* out) {
+                                     const uint8_t* __restrict__ visible, int64_t* out, uint32_t* nhub) {
+  if (nhub && threadIdx.x == 0) *nhub = 0;   // the next hop's hub list starts empty
   // one wave (launched with 64 threads): lane-strided minima, then a wave reduction
   Cand b{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
   for (int k = threadIdx.x; k < nparts; k += 64)
@@ -3177,7 +3234,8 @@ hipError_t ws_path_level_part(Workspace* w, const PathTypes& pt, int src, uint64
   // sum over every rank, so a bound on each rank's edges) is small sends per-owner slot arrays
   // of e_bound ids instead of the npad-bit bitmap segments — the same choice on every rank
   const uint64_t stride = (e_bound + 63) / 64 * 64;
-  const bool sparse = pt.n == 1 && e_bound && stride * 4 * 2 <= w->npad / 8 && !bits_off() && sparse_on();
+  const bool sparse = lv.global_bound && pt.n == 1 && e_bound && stride * 4 * 2 <= w->npad / 8 && !bits_off() &&
+                      sparse_on();
   HIP_TRY(hipMemsetAsync(&w->ps->n[dst], 0, sizeof(unsigned long long), w->stream));
   if (sparse) HIP_TRY(hipMemsetAsync(w->sendbits, 0xFF, G * stride * 4, w->stream));
   for (int t = 0; t < pt.n; ++t) {
@@ -3319,8 +3377,12 @@ hipError_t ws_path_greedy_part(Workspace* w, const PathTypes& bwd, const PathGre
   const uint64_t nblk = cdiv(w->nv ? w->nv : 1, BLOCK);
   constexpr unsigned kGrid = 1024;
   const unsigned grid = (unsigned)(nblk < kGrid ? nblk : kGrid);
+  constexpr unsigned kHubGrid = 256;
+  const size_t hub_off = ((size_t)kGrid + kHubGrid) * sizeof(Cand);
   if (!w->g_part) {
-    HIP_TRY(hipMalloc(&w->g_part, (size_t)kGrid * sizeof(Cand)));
+    HIP_TRY(hipMalloc(&w->g_part, hub_off + (GP_HUB_CAP + 1) * sizeof(uint32_t)));
+    HIP_TRY(hipMemsetAsync(static_cast<char*>(w->g_part) + hub_off, 0, (GP_HUB_CAP + 1) * sizeof(uint32_t),
+                           w->stream));
     HIP_TRY(hipMalloc((void**)&w->g_rec, GREC * 8));
     HIP_TRY(hipMalloc((void**)&w->g_all, (size_t)G * GREC * 8));
     HIP_TRY(hipMalloc((void**)&w->g_path, (1 + 3 * (size_t)MAX_PATH_LEN) * 8));
@@ -3362,12 +3424,16 @@ hipError_t ws_path_greedy_part(Workspace* w, const PathTypes& bwd, const PathGre
   g.lab_b = w->lab[LAB_B];
   g.eb = pg.eb;
   g.part = d_part;
+  g.hubs = reinterpret_cast<uint32_t*>(static_cast<char*>(w->g_part) + hub_off);
+  g.nhub = g.hubs + GP_HUB_CAP;
+  g.hub_base = grid;
   for (int pos = 1; pos <= pg.L; ++pos) {
     g.pos = pos;
     hipEvent_t p = prof_begin_p(w, K_GREEDY);
     hipLaunchKernelGGL(k_greedy_part, dim3(grid), dim3(BLOCK), 0, w->stream, g);
-    hipLaunchKernelGGL(k_greedy_part_reduce, dim3(1), dim3(64), 0, w->stream, d_part, (int)grid, gbase, visible,
-                       w->g_rec);
+    hipLaunchKernelGGL(k_greedy_hub, dim3(kHubGrid), dim3(BLOCK), 0, w->stream, g);
+    hipLaunchKernelGGL(k_greedy_part_reduce, dim3(1), dim3(64), 0, w->stream, d_part, (int)(grid + kHubGrid), gbase,
+                       visible, w->g_rec, g.nhub);
     prof_end_p(w, p, K_GREEDY, 0);
     HIP_TRY(hipGetLastError());
     if (w->comm->allgather(w->g_rec, w->g_all, GREC * 8, w->stream)) return hipErrorUnknown;

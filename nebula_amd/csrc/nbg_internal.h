@@ -516,6 +516,9 @@ struct PathLevel {
   uint32_t tstamp = 0;
   const PathTypes* deg = nullptr;   // non-null: k_expand<BFS> also sums the output list's degrees over
                                     // these CSRs into PState.ld[rec] (replaces a k_degsum launch)
+  bool global_bound = false;        // partitioned: e_bound is the same on every rank and bounds each
+                                    // rank's edges (a degree sum over ranks), so the level may
+                                    // exchange slot arrays instead of bitmaps
 };
 hipError_t ws_path_level(Workspace* w, const PathTypes& pt, int src, uint64_t n_bound, uint64_t e_bound, int dst,
                          const PathLevel& lv);

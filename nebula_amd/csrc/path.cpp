@@ -79,6 +79,7 @@ hipError_t level(PathCtx& c, const PathTypes& pt, int src, uint64_t n_bound, uin
 hipError_t level_ds(PathCtx& c, const PathTypes& pt, int src, uint64_t n_bound, uint64_t e_bound, int dst,
                     PathLevel lv, int side, int* rec) {
   if (!c.part) lv.deg = &pt;
+  lv.global_bound = true;   // e_bound: the frontier's degree sum over every rank
   hipError_t he = level(c, pt, src, n_bound, e_bound, dst, lv);
   *rec = ws_path_last_rec(c.ws);
   if (he == hipSuccess && c.part) he = ws_path_degsum(c.ws, dst, e_bound ? e_bound : 1, pt, side);
@@ -225,6 +226,7 @@ int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_pat
   int fcur = S_F0, bcur = S_B0, kf = 0, kb = 0;
   uint64_t nf = 1, nbk = 1;
   std::vector<uint64_t> fn(1, 1);   // forward level sizes
+  std::vector<uint64_t> bn(1, 1);   // backward level sizes
   bool met = false;
   while ((uint32_t)(kf + kb) < upto) {
     const bool forward = dsf <= dsb;
@@ -260,6 +262,7 @@ int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_pat
     else
       dsb = level_dsum(c, ps, rec, 1);
     if (forward) fn.push_back(nf);
+    else bn.push_back(nbk);
     if (ps.n[S_MEET]) { met = true; break; }
     if (nf == 0 || nbk == 0) break;
   }
@@ -271,9 +274,35 @@ int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_pat
     int slot = S_MEET;
     T(bsets(c, S_MEET, ps.n[S_MEET], kf, 1, ef, em, 0, fn, &slot));
   }
+  int gkf = kf;
+  // NBG_PART_FWD_BSETS=1 (partitioned, off by default): the positions past kf get true B-sets
+  // too, forward from the meet set over out-edges (B[i] = out-neighbours of B[i-1] at backward
+  // level L - i), and B[L] = {t}; the greedy then tests LAB_M at every position and scans the
+  // in-edge rows of path vertices only instead of whole backward BFS levels.  It costs a bitmap
+  // all-to-all per position past kf + 1; on the same-device rehearsal that outweighed the scans
+  // it saves (RMAT-20 p50 0.99 -> 1.21 ms, RMAT-26 2.01 -> 2.03 ms, profiles/r02_mm_*).
+  static const bool fwd_bsets = getenv("NBG_PART_FWD_BSETS") && atoi(getenv("NBG_PART_FWD_BSETS")) != 0;
+  if (c.part && fwd_bsets && kb >= 1 && he == hipSuccess) {
+    int cur = S_MEET;
+    uint64_t nb = ps.n[S_MEET];
+    for (int i = kf + 1; i < L && he == hipSuccess; ++i) {
+      PathLevel lv;
+      lv.lab = LAB_M;
+      lv.stamp = stamp(em, (uint32_t)i);
+      lv.rlab = LAB_B;
+      lv.rstamp = stamp(eb, (uint32_t)(L - i));
+      const int dst = cur == S_F0 ? S_F0 + 1 : S_F0;
+      he = level(c, c.fwd, cur, nb, c.bwd_edges, dst, lv);
+      cur = dst;
+      nb = (size_t)(L - i) < bn.size() ? bn[L - i] : c.E.snap.nv;
+    }
+    T(upload1(ws, S_B0, t));
+    T(ws_path_stamp(ws, S_B0, 1, LAB_M, stamp(em, (uint32_t)L)));
+    gkf = L;
+  }
   if (he != hipSuccess) return dev_fail(c.E, he, "path B-sets");
   mark("bsets_enq");
-  PathGreedy g{L, kf, em, eb, start_slot};
+  PathGreedy g{L, gkf, em, eb, start_slot};
   g.v0_gid = s_gid;   // B[0] = {s}
   g.v0_vid = s_vid;
   std::vector<int64_t> p;

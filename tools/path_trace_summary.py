@@ -1,3 +1,6 @@
+#!/usr/bin/env python3
+"""Summarise NBG_PATH_TRACE=1 stderr lines (per-pair host-side phase times of the partitioned
+FIND SHORTEST PATH, microseconds): python3 tools/path_trace_summary.py <stderr log>"""
 import re, statistics as st, collections, sys
 lines=[l for l in open(sys.argv[1]) if l.startswith('nbg path')]
 tot=[int(l.split('=')[1]) for l in lines if 'total=' in l]
