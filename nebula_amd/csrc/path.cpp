@@ -114,12 +114,16 @@ hipError_t upload1(Workspace* ws, int slot, uint32_t id) { return ws_path_upload
 
 // Recover B[i] for i = top-1 .. lo from B[top] (slot `cur`, <= n_top entries) through in-edges:
 // B[i] = { u : u -> B[i+1], forward label of u == i } (i >= 1) or u in S (i == 0).
+// first_bound (partitioned): the top list's in-degree sum over every rank (0: unknown), so the
+// first step may exchange slot arrays
 hipError_t bsets(PathCtx& c, int cur, uint64_t n_top, int top, int lo, uint32_t ef, uint32_t em, uint32_t es,
-                 const std::vector<uint64_t>& level_n, int* out_slot) {
+                 const std::vector<uint64_t>& level_n, int* out_slot, uint64_t first_bound = 0) {
   hipError_t he = hipSuccess;
   uint64_t nb = n_top;
   for (int i = top - 1; i >= lo && he == hipSuccess; --i) {
     PathLevel lv;
+    const bool first = i == top - 1 && first_bound;
+    lv.global_bound = first;
     lv.lab = LAB_M;
     lv.stamp = stamp(em, (uint32_t)i);
     if (i >= 1) {
@@ -134,7 +138,7 @@ hipError_t bsets(PathCtx& c, int cur, uint64_t n_top, int top, int lo, uint32_t 
       lv.rstamp = stamp(es, 0);
     }
     const int dst = cur == S_SET0 ? S_SET0 + 1 : S_SET0;
-    he = level(c, c.bwd, cur, nb, c.bwd_edges, dst, lv);
+    he = level(c, c.bwd, cur, nb, first ? first_bound : c.bwd_edges, dst, lv);
     cur = dst;
     nb = (size_t)i < level_n.size() ? level_n[i] : c.E.snap.nv;
   }
@@ -250,6 +254,7 @@ int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_pat
       bcur ^= 1;
       ++kb;
     }
+    if (c.part) T(ws_path_meet_degsum(ws, S_MEET, c.bwd));   // the first B-set step's bound
     mark(forward ? "fwd_enq" : "bwd_enq");
     T(sync(c, &ps));
     mark("sync");
@@ -272,7 +277,7 @@ int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_pat
   if (kf >= 1) {
     // B[kf] = the meet list; B[kf-1] .. B[1] through in-edges; B[0] = {s}
     int slot = S_MEET;
-    T(bsets(c, S_MEET, ps.n[S_MEET], kf, 1, ef, em, 0, fn, &slot));
+    T(bsets(c, S_MEET, ps.n[S_MEET], kf, 1, ef, em, 0, fn, &slot, c.part ? ps.mdsum : 0));
   }
   int gkf = kf;
   // NBG_PART_FWD_BSETS=1 (partitioned, off by default): the positions past kf get true B-sets
