@@ -3337,7 +3337,10 @@ hipError_t ws_path_sync_part(Workspace* w, PState* out) {
   HIP_TRY(hipGetLastError());
   if (w->comm->allreduce_sum_u64(w->pgst, PG_N, w->stream)) return hipErrorUnknown;
   HIP_TRY(hipMemcpyAsync(w->h_pgst, w->pgst, PG_N * sizeof(unsigned long long), hipMemcpyDeviceToHost, w->stream));
-  HIP_TRY(hipMemcpyAsync(w->h_ps, w->ps, sizeof(PState), hipMemcpyDeviceToHost, w->stream));
+  // the rank's own PState only feeds the profiler's byte counts (every field the callers read is
+  // in the reduced block): no second copy per level when nothing is being profiled
+  if (!w->prof.pending.empty())
+    HIP_TRY(hipMemcpyAsync(w->h_ps, w->ps, sizeof(PState), hipMemcpyDeviceToHost, w->stream));
   HIP_TRY(ws_wait(w));
   PState g = *w->h_ps;
   for (int k = 0; k < PSLOTS; ++k) g.n[k] = w->h_pgst[k];
