@@ -2826,10 +2826,11 @@ hipError_t ws_path_degsum(Workspace* w, int s, uint64_t n_bound, const PathTypes
   return hipGetLastError();
 }
 
-hipError_t ws_path_meet_degsum(Workspace* w, int s, const PathTypes& pt) {
+hipError_t ws_path_meet_degsum(Workspace* w, int s, const PathTypes& pt, bool out_edges) {
   const DegsumArgs d = degsum_args(pt);
-  HIP_TRY(hipMemsetAsync(&w->ps->mdsum, 0, sizeof(unsigned long long), w->stream));
-  hipLaunchKernelGGL(k_degsum, dim3(64), dim3(BLOCK), 0, w->stream, w->slot[s], &w->ps->n[s], d, &w->ps->mdsum,
+  unsigned long long* o = out_edges ? &w->ps->mdsum_out : &w->ps->mdsum;
+  HIP_TRY(hipMemsetAsync(o, 0, sizeof(unsigned long long), w->stream));
+  hipLaunchKernelGGL(k_degsum, dim3(64), dim3(BLOCK), 0, w->stream, w->slot[s], &w->ps->n[s], d, o,
                      (unsigned long long*)nullptr);
   return hipGetLastError();
 }
@@ -3313,7 +3314,7 @@ hipError_t ws_path_level_part(Workspace* w, const PathTypes& pt, int src, uint64
 }
 
 // The PState fields every rank needs, summed over ranks (n[], dsum[], found, err, le[]).
-constexpr int PG_N = PSLOTS + 2 + 2 + PATH_REC + 1;
+constexpr int PG_N = PSLOTS + 2 + 2 + PATH_REC + 2;
 __global__ void k_pgstats(const PState* __restrict__ ps, unsigned long long* __restrict__ g) {
   const int k = threadIdx.x;
   if (k < PSLOTS) g[k] = ps->n[k];
@@ -3324,6 +3325,7 @@ __global__ void k_pgstats(const PState* __restrict__ ps, unsigned long long* __r
   }
   if (k < PATH_REC) g[PSLOTS + 4 + k] = ps->le[k];
   if (k == 0) g[PSLOTS + 4 + PATH_REC] = ps->mdsum;
+  if (k == 1) g[PSLOTS + 5 + PATH_REC] = ps->mdsum_out;
 }
 
 // Synchronous: like ws_path_sync, with the per-rank sizes summed over ranks.
@@ -3349,6 +3351,7 @@ hipError_t ws_path_sync_part(Workspace* w, PState* out) {
   g.err = w->h_pgst[PSLOTS + 3];
   for (int k = 0; k < PATH_REC; ++k) g.le[k] = w->h_pgst[PSLOTS + 4 + k];
   g.mdsum = w->h_pgst[PSLOTS + 4 + PATH_REC];
+  g.mdsum_out = w->h_pgst[PSLOTS + 5 + PATH_REC];
   if (out) *out = g;
   prof_flush(w, nullptr, w->h_ps);
   return hipSuccess;

@@ -293,7 +293,8 @@ struct PState {                      // device-resident sizes of one FIND PATH q
   unsigned long long gv;              // greedy hop: the current path vertex (dense id)
   unsigned long long gpart[4 * GREEDY_HOP_BLOCKS];   // greedy hop: per-workgroup minimum candidate
   unsigned long long ld[PATH_REC];   // degree sum of the level's output list (summed by k_expand<BFS>)
-  unsigned long long mdsum;          // partitioned: degree sum of the meet list (its B-set step's bound)
+  unsigned long long mdsum;          // partitioned: in-degree sum of the meet list (its B-set step's bound)
+  unsigned long long mdsum_out;      // partitioned: its out-degree sum (the forward B-set step's bound)
 };
 
 struct PathTypes {                   // the CSRs one search direction expands (one per OVER type)
@@ -505,7 +506,7 @@ hipError_t ws_path_stamp(Workspace* w, int slot, uint64_t n_bound, int lab, uint
 hipError_t ws_path_degsum(Workspace* w, int slot, uint64_t n_bound, const PathTypes& pt, int side);
 // partitioned: the degree sum of a slot's list over pt into PState::mdsum (summed over ranks by
 // the next ws_path_sync_part); no expansion record
-hipError_t ws_path_meet_degsum(Workspace* w, int slot, const PathTypes& pt);
+hipError_t ws_path_meet_degsum(Workspace* w, int slot, const PathTypes& pt, bool out_edges = false);
 // one BFS level: expand slot `src` over pt, claim into lab `bp` fields, pack claims into `dst`
 struct PathLevel {
   int lab;                 // label claimed

@@ -168,6 +168,12 @@ int32_t greedy_path(PathCtx& c, const PathGreedy& g, std::vector<int64_t>* path)
   return NBG_OK;
 }
 
+// NBG_PART_FWD_BSETS (partitioned): true B-sets past kf before the greedy (see bidirectional)
+bool fwd_bsets_on() {
+  static const bool on = getenv("NBG_PART_FWD_BSETS") && atoi(getenv("NBG_PART_FWD_BSETS")) != 0;
+  return on;
+}
+
 // s, t: local ids (NO_ROW on a rank that does not own them); partitioned: s_gid / s_vid = the
 // source's global id and vid on every rank (the greedy's v0 without an exchange), deg = deg(s),
 // deg(t) over ranks when known (null: a set-up exchange)
@@ -254,7 +260,10 @@ int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_pat
       bcur ^= 1;
       ++kb;
     }
-    if (c.part) T(ws_path_meet_degsum(ws, S_MEET, c.bwd));   // the first B-set step's bound
+    if (c.part) {   // the first B-set steps' bounds (backward, and forward past kf)
+      T(ws_path_meet_degsum(ws, S_MEET, c.bwd));
+      if (fwd_bsets_on()) T(ws_path_meet_degsum(ws, S_MEET, c.fwd, true));
+    }
     mark(forward ? "fwd_enq" : "bwd_enq");
     T(sync(c, &ps));
     mark("sync");
@@ -286,18 +295,19 @@ int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_pat
   // in-edge rows of path vertices only instead of whole backward BFS levels.  It costs a bitmap
   // all-to-all per position past kf + 1; on the same-device rehearsal that outweighed the scans
   // it saves (RMAT-20 p50 0.99 -> 1.21 ms, RMAT-26 2.01 -> 2.03 ms, profiles/r02_mm_*).
-  static const bool fwd_bsets = getenv("NBG_PART_FWD_BSETS") && atoi(getenv("NBG_PART_FWD_BSETS")) != 0;
-  if (c.part && fwd_bsets && kb >= 1 && he == hipSuccess) {
+  if (c.part && fwd_bsets_on() && kb >= 1 && he == hipSuccess) {
     int cur = S_MEET;
     uint64_t nb = ps.n[S_MEET];
     for (int i = kf + 1; i < L && he == hipSuccess; ++i) {
       PathLevel lv;
+      const bool first = i == kf + 1 && ps.mdsum_out;
+      lv.global_bound = first;   // the meet list's out-degree sum over every rank
       lv.lab = LAB_M;
       lv.stamp = stamp(em, (uint32_t)i);
       lv.rlab = LAB_B;
       lv.rstamp = stamp(eb, (uint32_t)(L - i));
       const int dst = cur == S_F0 ? S_F0 + 1 : S_F0;
-      he = level(c, c.fwd, cur, nb, c.bwd_edges, dst, lv);
+      he = level(c, c.fwd, cur, nb, first ? ps.mdsum_out : c.bwd_edges, dst, lv);
       cur = dst;
       nb = (size_t)(L - i) < bn.size() ? bn[L - i] : c.E.snap.nv;
     }
