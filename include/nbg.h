@@ -403,6 +403,27 @@ int32_t nbg_comm_init(nbg_engine* e, const uint8_t id[NBG_UNIQUE_ID_BYTES], int3
  * collectives copy between the engines' buffers.  Each engine is then driven by its own host
  * thread (finalize and every query), exactly as the RCCL ranks are. */
 int32_t nbg_comm_init_local(nbg_engine* const* engines, int32_t n);
+/* Failure semantics of a partitioned engine.  The reference keeps a query alive when some
+ * storaged parts fail and reports them (StorageClient.inl:112-136, GoExecutor.cpp:424-442); a
+ * collective engine cannot run a hop without one of its ranks, so a query fails on EVERY rank
+ * with the same code instead:
+ *   - a rank-local failure before the query's first collective (allocation, a start list whose
+ *     edges exceed one rank's list limit, ...) is agreed in one small all-reduce: every rank
+ *     returns the code of the lowest-ranked rank that failed, and the engines stay usable;
+ *   - a failure between collectives (a device error on one rank) aborts the communicator; the
+ *     peers' pending collectives fail (in-process group at once, RCCL when their bounded wait of
+ *     NBG_COMM_TIMEOUT_S seconds, default 120, expires) and every later collective call fails
+ *     with NBG_E_DEVICE.
+ * nbg_comm_abort aborts the engine's communicator(s) from any thread (ncclCommAbort for RCCL):
+ * a host watchdog uses it to release a rank blocked in a collective.  Not under the engine
+ * lock.  nbg_comm_aborted: 1 after an abort (the engine must be rebuilt), else 0. */
+int32_t nbg_comm_abort(nbg_engine* e);
+int32_t nbg_comm_aborted(const nbg_engine* e);
+/* Testing hook: the next `count` queries of this engine fail at `site` exactly as a real failure
+ * there would (the failure paths above are otherwise hard to reach on purpose). */
+#define NBG_FAULT_ALLOC  1   /* the query's workspace / held-result hand-over allocation fails */
+#define NBG_FAULT_DEVICE 2   /* partitioned GO: a device error after the query's first collective */
+int32_t nbg_inject_fault(nbg_engine* e, int32_t site, int32_t count);
 
 #ifdef __cplusplus
 }

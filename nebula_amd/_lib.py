@@ -28,6 +28,8 @@ E_UNSUPPORTED = -1002
 E_DEVICE = -1003
 E_OUT_OF_MEMORY = -1004
 E_STATE = -1005
+FAULT_ALLOC = 1      # nbg_inject_fault sites (include/nbg.h)
+FAULT_DEVICE = 2
 
 
 class nbg_config(C.Structure):
@@ -144,6 +146,9 @@ SIGNATURES = [
     ("nbg_comm_unique_id", i32, [P(u8)]),
     ("nbg_comm_init", i32, [vp, P(u8), i32, i32]),
     ("nbg_comm_init_local", i32, [P(vp), i32]),
+    ("nbg_comm_abort", i32, [vp]),
+    ("nbg_comm_aborted", i32, [vp]),
+    ("nbg_inject_fault", i32, [vp, i32, i32]),
 ]
 
 _lib = None

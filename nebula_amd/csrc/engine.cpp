@@ -450,11 +450,20 @@ struct GoPending {
 };
 
 // Enqueue the whole query (every step, the final-step rows and the end-of-query copy) on the
-// workspace *wsp (its stream `stream`); no host synchronisation.
+// workspace *wsp (its stream `stream`); no host synchronisation.  *wsp may be null (created here)
+// or hold an earlier device result's rows (handed to it first, ws_release).
+//
+// Partitioned (every rank runs the same call): everything that can fail on one rank alone —
+// workspace (re)creation, the input index, the back tracker, the start list's edge space, the
+// row buffers — happens BEFORE the query's first collective and is agreed there (Comm::agree,
+// one small all-reduce): either every rank enqueues the query or every rank returns the same
+// code.  A device error after that point aborts the communicator (the peers' collectives fail).
 static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts, uint64_t num_starts, bool device,
-                         Workspace** wsp, hipStream_t stream, GoPending* p) {
+                         Workspace** wsp, hipStream_t stream, Comm* qcomm, GoPending* p) {
   if (num_starts && !starts) return E.fail(NBG_E_INVALID_ARGUMENT, "null argument");
   if (hipSetDevice(E.cfg.device) != hipSuccess) return E.fail(NBG_E_DEVICE, "hipSetDevice failed");
+  const bool part = E.partitioned();
+  if (part && !qcomm) return E.fail(NBG_E_STATE, "partitioned engine without a communicator");
   const std::vector<int32_t>& over = st->over;
   const std::vector<TypeProgram>& plist = st->plist;
   const int ncols = st->ncols;
@@ -472,31 +481,69 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
     std::sort(f0.begin(), f0.end());
     f0.erase(std::unique(f0.begin(), f0.end()), f0.end());
   }
-  auto* rows = new nbg_rows();
+  std::unique_ptr<nbg_rows> rows(new nbg_rows());
   rows->eng = &E;
   rows->ncols = ncols;
   rows->on_device = device;
-  p->rows = rows;
   p->device = device;
   // (partitioned: every rank runs the same collective sequence, even with no local start)
-  if (f0.empty() && !E.partitioned()) { p->finished = true; return NBG_OK; }
-  if (f0.size() > ws_cap_frontier(*wsp)) {   // room for a duplicated start list
-    Comm* cm = ws_get_comm(*wsp);
-    ws_destroy(*wsp);
-    *wsp = ws_create(f0.size(), E.snap.nv, E.snap.max_edges(), stream, &err);
-    if (!*wsp) { delete rows; p->rows = nullptr; return E.fail(NBG_E_OUT_OF_MEMORY, err); }
-    if (E.partitioned() && ws_set_partition(*wsp, cm ? cm : E.comm.get(), E.npad) != hipSuccess) {
-      delete rows;
-      p->rows = nullptr;
-      return E.fail(NBG_E_OUT_OF_MEMORY, "partition buffers");
+  if (f0.empty() && !part) {
+    p->finished = true;
+    p->rows = rows.release();
+    return NBG_OK;
+  }
+  // ---- rank-local preparation: the first failure is kept and agreed below
+  int32_t lrc = NBG_OK;
+  std::string lmsg;
+  auto local_fail = [&](int32_t code, const std::string& msg) {
+    if (!lrc) { lrc = code; lmsg = msg; }
+  };
+  if (E.fault(NBG_FAULT_ALLOC)) local_fail(NBG_E_OUT_OF_MEMORY, "query workspace allocation failed (injected)");
+  const uint32_t cap = (uint32_t)(E.cfg.max_edge_returned_per_vertex <= 0 ? 0x7fffffff
+                                                                          : E.cfg.max_edge_returned_per_vertex);
+  // The start list keeps duplicates, so its edge space is the one list not bounded by a type's
+  // edge count: the device lists carry it in 32 bits, and the workspace's merge-path tile splits
+  // must cover it (on a partitioned engine each rank checks its own share).
+  uint64_t start_edges = 0;
+  for (int32_t t : over) {
+    auto it = E.snap.types.find(t);
+    if (it == E.snap.types.end()) continue;
+    uint64_t sum = 0;
+    for (uint32_t d : f0) sum += std::min<uint64_t>(it->second.h_row_ptr[d + 1] - it->second.h_row_ptr[d], cap);
+    start_edges = std::max(start_edges, sum);
+  }
+  if (f0.size() + start_edges >= 0xFFFFFFFFull)   // merge-path items (entries + edges) are 32-bit too
+    local_fail(NBG_E_UNSUPPORTED, "the start list's edges exceed 2^32-1 (duplicated hub starts)");
+  if (!lrc && *wsp) {   // rows of an earlier device result still there: hand the workspace to them
+    const int32_t rrc = ws_release(E, wsp, stream);
+    if (rrc) local_fail(rrc, E.last_error);
+  }
+  // room for a duplicated start list: the decision comes from the whole start list, the same on
+  // every rank of a partitioned engine (its own share, f0, is at most that)
+  const uint64_t need = part ? std::max<uint64_t>(num_starts, 1) : f0.size();
+  const uint64_t e_need = std::max<uint64_t>(E.snap.max_edges(), start_edges);
+  if (!lrc && (!*wsp || need > ws_cap_frontier(*wsp) || f0.size() + start_edges > ws_cap_items(*wsp))) {
+    const uint64_t fcap = std::max<uint64_t>({need, E.snap.nv + 1024, ws_cap_frontier(*wsp ? *wsp : nullptr)});
+    Workspace* fresh = ws_create(fcap, E.snap.nv, e_need, stream, &err);
+    if (fresh && part && ws_set_partition(fresh, qcomm, E.npad) != hipSuccess) {
+      ws_destroy(fresh);
+      fresh = nullptr;
+      err = "partition buffers";
+    }
+    if (!fresh) {
+      local_fail(NBG_E_OUT_OF_MEMORY, err);
+    } else {
+      if (*wsp) {
+        ws_profile_inherit(fresh, *wsp);
+        ws_destroy(*wsp);
+      }
+      *wsp = fresh;
     }
   }
   Workspace* ws = *wsp;
-  p->ws = ws;
-  rows->ws = ws;
   int64_t *bt = nullptr, *bt_in = nullptr;   // VertexBackTracker roots ($- / $var props after >= 2 steps)
-  ws_backtracker_off(ws);
-  if (st->uses_input) {
+  if (ws) ws_backtracker_off(ws);
+  if (!lrc && st->uses_input) {
     auto* ms = const_cast<nbg_go_stmt*>(st);
     if (!ms->d_in_ids) {
       const size_t n = std::max<size_t>(ms->in_ids.size(), 1);
@@ -510,16 +557,21 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
       ok = ok && hipMalloc((void**)&ms->d_in_cols, std::max<size_t>(ms->in_cols.size(), 1) * 8) == hipSuccess &&
            hipMemcpy(ms->d_in_cols, ms->d_in_col_ptrs.data(), ms->in_cols.size() * 8, hipMemcpyHostToDevice) ==
                hipSuccess;
-      if (!ok) { delete rows; p->rows = nullptr; return E.fail(NBG_E_OUT_OF_MEMORY, "input index upload"); }
+      if (!ok) {
+        // a later execution retries the upload from scratch
+        if (ms->d_in_ids) (void)hipFree(ms->d_in_ids);
+        for (auto*& q : ms->d_in_col_ptrs)
+          if (q) (void)hipFree(q);
+        if (ms->d_in_cols) (void)hipFree(ms->d_in_cols);
+        ms->d_in_ids = nullptr;
+        ms->d_in_cols = nullptr;
+        ms->d_in_col_ptrs.clear();
+        local_fail(NBG_E_OUT_OF_MEMORY, "input index upload");
+      }
     }
-    if (steps > 1 && ws_backtracker(ws, &bt, &bt_in) != hipSuccess) {
-      delete rows;
-      p->rows = nullptr;
-      return E.fail(NBG_E_OUT_OF_MEMORY, "backtracker");
-    }
+    if (!lrc && steps > 1 && ws_backtracker(ws, &bt, &bt_in) != hipSuccess)
+      local_fail(NBG_E_OUT_OF_MEMORY, "backtracker");
   }
-  const uint32_t cap = (uint32_t)(E.cfg.max_edge_returned_per_vertex <= 0 ? 0x7fffffff
-                                                                          : E.cfg.max_edge_returned_per_vertex);
   auto args_for = [&](const DevEdgeType& dt) {
     ExpandArgs a{};
     a.row_ptr = dt.row_ptr;
@@ -546,18 +598,6 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
     }
     return a;
   };
-  // the start list keeps duplicates, so its edge space is the one frontier not bounded by E:
-  // the device lists carry it in 32 bits
-  for (int32_t t : over) {
-    auto it = E.snap.types.find(t);
-    if (it == E.snap.types.end()) continue;
-    uint64_t sum = 0;
-    for (uint32_t d : f0) sum += std::min<uint64_t>(it->second.h_row_ptr[d + 1] - it->second.h_row_ptr[d], cap);
-    if (sum >= 0xFFFFFFFFull) {
-      delete rows;
-      return E.fail(NBG_E_UNSUPPORTED, "the start list's edges exceed 2^32-1 (duplicated hub starts)");
-    }
-  }
   // final-step row regions: the frontier entering step N is a set (N >= 2) or the start list
   // (N == 1, exact edge count known on the host)
   const uint64_t n_final = steps == 1 ? f0.size() : E.snap.nv;
@@ -578,6 +618,20 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
     region[i] = cap_rows;
     cap_rows += blk_cap[i] * ws_final_grid(n_final, eb);
   }
+  if (!lrc && ws_reserve_rows(ws, cap_rows, ncols) != hipSuccess) local_fail(NBG_E_OUT_OF_MEMORY, "result rows");
+  // ---- agreement: the query runs on every rank or on none
+  if (part) {
+    int32_t agreed = NBG_OK;
+    if (qcomm->agree(stream, lrc, &agreed)) return E.fail(NBG_E_DEVICE, "query agreement: " + qcomm->last);
+    if (agreed) {
+      if (lrc) return E.fail(lrc, lmsg);
+      return E.fail(agreed, "the query failed on another rank (code " + std::to_string(agreed) + ")");
+    }
+  } else if (lrc) {
+    return E.fail(lrc, lmsg);
+  }
+  p->ws = ws;
+  rows->ws = ws;
   // a short start list travels to the first expansion in its kernel arguments, with its edge
   // space over each OVER type computed here from the host CSR offsets (no k_relist launch)
   std::vector<InlineList> inl;
@@ -603,10 +657,10 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
     }
   }
   auto inl_of = [&](size_t i, uint32_t s) -> const InlineList* { return s == 1 && !inl.empty() ? &inl[i] : nullptr; };
-  hipError_t he = ws_reserve_rows(ws, cap_rows, ncols);
-  if (he == hipSuccess) he = ws_begin_query(ws, f0.data(), f0.size(), &plist, st->id);
+  hipError_t he = ws_begin_query(ws, f0.data(), f0.size(), &plist, st->id);
   uint64_t n_bound = f0.size();
   ws_set_mark_claims(ws, over.size() == 1);
+  const bool inject = part && E.fault(NBG_FAULT_DEVICE);
   for (uint32_t s = 1; he == hipSuccess && s <= steps; ++s) {
     const bool final = s == steps;
     // the next step's first OVER type: the next frontier list carries its edge space
@@ -633,20 +687,23 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
                              inl_of(i, s));
       }
     }
+    if (inject) he = hipErrorLaunchFailure;   // NBG_FAULT_DEVICE: a device error between collectives
     if (!final && he == hipSuccess) {
-      he = E.partitioned() ? ws_exchange(ws, (int)s, np0) : ws_finish_step(ws, (int)s, np0);
+      he = part ? ws_exchange(ws, (int)s, np0) : ws_finish_step(ws, (int)s, np0);
       n_bound = E.snap.nv;
     }
   }
-  if (he == hipSuccess && E.partitioned()) he = ws_global_stats(ws, (int)over.size());
+  if (he == hipSuccess && part) he = ws_global_stats(ws, (int)over.size());
   if (he == hipSuccess) he = ws_end_query_async(ws);
   if (he != hipSuccess) {
-    delete rows;
-    p->rows = nullptr;
-    return E.fail(NBG_E_DEVICE, std::string("HIP: ") + hipGetErrorString(he));
+    // the peers may already wait in this query's next collective: release them
+    if (part) qcomm->abort();
+    const std::string cm = part && !qcomm->last.empty() ? " (" + qcomm->last + ")" : "";
+    return E.fail(NBG_E_DEVICE, std::string("HIP: ") + hipGetErrorString(he) + cm);
   }
   p->region = std::move(region);
   p->blk_cap = std::move(blk_cap);
+  p->rows = rows.release();
   return NBG_OK;
 }
 
@@ -737,6 +794,19 @@ static int32_t go_collect(Engine& E, const nbg_go_stmt* st, GoPending* p, nbg_ro
       rows->blocks[where[k].first].counts[where[k].second] = kept[k];
       rows->count += kept[k];
     }
+    if (E.partitioned()) {
+      // the exchange is collective: a local failure of the dedup pass is agreed first
+      Comm* cm = ws_get_comm(ws);
+      int32_t agreed = NBG_OK;
+      if (cm->agree(ws_stream(ws), de == hipSuccess ? NBG_OK : NBG_E_DEVICE, &agreed)) {
+        delete rows;
+        return E.fail(NBG_E_DEVICE, "DISTINCT agreement: " + cm->last);
+      }
+      if (agreed && de == hipSuccess) {
+        delete rows;
+        return E.fail(agreed, "YIELD DISTINCT failed on another rank");
+      }
+    }
     if (de == hipSuccess && E.partitioned()) {
       std::vector<DistinctBlock> db;
       de = ws_distinct_exchange(ws, segments(nullptr), ncols, rows->kinds, &db);
@@ -769,9 +839,7 @@ static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* start
   if (!out) return E.fail(NBG_E_INVALID_ARGUMENT, "null argument");
   *out = nullptr;
   GoPending p;
-  int32_t rc = ws_release(E, &E.ws, E.stream);
-  if (rc) return rc;
-  rc = go_launch(E, st, starts, num_starts, device, &E.ws, E.stream, &p);
+  int32_t rc = go_launch(E, st, starts, num_starts, device, &E.ws, E.stream, E.comm.get(), &p);
   if (rc) return rc;
   return go_collect(E, st, &p, out);
 }
@@ -820,18 +888,22 @@ static void complete_oldest(Engine& E) {
 int32_t nbg::ws_release(Engine& E, Workspace** wsp, hipStream_t stream) {
   auto it = E.holders.find(*wsp);
   if (it == E.holders.end()) return NBG_OK;
-  nbg_rows* r = it->second;
-  E.holders.erase(it);
+  // the fresh workspace first: on failure nothing changes (the rows keep their workspace, which
+  // stays busy until they are freed)
   Comm* cm = ws_get_comm(*wsp);   // (the fresh workspace keeps the slot's communicator)
-  r->owned_ws = *wsp;
   std::string err;
   Workspace* fresh = ws_create(E.snap.nv + 1024, E.snap.nv, E.snap.max_edges(), stream, &err);
-  if (!fresh) { *wsp = nullptr; return E.fail(NBG_E_OUT_OF_MEMORY, err); }
-  if (E.partitioned() && ws_set_partition(fresh, cm ? cm : E.comm.get(), E.npad) != hipSuccess) {
+  if (fresh && E.partitioned() && ws_set_partition(fresh, cm ? cm : E.comm.get(), E.npad) != hipSuccess) {
     ws_destroy(fresh);
-    *wsp = nullptr;
-    return E.fail(NBG_E_OUT_OF_MEMORY, "partition buffers");
+    fresh = nullptr;
+    err = "partition buffers";
   }
+  if (!fresh)
+    return E.fail(NBG_E_OUT_OF_MEMORY, "a held device result occupies the query workspace and a new one could not be "
+                                       "allocated (" + err + "); free device results first");
+  nbg_rows* r = it->second;
+  E.holders.erase(it);
+  r->owned_ws = *wsp;
   ws_profile_inherit(fresh, *wsp);
   *wsp = fresh;
   return NBG_OK;
@@ -882,30 +954,31 @@ int32_t nbg_go_submit(nbg_go_stmt* st, const int64_t* starts, uint64_t num_start
     if (split_ok) {
       std::string err;
       q.comm.reset(E.comm->split(&err));
+      // the split is collective: keep it only if every rank got one (else all share the engine's)
+      if (E.comm->kind() != std::string("local")) {
+        int32_t agreed = NBG_OK;
+        if (E.comm->agree(E.stream, q.comm ? NBG_OK : NBG_E_DEVICE, &agreed))
+          return E.fail(NBG_E_DEVICE, "slot communicator agreement: " + E.comm->last);
+        if (agreed) q.comm.reset();
+      }
     }
   }
   const bool own_stream = !E.partitioned() || q.comm != nullptr;
   Comm* const qcomm = q.comm ? q.comm.get() : E.comm.get();
+  hipStream_t qstream = own_stream ? q.stream : E.stream;
   if (own_stream && !q.stream) {
-    if (hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking) != hipSuccess)
+    if (hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking) != hipSuccess) {
+      if (!E.partitioned()) return E.fail(NBG_E_DEVICE, "hipStreamCreate failed");
+      int32_t agreed = NBG_OK;   // the peers are about to agree on this query: fail it with them
+      (void)qcomm->agree(E.stream, NBG_E_DEVICE, &agreed);
       return E.fail(NBG_E_DEVICE, "hipStreamCreate failed");
-  }
-  const hipStream_t qstream = own_stream ? q.stream : E.stream;
-  if (q.ws) {   // rows of an earlier device result still there: hand the workspace to them
-    int32_t rc = ws_release(E, &q.ws, qstream);
-    if (rc) return rc;
-  }
-  if (!q.ws) {
-    std::string err;
-    q.ws = ws_create(E.snap.nv + 1024, E.snap.nv, E.snap.max_edges(), qstream, &err);
-    if (!q.ws) return E.fail(NBG_E_OUT_OF_MEMORY, err);
-    if (E.partitioned() && ws_set_partition(q.ws, qcomm, E.npad) != hipSuccess)
-      return E.fail(NBG_E_OUT_OF_MEMORY, "partition buffers");
+    }
+    qstream = q.stream;
   }
   auto* t = new nbg_go_ticket();
   t->st = st;
   t->slot = slot;
-  int32_t rc = go_launch(E, st, starts, num_starts, device != 0, &q.ws, qstream, &t->p);
+  int32_t rc = go_launch(E, st, starts, num_starts, device != 0, &q.ws, qstream, qcomm, &t->p);
   if (rc) { delete t; return rc; }
   q.ticket = t;
   E.inflight.push_back(t);
@@ -964,6 +1037,14 @@ void nbg_destroy(nbg_engine* h) {
   E.free_snapshot();
   if (E.stream) (void)hipStreamDestroy(E.stream);
   delete h;
+}
+
+int32_t nbg_inject_fault(nbg_engine* h, int32_t site, int32_t count) {
+  if (!h || site < 0 || count < 0) return NBG_E_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lg(h->e.mu);
+  h->e.fault_site = count ? site : 0;
+  h->e.fault_count = count;
+  return NBG_OK;
 }
 
 const char* nbg_last_error(const nbg_engine* h) { return h ? h->e.last_error.c_str() : "null engine"; }

@@ -62,6 +62,13 @@ struct Engine {
   uint64_t npad = 0;
   bool partitioned() const { return cfg.num_gpus > 1; }
 
+  // nbg_inject_fault (tests): the next fault_count queries fail at fault_site
+  int fault_site = 0, fault_count = 0;
+  bool fault(int site) {
+    if (fault_site != site || fault_count <= 0) return false;
+    if (--fault_count == 0) fault_site = 0;
+    return true;
+  }
   int32_t fail(int32_t code, const std::string& msg) {
     last_error = msg;
     return code;

@@ -105,6 +105,7 @@ struct Workspace {
   uint32_t* h_blk_rows = nullptr;  // pinned mirror (valid after ws_end_query)
   unsigned final_grid[MAX_TYPES_Q] = {};
   uint64_t cap_tiles = 0;
+  uint64_t e_max = 0;              // edges of the longest list the tiles cover (beside cap_frontier entries)
   bool seg_ready = false;          // the compaction list carries the first OVER type's edge space
   const unsigned long long* list_acc = nullptr;   // packed size of frontier[cur] (null: q->n, plain)
   int pr = 0, pc = 0;              // ping-pong parity of the relist / compaction accumulators
@@ -175,6 +176,13 @@ struct Workspace {
   size_t fetch_out_cap = 0;
   unsigned long long* h_gst = nullptr;
 };
+
+// Wait for the workspace's stream.  A partitioned workspace's stream runs collectives: the wait
+// is bounded by the communicator timeout and aborts the communicator when a peer never arrives.
+static hipError_t ws_sync(Workspace* w) {
+  if (!w->comm) return hipStreamSynchronize(w->stream);
+  return w->comm->wait(w->stream) == 0 ? hipSuccess : hipErrorLaunchTimeOut;
+}
 
 // ----------------------------------------------------------------------------- helpers
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
@@ -1567,6 +1575,7 @@ Workspace* ws_create(uint64_t max_frontier, uint64_t nv, uint64_t e_max, hipStre
   M((void**)&w->rlist, w->cap_frontier * 4);
   M((void**)&w->flags, w->flag_bytes);
   M((void**)&w->seen, (nv + 1) * 4);
+  w->e_max = e_max;
   w->cap_tiles = cdiv(w->cap_frontier + e_max + 1, TILE) + 2;
   M((void**)&w->tsplit, w->cap_tiles * 4);
   M((void**)&w->tsplit1, w->cap_tiles * 4);
@@ -1628,7 +1637,8 @@ void ws_destroy(Workspace* w) {
   delete w;
 }
 
-uint64_t ws_cap_frontier(Workspace* w) { return w->cap_frontier; }
+uint64_t ws_cap_frontier(Workspace* w) { return w ? w->cap_frontier : 0; }
+uint64_t ws_cap_items(Workspace* w) { return w->cap_frontier + w->e_max; }
 unsigned ws_final_grid_of(Workspace* w, int tix) { return w->final_grid[tix]; }
 const uint32_t* ws_host_blk_rows(Workspace* w, int tix) { return w->h_blk_rows + (size_t)tix * EXPAND_GRID; }
 int64_t* ws_row_col(Workspace* w, int c) { return w->rows + (uint64_t)c * w->cap_rows; }
@@ -1637,7 +1647,7 @@ const uint32_t* ws_current_frontier(Workspace* w) { return w->frontier[w->cur]; 
 
 hipError_t ws_reserve_rows(Workspace* w, uint64_t rows, int ncols) {
   if (rows <= w->cap_rows && ncols <= w->ncols_alloc) return hipSuccess;
-  HIP_TRY(hipStreamSynchronize(w->stream));
+  HIP_TRY(ws_sync(w));
   if (w->rows) HIP_TRY(hipFree(w->rows));
   w->rows = nullptr;
   uint64_t cap = rows < 1024 ? 1024 : rows;
@@ -1661,7 +1671,7 @@ hipError_t ws_reserve_rows(Workspace* w, uint64_t rows, int ncols) {
 // hipStreamSynchronize; NBG_BLOCKING_SYNC=1 restores the blocking wait.
 hipError_t ws_wait(Workspace* w) {
   static const bool blocking = getenv("NBG_BLOCKING_SYNC") != nullptr;
-  if (blocking) return hipStreamSynchronize(w->stream);
+  if (blocking || w->comm) return ws_sync(w);
   if (!w->done_ev) HIP_TRY(hipEventCreateWithFlags(&w->done_ev, hipEventDisableTiming));
   HIP_TRY(hipEventRecord(w->done_ev, w->stream));
   hipError_t e;
@@ -2073,7 +2083,7 @@ hipError_t ws_distinct(Workspace* w, const std::vector<std::array<uint64_t, 3>>&
   if (!total) return hipSuccess;
   uint64_t tcap = 1024;
   while (tcap < 2 * total) tcap <<= 1;
-  HIP_TRY(hipStreamSynchronize(w->stream));
+  HIP_TRY(ws_sync(w));
   if (tcap > w->dtab_cap) {
     if (w->dtab) HIP_TRY(hipFree(w->dtab));
     w->dtab = nullptr;
@@ -2110,7 +2120,7 @@ hipError_t ws_distinct(Workspace* w, const std::vector<std::array<uint64_t, 3>>&
                      w->d_row_cols, ncols, w->dkeep, w->dcnt);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(counts->data(), w->dcnt, segs.size() * 4, hipMemcpyDeviceToHost, w->stream));
-  return hipStreamSynchronize(w->stream);
+  return ws_sync(w);
 }
 
 hipError_t ws_distinct_exchange(Workspace* w, const std::vector<std::array<uint64_t, 3>>& segs, int ncols,
@@ -2125,7 +2135,7 @@ hipError_t ws_distinct_exchange(Workspace* w, const std::vector<std::array<uint6
     meta.insert(meta.end(), {sg[0], sg[1], total, sg[2]});
     total += sg[1];
   }
-  HIP_TRY(hipStreamSynchronize(w->stream));
+  HIP_TRY(ws_sync(w));
   // scratch: owners, counts [G][T] local and gathered, bases, cursors
   auto grow = [&](void** p, uint64_t* cap, uint64_t need) -> hipError_t {
     if (need <= *cap) return hipSuccess;
@@ -2164,7 +2174,7 @@ hipError_t ws_distinct_exchange(Workspace* w, const std::vector<std::array<uint6
     HIP_TRY(hipGetLastError());
   }
   if (comm->allgather(cnt, all, GT * 8, w->stream)) return hipErrorUnknown;
-  HIP_TRY(hipStreamSynchronize(w->stream));
+  HIP_TRY(ws_sync(w));
   std::vector<unsigned long long> h_all((uint64_t)G * GT);
   HIP_TRY(hipMemcpy(h_all.data(), all, h_all.size() * 8, hipMemcpyDeviceToHost));
   auto at = [&](int r, int q, int t) { return h_all[(uint64_t)r * GT + (uint64_t)q * T + t]; };
@@ -2194,7 +2204,7 @@ hipError_t ws_distinct_exchange(Workspace* w, const std::vector<std::array<uint6
     HIP_TRY(hipGetLastError());
   }
   if (comm->alltoall(w->xsend, w->xrecv, maxc * ncols * 8, w->stream)) return hipErrorUnknown;
-  HIP_TRY(hipStreamSynchronize(w->stream));
+  HIP_TRY(ws_sync(w));
   // this rank's rows by type: type t's block b = rows received from rank b
   out->assign(T, DistinctBlock{});
   std::vector<unsigned long long> h_rcnt(GT), h_place(GT);
@@ -2276,7 +2286,7 @@ hipError_t ws_fetch_rows(Workspace* w, const std::vector<std::pair<uint64_t, uin
   auto grow = [&](void** p, size_t* cap, size_t bytes) -> hipError_t {
     if (bytes <= *cap) return hipSuccess;
     if (*p) {
-      hipError_t se = hipStreamSynchronize(w->stream);
+      hipError_t se = ws_sync(w);
       if (se != hipSuccess) return se;
       (void)hipFree(*p);
       *p = nullptr;
@@ -2299,7 +2309,7 @@ hipError_t ws_fetch_rows(Workspace* w, const std::vector<std::pair<uint64_t, uin
   }
   for (int c = 0; e == hipSuccess && c < ncols; ++c)
     e = hipMemcpyAsync(host_cols[c], d_out + (uint64_t)c * total, total * 8, hipMemcpyDeviceToHost, w->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(w->stream);
+  if (e == hipSuccess) e = ws_sync(w);
   return e;
 }
 
@@ -2327,7 +2337,7 @@ hipError_t ws_rows_digest(Workspace* w, const std::vector<std::pair<uint64_t, ui
     e = hipGetLastError();
   }
   if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, 3 * 8, hipMemcpyDeviceToHost, w->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(w->stream);
+  if (e == hipSuccess) e = ws_sync(w);
   if (d_meta) (void)hipFree(d_meta);
   if (d_out) (void)hipFree(d_out);
   return e;
@@ -2347,7 +2357,9 @@ hipError_t ws_end_query_async(Workspace* w) {
 
 hipError_t ws_end_query_wait(Workspace* w) {
   static const bool blocking = getenv("NBG_BLOCKING_SYNC") != nullptr;
-  if (blocking) {
+  if (w->comm) {
+    HIP_TRY(ws_sync(w));   // bounded: a peer that never arrives aborts the communicator
+  } else if (blocking) {
     HIP_TRY(hipEventSynchronize(w->done_ev));
   } else {
     hipError_t e;
@@ -2370,7 +2382,7 @@ hipError_t ws_end_query(Workspace* w) {
 hipError_t ws_set_partition(Workspace* w, Comm* comm, uint64_t npad) {
   if (!comm || npad % PART_ALIGN || PART_ALIGN % BITS_BLOCK || PART_ALIGN % FLAG_ALIGN) return hipErrorInvalidValue;
   const uint64_t G = (uint64_t)comm->world;
-  HIP_TRY(hipStreamSynchronize(w->stream));
+  HIP_TRY(ws_sync(w));
   w->comm = comm;
   w->npad = npad;
   if (w->flags) HIP_TRY(hipFree(w->flags));
@@ -2383,12 +2395,13 @@ hipError_t ws_set_partition(Workspace* w, Comm* comm, uint64_t npad) {
   HIP_TRY(hipMalloc((void**)&w->recvbits, G * npad / 8));
   HIP_TRY(hipMalloc((void**)&w->gst, GST_N * sizeof(unsigned long long)));
   HIP_TRY(hipHostMalloc((void**)&w->h_gst, GST_N * sizeof(unsigned long long), hipHostMallocDefault));
-  return hipStreamSynchronize(w->stream);
+  return ws_sync(w);
 }
 
 // After all OVER types of a non-final step marked their candidates (global ids) in the flags:
 // pack -> all-to-all of npad-bit segments -> owner OR + compaction into the next local frontier.
 Comm* ws_get_comm(const Workspace* w) { return w ? w->comm : nullptr; }
+hipStream_t ws_stream(const Workspace* w) { return w->stream; }
 
 hipError_t ws_exchange(Workspace* w, int step, const ExpandArgs* next0) {
   if (!w->comm) return hipErrorInvalidValue;
@@ -2696,7 +2709,7 @@ hipError_t ws_path_begin(Workspace* w, uint64_t scratch_entries, uint64_t list_e
     }
   }
   if (list_entries > w->slot_cap) {
-    HIP_TRY(hipStreamSynchronize(w->stream));
+    HIP_TRY(ws_sync(w));
     for (auto*& p : w->slot) {
       if (p) HIP_TRY(hipFree(p));
       p = nullptr;
@@ -2705,7 +2718,7 @@ hipError_t ws_path_begin(Workspace* w, uint64_t scratch_entries, uint64_t list_e
     for (auto*& p : w->slot) HIP_TRY(hipMalloc((void**)&p, w->slot_cap * sizeof(uint32_t)));
   }
   if (scratch_entries > w->pscratch_cap) {
-    HIP_TRY(hipStreamSynchronize(w->stream));
+    HIP_TRY(ws_sync(w));
     if (w->pscratch) HIP_TRY(hipFree(w->pscratch));
     w->pscratch = nullptr;
     w->pscratch_cap = scratch_entries;
@@ -2790,13 +2803,13 @@ hipError_t ws_path_upload(Workspace* w, int s, const uint32_t* ids, uint64_t n) 
                           w->stream);
   }
   if (n > w->cap_starts) {
-    HIP_TRY(hipStreamSynchronize(w->stream));
+    HIP_TRY(ws_sync(w));
     if (w->h_starts) HIP_TRY(hipHostFree(w->h_starts));
     w->cap_starts = n + n / 2 + 1024;
     HIP_TRY(hipHostMalloc((void**)&w->h_starts, w->cap_starts * 4, hipHostMallocDefault));
   }
   // the staging buffer may still feed an earlier copy of this query
-  HIP_TRY(hipStreamSynchronize(w->stream));
+  HIP_TRY(ws_sync(w));
   memcpy(w->h_starts, ids, n * 4);
   w->h_ps->n[s] = n;
   HIP_TRY(hipMemcpyAsync(w->slot[s], w->h_starts, n * 4, hipMemcpyHostToDevice, w->stream));
@@ -3362,7 +3375,7 @@ hipError_t ws_allreduce_host(Workspace* w, std::vector<unsigned long long>& v) {
   if (!w->comm || v.empty()) return hipSuccess;
   if (v.size() > w->ar_cap) {   // grow-only scratch (no allocation per query)
     if (w->ar_buf) {
-      HIP_TRY(hipStreamSynchronize(w->stream));
+      HIP_TRY(ws_sync(w));
       (void)hipFree(w->ar_buf);
       w->ar_buf = nullptr;
       w->ar_cap = 0;
@@ -3375,7 +3388,7 @@ hipError_t ws_allreduce_host(Workspace* w, std::vector<unsigned long long>& v) {
   hipError_t e = hipMemcpyAsync(d, v.data(), v.size() * 8, hipMemcpyHostToDevice, w->stream);
   if (e == hipSuccess && w->comm->allreduce_sum_u64(d, v.size(), w->stream)) e = hipErrorUnknown;
   if (e == hipSuccess) e = hipMemcpyAsync(v.data(), d, v.size() * 8, hipMemcpyDeviceToHost, w->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(w->stream);
+  if (e == hipSuccess) e = ws_sync(w);
   return e;
 }
 
@@ -3459,7 +3472,7 @@ hipError_t ws_path_greedy_part(Workspace* w, const PathTypes& bwd, const PathGre
   const size_t np = 1 + 3 * (size_t)pg.L;
   HIP_TRY(hipMemcpyAsync(w->h_gpath, w->g_path, np * 8, hipMemcpyDeviceToHost, w->stream));
   HIP_TRY(hipMemcpyAsync(w->h_gpath + np, w->g_cur, 2 * 8, hipMemcpyDeviceToHost, w->stream));
-  HIP_TRY(hipStreamSynchronize(w->stream));
+  HIP_TRY(ws_sync(w));
   if (w->h_gpath[np + 1]) return hipErrorNotFound;
   memcpy(path, w->h_gpath, np * 8);
   return hipSuccess;
@@ -3608,7 +3621,7 @@ struct WalkArena {
   size_t used = 0;
   explicit WalkArena(Workspace* ws) : w(ws) {}
   void release() {
-    (void)hipStreamSynchronize(w->stream);
+    (void)ws_sync(w);
     for (void* p : owned) (void)hipFree(p);
     owned.clear();
   }
@@ -3682,7 +3695,7 @@ hipError_t ws_all_paths(Workspace* w, const PathTypes& fwd, int lab, uint32_t ep
     hipLaunchKernelGGL(k_walk, dim3(grid), dim3(BLOCK), 0, w->stream, a);
     WALK_TRY(hipGetLastError());
     WALK_TRY(hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, w->stream));
-    WALK_TRY(hipStreamSynchronize(w->stream));
+    WALK_TRY(ws_sync(w));
     *scanned += h[2];
     if (!h[0]) break;
     total += h[0];
@@ -3731,7 +3744,7 @@ hipError_t ws_all_paths(Workspace* w, const PathTypes& fwd, int lab, uint32_t ep
     WALK_TRY(hipGetLastError());
     std::vector<int64_t> host(ncomp[l] * width);
     WALK_TRY(hipMemcpyAsync(host.data(), o, host.size() * 8, hipMemcpyDeviceToHost, w->stream));
-    WALK_TRY(hipStreamSynchronize(w->stream));
+    WALK_TRY(ws_sync(w));
     for (uint64_t c = 0; c < ncomp[l]; ++c)
       out->emplace_back(host.begin() + (ptrdiff_t)(c * width), host.begin() + (ptrdiff_t)((c + 1) * width));
   }
@@ -3951,7 +3964,7 @@ hipError_t ws_all_paths_part(Workspace* w, const PathTypes& fwd, int lab, uint32
     WALK_TRY(hipGetLastError());
     WALK_COMM(w->comm->allgather(cnt, all, 3 * 8, w->stream));
     WALK_TRY(hipMemcpyAsync(h.data(), all, h.size() * 8, hipMemcpyDeviceToHost, w->stream));
-    WALK_TRY(hipStreamSynchronize(w->stream));
+    WALK_TRY(ws_sync(w));
     uint64_t walks = 0, comps = 0, maxc = 0;
     for (int q = 0; q < G; ++q) {
       walks += h[3 * q];
@@ -3993,7 +4006,7 @@ hipError_t ws_all_paths_part(Workspace* w, const PathTypes& fwd, int lab, uint32
     WALK_TRY(hipGetLastError());
     std::vector<int64_t> host(ncomp[l] * width);
     WALK_TRY(hipMemcpyAsync(host.data(), o, host.size() * 8, hipMemcpyDeviceToHost, w->stream));
-    WALK_TRY(hipStreamSynchronize(w->stream));
+    WALK_TRY(ws_sync(w));
     for (uint64_t c = 0; c < ncomp[l]; ++c)
       out->emplace_back(host.begin() + (ptrdiff_t)(c * width), host.begin() + (ptrdiff_t)((c + 1) * width));
   }

@@ -128,9 +128,12 @@ struct Snapshot {
   int64_t** d_tcols = nullptr;          // device array: every tag column (DevTag::col_base + c)
   uint8_t** d_tpres = nullptr;          // device array: presence per tag (DevTag::index)
   uint64_t device_bytes = 0;
-  uint64_t max_edges() const {
+  uint64_t max_edges() const {   // the longest edge space of one CSR (superseded versions included)
     uint64_t m = 0;
-    for (auto& kv : types) m = kv.second.num_edges > m ? kv.second.num_edges : m;
+    for (auto& kv : types) {
+      m = kv.second.num_edges > m ? kv.second.num_edges : m;
+      if (kv.second.old && kv.second.old->num_edges > m) m = kv.second.old->num_edges;
+    }
     return m;
   }
 };
@@ -365,11 +368,31 @@ hipError_t sp_wait(SpCtx* c, SpResult* out);
 
 // ----------------------------------------------------------------------------- collectives (comm.cpp)
 // Transport of the partitioned engine.  Methods return 0 on success; `last` holds the error.
+//
+// Failure semantics (the reference keeps a query alive on partial failure and reports the
+// failed parts, StorageClient.inl:112-136, GoExecutor.cpp:424-442; here every rank must instead
+// leave a collective query TOGETHER, or its peers block in the next collective):
+//   * rank-local failures before a query's first collective (allocation, a start list too large
+//     for one rank, ...) are agreed with agree(): every rank learns every rank's code and returns
+//     the same one (the first failing rank's);
+//   * a failure after that point (a device error between collectives, a peer that never arrives)
+//     aborts the communicator: abort() wakes the peers' pending collectives with an error, and a
+//     host wait on a partitioned stream gives up after NBG_COMM_TIMEOUT_S (default 120) seconds
+//     and aborts too.  An aborted communicator fails every later collective at once.
 struct Comm {
   int world = 1, rank = 0;
   std::string last;
-  virtual ~Comm() {}
+  virtual ~Comm();
   virtual const char* kind() const = 0;
+  // Every rank passes its local status; *out = the status of the lowest-ranked rank that failed
+  // (NBG_OK when none did), the same on every rank.  Returns 0, or -1 when the exchange itself
+  // failed (the communicator is then aborted).  Synchronous (host round trip).
+  int agree(hipStream_t s, int32_t local, int32_t* out);
+  virtual void abort() { aborted = true; }
+  bool is_aborted() const { return aborted; }
+  // Wait for a stream that runs this communicator's collectives; gives up (aborting) after the
+  // communicator timeout.  0 = done, -1 = failed or timed out (`last` says which).
+  int wait(hipStream_t s);
   // recv[q * bytes ..] <- rank q's send[rank * bytes ..], for every q (stream-ordered)
   virtual int alltoall(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
   // recv[q * bytes ..] <- rank q's send[0 .. bytes)
@@ -381,7 +404,16 @@ struct Comm {
     (void)err;
     return nullptr;
   }
+
+ bool agree_ready(std::string* err);         // allocate agree()'s scratch (at communicator creation)
+
+ protected:
+  volatile bool aborted = false;
+  unsigned long long* agree_dev = nullptr;    // [AGREE_WORDS] device scratch of agree()
+  unsigned long long* agree_host = nullptr;   // pinned mirror
 };
+constexpr int AGREE_WORDS = 256;            // agree(): one status word per rank (world <= 256)
+double comm_timeout_s();                    // NBG_COMM_TIMEOUT_S
 Comm* comm_rccl(const uint8_t id[NBG_UNIQUE_ID_BYTES], int world, int rank, std::string* err);
 std::vector<Comm*> comm_local_group(int world);
 
@@ -426,6 +458,7 @@ void ws_profile(Workspace* w, int mode);   // 0 off, 1 every launch, 2 final/BFS
 int ws_profile_read(Workspace* w, nbg_kernel_stat* out, int cap);
 void ws_profile_inherit(Workspace* to, Workspace* from);   // profiling mode and counters
 uint64_t ws_cap_frontier(Workspace* w);
+uint64_t ws_cap_items(Workspace* w);   // entries + edges of one list the merge-path tiles cover
 hipError_t ws_reserve_rows(Workspace* w, uint64_t rows, int ncols);
 int64_t* ws_row_col(Workspace* w, int c);       // device pointer of output column c
 uint64_t ws_shard_cap(uint64_t n_bound, uint64_t e_bound);
@@ -483,6 +516,7 @@ hipError_t ws_end_query_wait(Workspace* w);    // wait for it (then as ws_end_qu
 constexpr uint64_t PART_ALIGN = 16384 * 4;   // npad granularity (flag / bit workgroups divide it)
 hipError_t ws_set_partition(Workspace* w, Comm* comm, uint64_t npad);
 Comm* ws_get_comm(const Workspace* w);   // the communicator of a partitioned workspace (else nullptr)
+hipStream_t ws_stream(const Workspace* w);
 hipError_t ws_exchange(Workspace* w, int step, const ExpandArgs* next0);   // replaces ws_compact
 hipError_t ws_global_stats(Workspace* w, int ntypes);      // before ws_end_query
 void ws_host_gstats(Workspace* w, unsigned long long* err, unsigned long long* step_n, unsigned long long* esum,

@@ -61,8 +61,15 @@ struct PathCtx {
   bool part = false;        // partitioned engine: collective levels and greedy
 };
 
+// A device error in the middle of a partitioned search leaves the peers in (or on their way to) the
+// next collective: abort the communicator so that they fail too instead of waiting.
 int32_t dev_fail(Engine& E, hipError_t e, const char* what) {
-  return E.fail(NBG_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+  std::string msg = std::string(what) + ": " + hipGetErrorString(e);
+  if (E.partitioned() && E.comm) {
+    if (!E.comm->last.empty()) msg += " (" + E.comm->last + ")";
+    E.comm->abort();
+  }
+  return E.fail(NBG_E_DEVICE, msg);
 }
 
 hipError_t level(PathCtx& c, const PathTypes& pt, int src, uint64_t n_bound, uint64_t e_bound, int dst,
@@ -547,9 +554,11 @@ int32_t find_path_locked(Engine& E, const nbg_path_request* rq, nbg_paths** out,
   // owner contributes), so the sum also tells every rank where each endpoint lives.  Next: the
   // OVER out-degree of the first source and in-degree of the first target (a pair's first
   // direction, summed like the rest: no set-up exchange later).
-  std::vector<unsigned long long> pres(fv.size() + tv.size() + 4, 0);
-  const size_t P_DEG = fv.size() + tv.size();
   const bool partd = E.partitioned();
+  const size_t G = partd ? (size_t)E.cfg.num_gpus : 0;
+  std::vector<unsigned long long> pres(fv.size() + tv.size() + 4 + G, 0);
+  const size_t P_DEG = fv.size() + tv.size();
+  const size_t P_ERR = P_DEG + 2;   // partitioned: one status word per rank (before the last two flags)
   auto presence = [&](uint32_t d) -> unsigned long long {
     if (d == NO_ROW) return 0;
     return partd ? (unsigned long long)E.cfg.rank * E.npad + d + 1 : 1;
@@ -576,9 +585,30 @@ int32_t find_path_locked(Engine& E, const nbg_path_request* rq, nbg_paths** out,
     if (out_edges) pres[pres.size() - 2] = 1;
     if (out_edges && !in_edges) pres[pres.size() - 1] = 1;
   }
-  if (E.partitioned()) {
+  if (partd) {
+    // Everything that can fail on this rank alone happens before the request's first collective
+    // and travels with it (one status word per rank): every rank then fails with the same code.
+    int32_t lrc = ws_release(E, &E.ws, E.stream);   // a held device GO result keeps its rows
+    std::string lmsg = lrc ? E.last_error : std::string();
+    if (!lrc) {
+      const hipError_t he = E.fault(NBG_FAULT_ALLOC)
+                                ? hipErrorOutOfMemory
+                                : ws_path_begin(E.ws, 0, E.snap.nv + fv.size() + tv.size() + 1024, true);
+      if (he != hipSuccess) {
+        lrc = NBG_E_OUT_OF_MEMORY;
+        lmsg = std::string("path workspace: ") + hipGetErrorString(he);
+      }
+    }
+    pres[P_ERR + (size_t)E.cfg.rank] = (unsigned long long)(int64_t)lrc;
     hipError_t he = ws_allreduce_host(E.ws, pres);
     if (he != hipSuccess) { delete res; return dev_fail(E, he, "path request exchange"); }
+    for (size_t q = 0; q < G; ++q) {
+      const int32_t code = (int32_t)(int64_t)pres[P_ERR + q];
+      if (!code) continue;
+      delete res;
+      if (lrc) return E.fail(lrc, lmsg);
+      return E.fail(code, "FIND PATH failed on rank " + std::to_string(q) + " (code " + std::to_string(code) + ")");
+    }
   }
   if (pres[pres.size() - 1]) {
     delete res;
@@ -599,7 +629,7 @@ int32_t find_path_locked(Engine& E, const nbg_path_request* rq, nbg_paths** out,
       Tg.push_back(td[i]);
     }
   if (Sv.empty() || Tv.empty() || rq->upto == 0 || !pres[pres.size() - 2]) { *out = res; return NBG_OK; }
-  {
+  if (!partd) {
     const int32_t rrc = ws_release(E, &E.ws, E.stream);   // a held device GO result keeps its rows
     if (rrc) { delete res; return rrc; }
   }
@@ -647,8 +677,10 @@ int32_t find_path_locked(Engine& E, const nbg_path_request* rq, nbg_paths** out,
     *out = res;
     return NBG_OK;
   }
-  hipError_t he = ws_path_begin(c.ws, 0, E.snap.nv + S.size() + Tg.size() + 1024, !(pair && !c.part));
-  if (he != hipSuccess) { delete res; return dev_fail(E, he, "path workspace"); }
+  if (!partd) {   // (partitioned: begun before the request exchange)
+    hipError_t he = ws_path_begin(c.ws, 0, E.snap.nv + S.size() + Tg.size() + 1024, !pair);
+    if (he != hipSuccess) { delete res; return dev_fail(E, he, "path workspace"); }
+  }
   int32_t rc;
   if (!rq->shortest) {
     std::vector<uint32_t> Tl;

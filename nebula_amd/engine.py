@@ -578,13 +578,34 @@ class LocalCluster:
 
     def each(self, fn):
         """Run fn(engine) on every rank concurrently; returns the per-rank results."""
-        futs = [self.pool.submit(fn, e) for e in self.engines]
-        return [f.result() for f in futs]
+        return self.each_indexed(lambda i, e: fn(e))
 
     def each_indexed(self, fn):
-        """Run fn(rank, engine) on every rank concurrently."""
+        """Run fn(rank, engine) on every rank concurrently.  Every rank's call is waited for; when
+        one raises something other than an engine status (a host-side bug, an assertion), its
+        peers may be left inside a collective, so the group is aborted to release them before
+        the first exception is re-raised (a rank that already failed returned through the
+        engine's own agreement / abort paths)."""
+        from concurrent.futures import FIRST_EXCEPTION, wait
         futs = [self.pool.submit(fn, i, e) for i, e in enumerate(self.engines)]
+        done, pending = wait(futs, return_when=FIRST_EXCEPTION)
+        if pending and any(f.exception() is not None and not isinstance(f.exception(), NbgError) for f in done):
+            self.abort()
+        wait(futs)
+        for f in futs:
+            if f.exception() is not None:
+                raise f.exception()
         return [f.result() for f in futs]
+
+    def abort(self):
+        """nbg_comm_abort on every rank: pending and later collectives fail at once."""
+        for e in self.engines:
+            e.lib.nbg_comm_abort(e.h)
+
+    def inject_fault(self, rank: int, site: int, count: int = 1):
+        """nbg_inject_fault on one rank (testing the fail-together paths)."""
+        self.engines[rank]._check(self.engines[rank].lib.nbg_inject_fault(self.engines[rank].h, site, count),
+                                  "nbg_inject_fault")
 
     @property
     def edge_types(self):
@@ -646,7 +667,7 @@ class LocalCluster:
         return res[0]
 
     def close(self):
-        self.pool.shutdown()
+        self.pool.shutdown(wait=True)
         for e in self.engines:
             e.close()
 

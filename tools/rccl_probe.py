@@ -87,6 +87,60 @@ def main():
             good = all(p == ref for p in parts)
             ok &= good
             print(f"path {s}->{t}: {ref[0] if ref else []} {'OK' if good else 'MISMATCH'}", flush=True)
+    # Failures on ONE rank: every rank must return the same code (agreed before the query's first
+    # collective) and stay usable afterwards (include/nbg.h, failure semantics).
+    from nebula_amd import NbgError, _lib as L
+    import numpy as np
+
+    def code_of(fn):
+        try:
+            fn()
+            return 0
+        except NbgError as ex:
+            return ex.code
+
+    def agreed(name, code, want):
+        nonlocal ok
+        codes = [None] * world
+        dist.all_gather_object(codes, code)
+        good = all(c == want for c in codes)
+        ok &= good
+        if rank == 0:
+            print(f"failure {name}: codes {codes} (want {want}) {'OK' if good else 'MISMATCH'}", flush=True)
+
+    # (1) a start list whose edges exceed one rank's 2^32 list limit: duplicated hub starts, all
+    #     owned by the hub's rank; the other rank alone would have run the query
+    pairs = np.unique(np.stack([src, dst], axis=1), axis=0)   # CSR degree: distinct (src, dst)
+    hub_ids, hub_deg = np.unique(pairs[:, 0], return_counts=True)
+    hub = int(hub_ids[np.argmax(hub_deg)])
+    reps = (1 << 32) // int(hub_deg.max()) + 1
+    starts = np.full(reps, hub, dtype=np.int64)
+    agreed("hub start list", code_of(lambda: eng.go(starts, [1], 2)), L.E_UNSUPPORTED)
+    # (2) an allocation failure on the last rank only (nbg_inject_fault)
+    if rank == world - 1:
+        eng.lib.nbg_inject_fault(eng.h, L.FAULT_ALLOC, 1)
+    r0 = graphs.roots(src, 1, seed=5)[0]
+    agreed("workspace allocation (GO)", code_of(lambda: eng.go([r0], [1], 3, where)), L.E_OUT_OF_MEMORY)
+    # (3) the engines still answer, with the single engine's rows
+    mine = eng.go([r0], [1], 3, where)
+    parts = [None] * world
+    dist.all_gather_object(parts, mine)
+    if rank == 0:
+        good = graphs.sorted_rows([row for p in parts for row in p]) == graphs.sorted_rows(single.go([r0], [1], 3, where))
+        ok &= good
+        print(f"after the failures: GO {'OK' if good else 'MISMATCH'}", flush=True)
+    # (4) FIND PATH: an allocation failure on rank 0 only, then a normal request
+    s0, t0 = rmat.pick_pairs(src, dst, 1, seed=17)[0]
+    if rank == 0:
+        eng.lib.nbg_inject_fault(eng.h, L.FAULT_ALLOC, 1)
+    agreed("path workspace (FIND PATH)", code_of(lambda: eng.find_path([s0], [t0], [1], 5)), L.E_OUT_OF_MEMORY)
+    mine = eng.find_path([s0], [t0], [1], 5)
+    parts = [None] * world
+    dist.all_gather_object(parts, mine)
+    if rank == 0:
+        good = all(p == single.find_path([s0], [t0], [1], 5) for p in parts)
+        ok &= good
+        print(f"after the failures: FIND PATH {'OK' if good else 'MISMATCH'}", flush=True)
     dist.barrier()
     if rank == 0:
         print("RCCL partitioned probe:", "PASS" if ok else "FAIL", flush=True)
