@@ -279,8 +279,11 @@ int32_t nbg_find_path_wait(nbg_path_ticket* ticket, nbg_paths** out);
  * One-pair SHORTEST requests on a single engine run NBG_SP_BATCH (default 32, at most 32) at a
  * time as one batched device level loop (every launch serves the whole batch; each of the batch's
  * workspaces holds 3 label arrays and 5 list buffers of nv entries); other requests run as
- * nbg_find_path would.  Results equal nbg_find_path's.  Returns NBG_OK unless the batch itself
- * could not run (arguments, device set-up). */
+ * nbg_find_path would.  Results equal nbg_find_path's.  Every request gets its status in rcs[i]
+ * (out[i] is NULL exactly when rcs[i] != NBG_OK), also when the batch itself fails part way (the
+ * requests that did not run carry that failure's code).  Returns NBG_OK unless the batch itself
+ * could not run (arguments, device set-up).  The batched chains use as many per-pair contexts
+ * (~72 B per vertex each) as NBG_SP_BATCH asks for and HBM allows. */
 int32_t nbg_find_path_batch(nbg_engine* e, const nbg_path_request* reqs, uint64_t n, nbg_paths** out,
                             int32_t* rcs);
 int64_t nbg_paths_count(const nbg_paths* p);

@@ -96,7 +96,7 @@ struct DevEdgeType {            // CSR for one signed edge type over this rank's
   // Superseded versions (multi-version data only): a CSR of the older versions of every edge, in
   // key order, with h_grp[i] = the live edge (index into this CSR's parent) of version i.  Read
   // by GetNeighbors' filtered walk, which sees older versions until an edge is accepted
-  // (QueryBaseProcessor.inl:394-456).  Owned by the parent; not persisted by snapshot_save.
+  // (QueryBaseProcessor.inl:394-456).  Owned by the parent; persisted by snapshot_save (format 2).
   DevEdgeType* old = nullptr;
   std::vector<uint32_t> h_grp;
 };

@@ -899,15 +899,27 @@ int32_t nbg_find_path_batch(nbg_engine* h, const nbg_path_request* reqs, uint64_
     out[i] = res;
   }
   if (pl.empty()) return NBG_OK;
-  const int B = sp_batch_size();
+  // From here on every deferred request gets its own status: a batch-level failure marks the
+  // requests that did not run (out[i] stays NULL only where rcs[i] != NBG_OK, nbg.h)
+  std::vector<char> ran(pl.size(), 0);
+  auto fail_rest = [&](int32_t code) {
+    for (size_t k = 0; k < pl.size(); ++k)
+      if (!ran[k]) rcs[at[k]] = code;
+    return code;
+  };
   if (!E.batch_stream && hipStreamCreateWithFlags(&E.batch_stream, hipStreamNonBlocking) != hipSuccess)
-    return E.fail(NBG_E_DEVICE, "hipStreamCreate failed");
-  while ((int)E.batch_sp.size() < std::min<int>(B, (int)pl.size())) {
-    std::string err;
-    SpCtx* c = sp_create(E.snap.nv, E.sp_item_cap(), E.sp_edge_cap(), E.batch_stream, &err);
-    if (!c) return E.fail(NBG_E_OUT_OF_MEMORY, err);
+    return fail_rest(E.fail(NBG_E_DEVICE, "hipStreamCreate failed"));
+  // batch contexts (each holds ~72 B per vertex): as many as NBG_SP_BATCH asks for and HBM
+  // allows — a context that cannot be allocated only makes the batches smaller
+  const int want = std::min<int>(sp_batch_size(), (int)pl.size());
+  std::string cerr;
+  while ((int)E.batch_sp.size() < want) {
+    SpCtx* c = sp_create(E.snap.nv, E.sp_item_cap(), E.sp_edge_cap(), E.batch_stream, &cerr);
+    if (!c) break;
     E.batch_sp.push_back(c);
   }
+  if (E.batch_sp.empty()) return fail_rest(E.fail(NBG_E_OUT_OF_MEMORY, cerr));
+  const int B = std::min<int>(want, (int)E.batch_sp.size());
   for (size_t b0 = 0; b0 < pl.size(); b0 += (size_t)B) {
     const int nb = (int)std::min<size_t>((size_t)B, pl.size() - b0);
     std::vector<SpPair> sp(nb);
@@ -920,10 +932,8 @@ int32_t nbg_find_path_batch(nbg_engine* h, const nbg_path_request* reqs, uint64_
       const uint64_t i = at[b0 + p];
       SpResult r;
       if (he == hipSuccess) he = sp_wait(E.batch_sp[p], &r);
-      if (he != hipSuccess) {
-        rcs[i] = dev_fail(E, he, "shortest path");
-        continue;
-      }
+      if (he != hipSuccess) break;
+      ran[b0 + p] = 1;
       if (r.err == 1) {
         rcs[i] = E.fail(NBG_E_UNKNOWN, "shortest-path reconstruction failed (in/out edges disagree)");
       } else if (r.err) {
@@ -932,7 +942,7 @@ int32_t nbg_find_path_batch(nbg_engine* h, const nbg_path_request* reqs, uint64_
         out[i] = paths_of(r);
       }
     }
-    if (he != hipSuccess) return dev_fail(E, he, "shortest path batch");
+    if (he != hipSuccess) return fail_rest(dev_fail(E, he, "shortest path batch"));
   }
   return NBG_OK;
 }

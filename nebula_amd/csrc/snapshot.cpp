@@ -8,6 +8,9 @@
 // tag columns.  Neighbour ids of a partitioned engine are global ids (owner * npad + local id),
 // so the file is per rank and the loading engine must have the same parts / GPUs / rank and its
 // communicator attached (tag columns are gathered again).  Narrow INT copies are re-derived.
+// Format 2 also holds each type's superseded-version CSR (multi-version data: GetNeighbors' filtered
+// walk reads the older versions until an edge is accepted, QueryBaseProcessor.inl:394-456), so a
+// restored engine answers exactly as the KV-loaded one; format 1 files (no such CSR) still load.
 #include <cstdio>
 #include <cstring>
 
@@ -17,7 +20,8 @@ using namespace nbg;
 
 namespace {
 
-constexpr char kMagic[8] = {'N', 'B', 'G', 'S', 'N', 'A', 'P', '1'};
+constexpr char kMagic[8] = {'N', 'B', 'G', 'S', 'N', 'A', 'P', '2'};
+constexpr char kMagic1[8] = {'N', 'B', 'G', 'S', 'N', 'A', 'P', '1'};   // format 1: no superseded versions
 
 struct Out {
   FILE* f;
@@ -137,10 +141,8 @@ int32_t Engine::save_snapshot(const char* path) {
   o.vec(snap.h_visible);
   o.put<uint32_t>((uint32_t)snap.types.size());
   bool dl = true;
-  for (auto& kv : snap.types) {
-    const DevEdgeType& dt = kv.second;
+  auto put_csr = [&](const DevEdgeType& dt) {
     const uint64_t E = dt.num_edges;
-    o.put<int32_t>(kv.first);
     o.put<uint64_t>(E);
     o.vec(dt.h_row_ptr);
     std::vector<uint32_t> col;
@@ -165,6 +167,15 @@ int32_t Engine::save_snapshot(const char* path) {
       std::vector<uint8_t> v8;
       dl = dl && download(v8, dt.valid, E);
       o.vec(v8);
+    }
+  };
+  for (auto& kv : snap.types) {
+    o.put<int32_t>(kv.first);
+    put_csr(kv.second);
+    o.put<uint8_t>(kv.second.old != nullptr);
+    if (kv.second.old) {
+      put_csr(*kv.second.old);
+      o.vec(kv.second.old->h_grp);
     }
   }
   o.put<uint32_t>((uint32_t)snap.tags.size());
@@ -197,7 +208,8 @@ int32_t Engine::load_snapshot(const char* path) {
   };
   char magic[8];
   in.raw(magic, sizeof magic);
-  if (!in.ok || memcmp(magic, kMagic, sizeof kMagic)) return bad("not a snapshot file");
+  const bool v1 = in.ok && !memcmp(magic, kMagic1, sizeof kMagic1);
+  if (!in.ok || (!v1 && memcmp(magic, kMagic, sizeof kMagic))) return bad("not a snapshot file");
   const int32_t parts = in.get<int32_t>(), gpus = in.get<int32_t>(), rank = in.get<int32_t>();
   if (parts != cfg.num_parts || gpus != cfg.num_gpus || rank != cfg.rank)
     return bad("written for another partitioning (parts / GPUs / rank)");
@@ -220,13 +232,12 @@ int32_t Engine::load_snapshot(const char* path) {
     return bad("vertex id space");
   // neighbour ids index [nv) on one GPU, the global id space [G * npad) when partitioned
   const uint64_t id_space = partitioned() ? (uint64_t)cfg.num_gpus * npad : nv;
-  const uint32_t nt = in.get<uint32_t>();
-  for (uint32_t k = 0; in.ok && k < nt; ++k) {
-    const int32_t type = in.get<int32_t>();
-    DevEdgeType& dt = snap.types[type];
+  // one CSR (a type's, or its superseded versions') read, validated and uploaded into dt
+  auto get_csr = [&](DevEdgeType& dt, int32_t type, const char* what) -> int32_t {
     dt.type = type;
     dt.num_edges = in.get<uint64_t>();
     const uint64_t E = dt.num_edges;
+    const std::string name = std::string(what) + " " + std::to_string(type);
     dt.h_row_ptr = in.vec<uint32_t>();
     std::vector<uint32_t> col = in.vec<uint32_t>();
     std::vector<int64_t> dvid = in.vec<int64_t>(), rk;
@@ -245,18 +256,33 @@ int32_t Engine::load_snapshot(const char* path) {
     bool sizes = dt.h_row_ptr.size() == nv + 1 && col.size() == E && dvid.size() == E && (!has_rank || rk.size() == E) &&
                  (!has_valid || valid.size() == E) && dt.h_row_ptr[nv] == E;
     for (auto& c : pc) sizes = sizes && c.size() == E;
-    if (!in.ok || !sizes) return bad("edge type " + std::to_string(type));
-    if (dt.h_row_ptr[0] != 0) return bad("edge type " + std::to_string(type) + ": row offsets");
+    if (!in.ok || !sizes) return bad(name);
+    if (dt.h_row_ptr[0] != 0) return bad(name + ": row offsets");
     for (uint64_t d = 0; d < nv; ++d)
-      if (dt.h_row_ptr[d] > dt.h_row_ptr[d + 1]) return bad("edge type " + std::to_string(type) + ": row offsets");
+      if (dt.h_row_ptr[d] > dt.h_row_ptr[d + 1]) return bad(name + ": row offsets");
     for (uint32_t c : col)
-      if (c != NO_ROW && c >= id_space) return bad("edge type " + std::to_string(type) + ": neighbour id");
+      if (c != NO_ROW && c >= id_space) return bad(name + ": neighbour id");
     for (VKind k : kinds)
-      if (k > VK_STRING) return bad("edge type " + std::to_string(type) + ": column kind");
+      if (k > VK_STRING) return bad(name + ": column kind");
     if (!upload_type(dt, nv, col, dvid, has_rank ? &rk : nullptr, pc, has_valid ? &valid : nullptr, kinds)) {
       fclose(f);
       free_snapshot();
       return fail(NBG_E_OUT_OF_MEMORY, "device allocation failed for the snapshot");
+    }
+    return NBG_OK;
+  };
+  const uint32_t nt = in.get<uint32_t>();
+  for (uint32_t k = 0; in.ok && k < nt; ++k) {
+    const int32_t type = in.get<int32_t>();
+    DevEdgeType& dt = snap.types[type];
+    if (int32_t rc = get_csr(dt, type, "edge type")) return rc;
+    if (!v1 && in.get<uint8_t>() != 0) {
+      dt.old = new DevEdgeType();
+      if (int32_t rc = get_csr(*dt.old, type, "superseded versions of edge type")) return rc;
+      dt.old->h_grp = in.vec<uint32_t>();
+      bool ok = in.ok && dt.old->h_grp.size() == dt.old->num_edges;
+      for (uint32_t g : dt.old->h_grp) ok = ok && g < dt.num_edges;
+      if (!ok) return bad("superseded versions of edge type " + std::to_string(type) + ": live edge index");
     }
   }
   const uint32_t ntag = in.get<uint32_t>();
@@ -295,7 +321,7 @@ int32_t Engine::load_snapshot(const char* path) {
     }
   }
   in.raw(magic, sizeof magic);
-  if (!in.ok || memcmp(magic, kMagic, sizeof kMagic)) return bad("truncated");
+  if (!in.ok || memcmp(magic, v1 ? kMagic1 : kMagic, sizeof kMagic)) return bad("truncated");
   fclose(f);
   int32_t rc = upload_tags();
   if (!rc) rc = upload_vertices(snap.h_visible, snap.h_visible.empty());

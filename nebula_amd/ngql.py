@@ -22,7 +22,7 @@ from .vidhash import std_hash
 
 _TOK = re.compile(r"""\s*(?:
     (?P<double>\d+\.\d*(?:[eE][+-]?\d+)?|\.\d+(?:[eE][+-]?\d+)?)
-   |(?P<int>0[xX][0-9a-fA-F]+|0[0-7]+|\d+)
+   |(?P<int>0[xX][0-9a-fA-F]+|\d+)
    |(?P<str>"(?:[^"\\]|\\.)*"|'(?:[^'\\]|\\.)*')
    |(?P<var>\$[A-Za-z_]\w*)
    |(?P<sym>\$\^|\$\$|\$-|<=|>=|==|!=|&&|\|\||[<>+\-*/%^!(),.;|=])
@@ -32,6 +32,29 @@ _TOK = re.compile(r"""\s*(?:
 
 class ParseError(Exception):
     pass
+
+
+def int_literal(text: str) -> int:
+    """An INTEGER token as scanner.lex:328-368 reads it.  Flex takes the longest match, first rule
+    on a tie: `0[Xx]{HEX}+` (sscanf %lx), `0{OCT}+` (%lo), `{DEC}+` (folly::to<int64_t>) — so
+    "0777" is octal but "09" and "0789" are decimal (the decimal match is longer).  Hex with more
+    than 16 significant digits and octal with more than 22 (or 22 not starting with 1) stop the
+    scan; the sscanf conversions wrap into int64, the decimal one rejects out-of-range values."""
+    if text[:2] in ("0x", "0X"):
+        if len(text[2:].lstrip("0")) > 16:
+            raise ParseError(f"hex literal out of range: {text}")
+        v = int(text, 16)
+        return v - (1 << 64) if v >= 1 << 63 else v
+    if len(text) > 1 and text[0] == "0" and all(c in "01234567" for c in text):
+        sig = text[1:].lstrip("0")
+        if len(sig) > 22 or (len(sig) == 22 and sig[0] != "1"):
+            raise ParseError(f"octal literal out of range: {text}")
+        v = int(text, 8)
+        return v - (1 << 64) if v >= 1 << 63 else v
+    v = int(text, 10)
+    if v >= 1 << 63:
+        raise ParseError(f"integer out of range: {text}")
+    return v
 
 
 def tokenize(s: str):
@@ -345,19 +368,8 @@ class Parser:
 
     def primary(self):
         kind, text = self.take()
-        if kind == "int":   # scanner.lex:328-368: hex (%lx), octal (%lo), decimal
-            if text[:2] in ("0x", "0X"):
-                v = int(text, 16)
-            elif len(text) > 1 and text[0] == "0":
-                v = int(text, 8)
-            else:
-                v = int(text)
-            if v >= 1 << 63:
-                if text[:2] in ("0x", "0X") or text[0] == "0":
-                    v -= 1 << 64   # the sscanf into int64_t wraps
-                else:
-                    raise ParseError(f"integer out of range: {text}")
-            return E.const(v)
+        if kind == "int":
+            return E.const(int_literal(text))
         if kind == "double":
             return E.const(float(text))
         if kind == "str":

@@ -389,3 +389,17 @@ def test_partitioned_input_props_backtracker(world, steps):
     finally:
         c.close()
         orc.close()
+
+
+def test_partitioned_shortest_forward_bsets_switch():
+    """NBG_PART_FWD_BSETS=1 (off by default): the forward B-set recovery past kf gives
+    the single engine's paths and scanned-edge counts.  The switch is read once per process, so
+    the check runs in a child process started with it set."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, NBG_PART_FWD_BSETS="1", NBG_COMM_TIMEOUT_S="60")
+    p = subprocess.run([sys.executable, os.path.join(root, "tests", "support", "fwd_bsets_probe.py")], cwd=root,
+                       env=env, capture_output=True, text=True, timeout=180)
+    assert p.returncode == 0 and "PASS" in p.stdout, p.stdout[-3000:] + p.stderr[-3000:]
