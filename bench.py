@@ -144,10 +144,11 @@ def go_leg(eng, stmt, roots, args, barrier, inflight, profile=True):
     barrier()
     elapsed = time.perf_counter() - t0
     lats = []
-    for r in roots:   # per-query latency: one query at a time
-        q0 = time.perf_counter()
-        stmt.run_device([r]).free()
-        lats.append(time.perf_counter() - q0)
+    for _ in range(4):   # per-query latency: one query at a time, 4 passes over the roots
+        for r in roots:
+            q0 = time.perf_counter()
+            stmt.run_device([r]).free()
+            lats.append(time.perf_counter() - q0)
     out = {"scanned": scanned, "rows": rows, "elapsed": elapsed, "lat": lats}
     if profile and not args.no_profile:
         # roofline pass: the same K steps with HIP events around every launch of the dominant
@@ -220,23 +221,31 @@ def roofline_of(g, workload, steps):
 
 def host_delivered(stmt, roots):
     """nbg_go semantics (rows copied to host memory, what ExecutionResponse carries): rows/s and
-    the device-to-host GB/s of the 8-byte cells."""
+    the device-to-host GB/s of the 8-byte cells.  Per query: nbg_go_execute (device), then
+    nbg_rows_fetch: the device packs the row segments and DMAs them into a pinned block of the
+    engine's pool (one untimed query first grows the pool, as a server's first response would)."""
+    res = stmt.run_device([roots[0]])
+    res.fetch_bits(copy=False)
+    res.free()
     rows = cells = 0
     t0 = time.perf_counter()
     for r in roots:
         res = stmt.run_device([r])
-        cols = res.fetch_bits()
+        cols = res.fetch_bits(copy=False)   # views of the pinned host copy (valid until free)
         rows += res.count
         cells += sum(len(c) for c in cols)
         res.free()
     el = time.perf_counter() - t0
     return {"queries": len(roots), "rows": rows, "seconds": round(el, 4), "rows_per_s": rows / el if el else None,
             "d2h_GBs": cells * 8 / el / 1e9 if el else None,
-            "timing": "nbg_go_execute (device) + nbg_rows_fetch of every row, one query at a time"}
+            "timing": "nbg_go_execute (device) + nbg_rows_fetch of every row into host memory, one query at a "
+                      "time, query time included"}
 
 
 def shortest_path_leg(eng, pairs, args, barrier, batch=True):
     """FIND SHORTEST PATH FROM s TO t OVER e UPTO n STEPS, one query per pair (C4)."""
+    if not args.sync:   # shortest-path contexts allocated now (start-up), not inside the first timed query
+        eng.path_reserve(int(os.environ.get("NBG_QUERY_SLOTS", "6")), int(os.environ.get("NBG_SP_BATCH", "32")))
     for s, t in pairs[:16]:   # warm-up
         eng.find_path([s], [t], [1], args.sp_upto)
     # the requests are input: their C structs are built before the clock, and each query is one
@@ -312,8 +321,12 @@ def shortest_path_leg(eng, pairs, args, barrier, batch=True):
                    "teps": b_edges / b_el if b_el else None, "seconds": round(b_el, 3), "found": b_found,
                    "timing": f"nbg_find_path_batch over the same pairs, {chunk} requests per call (request "
                              f"arrays built before the clock; results left in their nbg_paths)"}
-    kst, prof_pairs = {}, 0
-    if not args.no_profile:   # roofline pass: HIP events around k_expand<BFS> over the first pairs
+    kst, kall, prof_pairs, all_pairs = {}, {}, 0, 0
+    if not args.no_profile:
+        # roofline pass: HIP events around every step launch of the one-pair chains (k_ch_step; the
+        # host-driven loop's k_expand<BFS> on a partitioned engine), with each pair's algorithmic
+        # bytes (B_SP) from its device counters; then every launch of the chain
+        # (setup, steps, hops) over fewer pairs for the per-kernel table and launches per pair
         eng.profile(2)
         barrier()
         for s, t in pairs[:2000]:
@@ -321,28 +334,46 @@ def shortest_path_leg(eng, pairs, args, barrier, batch=True):
             prof_pairs += 1
         barrier()
         kst = eng.profile_read()
+        eng.profile(True)
+        barrier()
+        for s, t in pairs[:500]:
+            eng.find_path([s], [t], [1], args.sp_upto)
+            all_pairs += 1
+        barrier()
+        kall = eng.profile_read()
         eng.profile(False)
     lat_ms = np.array(lat) * 1e3
     out = {"query": f"FIND SHORTEST PATH FROM <s> TO <t> OVER e UPTO {args.sp_upto} STEPS",
            "pairs": len(pairs), "pairs_seed": 7, "found": found,
            "mean_hops": round(hops / found, 3) if found else None,
            "p50_ms": float(np.percentile(lat_ms, 50)), "p90_ms": float(np.percentile(lat_ms, 90)),
-           "p99_ms": float(np.percentile(lat_ms, 99)), "mean_ms": float(lat_ms.mean()),
+           "p99_ms": float(np.percentile(lat_ms, 99)), "max_ms": float(lat_ms.max()), "mean_ms": float(lat_ms.mean()),
            "teps": edges / elapsed if elapsed else None, "edges": edges, "seconds": round(elapsed, 3),
            "timing": "latency pass: one query at a time, uninstrumented; per query one nbg_find_path C call "
-                     "(request structs built before the clock)", "concurrent": conc, "batched": batched}
+                     "(request structs built before the clock; shortest-path contexts reserved before it with "
+                     "nbg_path_reserve, as a server does at start-up)", "concurrent": conc, "batched": batched}
+    ka = {k: v for k, v in kall.items() if v["launches"]} if kall else {}
+    if ka:
+        out["kernels"] = {k: {"launches": v["launches"], "launches_per_pair": round(v["launches"] / all_pairs, 3),
+                              "ms": round(v["ms"], 3), "avg_us": round(v["ms"] * 1e3 / v["launches"], 2),
+                              "algo_GBs": round(v["algo_bytes"] / (v["ms"] * 1e-3) / 1e9, 2) if v["ms"] else None}
+                          for k, v in ka.items()}
+        out["kernels_pairs"] = all_pairs
     ks = {k: v for k, v in kst.items() if v["launches"]} if kst else {}
     if ks:
-        out["kernels"] = {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
-                              "algo_GBs": round(v["algo_bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None}
-                          for k, v in ks.items()}
         name, v = max(ks.items(), key=lambda kv: kv[1]["ms"])
         ach = v["algo_bytes"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] else 0.0
-        out["roofline"] = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                           "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+        out["roofline"] = {"bound": "hbm", "kernel": name, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": None,
                            "avg_launch_us": round(v["ms"] * 1e3 / v["launches"], 2),
-                           "timing": f"HIP events around every k_expand<BFS> launch in a second pass over the "
-                                     f"first {prof_pairs} pairs; latencies come from the uninstrumented pass"}
+                           "launches_per_pair": round(v["launches"] / prof_pairs, 3),
+                           "algo_bytes_per_pair": v["algo_bytes"] / prof_pairs,
+                           "timing": f"HIP events around every {name} launch in a second pass over the first "
+                                     f"{prof_pairs} pairs; algorithmic bytes per pair = B_SP from the chain's device "
+                                     f"counters (12|F| + 4E + 4 appended per level and B-set step); latencies come "
+                                     f"from the uninstrumented pass",
+                           "note": "latency-bound: a level of a one-pair search touches a few KB; the fraction "
+                                   "shows how far the per-launch cost is from the bandwidth bound"}
     return out
 
 
@@ -444,7 +475,7 @@ def main():
     g = go_leg(eng, stmt, roots, args, barrier, inflight)
     workload = (f"RMAT-{args.scale}", len(roots)) if world == 1 and args.go_steps == 3 else None
     roofline, kernels = roofline_of(g, workload, args.steps)
-    delivered = host_delivered(stmt, roots[:4]) if world == 1 else None
+    delivered = host_delivered(stmt, roots[:8]) if world == 1 else None
     # device digests of the first headline queries (summed over ranks: rows stay where produced)
     dig = []
     for r in roots[:args.verify]:
@@ -562,7 +593,10 @@ def main():
         "cpu_baseline": cpu,
         "verification": verify,
         "query_latency_ms": {"p50": float(np.percentile(lat_ms, 50)), "p90": float(np.percentile(lat_ms, 90)),
-                             "max": float(lat_ms.max())},
+                             "p99": float(np.percentile(lat_ms, 99)), "max": float(lat_ms.max()),
+                             "queries": len(lat_ms),
+                             "timing": "one query at a time (nbg_go_execute, rows left in HBM), 4 passes over the "
+                                       "roots; the statement's row buffers were sized by nbg_go_prepare"},
         "rows_per_step": int(tot_rows) // max(1, args.steps),
         "edges_per_step": int(tot_scanned) // max(1, args.steps),
         "host_delivered": delivered,

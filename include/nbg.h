@@ -225,11 +225,16 @@ int32_t nbg_rows_num_cols(const nbg_rows* r);
 uint64_t nbg_rows_edges_scanned(const nbg_rows* r);
 /* Per-step counters: frontier size |F_s| and edges E_s, s = 1..steps (arrays of length steps). */
 int32_t nbg_rows_step_stats(const nbg_rows* r, uint64_t* frontier, uint64_t* edges, int32_t cap);
+/* Rows into host memory: the device packs the row segments into contiguous columns and DMAs them
+ * into pinned memory the engine reuses across results (returned by nbg_rows_free). */
 int32_t nbg_rows_fetch(nbg_rows* r);
 /* Host views (after nbg_go, or after nbg_rows_fetch): 8-byte cell payloads (int64, double bits,
- * bool as 0/1, string id) and value tags NBG_V_* per row. */
+ * bool as 0/1, string id) and value tags NBG_V_* per row.  The per-row tags are built on the first
+ * nbg_rows_col_tags call; nbg_rows_col_kind gives a column's NBG_V_* kind when it is the same for
+ * every row (the usual case: every OVER type yields the same kind), else -1. */
 const int64_t* nbg_rows_col_bits(const nbg_rows* r, int32_t col);
 const uint8_t* nbg_rows_col_tags(const nbg_rows* r, int32_t col);
+int32_t nbg_rows_col_kind(const nbg_rows* r, int32_t col);
 const char* nbg_rows_string(const nbg_rows* r, int64_t string_id);
 /* Device view of a column's 8-byte payloads (valid for nbg_go_device results).  Rows are not
  * contiguous: each producing workgroup appends to its own region, so the result is the union of
@@ -286,6 +291,11 @@ int32_t nbg_find_path_wait(nbg_path_ticket* ticket, nbg_paths** out);
  * (~72 B per vertex each) as NBG_SP_BATCH asks for and HBM allows. */
 int32_t nbg_find_path_batch(nbg_engine* e, const nbg_path_request* reqs, uint64_t n, nbg_paths** out,
                             int32_t* rcs);
+/* Allocate the one-pair SHORTEST contexts now instead of at their first query (what a server
+ * does at start-up): the engine's own, `slots` of nbg_find_path_submit's (at most NBG_QUERY_SLOTS)
+ * and `batch` of nbg_find_path_batch's (at most NBG_SP_BATCH).  Each context holds ~72 B per
+ * vertex plus its level-loop lists.  No-op on a partitioned engine. */
+int32_t nbg_path_reserve(nbg_engine* e, int32_t slots, int32_t batch);
 int64_t nbg_paths_count(const nbg_paths* p);
 int64_t nbg_path_len(const nbg_paths* p, int64_t i);
 const int64_t* nbg_path_entries(const nbg_paths* p, int64_t i);

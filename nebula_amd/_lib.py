@@ -29,6 +29,7 @@ E_DEVICE = -1003
 E_OUT_OF_MEMORY = -1004
 E_STATE = -1005
 FAULT_ALLOC = 1      # nbg_inject_fault sites (include/nbg.h)
+V_INT, V_DOUBLE, V_BOOL, V_STRING = 0, 1, 2, 3   # NBG_V_* value kinds
 FAULT_DEVICE = 2
 
 
@@ -104,6 +105,7 @@ SIGNATURES = [
     ("nbg_rows_fetch", i32, [vp]),
     ("nbg_rows_col_bits", P(i64), [vp, i32]),
     ("nbg_rows_col_tags", P(u8), [vp, i32]),
+    ("nbg_rows_col_kind", i32, [vp, i32]),
     ("nbg_rows_string", C.c_char_p, [vp, i64]),
     ("nbg_rows_device_col", vp, [vp, i32]),
     ("nbg_rows_num_segments", i64, [vp]),
@@ -149,6 +151,7 @@ SIGNATURES = [
     ("nbg_comm_abort", i32, [vp]),
     ("nbg_comm_aborted", i32, [vp]),
     ("nbg_inject_fault", i32, [vp, i32, i32]),
+    ("nbg_path_reserve", i32, [vp, i32, i32]),
 ]
 
 _lib = None

@@ -65,6 +65,12 @@ uint64_t Engine::sp_edge_cap() const {
   return std::max(e_out, e_in) + 1;
 }
 
+SpCtx* Engine::new_sp(hipStream_t s, std::string* err) {
+  SpCtx* c = sp_create(snap.nv, sp_item_cap(), sp_edge_cap(), s, err);
+  if (c && prof_mode) sp_profile(c, prof_mode);
+  return c;
+}
+
 uint32_t Engine::dense(int64_t vid) const {
   auto& v = snap.h_vids;
   auto it = std::lower_bound(v.begin(), v.end(), vid);
@@ -89,8 +95,11 @@ struct nbg_rows {
   bool on_device = false;
   bool fetched = false;
   std::vector<int64_t*> dcols;           // column bases; rows live in segs (disjoint regions)
-  std::vector<std::vector<int64_t>> bits;
-  std::vector<std::vector<uint8_t>> tags;
+  // host copy (nbg_rows_fetch): column c at hbits + c * count, in pinned memory from the engine's
+  // pool (DMA straight from the packed device copy, no staging and no zero-fill)
+  int64_t* hbits = nullptr;
+  size_t hbytes = 0;
+  std::vector<std::vector<uint8_t>> tags;   // per-cell kinds, built on the first nbg_rows_col_tags
   std::vector<std::string> strings;
   std::vector<Seg> segs;                 // built on first use from the per-workgroup counts
   struct TypeBlocks {
@@ -118,52 +127,134 @@ struct nbg_rows {
       }
     }
   }
+  int64_t* col(int c) const { return hbits + (uint64_t)c * count; }
+  // the kind of column c when every OVER type gives it the same one (else -1: per-cell tags)
+  int col_kind(int c) const {
+    int k = -1;
+    for (auto& kv : kinds) {
+      if ((int)kv.size() <= c) continue;
+      if (k < 0) k = kv[c];
+      else if (k != kv[c]) return -1;
+    }
+    return k < 0 ? VK_INT : k;
+  }
   uint64_t scanned = 0;
   std::vector<uint64_t> step_frontier, step_edges;
 };
 
+namespace nbg {
+
+// Pinned host blocks for fetched rows, reused across queries (a fresh pinned allocation per fetch
+// would cost more than the copy itself); at most kPinnedIdle blocks are kept idle.
+constexpr size_t kPinnedIdle = 4;
+
+void* Engine::pinned_get(size_t bytes, size_t* got) {
+  std::lock_guard<std::mutex> lg(pinned_mu);
+  size_t best = pinned_free.size();
+  for (size_t i = 0; i < pinned_free.size(); ++i)
+    if (pinned_free[i].first >= bytes && (best == pinned_free.size() || pinned_free[i].first < pinned_free[best].first))
+      best = i;
+  if (best < pinned_free.size()) {
+    void* p = pinned_free[best].second;
+    *got = pinned_free[best].first;
+    pinned_free.erase(pinned_free.begin() + (ptrdiff_t)best);
+    return p;
+  }
+  const size_t cap = std::max<size_t>(bytes + bytes / 8, 1 << 20);   // a little room to grow into
+  void* p = nullptr;
+  if (hipHostMalloc(&p, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+  *got = cap;
+  return p;
+}
+
+void Engine::pinned_put(void* p, size_t bytes) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lg(pinned_mu);
+  pinned_free.emplace_back(bytes, p);
+  if (pinned_free.size() > kPinnedIdle) {   // drop the smallest idle block
+    size_t small = 0;
+    for (size_t i = 1; i < pinned_free.size(); ++i)
+      if (pinned_free[i].first < pinned_free[small].first) small = i;
+    (void)hipHostFree(pinned_free[small].second);
+    pinned_free.erase(pinned_free.begin() + (ptrdiff_t)small);
+  }
+}
+
+void Engine::pinned_release() {
+  std::lock_guard<std::mutex> lg(pinned_mu);
+  for (auto& b : pinned_free) (void)hipHostFree(b.second);
+  pinned_free.clear();
+}
+
+}  // namespace nbg
+
 namespace {
 
+// The rows of a result into host memory: the device packs the segments into contiguous columns
+// and DMAs them into a pinned block (nbg.h nbg_rows_fetch).  Only STRING columns are touched per
+// cell on the host (dictionary code -> the result's string table).
 int32_t materialize_rows(nbg_rows* r) {
   if (r->fetched) return NBG_OK;
   r->build_segs();
-  const auto& dict = r->eng->snap.strings;
-  r->bits.assign(r->ncols, std::vector<int64_t>(r->count));
-  r->tags.assign(r->ncols, std::vector<uint8_t>(r->count));
-  {
+  Engine& E = *r->eng;
+  const auto& dict = E.snap.strings;
+  const size_t bytes = std::max<size_t>((size_t)r->count * (size_t)r->ncols * 8, 8);
+  r->hbits = static_cast<int64_t*>(E.pinned_get(bytes, &r->hbytes));
+  if (!r->hbits) return NBG_E_OUT_OF_MEMORY;
+  if (r->count) {
     std::vector<std::pair<uint64_t, uint64_t>> segs;
+    segs.reserve(r->segs.size());
     for (auto& s : r->segs) segs.emplace_back(s.begin, s.end - s.begin);
     std::vector<int64_t*> hc;
-    for (auto& b : r->bits) hc.push_back(b.data());
-    if (ws_fetch_rows(r->ws ? r->ws : r->eng->ws, segs, r->ncols, r->count, hc.data()) != hipSuccess)
+    for (int c = 0; c < r->ncols; ++c) hc.push_back(r->col(c));
+    if (ws_fetch_rows(r->ws ? r->ws : E.ws, segs, r->ncols, r->count, hc.data()) != hipSuccess)
       return NBG_E_DEVICE;
   }
-  std::unordered_map<int64_t, int64_t> sidx;
-  uint64_t o = 0;
-  for (auto& s : r->segs) {
-    uint64_t len = s.end - s.begin;
-    for (int c = 0; c < r->ncols; ++c) {
-      VKind k = r->kinds[s.type][c];
-      std::fill(r->tags[c].begin() + (ptrdiff_t)o, r->tags[c].begin() + (ptrdiff_t)(o + len), (uint8_t)k);
-      if (k != VK_STRING) continue;   // payloads are final as copied
-      for (uint64_t i = o; i < o + len; ++i) {
-        int64_t code = r->bits[c][i];
-        auto it = sidx.find(code);
-        if (it == sidx.end()) {
-          std::string txt = (code >= 0 && (code & 1) == 0 && (uint64_t)(code / 2) < dict.size())
-                                ? dict[code / 2] : r->const_str[s.type][c];
-          it = sidx.emplace(code, (int64_t)r->strings.size()).first;
-          r->strings.push_back(txt);
+  bool any_string = false;
+  for (auto& kv : r->kinds)
+    for (VKind k : kv) any_string = any_string || k == VK_STRING;
+  if (any_string) {
+    std::unordered_map<int64_t, int64_t> sidx;
+    uint64_t o = 0;
+    for (auto& s : r->segs) {
+      const uint64_t len = s.end - s.begin;
+      for (int c = 0; c < r->ncols; ++c) {
+        if (r->kinds[s.type][c] != VK_STRING) continue;   // payloads are final as copied
+        int64_t* col = r->col(c);
+        for (uint64_t i = o; i < o + len; ++i) {
+          const int64_t code = col[i];
+          auto it = sidx.find(code);
+          if (it == sidx.end()) {
+            std::string txt = (code >= 0 && (code & 1) == 0 && (uint64_t)(code / 2) < dict.size())
+                                  ? dict[code / 2] : r->const_str[s.type][c];
+            it = sidx.emplace(code, (int64_t)r->strings.size()).first;
+            r->strings.push_back(txt);
+          }
+          col[i] = it->second;
         }
-        r->bits[c][i] = it->second;
       }
+      o += len;
     }
-    o += len;
   }
   r->fetched = true;
   return NBG_OK;
 }
 
+// per-cell kinds of column c (nbg_rows_col_tags), built on first use
+const uint8_t* cell_tags(nbg_rows* r, int c) {
+  if (r->tags.empty()) r->tags.resize(r->ncols);
+  std::vector<uint8_t>& t = r->tags[c];
+  if (t.size() != r->count) {
+    t.resize(r->count);
+    uint64_t o = 0;
+    for (auto& s : r->segs) {
+      const uint64_t len = s.end - s.begin;
+      std::fill(t.begin() + (ptrdiff_t)o, t.begin() + (ptrdiff_t)(o + len), (uint8_t)r->kinds[s.type][c]);
+      o += len;
+    }
+  }
+  return t.data();
+}
 
 }  // namespace
 
@@ -529,6 +620,11 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
       ws_destroy(fresh);
       fresh = nullptr;
       err = "partition buffers";
+    }
+    if (fresh && E.row_reserve && ws_reserve_rows(fresh, E.row_reserve, E.col_reserve) != hipSuccess) {
+      ws_destroy(fresh);
+      fresh = nullptr;
+      err = "result rows";
     }
     if (!fresh) {
       local_fail(NBG_E_OUT_OF_MEMORY, err);
@@ -898,6 +994,11 @@ int32_t nbg::ws_release(Engine& E, Workspace** wsp, hipStream_t stream) {
     fresh = nullptr;
     err = "partition buffers";
   }
+  if (fresh && E.row_reserve && ws_reserve_rows(fresh, E.row_reserve, E.col_reserve) != hipSuccess) {
+    ws_destroy(fresh);
+    fresh = nullptr;
+    err = "result rows";
+  }
   if (!fresh)
     return E.fail(NBG_E_OUT_OF_MEMORY, "a held device result occupies the query workspace and a new one could not be "
                                        "allocated (" + err + "); free device results first");
@@ -1032,6 +1133,7 @@ void nbg_destroy(nbg_engine* h) {
     if (q.stream) (void)hipStreamDestroy(q.stream);
   }
   path_slots_release(E);
+  E.pinned_release();
   if (E.ws) ws_destroy(E.ws);
   if (E.sp) sp_destroy(E.sp);
   E.free_snapshot();
@@ -1135,10 +1237,38 @@ int32_t nbg_go_default_columns(nbg_engine* h, const int32_t* over, int32_t n, in
   return (int32_t)req.size();
 }
 
+// Result rows of a statement whose final frontier is a step's SET (N >= 2): the same bound
+// go_launch computes per query, so a prepared statement's first execution allocates nothing.
+static uint64_t stmt_row_bound(const Engine& E, const nbg_go_stmt* st) {
+  uint64_t cap_rows = 0;
+  for (int32_t t : st->over) {
+    auto it = E.snap.types.find(t);
+    const uint64_t eb = it == E.snap.types.end() ? 0 : it->second.num_edges;
+    cap_rows += ws_final_blk_cap(E.snap.nv, eb) * ws_final_grid(E.snap.nv, eb);
+  }
+  return cap_rows;
+}
+
 int32_t nbg_go_prepare(nbg_engine* h, const nbg_go_request* req, nbg_go_stmt** out) {
   if (!h) return NBG_E_INVALID_ARGUMENT;
-  std::lock_guard<std::mutex> lg(h->e.mu);
-  return go_prepare(h->e, req, out);
+  Engine& E = h->e;
+  std::lock_guard<std::mutex> lg(E.mu);
+  const int32_t rc = go_prepare(E, req, out);
+  if (rc || (*out)->steps < 2) return rc;
+  // GoExecutor::prepare() validates once and execute() then only runs: size the row buffers of
+  // the engine's workspace and of every query slot's now (growing a multi-GB buffer inside the
+  // first execution cost that query ~0.2 s at RMAT-26).  A failure here is not an error: the
+  // query grows (or fails) on its own.
+  if (hipSetDevice(E.cfg.device) != hipSuccess) return NBG_OK;
+  const uint64_t rows = stmt_row_bound(E, *out);
+  auto reserve = [&](Workspace* w) {
+    if (w && !E.holders.count(w)) (void)ws_reserve_rows(w, rows, (*out)->ncols);
+  };
+  reserve(E.ws);
+  for (auto& q : E.slots) reserve(q.ws);
+  E.row_reserve = std::max(E.row_reserve, rows);
+  E.col_reserve = std::max(E.col_reserve, (*out)->ncols);
+  return NBG_OK;
 }
 
 int32_t nbg_go_execute(nbg_go_stmt* st, const int64_t* starts, uint64_t num_starts, int32_t device, nbg_rows** out) {
@@ -1165,16 +1295,23 @@ int32_t nbg_rows_step_stats(const nbg_rows* r, uint64_t* frontier, uint64_t* edg
 
 int32_t nbg_rows_fetch(nbg_rows* r) {
   if (!r) return NBG_E_INVALID_ARGUMENT;
+  if (r->fetched) return NBG_OK;
+  std::lock_guard<std::mutex> lg(r->eng->mu);   // the fetch runs on the result's workspace stream
+  if (hipSetDevice(r->eng->cfg.device) != hipSuccess) return NBG_E_DEVICE;
   return materialize_rows(r);
 }
 
 const int64_t* nbg_rows_col_bits(const nbg_rows* r, int32_t col) {
   if (!r || !r->fetched || col < 0 || col >= r->ncols) return nullptr;
-  return r->bits[col].data();
+  return r->col(col);
 }
 const uint8_t* nbg_rows_col_tags(const nbg_rows* r, int32_t col) {
   if (!r || !r->fetched || col < 0 || col >= r->ncols) return nullptr;
-  return r->tags[col].data();
+  return cell_tags(const_cast<nbg_rows*>(r), col);
+}
+int32_t nbg_rows_col_kind(const nbg_rows* r, int32_t col) {
+  if (!r || col < 0 || col >= r->ncols) return -1;
+  return r->col_kind(col);
 }
 const char* nbg_rows_string(const nbg_rows* r, int64_t id) {
   if (!r || id < 0 || id >= (int64_t)r->strings.size()) return nullptr;
@@ -1204,7 +1341,7 @@ int32_t nbg_rows_digest(const nbg_rows* r, uint64_t* out) {
     for (uint64_t i = 0; i < r->count; ++i) {
       uint64_t h = 0;
       for (int c = 0; c < r->ncols; ++c) {
-        uint64_t z = (h ^ (uint64_t)r->bits[c][i]) + 0x9E3779B97F4A7C15ull;
+        uint64_t z = (h ^ (uint64_t)r->col(c)[i]) + 0x9E3779B97F4A7C15ull;
         z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
         z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
         h = z ^ (z >> 31);
@@ -1228,6 +1365,7 @@ int32_t nbg_rows_digest(const nbg_rows* r, uint64_t* out) {
 
 void nbg_rows_free(nbg_rows* r) {
   if (!r) return;
+  if (r->eng && r->hbits) r->eng->pinned_put(r->hbits, r->hbytes);
   if (r->eng && (r->owned_ws || r->ws)) {
     Engine& E = *r->eng;
     std::lock_guard<std::mutex> lg(E.mu);
@@ -1243,15 +1381,34 @@ void nbg_rows_free(nbg_rows* r) {
 
 int32_t nbg_profile(nbg_engine* h, int32_t enable) {
   if (!h) return NBG_E_INVALID_ARGUMENT;
-  std::lock_guard<std::mutex> lg(h->e.mu);
-  if (!h->e.ws) return h->e.fail(NBG_E_STATE, "engine not finalized");
-  ws_profile(h->e.ws, enable == 2 ? 2 : (enable != 0 ? 1 : 0));
+  Engine& E = h->e;
+  std::lock_guard<std::mutex> lg(E.mu);
+  if (!E.ws) return E.fail(NBG_E_STATE, "engine not finalized");
+  const int mode = enable == 2 ? 2 : (enable != 0 ? 1 : 0);
+  ws_profile(E.ws, mode);
+  // the one-pair SHORTEST contexts (device-driven chains): their launches and algorithmic bytes
+  E.prof_mode = mode;
+  sp_profile(E.sp, mode);
+  for (auto& ps : E.path_slots) sp_profile(ps.sp, mode);
+  for (SpCtx* c : E.batch_sp) sp_profile(c, mode);
   return NBG_OK;
 }
 
 int32_t nbg_profile_read(const nbg_engine* h, nbg_kernel_stat* out, int32_t cap) {
   if (!h || !out || !h->e.ws) return 0;
-  return ws_profile_read(h->e.ws, out, cap);
+  const Engine& E = h->e;
+  int n = ws_profile_read(E.ws, out, cap);
+  double launches[CHAIN_KINDS] = {}, ms[CHAIN_KINDS] = {}, bytes[CHAIN_KINDS] = {};
+  sp_profile_accum(E.sp, launches, ms, bytes);
+  for (auto& ps : E.path_slots) sp_profile_accum(ps.sp, launches, ms, bytes);
+  for (SpCtx* c : E.batch_sp) sp_profile_accum(c, launches, ms, bytes);
+  for (int k = 0; k < CHAIN_KINDS && n < cap; ++k, ++n) {
+    out[n].name = kChainKernelNames[k];
+    out[n].launches = (uint64_t)launches[k];
+    out[n].total_ms = ms[k];
+    out[n].algo_bytes = bytes[k];
+  }
+  return n;
 }
 
 int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* req, nbg_paths** out);

@@ -51,6 +51,16 @@ struct Engine {
   // launch chain, on workspaces sharing one stream
   std::vector<SpCtx*> batch_sp;
   hipStream_t batch_stream = nullptr;
+  uint64_t row_reserve = 0;             // result rows of the largest prepared GO statement (new
+  int col_reserve = 0;                  // query workspaces are sized for it before their first query)
+  int prof_mode = 0;
+  // pinned host blocks of fetched GO rows (nbg_rows_fetch), reused across queries
+  std::mutex pinned_mu;
+  std::vector<std::pair<size_t, void*>> pinned_free;
+  void* pinned_get(size_t bytes, size_t* got);
+  void pinned_put(void* p, size_t bytes);
+  void pinned_release();                    // nbg_profile mode (applied to shortest-path contexts made later)
+  SpCtx* new_sp(hipStream_t s, std::string* err);   // sp_create for this snapshot + the profile mode
   uint64_t sp_item_cap() const;         // items a shortest-path list may hold
   uint64_t sp_edge_cap() const;         // edges of the larger direction (a level's edge space)
   std::vector<void*> inflight;          // submitted tickets, oldest first

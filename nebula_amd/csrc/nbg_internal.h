@@ -321,6 +321,8 @@ struct SpResult {                    // one query's result block (device, copied
   unsigned long long edges;          // BFS adjacency entries scanned (both sides)
   unsigned long long err;            // 1 reconstruction failure, 2 spin bound, 3 list overflow
   unsigned long long levels;         // BFS levels run
+  unsigned long long abytes;         // algorithmic bytes of its level / B-set launches (chain mode)
+  unsigned long long launches;       // device launches of its chain (setup + steps + hops)
   long long path[1 + 3 * MAX_PATH_LEN];   // [v0, t0, r0, v1, ...]
   // phase trace (wall_clock64 ticks): trace[0] = launch start, then (kind << 56 | tick) per phase
   unsigned long long ntrace;
@@ -364,6 +366,14 @@ struct ChainQuery {
 };
 hipError_t chain_launch_batch(ChainCtx* const* cs, int n, const ChainQuery* qs);
 void chain_result(const ChainCtx* c, SpResult* out);
+constexpr int CHAIN_KINDS = 6;                       // profiled chain launch kinds
+extern const char* const kChainKernelNames[CHAIN_KINDS];
+void chain_profile(ChainCtx* c, int mode);           // nbg_profile modes; resets the counters
+void chain_profile_done(ChainCtx* c, const SpResult& r);
+void chain_profile_accum(const ChainCtx* c, double* launches, double* ms, double* bytes);
+void sp_profile(SpCtx* c, int mode);
+hipError_t sp_reserve_chain(SpCtx* c);               // the level-loop buffers now, not at the first query
+void sp_profile_accum(const SpCtx* c, double* launches, double* ms, double* bytes);
 hipError_t sp_wait(SpCtx* c, SpResult* out);
 
 // ----------------------------------------------------------------------------- collectives (comm.cpp)

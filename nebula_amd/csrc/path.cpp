@@ -355,7 +355,7 @@ int32_t device_pair(PathCtx& c, int mode, uint32_t s, uint32_t t, uint32_t upto,
   Engine& E = c.E;
   if (!E.sp) {
     std::string err;
-    E.sp = sp_create(E.snap.nv, E.sp_item_cap(), E.sp_edge_cap(), E.stream, &err);
+    E.sp = E.new_sp(E.stream, &err);
     if (!E.sp) return E.fail(NBG_E_OUT_OF_MEMORY, err);
   }
   if (!host_degree(c, c.fwd, s) || !host_degree(c, c.bwd, t)) return NBG_OK;   // an endpoint without edges
@@ -836,7 +836,7 @@ int32_t nbg_find_path_submit(nbg_engine* h, const nbg_path_request* rq, nbg_path
   }
   if (!ps.sp) {
     std::string err;
-    ps.sp = sp_create(E.snap.nv, E.sp_item_cap(), E.sp_edge_cap(), ps.stream, &err);
+    ps.sp = E.new_sp(ps.stream, &err);
     if (!ps.sp) { delete t; return E.fail(NBG_E_OUT_OF_MEMORY, err); }
   }
   hipError_t he = sp_launch(ps.sp, pl.mode, pl.fwd, pl.bwd, E.snap.d_visible, E.snap.d_vids, pl.s, pl.t, pl.upto);
@@ -873,7 +873,7 @@ int32_t nbg_find_path_batch(nbg_engine* h, const nbg_path_request* reqs, uint64_
       res = new nbg_paths();
       if (!E.sp) {
         std::string err;
-        E.sp = sp_create(E.snap.nv, E.sp_item_cap(), E.sp_edge_cap(), E.stream, &err);
+        E.sp = E.new_sp(E.stream, &err);
         if (!E.sp) {
           delete res;
           rcs[i] = E.fail(NBG_E_OUT_OF_MEMORY, err);
@@ -914,7 +914,7 @@ int32_t nbg_find_path_batch(nbg_engine* h, const nbg_path_request* reqs, uint64_
   const int want = std::min<int>(sp_batch_size(), (int)pl.size());
   std::string cerr;
   while ((int)E.batch_sp.size() < want) {
-    SpCtx* c = sp_create(E.snap.nv, E.sp_item_cap(), E.sp_edge_cap(), E.batch_stream, &cerr);
+    SpCtx* c = E.new_sp(E.batch_stream, &cerr);
     if (!c) break;
     E.batch_sp.push_back(c);
   }
@@ -943,6 +943,41 @@ int32_t nbg_find_path_batch(nbg_engine* h, const nbg_path_request* reqs, uint64_
       }
     }
     if (he != hipSuccess) return fail_rest(dev_fail(E, he, "shortest path batch"));
+  }
+  return NBG_OK;
+}
+
+int32_t nbg_path_reserve(nbg_engine* h, int32_t slots, int32_t batch) {
+  if (!h || slots < 0 || batch < 0) return NBG_E_INVALID_ARGUMENT;
+  Engine& E = h->e;
+  std::lock_guard<std::mutex> lg(E.mu);
+  if (!E.finalized) return E.fail(NBG_E_STATE, "engine not finalized");
+  if (E.partitioned()) return NBG_OK;   // partitioned searches run on the engine's workspace
+  if (hipSetDevice(E.cfg.device) != hipSuccess) return E.fail(NBG_E_DEVICE, "hipSetDevice failed");
+  std::string err;
+  auto ready = [&](SpCtx*& c, hipStream_t s) -> int32_t {
+    if (!c) c = E.new_sp(s, &err);
+    if (!c) return E.fail(NBG_E_OUT_OF_MEMORY, err);
+    return sp_reserve_chain(c) == hipSuccess ? NBG_OK : E.fail(NBG_E_OUT_OF_MEMORY, "shortest-path chain buffers");
+  };
+  if (int32_t rc = ready(E.sp, E.stream)) return rc;
+  if (E.path_slots.empty()) E.path_slots.resize(sp_query_slots());
+  for (int i = 0; i < slots && i < (int)E.path_slots.size(); ++i) {
+    Engine::PathSlot& ps = E.path_slots[i];
+    if (!ps.stream && hipStreamCreateWithFlags(&ps.stream, hipStreamNonBlocking) != hipSuccess)
+      return E.fail(NBG_E_DEVICE, "hipStreamCreate failed");
+    if (int32_t rc = ready(ps.sp, ps.stream)) return rc;
+  }
+  const int want = std::min(batch, sp_batch_size());
+  if (want > 0 && !E.batch_stream && hipStreamCreateWithFlags(&E.batch_stream, hipStreamNonBlocking) != hipSuccess)
+    return E.fail(NBG_E_DEVICE, "hipStreamCreate failed");
+  while ((int)E.batch_sp.size() < want) {
+    SpCtx* c = nullptr;
+    if (int32_t rc = ready(c, E.batch_stream)) {
+      if (c) sp_destroy(c);
+      return rc;
+    }
+    E.batch_sp.push_back(c);
   }
   return NBG_OK;
 }

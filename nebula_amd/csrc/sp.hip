@@ -836,7 +836,27 @@ struct SpCtx {
   unsigned long long tr_n[16] = {}, tr_ticks[16] = {}, queries = 0, total_ticks = 0, sub[8] = {};
   double host_us = 0;              // level loop: host time enqueueing a query's chain
   unsigned long long host_n = 0;
+  int prof = 0;                    // nbg_profile mode, applied to the chain when it is created
 };
+
+hipError_t sp_reserve_chain(SpCtx* c) {
+  if (c->chain) return hipSuccess;
+  std::string err;
+  c->chain = chain_create(c->nv, c->edge_cap, c->stream, &err);
+  if (!c->chain) return hipErrorOutOfMemory;
+  if (c->prof) chain_profile(c->chain, c->prof);
+  return hipSuccess;
+}
+
+void sp_profile(SpCtx* c, int mode) {
+  if (!c) return;
+  c->prof = mode;
+  if (c->chain) chain_profile(c->chain, mode);
+}
+
+void sp_profile_accum(const SpCtx* c, double* launches, double* ms, double* bytes) {
+  if (c && c->chain) chain_profile_accum(c->chain, launches, ms, bytes);
+}
 
 SpCtx* sp_create(uint64_t nv, uint64_t item_cap, uint64_t edge_cap, hipStream_t s, std::string* err) {
   auto* c = new SpCtx();
@@ -922,6 +942,7 @@ hipError_t sp_launch(SpCtx* c, int mode, const SpTypes& fwd, const SpTypes& bwd,
       std::string err;
       c->chain = chain_create(c->nv, c->edge_cap, c->stream, &err);
       if (!c->chain) return hipErrorOutOfMemory;
+      if (c->prof) chain_profile(c->chain, c->prof);
     }
     const auto t0 = std::chrono::steady_clock::now();
     HIP_TRY_SP(chain_launch(c->chain, fwd, bwd, visible, vids, c->lab, c->epoch, s, t, upto));
@@ -989,6 +1010,7 @@ hipError_t sp_launch_batch(SpCtx* const* cs, int n, const SpPair* pairs) {
       std::string err;
       c->chain = chain_create(c->nv, c->edge_cap, c->stream, &err);
       if (!c->chain) return hipErrorOutOfMemory;
+      if (c->prof) chain_profile(c->chain, c->prof);
     }
     chains[p] = c->chain;
     qs[p] = ChainQuery{x.fwd, x.bwd, x.visible, x.vids, c->lab, c->epoch, x.s, x.t, x.upto};
@@ -1014,6 +1036,7 @@ hipError_t sp_wait(SpCtx* c, SpResult* out) {
       if (e != hipSuccess) return e;
     }
     chain_result(c->chain, out);
+    chain_profile_done(c->chain, *out);
     return hipSuccess;
   }
   memcpy(out, c->h_res, sizeof(SpResult));

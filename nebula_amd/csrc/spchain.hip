@@ -53,6 +53,8 @@ constexpr int CH_MAXS = 2 * MAX_PATH_LEN + 2;   // step launches of one query, a
 
 enum ChListId : int { CL_F0 = 0, CL_F1 = 1, CL_B0 = 2, CL_B1 = 3, CL_M = 4, CH_NLISTS = 5 };
 enum ChPhase : uint32_t { PH_BFS = 0, PH_BSET = 1, PH_DONE = 2 };
+// profiled launch kinds (nbg_profile_read names: kChainKernelNames)
+enum ChKind : int { CHK_SETUP = 0, CHK_STEP, CHK_HOP, CHK_SETUP_B, CHK_STEP_B, CHK_HOP_B, CH_NKINDS };
 
 }  // namespace
 
@@ -71,6 +73,9 @@ struct ChSnap {         // the search state before one step launch
   unsigned long long bcnt;             // ... of the B-set step's source list
   unsigned long long edges;            // BFS edges expanded so far
   unsigned long long levels;
+  unsigned long long abytes;           // algorithmic bytes of the step launches so far (SURVEY §8(d)
+                                       // B_SP: 4|F| ids + 8|F| row offsets + 4 E neighbour ids + 4 per
+                                       // vertex appended, for every level and B-set step)
 };
 
 struct ChState {        // device; copied back per batch up to gpart
@@ -114,8 +119,13 @@ struct ChQ {
 __host__ __device__ inline ChSnap ch_advance(const ChSnap& p, unsigned long long out, unsigned long long meets,
                                               unsigned long long macc, unsigned long long err, uint32_t upto) {
   ChSnap s = p;
+  constexpr unsigned long long M32 = 0xFFFFFFFFull;
+  auto bytes_of = [](unsigned long long src, unsigned long long dst) {
+    return 12ull * (src >> 32) + 4ull * (src & M32) + 4ull * (dst >> 32);
+  };
   if (p.phase == PH_BFS) {
     const int side = (int)p.dir;
+    s.abytes += bytes_of(p.cnt[side], out);
     if (side == 0) s.fprev = p.cnt[0];
     s.edges += p.cnt[side] & 0xFFFFFFFFull;
     s.levels += 1;
@@ -138,6 +148,9 @@ __host__ __device__ inline ChSnap ch_advance(const ChSnap& p, unsigned long long
       s.dir = (s.cnt[0] & 0xFFFFFFFFull) <= (s.cnt[1] & 0xFFFFFFFFull) ? 0u : 1u;
     }
   } else if (p.phase == PH_BSET) {
+    // (the source list of this B-set step, as ch_step chose it: pull from the forward level or push)
+    const bool pull = p.bstep == 0 && (p.fprev & M32) < (p.bcnt & M32);
+    s.abytes += bytes_of(pull ? p.fprev : p.bcnt, out);
     s.bcnt = out;
     s.bstep += 1;
     if (err) {
@@ -761,6 +774,39 @@ struct ChainCtx {
   // recent queries: step launches and path lengths used (sizes the next chain)
   double ema_steps = 6, ema_hops = 2;
   unsigned long long batches = 0, queries = 0;
+  // nbg_profile: HIP events around the chain's launches (mode 1 every launch, 2 step launches only)
+  int prof = 0;
+  bool last_batched = false;       // the query in flight ran in a batched chain
+  struct PRec { int kind; hipEvent_t a, b; };
+  std::vector<PRec> pend;
+  std::vector<hipEvent_t> pool;
+  double launches[CH_NKINDS] = {}, ms[CH_NKINDS] = {}, bytes[CH_NKINDS] = {};
+  hipEvent_t ev() {
+    if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+  // one launch between two events (kind: CHK_*), when profiling that kind
+  template <class F>
+  void timed(int kind, F&& launch) {
+    if (!prof || (prof == 2 && kind != CHK_STEP && kind != CHK_STEP_B)) { launch(); return; }
+    PRec r{kind, ev(), ev()};
+    (void)hipEventRecord(r.a, stream);
+    launch();
+    (void)hipEventRecord(r.b, stream);
+    pend.push_back(r);
+  }
+  void flush() {   // the stream has passed every pending event
+    for (auto& r : pend) {
+      float t = 0;
+      if (hipEventElapsedTime(&t, r.a, r.b) == hipSuccess) ms[r.kind] += t;
+      launches[r.kind] += 1;
+      pool.push_back(r.a);
+      pool.push_back(r.b);
+    }
+    pend.clear();
+  }
 };
 
 static constexpr size_t CH_COPY = offsetof(ChState, gpart);
@@ -807,6 +853,8 @@ void chain_destroy(ChainCtx* c) {
   if (c->d_args) (void)hipFree(c->d_args);
   if (c->h_st) (void)hipHostFree(c->h_st);
   if (c->h_args) (void)hipHostFree(c->h_args);
+  for (auto& r : c->pend) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+  for (auto e : c->pool) (void)hipEventDestroy(e);
   delete c;
 }
 
@@ -814,9 +862,13 @@ void chain_destroy(ChainCtx* c) {
 static hipError_t chain_batch(ChainCtx* c, int k, int h) {
   const ChArgs* A = c->d_args;
   for (int j = 0; j < k; ++j, ++c->steps)
-    hipLaunchKernelGGL(k_ch_step, dim3(c->grid), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps);
+    c->timed(CHK_STEP, [&] {
+      hipLaunchKernelGGL(k_ch_step, dim3(c->grid), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps);
+    });
   for (int j = 0; j < h && c->hops < CH_MAXS; ++j, ++c->hops)
-    hipLaunchKernelGGL(k_ch_hop, dim3(CH_HOP_WGS), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps - 1, c->hops);
+    c->timed(CHK_HOP, [&] {
+      hipLaunchKernelGGL(k_ch_hop, dim3(CH_HOP_WGS), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps - 1, c->hops);
+    });
   HIP_TRY_CH(hipGetLastError());
   ++c->batches;
   return hipMemcpyAsync(c->h_st, c->d_st, CH_COPY, hipMemcpyDeviceToHost, c->stream);
@@ -855,6 +907,7 @@ static hipError_t chain_prepare(ChainCtx* c, const SpTypes& fwd, const SpTypes& 
   }
   c->q = ChQ{s, t, upto, epoch, epoch, epoch};
   c->steps = c->hops = 0;
+  c->last_batched = false;
   ++c->queries;
   return hipSuccess;
 }
@@ -875,7 +928,9 @@ hipError_t chain_launch(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, con
                         const int64_t* vids, uint32_t* const lab[3], uint32_t epoch, uint32_t s, uint32_t t,
                         uint32_t upto) {
   HIP_TRY_CH(chain_prepare(c, fwd, bwd, visible, vids, lab, epoch, s, t, upto));
-  hipLaunchKernelGGL(k_ch_setup, dim3(1), dim3(CH_BLOCK), 0, c->stream, (const ChArgs*)c->d_args, c->q);
+  c->timed(CHK_SETUP, [&] {
+    hipLaunchKernelGGL(k_ch_setup, dim3(1), dim3(CH_BLOCK), 0, c->stream, (const ChArgs*)c->d_args, c->q);
+  });
   int k, h;
   chain_length(c, &k, &h);
   return chain_batch(c, k, h);
@@ -904,13 +959,20 @@ hipError_t chain_launch_batch(ChainCtx* const* cs, int n, const ChainQuery* qs) 
     h = std::max(h, (int)x.upto);
   }
   const hipStream_t st = cs[0]->stream;
-  hipLaunchKernelGGL(k_ch_setup_b, dim3((unsigned)n), dim3(CH_BLOCK), 0, st, b);
-  for (int j = 0; j < k; ++j) hipLaunchKernelGGL(k_ch_step_b, dim3((unsigned)n * b.per), dim3(CH_BLOCK), 0, st, b, j);
+  ChainCtx* c0 = cs[0];   // (the batch's launch events are kept by its first context)
+  c0->timed(CHK_SETUP_B, [&] { hipLaunchKernelGGL(k_ch_setup_b, dim3((unsigned)n), dim3(CH_BLOCK), 0, st, b); });
+  for (int j = 0; j < k; ++j)
+    c0->timed(CHK_STEP_B, [&] {
+      hipLaunchKernelGGL(k_ch_step_b, dim3((unsigned)n * b.per), dim3(CH_BLOCK), 0, st, b, j);
+    });
   for (int j = 0; j < h; ++j)
-    hipLaunchKernelGGL(k_ch_hop_b, dim3((unsigned)n * CH_HOP_WGS), dim3(CH_BLOCK), 0, st, b, k - 1, j);
+    c0->timed(CHK_HOP_B, [&] {
+      hipLaunchKernelGGL(k_ch_hop_b, dim3((unsigned)n * CH_HOP_WGS), dim3(CH_BLOCK), 0, st, b, k - 1, j);
+    });
   HIP_TRY_CH(hipGetLastError());
   for (int p = 0; p < n; ++p) {
     ChainCtx* c = cs[p];
+    c->last_batched = true;
     // a query needing fewer launches than the batch's longest ran past its end: its launches
     // returned at once (k_ch_step: phase DONE; k_ch_hop: nothing left to walk), as in chain_batch
     c->steps = k;
@@ -953,11 +1015,40 @@ void chain_result(const ChainCtx* c, SpResult* out) {
   out->err = h.err;
   out->edges = F.edges;
   out->levels = F.levels;
+  out->abytes = F.abytes;
+  out->launches = (unsigned long long)(c->steps + c->hops + 1);
   const uint32_t hpos = (uint32_t)(h.hstart[c->hops] >> 32);
   out->L = (F.met && !h.err && hpos == F.L) ? F.L : 0;
   if (F.met && !h.err && hpos != F.L) out->err = 2;   // (cannot happen: the hops were enqueued)
   out->ntrace = 0;
   if (out->L) memcpy(out->path, h.path, (1 + 3 * (size_t)out->L) * sizeof(long long));
+}
+
+// nbg_profile over the chain: mode 0 off, 1 every launch, 2 step launches only (counters reset)
+void chain_profile(ChainCtx* c, int mode) {
+  c->flush();
+  c->prof = mode;
+  for (int k = 0; k < CH_NKINDS; ++k) c->launches[k] = c->ms[k] = c->bytes[k] = 0;
+}
+
+// after chain_result: resolve the query's launch events and credit its algorithmic bytes to the
+// step launches that moved them (setup and greedy hops touch O(path) bytes)
+void chain_profile_done(ChainCtx* c, const SpResult& r) {
+  if (!c->prof) return;
+  c->flush();
+  c->bytes[c->last_batched ? CHK_STEP_B : CHK_STEP] += (double)r.abytes;
+}
+
+static_assert(CH_NKINDS == CHAIN_KINDS, "chain kinds");
+const char* const kChainKernelNames[CH_NKINDS] = {"k_ch_setup", "k_ch_step", "k_ch_hop",
+                                                  "k_ch_setup_b", "k_ch_step_b", "k_ch_hop_b"};
+
+void chain_profile_accum(const ChainCtx* c, double* launches, double* ms, double* bytes) {
+  for (int k = 0; k < CH_NKINDS; ++k) {
+    launches[k] += c->launches[k];
+    ms[k] += c->ms[k];
+    bytes[k] += c->bytes[k];
+  }
 }
 
 }  // namespace nbg

@@ -63,15 +63,22 @@ class DeviceRows:
             raise NbgError(rc, "fetch failed")
         return self.eng._host_rows(self.h)
 
-    def fetch_bits(self) -> List[np.ndarray]:
+    def fetch_bits(self, copy: bool = True) -> List[np.ndarray]:
         """The rows as one int64 payload array per column (nbg_rows_col_bits; no per-cell
-        decoding — for large integer results)."""
+        decoding — for large integer results).  copy=False returns views of the result's pinned
+        host buffer, valid until free()."""
         rc = self.eng.lib.nbg_rows_fetch(self.h)
         if rc:
             raise NbgError(rc, "fetch failed")
         n, nc = self.count, self.eng.lib.nbg_rows_num_cols(self.h)
-        return [np.ctypeslib.as_array(self.eng.lib.nbg_rows_col_bits(self.h, c), shape=(n,)).copy() if n
-                else np.zeros(0, np.int64) for c in range(nc)]
+        out = []
+        for c in range(nc):
+            if not n:
+                out.append(np.zeros(0, np.int64))
+                continue
+            v = np.ctypeslib.as_array(self.eng.lib.nbg_rows_col_bits(self.h, c), shape=(n,))
+            out.append(v.copy() if copy else v)
+        return out
 
     def digest(self):
         """(rows, xor, sum) of the rows' splitmix64 chains, computed in HBM (nbg_rows_digest)."""
@@ -304,6 +311,16 @@ class Engine:
         cols = []
         for c in range(nc):
             bits = np.ctypeslib.as_array(self.lib.nbg_rows_col_bits(h, c), shape=(n,)) if n else np.zeros(0, np.int64)
+            kind = self.lib.nbg_rows_col_kind(h, c)
+            if kind == L.V_INT:   # one kind for the whole column: no per-row tags
+                cols.append(bits.tolist())
+                continue
+            if kind == L.V_DOUBLE:
+                cols.append(bits.view(np.float64).tolist())
+                continue
+            if kind == L.V_BOOL:
+                cols.append([bool(b) for b in bits.tolist()])
+                continue
             tags = np.ctypeslib.as_array(self.lib.nbg_rows_col_tags(h, c), shape=(n,)) if n else np.zeros(0, np.uint8)
             col = []
             for b, t in zip(bits.tolist(), tags.tolist()):
@@ -369,6 +386,10 @@ class Engine:
             e.ctypes.data_as(C.POINTER(C.c_int32)) if len(e) else None, len(e), int(over_all),
             t.ctypes.data_as(C.POINTER(C.c_int64)) if len(t) else None, len(t), upto, int(shortest))
         return req, (f, t, e)
+
+    def path_reserve(self, slots: int = 6, batch: int = 32):
+        """nbg_path_reserve: the one-pair SHORTEST contexts up front (server start-up)."""
+        self._check(self.lib.nbg_path_reserve(self.h, slots, batch), "nbg_path_reserve")
 
     def find_path_submit(self, frm, to, etypes, upto=5, shortest=True, over_all=False):
         """nbg_find_path_submit: a one-pair SHORTEST query on a free query slot (others run now);
