@@ -236,10 +236,30 @@ def host_delivered(stmt, roots):
         cells += sum(len(c) for c in cols)
         res.free()
     el = time.perf_counter() - t0
-    return {"queries": len(roots), "rows": rows, "seconds": round(el, 4), "rows_per_s": rows / el if el else None,
-            "d2h_GBs": cells * 8 / el / 1e9 if el else None,
-            "timing": "nbg_go_execute (device) + nbg_rows_fetch of every row into host memory, one query at a "
-                      "time, query time included"}
+    out = {"queries": len(roots), "rows": rows, "seconds": round(el, 4), "rows_per_s": rows / el if el else None,
+           "d2h_GBs": cells * 8 / el / 1e9 if el else None,
+           "timing": "nbg_go_execute (device) + nbg_rows_fetch of every row into host memory, one query at a "
+                     "time, query time included"}
+    # the host link itself: one pinned device-to-host copy of the same per-query size (torch as
+    # plumbing), so d2h_GBs reads as a fraction of what the box's link delivers
+    try:
+        import torch
+        if torch.cuda.is_available() and rows:
+            n = int(cells / len(roots))
+            src = torch.empty(n, dtype=torch.int64, device="cuda")
+            dst = torch.empty(n, dtype=torch.int64, pin_memory=True)
+            dst.copy_(src)
+            torch.cuda.synchronize()
+            reps = 4
+            l0 = time.perf_counter()
+            for _ in range(reps):
+                dst.copy_(src)
+            torch.cuda.synchronize()
+            out["link_d2h_GBs"] = reps * n * 8 / (time.perf_counter() - l0) / 1e9
+            del src, dst
+    except Exception as ex:  # pragma: no cover
+        log(f"link probe unavailable: {ex}")
+    return out
 
 
 def shortest_path_leg(eng, pairs, args, barrier, batch=True):

@@ -205,9 +205,7 @@ int32_t materialize_rows(nbg_rows* r) {
     std::vector<std::pair<uint64_t, uint64_t>> segs;
     segs.reserve(r->segs.size());
     for (auto& s : r->segs) segs.emplace_back(s.begin, s.end - s.begin);
-    std::vector<int64_t*> hc;
-    for (int c = 0; c < r->ncols; ++c) hc.push_back(r->col(c));
-    if (ws_fetch_rows(r->ws ? r->ws : E.ws, segs, r->ncols, r->count, hc.data()) != hipSuccess)
+    if (ws_fetch_rows_pinned(r->ws ? r->ws : E.ws, segs, r->ncols, r->count, r->hbits) != hipSuccess)
       return NBG_E_DEVICE;
   }
   bool any_string = false;

@@ -2313,6 +2313,48 @@ hipError_t ws_fetch_rows(Workspace* w, const std::vector<std::pair<uint64_t, uin
   return e;
 }
 
+// Rows into a pinned host block (columns back to back, `total` rows each).  Default: packed on the
+// device, then one DMA per column (above).  NBG_FETCH=direct: the packing kernel stores over the
+// host link itself (no staging copy).  Both reach the same ~16 GB/s on the measured box (the
+// host link, profiles/r03_c_*), so the DMA path stays the default.
+hipError_t ws_fetch_rows_pinned(Workspace* w, const std::vector<std::pair<uint64_t, uint64_t>>& segs, int ncols,
+                                uint64_t total, int64_t* host_block) {
+  if (!total || !ncols) return hipSuccess;
+  static const bool dma = !getenv("NBG_FETCH") || strcmp(getenv("NBG_FETCH"), "direct") != 0;
+  void* dptr = nullptr;
+  if (dma || hipHostGetDevicePointer(&dptr, host_block, 0) != hipSuccess || !dptr) {
+    std::vector<int64_t*> hc(ncols);
+    for (int c = 0; c < ncols; ++c) hc[c] = host_block + (uint64_t)c * total;
+    return ws_fetch_rows(w, segs, ncols, total, hc.data());
+  }
+  std::vector<uint64_t> meta;
+  uint64_t o = 0;
+  for (auto& sg : segs) {
+    if (!sg.second) continue;
+    meta.push_back(sg.first);
+    meta.push_back(sg.second);
+    meta.push_back(o);
+    o += sg.second;
+  }
+  if (o != total) return hipErrorInvalidValue;
+  if (meta.size() * 8 > w->fetch_meta_cap) {
+    if (w->fetch_meta) {
+      HIP_TRY(ws_sync(w));
+      (void)hipFree(w->fetch_meta);
+      w->fetch_meta = nullptr;
+      w->fetch_meta_cap = 0;
+    }
+    HIP_TRY(hipMalloc((void**)&w->fetch_meta, meta.size() * 8));
+    w->fetch_meta_cap = meta.size() * 8;
+  }
+  HIP_TRY(hipMemcpyAsync(w->fetch_meta, meta.data(), meta.size() * 8, hipMemcpyHostToDevice, w->stream));
+  const int nseg = (int)(meta.size() / 3);
+  hipLaunchKernelGGL(k_pack_rows, dim3((unsigned)(nseg < 4096 ? nseg : 4096)), dim3(BLOCK), 0, w->stream,
+                     w->fetch_meta, nseg, (int64_t* const*)w->d_row_cols, ncols, static_cast<int64_t*>(dptr), total);
+  HIP_TRY(hipGetLastError());
+  return ws_sync(w);
+}
+
 hipError_t ws_rows_digest(Workspace* w, const std::vector<std::pair<uint64_t, uint64_t>>& segs, int ncols,
                           uint64_t out[3]) {
   out[0] = out[1] = out[2] = 0;

@@ -479,6 +479,8 @@ unsigned ws_final_grid_of(Workspace* w, int tix);          // grid of the last f
 const uint32_t* ws_host_blk_rows(Workspace* w, int tix);    // rows per workgroup (after ws_end_query)
 hipError_t ws_fetch_rows(Workspace* w, const std::vector<std::pair<uint64_t, uint64_t>>& segs, int ncols,
                          uint64_t total, int64_t* const* host_cols);
+hipError_t ws_fetch_rows_pinned(Workspace* w, const std::vector<std::pair<uint64_t, uint64_t>>& segs, int ncols,
+                                uint64_t total, int64_t* host_block);   // pinned, columns back to back
 // order-independent digest {rows, xor, sum} of the rows in segs (splitmix64 chain per row)
 hipError_t ws_rows_digest(Workspace* w, const std::vector<std::pair<uint64_t, uint64_t>>& segs, int ncols,
                           uint64_t out[3]);
