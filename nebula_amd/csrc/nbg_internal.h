@@ -607,4 +607,29 @@ hipError_t ws_allreduce_host(Workspace* w, std::vector<unsigned long long>& v);
 hipError_t ws_path_greedy_part(Workspace* w, const PathTypes& bwd, const PathGreedy& pg, const int64_t* vids,
                                const uint8_t* visible, int64_t* path);
 
+// FIND SHORTEST / ALL PATH under max_edge_returned_per_vertex (pathcap.hip): the from side walks
+// the first K out-edges of each (vertex, type), the to side the first K in-edges, as
+// FindPathExecutor sees them through getNeighbors.  Ids are global ids (single engine: dense ids);
+// partitioned, every rank calls these collectively with the same endpoints.
+struct CapEnv {
+  hipStream_t stream = nullptr;
+  Comm* comm = nullptr;          // partitioned: the communicator (nullptr: single engine)
+  int world = 1, rank = 0;
+  uint64_t nv = 0, npad = 0;     // local vertices; global id = rank * npad + local id
+  const uint8_t* visible = nullptr;
+  const int64_t* vids = nullptr; // local dense id -> vid
+  uint32_t K = 0x7fffffff;
+};
+// one path per reachable target (lexicographically smallest entry list of minimum length);
+// hipErrorNotFound: the reconstruction found no edge the B-sets promised
+hipError_t cap_shortest(const CapEnv& env, const PathTypes& fwd, const PathTypes& bwd,
+                        const std::vector<uint32_t>& Sgid, const std::vector<int64_t>& Svid,
+                        const std::vector<uint32_t>& Tgid, uint32_t upto, std::vector<std::vector<int64_t>>* out,
+                        uint64_t* scanned);
+// every valid walk of 1..upto edges; hipErrorOutOfMemory past max_walks partial walks or paths
+hipError_t cap_all(const CapEnv& env, const PathTypes& fwd, const PathTypes& bwd, const std::vector<uint32_t>& Sgid,
+                   const std::vector<int64_t>& Svid, const std::vector<uint32_t>& Tgid,
+                   const std::vector<int64_t>& Tvid, uint32_t upto, uint64_t max_walks,
+                   std::vector<std::vector<int64_t>>* out, uint64_t* scanned);
+
 }  // namespace nbg

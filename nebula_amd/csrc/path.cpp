@@ -31,8 +31,9 @@
 // takes the minimum of the ranks' candidates, one small all-gather per hop.
 //
 // In-edge records mirror out-edges (InsertEdgeExecutor.cpp:180-196 writes both), so the to-side
-// sees exactly the reverse of the from-side; with a non-default max_edge_returned_per_vertex the
-// two caps differ and the device path reports NBG_E_UNSUPPORTED.
+// sees exactly the reverse of the from-side.  With a non-default max_edge_returned_per_vertex the
+// two sides see different capped graphs and the search follows the reference's rounds instead
+// (pathcap.hip).
 #include <algorithm>
 #include <chrono>
 #include <climits>
@@ -456,6 +457,12 @@ int32_t one_sided(PathCtx& c, const std::vector<uint32_t>& S, const std::vector<
   return NBG_OK;
 }
 
+// NBG_MAX_WALKS: partial walks FIND ALL PATH may store before it reports "too many paths"
+uint64_t max_walks() {
+  static const uint64_t n = getenv("NBG_MAX_WALKS") ? strtoull(getenv("NBG_MAX_WALKS"), nullptr, 10) : (1ull << 28);
+  return n;
+}
+
 // FIND ALL PATH: backward BFS distances from the targets over in-edges (LAB_B, levels
 // 0..upto-1), then the pruned forward walk enumeration (ws_all_paths; partitioned:
 // ws_all_paths_part, walks extended at their last vertex's owner, levels all-gathered).
@@ -488,14 +495,12 @@ int32_t all_paths(PathCtx& c, const std::vector<uint32_t>& S, const std::vector<
     ds = level_dsum(c, ps, rec, 1);
   }
   uint64_t scanned = 0;
-  static const uint64_t max_walks = getenv("NBG_MAX_WALKS") ? strtoull(getenv("NBG_MAX_WALKS"), nullptr, 10)
-                                                            : (1ull << 28);
   if (c.part)
     he = ws_all_paths_part(ws, c.fwd, LAB_B, eb, Sgid.data(), Svid.data(), Sgid.size(), upto, c.E.snap.nv,
-                           c.E.snap.d_visible, max_walks, &out->paths, &scanned);
+                           c.E.snap.d_visible, max_walks(), &out->paths, &scanned);
   else
-    he = ws_all_paths(ws, c.fwd, LAB_B, eb, S.data(), S.size(), upto, c.E.snap.d_vids, c.E.snap.d_visible, max_walks,
-                      &out->paths, &scanned);
+    he = ws_all_paths(ws, c.fwd, LAB_B, eb, S.data(), S.size(), upto, c.E.snap.d_vids, c.E.snap.d_visible,
+                      max_walks(), &out->paths, &scanned);
   if (he == hipErrorOutOfMemory) return c.E.fail(NBG_E_OUT_OF_MEMORY, "FIND ALL PATH: too many paths");
   if (he != hipSuccess) return dev_fail(c.E, he, "path enumeration");
   c.edges += scanned;
@@ -518,8 +523,6 @@ int32_t find_path_locked(Engine& E, const nbg_path_request* rq, nbg_paths** out,
   if (hipSetDevice(E.cfg.device) != hipSuccess) return E.fail(NBG_E_DEVICE, "hipSetDevice failed");
   if (!rq->shortest && rq->upto > 32) return E.fail(NBG_E_UNSUPPORTED, "FIND ALL PATH UPTO exceeds 32");
   if (rq->upto > MAX_PATH_LEN) return E.fail(NBG_E_UNSUPPORTED, "UPTO exceeds the device path limit (63)");
-  if (E.cfg.max_edge_returned_per_vertex > 0 && E.cfg.max_edge_returned_per_vertex != INT_MAX)
-    return E.fail(NBG_E_UNSUPPORTED, "FIND PATH with max_edge_returned_per_vertex is not supported on the device");
   // OVER (FindPathExecutor::prepareOver)
   std::vector<int32_t> over;
   if (rq->over_all) {
@@ -616,7 +619,7 @@ int32_t find_path_locked(Engine& E, const nbg_path_request* rq, nbg_paths** out,
   }
   std::vector<uint32_t> S, Tg;        // local sources; targets by global position (NO_ROW: not here)
   std::vector<int64_t> Sv, Tv;        // their vids
-  std::vector<uint32_t> Sgid;         // partitioned: every source's global id
+  std::vector<uint32_t> Sgid, Tgid;   // partitioned: every source's / target's global id
   for (size_t i = 0; i < fv.size(); ++i)
     if (pres[i]) {
       Sv.push_back(fv[i]);
@@ -627,6 +630,7 @@ int32_t find_path_locked(Engine& E, const nbg_path_request* rq, nbg_paths** out,
     if (pres[fv.size() + i]) {
       Tv.push_back(tv[i]);
       Tg.push_back(td[i]);
+      if (partd) Tgid.push_back((uint32_t)(pres[fv.size() + i] - 1));
     }
   if (Sv.empty() || Tv.empty() || rq->upto == 0 || !pres[pres.size() - 2]) { *out = res; return NBG_OK; }
   if (!partd) {
@@ -656,6 +660,38 @@ int32_t find_path_locked(Engine& E, const nbg_path_request* rq, nbg_paths** out,
   for (int32_t t : over) {
     add(c.fwd, t);
     add(c.bwd, -t);
+  }
+  if (E.cfg.max_edge_returned_per_vertex != INT_MAX) {
+    // capped rows: the reference's rounds over the two capped graphs (pathcap.hip); every
+    // endpoint by global id (single engine: its dense id)
+    CapEnv env;
+    env.stream = ws_stream(E.ws);
+    env.comm = partd ? ws_get_comm(E.ws) : nullptr;
+    env.world = partd ? (int)G : 1;
+    env.rank = partd ? E.cfg.rank : 0;
+    env.nv = E.snap.nv;
+    env.npad = E.npad;
+    env.visible = E.snap.d_visible;
+    env.vids = E.snap.d_vids;
+    env.K = (uint32_t)E.cfg.max_edge_returned_per_vertex;
+    const std::vector<uint32_t>& sg = partd ? Sgid : S;
+    const std::vector<uint32_t>& tg = partd ? Tgid : Tg;
+    uint64_t scanned = 0;
+    const hipError_t he = rq->shortest
+                              ? cap_shortest(env, c.fwd, c.bwd, sg, Sv, tg, rq->upto, &res->paths, &scanned)
+                              : cap_all(env, c.fwd, c.bwd, sg, Sv, tg, Tv, rq->upto, max_walks(), &res->paths, &scanned);
+    int32_t rc = NBG_OK;
+    if (he == hipErrorNotFound)
+      rc = E.fail(NBG_E_UNKNOWN, "shortest-path reconstruction failed (capped rows)");
+    else if (he == hipErrorOutOfMemory)
+      rc = E.fail(NBG_E_OUT_OF_MEMORY, "FIND PATH: too many paths or out of device memory");
+    else if (he != hipSuccess)
+      rc = dev_fail(E, he, "capped FIND PATH");
+    if (rc) { delete res; return rc; }
+    std::sort(res->paths.begin(), res->paths.end());
+    res->edges = scanned;
+    *out = res;
+    return NBG_OK;
   }
   const bool pair = rq->shortest && Sv.size() == 1 && Tv.size() == 1 && Sv[0] != Tv[0];
   const int pmode = pair && !c.part ? sp_mode(c) : PM_HOST;

@@ -1,6 +1,7 @@
-"""The storage-boundary fixtures of tests/golden/querybound.json and row_codec.json as data sets
-and checks (QueryBoundTest.cpp mockData / buildRequest / checkResponse, RowReaderTest.cpp and
-RowWriterTest.cpp), usable against the oracle and the device engine alike."""
+"""The storage-boundary fixtures of tests/golden/querybound.json, querystats.json and
+row_codec.json as data sets and checks (QueryBoundTest.cpp / QueryStatsTest.cpp mockData /
+buildRequest / checkResponse, RowReaderTest.cpp and RowWriterTest.cpp), usable against the oracle
+and the device engine alike."""
 from nebula_amd import expr as E
 from nebula_amd import kvgen
 from nebula_amd.kvgen import INT, STRING
@@ -8,6 +9,7 @@ from tests.support import golden, rowcodec
 
 QB = golden.load("querybound.json")
 RC = golden.load("row_codec.json")
+QS = golden.load("querystats.json")
 INT_MAX = (1 << 31) - 1
 SRC, EDGE = 1, 3
 
@@ -120,6 +122,70 @@ def check_response(resp, case):
                     if v[7:12] != [f"string_col_{(k + 5) * 2}_{ver}" for k in range(5)]:
                         errs.append(f"vertex {vid} row {r}: strings {v[7:12]}")
     return errs[:10]
+
+
+# ------------------------------------------------------------------- QueryStatsTest.cpp
+STAT_CODES = {"SUM": 1, "COUNT": 2, "AVG": 3}
+TYPE_CODES = {"INT": INT, "DOUBLE": kvgen.DOUBLE}
+
+
+def qs_schemas(d=QS["data"]):
+    """mockSchemaMan: edge 101 with col_0..col_9 INT, col_10..col_19 STRING; tags as qb_schemas."""
+    ni, ns = d["edge_int_cols"], d["edge_string_cols"]
+    edges = {d["edge_type"]: [(f"col_{i}", INT if i < ni else STRING) for i in range(ni + ns)]}
+    ti, ts = d["tag_int_cols"], d["tag_string_cols"]
+    tags = {g: [(f"tag_{g}_col_{i}", INT if i < ti else STRING) for i in range(ti + ts)] for g in d["tags"]}
+    return edges, tags
+
+
+def qs_builder(d=QS["data"]):
+    """mockData (QueryStatsTest.cpp:20-58), parts shifted to 1..3."""
+    edges, tags = qs_schemas(d)
+    kb = kvgen.KVBuilder(len(d["parts"]))
+    n, t = d["vertices_per_part"], d["edge_type"]
+    ti, ni = d["tag_int_cols"], d["edge_int_cols"]
+    for k, part in enumerate(d["parts"]):
+        for vid in range(k * n, (k + 1) * n):
+            for g in d["tags"]:
+                vals = list(range(ti)) + [f"tag_string_col_{i}" for i in range(ti, ti + d["tag_string_cols"])]
+                kb.put(part, kvgen.vertex_key(part, vid, g, 0), kvgen.encode_row(tags[g], vals))
+            for dst in d["dsts"]:
+                vals = list(range(ni)) + [f"string_col_{i}" for i in range(ni, ni + d["edge_string_cols"])]
+                kb.put(part, kvgen.edge_key(part, vid, t, dst - d["dsts"][0], dst, 0), kvgen.encode_row(edges[t], vals))
+    return kb
+
+
+def qs_register(backend, d=QS["data"]):
+    edges, tags = qs_schemas(d)
+    for t, cols in edges.items():
+        backend.register(True, t, str(t), cols) if hasattr(backend, "register") else backend.register_edge(t, str(t), cols)
+    for g, cols in tags.items():
+        backend.register(False, g, str(g), cols) if hasattr(backend, "register") else backend.register_tag(g, str(g), cols)
+
+
+def qs_request(d=QS["data"], rq=QS["request"]):
+    """buildRequest (QueryStatsTest.cpp:61-85): (part_vids, types, returns, stat codes)."""
+    n = d["vertices_per_part"]
+    pv = [(p, vid) for k, p in enumerate(d["parts"]) for vid in range(k * n, (k + 1) * n)]
+    rets = [(SRC if o == "src" else EDGE, i, name) for o, i, name, _ in rq["returns"]]
+    return pv, rq["types"], rets, [STAT_CODES[s] for _, _, _, s in rq["returns"]]
+
+
+def check_stats(resp, exp=QS["expected"]):
+    """checkResponse (QueryStatsTest.cpp:88-133) on a bound_stats result (failed, cols, data);
+    returns a list of mismatches."""
+    failed, cols, data = resp
+    errs = []
+    if len(failed) != exp["failed"]:
+        errs.append(f"failed parts {failed}")
+    want = exp["columns"]
+    if [(c[0], c[1]) for c in cols] != [(n, TYPE_CODES[t]) for n, t, _ in want]:
+        errs.append(f"columns {[(c[0], c[1]) for c in cols]}")
+        return errs
+    vals = rowcodec.decode_row(data, [TYPE_CODES[t] for _, t, _ in want])
+    if vals != [v for _, _, v in want]:
+        errs.append(f"values {vals}")
+    return errs
 
 
 def codec_rows():

@@ -119,3 +119,22 @@ def test_snapshot_roundtrip_keeps_superseded_versions(qb, tmp_path):
             assert F.check_response(got, case) == []
     finally:
         re.close()
+
+
+def test_querystats_pinned_on_gpu():
+    """QueryStatsTest.cpp StatsSimpleTest on the device (nbg_bound_stats): the reference's
+    checkResponse expectations hold and the response equals the oracle's byte for byte."""
+    parts = len(F.QS["data"]["parts"])
+    eng, orc = Engine(parts), Oracle(parts)
+    try:
+        kb = F.qs_builder()
+        for be in (eng, orc):
+            F.qs_register(be)
+            be.load_builder(kb)
+        pv, types, rets, stats = F.qs_request()
+        got = eng.bound_stats(pv, types, b"", rets, stats)
+        assert F.check_stats(got) == []
+        assert got == orc.bound_stats(pv, types, b"", rets, stats)
+    finally:
+        eng.close()
+        orc.close()

@@ -82,3 +82,17 @@ def test_row_codec_through_oracle_storage(i):
         assert rowcodec.decode_row(trow, rowcodec.value_kinds([t for _, t in cols])) == case["values"]
     finally:
         o.close()
+
+
+def test_querystats_pinned_oracle():
+    """QueryStatsTest.cpp StatsSimpleTest: boundStats over its mockData — no failed parts, the 7
+    columns in request order, AVG of the tag columns as DOUBLE 0 / 2, SUM of col_0 .. col_8 as
+    INT k * 210 (tests/golden/querystats.json)."""
+    o = Oracle(len(F.QS["data"]["parts"]))
+    try:
+        F.qs_register(o)
+        o.load_builder(F.qs_builder())
+        pv, types, rets, stats = F.qs_request()
+        assert F.check_stats(o.bound_stats(pv, types, b"", rets, stats)) == []
+    finally:
+        o.close()

@@ -17,6 +17,16 @@ querybound.json — src/storage/test/QueryBoundTest.cpp:
     behaviour of QueryBaseProcessor.inl:394-456: older versions are read until an edge is
     accepted) — expectation derived from that code, not a reference assertion.
 
+querystats.json — src/storage/test/QueryStatsTest.cpp (boundStats / QueryStatsProcessor):
+  * "data": mockData (:20-58): 3 parts x 10 vertices, tags 3001..3009 whose 3 INT columns hold
+    0, 1, 2 and 3 STRING columns "tag_string_col_<k>"; 7 out-edges of type 101 per vertex, dst
+    10001..10007 with rank dst - 10001 and version 0, 10 INT columns 0..9 and 10 STRING columns
+    "string_col_<k>" (parts 1..3 here, as for querybound.json);
+  * "request": buildRequest (:61-85): every vertex, AVG of tag_3001_col_0 and tag_3003_col_2, SUM
+    of col_0, col_2 .. col_8 over edge type 101;
+  * "expected": checkResponse (:88-133): no failed parts, 7 columns, the AVGs as DOUBLE 0 and 2,
+    the SUMs as INT k * 210 (30 vertices x 7 edges).
+
 row_codec.json — src/dataman/test/RowReaderTest.cpp:74-240 (the hand-encoded row and its
 decoded values) and :275-316 (64 INT fields with 4 block offsets), RowWriterTest.cpp:133-290
 (offsets, writing with a schema, Skip).
@@ -75,6 +85,20 @@ def querybound():
     return {"source": "src/storage/test/QueryBoundTest.cpp", "data": data, "cases": cases, "quirk": quirk}
 
 
+def querystats():
+    data = {"parts": [1, 2, 3], "vertices_per_part": 10, "tags": list(range(3001, 3010)), "tag_int_cols": 3,
+            "tag_string_cols": 3, "edge_type": 101, "dsts": list(range(10001, 10008)), "edge_int_cols": 10,
+            "edge_string_cols": 10}
+    request = {"types": [101],
+               "returns": [["src", 3001 + 2 * i, f"tag_{3001 + 2 * i}_col_{2 * i}", "AVG"] for i in range(2)] +
+                          [["edge", 101, f"col_{2 * i}", "SUM"] for i in range(5)]}
+    expected = {"failed": 0,
+                "columns": [["tag_3001_col_0", "DOUBLE", 0], ["tag_3003_col_2", "DOUBLE", 2]] +
+                           [[f"col_{2 * i}", "INT", 2 * i * 210] for i in range(5)]}
+    return {"source": "src/storage/test/QueryStatsTest.cpp", "data": data, "request": request,
+            "expected": expected}
+
+
 def row_codec():
     # RowReaderTest.encodedData (:74-148): the bytes, exactly as the test appends them
     pi = struct.unpack("<f", struct.pack("<f", 3.1415926))[0]
@@ -121,7 +145,8 @@ def row_codec():
 
 
 if __name__ == "__main__":
-    for name, obj in (("querybound.json", querybound()), ("row_codec.json", row_codec())):
+    for name, obj in (("querybound.json", querybound()), ("querystats.json", querystats()),
+                      ("row_codec.json", row_codec())):
         with open(os.path.join(OUT, name), "w") as f:
             json.dump(obj, f, indent=1)
             f.write("\n")
