@@ -400,7 +400,13 @@ def shortest_path_leg(eng, pairs, args, barrier, batch=True):
 def load_engine(scale, args, world, rank, local, comm_init):
     from nebula_amd import Engine, rmat
     t0 = time.time()
-    src, dst, w = rmat.rmat_edges_fast(scale)
+    if world > 1 and rank != 0:
+        # a rank keeps only the samples of its own parts (out-edges at the source's part, in-edges
+        # at the destination's): ~1 - (1 - 1/N)^2 of the graph, 6 GB instead of 26 GB at RMAT-26 / N = 8;
+        # rank 0 keeps them all for the CSR oracle (verification, CPU baseline mode (ii))
+        src, dst, w = rmat.rmat_edges_owned(scale, args.parts, world, rank)
+    else:
+        src, dst, w = rmat.rmat_edges_fast(scale)
     gen_s = time.time() - t0
     eng = Engine(args.parts, num_gpus=world, rank=rank, device=local)
     if world > 1:

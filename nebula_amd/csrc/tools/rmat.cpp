@@ -4,6 +4,7 @@
 #include <omp.h>
 
 #include <cstdint>
+#include <vector>
 
 namespace {
 inline uint64_t mix(uint64_t z) {
@@ -66,4 +67,61 @@ extern "C" int nbgtool_rmat_vids(uint64_t seed, const uint64_t* u, uint64_t n, i
 #pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < (int64_t)n; ++i) out[i] = (int64_t)(mix(u[i] + seed) & 0x7FFFFFFFFFFFFFFFull);
   return 0;
+}
+
+// The samples of the same graph a partitioned rank keeps: those whose source or destination lives
+// on GPU `rank` of `gpus` (part = (uint64)vid % parts + 1, GPU = part % gpus; the loader keeps
+// out-edges at the source's part and in-edges at the destination's), in sample order, so that
+// "the last of duplicate samples wins" is unchanged.  A rank then holds about 2/gpus of the
+// samples instead of all of them.  src == nullptr: returns the count only.
+extern "C" int64_t nbgtool_rmat_owned(int scale, int edge_factor, uint64_t seed, int parts, int gpus, int rank,
+                                      int64_t* src, int64_t* dst, int64_t* w) {
+  const uint64_t n = (uint64_t)edge_factor << scale;
+  const uint64_t ta = (uint64_t)(0.57 * 9007199254740992.0);
+  const uint64_t tab = (uint64_t)((0.57 + 0.19) * 9007199254740992.0);
+  const uint64_t tabc = (uint64_t)((0.57 + 0.19 + 0.19) * 9007199254740992.0);
+  constexpr uint64_t CH = 65536;
+  const uint64_t nch = (n + CH - 1) / CH;
+  auto sample = [&](uint64_t i, int64_t* s, int64_t* d) {
+    uint64_t u = 0, v = 0, base = i * 64;
+    for (int l = 0; l < scale; ++l) {
+      uint64_t r = splitmix64(seed ^ (base + (uint64_t)l)) >> 11;
+      uint64_t bu = r >= tab;
+      uint64_t bv = ((r >= ta) && (r < tab)) || (r >= tabc);
+      u |= bu << l;
+      v |= bv << l;
+    }
+    *s = (int64_t)(mix(u + seed) & 0x7FFFFFFFFFFFFFFFull);
+    *d = (int64_t)(mix(v + seed) & 0x7FFFFFFFFFFFFFFFull);
+  };
+  auto owned = [&](int64_t vid) { return (int)(((uint64_t)vid % (uint64_t)parts + 1) % (uint64_t)gpus) == rank; };
+  std::vector<int64_t> cnt(nch + 1, 0);
+#pragma omp parallel for schedule(static, 1)
+  for (int64_t c = 0; c < (int64_t)nch; ++c) {
+    int64_t k = 0;
+    const uint64_t e = ((uint64_t)c + 1) * CH < n ? ((uint64_t)c + 1) * CH : n;
+    for (uint64_t i = (uint64_t)c * CH; i < e; ++i) {
+      int64_t s, d;
+      sample(i, &s, &d);
+      k += owned(s) || owned(d);
+    }
+    cnt[c + 1] = k;
+  }
+  for (uint64_t c = 0; c < nch; ++c) cnt[c + 1] += cnt[c];
+  if (!src) return cnt[nch];
+#pragma omp parallel for schedule(static, 1)
+  for (int64_t c = 0; c < (int64_t)nch; ++c) {
+    int64_t o = cnt[c];
+    const uint64_t e = ((uint64_t)c + 1) * CH < n ? ((uint64_t)c + 1) * CH : n;
+    for (uint64_t i = (uint64_t)c * CH; i < e; ++i) {
+      int64_t s, d;
+      sample(i, &s, &d);
+      if (!(owned(s) || owned(d))) continue;
+      src[o] = s;
+      dst[o] = d;
+      w[o] = (int64_t)(splitmix64(seed ^ ~i) % 100);
+      ++o;
+    }
+  }
+  return cnt[nch];
 }

@@ -79,6 +79,30 @@ def rmat_edges_fast(scale: int, edge_factor: int = 16, seed: int | None = None):
     return src, dst, w
 
 
+def rmat_edges_owned(scale: int, parts: int, gpus: int, rank: int, edge_factor: int = 16, seed: int | None = None):
+    """The samples of rmat_edges(scale) that rank `rank` of a `gpus`-way partitioned engine keeps
+    (source or destination in one of its parts: part = vid % parts + 1, GPU = part % gpus), in
+    sample order — about 2/gpus of the graph instead of all of it (C++ tool)."""
+    import ctypes as C
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libnbgtools.so")
+    seed = (SEED_BASE ^ scale) if seed is None else seed
+    if not os.path.exists(path):
+        src, dst, w = rmat_edges(scale, edge_factor, seed)
+        own = lambda v: ((v.astype(np.uint64) % np.uint64(parts) + np.uint64(1)) % np.uint64(gpus)) == rank
+        keep = own(src) | own(dst)
+        return src[keep], dst[keep], w[keep]
+    lib = C.CDLL(path)
+    lib.nbgtool_rmat_owned.restype = C.c_int64
+    lib.nbgtool_rmat_owned.argtypes = [C.c_int, C.c_int, C.c_uint64, C.c_int, C.c_int, C.c_int,
+                                       C.c_void_p, C.c_void_p, C.c_void_p]
+    s64 = seed & 0xFFFFFFFFFFFFFFFF
+    n = lib.nbgtool_rmat_owned(scale, edge_factor, s64, parts, gpus, rank, None, None, None)
+    src, dst, w = (np.empty(n, np.int64) for _ in range(3))
+    lib.nbgtool_rmat_owned(scale, edge_factor, s64, parts, gpus, rank, src.ctypes.data, dst.ctypes.data, w.ctypes.data)
+    return src, dst, w
+
+
 def dedup_last(src, dst, w):
     """Collapse duplicate (src, dst) samples keeping the last one (for reference counting)."""
     key = np.stack([src, dst], axis=1)
