@@ -363,7 +363,10 @@ def shortest_path_leg(eng, pairs, args, barrier, batch=True):
         kall = eng.profile_read()
         eng.profile(False)
     lat_ms = np.array(lat) * 1e3
-    out = {"query": f"FIND SHORTEST PATH FROM <s> TO <t> OVER e UPTO {args.sp_upto} STEPS",
+    raw = {"lat_ms": lat_ms.tolist(), "edges": edges, "found": found, "hops": hops, "elapsed": elapsed,
+           "conc": (conc["seconds"], conc["found"]) if conc else None,
+           "batched": (batched["seconds"], batched["found"]) if batched else None}
+    out = {"_raw": raw, "query": f"FIND SHORTEST PATH FROM <s> TO <t> OVER e UPTO {args.sp_upto} STEPS",
            "pairs": len(pairs), "pairs_seed": 7, "found": found,
            "mean_hops": round(hops / found, 3) if found else None,
            "p50_ms": float(np.percentile(lat_ms, 50)), "p90_ms": float(np.percentile(lat_ms, 90)),
@@ -509,7 +512,53 @@ def main():
         dig.append(list(res.digest()) + [res.edges_scanned])
         res.free()
     stmt.free()
-    sp = shortest_path_leg(eng, pairs, args, barrier, batch=world == 1) if pairs else None
+    sp = None
+    replica = world > 1 and eng.path_replica_active
+    if pairs and replica:
+        # the FIND PATH replica (replica.hip): every rank answers its own share of the pairs
+        # rank-locally (pairs r, r + N, ...); the line reports all pairs (latencies of every rank,
+        # throughput = all pairs / the slowest rank's time), then the collective search over the
+        # partitioned snapshot on a sample for comparison
+        mine = shortest_path_leg(eng, pairs[rank::world], args, barrier, batch=True)
+        raws = [None] * world
+        dist.all_gather_object(raws, mine.pop("_raw"))
+        sp = mine
+        if rank == 0:
+            lat_ms = np.concatenate([np.array(r["lat_ms"]) for r in raws])
+            el = max(r["elapsed"] for r in raws)
+            sp.update({"pairs": len(pairs), "found": sum(r["found"] for r in raws),
+                       "mean_hops": round(sum(r["hops"] for r in raws) / max(1, sum(r["found"] for r in raws)), 3),
+                       "p50_ms": float(np.percentile(lat_ms, 50)), "p90_ms": float(np.percentile(lat_ms, 90)),
+                       "p99_ms": float(np.percentile(lat_ms, 99)), "max_ms": float(lat_ms.max()),
+                       "mean_ms": float(lat_ms.mean()), "edges": sum(r["edges"] for r in raws),
+                       "teps": sum(r["edges"] for r in raws) / el if el else None, "seconds": round(el, 3),
+                       "mode": f"FIND PATH replica on every rank, pairs split {world} ways (rank-local queries)"})
+            for key, rk in (("concurrent", "conc"), ("batched", "batched")):
+                secs = [r[rk][0] for r in raws if r[rk]]
+                if sp.get(key) and secs:
+                    sp[key]["pairs_per_s"] = len(pairs) / max(secs)
+                    sp[key]["found"] = sum(r[rk][1] for r in raws if r[rk])
+                    sp[key]["seconds"] = round(max(secs), 3)
+                    sp[key].pop("teps", None)
+        eng.set_path_replica(0)
+        coll = pairs[:min(len(pairs), 500)]
+        barrier()
+        clat = []
+        for s_, t_ in coll:
+            q0 = time.perf_counter()
+            eng.find_path([s_], [t_], [1], args.sp_upto)
+            clat.append(time.perf_counter() - q0)
+        barrier()
+        eng.set_path_replica(1)
+        if rank == 0:
+            cl = np.array(clat) * 1e3
+            sp["collective"] = {"pairs": len(coll), "p50_ms": float(np.percentile(cl, 50)),
+                                "p90_ms": float(np.percentile(cl, 90)),
+                                "timing": "the same pairs through the collective search over the partitioned "
+                                          "snapshot (nbg_set_path_replica(e, 0)), every rank calling together"}
+    elif pairs:
+        sp = shortest_path_leg(eng, pairs, args, barrier, batch=world == 1)
+        sp.pop("_raw", None)
     sp_sample = []
     if pairs and args.verify:   # device paths for the verification sample
         sp_sample = [eng.find_path([s], [t], [1], args.sp_upto) for s, t in pairs[:64]]
@@ -656,6 +705,7 @@ def c2_leg(args, barrier, inflight):
     if args.sp_pairs > 0:
         a2 = argparse.Namespace(**vars(args))
         sp = shortest_path_leg(eng, rmat.pick_pairs(src, dst, args.sp_pairs, 7, verts=av), a2, barrier)
+        sp.pop("_raw", None)
     eng.close()
     lat_ms = np.array(g["lat"]) * 1e3
     return {"graph": "RMAT-22", "roots": 64, "teps": g["scanned"] / g["elapsed"],

@@ -389,6 +389,19 @@ typedef struct {
 /* enable = 1 starts (and resets) timing of every launch; 2 times only the final-step /
  * shortest-path expansion kernels (two events per query: minimal perturbation of the timed
  * region); 0 stops timing. */
+/* ---- FIND PATH replica of a partitioned engine (replica.hip) ---------------------------------
+ * A partitioned engine (num_gpus > 1) also builds, at nbg_finalize (collectively), a replica of
+ * every rank's path CSRs (offsets, neighbour ids and vids, ranks; no property columns) when it fits
+ * in free HBM.  While it is in use, nbg_find_path / _submit / _batch / nbg_path_reserve run on it
+ * RANK-LOCALLY: no collective, each rank may answer different requests, and the results equal the
+ * single engine's over the same records.  Without it they are collectives over the partitioned
+ * snapshot (every rank calls them with the same requests).
+ * nbg_set_path_replica: before nbg_finalize, whether to build it (default: NBG_PATH_REPLICA, 1);
+ * after, whether FIND PATH uses it (1 needs a built replica: else NBG_E_STATE).  It replaces
+ * no reference interface (graphd reaches storaged for every FindPathExecutor round). */
+int32_t nbg_set_path_replica(nbg_engine* e, int32_t mode);
+int32_t nbg_path_replica_active(const nbg_engine* e);   /* 1: FIND PATH runs on the replica */
+
 int32_t nbg_profile(nbg_engine* e, int32_t enable);
 /* Copies up to cap kernel records; returns the number of kernels. */
 int32_t nbg_profile_read(const nbg_engine* e, nbg_kernel_stat* out, int32_t cap);

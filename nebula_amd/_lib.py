@@ -144,6 +144,8 @@ SIGNATURES = [
     ("nbg_stats_data", i32, [vp, P(P(u8)), P(u64)]),
     ("nbg_stats_free", None, [vp]),
     ("nbg_profile", i32, [vp, i32]),
+    ("nbg_set_path_replica", i32, [vp, i32]),
+    ("nbg_path_replica_active", i32, [vp]),
     ("nbg_profile_read", i32, [vp, vp, i32]),
     ("nbg_comm_unique_id", i32, [P(u8)]),
     ("nbg_comm_init", i32, [vp, P(u8), i32, i32]),

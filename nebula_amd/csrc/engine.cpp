@@ -140,6 +140,12 @@ struct nbg_rows {
   }
   uint64_t scanned = 0;
   std::vector<uint64_t> step_frontier, step_edges;
+  // the result schema (GoExecutor::setupInterimResult): NBG_T_* per column, what RowWriter wrote
+  // per (OVER type, column), and the read-back hazards it implies (see go_prepare)
+  std::vector<int32_t> col_types;
+  std::vector<std::vector<uint8_t>> wclass;
+  bool misaligned = false;   // some column's written bytes differ in length from what its reader takes
+  bool float_col = false;    // a FLOAT column: InterimResult::getRows fails on it
 };
 
 namespace nbg {
@@ -193,10 +199,134 @@ namespace {
 // The rows of a result into host memory: the device packs the segments into contiguous columns
 // and DMAs them into a pinned block (nbg.h nbg_rows_fetch).  Only STRING columns are touched per
 // cell on the host (dictionary code -> the result's string table).
+// RowWriter's written form of one value (RowWriter.cpp:103-186, RowWriter.inl:9-33): the value
+// itself (ID), or the default it falls back to for an incompatible column type — varint 0 / a
+// false byte (ONE zero byte) or a 0.0 double (EIGHT zero bytes).
+enum WClass : uint8_t { W_ID = 0, W_ONE = 1, W_EIGHT = 2 };
+WClass written_class(VKind k, int32_t t) {
+  switch (k) {
+    case VK_INT: return (t == NBG_T_INT || t == NBG_T_TIMESTAMP || t == NBG_T_VID) ? W_ID : W_ONE;
+    case VK_DOUBLE: return (t == NBG_T_DOUBLE || t == NBG_T_FLOAT) ? W_ID : W_EIGHT;
+    case VK_BOOL: return t == NBG_T_BOOL ? W_ID : W_ONE;
+    default: return t == NBG_T_STRING ? W_ID : W_ONE;
+  }
+}
+// does the reader of a `t` column take exactly the bytes written? (else the row's later columns
+// are read at shifted positions)
+bool read_aligned(WClass w, int32_t t) {
+  if (w == W_ID) return true;
+  if (w == W_ONE) return t == NBG_T_INT || t == NBG_T_TIMESTAMP || t == NBG_T_BOOL || t == NBG_T_STRING;
+  return t == NBG_T_VID;
+}
+VKind read_kind(int32_t t) {   // the value InterimResult::getRows reads from a `t` column
+  switch (t) {
+    case NBG_T_BOOL: return VK_BOOL;
+    case NBG_T_FLOAT: case NBG_T_DOUBLE: return VK_DOUBLE;
+    case NBG_T_STRING: return VK_STRING;
+    default: return VK_INT;
+  }
+}
+
+// Rows whose schema makes RowReader read columns at shifted positions: the reference's bytes are
+// rebuilt per row (RowWriter with the result schema) and read back column by column as
+// InterimResult::getRows does (InterimResult.cpp:74-153); a read past the row's end fails the
+// query.  Runs on the fetched host copy (strings already dictionary-decoded).
+int32_t reread_rows(nbg_rows* r) {
+  Engine& E = *r->eng;
+  const int nc = r->ncols;
+  std::vector<uint8_t> b;
+  uint64_t o = 0;
+  for (auto& s : r->segs) {
+    const uint64_t len = s.end - s.begin;
+    const std::vector<uint8_t>& wc = r->wclass[s.type];
+    for (uint64_t i = o; i < o + len; ++i) {
+      b.clear();
+      for (int c = 0; c < nc; ++c) {
+        const int64_t v = r->col(c)[i];
+        const int32_t t = r->col_types[c];
+        if (wc[c] == W_ONE) { b.push_back(0); continue; }
+        if (wc[c] == W_EIGHT) { b.insert(b.end(), 8, 0); continue; }
+        switch (t) {
+          case NBG_T_BOOL: b.push_back(v != 0); break;
+          case NBG_T_VID: case NBG_T_DOUBLE:
+            for (int k = 0; k < 8; ++k) b.push_back((uint8_t)((uint64_t)v >> (8 * k)));
+            break;
+          case NBG_T_STRING: {
+            const std::string& str = r->strings[(size_t)v];
+            for (uint64_t n = str.size();; n >>= 7) {
+              b.push_back((uint8_t)((n & 0x7f) | (n > 0x7f ? 0x80 : 0)));
+              if (n <= 0x7f) break;
+            }
+            b.insert(b.end(), str.begin(), str.end());
+            break;
+          }
+          default:   // INT / TIMESTAMP: varint of the two's-complement bits
+            for (uint64_t n = (uint64_t)v;; n >>= 7) {
+              b.push_back((uint8_t)((n & 0x7f) | (n > 0x7f ? 0x80 : 0)));
+              if (n <= 0x7f) break;
+            }
+        }
+      }
+      size_t p = 0;
+      for (int c = 0; c < nc; ++c) {
+        const int32_t t = r->col_types[c];
+        int64_t out = 0;
+        bool ok = true;
+        auto varint = [&](uint64_t* x) {
+          *x = 0;
+          for (int sh = 0; sh < 64; sh += 7) {
+            if (p >= b.size()) return false;
+            const uint8_t y = b[p++];
+            *x |= (uint64_t)(y & 0x7f) << sh;
+            if (!(y & 0x80)) return true;
+          }
+          return false;
+        };
+        switch (t) {
+          case NBG_T_BOOL:
+            ok = p < b.size();
+            if (ok) out = b[p++] != 0;
+            break;
+          case NBG_T_VID: case NBG_T_DOUBLE:
+            ok = p + 8 <= b.size();
+            if (ok) {
+              uint64_t x = 0;
+              for (int k = 0; k < 8; ++k) x |= (uint64_t)b[p + k] << (8 * k);
+              p += 8;
+              out = (int64_t)x;
+            }
+            break;
+          case NBG_T_STRING: {
+            uint64_t n = 0;
+            ok = varint(&n) && n <= b.size() - p;
+            if (ok) {
+              out = (int64_t)r->strings.size();
+              r->strings.emplace_back(reinterpret_cast<const char*>(b.data() + p), (size_t)n);
+              p += n;
+            }
+            break;
+          }
+          default: {
+            uint64_t x = 0;
+            ok = varint(&x);
+            out = (int64_t)x;
+          }
+        }
+        if (!ok) return E.fail(NBG_E_EXECUTION_ERROR, "Get value from interim failed (column " + std::to_string(c) + ")");
+        r->col(c)[i] = out;
+      }
+    }
+    o += len;
+  }
+  return NBG_OK;
+}
+
 int32_t materialize_rows(nbg_rows* r) {
   if (r->fetched) return NBG_OK;
   r->build_segs();
   Engine& E = *r->eng;
+  // InterimResult::getRows has no case for a FLOAT column: "Unknown Type: 4" (InterimResult.cpp:142-146)
+  if (r->float_col && r->count) return E.fail(NBG_E_EXECUTION_ERROR, "Unknown Type: 4");
   const auto& dict = E.snap.strings;
   const size_t bytes = std::max<size_t>((size_t)r->count * (size_t)r->ncols * 8, 8);
   r->hbits = static_cast<int64_t*>(E.pinned_get(bytes, &r->hbytes));
@@ -234,6 +364,10 @@ int32_t materialize_rows(nbg_rows* r) {
       o += len;
     }
   }
+  if (r->misaligned && r->count) {
+    const int32_t rc = reread_rows(r);
+    if (rc) return rc;
+  }
   r->fetched = true;
   return NBG_OK;
 }
@@ -270,6 +404,9 @@ struct nbg_go_stmt {
   std::string deferred_msg;
   std::string dst_unknown;           // a $$ tag name is unknown: fails once the final step has edges
   bool distinct = false;             // YIELD DISTINCT: distinct starts and rows
+  std::vector<int32_t> col_types;    // the result schema (NBG_T_* per column)
+  std::vector<std::vector<uint8_t>> wclass;   // per OVER position: WClass of each column
+  bool misaligned = false, float_col = false;
   // $- / $var input: index rows (the FROM vid, ascending; last row per vid) and their columns,
   // uploaded on first execution (the same index on every rank of a partitioned engine)
   bool uses_input = false;
@@ -313,6 +450,17 @@ static void alias_props(const Node* n, std::map<std::string, std::set<std::strin
 // the response's edge_schema (an unordered_map, QueryBoundProcessor.cpp:139-158), and graphd
 // decodes that into another unordered_map (storage.thrift:104).  The same three containers, keyed
 // the same way, reproduce it.
+// the iteration order of storaged's edgeContexts_ for a request's edge types: the order
+// processVertex emits a vertex's edge data in (QueryBaseProcessor.inl:46-57, QueryBoundProcessor.cpp:120-167)
+static std::vector<int32_t> edge_context_order(const std::vector<int32_t>& req) {
+  std::unordered_map<int32_t, int> contexts;
+  std::transform(req.begin(), req.end(), std::inserter(contexts, contexts.end()),
+                 [](int32_t t) { return std::make_pair(t, 0); });
+  std::vector<int32_t> order;
+  for (const auto& kv : contexts) order.push_back(kv.first);
+  return order;
+}
+
 static std::vector<int32_t> response_schema_order(const std::vector<int32_t>& req) {
   std::unordered_map<int32_t, int> contexts;
   std::transform(req.begin(), req.end(), std::inserter(contexts, contexts.end()),
@@ -506,6 +654,66 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
   }
   if ((int)over.size() > MAX_TYPES_Q || rq->steps > (uint32_t)MAX_STEPS)
     return E.fail(NBG_E_UNSUPPORTED, "too many OVER types or steps");
+  // ---- the result schema and what RowWriter makes of each value (GoExecutor::setupInterimResult,
+  // GoExecutor.cpp:707-788).  The reference types every column from the FIRST row it evaluates
+  // (yield_column_type) and writes every row through that schema: a value of another kind becomes
+  // the writer's default (RowWriter.cpp:103-186), and a default of another length shifts the
+  // columns after it when InterimResult::getRows reads the row back.  Which row is first follows
+  // hash-map order; the canonical row here is an edge of the first type in the request's
+  // edge-context order (QueryBaseProcessor.inl:46-57, the order processVertex emits edge data in)
+  // whose source has the $^ tags the columns read.  Aligned defaults become constants of the
+  // compiled programs (the expression still runs, so its errors still fail the query); shifted
+  // rows are re-read on the host copy (reread_rows); a FLOAT column fails the fetch.
+  std::vector<int32_t> ctype(ncols, NBG_T_INT);
+  std::vector<std::vector<uint8_t>> wclass(over.size(), std::vector<uint8_t>(ncols, W_ID));
+  bool misaligned = false, float_col = false;
+  {
+    const int32_t t0 = edge_context_order(over)[0];
+    std::map<std::string, int32_t> row_types{{"_dst", NBG_T_VID}};
+    for (auto& p : named[E.edges[t0].name]) {
+      if (p == "_src" || p == "_dst") { row_types[p] = NBG_T_VID; continue; }
+      if (p == "_rank" || p == "_type") { row_types[p] = NBG_T_INT; continue; }
+      const Schema* sc = E.edges[t0].latest();
+      const int c = sc ? sc->find(p) : -1;
+      if (c >= 0) row_types[p] = sc->cols[c].type;
+    }
+    ColTypeEnv cenv;
+    cenv.row_type = t0;
+    cenv.edges = &E.edges;
+    cenv.tags = &E.tags;
+    cenv.row_types = &row_types;
+    if (uses_input) {
+      cenv.input_names = &in_names;
+      cenv.input_kinds = &in_kinds;
+    }
+    auto p0 = progs.find(t0);
+    if (p0 == progs.end()) p0 = progs.begin();
+    for (int y = 0; y < ncols; ++y) {
+      ctype[y] = yield_column_type(*yields[y], cenv);
+      if (!ctype[y] && p0 != progs.end()) {
+        const VKind k = p0->second.yield_kind[y];
+        ctype[y] = k == VK_DOUBLE ? NBG_T_DOUBLE : k == VK_BOOL ? NBG_T_BOOL : k == VK_STRING ? NBG_T_STRING : NBG_T_INT;
+      }
+      if (!ctype[y]) ctype[y] = NBG_T_INT;
+      float_col = float_col || ctype[y] == NBG_T_FLOAT;
+    }
+    for (size_t i = 0; i < over.size(); ++i) {
+      auto it = progs.find(over[i]);
+      if (it == progs.end()) continue;
+      TypeProgram& tp = it->second;
+      for (int y = 0; y < ncols; ++y) {
+        const WClass w = written_class(tp.yield_kind[y], ctype[y]);
+        wclass[i][y] = w;
+        if (w == W_ID) continue;
+        misaligned = misaligned || !read_aligned(w, ctype[y]);
+        const VKind rk = read_kind(ctype[y]);
+        tp.yield_reg[y] = -1;
+        tp.yield_kind[y] = rk;
+        tp.yield_const[y] = rk == VK_STRING ? string_code(E.snap.strings, "") : 0;
+        tp.yield_const_str[y] = std::string();
+      }
+    }
+  }
   static std::atomic<uint64_t> next_id{1};
   auto* st = new nbg_go_stmt();
   st->eng = &E;
@@ -522,6 +730,10 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
   st->deferred_msg = deferred_msg;
   st->dst_unknown = dst_unknown;
   st->distinct = rq->distinct != 0;
+  st->col_types = std::move(ctype);
+  st->wclass = std::move(wclass);
+  st->misaligned = misaligned;
+  st->float_col = float_col;
   st->uses_input = uses_input;
   st->in_ids = std::move(in_ids);
   st->in_cols = std::move(in_cols);
@@ -849,6 +1061,10 @@ static int32_t go_collect(Engine& E, const nbg_go_stmt* st, GoPending* p, nbg_ro
     delete rows;
     return E.fail(NBG_E_EXECUTION_ERROR, "Unknown Vertex");
   }
+  rows->col_types = st->col_types;
+  rows->wclass = st->wclass;
+  rows->misaligned = st->misaligned;
+  rows->float_col = st->float_col;
   for (size_t i = 0; i < over.size(); ++i) {
     rows->kinds.push_back(plist[i].yield_kind);
     rows->const_str.push_back(plist[i].yield_const_str);
@@ -920,7 +1136,10 @@ static int32_t go_collect(Engine& E, const nbg_go_stmt* st, GoPending* p, nbg_ro
   for (int c = 0; c < ncols; ++c) rows->dcols.push_back(ws_row_col(ws, c));
   if (!device) {
     int32_t rc = materialize_rows(rows);
-    if (rc) { delete rows; return E.fail(rc, "row fetch failed"); }
+    if (rc) {
+      delete rows;
+      return rc == NBG_E_EXECUTION_ERROR ? rc : E.fail(rc, "row fetch failed");
+    }
   } else if (rows->count) {
     E.holders[ws] = rows;   // the rows stay valid until nbg_rows_free (ws_release)
   }
@@ -1016,6 +1235,7 @@ int32_t nbg::engine_ready(Engine& E) {
   if (E.partitioned()) {
     hipError_t he = ws_set_partition(E.ws, E.comm.get(), E.npad);
     if (he != hipSuccess) return E.fail(NBG_E_OUT_OF_MEMORY, std::string("partition buffers: ") + hipGetErrorString(he));
+    return build_path_replica(E);   // collective: every rank finalizes together
   }
   return NBG_OK;
 }
@@ -1131,6 +1351,7 @@ void nbg_destroy(nbg_engine* h) {
     if (q.stream) (void)hipStreamDestroy(q.stream);
   }
   path_slots_release(E);
+  destroy_path_replica(E);
   E.pinned_release();
   if (E.ws) ws_destroy(E.ws);
   if (E.sp) sp_destroy(E.sp);
@@ -1377,6 +1598,21 @@ void nbg_rows_free(nbg_rows* r) {
   delete r;
 }
 
+int32_t nbg_set_path_replica(nbg_engine* h, int32_t mode) {
+  if (!h || mode < 0 || mode > 1) return NBG_E_INVALID_ARGUMENT;
+  Engine& E = h->e;
+  std::lock_guard<std::mutex> lg(E.mu);
+  if (!E.finalized) {   // before finalize: whether to build it
+    E.path_replica_mode = mode;
+    return NBG_OK;
+  }
+  if (mode && !E.rep) return E.fail(NBG_E_STATE, "this engine has no FIND PATH replica");
+  E.path_replica_use = mode != 0;   // after: whether FIND PATH uses it
+  return NBG_OK;
+}
+
+int32_t nbg_path_replica_active(const nbg_engine* h) { return h && h->e.rep && h->e.path_replica_use ? 1 : 0; }
+
 int32_t nbg_profile(nbg_engine* h, int32_t enable) {
   if (!h) return NBG_E_INVALID_ARGUMENT;
   Engine& E = h->e;
@@ -1385,10 +1621,13 @@ int32_t nbg_profile(nbg_engine* h, int32_t enable) {
   const int mode = enable == 2 ? 2 : (enable != 0 ? 1 : 0);
   ws_profile(E.ws, mode);
   // the one-pair SHORTEST contexts (device-driven chains): their launches and algorithmic bytes
-  E.prof_mode = mode;
-  sp_profile(E.sp, mode);
-  for (auto& ps : E.path_slots) sp_profile(ps.sp, mode);
-  for (SpCtx* c : E.batch_sp) sp_profile(c, mode);
+  for (Engine* P : {&E, E.rep.get()}) {   // (and the FIND PATH replica's)
+    if (!P) continue;
+    P->prof_mode = mode;
+    sp_profile(P->sp, mode);
+    for (auto& ps : P->path_slots) sp_profile(ps.sp, mode);
+    for (SpCtx* c : P->batch_sp) sp_profile(c, mode);
+  }
   return NBG_OK;
 }
 
@@ -1397,9 +1636,12 @@ int32_t nbg_profile_read(const nbg_engine* h, nbg_kernel_stat* out, int32_t cap)
   const Engine& E = h->e;
   int n = ws_profile_read(E.ws, out, cap);
   double launches[CHAIN_KINDS] = {}, ms[CHAIN_KINDS] = {}, bytes[CHAIN_KINDS] = {};
-  sp_profile_accum(E.sp, launches, ms, bytes);
-  for (auto& ps : E.path_slots) sp_profile_accum(ps.sp, launches, ms, bytes);
-  for (SpCtx* c : E.batch_sp) sp_profile_accum(c, launches, ms, bytes);
+  for (const Engine* P : {&E, (const Engine*)E.rep.get()}) {
+    if (!P) continue;
+    sp_profile_accum(P->sp, launches, ms, bytes);
+    for (auto& ps : P->path_slots) sp_profile_accum(ps.sp, launches, ms, bytes);
+    for (SpCtx* c : P->batch_sp) sp_profile_accum(c, launches, ms, bytes);
+  }
   for (int k = 0; k < CHAIN_KINDS && n < cap; ++k, ++n) {
     out[n].name = kChainKernelNames[k];
     out[n].launches = (uint64_t)launches[k];

@@ -72,6 +72,13 @@ struct Engine {
   uint64_t npad = 0;
   bool partitioned() const { return cfg.num_gpus > 1; }
 
+  // FIND PATH replica of a partitioned snapshot (replica.hip): a single-GPU engine over every
+  // rank's path CSRs; FIND PATH runs on it rank-locally while it is in use
+  std::unique_ptr<Engine> rep;
+  int path_replica_mode = -1;   // build it at finalize: 1 yes (when it fits), 0 no, -1 NBG_PATH_REPLICA (default 1)
+  bool path_replica_use = true; // nbg_set_path_replica after finalize: 0 = the collective search
+  Engine* path_engine() { return rep && path_replica_use ? rep.get() : this; }
+
   // nbg_inject_fault (tests): the next fault_count queries fail at fault_site
   int fault_site = 0, fault_count = 0;
   bool fault(int site) {
@@ -111,6 +118,11 @@ struct Engine {
 };
 
 int32_t engine_ready(Engine& E);   // workspace (+ partition buffers) after finalize / snapshot load
+// replica.hip: the FIND PATH replica of a partitioned engine (collective; no replica when it does
+// not fit, is not wanted, or a vertex sits on two ranks)
+int32_t build_path_replica(Engine& E);
+void destroy_path_replica(Engine& E);
+bool path_replica_wanted(const Engine& E);
 void path_slots_release(Engine& E); // completes outstanding path tickets, frees the path slots
 // Make *wsp free for a new query: if live device rows still sit in it, the rows take the
 // workspace over and *wsp becomes a fresh one on `stream` (profiling state carried over).

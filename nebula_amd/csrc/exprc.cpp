@@ -708,3 +708,75 @@ int32_t compile_expr(const Node& e, const CompileEnv& env, ProgramBuilder& pb, C
 }
 
 }  // namespace nbg
+
+namespace nbg {
+
+// ============================================================================= result column types
+namespace {
+int32_t natural_type(VKind k) {
+  switch (k) {
+    case VK_DOUBLE: return NBG_T_DOUBLE;
+    case VK_BOOL: return NBG_T_BOOL;
+    case VK_STRING: return NBG_T_STRING;
+    default: return NBG_T_INT;
+  }
+}
+
+const SchemaSet* by_name(const std::map<int32_t, SchemaSet>* m, const std::string& name) {
+  if (!m) return nullptr;
+  for (auto& kv : *m)
+    if (kv.second.name == name) return &kv.second;
+  return nullptr;
+}
+
+int32_t prop_type(const SchemaSet* ss, const std::string& prop) {   // getFieldType: 0 if absent
+  const Schema* sc = ss ? ss->latest() : nullptr;
+  const int c = sc ? sc->find(prop) : -1;
+  return c < 0 ? 0 : sc->cols[c].type;
+}
+
+// post-order, left operand first: *t = the type set by the last getter evaluated
+void last_getter(const Node& e, const ColTypeEnv& env, int32_t* t) {
+  for (auto& k : e.kids)
+    if (k) last_getter(*k, env, t);
+  switch (e.kind) {
+    case EK_ALIAS: case EK_DST: case EK_SRCID: case EK_RANK: {
+      // getAliasProp: an unknown edge fails before the type is saved; else the type comes from the
+      // ROW's schema (iter->getSchema()->getFieldType(prop)), whatever edge the alias names
+      if (!by_name(env.edges, e.alias)) return;
+      *t = 0;
+      if (env.row_types) {
+        auto it = env.row_types->find(e.prop);
+        if (it != env.row_types->end()) *t = it->second;
+      }
+      return;
+    }
+    case EK_SRCPROP:   // getSrcTagProp: saved when the source has the tag (the fixed row context)
+      if (const SchemaSet* ts = by_name(env.tags, e.alias)) *t = prop_type(ts, e.prop);
+      return;
+    case EK_DSTPROP:   // VertexHolder::getType: the tag schema's type of the prop
+      if (const SchemaSet* ts = by_name(env.tags, e.alias)) *t = prop_type(ts, e.prop);
+      return;
+    case EK_INPUT: case EK_VAR: {   // getPropTypeFromInterim: the input column's type
+      if (!env.input_names || !env.input_kinds) return;
+      for (size_t c = 0; c < env.input_names->size(); ++c)
+        if ((*env.input_names)[c] == e.prop) { *t = natural_type((*env.input_kinds)[c]); return; }
+      *t = 0;
+      return;
+    }
+    default: return;
+  }
+}
+}  // namespace
+
+int32_t yield_column_type(const Node& e, const ColTypeEnv& env) {
+  if (e.kind == EK_CAST) {   // SchemaHelper::columnTypeToSupportedType of the cast's ColumnType
+    static const int32_t m[6] = {NBG_T_INT, NBG_T_STRING, NBG_T_DOUBLE, NBG_T_INT, NBG_T_BOOL, NBG_T_TIMESTAMP};
+    return e.op < 6 ? m[e.op] : 0;
+  }
+  int32_t t = 0;
+  last_getter(e, env, &t);
+  return t;
+}
+
+}  // namespace nbg

@@ -79,4 +79,21 @@ bool fold_constant(const Node& e, CVal* out, bool* error);
 
 int64_t string_code(const std::vector<std::string>& dict, const std::string& s);
 
+// ---- result column types (GoExecutor::setupInterimResult's schema, GoExecutor.cpp:707-748)
+// The schema of a GO result comes from the first row the reference evaluates: a column's type is
+// the type the LAST prop getter of its expression set while evaluating it (operands left before
+// right, no short-circuit: Expressions.cpp:835-1131; getters GoExecutor.cpp:851-945), or the cast
+// type of a root TypeCasting (:970-974), else (0 here) the value's own kind.  The row context is
+// fixed statically (see go_prepare): an edge of `row_type` whose source carries the $^ tags read.
+struct ColTypeEnv {
+  int32_t row_type = 0;                                 // edge type of the first row
+  const std::map<int32_t, SchemaSet>* edges = nullptr;  // registered edge schemas
+  const std::map<int32_t, SchemaSet>* tags = nullptr;   // registered tag schemas
+  // the response edge row schema of row_type: `_dst` plus every prop the query names on it
+  const std::map<std::string, int32_t>* row_types = nullptr;
+  const std::vector<std::string>* input_names = nullptr;   // $- / $var columns and their kinds
+  const std::vector<VKind>* input_kinds = nullptr;
+};
+int32_t yield_column_type(const Node& e, const ColTypeEnv& env);   // NBG_T_* or 0 (the value's kind)
+
 }  // namespace nbg

@@ -251,9 +251,35 @@ __device__ __forceinline__ uint32_t vdeg(const DegSrc& ds, uint32_t v, uint32_t*
 // Entry i owns merge-path positions [i + start_i, i + end_i] (its edges, then its terminator);
 // the split of tile t (entries consumed before position t * TILE) is the entry whose range holds
 // t * TILE, so each entry records the tile boundaries it covers and k_expand reads its split.
-__device__ __forceinline__ void record_splits(uint32_t* tsplit, uint32_t i, uint32_t end_incl, uint32_t deg) {
+// An entry covering up to SPLITS_SOLO boundaries writes them itself; a hub's (one boundary per
+// 256 edges: a vertex of degree 10^6 covers ~4000) are left in [*t0, *t1) for wave_splits, which
+// spreads them over the wave's lanes — one lane storing them serially cost a claim-mode MARK step
+// ~40 us whenever the claimed set held a hub (RMAT-26 step 2: 50-60 us for 292 claims or 282 k).
+constexpr uint64_t SPLITS_SOLO = 4;
+__device__ __forceinline__ void record_splits(uint32_t* tsplit, uint32_t i, uint32_t end_incl, uint32_t deg,
+                                              uint64_t* t0, uint64_t* t1) {
   const uint64_t lo = (uint64_t)i + end_incl - deg, hi = (uint64_t)i + end_incl;
-  for (uint64_t t = (lo + TILE - 1) / TILE; t * TILE <= hi; ++t) tsplit[t] = i;
+  const uint64_t a = (lo + TILE - 1) / TILE, b = hi / TILE + 1;
+  if (b - a <= SPLITS_SOLO) {
+    for (uint64_t t = a; t < b; ++t) tsplit[t] = i;
+    return;
+  }
+  *t0 = a;
+  *t1 = b;
+}
+
+// The hub boundaries of one round of list_put calls (every lane of the wave takes part; a lane
+// without an entry passes t0 == t1): each hub's boundaries are stored lane-strided by the wave.
+__device__ __forceinline__ void wave_splits(uint32_t* tsplit, uint64_t t0, uint64_t t1, uint32_t pos) {
+  unsigned long long bm = __ballot(t1 > t0);
+  const uint64_t lane = threadIdx.x & 63;
+  while (bm) {
+    const int l = __ffsll((long long)bm) - 1;
+    bm &= bm - 1;
+    const uint64_t a = __shfl(t0, l, 64), b = __shfl(t1, l, 64);
+    const uint32_t p = __shfl(pos, l, 64);
+    for (uint64_t t = a + lane; t < b; t += 64) tsplit[t] = p;
+  }
 }
 
 // Block-wide reservation: exclusive per-thread offsets (*pc list position, *pd edge offset).
@@ -270,14 +296,15 @@ __device__ __forceinline__ void reserve(uint32_t c, uint32_t d, unsigned long lo
   *pd = (uint32_t)s_old + xd;
 }
 
+// One list entry; a hub's tile boundaries come back in [*t0, *t1) for wave_splits (t0 == t1 else).
 __device__ __forceinline__ void list_put(const ListOut& o, const DegSrc& ds, uint32_t pos, uint32_t v, uint32_t* pd,
-                                         uint32_t dg, uint32_t rs) {
+                                         uint32_t dg, uint32_t rs, uint64_t* t0, uint64_t* t1) {
   o.ids[pos] = v;
   if (ds.row_ptr) {
     *pd += dg;
     o.seg_end[pos] = *pd;
     o.seg_rs[pos] = rs;
-    record_splits(o.tsplit, pos, *pd, dg);
+    record_splits(o.tsplit, pos, *pd, dg, t0, t1);
   }
 }
 
@@ -319,8 +346,12 @@ __global__ void __launch_bounds__(BLOCK) k_relist(const uint32_t* __restrict__ i
   uint32_t pc, pd;
   reserve<BLOCK>(c, d, o.acc, &pc, &pd);
 #pragma unroll
-  for (int k = 0; k < RL_ITEMS; ++k)
-    if (dg[k]) list_put(o, ds, pc++, v[k], &pd, dg[k], rs[k]);
+  for (int k = 0; k < RL_ITEMS; ++k) {
+    uint64_t t0 = 0, t1 = 0;
+    const uint32_t p = pc;
+    if (dg[k]) list_put(o, ds, pc++, v[k], &pd, dg[k], rs[k], &t0, &t1);
+    wave_splits(o.tsplit, t0, t1, p);
+  }
 }
 
 // k_compact: next frontier = the byte flags set by k_expand<MARK> (the per-step dst SET),
@@ -347,10 +378,13 @@ __global__ void __launch_bounds__(CP_THREADS) k_compact(uint8_t* __restrict__ fl
   }
   uint32_t pc, pd;
   reserve<CP_THREADS>(c, d, o.acc, &pc, &pd);
-  if (!c) return;
 #pragma unroll
-  for (int b = 0; b < 16; ++b)
-    if ((ws[b >> 2] >> ((b & 3) * 8)) & 1u) list_put(o, ds, pc++, (uint32_t)(off + b), &pd, dg[b], rs[b]);
+  for (int b = 0; b < 16; ++b) {   // (every lane: wave_splits is wave-wide)
+    uint64_t t0 = 0, t1 = 0;
+    const uint32_t pp = pc;
+    if ((ws[b >> 2] >> ((b & 3) * 8)) & 1u) list_put(o, ds, pc++, (uint32_t)(off + b), &pd, dg[b], rs[b], &t0, &t1);
+    wave_splits(o.tsplit, t0, t1, pp);
+  }
   *p = make_uint4(0, 0, 0, 0);
 }
 
@@ -630,8 +664,12 @@ __device__ __forceinline__ void claim_append(const uint32_t (&u)[VT], const BfsP
   uint32_t pos = (uint32_t)(old >> 32) + ic - c;
   uint32_t pd = (uint32_t)old + id - d;
 #pragma unroll
-  for (int i = 0; i < VT; ++i)
-    if ((cmask >> i) & 1u) list_put(bp.nlist, bp.nds, pos++, u[i], &pd, dg[i], rs[i]);
+  for (int i = 0; i < VT; ++i) {
+    uint64_t t0 = 0, t1 = 0;
+    const uint32_t p = pos;
+    if ((cmask >> i) & 1u) list_put(bp.nlist, bp.nds, pos++, u[i], &pd, dg[i], rs[i], &t0, &t1);
+    wave_splits(bp.nlist.tsplit, t0, t1, p);
+  }
 }
 
 // Merge-path split of tile t: entries consumed before position t * TILE (which 0) or before the
@@ -1212,8 +1250,12 @@ __global__ void __launch_bounds__(BLOCK) k_bits_compact(const unsigned long long
   uint32_t pc, pd;
   reserve<BLOCK>((uint32_t)__popc(m), d, o.acc, &pc, &pd);
 #pragma unroll
-  for (int b = 0; b < 16; ++b)
-    if ((m >> b) & 1u) list_put(o, ds, pc++, (uint32_t)(lo + b), &pd, dg[b], rs[b]);
+  for (int b = 0; b < 16; ++b) {
+    uint64_t t0 = 0, t1 = 0;
+    const uint32_t pp = pc;
+    if ((m >> b) & 1u) list_put(o, ds, pc++, (uint32_t)(lo + b), &pd, dg[b], rs[b], &t0, &t1);
+    wave_splits(o.tsplit, t0, t1, pp);
+  }
   if (bt_recv && m) {
     for (int b = 0; b < 16; ++b) {
       if (!((m >> b) & 1u)) continue;

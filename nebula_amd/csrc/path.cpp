@@ -828,7 +828,7 @@ extern "C" {
 int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* rq, nbg_paths** out) {
   if (!h || !rq || !out) return NBG_E_INVALID_ARGUMENT;
   *out = nullptr;
-  Engine& E = h->e;
+  Engine& E = *h->e.path_engine();   // a partitioned engine's replica runs it rank-locally
   std::lock_guard<std::mutex> lg(E.mu);
   static const bool trace = getenv("NBG_PATH_TRACE") != nullptr;
   if (!trace) return find_path_locked(E, rq, out, nullptr);
@@ -843,7 +843,7 @@ int32_t nbg_find_path(nbg_engine* h, const nbg_path_request* rq, nbg_paths** out
 int32_t nbg_find_path_submit(nbg_engine* h, const nbg_path_request* rq, nbg_path_ticket** out) {
   if (!h || !rq || !out) return NBG_E_INVALID_ARGUMENT;
   *out = nullptr;
-  Engine& E = h->e;
+  Engine& E = *h->e.path_engine();   // a partitioned engine's replica runs it rank-locally
   std::lock_guard<std::mutex> lg(E.mu);
   auto* t = new nbg_path_ticket();
   t->eng = &E;
@@ -886,7 +886,7 @@ int32_t nbg_find_path_submit(nbg_engine* h, const nbg_path_request* rq, nbg_path
 
 int32_t nbg_find_path_batch(nbg_engine* h, const nbg_path_request* reqs, uint64_t n, nbg_paths** out, int32_t* rcs) {
   if (!h || (n && (!reqs || !out || !rcs))) return NBG_E_INVALID_ARGUMENT;
-  Engine& E = h->e;
+  Engine& E = *h->e.path_engine();
   std::lock_guard<std::mutex> lg(E.mu);
   for (uint64_t i = 0; i < n; ++i) {
     out[i] = nullptr;
@@ -985,7 +985,7 @@ int32_t nbg_find_path_batch(nbg_engine* h, const nbg_path_request* reqs, uint64_
 
 int32_t nbg_path_reserve(nbg_engine* h, int32_t slots, int32_t batch) {
   if (!h || slots < 0 || batch < 0) return NBG_E_INVALID_ARGUMENT;
-  Engine& E = h->e;
+  Engine& E = *h->e.path_engine();
   std::lock_guard<std::mutex> lg(E.mu);
   if (!E.finalized) return E.fail(NBG_E_STATE, "engine not finalized");
   if (E.partitioned()) return NBG_OK;   // partitioned searches run on the engine's workspace

@@ -248,6 +248,15 @@ class Engine:
                 "num_edge_types": s.num_edge_types}
 
     # ------------------------------------------------------------------ profiling
+    def set_path_replica(self, mode: int):
+        """nbg_set_path_replica: before finalize, whether a partitioned engine builds its FIND PATH
+        replica; after, whether FIND PATH uses it (rank-local) or the collective search."""
+        self._check(self.lib.nbg_set_path_replica(self.h, int(mode)), "set_path_replica")
+
+    @property
+    def path_replica_active(self) -> bool:
+        return bool(self.lib.nbg_path_replica_active(self.h))
+
     def profile(self, enable=True):
         """True/1: time every launch; 2: only the final-step / BFS expansion kernels; False/0: off."""
         self._check(self.lib.nbg_profile(self.h, int(enable)), "profile")
@@ -667,6 +676,15 @@ class LocalCluster:
 
     def finalize(self):
         self.each(lambda e: e.finalize())
+
+    def set_path_replica(self, mode: int):
+        """Every rank's nbg_set_path_replica (before finalize: build it or not; after: use it or not)."""
+        for e in self.engines:
+            e.set_path_replica(mode)
+
+    @property
+    def path_replica_active(self) -> bool:
+        return all(e.path_replica_active for e in self.engines)
 
     def go(self, *a, **k):
         """Union of the ranks' rows (each rank keeps the rows its final frontier produced)."""

@@ -103,6 +103,7 @@ void orc_set_input(int32_t ncols, const char* const* names, const uint8_t* kinds
   g_input = GoQuery();
   g_input.inputVidCol = vid_col;
   for (int32_t c = 0; c < ncols; ++c) g_input.inputNames.emplace_back(names[c]);
+  g_input.inputKinds.assign(kinds, kinds + ncols);
   g_input.inputRows.assign(nrows, std::vector<Value>(ncols));
   for (uint64_t r = 0; r < nrows; ++r)
     for (int32_t c = 0; c < ncols; ++c) {
@@ -133,6 +134,7 @@ int32_t orc_go(void* h, const int64_t* starts, uint64_t nstarts, const int32_t* 
   }
   q.distinct = distinct != 0;
   q.inputNames = std::move(g_input.inputNames);
+  q.inputKinds = std::move(g_input.inputKinds);
   q.inputRows = std::move(g_input.inputRows);
   q.inputVidCol = g_input.inputVidCol;
   g_input = GoQuery();

@@ -27,6 +27,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <numeric>
 #include <vector>
 
@@ -457,9 +458,154 @@ int shortest(Csr& g, int64_t sv, int64_t tv, uint32_t upto, std::vector<int64_t>
   return (int)L;
 }
 
+// ---------------------------------------------------------------- several OVER types (C5)
+// GO N STEPS FROM starts OVER t_0, .., t_{k-1} with the default YIELD (one `<t_i>._dst` column per
+// OVER type, parser.yy:518-531): a row of a t_i edge holds its dst in column i and the other edge
+// types' default 0 (GoExecutor.cpp:863-869).  Each type is its own Csr (own dense ids), so the
+// frontier travels as sorted unique vids; the per-step SET is the union over the types.
+GoOut go_multi(Csr* const* gs, int nt, const int64_t* starts, uint64_t ns, uint32_t steps) {
+  GoOut out;
+  const int T = gs[0]->threads;
+  std::vector<int64_t> f(starts, starts + ns);   // duplicates kept at step 1
+  for (uint32_t s = 1; s < steps && !f.empty(); ++s) {
+    std::vector<std::vector<int64_t>> nx(T);
+    uint64_t sc = 0;
+    for (int k = 0; k < nt; ++k) {
+      const Csr& g = *gs[k];
+#pragma omp parallel num_threads(T) reduction(+ : sc)
+      {
+        std::vector<int64_t>& mine = nx[omp_get_thread_num()];
+#pragma omp for schedule(dynamic, 64)
+        for (int64_t i = 0; i < (int64_t)f.size(); ++i) {
+          const int64_t d = g.dense(f[i]);
+          if (d < 0) continue;
+          sc += g.off[d + 1] - g.off[d];
+          for (uint64_t j = g.off[d]; j < g.off[d + 1]; ++j) mine.push_back(g.vid[g.nbr[j]]);
+        }
+      }
+    }
+    out.scanned += sc;
+    f.clear();
+    for (auto& v : nx) f.insert(f.end(), v.begin(), v.end());
+    std::sort(f.begin(), f.end());
+    f.erase(std::unique(f.begin(), f.end()), f.end());
+  }
+  uint64_t rows = 0, x = 0, sum = 0, sc = 0;
+  for (int k = 0; k < nt; ++k) {
+    const Csr& g = *gs[k];
+#pragma omp parallel for schedule(dynamic, 64) reduction(+ : rows, sum, sc) reduction(^ : x) num_threads(T)
+    for (int64_t i = 0; i < (int64_t)f.size(); ++i) {
+      const int64_t d = g.dense(f[i]);
+      if (d < 0) continue;
+      sc += g.off[d + 1] - g.off[d];
+      for (uint64_t j = g.off[d]; j < g.off[d + 1]; ++j) {
+        uint64_t h = 0;
+        for (int q = 0; q < nt; ++q) h = splitmix64(h ^ (uint64_t)(q == k ? g.vid[g.nbr[j]] : 0));
+        ++rows;
+        x ^= h;
+        sum += h;
+      }
+    }
+  }
+  out.rows = rows;
+  out.x = x;
+  out.sum = sum;
+  out.scanned += sc;
+  return out;
+}
+
+// ---------------------------------------------------------------- FIND ALL PATH (walks)
+// FIND ALL PATH s -> t UPTO n over one type returns every walk of 1..n edges (cycles included,
+// FindPathExecutor.cpp:292-411).  Counted per length by dynamic programming over the walk-count
+// vector (count[L] = (A^L)[s, t]); enumerated by a depth-first search pruned with the backward
+// BFS distance to t.
+void walk_counts(const Csr& g, int64_t sv, int64_t tv, uint32_t upto, uint64_t* cnt) {
+  for (uint32_t L = 0; L <= upto; ++L) cnt[L] = 0;
+  const int64_t s = g.dense(sv), t = g.dense(tv);
+  if (s < 0 || t < 0) return;
+  std::vector<uint64_t> cur(g.nv, 0), nxt(g.nv, 0);
+  std::vector<uint32_t> act{(uint32_t)s}, nact;
+  cur[s] = 1;
+  std::vector<uint8_t> in(g.nv, 0);
+  for (uint32_t L = 1; L <= upto && !act.empty(); ++L) {
+    nact.clear();
+    for (uint32_t v : act)
+      for (uint64_t j = g.off[v]; j < g.off[v + 1]; ++j) {
+        const uint32_t u = g.nbr[j];
+        nxt[u] += cur[v];
+        if (!in[u]) { in[u] = 1; nact.push_back(u); }
+      }
+    for (uint32_t v : act) cur[v] = 0;
+    for (uint32_t u : nact) { in[u] = 0; cur[u] = nxt[u]; nxt[u] = 0; }
+    act.swap(nact);
+    cnt[L] = cur[t];
+  }
+}
+
+uint64_t all_walks(const Csr& g, int64_t sv, int64_t tv, uint32_t upto, int64_t* out, uint64_t cap) {
+  const int64_t s = g.dense(sv), t = g.dense(tv);
+  if (s < 0 || t < 0) return 0;
+  // distance to t over out-edges (backward BFS over in-edges), capped at upto
+  std::vector<uint32_t> dist(g.nv, 0xFFFFFFFFu);
+  std::vector<uint32_t> fr{(uint32_t)t}, nx;
+  dist[t] = 0;
+  for (uint32_t d = 1; d <= upto && !fr.empty(); ++d) {
+    nx.clear();
+    for (uint32_t v : fr)
+      for (uint64_t j = g.ioff[v]; j < g.ioff[v + 1]; ++j)
+        if (dist[g.inbr[j]] == 0xFFFFFFFFu) { dist[g.inbr[j]] = d; nx.push_back(g.inbr[j]); }
+    fr.swap(nx);
+  }
+  uint64_t n = 0;
+  std::vector<uint32_t> walk{(uint32_t)s};
+  const uint64_t width = 1 + (uint64_t)upto;   // vids of one walk, padded with -1
+  std::function<void()> dfs = [&]() {
+    const uint32_t v = walk.back();
+    const uint32_t len = (uint32_t)walk.size() - 1;
+    if (len >= upto) return;
+    for (uint64_t j = g.off[v]; j < g.off[v + 1]; ++j) {
+      const uint32_t u = g.nbr[j];
+      if (dist[u] == 0xFFFFFFFFu || len + 1 + dist[u] > upto) continue;
+      walk.push_back(u);
+      if (u == (uint32_t)t) {
+        if (n < cap)
+          for (uint64_t k = 0; k < width; ++k) out[n * width + k] = k < walk.size() ? g.vid[walk[k]] : -1;
+        ++n;
+      }
+      dfs();
+      walk.pop_back();
+    }
+  };
+  dfs();
+  return n;
+}
+
 }  // namespace
 
 extern "C" {
+
+// GO steps STEPS FROM starts OVER the nt types (one Csr each), default YIELD: out4 as orc_csr_go
+double orc_csr_go_multi(void* const* hs, int32_t nt, const int64_t* starts, uint64_t ns, uint32_t steps,
+                        uint64_t* out4) {
+  auto t0 = std::chrono::steady_clock::now();
+  GoOut r = go_multi(reinterpret_cast<Csr* const*>(hs), nt, starts, ns, steps);
+  out4[0] = r.rows;
+  out4[1] = r.x;
+  out4[2] = r.sum;
+  out4[3] = r.scanned;
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// walks s -> t of exactly L edges, for L = 0..upto, into cnt[0..upto]
+void orc_csr_walk_counts(void* h, int64_t s, int64_t t, uint32_t upto, uint64_t* cnt) {
+  walk_counts(*static_cast<Csr*>(h), s, t, upto, cnt);
+}
+
+// every walk s -> t of 1..upto edges as upto + 1 vids (-1 padded), the first `cap` of them;
+// returns how many there are
+uint64_t orc_csr_all_walks(void* h, int64_t s, int64_t t, uint32_t upto, int64_t* out, uint64_t cap) {
+  return all_walks(*static_cast<Csr*>(h), s, t, upto, out, cap);
+}
 
 void* orc_csr_build(const int64_t* src, const int64_t* dst, const int64_t* w, uint64_t n, int32_t threads) {
   return build(src, dst, w, n, threads > 0 ? threads : omp_get_max_threads());

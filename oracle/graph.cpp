@@ -170,6 +170,16 @@ std::vector<int32_t> responseEdgeSchemaOrder(const std::vector<int32_t>& reqType
   return names;
 }
 
+// storaged's edgeContexts_ iteration order for the request's types: the order processVertex
+// emits a vertex's edge data in (QueryBaseProcessor.inl:46-57)
+std::vector<int32_t> edgeContextOrder(const std::vector<int32_t>& reqTypes) {
+  std::unordered_map<int32_t, std::vector<int>> edgeContexts;
+  for (int32_t t : reqTypes) edgeContexts.insert(edgeContexts.end(), {t, std::vector<int>{}});
+  std::vector<int32_t> order;
+  for (const auto& kv : edgeContexts) order.push_back(kv.first);
+  return order;
+}
+
 ResultSet runGo(const Store& st, const GoQuery& q) {
   ResultSet out;
   // prepareOver (GoExecutor.cpp:197-263)
@@ -235,6 +245,117 @@ ResultSet runGo(const Store& st, const GoQuery& q) {
   if (hasInput)
     for (size_t r = 0; r < q.inputRows.size(); ++r) index[std::get<0>(q.inputRows[r][q.inputVidCol])] = r;
   std::unordered_map<int64_t, int64_t> tracker;
+
+  // ---- processFinalResult + setupInterimResult + InterimResult::getRows (GoExecutor.cpp:707-984,
+  // InterimResult.cpp:74-153).  The result schema comes from the first row the reference
+  // evaluates: a column's type is the type the LAST prop getter of its expression set (operands
+  // left before right, no short-circuit), a root cast's type, else the value's kind; every row is
+  // then written through that schema (RowWriter's incompatible-type defaults) and read back by it
+  // (a default of another length shifts the later columns; a read past the row's end, or a FLOAT
+  // column, fails the query).  Which row is first follows hash-map order; this restatement fixes
+  // it (as the engine does) to an edge of the first type in the request's edge-context order whose
+  // source carries the $^ tags the columns read.
+  auto finish = [&](const QueryResponse& resp, const VertexHolder* holder) -> ResultSet {
+    GoGetters g(st);
+    g.holder = holder;
+    g.q = &q;
+    g.index = hasInput ? &index : nullptr;
+    g.tracker = steps > 1 ? &tracker : nullptr;
+    struct Rec { std::vector<Value> v; int32_t type; };
+    std::vector<Rec> recs;
+    for (auto& vd : resp.vertices) {
+      for (auto& ed : vd.edges) {
+        const Schema& s = resp.edgeSchema.at(ed.type);
+        for (auto& row : rowSetSplit(ed.data)) {
+          RowReader r(row, &s);
+          g.edgeType = ed.type; g.row = &r; g.rowSchema = &s; g.srcVid = vd.vid;
+          g.edgeSchema = &resp.edgeSchema; g.tagSchema = &resp.vertexSchema; g.tagData = &vd.tags;
+          g.saveType = false;
+          if (filter) {
+            auto v = filter->eval(g);
+            if (!v.ok()) return goError(v.st.msg);
+            if (!asBool(v.v)) continue;
+          }
+          Rec rc;
+          rc.type = ed.type;
+          for (auto& y : yields) {
+            auto v = y->eval(g);
+            if (!v.ok()) return goError(v.st.msg);
+            rc.v.push_back(v.v);
+          }
+          recs.push_back(std::move(rc));
+        }
+      }
+    }
+    if (recs.empty()) return out;
+    const int32_t t0 = edgeContextOrder(etypes)[0];
+    const Schema* rowSchema = resp.edgeSchema.count(t0) ? &resp.edgeSchema.at(t0) : nullptr;
+    // the last getter's type, post-order (GoExecutor.cpp:851-945 save the type as they run)
+    std::function<void(const Expr*, SType*)> last = [&](const Expr* e, SType* t) {
+      if (!e) return;
+      last(e->a.get(), t);
+      last(e->b.get(), t);
+      for (auto& x : e->args) last(x.get(), t);
+      switch (e->kind) {
+        case kAliasProp: case kEdgeRank: case kEdgeDstId: case kEdgeSrcId:
+          if (st.edgeByName.count(e->alias)) *t = rowSchema ? rowSchema->typeOf(e->prop) : ST_UNKNOWN;
+          break;
+        case kSourceProp: case kDestProp: {
+          auto it = st.tagByName.find(e->alias);
+          if (it == st.tagByName.end()) break;
+          const Schema* ts = st.tagSchema(it->second);
+          *t = ts ? ts->typeOf(e->prop) : ST_UNKNOWN;
+          break;
+        }
+        case kInputProp: case kVariableProp: {
+          static const SType km[4] = {ST_INT, ST_DOUBLE, ST_BOOL, ST_STRING};
+          *t = ST_UNKNOWN;
+          for (size_t c = 0; c < q.inputNames.size(); ++c)
+            if (q.inputNames[c] == e->prop && c < q.inputKinds.size()) *t = km[q.inputKinds[c] & 3];
+          break;
+        }
+        default: break;
+      }
+    };
+    const Rec* first = &recs[0];
+    for (auto& r : recs)
+      if (r.type == t0) { first = &r; break; }
+    Schema outSchema;
+    bool floatCol = false;
+    for (size_t i = 0; i < yields.size(); ++i) {
+      SType t = ST_UNKNOWN;
+      if (yields[i]->kind == kTypeCasting) {
+        static const SType m[] = {ST_INT, ST_STRING, ST_DOUBLE, ST_INT, ST_BOOL, ST_TIMESTAMP};
+        t = m[yields[i]->castType % 6];
+      } else {
+        last(yields[i].get(), &t);
+      }
+      if (t == ST_UNKNOWN) {
+        static const SType m[] = {ST_INT, ST_DOUBLE, ST_BOOL, ST_STRING};
+        t = m[first->v[i].index()];
+      }
+      floatCol = floatCol || t == ST_FLOAT;
+      outSchema.cols.push_back({colNames[i], t});
+    }
+    if (floatCol) return goError("Unknown Type: 4");
+    std::unordered_set<std::string> uniq;
+    for (auto& r : recs) {
+      RowWriter w(&outSchema);
+      for (auto& v : r.v) w.putValue(v, ST_UNKNOWN);
+      std::string enc = w.encode();
+      if (q.distinct && !uniq.insert(enc).second) continue;
+      RowReader back(enc, &outSchema);
+      std::vector<Value> decoded;
+      for (size_t i = 0; i < r.v.size(); ++i) {
+        auto v = back.getIdx((int)i);
+        if (!v.ok()) return goError("Get value from interim failed");
+        decoded.push_back(v.v);
+      }
+      out.rows.push_back(std::move(decoded));
+    }
+    return out;
+  };
+
   for (uint32_t cur = 1;; ++cur) {
     bool final = cur >= steps;
     // getStepOutProps (GoExecutor.cpp:587-630)
@@ -297,128 +418,11 @@ ResultSet runGo(const Store& st, const GoQuery& q) {
       VertexHolder holder;
       holder.add(vresp);
       // fallthrough to finish with holder
-      GoGetters g(st);
-      g.holder = &holder;
-      g.q = &q;
-      g.index = hasInput ? &index : nullptr;
-      g.tracker = steps > 1 ? &tracker : nullptr;
-      // processFinalResult + setupInterimResult
-      std::unique_ptr<Schema> outSchema;
-      std::unordered_set<std::string> uniq;
-      for (auto& vd : resp.vertices) {
-        for (auto& ed : vd.edges) {
-          const Schema& s = resp.edgeSchema.at(ed.type);
-          for (auto& row : rowSetSplit(ed.data)) {
-            RowReader r(row, &s);
-            g.edgeType = ed.type; g.row = &r; g.rowSchema = &s; g.srcVid = vd.vid;
-            g.edgeSchema = &resp.edgeSchema; g.tagSchema = &resp.vertexSchema; g.tagData = &vd.tags;
-            g.saveType = false;
-            if (filter) {
-              auto v = filter->eval(g);
-              if (!v.ok()) { ResultSet e = goError(v.st.msg); return e; }
-              if (!asBool(v.v)) continue;
-            }
-            std::vector<Value> rec; std::vector<SType> types;
-            for (auto& y : yields) {
-              types.push_back(ST_UNKNOWN);
-              g.saveType = true; g.colType = &types.back();
-              auto v = y->eval(g);
-              g.saveType = false;
-              if (!v.ok()) { ResultSet e = goError(v.st.msg); return e; }
-              if (y->kind == kTypeCasting) {
-                static const SType m[] = {ST_INT, ST_STRING, ST_DOUBLE, ST_INT, ST_BOOL, ST_TIMESTAMP};
-                types.back() = m[y->castType % 6];
-              }
-              rec.push_back(v.v);
-            }
-            if (!outSchema) {
-              outSchema = std::make_unique<Schema>();
-              for (size_t i = 0; i < rec.size(); ++i) {
-                SType t = types[i];
-                if (t == ST_UNKNOWN) {
-                  static const SType m[] = {ST_INT, ST_DOUBLE, ST_BOOL, ST_STRING};
-                  t = m[rec[i].index()];
-                }
-                outSchema->cols.push_back({colNames[i], t});
-              }
-            }
-            RowWriter w(outSchema.get());
-            for (size_t i = 0; i < rec.size(); ++i) w.putValue(rec[i], ST_UNKNOWN);
-            std::string enc = w.encode();
-            if (q.distinct && !uniq.insert(enc).second) continue;
-            RowReader back(enc, outSchema.get());
-            std::vector<Value> decoded;
-            for (size_t i = 0; i < rec.size(); ++i) {
-              auto v = back.getIdx((int)i);
-              decoded.push_back(v.ok() ? v.v : Value(int64_t(0)));
-            }
-            out.rows.push_back(std::move(decoded));
-          }
-        }
-      }
-      return out;
+      return finish(resp, &holder);
     }
     // final step without $$ props
     VertexHolder holder;
-    GoGetters g(st);
-    g.holder = &holder;
-    g.q = &q;
-    g.index = hasInput ? &index : nullptr;
-    g.tracker = steps > 1 ? &tracker : nullptr;
-    std::unique_ptr<Schema> outSchema;
-    std::unordered_set<std::string> uniq;
-    for (auto& vd : resp.vertices) {
-      for (auto& ed : vd.edges) {
-        const Schema& s = resp.edgeSchema.at(ed.type);
-        for (auto& row : rowSetSplit(ed.data)) {
-          RowReader r(row, &s);
-          g.edgeType = ed.type; g.row = &r; g.rowSchema = &s; g.srcVid = vd.vid;
-          g.edgeSchema = &resp.edgeSchema; g.tagSchema = &resp.vertexSchema; g.tagData = &vd.tags;
-          g.saveType = false;
-          if (filter) {
-            auto v = filter->eval(g);
-            if (!v.ok()) return goError(v.st.msg);
-            if (!asBool(v.v)) continue;
-          }
-          std::vector<Value> rec; std::vector<SType> types;
-          for (auto& y : yields) {
-            types.push_back(ST_UNKNOWN);
-            g.saveType = true; g.colType = &types.back();
-            auto v = y->eval(g);
-            g.saveType = false;
-            if (!v.ok()) return goError(v.st.msg);
-            if (y->kind == kTypeCasting) {
-              static const SType m[] = {ST_INT, ST_STRING, ST_DOUBLE, ST_INT, ST_BOOL, ST_TIMESTAMP};
-              types.back() = m[y->castType % 6];
-            }
-            rec.push_back(v.v);
-          }
-          if (!outSchema) {
-            outSchema = std::make_unique<Schema>();
-            for (size_t i = 0; i < rec.size(); ++i) {
-              SType t = types[i];
-              if (t == ST_UNKNOWN) {
-                static const SType m[] = {ST_INT, ST_DOUBLE, ST_BOOL, ST_STRING};
-                t = m[rec[i].index()];
-              }
-              outSchema->cols.push_back({colNames[i], t});
-            }
-          }
-          RowWriter w(outSchema.get());
-          for (size_t i = 0; i < rec.size(); ++i) w.putValue(rec[i], ST_UNKNOWN);
-          std::string enc = w.encode();
-          if (q.distinct && !uniq.insert(enc).second) continue;
-          RowReader back(enc, outSchema.get());
-          std::vector<Value> decoded;
-          for (size_t i = 0; i < rec.size(); ++i) {
-            auto v = back.getIdx((int)i);
-            decoded.push_back(v.ok() ? v.v : Value(int64_t(0)));
-          }
-          out.rows.push_back(std::move(decoded));
-        }
-      }
-    }
-    return out;
+    return finish(resp, &holder);
   }
 }
 

@@ -271,6 +271,7 @@ struct GoQuery {
   bool distinct = false;
   // piped / variable input ($-.col, $var.col): the FROM source's rows (InterimResult)
   std::vector<std::string> inputNames;
+  std::vector<uint8_t> inputKinds;   // 0 INT, 1 DOUBLE, 2 BOOL, 3 STRING per input column
   std::vector<std::vector<Value>> inputRows;
   int inputVidCol = -1;
 };

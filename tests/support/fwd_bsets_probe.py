@@ -18,6 +18,7 @@ def main():
         src, dst, w = graphs.rmat_graph(scale)
         single = graphs.rmat_engine(src, dst, w)
         c = LocalCluster(100, world)
+        c.set_path_replica(0)
         c.register_edge(graphs.E_TYPE, "e", graphs.E_SCHEMA)
         c.load_edges(graphs.E_TYPE, src, dst, [w])
         c.finalize()

@@ -107,11 +107,13 @@ def tagged_register(be, is_engine):
             be.register_tag(ident, name, cols)
 
 
-def tagged_pair_cluster(scale, world, parts=7, seed=5, max_edge=0x7FFFFFFF):
-    """The tagged_pair records on a partitioned in-process cluster of `world` ranks."""
+def tagged_pair_cluster(scale, world, parts=7, seed=5, max_edge=0x7FFFFFFF, replica=False):
+    """The tagged_pair records on a partitioned in-process cluster of `world` ranks (FIND PATH:
+    the collective search unless `replica`)."""
     from nebula_amd import LocalCluster
     _, _, kb = tagged_kv(scale, parts, seed)
     c = LocalCluster(parts, world, max_edge_returned_per_vertex=max_edge)
+    c.set_path_replica(1 if replica else 0)
     tagged_register(c, True)
     c.load_builder(kb)
     return c

@@ -329,6 +329,11 @@ class CsrOracle:
         L.orc_csr_go.argtypes = [vp, vp, u64, u32, i32, i64, i32, vp, vp, u64]
         L.orc_csr_shortest.restype = i32
         L.orc_csr_shortest.argtypes = [vp, i64, i64, u32, vp, C.POINTER(u64)]
+        L.orc_csr_go_multi.restype = C.c_double
+        L.orc_csr_go_multi.argtypes = [vp, i32, vp, u64, u32, vp]
+        L.orc_csr_walk_counts.argtypes = [vp, i64, i64, u32, vp]
+        L.orc_csr_all_walks.restype = u64
+        L.orc_csr_all_walks.argtypes = [vp, i64, i64, u32, vp, u64]
         self.L = L
         src = np.ascontiguousarray(src, np.int64)
         dst = np.ascontiguousarray(dst, np.int64)
@@ -371,6 +376,30 @@ class CsrOracle:
         sc = C.c_uint64()
         n = self.L.orc_csr_shortest(self.h, int(s), int(t), upto, _ptr(buf), C.byref(sc))
         return ([int(x) for x in buf[:n + 1]] if n else []), sc.value
+
+    @staticmethod
+    def go_multi(csrs, starts, steps):
+        """GO `steps` STEPS OVER several types (one CsrOracle per OVER type, in OVER order), default
+        YIELD (one _dst column per type): -> (digest, edges scanned)."""
+        s = np.asarray(starts, np.int64)
+        hs = (C.c_void_p * len(csrs))(*[c.h for c in csrs])
+        out = np.zeros(4, np.uint64)
+        csrs[0].L.orc_csr_go_multi(hs, len(csrs), _ptr(s), len(s), steps, _ptr(out))
+        return (int(out[0]), int(out[1]), int(out[2])), int(out[3])
+
+    def walk_counts(self, s, t, upto):
+        """Walks s -> t of exactly L edges for L = 0..upto (FIND ALL PATH's answer size per length)."""
+        out = np.zeros(upto + 1, np.uint64)
+        self.L.orc_csr_walk_counts(self.h, int(s), int(t), upto, _ptr(out))
+        return [int(x) for x in out]
+
+    def all_walks(self, s, t, upto, cap=100000):
+        """Every walk s -> t of 1..upto edges as a vid list (None when there are more than cap)."""
+        buf = np.zeros((cap, upto + 1), np.int64)
+        n = self.L.orc_csr_all_walks(self.h, int(s), int(t), upto, _ptr(buf), cap)
+        if n > cap:
+            return None
+        return [[int(v) for v in row if v != -1] for row in buf[:n]]
 
     def close(self):
         if getattr(self, "h", None):

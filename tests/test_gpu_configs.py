@@ -5,7 +5,11 @@
   C4  FIND SHORTEST PATH UPTO 5 on RMAT-22: 256 pairs (seed 7), canonical paths
   C3  RMAT-26 (1.07 G samples, the headline graph): device digest (nbg_rows_digest) vs the CSR
       oracle's digest for the bench's 16 roots, a sampled full compare for 2 roots, and 64
-      SHORTEST pairs
+      SHORTEST pairs; the same graph PARTITIONED over 2 ranks (P = 100, parts p % 2), digests
+      summed over ranks for the 16 roots and 32 SHORTEST pairs entry by entry
+  C5  the LDBC substitute at the bench's size (knows RMAT-20 + likes RMAT-19): GO 4 STEPS OVER
+      knows, likes by digest for the bench's 16 roots (two-type CSR oracle), FIND ALL PATH UPTO 4
+      for its 64 pairs: path counts vs walk counts, entry lists where a pair has <= 20 k paths
 
 The checker is oracle/csr.cpp (CSR restatement, pinned to the storaged-faithful oracle on
 RMAT <= 12 by tests/test_oracle_csr.py).  Graphs are the bench's own (nebula_amd.rmat)."""
@@ -110,6 +114,50 @@ def rmat26():
     csr.close()
 
 
+def _combine(digests):
+    """Per-rank row digests of one partitioned query -> the query's (rows +, xor ^, sum + mod 2^64)."""
+    rows, x, sm = 0, 0, 0
+    for d in digests:
+        rows += d[0]
+        x ^= d[1]
+        sm = (sm + d[2]) & ((1 << 64) - 1)
+    return rows, x, sm
+
+
+@pytest.mark.timeout(1200)
+def test_c3_rmat26_partitioned_two_ranks(rmat26):
+    """BASELINE C3's sharded form at full size: RMAT-26, P = 100, 2 ranks (parts p % 2) in one
+    process on one MI355X (the in-process transport; the RCCL path is test_gpu_rccl.py).  Every
+    bench root's rows (summed over the ranks that produced them) and scanned-edge count equal the
+    CSR oracle's; 32 bench SHORTEST pairs equal the oracle's canonical paths."""
+    from nebula_amd import LocalCluster
+    src, dst, eng, csr, sv, av = rmat26
+    _, _, w = rmat.rmat_edges_fast(26)
+    c = LocalCluster(100, 2)
+    try:
+        c.register_edge(1, "e", [("w", 2)])
+        c.load_edges(1, src, dst, [w])
+        del w
+        c.finalize()
+        stmts = c.each(lambda e: e.prepare_go([1], 3, WHERE))
+        roots = [int(x) for x in rmat.pick_roots(src, 16, 42, verts=sv)]
+        for r in roots:
+            res = c.each_indexed(lambda i, e: stmts[i].run_device([r]))
+            got = _combine([x.digest() for x in res])
+            scanned = {x.edges_scanned for x in res}   # every rank reports the whole query
+            for x in res:
+                x.free()
+            digest, exp_scanned, _, _ = csr.go([r], 3, "<", 50, Y_DST)
+            assert got == digest, r
+            assert scanned == {exp_scanned}, r
+        for st in stmts:
+            st.free()
+        pairs = rmat.pick_pairs(src, dst, 32, 7, verts=av)
+        assert _check_pairs(c, csr, pairs) > 10
+    finally:
+        c.close()
+
+
 @pytest.mark.timeout(1200)
 def test_c3_rmat26_digests(rmat26):
     src, dst, eng, csr, sv, _ = rmat26
@@ -197,3 +245,64 @@ def test_c5_substitute_go4_and_all_paths():
     finally:
         eng.close()
         orc.close()
+
+
+@pytest.fixture(scope="module")
+def c5_bench():
+    """The bench's C5 graph (bench.py c5_leg at its default --c5-scale 20) on one engine and as two
+    CSR oracles (knows, likes)."""
+    (ks, kd, kw), (ls, ld, lw) = _c5_graph(20)
+    eng = Engine(100)
+    eng.register_edge(1, "knows", [("w", 2)])
+    eng.register_edge(2, "likes", [("w", 2)])
+    eng.load_edges(1, ks, kd, [kw])
+    eng.load_edges(2, ls, ld, [lw])
+    eng.finalize()
+    th = min(16, os.cpu_count() or 8)
+    ck, cl = CsrOracle(ks, kd, kw, threads=th), CsrOracle(ls, ld, lw, threads=th)
+    yield ks, kd, eng, ck, cl
+    eng.close()
+    ck.close()
+    cl.close()
+
+
+@pytest.mark.timeout(900)
+def test_c5_rmat20_go4_digests(c5_bench):
+    """GO 4 STEPS OVER knows, likes (default YIELD knows._dst, likes._dst) from the bench's 16
+    roots: device digest and scanned edges equal the two-type CSR oracle's."""
+    ks, kd, eng, ck, cl = c5_bench
+    roots = [int(x) for x in rmat.pick_roots(ks, 16, 42)]
+    stmt = eng.prepare_go([1, 2], 4)
+    try:
+        total = 0
+        for r in roots:
+            res = stmt.run_device([r])
+            digest, scanned = CsrOracle.go_multi([ck, cl], [r], 4)
+            assert res.digest() == digest, r
+            assert res.edges_scanned == scanned, r
+            total += res.count
+            res.free()
+        assert total > 10 ** 6
+    finally:
+        stmt.free()
+
+
+@pytest.mark.timeout(900)
+def test_c5_rmat20_all_paths(c5_bench):
+    """FIND ALL PATH UPTO 4 STEPS OVER knows for the bench's 64 pairs: every pair's path count equals
+    the number of walks of 1..4 edges (walk-count DP); pairs with at most 20 k paths are compared
+    entry list by entry list with the oracle's walk enumeration."""
+    ks, kd, eng, ck, cl = c5_bench
+    persons = np.union1d(np.unique(ks), np.unique(kd))
+    pairs = rmat.pick_pairs(ks, kd, 64, 7, verts=persons)
+    total = compared = 0
+    for s, t in pairs:
+        got = eng.find_path([s], [t], [1], 4, shortest=False)
+        assert len(got) == sum(ck.walk_counts(s, t, 4)[1:]), (s, t)
+        total += len(got)
+        if len(got) <= 20000:
+            walks = ck.all_walks(s, t, 4, cap=20000)
+            exp = sorted([w[0]] + [x for v in w[1:] for x in (1, 0, v)] for w in walks)
+            assert got == exp, (s, t)
+            compared += 1
+    assert total > 10000 and compared >= 32

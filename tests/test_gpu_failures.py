@@ -51,6 +51,7 @@ def _hub(src, dst):
 
 def _cluster(src, dst, w, world):
     c = LocalCluster(100, world)
+    c.set_path_replica(0)   # FIND PATH failures of the collective search
     c.register_edge(graphs.E_TYPE, "e", graphs.E_SCHEMA)
     c.load_edges(graphs.E_TYPE, src, dst, [w])
     c.finalize()

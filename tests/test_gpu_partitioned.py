@@ -22,8 +22,11 @@ WHERES = {
 }
 
 
-def cluster_for(src, dst, w, world, parts=100, max_edge=0x7FFFFFFF):
+def cluster_for(src, dst, w, world, parts=100, max_edge=0x7FFFFFFF, replica=False):
+    """A partitioned cluster.  FIND PATH here tests the COLLECTIVE search over the partitioned
+    snapshot, so the path replica is off unless asked for (test_gpu_replica.py covers it)."""
     c = LocalCluster(parts, world, max_edge_returned_per_vertex=max_edge)
+    c.set_path_replica(1 if replica else 0)
     c.register_edge(graphs.E_TYPE, "e", graphs.E_SCHEMA)
     c.load_edges(graphs.E_TYPE, src, dst, [w])
     c.finalize()
@@ -255,6 +258,7 @@ def test_partitioned_all_paths_multi_edge_ranks():
 def test_partitioned_shortest_nba_golden(nba_data):
     """The reference's FindPathTest golden cases on 3 ranks (7 parts)."""
     c = LocalCluster(7, 3)
+    c.set_path_replica(0)   # the collective search
     for (kind, name), cols in kvgen.NBA_SCHEMAS.items():
         if kind == "edge":
             c.register_edge(kvgen.NBA_EDGES[name], name, cols)

@@ -149,6 +149,7 @@ def test_partitioned_capped_paths(rmat11, world, k):
     so every rank returns the single engine's (and the oracle's) paths."""
     src, dst, w = rmat11
     c = LocalCluster(100, world, max_edge_returned_per_vertex=k)
+    c.set_path_replica(0)   # the collective capped search (the replica runs the single-engine one)
     c.register_edge(graphs.E_TYPE, "e", graphs.E_SCHEMA)
     c.load_edges(graphs.E_TYPE, src, dst, [w])
     c.finalize()

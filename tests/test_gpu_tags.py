@@ -91,10 +91,10 @@ def test_unknown_dst_tag_without_final_edges(tg):
     [E.binop("%", E.edge_prop("e", "w"), E.const(10))],
     [DP("person", "name"), DP("city", "pop")],
     [E.edge_prop("e", "_dst"), E.edge_prop("f", "_dst")],
-    # (a YIELD whose result kind differs from the prop it reads, e.g. `$$.p.score > 5.0`, is written
-    # by the reference into a column typed by the prop: RowWriter logs "Incompatible value type"
-    # and emits a default, RowWriter.cpp:103-119 — a garbled row; such columns are not compared)
     [E.binop("*", DP("person", "score"), E.const(2.0)), E.const("x")],
+    # kinds other than the column's type: RowWriter's defaults, then DISTINCT on the encoded rows
+    [E.binop(">", E.edge_prop("e", "w"), E.const(30))],
+    [E.binop("*", E.edge_prop("e", "w"), E.const(1.5)), SP("person", "name")],
 ])
 def test_distinct_parity(tg, steps, yields):
     src, persons, eng, orc = tg
@@ -122,3 +122,36 @@ def test_distinct_rmat_large():
     finally:
         eng.close()
         orc.close()
+
+
+# ---------------------------------------------------------------------------- result column typing
+# GoExecutor::setupInterimResult types each YIELD column by the last prop its expression reads (or
+# a root cast), writes every row through that schema with RowWriter — a value of another kind
+# becomes the writer's default, RowWriter.cpp:103-186 — and InterimResult::getRows reads the rows
+# back by the schema (InterimResult.cpp:74-153): aligned defaults read as 0 / false / "", a default
+# of another length shifts the later columns, a read past the row's end or a FLOAT column fails.
+TYPING = {
+    "bool_in_int": [E.binop(">", E.edge_prop("e", "w"), E.const(30))],
+    "bool_in_string": [E.binop("==", SP("person", "name"), E.const("p3")), E.edge_prop("e", "_dst")],
+    "double_in_int_last": [E.binop("*", E.edge_prop("e", "w"), E.const(1.5))],
+    "double_in_int_then_string": [E.binop("*", E.edge_prop("e", "w"), E.const(1.5)), SP("person", "name")],
+    "double_in_int_then_int": [E.binop("+", SP("person", "age"), E.const(0.5)), E.edge_prop("e", "w")],
+    "double_in_int_then_vid": [E.binop("+", E.edge_prop("e", "w"), E.const(0.5)), E.edge_prop("e", "_dst")],
+    "bool_in_double_last": [E.binop(">", DP("person", "score"), E.const(5.0))],
+    "bool_in_double_then_vid": [E.binop(">", DP("person", "score"), E.const(5.0)), E.edge_prop("e", "_dst")],
+    "cast_root": [E.cast("int", DP("person", "score")), E.binop("+", E.edge_prop("e", "w"), E.const(1))],
+    "bool_in_vid_then_int": [E.binop(">", E.edge_prop("e", "_dst"), E.const(0)), E.edge_prop("e", "w")],
+    "int_in_double_then_string": [E.binop("+", E.cast("int", DP("person", "score")), E.const(0)), SP("person", "name")],
+}
+
+
+@pytest.mark.parametrize("name", list(TYPING))
+@pytest.mark.parametrize("distinct", [False, True])
+def test_result_column_typing(tg, name, distinct):
+    src, persons, eng, orc = tg
+    starts = person_roots(src, persons, 4, seed=len(name))
+    yields = [y.encode() for y in TYPING[name]]
+    for over in ([graphs.E_TYPE], [graphs.E_TYPE, graphs.E_F]):
+        (g, ge), (o, oe) = both(eng, orc, starts, over, 1, b"", yields, distinct=distinct)
+        assert (ge is None) == (oe is None), (name, over, ge, oe)
+        assert g == o, (name, over)

@@ -101,3 +101,44 @@ def test_shortest_csr_self_cycles():
     finally:
         orc.close()
         csr.close()
+
+
+def test_csr_multi_type_go_and_walks_match_faithful_oracle():
+    """The C5 extensions of the CSR oracle (several OVER types with the default YIELD; FIND ALL
+    PATH walk counts and enumeration) against the storaged-faithful restatement on small graphs
+    (the C5 substitute's shape: knows RMAT + likes bipartite RMAT)."""
+    import numpy as np
+    from nebula_amd import rmat
+    from tests.support import graphs
+    from tests.support.oracle import CsrOracle, Oracle, row_digest
+    ks, kd, kw = rmat.rmat_edges_fast(9)
+    ls, ld, lw = rmat.rmat_edges_fast(8, seed=rmat.SEED_BASE ^ 0x6C696B6573)
+    persons = np.union1d(np.unique(ks), np.unique(kd))
+    ls = persons[(ls.astype(np.uint64) % np.uint64(len(persons))).astype(np.int64)]
+    ld = ld ^ (1 << 61)
+    orc = Oracle(100)
+    for t, name in ((1, "knows"), (2, "likes")):
+        orc.register(True, t, name, [("w", 2)])
+    orc.load_edges(1, ks, kd, [kw])
+    orc.load_edges(2, ls, ld, [lw])
+    orc.finalize()
+    ck, cl = CsrOracle(ks, kd, kw, threads=2), CsrOracle(ls, ld, lw, threads=2)
+    try:
+        for r in [int(x) for x in rmat.pick_roots(ks, 6, 42)]:
+            for steps in (1, 2, 4):
+                rows = orc.go([r], [1, 2], steps)
+                dig, _ = CsrOracle.go_multi([ck, cl], [r], steps)
+                assert dig == row_digest(rows), (r, steps)
+        n = 0
+        for s, t in rmat.pick_pairs(ks, kd, 12, 7):
+            exp = sorted(orc.find_path([s], [t], [1], 4, False))
+            cnt = ck.walk_counts(s, t, 4)
+            assert sum(cnt[1:]) == len(exp)
+            walks = ck.all_walks(s, t, 4)
+            assert sorted([w[0]] + [x for v in w[1:] for x in (1, 0, v)] for w in walks) == exp
+            n += len(exp)
+        assert n > 0
+    finally:
+        orc.close()
+        ck.close()
+        cl.close()

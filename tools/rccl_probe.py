@@ -76,17 +76,27 @@ def main():
                 print(f"slot query {i} (device={bool(rnd)}) root {r}: {len(got)} rows {'OK' if good else 'MISMATCH'}",
                       flush=True)
     stmt.free()
-    # FIND SHORTEST PATH: every rank reconstructs the same paths (collective BFS + greedy)
+    # FIND SHORTEST PATH: on the replica (built at finalize over RCCL, rank-local queries), then
+    # the collective search (BFS levels + greedy over the partitioned snapshot); every rank
+    # returns the single engine's paths
     from nebula_amd import rmat
-    for s, t in rmat.pick_pairs(src, dst, 8, seed=17):
-        mine = eng.find_path([s], [t], [1], 5)
-        parts = [None] * world
-        dist.all_gather_object(parts, mine)
-        if rank == 0:
-            ref = single.find_path([s], [t], [1], 5)
-            good = all(p == ref for p in parts)
-            ok &= good
-            print(f"path {s}->{t}: {ref[0] if ref else []} {'OK' if good else 'MISMATCH'}", flush=True)
+    replica = eng.path_replica_active
+    if rank == 0:
+        print(f"path replica built over RCCL: {replica}", flush=True)
+    ok &= replica
+    for mode in (1, 0):
+        if replica:
+            eng.set_path_replica(mode)
+        for s, t in rmat.pick_pairs(src, dst, 8, seed=17 + mode):
+            mine = eng.find_path([s], [t], [1], 5)
+            parts = [None] * world
+            dist.all_gather_object(parts, mine)
+            if rank == 0:
+                ref = single.find_path([s], [t], [1], 5)
+                good = all(p == ref for p in parts)
+                ok &= good
+                print(f"path ({'replica' if mode else 'collective'}) {s}->{t}: {ref[0] if ref else []} "
+                      f"{'OK' if good else 'MISMATCH'}", flush=True)
     # Failures on ONE rank: every rank must return the same code (agreed before the query's first
     # collective) and stay usable afterwards (include/nbg.h, failure semantics).
     from nebula_amd import NbgError, _lib as L
