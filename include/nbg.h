@@ -450,6 +450,13 @@ int32_t nbg_comm_aborted(const nbg_engine* e);
 #define NBG_FAULT_ALLOC  1   /* the query's workspace / held-result hand-over allocation fails */
 #define NBG_FAULT_DEVICE 2   /* partitioned GO: a device error after the query's first collective */
 int32_t nbg_inject_fault(nbg_engine* e, int32_t site, int32_t count);
+/* The edge records this engine staged for signed edge type `type` (+t: out-edges keyed at src,
+ * -t: in-edges keyed at dst), in load order, before nbg_finalize: a partitioned rank keeps the
+ * records of the parts it serves (CreateSpaceProcessor.cpp:84-95 with GPUs as hosts), so the
+ * ranks' lists partition the load.  Host only (no device call).  *n = the record count; up to
+ * `cap` of them are written to src / dst / rank (any may be NULL).  NBG_E_STATE once finalized. */
+int32_t nbg_staged_edges(const nbg_engine* e, int32_t type, int64_t* src, int64_t* dst, int64_t* rank, uint64_t cap,
+                         uint64_t* n);
 
 #ifdef __cplusplus
 }

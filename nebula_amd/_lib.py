@@ -153,6 +153,7 @@ SIGNATURES = [
     ("nbg_comm_abort", i32, [vp]),
     ("nbg_comm_aborted", i32, [vp]),
     ("nbg_inject_fault", i32, [vp, i32, i32]),
+    ("nbg_staged_edges", i32, [vp, i32, vp, vp, vp, u64, C.POINTER(u64)]),
     ("nbg_path_reserve", i32, [vp, i32, i32]),
 ]
 

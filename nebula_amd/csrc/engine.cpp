@@ -1368,6 +1368,26 @@ int32_t nbg_inject_fault(nbg_engine* h, int32_t site, int32_t count) {
   return NBG_OK;
 }
 
+int32_t nbg_staged_edges(const nbg_engine* h, int32_t type, int64_t* src, int64_t* dst, int64_t* rank, uint64_t cap,
+                         uint64_t* n) {
+  if (!h || !n || type == 0) return NBG_E_INVALID_ARGUMENT;
+  const Engine& E = h->e;
+  std::lock_guard<std::mutex> lg(const_cast<Engine&>(E).mu);
+  if (E.finalized) return NBG_E_STATE;
+  *n = 0;
+  auto it = E.stage.find(type);
+  if (it == E.stage.end()) return NBG_OK;
+  const EdgeStage& st = it->second;
+  *n = st.size();
+  const uint64_t m = std::min<uint64_t>(cap, st.size());
+  for (uint64_t i = 0; i < m; ++i) {
+    if (src) src[i] = st.src[i];
+    if (dst) dst[i] = st.dst[i];
+    if (rank) rank[i] = st.rank.empty() ? 0 : st.rank[i];
+  }
+  return NBG_OK;
+}
+
 const char* nbg_last_error(const nbg_engine* h) { return h ? h->e.last_error.c_str() : "null engine"; }
 
 static int32_t reg_schema(std::map<int32_t, SchemaSet>& m, int32_t id, const char* name, int64_t ver,

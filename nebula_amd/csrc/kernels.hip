@@ -114,7 +114,8 @@ struct Workspace {
   InlineIds inl{};
   uint64_t prog_stmt = 0;          // statement whose programs d_prog holds
   QState* q = nullptr;            // device query state
-  QState* h_q = nullptr;          // pinned host mirror
+  QState* h_q = nullptr;          // pinned host mirror (mapped: k_q_out stores into it)
+  QState* d_hq = nullptr;         // its device address
   uint32_t* h_starts = nullptr;   // pinned staging for start ids
   uint64_t cap_starts = 0;
   Ins* h_prog = nullptr;          // pinned staging for programs
@@ -603,6 +604,9 @@ struct BfsParams {
   // over nds (the next step's first OVER type); nlist.zero_next is zeroed by workgroup 0
   ListOut nlist;
   DegSrc nds;
+  // MARK claim mode: a per-wave direct-mapped LDS cache of the neighbours this wave already
+  // claimed or saw claimed filters repeats before the global label read + CAS (NBG_MARK_DEDUP)
+  int lds_dedup;
   // MARK on a partitioned engine (non-null): neighbours set their bit of the global id space in
   // this bitmap (the hop's all-to-all send buffer) instead of a byte flag — no pack pass
   unsigned long long* bits;
@@ -638,14 +642,28 @@ struct FinalParams {
 // owns it — and the owners appended to the next frontier list together with their edge space
 // over the next step's first OVER type: one packed atomic per wave for list positions and edge
 // offsets.  A vertex without edges there is kept (the list is the frontier of every OVER type).
-__device__ __forceinline__ void claim_append(const uint32_t (&u)[VT], const BfsParams& bp, int lane) {
+constexpr int SEEN_BITS = 9;                     // MARK LDS pre-dedup: 512 entries per wave
+__device__ __forceinline__ uint32_t seen_slot(uint32_t x) { return (x * 0x9E3779B1u) >> (32 - SEEN_BITS); }
+
+__device__ __forceinline__ void claim_append(const uint32_t (&u)[VT], const BfsParams& bp, int lane, uint32_t* seen) {
   uint32_t dg[VT], rs[VT], cmask = 0;
+  uint32_t hit = 0;
+  if (seen) {   // (a vertex in the cache was claimed at this step by this wave or by someone before it)
+#pragma unroll
+    for (int i = 0; i < VT; ++i) {
+      const uint32_t x = u[i];
+      if (x == NO_ROW) continue;
+      const uint32_t sl = seen_slot(x);
+      if (seen[sl] == x) hit |= 1u << i;
+      else seen[sl] = x;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < VT; ++i) {
     dg[i] = 0;
     rs[i] = 0;
     const uint32_t x = u[i];
-    if (x == NO_ROW) continue;
+    if (x == NO_ROW || ((hit >> i) & 1u)) continue;
     const uint32_t old = bp.lab[x];
     if (old == bp.stamp) continue;
     if (atomicCAS(bp.lab + x, old, bp.stamp) != old) continue;
@@ -739,6 +757,8 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
   extern __shared__ int64_t regs[];               // FINAL generic path: [nregs][BLOCK]
 
   __shared__ uint32_t sIl[INL ? 3 * INLINE_STARTS : 1];   // INL: end[], rs[], id[] of the start list
+  constexpr bool kClaims = M == MARK || M == MARKB;
+  __shared__ uint32_t sSeenAll[WAVES][kClaims ? (1 << SEEN_BITS) : 1];   // MARK: LDS pre-dedup cache
   uint64_t n, total;   // list entries, edges
   if constexpr (INL) {
     n = il.n;
@@ -769,6 +789,13 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
   const uint64_t ntiles = (npath + TV - 1) / TV;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar registers
+  uint32_t* seen = nullptr;
+  if constexpr (kClaims) {
+    if (bp.lab && bp.lds_dedup) {
+      seen = sSeenAll[w];
+      for (int k = lane; k < (1 << SEEN_BITS); k += 64) seen[k] = NO_ROW;
+    }
+  }
   uint32_t* const sEnd = sEndAll[w];
   uint32_t* const sRs = sRsAll[w];
   uint16_t* const sSeg = sSegAll[w];
@@ -942,7 +969,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
           if (!bp.lab) flags[u[i]] = 1;
         }
       }
-      if (bp.lab) claim_append(u, bp, lane);
+      if (bp.lab) claim_append(u, bp, lane, seen);
     } else if constexpr (M == MARK) {
       uint32_t u[V];   // all neighbour loads in flight before the flag stores / claims
 #pragma unroll
@@ -955,7 +982,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
         }
       }
       if (bp.lab) {
-        claim_append(u, bp, lane);
+        claim_append(u, bp, lane, seen);
       } else if (bp.sparse) {
 #pragma unroll
         for (int i = 0; i < V; ++i) {
@@ -1628,7 +1655,9 @@ Workspace* ws_create(uint64_t max_frontier, uint64_t nv, uint64_t e_max, hipStre
   M((void**)&w->d_prog, (size_t)MAX_TYPES_Q * MAX_PROGRAM * sizeof(Ins));
   M((void**)&w->d_row_cols, MAX_YIELDS * sizeof(int64_t*));
   if (e == hipSuccess)
-    e = hipHostMalloc((void**)&w->h_q, sizeof(QState) + (size_t)MAX_TYPES_Q * EXPAND_GRID * 4, hipHostMallocDefault);
+    e = hipHostMalloc((void**)&w->h_q, sizeof(QState) + (size_t)MAX_TYPES_Q * EXPAND_GRID * 4,
+                      hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&w->d_hq, w->h_q, 0);
   if (e == hipSuccess) {
     w->blk_rows = reinterpret_cast<uint32_t*>(w->q + 1);
     w->h_blk_rows = reinterpret_cast<uint32_t*>(w->h_q + 1);
@@ -1860,6 +1889,8 @@ hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, 
       w->step_stamp = w->seen_stamp;
     }
     bp.lab = w->seen;
+    static const int dedup = getenv("NBG_MARK_DEDUP") ? atoi(getenv("NBG_MARK_DEDUP")) : 0;
+    bp.lds_dedup = dedup;
     bp.stamp = w->step_stamp;
     const int nset = w->cur ^ 1;
     bp.nds = deg_src(next0);
@@ -2427,14 +2458,24 @@ hipError_t ws_rows_digest(Workspace* w, const std::vector<std::pair<uint64_t, ui
   return e;
 }
 
-// The end of a query in two halves: the QState / row-count copy and an event behind it (async),
-// then the wait for that event and the reset of QState for the next query on this workspace.
+// QState + row counts -> the mapped host mirror with a kernel's stores: a hipMemcpyAsync of these
+// ~13 KB took the copy engine's path, ~130 us against ~3 us (profiles/r03_l_d2h_probe.json).
+__global__ void __launch_bounds__(BLOCK) k_q_out(const unsigned long long* __restrict__ src, unsigned long long* dst,
+                                                 uint32_t n8) {
+  for (uint32_t i = threadIdx.x; i < n8; i += BLOCK) dst[i] = src[i];
+}
+
+// The end of a query in two halves: the QState / row-count store into host memory and an event
+// behind it (async), then the wait for that event and the reset of QState for the next query.
 hipError_t ws_end_query_async(Workspace* w) {
   int nt = 0;
   for (int t = 0; t < MAX_TYPES_Q; ++t)
     if (w->final_grid[t]) nt = t + 1;
-  HIP_TRY(hipMemcpyAsync(w->h_q, w->q, sizeof(QState) + (size_t)nt * EXPAND_GRID * 4, hipMemcpyDeviceToHost,
-                         w->stream));
+  static_assert(sizeof(QState) % 8 == 0 && EXPAND_GRID % 2 == 0, "k_q_out copies 8-byte words");
+  const size_t bytes = sizeof(QState) + (size_t)nt * EXPAND_GRID * 4;
+  hipLaunchKernelGGL(k_q_out, dim3(1), dim3(BLOCK), 0, w->stream, reinterpret_cast<const unsigned long long*>(w->q),
+                     reinterpret_cast<unsigned long long*>(w->d_hq), (uint32_t)(bytes / 8));
+  HIP_TRY(hipGetLastError());
   if (!w->done_ev) HIP_TRY(hipEventCreateWithFlags(&w->done_ev, hipEventDisableTiming));
   return hipEventRecord(w->done_ev, w->stream);
 }

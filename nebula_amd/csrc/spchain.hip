@@ -3,7 +3,7 @@
 // Same semantics and result as path.cpp's bidirectional() (FindPathExecutor.cpp:173-290
 // restated: minimal hop count, UPTO N, one path per target, ties broken by the lexicographically
 // smallest entry list [v0, t0, r0, v1, ...]).  The host enqueues a chain per pair —
-//   k_ch_setup, K x k_ch_step, H x k_ch_hop, one copy of the state —
+//   k_ch_setup, K x k_ch_step, H x k_ch_hop, k_ch_out (the result into mapped host memory) —
 // and waits once.  Step launch i derives what it does from the state snapshot of launch i - 1
 // (snap[i - 1]) and that launch's results (its output-list and meet counters, lacc / lmeet[i - 1]),
 // which are final at the launch boundary: the BFS level loop (direction = the side with the
@@ -78,7 +78,7 @@ struct ChSnap {         // the search state before one step launch
                                        // vertex appended, for every level and B-set step)
 };
 
-struct ChState {        // device; copied back per batch up to gpart
+struct ChState {        // device; the host reads what k_ch_out derives from it (ChOut)
   unsigned long long lacc[CH_MAXS];    // packed output list of step launch i
   unsigned long long lmeet[CH_MAXS];   // meet vertices found by step launch i
   unsigned long long macc;             // packed meet list (over in-edges)
@@ -92,6 +92,17 @@ struct ChState {        // device; copied back per batch up to gpart
   ChSnap snap[CH_MAXS];
   long long path[1 + 3 * MAX_PATH_LEN];
   unsigned long long gpart[4 * CH_HOP_WGS];
+};
+
+// What the host reads after a chain, stored by k_ch_out straight into mapped pinned memory (a
+// hipMemcpyAsync of the 17 KB ChState went down the copy engine's path: ~130 us per pair on
+// MI355X against ~3 us for a kernel's stores, profiles/r03_l_d2h_probe.json).
+struct ChOut {
+  ChSnap F;                            // the state after the last step launch
+  unsigned long long err;              // ChState::err
+  unsigned long long hpos;             // hstart[hops] (position << 32 | vertex)
+  unsigned long long hlaunch;
+  long long path[1 + 3 * MAX_PATH_LEN];
 };
 
 struct ChArgs {         // device memory (indexed at run time: never a by-value kernel argument)
@@ -124,15 +135,22 @@ __host__ __device__ inline ChSnap ch_advance(const ChSnap& p, unsigned long long
     return 12ull * (src >> 32) + 4ull * (src & M32) + 4ull * (dst >> 32);
   };
   if (p.phase == PH_BFS) {
-    const int side = (int)p.dir;
-    s.abytes += bytes_of(p.cnt[side], out);
-    if (side == 0) s.fprev = p.cnt[0];
-    s.edges += p.cnt[side] & 0xFFFFFFFFull;
+    // (constant indices only: a runtime index into the snapshot's arrays puts it in scratch memory)
+    const bool fwd = p.dir == 0;
+    const unsigned long long pc = fwd ? p.cnt[0] : p.cnt[1];
+    s.abytes += bytes_of(pc, out);
+    s.edges += pc & 0xFFFFFFFFull;
     s.levels += 1;
-    s.cnt[side] = out;
-    s.cur[side] ^= 1u;
-    if (side == 0) ++s.kf;
-    else ++s.kb;
+    if (fwd) {
+      s.fprev = p.cnt[0];
+      s.cnt[0] = out;
+      s.cur[0] ^= 1u;
+      ++s.kf;
+    } else {
+      s.cnt[1] = out;
+      s.cur[1] ^= 1u;
+      ++s.kb;
+    }
     if (err) {
       s.phase = PH_DONE;
       s.err = 1;
@@ -344,11 +362,12 @@ __device__ __forceinline__ void ch_setup(const ChArgs& A, const ChQ& q) {
 //   B-set step k: B[kf - 1 - k] = vertices of forward level kf - 1 - k with an edge into
 //     B[kf - k], claimed in LAB_M (push: in-edges of B[kf - k]; pull, k == 0 only: out-edges of
 //     forward level kf - 1).
-// (bid, nblk: this workgroup among the query's workgroups of the launch)
+// (bid, nblk: this workgroup among the query's workgroups of the launch; NW waves per workgroup)
+template <int NW>
 __device__ __forceinline__ void ch_step(const ChArgs& A, const ChQ& q, int i, uint32_t bid, uint32_t nblk) {
-  __shared__ uint32_t sEndAll[CH_WAVES][CH_TILE + 2];
-  __shared__ uint32_t sRsAll[CH_WAVES][CH_TILE + 1];
-  __shared__ uint16_t sSegAll[CH_WAVES][CH_TILE];
+  __shared__ uint32_t sEndAll[NW][CH_TILE + 2];
+  __shared__ uint32_t sRsAll[NW][CH_TILE + 1];
+  __shared__ uint16_t sSegAll[NW][CH_TILE];
   ChState* st = A.st;
   const ChSnap P = snap_for(st, i, q.upto);
   if (i > 0 && bid == 0 && threadIdx.x == 0) st->snap[i] = P;   // for launch i + 1
@@ -368,10 +387,10 @@ __device__ __forceinline__ void ch_step(const ChArgs& A, const ChQ& q, int i, ui
   bool append = true;
   if (bfs) {
     side = (int)P.dir;
-    const int src = side * 2 + (int)P.cur[side];
+    const int src = side * 2 + (int)(side ? P.cur[1] : P.cur[0]);
     S = A.list[src];
     D = A.list[src ^ 1];
-    scnt = P.cnt[side];
+    scnt = side ? P.cnt[1] : P.cnt[0];
     lab = A.lab[side];
     epoch = side ? q.eb : q.ef;
     stamp = stamp_of(epoch, (side ? P.kb : P.kf) + 1);
@@ -412,7 +431,7 @@ __device__ __forceinline__ void ch_step(const ChArgs& A, const ChQ& q, int i, ui
   uint32_t* const sEnd = sEndAll[w];
   uint32_t* const sRs = sRsAll[w];
   uint16_t* const sSeg = sSegAll[w];
-  for (uint64_t t = (uint64_t)bid * CH_WAVES + w; t < ntiles; t += (uint64_t)nblk * CH_WAVES) {
+  for (uint64_t t = (uint64_t)bid * NW + w; t < ntiles; t += (uint64_t)nblk * NW) {
     // once this level has met, its claims are not expanded again: their appends are skipped
     // (read now, used after the claims: the load is off the critical path)
     const unsigned long long met_now = bfs ? ld_agent(&st->lmeet[i]) : 0ull;
@@ -724,10 +743,34 @@ __device__ __forceinline__ void ch_hop(const ChArgs& A, const ChQ& q, int last, 
 __global__ void __launch_bounds__(CH_BLOCK) k_ch_setup(const ChArgs* __restrict__ Ap, ChQ q) { ch_setup(*Ap, q); }
 // (4 waves per SIMD, as the kernel had before it served batches: at most 128 VGPRs)
 __global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) k_ch_step(const ChArgs* __restrict__ Ap, ChQ q, int i) {
-  ch_step(*Ap, q, i, blockIdx.x, gridDim.x);
+  ch_step<CH_WAVES>(*Ap, q, i, blockIdx.x, gridDim.x);
+}
+// ... with 16 waves per workgroup (NBG_SP_BLOCK=1024): a big level gets 4x the waves in flight for
+// the same number of workgroups to dispatch
+constexpr int CH_WIDE = 16;
+__global__ void __launch_bounds__(64 * CH_WIDE) __attribute__((amdgpu_waves_per_eu(4))) k_ch_step_w(const ChArgs* __restrict__ Ap, ChQ q, int i) {
+  ch_step<CH_WIDE>(*Ap, q, i, blockIdx.x, gridDim.x);
 }
 __global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ Ap, ChQ q, int last, int h) {
   ch_hop(*Ap, q, last, h, blockIdx.x, gridDim.x);
+}
+
+// The chain's result (after `steps` step and `hops` hop launches) into the host's ChOut (one
+// workgroup; vector stores over the mapped pinned page).
+__device__ __forceinline__ void ch_out(const ChArgs& A, const ChQ& q, int steps, int hops, ChOut* out) {
+  const ChState* st = A.st;
+  const ChSnap F = ch_advance(st->snap[steps - 1], st->lacc[steps - 1], st->lmeet[steps - 1], st->macc, st->err, q.upto);
+  const uint32_t L = F.met && F.L <= MAX_PATH_LEN ? F.L : 0;
+  for (uint32_t k = threadIdx.x; k < 1 + 3 * L; k += blockDim.x) out->path[k] = st->path[k];
+  if (threadIdx.x == 0) {
+    out->F = F;
+    out->err = st->err;
+    out->hpos = st->hstart[hops];
+    out->hlaunch = st->hlaunch;
+  }
+}
+__global__ void __launch_bounds__(64) k_ch_out(const ChArgs* __restrict__ Ap, ChQ q, int steps, int hops, ChOut* out) {
+  ch_out(*Ap, q, steps, hops, out);
 }
 
 // ... or up to CH_BMAX queries per launch (a batch of pairs, each with its own workspace, state and
@@ -737,6 +780,7 @@ constexpr int CH_BMAX = 32;
 struct ChBatch {
   const ChArgs* A[CH_BMAX];
   ChQ q[CH_BMAX];
+  ChOut* out[CH_BMAX];
   int n;
   uint32_t per;
 };
@@ -745,11 +789,14 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_setup_b(ChBatch b) {
 }
 __global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) k_ch_step_b(ChBatch b, int i) {
   const uint32_t p = blockIdx.x / b.per;
-  if ((int)p < b.n) ch_step(*b.A[p], b.q[p], i, blockIdx.x % b.per, b.per);
+  if ((int)p < b.n) ch_step<CH_WAVES>(*b.A[p], b.q[p], i, blockIdx.x % b.per, b.per);
 }
 __global__ void __launch_bounds__(CH_BLOCK) k_ch_hop_b(ChBatch b, int last, int h) {
   const uint32_t p = blockIdx.x / CH_HOP_WGS;
   if ((int)p < b.n) ch_hop(*b.A[p], b.q[p], last, h, blockIdx.x % CH_HOP_WGS, CH_HOP_WGS);
+}
+__global__ void __launch_bounds__(64) k_ch_out_b(ChBatch b, int steps, int hops) {
+  if ((int)blockIdx.x < b.n) ch_out(*b.A[blockIdx.x], b.q[blockIdx.x], steps, hops, b.out[blockIdx.x]);
 }
 
 // ---------------------------------------------------------------------------- host side
@@ -758,7 +805,8 @@ struct ChainCtx {
   uint64_t nv = 0, list_cap = 0, tsplit_cap = 0;
   ChList list[CH_NLISTS] = {};
   ChState* d_st = nullptr;
-  ChState* h_st = nullptr;
+  ChOut* h_out = nullptr;          // mapped pinned: k_ch_out stores the result here
+  ChOut* d_out = nullptr;          // its device address
   ChArgs* d_args = nullptr;
   ChArgs* h_args = nullptr;
   ChArgs cached{};
@@ -768,6 +816,7 @@ struct ChainCtx {
   // (profiles/r02_x_sp_grid_sweep.json): p50 0.159 ms at 512, 0.151 at 256, 0.148 at 128 and 96,
   // 0.154 at 32.  NBG_SP_GRID overrides.
   unsigned grid = 128;
+  unsigned block = CH_BLOCK;       // step launch block: CH_BLOCK, or 64 * CH_WIDE (NBG_SP_BLOCK=1024)
   // the query in flight: what has been enqueued
   ChQ q{};
   int steps = 0, hops = 0;
@@ -809,8 +858,6 @@ struct ChainCtx {
   }
 };
 
-static constexpr size_t CH_COPY = offsetof(ChState, gpart);
-
 ChainCtx* chain_create(uint64_t nv, uint64_t edge_cap, hipStream_t s, std::string* err) {
   auto* c = new ChainCtx();
   c->stream = s;
@@ -819,6 +866,8 @@ ChainCtx* chain_create(uint64_t nv, uint64_t edge_cap, hipStream_t s, std::strin
   c->tsplit_cap = (nv + 1 + edge_cap) / CH_TILE + 2;
   const char* g = getenv("NBG_SP_GRID");
   if (g && atoi(g) > 0) c->grid = (unsigned)atoi(g);
+  const char* bs = getenv("NBG_SP_BLOCK");
+  if (bs && atoi(bs) == 64 * CH_WIDE) c->block = 64 * CH_WIDE;
   hipError_t he = hipSuccess;
   auto M = [&](void** p, size_t b) { if (he == hipSuccess) he = hipMalloc(p, b); };
   for (auto& L : c->list) {
@@ -829,7 +878,8 @@ ChainCtx* chain_create(uint64_t nv, uint64_t edge_cap, hipStream_t s, std::strin
   }
   M((void**)&c->d_st, sizeof(ChState));
   M((void**)&c->d_args, sizeof(ChArgs));
-  if (he == hipSuccess) he = hipHostMalloc((void**)&c->h_st, sizeof(ChState), hipHostMallocDefault);
+  if (he == hipSuccess) he = hipHostMalloc((void**)&c->h_out, sizeof(ChOut), hipHostMallocMapped | hipHostMallocCoherent);
+  if (he == hipSuccess) he = hipHostGetDevicePointer((void**)&c->d_out, c->h_out, 0);
   if (he == hipSuccess) he = hipHostMalloc((void**)&c->h_args, sizeof(ChArgs), hipHostMallocDefault);
   if (he == hipSuccess) he = hipMemsetAsync(c->d_st, 0, sizeof(ChState), s);
   if (he == hipSuccess) he = hipStreamSynchronize(s);
@@ -851,27 +901,30 @@ void chain_destroy(ChainCtx* c) {
       if (p) (void)hipFree(p);
   if (c->d_st) (void)hipFree(c->d_st);
   if (c->d_args) (void)hipFree(c->d_args);
-  if (c->h_st) (void)hipHostFree(c->h_st);
+  if (c->h_out) (void)hipHostFree(c->h_out);
   if (c->h_args) (void)hipHostFree(c->h_args);
   for (auto& r : c->pend) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
   for (auto e : c->pool) (void)hipEventDestroy(e);
   delete c;
 }
 
-// Enqueue step launches [steps, steps + k) and h hop launches, then the state copy.
+// Enqueue step launches [steps, steps + k) and h hop launches, then the result (k_ch_out).
 static hipError_t chain_batch(ChainCtx* c, int k, int h) {
   const ChArgs* A = c->d_args;
   for (int j = 0; j < k; ++j, ++c->steps)
     c->timed(CHK_STEP, [&] {
-      hipLaunchKernelGGL(k_ch_step, dim3(c->grid), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps);
+      if (c->block == CH_BLOCK)
+        hipLaunchKernelGGL(k_ch_step, dim3(c->grid), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps);
+      else
+        hipLaunchKernelGGL(k_ch_step_w, dim3(c->grid), dim3(64 * CH_WIDE), 0, c->stream, A, c->q, c->steps);
     });
   for (int j = 0; j < h && c->hops < CH_MAXS; ++j, ++c->hops)
     c->timed(CHK_HOP, [&] {
       hipLaunchKernelGGL(k_ch_hop, dim3(CH_HOP_WGS), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps - 1, c->hops);
     });
-  HIP_TRY_CH(hipGetLastError());
+  hipLaunchKernelGGL(k_ch_out, dim3(1), dim3(64), 0, c->stream, A, c->q, c->steps, c->hops, c->d_out);
   ++c->batches;
-  return hipMemcpyAsync(c->h_st, c->d_st, CH_COPY, hipMemcpyDeviceToHost, c->stream);
+  return hipGetLastError();
 }
 
 // The query's arguments into c (uploaded when they changed) and its ChQ; nothing launched.
@@ -953,6 +1006,7 @@ hipError_t chain_launch_batch(ChainCtx* const* cs, int n, const ChainQuery* qs) 
     HIP_TRY_CH(chain_prepare(c, *x.fwd, *x.bwd, x.visible, x.vids, x.lab, x.epoch, x.s, x.t, x.upto));
     b.A[p] = c->d_args;
     b.q[p] = c->q;
+    b.out[p] = c->d_out;
     // the whole chain at once (every step and hop launch UPTO allows): a continuation would cost
     // the batch a host round trip per context, while a launch past a query's end returns at once
     k = std::max(k, 2 * (int)x.upto - 1);
@@ -969,6 +1023,7 @@ hipError_t chain_launch_batch(ChainCtx* const* cs, int n, const ChainQuery* qs) 
     c0->timed(CHK_HOP_B, [&] {
       hipLaunchKernelGGL(k_ch_hop_b, dim3((unsigned)n * CH_HOP_WGS), dim3(CH_BLOCK), 0, st, b, k - 1, j);
     });
+  hipLaunchKernelGGL(k_ch_out_b, dim3((unsigned)n), dim3(64), 0, st, b, k, h);
   HIP_TRY_CH(hipGetLastError());
   for (int p = 0; p < n; ++p) {
     ChainCtx* c = cs[p];
@@ -978,7 +1033,6 @@ hipError_t chain_launch_batch(ChainCtx* const* cs, int n, const ChainQuery* qs) 
     c->steps = k;
     c->hops = h;
     ++c->batches;
-    HIP_TRY_CH(hipMemcpyAsync(c->h_st, c->d_st, CH_COPY, hipMemcpyDeviceToHost, st));
   }
   return hipSuccess;
 }
@@ -987,15 +1041,14 @@ hipError_t chain_launch_batch(ChainCtx* const* cs, int n, const ChainQuery* qs) 
 // enqueued (the caller waits again).
 bool chain_more(ChainCtx* c, hipError_t* he) {
   *he = hipSuccess;
-  const ChState& h = *c->h_st;
-  const ChSnap F = ch_advance(h.snap[c->steps - 1], h.lacc[c->steps - 1], h.lmeet[c->steps - 1], h.macc, h.err,
-                              c->q.upto);
+  const ChOut& h = *c->h_out;
+  const ChSnap F = h.F;
   const int max_steps = 2 * (int)c->q.upto - 1;
   if (F.phase != PH_DONE && c->steps < max_steps) {
     *he = chain_batch(c, max_steps - c->steps, (int)c->q.upto);   // the rest, at once
     return false;
   }
-  const uint32_t hpos = (uint32_t)(h.hstart[c->hops] >> 32);
+  const uint32_t hpos = (uint32_t)(h.hpos >> 32);
   if (F.met && !F.err && !h.err && hpos < F.L && c->hops < CH_MAXS) {
     *he = chain_batch(c, 0, (int)F.L - (int)hpos);
     return false;
@@ -1009,15 +1062,14 @@ bool chain_more(ChainCtx* c, hipError_t* he) {
 
 // the final state -> SpResult
 void chain_result(const ChainCtx* c, SpResult* out) {
-  const ChState& h = *c->h_st;
-  const ChSnap F = ch_advance(h.snap[c->steps - 1], h.lacc[c->steps - 1], h.lmeet[c->steps - 1], h.macc, h.err,
-                              c->q.upto);
+  const ChOut& h = *c->h_out;
+  const ChSnap& F = h.F;
   out->err = h.err;
   out->edges = F.edges;
   out->levels = F.levels;
   out->abytes = F.abytes;
   out->launches = (unsigned long long)(c->steps + c->hops + 1);
-  const uint32_t hpos = (uint32_t)(h.hstart[c->hops] >> 32);
+  const uint32_t hpos = (uint32_t)(h.hpos >> 32);
   out->L = (F.met && !h.err && hpos == F.L) ? F.L : 0;
   if (F.met && !h.err && hpos != F.L) out->err = 2;   // (cannot happen: the hops were enqueued)
   out->ntrace = 0;

@@ -229,6 +229,16 @@ class Engine:
         self._check(self.lib.nbg_load_edges(self.h, etype, _ptr(src), _ptr(dst), _ptr(rk), len(src), arr,
                                             len(props)), "load_edges")
 
+    def staged_edges(self, etype: int):
+        """nbg_staged_edges: (src, dst, rank) of the records staged for signed type `etype` before
+        finalize — on a partitioned rank, only the records of the parts it serves."""
+        n = C.c_uint64(0)
+        self._check(self.lib.nbg_staged_edges(self.h, etype, None, None, None, 0, C.byref(n)), "staged_edges")
+        src, dst, rank = (np.empty(n.value, np.int64) for _ in range(3))
+        self._check(self.lib.nbg_staged_edges(self.h, etype, _ptr(src), _ptr(dst), _ptr(rank), n.value, C.byref(n)),
+                    "staged_edges")
+        return src, dst, rank
+
     def finalize(self):
         self._check(self.lib.nbg_finalize(self.h), "finalize")
 
