@@ -222,11 +222,13 @@ def roofline_of(g, workload, steps):
 def host_delivered(stmt, roots):
     """nbg_go semantics (rows copied to host memory, what ExecutionResponse carries): rows/s and
     the device-to-host GB/s of the 8-byte cells.  Per query: nbg_go_execute (device), then
-    nbg_rows_fetch: the device packs the row segments and DMAs them into a pinned block of the
-    engine's pool (one untimed query first grows the pool, as a server's first response would)."""
-    res = stmt.run_device([roots[0]])
-    res.fetch_bits(copy=False)
-    res.free()
+    nbg_rows_fetch: the device packs the row segments into a pinned block of the engine's pool
+    (one untimed pass over the roots first grows the pool to the sizes these responses need, as a
+    serving engine's pool is after its first responses)."""
+    for r in roots:
+        res = stmt.run_device([r])
+        res.fetch_bits(copy=False)
+        res.free()
     rows = cells = 0
     t0 = time.perf_counter()
     for r in roots:

@@ -1332,6 +1332,29 @@ __global__ void __launch_bounds__(BLOCK) k_pack_rows(const uint64_t* __restrict_
   }
 }
 
+// k_pack_rows into host memory (the pinned block, over the host link): 16-byte stores wherever the
+// destination is 16-byte aligned (a 16-byte store per lane reaches ~54 GB/s into pinned memory,
+// the DMA engine ~30, profiles/r03_q_d2h_bw_probe.json)
+__global__ void __launch_bounds__(BLOCK) k_pack_rows_host(const uint64_t* __restrict__ seg, int nseg,
+                                                          int64_t* const* __restrict__ cols, int ncols,
+                                                          int64_t* __restrict__ out, uint64_t total) {
+  for (int k = blockIdx.x; k < nseg; k += gridDim.x) {
+    const uint64_t b = seg[3 * k], len = seg[3 * k + 1], o = seg[3 * k + 2];
+    for (int c = 0; c < ncols; ++c) {
+      const int64_t* src = cols[c] + b;
+      int64_t* dst = out + (uint64_t)c * total + o;
+      const uint64_t head = ((uintptr_t)dst & 15) ? 1 : 0;   // (8-byte aligned: at most one odd cell)
+      if (head && threadIdx.x == 0 && len) dst[0] = src[0];
+      const uint64_t body = len > head ? (len - head) / 2 : 0;
+      const int64_t* s2 = src + head;
+      longlong2* d2 = reinterpret_cast<longlong2*>(dst + head);
+      for (uint64_t i = threadIdx.x; i < body; i += BLOCK) d2[i] = make_longlong2(s2[2 * i], s2[2 * i + 1]);
+      const uint64_t done = head + 2 * body;
+      if (done < len && threadIdx.x == 0) dst[done] = src[done];
+    }
+  }
+}
+
 // Order-independent digest of a result: per row h = splitmix64-chain of its 8-byte cell
 // payloads (column order), summed and xor-ed over the rows (out = {rows, xor, sum}).
 __device__ __forceinline__ uint64_t splitmix64_d(uint64_t z) {
@@ -2422,7 +2445,7 @@ hipError_t ws_fetch_rows_pinned(Workspace* w, const std::vector<std::pair<uint64
   }
   HIP_TRY(hipMemcpyAsync(w->fetch_meta, meta.data(), meta.size() * 8, hipMemcpyHostToDevice, w->stream));
   const int nseg = (int)(meta.size() / 3);
-  hipLaunchKernelGGL(k_pack_rows, dim3((unsigned)(nseg < 4096 ? nseg : 4096)), dim3(BLOCK), 0, w->stream,
+  hipLaunchKernelGGL(k_pack_rows_host, dim3((unsigned)(nseg < 4096 ? nseg : 4096)), dim3(BLOCK), 0, w->stream,
                      w->fetch_meta, nseg, (int64_t* const*)w->d_row_cols, ncols, static_cast<int64_t*>(dptr), total);
   HIP_TRY(hipGetLastError());
   return ws_sync(w);
@@ -3209,16 +3232,19 @@ __device__ __forceinline__ bool part_valid(const GreedyPart& g, uint32_t u) {
 __global__ void __launch_bounds__(BLOCK) k_greedy_part(GreedyPart g) {
   __shared__ Cand lds[WAVES + 1];
   Cand best{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
+  // (locals, not writes into the by-value argument: a written kernel argument is copied to scratch)
+  uint64_t nv = g.nv;
+  uint32_t v = g.v;
   if (g.vp) {
-    if (g.vp[1]) g.nv = 0;   // an earlier hop failed: no candidates
-    g.v = (uint32_t)g.vp[0];
+    if (g.vp[1]) nv = 0;   // an earlier hop failed: no candidates
+    v = (uint32_t)g.vp[0];
   }
   // a wave tests 64 consecutive vertices, then scans each B-set member's in-edge row together
   // (lane-strided, coalesced): a hub's row is not left to one thread
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (uint64_t base = ((uint64_t)blockIdx.x * WAVES + w) * 64; base < g.nv; base += (uint64_t)gridDim.x * BLOCK) {
+  for (uint64_t base = ((uint64_t)blockIdx.x * WAVES + w) * 64; base < nv; base += (uint64_t)gridDim.x * BLOCK) {
     const uint64_t mine = base + lane;
-    unsigned long long m = __ballot(mine < g.nv && part_valid(g, (uint32_t)mine));
+    unsigned long long m = __ballot(mine < nv && part_valid(g, (uint32_t)mine));
     while (m) {
       const uint32_t u = (uint32_t)(base + __builtin_ctzll(m));
       m &= m - 1;
@@ -3237,7 +3263,7 @@ __global__ void __launch_bounds__(BLOCK) k_greedy_part(GreedyPart g) {
       for (int t = 0; t < g.ntypes; ++t) {
         const uint32_t rs = g.row_ptr[t][u], re = g.row_ptr[t][u + 1];
         for (uint32_t j = rs + lane; j < re; j += 64) {
-          if (g.col[t][j] != g.v) continue;
+          if (g.col[t][j] != v) continue;
           Cand x{(int64_t)g.type[t], g.rank[t] ? g.rank[t][j] : 0, uvid, u};
           if (cand_less(x, best)) best = x;
         }
@@ -3266,9 +3292,10 @@ __global__ void __launch_bounds__(BLOCK) k_greedy_hub(GreedyPart g) {
   Cand best{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
   uint32_t nh = *g.nhub;
   if (nh > GP_HUB_CAP) nh = GP_HUB_CAP;
+  uint32_t v = g.v;
   if (g.vp) {
     if (g.vp[1]) nh = 0;
-    g.v = (uint32_t)g.vp[0];
+    v = (uint32_t)g.vp[0];
   }
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint32_t h = 0; h < nh; ++h) {
@@ -3277,7 +3304,7 @@ __global__ void __launch_bounds__(BLOCK) k_greedy_hub(GreedyPart g) {
     for (int t = 0; t < g.ntypes; ++t) {
       const uint64_t rs = g.row_ptr[t][u], re = g.row_ptr[t][u + 1];
       for (uint64_t j = rs + (uint64_t)blockIdx.x * BLOCK + threadIdx.x; j < re; j += stride) {
-        if (g.col[t][j] != g.v) continue;
+        if (g.col[t][j] != v) continue;
         Cand x{(int64_t)g.type[t], g.rank[t] ? g.rank[t][j] : 0, uvid, u};
         if (cand_less(x, best)) best = x;
       }

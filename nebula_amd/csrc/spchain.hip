@@ -89,6 +89,11 @@ struct ChState {        // device; the host reads what k_ch_out derives from it 
   // its workgroups writes hstart[h + 1]: state that no launch mutates while its own workgroups
   // may still read it (workgroups of one launch start at different times)
   unsigned long long hstart[CH_MAXS + 1];
+  // step launch i starts at step first[i] (a BFS level or B-set step; first[0] = 0) and writes
+  // first[i + 1]: one step, several (a workgroup alone runs small steps back to back, ChQ::solo)
+  // or none (the search is over)
+  unsigned long long first[CH_MAXS + 1];
+  unsigned long long busy;             // step launches that ran a step
   ChSnap snap[CH_MAXS];
   long long path[1 + 3 * MAX_PATH_LEN];
   unsigned long long gpart[4 * CH_HOP_WGS];
@@ -102,6 +107,7 @@ struct ChOut {
   unsigned long long err;              // ChState::err
   unsigned long long hpos;             // hstart[hops] (position << 32 | vertex)
   unsigned long long hlaunch;
+  unsigned long long busy;             // ChState::busy
   long long path[1 + 3 * MAX_PATH_LEN];
 };
 
@@ -123,11 +129,13 @@ struct ChArgs {         // device memory (indexed at run time: never a by-value 
 struct ChQ {
   uint32_t s, t, upto;
   uint32_t ef, eb, em;
+  uint32_t solo;                       // a step over at most this many items (entries + edges) is run
+                                       // by workgroup 0 alone, which goes on with the next step (0: off)
 };
 
 // The state after step launch `i` (snapshot p before it, its results from st): every step launch
 // and the host derive it the same way.
-__host__ __device__ inline ChSnap ch_advance(const ChSnap& p, unsigned long long out, unsigned long long meets,
+__host__ __device__ __forceinline__ ChSnap ch_advance(const ChSnap& p, unsigned long long out, unsigned long long meets,
                                               unsigned long long macc, unsigned long long err, uint32_t upto) {
   ChSnap s = p;
   constexpr unsigned long long M32 = 0xFFFFFFFFull;
@@ -313,7 +321,7 @@ __device__ __forceinline__ void wave_append(const ChArgs& A, const ChList& L, un
   }
 }
 
-// The snapshot step launch i runs under: snap[0] (set-up) or derived from launch i - 1.
+// The snapshot step i runs under: snap[0] (set-up) or derived from step i - 1.
 __device__ __forceinline__ ChSnap snap_for(const ChState* st, int i, uint32_t upto) {
   if (i == 0) return st->snap[0];
   return ch_advance(st->snap[i - 1], st->lacc[i - 1], st->lmeet[i - 1], st->macc, st->err, upto);
@@ -333,7 +341,8 @@ __device__ __forceinline__ void ch_setup(const ChArgs& A, const ChQ& q) {
     st->lmeet[i] = 0;
   }
   if (threadIdx.x != 0) return;
-  st->macc = st->err = st->gticket = st->hlaunch = 0;
+  st->macc = st->err = st->gticket = st->hlaunch = st->busy = 0;
+  st->first[0] = 0;
   ChSnap s;
   memset(&s, 0, sizeof(s));
   s.phase = dsf && dsb ? PH_BFS : PH_DONE;
@@ -355,7 +364,7 @@ __device__ __forceinline__ void ch_setup(const ChArgs& A, const ChQ& q) {
   st->path[0] = gld(A.vids, q.s, A.nv, 16, st);
 }
 
-// Step launch i: a BFS level, a B-set step or nothing, as its snapshot says.
+// Step j (snapshot P, not DONE): a BFS level or a B-set step.
 //   BFS, side d: expand side d's current list over d's CSR; claim unlabelled neighbours with the
 //     side's next level stamp, append them to d's other list, and record meets (claimed vertices
 //     the other side already labelled: LAB_M stamp, meet list over in-edges).
@@ -364,14 +373,12 @@ __device__ __forceinline__ void ch_setup(const ChArgs& A, const ChQ& q) {
 //     forward level kf - 1).
 // (bid, nblk: this workgroup among the query's workgroups of the launch; NW waves per workgroup)
 template <int NW>
-__device__ __forceinline__ void ch_step(const ChArgs& A, const ChQ& q, int i, uint32_t bid, uint32_t nblk) {
+__device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const ChSnap& P, int i, uint32_t bid,
+                                         uint32_t nblk) {
   __shared__ uint32_t sEndAll[NW][CH_TILE + 2];
   __shared__ uint32_t sRsAll[NW][CH_TILE + 1];
   __shared__ uint16_t sSegAll[NW][CH_TILE];
   ChState* st = A.st;
-  const ChSnap P = snap_for(st, i, q.upto);
-  if (i > 0 && bid == 0 && threadIdx.x == 0) st->snap[i] = P;   // for launch i + 1
-  if (P.phase == PH_DONE) return;
   const bool bfs = P.phase == PH_BFS;
   // ---- this launch's lists, labels and stamps (uniform)
   int side;              // CSR expanded
@@ -576,6 +583,55 @@ __device__ __forceinline__ void ch_step(const ChArgs& A, const ChQ& q, int i, ui
   }
 }
 
+// Items (entries + edges) of the source list of step P (as ch_level picks it).
+__device__ __forceinline__ uint64_t step_items(const ChSnap& P) {
+  unsigned long long c;
+  if (P.phase == PH_BFS) {
+    c = P.dir ? P.cnt[1] : P.cnt[0];
+  } else {
+    const bool pull = P.bstep == 0 && (P.fprev & 0xFFFFFFFFull) < (P.bcnt & 0xFFFFFFFFull);
+    c = pull ? P.fprev : P.bcnt;
+  }
+  return (c >> 32) + (c & 0xFFFFFFFFull);
+}
+
+// Step launch i: from step first[i], one step over the whole grid, or — for a step of at most
+// q.solo items — steps run by workgroup 0 alone, back to back, until the search is over or a step
+// needs the grid (the launch boundary then orders it after this workgroup's writes).
+template <int NW>
+__device__ __forceinline__ void ch_step(const ChArgs& A, const ChQ& q, int i, uint32_t bid, uint32_t nblk) {
+  ChState* st = A.st;
+  uint32_t j = i == 0 ? 0u : (uint32_t)st->first[i];
+  ChSnap P = snap_for(st, (int)j, q.upto);
+  const bool lead = bid == 0 && threadIdx.x == 0;
+  if (P.phase == PH_DONE) {
+    if (lead) st->first[i + 1] = j;
+    return;
+  }
+  const bool solo = step_items(P) <= q.solo;
+  if (solo && bid != 0) return;
+  if (lead) st->busy += 1;
+  for (;;) {   // (one call site of ch_level: the grid's step and the solo steps share its registers)
+    if (lead) {
+      if (j > 0) st->snap[j] = P;   // (step j + 1 derives its snapshot from it; snap[0] is the set-up's)
+      if (!solo) st->first[i + 1] = j + 1;
+    }
+    ch_level<NW>(A, q, P, (int)j, solo ? 0u : bid, solo ? 1u : nblk);
+    if (!solo) return;
+    // this workgroup's stores and atomics before the next step's reads (labels, lists, counters;
+    // the acquire drops L1 lines read before another wave's claims); the snapshot is read back
+    // rather than kept in registers across the step
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    P = ch_advance(st->snap[j], ld_agent(&st->lacc[j]), ld_agent(&st->lmeet[j]), ld_agent(&st->macc),
+                   ld_agent(&st->err), q.upto);
+    ++j;
+    if (P.phase == PH_DONE || step_items(P) > q.solo || j + 1 >= (uint32_t)CH_MAXS) break;
+  }
+  if (lead) st->first[i + 1] = j;
+}
+
 namespace {
 
 struct Cand {
@@ -645,11 +701,11 @@ __device__ __forceinline__ Cand hop_scan(const ChArgs& A, const uint32_t* vlab, 
 // hub), which walks on until the path is complete or the next vertex is a hub — left to the next
 // launch — and writes hstart[h + 1].
 // (bid, nblk: this workgroup among the query's nblk <= CH_HOP_WGS workgroups of the launch)
-__device__ __forceinline__ void ch_hop(const ChArgs& A, const ChQ& q, int last, int h, uint32_t bid, uint32_t nblk) {
+__device__ __forceinline__ void ch_hop(const ChArgs& A, const ChQ& q, int nl, int h, uint32_t bid, uint32_t nblk) {
   __shared__ Cand lds[CH_WAVES + 1];
   __shared__ int s_last;
   ChState* st = A.st;
-  const ChSnap F = ch_advance(st->snap[last], st->lacc[last], st->lmeet[last], st->macc, st->err, q.upto);
+  const ChSnap F = snap_for(st, (int)st->first[nl], q.upto);   // the state after the nl step launches
   const unsigned long long H = st->hstart[h];
   uint32_t pos = (uint32_t)(H >> 32), c = (uint32_t)H;
   auto finish = [&](uint32_t p, uint32_t v) {   // (thread 0 of the one writer)
@@ -741,25 +797,22 @@ __device__ __forceinline__ void ch_hop(const ChArgs& A, const ChQ& q, int last, 
 // ---------------------------------------------------------------------------- kernels
 // One query per launch (the chain of one pair) ...
 __global__ void __launch_bounds__(CH_BLOCK) k_ch_setup(const ChArgs* __restrict__ Ap, ChQ q) { ch_setup(*Ap, q); }
-// (4 waves per SIMD, as the kernel had before it served batches: at most 128 VGPRs)
-__global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) k_ch_step(const ChArgs* __restrict__ Ap, ChQ q, int i) {
+// (at most 2 waves per SIMD: 256 VGPRs, no spills; a one-pair launch has 128 workgroups of 4 waves,
+// 2 waves per CU, so the occupancy bound costs nothing.  16-wave workgroups, tried for more waves
+// per big level, were slower: RMAT-26 p50 0.137 -> 0.197 ms, profiles/r03_n_sp_block_ab.txt)
+__global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) k_ch_step(const ChArgs* __restrict__ Ap, ChQ q, int i) {
   ch_step<CH_WAVES>(*Ap, q, i, blockIdx.x, gridDim.x);
 }
-// ... with 16 waves per workgroup (NBG_SP_BLOCK=1024): a big level gets 4x the waves in flight for
-// the same number of workgroups to dispatch
-constexpr int CH_WIDE = 16;
-__global__ void __launch_bounds__(64 * CH_WIDE) __attribute__((amdgpu_waves_per_eu(4))) k_ch_step_w(const ChArgs* __restrict__ Ap, ChQ q, int i) {
-  ch_step<CH_WIDE>(*Ap, q, i, blockIdx.x, gridDim.x);
-}
-__global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ Ap, ChQ q, int last, int h) {
-  ch_hop(*Ap, q, last, h, blockIdx.x, gridDim.x);
+
+__global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ Ap, ChQ q, int nl, int h) {
+  ch_hop(*Ap, q, nl, h, blockIdx.x, gridDim.x);
 }
 
 // The chain's result (after `steps` step and `hops` hop launches) into the host's ChOut (one
 // workgroup; vector stores over the mapped pinned page).
 __device__ __forceinline__ void ch_out(const ChArgs& A, const ChQ& q, int steps, int hops, ChOut* out) {
   const ChState* st = A.st;
-  const ChSnap F = ch_advance(st->snap[steps - 1], st->lacc[steps - 1], st->lmeet[steps - 1], st->macc, st->err, q.upto);
+  const ChSnap F = snap_for(st, (int)st->first[steps], q.upto);
   const uint32_t L = F.met && F.L <= MAX_PATH_LEN ? F.L : 0;
   for (uint32_t k = threadIdx.x; k < 1 + 3 * L; k += blockDim.x) out->path[k] = st->path[k];
   if (threadIdx.x == 0) {
@@ -767,6 +820,7 @@ __device__ __forceinline__ void ch_out(const ChArgs& A, const ChQ& q, int steps,
     out->err = st->err;
     out->hpos = st->hstart[hops];
     out->hlaunch = st->hlaunch;
+    out->busy = st->busy;
   }
 }
 __global__ void __launch_bounds__(64) k_ch_out(const ChArgs* __restrict__ Ap, ChQ q, int steps, int hops, ChOut* out) {
@@ -787,13 +841,16 @@ struct ChBatch {
 __global__ void __launch_bounds__(CH_BLOCK) k_ch_setup_b(ChBatch b) {
   if ((int)blockIdx.x < b.n) ch_setup(*b.A[blockIdx.x], b.q[blockIdx.x]);
 }
-__global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) k_ch_step_b(ChBatch b, int i) {
+#ifndef NBG_STEPB_WPE
+#define NBG_STEPB_WPE 4
+#endif
+__global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(NBG_STEPB_WPE))) k_ch_step_b(ChBatch b, int i) {
   const uint32_t p = blockIdx.x / b.per;
   if ((int)p < b.n) ch_step<CH_WAVES>(*b.A[p], b.q[p], i, blockIdx.x % b.per, b.per);
 }
-__global__ void __launch_bounds__(CH_BLOCK) k_ch_hop_b(ChBatch b, int last, int h) {
+__global__ void __launch_bounds__(CH_BLOCK) k_ch_hop_b(ChBatch b, int nl, int h) {
   const uint32_t p = blockIdx.x / CH_HOP_WGS;
-  if ((int)p < b.n) ch_hop(*b.A[p], b.q[p], last, h, blockIdx.x % CH_HOP_WGS, CH_HOP_WGS);
+  if ((int)p < b.n) ch_hop(*b.A[p], b.q[p], nl, h, blockIdx.x % CH_HOP_WGS, CH_HOP_WGS);
 }
 __global__ void __launch_bounds__(64) k_ch_out_b(ChBatch b, int steps, int hops) {
   if ((int)blockIdx.x < b.n) ch_out(*b.A[blockIdx.x], b.q[blockIdx.x], steps, hops, b.out[blockIdx.x]);
@@ -816,7 +873,7 @@ struct ChainCtx {
   // (profiles/r02_x_sp_grid_sweep.json): p50 0.159 ms at 512, 0.151 at 256, 0.148 at 128 and 96,
   // 0.154 at 32.  NBG_SP_GRID overrides.
   unsigned grid = 128;
-  unsigned block = CH_BLOCK;       // step launch block: CH_BLOCK, or 64 * CH_WIDE (NBG_SP_BLOCK=1024)
+  uint32_t solo = 0;               // ChQ::solo (NBG_SP_SOLO items)
   // the query in flight: what has been enqueued
   ChQ q{};
   int steps = 0, hops = 0;
@@ -866,8 +923,8 @@ ChainCtx* chain_create(uint64_t nv, uint64_t edge_cap, hipStream_t s, std::strin
   c->tsplit_cap = (nv + 1 + edge_cap) / CH_TILE + 2;
   const char* g = getenv("NBG_SP_GRID");
   if (g && atoi(g) > 0) c->grid = (unsigned)atoi(g);
-  const char* bs = getenv("NBG_SP_BLOCK");
-  if (bs && atoi(bs) == 64 * CH_WIDE) c->block = 64 * CH_WIDE;
+  const char* so = getenv("NBG_SP_SOLO");
+  if (so) c->solo = (uint32_t)strtoul(so, nullptr, 10);
   hipError_t he = hipSuccess;
   auto M = [&](void** p, size_t b) { if (he == hipSuccess) he = hipMalloc(p, b); };
   for (auto& L : c->list) {
@@ -913,14 +970,11 @@ static hipError_t chain_batch(ChainCtx* c, int k, int h) {
   const ChArgs* A = c->d_args;
   for (int j = 0; j < k; ++j, ++c->steps)
     c->timed(CHK_STEP, [&] {
-      if (c->block == CH_BLOCK)
-        hipLaunchKernelGGL(k_ch_step, dim3(c->grid), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps);
-      else
-        hipLaunchKernelGGL(k_ch_step_w, dim3(c->grid), dim3(64 * CH_WIDE), 0, c->stream, A, c->q, c->steps);
+      hipLaunchKernelGGL(k_ch_step, dim3(c->grid), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps);
     });
   for (int j = 0; j < h && c->hops < CH_MAXS; ++j, ++c->hops)
     c->timed(CHK_HOP, [&] {
-      hipLaunchKernelGGL(k_ch_hop, dim3(CH_HOP_WGS), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps - 1, c->hops);
+      hipLaunchKernelGGL(k_ch_hop, dim3(CH_HOP_WGS), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps, c->hops);
     });
   hipLaunchKernelGGL(k_ch_out, dim3(1), dim3(64), 0, c->stream, A, c->q, c->steps, c->hops, c->d_out);
   ++c->batches;
@@ -958,7 +1012,7 @@ static hipError_t chain_prepare(ChainCtx* c, const SpTypes& fwd, const SpTypes& 
     c->cached = a;
     c->args_valid = true;
   }
-  c->q = ChQ{s, t, upto, epoch, epoch, epoch};
+  c->q = ChQ{s, t, upto, epoch, epoch, epoch, c->solo};
   c->steps = c->hops = 0;
   c->last_batched = false;
   ++c->queries;
@@ -1021,7 +1075,7 @@ hipError_t chain_launch_batch(ChainCtx* const* cs, int n, const ChainQuery* qs) 
     });
   for (int j = 0; j < h; ++j)
     c0->timed(CHK_HOP_B, [&] {
-      hipLaunchKernelGGL(k_ch_hop_b, dim3((unsigned)n * CH_HOP_WGS), dim3(CH_BLOCK), 0, st, b, k - 1, j);
+      hipLaunchKernelGGL(k_ch_hop_b, dim3((unsigned)n * CH_HOP_WGS), dim3(CH_BLOCK), 0, st, b, k, j);
     });
   hipLaunchKernelGGL(k_ch_out_b, dim3((unsigned)n), dim3(64), 0, st, b, k, h);
   HIP_TRY_CH(hipGetLastError());
@@ -1053,8 +1107,8 @@ bool chain_more(ChainCtx* c, hipError_t* he) {
     *he = chain_batch(c, 0, (int)F.L - (int)hpos);
     return false;
   }
-  // steps used: the BFS levels and B-set steps; decay toward this query's needs
-  const double used = (double)F.levels + (F.met && F.kf >= 2 ? F.kf - 1 : 0);
+  // step launches that ran a step; decay toward this query's needs
+  const double used = (double)h.busy;
   c->ema_steps = 0.9 * c->ema_steps + 0.1 * (used + 0.5);
   if (F.met) c->ema_hops = 0.9 * c->ema_hops + 0.1 * ((double)h.hlaunch + 0.3);
   return true;
