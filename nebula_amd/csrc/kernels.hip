@@ -604,9 +604,6 @@ struct BfsParams {
   // over nds (the next step's first OVER type); nlist.zero_next is zeroed by workgroup 0
   ListOut nlist;
   DegSrc nds;
-  // MARK claim mode: a per-wave direct-mapped LDS cache of the neighbours this wave already
-  // claimed or saw claimed filters repeats before the global label read + CAS (NBG_MARK_DEDUP)
-  int lds_dedup;
   // MARK on a partitioned engine (non-null): neighbours set their bit of the global id space in
   // this bitmap (the hop's all-to-all send buffer) instead of a byte flag — no pack pass
   unsigned long long* bits;
@@ -642,28 +639,14 @@ struct FinalParams {
 // owns it — and the owners appended to the next frontier list together with their edge space
 // over the next step's first OVER type: one packed atomic per wave for list positions and edge
 // offsets.  A vertex without edges there is kept (the list is the frontier of every OVER type).
-constexpr int SEEN_BITS = 9;                     // MARK LDS pre-dedup: 512 entries per wave
-__device__ __forceinline__ uint32_t seen_slot(uint32_t x) { return (x * 0x9E3779B1u) >> (32 - SEEN_BITS); }
-
-__device__ __forceinline__ void claim_append(const uint32_t (&u)[VT], const BfsParams& bp, int lane, uint32_t* seen) {
+__device__ __forceinline__ void claim_append(const uint32_t (&u)[VT], const BfsParams& bp, int lane) {
   uint32_t dg[VT], rs[VT], cmask = 0;
-  uint32_t hit = 0;
-  if (seen) {   // (a vertex in the cache was claimed at this step by this wave or by someone before it)
-#pragma unroll
-    for (int i = 0; i < VT; ++i) {
-      const uint32_t x = u[i];
-      if (x == NO_ROW) continue;
-      const uint32_t sl = seen_slot(x);
-      if (seen[sl] == x) hit |= 1u << i;
-      else seen[sl] = x;
-    }
-  }
 #pragma unroll
   for (int i = 0; i < VT; ++i) {
     dg[i] = 0;
     rs[i] = 0;
     const uint32_t x = u[i];
-    if (x == NO_ROW || ((hit >> i) & 1u)) continue;
+    if (x == NO_ROW) continue;
     const uint32_t old = bp.lab[x];
     if (old == bp.stamp) continue;
     if (atomicCAS(bp.lab + x, old, bp.stamp) != old) continue;
@@ -757,8 +740,6 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
   extern __shared__ int64_t regs[];               // FINAL generic path: [nregs][BLOCK]
 
   __shared__ uint32_t sIl[INL ? 3 * INLINE_STARTS : 1];   // INL: end[], rs[], id[] of the start list
-  constexpr bool kClaims = M == MARK || M == MARKB;
-  __shared__ uint32_t sSeenAll[WAVES][kClaims ? (1 << SEEN_BITS) : 1];   // MARK: LDS pre-dedup cache
   uint64_t n, total;   // list entries, edges
   if constexpr (INL) {
     n = il.n;
@@ -789,13 +770,6 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
   const uint64_t ntiles = (npath + TV - 1) / TV;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar registers
-  uint32_t* seen = nullptr;
-  if constexpr (kClaims) {
-    if (bp.lab && bp.lds_dedup) {
-      seen = sSeenAll[w];
-      for (int k = lane; k < (1 << SEEN_BITS); k += 64) seen[k] = NO_ROW;
-    }
-  }
   uint32_t* const sEnd = sEndAll[w];
   uint32_t* const sRs = sRsAll[w];
   uint16_t* const sSeg = sSegAll[w];
@@ -969,7 +943,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
           if (!bp.lab) flags[u[i]] = 1;
         }
       }
-      if (bp.lab) claim_append(u, bp, lane, seen);
+      if (bp.lab) claim_append(u, bp, lane);
     } else if constexpr (M == MARK) {
       uint32_t u[V];   // all neighbour loads in flight before the flag stores / claims
 #pragma unroll
@@ -982,7 +956,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
         }
       }
       if (bp.lab) {
-        claim_append(u, bp, lane, seen);
+        claim_append(u, bp, lane);
       } else if (bp.sparse) {
 #pragma unroll
         for (int i = 0; i < V; ++i) {
@@ -1912,8 +1886,6 @@ hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, 
       w->step_stamp = w->seen_stamp;
     }
     bp.lab = w->seen;
-    static const int dedup = getenv("NBG_MARK_DEDUP") ? atoi(getenv("NBG_MARK_DEDUP")) : 0;
-    bp.lds_dedup = dedup;
     bp.stamp = w->step_stamp;
     const int nset = w->cur ^ 1;
     bp.nds = deg_src(next0);

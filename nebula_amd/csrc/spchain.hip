@@ -197,6 +197,24 @@ namespace {
 #ifndef CH_GUARD
 #define CH_GUARD 0
 #endif
+// CH_PHASE=1 (an experiment build, `make EXTRA=-DCH_PHASE=1`): workgroup 0's wave 0 of every step
+// launch over more than 64 tiles prints the 100 MHz wall-clock ticks spent in each phase of its tiles.
+#ifndef CH_PHASE
+#define CH_PHASE 0
+#endif
+#if CH_PHASE
+#define CH_PH(k)                                          \
+  do {                                                    \
+    const unsigned long long c_ = wall_clock64();         \
+    ph[k] += c_ - ph_prev;                                \
+    ph_prev = c_;                                         \
+  } while (0)
+#else
+#define CH_PH(k) \
+  do {           \
+  } while (0)
+#endif
+
 template <typename T>
 __device__ __forceinline__ T gld(const T* p, uint64_t i, uint64_t n, int site, ChState* st) {
   if (CH_GUARD && i >= n) {
@@ -438,10 +456,16 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
   uint32_t* const sEnd = sEndAll[w];
   uint32_t* const sRs = sRsAll[w];
   uint16_t* const sSeg = sSegAll[w];
+#if CH_PHASE
+  unsigned long long ph[12] = {0}, ph_prev = wall_clock64(), rounds = 0;
+#endif
   for (uint64_t t = (uint64_t)bid * NW + w; t < ntiles; t += (uint64_t)nblk * NW) {
+    uint32_t c[CH_VT];   // the vertex a claim is about: the neighbour, or (pull) the list entry
+    uint32_t cm = 0, mm = 0;
     // once this level has met, its claims are not expanded again: their appends are skipped
     // (read now, used after the claims: the load is off the critical path)
     const unsigned long long met_now = bfs ? ld_agent(&st->lmeet[i]) : 0ull;
+    CH_PH(0);
     uint64_t sp = 0;
     if (ntiles > 1) {
       if (lane == 0) sp = gld(S.tsplit, t, A.tsplit_cap, 3, st);
@@ -460,6 +484,7 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
       if (kk <= na) sRs[kk] = (uint64_t)(e + 1) < n ? gld(S.seg_rs, (uint64_t)(e + 1), A.list_cap, 4, st) : 0u;
     }
     wave_lds_sync();
+    CH_PH(1);
     const uint32_t* Aend = sEnd + 1;   // Aend[j] = end of entry a0 + j
     {   // lane-level merge path: the entry of every edge item
       const int diag = lane * CH_VT, dmax = na + nb;
@@ -498,7 +523,7 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
       }
     }
     wave_lds_sync();   // (the next tile rewrites the window)
-    uint32_t c[CH_VT];   // the vertex a claim is about: the neighbour, or (pull) the list entry
+    CH_PH(2);
     if (pull) {
       uint32_t tl[CH_VT], vis[CH_VT];
 #pragma unroll
@@ -513,13 +538,13 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
 #pragma unroll
       for (int j = 0; j < CH_VT; ++j) c[j] = x[j];
     }
+    CH_PH(3);
     uint32_t old[CH_VT], gate[CH_VT];
 #pragma unroll
     for (int j = 0; j < CH_VT; ++j) {
       old[j] = c[j] != NO_ROW ? gld(lab, c[j], A.nv, 8, st) : 0u;
       gate[j] = (c[j] != NO_ROW && rlab) ? gld(rlab, c[j], A.nv, 8, st) : rstamp;
     }
-    uint32_t cm = 0, mm = 0;
     if (met_now) {
       // the level has met: only meet vertices matter now (B[kf] is the met set; this level's other
       // labels are read by nothing), so the other side's label is tested before claiming
@@ -543,8 +568,8 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
         cm |= 1u << j;
       }
     }
-    if (!__ballot((cm | mm) != 0)) continue;
-    if (bfs && !met_now) {   // meet test: claimed vertices only (most neighbours of a big level are not)
+    CH_PH(4);
+    if (bfs && !met_now && __ballot(cm != 0)) {   // meet test: claimed vertices only (most neighbours of a big level are not)
       uint32_t ol[CH_VT];
 #pragma unroll
       for (int j = 0; j < CH_VT; ++j) ol[j] = ((cm >> j) & 1u) ? gld(olab, c[j], A.nv, 9, st) : 0u;
@@ -552,35 +577,54 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
       for (int j = 0; j < CH_VT; ++j)
         if (((cm >> j) & 1u) && live(ol[j], oepoch)) mm |= 1u << j;
     }
-    if (append && !met_now) {
-      uint32_t dg[CH_VT], rs[CH_VT];
+    CH_PH(5);
+    if (!__ballot((cm | mm) != 0)) continue;
+    // appends: one packed atomic per wave and list (aggregating them per workgroup behind two
+    // barriers measured 4 % slower, profiles/r03_v_sp_wg_append_ab.txt)
+    const uint32_t am = append && !met_now ? cm : 0u;
+    uint32_t dg[CH_VT], rs[CH_VT];
 #pragma unroll
-      for (int j = 0; j < CH_VT; ++j) {
-        dg[j] = 0;
-        rs[j] = 0;
-        if ((cm >> j) & 1u) dg[j] = vdeg(A, oside, c[j], &rs[j]);
-      }
-      wave_append(A, D, out_acc, c, cm, dg, rs);
+    for (int j = 0; j < CH_VT; ++j) {
+      dg[j] = 0;
+      rs[j] = 0;
+      if ((am >> j) & 1u) dg[j] = vdeg(A, oside, c[j], &rs[j]);
     }
-    if (__ballot(mm != 0)) {   // the sides met: LAB_M stamps, the meet list over in-edges
-      uint32_t dg[CH_VT], rs[CH_VT];
-      uint32_t nm = 0;
+#if CH_PHASE
+    { uint32_t sink = 0; for (int j = 0; j < CH_VT; ++j) sink += dg[j] + rs[j]; if (sink == 0xFFFFFFFFu) ph[11] += 1; }
+#endif
+    CH_PH(6);
+    if (append && !met_now) wave_append(A, D, out_acc, c, am, dg, rs);   // (a wave-uniform condition)
+    CH_PH(7);
+    // the sides met: LAB_M stamps, the meet list over in-edges, the level's meet count
+    uint32_t nm = 0;
 #pragma unroll
-      for (int j = 0; j < CH_VT; ++j) {
-        dg[j] = 0;
-        rs[j] = 0;
-        if ((mm >> j) & 1u) {
-          gst(A.lab[2], c[j], A.nv, mstamp, 10, st);
-          dg[j] = vdeg(A, 1, c[j], &rs[j]);
-          ++nm;
-        }
+    for (int j = 0; j < CH_VT; ++j) {
+      dg[j] = 0;
+      rs[j] = 0;
+      if ((mm >> j) & 1u) {
+        gst(A.lab[2], c[j], A.nv, mstamp, 10, st);
+        dg[j] = vdeg(A, 1, c[j], &rs[j]);
+        ++nm;
       }
+    }
+    CH_PH(8);
+    if (__ballot(mm != 0)) {
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) nm += __shfl_xor(nm, o, 64);
       if (lane == 0) atomicAdd(&st->lmeet[i], (unsigned long long)nm);
       wave_append(A, A.list[CL_M], &st->macc, c, mm, dg, rs);
     }
+    CH_PH(9);
+#if CH_PHASE
+    ++rounds;
+#endif
   }
+#if CH_PHASE
+  if (bid == 0 && threadIdx.x == 0 && ntiles > 64 && nblk > 1)
+    printf("CHPH step %d bfs %d ntiles %llu items %llu rounds %llu ticks %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu\n", i,
+           (int)bfs, (unsigned long long)ntiles, (unsigned long long)npath, rounds, ph[0], ph[1], ph[2], ph[3], ph[4], ph[5],
+           ph[6], ph[7], ph[8], ph[9]);
+#endif
 }
 
 // Items (entries + edges) of the source list of step P (as ch_level picks it).

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2 GPU-box steps (from the repo root, via gpurun): bash tools/gpu_r02.sh <tag> <step>...
+# GPU-box steps (rounds 2-3) (from the repo root, via gpurun): bash tools/gpu_r02.sh <tag> <step>...
 #   tests  — pytest -m gpu;  load26 — RMAT-26 generate + load + GO leg only (load time);
 #   bench  — default bench.py
 set -u
@@ -29,6 +29,13 @@ for step in "$@"; do
       done
       python3 tools/pmc_summary.py $(find "$OUT/pmc${sc}_FETCH_SIZE" "$OUT/pmc${sc}_WRITE_SIZE" -name '*counter_collection.csv') \
         > "$OUT/pmc_hbm_rmat${sc}.json" ;;
+    sppmc26)   # per-dispatch HBM bytes and durations of the one-pair SP chain (300 RMAT-26 pairs)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 400 rocprofv3 --pmc $c -d "$OUT/sppmc_$c" -o run --output-format csv -- \
+          python3 -u tools/sp_probe.py 26 300 > "$OUT/sppmc_$c.txt" 2>&1 || { tail -30 "$OUT/sppmc_$c.txt"; exit 1; }
+      done
+      timeout -k 10 400 rocprofv3 --kernel-trace -d "$OUT/sptrace" -o run --output-format csv -- \
+        python3 -u tools/sp_probe.py 26 300 > "$OUT/sptrace.txt" 2>&1 || { tail -30 "$OUT/sptrace.txt"; exit 1; } ;;
     prof26)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof26" -o run --output-format csv -- \
         python3 -u bench.py --sp-pairs 2000 --no-cpu-baseline --verify 0 --c2 0 --c5-scale 0 --getbound-reqs 0 --c1-reqs 0 \
