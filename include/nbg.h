@@ -434,8 +434,12 @@ int32_t nbg_comm_init_local(nbg_engine* const* engines, int32_t n);
  * collective engine cannot run a hop without one of its ranks, so a query fails on EVERY rank
  * with the same code instead:
  *   - a rank-local failure before the query's first collective (allocation, a start list whose
- *     edges exceed one rank's list limit, ...) is agreed in one small all-reduce: every rank
- *     returns the code of the lowest-ranked rank that failed, and the engines stay usable;
+ *     edges exceed one rank's list limit, ...) reaches every rank: every rank returns the code of
+ *     the lowest-ranked rank that failed, and the engines stay usable.  For GO without YIELD
+ *     DISTINCT and without $- / $var inputs the failing rank still takes part in the query's
+ *     collectives and its status travels with the query's statistics (no extra round trip): its
+ *     own nbg_go_submit fails, its peers' nbg_go_wait returns the code.  Other statements (and
+ *     FIND PATH) agree in one small all-reduce before the query, so every rank's call fails;
  *   - a failure between collectives (a device error on one rank) aborts the communicator; the
  *     peers' pending collectives fail (in-process group at once, RCCL when their bounded wait of
  *     NBG_COMM_TIMEOUT_S seconds, default 120, expires) and every later collective call fails

@@ -925,8 +925,25 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
     cap_rows += blk_cap[i] * ws_final_grid(n_final, eb);
   }
   if (!lrc && ws_reserve_rows(ws, cap_rows, ncols) != hipSuccess) local_fail(NBG_E_OUT_OF_MEMORY, "result rows");
-  // ---- agreement: the query runs on every rank or on none
-  if (part) {
+  // ---- agreement: the query runs on every rank or on none.  A statement whose only collectives
+  // are the hop bitmaps and the statistics (no YIELD DISTINCT owner exchange, no $- / $var roots)
+  // needs no host round trip for it: a rank whose preparation failed still takes part in those
+  // collectives, with zero bitmaps and its status word in the statistics, and every rank fails the
+  // query when it reads them (go_collect).  Other statements agree first (Comm::agree).
+  static const bool force_agree = getenv("NBG_GO_AGREE") && atoi(getenv("NBG_GO_AGREE")) != 0;
+  const bool in_band = part && !st->distinct && !st->uses_input && !force_agree;
+  if (in_band) {
+    if (lrc) {
+      int32_t agreed = NBG_OK;
+      const hipError_t he = part_empty_query(qcomm, stream, (int)steps - 1, E.fb_send, E.fb_recv, E.npad / 8,
+                                             E.fb_gst, E.fb_hgst, lrc, &agreed);
+      if (he != hipSuccess) {
+        qcomm->abort();
+        return E.fail(NBG_E_DEVICE, "query statistics exchange: " + qcomm->last);
+      }
+      return E.fail(lrc, lmsg);
+    }
+  } else if (part) {
     int32_t agreed = NBG_OK;
     if (qcomm->agree(stream, lrc, &agreed)) return E.fail(NBG_E_DEVICE, "query agreement: " + qcomm->last);
     if (agreed) {
@@ -1031,6 +1048,13 @@ static int32_t go_collect(Engine& E, const nbg_go_stmt* st, GoPending* p, nbg_ro
   if (he != hipSuccess) {
     delete rows;
     return E.fail(NBG_E_DEVICE, std::string("HIP: ") + hipGetErrorString(he));
+  }
+  if (E.partitioned()) {   // a rank whose preparation failed (go_launch, in-band statuses)
+    const int32_t code = ws_host_gstatus(ws);
+    if (code) {
+      delete rows;
+      return E.fail(code, "the query failed on another rank (code " + std::to_string(code) + ")");
+    }
   }
   const QState& q = *ws_host_state(ws);
   // statistics of the whole query: this engine's, or summed over all ranks when partitioned
@@ -1234,6 +1258,12 @@ int32_t nbg::engine_ready(Engine& E) {
   if (!E.ws) return E.fail(NBG_E_OUT_OF_MEMORY, err);
   if (E.partitioned()) {
     hipError_t he = ws_set_partition(E.ws, E.comm.get(), E.npad);
+    const size_t G = (size_t)E.cfg.num_gpus, seg = E.npad / 8, gw = part_gst_words((int)G);
+    if (he == hipSuccess) he = hipMalloc(&E.fb_send, G * seg);
+    if (he == hipSuccess) he = hipMemset(E.fb_send, 0, G * seg);
+    if (he == hipSuccess) he = hipMalloc(&E.fb_recv, G * seg);
+    if (he == hipSuccess) he = hipMalloc((void**)&E.fb_gst, gw * 8);
+    if (he == hipSuccess) he = hipHostMalloc((void**)&E.fb_hgst, gw * 8, hipHostMallocDefault);
     if (he != hipSuccess) return E.fail(NBG_E_OUT_OF_MEMORY, std::string("partition buffers: ") + hipGetErrorString(he));
     return build_path_replica(E);   // collective: every rank finalizes together
   }
@@ -1352,6 +1382,10 @@ void nbg_destroy(nbg_engine* h) {
   }
   path_slots_release(E);
   destroy_path_replica(E);
+  if (E.stream) (void)hipStreamSynchronize(E.stream);
+  for (void* p : {E.fb_send, E.fb_recv, (void*)E.fb_gst})
+    if (p) (void)hipFree(p);
+  if (E.fb_hgst) (void)hipHostFree(E.fb_hgst);
   E.pinned_release();
   if (E.ws) ws_destroy(E.ws);
   if (E.sp) sp_destroy(E.sp);

@@ -75,6 +75,12 @@ struct Engine {
   // FIND PATH replica of a partitioned snapshot (replica.hip): a single-GPU engine over every
   // rank's path CSRs; FIND PATH runs on it rank-locally while it is in use
   std::unique_ptr<Engine> rep;
+  // partitioned GO: what a rank whose query preparation failed takes part in the query's
+  // collectives with (go_launch): a zero send bitmap, a receive scratch, the statistics words
+  void* fb_send = nullptr;
+  void* fb_recv = nullptr;
+  unsigned long long* fb_gst = nullptr;
+  unsigned long long* fb_hgst = nullptr;
   int path_replica_mode = -1;   // build it at finalize: 1 yes (when it fits), 0 no, -1 NBG_PATH_REPLICA (default 1)
   bool path_replica_use = true; // nbg_set_path_replica after finalize: 0 = the collective search
   Engine* path_engine() { return rep && path_replica_use ? rep.get() : this; }

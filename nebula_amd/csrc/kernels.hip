@@ -1278,9 +1278,13 @@ __global__ void k_note(const unsigned long long* __restrict__ acc, unsigned long
 }
 
 // Query statistics every rank needs globally: [err, step_n[0..MAX_STEPS+1], Σ_types e_st[s]].
-// Then one counter per QState::tagbits bit (summed: > 0 is the OR over ranks).
+// Then one counter per QState::tagbits bit (summed: > 0 is the OR over ranks), then one status
+// word per rank (the rank's local status of the query: its own word, the others 0).
 constexpr int GST_N0 = 1 + 2 * (MAX_STEPS + 2);
 constexpr int GST_N = GST_N0 + 2 * MAX_TAG_BITS;
+__global__ void k_gst_status(unsigned long long* __restrict__ g, int world, int rank, long long status) {
+  for (int r = threadIdx.x; r < world; r += blockDim.x) g[GST_N + r] = r == rank ? (unsigned long long)status : 0ull;
+}
 __global__ void k_gstats(const QState* __restrict__ q, int ntypes, unsigned long long* __restrict__ g) {
   const int s = threadIdx.x;
   if (s == 0) g[0] = q->err ? 1ull : 0ull;
@@ -2513,10 +2517,36 @@ hipError_t ws_set_partition(Workspace* w, Comm* comm, uint64_t npad) {
   HIP_TRY(hipMalloc((void**)&w->sendbits, G * npad / 8));
   HIP_TRY(hipMemsetAsync(w->sendbits, 0, G * npad / 8, w->stream));   // all-zero between hops
   HIP_TRY(hipMalloc((void**)&w->recvbits, G * npad / 8));
-  HIP_TRY(hipMalloc((void**)&w->gst, GST_N * sizeof(unsigned long long)));
-  HIP_TRY(hipHostMalloc((void**)&w->h_gst, GST_N * sizeof(unsigned long long), hipHostMallocDefault));
+  HIP_TRY(hipMalloc((void**)&w->gst, (GST_N + G) * sizeof(unsigned long long)));
+  HIP_TRY(hipHostMalloc((void**)&w->h_gst, (GST_N + G) * sizeof(unsigned long long), hipHostMallocDefault));
   return ws_sync(w);
 }
+
+// A rank whose preparation of a query failed still takes part in the query's collectives (the
+// fast path of a partitioned GO, engine.cpp go_launch): `hops` all-to-alls of the zero bitmap
+// `send0` (G segments of seg_bytes; received into `recv`, never read), then the statistics
+// all-reduce with zero statistics and its status word.  Synchronous; *agreed = the first failing
+// rank's status.
+hipError_t part_empty_query(Comm* c, hipStream_t s, int hops, const void* send0, void* recv, size_t seg_bytes,
+                            unsigned long long* gst, unsigned long long* h_gst, int32_t status, int32_t* agreed) {
+  const int G = c->world;
+  for (int h = 0; h < hops; ++h)
+    if (c->alltoall(send0, recv, seg_bytes, s)) return hipErrorUnknown;
+  HIP_TRY(hipMemsetAsync(gst, 0, GST_N * sizeof(unsigned long long), s));
+  hipLaunchKernelGGL(k_gst_status, dim3(1), dim3(64), 0, s, gst, G, c->rank, (long long)status);
+  HIP_TRY(hipGetLastError());
+  if (c->allreduce_sum_u64(gst, GST_N + G, s)) return hipErrorUnknown;
+  HIP_TRY(hipMemcpyAsync(h_gst, gst, (GST_N + G) * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  if (c->wait(s)) return hipErrorUnknown;
+  *agreed = NBG_OK;
+  for (int r = 0; r < G; ++r)
+    if (h_gst[GST_N + r]) {
+      *agreed = (int32_t)(long long)h_gst[GST_N + r];
+      break;
+    }
+  return hipSuccess;
+}
+size_t part_gst_words(int world) { return (size_t)GST_N + (size_t)world; }
 
 // After all OVER types of a non-final step marked their candidates (global ids) in the flags:
 // pack -> all-to-all of npad-bit segments -> owner OR + compaction into the next local frontier.
@@ -2560,10 +2590,22 @@ hipError_t ws_exchange(Workspace* w, int step, const ExpandArgs* next0) {
 // end; valid in ws_host_gstats() after ws_end_query.
 hipError_t ws_global_stats(Workspace* w, int ntypes) {
   if (!w->comm) return hipErrorInvalidValue;
+  const int G = w->comm->world;
   hipLaunchKernelGGL(k_gstats, dim3(1), dim3(64), 0, w->stream, w->q, ntypes, w->gst);
   HIP_TRY(hipGetLastError());
-  if (w->comm->allreduce_sum_u64(w->gst, GST_N, w->stream)) return hipErrorUnknown;
-  return hipMemcpyAsync(w->h_gst, w->gst, GST_N * sizeof(unsigned long long), hipMemcpyDeviceToHost, w->stream);
+  hipLaunchKernelGGL(k_gst_status, dim3(1), dim3(64), 0, w->stream, w->gst, G, w->comm->rank, 0ll);
+  HIP_TRY(hipGetLastError());
+  if (w->comm->allreduce_sum_u64(w->gst, GST_N + G, w->stream)) return hipErrorUnknown;
+  return hipMemcpyAsync(w->h_gst, w->gst, (GST_N + G) * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                        w->stream);
+}
+
+// the first failing rank's status word of the last query's statistics (NBG_OK: none failed)
+int32_t ws_host_gstatus(Workspace* w) {
+  if (!w->comm) return NBG_OK;
+  for (int r = 0; r < w->comm->world; ++r)
+    if (w->h_gst[GST_N + r]) return (int32_t)(long long)w->h_gst[GST_N + r];
+  return NBG_OK;
 }
 
 void ws_host_gstats(Workspace* w, unsigned long long* err, unsigned long long* step_n, unsigned long long* esum,

@@ -531,6 +531,10 @@ Comm* ws_get_comm(const Workspace* w);   // the communicator of a partitioned wo
 hipStream_t ws_stream(const Workspace* w);
 hipError_t ws_exchange(Workspace* w, int step, const ExpandArgs* next0);   // replaces ws_compact
 hipError_t ws_global_stats(Workspace* w, int ntypes);      // before ws_end_query
+int32_t ws_host_gstatus(Workspace* w);                     // after it: the first failing rank's status
+hipError_t part_empty_query(Comm* c, hipStream_t s, int hops, const void* send0, void* recv, size_t seg_bytes,
+                            unsigned long long* gst, unsigned long long* h_gst, int32_t status, int32_t* agreed);
+size_t part_gst_words(int world);
 void ws_host_gstats(Workspace* w, unsigned long long* err, unsigned long long* step_n, unsigned long long* esum,
                     unsigned long long* tagbits);
 

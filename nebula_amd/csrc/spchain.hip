@@ -271,6 +271,20 @@ __device__ __forceinline__ uint32_t vdeg(const ChArgs& A, int side, uint32_t v, 
   return gld(A.row_ptr[side], (uint64_t)v + 1, A.nv + 1, 1, A.st) - r;
 }
 
+// vdeg with every load issued at once (visibility and both row offsets), for a vertex that may
+// not be claimed: its loads then travel with the claim's instead of after it
+__device__ __forceinline__ uint32_t vdeg_spec(const ChArgs& A, int side, uint32_t v, uint32_t* rs) {
+  if (v == NO_ROW) {
+    *rs = 0;
+    return 0;
+  }
+  const uint8_t vis = A.visible ? gld(A.visible, v, A.nv, 0, A.st) : (uint8_t)1;
+  const uint32_t r = gld(A.row_ptr[side], v, A.nv + 1, 1, A.st);
+  const uint32_t e = gld(A.row_ptr[side], (uint64_t)v + 1, A.nv + 1, 1, A.st);
+  *rs = vis ? r : 0u;
+  return vis ? e - r : 0u;
+}
+
 // Entry pos of list L: vertex v, its deg edges ending at edge offset end, from row rs; the tile
 // boundaries its merge-path range [pos + end - deg, pos + end] covers get their split.
 constexpr uint32_t CH_SPLITS_SOLO = 4;   // an entry covering more tile boundaries: the wave writes them
@@ -540,10 +554,23 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
     }
     CH_PH(3);
     uint32_t old[CH_VT], gate[CH_VT];
+    // a BFS level before its meet: the other side's label and the degree / row start of EVERY
+    // neighbour are loaded with its own label, so the meet test and the append do not wait for
+    // two more round trips after the claim (the extra loads are cheap: a level runs far below the
+    // HBM bandwidth, profiles/r03_t_sp_step_pmc.txt)
+    const bool spec = bfs && !met_now;   // (wave-uniform)
+    uint32_t sol[CH_VT], sdg[CH_VT], srs[CH_VT];
 #pragma unroll
     for (int j = 0; j < CH_VT; ++j) {
       old[j] = c[j] != NO_ROW ? gld(lab, c[j], A.nv, 8, st) : 0u;
       gate[j] = (c[j] != NO_ROW && rlab) ? gld(rlab, c[j], A.nv, 8, st) : rstamp;
+      sol[j] = 0;
+      sdg[j] = 0;
+      srs[j] = 0;
+      if (spec && c[j] != NO_ROW) {
+        sol[j] = gld(olab, c[j], A.nv, 9, st);
+        sdg[j] = vdeg_spec(A, oside, c[j], &srs[j]);
+      }
     }
     if (met_now) {
       // the level has met: only meet vertices matter now (B[kf] is the met set; this level's other
@@ -569,13 +596,10 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
       }
     }
     CH_PH(4);
-    if (bfs && !met_now && __ballot(cm != 0)) {   // meet test: claimed vertices only (most neighbours of a big level are not)
-      uint32_t ol[CH_VT];
-#pragma unroll
-      for (int j = 0; j < CH_VT; ++j) ol[j] = ((cm >> j) & 1u) ? gld(olab, c[j], A.nv, 9, st) : 0u;
+    if (spec) {   // meet test: the claimed vertices the other side has labelled
 #pragma unroll
       for (int j = 0; j < CH_VT; ++j)
-        if (((cm >> j) & 1u) && live(ol[j], oepoch)) mm |= 1u << j;
+        if (((cm >> j) & 1u) && live(sol[j], oepoch)) mm |= 1u << j;
     }
     CH_PH(5);
     if (!__ballot((cm | mm) != 0)) continue;
@@ -587,7 +611,14 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
     for (int j = 0; j < CH_VT; ++j) {
       dg[j] = 0;
       rs[j] = 0;
-      if ((am >> j) & 1u) dg[j] = vdeg(A, oside, c[j], &rs[j]);
+      if ((am >> j) & 1u) {
+        if (spec) {
+          dg[j] = sdg[j];
+          rs[j] = srs[j];
+        } else {
+          dg[j] = vdeg(A, oside, c[j], &rs[j]);
+        }
+      }
     }
 #if CH_PHASE
     { uint32_t sink = 0; for (int j = 0; j < CH_VT; ++j) sink += dg[j] + rs[j]; if (sink == 0xFFFFFFFFu) ph[11] += 1; }
@@ -886,7 +917,7 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_setup_b(ChBatch b) {
   if ((int)blockIdx.x < b.n) ch_setup(*b.A[blockIdx.x], b.q[blockIdx.x]);
 }
 #ifndef NBG_STEPB_WPE
-#define NBG_STEPB_WPE 4
+#define NBG_STEPB_WPE 2   // (2 waves/SIMD: no spills; batched 33.3-33.9k -> 34.7-35.0k pairs/s, profiles/r03_y_sp_spec_ab.txt)
 #endif
 __global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(NBG_STEPB_WPE))) k_ch_step_b(ChBatch b, int i) {
   const uint32_t p = blockIdx.x / b.per;

@@ -75,14 +75,15 @@ def test_agreed_failures_leave_engines_usable(graph, world):
         starts = np.full((1 << 32) // hdeg + 1, hub, dtype=np.int64)
         assert _codes(c, lambda e: e.go(starts, [1], 2)) == [L.E_UNSUPPORTED] * world
         assert graphs.sorted_rows(c.go([r0], [1], 3, WHERE)) == exp
-        # (3) asynchronous submission: the failing query's submit fails everywhere, the next runs
+        # (3) asynchronous submission: the failing rank's submit fails; its peers' statuses arrive
+        #     with the query's statistics, so their wait fails with the same code; the next runs
         c.inject_fault(0, L.FAULT_ALLOC)
 
         def submit_twice(e):
             st = e.prepare_go([1], 3, WHERE)
             try:
                 try:
-                    st.submit([r0], device=False)
+                    st.wait(st.submit([r0], device=False)).free()
                     first = 0
                 except NbgError as ex:
                     first = ex.code
@@ -95,6 +96,13 @@ def test_agreed_failures_leave_engines_usable(graph, world):
         out = c.each(submit_twice)
         assert [o[0] for o in out] == [L.E_OUT_OF_MEMORY] * world
         assert graphs.sorted_rows([r for o in out for r in o[1]]) == exp
+        # (3b) YIELD DISTINCT has an owner exchange of its own: its failures are agreed before
+        #      the query (Comm::agree) instead of carried in the statistics
+        yd = [E.edge_prop("e", "_dst").encode()]
+        exp_d = graphs.sorted_rows(single.go([r0], [1], 2, WHERE, yd, distinct=True))
+        c.inject_fault(world - 1, L.FAULT_ALLOC)
+        assert _codes(c, lambda e: e.go([r0], [1], 2, WHERE, yd, distinct=True)) == [L.E_OUT_OF_MEMORY] * world
+        assert graphs.sorted_rows(c.go([r0], [1], 2, WHERE, yd, distinct=True)) == exp_d
         # (4) FIND PATH: an allocation failure on rank 0, then a normal request
         s, t = rmat.pick_pairs(src, dst, 1, seed=17)[0]
         c.inject_fault(0, L.FAULT_ALLOC)
