@@ -420,10 +420,18 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
           segs.emplace_back(region[i] + (uint64_t)b * blk_cap[i], per[b]);
           total += per[b];
         }
-      std::vector<std::vector<int64_t>> cols(nc, std::vector<int64_t>(total));
-      std::vector<int64_t*> hc;
-      for (auto& c : cols) hc.push_back(c.data());
-      if (total && ws_fetch_rows(ws, segs, nc, total, hc.data()) != hipSuccess)
+      // the rows into a pinned block of the engine's pool (column c at c * total), packed there
+      // by the device (a pageable copy per column cost more than the request's expansion)
+      size_t hbytes = 0;
+      int64_t* hb = total ? static_cast<int64_t*>(E.pinned_get(total * (size_t)nc * 8, &hbytes)) : nullptr;
+      if (total && !hb) return E.fail(NBG_E_OUT_OF_MEMORY, "row fetch staging");
+      struct Put {   // (the block goes back to the pool on every path out of this scope)
+        Engine& e; int64_t* p; size_t n;
+        ~Put() { if (p) e.pinned_put(p, n); }
+      } put{E, hb, hbytes};
+      std::vector<const int64_t*> cols(nc);
+      for (int c = 0; c < nc; ++c) cols[c] = hb + (size_t)c * total;
+      if (total && ws_fetch_rows_pinned(ws, segs, nc, total, hb) != hipSuccess)
         return E.fail(NBG_E_DEVICE, "row fetch failed");
       // key order: CSR index order (rows of one source are contiguous and sorted)
       std::vector<uint64_t> ord(total);

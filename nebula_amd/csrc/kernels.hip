@@ -2379,20 +2379,27 @@ hipError_t ws_fetch_rows(Workspace* w, const std::vector<std::pair<uint64_t, uin
                        nseg, (int64_t* const*)w->d_row_cols, ncols, d_out, total);
     e = hipGetLastError();
   }
-  for (int c = 0; e == hipSuccess && c < ncols; ++c)
+  bool contiguous = true;   // host columns back to back (a pinned block): one copy for all of them
+  for (int c = 1; c < ncols; ++c) contiguous = contiguous && host_cols[c] == host_cols[0] + (uint64_t)c * total;
+  if (contiguous && e == hipSuccess)
+    e = hipMemcpyAsync(host_cols[0], d_out, total * (uint64_t)ncols * 8, hipMemcpyDeviceToHost, w->stream);
+  for (int c = 0; !contiguous && e == hipSuccess && c < ncols; ++c)
     e = hipMemcpyAsync(host_cols[c], d_out + (uint64_t)c * total, total * 8, hipMemcpyDeviceToHost, w->stream);
   if (e == hipSuccess) e = ws_sync(w);
   return e;
 }
 
-// Rows into a pinned host block (columns back to back, `total` rows each).  Default: packed on the
-// device, then one DMA per column (above).  NBG_FETCH=direct: the packing kernel stores over the
-// host link itself (no staging copy).  Both reach the same ~16 GB/s on the measured box (the
-// host link, profiles/r03_c_*), so the DMA path stays the default.
+// Rows into a pinned host block (columns back to back, `total` rows each): packed by the device
+// straight into the block over the host link (16-byte stores), or — for results of 32 MB and
+// more — packed on the device and DMAed (above; ~50 GB/s either way at that size,
+// profiles/r03_r_host_delivered_ab.txt, while a copy-engine transfer of a small result costs
+// ~130 us of latency, r03_m_d2h_probe.json).  NBG_FETCH=direct / dma forces one of them.
 hipError_t ws_fetch_rows_pinned(Workspace* w, const std::vector<std::pair<uint64_t, uint64_t>>& segs, int ncols,
                                 uint64_t total, int64_t* host_block) {
   if (!total || !ncols) return hipSuccess;
-  static const bool dma = !getenv("NBG_FETCH") || strcmp(getenv("NBG_FETCH"), "direct") != 0;
+  static const char* mode = getenv("NBG_FETCH");
+  const bool big = total * (uint64_t)ncols * 8 >= (32ull << 20);
+  const bool dma = mode ? strcmp(mode, "direct") != 0 : big;
   void* dptr = nullptr;
   if (dma || hipHostGetDevicePointer(&dptr, host_block, 0) != hipSuccess || !dptr) {
     std::vector<int64_t*> hc(ncols);
