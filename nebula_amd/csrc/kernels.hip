@@ -725,6 +725,9 @@ using InlineArg = typename std::conditional<INL, InlineList, NoInline>::type;
 // TILE = 64 * VT; a V = 2 * VT instantiation reads every other split.  (FINALD with V = 8 at 5 or
 // 6 waves per SIMD measured 307-338 us per RMAT-26 launch against 222 us at V = 4 and 8 waves,
 // profiles/r02_q_final_vt8_ab.json: the default V = VT is the only one launched.)
+#ifndef NBG_MARK_PACKED
+#define NBG_MARK_PACKED 0   // 1: MARK tiles packed WAVES to a workgroup (the round-2 order, for A/B)
+#endif
 template <int M, bool INL = false, int V = VT>
 #ifndef NBG_WIDE_WAVES
 #define NBG_WIDE_WAVES 6
@@ -857,7 +860,11 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
   const uint32_t xb = (gridDim.x % 8 == 0) ? (blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8 : blockIdx.x;
   uint64_t t = (uint64_t)xb * WAVES + w;
 #else
-  uint64_t t = (uint64_t)blockIdx.x * WAVES + w;
+  // MARK: tile t -> workgroup t % grid first (a step's few tiles spread over CUs, each CU's miss
+  // queue serving one wave's random claims; see spchain.hip); the final step keeps adjacent tiles
+  // in one workgroup (they share lines at their boundaries)
+  uint64_t t = (M == MARK || M == MARKB) && !NBG_MARK_PACKED ? (uint64_t)w * gridDim.x + blockIdx.x
+                                                             : (uint64_t)blockIdx.x * WAVES + w;
 #endif
   uint64_t sp_next = 0;            // lanes 0, 1: split (start, end) of tile t + g
   uint64_t a0 = 0, a1 = 0;         // split of tile t

@@ -473,7 +473,15 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
 #if CH_PHASE
   unsigned long long ph[12] = {0}, ph_prev = wall_clock64(), rounds = 0;
 #endif
+  // tile t -> workgroup t % nblk, wave (t / nblk) % NW: the tiles of a level spread over as many
+  // CUs as it has tiles (up to the grid) before any CU gets a second one.  A tile's random loads
+  // and atomics (8 per lane) queue at its CU, so tiles packed 4 to a workgroup had 4 waves' misses
+  // in one CU's queue while most CUs idled (NBG_SP_PACKED=1: the packed order, for A/B)
+#ifdef NBG_SP_PACKED
   for (uint64_t t = (uint64_t)bid * NW + w; t < ntiles; t += (uint64_t)nblk * NW) {
+#else
+  for (uint64_t t = (uint64_t)w * nblk + bid; t < ntiles; t += (uint64_t)nblk * NW) {
+#endif
     uint32_t c[CH_VT];   // the vertex a claim is about: the neighbour, or (pull) the list entry
     uint32_t cm = 0, mm = 0;
     // once this level has met, its claims are not expanded again: their appends are skipped
