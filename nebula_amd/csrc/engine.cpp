@@ -144,6 +144,7 @@ struct nbg_rows {
   // per (OVER type, column), and the read-back hazards it implies (see go_prepare)
   std::vector<int32_t> col_types;
   std::vector<std::vector<uint8_t>> wclass;
+  bool small_ok = false;     // the end-of-query kernel may have packed these rows (ws_host_small_rows)
   bool misaligned = false;   // some column's written bytes differ in length from what its reader takes
   bool float_col = false;    // a FLOAT column: InterimResult::getRows fails on it
 };
@@ -331,7 +332,11 @@ int32_t materialize_rows(nbg_rows* r) {
   const size_t bytes = std::max<size_t>((size_t)r->count * (size_t)r->ncols * 8, 8);
   r->hbits = static_cast<int64_t*>(E.pinned_get(bytes, &r->hbytes));
   if (!r->hbits) return NBG_E_OUT_OF_MEMORY;
-  if (r->count) {
+  // packed at the query's end already (a small result, go_launch): the segments' cells in this order
+  const int64_t* pre = r->count && r->ws && r->small_ok ? ws_host_small_rows(r->ws, r->count) : nullptr;
+  if (pre) {
+    memcpy(r->hbits, pre, (size_t)r->count * (size_t)r->ncols * 8);
+  } else if (r->count) {
     std::vector<std::pair<uint64_t, uint64_t>> segs;
     segs.reserve(r->segs.size());
     for (auto& s : r->segs) segs.emplace_back(s.begin, s.end - s.begin);
@@ -1017,7 +1022,22 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
     }
   }
   if (he == hipSuccess && part) he = ws_global_stats(ws, (int)over.size());
-  if (he == hipSuccess) he = ws_end_query_async(ws);
+  // a single engine's result that will be fetched to the host is packed there by the end-of-query
+  // kernel when it is small (one host round trip less for it; YIELD DISTINCT compacts the rows
+  // after this point, so it fetches them the usual way)
+  if (he == hipSuccess && !part && !st->distinct && ncols > 0) {
+    SmallPack sp{};
+    sp.ntypes = (int)over.size();
+    sp.ncols = ncols;
+    for (size_t i = 0; i < over.size(); ++i) {
+      sp.region[i] = region[i];
+      sp.blk_cap[i] = blk_cap[i];
+      sp.grid[i] = ws_final_grid_of(ws, (int)i);
+    }
+    he = ws_end_query_async_small(ws, sp);
+  } else if (he == hipSuccess) {
+    he = ws_end_query_async(ws);
+  }
   if (he != hipSuccess) {
     // the peers may already wait in this query's next collective: release them
     if (part) qcomm->abort();
@@ -1158,6 +1178,7 @@ static int32_t go_collect(Engine& E, const nbg_go_stmt* st, GoPending* p, nbg_ro
     }
   }
   for (int c = 0; c < ncols; ++c) rows->dcols.push_back(ws_row_col(ws, c));
+  rows->small_ok = !E.partitioned() && !st->distinct;   // (go_launch packed a small result)
   if (!device) {
     int32_t rc = materialize_rows(rows);
     if (rc) {

@@ -116,6 +116,8 @@ struct Workspace {
   QState* q = nullptr;            // device query state
   QState* h_q = nullptr;          // pinned host mirror (mapped: k_q_out stores into it)
   QState* d_hq = nullptr;         // its device address
+  int64_t* h_small = nullptr;     // mapped pinned: [0] = rows + 1 when packed, then the cells
+  int64_t* d_small = nullptr;     // its device address
   uint32_t* h_starts = nullptr;   // pinned staging for start ids
   uint64_t cap_starts = 0;
   Ins* h_prog = nullptr;          // pinned staging for programs
@@ -1666,6 +1668,10 @@ Workspace* ws_create(uint64_t max_frontier, uint64_t nv, uint64_t e_max, hipStre
     e = hipHostMalloc((void**)&w->h_q, sizeof(QState) + (size_t)MAX_TYPES_Q * EXPAND_GRID * 4,
                       hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&w->d_hq, w->h_q, 0);
+  if (e == hipSuccess)
+    e = hipHostMalloc((void**)&w->h_small, (SMALL_ROWS_WORDS + 1) * 8, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&w->d_small, w->h_small, 0);
+  if (e == hipSuccess) w->h_small[0] = 0;
   if (e == hipSuccess) {
     w->blk_rows = reinterpret_cast<uint32_t*>(w->q + 1);
     w->h_blk_rows = reinterpret_cast<uint32_t*>(w->h_q + 1);
@@ -1695,7 +1701,7 @@ void ws_destroy(Workspace* w) {
                   (void*)w->xcnt, (void*)w->xsend, (void*)w->xrecv, (void*)w->bt_out, (void*)w->bt_recv})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)w->h_q, (void*)w->h_starts, (void*)w->h_prog, (void*)w->h_ps, (void*)w->h_path,
-                  (void*)w->h_stage})
+                  (void*)w->h_stage, (void*)w->h_small})
     if (p) (void)hipHostFree(p);
   if (w->h_pgst) (void)hipHostFree(w->h_pgst);
   if (w->done_ev) (void)hipEventDestroy(w->done_ev);
@@ -2489,6 +2495,8 @@ hipError_t ws_end_query_async(Workspace* w) {
   hipLaunchKernelGGL(k_q_out, dim3(1), dim3(BLOCK), 0, w->stream, reinterpret_cast<const unsigned long long*>(w->q),
                      reinterpret_cast<unsigned long long*>(w->d_hq), (uint32_t)(bytes / 8));
   HIP_TRY(hipGetLastError());
+  if (w->h_small) w->h_small[0] = 0;   // (this query's rows are not packed: the device does not run
+                                       // ahead of this host write, the stream is idle on this slot)
   if (!w->done_ev) HIP_TRY(hipEventCreateWithFlags(&w->done_ev, hipEventDisableTiming));
   return hipEventRecord(w->done_ev, w->stream);
 }
@@ -2509,6 +2517,59 @@ hipError_t ws_end_query_wait(Workspace* w) {
   HIP_TRY(hipMemsetAsync(w->q, 0, sizeof(QState), w->stream));
   prof_flush(w, w->h_q);
   return hipSuccess;
+}
+
+// k_q_out, then (one workgroup) the result's rows into the mapped small-rows buffer when they fit:
+// segment (type t, block b) = rows [region_t + b * blk_cap_t, + count) of every column, packed in
+// (t, b) order at column-major offsets, as nbg_rows / ws_fetch_rows lay them out.
+__global__ void __launch_bounds__(BLOCK) k_q_out_small(const unsigned long long* __restrict__ src, unsigned long long* dst,
+                                                       uint32_t n8, const uint32_t* __restrict__ blk_rows, SmallPack sp,
+                                                       int64_t* const* __restrict__ cols, int64_t* small) {
+  for (uint32_t i = threadIdx.x; i < n8; i += BLOCK) dst[i] = src[i];
+  __shared__ unsigned long long s_total;
+  if (threadIdx.x == 0) s_total = 0;
+  __syncthreads();
+  unsigned long long part = 0;
+  for (int t = 0; t < sp.ntypes; ++t)
+    for (uint32_t b = threadIdx.x; b < sp.grid[t]; b += BLOCK) part += blk_rows[(size_t)t * EXPAND_GRID + b];
+  atomicAdd(&s_total, part);
+  __syncthreads();
+  const unsigned long long total = s_total;
+  if (total * (unsigned long long)sp.ncols > SMALL_ROWS_WORDS) {
+    if (threadIdx.x == 0) small[0] = 0;
+    return;
+  }
+  uint64_t off = 0;
+  for (int t = 0; t < sp.ntypes; ++t)
+    for (uint32_t b = 0; b < sp.grid[t]; ++b) {
+      const uint32_t n = blk_rows[(size_t)t * EXPAND_GRID + b];
+      if (!n) continue;
+      const uint64_t base = sp.region[t] + (uint64_t)b * sp.blk_cap[t];
+      for (int c = 0; c < sp.ncols; ++c)
+        for (uint32_t i = threadIdx.x; i < n; i += BLOCK) small[1 + (uint64_t)c * total + off + i] = cols[c][base + i];
+      off += n;
+    }
+  __syncthreads();
+  if (threadIdx.x == 0) small[0] = (int64_t)total + 1;
+}
+
+hipError_t ws_end_query_async_small(Workspace* w, const SmallPack& sp) {
+  if (sp.ntypes > MAX_TYPES_Q || sp.ncols > MAX_YIELDS) return hipErrorInvalidValue;
+  int nt = 0;
+  for (int t = 0; t < MAX_TYPES_Q; ++t)
+    if (w->final_grid[t]) nt = t + 1;
+  const size_t bytes = sizeof(QState) + (size_t)nt * EXPAND_GRID * 4;
+  hipLaunchKernelGGL(k_q_out_small, dim3(1), dim3(BLOCK), 0, w->stream, reinterpret_cast<const unsigned long long*>(w->q),
+                     reinterpret_cast<unsigned long long*>(w->d_hq), (uint32_t)(bytes / 8), w->blk_rows, sp,
+                     (int64_t* const*)w->d_row_cols, w->d_small);
+  HIP_TRY(hipGetLastError());
+  if (!w->done_ev) HIP_TRY(hipEventCreateWithFlags(&w->done_ev, hipEventDisableTiming));
+  return hipEventRecord(w->done_ev, w->stream);
+}
+
+const int64_t* ws_host_small_rows(Workspace* w, uint64_t count) {
+  if (!w->h_small || w->h_small[0] != (int64_t)count + 1) return nullptr;
+  return w->h_small + 1;
 }
 
 hipError_t ws_end_query(Workspace* w) {

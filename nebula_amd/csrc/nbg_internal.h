@@ -523,6 +523,19 @@ hipError_t ws_backtracker(Workspace* w, int64_t** out, int64_t** in);
 void ws_backtracker_off(Workspace* w);
 hipError_t ws_end_query(Workspace* w);
 hipError_t ws_end_query_async(Workspace* w);   // enqueue the end-of-query copy + event
+// ... and, for a result small enough (SMALL_ROWS_WORDS cells), its rows packed into host memory
+// by the same kernel (no second host round trip to fetch them): the final step's row segments per
+// OVER type, in the order nbg_rows lays them out
+struct SmallPack {
+  int ntypes, ncols;
+  uint64_t region[MAX_TYPES_Q], blk_cap[MAX_TYPES_Q];
+  uint32_t grid[MAX_TYPES_Q];
+};
+constexpr uint64_t SMALL_ROWS_WORDS = 32768;   // 256 KB of 8-byte cells
+hipError_t ws_end_query_async_small(Workspace* w, const SmallPack& sp);
+// the rows ws_end_query_async_small packed (column c at c * count), or nullptr when the last
+// query's result was not packed or has a count other than `count`
+const int64_t* ws_host_small_rows(Workspace* w, uint64_t count);
 hipError_t ws_end_query_wait(Workspace* w);    // wait for it (then as ws_end_query)
 // partitioned mode: flags over [world * npad) global ids, per-hop bitmap all-to-all
 constexpr uint64_t PART_ALIGN = 16384 * 4;   // npad granularity (flag / bit workgroups divide it)
