@@ -69,6 +69,34 @@ def test_rmat_go_parity(rmat12, steps, where):
     assert graphs.sorted_rows(got) == graphs.sorted_rows(exp)
 
 
+def test_small_results_packed_at_query_end(rmat12):
+    """Results of at most 32 k cells are packed into host memory by the end-of-query kernel (one
+    round trip), larger ones are fetched after it: rows from both sides of the bound equal the
+    oracle's, through nbg_go (host rows) and through a device result fetched later."""
+    src, eng, orc = rmat12
+    yields = [E.edge_prop("e", "_dst").encode(), E.edge_prop("e", "w").encode(),
+              E.edge_prop("e", "_src").encode()]
+    wb = WHERES["w<50"].encode()
+    small = big = 0
+    stmt = eng.prepare_go([1], 2, wb, yields)
+    try:
+        for r in graphs.roots(src, 24, seed=11):
+            exp = graphs.sorted_rows(orc.go([r], [1], 2, wb, yields))
+            assert graphs.sorted_rows(eng.go([r], [1], 2, wb, yields)) == exp, r
+            res = stmt.run_device([r])
+            try:
+                assert graphs.sorted_rows(res.fetch()) == exp, r
+            finally:
+                res.free()
+            if len(exp) * len(yields) <= 32768:
+                small += 1
+            else:
+                big += 1
+    finally:
+        stmt.free()
+    assert small and big, (small, big)
+
+
 def test_rmat_go_each_root(rmat12):
     """GO 3 STEPS with WHERE from 16 single roots (one query each), default YIELD."""
     src, eng, orc = rmat12
