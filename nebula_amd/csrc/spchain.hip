@@ -42,7 +42,10 @@ namespace {
 
 constexpr int CH_BLOCK = 256;
 constexpr int CH_WAVES = CH_BLOCK / 64;
-constexpr int CH_VT = 8;                  // merge-path items per lane per tile
+#ifndef NBG_CH_VT
+#define NBG_CH_VT 8
+#endif
+constexpr int CH_VT = NBG_CH_VT;          // merge-path items per lane per tile (NBG_CH_VT: an A/B build switch)
 constexpr int CH_TILE = 64 * CH_VT;       // items (entries + edges) per wave tile
 #ifndef NBG_CH_HOP_WGS
 #define NBG_CH_HOP_WGS 64
