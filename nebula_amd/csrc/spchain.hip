@@ -43,9 +43,13 @@ namespace {
 constexpr int CH_BLOCK = 256;
 constexpr int CH_WAVES = CH_BLOCK / 64;
 #ifndef NBG_CH_VT
-#define NBG_CH_VT 8
+#define NBG_CH_VT 4
 #endif
-constexpr int CH_VT = NBG_CH_VT;          // merge-path items per lane per tile (NBG_CH_VT: an A/B build switch)
+// merge-path items per lane per tile (NBG_CH_VT: an A/B build switch).  A level's critical path is
+// the slowest wave's chain of dependent accesses, so shorter tiles spread a level over more waves:
+// RMAT-26 10k pairs, p50 0.131 ms at 8, 0.110 at 4, 0.107 at 2, 0.103 at 1; 4 keeps p99 (0.25 vs
+// 0.27-0.34 ms) and the batched rate (36 k vs 30 k pairs/s at 1) (profiles/r03_vt2_sp_vt_ab.txt)
+constexpr int CH_VT = NBG_CH_VT;
 constexpr int CH_TILE = 64 * CH_VT;       // items (entries + edges) per wave tile
 #ifndef NBG_CH_HOP_WGS
 #define NBG_CH_HOP_WGS 64
