@@ -43,12 +43,13 @@ namespace {
 constexpr int CH_BLOCK = 256;
 constexpr int CH_WAVES = CH_BLOCK / 64;
 #ifndef NBG_CH_VT
-#define NBG_CH_VT 4
+#define NBG_CH_VT 2
 #endif
 // merge-path items per lane per tile (NBG_CH_VT: an A/B build switch).  A level's critical path is
 // the slowest wave's chain of dependent accesses, so shorter tiles spread a level over more waves:
-// RMAT-26 10k pairs, p50 0.131 ms at 8, 0.110 at 4, 0.107 at 2, 0.103 at 1; 4 keeps p99 (0.25 vs
-// 0.27-0.34 ms) and the batched rate (36 k vs 30 k pairs/s at 1) (profiles/r03_vt2_sp_vt_ab.txt)
+// RMAT-26 10k pairs, p50 0.131 ms at 8, 0.110 at 4, 0.107 at 2 (0.104 with a 256-workgroup step
+// grid), 0.103 at 1 but p99 0.30-0.34 ms and batched -17 % (profiles/r03_vt2_sp_vt_ab.txt,
+// r03_fin2_sp_vt2_batch_ab.txt)
 constexpr int CH_VT = NBG_CH_VT;
 constexpr int CH_TILE = 64 * CH_VT;       // items (entries + edges) per wave tile
 #ifndef NBG_CH_HOP_WGS
@@ -961,8 +962,10 @@ struct ChainCtx {
   // step launch grid: most levels are a few tiles, so the launch's own cost (workgroups to
   // dispatch, each reading the state snapshot first) dominates; RMAT-26 10k-pair sweep
   // (profiles/r02_x_sp_grid_sweep.json): p50 0.159 ms at 512, 0.151 at 256, 0.148 at 128 and 96,
-  // 0.154 at 32.  NBG_SP_GRID overrides.
-  unsigned grid = 128;
+  // 0.154 at 32.  With 2-item-per-lane tiles (more tiles per level) 256: 0.104-0.106 against
+  // 0.109-0.113 at 128 (profiles/r03_vt3_sp_grid_ab.txt, r03_fin2_sp_vt2_batch_ab.txt).
+  // NBG_SP_GRID overrides.
+  unsigned grid = 256;
   uint32_t solo = 0;               // ChQ::solo (NBG_SP_SOLO items)
   // the query in flight: what has been enqueued
   ChQ q{};
@@ -1141,7 +1144,9 @@ hipError_t chain_launch_batch(ChainCtx* const* cs, int n, const ChainQuery* qs) 
   memset(&b, 0, sizeof(b));
   b.n = n;
   static const unsigned per_env = getenv("NBG_SP_BATCH_WGS") ? (unsigned)atoi(getenv("NBG_SP_BATCH_WGS")) : 0u;
-  b.per = per_env ? per_env : std::max(32u, 1024u / (unsigned)n);
+  // (2048 workgroups for a full batch: 64 per pair at 32 pairs, 39.4-40.5 k pairs/s against
+  // 34.3-34.7 k at 32 per pair with 2-item tiles, profiles/r03_fin2_sp_vt2_batch_ab.txt)
+  b.per = per_env ? per_env : std::max(64u, 2048u / (unsigned)n);
   int k = 1, h = 1;
   for (int p = 0; p < n; ++p) {
     ChainCtx* c = cs[p];
