@@ -591,6 +591,7 @@ def main():
     # ---------------- verification + CPU baseline mode (ii): the CSR oracle on the same graph
     verify = None
     cpu_csr = None
+    part_load = None
     if (args.verify or not args.no_cpu_baseline) and world >= 1:
         try:
             from tests.support.oracle import CsrOracle, Y_DST
@@ -616,6 +617,7 @@ def main():
                       "method": "device nbg_rows_digest (rows, xor, sum of splitmix64 row chains; summed over ranks) "
                                 "and edges scanned vs oracle/csr.cpp on the same graph; SHORTEST paths compared "
                                 "entry by entry", "oracle_build_s": round(build_s, 1)}
+            part_load = partition_load(csr, roots, args)
             if not args.no_cpu_baseline and world == 1:
                 cpu_csr = csr_baseline(csr, roots, pairs, args, threads, model, ncpu)
             csr.close()
@@ -688,6 +690,7 @@ def main():
         "c5_substitute": c5,
         "getbound": getbound,
         "c1_nba": c1,
+        "partition_load": part_load,
         "gen_seconds": round(gen_s, 2),
         "load_seconds": round(load_s, 2),
     }
@@ -720,6 +723,30 @@ def c2_leg(args, barrier, inflight):
             "edges_per_step": g["scanned"] // args.steps, "query_latency_ms": {"p50": float(np.percentile(lat_ms, 50)),
                                                                              "p90": float(np.percentile(lat_ms, 90))},
             "roofline": roof, "kernels": kernels, "find_shortest_path": sp, "load_seconds": round(load_s, 2)}
+
+
+def partition_load(csr, roots, args, worlds=(2, 4, 8)):
+    """The strong-scaling ceiling the partition itself sets: for each G, the edges
+    every rank scans per step of the headline queries when rank r holds parts p % G == r
+    (CreateSpaceProcessor.cpp:84-95), from the CSR oracle on the same graph.  `ceiling_overlapped`
+    = total / busiest rank's total (queries in flight fill each other's gaps); `ceiling_lockstep`
+    = total / Σ over (query, step) of the busiest rank's edges (every hop waits for its slowest
+    rank)."""
+    out = {}
+    for G in worlds:
+        t = csr.rank_edges(roots, args.go_steps, args.parts, G).astype(np.float64)   # [q, s, G]
+        total = t.sum()
+        per_rank = t.sum(axis=(0, 1))
+        per_step = t.sum(axis=0)                       # [s, G]
+        out[f"G{G}"] = {
+            "rank_share": [round(x / total, 4) for x in per_rank],
+            "step_max_over_mean": [round(float(r.max() / r.mean()), 3) if r.sum() else None for r in per_step],
+            "ceiling_overlapped": round(float(total / per_rank.max()), 3),
+            "ceiling_lockstep": round(float(total / t.max(axis=2).sum()), 3),
+        }
+    out["method"] = ("oracle/csr.cpp rank_edges: per (query, step, rank) edges scanned at the frontier vertex's "
+                     f"owner, {len(roots)} headline roots, P = {args.parts}")
+    return out
 
 
 def csr_baseline(csr, roots, pairs, args, threads, model, ncpu):

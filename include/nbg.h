@@ -437,8 +437,9 @@ int32_t nbg_comm_init_local(nbg_engine* const* engines, int32_t n);
  *     edges exceed one rank's list limit, ...) reaches every rank: every rank returns the code of
  *     the lowest-ranked rank that failed, and the engines stay usable.  For GO without YIELD
  *     DISTINCT and without $- / $var inputs the failing rank still takes part in the query's
- *     collectives and its status travels with the query's statistics (no extra round trip): its
- *     own nbg_go_submit fails, its peers' nbg_go_wait returns the code.  Other statements (and
+ *     collectives and its status travels with the query's statistics (no extra round trip):
+ *     nbg_go_execute fails on every rank; nbg_go_submit returns a ticket on every rank (so every
+ *     rank's query slots stay in step) and nbg_go_wait on it returns the code.  Other statements (and
  *     FIND PATH) agree in one small all-reduce before the query, so every rank's call fails;
  *   - a failure between collectives (a device error on one rank) aborts the communicator; the
  *     peers' pending collectives fail (in-process group at once, RCCL when their bounded wait of
@@ -453,6 +454,7 @@ int32_t nbg_comm_aborted(const nbg_engine* e);
  * there would (the failure paths above are otherwise hard to reach on purpose). */
 #define NBG_FAULT_ALLOC  1   /* the query's workspace / held-result hand-over allocation fails */
 #define NBG_FAULT_DEVICE 2   /* partitioned GO: a device error after the query's first collective */
+#define NBG_FAULT_STREAM 3   /* nbg_go_submit: the query slot's stream cannot be created */
 int32_t nbg_inject_fault(nbg_engine* e, int32_t site, int32_t count);
 /* The edge records this engine staged for signed edge type `type` (+t: out-edges keyed at src,
  * -t: in-edges keyed at dst), in load order, before nbg_finalize: a partitioned rank keeps the

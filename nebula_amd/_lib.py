@@ -31,6 +31,7 @@ E_STATE = -1005
 FAULT_ALLOC = 1      # nbg_inject_fault sites (include/nbg.h)
 V_INT, V_DOUBLE, V_BOOL, V_STRING = 0, 1, 2, 3   # NBG_V_* value kinds
 FAULT_DEVICE = 2
+FAULT_STREAM = 3
 
 
 class nbg_config(C.Structure):

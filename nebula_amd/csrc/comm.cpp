@@ -45,8 +45,8 @@ Comm::~Comm() {
 
 bool Comm::agree_ready(std::string* err) {
   if (agree_dev) return true;
-  if (hipMalloc((void**)&agree_dev, AGREE_WORDS * 8) != hipSuccess ||
-      hipHostMalloc((void**)&agree_host, AGREE_WORDS * 8, hipHostMallocDefault) != hipSuccess) {
+  if (hipMalloc((void**)&agree_dev, GATHER_WORDS * 8) != hipSuccess ||
+      hipHostMalloc((void**)&agree_host, GATHER_WORDS * 8, hipHostMallocDefault) != hipSuccess) {
     if (err) *err = "communicator scratch allocation failed";
     return false;
   }
@@ -108,6 +108,31 @@ int Comm::agree(hipStream_t s, int32_t local, int32_t* out) {
       *out = (int32_t)(int64_t)agree_host[q];
       break;
     }
+  return 0;
+}
+
+int Comm::gather_u64(hipStream_t s, const uint64_t* mine, size_t k, std::vector<uint64_t>* out) {
+  const size_t n = (size_t)world * k;
+  if (aborted) {
+    last = "communicator aborted by an earlier failure";
+    return -1;
+  }
+  if (!agree_dev || n > GATHER_WORDS) {   // (the same on every rank: nobody enters the exchange)
+    last = "gather scratch missing or too small";
+    return -1;
+  }
+  memset(agree_host, 0, n * 8);
+  for (size_t i = 0; i < k; ++i) agree_host[(size_t)rank * k + i] = mine[i];
+  int rc = hipMemcpyAsync(agree_dev, agree_host, n * 8, hipMemcpyHostToDevice, s) == hipSuccess ? 0 : -1;
+  if (!rc) rc = allreduce_sum_u64(agree_dev, n, s);
+  if (!rc) rc = hipMemcpyAsync(agree_host, agree_dev, n * 8, hipMemcpyDeviceToHost, s) == hipSuccess ? 0 : -1;
+  if (!rc) rc = wait(s);
+  if (rc) {
+    if (last.empty()) last = "gather exchange failed";
+    abort();
+    return -1;
+  }
+  out->assign(agree_host, agree_host + n);
   return 0;
 }
 

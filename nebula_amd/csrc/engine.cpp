@@ -44,9 +44,59 @@ void Engine::free_snapshot() {
     for (auto* p : kv.second.cols)
       if (p) (void)hipFree(p);
   }
-  for (void* p : {(void*)snap.d_tcols, (void*)snap.d_tpres, (void*)snap.d_vids, (void*)snap.d_visible})
+  for (void* p : {(void*)snap.d_tcols, (void*)snap.d_tpres, (void*)snap.d_vids, (void*)snap.d_visible,
+                  (void*)snap.d_soff, (void*)snap.d_sbytes, (void*)snap.d_s2i, (void*)snap.d_s2f, (void*)snap.d_s2ok})
     if (p) (void)hipFree(p);
   snap = Snapshot();
+}
+
+// The dictionary's device tables: its bytes (piece lists of derived strings read them) and what
+// Expression::toInt / toDouble make of every string (Expressions.h:294-321; a string that is not
+// a whole number fails the cast, as the host's constant folding and the oracle decide it).
+int32_t Engine::upload_strings() {
+  const auto& d = snap.strings;
+  if (d.empty()) return NBG_OK;
+  const size_t n = d.size();
+  std::vector<uint32_t> off(n + 1, 0);
+  for (size_t i = 0; i < n; ++i) {
+    if ((uint64_t)off[i] + d[i].size() > 0xFFFFFFFFull) return fail(NBG_E_UNSUPPORTED, "string dictionary over 4 GB");
+    off[i + 1] = off[i] + (uint32_t)d[i].size();
+  }
+  std::vector<char> bytes(std::max<size_t>(off[n], 1));
+  std::vector<int64_t> s2i(n), s2f(n);
+  std::vector<uint8_t> ok(n);
+  for (size_t i = 0; i < n; ++i) {
+    memcpy(bytes.data() + off[i], d[i].data(), d[i].size());
+    CVal vi, vf;
+    uint8_t b = 0;
+    if (evalCast(0, CVal(d[i]), &vi)) { s2i[i] = std::get<int64_t>(vi); b |= 1; }
+    if (evalCast(2, CVal(d[i]), &vf)) { const double x = std::get<double>(vf); memcpy(&s2f[i], &x, 8); b |= 2; }
+    ok[i] = b;
+  }
+  hipError_t e = hipMalloc((void**)&snap.d_soff, (n + 1) * 4);
+  if (e == hipSuccess) e = hipMalloc((void**)&snap.d_sbytes, bytes.size());
+  if (e == hipSuccess) e = hipMalloc((void**)&snap.d_s2i, n * 8);
+  if (e == hipSuccess) e = hipMalloc((void**)&snap.d_s2f, n * 8);
+  if (e == hipSuccess) e = hipMalloc((void**)&snap.d_s2ok, n);
+  if (e == hipSuccess) e = hipMemcpy(snap.d_soff, off.data(), (n + 1) * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(snap.d_sbytes, bytes.data(), bytes.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(snap.d_s2i, s2i.data(), n * 8, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(snap.d_s2f, s2f.data(), n * 8, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(snap.d_s2ok, ok.data(), n, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return fail(NBG_E_OUT_OF_MEMORY, std::string("string tables: ") + hipGetErrorString(e));
+  snap.device_bytes += (n + 1) * 4 + bytes.size() + n * 17;
+  return NBG_OK;
+}
+
+DevStrings Engine::dev_strings() const {
+  DevStrings s;
+  s.off = snap.d_soff;
+  s.bytes = snap.d_sbytes;
+  s.s2i = snap.d_s2i;
+  s.s2f = snap.d_s2f;
+  s.s2ok = snap.d_s2ok;
+  s.n = snap.strings.size();
+  return s;
 }
 
 uint64_t Engine::sp_item_cap() const {
@@ -101,6 +151,7 @@ struct nbg_rows {
   size_t hbytes = 0;
   std::vector<std::vector<uint8_t>> tags;   // per-cell kinds, built on the first nbg_rows_col_tags
   std::vector<std::string> strings;
+  std::unordered_map<int64_t, std::string> derived;   // STR_DERIVED codes -> their text
   std::vector<Seg> segs;                 // built on first use from the per-workgroup counts
   struct TypeBlocks {
     uint64_t region = 0, blk_cap = 0;
@@ -358,8 +409,15 @@ int32_t materialize_rows(nbg_rows* r) {
           const int64_t code = col[i];
           auto it = sidx.find(code);
           if (it == sidx.end()) {
-            std::string txt = (code >= 0 && (code & 1) == 0 && (uint64_t)(code / 2) < dict.size())
-                                  ? dict[code / 2] : r->const_str[s.type][c];
+            std::string txt;
+            if (is_derived_code(code)) {
+              auto d = r->derived.find(code);
+              if (d == r->derived.end()) return E.fail(NBG_E_DEVICE, "a derived string's text is missing");
+              txt = d->second;
+            } else {
+              txt = (code >= 0 && (code & 1) == 0 && (uint64_t)(code / 2) < dict.size()) ? dict[code / 2]
+                                                                                          : r->const_str[s.type][c];
+            }
             it = sidx.emplace(code, (int64_t)r->strings.size()).first;
             r->strings.push_back(txt);
           }
@@ -414,6 +472,8 @@ struct nbg_go_stmt {
   bool misaligned = false, float_col = false;
   // $- / $var input: index rows (the FROM vid, ascending; last row per vid) and their columns,
   // uploaded on first execution (the same index on every rank of a partitioned engine)
+  bool derived = false;              // some YIELD stores derived strings (OP_SOUT: the string arena)
+  uint64_t arena_bytes = 0;          // the arena a query reserves
   bool uses_input = false;
   std::vector<int64_t> in_ids;
   std::vector<std::vector<int64_t>> in_cols;
@@ -633,7 +693,7 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
     }
     for (int y = 0; rc == NBG_OK && y < ncols; ++y) {
       Compiled c;
-      rc = compile_expr(*yields[y], env, pb, &c, &err);
+      rc = compile_expr(*yields[y], env, pb, &c, &err, true);
       if (rc) break;
       tp.yield_kind.push_back(c.kind);
       if (c.is_const) {
@@ -652,9 +712,11 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
       continue;
     }
     tp.code = pb.code;
+    tp.data = pb.data;
+    for (const Ins& i : tp.code) tp.sout = tp.sout || i.op == OP_SOUT;
     tp.probe_mask = probe;
     tp.nregs = std::max(1, pb.max_reg);
-    if ((int)tp.code.size() > MAX_PROGRAM) return E.fail(NBG_E_UNSUPPORTED, "program too long");
+    if ((int)(tp.code.size() + tp.data.size()) > MAX_PROGRAM) return E.fail(NBG_E_UNSUPPORTED, "program too long");
     progs[t] = std::move(tp);
   }
   if ((int)over.size() > MAX_TYPES_Q || rq->steps > (uint32_t)MAX_STEPS)
@@ -719,8 +781,23 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
       }
     }
   }
+  // Derived strings (concatenation, casts to string): a YIELD column's string has ONE code
+  // whatever produced it — the dictionary's, else STR_DERIVED | its content hash — so constant
+  // strings absent from the dictionary take the hash code too (YIELD DISTINCT compares codes).
+  bool derived = false;
+  for (auto& kv : progs) derived = derived || kv.second.sout;
+  if (derived)
+    for (auto& kv : progs)
+      for (int y = 0; y < ncols; ++y) {
+        TypeProgram& tp = kv.second;
+        if (tp.yield_reg[y] >= 0 || tp.yield_kind[y] != VK_STRING || !(tp.yield_const[y] & 1)) continue;
+        uint64_t h = STR_HASH_INIT;
+        for (char ch : tp.yield_const_str[y]) h = str_hash_step(h, (uint8_t)ch);
+        tp.yield_const[y] = str_derived_code(h, tp.yield_const_str[y].size());
+      }
   static std::atomic<uint64_t> next_id{1};
   auto* st = new nbg_go_stmt();
+  st->derived = derived;
   st->eng = &E;
   st->id = next_id++;
   st->over = over;
@@ -752,6 +829,11 @@ struct GoPending {
   Workspace* ws = nullptr;
   bool device = false;
   bool finished = false;                 // nothing was enqueued (no start has rows)
+  // partitioned, in band: this rank's preparation failed but it took part in the query's
+  // collectives; nbg_go_submit keeps the ticket in its slot (so every rank's slot sequence stays
+  // the same) and nbg_go_wait reports the code
+  int32_t failed_rc = NBG_OK;
+  std::string failed_msg;
   std::vector<uint64_t> region, blk_cap;
 };
 
@@ -764,8 +846,12 @@ struct GoPending {
 // row buffers — happens BEFORE the query's first collective and is agreed there (Comm::agree,
 // one small all-reduce): either every rank enqueues the query or every rank returns the same
 // code.  A device error after that point aborts the communicator (the peers' collectives fail).
+// pre_rc: a failure the caller already had on this rank (nbg_go_submit's slot stream); it is
+// reported through the same agreement as the preparation failures below, so the peers' collective
+// sequence for the query still matches.
 static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts, uint64_t num_starts, bool device,
-                         Workspace** wsp, hipStream_t stream, Comm* qcomm, GoPending* p) {
+                         Workspace** wsp, hipStream_t stream, Comm* qcomm, GoPending* p, int32_t pre_rc = NBG_OK,
+                         const char* pre_msg = nullptr) {
   if (num_starts && !starts) return E.fail(NBG_E_INVALID_ARGUMENT, "null argument");
   if (hipSetDevice(E.cfg.device) != hipSuccess) return E.fail(NBG_E_DEVICE, "hipSetDevice failed");
   const bool part = E.partitioned();
@@ -804,6 +890,7 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
   auto local_fail = [&](int32_t code, const std::string& msg) {
     if (!lrc) { lrc = code; lmsg = msg; }
   };
+  if (pre_rc) local_fail(pre_rc, pre_msg ? pre_msg : "query set-up failed");
   if (E.fault(NBG_FAULT_ALLOC)) local_fail(NBG_E_OUT_OF_MEMORY, "query workspace allocation failed (injected)");
   const uint32_t cap = (uint32_t)(E.cfg.max_edge_returned_per_vertex <= 0 ? 0x7fffffff
                                                                           : E.cfg.max_edge_returned_per_vertex);
@@ -902,6 +989,7 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
     a.gbase = E.partitioned() ? (uint32_t)((uint64_t)E.cfg.rank * E.npad) : 0u;
     a.bt = bt;
     a.bt_in = bt_in;
+    a.str = E.dev_strings();
     if (st->uses_input) {
       a.in_ids = st->d_in_ids;
       a.in_n = st->in_ids.size();
@@ -930,6 +1018,15 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
     cap_rows += blk_cap[i] * ws_final_grid(n_final, eb);
   }
   if (!lrc && ws_reserve_rows(ws, cap_rows, ncols) != hipSuccess) local_fail(NBG_E_OUT_OF_MEMORY, "result rows");
+  if (!lrc && st->derived) {
+    // derived strings: 32 bytes per row and column (an entry's 16-byte header + 16 bytes) up to
+    // NBG_STR_ARENA_KB (default 2 GB); a query that needs more fails with E_OUT_OF_MEMORY
+    static const uint64_t cap_kb =
+        getenv("NBG_STR_ARENA_KB") ? strtoull(getenv("NBG_STR_ARENA_KB"), nullptr, 10) : (2ull << 20);
+    const uint64_t want = std::min<uint64_t>(std::max<uint64_t>(cap_rows * (uint64_t)ncols * 32, 1ull << 20),
+                                             std::max<uint64_t>(cap_kb, 1) << 10);
+    if (ws_reserve_arena(ws, want) != hipSuccess) local_fail(NBG_E_OUT_OF_MEMORY, "derived-string arena");
+  }
   // ---- agreement: the query runs on every rank or on none.  A statement whose only collectives
   // are the hop bitmaps and the statistics (no YIELD DISTINCT owner exchange, no $- / $var roots)
   // needs no host round trip for it: a rank whose preparation failed still takes part in those
@@ -946,6 +1043,9 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
         qcomm->abort();
         return E.fail(NBG_E_DEVICE, "query statistics exchange: " + qcomm->last);
       }
+      p->finished = true;
+      p->failed_rc = lrc;
+      p->failed_msg = lmsg;
       return E.fail(lrc, lmsg);
     }
   } else if (part) {
@@ -1051,9 +1151,78 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
 }
 
 // Wait for a launched query and build its result.
+// The text of every derived-string code in a result (nbg_rows::derived): the arena entries the
+// query's OP_SOUT stored, and the statement's constants that carry the hash code.  Partitioned
+// with YIELD DISTINCT, rows have moved between ranks, so every rank's entries are all-gathered
+// (each rank runs this for the same query, in submission order).
+static int32_t derived_strings(Engine& E, const nbg_go_stmt* st, Workspace* ws, uint64_t used, bool gather,
+                               nbg_rows* rows) {
+  std::vector<char> buf;
+  std::vector<std::pair<uint64_t, uint64_t>> parts;   // (offset, bytes) per rank in buf
+  if (!gather) {
+    if (ws_read_arena(ws, used, &buf) != hipSuccess) return E.fail(NBG_E_DEVICE, "derived-string arena read");
+    parts.emplace_back(0, used);
+  } else {
+    Comm* cm = ws_get_comm(ws);
+    hipStream_t s = ws_stream(ws);
+    std::vector<uint64_t> sizes;
+    const uint64_t u = used;
+    if (cm->gather_u64(s, &u, 1, &sizes)) return E.fail(NBG_E_DEVICE, "derived strings: " + cm->last);
+    uint64_t mx = 8;
+    for (uint64_t x : sizes) mx = std::max(mx, x);
+    uint64_t cap = 0;
+    const char* arena = ws_arena(ws, &cap);
+    char *send = nullptr, *recv = nullptr;
+    bool ok = hipMalloc((void**)&recv, mx * sizes.size()) == hipSuccess;
+    if (ok && cap < mx) ok = hipMalloc((void**)&send, mx) == hipSuccess &&
+                             (!used || hipMemcpyAsync(send, arena, used, hipMemcpyDeviceToDevice, s) == hipSuccess);
+    // (a rank that cannot allocate cannot take part: the communicator is aborted, as for any
+    // device failure between collectives)
+    ok = ok && cm->allgather(send ? send : arena, recv, mx, s) == 0;
+    buf.resize(mx * sizes.size());
+    ok = ok && hipMemcpyAsync(buf.data(), recv, buf.size(), hipMemcpyDeviceToHost, s) == hipSuccess &&
+         hipStreamSynchronize(s) == hipSuccess;
+    if (send) (void)hipFree(send);
+    if (recv) (void)hipFree(recv);
+    if (!ok) {
+      cm->abort();
+      return E.fail(NBG_E_DEVICE, "derived strings all-gather");
+    }
+    for (size_t q = 0; q < sizes.size(); ++q) parts.emplace_back(q * mx, sizes[q]);
+  }
+  auto add = [&](int64_t code, std::string text) {
+    auto it = rows->derived.find(code);
+    if (it == rows->derived.end()) rows->derived.emplace(code, std::move(text));
+    else if (it->second != text) return false;   // two strings with one 62-bit hash
+    return true;
+  };
+  for (auto& pr : parts) {
+    for (uint64_t o = pr.first; o + 16 <= pr.first + pr.second;) {
+      int64_t code;
+      uint64_t len;
+      memcpy(&code, buf.data() + o, 8);
+      memcpy(&len, buf.data() + o + 8, 8);
+      if (o + 16 + len > pr.first + pr.second) return E.fail(NBG_E_DEVICE, "derived-string arena entry");
+      if (!add(code, std::string(buf.data() + o + 16, len)))
+        return E.fail(NBG_E_EXECUTION_ERROR, "derived-string hash collision");
+      o += 16 + ((len + 7) & ~7ull);
+    }
+  }
+  for (const TypeProgram& tp : st->plist)
+    for (size_t y = 0; y < tp.yield_const.size(); ++y)
+      if (tp.yield_reg[y] < 0 && tp.yield_kind[y] == VK_STRING && is_derived_code(tp.yield_const[y]) &&
+          !add(tp.yield_const[y], tp.yield_const_str[y]))
+        return E.fail(NBG_E_EXECUTION_ERROR, "derived-string hash collision");
+  return NBG_OK;
+}
+
 static int32_t go_collect(Engine& E, const nbg_go_stmt* st, GoPending* p, nbg_rows** out) {
   nbg_rows* rows = p->rows;
   p->rows = nullptr;
+  if (p->failed_rc) {
+    delete rows;
+    return E.fail(p->failed_rc, p->failed_msg);
+  }
   if (p->finished) { *out = rows; return NBG_OK; }
   Workspace* ws = p->ws;
   const std::vector<int32_t>& over = st->over;
@@ -1098,6 +1267,10 @@ static int32_t go_collect(Engine& E, const nbg_go_stmt* st, GoPending* p, nbg_ro
   if (reached_final && g_e[steps] > 0 && !st->dst_unknown.empty()) {
     delete rows;
     return E.fail(NBG_E_EXECUTION_ERROR, st->dst_unknown);
+  }
+  if (g_err >= ARENA_OVERFLOW) {
+    delete rows;
+    return E.fail(NBG_E_OUT_OF_MEMORY, "the derived strings of the result exceed the string arena (NBG_STR_ARENA_KB)");
   }
   if (g_err) { delete rows; return E.fail(NBG_E_EXECUTION_ERROR, "WHERE/YIELD evaluation error"); }
   // a $$ default read for a tag no final destination has: VertexHolder::defaultFor fails
@@ -1175,6 +1348,13 @@ static int32_t go_collect(Engine& E, const nbg_go_stmt* st, GoPending* p, nbg_ro
     if (de != hipSuccess) {
       delete rows;
       return E.fail(NBG_E_DEVICE, std::string("HIP (distinct): ") + hipGetErrorString(de));
+    }
+  }
+  if (st->derived) {
+    const int32_t rc = derived_strings(E, st, ws, q.arena_used, E.partitioned() && st->distinct, rows);
+    if (rc) {
+      delete rows;
+      return rc;
     }
   }
   for (int c = 0; c < ncols; ++c) rows->dcols.push_back(ws_row_col(ws, c));
@@ -1274,6 +1454,7 @@ int32_t nbg::ws_release(Engine& E, Workspace** wsp, hipStream_t stream) {
 
 // The query workspace of a finalized (or snapshot-loaded) engine.
 int32_t nbg::engine_ready(Engine& E) {
+  if (int32_t rc = E.upload_strings()) return rc;
   std::string err;
   E.ws = ws_create(E.snap.nv + 1024, E.snap.nv, E.snap.max_edges(), E.stream, &err);
   if (!E.ws) return E.fail(NBG_E_OUT_OF_MEMORY, err);
@@ -1336,20 +1517,28 @@ int32_t nbg_go_submit(nbg_go_stmt* st, const int64_t* starts, uint64_t num_start
   const bool own_stream = !E.partitioned() || q.comm != nullptr;
   Comm* const qcomm = q.comm ? q.comm.get() : E.comm.get();
   hipStream_t qstream = own_stream ? q.stream : E.stream;
-  if (own_stream && !q.stream) {
-    if (hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking) != hipSuccess) {
+  int32_t pre_rc = NBG_OK;
+  const bool stream_fault = own_stream && E.fault(NBG_FAULT_STREAM);
+  if (own_stream && (!q.stream || stream_fault)) {
+    if (stream_fault || hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking) != hipSuccess) {
+      if (!stream_fault) q.stream = nullptr;
       if (!E.partitioned()) return E.fail(NBG_E_DEVICE, "hipStreamCreate failed");
-      int32_t agreed = NBG_OK;   // the peers are about to agree on this query: fail it with them
-      (void)qcomm->agree(E.stream, NBG_E_DEVICE, &agreed);
-      return E.fail(NBG_E_DEVICE, "hipStreamCreate failed");
+      // the peers run this query's collectives (in band or an agreement, per statement): fail it
+      // with them through go_launch, on the engine's stream
+      pre_rc = NBG_E_DEVICE;
+      qstream = E.stream;
+    } else {
+      qstream = q.stream;
     }
-    qstream = q.stream;
   }
   auto* t = new nbg_go_ticket();
   t->st = st;
   t->slot = slot;
-  int32_t rc = go_launch(E, st, starts, num_starts, device != 0, &q.ws, qstream, qcomm, &t->p);
-  if (rc) { delete t; return rc; }
+  int32_t rc = go_launch(E, st, starts, num_starts, device != 0, &q.ws, qstream, qcomm, &t->p, pre_rc,
+                         "hipStreamCreate failed");
+  // an in-band failure keeps its slot like any submitted query (the peers' slot holds theirs);
+  // nbg_go_wait returns the code
+  if (rc && !t->p.failed_rc) { delete t; return rc; }
   q.ticket = t;
   E.inflight.push_back(t);
   *out = t;

@@ -1,5 +1,6 @@
 // Engine object behind the C ABI.
 #pragma once
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -82,8 +83,11 @@ struct Engine {
   unsigned long long* fb_gst = nullptr;
   unsigned long long* fb_hgst = nullptr;
   int path_replica_mode = -1;   // build it at finalize: 1 yes (when it fits), 0 no, -1 NBG_PATH_REPLICA (default 1)
-  bool path_replica_use = true; // nbg_set_path_replica after finalize: 0 = the collective search
-  Engine* path_engine() { return rep && path_replica_use ? rep.get() : this; }
+  std::atomic<bool> path_replica_use{true};   // nbg_set_path_replica after finalize: 0 = the collective search
+  Engine* path_engine() { return rep && path_replica_use.load() ? rep.get() : this; }
+  // the replica's failures are reported through its parent's nbg_last_error too
+  Engine* err_parent = nullptr;
+  std::mutex err_mu;
 
   // nbg_inject_fault (tests): the next fault_count queries fail at fault_site
   int fault_site = 0, fault_count = 0;
@@ -93,7 +97,14 @@ struct Engine {
     return true;
   }
   int32_t fail(int32_t code, const std::string& msg) {
-    last_error = msg;
+    {
+      std::lock_guard<std::mutex> lg(err_mu);
+      last_error = msg;
+    }
+    if (err_parent) {
+      std::lock_guard<std::mutex> lg(err_parent->err_mu);
+      err_parent->last_error = msg;
+    }
     return code;
   }
   int64_t intern(const std::string& s);
@@ -121,6 +132,8 @@ struct Engine {
                               std::vector<uint64_t>* gcount);
   uint32_t dense(int64_t vid) const;
   void free_snapshot();   // release every device array of `snap` and reset it
+  int32_t upload_strings();         // the dictionary's device tables (engine_ready)
+  DevStrings dev_strings() const;   // ... as the kernels read them (no arena)
 };
 
 int32_t engine_ready(Engine& E);   // workspace (+ partition buffers) after finalize / snapshot load

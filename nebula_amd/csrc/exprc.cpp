@@ -164,7 +164,7 @@ bool evalUnary(uint8_t op, const CVal& v, CVal* out) {      // Expressions.cpp:6
   return true;
 }
 
-bool evalCast(uint8_t ct, const CVal& v, CVal* out) {       // Expressions.cpp:773-793
+bool cast_value(uint8_t ct, const CVal& v, CVal* out) {     // Expressions.cpp:773-793
   switch (ct) {
     case 0: case 5:
       if (v.index() == 3) {
@@ -256,6 +256,8 @@ bool evalLogic(uint8_t op, const CVal& l, const CVal& r, CVal* out) {   // Expre
 
 }  // namespace
 
+bool evalCast(uint8_t ct, const CVal& v, CVal* out) { return cast_value(ct, v, out); }
+
 bool fold_constant(const Node& e, CVal* out, bool* error) {
   *error = false;
   switch (e.kind) {
@@ -264,7 +266,7 @@ bool fold_constant(const Node& e, CVal* out, bool* error) {
       CVal v; bool er;
       if (!fold_constant(*e.kids[0], &v, &er)) return false;
       if (er) { *error = true; return true; }
-      bool ok = e.kind == EK_UNARY ? evalUnary(e.op, v, out) : evalCast(e.op, v, out);
+      bool ok = e.kind == EK_UNARY ? evalUnary(e.op, v, out) : cast_value(e.op, v, out);
       *error = !ok;
       return true;
     }
@@ -332,7 +334,68 @@ struct Ctx {
     emit(OP_CONST, c.reg, 0, 0, 0, c.const_bits);
     return c.reg;
   }
+  // ---- derived strings: piece lists in the program's data
+  std::vector<Piece> pieces_of(const Compiled& c) {
+    if (c.derived) return c.pieces;
+    if (c.is_const) return {Piece{PC_CONST, -1, c.const_str}};
+    return {Piece{PC_DICT, c.reg, {}}};
+  }
+  static int low_reg(const std::vector<Piece>& ps) {
+    int r = -1;
+    for (auto& p : ps)
+      if (p.reg >= 0 && (r < 0 || p.reg < r)) r = p.reg;
+    return r;
+  }
+  // header entry {d = pieces, aux = first piece}, the pieces {op = kind, d = reg, aux = byte offset
+  // of a constant's bytes from the data's start, imm = its length}, then the constants' bytes
+  int32_t emit_pieces(const std::vector<Piece>& ps) {
+    auto& D = pb.data;
+    const int32_t hdr = (int32_t)D.size();
+    D.push_back(Ins{0, (uint8_t)ps.size(), 0, 0, hdr + 1, 0});
+    for (auto& p : ps) D.push_back(Ins{(uint8_t)p.kind, (uint8_t)(p.reg < 0 ? 0 : p.reg), 0, 0, 0, (int64_t)p.text.size()});
+    for (size_t k = 0; k < ps.size(); ++k) {
+      if (ps[k].kind != PC_CONST || ps[k].text.empty()) continue;
+      const size_t at = D.size();
+      D[hdr + 1 + k].aux = (int32_t)(at * sizeof(Ins));
+      D.resize(at + (ps[k].text.size() + sizeof(Ins) - 1) / sizeof(Ins), Ins{});
+      memcpy(reinterpret_cast<char*>(D.data() + at), ps[k].text.data(), ps[k].text.size());
+    }
+    return hdr;
+  }
+  // the register a sink over these pieces writes (the lowest one they read: all are read first)
+  int sink_reg(const std::vector<Piece>& a, const std::vector<Piece>& b = {}) {
+    int r = low_reg(a), q = low_reg(b);
+    if (q >= 0 && (r < 0 || q < r)) r = q;
+    if (r < 0) r = push();
+    top = r + 1;
+    if (top > max_reg) max_reg = top;
+    return r;
+  }
+  Compiled derived_of(std::vector<Piece> ps) {
+    Compiled c;
+    c.kind = VK_STRING;
+    c.derived = true;
+    c.pieces = std::move(ps);
+    c.reg = low_reg(c.pieces);
+    return c;
+  }
+  // asBool of a derived string: empty() (Expressions.h:228-241)
+  int empty_reg(const Compiled& c) {
+    const int32_t h = emit_pieces(c.pieces);
+    const int r = sink_reg(c.pieces);
+    emit(OP_SEMPTY, r, 0, 0, h);
+    return r;
+  }
+  // a derived string as a result value: its canonical code (OP_SOUT)
+  int value_reg(const Compiled& c) {
+    const int32_t h = emit_pieces(c.pieces);
+    const int r = sink_reg(c.pieces);
+    emit(OP_SOUT, r, 0, 0, h);
+    return r;
+  }
+
   int truthy_reg(Compiled& c) {
+    if (c.derived) return empty_reg(c);
     int r = materialize(c);
     switch (c.kind) {
       case VK_INT: emit(OP_TRUTHY_I, r, r); break;
@@ -528,7 +591,7 @@ struct Ctx {
         *out = c;
         return NBG_OK;
       }
-      case EK_FUNC: *err = "function calls are not supported"; return NBG_E_UNSUPPORTED;
+      case EK_FUNC: return function(e, out);
       case EK_UNARY: {
         Compiled a;
         int32_t rc = compile(*e.kids[0], &a);
@@ -541,7 +604,7 @@ struct Ctx {
         }
         if (e.op == 0) { *out = a; return NBG_OK; }
         if (e.op == 1) {
-          if (a.kind == VK_INT || a.kind == VK_DOUBLE) {
+          if (!a.derived && (a.kind == VK_INT || a.kind == VK_DOUBLE)) {
             int r = materialize(a);
             emit(a.kind == VK_INT ? OP_NEG_I : OP_NEG_F, r, r);
             *out = a;
@@ -563,8 +626,34 @@ struct Ctx {
         if (a.always_error) { *out = a; return NBG_OK; }
         if (a.is_const) {
           CVal v;
-          *out = evalCast(e.op, a.cval, &v) ? make_const(v) : make_error();
+          *out = cast_value(e.op, a.cval, &v) ? make_const(v) : make_error();
           return NBG_OK;
+        }
+        if (a.derived) {   // a concatenation / cast result: parsed from its bytes
+          Compiled c;
+          switch (e.op) {
+            case 0: case 5: case 2: {
+              const int32_t h = emit_pieces(a.pieces);
+              c.reg = sink_reg(a.pieces);
+              c.kind = e.op == 2 ? VK_DOUBLE : VK_INT;
+              emit(e.op == 2 ? OP_SPARSE_F : OP_SPARSE_I, c.reg, 0, 0, h);
+              break;
+            }
+            case 4: c.reg = empty_reg(a); c.kind = VK_BOOL; break;
+            case 1: c = a; break;
+            default: *out = make_error(); return NBG_OK;
+          }
+          *out = c;
+          return NBG_OK;
+        }
+        if (e.op == 1) {   // to STRING (Expression::toString): a derived string of the value's text
+          switch (a.kind) {
+            case VK_STRING: *out = a; return NBG_OK;
+            case VK_INT: *out = derived_of({Piece{PC_INT, a.reg, {}}}); return NBG_OK;
+            case VK_BOOL: *out = derived_of({Piece{PC_BOOL, a.reg, {}}}); return NBG_OK;
+            // folly::to<std::string>(double) is not restated (unpinned, as for constants)
+            default: *out = make_error(); return NBG_OK;
+          }
         }
         Compiled c; c.reg = materialize(a);
         switch (e.op) {
@@ -572,22 +661,18 @@ struct Ctx {
             c.kind = VK_INT;
             if (a.kind == VK_DOUBLE) emit(OP_F2I, c.reg, c.reg);
             else if (a.kind == VK_BOOL) emit(OP_B2I, c.reg, c.reg);
-            else if (a.kind == VK_STRING) { *err = "string->int cast of a column"; return NBG_E_UNSUPPORTED; }
+            else if (a.kind == VK_STRING) emit(OP_S2I, c.reg, c.reg);   // per-string table
             break;
           case 2:
             c.kind = VK_DOUBLE;
             if (a.kind == VK_INT) emit(OP_I2F, c.reg, c.reg);
             else if (a.kind == VK_BOOL) emit(OP_B2F, c.reg, c.reg);
-            else if (a.kind == VK_STRING) { *err = "string->double cast of a column"; return NBG_E_UNSUPPORTED; }
+            else if (a.kind == VK_STRING) emit(OP_S2F, c.reg, c.reg);
             break;
           case 4:
             c.reg = truthy_reg(a);
             c.kind = VK_BOOL;
             break;
-          case 1:
-            if (a.kind == VK_STRING) { c.kind = VK_STRING; break; }
-            *err = "cast of a column to string";
-            return NBG_E_UNSUPPORTED;
           default:
             *out = make_error();
             return NBG_OK;
@@ -615,6 +700,166 @@ struct Ctx {
     }
   }
 
+  // FunctionCallExpression (Expressions.cpp:589-621) over FunctionManager's functions
+  // (FunctionManager.cpp): udf_is_in and the exact double math ones; a name the manager does not
+  // define, or the wrong arity, fails the statement as FunctionManager::get does.  Arguments are
+  // evaluated left to right before the call; an argument's error is the call's error.
+  int32_t function(const Node& e, Compiled* out) {
+    const std::string& f = e.alias;
+    const size_t n = e.kids.size();
+    static const char* math[] = {"abs", "floor", "ceil", "round", "sqrt"};
+    static const char* known[] = {"abs", "floor", "ceil", "round", "sqrt", "cbrt", "hypot", "pow", "exp", "exp2",
+                                  "log", "log2", "log10", "sin", "asin", "cos", "acos", "tan", "atan", "rand32",
+                                  "rand64", "now", "strcasecmp", "lower", "upper", "length", "trim", "ltrim",
+                                  "rtrim", "left", "right", "lpad", "rpad", "substr", "hash", "udf_is_in"};
+    bool defined = false;
+    for (const char* k : known) defined = defined || f == k;
+    if (!defined) {
+      *err = "Function `" + f + "' not defined";
+      return NBG_E_EXECUTION_ERROR;
+    }
+    int mi = -1;
+    for (int i = 0; i < 5; ++i)
+      if (f == math[i]) mi = i;
+    if (mi >= 0) {
+      if (n != 1) {
+        *err = "Arity not match for function `" + f + "'";
+        return NBG_E_EXECUTION_ERROR;
+      }
+      Compiled a;
+      int32_t rc = compile(*e.kids[0], &a);
+      if (rc) return rc;
+      if (a.always_error) { *out = a; return NBG_OK; }
+      // Expression::asDouble: an INT widens, a DOUBLE is itself, anything else is not a double
+      if (a.derived || (a.kind != VK_INT && a.kind != VK_DOUBLE)) { *out = make_error(); return NBG_OK; }
+      if (a.is_const) {
+        const double x = toD(a.cval);
+        const double r = mi == 0 ? std::fabs(x) : mi == 1 ? std::floor(x) : mi == 2 ? std::ceil(x)
+                       : mi == 3 ? std::round(x) : std::sqrt(x);
+        *out = make_const(CVal(r));
+        return NBG_OK;
+      }
+      Compiled c;
+      c.reg = a.reg;
+      if (a.kind == VK_INT) emit(OP_I2F, c.reg, c.reg);
+      static const uint8_t ops[] = {OP_ABS_F, OP_FLOOR_F, OP_CEIL_F, OP_ROUND_F, OP_SQRT_F};
+      emit(ops[mi], c.reg, c.reg);
+      c.kind = VK_DOUBLE;
+      *out = c;
+      return NBG_OK;
+    }
+    if (f != "udf_is_in") {
+      *err = "function `" + f + "' is not supported on the device";
+      return NBG_E_UNSUPPORTED;
+    }
+    if (n < 2) {
+      *err = "Arity not match for function `udf_is_in'";
+      return NBG_E_EXECUTION_ERROR;
+    }
+    return is_in(e, out);
+  }
+
+  // udf_is_in(cmp, v1, ...) (FunctionManager.cpp:440-486): every vi converted to cmp's kind
+  // (toInt / toDouble / toBool / toString), then set membership (exact equality).
+  int32_t is_in(const Node& e, Compiled* out) {
+    Compiled cmp;
+    int32_t rc = compile(*e.kids[0], &cmp);
+    if (rc) return rc;
+    std::vector<Compiled> args(e.kids.size() - 1);
+    bool any_error = cmp.always_error;
+    for (size_t i = 1; i < e.kids.size(); ++i) {
+      rc = compile(*e.kids[i], &args[i - 1]);
+      if (rc) return rc;
+      any_error = any_error || args[i - 1].always_error;
+    }
+    if (any_error) { *out = make_error(); return NBG_OK; }
+    const VKind K = cmp.kind;
+    if (K == VK_STRING) return is_in_string(cmp, args, out);
+    // numeric / bool: the comparand in a register, the accumulator above everything compiled so far
+    const int x = materialize(cmp);
+    const int acc = push();
+    emit(OP_CONST, acc, 0, 0, 0, 0);
+    for (Compiled& a : args) {
+      if (a.is_const && !a.derived) {
+        CVal v;
+        bool ok = true;
+        if (K == VK_INT) ok = cast_value(0, a.cval, &v);
+        else if (K == VK_DOUBLE) ok = cast_value(2, a.cval, &v);
+        else v = CVal(truthy(a.cval));
+        if (!ok) { *out = make_error(); return NBG_OK; }   // folly::to throws on the set's build
+        const int64_t bits = bits_of(v);
+        emit(K == VK_DOUBLE ? OP_ISIN_F : OP_ISIN_I, acc, x, acc, 0, bits);
+        continue;
+      }
+      // a value computed per edge: converted into a register, compared, OR-ed in
+      int r;
+      if (K == VK_BOOL) {
+        r = truthy_reg(a);
+      } else if (a.derived) {
+        const int32_t h = emit_pieces(a.pieces);
+        r = sink_reg(a.pieces);
+        emit(K == VK_DOUBLE ? OP_SPARSE_F : OP_SPARSE_I, r, 0, 0, h);
+      } else {
+        r = a.reg;
+        const bool dbl = K == VK_DOUBLE;
+        switch (a.kind) {
+          case VK_INT: if (dbl) emit(OP_I2F, r, r); break;
+          case VK_DOUBLE: if (!dbl) emit(OP_F2I, r, r); break;
+          case VK_BOOL: emit(dbl ? OP_B2F : OP_B2I, r, r); break;
+          case VK_STRING: emit(dbl ? OP_S2F : OP_S2I, r, r); break;
+        }
+      }
+      emit(K == VK_DOUBLE ? OP_EQX_F : OP_EQ_I, r, x, r);
+      emit(OP_OR, acc, acc, r);
+      top = acc + 1;
+    }
+    // the result lands in the comparand's register (the lowest live one)
+    emit(OP_B2I, x, acc);
+    Compiled c;
+    c.kind = VK_BOOL;
+    c.reg = x;
+    top = x + 1;
+    *out = c;
+    return NBG_OK;
+  }
+
+  int32_t is_in_string(const Compiled& cmp, std::vector<Compiled>& args, Compiled* out) {
+    const std::vector<Piece> pc = pieces_of(cmp);
+    int acc = -1;
+    for (Compiled& a : args) {
+      std::vector<Piece> pa;
+      if (a.kind == VK_STRING) {
+        pa = pieces_of(a);
+      } else if (a.is_const) {   // Expression::toString of a constant
+        CVal v;
+        if (!cast_value(1, a.cval, &v)) { *out = make_error(); return NBG_OK; }
+        pa = {Piece{PC_CONST, -1, std::get<3>(v)}};
+      } else if (a.kind == VK_INT || a.kind == VK_BOOL) {
+        pa = {Piece{a.kind == VK_INT ? PC_INT : PC_BOOL, a.reg, {}}};
+      } else {   // folly's double formatting: unpinned
+        *out = make_error();
+        return NBG_OK;
+      }
+      const int32_t ha = emit_pieces(pc), hb = emit_pieces(pa);
+      // the comparison writes above every live piece register; the accumulator sits below it
+      int r = push();
+      for (auto& p : pc) r = std::max(r, p.reg + 1);
+      for (auto& p : pa) r = std::max(r, p.reg + 1);
+      if (r >= top) { top = r + 1; if (top > max_reg) max_reg = top; }
+      emit(OP_SCMP, r, 4, 0, ha, hb);
+      if (acc < 0) {
+        acc = r;
+      } else {
+        emit(OP_OR, acc, acc, r);
+      }
+    }
+    Compiled c;
+    c.kind = VK_BOOL;
+    c.reg = acc;
+    *out = c;
+    return NBG_OK;
+  }
+
   // Registers of a (left) and b (right): constants are materialised lazily so that the
   // result ends up in the lower slot.
   int32_t binary(const Node& e, Compiled& a, Compiled& b, Compiled* out) {
@@ -638,11 +883,14 @@ struct Ctx {
       return NBG_OK;
     }
     if (e.kind == EK_ARITH) {
-      bool arith = (a.kind == VK_INT || a.kind == VK_DOUBLE) && (b.kind == VK_INT || b.kind == VK_DOUBLE);
+      bool arith = !a.derived && !b.derived && (a.kind == VK_INT || a.kind == VK_DOUBLE) &&
+                   (b.kind == VK_INT || b.kind == VK_DOUBLE);
       if (!arith) {
-        if (e.op == 0 && a.kind == VK_STRING && b.kind == VK_STRING) {
-          *err = "string concatenation of columns";
-          return NBG_E_UNSUPPORTED;
+        if (e.op == 0 && a.kind == VK_STRING && b.kind == VK_STRING) {   // Expressions.cpp:858-860
+          std::vector<Piece> ps = pieces_of(a), pb2 = pieces_of(b);
+          ps.insert(ps.end(), pb2.begin(), pb2.end());
+          *out = derived_of(std::move(ps));
+          return NBG_OK;
         }
         *out = make_error();
         return NBG_OK;
@@ -667,6 +915,15 @@ struct Ctx {
     if (e.op > 5) { *out = make_error(); return NBG_OK; }
     VKind ka = a.kind, kb = b.kind;
     if (ka != kb && (ka == VK_STRING || kb == VK_STRING)) { *out = make_error(); return NBG_OK; }
+    if (a.derived || b.derived) {   // string bytes compared (std::string operators)
+      const std::vector<Piece> pa = pieces_of(a), pbb = pieces_of(b);
+      const int32_t ha = emit_pieces(pa), hb = emit_pieces(pbb);
+      c.reg = sink_reg(pa, pbb);
+      emit(OP_SCMP, c.reg, e.op, 0, ha, hb);
+      c.kind = VK_BOOL;
+      *out = c;
+      return NBG_OK;
+    }
     bool dbl = (ka != kb) ? (ka == VK_DOUBLE || kb == VK_DOUBLE) : ka == VK_DOUBLE;
     int lr = materialize(a);
     if (ka != kb) {
@@ -692,12 +949,23 @@ struct Ctx {
 
 }  // namespace
 
-int32_t compile_expr(const Node& e, const CompileEnv& env, ProgramBuilder& pb, Compiled* out, std::string* err) {
+int32_t compile_expr(const Node& e, const CompileEnv& env, ProgramBuilder& pb, Compiled* out, std::string* err,
+                     bool yield_value) {
   Ctx c{env, pb, err};
   c.top = pb.next_reg;
   c.max_reg = pb.next_reg;
   int32_t rc = c.compile(e, out);
   if (rc) return rc;
+  if (out->derived) {   // the sink of a derived string: a result value, or a WHERE's asBool
+    Compiled v;
+    v.kind = yield_value ? VK_STRING : VK_BOOL;
+    v.reg = yield_value ? c.value_reg(*out) : c.empty_reg(*out);
+    *out = v;
+  }
+  if ((int)(pb.code.size() + pb.data.size()) > MAX_PROGRAM) {
+    *err = "program too long";
+    return NBG_E_UNSUPPORTED;
+  }
   if (!out->is_const && out->reg >= 0) pb.next_reg = out->reg + 1;
   if (c.max_reg > MAX_REGS) {
     *err = "expression too deep for the device register file";

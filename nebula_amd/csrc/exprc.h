@@ -52,6 +52,15 @@ struct CompileEnv {
   const std::vector<VKind>* input_kinds = nullptr;
 };
 
+// One piece of a derived string (a STRING value built on the device: concatenation, casts to
+// string): its bytes are those of a dictionary string (register holding a code), of an INT
+// register in decimal, of a BOOL register ("true" / "false"), or of a constant.
+struct Piece {
+  PieceKind kind;
+  int reg = -1;
+  std::string text;   // PC_CONST
+};
+
 // Result of compiling one expression for one edge type.
 struct Compiled {
   VKind kind = VK_INT;
@@ -61,23 +70,37 @@ struct Compiled {
   CVal cval;                  // the constant value when is_const
   bool always_error = false;
   int reg = -1;
+  // a derived STRING (kind VK_STRING): its pieces, in order; the registers they read stay live
+  // until a sink (compare, cast, truthiness, YIELD) consumes them
+  bool derived = false;
+  std::vector<Piece> pieces;
 };
 
 // Status codes: NBG_OK, NBG_E_UNSUPPORTED, NBG_E_IMPROPER_DATA_TYPE (deferred: the reference
 // reports it only when the final step is reached), NBG_E_INVALID_ARGUMENT.
+// `data` follows `code` in the device program slot: derived-string piece lists and constant
+// bytes, addressed by instructions relative to the data's start (Ins-sized entries).
 struct ProgramBuilder {
   std::vector<Ins> code;
+  std::vector<Ins> data;
   int next_reg = 0;
   int max_reg = 0;
 };
 
-int32_t compile_expr(const Node& e, const CompileEnv& env, ProgramBuilder& pb, Compiled* out, std::string* err);
+// yield_value: the expression is a YIELD column (a derived string becomes its canonical code,
+// OP_SOUT); otherwise a derived string at the top is a WHERE, read as asBool (empty()).
+int32_t compile_expr(const Node& e, const CompileEnv& env, ProgramBuilder& pb, Compiled* out, std::string* err,
+                     bool yield_value = false);
 
 // Evaluate constant-only expressions on the host with the reference's exact rules
 // (Expressions.cpp eval); returns false if the expression is not constant.
 bool fold_constant(const Node& e, CVal* out, bool* error);
 
 int64_t string_code(const std::vector<std::string>& dict, const std::string& s);
+
+// TypeCastingExpression's conversions of one value (Expressions.cpp:773-793): cast type ct
+// (ColumnType: 0 INT, 1 STRING, 2 DOUBLE, 3 BIGINT, 4 BOOL, 5 TIMESTAMP); false = evaluation error
+bool evalCast(uint8_t ct, const CVal& v, CVal* out);
 
 // ---- result column types (GoExecutor::setupInterimResult's schema, GoExecutor.cpp:707-748)
 // The schema of a GO result comes from the first row the reference evaluates: a column's type is

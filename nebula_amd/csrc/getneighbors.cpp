@@ -397,6 +397,7 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
       a.valid = dt.valid;
       a.visible = nullptr;   // the part check above replaces the visibility test
       a.vids = E.snap.d_vids;
+      a.str = E.dev_strings();
       a.props = dt.d_props;
       a.hprops = dt.props.data();
       a.hnarrow = nullptr;

@@ -138,6 +138,8 @@ struct Workspace {
   uint8_t* walk_arena = nullptr;  // FIND ALL PATH level arrays (grow-only)
   size_t walk_cap = 0;
   Ins* d_prog = nullptr;          // [MAX_TYPES_Q][MAX_PROGRAM]
+  char* sarena = nullptr;         // derived strings of the query's rows (OP_SOUT; grow-only)
+  uint64_t sarena_cap = 0;
   // FIND PATH (allocated on first use)
   PState* ps = nullptr;
   PState* h_ps = nullptr;         // pinned mirror
@@ -446,11 +448,257 @@ struct EdgeCtx {
 __device__ __forceinline__ double as_f(int64_t x) { return __longlong_as_double(x); }
 __device__ __forceinline__ int64_t fbits(double d) { return __double_as_longlong(d); }
 
+// ----------------------------------------------------------------------------- derived strings
+// A piece list (exprc.cpp emit_pieces) streamed byte by byte: dictionary strings from the
+// snapshot's string bytes, constants from the program's data, INT pieces as decimal digits
+// computed in place (no per-lane buffer), BOOL pieces as "true" / "false".
+__constant__ unsigned long long kPow10[20] = {1ull, 10ull, 100ull, 1000ull, 10000ull, 100000ull, 1000000ull,
+                                              10000000ull, 100000000ull, 1000000000ull, 10000000000ull,
+                                              100000000000ull, 1000000000000ull, 10000000000000ull,
+                                              100000000000000ull, 1000000000000000ull, 10000000000000000ull,
+                                              100000000000000000ull, 1000000000000000000ull,
+                                              10000000000000000000ull};
+__constant__ char kTrueFalse[10] = "truefalse";
+
+struct PieceView {
+  const char* p;     // the bytes, or nullptr: the decimal of u (negative when neg)
+  uint64_t u;
+  uint32_t len;
+  uint32_t nd, neg;
+};
+
+__device__ __forceinline__ PieceView piece_view(const Ins& pc, const char* dbase, const DevStrings& S,
+                                                const int64_t* regs, int tid, bool& bad) {
+  PieceView v{dbase, 0, 0, 0, 0};
+  const int64_t x = regs[pc.d * BLOCK + tid];
+  switch (pc.op) {
+    case PC_DICT:
+      // -1: "" absent from the dictionary (the schema default of a string prop)
+      if (x != -1) {
+        if (x < 0 || (x & 1) || (uint64_t)(x >> 1) >= S.n) {
+          bad = true;
+        } else {
+          const uint64_t i = (uint64_t)x >> 1;
+          v.p = S.bytes + S.off[i];
+          v.len = S.off[i + 1] - S.off[i];
+        }
+      }
+      break;
+    case PC_CONST: v.p = dbase + pc.aux; v.len = (uint32_t)pc.imm; break;
+    case PC_BOOL: v.p = kTrueFalse + (x ? 0 : 4); v.len = x ? 4u : 5u; break;
+    default: {   // PC_INT: folly::to<std::string>(int64_t)
+      v.p = nullptr;
+      v.neg = x < 0;
+      v.u = v.neg ? 0ull - (uint64_t)x : (uint64_t)x;
+      uint32_t nd = 1;
+      while (nd < 20 && v.u >= kPow10[nd]) ++nd;
+      v.nd = nd;
+      v.len = nd + v.neg;
+    }
+  }
+  return v;
+}
+
+__device__ __forceinline__ uint32_t piece_byte(const PieceView& v, uint32_t i) {
+  if (v.p) return (uint8_t)v.p[i];
+  if (v.neg) {
+    if (!i) return '-';
+    --i;
+  }
+  return '0' + (uint32_t)((v.u / kPow10[v.nd - 1 - i]) % 10);
+}
+
+struct StrIter {
+  const Ins* list;   // the pieces
+  const char* dbase;
+  int n, k;
+  uint32_t i;
+  PieceView v;
+};
+
+__device__ __forceinline__ void str_open(StrIter& it, const Ins* data, int32_t hdr, const DevStrings& S,
+                                         const int64_t* regs, int tid, bool& bad) {
+  const Ins h = data[hdr];
+  it.list = data + h.aux;
+  it.dbase = reinterpret_cast<const char*>(data);
+  it.n = h.d;
+  it.k = 0;
+  it.i = 0;
+  it.v = PieceView{it.dbase, 0, 0, 0, 0};
+  if (it.n) it.v = piece_view(it.list[0], it.dbase, S, regs, tid, bad);
+}
+
+// the next byte (-1 at the end)
+__device__ __forceinline__ int str_next(StrIter& it, const DevStrings& S, const int64_t* regs, int tid, bool& bad) {
+  while (it.i >= it.v.len) {
+    if (++it.k >= it.n) return -1;
+    it.v = piece_view(it.list[it.k], it.dbase, S, regs, tid, bad);
+    it.i = 0;
+  }
+  return (int)piece_byte(it.v, it.i++);
+}
+
+__device__ __forceinline__ uint64_t str_len(const Ins* data, int32_t hdr, const DevStrings& S, const int64_t* regs,
+                                            int tid, bool& bad) {
+  const Ins h = data[hdr];
+  uint64_t n = 0;
+  for (int k = 0; k < h.d; ++k) n += piece_view(data[h.aux + k], reinterpret_cast<const char*>(data), S, regs, tid, bad).len;
+  return n;
+}
+
+// std::string::compare of two piece lists: <0, 0, >0
+__device__ int str_cmp(const Ins* data, int32_t ha, int32_t hb, const DevStrings& S, const int64_t* regs, int tid,
+                       bool& bad) {
+  StrIter x, y;
+  str_open(x, data, ha, S, regs, tid, bad);
+  str_open(y, data, hb, S, regs, tid, bad);
+  for (;;) {
+    const int cx = str_next(x, S, regs, tid, bad), cy = str_next(y, S, regs, tid, bad);
+    if (cx != cy) return cx < cy ? -1 : 1;   // (the end, -1, sorts first: a prefix is smaller)
+    if (cx < 0) return 0;
+  }
+}
+
+__device__ __forceinline__ bool is_space(int ch) { return ch == ' ' || (ch >= '\t' && ch <= '\r'); }
+
+// strtoll(s, &end, 10) consuming the whole string, no overflow (Expression::toInt of a string,
+// as exprc.cpp cast_value restates folly::to<int64_t>); false = evaluation error
+__device__ bool str_to_int(StrIter& it, const DevStrings& S, const int64_t* regs, int tid, bool& bad, int64_t* out) {
+  int ch = str_next(it, S, regs, tid, bad);
+  while (ch >= 0 && is_space(ch)) ch = str_next(it, S, regs, tid, bad);
+  bool neg = false;
+  if (ch == '+' || ch == '-') {
+    neg = ch == '-';
+    ch = str_next(it, S, regs, tid, bad);
+  }
+  if (ch < '0' || ch > '9') return false;
+  uint64_t u = 0;
+  const uint64_t lim = neg ? (1ull << 63) : (1ull << 63) - 1;
+  bool over = false;
+  for (; ch >= '0' && ch <= '9'; ch = str_next(it, S, regs, tid, bad)) {
+    const uint64_t d = (uint64_t)(ch - '0');
+    if (u > (lim - d) / 10) over = true;
+    else u = u * 10 + d;
+  }
+  if (ch >= 0 || over) return false;
+  *out = neg ? (int64_t)(0ull - u) : (int64_t)u;
+  return true;
+}
+
+// strtod(s, &end) consuming the whole string, for decimal forms whose value is exact in the
+// fast path (<= 19 significant digits, m * 10^e with m < 2^53 and |e| <= 22, both exact, so the
+// one rounding is IEEE's); other spellings (hex, inf, nan, longer mantissas) return false
+__device__ bool str_to_double(StrIter& it, const DevStrings& S, const int64_t* regs, int tid, bool& bad, double* out) {
+  int ch = str_next(it, S, regs, tid, bad);
+  while (ch >= 0 && is_space(ch)) ch = str_next(it, S, regs, tid, bad);
+  bool neg = false;
+  if (ch == '+' || ch == '-') {
+    neg = ch == '-';
+    ch = str_next(it, S, regs, tid, bad);
+  }
+  uint64_t m = 0;
+  int sig = 0, e10 = 0;
+  bool any = false;
+  for (; ch >= '0' && ch <= '9'; ch = str_next(it, S, regs, tid, bad)) {
+    any = true;
+    if (m || ch != '0') {
+      if (sig >= 19) return false;
+      m = m * 10 + (uint64_t)(ch - '0');
+      ++sig;
+    }
+  }
+  if (ch == '.') {
+    ch = str_next(it, S, regs, tid, bad);
+    for (; ch >= '0' && ch <= '9'; ch = str_next(it, S, regs, tid, bad)) {
+      any = true;
+      if (m || ch != '0') {
+        if (sig >= 19) return false;
+        m = m * 10 + (uint64_t)(ch - '0');
+        ++sig;
+      }
+      --e10;
+    }
+  }
+  if (!any) return false;
+  if (ch == 'e' || ch == 'E') {
+    ch = str_next(it, S, regs, tid, bad);
+    bool eneg = false;
+    if (ch == '+' || ch == '-') {
+      eneg = ch == '-';
+      ch = str_next(it, S, regs, tid, bad);
+    }
+    if (ch < '0' || ch > '9') return false;   // strtod would stop before the 'e'
+    int ex = 0;
+    for (; ch >= '0' && ch <= '9'; ch = str_next(it, S, regs, tid, bad)) ex = ex < 100000 ? ex * 10 + (ch - '0') : ex;
+    e10 += eneg ? -ex : ex;
+  }
+  if (ch >= 0) return false;
+  double v;
+  if (m == 0) {
+    v = 0.0;
+  } else {
+    if (m > (1ull << 53)) return false;
+    if (e10 > 22 && e10 <= 22 + 15) {   // m * 10^(e10 - 22) may still be exact
+      const uint64_t k = kPow10[e10 - 22];
+      if (m > (1ull << 53) / k) return false;
+      m *= k;
+      e10 = 22;
+    }
+    if (e10 < -22 || e10 > 22) return false;
+    v = e10 >= 0 ? (double)m * (double)kPow10[e10] : (double)m / (double)kPow10[-e10];
+  }
+  *out = neg ? -v : v;
+  return true;
+}
+
+// OP_SOUT: the derived string into the arena; its canonical code (dictionary code when the
+// dictionary holds it, else STR_DERIVED | content hash, str_derived_code)
+__device__ int64_t str_store(const Ins* data, int32_t hdr, const DevStrings& S, const int64_t* regs, int tid,
+                             bool& bad, bool& err) {
+  const uint64_t len = str_len(data, hdr, S, regs, tid, bad);
+  const uint64_t need = 16 + ((len + 7) & ~7ull);
+  const uint64_t at = atomicAdd(S.arena_used, (unsigned long long)need);
+  if (!S.arena || at + need > S.arena_cap) {   // the host fails the query with E_OUT_OF_MEMORY
+    if (S.err_flag) atomicOr(S.err_flag, ARENA_OVERFLOW);
+    err = true;
+    return 0;
+  }
+  char* e = S.arena + at;
+  StrIter it;
+  str_open(it, data, hdr, S, regs, tid, bad);
+  uint64_t h = STR_HASH_INIT;
+  for (uint64_t i = 0; i < len; ++i) {
+    const int ch = str_next(it, S, regs, tid, bad);
+    e[16 + i] = (char)ch;
+    h = str_hash_step(h, (uint8_t)ch);
+  }
+  const int64_t code = str_derived_code(h, len);
+  *reinterpret_cast<int64_t*>(e) = code;
+  *reinterpret_cast<uint64_t*>(e + 8) = len;
+  // the dictionary's code when it holds the string (so a value has one code, whatever made it)
+  uint64_t lo = 0, hi = S.n;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    const uint32_t b = S.off[mid], n = S.off[mid + 1] - b;
+    int c = 0;
+    for (uint32_t i = 0; i < n && i < len && !c; ++i) {
+      const uint32_t x = (uint8_t)S.bytes[b + i], y = (uint8_t)e[16 + i];
+      c = x < y ? -1 : x > y ? 1 : 0;
+    }
+    if (!c) c = n < len ? -1 : n > len ? 1 : 0;
+    if (c == 0) return (int64_t)(2 * mid);
+    if (c < 0) lo = mid + 1;
+    else hi = mid;
+  }
+  return code;
+}
+
 // Evaluate instructions [pc0, pc1) for this lane.  Registers live in LDS, one 8-byte slot per
-// lane per register ([reg][BLOCK]); instruction fetch is wave-uniform (scalar loads).
-__device__ __forceinline__ void run_program(const Ins* __restrict__ prog, int pc0, int pc1, const EdgeCtx& c,
-                                            const ExpandArgs& a, int64_t* __restrict__ regs, bool active,
-                                            bool& err, uint32_t& tbits) {
+// lane per register ([reg][BLOCK]); instruction fetch is wave-uniform (scalar loads).  `data`:
+// the program's piece lists and constant bytes (derived strings).
+__device__ __forceinline__ void run_program(const Ins* __restrict__ prog, const Ins* __restrict__ data, int pc0,
+                                            int pc1, const EdgeCtx& c, const ExpandArgs& a,
+                                            int64_t* __restrict__ regs, bool active, bool& err, uint32_t& tbits) {
   const int tid = threadIdx.x;
   for (int pc = pc0; pc < pc1; ++pc) {
     const Ins ins = prog[pc];
@@ -546,6 +794,71 @@ __device__ __forceinline__ void run_program(const Ins* __restrict__ prog, int pc
       case OP_AND: r = (x != 0) && (y != 0); break;
       case OP_OR: r = (x != 0) || (y != 0); break;
       case OP_XORB: r = (x != 0) != (y != 0); break;
+      case OP_S2I:
+      case OP_S2F: {
+        const bool dbl = ins.op == OP_S2F;
+        if (x >= 0 && !(x & 1) && (uint64_t)(x >> 1) < a.str.n &&
+            (a.str.s2ok[x >> 1] & (dbl ? 2 : 1))) {
+          r = dbl ? a.str.s2f[x >> 1] : a.str.s2i[x >> 1];
+        } else if (active) {
+          err = true;   // not a number ("" too)
+        }
+        break;
+      }
+      case OP_SCMP:
+        if (active) {
+          bool bad = false;
+          const int cm = str_cmp(data, ins.aux, (int32_t)ins.imm, a.str, regs, tid, bad);
+          switch (ins.a) {   // EK_REL op: < <= > >= == !=
+            case 0: r = cm < 0; break;
+            case 1: r = cm <= 0; break;
+            case 2: r = cm > 0; break;
+            case 3: r = cm >= 0; break;
+            case 4: r = cm == 0; break;
+            default: r = cm != 0; break;
+          }
+          err = err || bad;
+        }
+        break;
+      case OP_SPARSE_I:
+      case OP_SPARSE_F:
+        if (active) {
+          bool bad = false;
+          StrIter it;
+          str_open(it, data, ins.aux, a.str, regs, tid, bad);
+          bool ok;
+          if (ins.op == OP_SPARSE_I) {
+            ok = str_to_int(it, a.str, regs, tid, bad, &r);
+          } else {
+            double v = 0.0;
+            ok = str_to_double(it, a.str, regs, tid, bad, &v);
+            r = fbits(v);
+          }
+          err = err || bad || !ok;
+        }
+        break;
+      case OP_SEMPTY:
+        if (active) {
+          bool bad = false;
+          r = str_len(data, ins.aux, a.str, regs, tid, bad) == 0;
+          err = err || bad;
+        }
+        break;
+      case OP_SOUT:
+        if (active) {
+          bool bad = false;
+          r = str_store(data, ins.aux, a.str, regs, tid, bad, err);
+          err = err || bad;
+        }
+        break;
+      case OP_ISIN_I: r = (y != 0) || x == ins.imm; break;
+      case OP_ISIN_F: r = (y != 0) || as_f(x) == as_f(ins.imm); break;
+      case OP_EQX_F: r = as_f(x) == as_f(y); break;
+      case OP_ABS_F: r = fbits(fabs(as_f(x))); break;
+      case OP_FLOOR_F: r = fbits(floor(as_f(x))); break;
+      case OP_CEIL_F: r = fbits(ceil(as_f(x))); break;
+      case OP_ROUND_F: r = fbits(round(as_f(x))); break;
+      case OP_SQRT_F: r = fbits(sqrt(as_f(x))); break;
       default: break;
     }
     regs[ins.d * BLOCK + tid] = r;
@@ -1107,7 +1420,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
           if (fp.where_reg >= 0) {
             bool werr = false;
             EdgeCtx c{jj[i], active ? list_id(a0 + vv[i]) : 0u};
-            run_program(fp.prog, 0, fp.where_len, c, a, regs, active, werr, tbits);
+            run_program(fp.prog, fp.prog + fp.prog_len, 0, fp.where_len, c, a, regs, active, werr, tbits);
             if (fp.keep_on_error) {
               pass = active && (werr || regs[fp.where_reg * BLOCK + threadIdx.x] != 0);
             } else {
@@ -1162,7 +1475,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
         } else {
           bool yerr = false;
           EdgeCtx c{jj[i], pass ? list_id(a0 + vv[i]) : 0u};
-          run_program(fp.prog, fp.where_len, fp.prog_len, c, a, regs, pass, yerr, tbits);
+          run_program(fp.prog, fp.prog + fp.prog_len, fp.where_len, fp.prog_len, c, a, regs, pass, yerr, tbits);
           if (pass && yerr) anyErr = true;
           if (pass) {
             for (int y = 0; y < fp.nyields; ++y) {
@@ -1697,7 +2010,7 @@ void ws_destroy(Workspace* w) {
                   (void*)w->rlist, (void*)w->flags, (void*)w->tsplit,
                   (void*)w->q, (void*)w->rows,
                   (void*)w->d_row_cols, (void*)w->d_prog, (void*)w->dtab, (void*)w->dkeep, (void*)w->dseg,
-                  (void*)w->dcnt, (void*)w->dkinds, (void*)w->bt, (void*)w->walk_arena, (void*)w->xown,
+                  (void*)w->dcnt, (void*)w->dkinds, (void*)w->bt, (void*)w->walk_arena, (void*)w->sarena, (void*)w->xown,
                   (void*)w->xcnt, (void*)w->xsend, (void*)w->xrecv, (void*)w->bt_out, (void*)w->bt_recv})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)w->h_q, (void*)w->h_starts, (void*)w->h_prog, (void*)w->h_ps, (void*)w->h_path,
@@ -1729,6 +2042,32 @@ const uint32_t* ws_host_blk_rows(Workspace* w, int tix) { return w->h_blk_rows +
 int64_t* ws_row_col(Workspace* w, int c) { return w->rows + (uint64_t)c * w->cap_rows; }
 const QState* ws_host_state(Workspace* w) { return w->h_q; }
 const uint32_t* ws_current_frontier(Workspace* w) { return w->frontier[w->cur]; }
+
+// The derived-string arena (OP_SOUT): at least `bytes`, grow-only.
+hipError_t ws_reserve_arena(Workspace* w, uint64_t bytes) {
+  if (bytes <= w->sarena_cap) return hipSuccess;
+  HIP_TRY(ws_sync(w));
+  if (w->sarena) HIP_TRY(hipFree(w->sarena));
+  w->sarena = nullptr;
+  w->sarena_cap = 0;
+  HIP_TRY(hipMalloc((void**)&w->sarena, bytes));
+  w->sarena_cap = bytes;
+  return hipSuccess;
+}
+
+// The arena entries the finished query stored (QState::arena_used, read from the host copy).
+hipError_t ws_read_arena(Workspace* w, uint64_t used, std::vector<char>* out) {
+  if (used > w->sarena_cap) return hipErrorInvalidValue;
+  out->resize(used);
+  if (!used) return hipSuccess;
+  HIP_TRY(hipMemcpyAsync(out->data(), w->sarena, used, hipMemcpyDeviceToHost, w->stream));
+  return hipStreamSynchronize(w->stream);
+}
+
+const char* ws_arena(Workspace* w, uint64_t* cap) {
+  *cap = w->sarena_cap;
+  return w->sarena;
+}
 
 hipError_t ws_reserve_rows(Workspace* w, uint64_t rows, int ncols) {
   if (rows <= w->cap_rows && ncols <= w->ncols_alloc) return hipSuccess;
@@ -1792,7 +2131,10 @@ hipError_t ws_begin_query(Workspace* w, const uint32_t* starts, uint64_t n, cons
     w->prog_stmt = stmt_id;
     size_t k = 0;
     for (auto& p : *progs) {
+      if (p.code.size() + p.data.size() > (size_t)MAX_PROGRAM) return hipErrorInvalidValue;
       memcpy(w->h_prog + k * MAX_PROGRAM, p.code.data(), p.code.size() * sizeof(Ins));
+      if (!p.data.empty())   // derived-string piece lists: right after the code (run_program's `data`)
+        memcpy(w->h_prog + k * MAX_PROGRAM + p.code.size(), p.data.data(), p.data.size() * sizeof(Ins));
       ++k;
     }
     HIP_TRY(hipMemcpyAsync(w->d_prog, w->h_prog, k * MAX_PROGRAM * sizeof(Ins), hipMemcpyHostToDevice, w->stream));
@@ -2120,6 +2462,10 @@ hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound,
   fp.probe_mask = prog.probe_mask;
   fp.keep_on_error = prog.keep_on_error ? 1 : 0;
   fp.tag_bits = &w->q->tagbits;
+  a.str.arena = w->sarena;
+  a.str.arena_cap = w->sarena_cap;
+  a.str.arena_used = &w->q->arena_used;
+  a.str.err_flag = &w->q->err;
   fp.fast = detect_fast(prog, a);
   size_t lds = fp.fast.enabled ? 0 : (size_t)(prog.nregs > 0 ? prog.nregs : 1) * BLOCK * sizeof(int64_t);
   bool dst_only = fp.fast.enabled;   // YIELDs are _dst / constants: the deferred-store instantiation

@@ -124,6 +124,12 @@ struct Snapshot {
   std::vector<int32_t> h_part;          // home part per dense id
   std::map<int32_t, DevEdgeType> types; // signed type -> CSR
   std::vector<std::string> strings;     // sorted dictionary; device code = 2 * index
+  // its device tables (DevStrings): bytes, offsets, per-string toInt / toDouble (casts of columns)
+  uint32_t* d_soff = nullptr;
+  char* d_sbytes = nullptr;
+  int64_t* d_s2i = nullptr;
+  int64_t* d_s2f = nullptr;
+  uint8_t* d_s2ok = nullptr;
   std::map<int32_t, DevTag> tags;       // tag id -> per-vertex columns
   int64_t** d_tcols = nullptr;          // device array: every tag column (DevTag::col_base + c)
   uint8_t** d_tpres = nullptr;          // device array: presence per tag (DevTag::index)
@@ -165,6 +171,19 @@ enum Op : uint8_t {
   OP_I2F, OP_B2I, OP_B2F, OP_F2I, OP_NOT,
   OP_TRUTHY_I, OP_TRUTHY_F, OP_TRUTHY_S,   // asBool (string: code == imm, the empty string)
   OP_AND, OP_OR, OP_XORB,
+  // strings beyond dictionary codes (ExpandArgs::str; piece lists live in the program's data):
+  OP_S2I,        // r[d] = toInt(dictionary string r[a]) (a per-string table; not a number: error)
+  OP_S2F,        // r[d] = toDouble(dictionary string r[a])
+  OP_SCMP,       // r[d] = piece list at data[aux] <rel a> piece list at data[imm] (bytes compared)
+  OP_SPARSE_I,   // r[d] = toInt(piece list data[aux])
+  OP_SPARSE_F,   // r[d] = toDouble(piece list data[aux])
+  OP_SEMPTY,     // r[d] = piece list data[aux] is "" (asBool of a string)
+  OP_SOUT,       // r[d] = the derived string of piece list data[aux], stored in the workspace's string
+                 //        arena; its code is STR_DERIVED | content hash
+  OP_ISIN_I,     // r[d] = r[b] || r[a] == imm   (udf_is_in over int64 / codes / bools)
+  OP_ISIN_F,     // r[d] = r[b] || double(r[a]) == double(imm) (exact, as std::unordered_set<double>)
+  OP_EQX_F,      // r[d] = double(r[a]) == double(r[b]) (exact)
+  OP_ABS_F, OP_FLOOR_F, OP_CEIL_F, OP_ROUND_F, OP_SQRT_F,   // FunctionManager's exact math
   OP_COUNT_
 };
 
@@ -174,6 +193,48 @@ struct Ins {
   int64_t imm;
 };
 static_assert(sizeof(Ins) == 16, "Ins layout");
+// piece kinds of a derived string's piece list (exprc.cpp emit_pieces, kernels.hip piece_view)
+enum PieceKind : uint8_t { PC_DICT = 1, PC_INT = 2, PC_BOOL = 3, PC_CONST = 4 };
+
+// A derived string's code in a result / register: the tag bit plus a 62-bit content hash, so
+// equal strings have equal codes (YIELD DISTINCT, the partitioned owner exchange); its bytes are
+// in the producing workspace's arena (nbg_rows_fetch decodes them).  Dictionary codes are < 2^33.
+constexpr int64_t STR_DERIVED = (int64_t)1 << 62;
+constexpr uint64_t STR_HASH_MASK = ((uint64_t)1 << 62) - 1;
+// (negative codes are dictionary codes too: -1 is "" when the dictionary lacks it)
+inline bool is_derived_code(int64_t c) { return ((uint64_t)c >> 62) == 1; }
+constexpr uint64_t STR_HASH_INIT = 0xcbf29ce484222325ull;   // FNV-1a over the bytes, then mixed
+
+#if defined(__HIPCC__)
+#define NBG_HD __host__ __device__
+#else
+#define NBG_HD
+#endif
+NBG_HD inline uint64_t str_hash_step(uint64_t h, uint8_t b) { return (h ^ b) * 0x100000001b3ull; }
+NBG_HD inline int64_t str_derived_code(uint64_t h, uint64_t len) {
+  uint64_t z = h ^ (len * 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return STR_DERIVED | (int64_t)(z & STR_HASH_MASK);
+}
+
+// Device string tables of a snapshot (built at finalize when the dictionary is not empty): the
+// dictionary's bytes and the per-string toInt / toDouble results the casts read
+struct DevStrings {
+  const uint32_t* off = nullptr;    // [n + 1] byte offsets into bytes
+  const char* bytes = nullptr;
+  const int64_t* s2i = nullptr;     // [n] toInt(string) payload
+  const int64_t* s2f = nullptr;     // [n] toDouble(string) bits
+  const uint8_t* s2ok = nullptr;    // [n] bit 0: toInt ok, bit 1: toDouble ok
+  uint64_t n = 0;
+  // the query's derived-string arena (OP_SOUT): entries [u64 hash][u32 len][u32 0][bytes, 8-aligned]
+  char* arena = nullptr;
+  unsigned long long* arena_used = nullptr;   // bytes claimed (may exceed arena_cap: overflow)
+  uint64_t arena_cap = 0;
+  unsigned long long* err_flag = nullptr;     // QState::err: an overflow ORs in ARENA_OVERFLOW
+};
+constexpr unsigned long long ARENA_OVERFLOW = 1ull << 32;   // (summed over ranks, still >= 2^32)
 
 constexpr int MAX_REGS = 16;
 constexpr int MAX_PROGRAM = 256;   // instructions per query/type (WHERE + all YIELDs)
@@ -193,6 +254,8 @@ struct TypeProgram {
   std::vector<VKind> yield_kind;
   std::vector<int64_t> yield_const;   // constant payload when yield_reg == -1
   std::vector<std::string> yield_const_str;   // string constants (may be absent from the dictionary)
+  std::vector<Ins> data;           // piece lists and constant bytes of derived strings (after `code`)
+  bool sout = false;               // some YIELD stores a derived string (OP_SOUT: the string arena)
   bool needs_error_check = false;  // any op can raise an error
   uint32_t probe_mask = 0;         // tags read through $$: presence probed for every final edge
   bool keep_on_error = false;      // storage filter: an evaluation error keeps the edge (inl:444-448)
@@ -237,6 +300,7 @@ struct QState {
   // $$ holder semantics (GoExecutor::VertexHolder, GoExecutor.cpp:986-1064): bit t = some final
   // destination has tag t; bit 16 + t = a row read tag t's default for a destination without it
   unsigned long long tagbits;
+  unsigned long long arena_used;       // bytes the query's OP_SOUT claimed in the string arena
 };
 
 struct ExpandArgs {                // one (step, edge type) expansion
@@ -267,6 +331,7 @@ struct ExpandArgs {                // one (step, edge type) expansion
   const int64_t* in_ids;           // input index: the rows' vids, ascending (last row wins)
   uint64_t in_n;
   const int64_t* const* in_cols;   // [col][k] 8-byte payloads of the indexed rows
+  DevStrings str;                  // strings beyond dictionary codes (casts, concatenation)
 };
 
 // ----------------------------------------------------------------------------- FIND PATH state
@@ -398,6 +463,10 @@ struct Comm {
   // (NBG_OK when none did), the same on every rank.  Returns 0, or -1 when the exchange itself
   // failed (the communicator is then aborted).  Synchronous (host round trip).
   int agree(hipStream_t s, int32_t local, int32_t* out);
+  // out[q * k + i] = rank q's mine[i], on every rank (k equal on every rank, world * k <=
+  // GATHER_WORDS); through the communicator's own scratch, so nothing is allocated per call.
+  // Returns 0, or -1 when the exchange failed (the communicator is then aborted) or is too large.
+  int gather_u64(hipStream_t s, const uint64_t* mine, size_t k, std::vector<uint64_t>* out);
   virtual void abort() { aborted = true; }
   bool is_aborted() const { return aborted; }
   // Wait for a stream that runs this communicator's collectives; gives up (aborting) after the
@@ -419,10 +488,11 @@ struct Comm {
 
  protected:
   volatile bool aborted = false;
-  unsigned long long* agree_dev = nullptr;    // [AGREE_WORDS] device scratch of agree()
+  unsigned long long* agree_dev = nullptr;    // [GATHER_WORDS] device scratch of agree() / gather_u64()
   unsigned long long* agree_host = nullptr;   // pinned mirror
 };
 constexpr int AGREE_WORDS = 256;            // agree(): one status word per rank (world <= 256)
+constexpr size_t GATHER_WORDS = 8192;       // gather_u64(): world * k words (the scratch's size)
 double comm_timeout_s();                    // NBG_COMM_TIMEOUT_S
 Comm* comm_rccl(const uint8_t id[NBG_UNIQUE_ID_BYTES], int world, int rank, std::string* err);
 std::vector<Comm*> comm_local_group(int world);
@@ -469,6 +539,9 @@ int ws_profile_read(Workspace* w, nbg_kernel_stat* out, int cap);
 void ws_profile_inherit(Workspace* to, Workspace* from);   // profiling mode and counters
 uint64_t ws_cap_frontier(Workspace* w);
 uint64_t ws_cap_items(Workspace* w);   // entries + edges of one list the merge-path tiles cover
+hipError_t ws_reserve_arena(Workspace* w, uint64_t bytes);   // derived strings (OP_SOUT), grow-only
+hipError_t ws_read_arena(Workspace* w, uint64_t used, std::vector<char>* out);
+const char* ws_arena(Workspace* w, uint64_t* cap);           // device pointer + capacity
 hipError_t ws_reserve_rows(Workspace* w, uint64_t rows, int ncols);
 int64_t* ws_row_col(Workspace* w, int c);       // device pointer of output column c
 uint64_t ws_shard_cap(uint64_t n_bound, uint64_t e_bound);

@@ -29,6 +29,7 @@
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 #include <string>
+#include <unistd.h>
 #include <vector>
 
 #include "engine.h"
@@ -90,6 +91,12 @@ __global__ void k_rp_scatter_deg(const uint32_t* __restrict__ gdeg, const uint32
     if (g2d[g] != NO_ROW) ddeg[g2d[g]] = gdeg[g];
 }
 
+// the merged dictionary must hold every vid once (ranks own disjoint vertex sets)
+__global__ void k_rp_dups(const int64_t* __restrict__ D, uint64_t n, uint32_t* __restrict__ dups) {
+  for (uint64_t i = (uint64_t)blockIdx.x * RB + threadIdx.x + 1; i < n; i += (uint64_t)gridDim.x * RB)
+    if (D[i] == D[i - 1]) atomicAdd(dups, 1u);
+}
+
 struct ChunkArgs {
   const uint32_t* col;      // [G * C] received neighbour global ids
   const int64_t* dst;       // [G * C] neighbour vids
@@ -140,42 +147,45 @@ __global__ void k_rp_vis_local(const uint8_t* __restrict__ vis, uint64_t nv, uin
     out[i] = i < nv ? (vis ? vis[i] : 1) : 0;
 }
 
+// the replica's scratch and kept arrays: every allocation of the build is made before its first
+// data collective (a rank-local OOM after that point could only abort the communicator)
 struct Builder {
   Engine& E;
   Comm* cm;
   hipStream_t s;
   int G;
   uint64_t npad;
-  std::vector<void*> tmp;
+  std::vector<void*> tmp;    // freed when the build ends
+  std::vector<void*> kept;   // the replica's arrays (freed on failure, else held by its snapshot)
+  bool oom = false;
   std::string err;
   explicit Builder(Engine& e) : E(e), cm(e.comm.get()), s(e.stream), G(e.cfg.num_gpus), npad(e.npad) {}
   ~Builder() {
     (void)hipStreamSynchronize(s);
     for (void* p : tmp) (void)hipFree(p);
+    for (void* p : kept) (void)hipFree(p);
   }
   hipError_t fail(hipError_t e, const char* what) {
     if (err.empty()) err = std::string(what) + ": " + hipGetErrorString(e);
     return e;
   }
   template <class T>
-  hipError_t get(T** p, uint64_t n) {
+  T* alloc(uint64_t n, std::vector<void*>& into) {
+    if (oom) return nullptr;
     void* q = nullptr;
-    const hipError_t e = hipMalloc(&q, std::max<uint64_t>(n, 1) * sizeof(T));
-    if (e != hipSuccess) return e;
-    tmp.push_back(q);
-    *p = static_cast<T*>(q);
-    return hipSuccess;
+    if (hipMalloc(&q, std::max<uint64_t>(n, 1) * sizeof(T)) != hipSuccess) {
+      oom = true;
+      err = "hipMalloc of " + std::to_string(n * sizeof(T)) + " bytes";
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    into.push_back(q);
+    return static_cast<T*>(q);
   }
-  // a device allocation kept by the replica (freed with it on failure by the caller)
   template <class T>
-  hipError_t keep(T** p, uint64_t n, std::vector<void*>* owned) {
-    void* q = nullptr;
-    const hipError_t e = hipMalloc(&q, std::max<uint64_t>(n, 1) * sizeof(T));
-    if (e != hipSuccess) return e;
-    owned->push_back(q);
-    *p = static_cast<T*>(q);
-    return hipSuccess;
-  }
+  T* get(uint64_t n) { return alloc<T>(n, tmp); }
+  template <class T>
+  T* keep(uint64_t n) { return alloc<T>(n, kept); }
   hipError_t gather(const void* send, void* recv, size_t bytes) {
     if (cm->allgather(send, recv, bytes, s)) {
       err = "all-gather: " + cm->last;
@@ -183,35 +193,29 @@ struct Builder {
     }
     return hipSuccess;
   }
-  hipError_t scan(const uint32_t* in, uint32_t* out, uint64_t n) {
-    size_t bytes = 0;
-    RP_TRY(rocprim::exclusive_scan(nullptr, bytes, in, out, 0u, n, rocprim::plus<uint32_t>(), s));
-    void* t = nullptr;
-    RP_TRY(get(reinterpret_cast<uint8_t**>(&t), bytes));
-    RP_TRY(rocprim::exclusive_scan(t, bytes, in, out, 0u, n, rocprim::plus<uint32_t>(), s));
-    return hipSuccess;
-  }
-  template <class T>
-  hipError_t host_all(T v, std::vector<T>* out) {   // all-gather of one value per rank
-    T* d = nullptr;
-    T* r = nullptr;
-    RP_TRY(get(&d, 1));
-    RP_TRY(get(&r, (uint64_t)G));
-    RP_TRY(hipMemcpyAsync(d, &v, sizeof(T), hipMemcpyHostToDevice, s));
-    RP_TRY(gather(d, r, sizeof(T)));
-    out->resize(G);
-    RP_TRY(hipMemcpyAsync(out->data(), r, G * sizeof(T), hipMemcpyDeviceToHost, s));
-    return hipStreamSynchronize(s);
-  }
 };
+
+// a key naming the physical device this rank runs on (host name + PCI bus id): ranks sharing one
+// GPU (the one-GPU rehearsals, in-process groups) share its free memory
+uint64_t device_key(int dev) {
+  char host[256] = {0};
+  (void)gethostname(host, sizeof(host) - 1);
+  char bus[64] = {0};
+  (void)hipDeviceGetPCIBusId(bus, sizeof(bus) - 1, dev);
+  uint64_t h = 1469598103934665603ull;
+  for (const char* p : {static_cast<const char*>(host), static_cast<const char*>(bus)})
+    for (; *p; ++p) h = (h ^ (uint8_t)*p) * 1099511628211ull;
+  return h;
+}
 
 // replica bytes this rank would hold (path CSRs over every rank's vertices and edges) and the
 // build's peak scratch
-uint64_t replica_bytes(const Engine& E, uint64_t n_all, uint64_t e_all_per_type, bool ranks, uint64_t chunk) {
+uint64_t replica_bytes(const Engine& E, uint64_t n_all, uint64_t e_all_per_type, uint64_t ntypes, bool ranks,
+                       uint64_t chunk) {
   const uint64_t G = (uint64_t)E.cfg.num_gpus;
-  uint64_t b = n_all * 9 + G * E.npad * 16;
-  b += E.snap.types.size() * ((n_all + 1) * 4 + e_all_per_type * (12 + (ranks ? 8 : 0)));
-  return b + G * chunk * 20 + chunk * 20;
+  uint64_t b = n_all * 26 + G * E.npad * 25;
+  b += ntypes * ((n_all + 1) * 4 + e_all_per_type * (12 + (ranks ? 8 : 0)));
+  return b + (G + 1) * chunk * (12 + (ranks ? 8 : 0));
 }
 
 }  // namespace
@@ -236,66 +240,153 @@ void destroy_path_replica(Engine& E) {
 int32_t build_path_replica(Engine& E) {
   destroy_path_replica(E);
   if (!E.partitioned() || !E.comm) return NBG_OK;
-  Builder B(E);
-  const int G = B.G;
-  const uint64_t npad = B.npad;
-  const uint64_t CHUNK = getenv("NBG_REPLICA_CHUNK") ? strtoull(getenv("NBG_REPLICA_CHUNK"), nullptr, 10) : (1ull << 25);
-  // ---- sizes, and whether every rank wants and can hold the replica (agreed: all or none)
-  std::vector<uint64_t> vcount;
-  if (B.host_all<uint64_t>(E.snap.nv, &vcount) != hipSuccess) return E.fail(NBG_E_DEVICE, "replica: " + B.err);
-  std::vector<int32_t> types;   // union of the ranks' signed types (each rank lists up to 64)
-  {
-    int32_t mine[64] = {0};
-    int k = 0;
-    for (auto& kv : E.snap.types)
-      if (k < 64) mine[k++] = kv.first;
-    int32_t *d = nullptr, *r = nullptr;
-    if (B.get(&d, 64) != hipSuccess || B.get(&r, 64 * (uint64_t)G) != hipSuccess ||
-        hipMemcpyAsync(d, mine, sizeof(mine), hipMemcpyHostToDevice, B.s) != hipSuccess ||
-        B.gather(d, r, sizeof(mine)) != hipSuccess)
-      return E.fail(NBG_E_DEVICE, "replica: " + B.err);
-    std::vector<int32_t> all(64 * (size_t)G);
-    if (hipMemcpyAsync(all.data(), r, all.size() * 4, hipMemcpyDeviceToHost, B.s) != hipSuccess ||
-        hipStreamSynchronize(B.s) != hipSuccess)
-      return E.fail(NBG_E_DEVICE, "replica: type list");
-    for (int32_t t : all)
-      if (t && std::find(types.begin(), types.end(), t) == types.end()) types.push_back(t);
-    std::sort(types.begin(), types.end());
-  }
-  uint64_t n_all = 0, e_max = 0;
-  for (uint64_t c : vcount) n_all += c;
+  Comm* const cm = E.comm.get();
+  const int G = E.cfg.num_gpus;
+  const uint64_t npad = E.npad;
+  const hipStream_t st = E.stream;
+  auto xfail = [&](const char* what) { return E.fail(NBG_E_DEVICE, std::string("replica ") + what + ": " + cm->last); };
+  // ---- 1. sizes: host words through the communicator's own scratch (nothing allocated here)
+  uint64_t hidden = 0;
+  for (uint8_t v : E.snap.h_visible) hidden += v == 0;
   bool any_rank = false;
   for (auto& kv : E.snap.types) any_rank = any_rank || kv.second.rank;
-  std::vector<uint64_t> etot(types.size(), 0);
-  std::vector<std::vector<uint64_t>> ecount(types.size());
-  for (size_t k = 0; k < types.size(); ++k) {
-    auto it = E.snap.types.find(types[k]);
-    if (B.host_all<uint64_t>(it == E.snap.types.end() ? 0 : it->second.num_edges, &ecount[k]) != hipSuccess)
-      return E.fail(NBG_E_DEVICE, "replica: " + B.err);
-    for (uint64_t c : ecount[k]) etot[k] += c;
-    e_max = std::max(e_max, etot[k]);
-  }
-  std::vector<uint64_t> ranks_any;
-  if (B.host_all<uint64_t>(any_rank ? 1 : 0, &ranks_any) != hipSuccess) return E.fail(NBG_E_DEVICE, "replica: " + B.err);
+  const uint64_t me_key = device_key(E.cfg.device);
+  const uint64_t w1[5] = {E.snap.nv, E.snap.types.size(), any_rank ? 1ull : 0ull, hidden, me_key};
+  std::vector<uint64_t> g1;
+  if (cm->gather_u64(st, w1, 5, &g1)) return xfail("sizes");
+  std::vector<uint64_t> vcount(G);
+  uint64_t n_all = 0, max_types = 0, hidden_all = 0, coresident = 0;
   any_rank = false;
-  for (uint64_t x : ranks_any) any_rank = any_rank || x;
+  for (int q = 0; q < G; ++q) {
+    vcount[q] = g1[q * 5];
+    n_all += vcount[q];
+    max_types = std::max(max_types, g1[q * 5 + 1]);
+    any_rank = any_rank || g1[q * 5 + 2];
+    hidden_all += g1[q * 5 + 3];
+    coresident += g1[q * 5 + 4] == me_key;
+  }
+  // (every rank decides the same from the same words: no agreement needed to skip)
+  if (max_types == 0 || (uint64_t)G * max_types > GATHER_WORDS) return NBG_OK;
+  std::vector<int32_t> types;   // union of the ranks' signed types, sorted
+  {
+    std::vector<uint64_t> mine(max_types, 0), all;
+    size_t k = 0;
+    for (auto& kv : E.snap.types) mine[k++] = (uint64_t)(uint32_t)kv.first;
+    if (cm->gather_u64(st, mine.data(), max_types, &all)) return xfail("type list");
+    for (uint64_t x : all)
+      if (x && std::find(types.begin(), types.end(), (int32_t)(uint32_t)x) == types.end())
+        types.push_back((int32_t)(uint32_t)x);
+    std::sort(types.begin(), types.end());
+  }
+  if ((uint64_t)G * types.size() > GATHER_WORDS) return NBG_OK;
+  std::vector<std::vector<uint64_t>> ecount(types.size(), std::vector<uint64_t>(G));
+  std::vector<uint64_t> etot(types.size(), 0);
+  uint64_t e_max = 0, e_rank_max = 0;
+  {
+    std::vector<uint64_t> mine(types.size(), 0), all;
+    for (size_t k = 0; k < types.size(); ++k) {
+      auto it = E.snap.types.find(types[k]);
+      mine[k] = it == E.snap.types.end() ? 0 : it->second.num_edges;
+    }
+    if (cm->gather_u64(st, mine.data(), types.size(), &all)) return xfail("edge counts");
+    for (size_t k = 0; k < types.size(); ++k) {
+      for (int q = 0; q < G; ++q) {
+        ecount[k][q] = all[(size_t)q * types.size() + k];
+        etot[k] += ecount[k][q];
+        e_rank_max = std::max(e_rank_max, ecount[k][q]);
+      }
+      e_max = std::max(e_max, etot[k]);
+    }
+  }
+  const uint64_t CHUNK0 = getenv("NBG_REPLICA_CHUNK") ? strtoull(getenv("NBG_REPLICA_CHUNK"), nullptr, 10) : (1ull << 25);
+  const uint64_t CHUNK = std::max<uint64_t>(1, std::min<uint64_t>(CHUNK0, e_rank_max));
   size_t free_b = 0, total_b = 0;
   (void)hipMemGetInfo(&free_b, &total_b);
+  const uint64_t my_share = free_b / std::max<uint64_t>(coresident, 1);   // ranks sharing this GPU
   int32_t local = NBG_OK;
   if (!path_replica_wanted(E)) local = NBG_E_UNSUPPORTED;
   else if (e_max >= 0xFFFFFFFFull || n_all >= NO_ROW) local = NBG_E_UNSUPPORTED;
-  else if (replica_bytes(E, n_all, e_max, any_rank, CHUNK) > free_b / 10 * 8) local = NBG_E_OUT_OF_MEMORY;
+  else if (replica_bytes(E, n_all, e_max, types.size(), any_rank, CHUNK) > my_share / 10 * 8) local = NBG_E_OUT_OF_MEMORY;
   int32_t agreed = NBG_OK;
-  if (B.cm->agree(B.s, local, &agreed)) return E.fail(NBG_E_DEVICE, "replica agreement: " + B.cm->last);
+  if (cm->agree(st, local, &agreed)) return xfail("agreement");
   if (agreed) return NBG_OK;   // no replica on any rank: FIND PATH stays collective
 
+  // ---- 2. every allocation of the build and of the replica engine, then a second agreement: a
+  //         rank that cannot allocate makes every rank go without the replica (not an abort)
+  Builder B(E);
+  const uint64_t N = n_all;   // (checked below: the ranks' dictionaries are disjoint)
+  uint64_t* d_cnt = B.get<uint64_t>(G);
+  uint64_t* d_base = B.get<uint64_t>(G);
+  int64_t* lv = B.get<int64_t>(npad);
+  int64_t* gd = B.get<int64_t>((uint64_t)G * npad);
+  int64_t* packed = B.get<int64_t>(n_all);
+  int64_t* D = B.keep<int64_t>(N);
+  uint32_t* dups = B.get<uint32_t>(1);
+  uint32_t* g2d = B.get<uint32_t>((uint64_t)G * npad);
+  uint32_t* ldeg = B.get<uint32_t>(npad);
+  uint32_t* gdeg = B.get<uint32_t>((uint64_t)G * npad);
+  uint32_t* goff = B.get<uint32_t>((uint64_t)G * npad);
+  uint32_t* ddeg = B.get<uint32_t>(N + 1);
+  uint64_t* d_ecnt = B.get<uint64_t>(G);
+  uint32_t* s_col = B.get<uint32_t>(CHUNK);
+  uint32_t* r_col = B.get<uint32_t>((uint64_t)G * CHUNK);
+  int64_t* s_dst = B.get<int64_t>(CHUNK);
+  int64_t* r_dst = B.get<int64_t>((uint64_t)G * CHUNK);
+  int64_t* s_rank = any_rank ? B.get<int64_t>(CHUNK) : nullptr;
+  int64_t* r_rank = any_rank ? B.get<int64_t>((uint64_t)G * CHUNK) : nullptr;
+  uint8_t* lvis = hidden_all ? B.get<uint8_t>(npad) : nullptr;
+  uint8_t* gvis = hidden_all ? B.get<uint8_t>((uint64_t)G * npad) : nullptr;
+  uint8_t* rvis = hidden_all ? B.keep<uint8_t>(N) : nullptr;
+  size_t sort_bytes = 0, scan_bytes = 0, b2 = 0;
+  (void)rocprim::radix_sort_keys(nullptr, sort_bytes, packed, D, n_all, 0, 64, st);
+  (void)rocprim::exclusive_scan(nullptr, scan_bytes, ldeg, goff, 0u, npad, rocprim::plus<uint32_t>(), st);
+  (void)rocprim::exclusive_scan(nullptr, b2, ddeg, ddeg, 0u, N + 1, rocprim::plus<uint32_t>(), st);
+  scan_bytes = std::max(scan_bytes, b2);
+  void* sort_tmp = B.get<uint8_t>(sort_bytes);
+  void* scan_tmp = B.get<uint8_t>(scan_bytes);
+  std::vector<DevEdgeType> dts(types.size());
+  for (size_t k = 0; k < types.size(); ++k) {
+    dts[k].type = types[k];
+    dts[k].num_edges = etot[k];
+    dts[k].row_ptr = B.keep<uint32_t>(N + 1);
+    dts[k].col = B.keep<uint32_t>(etot[k]);
+    dts[k].dst_vid = B.keep<int64_t>(etot[k]);
+    if (any_rank) dts[k].rank = B.keep<int64_t>(etot[k]);
+  }
   auto R = std::make_unique<Engine>();
-  std::vector<void*> owned;   // the replica's device arrays until its snapshot holds them
+  R->cfg = E.cfg;
+  R->cfg.num_gpus = 1;
+  R->cfg.rank = 0;
+  std::string werr;
+  if (!B.oom && hipStreamCreateWithFlags(&R->stream, hipStreamNonBlocking) != hipSuccess) {
+    R->stream = nullptr;
+    B.oom = true;
+    B.err = "replica stream";
+  }
+  if (!B.oom && !(R->ws = ws_create(N + 1024, N, e_max, R->stream, &werr))) {
+    B.oom = true;
+    B.err = "replica workspace: " + werr;
+  }
+  auto drop_engine = [&]() {
+    if (R->ws) ws_destroy(R->ws);
+    R->ws = nullptr;
+    if (R->stream) (void)hipStreamDestroy(R->stream);
+    R->stream = nullptr;
+  };
+  if (cm->agree(st, B.oom ? NBG_E_OUT_OF_MEMORY : NBG_OK, &agreed)) {
+    drop_engine();
+    return xfail("allocation agreement");
+  }
+  if (agreed) {   // some rank could not hold it: every rank goes without (B frees the arrays)
+    drop_engine();
+    return NBG_OK;
+  }
+
+  // ---- 3. the build: from here on only a device or transport error fails, and it aborts the
+  //         communicator (every rank reaches the same collectives)
   auto bail = [&](hipError_t e) {
-    for (void* p : owned) (void)hipFree(p);
-    // every rank reaches the same point of the build; a local failure here aborts the
-    // communicator so the peers' pending collectives fail too
-    B.cm->abort();
+    drop_engine();
+    cm->abort();
     return E.fail(e == hipErrorOutOfMemory ? NBG_E_OUT_OF_MEMORY : NBG_E_DEVICE, "path replica: " + B.err);
   };
 #define RB_TRY(x)                                  \
@@ -306,89 +397,68 @@ int32_t build_path_replica(Engine& E) {
       return bail(e__);                            \
     }                                              \
   } while (0)
-  // ---- 1. global dictionary
-  uint64_t *d_cnt = nullptr, *d_base = nullptr;
-  RB_TRY(B.get(&d_cnt, G));
-  RB_TRY(B.get(&d_base, G));
+  auto scan = [&](const uint32_t* in, uint32_t* out, uint64_t n) {
+    size_t bytes = scan_bytes;
+    return rocprim::exclusive_scan(scan_tmp, bytes, in, out, 0u, n, rocprim::plus<uint32_t>(), st);
+  };
+  // 3a. global dictionary
   std::vector<uint64_t> base(G, 0);
   for (int q = 1; q < G; ++q) base[q] = base[q - 1] + vcount[q - 1];
-  RB_TRY(hipMemcpyAsync(d_cnt, vcount.data(), G * 8, hipMemcpyHostToDevice, B.s));
-  RB_TRY(hipMemcpyAsync(d_base, base.data(), G * 8, hipMemcpyHostToDevice, B.s));
-  int64_t *lv = nullptr, *gd = nullptr, *packed = nullptr, *D = nullptr;
-  RB_TRY(B.get(&lv, npad));
-  RB_TRY(B.get(&gd, (uint64_t)G * npad));
-  RB_TRY(hipMemsetAsync(lv, 0, npad * 8, B.s));
-  if (E.snap.nv) RB_TRY(hipMemcpyAsync(lv, E.snap.d_vids, E.snap.nv * 8, hipMemcpyDeviceToDevice, B.s));
+  RB_TRY(hipMemcpyAsync(d_cnt, vcount.data(), G * 8, hipMemcpyHostToDevice, st));
+  RB_TRY(hipMemcpyAsync(d_base, base.data(), G * 8, hipMemcpyHostToDevice, st));
+  RB_TRY(hipMemsetAsync(lv, 0, npad * 8, st));
+  if (E.snap.nv) RB_TRY(hipMemcpyAsync(lv, E.snap.d_vids, E.snap.nv * 8, hipMemcpyDeviceToDevice, st));
   RB_TRY(B.gather(lv, gd, npad * 8));
-  RB_TRY(B.get(&packed, n_all));
-  hipLaunchKernelGGL(k_rp_pack, dim3(rgrid((uint64_t)G * npad)), dim3(RB), 0, B.s, gd, npad, G, d_cnt, d_base, packed);
+  hipLaunchKernelGGL(k_rp_pack, dim3(rgrid((uint64_t)G * npad)), dim3(RB), 0, st, gd, npad, G, d_cnt, d_base, packed);
   RB_TRY(hipGetLastError());
-  uint64_t N = 0;
-  RB_TRY(bd_sort_unique(packed, n_all, &D, &N, B.s));
-  owned.push_back(D);
-  if (N != n_all) {   // a vid held by two ranks: every rank sees the same gathered data, so all stop here
-    for (void* p : owned) (void)hipFree(p);
+  {
+    size_t bytes = sort_bytes;
+    RB_TRY(rocprim::radix_sort_keys(sort_tmp, bytes, packed, D, n_all, 0, 64, st));
+  }
+  RB_TRY(hipMemsetAsync(dups, 0, 4, st));
+  hipLaunchKernelGGL(k_rp_dups, dim3(rgrid(N)), dim3(RB), 0, st, D, N, dups);
+  RB_TRY(hipGetLastError());
+  uint32_t h_dups = 0;
+  RB_TRY(hipMemcpyAsync(&h_dups, dups, 4, hipMemcpyDeviceToHost, st));
+  RB_TRY(hipStreamSynchronize(st));
+  if (h_dups) {   // a vid held by two ranks: every rank sees the same gathered data, so all stop here
+    drop_engine();
     return NBG_OK;
   }
-  uint32_t* g2d = nullptr;
-  RB_TRY(B.get(&g2d, (uint64_t)G * npad));
-  hipLaunchKernelGGL(k_rp_g2d, dim3(rgrid((uint64_t)G * npad)), dim3(RB), 0, B.s, gd, npad, G, d_cnt, D, N, g2d);
+  hipLaunchKernelGGL(k_rp_g2d, dim3(rgrid((uint64_t)G * npad)), dim3(RB), 0, st, gd, npad, G, d_cnt, D, N, g2d);
   RB_TRY(hipGetLastError());
   Snapshot& rs = R->snap;
   rs.nv = N;
   rs.d_vids = D;
   rs.h_vids.resize(N);
-  RB_TRY(hipMemcpyAsync(rs.h_vids.data(), D, N * 8, hipMemcpyDeviceToHost, B.s));
-  // ---- 2. per signed type
-  uint32_t *ldeg = nullptr, *gdeg = nullptr, *goff = nullptr, *ddeg = nullptr;
-  RB_TRY(B.get(&ldeg, npad));
-  RB_TRY(B.get(&gdeg, (uint64_t)G * npad));
-  RB_TRY(B.get(&goff, (uint64_t)G * npad));
-  RB_TRY(B.get(&ddeg, N + 1));
-  uint64_t* d_ecnt = nullptr;
-  RB_TRY(B.get(&d_ecnt, G));
-  uint32_t *s_col = nullptr, *r_col = nullptr;
-  int64_t *s_dst = nullptr, *r_dst = nullptr, *s_rank = nullptr, *r_rank = nullptr;
-  RB_TRY(B.get(&s_col, CHUNK));
-  RB_TRY(B.get(&r_col, (uint64_t)G * CHUNK));
-  RB_TRY(B.get(&s_dst, CHUNK));
-  RB_TRY(B.get(&r_dst, (uint64_t)G * CHUNK));
-  if (any_rank) {
-    RB_TRY(B.get(&s_rank, CHUNK));
-    RB_TRY(B.get(&r_rank, (uint64_t)G * CHUNK));
-  }
+  RB_TRY(hipMemcpyAsync(rs.h_vids.data(), D, N * 8, hipMemcpyDeviceToHost, st));
+  // 3b. per signed type
   for (size_t k = 0; k < types.size(); ++k) {
     const int32_t t = types[k];
     auto it = E.snap.types.find(t);
     const DevEdgeType* lt = it == E.snap.types.end() ? nullptr : &it->second;
-    hipLaunchKernelGGL(k_rp_deg, dim3(rgrid(npad)), dim3(RB), 0, B.s, lt ? lt->row_ptr : nullptr, E.snap.nv, npad, ldeg);
+    DevEdgeType& dt = dts[k];
+    hipLaunchKernelGGL(k_rp_deg, dim3(rgrid(npad)), dim3(RB), 0, st, lt ? lt->row_ptr : nullptr, E.snap.nv, npad, ldeg);
     RB_TRY(hipGetLastError());
     RB_TRY(B.gather(ldeg, gdeg, npad * 4));
-    for (int q = 0; q < G; ++q) RB_TRY(B.scan(gdeg + (uint64_t)q * npad, goff + (uint64_t)q * npad, npad));
-    RB_TRY(hipMemsetAsync(ddeg, 0, (N + 1) * 4, B.s));
-    hipLaunchKernelGGL(k_rp_scatter_deg, dim3(rgrid((uint64_t)G * npad)), dim3(RB), 0, B.s, gdeg, g2d,
+    for (int q = 0; q < G; ++q) RB_TRY(scan(gdeg + (uint64_t)q * npad, goff + (uint64_t)q * npad, npad));
+    RB_TRY(hipMemsetAsync(ddeg, 0, (N + 1) * 4, st));
+    hipLaunchKernelGGL(k_rp_scatter_deg, dim3(rgrid((uint64_t)G * npad)), dim3(RB), 0, st, gdeg, g2d,
                        (uint64_t)G * npad, ddeg);
     RB_TRY(hipGetLastError());
-    DevEdgeType dt;
-    dt.type = t;
-    dt.num_edges = etot[k];
-    RB_TRY(B.keep(&dt.row_ptr, N + 1, &owned));
-    RB_TRY(B.scan(ddeg, dt.row_ptr, N + 1));   // row_ptr[N] = the total (ddeg[N] == 0)
-    RB_TRY(B.keep(&dt.col, etot[k], &owned));
-    RB_TRY(B.keep(&dt.dst_vid, etot[k], &owned));
-    if (any_rank) RB_TRY(B.keep(&dt.rank, etot[k], &owned));
-    RB_TRY(hipMemcpyAsync(d_ecnt, ecount[k].data(), G * 8, hipMemcpyHostToDevice, B.s));
+    RB_TRY(scan(ddeg, dt.row_ptr, N + 1));   // row_ptr[N] = the total (ddeg[N] == 0)
+    RB_TRY(hipMemcpyAsync(d_ecnt, ecount[k].data(), G * 8, hipMemcpyHostToDevice, st));
     uint64_t emax = 0;
     for (uint64_t c : ecount[k]) emax = std::max(emax, c);
     const uint64_t mine = lt ? lt->num_edges : 0;
     for (uint64_t k0 = 0; k0 < emax; k0 += CHUNK) {
       const uint64_t n = k0 < mine ? std::min<uint64_t>(CHUNK, mine - k0) : 0;
       if (n) {
-        RB_TRY(hipMemcpyAsync(s_col, lt->col + k0, n * 4, hipMemcpyDeviceToDevice, B.s));
-        RB_TRY(hipMemcpyAsync(s_dst, lt->dst_vid + k0, n * 8, hipMemcpyDeviceToDevice, B.s));
+        RB_TRY(hipMemcpyAsync(s_col, lt->col + k0, n * 4, hipMemcpyDeviceToDevice, st));
+        RB_TRY(hipMemcpyAsync(s_dst, lt->dst_vid + k0, n * 8, hipMemcpyDeviceToDevice, st));
         if (any_rank) {
-          if (lt->rank) RB_TRY(hipMemcpyAsync(s_rank, lt->rank + k0, n * 8, hipMemcpyDeviceToDevice, B.s));
-          else RB_TRY(hipMemsetAsync(s_rank, 0, n * 8, B.s));
+          if (lt->rank) RB_TRY(hipMemcpyAsync(s_rank, lt->rank + k0, n * 8, hipMemcpyDeviceToDevice, st));
+          else RB_TRY(hipMemsetAsync(s_rank, 0, n * 8, st));
         }
       }
       RB_TRY(B.gather(s_col, r_col, CHUNK * 4));
@@ -410,63 +480,40 @@ int32_t build_path_replica(Engine& E) {
       a.out_col = dt.col;
       a.out_dst = dt.dst_vid;
       a.out_rank = dt.rank;
-      hipLaunchKernelGGL(k_rp_place, dim3(rgrid((uint64_t)G * CHUNK)), dim3(RB), 0, B.s, a);
+      hipLaunchKernelGGL(k_rp_place, dim3(rgrid((uint64_t)G * CHUNK)), dim3(RB), 0, st, a);
       RB_TRY(hipGetLastError());
     }
     dt.h_row_ptr.resize(N + 1);
-    RB_TRY(hipMemcpyAsync(dt.h_row_ptr.data(), dt.row_ptr, (N + 1) * 4, hipMemcpyDeviceToHost, B.s));
-    RB_TRY(hipStreamSynchronize(B.s));
+    RB_TRY(hipMemcpyAsync(dt.h_row_ptr.data(), dt.row_ptr, (N + 1) * 4, hipMemcpyDeviceToHost, st));
+    RB_TRY(hipStreamSynchronize(st));
     uint32_t md = 0;
     for (uint64_t v = 0; v < N; ++v) md = std::max(md, dt.h_row_ptr[v + 1] - dt.h_row_ptr[v]);
     dt.max_degree = (int)md;
-    rs.types[t] = std::move(dt);
     rs.device_bytes += (N + 1) * 4 + etot[k] * (12 + (any_rank ? 8 : 0));
   }
-  // ---- 3. visibility
-  {
-    uint8_t *lvis = nullptr, *gvis = nullptr;
-    RB_TRY(B.get(&lvis, npad));
-    RB_TRY(B.get(&gvis, (uint64_t)G * npad));
-    hipLaunchKernelGGL(k_rp_vis_local, dim3(rgrid(npad)), dim3(RB), 0, B.s, E.snap.d_visible, E.snap.nv, npad, lvis);
+  // 3c. visibility
+  if (hidden_all) {
+    hipLaunchKernelGGL(k_rp_vis_local, dim3(rgrid(npad)), dim3(RB), 0, st, E.snap.d_visible, E.snap.nv, npad, lvis);
     RB_TRY(hipGetLastError());
     RB_TRY(B.gather(lvis, gvis, npad));
-    std::vector<uint64_t> any_hidden;
-    uint64_t hidden = 0;
-    if (!E.snap.h_visible.empty())
-      for (uint8_t v : E.snap.h_visible) hidden += v == 0;
-    if (B.host_all<uint64_t>(hidden, &any_hidden) != hipSuccess) return bail(hipErrorUnknown);
-    hidden = 0;
-    for (uint64_t x : any_hidden) hidden += x;
-    if (hidden) {
-      RB_TRY(B.keep(&rs.d_visible, N, &owned));
-      hipLaunchKernelGGL(k_rp_vis, dim3(rgrid((uint64_t)G * npad)), dim3(RB), 0, B.s, gvis, g2d, (uint64_t)G * npad,
-                         rs.d_visible);
-      RB_TRY(hipGetLastError());
-      rs.h_visible.resize(N);
-      RB_TRY(hipMemcpyAsync(rs.h_visible.data(), rs.d_visible, N, hipMemcpyDeviceToHost, B.s));
-    }
+    rs.d_visible = rvis;
+    hipLaunchKernelGGL(k_rp_vis, dim3(rgrid((uint64_t)G * npad)), dim3(RB), 0, st, gvis, g2d, (uint64_t)G * npad, rvis);
+    RB_TRY(hipGetLastError());
+    rs.h_visible.resize(N);
+    RB_TRY(hipMemcpyAsync(rs.h_visible.data(), rvis, N, hipMemcpyDeviceToHost, st));
   }
-  RB_TRY(hipStreamSynchronize(B.s));
+  RB_TRY(hipStreamSynchronize(st));
 #undef RB_TRY
-  owned.clear();   // the snapshot holds them now
+  for (size_t k = 0; k < types.size(); ++k) rs.types[types[k]] = std::move(dts[k]);
+  B.kept.clear();   // the snapshot holds them now
   rs.device_bytes += N * 9;
-  // ---- the replica engine: a single-GPU engine over the replica snapshot (no props, no tags)
-  R->cfg = E.cfg;
-  R->cfg.num_gpus = 1;
-  R->cfg.rank = 0;
+  // ---- the replica engine: a single-GPU engine over the replica snapshot (no props, no tags);
+  //      its workspace was made in step 2 (engine_ready's only step for a single engine)
   R->edges = E.edges;
   R->tags = E.tags;
   R->prof_mode = E.prof_mode;
   R->finalized = true;
-  if (hipStreamCreateWithFlags(&R->stream, hipStreamNonBlocking) != hipSuccess) {
-    R->free_snapshot();
-    return E.fail(NBG_E_DEVICE, "replica stream");
-  }
-  if (int32_t rc = engine_ready(*R)) {
-    R->free_snapshot();
-    (void)hipStreamDestroy(R->stream);
-    return E.fail(rc, "path replica workspace: " + R->last_error);
-  }
+  R->err_parent = &E;
   E.rep = std::move(R);
   return NBG_OK;
 }

@@ -580,9 +580,49 @@ uint64_t all_walks(const Csr& g, int64_t sv, int64_t tv, uint32_t upto, int64_t*
   return n;
 }
 
+// Per-rank load of GO `steps` STEPS from each start (one query per start), for the partition
+// part = (uint64)vid % parts + 1 (NebulaKeyUtils / StorageClient::partId), rank = part % G
+// (CreateSpaceProcessor.cpp:84-95 with GPUs as hosts).  A step's edges are scanned at the frontier
+// vertex's part, so out[((q * steps) + s) * G + r] = edges that rank r scans in step s of query q.
+void rank_edges(const Csr& g, const int64_t* starts, uint64_t ns, uint32_t steps, uint32_t parts, uint32_t G,
+                uint64_t* out) {
+  std::vector<uint8_t> owner(g.nv);
+#pragma omp parallel for schedule(static) num_threads(g.threads)
+  for (int64_t d = 0; d < (int64_t)g.nv; ++d) owner[d] = (uint8_t)(((uint64_t)g.vid[d] % parts + 1) % G);
+  std::vector<uint64_t> bits((g.nv + 63) / 64);
+  for (uint64_t q = 0; q < ns; ++q) {
+    uint64_t* o = out + q * steps * G;
+    std::fill(o, o + (uint64_t)steps * G, 0);
+    std::vector<uint32_t> f;
+    const int64_t d0 = g.dense(starts[q]);
+    if (d0 >= 0) f.push_back((uint32_t)d0);
+    for (uint32_t s = 0; s < steps && !f.empty(); ++s) {
+      std::vector<uint64_t> per(G, 0);
+      for (uint32_t v : f) per[owner[v]] += g.off[v + 1] - g.off[v];
+      for (uint32_t r = 0; r < G; ++r) o[s * G + r] = per[r];
+      if (s + 1 == steps) break;
+      std::fill(bits.begin(), bits.end(), 0);
+#pragma omp parallel for schedule(dynamic, 64) num_threads(g.threads)
+      for (int64_t k = 0; k < (int64_t)f.size(); ++k)
+        for (uint64_t j = g.off[f[k]]; j < g.off[f[k] + 1]; ++j) {
+          const uint32_t u = g.nbr[j];
+          __atomic_fetch_or(&bits[u >> 6], 1ull << (u & 63), __ATOMIC_RELAXED);
+        }
+      f.clear();
+      for (uint64_t wd = 0; wd < bits.size(); ++wd)
+        for (uint64_t b = bits[wd]; b; b &= b - 1) f.push_back((uint32_t)(wd * 64 + __builtin_ctzll(b)));
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+void orc_csr_rank_edges(void* h, const int64_t* starts, uint64_t ns, uint32_t steps, uint32_t parts, uint32_t G,
+                        uint64_t* out) {
+  rank_edges(*static_cast<Csr*>(h), starts, ns, steps, parts, G, out);
+}
 
 // GO steps STEPS FROM starts OVER the nt types (one Csr each), default YIELD: out4 as orc_csr_go
 double orc_csr_go_multi(void* const* hs, int32_t nt, const int64_t* starts, uint64_t ns, uint32_t steps,

@@ -152,7 +152,51 @@ int cmpSame(const Value& l, const Value& r) {
   }
 }
 
+// Expression::toString (Expressions.h:274-288); folly's double formatting is not restated
+bool toStr(const Value& v, std::string* out) {
+  switch (v.index()) {
+    case 0: *out = std::to_string(std::get<0>(v)); return true;
+    case 2: *out = std::get<2>(v) ? "true" : "false"; return true;
+    case 3: *out = std::get<3>(v); return true;
+    default: return false;
+  }
+}
+
 }  // namespace
+
+// FunctionManager's bodies (FunctionManager.cpp): the exact double math functions and udf_is_in
+// (:440-486, std::unordered_set membership after converting every candidate to the comparand's
+// alternative).  Other functions are not restated.
+OptValue callFunction(const std::string& f, const std::vector<Value>& av) {
+  static const char* math[] = {"abs", "floor", "ceil", "round", "sqrt"};
+  for (int i = 0; i < 5; ++i) {
+    if (f != math[i]) continue;
+    if (av.size() != 1) return Status::Err("Arity not match");
+    if (!isArith(av[0])) return Status::Err("asDouble of a non-number");   // boost::bad_get
+    const double x = asDouble(av[0]);
+    return Value(i == 0 ? std::fabs(x) : i == 1 ? std::floor(x) : i == 2 ? std::ceil(x) : i == 3 ? std::round(x)
+                                                                                                  : std::sqrt(x));
+  }
+  if (f != "udf_is_in") return Status::Err("function not restated by this oracle");
+  if (av.size() < 2) return Status::Err("Arity not match");
+  const Value& cmp = av[0];
+  bool found = false;
+  for (size_t i = 1; i < av.size(); ++i) {
+    bool ok = true;
+    switch (cmp.index()) {
+      case 0: { int64_t x = toInt(av[i], ok); found = found || (ok && x == std::get<0>(cmp)); break; }
+      case 1: { double x = toDouble(av[i], ok); found = found || (ok && x == std::get<1>(cmp)); break; }
+      case 2: found = found || asBool(av[i]) == std::get<2>(cmp); break;
+      default: {
+        std::string x;
+        ok = toStr(av[i], &x);
+        found = found || (ok && x == std::get<3>(cmp));
+      }
+    }
+    if (!ok) return Status::Err("conversion failed");   // folly::to throws
+  }
+  return Value(found);
+}
 
 bool asBool(const Value& v) {   // Expressions.h:228-241 (string -> empty())
   switch (v.index()) {
@@ -180,7 +224,15 @@ OptValue Expr::eval(Getters& g) const {
     case kSourceProp: return g.srcTagProp(alias, prop);         // :429-431
     case kDestProp: return g.dstTagProp(alias, prop);           // :217-219
     case kInputProp: case kVariableProp: return g.inputProp(prop);   // GoExecutor.cpp:932-945
-    case kFunctionCall: return Status::Err("function calls are not supported by this oracle");
+    case kFunctionCall: {   // FunctionCallExpression::eval (:589-603): arguments first, then the body
+      std::vector<Value> av;
+      for (auto& x : args) {
+        auto v = x->eval(g);
+        if (!v.ok()) return v;
+        av.push_back(v.v);
+      }
+      return callFunction(alias, av);
+    }
     case kUnary: {        // UnaryExpression::eval (:698-716)
       auto v = a->eval(g);
       if (v.ok()) {

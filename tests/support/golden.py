@@ -10,7 +10,6 @@ GOLDEN = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))
 
 # Cases whose features are outside the hot path this build covers (documented in DESIGN.md).
 UNSUPPORTED = (
-    ("udf_is_in", "function calls (FunctionManager) are rejected by the storage filter and out of scope"),
     ("REVERSELY", "REVERSELY is rejected by the reference GoExecutor (GoExecutor.cpp:243-246)"),
 )
 

@@ -334,6 +334,7 @@ class CsrOracle:
         L.orc_csr_walk_counts.argtypes = [vp, i64, i64, u32, vp]
         L.orc_csr_all_walks.restype = u64
         L.orc_csr_all_walks.argtypes = [vp, i64, i64, u32, vp, u64]
+        L.orc_csr_rank_edges.argtypes = [vp, vp, u64, u32, u32, u32, vp]
         self.L = L
         src = np.ascontiguousarray(src, np.int64)
         dst = np.ascontiguousarray(dst, np.int64)
@@ -386,6 +387,14 @@ class CsrOracle:
         out = np.zeros(4, np.uint64)
         csrs[0].L.orc_csr_go_multi(hs, len(csrs), _ptr(s), len(s), steps, _ptr(out))
         return (int(out[0]), int(out[1]), int(out[2])), int(out[3])
+
+    def rank_edges(self, starts, steps, parts, world):
+        """Edges each rank scans per step when every start is its own GO `steps` STEPS query on
+        `world` ranks holding parts p % world: -> uint64 [len(starts), steps, world]."""
+        s = np.asarray(starts, np.int64)
+        out = np.zeros((len(s), steps, world), np.uint64)
+        self.L.orc_csr_rank_edges(self.h, _ptr(s), len(s), steps, parts, world, _ptr(out))
+        return out
 
     def walk_counts(self, s, t, upto):
         """Walks s -> t of exactly L edges for L = 0..upto (FIND ALL PATH's answer size per length)."""

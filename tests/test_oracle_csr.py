@@ -142,3 +142,28 @@ def test_csr_multi_type_go_and_walks_match_faithful_oracle():
         orc.close()
         ck.close()
         cl.close()
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_rank_edges_partition_the_scanned_edges(pair, world):
+    """orc_csr_rank_edges (bench partition_load): per (query, step, rank) edges add up to the
+    query's scanned edges, and a brute-force restatement of the owner rule ((vid % P + 1) % G)
+    over the faithful oracle's per-step frontiers gives the same split."""
+    scale, src, dst, orc, csr = pair
+    roots = graphs.roots(src, 4, seed=world)
+    t = csr.rank_edges(roots, 3, 100, world)
+    assert t.shape == (4, 3, world)
+    pairs = np.unique(np.stack([src, dst], axis=1), axis=0)
+    adj = {}
+    for s_, d_ in pairs.tolist():
+        adj.setdefault(s_, []).append(d_)
+    for q, r in enumerate(roots):
+        _, sc, _, _ = csr.go([r], 3)
+        assert int(t[q].sum()) == sc
+        f = {r}
+        for s in range(3):
+            exp = [0] * world
+            for v in f:
+                exp[((v % (1 << 64)) % 100 + 1) % world] += len(adj.get(v, ()))
+            assert [int(x) for x in t[q, s]] == exp, (q, s)
+            f = {u for v in f for u in adj.get(v, ())}

@@ -1,0 +1,84 @@
+#!/bin/bash
+# Round-4 GPU-box steps (from the repo root, via gpurun): bash tools/gpu_r04.sh <tag> <step>...
+#   tests  — pytest -m gpu;  load26 — RMAT-26 generate + load + GO leg only (load time);
+#   bench  — default bench.py
+set -u
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+TAG=$1; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+for step in "$@"; do
+  case $step in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        > "$OUT/pytest_gpu.log" 2>&1 || { tail -40 "$OUT/pytest_gpu.log"; exit 1; } ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+        || { tail -20 "$OUT/smoke.log"; exit 1; } ;;
+    configs)
+      timeout -k 10 1100 python -u -m pytest tests/test_gpu_configs.py -x -v --timeout 1200 --timeout-method thread \
+        > "$OUT/pytest_configs.log" 2>&1 || { tail -40 "$OUT/pytest_configs.log"; exit 1; } ;;
+    load26)
+      timeout -k 10 900 python -u bench.py --scale 26 --roots 16 --steps 2 --sp-pairs 0 --no-cpu-baseline \
+        --c5-scale 0 --getbound-reqs 0 --no-profile > "$OUT/load26.json" 2> "$OUT/load26.log" \
+        || { tail -30 "$OUT/load26.log"; exit 1; } ;;
+    pmc26|pmc22)
+      sc=${step#pmc}
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 400 rocprofv3 --pmc $c -d "$OUT/pmc${sc}_$c" -o run --output-format csv -- \
+          python3 -u bench.py --scale $sc --steps 1 --warmup 1 --sp-pairs 0 --no-cpu-baseline --no-profile \
+          --verify 0 --c2 0 --c5-scale 0 --getbound-reqs 0 --c1-reqs 0 > "$OUT/pmc${sc}_$c.json" 2> "$OUT/pmc${sc}_$c.log" \
+          || { tail -30 "$OUT/pmc${sc}_$c.log"; exit 1; }
+      done
+      python3 tools/pmc_summary.py $(find "$OUT/pmc${sc}_FETCH_SIZE" "$OUT/pmc${sc}_WRITE_SIZE" -name '*counter_collection.csv') \
+        > "$OUT/pmc_hbm_rmat${sc}.json" ;;
+    prof26)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof26" -o run --output-format csv -- \
+        python3 -u bench.py --sp-pairs 2000 --no-cpu-baseline --verify 0 --c2 0 --c5-scale 0 --getbound-reqs 0 --c1-reqs 0 \
+        > "$OUT/bench_prof26.json" 2> "$OUT/bench_prof26.log" || { tail -30 "$OUT/bench_prof26.log"; exit 1; } ;;
+    go26|go26flags)
+      [ "$step" = go26flags ] && export NBG_MARK_FLAGS=1
+      timeout -k 10 600 python -u bench.py --sp-pairs 0 --no-cpu-baseline --verify 4 --c2 0 --c5-scale 0 \
+        --getbound-reqs 0 > "$OUT/$step.json" 2> "$OUT/$step.log" || { tail -30 "$OUT/$step.log"; exit 1; }
+      unset NBG_MARK_FLAGS ;;
+    ptest)
+      timeout -k 10 400 python -u -m pytest tests/test_gpu_path.py tests/test_gpu_configs.py -x -v --timeout 300 \
+        --timeout-method thread > "$OUT/pytest_path.log" 2>&1 || { tail -40 "$OUT/pytest_path.log"; exit 1; } ;;
+    sp26|sp26host)
+      [ "$step" = sp26host ] && export NBG_SP_MODE=host
+      timeout -k 10 600 python -u bench.py --steps 1 --warmup 1 --no-profile --no-cpu-baseline --verify 4 --c2 0 \
+        --c5-scale 0 --getbound-reqs 0 > "$OUT/$step.json" 2> "$OUT/$step.log" || { tail -30 "$OUT/$step.log"; exit 1; }
+      unset NBG_SP_MODE ;;
+    probe22|probe26)
+      sc=${step#probe}
+      timeout -k 10 300 python -u tools/sp_probe.py $sc 4000 > "$OUT/$step.txt" 2>&1 \
+        || { tail -30 "$OUT/$step.txt"; exit 1; }
+      NBG_SP_MODE=host timeout -k 10 300 python -u tools/sp_probe.py $sc 4000 > "$OUT/${step}_legacy.txt" 2>&1 \
+        || { tail -30 "$OUT/${step}_legacy.txt"; exit 1; } ;;
+    spprof26)   # kernel trace of the one-pair SP queries (default path)
+      timeout -k 10 600 rocprofv3 --kernel-trace -d "$OUT/spprof26" -o run --output-format csv -- \
+        python3 -u tools/sp_probe.py 26 400 > "$OUT/spprof26.txt" 2>&1 || { tail -30 "$OUT/spprof26.txt"; exit 1; } ;;
+    wgs26)   # persistent SP: workgroup-count sweep
+      for w in 1 8 32 64 128; do
+        NBG_SP_PERSISTENT=1 NBG_SP_WGS=$w NBG_SP_TRACE=1 timeout -k 10 300 python -u tools/sp_probe.py 26 1500 > "$OUT/wgs26_$w.txt" 2>&1 \
+          || { tail -30 "$OUT/wgs26_$w.txt"; exit 1; }
+      done ;;
+    p8)   # the 8-way partition, in-process ranks on one GPU
+      timeout -k 10 900 python -u -m pytest tests/test_gpu_partition8.py -x -v --timeout 300 --timeout-method thread \
+        > "$OUT/pytest_partition8.log" 2>&1 || { tail -40 "$OUT/pytest_partition8.log"; exit 1; } ;;
+    rccl8)   # 8 RCCL processes on one GPU (socket transport)
+      timeout -k 10 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29511 tools/rccl_probe.py --same-device > "$OUT/rccl8_probe.log" 2>&1 \
+        || { tail -40 "$OUT/rccl8_probe.log"; exit 1; } ;;
+    bench8)   # 8-rank bench rehearsal on one GPU (RMAT-20, socket transport)
+      NBG_SAME_DEVICE=1 timeout -k 10 900 python -u bench.py --gpus 8 --scale 20 --sp-pairs 2000 \
+        > "$OUT/bench8_rmat20_same_device.json" 2> "$OUT/bench8.log" || { tail -40 "$OUT/bench8.log"; exit 1; } ;;
+    pytest:*)   # one test file or node id
+      t=${step#pytest:}; n=$(basename "${t%%::*}" .py)
+      timeout -k 10 900 python -u -m pytest "$t" -x -v --timeout 300 --timeout-method thread \
+        > "$OUT/pytest_$n.log" 2>&1 || { tail -40 "$OUT/pytest_$n.log"; exit 1; } ;;
+    bench)
+      timeout -k 10 900 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.log" || { tail -30 "$OUT/bench.log"; exit 1; } ;;
+  esac
+  echo "step $step done"
+done

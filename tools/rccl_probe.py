@@ -151,6 +151,30 @@ def main():
         good = all(p == single.find_path([s0], [t0], [1], 5) for p in parts)
         ok &= good
         print(f"after the failures: FIND PATH {'OK' if good else 'MISMATCH'}", flush=True)
+    # (5) nbg_go_submit cannot create its slot stream on the last rank only: a plain
+    #     GO carries the failure in band (the peers' wait fails), a YIELD DISTINCT agrees before
+    #     the query (the peers' submit fails); either way every rank reports E_DEVICE, the
+    #     collective sequences match, and the next query runs
+    for distinct in (False, True):
+        yd = [E.edge_prop("e", "_dst").encode()] if distinct else ()
+        st5 = eng.prepare_go([1], 3, where, yd, distinct=distinct)
+        if rank == world - 1:
+            eng.lib.nbg_inject_fault(eng.h, L.FAULT_STREAM, 1)
+
+        def submit_wait():
+            st5.wait(st5.submit([r0], device=False)).free()
+        agreed(f"slot stream (GO{' DISTINCT' if distinct else ''})", code_of(submit_wait), L.E_DEVICE)
+        res = st5.wait(st5.submit([r0], device=False))
+        mine = res.fetch()
+        res.free()
+        st5.free()
+        parts = [None] * world
+        dist.all_gather_object(parts, mine)
+        if rank == 0:
+            good = graphs.sorted_rows([row for p in parts for row in p]) == \
+                graphs.sorted_rows(single.go([r0], [1], 3, where, yd, distinct=distinct))
+            ok &= good
+            print(f"after the stream failure (distinct={distinct}): GO {'OK' if good else 'MISMATCH'}", flush=True)
     dist.barrier()
     if rank == 0:
         print("RCCL partitioned probe:", "PASS" if ok else "FAIL", flush=True)
