@@ -3,7 +3,8 @@
 // Same semantics and result as path.cpp's bidirectional() (FindPathExecutor.cpp:173-290
 // restated: minimal hop count, UPTO N, one path per target, ties broken by the lexicographically
 // smallest entry list [v0, t0, r0, v1, ...]).  The host enqueues a chain per pair —
-//   k_ch_setup, K x k_ch_step, H x k_ch_hop, k_ch_out (the result into mapped host memory) —
+//   K x k_ch_step (the first starts the search), H x k_ch_hop (the last stores the result into
+//   mapped host memory; k_ch_out when a continuation has no hop launch) —
 // and waits once.  Step launch i derives what it does from the state snapshot of launch i - 1
 // (snap[i - 1]) and that launch's results (its output-list and meet counters, lacc / lmeet[i - 1]),
 // which are final at the launch boundary: the BFS level loop (direction = the side with the
@@ -86,13 +87,23 @@ struct ChSnap {         // the search state before one step launch
                                        // vertex appended, for every level and B-set step)
 };
 
-struct ChState {        // device; the host reads what k_ch_out derives from it (ChOut)
+// A query's counters.  Two sets, used by alternate queries of a context (ChQ::par): the launch
+// that writes a query's result zeroes the OTHER set — the next query's — so the next query needs
+// no set-up launch, and nothing of the current query (whose workgroups may still be reading its
+// own set) is touched.
+struct ChCtr {
   unsigned long long lacc[CH_MAXS];    // packed output list of step launch i
   unsigned long long lmeet[CH_MAXS];   // meet vertices found by step launch i
   unsigned long long macc;             // packed meet list (over in-edges)
   unsigned long long err;              // 1 reconstruction failure, 3 list overflow
-  unsigned long long gticket;          // greedy hop: workgroups done (the last one reduces)
   unsigned long long hlaunch;          // greedy launches that did work
+  unsigned long long busy;             // step launches that ran a step
+};
+
+struct ChState {        // device; the host reads what the result launch derives from it (ChOut)
+  ChCtr c[2];
+  unsigned long long gerr;             // CH_GUARD builds: bit 8 + site of a bounds violation
+  unsigned long long gticket;          // greedy hop: workgroups done (the last one reduces, resets)
   // greedy launch h starts from hstart[h] = (position << 32 | current vertex) and exactly one of
   // its workgroups writes hstart[h + 1]: state that no launch mutates while its own workgroups
   // may still read it (workgroups of one launch start at different times)
@@ -101,7 +112,6 @@ struct ChState {        // device; the host reads what k_ch_out derives from it 
   // first[i + 1]: one step, several (a workgroup alone runs small steps back to back, ChQ::solo)
   // or none (the search is over)
   unsigned long long first[CH_MAXS + 1];
-  unsigned long long busy;             // step launches that ran a step
   ChSnap snap[CH_MAXS];
   long long path[1 + 3 * MAX_PATH_LEN];
   unsigned long long gpart[4 * CH_HOP_WGS];
@@ -139,6 +149,7 @@ struct ChQ {
   uint32_t ef, eb, em;
   uint32_t solo;                       // a step over at most this many items (entries + edges) is run
                                        // by workgroup 0 alone, which goes on with the next step (0: off)
+  uint32_t par;                        // the query's counter set (ChState::c)
 };
 
 // The state after step launch `i` (snapshot p before it, its results from st): every step launch
@@ -226,7 +237,7 @@ namespace {
 template <typename T>
 __device__ __forceinline__ T gld(const T* p, uint64_t i, uint64_t n, int site, ChState* st) {
   if (CH_GUARD && i >= n) {
-    atomicOr(&st->err, 1ull << (8 + site));
+    atomicOr(&st->gerr, 1ull << (8 + site));
     return T(0);
   }
   return p[i];
@@ -234,7 +245,7 @@ __device__ __forceinline__ T gld(const T* p, uint64_t i, uint64_t n, int site, C
 template <typename T>
 __device__ __forceinline__ void gst(T* p, uint64_t i, uint64_t n, T v, int site, ChState* st) {
   if (CH_GUARD && i >= n) {
-    atomicOr(&st->err, 1ull << (8 + site));
+    atomicOr(&st->gerr, 1ull << (8 + site));
     return;
   }
   p[i] = v;
@@ -320,8 +331,8 @@ __device__ __forceinline__ void list_put(const ChArgs& A, const ChList& L, uint3
 // list L (counter *acc): one packed atomic per wave for positions and edge offsets; the tile
 // splits of hubs (entries spanning many tiles) are written by the whole wave, lane-strided.
 __device__ __forceinline__ void wave_append(const ChArgs& A, const ChList& L, unsigned long long* acc,
-                                            const uint32_t (&x)[CH_VT], uint32_t m, const uint32_t (&dg)[CH_VT],
-                                            const uint32_t (&rs)[CH_VT]) {
+                                            unsigned long long* err, const uint32_t (&x)[CH_VT], uint32_t m,
+                                            const uint32_t (&dg)[CH_VT], const uint32_t (&rs)[CH_VT]) {
   const int lane = threadIdx.x & 63;
   uint32_t c = 0, d = 0;
 #pragma unroll
@@ -337,7 +348,7 @@ __device__ __forceinline__ void wave_append(const ChArgs& A, const ChList& L, un
   if (lane == 0) old = atomicAdd(acc, ((unsigned long long)tc << 32) | td);
   old = __shfl(old, 0, 64);
   if ((old >> 32) + tc > A.list_cap) {
-    if (lane == 0) atomicOr(&A.st->err, 3ull);
+    if (lane == 0) atomicOr(err, 3ull);
     return;
   }
   uint32_t pos = (uint32_t)(old >> 32) + ic - c;
@@ -362,44 +373,50 @@ __device__ __forceinline__ void wave_append(const ChArgs& A, const ChList& L, un
 }
 
 // The snapshot step i runs under: snap[0] (set-up) or derived from step i - 1.
-__device__ __forceinline__ ChSnap snap_for(const ChState* st, int i, uint32_t upto) {
+__device__ __forceinline__ ChSnap snap_for(const ChState* st, const ChQ& q, int i) {
   if (i == 0) return st->snap[0];
-  return ch_advance(st->snap[i - 1], st->lacc[i - 1], st->lmeet[i - 1], st->macc, st->err, upto);
+  const ChCtr& C = st->c[q.par];
+  return ch_advance(st->snap[i - 1], C.lacc[i - 1], C.lmeet[i - 1], C.macc, C.err, q.upto);
 }
 
 }  // namespace
 
-// Set-up (one workgroup): the state block, the labels of s and t, the one-entry lists {s}, {t}.
-__device__ __forceinline__ void ch_setup(const ChArgs& A, const ChQ& q) {
-  ChState* st = A.st;
-  uint32_t rsf, rsb;
-  const uint32_t dsf = vdeg(A, 0, q.s, &rsf), dsb = vdeg(A, 1, q.t, &rsb);
-  for (uint64_t t = threadIdx.x; t * CH_TILE <= dsf && t < A.tsplit_cap; t += CH_BLOCK) A.list[CL_F0].tsplit[t] = 0;
-  for (uint64_t t = threadIdx.x; t * CH_TILE <= dsb && t < A.tsplit_cap; t += CH_BLOCK) A.list[CL_B0].tsplit[t] = 0;
-  for (int i = threadIdx.x; i < CH_MAXS; i += CH_BLOCK) {
-    st->lacc[i] = 0;
-    st->lmeet[i] = 0;
-  }
-  if (threadIdx.x != 0) return;
-  st->macc = st->err = st->gticket = st->hlaunch = st->busy = 0;
-  st->first[0] = 0;
+// The first step needs no set-up launch: every workgroup of step launch 0 derives the search's
+// start from (s, t) — the one-entry lists {s}, {t} are the registers below, not list memory, and
+// s / t count as labelled (level 0 of their side) before workgroup 0 stores their labels — and
+// workgroup 0 stores what later launches read: the labels of s and t, the lists {s} and {t} (the
+// B-set steps and the greedy read them), snapshot 0, the greedy's start.  The counters are zero
+// (the previous query's result launch zeroed this query's set; chain_prepare does it after a
+// query that did not finish).
+struct ChFirst {
+  uint32_t dsf, rsf, dsb, rsb;   // degree and row start of s (forward) and t (backward)
+};
+
+__device__ __forceinline__ ChSnap first_snap(const ChArgs& A, const ChQ& q, ChFirst* f) {
+  f->dsf = vdeg_spec(A, 0, q.s, &f->rsf);
+  f->dsb = vdeg_spec(A, 1, q.t, &f->rsb);
   ChSnap s;
   memset(&s, 0, sizeof(s));
-  s.phase = dsf && dsb ? PH_BFS : PH_DONE;
-  s.dir = dsf <= dsb ? 0u : 1u;
-  s.cnt[0] = (1ull << 32) | dsf;
-  s.cnt[1] = (1ull << 32) | dsb;
+  s.phase = f->dsf && f->dsb ? PH_BFS : PH_DONE;
+  s.dir = f->dsf <= f->dsb ? 0u : 1u;
+  s.cnt[0] = (1ull << 32) | f->dsf;
+  s.cnt[1] = (1ull << 32) | f->dsb;
+  return s;
+}
+
+__device__ __forceinline__ void first_store(const ChArgs& A, const ChQ& q, const ChFirst& f, const ChSnap& s) {
+  ChState* st = A.st;
   st->snap[0] = s;
   A.lab[0][q.s] = stamp_of(q.ef, 0);
   A.lab[1][q.t] = stamp_of(q.eb, 0);
   const ChList& F = A.list[CL_F0];
   F.ids[0] = q.s;
-  F.seg_end[0] = dsf;
-  F.seg_rs[0] = rsf;
+  F.seg_end[0] = f.dsf;
+  F.seg_rs[0] = f.rsf;
   const ChList& B = A.list[CL_B0];
   B.ids[0] = q.t;
-  B.seg_end[0] = dsb;
-  B.seg_rs[0] = rsb;
+  B.seg_end[0] = f.dsb;
+  B.seg_rs[0] = f.rsb;
   st->hstart[0] = q.s;   // position 0, vertex s
   st->path[0] = gld(A.vids, q.s, A.nv, 16, st);
 }
@@ -412,9 +429,10 @@ __device__ __forceinline__ void ch_setup(const ChArgs& A, const ChQ& q) {
 //     B[kf - k], claimed in LAB_M (push: in-edges of B[kf - k]; pull, k == 0 only: out-edges of
 //     forward level kf - 1).
 // (bid, nblk: this workgroup among the query's workgroups of the launch; NW waves per workgroup)
+// (first: step 0, whose source list {s} or {t} is f's registers)
 template <int NW>
 __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const ChSnap& P, int i, uint32_t bid,
-                                         uint32_t nblk) {
+                                         uint32_t nblk, const ChFirst* first) {
   __shared__ uint32_t sEndAll[NW][CH_TILE + 2];
   __shared__ uint32_t sRsAll[NW][CH_TILE + 1];
   __shared__ uint16_t sSegAll[NW][CH_TILE];
@@ -469,7 +487,13 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
     }
   }
   const bool pull = tlab != nullptr;
-  unsigned long long* const out_acc = &st->lacc[i];
+  ChCtr& C = st->c[q.par];
+  unsigned long long* const out_acc = &C.lacc[i];
+  // step 0: the one entry of the source list (s forward, t backward) from registers; s and t are
+  // labelled level 0 of their sides (workgroup 0 stores those labels during this launch)
+  const uint32_t f_deg = first ? (side ? first->dsb : first->dsf) : 0u;
+  const uint32_t f_rs = first ? (side ? first->rsb : first->rsf) : 0u;
+  const uint32_t f_own = first ? (side ? q.t : q.s) : NO_ROW, f_other = first ? (side ? q.s : q.t) : NO_ROW;
   const uint64_t n = scnt >> 32, total = scnt & 0xFFFFFFFFull;
   const uint32_t* __restrict__ col = A.col[side];
   const uint64_t npath = n + total, ntiles = (npath + CH_TILE - 1) / CH_TILE;
@@ -494,10 +518,12 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
     uint32_t cm = 0, mm = 0;
     // once this level has met, its claims are not expanded again: their appends are skipped
     // (read now, used after the claims: the load is off the critical path)
-    const unsigned long long met_now = bfs ? ld_agent(&st->lmeet[i]) : 0ull;
+    const unsigned long long met_now = bfs ? ld_agent(&C.lmeet[i]) : 0ull;
     CH_PH(0);
     uint64_t sp = 0;
-    if (ntiles > 1) {
+    if (first) {   // one entry: every tile's split is 0, the last tile's end is 1
+      sp = lane == 1 && (t + 1) * CH_TILE >= npath ? n : 0;
+    } else if (ntiles > 1) {
       if (lane == 0) sp = gld(S.tsplit, t, A.tsplit_cap, 3, st);
       if (lane == 1) sp = (t + 1) * CH_TILE >= npath ? n : gld(S.tsplit, t + 1, A.tsplit_cap, 3, st);
     } else {
@@ -510,8 +536,13 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
     // the tile's window: sEnd[k] = seg_end[a0 - 1 + k], sRs[k] = seg_rs[a0 + k]
     for (int kk = lane; kk <= na + 1; kk += 64) {
       const int64_t e = (int64_t)a0 - 1 + kk;
-      sEnd[kk] = e < 0 ? 0u : (e < (int64_t)n ? gld(S.seg_end, (uint64_t)e, A.list_cap, 4, st) : 0xFFFFFFFFu);
-      if (kk <= na) sRs[kk] = (uint64_t)(e + 1) < n ? gld(S.seg_rs, (uint64_t)(e + 1), A.list_cap, 4, st) : 0u;
+      if (first) {
+        sEnd[kk] = e < 0 ? 0u : (e < (int64_t)n ? f_deg : 0xFFFFFFFFu);
+        if (kk <= na) sRs[kk] = (uint64_t)(e + 1) < n ? f_rs : 0u;
+      } else {
+        sEnd[kk] = e < 0 ? 0u : (e < (int64_t)n ? gld(S.seg_end, (uint64_t)e, A.list_cap, 4, st) : 0xFFFFFFFFu);
+        if (kk <= na) sRs[kk] = (uint64_t)(e + 1) < n ? gld(S.seg_rs, (uint64_t)(e + 1), A.list_cap, 4, st) : 0u;
+      }
     }
     wave_lds_sync();
     CH_PH(1);
@@ -587,14 +618,20 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
         sol[j] = gld(olab, c[j], A.nv, 9, st);
         sdg[j] = vdeg_spec(A, oside, c[j], &srs[j]);
       }
+      if (first) {   // (the stores of these labels may still be in flight)
+        if (c[j] == f_own) old[j] = stamp_of(epoch, 0);
+        if (c[j] == f_other) sol[j] = stamp_of(oepoch, 0);
+      }
     }
     if (met_now) {
       // the level has met: only meet vertices matter now (B[kf] is the met set; this level's other
       // labels are read by nothing), so the other side's label is tested before claiming
       uint32_t ol[CH_VT];
 #pragma unroll
-      for (int j = 0; j < CH_VT; ++j)
+      for (int j = 0; j < CH_VT; ++j) {
         ol[j] = (c[j] != NO_ROW && !live(old[j], epoch)) ? gld(olab, c[j], A.nv, 9, st) : 0u;
+        if (first && c[j] == f_other) ol[j] = stamp_of(oepoch, 0);
+      }
 #pragma unroll
       for (int j = 0; j < CH_VT; ++j) {
         if (c[j] == NO_ROW || live(old[j], epoch) || !live(ol[j], oepoch)) continue;
@@ -640,7 +677,7 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
     { uint32_t sink = 0; for (int j = 0; j < CH_VT; ++j) sink += dg[j] + rs[j]; if (sink == 0xFFFFFFFFu) ph[11] += 1; }
 #endif
     CH_PH(6);
-    if (append && !met_now) wave_append(A, D, out_acc, c, am, dg, rs);   // (a wave-uniform condition)
+    if (append && !met_now) wave_append(A, D, out_acc, &C.err, c, am, dg, rs);   // (a wave-uniform condition)
     CH_PH(7);
     // the sides met: LAB_M stamps, the meet list over in-edges, the level's meet count
     uint32_t nm = 0;
@@ -658,8 +695,8 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
     if (__ballot(mm != 0)) {
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) nm += __shfl_xor(nm, o, 64);
-      if (lane == 0) atomicAdd(&st->lmeet[i], (unsigned long long)nm);
-      wave_append(A, A.list[CL_M], &st->macc, c, mm, dg, rs);
+      if (lane == 0) atomicAdd(&C.lmeet[i], (unsigned long long)nm);
+      wave_append(A, A.list[CL_M], &C.macc, &C.err, c, mm, dg, rs);
     }
     CH_PH(9);
 #if CH_PHASE
@@ -692,22 +729,25 @@ __device__ __forceinline__ uint64_t step_items(const ChSnap& P) {
 template <int NW>
 __device__ __forceinline__ void ch_step(const ChArgs& A, const ChQ& q, int i, uint32_t bid, uint32_t nblk) {
   ChState* st = A.st;
+  ChCtr& C = st->c[q.par];
   uint32_t j = i == 0 ? 0u : (uint32_t)st->first[i];
-  ChSnap P = snap_for(st, (int)j, q.upto);
+  ChFirst f0{};
+  ChSnap P = i == 0 ? first_snap(A, q, &f0) : snap_for(st, q, (int)j);
   const bool lead = bid == 0 && threadIdx.x == 0;
+  if (i == 0 && lead) first_store(A, q, f0, P);
   if (P.phase == PH_DONE) {
     if (lead) st->first[i + 1] = j;
     return;
   }
   const bool solo = step_items(P) <= q.solo;
   if (solo && bid != 0) return;
-  if (lead) st->busy += 1;
+  if (lead) C.busy += 1;
   for (;;) {   // (one call site of ch_level: the grid's step and the solo steps share its registers)
     if (lead) {
-      if (j > 0) st->snap[j] = P;   // (step j + 1 derives its snapshot from it; snap[0] is the set-up's)
+      if (j > 0) st->snap[j] = P;   // (step j + 1 derives its snapshot from it; snap[0]: first_store)
       if (!solo) st->first[i + 1] = j + 1;
     }
-    ch_level<NW>(A, q, P, (int)j, solo ? 0u : bid, solo ? 1u : nblk);
+    ch_level<NW>(A, q, P, (int)j, solo ? 0u : bid, solo ? 1u : nblk, j == 0 ? &f0 : nullptr);
     if (!solo) return;
     // this workgroup's stores and atomics before the next step's reads (labels, lists, counters;
     // the acquire drops L1 lines read before another wave's claims); the snapshot is read back
@@ -715,8 +755,8 @@ __device__ __forceinline__ void ch_step(const ChArgs& A, const ChQ& q, int i, ui
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    P = ch_advance(st->snap[j], ld_agent(&st->lacc[j]), ld_agent(&st->lmeet[j]), ld_agent(&st->macc),
-                   ld_agent(&st->err), q.upto);
+    P = ch_advance(st->snap[j], ld_agent(&C.lacc[j]), ld_agent(&C.lmeet[j]), ld_agent(&C.macc),
+                   ld_agent(&C.err), q.upto);
     ++j;
     if (P.phase == PH_DONE || step_items(P) > q.solo || j + 1 >= (uint32_t)CH_MAXS) break;
   }
@@ -790,13 +830,15 @@ __device__ __forceinline__ Cand hop_scan(const ChArgs& A, const uint32_t* vlab, 
 // L - pos - 1 beyond).  A hub's hop is scanned by every workgroup and reduced by the last one to
 // finish; small hops are taken by one workgroup alone (workgroup 0, or the reducing one after a
 // hub), which walks on until the path is complete or the next vertex is a hub — left to the next
-// launch — and writes hstart[h + 1].
+// launch — and writes hstart[h + 1].  Returns true in that one writing workgroup (every thread):
+// it is the launch's last to touch the query's state, so it may also store the result.
 // (bid, nblk: this workgroup among the query's nblk <= CH_HOP_WGS workgroups of the launch)
-__device__ __forceinline__ void ch_hop(const ChArgs& A, const ChQ& q, int nl, int h, uint32_t bid, uint32_t nblk) {
+__device__ __forceinline__ bool ch_hop(const ChArgs& A, const ChQ& q, int nl, int h, uint32_t bid, uint32_t nblk) {
   __shared__ Cand lds[CH_WAVES + 1];
   __shared__ int s_last;
   ChState* st = A.st;
-  const ChSnap F = snap_for(st, (int)st->first[nl], q.upto);   // the state after the nl step launches
+  ChCtr& C = st->c[q.par];
+  const ChSnap F = snap_for(st, q, (int)st->first[nl]);   // the state after the nl step launches
   const unsigned long long H = st->hstart[h];
   uint32_t pos = (uint32_t)(H >> 32), c = (uint32_t)H;
   auto finish = [&](uint32_t p, uint32_t v) {   // (thread 0 of the one writer)
@@ -804,7 +846,7 @@ __device__ __forceinline__ void ch_hop(const ChArgs& A, const ChQ& q, int nl, in
   };
   if (!F.met || F.phase != PH_DONE || F.err || pos >= F.L || c == NO_ROW) {
     if (bid == 0 && threadIdx.x == 0) finish(pos, c);
-    return;
+    return bid == 0;
   }
   const uint32_t L = F.L, kf = F.kf;
   const Cand none{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
@@ -823,7 +865,7 @@ __device__ __forceinline__ void ch_hop(const ChArgs& A, const ChQ& q, int nl, in
   // record hop p (thread 0): false when it has no candidate (reconstruction failure)
   auto record = [&](uint32_t p, const Cand& r) {
     if (r.d == NO_ROW) {
-      atomicOr(&st->err, 1ull);
+      atomicOr(&C.err, 1ull);
       finish(p, NO_ROW);
       return false;
     }
@@ -849,7 +891,7 @@ __device__ __forceinline__ void ch_hop(const ChArgs& A, const ChQ& q, int nl, in
       s_last = atomicAdd(&st->gticket, 1ull) == nblk - 1;
     }
     __syncthreads();
-    if (!s_last) return;
+    if (!s_last) return false;
     __threadfence();
     Cand r = none;
     if (threadIdx.x < nblk) {
@@ -862,14 +904,14 @@ __device__ __forceinline__ void ch_hop(const ChArgs& A, const ChQ& q, int nl, in
       s_last = record(pos, r);
     }
     __syncthreads();
-    if (!s_last) return;
+    if (!s_last) return true;   // (a reconstruction failure: recorded and finished)
     c = r.d;
     ++pos;
   } else if (bid != 0) {
-    return;
+    return false;
   }
   // this workgroup alone: small hops
-  if (threadIdx.x == 0) st->hlaunch += 1;
+  if (threadIdx.x == 0) C.hlaunch += 1;
   while (pos < L) {
     range(c, &rs, &re);
     if (re - rs > CH_SOLO_DEG) break;   // a hub: the next launch spreads it
@@ -878,16 +920,37 @@ __device__ __forceinline__ void ch_hop(const ChArgs& A, const ChQ& q, int nl, in
     const Cand r = block_min(hop_scan(A, vlab, want, rs, re, threadIdx.x, CH_BLOCK), lds);
     if (threadIdx.x == 0) s_last = record(pos, r);
     __syncthreads();
-    if (!s_last) return;
+    if (!s_last) return true;
     c = r.d;
     ++pos;
   }
   if (threadIdx.x == 0) finish(pos, c);
+  return true;
 }
 
 // ---------------------------------------------------------------------------- kernels
-// One query per launch (the chain of one pair) ...
-__global__ void __launch_bounds__(CH_BLOCK) k_ch_setup(const ChArgs* __restrict__ Ap, ChQ q) { ch_setup(*Ap, q); }
+// The chain's result (after `steps` step and `hops` hop launches) into the host's ChOut (one
+// workgroup; vector stores over the mapped pinned page), and the next query's counter set zeroed.
+__device__ __forceinline__ void ch_out(const ChArgs& A, const ChQ& q, int steps, int hops, ChOut* out) {
+  ChState* st = A.st;
+  __syncthreads();   // (the writing workgroup's own stores: the path, hstart)
+  const ChSnap F = snap_for(st, q, (int)st->first[steps]);
+  const ChCtr& C = st->c[q.par];
+  const uint32_t L = F.met && F.L <= MAX_PATH_LEN ? F.L : 0;
+  for (uint32_t k = threadIdx.x; k < 1 + 3 * L; k += blockDim.x) out->path[k] = st->path[k];
+  if (threadIdx.x == 0) {
+    out->F = F;
+    out->err = C.err | st->gerr;
+    out->hpos = st->hstart[hops];
+    out->hlaunch = C.hlaunch;
+    out->busy = C.busy;
+  }
+  unsigned long long* nxt = reinterpret_cast<unsigned long long*>(&st->c[q.par ^ 1u]);
+  for (uint32_t k = threadIdx.x; k < sizeof(ChCtr) / 8; k += blockDim.x) nxt[k] = 0;
+}
+
+// One query per launch (the chain of one pair): step launch 0 starts the search (no set-up
+// launch), and the batch's last hop launch stores the result (no result launch) ...
 // (at most 2 waves per SIMD: 256 VGPRs, no spills; a one-pair launch has 128 workgroups of 4 waves,
 // 2 waves per CU, so the occupancy bound costs nothing.  16-wave workgroups, tried for more waves
 // per big level, were slower: RMAT-26 p50 0.137 -> 0.197 ms, profiles/r03_n_sp_block_ab.txt)
@@ -895,25 +958,12 @@ __global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(2
   ch_step<CH_WAVES>(*Ap, q, i, blockIdx.x, gridDim.x);
 }
 
-__global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ Ap, ChQ q, int nl, int h) {
-  ch_hop(*Ap, q, nl, h, blockIdx.x, gridDim.x);
+// (out: the batch's last hop launch stores the result: the steps launched so far, hops h + 1)
+__global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ Ap, ChQ q, int nl, int h, ChOut* out) {
+  if (ch_hop(*Ap, q, nl, h, blockIdx.x, gridDim.x) && out) ch_out(*Ap, q, nl, h + 1, out);
 }
 
-// The chain's result (after `steps` step and `hops` hop launches) into the host's ChOut (one
-// workgroup; vector stores over the mapped pinned page).
-__device__ __forceinline__ void ch_out(const ChArgs& A, const ChQ& q, int steps, int hops, ChOut* out) {
-  const ChState* st = A.st;
-  const ChSnap F = snap_for(st, (int)st->first[steps], q.upto);
-  const uint32_t L = F.met && F.L <= MAX_PATH_LEN ? F.L : 0;
-  for (uint32_t k = threadIdx.x; k < 1 + 3 * L; k += blockDim.x) out->path[k] = st->path[k];
-  if (threadIdx.x == 0) {
-    out->F = F;
-    out->err = st->err;
-    out->hpos = st->hstart[hops];
-    out->hlaunch = st->hlaunch;
-    out->busy = st->busy;
-  }
-}
+// (a batch without a hop launch: the result alone)
 __global__ void __launch_bounds__(64) k_ch_out(const ChArgs* __restrict__ Ap, ChQ q, int steps, int hops, ChOut* out) {
   ch_out(*Ap, q, steps, hops, out);
 }
@@ -929,9 +979,6 @@ struct ChBatch {
   int n;
   uint32_t per;
 };
-__global__ void __launch_bounds__(CH_BLOCK) k_ch_setup_b(ChBatch b) {
-  if ((int)blockIdx.x < b.n) ch_setup(*b.A[blockIdx.x], b.q[blockIdx.x]);
-}
 #ifndef NBG_STEPB_WPE
 #define NBG_STEPB_WPE 2   // (2 waves/SIMD: no spills; batched 33.3-33.9k -> 34.7-35.0k pairs/s, profiles/r03_y_sp_spec_ab.txt)
 #endif
@@ -939,12 +986,10 @@ __global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(N
   const uint32_t p = blockIdx.x / b.per;
   if ((int)p < b.n) ch_step<CH_WAVES>(*b.A[p], b.q[p], i, blockIdx.x % b.per, b.per);
 }
-__global__ void __launch_bounds__(CH_BLOCK) k_ch_hop_b(ChBatch b, int nl, int h) {
+__global__ void __launch_bounds__(CH_BLOCK) k_ch_hop_b(ChBatch b, int nl, int h, int last) {
   const uint32_t p = blockIdx.x / CH_HOP_WGS;
-  if ((int)p < b.n) ch_hop(*b.A[p], b.q[p], nl, h, blockIdx.x % CH_HOP_WGS, CH_HOP_WGS);
-}
-__global__ void __launch_bounds__(64) k_ch_out_b(ChBatch b, int steps, int hops) {
-  if ((int)blockIdx.x < b.n) ch_out(*b.A[blockIdx.x], b.q[blockIdx.x], steps, hops, b.out[blockIdx.x]);
+  if ((int)p < b.n && ch_hop(*b.A[p], b.q[p], nl, h, blockIdx.x % CH_HOP_WGS, CH_HOP_WGS) && last)
+    ch_out(*b.A[p], b.q[p], nl, h + 1, b.out[p]);
 }
 
 // ---------------------------------------------------------------------------- host side
@@ -970,6 +1015,8 @@ struct ChainCtx {
   // the query in flight: what has been enqueued
   ChQ q{};
   int steps = 0, hops = 0;
+  uint32_t par = 0;                // the query's counter set (ChQ::par)
+  bool clean = true;               // the next query's counter set is zero
   // recent queries: step launches and path lengths used (sizes the next chain)
   double ema_steps = 6, ema_hops = 2;
   unsigned long long batches = 0, queries = 0;
@@ -1058,18 +1105,21 @@ void chain_destroy(ChainCtx* c) {
   delete c;
 }
 
-// Enqueue step launches [steps, steps + k) and h hop launches, then the result (k_ch_out).
+// Enqueue step launches [steps, steps + k) and h hop launches; the last hop launch stores the
+// result (k_ch_out only when the batch has no hop launch).
 static hipError_t chain_batch(ChainCtx* c, int k, int h) {
   const ChArgs* A = c->d_args;
   for (int j = 0; j < k; ++j, ++c->steps)
     c->timed(CHK_STEP, [&] {
       hipLaunchKernelGGL(k_ch_step, dim3(c->grid), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps);
     });
-  for (int j = 0; j < h && c->hops < CH_MAXS; ++j, ++c->hops)
+  h = std::min(h, CH_MAXS - c->hops);
+  for (int j = 0; j < h; ++j, ++c->hops)
     c->timed(CHK_HOP, [&] {
-      hipLaunchKernelGGL(k_ch_hop, dim3(CH_HOP_WGS), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps, c->hops);
+      hipLaunchKernelGGL(k_ch_hop, dim3(CH_HOP_WGS), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps, c->hops,
+                         j + 1 == h ? c->d_out : (ChOut*)nullptr);
     });
-  hipLaunchKernelGGL(k_ch_out, dim3(1), dim3(64), 0, c->stream, A, c->q, c->steps, c->hops, c->d_out);
+  if (h <= 0) hipLaunchKernelGGL(k_ch_out, dim3(1), dim3(64), 0, c->stream, A, c->q, c->steps, c->hops, c->d_out);
   ++c->batches;
   return hipGetLastError();
 }
@@ -1105,10 +1155,14 @@ static hipError_t chain_prepare(ChainCtx* c, const SpTypes& fwd, const SpTypes& 
     c->cached = a;
     c->args_valid = true;
   }
-  c->q = ChQ{s, t, upto, epoch, epoch, epoch, c->solo};
+  c->par ^= 1u;
+  c->q = ChQ{s, t, upto, epoch, epoch, epoch, c->solo, c->par};
   c->steps = c->hops = 0;
   c->last_batched = false;
   ++c->queries;
+  // the previous query's result launch zeroed this query's counters, unless it never ran
+  if (!c->clean) HIP_TRY_CH(hipMemsetAsync(&c->d_st->c[c->par], 0, sizeof(ChCtr), c->stream));
+  c->clean = false;
   return hipSuccess;
 }
 
@@ -1128,9 +1182,6 @@ hipError_t chain_launch(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, con
                         const int64_t* vids, uint32_t* const lab[3], uint32_t epoch, uint32_t s, uint32_t t,
                         uint32_t upto) {
   HIP_TRY_CH(chain_prepare(c, fwd, bwd, visible, vids, lab, epoch, s, t, upto));
-  c->timed(CHK_SETUP, [&] {
-    hipLaunchKernelGGL(k_ch_setup, dim3(1), dim3(CH_BLOCK), 0, c->stream, (const ChArgs*)c->d_args, c->q);
-  });
   int k, h;
   chain_length(c, &k, &h);
   return chain_batch(c, k, h);
@@ -1163,16 +1214,14 @@ hipError_t chain_launch_batch(ChainCtx* const* cs, int n, const ChainQuery* qs) 
   }
   const hipStream_t st = cs[0]->stream;
   ChainCtx* c0 = cs[0];   // (the batch's launch events are kept by its first context)
-  c0->timed(CHK_SETUP_B, [&] { hipLaunchKernelGGL(k_ch_setup_b, dim3((unsigned)n), dim3(CH_BLOCK), 0, st, b); });
   for (int j = 0; j < k; ++j)
     c0->timed(CHK_STEP_B, [&] {
       hipLaunchKernelGGL(k_ch_step_b, dim3((unsigned)n * b.per), dim3(CH_BLOCK), 0, st, b, j);
     });
   for (int j = 0; j < h; ++j)
     c0->timed(CHK_HOP_B, [&] {
-      hipLaunchKernelGGL(k_ch_hop_b, dim3((unsigned)n * CH_HOP_WGS), dim3(CH_BLOCK), 0, st, b, k, j);
+      hipLaunchKernelGGL(k_ch_hop_b, dim3((unsigned)n * CH_HOP_WGS), dim3(CH_BLOCK), 0, st, b, k, j, j + 1 == h);
     });
-  hipLaunchKernelGGL(k_ch_out_b, dim3((unsigned)n), dim3(64), 0, st, b, k, h);
   HIP_TRY_CH(hipGetLastError());
   for (int p = 0; p < n; ++p) {
     ChainCtx* c = cs[p];
@@ -1202,6 +1251,7 @@ bool chain_more(ChainCtx* c, hipError_t* he) {
     *he = chain_batch(c, 0, (int)F.L - (int)hpos);
     return false;
   }
+  c->clean = true;   // (its result launch zeroed the next query's counters)
   // step launches that ran a step; decay toward this query's needs
   const double used = (double)h.busy;
   c->ema_steps = 0.9 * c->ema_steps + 0.1 * (used + 0.5);
@@ -1217,7 +1267,7 @@ void chain_result(const ChainCtx* c, SpResult* out) {
   out->edges = F.edges;
   out->levels = F.levels;
   out->abytes = F.abytes;
-  out->launches = (unsigned long long)(c->steps + c->hops + 1);
+  out->launches = (unsigned long long)(c->steps + c->hops + (c->hops ? 0 : 1));
   const uint32_t hpos = (uint32_t)(h.hpos >> 32);
   out->L = (F.met && !h.err && hpos == F.L) ? F.L : 0;
   if (F.met && !h.err && hpos != F.L) out->err = 2;   // (cannot happen: the hops were enqueued)
