@@ -142,6 +142,7 @@ typedef struct {
   uint64_t device_bytes;      /* HBM held by the snapshot                                      */
   int32_t num_edge_types;     /* signed edge types present                                     */
   int32_t reserved;
+  uint64_t tiny_queries;      /* GO queries run as one single-workgroup launch (tiny path)       */
 } nbg_stats;
 int32_t nbg_get_stats(const nbg_engine* e, nbg_stats* out);
 

@@ -1086,6 +1086,39 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
   }
   auto inl_of = [&](size_t i, uint32_t s) -> const InlineList* { return s == 1 && !inl.empty() ? &inl[i] : nullptr; };
   hipError_t he = ws_begin_query(ws, f0.data(), f0.size(), &plist, st->id);
+  // A tiny query — its walk bound (DevEdgeType::h_w2 / h_w3) keeps every step within one
+  // workgroup — runs as one launch (ws_go_tiny); NBG_TINY=0 turns it off.
+  static const bool tiny_on = !getenv("NBG_TINY") || atoi(getenv("NBG_TINY")) != 0;
+  bool tiny = tiny_on && he == hipSuccess && !part && !device && !st->distinct && !st->uses_input && !st->derived &&
+              over.size() == 1 && ncols > 0 && !deferred && !(plist[0].where_const && !plist[0].where_const_val) &&
+              f0.size() <= (size_t)INLINE_STARTS && steps <= 3;
+  const DevEdgeType* tdt = nullptr;
+  if (tiny) {
+    auto it = E.snap.types.find(over[0]);
+    tdt = it == E.snap.types.end() ? nullptr : &it->second;
+    tiny = tdt && (steps == 1 || (tdt->h_w2.size() == E.snap.nv && tdt->h_w3.size() == E.snap.nv));
+  }
+  if (tiny) {
+    uint64_t bound = 0;
+    for (uint32_t d : f0) {
+      if (steps == 1) {
+        const bool vis = E.snap.h_visible.empty() || E.snap.h_visible[d];
+        bound += vis ? std::min<uint64_t>(tdt->h_row_ptr[d + 1] - tdt->h_row_ptr[d], cap) : 0;
+      } else {
+        bound += steps == 2 ? tdt->h_w2[d] : tdt->h_w3[d];
+      }
+    }
+    tiny = bound <= TINY_EDGES;
+  }
+  if (tiny) {
+    he = ws_go_tiny(ws, args_for(*tdt), f0.data(), (uint32_t)f0.size(), steps, plist[0], ncols);
+    if (he != hipSuccess) return E.fail(NBG_E_DEVICE, std::string("HIP: ") + hipGetErrorString(he));
+    ++E.tiny_queries;
+    p->region.assign(1, 0);
+    p->blk_cap.assign(1, TINY_EDGES);
+    p->rows = rows.release();
+    return NBG_OK;
+  }
   uint64_t n_bound = f0.size();
   ws_set_mark_claims(ws, over.size() == 1);
   const bool inject = part && E.fault(NBG_FAULT_DEVICE);
@@ -1455,6 +1488,14 @@ int32_t nbg::ws_release(Engine& E, Workspace** wsp, hipStream_t stream) {
 // The query workspace of a finalized (or snapshot-loaded) engine.
 int32_t nbg::engine_ready(Engine& E) {
   if (int32_t rc = E.upload_strings()) return rc;
+  if (!E.partitioned()) {   // walk bounds of the tiny GO path (a failure only disables it)
+    const uint32_t cap = (uint32_t)(E.cfg.max_edge_returned_per_vertex <= 0 ? 0x7fffffff
+                                                                            : E.cfg.max_edge_returned_per_vertex);
+    for (auto& kv : E.snap.types)
+      if (kv.first > 0)
+        (void)tiny_bounds(kv.second.row_ptr, kv.second.col, E.snap.d_visible, cap, E.snap.nv, &kv.second.h_w2,
+                          &kv.second.h_w3, E.stream);
+  }
   std::string err;
   E.ws = ws_create(E.snap.nv + 1024, E.snap.nv, E.snap.max_edges(), E.stream, &err);
   if (!E.ws) return E.fail(NBG_E_OUT_OF_MEMORY, err);
@@ -1698,6 +1739,7 @@ int32_t nbg_get_stats(const nbg_engine* h, nbg_stats* out) {
   for (auto& kv : E.snap.types) out->num_edges += kv.second.num_edges;
   out->device_bytes = E.snap.device_bytes;
   out->num_edge_types = (int32_t)E.snap.types.size();
+  out->tiny_queries = E.tiny_queries;
   return NBG_OK;
 }
 

@@ -89,6 +89,7 @@ struct Engine {
   Engine* err_parent = nullptr;
   std::mutex err_mu;
 
+  uint64_t tiny_queries = 0;    // GO queries run by ws_go_tiny (nbg_stats)
   // nbg_inject_fault (tests): the next fault_count queries fail at fault_site
   int fault_site = 0, fault_count = 0;
   bool fault(int site) {

@@ -24,6 +24,7 @@
 // GoExecutor::getDstIdsFromResp (per-step dst SET, no global visited set).
 #include <hip/hip_runtime.h>
 #include <array>
+#include <cstddef>
 
 #include <cstdio>
 #include <cstring>
@@ -2921,6 +2922,251 @@ const int64_t* ws_host_small_rows(Workspace* w, uint64_t count) {
 hipError_t ws_end_query(Workspace* w) {
   HIP_TRY(ws_end_query_async(w));
   return ws_end_query_wait(w);
+}
+
+// ----------------------------------------------------------------------------- tiny GO queries
+// A GO N STEPS whose whole expansion is small (the host bounds it before launching: at most
+// TINY_EDGES edge visits over all steps, nbg::tiny_bound) runs as ONE workgroup in ONE launch:
+// the per-step sets in LDS (an open-addressing table), the final step's WHERE / YIELD through the
+// interpreter, and the QState, row count and rows stored straight into the mapped host block the
+// multi-launch path's k_q_out_small fills — the same host code reads them (go_collect,
+// materialize_rows).  A query that small spends its time on launches and round trips
+// (GoExecutor.cpp:410-474 per hop), so one launch and one wait are the whole query.
+struct TinyParams {
+  ExpandArgs a;
+  const Ins* prog;
+  int where_len, where_reg, prog_len, nyields;
+  int yield_reg[MAX_YIELDS];
+  int64_t yield_const[MAX_YIELDS];
+  uint32_t probe_mask;
+  uint32_t steps, n0;
+  uint32_t start[INLINE_STARTS];
+  int64_t* const* cols;            // the workspace's row columns (device)
+  unsigned long long* hq;          // mapped: QState, then the per-workgroup row counts
+  int64_t* small;                  // mapped: [0] = rows + 1, then the cells column by column
+};
+
+constexpr uint32_t TINY_HASH = 2 * TINY_EDGES;   // set slots (power of two, half full at most)
+
+__global__ void __launch_bounds__(BLOCK) k_go_tiny(TinyParams t) {
+  __shared__ uint32_t sF[2][TINY_EDGES + INLINE_STARTS];   // frontier (entry ids) of this / the next step
+  __shared__ uint32_t sEnd[TINY_EDGES + INLINE_STARTS];    // inclusive prefix of the capped degrees
+  __shared__ uint32_t sRs[TINY_EDGES + INLINE_STARTS];
+  __shared__ uint32_t sSet[TINY_HASH];
+  __shared__ uint32_t sScan[BLOCK / 64];
+  __shared__ uint32_t sNext, sRows;
+  __shared__ unsigned long long sStepN[MAX_STEPS + 2], sStepE[MAX_STEPS + 2];
+  __shared__ uint32_t sErr, sTags;
+  extern __shared__ int64_t regs[];   // [nregs][BLOCK], run_program's registers
+  const ExpandArgs& a = t.a;
+  const DegSrc ds{a.row_ptr, a.visible, a.cap};
+  const int tid = threadIdx.x;
+  uint32_t n = t.n0, cur = 0;
+  for (uint32_t i = tid; i < n; i += BLOCK) sF[0][i] = t.start[i];
+  if (tid == 0) {
+    sErr = 0;
+    sTags = 0;
+    sRows = 0;
+  }
+  for (int s = tid; s < MAX_STEPS + 2; s += BLOCK) sStepN[s] = sStepE[s] = 0;
+  __syncthreads();
+  bool anyErr = false;
+  uint32_t tbits = 0;
+  for (uint32_t step = 1; step <= t.steps; ++step) {
+    const bool final = step == t.steps;
+    // the frontier's edge space: capped degrees, prefix, row starts (entries in chunks of BLOCK)
+    uint32_t total = 0;
+    for (uint32_t b = 0; b < n; b += BLOCK) {
+      uint32_t rs = 0, d = 0;
+      if (b + tid < n) d = vdeg(ds, sF[cur][b + tid], &rs);
+      uint32_t tot = 0;
+      const uint32_t x = block_excl_scan(d, &tot, sScan);
+      if (b + tid < n) {
+        sEnd[b + tid] = total + x + d;
+        sRs[b + tid] = rs;
+      }
+      total += tot;
+    }
+    if (tid == 0) {
+      sStepN[step] = n;
+      sStepE[step] = total;
+      sNext = 0;
+    }
+    if (!final)
+      for (uint32_t k = tid; k < TINY_HASH; k += BLOCK) sSet[k] = 0;
+    __syncthreads();
+    // every edge of the frontier: its entry by binary search over the prefix
+    for (uint32_t e0 = 0; e0 < total; e0 += BLOCK) {
+      const uint32_t e = e0 + tid;
+      const bool act = e < total;
+      uint32_t lo = 0, hi = n;
+      while (act && lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sEnd[mid] <= e) lo = mid + 1;
+        else hi = mid;
+      }
+      const uint32_t ent = act ? lo : 0;
+      const uint32_t v = act ? sF[cur][ent] : 0;
+      const uint32_t start = (act && ent) ? sEnd[ent - 1] : 0;
+      const uint64_t j = act ? (uint64_t)sRs[ent] + (e - start) : 0;
+      if (!final) {
+        // the per-step SET of destinations (GoExecutor::getDstIdsFromResp)
+        const uint32_t u = act ? a.col[j] : NO_ROW;
+        if (u != NO_ROW) {
+          uint32_t h = (u * 2654435761u) & (TINY_HASH - 1);
+          for (uint32_t probe = 0; probe < TINY_HASH; ++probe) {   // (at most half full: the host's bound)
+            const uint32_t old = atomicCAS(&sSet[h], 0u, u + 1);
+            if (old == 0) {
+              const uint32_t at = atomicAdd(&sNext, 1u);
+              if (at < TINY_EDGES + INLINE_STARTS) sF[cur ^ 1][at] = u;   // (the host's bound: always)
+              break;
+            }
+            if (old == u + 1) break;
+            h = (h + 1) & (TINY_HASH - 1);
+          }
+        }
+        continue;
+      }
+      // the final step: the holder's tags, WHERE, YIELD (as k_expand<FINAL>)
+      if (act && t.probe_mask) {
+        const uint32_t d = a.col[j];
+        if (d != NO_ROW)
+          for (uint32_t m = t.probe_mask; m; m &= m - 1) {
+            const int tg = __builtin_ctz(m);
+            if (a.tpres[tg][d]) tbits |= 1u << tg;
+          }
+      }
+      const EdgeCtx c{j, v};
+      bool pass = act;
+      if (t.where_reg >= 0) {
+        bool werr = false;
+        run_program(t.prog, t.prog + t.prog_len, 0, t.where_len, c, a, regs, act, werr, tbits);
+        pass = act && !werr && regs[t.where_reg * BLOCK + tid] != 0;
+        if (act && werr) anyErr = true;
+      }
+      bool yerr = false;
+      run_program(t.prog, t.prog + t.prog_len, t.where_len, t.prog_len, c, a, regs, pass, yerr, tbits);
+      if (pass && yerr) anyErr = true;
+      if (pass) {
+        const uint32_t row = atomicAdd(&sRows, 1u);
+        if (row >= TINY_EDGES) continue;   // (the host's bound: never)
+        for (int y = 0; y < t.nyields; ++y) {
+          const int r = t.yield_reg[y];
+          t.cols[y][row] = r >= 0 ? regs[r * BLOCK + tid] : t.yield_const[y];
+        }
+      }
+    }
+    __syncthreads();
+    n = min(sNext, TINY_EDGES + INLINE_STARTS);
+    cur ^= 1;
+  }
+  if (anyErr) atomicOr(&sErr, 1u);
+  if (tbits) atomicOr(&sTags, tbits);
+  __syncthreads();
+  // QState (every word: the fields go_collect reads, the rest zero), then one workgroup's row count
+  const uint32_t nrows = min(sRows, TINY_EDGES);
+  constexpr uint32_t NQ = sizeof(QState) / 8;
+  for (uint32_t k = tid; k < NQ; k += BLOCK) {
+    unsigned long long x = 0;
+    if (k == offsetof(QState, err) / 8) x = sErr;
+    else if (k == offsetof(QState, tagbits) / 8) x = sTags;
+    else if (k >= offsetof(QState, step_n) / 8 && k < offsetof(QState, step_n) / 8 + MAX_STEPS + 2)
+      x = sStepN[k - offsetof(QState, step_n) / 8];
+    else if (k >= offsetof(QState, e_st) / 8 && k < offsetof(QState, e_st) / 8 + (MAX_STEPS + 2) * MAX_TYPES_Q) {
+      const uint32_t o = k - (uint32_t)(offsetof(QState, e_st) / 8);
+      x = o % MAX_TYPES_Q == 0 ? sStepE[o / MAX_TYPES_Q] : 0ull;
+    }
+    t.hq[k] = x;
+  }
+  if (tid == 0) reinterpret_cast<uint32_t*>(t.hq + NQ)[0] = nrows;
+  // the rows, column by column, then the count that makes them valid
+  const bool fits = (uint64_t)nrows * t.nyields <= SMALL_ROWS_WORDS;
+  for (int y = 0; fits && y < t.nyields; ++y)
+    for (uint32_t i = tid; i < nrows; i += BLOCK) t.small[1 + (uint64_t)y * nrows + i] = t.cols[y][i];
+  __syncthreads();
+  if (tid == 0) t.small[0] = fits ? (int64_t)nrows + 1 : 0;
+}
+
+// Walk bounds of one CSR for the tiny path: W_k(v) = deg(v) + sum over v's (capped) edges of
+// W_{k-1}(neighbour), W_1 = deg (capped, 0 when invisible), saturated at TINY_EDGES + 1 (a vertex
+// past it is not tiny, so a row longer than that is not read).
+__global__ void __launch_bounds__(BLOCK) k_walk_bound(const uint32_t* __restrict__ row_ptr, const uint32_t* __restrict__ col,
+                                                      const uint8_t* __restrict__ visible, uint32_t cap, uint64_t nv,
+                                                      const uint16_t* __restrict__ prev, uint16_t* __restrict__ out) {
+  const uint64_t v = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (v >= nv) return;
+  constexpr uint32_t SAT = TINY_EDGES + 1;
+  uint32_t deg = 0;
+  if (!visible || visible[v]) {
+    deg = row_ptr[v + 1] - row_ptr[v];
+    deg = deg < cap ? deg : cap;
+  }
+  uint32_t w = deg < SAT ? deg : SAT;
+  if (prev && w < SAT) {
+    const uint32_t rs = row_ptr[v];
+    for (uint32_t k = 0; k < deg && w < SAT; ++k) {
+      const uint32_t u = col[rs + k];
+      if (u != NO_ROW) w += prev[u];
+    }
+  }
+  out[v] = (uint16_t)(w < SAT ? w : SAT);
+}
+
+hipError_t tiny_bounds(const uint32_t* row_ptr, const uint32_t* col, const uint8_t* visible, uint32_t cap, uint64_t nv,
+                       std::vector<uint16_t>* w2, std::vector<uint16_t>* w3, hipStream_t s) {
+  w2->clear();
+  w3->clear();
+  if (!nv) return hipSuccess;
+  uint16_t* d = nullptr;
+  HIP_TRY(hipMalloc((void**)&d, nv * 3 * sizeof(uint16_t)));
+  const dim3 g((unsigned)((nv + BLOCK - 1) / BLOCK));
+  hipLaunchKernelGGL(k_walk_bound, g, dim3(BLOCK), 0, s, row_ptr, col, visible, cap, nv, (const uint16_t*)nullptr, d);
+  hipLaunchKernelGGL(k_walk_bound, g, dim3(BLOCK), 0, s, row_ptr, col, visible, cap, nv, (const uint16_t*)d, d + nv);
+  hipLaunchKernelGGL(k_walk_bound, g, dim3(BLOCK), 0, s, row_ptr, col, visible, cap, nv, (const uint16_t*)(d + nv),
+                     d + 2 * nv);
+  hipError_t e = hipGetLastError();
+  w2->resize(nv);
+  w3->resize(nv);
+  if (e == hipSuccess) e = hipMemcpyAsync(w2->data(), d + nv, nv * 2, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(w3->data(), d + 2 * nv, nv * 2, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipFree(d);
+  if (e != hipSuccess) {
+    w2->clear();
+    w3->clear();
+  }
+  return e;
+}
+
+hipError_t ws_go_tiny(Workspace* w, const ExpandArgs& a, const uint32_t* starts, uint32_t n, uint32_t steps,
+                      const TypeProgram& prog, int ncols) {
+  if (n > INLINE_STARTS || steps < 1 || steps > MAX_STEPS || ncols > MAX_YIELDS || ncols < 1) return hipErrorInvalidValue;
+  HIP_TRY(ws_reserve_rows(w, TINY_EDGES, ncols));
+  TinyParams t{};
+  t.a = a;
+  t.prog = w->d_prog;
+  t.where_len = prog.where_len;
+  t.where_reg = prog.where_reg;
+  t.prog_len = (int)prog.code.size();
+  t.nyields = (int)prog.yield_reg.size();
+  for (int y = 0; y < t.nyields; ++y) {
+    t.yield_reg[y] = prog.yield_reg[y];
+    t.yield_const[y] = prog.yield_const[y];
+  }
+  t.probe_mask = prog.probe_mask;
+  t.steps = steps;
+  t.n0 = n;
+  for (uint32_t i = 0; i < n; ++i) t.start[i] = starts[i];
+  t.cols = (int64_t* const*)w->d_row_cols;
+  t.hq = reinterpret_cast<unsigned long long*>(w->d_hq);
+  t.small = w->d_small;
+  for (auto& g : w->final_grid) g = 0;
+  w->final_grid[0] = 1;   // (one workgroup's rows: go_collect reads one count)
+  const size_t lds = (size_t)(prog.nregs > 0 ? prog.nregs : 1) * BLOCK * sizeof(int64_t);
+  hipLaunchKernelGGL(k_go_tiny, dim3(1), dim3(BLOCK), lds, w->stream, t);
+  HIP_TRY(hipGetLastError());
+  if (!w->done_ev) HIP_TRY(hipEventCreateWithFlags(&w->done_ev, hipEventDisableTiming));
+  return hipEventRecord(w->done_ev, w->stream);
 }
 
 // ----------------------------------------------------------------------------- partitioned mode

@@ -93,6 +93,7 @@ struct DevEdgeType {            // CSR for one signed edge type over this rank's
   uint8_t* valid = nullptr;     // [E] or nullptr when every value decoded
   int max_degree = 0;
   std::vector<uint32_t> h_row_ptr;   // host copy (path reconstruction, host planning)
+  std::vector<uint16_t> h_w2, h_w3;  // tiny-path walk bounds (single engine, positive types; tiny_bounds)
   // Superseded versions (multi-version data only): a CSR of the older versions of every edge, in
   // key order, with h_grp[i] = the live edge (index into this CSR's parent) of version i.  Read
   // by GetNeighbors' filtered walk, which sees older versions until an edge is accepted
@@ -610,6 +611,16 @@ hipError_t ws_end_query_async_small(Workspace* w, const SmallPack& sp);
 // query's result was not packed or has a count other than `count`
 const int64_t* ws_host_small_rows(Workspace* w, uint64_t count);
 hipError_t ws_end_query_wait(Workspace* w);    // wait for it (then as ws_end_query)
+// A GO query bounded by TINY_EDGES edge visits over all its steps (one OVER type, inline starts,
+// rows fetched to the host): the whole query in one single-workgroup launch whose results land
+// where ws_end_query_async_small puts them; then ws_end_query_wait.
+constexpr uint32_t TINY_EDGES = 1024;
+// W_2 / W_3 of every vertex of one CSR (saturated at TINY_EDGES + 1): the edge visits GO 2 / 3
+// STEPS from it can make at most (empty vectors on failure: no tiny path for that type)
+hipError_t tiny_bounds(const uint32_t* row_ptr, const uint32_t* col, const uint8_t* visible, uint32_t cap, uint64_t nv,
+                       std::vector<uint16_t>* w2, std::vector<uint16_t>* w3, hipStream_t s);
+hipError_t ws_go_tiny(Workspace* w, const ExpandArgs& a, const uint32_t* starts, uint32_t n, uint32_t steps,
+                      const TypeProgram& prog, int ncols);
 // partitioned mode: flags over [world * npad) global ids, per-hop bitmap all-to-all
 constexpr uint64_t PART_ALIGN = 16384 * 4;   // npad granularity (flag / bit workgroups divide it)
 hipError_t ws_set_partition(Workspace* w, Comm* comm, uint64_t npad);
