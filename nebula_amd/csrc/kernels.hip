@@ -406,25 +406,12 @@ __device__ __forceinline__ int64_t load_col(const void* p, int bytes, uint32_t j
   }
 }
 
-// Final-step streams that are read or written once per query (the WHERE column, _dst, the rows):
-// non-temporal when built with NBG_NT_LD / NBG_NT_ST (an A/B switch of the build).
-#ifdef NBG_NT_LD
-#define NBG_LD_STREAM(p) __builtin_nontemporal_load(p)
-#else
-#define NBG_LD_STREAM(p) (*(p))
-#endif
-#ifdef NBG_NT_ST
-#define NBG_ST_STREAM(v, p) __builtin_nontemporal_store((v), (p))
-#else
-#define NBG_ST_STREAM(v, p) (*(p) = (v))
-#endif
-
 // VT loads of a column of type T (sign-extended), all in flight at once
 template <typename T, int V = VT>
 __device__ __forceinline__ void load_narrow(const void* p, const uint32_t* jj, int nb, int lane, int64_t* x) {
   const T* c = reinterpret_cast<const T*>(p);
 #pragma unroll
-  for (int i = 0; i < V; ++i) x[i] = (i * 64 + lane < nb) ? (int64_t)NBG_LD_STREAM(c + jj[i]) : 0;
+  for (int i = 0; i < V; ++i) x[i] = (i * 64 + lane < nb) ? (int64_t)c[jj[i]] : 0;
 }
 
 struct FastProg {
@@ -1041,14 +1028,8 @@ using InlineArg = typename std::conditional<INL, InlineList, NoInline>::type;
 // TILE = 64 * VT; a V = 2 * VT instantiation reads every other split.  (FINALD with V = 8 at 5 or
 // 6 waves per SIMD measured 307-338 us per RMAT-26 launch against 222 us at V = 4 and 8 waves,
 // profiles/r02_q_final_vt8_ab.json: the default V = VT is the only one launched.)
-#ifndef NBG_MARK_PACKED
-#define NBG_MARK_PACKED 0   // 1: MARK tiles packed WAVES to a workgroup (the round-2 order, for A/B)
-#endif
 template <int M, bool INL = false, int V = VT>
-#ifndef NBG_WIDE_WAVES
-#define NBG_WIDE_WAVES 6
-#endif
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M == FINAL ? 4 : (V > VT ? NBG_WIDE_WAVES : 8))))
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M == FINAL ? 4 : (V > VT ? 6 : 8))))
 k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_t* __restrict__ seg_end,
          const uint32_t* __restrict__ seg_rs, uint8_t* __restrict__ flags, FinalParams fp, BfsParams bp,
          unsigned long long* stat_e, unsigned long long* stat_n, InlineArg<INL> il) {
@@ -1149,7 +1130,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
       const uint64_t row = region + off + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
       off += (uint32_t)__popcll(bal);
       if (pass)
-        for (int y = 0; y < fp.nyields; ++y) NBG_ST_STREAM(fp.fast.ykind[y] == 0 ? vdv[i] : fp.yield_const[y], ycols[y] + row);
+        for (int y = 0; y < fp.nyields; ++y) ycols[y][row] = fp.fast.ykind[y] == 0 ? vdv[i] : fp.yield_const[y];
     }
   };
   if (kFinal) {
@@ -1157,31 +1138,12 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
     __syncthreads();
   }
   if ((M == MARK || M == MARKB) && bp.nlist.zero_next && blockIdx.x == 0 && threadIdx.x == 0) *bp.nlist.zero_next = 0;
-#ifdef NBG_PHASE_TIMING   // experiment builds only: cycles per tile phase (lane 0 of wave 0), printed
-  unsigned long long ph[5] = {0, 0, 0, 0, 0}, ph_prev = clock64();
-#define NBG_PH(k)                                        \
-  if (threadIdx.x == 0) {                                \
-    const unsigned long long c_ = clock64();             \
-    ph[k] += c_ - ph_prev;                               \
-    ph_prev = c_;                                        \
-  }
-#else
-#define NBG_PH(k)
-#endif
   const uint64_t g = (uint64_t)gridDim.x * WAVES;
-#ifdef NBG_XCD_TILES
-  // XCD-aware tile order (A/B switch of the build): workgroups are dealt round-robin to the 8
-  // XCDs, so number them XCD-major and the adjacent tiles (which share cache lines at their
-  // boundaries) stay on one XCD's L2
-  const uint32_t xb = (gridDim.x % 8 == 0) ? (blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8 : blockIdx.x;
-  uint64_t t = (uint64_t)xb * WAVES + w;
-#else
   // MARK: tile t -> workgroup t % grid first (a step's few tiles spread over CUs, each CU's miss
   // queue serving one wave's random claims; see spchain.hip); the final step keeps adjacent tiles
-  // in one workgroup (they share lines at their boundaries)
-  uint64_t t = (M == MARK || M == MARKB) && !NBG_MARK_PACKED ? (uint64_t)w * gridDim.x + blockIdx.x
-                                                             : (uint64_t)blockIdx.x * WAVES + w;
-#endif
+  // in one workgroup (they share lines at their boundaries; an XCD-major order measured -4 %,
+  // DESIGN.md §5)
+  uint64_t t = (M == MARK || M == MARKB) ? (uint64_t)w * gridDim.x + blockIdx.x : (uint64_t)blockIdx.x * WAVES + w;
   uint64_t sp_next = 0;            // lanes 0, 1: split (start, end) of tile t + g
   uint64_t a0 = 0, a1 = 0;         // split of tile t
   uint32_t e_pre = 0, r_pre = 0;   // lane's entry of tile t's segment-end window / row starts
@@ -1220,7 +1182,6 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
       if (lane < 2 && t + 2 * g < ntiles) sp_next = split_of(t + 2 * g, lane);
     }
     wave_lds_sync();
-    NBG_PH(0)
     const uint32_t* A = sEnd + 1;   // A[k] = end of segment a0 + k
 
     // lane-level merge path over this tile: assign a segment to every edge item
@@ -1249,7 +1210,6 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
       }
     }
     wave_lds_sync();
-    NBG_PH(1)
 
     if constexpr (M == MARKB) {
       uint32_t u[V];
@@ -1382,7 +1342,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
 #pragma unroll
         for (int i = 0; i < V; ++i) {
           const bool act = i * 64 + lane < nb;
-          dv[i] = (act && fp.fast.dst_yield) ? NBG_LD_STREAM(a.dst_vid + jj[i]) : 0;
+          dv[i] = (act && fp.fast.dst_yield) ? a.dst_vid[jj[i]] : 0;
         }
         // the WHERE column at its stored width (narrow copy of an INT column when it fits)
         switch (fp.fast.has_where ? fp.fast.wbytes : 0) {
@@ -1432,7 +1392,6 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
           pmask |= (uint32_t)pass << i;
         }
       }
-      NBG_PH(2)
       // row offsets in item order: wave-uniform prefix over the V ballots, then one LDS atomic
       // on the workgroup's cursor (rows go to the workgroup's own region: no global atomics)
       uint32_t run = 0;
@@ -1441,7 +1400,6 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
       unsigned long long base = 0;
       if (lane == 0 && run) base = atomicAdd(&sBase, (unsigned long long)run);
       base = __shfl(base, 0, 64);
-      NBG_PH(3)
       // phase B: YIELD for the passing items, written at their final rows
       const uint64_t region = fp.region_base + (uint64_t)blockIdx.x * fp.blk_cap + base;
       if (kDefer) {   // stored behind the next tile's loads (or after the loop)
@@ -1486,7 +1444,6 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
           }
         }
       }
-      NBG_PH(4)
     }
     a0 = na0;
     a1 = na1;
@@ -1500,11 +1457,6 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
         else flags[pu[i]] = 1;
       }
   }
-#ifdef NBG_PHASE_TIMING
-  if (kFinal && threadIdx.x == 0 && blockIdx.x % 256 == 0 && ntiles > 8192)
-    printf("PH blk %u tiles %llu fill %llu merge %llu loadA %llu scan %llu storeB %llu\n", blockIdx.x,
-           (unsigned long long)ntiles, ph[0], ph[1], ph[2], ph[3], ph[4]);
-#endif
   if (kFinal) {
     __syncthreads();   // every wave of the workgroup has reserved its rows
     if (threadIdx.x == 0) fp.blk_rows[blockIdx.x] = (uint32_t)sBase;

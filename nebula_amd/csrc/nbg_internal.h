@@ -382,29 +382,25 @@ struct SpTypes {                     // the CSRs one search direction expands (O
   const int64_t* rank[MAX_TYPES_Q];
   uint64_t ne[MAX_TYPES_Q];          // edges of each CSR (bounds of the checked build)
 };
-struct SpResult {                    // one query's result block (device, copied to pinned memory)
+struct SpResult {                    // one query's result (from the chain's ChOut)
   unsigned long long L;              // path length, 0 = no path within UPTO
   unsigned long long edges;          // BFS adjacency entries scanned (both sides)
-  unsigned long long err;            // 1 reconstruction failure, 2 spin bound, 3 list overflow
+  unsigned long long err;            // 1 reconstruction failure, 3 list overflow
   unsigned long long levels;         // BFS levels run
   unsigned long long abytes;         // algorithmic bytes of its level / B-set launches (chain mode)
   unsigned long long launches;       // device launches of its chain (setup + steps + hops)
   long long path[1 + 3 * MAX_PATH_LEN];   // [v0, t0, r0, v1, ...]
-  // phase trace (wall_clock64 ticks): trace[0] = launch start, then (kind << 56 | tick) per phase
-  unsigned long long ntrace;
-  unsigned long long trace[40];
-  unsigned long long sub[8];         // ticks of run_level's sub-steps on the leader (NBG_SP_TRACE)
 };
-struct SpCtx;                        // labels, item lists, control block, result block of one slot
+struct SpCtx;                        // labels and level-loop buffers of one slot (sp.hip)
 // item_cap: items a list may hold = sum over a side's types of (nv + E_t / 64), plus slack
-// One query at a time per context; the device buffers of each mode are allocated on its first use.
-enum SpMode : int { SP_PERSISTENT = 0, SP_CHAIN = 1 };
+// One query at a time per context; the level-loop buffers are allocated on its first use.
+enum SpMode : int { SP_CHAIN = 1 };
 SpCtx* sp_create(uint64_t nv, uint64_t item_cap, uint64_t edge_cap, hipStream_t s, std::string* err);
 void sp_destroy(SpCtx* c);
-// enqueue the search for s -> t (local dense ids, s != t) and its result copy: SP_PERSISTENT = one
-// persistent launch (sp.hip), SP_CHAIN = the device-driven level loop (spchain.hip, one OVER type)
-hipError_t sp_launch(SpCtx* c, int mode, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible,
-                     const int64_t* vids, uint32_t s, uint32_t t, uint32_t upto);
+// enqueue the search for s -> t (local dense ids, s != t): the device-driven level loop
+// (spchain.hip, one OVER type per direction), its result stored into mapped host memory
+hipError_t sp_launch(SpCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible, const int64_t* vids,
+                     uint32_t s, uint32_t t, uint32_t upto);
 bool sp_ready(SpCtx* c);
 struct SpPair {                 // one query of sp_launch_batch
   const SpTypes* fwd;

@@ -360,7 +360,7 @@ int32_t device_pair(PathCtx& c, int mode, uint32_t s, uint32_t t, uint32_t upto,
     if (!E.sp) return E.fail(NBG_E_OUT_OF_MEMORY, err);
   }
   if (!host_degree(c, c.fwd, s) || !host_degree(c, c.bwd, t)) return NBG_OK;   // an endpoint without edges
-  hipError_t he = sp_launch(E.sp, mode, sp_types(c.E, c.fwd), sp_types(c.E, c.bwd), E.snap.d_visible, E.snap.d_vids, s, t, upto);
+  hipError_t he = sp_launch(E.sp, sp_types(c.E, c.fwd), sp_types(c.E, c.bwd), E.snap.d_visible, E.snap.d_vids, s, t, upto);
   SpResult r;
   if (he == hipSuccess) he = sp_wait(E.sp, &r);
   if (he != hipSuccess) return dev_fail(E, he, "shortest path");
@@ -374,15 +374,11 @@ int32_t device_pair(PathCtx& c, int mode, uint32_t s, uint32_t t, uint32_t upto,
 // One-pair SHORTEST on a single engine.  NBG_SP_MODE (read per query: tests switch it):
 //   chain (default) - the device-driven level loop (spchain.hip): one host round trip per pair;
 //                     one OVER type per direction, other requests take the host loop
-//   persistent      - one persistent launch (sp.hip); NBG_SP_PERSISTENT=1 means the same
 //   host            - the host-driven level loop (bidirectional above), one round trip per level
 constexpr int PM_HOST = -1;
 int sp_mode(const PathCtx& c) {
-  const char* p = getenv("NBG_SP_PERSISTENT");
-  if (p && atoi(p) != 0) return SP_PERSISTENT;
   const char* m = getenv("NBG_SP_MODE");
   if (m && !strcmp(m, "host")) return PM_HOST;
-  if (m && !strcmp(m, "persistent")) return SP_PERSISTENT;
   return c.fwd.n == 1 && c.bwd.n == 1 ? (int)SP_CHAIN : PM_HOST;
 }
 
@@ -875,7 +871,7 @@ int32_t nbg_find_path_submit(nbg_engine* h, const nbg_path_request* rq, nbg_path
     ps.sp = E.new_sp(ps.stream, &err);
     if (!ps.sp) { delete t; return E.fail(NBG_E_OUT_OF_MEMORY, err); }
   }
-  hipError_t he = sp_launch(ps.sp, pl.mode, pl.fwd, pl.bwd, E.snap.d_visible, E.snap.d_vids, pl.s, pl.t, pl.upto);
+  hipError_t he = sp_launch(ps.sp, pl.fwd, pl.bwd, E.snap.d_visible, E.snap.d_vids, pl.s, pl.t, pl.upto);
   if (he != hipSuccess) { delete t; return dev_fail(E, he, "shortest path"); }
   t->slot = slot;
   ps.ticket = t;
@@ -917,7 +913,7 @@ int32_t nbg_find_path_batch(nbg_engine* h, const nbg_path_request* reqs, uint64_
         }
       }
       SpResult r;
-      hipError_t he = sp_launch(E.sp, x.mode, x.fwd, x.bwd, E.snap.d_visible, E.snap.d_vids, x.s, x.t, x.upto);
+      hipError_t he = sp_launch(E.sp, x.fwd, x.bwd, E.snap.d_visible, E.snap.d_vids, x.s, x.t, x.upto);
       if (he == hipSuccess) he = sp_wait(E.sp, &r);
       delete res;
       if (he != hipSuccess) {

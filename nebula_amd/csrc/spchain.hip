@@ -43,20 +43,14 @@ namespace {
 
 constexpr int CH_BLOCK = 256;
 constexpr int CH_WAVES = CH_BLOCK / 64;
-#ifndef NBG_CH_VT
-#define NBG_CH_VT 2
-#endif
-// merge-path items per lane per tile (NBG_CH_VT: an A/B build switch).  A level's critical path is
+// merge-path items per lane per tile.  A level's critical path is
 // the slowest wave's chain of dependent accesses, so shorter tiles spread a level over more waves:
 // RMAT-26 10k pairs, p50 0.131 ms at 8, 0.110 at 4, 0.107 at 2 (0.104 with a 256-workgroup step
 // grid), 0.103 at 1 but p99 0.30-0.34 ms and batched -17 % (profiles/r03_vt2_sp_vt_ab.txt,
 // r03_fin2_sp_vt2_batch_ab.txt)
-constexpr int CH_VT = NBG_CH_VT;
+constexpr int CH_VT = 2;
 constexpr int CH_TILE = 64 * CH_VT;       // items (entries + edges) per wave tile
-#ifndef NBG_CH_HOP_WGS
-#define NBG_CH_HOP_WGS 64
-#endif
-constexpr int CH_HOP_WGS = NBG_CH_HOP_WGS;   // workgroups scanning one greedy hop
+constexpr int CH_HOP_WGS = 64;            // workgroups scanning one greedy hop
 constexpr int CH_HOP_U = 4;               // neighbours per thread in flight (greedy)
 constexpr int CH_MAXS = 2 * MAX_PATH_LEN + 2;   // step launches of one query, at most
 
@@ -215,23 +209,6 @@ namespace {
 // memory, and the query fails with that code.
 #ifndef CH_GUARD
 #define CH_GUARD 0
-#endif
-// CH_PHASE=1 (an experiment build, `make EXTRA=-DCH_PHASE=1`): workgroup 0's wave 0 of every step
-// launch over more than 64 tiles prints the 100 MHz wall-clock ticks spent in each phase of its tiles.
-#ifndef CH_PHASE
-#define CH_PHASE 0
-#endif
-#if CH_PHASE
-#define CH_PH(k)                                          \
-  do {                                                    \
-    const unsigned long long c_ = wall_clock64();         \
-    ph[k] += c_ - ph_prev;                                \
-    ph_prev = c_;                                         \
-  } while (0)
-#else
-#define CH_PH(k) \
-  do {           \
-  } while (0)
 #endif
 
 template <typename T>
@@ -502,24 +479,16 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
   uint32_t* const sEnd = sEndAll[w];
   uint32_t* const sRs = sRsAll[w];
   uint16_t* const sSeg = sSegAll[w];
-#if CH_PHASE
-  unsigned long long ph[12] = {0}, ph_prev = wall_clock64(), rounds = 0;
-#endif
   // tile t -> workgroup t % nblk, wave (t / nblk) % NW: the tiles of a level spread over as many
   // CUs as it has tiles (up to the grid) before any CU gets a second one.  A tile's random loads
   // and atomics (8 per lane) queue at its CU, so tiles packed 4 to a workgroup had 4 waves' misses
-  // in one CU's queue while most CUs idled (NBG_SP_PACKED=1: the packed order, for A/B)
-#ifdef NBG_SP_PACKED
-  for (uint64_t t = (uint64_t)bid * NW + w; t < ntiles; t += (uint64_t)nblk * NW) {
-#else
+  // in one CU's queue while most CUs idled
   for (uint64_t t = (uint64_t)w * nblk + bid; t < ntiles; t += (uint64_t)nblk * NW) {
-#endif
     uint32_t c[CH_VT];   // the vertex a claim is about: the neighbour, or (pull) the list entry
     uint32_t cm = 0, mm = 0;
     // once this level has met, its claims are not expanded again: their appends are skipped
     // (read now, used after the claims: the load is off the critical path)
     const unsigned long long met_now = bfs ? ld_agent(&C.lmeet[i]) : 0ull;
-    CH_PH(0);
     uint64_t sp = 0;
     if (first) {   // one entry: every tile's split is 0, the last tile's end is 1
       sp = lane == 1 && (t + 1) * CH_TILE >= npath ? n : 0;
@@ -545,7 +514,6 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
       }
     }
     wave_lds_sync();
-    CH_PH(1);
     const uint32_t* Aend = sEnd + 1;   // Aend[j] = end of entry a0 + j
     {   // lane-level merge path: the entry of every edge item
       const int diag = lane * CH_VT, dmax = na + nb;
@@ -584,7 +552,6 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
       }
     }
     wave_lds_sync();   // (the next tile rewrites the window)
-    CH_PH(2);
     if (pull) {
       uint32_t tl[CH_VT], vis[CH_VT];
 #pragma unroll
@@ -599,7 +566,6 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
 #pragma unroll
       for (int j = 0; j < CH_VT; ++j) c[j] = x[j];
     }
-    CH_PH(3);
     uint32_t old[CH_VT], gate[CH_VT];
     // a BFS level before its meet: the other side's label and the degree / row start of EVERY
     // neighbour are loaded with its own label, so the meet test and the append do not wait for
@@ -648,13 +614,11 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
         cm |= 1u << j;
       }
     }
-    CH_PH(4);
     if (spec) {   // meet test: the claimed vertices the other side has labelled
 #pragma unroll
       for (int j = 0; j < CH_VT; ++j)
         if (((cm >> j) & 1u) && live(sol[j], oepoch)) mm |= 1u << j;
     }
-    CH_PH(5);
     if (!__ballot((cm | mm) != 0)) continue;
     // appends: one packed atomic per wave and list (aggregating them per workgroup behind two
     // barriers measured 4 % slower, profiles/r03_v_sp_wg_append_ab.txt)
@@ -673,12 +637,7 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
         }
       }
     }
-#if CH_PHASE
-    { uint32_t sink = 0; for (int j = 0; j < CH_VT; ++j) sink += dg[j] + rs[j]; if (sink == 0xFFFFFFFFu) ph[11] += 1; }
-#endif
-    CH_PH(6);
     if (append && !met_now) wave_append(A, D, out_acc, &C.err, c, am, dg, rs);   // (a wave-uniform condition)
-    CH_PH(7);
     // the sides met: LAB_M stamps, the meet list over in-edges, the level's meet count
     uint32_t nm = 0;
 #pragma unroll
@@ -691,24 +650,13 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
         ++nm;
       }
     }
-    CH_PH(8);
     if (__ballot(mm != 0)) {
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) nm += __shfl_xor(nm, o, 64);
       if (lane == 0) atomicAdd(&C.lmeet[i], (unsigned long long)nm);
       wave_append(A, A.list[CL_M], &C.macc, &C.err, c, mm, dg, rs);
     }
-    CH_PH(9);
-#if CH_PHASE
-    ++rounds;
-#endif
   }
-#if CH_PHASE
-  if (bid == 0 && threadIdx.x == 0 && ntiles > 64 && nblk > 1)
-    printf("CHPH step %d bfs %d ntiles %llu items %llu rounds %llu ticks %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu\n", i,
-           (int)bfs, (unsigned long long)ntiles, (unsigned long long)npath, rounds, ph[0], ph[1], ph[2], ph[3], ph[4], ph[5],
-           ph[6], ph[7], ph[8], ph[9]);
-#endif
 }
 
 // Items (entries + edges) of the source list of step P (as ch_level picks it).
@@ -979,10 +927,8 @@ struct ChBatch {
   int n;
   uint32_t per;
 };
-#ifndef NBG_STEPB_WPE
-#define NBG_STEPB_WPE 2   // (2 waves/SIMD: no spills; batched 33.3-33.9k -> 34.7-35.0k pairs/s, profiles/r03_y_sp_spec_ab.txt)
-#endif
-__global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(NBG_STEPB_WPE))) k_ch_step_b(ChBatch b, int i) {
+// (2 waves/SIMD: no spills; batched 33.3-33.9k -> 34.7-35.0k pairs/s, profiles/r03_y_sp_spec_ab.txt)
+__global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) k_ch_step_b(ChBatch b, int i) {
   const uint32_t p = blockIdx.x / b.per;
   if ((int)p < b.n) ch_step<CH_WAVES>(*b.A[p], b.q[p], i, blockIdx.x % b.per, b.per);
 }
@@ -1271,7 +1217,6 @@ void chain_result(const ChainCtx* c, SpResult* out) {
   const uint32_t hpos = (uint32_t)(h.hpos >> 32);
   out->L = (F.met && !h.err && hpos == F.L) ? F.L : 0;
   if (F.met && !h.err && hpos != F.L) out->err = 2;   // (cannot happen: the hops were enqueued)
-  out->ntrace = 0;
   if (out->L) memcpy(out->path, h.path, (1 + 3 * (size_t)out->L) * sizeof(long long));
 }
 

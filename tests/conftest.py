@@ -25,9 +25,9 @@ def nba_data():
         return json.load(f)
 
 
-@pytest.fixture(params=["chain", "host", "persistent"])
+@pytest.fixture(params=["chain", "host"])
 def sp_mode(request, monkeypatch):
-    """Every one-pair FIND SHORTEST PATH device path (NBG_SP_MODE, read per query): the
+    """Both one-pair FIND SHORTEST PATH paths (NBG_SP_MODE, read per query): the
     device-driven level loop (default), the host-driven level loop and the persistent search."""
     monkeypatch.delenv("NBG_SP_PERSISTENT", raising=False)
     monkeypatch.setenv("NBG_SP_MODE", request.param)
