@@ -432,8 +432,10 @@ struct Ctx {
     return hipStreamSynchronize(env.stream);
   }
   hipError_t comm_err() { return hipErrorUnknown; }
-  hipError_t bitmap(unsigned long long** p) {
-    CAP_TRY(arena.get(p, words));
+  // (into `a`, default the search's arena: a per-target arena keeps a multi-target search's
+  // memory at one target's bitmaps)
+  hipError_t bitmap(unsigned long long** p, Arena* a = nullptr) {
+    CAP_TRY((a ? a : &arena)->get(p, words));
     return hipMemsetAsync(*p, 0, words * 8, env.stream);
   }
   // replicate a bitmap whose bits were set by every rank anywhere in the global id space
@@ -451,8 +453,8 @@ struct Ctx {
     if (env.comm->allgather(local, Y, seg_words * 8, env.stream)) return comm_err();
     return hipSuccess;
   }
-  hipError_t expand(const CapCsr& cs, const unsigned long long* X, unsigned long long** Y) {
-    CAP_TRY(bitmap(Y));
+  hipError_t expand(const CapCsr& cs, const unsigned long long* X, unsigned long long** Y, Arena* a = nullptr) {
+    CAP_TRY(bitmap(Y, a));
     hipLaunchKernelGGL(k_cap_expand, dim3(gridc(env.nv, 8192)), dim3(CB), 0, env.stream, cs, X, *Y, env.nv, gbase,
                        env.K, env.visible, ctr + 3);
     CAP_TRY(hipGetLastError());
@@ -470,11 +472,11 @@ struct Ctx {
     *n = h_ctr[0];
     return hipSuccess;
   }
-  hipError_t set_ids(const std::vector<uint32_t>& ids, unsigned long long** bm) {
-    CAP_TRY(bitmap(bm));
+  hipError_t set_ids(const std::vector<uint32_t>& ids, unsigned long long** bm, Arena* a = nullptr) {
+    CAP_TRY(bitmap(bm, a));
     if (ids.empty()) return hipSuccess;
     uint32_t* d = nullptr;
-    CAP_TRY(arena.get(&d, ids.size()));
+    CAP_TRY((a ? a : &arena)->get(&d, ids.size()));
     CAP_TRY(hipMemcpyAsync(d, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, env.stream));
     hipLaunchKernelGGL(k_cap_set, dim3(gridc(ids.size())), dim3(CB), 0, env.stream, d, (uint64_t)ids.size(), *bm);
     CAP_TRY(hipGetLastError());
@@ -547,9 +549,10 @@ hipError_t cap_shortest(const CapEnv& env, const PathTypes& fwd, const PathTypes
   CAP_TRY(hipMemcpyAsync(d_sg, Sgid.data(), Sgid.size() * 4, hipMemcpyHostToDevice, env.stream));
   CAP_TRY(hipMemcpyAsync(d_sv, Svid.data(), Svid.size() * 8, hipMemcpyHostToDevice, env.stream));
   for (uint32_t t : Tgid) {
+    Arena ta{env.stream};   // this target's to-side levels and B-sets, freed before the next target
     std::vector<unsigned long long*> T;
     unsigned long long* t0 = nullptr;
-    CAP_TRY(x.set_ids(std::vector<uint32_t>{t}, &t0));
+    CAP_TRY(x.set_ids(std::vector<uint32_t>{t}, &t0, &ta));
     T.push_back(t0);
     uint32_t L = 0;
     for (uint32_t c = 1; c <= steps && !L; ++c) {
@@ -561,7 +564,7 @@ hipError_t cap_shortest(const CapEnv& env, const PathTypes& fwd, const PathTypes
       CAP_TRY(x.and_count(F[c], F[c], nullptr, &nf));
       if (2 * c > upto && c == steps) break;
       unsigned long long* y = nullptr;
-      CAP_TRY(x.expand(cb, T[c - 1], &y));
+      CAP_TRY(x.expand(cb, T[c - 1], &y, &ta));
       T.push_back(y);
       uint64_t nt = 0;
       CAP_TRY(x.and_count(y, y, nullptr, &nt));
@@ -577,13 +580,13 @@ hipError_t cap_shortest(const CapEnv& env, const PathTypes& fwd, const PathTypes
     std::vector<unsigned long long*> B(L + 1, nullptr);
     for (uint32_t i = h + 1; i <= L; ++i) B[i] = T[L - i];
     unsigned long long* bh = nullptr;
-    CAP_TRY(x.bitmap(&bh));
+    CAP_TRY(x.bitmap(&bh, &ta));
     uint64_t nb = 0;
     CAP_TRY(x.and_count(F[h], T[L - h], bh, &nb));
     B[h] = bh;
     for (int i = (int)h - 1; i >= 0; --i) {
       unsigned long long* bi = nullptr;
-      CAP_TRY(x.bitmap(&bi));
+      CAP_TRY(x.bitmap(&bi, &ta));
       unsigned long long* local = bi;   // single engine: the segment is the whole bitmap
       if (env.world > 1) {
         CAP_TRY(hipMemsetAsync(x.seg, 0, x.seg_words * 8, env.stream));
