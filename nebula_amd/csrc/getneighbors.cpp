@@ -408,8 +408,29 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
       a.gbase = E.partitioned() ? (uint32_t)((uint64_t)E.cfg.rank * E.npad) : 0u;
       he = ws_expand_final(ws, a, starts.size(), ebound[i], 1, (int)i, plist[i], region[i], blk_cap[i], nullptr);
     }
-    if (he == hipSuccess) he = ws_end_query(ws);
+    // the end of the request packs a small result into mapped host memory with the query's state
+    // (k_q_out_small): such a request costs one host round trip, not two
+    if (he == hipSuccess) {
+      SmallPack sp{};
+      sp.ntypes = (int)plist.size();
+      sp.ncols = ncols;
+      for (size_t i = 0; i < plist.size(); ++i) {
+        sp.region[i] = region[i];
+        sp.blk_cap[i] = blk_cap[i];
+        sp.grid[i] = ws_final_grid_of(ws, (int)i);
+      }
+      he = ws_end_query_async_small(ws, sp);
+    }
+    if (he == hipSuccess) he = ws_end_query_wait(ws);
     if (he != hipSuccess) return E.fail(NBG_E_DEVICE, std::string("HIP: ") + hipGetErrorString(he));
+    uint64_t all_rows = 0;
+    for (size_t i = 0; i < plist.size(); ++i) {
+      const unsigned grid = ws_final_grid_of(ws, (int)i);
+      const uint32_t* per = ws_host_blk_rows(ws, (int)i);
+      for (unsigned b = 0; b < grid; ++b) all_rows += per[b];
+    }
+    const int64_t* small = ws_host_small_rows(ws, all_rows);   // (nullptr: too large, fetched below)
+    uint64_t small_off = 0;
     for (size_t i = 0; i < plist.size(); ++i) {
       const int nc = (int)plist[i].yield_reg.size();
       const unsigned grid = ws_final_grid_of(ws, (int)i);
@@ -421,18 +442,25 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
           segs.emplace_back(region[i] + (uint64_t)b * blk_cap[i], per[b]);
           total += per[b];
         }
-      // the rows into a pinned block of the engine's pool (column c at c * total), packed there
-      // by the device (a pageable copy per column cost more than the request's expansion)
+      std::vector<const int64_t*> cols(nc);
+      // the rows: in the mapped small block (column c at c * all_rows, this type's rows after the
+      // earlier types'), or into a pinned block of the engine's pool (column c at c * total),
+      // packed there by the device (a pageable copy per column cost more than the expansion)
       size_t hbytes = 0;
-      int64_t* hb = total ? static_cast<int64_t*>(E.pinned_get(total * (size_t)nc * 8, &hbytes)) : nullptr;
-      if (total && !hb) return E.fail(NBG_E_OUT_OF_MEMORY, "row fetch staging");
+      int64_t* hb = nullptr;
+      if (small) {
+        for (int c = 0; c < nc; ++c) cols[c] = small + (size_t)c * all_rows + small_off;
+        small_off += total;
+      } else {
+        hb = total ? static_cast<int64_t*>(E.pinned_get(total * (size_t)nc * 8, &hbytes)) : nullptr;
+        if (total && !hb) return E.fail(NBG_E_OUT_OF_MEMORY, "row fetch staging");
+        for (int c = 0; c < nc; ++c) cols[c] = hb + (size_t)c * total;
+      }
       struct Put {   // (the block goes back to the pool on every path out of this scope)
         Engine& e; int64_t* p; size_t n;
         ~Put() { if (p) e.pinned_put(p, n); }
       } put{E, hb, hbytes};
-      std::vector<const int64_t*> cols(nc);
-      for (int c = 0; c < nc; ++c) cols[c] = hb + (size_t)c * total;
-      if (total && ws_fetch_rows_pinned(ws, segs, nc, total, hb) != hipSuccess)
+      if (!small && total && ws_fetch_rows_pinned(ws, segs, nc, total, hb) != hipSuccess)
         return E.fail(NBG_E_DEVICE, "row fetch failed");
       // key order: CSR index order (rows of one source are contiguous and sorted)
       std::vector<uint64_t> ord(total);

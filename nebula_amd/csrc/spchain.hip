@@ -682,7 +682,13 @@ __device__ __forceinline__ void ch_step(const ChArgs& A, const ChQ& q, int i, ui
   ChFirst f0{};
   ChSnap P = i == 0 ? first_snap(A, q, &f0) : snap_for(st, q, (int)j);
   const bool lead = bid == 0 && threadIdx.x == 0;
-  if (i == 0 && lead) first_store(A, q, f0, P);
+  if (i == 0 && bid == 0) {
+    // the splits of {s} and {t} for later launches (a backward level from {t}, a pull B-set step
+    // from {s}): one entry, so every tile's split is 0
+    for (uint64_t t = threadIdx.x; t * CH_TILE <= f0.dsf && t < A.tsplit_cap; t += CH_BLOCK) A.list[CL_F0].tsplit[t] = 0;
+    for (uint64_t t = threadIdx.x; t * CH_TILE <= f0.dsb && t < A.tsplit_cap; t += CH_BLOCK) A.list[CL_B0].tsplit[t] = 0;
+    if (lead) first_store(A, q, f0, P);
+  }
   if (P.phase == PH_DONE) {
     if (lead) st->first[i + 1] = j;
     return;
