@@ -436,8 +436,8 @@ int32_t nbg_comm_init_local(nbg_engine* const* engines, int32_t n);
  * with the same code instead:
  *   - a rank-local failure before the query's first collective (allocation, a start list whose
  *     edges exceed one rank's list limit, ...) reaches every rank: every rank returns the code of
- *     the lowest-ranked rank that failed, and the engines stay usable.  For GO without YIELD
- *     DISTINCT and without $- / $var inputs the failing rank still takes part in the query's
+ *     the lowest-ranked rank that failed, and the engines stay usable.  For GO without $- / $var
+ *     inputs (YIELD DISTINCT included) the failing rank still takes part in the query's
  *     collectives and its status travels with the query's statistics (no extra round trip):
  *     nbg_go_execute fails on every rank; nbg_go_submit returns a ticket on every rank (so every
  *     rank's query slots stay in step) and nbg_go_wait on it returns the code.  Other statements (and

@@ -1033,7 +1033,9 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
   // collectives, with zero bitmaps and its status word in the statistics, and every rank fails the
   // query when it reads them (go_collect).  Other statements agree first (Comm::agree).
   static const bool force_agree = getenv("NBG_GO_AGREE") && atoi(getenv("NBG_GO_AGREE")) != 0;
-  const bool in_band = part && !st->distinct && !st->uses_input && !force_agree;
+  // (YIELD DISTINCT too: its owner exchange runs in go_collect, which every rank leaves at the
+  // in-band status before reaching it)
+  const bool in_band = part && !st->uses_input && !force_agree;
   if (in_band) {
     if (lrc) {
       int32_t agreed = NBG_OK;
@@ -1355,21 +1357,18 @@ static int32_t go_collect(Engine& E, const nbg_go_stmt* st, GoPending* p, nbg_ro
       rows->count += kept[k];
     }
     if (E.partitioned()) {
-      // the exchange is collective: a local failure of the dedup pass is agreed first
-      Comm* cm = ws_get_comm(ws);
-      int32_t agreed = NBG_OK;
-      if (cm->agree(ws_stream(ws), de == hipSuccess ? NBG_OK : NBG_E_DEVICE, &agreed)) {
-        delete rows;
-        return E.fail(NBG_E_DEVICE, "DISTINCT agreement: " + cm->last);
-      }
-      if (agreed && de == hipSuccess) {
-        delete rows;
-        return E.fail(agreed, "YIELD DISTINCT failed on another rank");
-      }
-    }
-    if (de == hipSuccess && E.partitioned()) {
+      // the exchange is collective: every rank takes part, a rank whose dedup pass failed with no
+      // rows and its status, which travels with the exchange's counts (no agreement of its own)
       std::vector<DistinctBlock> db;
-      de = ws_distinct_exchange(ws, segments(nullptr), ncols, rows->kinds, &db);
+      int32_t gstatus = NBG_OK;
+      const int32_t mine = de == hipSuccess ? NBG_OK : NBG_E_DEVICE;
+      de = ws_distinct_exchange(ws, mine ? std::vector<std::array<uint64_t, 3>>{} : segments(nullptr), ncols,
+                                rows->kinds, &db, mine, &gstatus);
+      if (de == hipSuccess && gstatus) {
+        delete rows;
+        return E.fail(gstatus, mine ? std::string("YIELD DISTINCT: the dedup pass failed")
+                                    : "YIELD DISTINCT failed on another rank (code " + std::to_string(gstatus) + ")");
+      }
       rows->count = 0;
       for (size_t i = 0; de == hipSuccess && i < rows->blocks.size() && i < db.size(); ++i) {
         rows->blocks[i].region = db[i].region;

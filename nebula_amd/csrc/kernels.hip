@@ -2508,7 +2508,9 @@ hipError_t ws_distinct(Workspace* w, const std::vector<std::array<uint64_t, 3>>&
 }
 
 hipError_t ws_distinct_exchange(Workspace* w, const std::vector<std::array<uint64_t, 3>>& segs, int ncols,
-                                const std::vector<std::vector<VKind>>& kinds, std::vector<DistinctBlock>* out) {
+                                const std::vector<std::vector<VKind>>& kinds, std::vector<DistinctBlock>* out,
+                                int32_t status, int32_t* gstatus) {
+  *gstatus = NBG_OK;
   Comm* comm = w->comm;
   const int G = comm ? comm->world : 1, me = comm ? comm->rank : 0;
   const int T = (int)kinds.size();
@@ -2530,10 +2532,13 @@ hipError_t ws_distinct_exchange(Workspace* w, const std::vector<std::array<uint6
   };
   const uint64_t GT = (uint64_t)G * T;
   HIP_TRY(grow((void**)&w->xown, &w->xown_cap, std::max<uint64_t>(total, 1) * 4));
-  HIP_TRY(grow((void**)&w->xcnt, &w->xcnt_cap, (GT + (uint64_t)G * GT + 2 * GT) * 8));
-  unsigned long long* cnt = w->xcnt;            // [G][T] this rank's rows per (owner, type)
-  unsigned long long* all = cnt + GT;           // [G ranks][G][T]
-  unsigned long long* base = all + (uint64_t)G * GT;
+  // each rank's counts carry its status word (the local dedup pass): a failure reaches every rank
+  // with the counts, so the exchange needs no agreement of its own
+  const uint64_t GS = GT + 1;
+  HIP_TRY(grow((void**)&w->xcnt, &w->xcnt_cap, (GS + (uint64_t)G * GS + 2 * GT) * 8));
+  unsigned long long* cnt = w->xcnt;            // [G][T] this rank's rows per (owner, type), then its status
+  unsigned long long* all = cnt + GS;           // [G ranks][G][T + status]
+  unsigned long long* base = all + (uint64_t)G * GS;
   unsigned long long* cursor = base + GT;
   if (!w->dkinds) HIP_TRY(hipMalloc((void**)&w->dkinds, MAX_TYPES_Q * MAX_YIELDS));
   uint8_t hk[MAX_TYPES_Q * MAX_YIELDS] = {};
@@ -2551,17 +2556,24 @@ hipError_t ws_distinct_exchange(Workspace* w, const std::vector<std::array<uint6
   }
   if (!meta.empty()) HIP_TRY(hipMemcpy(w->dseg, meta.data(), meta.size() * 8, hipMemcpyHostToDevice));
   HIP_TRY(hipMemsetAsync(cnt, 0, GT * 8, w->stream));
+  const unsigned long long st_word = (unsigned long long)(long long)status;
+  HIP_TRY(hipMemcpyAsync(cnt + GT, &st_word, 8, hipMemcpyHostToDevice, w->stream));
   const unsigned grid = (unsigned)std::min<uint64_t>(std::max<size_t>(segs.size(), 1), 8192);
   if (!segs.empty()) {
     hipLaunchKernelGGL(k_row_route, dim3(grid), dim3(BLOCK), 0, w->stream, w->dseg, (int)segs.size(), w->d_row_cols,
                        ncols, w->dkinds, G, T, w->xown, cnt);
     HIP_TRY(hipGetLastError());
   }
-  if (comm->allgather(cnt, all, GT * 8, w->stream)) return hipErrorUnknown;
+  if (comm->allgather(cnt, all, GS * 8, w->stream)) return hipErrorUnknown;
   HIP_TRY(ws_sync(w));
-  std::vector<unsigned long long> h_all((uint64_t)G * GT);
+  std::vector<unsigned long long> h_all((uint64_t)G * GS);
   HIP_TRY(hipMemcpy(h_all.data(), all, h_all.size() * 8, hipMemcpyDeviceToHost));
-  auto at = [&](int r, int q, int t) { return h_all[(uint64_t)r * GT + (uint64_t)q * T + t]; };
+  for (int r = 0; r < G; ++r)   // the first failing rank's code, on every rank: nothing more is exchanged
+    if (h_all[(uint64_t)r * GS + GT]) {
+      *gstatus = (int32_t)(long long)h_all[(uint64_t)r * GS + GT];
+      return hipSuccess;
+    }
+  auto at = [&](int r, int q, int t) { return h_all[(uint64_t)r * GS + (uint64_t)q * T + t]; };
   uint64_t maxc = 1;
   for (int r = 0; r < G; ++r)
     for (int q = 0; q < G; ++q) {

@@ -564,8 +564,11 @@ struct DistinctBlock {
   uint64_t region = 0, blk_cap = 0;
   std::vector<uint32_t> counts;
 };
+// status: this rank's local status (its dedup pass); *gstatus: the first failing rank's, the same on
+// every rank (then nothing was exchanged and the query fails everywhere)
 hipError_t ws_distinct_exchange(Workspace* w, const std::vector<std::array<uint64_t, 3>>& segs, int ncols,
-                                const std::vector<std::vector<VKind>>& kinds, std::vector<DistinctBlock>* out);
+                                const std::vector<std::vector<VKind>>& kinds, std::vector<DistinctBlock>* out,
+                                int32_t status, int32_t* gstatus);
 hipError_t ws_distinct(Workspace* w, const std::vector<std::array<uint64_t, 3>>& segs, int ncols,
                        const std::vector<std::vector<VKind>>& kinds, std::vector<uint32_t>* counts);
 const uint32_t* ws_current_frontier(Workspace* w);

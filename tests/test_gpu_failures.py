@@ -96,8 +96,8 @@ def test_agreed_failures_leave_engines_usable(graph, world):
         out = c.each(submit_twice)
         assert [o[0] for o in out] == [L.E_OUT_OF_MEMORY] * world
         assert graphs.sorted_rows([r for o in out for r in o[1]]) == exp
-        # (3b) YIELD DISTINCT has an owner exchange of its own: its failures are agreed before
-        #      the query (Comm::agree) instead of carried in the statistics
+        # (3b) YIELD DISTINCT: its failures travel in band too (the statistics, then the owner
+        #      exchange's counts), with no agreement round trip of their own
         yd = [E.edge_prop("e", "_dst").encode()]
         exp_d = graphs.sorted_rows(single.go([r0], [1], 2, WHERE, yd, distinct=True))
         c.inject_fault(world - 1, L.FAULT_ALLOC)
