@@ -166,6 +166,20 @@ struct RcclComm final : Comm {
     if (aborted) return check(ncclSuccess, "ncclAllToAll");
     return check(ncclAllToAll(send, recv, bytes, ncclUint8, comm, s), "ncclAllToAll");
   }
+  int alltoallv(const void* send, const uint64_t* scount, const uint64_t* sdisp, void* recv, const uint64_t* rcount,
+                const uint64_t* rdisp, size_t elem, hipStream_t s) override {
+    if (aborted) return check(ncclSuccess, "ncclSend/ncclRecv");
+    const char* sp = static_cast<const char*>(send);
+    char* rp = static_cast<char*>(recv);
+    int rc = check(ncclGroupStart(), "ncclGroupStart");
+    for (int q = 0; q < world && !rc; ++q) {
+      if (scount[q]) rc = check(ncclSend(sp + sdisp[q] * elem, scount[q] * elem, ncclUint8, q, comm, s), "ncclSend");
+      if (!rc && rcount[q])
+        rc = check(ncclRecv(rp + rdisp[q] * elem, rcount[q] * elem, ncclUint8, q, comm, s), "ncclRecv");
+    }
+    const int end = check(ncclGroupEnd(), "ncclGroupEnd");
+    return rc ? rc : end;
+  }
   int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
     if (aborted) return check(ncclSuccess, "ncclAllGather");
     return check(ncclAllGather(send, recv, bytes, ncclUint8, comm, s), "ncclAllGather");
@@ -206,8 +220,9 @@ struct LocalGroup {
   uint64_t generation = 0;
   bool aborted = false;
   std::vector<const void*> send;
+  std::vector<const uint64_t*> vcount, vdisp;   // alltoallv: each rank's send counts / displacements
   std::vector<std::vector<unsigned long long>> red;
-  explicit LocalGroup(int w) : world(w), send(w, nullptr), red(w) {}
+  explicit LocalGroup(int w) : world(w), send(w, nullptr), vcount(w, nullptr), vdisp(w, nullptr), red(w) {}
   // false: the group was aborted (by a failing rank, or a peer that did not arrive in time)
   bool barrier() {
     std::unique_lock<std::mutex> lk(mu);
@@ -271,6 +286,29 @@ struct LocalComm final : Comm {
   }
   int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
     return exchange(send, recv, bytes, s, false);
+  }
+  int alltoallv(const void* send, const uint64_t* scount, const uint64_t* sdisp, void* recv, const uint64_t* rcount,
+                const uint64_t* rdisp, size_t elem, hipStream_t s) override {
+    int rc = hip(hipStreamSynchronize(s), "local alltoallv (producer)");
+    g->send[rank] = send;
+    g->vcount[rank] = scount;
+    g->vdisp[rank] = sdisp;
+    if (!g->barrier()) return gone("local alltoallv");
+    for (int q = 0; q < world && !rc; ++q) {
+      const uint64_t n = g->vcount[q][rank];
+      if (n != rcount[q]) {
+        last = "local alltoallv: count mismatch";
+        rc = -1;
+        break;
+      }
+      if (!n) continue;
+      const char* src = static_cast<const char*>(g->send[q]) + g->vdisp[q][rank] * elem;
+      rc = hip(hipMemcpyAsync(static_cast<char*>(recv) + rdisp[q] * elem, src, n * elem, hipMemcpyDeviceToDevice, s),
+               "local alltoallv copy");
+    }
+    if (!rc) rc = hip(hipStreamSynchronize(s), "local alltoallv (consumer)");
+    if (!g->barrier()) return gone("local alltoallv");
+    return rc;
   }
   int allreduce_sum_u64(unsigned long long* buf, size_t n, hipStream_t s) override {
     auto& mine = g->red[rank];

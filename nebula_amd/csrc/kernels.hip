@@ -40,11 +40,13 @@ constexpr int FLAG_ALIGN = 1024 * 16;           // flag array granularity (k_com
 constexpr int EXPAND_GRID = 2048;                // persistent k_expand grid (8 blocks / CU)
 
 enum KernelId { K_RELIST = 0, K_EXPAND_MARK, K_COMPACT, K_EXPAND_FINAL, K_BFS, K_GATHER, K_DEGSUM, K_GREEDY,
-                K_STAMP, K_PACK, K_ALLTOALL, K_BITS_COMPACT, K_COUNT };
+                K_STAMP, K_PACK, K_ALLTOALL, K_BITS_COMPACT, K_ROOTS, K_COUNT };
 static const char* const kKernelNames[K_COUNT] = {"k_relist", "k_expand<MARK>", "k_compact", "k_expand<FINAL>",
                                                   "k_expand<BFS>", "k_gather", "k_degsum", "k_greedy",
-                                                  "k_stamp", "k_pack_bits", "alltoall(xGMI)", "k_bits_compact"};
+                                                  "k_stamp", "k_pack_bits", "alltoall(xGMI)", "k_bits_compact",
+                                                  "alltoallv(roots)"};
 constexpr int BITS_BLOCK = BLOCK * 16;           // k_bits_compact: vertices (bits) per block
+constexpr uint64_t RW_BLOCK = 4 * BLOCK;          // root packing: bitmap words per prefix block
 
 struct InlineIds {                 // a short start list passed by value in the kernel arguments
   uint32_t n;
@@ -82,13 +84,25 @@ struct Workspace {
   uint32_t* seg_end1 = nullptr;   // set 1
   uint32_t* seg_rs1 = nullptr;
   uint32_t* tsplit1 = nullptr;
-  uint32_t* seen = nullptr;       // [nv + 1] claim stamps of the per-step dst SET (single engine)
-  uint32_t seen_stamp = 0;        // last stamp handed out
-  uint32_t step_stamp = 0;        // stamp of the current step (all its OVER types)
-  // partitioned DISTINCT exchange scratch (row owners, counts, send / receive buffers)
-  int64_t* bt_out = nullptr;      // partitioned roots: written over the global id space,
-  int64_t* bt_recv = nullptr;     // received per rank segment (G * npad each)
+  // claim bitmaps of the per-step dst SETs (single engine): one bit per vertex and MARK step,
+  // cleared behind the query's end (ws_end_query_wait); cbits_used = steps dirtied since
+  uint32_t* cbits = nullptr;
+  uint64_t cbits_words = 0;       // words per step bitmap (64-byte aligned)
+  int cbits_cap = 0;              // step bitmaps allocated
+  int cbits_used = 0;
+  // partitioned roots ($- / $var props read after 2+ steps): MARKB writes them over the global
+  // id space (bt_out); a hop sends only the roots of the vertices whose bits it sends, packed in
+  // bit order (bt_pack -> bt_recv), at offsets from the bitmaps' popcount prefixes (ws_roots)
+  int64_t* bt_out = nullptr;
+  int64_t* bt_pack = nullptr;
+  int64_t* bt_recv = nullptr;
+  uint32_t* bt_pre = nullptr;     // [2][world * npad / 64] popcount before each word in its RW_BLOCK
+  uint32_t* bt_boff = nullptr;    // [2][blocks] then the block's offset in its rank segment
+  uint64_t* bt_disp = nullptr;    // [2][world] packed displacements: sent, received
+  uint64_t* h_btc = nullptr;      // mapped pinned [2][world] counts: sent to / received from rank q
+  uint64_t* d_btc = nullptr;
   bool bt_active = false;         // this query tracks roots: the hop exchange carries them
+  // partitioned DISTINCT exchange scratch (row owners, counts, send / receive buffers)
   uint32_t* xown = nullptr;
   uint64_t xown_cap = 0;
   unsigned long long* xcnt = nullptr;
@@ -887,6 +901,7 @@ __device__ unsigned long long degree_of(const DegsumArgs& d, uint32_t v) {
 struct BfsParams {
   uint32_t* lab;                  // claim labels
   uint32_t stamp;                 // claimed label value
+  uint32_t* cbits;                // MARK claim mode: the step's claim bitmap
   uint32_t epoch;                 // a label is live when (lab >> LVL_BITS) == epoch
   const uint32_t* rlab;           // restriction (nullable): claim w only if rlab[w] == rstamp
   uint32_t rstamp;
@@ -903,7 +918,7 @@ struct BfsParams {
   unsigned long long* out_n;      // its length, zero before the level
   DegsumArgs deg;
   unsigned long long* dsum;       // nullable
-  // MARK claim mode (lab != nullptr): claimed neighbours go to this list with their edge space
+  // MARK claim mode (cbits != nullptr): claimed neighbours go to this list with their edge space
   // over nds (the next step's first OVER type); nlist.zero_next is zeroed by workgroup 0
   ListOut nlist;
   DegSrc nds;
@@ -938,8 +953,9 @@ struct FinalParams {
 };
 
 // MARK claim mode: the per-step dst SET (GoExecutor::getDstIdsFromResp, GoExecutor.cpp:501-541)
-// as claims — the first expansion of the step to CAS a neighbour's stamp to the step's stamp
-// owns it — and the owners appended to the next frontier list together with their edge space
+// as claims — the first expansion of the step to set a neighbour's bit in the step's bitmap
+// (nv / 8 bytes: L2-resident where per-vertex stamps were not; a plain load filters the
+// already-claimed before the atomic) owns it — and the owners appended to the next frontier list together with their edge space
 // over the next step's first OVER type: one packed atomic per wave for list positions and edge
 // offsets.  A vertex without edges there is kept (the list is the frontier of every OVER type).
 __device__ __forceinline__ void claim_append(const uint32_t (&u)[VT], const BfsParams& bp, int lane) {
@@ -950,9 +966,9 @@ __device__ __forceinline__ void claim_append(const uint32_t (&u)[VT], const BfsP
     rs[i] = 0;
     const uint32_t x = u[i];
     if (x == NO_ROW) continue;
-    const uint32_t old = bp.lab[x];
-    if (old == bp.stamp) continue;
-    if (atomicCAS(bp.lab + x, old, bp.stamp) != old) continue;
+    const uint32_t m = 1u << (x & 31);
+    if (bp.cbits[x >> 5] & m) continue;
+    if (atomicOr(bp.cbits + (x >> 5), m) & m) continue;
     cmask |= 1u << i;
     dg[i] = vdeg(bp.nds, x, &rs[i]);
   }
@@ -1223,10 +1239,10 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
           if (u[i] == NO_ROW) continue;
           const uint32_t src = list_id(a0 + s);
           a.bt[u[i]] = a.bt_first ? a.vids[src] : a.bt_in[src];
-          if (!bp.lab) flags[u[i]] = 1;
+          if (!bp.cbits) flags[u[i]] = 1;
         }
       }
-      if (bp.lab) claim_append(u, bp, lane);
+      if (bp.cbits) claim_append(u, bp, lane);
     } else if constexpr (M == MARK) {
       uint32_t u[V];   // all neighbour loads in flight before the flag stores / claims
 #pragma unroll
@@ -1238,7 +1254,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
           u[i] = a.col[(uint64_t)sRs[s] + (b0 + k - (uint64_t)sEnd[s])];   // sEnd[s] = start of a0+s
         }
       }
-      if (bp.lab) {
+      if (bp.cbits) {
         claim_append(u, bp, lane);
       } else if (bp.sparse) {
 #pragma unroll
@@ -1501,12 +1517,19 @@ __global__ void __launch_bounds__(BLOCK) k_pack_bits(uint8_t* __restrict__ flags
 // Owner side: OR the G received segments (one per sending rank) of this rank's id range; the
 // union is the global per-step dst SET restricted to the owner (getDstIdsFromResp).  Listed as
 // k_compact does: 16 vertices (bits) per thread.
-// bt_recv (nullable): the roots each rank wrote for this rank's vertices; a vertex reached from
-// several ranks takes the highest such rank's (the reference's last write is arbitrary as well)
+// rt.recv (nullable): the roots each rank sent for this rank's vertices, packed per sending rank
+// in bit order (k_rt_pack); a vertex reached from several ranks takes the highest such rank's
+// (the reference's last write is arbitrary as well)
+struct RootsIn {
+  const int64_t* recv;    // packed roots, rank q's from disp[world + q]
+  const uint32_t* pre;    // popcount prefixes of the received bitmap (k_rt_prefix, second half)
+  const uint32_t* boff;   // block offsets (k_rt_offsets, second half)
+  const uint64_t* disp;
+  uint64_t nwords;        // words of one bitmap (world * npad / 64)
+};
 __global__ void __launch_bounds__(BLOCK) k_bits_compact(const unsigned long long* __restrict__ recv, int world,
                                                         uint64_t seg_words, uint64_t nv, DegSrc ds, ListOut o,
-                                                        const int64_t* __restrict__ bt_recv, int64_t* __restrict__ bt_in,
-                                                        uint64_t npad) {
+                                                        RootsIn rt, int64_t* __restrict__ bt_in) {
   if (blockIdx.x == 0 && threadIdx.x == 0) *o.zero_next = 0;
   const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;   // 16-bit slice index
   const uint64_t word = i >> 2;
@@ -1532,15 +1555,113 @@ __global__ void __launch_bounds__(BLOCK) k_bits_compact(const unsigned long long
     if ((m >> b) & 1u) list_put(o, ds, pc++, (uint32_t)(lo + b), &pd, dg[b], rs[b], &t0, &t1);
     wave_splits(o.tsplit, t0, t1, pp);
   }
-  if (bt_recv && m) {
+  if (rt.recv && m) {
     for (int b = 0; b < 16; ++b) {
       if (!((m >> b) & 1u)) continue;
-      for (int q = world - 1; q >= 0; --q)
-        if ((recv[(uint64_t)q * seg_words + word] >> (sh + b)) & 1ull) {
-          bt_in[lo + b] = bt_recv[(uint64_t)q * npad + lo + b];
-          break;
-        }
+      for (int q = world - 1; q >= 0; --q) {
+        const uint64_t rw = (uint64_t)q * seg_words + word;
+        const unsigned long long bits = recv[rw];
+        if (!((bits >> (sh + b)) & 1ull)) continue;
+        const uint64_t at = rt.disp[world + q] + rt.boff[(rt.nwords + rw) / RW_BLOCK] + rt.pre[rt.nwords + rw] +
+                            (uint64_t)__popcll(bits & ((1ull << (sh + b)) - 1ull));
+        bt_in[lo + b] = rt.recv[at];
+        break;
+      }
     }
+  }
+}
+
+// Partitioned roots, 1 of 3: the popcount before every bitmap word within its block of RW_BLOCK
+// words, and each block's total, over the send bitmap (blocks [0, nb)) and the received one
+// ([nb, 2 nb)); 4 words per thread.
+__global__ void __launch_bounds__(BLOCK) k_rt_prefix(const unsigned long long* __restrict__ sb,
+                                                     const unsigned long long* __restrict__ rb, uint64_t nb,
+                                                     uint32_t* __restrict__ pre, uint32_t* __restrict__ bsum) {
+  __shared__ uint32_t s_w[WAVES];
+  const uint64_t blk = blockIdx.x;
+  const unsigned long long* src = blk < nb ? sb : rb;
+  const uint64_t w0 = (blk < nb ? blk : blk - nb) * RW_BLOCK + threadIdx.x * 4;
+  uint32_t c[4], t = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    c[k] = (uint32_t)__popcll(src[w0 + k]);
+    t += c[k];
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t inc = wave_incl_scan(t);
+  if (lane == 63) s_w[wv] = inc;
+  __syncthreads();
+  uint32_t run = inc - t;
+  for (int k = 0; k < wv; ++k) run += s_w[k];
+  uint32_t* out = pre + blk * RW_BLOCK + threadIdx.x * 4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    out[k] = run;
+    run += c[k];
+  }
+  if (threadIdx.x == BLOCK - 1) bsum[blk] = run;
+}
+
+// 2 of 3 (one workgroup): block totals -> offsets within their rank segment (spb blocks each;
+// segments 0..world-1 of the send bitmap, then world..2 world-1 of the received one), the
+// per-rank counts (cnt: mapped host memory, the host sizes the exchange from them) and the
+// packed displacements.
+__global__ void __launch_bounds__(BLOCK) k_rt_offsets(uint32_t* __restrict__ bsum, uint64_t spb, int world,
+                                                      uint64_t* __restrict__ disp, uint64_t* cnt) {
+  __shared__ uint32_t s_w[WAVES];
+  __shared__ unsigned long long s_run;
+  __shared__ unsigned long long s_cnt[2 * AGREE_WORDS];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int g = 0; g < 2 * world; ++g) {
+    if (threadIdx.x == 0) s_run = 0;
+    __syncthreads();
+    uint32_t* b = bsum + (uint64_t)g * spb;
+    for (uint64_t k0 = 0; k0 < spb; k0 += BLOCK) {
+      const uint64_t k = k0 + threadIdx.x;
+      const uint32_t v = k < spb ? b[k] : 0u;
+      const uint32_t inc = wave_incl_scan(v);
+      if (lane == 63) s_w[wv] = inc;
+      __syncthreads();
+      uint32_t base = 0, tot = 0;
+      for (int j = 0; j < WAVES; ++j) {
+        if (j < wv) base += s_w[j];
+        tot += s_w[j];
+      }
+      const unsigned long long run = s_run;
+      if (k < spb) b[k] = (uint32_t)(run + base + inc - v);
+      __syncthreads();
+      if (threadIdx.x == 0) s_run = run + tot;
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) s_cnt[g] = s_run;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int h = 0; h < 2; ++h) {
+      unsigned long long d = 0;
+      for (int q = 0; q < world; ++q) {
+        disp[h * world + q] = d;
+        d += s_cnt[h * world + q];
+      }
+    }
+  }
+  for (int g = threadIdx.x; g < 2 * world; g += BLOCK) cnt[g] = s_cnt[g];
+}
+
+// 3 of 3: the roots of the set bits of the send bitmap, packed per destination rank in bit order.
+__global__ void __launch_bounds__(BLOCK) k_rt_pack(const unsigned long long* __restrict__ sb, uint64_t nwords,
+                                                   uint64_t seg_words, const uint32_t* __restrict__ pre,
+                                                   const uint32_t* __restrict__ boff, const uint64_t* __restrict__ disp,
+                                                   const int64_t* __restrict__ bt_out, int64_t* __restrict__ pack) {
+  const uint64_t w = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (w >= nwords) return;
+  unsigned long long m = sb[w];
+  if (!m) return;
+  uint64_t at = disp[w / seg_words] + boff[w / RW_BLOCK] + pre[w];
+  const int64_t* src = bt_out + w * 64;
+  while (m) {
+    pack[at++] = src[__ffsll((long long)m) - 1];
+    m &= m - 1;
   }
 }
 
@@ -1826,7 +1947,7 @@ static double prof_bytes(const Workspace* w, const Prof::Rec& r, const QState& q
     case K_EXPAND_MARK: return 4.0 * (double)q.e_st[r.step][r.tix];        // 4 E_s neighbour ids
     // next frontier: 4|F_{s+1}| ids written + the fused degree pass of the next step (12|F_{s+1}|)
     case K_COMPACT: case K_BITS_COMPACT: return 16.0 * (double)q.step_n[r.step + 1];
-    case K_PACK: case K_ALLTOALL: return r.cols;                           // fixed sizes (set at launch)
+    case K_PACK: case K_ALLTOALL: case K_ROOTS: return r.cols;             // sizes known at launch
     case K_EXPAND_FINAL: {
       double rows = 0;
       for (unsigned b = 0; b < w->final_grid[r.tix]; ++b) rows += (double)w->h_blk_rows[(size_t)r.tix * EXPAND_GRID + b];
@@ -1919,7 +2040,9 @@ Workspace* ws_create(uint64_t max_frontier, uint64_t nv, uint64_t e_max, hipStre
   M((void**)&w->seg_rs1, w->cap_frontier * 4);
   M((void**)&w->rlist, w->cap_frontier * 4);
   M((void**)&w->flags, w->flag_bytes);
-  M((void**)&w->seen, (nv + 1) * 4);
+  w->cbits_words = cdiv(nv + 1, 512) * 16;
+  w->cbits_cap = 3;   // GO up to 4 STEPS without growing
+  M((void**)&w->cbits, w->cbits_cap * w->cbits_words * 4);
   w->e_max = e_max;
   w->cap_tiles = cdiv(w->cap_frontier + e_max + 1, TILE) + 2;
   M((void**)&w->tsplit, w->cap_tiles * 4);
@@ -1946,7 +2069,7 @@ Workspace* ws_create(uint64_t max_frontier, uint64_t nv, uint64_t e_max, hipStre
   if (e == hipSuccess) e = hipHostMalloc((void**)&w->h_prog, (size_t)MAX_TYPES_Q * MAX_PROGRAM * sizeof(Ins),
                                          hipHostMallocDefault);
   if (e == hipSuccess) e = hipMemsetAsync(w->flags, 0, w->flag_bytes, s);
-  if (e == hipSuccess) e = hipMemsetAsync(w->seen, 0, (nv + 1) * 4, s);
+  if (e == hipSuccess) e = hipMemsetAsync(w->cbits, 0, w->cbits_cap * w->cbits_words * 4, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
     if (err) *err = std::string("workspace allocation failed: ") + hipGetErrorString(e);
@@ -1959,12 +2082,13 @@ Workspace* ws_create(uint64_t max_frontier, uint64_t nv, uint64_t e_max, hipStre
 void ws_destroy(Workspace* w) {
   if (!w) return;
   for (void* p : {(void*)w->frontier[0], (void*)w->frontier[1], (void*)w->seg_end, (void*)w->seg_rs,
-                  (void*)w->seg_end1, (void*)w->seg_rs1, (void*)w->tsplit1, (void*)w->seen,
+                  (void*)w->seg_end1, (void*)w->seg_rs1, (void*)w->tsplit1, (void*)w->cbits,
                   (void*)w->rlist, (void*)w->flags, (void*)w->tsplit,
                   (void*)w->q, (void*)w->rows,
                   (void*)w->d_row_cols, (void*)w->d_prog, (void*)w->dtab, (void*)w->dkeep, (void*)w->dseg,
                   (void*)w->dcnt, (void*)w->dkinds, (void*)w->bt, (void*)w->walk_arena, (void*)w->sarena, (void*)w->xown,
-                  (void*)w->xcnt, (void*)w->xsend, (void*)w->xrecv, (void*)w->bt_out, (void*)w->bt_recv})
+                  (void*)w->xcnt, (void*)w->xsend, (void*)w->xrecv, (void*)w->bt_out, (void*)w->bt_recv,
+                  (void*)w->bt_pack, (void*)w->bt_pre, (void*)w->bt_boff, (void*)w->bt_disp})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)w->h_q, (void*)w->h_starts, (void*)w->h_prog, (void*)w->h_ps, (void*)w->h_path,
                   (void*)w->h_stage, (void*)w->h_small})
@@ -1977,6 +2101,7 @@ void ws_destroy(Workspace* w) {
     if (p) (void)hipFree(p);
   if (w->h_gpath) (void)hipHostFree(w->h_gpath);
   if (w->h_gst) (void)hipHostFree(w->h_gst);
+  if (w->h_btc) (void)hipHostFree(w->h_btc);
   for (void* p : {(void*)w->ps, (void*)w->pscratch, (void*)w->d_path})
     if (p) (void)hipFree(p);
   for (auto* p : w->lab)
@@ -2057,9 +2182,19 @@ hipError_t ws_wait(Workspace* w) {
   return e;
 }
 
+// The claim bitmaps a query dirtied, zeroed on its stream: behind the query's end event (off its
+// latency), or at the next begin when a query was abandoned after its MARKs were enqueued.
+static hipError_t ws_clear_claims(Workspace* w) {
+  if (!w->cbits_used) return hipSuccess;
+  const hipError_t e = hipMemsetAsync(w->cbits, 0, (size_t)w->cbits_used * w->cbits_words * 4, w->stream);
+  if (e == hipSuccess) w->cbits_used = 0;
+  return e;
+}
+
 hipError_t ws_begin_query(Workspace* w, const uint32_t* starts, uint64_t n, const std::vector<TypeProgram>* progs,
                           uint64_t stmt_id) {
   if (n > w->cap_frontier) return hipErrorInvalidValue;
+  HIP_TRY(ws_clear_claims(w));
   w->cur = 0;
   w->seg_ready = false;
   w->list_acc = nullptr;
@@ -2190,15 +2325,20 @@ hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, 
   // step + 2, whose list (step - 1) nobody reads any more)
   BfsParams bp{};
   if (!w->comm && !w->mark_flags) {
-    if (tix == 0) {
-      if (++w->seen_stamp == 0) {   // wrap: clear the stamps once
-        HIP_TRY(hipMemsetAsync(w->seen, 0, (w->nv + 1) * 4, w->stream));
-        w->seen_stamp = 1;
-      }
-      w->step_stamp = w->seen_stamp;
+    if (step < 1) return hipErrorInvalidValue;
+    if (step > w->cbits_cap) {   // a longer GO than any before: grow (rare; the stream drains first)
+      HIP_TRY(hipStreamSynchronize(w->stream));
+      HIP_TRY(hipFree(w->cbits));
+      w->cbits = nullptr;
+      w->cbits_cap = 0;
+      const int cap = step + 1 > MAX_STEPS ? MAX_STEPS : step + 1;
+      HIP_TRY(hipMalloc((void**)&w->cbits, (size_t)cap * w->cbits_words * 4));
+      HIP_TRY(hipMemsetAsync(w->cbits, 0, (size_t)cap * w->cbits_words * 4, w->stream));
+      w->cbits_cap = cap;
+      w->cbits_used = 0;
     }
-    bp.lab = w->seen;
-    bp.stamp = w->step_stamp;
+    bp.cbits = w->cbits + (size_t)(step - 1) * w->cbits_words;
+    if (step > w->cbits_used) w->cbits_used = step;
     const int nset = w->cur ^ 1;
     bp.nds = deg_src(next0);
     bp.nlist = list_out(w, w->frontier[nset], &w->q->acc[2 + (step + 1) % 3],
@@ -2643,10 +2783,16 @@ hipError_t ws_distinct_exchange(Workspace* w, const std::vector<std::array<uint6
 
 hipError_t ws_backtracker(Workspace* w, int64_t** out, int64_t** in) {
   if (!w->bt) HIP_TRY(hipMalloc((void**)&w->bt, (w->nv + 1) * 8));
-  if (w->comm && !w->bt_out) {
-    const uint64_t G = (uint64_t)w->comm->world;
-    HIP_TRY(hipMalloc((void**)&w->bt_out, G * w->npad * 8));
-    HIP_TRY(hipMalloc((void**)&w->bt_recv, G * w->npad * 8));
+  if (w->comm && !w->h_btc) {
+    const uint64_t G = (uint64_t)w->comm->world, nwords = G * w->npad / 64;
+    if (!w->bt_out) HIP_TRY(hipMalloc((void**)&w->bt_out, G * w->npad * 8));
+    if (!w->bt_pack) HIP_TRY(hipMalloc((void**)&w->bt_pack, G * w->npad * 8));
+    if (!w->bt_recv) HIP_TRY(hipMalloc((void**)&w->bt_recv, G * w->npad * 8));
+    if (!w->bt_pre) HIP_TRY(hipMalloc((void**)&w->bt_pre, 2 * nwords * 4));
+    if (!w->bt_boff) HIP_TRY(hipMalloc((void**)&w->bt_boff, 2 * (nwords / RW_BLOCK) * 4));
+    if (!w->bt_disp) HIP_TRY(hipMalloc((void**)&w->bt_disp, 2 * G * 8));
+    HIP_TRY(hipHostMalloc((void**)&w->h_btc, 2 * G * 8, hipHostMallocMapped | hipHostMallocCoherent));
+    HIP_TRY(hipHostGetDevicePointer((void**)&w->d_btc, w->h_btc, 0));
   }
   w->bt_active = true;
   *in = w->bt;
@@ -2826,6 +2972,7 @@ hipError_t ws_end_query_wait(Workspace* w) {
   }
   // reset for the next query; runs while the host reads the results
   HIP_TRY(hipMemsetAsync(w->q, 0, sizeof(QState), w->stream));
+  HIP_TRY(ws_clear_claims(w));
   prof_flush(w, w->h_q);
   return hipSuccess;
 }
@@ -3184,6 +3331,39 @@ size_t part_gst_words(int world) { return (size_t)GST_N + (size_t)world; }
 Comm* ws_get_comm(const Workspace* w) { return w ? w->comm : nullptr; }
 hipStream_t ws_stream(const Workspace* w) { return w->stream; }
 
+// The hop's roots: only those of the vertices whose bits this rank sends, packed per destination
+// in bit order, so a hop moves 8 bytes per sent vertex beside the bitmap instead of npad * 8 per
+// peer.  RCCL's send/recv counts are host values: the per-rank counts (popcounts of the send and
+// received bitmaps) come back through mapped memory with one host wait per hop — such queries
+// already agree on their inputs before the first hop, so their hops are host-paced anyway.
+static hipError_t ws_roots(Workspace* w, int step) {
+  const int G = w->comm->world;
+  const uint64_t nwords = (uint64_t)G * w->npad / 64, seg_words = w->npad / 64;
+  const uint64_t nb = nwords / RW_BLOCK, spb = seg_words / RW_BLOCK;
+  hipEvent_t p = prof_begin(w, K_ROOTS);
+  hipLaunchKernelGGL(k_rt_prefix, dim3((unsigned)(2 * nb)), dim3(BLOCK), 0, w->stream, w->sendbits, w->recvbits, nb,
+                     w->bt_pre, w->bt_boff);
+  hipLaunchKernelGGL(k_rt_offsets, dim3(1), dim3(BLOCK), 0, w->stream, w->bt_boff, spb, G, w->bt_disp, w->d_btc);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(ws_sync(w));
+  std::vector<uint64_t> sc(w->h_btc, w->h_btc + G), rc(w->h_btc + G, w->h_btc + 2 * G), sd(G), rd(G);
+  uint64_t ts = 0, tr = 0, moved = 0;
+  for (int q = 0; q < G; ++q) {
+    sd[q] = ts;
+    rd[q] = tr;
+    ts += sc[q];
+    tr += rc[q];
+    if (q != w->comm->rank) moved += sc[q] * 8;
+  }
+  hipLaunchKernelGGL(k_rt_pack, dim3((unsigned)cdiv(nwords, BLOCK)), dim3(BLOCK), 0, w->stream, w->sendbits, nwords,
+                     seg_words, w->bt_pre, w->bt_boff, w->bt_disp, w->bt_out, w->bt_pack);
+  HIP_TRY(hipGetLastError());
+  if (w->comm->alltoallv(w->bt_pack, sc.data(), sd.data(), w->bt_recv, rc.data(), rd.data(), 8, w->stream))
+    return hipErrorUnknown;
+  prof_end(w, p, K_ROOTS, step, 0, (double)moved);
+  return hipSuccess;
+}
+
 hipError_t ws_exchange(Workspace* w, int step, const ExpandArgs* next0) {
   if (!w->comm) return hipErrorInvalidValue;
   const uint64_t G = (uint64_t)w->comm->world;
@@ -3200,16 +3380,20 @@ hipError_t ws_exchange(Workspace* w, int step, const ExpandArgs* next0) {
   p = prof_begin(w, K_ALLTOALL);
   if (w->comm->alltoall(w->sendbits, w->recvbits, w->npad / 8, w->stream)) return hipErrorUnknown;
   prof_end(w, p, K_ALLTOALL, step, 0, (double)((G - 1) * w->npad / 8));
+  RootsIn rt{};
+  if (w->bt_active) {
+    HIP_TRY(ws_roots(w, step));
+    rt = RootsIn{w->bt_recv, w->bt_pre, w->bt_boff, w->bt_disp, nwords};
+  }
   // the send bitmap is all-zero between hops (the next hop's MARKs OR into it)
   HIP_TRY(hipMemsetAsync(w->sendbits, 0, G * w->npad / 8, w->stream));
-  if (w->bt_active && w->comm->alltoall(w->bt_out, w->bt_recv, w->npad * 8, w->stream)) return hipErrorUnknown;
   unsigned long long* acc = &w->q->acc[2 + w->pc];
   unsigned long long* other = &w->q->acc[2 + (w->pc ^ 1)];
   w->pc ^= 1;
   p = prof_begin(w, K_BITS_COMPACT);
   hipLaunchKernelGGL(k_bits_compact, dim3((unsigned)nb), dim3(BLOCK), 0, w->stream, w->recvbits, (int)G, seg_words,
                      w->nv, deg_src(next0), list_out(w, w->frontier[w->cur ^ 1], acc, other, nullptr, w->cur ^ 1),
-                     w->bt_active ? (const int64_t*)w->bt_recv : nullptr, w->bt, w->npad);
+                     rt, w->bt);
   prof_end(w, p, K_BITS_COMPACT, step, 0);
   w->cur ^= 1;
   w->list_acc = acc;

@@ -471,6 +471,10 @@ struct Comm {
   int wait(hipStream_t s);
   // recv[q * bytes ..] <- rank q's send[rank * bytes ..], for every q (stream-ordered)
   virtual int alltoall(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
+  // recv[rdisp[q] * elem ..] <- rank q's send[sdisp[rank] * elem ..], rcount[q] elements of elem
+  // bytes (rank q's scount[rank]); counts and displacements are host values on every rank
+  virtual int alltoallv(const void* send, const uint64_t* scount, const uint64_t* sdisp, void* recv,
+                        const uint64_t* rcount, const uint64_t* rdisp, size_t elem, hipStream_t s) = 0;
   // recv[q * bytes ..] <- rank q's send[0 .. bytes)
   virtual int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
   virtual int allreduce_sum_u64(unsigned long long* buf, size_t n, hipStream_t s) = 0;

@@ -129,6 +129,28 @@ def test_go_input_props_backtracker(steps):
         orc.close()
 
 
+def test_input_props_roots_travel_packed(rmat14):
+    """The `$-` roots of a hop travel only for the vertices whose bits the hop sends, packed in
+    bit order per destination rank: at most twice the bitmap's bytes for these frontiers (they
+    were npad * 8 bytes per peer, 64x the bitmap), and the rows equal the single engine's."""
+    src, dst, w, single, orc, c = rmat14
+    roots = graphs.roots(src, 6, seed=21)
+    inputs = (["id", "tag"], [[r, 7000 + i] for i, r in enumerate(roots)], "id")
+    yields = [E.input_prop("tag").encode(), E.edge_prop("e", "_dst").encode()]
+    c.each(lambda e: e.profile(True))
+    try:
+        got = c.go(roots, [1], 3, b"", yields, inputs=inputs)
+        profs = c.each(lambda e: e.profile_read())
+    finally:
+        c.each(lambda e: e.profile(False))
+    exp = single.go(roots, [1], 3, b"", yields, inputs=inputs)
+    assert graphs.sorted_rows(got) == graphs.sorted_rows(exp) and got
+    bits = sum(p["alltoall(xGMI)"]["algo_bytes"] for p in profs)
+    sent = sum(p["alltoallv(roots)"]["algo_bytes"] for p in profs)
+    assert all(p["alltoallv(roots)"]["launches"] == 2 for p in profs)   # one per hop
+    assert 0 < sent <= 2 * bits, (sent, bits)
+
+
 def test_go_async_slots_split_communicators(rmat14):
     """More queries in flight than slots on every rank: each slot's collectives run on its own
     communicator (7 peers each); the union of the ranks' rows equals the single engine's."""
