@@ -514,6 +514,7 @@ def main():
         dig.append(list(res.digest()) + [res.edges_scanned])
         res.free()
     stmt.free()
+    fixed = partitioned_costs(eng, roots[:4], barrier) if world > 1 else None
     sp = None
     replica = world > 1 and eng.path_replica_active
     if pairs and replica:
@@ -691,6 +692,7 @@ def main():
         "getbound": getbound,
         "c1_nba": c1,
         "partition_load": part_load,
+        "partitioned_fixed_costs": fixed,
         "gen_seconds": round(gen_s, 2),
         "load_seconds": round(load_s, 2),
     }
@@ -723,6 +725,44 @@ def c2_leg(args, barrier, inflight):
             "edges_per_step": g["scanned"] // args.steps, "query_latency_ms": {"p50": float(np.percentile(lat_ms, 50)),
                                                                              "p90": float(np.percentile(lat_ms, 90))},
             "roofline": roof, "kernels": kernels, "find_shortest_path": sp, "load_seconds": round(load_s, 2)}
+
+
+def partitioned_costs(eng, roots, barrier):
+    """A partitioned engine's per-query fixed costs beyond the plain GO (rank 0's view): YIELD
+    DISTINCT, whose rank-local statuses travel in band (no host agreement before its first
+    collective), and a `$-` query, whose roots travel beside each hop's bitmap packed by the
+    bitmap's popcount (kernels.hip ws_roots) — bytes per hop from the in-library profile."""
+    from nebula_amd import expr as E
+    where = E.binop("<", E.edge_prop("e", "w"), E.const(50)).encode()
+    a0 = eng.stats()["host_agreements"]
+    barrier()
+    lat = []
+    for r in roots:
+        q0 = time.perf_counter()
+        eng.go([r], [1], 3, where, [E.edge_prop("e", "w").encode()], distinct=True)
+        lat.append(time.perf_counter() - q0)
+    a1 = eng.stats()["host_agreements"]
+    inputs = (["id", "tag"], [[r, i] for i, r in enumerate(roots[:2])], "id")
+    eng.profile(True)
+    barrier()
+    q0 = time.perf_counter()
+    eng.go(roots[:2], [1], 3, where, [E.input_prop("tag").encode()], distinct=True, inputs=inputs)
+    t_in = time.perf_counter() - q0
+    prof = eng.profile_read()
+    eng.profile(False)
+    a2 = eng.stats()["host_agreements"]
+    bits = prof.get("alltoall(xGMI)", {})
+    rts = prof.get("alltoallv(roots)", {})
+    hops = max(1, rts.get("launches", 0))
+    return {"distinct": {"query": "GO 3 STEPS FROM <root> OVER e WHERE e.w < 50 YIELD DISTINCT e.w",
+                         "p50_ms": float(np.percentile(np.array(lat) * 1e3, 50)), "queries": len(lat),
+                         "host_agreements": a1 - a0},
+            "input_props": {"query": "GO 3 STEPS FROM $-.id (2 roots) OVER e WHERE e.w < 50 YIELD DISTINCT $-.tag",
+                            "ms": t_in * 1e3, "host_agreements": a2 - a1, "hops": rts.get("launches", 0),
+                            "bitmap_bytes_per_hop": bits.get("algo_bytes", 0) / hops,
+                            "root_bytes_per_hop": rts.get("algo_bytes", 0) / hops,
+                            # the round-3 exchange: npad * 8 bytes per peer = 64x the bitmap's npad / 8
+                            "root_bytes_per_hop_unpacked": 64 * bits.get("algo_bytes", 0) / hops}}
 
 
 def partition_load(csr, roots, args, worlds=(2, 4, 8)):

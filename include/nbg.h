@@ -143,6 +143,9 @@ typedef struct {
   int32_t num_edge_types;     /* signed edge types present                                     */
   int32_t reserved;
   uint64_t tiny_queries;      /* GO queries run as one single-workgroup launch (tiny path)       */
+  uint64_t host_agreements;   /* partitioned GO queries that agreed on rank-local statuses on the
+                                 host before their first collective ($- / $var inputs); the others
+                                 carry them in band                                              */
 } nbg_stats;
 int32_t nbg_get_stats(const nbg_engine* e, nbg_stats* out);
 

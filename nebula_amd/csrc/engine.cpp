@@ -1052,6 +1052,7 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
     }
   } else if (part) {
     int32_t agreed = NBG_OK;
+    ++E.host_agreements;
     if (qcomm->agree(stream, lrc, &agreed)) return E.fail(NBG_E_DEVICE, "query agreement: " + qcomm->last);
     if (agreed) {
       if (lrc) return E.fail(lrc, lmsg);
@@ -1739,6 +1740,7 @@ int32_t nbg_get_stats(const nbg_engine* h, nbg_stats* out) {
   out->device_bytes = E.snap.device_bytes;
   out->num_edge_types = (int32_t)E.snap.types.size();
   out->tiny_queries = E.tiny_queries;
+  out->host_agreements = E.host_agreements;
   return NBG_OK;
 }
 

@@ -90,6 +90,7 @@ struct Engine {
   std::mutex err_mu;
 
   uint64_t tiny_queries = 0;    // GO queries run by ws_go_tiny (nbg_stats)
+  uint64_t host_agreements = 0; // partitioned GO queries that agreed on the host first (nbg_stats)
   // nbg_inject_fault (tests): the next fault_count queries fail at fault_site
   int fault_site = 0, fault_count = 0;
   bool fault(int site) {

@@ -255,7 +255,8 @@ class Engine:
         s = L.nbg_stats()
         self._check(self.lib.nbg_get_stats(self.h, C.byref(s)), "stats")
         return {"num_vertices": s.num_vertices, "num_edges": s.num_edges, "device_bytes": s.device_bytes,
-                "num_edge_types": s.num_edge_types, "tiny_queries": s.tiny_queries}
+                "num_edge_types": s.num_edge_types, "tiny_queries": s.tiny_queries,
+                "host_agreements": s.host_agreements}
 
     # ------------------------------------------------------------------ profiling
     def set_path_replica(self, mode: int):

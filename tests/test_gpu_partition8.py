@@ -96,6 +96,7 @@ def test_go_multi_start_duplicates_and_unknown(rmat14):
 def test_go_distinct(rmat14, steps):
     src, dst, w, single, orc, c = rmat14
     wb = WHERE.encode()
+    agreed = [e.stats()["host_agreements"] for e in c.engines]
     for yields in ([E.edge_prop("e", "_dst")],
                    [E.edge_prop("e", "w"), E.binop("%", E.edge_prop("e", "_dst"), E.const(7))]):
         yb = [y.encode() for y in yields]
@@ -103,6 +104,8 @@ def test_go_distinct(rmat14, steps):
             got = graphs.sorted_rows(c.go([r], [1], steps, wb, yb, distinct=True))
             assert got == graphs.sorted_rows(single.go([r], [1], steps, wb, yb, distinct=True)), (steps, r)
             assert len(set(got)) == len(got)
+    # statuses in band: no host agreement before a DISTINCT query's first collective
+    assert [e.stats()["host_agreements"] for e in c.engines] == agreed
 
 
 @pytest.mark.parametrize("steps", [1, 2, 3])
@@ -137,6 +140,7 @@ def test_input_props_roots_travel_packed(rmat14):
     roots = graphs.roots(src, 6, seed=21)
     inputs = (["id", "tag"], [[r, 7000 + i] for i, r in enumerate(roots)], "id")
     yields = [E.input_prop("tag").encode(), E.edge_prop("e", "_dst").encode()]
+    agreed = [e.stats()["host_agreements"] for e in c.engines]
     c.each(lambda e: e.profile(True))
     try:
         got = c.go(roots, [1], 3, b"", yields, inputs=inputs)
@@ -149,6 +153,7 @@ def test_input_props_roots_travel_packed(rmat14):
     sent = sum(p["alltoallv(roots)"]["algo_bytes"] for p in profs)
     assert all(p["alltoallv(roots)"]["launches"] == 2 for p in profs)   # one per hop
     assert 0 < sent <= 2 * bits, (sent, bits)
+    assert [e.stats()["host_agreements"] for e in c.engines] == [a + 1 for a in agreed]   # ($- inputs agree)
 
 
 def test_go_async_slots_split_communicators(rmat14):
