@@ -250,7 +250,9 @@ int32_t nbg_rows_segment(const nbg_rows* r, int64_t i, uint64_t* begin, uint64_t
  * results): per row h = splitmix64(... splitmix64(0 ^ cell_0) ... ^ cell_{k-1}) over its 8-byte
  * cell payloads in column order; out[0] = rows, out[1] = XOR of h, out[2] = sum of h (mod 2^64).
  * Verifies results at sizes too large to fetch.  String cells hash their payload: the snapshot's
- * dictionary code for device rows, the result's string index (nbg_rows_string) for host rows. */
+ * dictionary code for device rows (a string the query built — a concatenation, a cast to string —
+ * is 1 << 62 | a 62-bit hash of its bytes, so equal strings hash alike), the result's string
+ * index (nbg_rows_string) for host rows. */
 int32_t nbg_rows_digest(const nbg_rows* r, uint64_t* out);
 void nbg_rows_free(nbg_rows* r);
 

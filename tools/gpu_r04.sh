@@ -58,11 +58,12 @@ for step in "$@"; do
     spprof26)   # kernel trace of the one-pair SP queries (default path)
       timeout -k 10 600 rocprofv3 --kernel-trace -d "$OUT/spprof26" -o run --output-format csv -- \
         python3 -u tools/sp_probe.py 26 400 > "$OUT/spprof26.txt" 2>&1 || { tail -30 "$OUT/spprof26.txt"; exit 1; } ;;
-    wgs26)   # persistent SP: workgroup-count sweep
-      for w in 1 8 32 64 128; do
-        NBG_SP_PERSISTENT=1 NBG_SP_WGS=$w NBG_SP_TRACE=1 timeout -k 10 300 python -u tools/sp_probe.py 26 1500 > "$OUT/wgs26_$w.txt" 2>&1 \
-          || { tail -30 "$OUT/wgs26_$w.txt"; exit 1; }
-      done ;;
+    goab)   # GO A/B: claim bitmaps (libnbg.so) vs 4-byte claim stamps (libnbg_stamps.so)
+      timeout -k 10 1000 bash tools/go_ab.sh "$TAG/goab" nebula_amd/libnbg.so nebula_amd/libnbg_stamps.so \
+        > "$OUT/goab.txt" 2>&1 || { tail -30 "$OUT/goab.txt"; exit 1; } ;;
+    spab)   # SHORTEST A/B: atomicMax level claims (libnbg.so) vs load + CAS (libnbg_cas.so)
+      timeout -k 10 1000 bash tools/sp_ab.sh "$TAG/spab" nebula_amd/libnbg.so nebula_amd/libnbg_cas.so \
+        > "$OUT/spab.txt" 2>&1 || { tail -30 "$OUT/spab.txt"; exit 1; } ;;
     p8)   # the 8-way partition, in-process ranks on one GPU
       timeout -k 10 900 python -u -m pytest tests/test_gpu_partition8.py -x -v --timeout 300 --timeout-method thread \
         > "$OUT/pytest_partition8.log" 2>&1 || { tail -40 "$OUT/pytest_partition8.log"; exit 1; } ;;
