@@ -161,3 +161,40 @@ def test_replica_nba_findpath_golden(nba_data):
             assert ok, msg
     finally:
         c.close()
+
+
+def test_replica_many_edge_types():
+    """40 edge types (80 signed types) on 2 ranks: the replica's type union is gathered at its
+    real size, so FIND PATH over the highest types runs on the replica with every edge (ADVICE
+    r03: the union used to stop at 64 signed types per rank, silently dropping the rest)."""
+    import numpy as np
+    from nebula_amd import Engine
+    rng = np.random.default_rng(3)
+    vids = rng.integers(-(1 << 62), 1 << 62, 400)
+    types = list(range(10, 50))
+    data = {t: (vids[rng.integers(0, 400, 700)], vids[rng.integers(0, 400, 700)], rng.integers(0, 100, 700))
+            for t in types}
+    c, single = LocalCluster(100, 2), Engine(100)
+    try:
+        for be in (c, single):
+            for t in types:
+                be.register_edge(t, f"e{t}", graphs.E_SCHEMA)
+            for t in types:
+                s, d, w = data[t]
+                be.load_edges(t, s, d, [w])
+            be.finalize()
+        assert c.path_replica_active
+        found = 0
+        for k in range(24):
+            s, t = int(vids[rng.integers(0, 400)]), int(vids[rng.integers(0, 400)])
+            for over in ([49], [47, 12], [33, 44, 48]):
+                got = c.find_path([s], [t], over, 4)
+                assert got == single.find_path([s], [t], over, 4), (s, t, over)
+                found += len(got)
+            if k < 6:
+                assert c.find_path([s], [t], [49, 11], 3, shortest=False) == \
+                    single.find_path([s], [t], [49, 11], 3, shortest=False)
+        assert found > 0
+    finally:
+        c.close()
+        single.close()
