@@ -134,6 +134,7 @@ hipError_t sp_wait(SpCtx* c, SpResult* out) {
     }
     if (e != hipSuccess) return e;
   }
+  if (e != hipSuccess) return e;
   chain_result(c->chain, out);
   chain_profile_done(c->chain, *out);
   return hipSuccess;

@@ -3,15 +3,16 @@
 // Same semantics and result as path.cpp's bidirectional() (FindPathExecutor.cpp:173-290
 // restated: minimal hop count, UPTO N, one path per target, ties broken by the lexicographically
 // smallest entry list [v0, t0, r0, v1, ...]).  The host enqueues a chain per pair —
-//   K x k_ch_step (the first starts the search), H x k_ch_hop (the last stores the result into
-//   mapped host memory; k_ch_out when a continuation has no hop launch) —
+//   K x k_ch_step (the first starts the search; the last stores the result into mapped host
+//   memory), plus k_ch_hop launches only when a continuation needs them —
 // and waits once.  Step launch i derives what it does from the state snapshot of launch i - 1
 // (snap[i - 1]) and that launch's results (its output-list and meet counters, lacc / lmeet[i - 1]),
 // which are final at the launch boundary: the BFS level loop (direction = the side with the
-// smaller edge total, meet / empty / UPTO tests), then the B-set steps, then nothing (a launch
-// past the end returns at once).  Workgroup 0 stores the derived snapshot for launch i + 1, so no
-// launch waits for the host or for a last-workgroup ticket.  K and H follow the recent queries
-// (steps and path lengths seen); a query that needs more gets a continuation batch.
+// smaller edge total, meet / empty / UPTO tests), then the B-set steps, and once the search is
+// over the greedy path walk (a launch finding nothing left returns at once).  Workgroup 0 stores
+// the derived snapshot for launch i + 1, so no launch waits for the host or for a last-workgroup
+// ticket.  K follows the recent queries (launches used); a query that needs more gets a
+// continuation batch.
 //
 // Frontier lists carry their edge space (the packed-atomic protocol of kernels.hip's lists):
 // entry i = vertex ids[i], its edges at positions [seg_end[i] - deg, seg_end[i]) of the list's
@@ -100,8 +101,9 @@ struct ChState {        // device; the host reads what the result launch derives
   unsigned long long gticket;          // greedy hop: workgroups done (the last one reduces, resets)
   // greedy launch h starts from hstart[h] = (position << 32 | current vertex) and exactly one of
   // its workgroups writes hstart[h + 1]: state that no launch mutates while its own workgroups
-  // may still read it (workgroups of one launch start at different times)
-  unsigned long long hstart[CH_MAXS + 1];
+  // may still read it (workgroups of one launch start at different times).  Greedy launches are
+  // the step launches that find the search over (hop_first) and then the k_ch_hop launches.
+  unsigned long long hstart[2 * CH_MAXS + 2];
   // step launch i starts at step first[i] (a BFS level or B-set step; first[0] = 0) and writes
   // first[i + 1]: one step, several (a workgroup alone runs small steps back to back, ChQ::solo)
   // or none (the search is over)
@@ -111,15 +113,16 @@ struct ChState {        // device; the host reads what the result launch derives
   unsigned long long gpart[4 * CH_HOP_WGS];
 };
 
-// What the host reads after a chain, stored by k_ch_out straight into mapped pinned memory (a
-// hipMemcpyAsync of the 17 KB ChState went down the copy engine's path: ~130 us per pair on
-// MI355X against ~3 us for a kernel's stores, profiles/r03_l_d2h_probe.json).
+// What the host reads after a chain, stored by its last launch (ch_out) straight into mapped
+// pinned memory (a hipMemcpyAsync of the 17 KB ChState went down the copy engine's path: ~130 us
+// per pair on MI355X against ~3 us for a kernel's stores, profiles/r03_l_d2h_probe.json).
 struct ChOut {
   ChSnap F;                            // the state after the last step launch
   unsigned long long err;              // ChState::err
   unsigned long long hpos;             // hstart[hops] (position << 32 | vertex)
   unsigned long long hlaunch;
   unsigned long long busy;             // ChState::busy
+  unsigned long long tag;              // ChQ::tag of the batch whose launch stored this
   long long path[1 + 3 * MAX_PATH_LEN];
 };
 
@@ -144,6 +147,7 @@ struct ChQ {
   uint32_t solo;                       // a step over at most this many items (entries + edges) is run
                                        // by workgroup 0 alone, which goes on with the next step (0: off)
   uint32_t par;                        // the query's counter set (ChState::c)
+  uint32_t tag;                        // this batch of launches (ChOut::tag: which batch stored)
 };
 
 // The state after step launch `i` (snapshot p before it, its results from st): every step launch
@@ -690,8 +694,9 @@ __device__ __forceinline__ uint64_t step_items(const ChSnap& P) {
 // Step launch i: from step first[i], one step over the whole grid, or — for a step of at most
 // q.solo items — steps run by workgroup 0 alone, back to back, until the search is over or a step
 // needs the grid (the launch boundary then orders it after this workgroup's writes).
+// Returns false when the search was over before this launch (the launch is then a greedy one).
 template <int NW>
-__device__ __forceinline__ void ch_step(const ChArgs& A, const ChQ& q, int i, uint32_t bid, uint32_t nblk) {
+__device__ __forceinline__ bool ch_step(const ChArgs& A, const ChQ& q, int i, uint32_t bid, uint32_t nblk) {
   ChState* st = A.st;
   ChCtr& C = st->c[q.par];
   uint32_t j = i == 0 ? 0u : (uint32_t)st->first[i];
@@ -707,10 +712,10 @@ __device__ __forceinline__ void ch_step(const ChArgs& A, const ChQ& q, int i, ui
   }
   if (P.phase == PH_DONE) {
     if (lead) st->first[i + 1] = j;
-    return;
+    return false;
   }
   const bool solo = step_items(P) <= q.solo;
-  if (solo && bid != 0) return;
+  if (solo && bid != 0) return true;
   if (lead) C.busy += 1;
   for (;;) {   // (one call site of ch_level: the grid's step and the solo steps share its registers)
     if (lead) {
@@ -718,7 +723,7 @@ __device__ __forceinline__ void ch_step(const ChArgs& A, const ChQ& q, int i, ui
       if (!solo) st->first[i + 1] = j + 1;
     }
     ch_level<NW>(A, q, P, (int)j, solo ? 0u : bid, solo ? 1u : nblk, j == 0 ? &f0 : nullptr);
-    if (!solo) return;
+    if (!solo) return true;
     // this workgroup's stores and atomics before the next step's reads (labels, lists, counters;
     // the acquire drops L1 lines read before another wave's claims); the snapshot is read back
     // rather than kept in registers across the step
@@ -731,6 +736,7 @@ __device__ __forceinline__ void ch_step(const ChArgs& A, const ChQ& q, int i, ui
     if (P.phase == PH_DONE || step_items(P) > q.solo || j + 1 >= (uint32_t)CH_MAXS) break;
   }
   if (lead) st->first[i + 1] = j;
+  return true;
 }
 
 namespace {
@@ -898,10 +904,18 @@ __device__ __forceinline__ bool ch_hop(const ChArgs& A, const ChQ& q, int nl, in
   return true;
 }
 
+// The first greedy launch of the query: the first step launch that finds the search over (busy =
+// the step launches that ran a step), never launch 0 (it stores the greedy's start).
+__device__ __forceinline__ int hop_first(const ChCtr& C) {
+  const int b = (int)C.busy;
+  return b > 1 ? b : 1;
+}
+
 // ---------------------------------------------------------------------------- kernels
-// The chain's result (after `steps` step and `hops` hop launches) into the host's ChOut (one
-// workgroup; vector stores over the mapped pinned page), and the next query's counter set zeroed.
-__device__ __forceinline__ void ch_out(const ChArgs& A, const ChQ& q, int steps, int hops, ChOut* out) {
+// The chain's result (the state after `steps` step launches; the greedy's position hstart[hend])
+// into the host's ChOut (one workgroup; vector stores over the mapped pinned page), and the next
+// query's counter set zeroed.
+__device__ __forceinline__ void ch_out(const ChArgs& A, const ChQ& q, int steps, int hend, ChOut* out) {
   ChState* st = A.st;
   __syncthreads();   // (the writing workgroup's own stores: the path, hstart)
   const ChSnap F = snap_for(st, q, (int)st->first[steps]);
@@ -911,7 +925,8 @@ __device__ __forceinline__ void ch_out(const ChArgs& A, const ChQ& q, int steps,
   if (threadIdx.x == 0) {
     out->F = F;
     out->err = C.err | st->gerr;
-    out->hpos = st->hstart[hops];
+    out->hpos = st->hstart[hend];
+    out->tag = q.tag;
     out->hlaunch = C.hlaunch;
     out->busy = C.busy;
   }
@@ -924,18 +939,26 @@ __device__ __forceinline__ void ch_out(const ChArgs& A, const ChQ& q, int steps,
 // (at most 2 waves per SIMD: 256 VGPRs, no spills; a one-pair launch has 128 workgroups of 4 waves,
 // 2 waves per CU, so the occupancy bound costs nothing.  16-wave workgroups, tried for more waves
 // per big level, were slower: RMAT-26 p50 0.137 -> 0.197 ms, profiles/r03_n_sp_block_ab.txt)
-__global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) k_ch_step(const ChArgs* __restrict__ Ap, ChQ q, int i) {
-  ch_step<CH_WAVES>(*Ap, q, i, blockIdx.x, gridDim.x);
+// Step launch i: a search step, or — the search over — greedy launch i - hop_first (its first
+// CH_HOP_WGS workgroups), so the walk runs in the launches that used to return at once.  (out:
+// the batch's last launch stores the result, when the search was over before it.)
+template <int NW>
+__device__ __forceinline__ void ch_any(const ChArgs& A, const ChQ& q, int i, uint32_t bid, uint32_t nblk, ChOut* out) {
+  if (ch_step<NW>(A, q, i, bid, nblk) || i == 0 || bid >= (uint32_t)CH_HOP_WGS) return;
+  const int h = i - hop_first(A.st->c[q.par]);
+  if (ch_hop(A, q, i, h, bid, nblk < (uint32_t)CH_HOP_WGS ? nblk : (uint32_t)CH_HOP_WGS) && out)
+    ch_out(A, q, i, h + 1, out);
 }
 
-// (out: the batch's last hop launch stores the result: the steps launched so far, hops h + 1)
-__global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ Ap, ChQ q, int nl, int h, ChOut* out) {
+__global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) k_ch_step(const ChArgs* __restrict__ Ap, ChQ q, int i, ChOut* out) {
+  ch_any<CH_WAVES>(*Ap, q, i, blockIdx.x, gridDim.x, out);
+}
+
+// Greedy launches of a continuation (a hub's hop ended the walk's launch): launch j after the nl
+// step launches is greedy launch nl - hop_first + j; the batch's last stores the result.
+__global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ Ap, ChQ q, int nl, int j, ChOut* out) {
+  const int h = nl - hop_first(Ap->st->c[q.par]) + j;
   if (ch_hop(*Ap, q, nl, h, blockIdx.x, gridDim.x) && out) ch_out(*Ap, q, nl, h + 1, out);
-}
-
-// (a batch without a hop launch: the result alone)
-__global__ void __launch_bounds__(64) k_ch_out(const ChArgs* __restrict__ Ap, ChQ q, int steps, int hops, ChOut* out) {
-  ch_out(*Ap, q, steps, hops, out);
 }
 
 // ... or up to CH_BMAX queries per launch (a batch of pairs, each with its own workspace, state and
@@ -950,14 +973,9 @@ struct ChBatch {
   uint32_t per;
 };
 // (2 waves/SIMD: no spills; batched 33.3-33.9k -> 34.7-35.0k pairs/s, profiles/r03_y_sp_spec_ab.txt)
-__global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) k_ch_step_b(ChBatch b, int i) {
+__global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) k_ch_step_b(ChBatch b, int i, int last) {
   const uint32_t p = blockIdx.x / b.per;
-  if ((int)p < b.n) ch_step<CH_WAVES>(*b.A[p], b.q[p], i, blockIdx.x % b.per, b.per);
-}
-__global__ void __launch_bounds__(CH_BLOCK) k_ch_hop_b(ChBatch b, int nl, int h, int last) {
-  const uint32_t p = blockIdx.x / CH_HOP_WGS;
-  if ((int)p < b.n && ch_hop(*b.A[p], b.q[p], nl, h, blockIdx.x % CH_HOP_WGS, CH_HOP_WGS) && last)
-    ch_out(*b.A[p], b.q[p], nl, h + 1, b.out[p]);
+  if ((int)p < b.n) ch_any<CH_WAVES>(*b.A[p], b.q[p], i, blockIdx.x % b.per, b.per, last ? b.out[p] : nullptr);
 }
 
 // ---------------------------------------------------------------------------- host side
@@ -966,7 +984,7 @@ struct ChainCtx {
   uint64_t nv = 0, list_cap = 0, tsplit_cap = 0;
   ChList list[CH_NLISTS] = {};
   ChState* d_st = nullptr;
-  ChOut* h_out = nullptr;          // mapped pinned: k_ch_out stores the result here
+  ChOut* h_out = nullptr;          // mapped pinned: the chain's last launch stores the result here
   ChOut* d_out = nullptr;          // its device address
   ChArgs* d_args = nullptr;
   ChArgs* h_args = nullptr;
@@ -985,8 +1003,9 @@ struct ChainCtx {
   int steps = 0, hops = 0;
   uint32_t par = 0;                // the query's counter set (ChQ::par)
   bool clean = true;               // the next query's counter set is zero
-  // recent queries: step launches and path lengths used (sizes the next chain)
-  double ema_steps = 6, ema_hops = 2;
+  // recent queries: launches used (search steps + greedy launches; sizes the next chain)
+  double ema_launches = 6;
+  uint32_t tag_seq = 0;            // ChQ::tag of the next batch
   unsigned long long batches = 0, queries = 0;
   // nbg_profile: HIP events around the chain's launches (mode 1 every launch, 2 step launches only)
   int prof = 0;
@@ -1059,8 +1078,8 @@ ChainCtx* chain_create(uint64_t nv, uint64_t edge_cap, hipStream_t s, std::strin
 void chain_destroy(ChainCtx* c) {
   if (!c) return;
   if (getenv("NBG_SP_TRACE") && c->queries)
-    fprintf(stderr, "[sp trace] level loop: %llu queries, %.3f batches each, chain sized for %.2f steps, %.2f hops\n",
-            c->queries, (double)c->batches / c->queries, c->ema_steps, c->ema_hops);
+    fprintf(stderr, "[sp trace] level loop: %llu queries, %.3f batches each, chain sized for %.2f launches\n",
+            c->queries, (double)c->batches / c->queries, c->ema_launches);
   for (auto& L : c->list)
     for (uint32_t* p : {L.ids, L.seg_end, L.seg_rs, L.tsplit})
       if (p) (void)hipFree(p);
@@ -1073,21 +1092,23 @@ void chain_destroy(ChainCtx* c) {
   delete c;
 }
 
-// Enqueue step launches [steps, steps + k) and h hop launches; the last hop launch stores the
-// result (k_ch_out only when the batch has no hop launch).
+// Enqueue step launches [steps, steps + k) then h greedy launches; the batch's last launch stores
+// the result (a step launch only when the search was over before it: else the stored tag stays
+// the previous batch's and chain_more continues).
 static hipError_t chain_batch(ChainCtx* c, int k, int h) {
   const ChArgs* A = c->d_args;
+  c->q.tag = ++c->tag_seq;
+  h = std::min(h, CH_MAXS - c->hops);
   for (int j = 0; j < k; ++j, ++c->steps)
     c->timed(CHK_STEP, [&] {
-      hipLaunchKernelGGL(k_ch_step, dim3(c->grid), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps);
+      hipLaunchKernelGGL(k_ch_step, dim3(c->grid), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps,
+                         h <= 0 && j + 1 == k ? c->d_out : (ChOut*)nullptr);
     });
-  h = std::min(h, CH_MAXS - c->hops);
   for (int j = 0; j < h; ++j, ++c->hops)
     c->timed(CHK_HOP, [&] {
       hipLaunchKernelGGL(k_ch_hop, dim3(CH_HOP_WGS), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps, c->hops,
                          j + 1 == h ? c->d_out : (ChOut*)nullptr);
     });
-  if (h <= 0) hipLaunchKernelGGL(k_ch_out, dim3(1), dim3(64), 0, c->stream, A, c->q, c->steps, c->hops, c->d_out);
   ++c->batches;
   return hipGetLastError();
 }
@@ -1124,7 +1145,7 @@ static hipError_t chain_prepare(ChainCtx* c, const SpTypes& fwd, const SpTypes& 
     c->args_valid = true;
   }
   c->par ^= 1u;
-  c->q = ChQ{s, t, upto, epoch, epoch, epoch, c->solo, c->par};
+  c->q = ChQ{s, t, upto, epoch, epoch, epoch, c->solo, c->par, 0};
   c->steps = c->hops = 0;
   c->last_batched = false;
   ++c->queries;
@@ -1134,25 +1155,22 @@ static hipError_t chain_prepare(ChainCtx* c, const SpTypes& fwd, const SpTypes& 
   return hipSuccess;
 }
 
-// chain length for c's query: sized by the recent queries; a longer one gets a continuation
-// batch (chain_more)
-static void chain_length(const ChainCtx* c, int* k, int* h) {
-  // NBG_SP_KPAD / NBG_SP_HPAD: launches added to the sized chain (A/B switches; an empty launch
-  // costs a few us, a continuation a host round trip)
+// Step launches a query can use: its search steps (at most 2 UPTO - 1) and one launch past them,
+// in which the greedy walk (or, with no path, the result) runs.
+static int chain_max(const ChainCtx* c) { return 2 * (int)c->q.upto; }
+
+// chain length for c's query: sized by the recent queries (NBG_SP_KPAD launches added: an empty
+// launch costs a few us, a continuation a host round trip); a longer query continues (chain_more)
+static int chain_length(const ChainCtx* c) {
   static const int kpad = getenv("NBG_SP_KPAD") ? atoi(getenv("NBG_SP_KPAD")) : 0;
-  static const int hpad = getenv("NBG_SP_HPAD") ? atoi(getenv("NBG_SP_HPAD")) : 0;
-  const int max_steps = 2 * (int)c->q.upto - 1;
-  *k = std::min(max_steps, std::max(1, (int)std::ceil(c->ema_steps) + kpad));
-  *h = std::min((int)c->q.upto, std::max(1, (int)std::ceil(c->ema_hops) + hpad));
+  return std::min(chain_max(c), std::max(2, (int)std::ceil(c->ema_launches) + kpad));
 }
 
 hipError_t chain_launch(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible,
                         const int64_t* vids, uint32_t* const lab[3], uint32_t epoch, uint32_t s, uint32_t t,
                         uint32_t upto) {
   HIP_TRY_CH(chain_prepare(c, fwd, bwd, visible, vids, lab, epoch, s, t, upto));
-  int k, h;
-  chain_length(c, &k, &h);
-  return chain_batch(c, k, h);
+  return chain_batch(c, chain_length(c), 0);
 }
 
 // n <= CH_BMAX queries (contexts on one stream) in one chain of batched launches; each context
@@ -1166,38 +1184,35 @@ hipError_t chain_launch_batch(ChainCtx* const* cs, int n, const ChainQuery* qs) 
   // (2048 workgroups for a full batch: 64 per pair at 32 pairs, 39.4-40.5 k pairs/s against
   // 34.3-34.7 k at 32 per pair with 2-item tiles, profiles/r03_fin2_sp_vt2_batch_ab.txt)
   b.per = per_env ? per_env : std::max(64u, 2048u / (unsigned)n);
-  int k = 1, h = 1;
+  int k = 1;
   for (int p = 0; p < n; ++p) {
     ChainCtx* c = cs[p];
     if (c->stream != cs[0]->stream) return hipErrorInvalidValue;
     const ChainQuery& x = qs[p];
     HIP_TRY_CH(chain_prepare(c, *x.fwd, *x.bwd, x.visible, x.vids, x.lab, x.epoch, x.s, x.t, x.upto));
+    c->q.tag = ++c->tag_seq;
     b.A[p] = c->d_args;
     b.q[p] = c->q;
     b.out[p] = c->d_out;
-    // the whole chain at once (every step and hop launch UPTO allows): a continuation would cost
-    // the batch a host round trip per context, while a launch past a query's end returns at once
-    k = std::max(k, 2 * (int)x.upto - 1);
-    h = std::max(h, (int)x.upto);
+    // the whole chain at once (every search step UPTO allows and one launch past them, which
+    // walks the greedy path): a continuation would cost the batch a host round trip per context,
+    // while a launch past a query's end returns at once
+    k = std::max(k, chain_max(c));
   }
   const hipStream_t st = cs[0]->stream;
   ChainCtx* c0 = cs[0];   // (the batch's launch events are kept by its first context)
   for (int j = 0; j < k; ++j)
     c0->timed(CHK_STEP_B, [&] {
-      hipLaunchKernelGGL(k_ch_step_b, dim3((unsigned)n * b.per), dim3(CH_BLOCK), 0, st, b, j);
-    });
-  for (int j = 0; j < h; ++j)
-    c0->timed(CHK_HOP_B, [&] {
-      hipLaunchKernelGGL(k_ch_hop_b, dim3((unsigned)n * CH_HOP_WGS), dim3(CH_BLOCK), 0, st, b, k, j, j + 1 == h);
+      hipLaunchKernelGGL(k_ch_step_b, dim3((unsigned)n * b.per), dim3(CH_BLOCK), 0, st, b, j, j + 1 == k);
     });
   HIP_TRY_CH(hipGetLastError());
   for (int p = 0; p < n; ++p) {
     ChainCtx* c = cs[p];
     c->last_batched = true;
     // a query needing fewer launches than the batch's longest ran past its end: its launches
-    // returned at once (k_ch_step: phase DONE; k_ch_hop: nothing left to walk), as in chain_batch
+    // returned at once (the search over, nothing left to walk), as in chain_batch
     c->steps = k;
-    c->hops = h;
+    c->hops = 0;
     ++c->batches;
   }
   return hipSuccess;
@@ -1209,9 +1224,14 @@ bool chain_more(ChainCtx* c, hipError_t* he) {
   *he = hipSuccess;
   const ChOut& h = *c->h_out;
   const ChSnap F = h.F;
-  const int max_steps = 2 * (int)c->q.upto - 1;
-  if (F.phase != PH_DONE && c->steps < max_steps) {
-    *he = chain_batch(c, max_steps - c->steps, (int)c->q.upto);   // the rest, at once
+  if (h.tag != c->q.tag || F.phase != PH_DONE) {
+    // the batch ended inside the search (its last launch stored nothing): the rest, at once; the
+    // last of them is past every search step, so it stores
+    if (c->steps >= chain_max(c)) {   // (cannot happen: a search has at most 2 UPTO - 1 steps)
+      *he = hipErrorUnknown;
+      return true;
+    }
+    *he = chain_batch(c, chain_max(c) - c->steps, 0);
     return false;
   }
   const uint32_t hpos = (uint32_t)(h.hpos >> 32);
@@ -1220,10 +1240,9 @@ bool chain_more(ChainCtx* c, hipError_t* he) {
     return false;
   }
   c->clean = true;   // (its result launch zeroed the next query's counters)
-  // step launches that ran a step; decay toward this query's needs
-  const double used = (double)h.busy;
-  c->ema_steps = 0.9 * c->ema_steps + 0.1 * (used + 0.5);
-  if (F.met) c->ema_hops = 0.9 * c->ema_hops + 0.1 * ((double)h.hlaunch + 0.3);
+  // launches used (search steps, then the greedy's, at least one); decay toward this query's needs
+  const double used = (double)h.busy + (double)std::max(1ull, h.hlaunch);
+  c->ema_launches = 0.9 * c->ema_launches + 0.1 * (used + 0.3);
   return true;
 }
 
@@ -1235,7 +1254,7 @@ void chain_result(const ChainCtx* c, SpResult* out) {
   out->edges = F.edges;
   out->levels = F.levels;
   out->abytes = F.abytes;
-  out->launches = (unsigned long long)(c->steps + c->hops + (c->hops ? 0 : 1));
+  out->launches = (unsigned long long)(c->steps + c->hops);
   const uint32_t hpos = (uint32_t)(h.hpos >> 32);
   out->L = (F.met && !h.err && hpos == F.L) ? F.L : 0;
   if (F.met && !h.err && hpos != F.L) out->err = 2;   // (cannot happen: the hops were enqueued)
