@@ -65,25 +65,38 @@ struct RowBytes {
   void put_double(int64_t bits) { cord.append(reinterpret_cast<const char*>(&bits), 8); done(); }
   void put_bool(int64_t v) { cord.push_back(v ? 1 : 0); done(); }
   void put_string(const std::string& s) { varint(s.size()); cord += s; done(); }
-  std::string encode() const {
+  void clear() {   // (keeps the buffers: one RowBytes serves every row of a response)
+    cord.clear();
+    blocks.clear();
+    cols = 0;
+  }
+  int offset_bytes() const {
     int off = 0;
     uint64_t n = cord.size();
     do { ++off; n >>= 8; } while (n);
+    return off;
+  }
+  std::string encode() const {
+    const int off = offset_bytes();
     std::string out(1, (char)(off - 1));
     for (uint64_t b : blocks) out.append(reinterpret_cast<const char*>(&b), off);
     return out + cord;
   }
-};
-
-void rowset_add(std::string& rs, const std::string& row) {   // RowSetWriter::addRow
-  uint64_t v = row.size();
-  while (v >= 0x80) {
-    rs.push_back((char)(v | 0x80));
-    v >>= 7;
+  // RowSetWriter::addRow(encode()) (RowSetWriter.cpp:21-43) without the temporaries: varint
+  // length, then the row
+  void append_to(std::string& rs) const {
+    const int off = offset_bytes();
+    uint64_t v = 1 + blocks.size() * (uint64_t)off + cord.size();
+    while (v >= 0x80) {
+      rs.push_back((char)(v | 0x80));
+      v >>= 7;
+    }
+    rs.push_back((char)v);
+    rs.push_back((char)(off - 1));
+    for (uint64_t b : blocks) rs.append(reinterpret_cast<const char*>(&b), off);
+    rs += cord;
   }
-  rs.push_back((char)v);
-  rs += row;
-}
+};
 
 struct PropCtx {
   std::string name;
@@ -161,10 +174,32 @@ bool part_served(const Engine& E, int32_t part) {
 
 }  // namespace
 
+// NBG_GN_TRACE=1: mean time per phase (contexts + compile, device walk + fetch, response bytes),
+// printed every 500 requests
+struct GnTrace {
+  bool on = getenv("NBG_GN_TRACE") != nullptr;
+  uint64_t n = 0;
+  double ms[3] = {};
+  std::chrono::steady_clock::time_point t;
+  void mark(int phase) {
+    const auto now = std::chrono::steady_clock::now();
+    if (phase >= 0) ms[phase] += std::chrono::duration<double, std::milli>(now - t).count();
+    t = now;
+  }
+  void done() {
+    if (++n % 500) return;
+    fprintf(stderr, "[gn trace] %llu requests: contexts %.4f ms, device %.4f ms, response %.4f ms\n",
+            (unsigned long long)n, ms[0] / n, ms[1] / n, ms[2] / n);
+  }
+};
+static GnTrace g_gn_trace;
+
 // stats != nullptr: boundStats — accumulate per returned column (stat_types[i] per request column)
 static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_response* resp,
                              const int32_t* stat_types = nullptr, StatsSink* stats = nullptr) {
   int ret_index = 0;
+  GnTrace& tr_ = g_gn_trace;
+  if (tr_.on) tr_.mark(-1);
   // QueryBaseProcessor::validOperation (QueryBaseProcessor.inl:18-35)
   auto valid_op = [](int32_t type, int32_t stat) {
     if (stat != NBG_STAT_SUM && stat != NBG_STAT_AVG) return true;
@@ -384,6 +419,7 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
     if (starts.size() > ws_cap_frontier(E.ws)) return E.fail(NBG_E_UNSUPPORTED, "too many vertices in one request");
     static std::atomic<uint64_t> gn_id{1ull << 62};   // program cache keys disjoint from GO statements
     Workspace* ws = E.ws;
+    if (tr_.on) tr_.mark(0);
     hipError_t he = ws_reserve_rows(ws, cap_rows, ncols);
     if (he == hipSuccess) he = ws_begin_query(ws, starts.data(), starts.size(), &plist, gn_id++);
     for (size_t i = 0; he == hipSuccess && i < plist.size(); ++i) {
@@ -423,6 +459,7 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
     }
     if (he == hipSuccess) he = ws_end_query_wait(ws);
     if (he != hipSuccess) return E.fail(NBG_E_DEVICE, std::string("HIP: ") + hipGetErrorString(he));
+    if (tr_.on) tr_.mark(1);
     uint64_t all_rows = 0;
     for (size_t i = 0; i < plist.size(); ++i) {
       const unsigned grid = ws_final_grid_of(ws, (int)i);
@@ -500,8 +537,9 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
   // --- responses per requested vertex, in part order (QueryBaseProcessor::genBuckets order)
   const uint64_t cap = (uint64_t)(E.cfg.max_edge_returned_per_vertex <= 0 ? 0x7fffffff : E.cfg.max_edge_returned_per_vertex);
   const auto& dict = E.snap.strings;
-  auto str_of = [&](int64_t code) -> std::string {
-    return (code >= 0 && (code & 1) == 0 && (uint64_t)(code / 2) < dict.size()) ? dict[code / 2] : std::string();
+  static const std::string kEmpty;
+  auto str_of = [&](int64_t code) -> const std::string& {
+    return (code >= 0 && (code & 1) == 0 && (uint64_t)(code / 2) < dict.size()) ? dict[code / 2] : kEmpty;
   };
   auto put_value = [&](RowBytes& w, int32_t type, int64_t bits) {
     switch (kindOfType(type)) {   // RowReader::getPropByName -> VariantType -> PropsCollector
@@ -580,12 +618,13 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
       if (it == tr.range.end() && !first_old) continue;
       std::string rs;
       uint64_t lo = 0, hi = 0;
+      RowBytes w;
       if (it != tr.range.end()) {
         lo = it->second.first;
         hi = std::min(it->second.second, it->second.first + cap - (first_old ? 1 : 0));
       }
       auto put_row = [&](const std::vector<int64_t>* row, uint64_t r) {
-        RowBytes w;
+        w.clear();
         for (size_t p = 0; p < ec.props.size(); ++p) {
           const PropCtx& pc = ec.props[p];
           const int64_t x = row ? (*row)[p] : tr.vals[p][r];
@@ -595,7 +634,7 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
             default: put_value(w, pc.type, x);
           }
         }
-        rowset_add(rs, w.encode());
+        w.append_to(rs);
         ++resp->edges;
       };
       if (stats) {
@@ -623,6 +662,10 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
     nbg_gn_response::Sch s{ec.type, {}};
     for (auto& pc : ec.props) s.cols.emplace_back(pc.name, pc.type);
     if (!s.cols.empty()) resp->eschema.push_back(std::move(s));
+  }
+  if (tr_.on) {
+    tr_.mark(2);
+    tr_.done();
   }
   return NBG_OK;
 }

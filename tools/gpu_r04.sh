@@ -61,9 +61,13 @@ for step in "$@"; do
     goab)   # GO A/B: claim bitmaps (libnbg.so) vs 4-byte claim stamps (libnbg_stamps.so)
       timeout -k 10 1000 bash tools/go_ab.sh "$TAG/goab" nebula_amd/libnbg.so nebula_amd/libnbg_stamps.so \
         > "$OUT/goab.txt" 2>&1 || { tail -30 "$OUT/goab.txt"; exit 1; } ;;
-    spab)   # SHORTEST A/B: atomicMax level claims (libnbg.so) vs load + CAS (libnbg_cas.so)
-      timeout -k 10 1000 bash tools/sp_ab.sh "$TAG/spab" nebula_amd/libnbg.so nebula_amd/libnbg_cas.so \
+    spab)   # SHORTEST A/B: atomicMax claims + walk in step launches vs load + CAS (_cas) vs separate hop launches (_nofold)
+      timeout -k 10 1000 bash tools/sp_ab.sh "$TAG/spab" nebula_amd/libnbg.so nebula_amd/libnbg_cas.so nebula_amd/libnbg_nofold.so \
         > "$OUT/spab.txt" 2>&1 || { tail -30 "$OUT/spab.txt"; exit 1; } ;;
+    small)   # the small-request legs (C1 nba, getBound) with the getBound phase trace
+      NBG_GN_TRACE=1 timeout -k 10 400 python -u bench.py --scale 16 --roots 4 --steps 1 --warmup 1 --sp-pairs 0 \
+        --c2 0 --c5-scale 0 --c1-reqs 3000 --getbound-reqs 2000 --verify 0 --no-profile \
+        > "$OUT/small.json" 2> "$OUT/small.log" || { tail -30 "$OUT/small.log"; exit 1; } ;;
     p8)   # the 8-way partition, in-process ranks on one GPU
       timeout -k 10 900 python -u -m pytest tests/test_gpu_partition8.py -x -v --timeout 300 --timeout-method thread \
         > "$OUT/pytest_partition8.log" 2>&1 || { tail -40 "$OUT/pytest_partition8.log"; exit 1; } ;;
