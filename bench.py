@@ -913,11 +913,28 @@ def c1_leg(args):
         q0 = time.perf_counter()
         stmt.run([tim])
         lat.append(time.perf_counter() - q0)
+    # the same at the C ABI: nbg_go_execute alone (the rows land in the result's host columns),
+    # without the Python row conversion that stmt.run adds on both sides
+    import ctypes as C
+    starts = np.asarray([tim], np.int64)
+    sp_ = starts.ctypes.data_as(C.POINTER(C.c_int64))
+    clat = []
+    for _ in range(args.c1_reqs):
+        res = C.c_void_p()
+        q0 = time.perf_counter()
+        rc = eng.lib.nbg_go_execute(stmt.h, sp_, 1, 0, C.byref(res))
+        clat.append(time.perf_counter() - q0)
+        assert rc == 0, rc
+        eng.lib.nbg_rows_free(res)
+    tiny = eng.stats()["tiny_queries"]
     stmt.free()
     eng.close()
     out = {"query": "GO 2 STEPS FROM \"Tim Duncan\" OVER like", "rows": len(rows), "queries": args.c1_reqs,
            "p50_ms": float(np.percentile(np.array(lat) * 1e3, 50)),
-           "timing": "prepared statement executed on the device, rows fetched to the host (nbg_go_execute + nbg_rows_fetch)"}
+           "c_abi_p50_ms": float(np.percentile(np.array(clat) * 1e3, 50)),
+           "single_launch_queries": tiny,
+           "timing": "prepared statement executed on the device, rows fetched to the host (nbg_go_execute + "
+                     "nbg_rows_fetch, through Python); c_abi_p50_ms: the nbg_go_execute call alone"}
     try:
         orc = nba_oracle(data, 1)
         olat, orows = [], None
@@ -925,9 +942,20 @@ def c1_leg(args):
             q0 = time.perf_counter()
             orows = orc.go([tim], [like], 2)
             olat.append(time.perf_counter() - q0)
+        # the oracle's own C call alone (orc_go: storaged + graphd restatement, result object built)
+        from tests.support.oracle import _ptr
+        o_t = np.asarray([like], np.int32)
+        oclat = []
+        for _ in range(args.c1_reqs):
+            res = C.c_void_p()
+            q0 = time.perf_counter()
+            orc.L.orc_go(orc.h, _ptr(starts), 1, _ptr(o_t), 1, 0, 2, None, 0, None, None, 0, 0, C.byref(res))
+            oclat.append(time.perf_counter() - q0)
+            orc.L.orc_result_free(res)
         orc.close()
         out["parity_vs_oracle"] = graphs.sorted_rows(orows) == graphs.sorted_rows(rows)
         out["cpu_baseline"] = {"p50_ms": float(np.percentile(np.array(olat) * 1e3, 50)), "cores": 1, "kind": "port",
+                               "c_abi_p50_ms": float(np.percentile(np.array(oclat) * 1e3, 50)),
                                "sample": f"{args.c1_reqs} queries, storaged-faithful oracle (RowSet encode/decode per hop)"}
     except Exception as ex:   # the oracle library is test infrastructure: the leg reports without it
         log(f"c1 cpu baseline unavailable: {ex}")
