@@ -151,10 +151,23 @@ def main():
         good = all(p == single.find_path([s0], [t0], [1], 5) for p in parts)
         ok &= good
         print(f"after the failures: FIND PATH {'OK' if good else 'MISMATCH'}", flush=True)
-    # (5) nbg_go_submit cannot create its slot stream on the last rank only: a plain
-    #     GO carries the failure in band (the peers' wait fails), a YIELD DISTINCT agrees before
-    #     the query (the peers' submit fails); either way every rank reports E_DEVICE, the
-    #     collective sequences match, and the next query runs
+    # $- props after 3 steps: each hop's roots travel packed beside the bitmap (RCCL send/recv
+    # with host counts, kernels.hip ws_roots); every rank's rows together equal the single engine's
+    ins = graphs.roots(src, 5, seed=23)
+    inputs = (["id", "tag"], [[v, 100 + i] for i, v in enumerate(ins)], "id")
+    yin = [E.input_prop("tag").encode(), E.edge_prop("e", "_dst").encode()]
+    for steps in (2, 3):
+        mine = eng.go(ins, [1], steps, where, yin, inputs=inputs)
+        parts = [None] * world
+        dist.all_gather_object(parts, mine)
+        if rank == 0:
+            got = graphs.sorted_rows([row for p in parts for row in p])
+            good = got == graphs.sorted_rows(single.go(ins, [1], steps, where, yin, inputs=inputs)) and len(got) > 0
+            ok &= good
+            print(f"$- props, {steps} steps: {len(got)} rows {'OK' if good else 'MISMATCH'}", flush=True)
+    # (5) nbg_go_submit cannot create its slot stream on the last rank only: GO and
+    #     YIELD DISTINCT both carry the failure in band (the peers' wait fails); every rank reports
+    #     E_DEVICE, the collective sequences match, and the next query runs
     for distinct in (False, True):
         yd = [E.edge_prop("e", "_dst").encode()] if distinct else ()
         st5 = eng.prepare_go([1], 3, where, yd, distinct=distinct)
