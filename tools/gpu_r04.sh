@@ -10,7 +10,7 @@ mkdir -p "$OUT"
 for step in "$@"; do
   case $step in
     tests)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+      NBG_COMM_TIMEOUT_S=60 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread \
         > "$OUT/pytest_gpu.log" 2>&1 || { tail -40 "$OUT/pytest_gpu.log"; exit 1; } ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
@@ -69,7 +69,7 @@ for step in "$@"; do
         --c2 0 --c5-scale 0 --c1-reqs 3000 --getbound-reqs 2000 --verify 0 --no-profile \
         > "$OUT/small.json" 2> "$OUT/small.log" || { tail -30 "$OUT/small.log"; exit 1; } ;;
     p8)   # the 8-way partition, in-process ranks on one GPU
-      timeout -k 10 900 python -u -m pytest tests/test_gpu_partition8.py -x -v --timeout 300 --timeout-method thread \
+      NBG_COMM_TIMEOUT_S=60 timeout -k 10 900 python -u -m pytest tests/test_gpu_partition8.py -x -v --timeout 150 --timeout-method thread \
         > "$OUT/pytest_partition8.log" 2>&1 || { tail -40 "$OUT/pytest_partition8.log"; exit 1; } ;;
     rccl8)   # 8 RCCL processes on one GPU (socket transport)
       timeout -k 10 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
@@ -78,9 +78,10 @@ for step in "$@"; do
     bench8)   # 8-rank bench rehearsal on one GPU (RMAT-20, socket transport)
       NBG_SAME_DEVICE=1 timeout -k 10 900 python -u bench.py --gpus 8 --scale 20 --sp-pairs 2000 \
         > "$OUT/bench8_rmat20_same_device.json" 2> "$OUT/bench8.log" || { tail -40 "$OUT/bench8.log"; exit 1; } ;;
-    pytest:*)   # one test file or node id
+    pytest:*)   # one test file or node id (a hang dumps every thread's stack at 150 s, before the
+                # box's 180 s silence limit; collectives give up after NBG_COMM_TIMEOUT_S)
       t=${step#pytest:}; n=$(basename "${t%%::*}" .py)
-      timeout -k 10 900 python -u -m pytest "$t" -x -v --timeout 300 --timeout-method thread \
+      NBG_COMM_TIMEOUT_S=${NBG_COMM_TIMEOUT_S:-60} timeout -k 10 900 python -u -m pytest "$t" -x -v --timeout 150 --timeout-method thread \
         > "$OUT/pytest_$n.log" 2>&1 || { tail -40 "$OUT/pytest_$n.log"; exit 1; } ;;
     bench)
       timeout -k 10 900 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.log" || { tail -30 "$OUT/bench.log"; exit 1; } ;;
