@@ -132,28 +132,39 @@ def test_go_input_props_backtracker(steps):
         orc.close()
 
 
-def test_input_props_roots_travel_packed(rmat14):
+def test_input_props_roots_travel_packed():
     """The `$-` roots of a hop travel only for the vertices whose bits the hop sends, packed in
     bit order per destination rank: at most twice the bitmap's bytes for these frontiers (they
-    were npad * 8 bytes per peer, 64x the bitmap), and the rows equal the single engine's."""
-    src, dst, w, single, orc, c = rmat14
-    roots = graphs.roots(src, 6, seed=21)
-    inputs = (["id", "tag"], [[r, 7000 + i] for i, r in enumerate(roots)], "id")
-    yields = [E.input_prop("tag").encode(), E.edge_prop("e", "_dst").encode()]
-    agreed = [e.stats()["host_agreements"] for e in c.engines]
-    c.each(lambda e: e.profile(True))
+    were npad * 8 bytes per peer, 64x the bitmap), and the rows equal the oracle's.  (A forest:
+    each vertex has one root, so the reference's last-write-wins backtracker has one answer.)"""
+    from tests.test_gpu_go import _forest
+    roots, src, dst, w = _forest(seed=11, roots=10)
+    c = LocalCluster(100, G)
+    c.register_edge(graphs.E_TYPE, "e", graphs.E_SCHEMA)
+    c.load_edges(graphs.E_TYPE, src, dst, [w])
+    c.finalize()
+    orc = graphs.rmat_oracle(src, dst, w)
     try:
-        got = c.go(roots, [1], 3, b"", yields, inputs=inputs)
-        profs = c.each(lambda e: e.profile_read())
+        inputs = (["id", "tag"], [[r, 7000 + i] for i, r in enumerate(roots)], "id")
+        yields = [E.input_prop("tag").encode(), E.edge_prop("e", "_dst").encode()]
+        agreed = [e.stats()["host_agreements"] for e in c.engines]
+        c.each(lambda e: e.profile(True))
+        try:
+            got = graphs.sorted_rows(c.go(roots, [1], 3, b"", yields, inputs=inputs))
+            profs = c.each(lambda e: e.profile_read())
+        finally:
+            c.each(lambda e: e.profile(False))
+        exp = graphs.sorted_rows(orc.go(roots, [1], 3, b"", yields, inputs=inputs))
+        assert len(got) == len(exp) and got, (len(got), len(exp))
+        assert got == exp
+        bits = sum(p["alltoall(xGMI)"]["algo_bytes"] for p in profs)
+        sent = sum(p["alltoallv(roots)"]["algo_bytes"] for p in profs)
+        assert all(p["alltoallv(roots)"]["launches"] == 2 for p in profs)   # one per hop
+        assert 0 < sent <= 2 * bits, (sent, bits)
+        assert [e.stats()["host_agreements"] for e in c.engines] == [a + 1 for a in agreed]   # ($- inputs agree)
     finally:
-        c.each(lambda e: e.profile(False))
-    exp = single.go(roots, [1], 3, b"", yields, inputs=inputs)
-    assert graphs.sorted_rows(got) == graphs.sorted_rows(exp) and got
-    bits = sum(p["alltoall(xGMI)"]["algo_bytes"] for p in profs)
-    sent = sum(p["alltoallv(roots)"]["algo_bytes"] for p in profs)
-    assert all(p["alltoallv(roots)"]["launches"] == 2 for p in profs)   # one per hop
-    assert 0 < sent <= 2 * bits, (sent, bits)
-    assert [e.stats()["host_agreements"] for e in c.engines] == [a + 1 for a in agreed]   # ($- inputs agree)
+        c.close()
+        orc.close()
 
 
 def test_go_async_slots_split_communicators(rmat14):

@@ -151,20 +151,22 @@ def main():
         good = all(p == single.find_path([s0], [t0], [1], 5) for p in parts)
         ok &= good
         print(f"after the failures: FIND PATH {'OK' if good else 'MISMATCH'}", flush=True)
-    # $- props after 3 steps: each hop's roots travel packed beside the bitmap (RCCL send/recv
-    # with host counts, kernels.hip ws_roots); every rank's rows together equal the single engine's
-    ins = graphs.roots(src, 5, seed=23)
-    inputs = (["id", "tag"], [[v, 100 + i] for i, v in enumerate(ins)], "id")
+    # $- props after 2 / 3 steps: each hop's roots travel packed beside the bitmap (RCCL send/recv
+    # with host counts, kernels.hip ws_roots); every rank's rows together equal the single
+    # engine's.  One start per query: with several, a vertex reached from two roots keeps either
+    # (the reference's backtracker is last-write-wins over unordered responses)
     yin = [E.input_prop("tag").encode(), E.edge_prop("e", "_dst").encode()]
-    for steps in (2, 3):
-        mine = eng.go(ins, [1], steps, where, yin, inputs=inputs)
-        parts = [None] * world
-        dist.all_gather_object(parts, mine)
-        if rank == 0:
-            got = graphs.sorted_rows([row for p in parts for row in p])
-            good = got == graphs.sorted_rows(single.go(ins, [1], steps, where, yin, inputs=inputs)) and len(got) > 0
-            ok &= good
-            print(f"$- props, {steps} steps: {len(got)} rows {'OK' if good else 'MISMATCH'}", flush=True)
+    for i, v in enumerate(graphs.roots(src, 3, seed=23)):
+        inputs = (["id", "tag"], [[v, 100 + i]], "id")
+        for steps in (2, 3):
+            mine = eng.go([v], [1], steps, where, yin, inputs=inputs)
+            parts = [None] * world
+            dist.all_gather_object(parts, mine)
+            if rank == 0:
+                got = graphs.sorted_rows([row for p in parts for row in p])
+                good = got == graphs.sorted_rows(single.go([v], [1], steps, where, yin, inputs=inputs)) and len(got) > 0
+                ok &= good
+                print(f"$- props from {v}, {steps} steps: {len(got)} rows {'OK' if good else 'MISMATCH'}", flush=True)
     # (5) nbg_go_submit cannot create its slot stream on the last rank only: GO and
     #     YIELD DISTINCT both carry the failure in band (the peers' wait fails); every rank reports
     #     E_DEVICE, the collective sequences match, and the next query runs
