@@ -44,7 +44,7 @@ void Engine::free_snapshot() {
     for (auto* p : kv.second.cols)
       if (p) (void)hipFree(p);
   }
-  for (void* p : {(void*)snap.d_tcols, (void*)snap.d_tpres, (void*)snap.d_vids, (void*)snap.d_visible,
+  for (void* p : {(void*)snap.d_tcols, (void*)snap.d_tpres, (void*)snap.d_vids, (void*)snap.d_visible, (void*)snap.d_zero_rows,
                   (void*)snap.d_soff, (void*)snap.d_sbytes, (void*)snap.d_s2i, (void*)snap.d_s2f, (void*)snap.d_s2ok})
     if (p) (void)hipFree(p);
   snap = Snapshot();
@@ -1488,6 +1488,11 @@ int32_t nbg::ws_release(Engine& E, Workspace** wsp, hipStream_t stream) {
 // The query workspace of a finalized (or snapshot-loaded) engine.
 int32_t nbg::engine_ready(Engine& E) {
   if (int32_t rc = E.upload_strings()) return rc;
+  if (E.partitioned() && !E.snap.d_zero_rows) {   // (path.cpp: OVER types this rank has no edges of)
+    const size_t zb = ((size_t)E.snap.nv + 1) * 4;
+    if (hipMalloc((void**)&E.snap.d_zero_rows, zb) != hipSuccess || hipMemset(E.snap.d_zero_rows, 0, zb) != hipSuccess)
+      return E.fail(NBG_E_OUT_OF_MEMORY, "empty CSR rows");
+  }
   if (!E.partitioned()) {   // walk bounds of the tiny GO path (a failure only disables it)
     const uint32_t cap = (uint32_t)(E.cfg.max_edge_returned_per_vertex <= 0 ? 0x7fffffff
                                                                             : E.cfg.max_edge_returned_per_vertex);

@@ -121,6 +121,8 @@ struct Snapshot {
   int64_t* d_vids = nullptr;            // dense id -> vid (sorted ascending, signed)
   std::vector<int64_t> h_vids;
   uint8_t* d_visible = nullptr;         // home part == hash part; nullptr when all visible
+  uint32_t* d_zero_rows = nullptr;      // [nv + 1] zeros: the CSR of an OVER type this rank has no
+                                        // edges of (partitioned FIND PATH, allocated on first use)
   std::vector<uint8_t> h_visible;       // host copy (empty when all visible)
   std::vector<int32_t> h_part;          // home part per dense id
   std::map<int32_t, DevEdgeType> types; // signed type -> CSR

@@ -635,9 +635,32 @@ int32_t find_path_locked(Engine& E, const nbg_path_request* rq, nbg_paths** out,
   }
   PathCtx c{E, E.ws, {}, {}, 0, 0, E.partitioned()};
   const uint32_t cap = 0x7fffffff;
+  // Partitioned, every rank lists every OVER type in the same order: lists, walk records and
+  // greedy candidates name a type by its position, and a rank without edges of a type (a rank
+  // with few or no parts) must not shift the others.  Such a type gets an empty CSR.
+  bool zero_fail = false;
   auto add = [&](PathTypes& pt, int32_t signed_type) {
     auto it = E.snap.types.find(signed_type);
-    if (it == E.snap.types.end()) return;
+    if (it == E.snap.types.end()) {
+      if (!partd) return;
+      if (!E.snap.d_zero_rows) {
+        void* z = nullptr;
+        if (hipMalloc(&z, ((size_t)E.snap.nv + 1) * 4) != hipSuccess || hipMemset(z, 0, ((size_t)E.snap.nv + 1) * 4) != hipSuccess) {
+          if (z) (void)hipFree(z);
+          zero_fail = true;
+          return;
+        }
+        E.snap.d_zero_rows = static_cast<uint32_t*>(z);
+      }
+      ExpandArgs a{};
+      a.row_ptr = E.snap.d_zero_rows;
+      a.visible = E.snap.d_visible;
+      a.vids = E.snap.d_vids;
+      a.cap = cap;
+      pt.type[pt.n] = signed_type;
+      pt.a[pt.n++] = a;
+      return;
+    }
     const DevEdgeType& dt = it->second;
     ExpandArgs a{};
     a.row_ptr = dt.row_ptr;
@@ -656,6 +679,11 @@ int32_t find_path_locked(Engine& E, const nbg_path_request* rq, nbg_paths** out,
   for (int32_t t : over) {
     add(c.fwd, t);
     add(c.bwd, -t);
+  }
+  if (zero_fail) {   // (after the request exchange: the collectives below would run without this rank)
+    if (E.comm) E.comm->abort();
+    delete res;
+    return E.fail(NBG_E_OUT_OF_MEMORY, "empty CSR of an absent OVER type");
   }
   if (E.cfg.max_edge_returned_per_vertex != INT_MAX) {
     // capped rows: the reference's rounds over the two capped graphs (pathcap.hip); every

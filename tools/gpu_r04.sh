@@ -78,6 +78,9 @@ for step in "$@"; do
     bench8)   # 8-rank bench rehearsal on one GPU (RMAT-20, socket transport)
       NBG_SAME_DEVICE=1 timeout -k 10 900 python -u bench.py --gpus 8 --scale 20 --sp-pairs 2000 \
         > "$OUT/bench8_rmat20_same_device.json" 2> "$OUT/bench8.log" || { tail -40 "$OUT/bench8.log"; exit 1; } ;;
+    diagnba)   # FindPathTest goldens over 8 / 7 in-process ranks, per case and mode
+      NBG_COMM_TIMEOUT_S=60 timeout -k 10 300 python -u tools/diag_nba_paths.py 8 7 > "$OUT/diag_nba_paths.txt" 2>&1 \
+        || { tail -30 "$OUT/diag_nba_paths.txt"; exit 1; } ;;
     pytest:*)   # one test file or node id (a hang dumps every thread's stack at 150 s, before the
                 # box's 180 s silence limit; collectives give up after NBG_COMM_TIMEOUT_S)
       t=${step#pytest:}; n=$(basename "${t%%::*}" .py)
