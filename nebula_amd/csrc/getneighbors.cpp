@@ -179,7 +179,7 @@ bool part_served(const Engine& E, int32_t part) {
 struct GnTrace {
   bool on = getenv("NBG_GN_TRACE") != nullptr;
   uint64_t n = 0;
-  double ms[3] = {};
+  double ms[5] = {};
   std::chrono::steady_clock::time_point t;
   void mark(int phase) {
     const auto now = std::chrono::steady_clock::now();
@@ -188,8 +188,10 @@ struct GnTrace {
   }
   void done() {
     if (++n % 500) return;
-    fprintf(stderr, "[gn trace] %llu requests: contexts %.4f ms, device %.4f ms, response %.4f ms\n",
-            (unsigned long long)n, ms[0] / n, ms[1] / n, ms[2] / n);
+    fprintf(stderr,
+            "[gn trace] %llu requests: contexts %.4f ms, device %.4f ms, small-rows read %.4f ms, regroup %.4f ms, "
+            "row bytes %.4f ms\n",
+            (unsigned long long)n, ms[0] / n, ms[1] / n, ms[2] / n, ms[3] / n, ms[4] / n);
   }
 };
 static GnTrace g_gn_trace;
@@ -467,6 +469,14 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
       for (unsigned b = 0; b < grid; ++b) all_rows += per[b];
     }
     const int64_t* small = ws_host_small_rows(ws, all_rows);   // (nullptr: too large, fetched below)
+    // the packed rows out of the mapped block in one pass (each column below is then walked
+    // in key order, a gather the mapped pages would serve a line at a time)
+    std::vector<int64_t> small_rows;
+    if (small) {
+      small_rows.assign(small, small + (size_t)ncols * all_rows);   // (k_q_out_small: ncols columns)
+      small = small_rows.data();
+    }
+    if (tr_.on) tr_.mark(2);
     uint64_t small_off = 0;
     for (size_t i = 0; i < plist.size(); ++i) {
       const int nc = (int)plist[i].yield_reg.size();
@@ -534,6 +544,7 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
     }
   }
 
+  if (tr_.on) tr_.mark(3);
   // --- responses per requested vertex, in part order (QueryBaseProcessor::genBuckets order)
   const uint64_t cap = (uint64_t)(E.cfg.max_edge_returned_per_vertex <= 0 ? 0x7fffffff : E.cfg.max_edge_returned_per_vertex);
   const auto& dict = E.snap.strings;
@@ -664,7 +675,7 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
     if (!s.cols.empty()) resp->eschema.push_back(std::move(s));
   }
   if (tr_.on) {
-    tr_.mark(2);
+    tr_.mark(4);
     tr_.done();
   }
   return NBG_OK;

@@ -68,6 +68,11 @@ for step in "$@"; do
       NBG_GN_TRACE=1 timeout -k 10 400 python -u bench.py --scale 16 --roots 4 --steps 1 --warmup 1 --sp-pairs 0 \
         --c2 0 --c5-scale 0 --c1-reqs 3000 --getbound-reqs 2000 --verify 0 --no-profile \
         > "$OUT/small.json" 2> "$OUT/small.log" || { tail -30 "$OUT/small.log"; exit 1; } ;;
+    smallprof)   # kernel trace of the small-request legs
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/smallprof" -o run --output-format csv -- \
+        python3 -u bench.py --scale 16 --roots 4 --steps 1 --warmup 1 --sp-pairs 0 --c2 0 --c5-scale 0 \
+        --c1-reqs 2000 --getbound-reqs 2000 --verify 0 --no-profile --no-cpu-baseline \
+        > "$OUT/smallprof.json" 2> "$OUT/smallprof.log" || { tail -30 "$OUT/smallprof.log"; exit 1; } ;;
     p8)   # the 8-way partition, in-process ranks on one GPU
       NBG_COMM_TIMEOUT_S=60 timeout -k 10 900 python -u -m pytest tests/test_gpu_partition8.py -x -v --timeout 150 --timeout-method thread \
         > "$OUT/pytest_partition8.log" 2>&1 || { tail -40 "$OUT/pytest_partition8.log"; exit 1; } ;;
