@@ -84,12 +84,9 @@ struct Workspace {
   uint32_t* seg_end1 = nullptr;   // set 1
   uint32_t* seg_rs1 = nullptr;
   uint32_t* tsplit1 = nullptr;
-  // claim bitmaps of the per-step dst SETs (single engine): one bit per vertex and MARK step,
-  // cleared behind the query's end (ws_end_query_wait); cbits_used = steps dirtied since
-  uint32_t* cbits = nullptr;
-  uint64_t cbits_words = 0;       // words per step bitmap (64-byte aligned)
-  int cbits_cap = 0;              // step bitmaps allocated
-  int cbits_used = 0;
+  uint32_t* seen = nullptr;       // [nv + 1] claim stamps of the per-step dst SET (single engine)
+  uint32_t seen_stamp = 0;        // last stamp handed out
+  uint32_t step_stamp = 0;        // stamp of the current step (all its OVER types)
   // partitioned roots ($- / $var props read after 2+ steps): MARKB writes them over the global
   // id space (bt_out); a hop sends only the roots of the vertices whose bits it sends, packed in
   // bit order (bt_pack -> bt_recv), at offsets from the bitmaps' popcount prefixes (ws_roots)
@@ -435,7 +432,7 @@ struct FastProg {
   int64_t lo, hi;
   const void* wcol;        // WHERE column (device pointer, resolved on the host) ...
   int wbytes;              // ... at this width (1/2/4: narrow copy of an INT column; 8)
-  int ykind[MAX_YIELDS];   // 0 DST, 1 SRC, 2 RANK, 3 COL, 4 CONST
+  int ykind[MAX_YIELDS];   // 0 DST, 1 SRC, 2 RANK, 3 COL, 4 CONST, 5 the edge's CSR index
   const void* ycol[MAX_YIELDS];
   int ybytes[MAX_YIELDS];
   int dst_yield;           // some YIELD is _dst
@@ -901,7 +898,6 @@ __device__ unsigned long long degree_of(const DegsumArgs& d, uint32_t v) {
 struct BfsParams {
   uint32_t* lab;                  // claim labels
   uint32_t stamp;                 // claimed label value
-  uint32_t* cbits;                // MARK claim mode: the step's claim bitmap
   uint32_t epoch;                 // a label is live when (lab >> LVL_BITS) == epoch
   const uint32_t* rlab;           // restriction (nullable): claim w only if rlab[w] == rstamp
   uint32_t rstamp;
@@ -918,7 +914,7 @@ struct BfsParams {
   unsigned long long* out_n;      // its length, zero before the level
   DegsumArgs deg;
   unsigned long long* dsum;       // nullable
-  // MARK claim mode (cbits != nullptr): claimed neighbours go to this list with their edge space
+  // MARK claim mode (lab != nullptr): claimed neighbours go to this list with their edge space
   // over nds (the next step's first OVER type); nlist.zero_next is zeroed by workgroup 0
   ListOut nlist;
   DegSrc nds;
@@ -953,9 +949,8 @@ struct FinalParams {
 };
 
 // MARK claim mode: the per-step dst SET (GoExecutor::getDstIdsFromResp, GoExecutor.cpp:501-541)
-// as claims — the first expansion of the step to set a neighbour's bit in the step's bitmap
-// (nv / 8 bytes: L2-resident where per-vertex stamps were not; a plain load filters the
-// already-claimed before the atomic) owns it — and the owners appended to the next frontier list together with their edge space
+// as claims — the first expansion of the step to CAS a neighbour's stamp to the step's stamp
+// owns it — and the owners appended to the next frontier list together with their edge space
 // over the next step's first OVER type: one packed atomic per wave for list positions and edge
 // offsets.  A vertex without edges there is kept (the list is the frontier of every OVER type).
 __device__ __forceinline__ void claim_append(const uint32_t (&u)[VT], const BfsParams& bp, int lane) {
@@ -966,9 +961,9 @@ __device__ __forceinline__ void claim_append(const uint32_t (&u)[VT], const BfsP
     rs[i] = 0;
     const uint32_t x = u[i];
     if (x == NO_ROW) continue;
-    const uint32_t m = 1u << (x & 31);
-    if (bp.cbits[x >> 5] & m) continue;
-    if (atomicOr(bp.cbits + (x >> 5), m) & m) continue;
+    const uint32_t old = bp.lab[x];
+    if (old == bp.stamp) continue;
+    if (atomicCAS(bp.lab + x, old, bp.stamp) != old) continue;
     cmask |= 1u << i;
     dg[i] = vdeg(bp.nds, x, &rs[i]);
   }
@@ -1239,10 +1234,10 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
           if (u[i] == NO_ROW) continue;
           const uint32_t src = list_id(a0 + s);
           a.bt[u[i]] = a.bt_first ? a.vids[src] : a.bt_in[src];
-          if (!bp.cbits) flags[u[i]] = 1;
+          if (!bp.lab) flags[u[i]] = 1;
         }
       }
-      if (bp.cbits) claim_append(u, bp, lane);
+      if (bp.lab) claim_append(u, bp, lane);
     } else if constexpr (M == MARK) {
       uint32_t u[V];   // all neighbour loads in flight before the flag stores / claims
 #pragma unroll
@@ -1254,7 +1249,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
           u[i] = a.col[(uint64_t)sRs[s] + (b0 + k - (uint64_t)sEnd[s])];   // sEnd[s] = start of a0+s
         }
       }
-      if (bp.cbits) {
+      if (bp.lab) {
         claim_append(u, bp, lane);
       } else if (bp.sparse) {
 #pragma unroll
@@ -1426,28 +1421,53 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
       }
       int64_t* const* cols = fp.out_cols;   // kernel-argument array
       uint32_t off = 0;                     // rows of the earlier items of this tile
+      if (kFast && !kDefer) {
+        // the tile's rows first, then one YIELD column at a time with the loads of all V items
+        // in flight together (a load-store pair per item and column left one memory round trip
+        // per cell on the critical path)
+        uint64_t rowv[V];
 #pragma unroll
-      for (int i = 0; i < V && !kDefer; ++i) {
+        for (int i = 0; i < V; ++i) {
+          const bool pass = (pmask >> i) & 1u;
+          const unsigned long long bal = __ballot(pass);
+          rowv[i] = region + off + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+          off += (uint32_t)__popcll(bal);
+        }
+        uint32_t srcv[V];   // (SRC: the list entry's id, loaded once for every column that needs it)
+#pragma unroll
+        for (int i = 0; i < V; ++i) srcv[i] = NO_ROW;
+        for (int y = 0; y < fp.nyields; ++y) {
+          const int kind = fp.fast.ykind[y];
+          int64_t val[V];
+#pragma unroll
+          for (int i = 0; i < V; ++i) {
+            val[i] = 0;
+            if (!((pmask >> i) & 1u)) continue;
+            switch (kind) {
+              case 0: val[i] = dv[i]; break;
+              case 1:
+                if (srcv[i] == NO_ROW) srcv[i] = list_id(a0 + vv[i]);
+                val[i] = a.vids[srcv[i]];
+                break;
+              case 2: val[i] = a.rank ? a.rank[jj[i]] : 0; break;
+              case 3: val[i] = load_col(fp.fast.ycol[y], fp.fast.ybytes[y], jj[i]); break;
+              case 5: val[i] = (int64_t)jj[i]; break;
+              default: val[i] = fp.yield_const[y]; break;
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < V; ++i)
+            if ((pmask >> i) & 1u) cols[y][rowv[i]] = val[i];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < V && !kFast; ++i) {
         const bool pass = (pmask >> i) & 1u;
         const unsigned long long bal = __ballot(pass);
         if (!bal) continue;
         const uint64_t row = region + off + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
         off += (uint32_t)__popcll(bal);
-        if (kFast) {
-          if (pass) {
-            for (int y = 0; y < fp.nyields; ++y) {
-              int64_t val;
-              switch (fp.fast.ykind[y]) {
-                case 0: val = dv[i]; break;
-                case 1: val = a.vids[list_id(a0 + vv[i])]; break;
-                case 2: val = a.rank ? a.rank[jj[i]] : 0; break;
-                case 3: val = load_col(fp.fast.ycol[y], fp.fast.ybytes[y], jj[i]); break;
-                default: val = fp.yield_const[y]; break;
-              }
-              cols[y][row] = val;
-            }
-          }
-        } else {
+        {
           bool yerr = false;
           EdgeCtx c{jj[i], pass ? list_id(a0 + vv[i]) : 0u};
           run_program(fp.prog, fp.prog + fp.prog_len, fp.where_len, fp.prog_len, c, a, regs, pass, yerr, tbits);
@@ -2040,9 +2060,7 @@ Workspace* ws_create(uint64_t max_frontier, uint64_t nv, uint64_t e_max, hipStre
   M((void**)&w->seg_rs1, w->cap_frontier * 4);
   M((void**)&w->rlist, w->cap_frontier * 4);
   M((void**)&w->flags, w->flag_bytes);
-  w->cbits_words = cdiv(nv + 1, 512) * 16;
-  w->cbits_cap = 3;   // GO up to 4 STEPS without growing
-  M((void**)&w->cbits, w->cbits_cap * w->cbits_words * 4);
+  M((void**)&w->seen, (nv + 1) * 4);
   w->e_max = e_max;
   w->cap_tiles = cdiv(w->cap_frontier + e_max + 1, TILE) + 2;
   M((void**)&w->tsplit, w->cap_tiles * 4);
@@ -2069,7 +2087,7 @@ Workspace* ws_create(uint64_t max_frontier, uint64_t nv, uint64_t e_max, hipStre
   if (e == hipSuccess) e = hipHostMalloc((void**)&w->h_prog, (size_t)MAX_TYPES_Q * MAX_PROGRAM * sizeof(Ins),
                                          hipHostMallocDefault);
   if (e == hipSuccess) e = hipMemsetAsync(w->flags, 0, w->flag_bytes, s);
-  if (e == hipSuccess) e = hipMemsetAsync(w->cbits, 0, w->cbits_cap * w->cbits_words * 4, s);
+  if (e == hipSuccess) e = hipMemsetAsync(w->seen, 0, (nv + 1) * 4, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
     if (err) *err = std::string("workspace allocation failed: ") + hipGetErrorString(e);
@@ -2082,7 +2100,7 @@ Workspace* ws_create(uint64_t max_frontier, uint64_t nv, uint64_t e_max, hipStre
 void ws_destroy(Workspace* w) {
   if (!w) return;
   for (void* p : {(void*)w->frontier[0], (void*)w->frontier[1], (void*)w->seg_end, (void*)w->seg_rs,
-                  (void*)w->seg_end1, (void*)w->seg_rs1, (void*)w->tsplit1, (void*)w->cbits,
+                  (void*)w->seg_end1, (void*)w->seg_rs1, (void*)w->tsplit1, (void*)w->seen,
                   (void*)w->rlist, (void*)w->flags, (void*)w->tsplit,
                   (void*)w->q, (void*)w->rows,
                   (void*)w->d_row_cols, (void*)w->d_prog, (void*)w->dtab, (void*)w->dkeep, (void*)w->dseg,
@@ -2182,19 +2200,9 @@ hipError_t ws_wait(Workspace* w) {
   return e;
 }
 
-// The claim bitmaps a query dirtied, zeroed on its stream: behind the query's end event (off its
-// latency), or at the next begin when a query was abandoned after its MARKs were enqueued.
-static hipError_t ws_clear_claims(Workspace* w) {
-  if (!w->cbits_used) return hipSuccess;
-  const hipError_t e = hipMemsetAsync(w->cbits, 0, (size_t)w->cbits_used * w->cbits_words * 4, w->stream);
-  if (e == hipSuccess) w->cbits_used = 0;
-  return e;
-}
-
 hipError_t ws_begin_query(Workspace* w, const uint32_t* starts, uint64_t n, const std::vector<TypeProgram>* progs,
                           uint64_t stmt_id) {
   if (n > w->cap_frontier) return hipErrorInvalidValue;
-  HIP_TRY(ws_clear_claims(w));
   w->cur = 0;
   w->seg_ready = false;
   w->list_acc = nullptr;
@@ -2325,20 +2333,15 @@ hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, 
   // step + 2, whose list (step - 1) nobody reads any more)
   BfsParams bp{};
   if (!w->comm && !w->mark_flags) {
-    if (step < 1) return hipErrorInvalidValue;
-    if (step > w->cbits_cap) {   // a longer GO than any before: grow (rare; the stream drains first)
-      HIP_TRY(hipStreamSynchronize(w->stream));
-      HIP_TRY(hipFree(w->cbits));
-      w->cbits = nullptr;
-      w->cbits_cap = 0;
-      const int cap = step + 1 > MAX_STEPS ? MAX_STEPS : step + 1;
-      HIP_TRY(hipMalloc((void**)&w->cbits, (size_t)cap * w->cbits_words * 4));
-      HIP_TRY(hipMemsetAsync(w->cbits, 0, (size_t)cap * w->cbits_words * 4, w->stream));
-      w->cbits_cap = cap;
-      w->cbits_used = 0;
+    if (tix == 0) {
+      if (++w->seen_stamp == 0) {   // wrap: clear the stamps once
+        HIP_TRY(hipMemsetAsync(w->seen, 0, (w->nv + 1) * 4, w->stream));
+        w->seen_stamp = 1;
+      }
+      w->step_stamp = w->seen_stamp;
     }
-    bp.cbits = w->cbits + (size_t)(step - 1) * w->cbits_words;
-    if (step > w->cbits_used) w->cbits_used = step;
+    bp.lab = w->seen;
+    bp.stamp = w->step_stamp;
     const int nset = w->cur ^ 1;
     bp.nds = deg_src(next0);
     bp.nlist = list_out(w, w->frontier[nset], &w->q->acc[2 + (step + 1) % 3],
@@ -2493,6 +2496,7 @@ static FastProg detect_fast(const TypeProgram& prog, const ExpandArgs& a) {
     if (i.op == OP_DST) { f.ykind[y] = 0; f.dst_yield = 1; }
     else if (i.op == OP_SRC) f.ykind[y] = 1;
     else if (i.op == OP_RANK) f.ykind[y] = 2;
+    else if (i.op == OP_EIDX) f.ykind[y] = 5;
     else if (leaf_col(i)) { f.ykind[y] = 3; f.ycol[y] = col_ptr(a, i.aux, &f.ybytes[y]); }
     else return f;
   }
@@ -2972,41 +2976,69 @@ hipError_t ws_end_query_wait(Workspace* w) {
   }
   // reset for the next query; runs while the host reads the results
   HIP_TRY(hipMemsetAsync(w->q, 0, sizeof(QState), w->stream));
-  HIP_TRY(ws_clear_claims(w));
   prof_flush(w, w->h_q);
   return hipSuccess;
 }
 
 // k_q_out, then (one workgroup) the result's rows into the mapped small-rows buffer when they fit:
 // segment (type t, block b) = rows [region_t + b * blk_cap_t, + count) of every column, packed in
-// (t, b) order at column-major offsets, as nbg_rows / ws_fetch_rows lay them out.
+// (t, b) order at column-major offsets, as nbg_rows / ws_fetch_rows lay them out.  The non-empty
+// segments are listed first (block scans over the row counts, in order), then each is copied by
+// the whole workgroup, one cell per thread (column-major within the segment); a result with more
+// than SMALL_SEGS non-empty segments is left to the host fetch like a large one.
+constexpr int SMALL_SEGS = 2048;
 __global__ void __launch_bounds__(BLOCK) k_q_out_small(const unsigned long long* __restrict__ src, unsigned long long* dst,
                                                        uint32_t n8, const uint32_t* __restrict__ blk_rows, SmallPack sp,
                                                        int64_t* const* __restrict__ cols, int64_t* small) {
   for (uint32_t i = threadIdx.x; i < n8; i += BLOCK) dst[i] = src[i];
-  __shared__ unsigned long long s_total;
-  if (threadIdx.x == 0) s_total = 0;
+  __shared__ uint32_t s_seg[SMALL_SEGS];        // t << 16 | b of the non-empty segments, in order
+  __shared__ uint32_t s_off[SMALL_SEGS + 1];    // their first row in the packed result
+  __shared__ uint32_t s_lds[WAVES];
+  __shared__ uint32_t s_n, s_rows;
+  if (threadIdx.x == 0) s_n = s_rows = 0;
   __syncthreads();
-  unsigned long long part = 0;
-  for (int t = 0; t < sp.ntypes; ++t)
-    for (uint32_t b = threadIdx.x; b < sp.grid[t]; b += BLOCK) part += blk_rows[(size_t)t * EXPAND_GRID + b];
-  atomicAdd(&s_total, part);
-  __syncthreads();
-  const unsigned long long total = s_total;
-  if (total * (unsigned long long)sp.ncols > SMALL_ROWS_WORDS) {
+  bool over = false;
+  for (int t = 0; t < sp.ntypes && !over; ++t) {
+    for (uint32_t b0 = 0; b0 < sp.grid[t]; b0 += BLOCK) {
+      const uint32_t b = b0 + threadIdx.x;
+      const uint32_t n = b < sp.grid[t] ? blk_rows[(size_t)t * EXPAND_GRID + b] : 0u;
+      uint32_t tn = 0, tr = 0;
+      const uint32_t xn = block_excl_scan<BLOCK>(n ? 1u : 0u, &tn, s_lds);
+      const uint32_t xr = block_excl_scan<BLOCK>(n, &tr, s_lds);
+      const uint32_t base_n = s_n, base_r = s_rows;
+      if (base_n + tn > SMALL_SEGS) {   // (uniform)
+        over = true;
+        break;
+      }
+      if (n) {
+        s_seg[base_n + xn] = ((uint32_t)t << 16) | b;
+        s_off[base_n + xn] = base_r + xr;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        s_n = base_n + tn;
+        s_rows = base_r + tr;
+      }
+      __syncthreads();
+    }
+  }
+  const uint64_t total = s_rows;
+  if (over || total * (uint64_t)sp.ncols > SMALL_ROWS_WORDS) {
     if (threadIdx.x == 0) small[0] = 0;
     return;
   }
-  uint64_t off = 0;
-  for (int t = 0; t < sp.ntypes; ++t)
-    for (uint32_t b = 0; b < sp.grid[t]; ++b) {
-      const uint32_t n = blk_rows[(size_t)t * EXPAND_GRID + b];
-      if (!n) continue;
-      const uint64_t base = sp.region[t] + (uint64_t)b * sp.blk_cap[t];
-      for (int c = 0; c < sp.ncols; ++c)
-        for (uint32_t i = threadIdx.x; i < n; i += BLOCK) small[1 + (uint64_t)c * total + off + i] = cols[c][base + i];
-      off += n;
+  const uint32_t nseg = s_n;
+  if (threadIdx.x == 0) s_off[nseg] = (uint32_t)total;
+  __syncthreads();
+  for (uint32_t j = 0; j < nseg; ++j) {
+    const uint32_t t = s_seg[j] >> 16, b = s_seg[j] & 0xFFFFu;
+    const uint32_t off = s_off[j], n = s_off[j + 1] - off;
+    const uint64_t base = sp.region[t] + (uint64_t)b * sp.blk_cap[t];
+    for (uint32_t k = threadIdx.x; k < n * (uint32_t)sp.ncols; k += BLOCK) {
+      const uint32_t c = k / n, i = k - c * n;
+      small[1 + (uint64_t)c * total + off + i] = cols[c][base + i];
     }
+  }
   __syncthreads();
   if (threadIdx.x == 0) small[0] = (int64_t)total + 1;
 }

@@ -28,7 +28,7 @@ struct SpCtx {
   hipStream_t stream = nullptr;
   uint64_t nv = 0, cap = 0, edge_cap = 0;
   ChainCtx* chain = nullptr;       // the level-loop buffers (first query)
-  uint32_t* lab[3] = {};           // forward, backward, B-set labels (spchain.hip stamp_of)
+  uint32_t* lab[3] = {};           // forward, backward, B-set labels (epoch << LVL_BITS | level)
   uint32_t epoch = 0;
   hipEvent_t done = nullptr;
   int prof = 0;                    // nbg_profile mode, applied to the chain when it is created

@@ -232,15 +232,7 @@ __device__ __forceinline__ void gst(T* p, uint64_t i, uint64_t n, T v, int site,
   p[i] = v;
 }
 
-// A label is epoch << LVL_BITS | (63 - level): within one search, an earlier level's label is the
-// larger, so a BFS level claims with one atomicMax (ch_level) — a vertex labelled before keeps its
-// label, an unlabelled one (an older epoch's value) takes the stamp — and no label load first.
-__device__ __forceinline__ uint32_t stamp_of(uint32_t epoch, uint32_t level) {
-  return (epoch << LVL_BITS) | (((1u << LVL_BITS) - 1u) - level);
-}
-#ifndef CH_MAXCLAIM
-#define CH_MAXCLAIM 1
-#endif
+__device__ __forceinline__ uint32_t stamp_of(uint32_t epoch, uint32_t level) { return (epoch << LVL_BITS) | level; }
 __device__ __forceinline__ bool live(uint32_t lab, uint32_t epoch) { return (lab >> LVL_BITS) == epoch; }
 __device__ __forceinline__ unsigned long long ld_agent(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -587,7 +579,7 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
     uint32_t sol[CH_VT], sdg[CH_VT], srs[CH_VT];
 #pragma unroll
     for (int j = 0; j < CH_VT; ++j) {
-      old[j] = c[j] != NO_ROW && !(CH_MAXCLAIM && spec) ? gld(lab, c[j], A.nv, 8, st) : 0u;
+      old[j] = c[j] != NO_ROW ? gld(lab, c[j], A.nv, 8, st) : 0u;
       gate[j] = (c[j] != NO_ROW && rlab) ? gld(rlab, c[j], A.nv, 8, st) : rstamp;
       sol[j] = 0;
       sdg[j] = 0;
@@ -616,14 +608,6 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
         if (CH_GUARD && c[j] >= A.nv) continue;
         if (atomicCAS(lab + c[j], old[j], stamp) != old[j]) continue;
         mm |= 1u << j;
-      }
-    } else if (CH_MAXCLAIM && spec) {
-      const uint32_t fresh = epoch << LVL_BITS;   // labels below it are older searches'
-#pragma unroll
-      for (int j = 0; j < CH_VT; ++j) {
-        if (c[j] == NO_ROW || (first && c[j] == f_own)) continue;   // (s / t: its level-0 label may be in flight)
-        if (CH_GUARD && c[j] >= A.nv) continue;
-        if (atomicMax(lab + c[j], stamp) < fresh) cm |= 1u << j;
       }
     } else {
 #pragma unroll

@@ -58,12 +58,6 @@ for step in "$@"; do
     spprof26)   # kernel trace of the one-pair SP queries (default path)
       timeout -k 10 600 rocprofv3 --kernel-trace -d "$OUT/spprof26" -o run --output-format csv -- \
         python3 -u tools/sp_probe.py 26 400 > "$OUT/spprof26.txt" 2>&1 || { tail -30 "$OUT/spprof26.txt"; exit 1; } ;;
-    goab)   # GO A/B: claim bitmaps (libnbg.so) vs 4-byte claim stamps (libnbg_stamps.so)
-      timeout -k 10 1000 bash tools/go_ab.sh "$TAG/goab" nebula_amd/libnbg.so nebula_amd/libnbg_stamps.so \
-        > "$OUT/goab.txt" 2>&1 || { tail -30 "$OUT/goab.txt"; exit 1; } ;;
-    spab)   # SHORTEST A/B: atomicMax claims + walk in step launches vs load + CAS (_cas) vs separate hop launches (_nofold)
-      timeout -k 10 1000 bash tools/sp_ab.sh "$TAG/spab" nebula_amd/libnbg.so nebula_amd/libnbg_cas.so nebula_amd/libnbg_nofold.so \
-        > "$OUT/spab.txt" 2>&1 || { tail -30 "$OUT/spab.txt"; exit 1; } ;;
     small)   # the small-request legs (C1 nba, getBound) with the getBound phase trace
       NBG_GN_TRACE=1 timeout -k 10 400 python -u bench.py --scale 16 --roots 4 --steps 1 --warmup 1 --sp-pairs 0 \
         --c2 0 --c5-scale 0 --c1-reqs 3000 --getbound-reqs 2000 --verify 0 --no-profile \
