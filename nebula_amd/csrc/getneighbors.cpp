@@ -583,9 +583,10 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
   for (uint64_t i = 0; i < rq->num_vids; ++i) order[i] = i;
   std::stable_sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return rq->parts[a] < rq->parts[b]; });
   std::vector<int32_t> stat_failed;   // parts with a failed vertex (boundStats)
-  for (uint64_t i : order) {
-    if (!part_ok(rq->parts[i])) continue;
-    nbg_gn_response::Vertex v;
+  // one requested vertex: its tag rows and RowSets (boundStats: its values collected) -> whether
+  // it is returned; `edges` counts the rows it returned
+  auto vertex = [&](uint64_t i, nbg_gn_response::Vertex& v, uint64_t& edges) -> bool {
+    if (!part_ok(rq->parts[i])) return false;
     v.vid = rq->vids[i];
     const uint32_t d = dense[i];
     if (stats) {
@@ -598,10 +599,10 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
           stat_failed.push_back(rq->parts[i]);
           resp->failed.emplace_back(NBG_E_UNKNOWN, rq->parts[i]);
         }
-        continue;
+        return false;
       }
     }
-    if (d == NO_ROW) continue;   // no keys in this part: no edges, not returned
+    if (d == NO_ROW) return false;   // no keys in this part: no edges, not returned
     for (auto& tc : tctx) {      // collectVertexProps: the tag's live record, returned props
       const DevTag& dtg = E.snap.tags.at(tc.tag);
       if (!dtg.h_present[d]) continue;
@@ -646,22 +647,43 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
           }
         }
         w.append_to(rs);
-        ++resp->edges;
+        ++edges;
       };
       if (stats) {
         if (first_old)
           for (size_t p = 0; p < ec.props.size(); ++p) collect(ec.props[p], (*first_old)[p]);
         for (uint64_t r = lo; r < hi; ++r)
           for (size_t p = 0; p < ec.props.size(); ++p) collect(ec.props[p], tr.vals[p][r]);
-        resp->edges += hi - lo + (first_old ? 1 : 0);
+        edges += hi - lo + (first_old ? 1 : 0);
         continue;
       }
       if (first_old) put_row(first_old, 0);
       for (uint64_t r = lo; r < hi; ++r) put_row(nullptr, r);
       if (!rs.empty()) v.edges.emplace_back(ec.type, std::move(rs));
     }
-    if (v.edges.empty()) continue;   // only vertices with edges (QueryBoundProcessor.cpp:104-107)
-    resp->vertices.push_back(std::move(v));
+    return !v.edges.empty();   // only vertices with edges (QueryBoundProcessor.cpp:104-107)
+  };
+  if (stats) {   // (collects into shared sums: in order, on this thread)
+    for (uint64_t i : order) {
+      nbg_gn_response::Vertex v;
+      uint64_t e = 0;
+      vertex(i, v, e);
+      resp->edges += e;
+    }
+  } else {
+    // the vertices' responses are independent: encoded in parallel (storaged's handler threads
+    // split a request's vertices the same way, QueryBaseProcessor::genBuckets), kept in order
+    const int64_t nq = (int64_t)order.size();
+    std::vector<nbg_gn_response::Vertex> outv((size_t)nq);
+    std::vector<uint64_t> ne((size_t)nq, 0);
+    std::vector<uint8_t> keep((size_t)nq, 0);
+#pragma omp parallel for schedule(dynamic, 16) if (nq >= 64)
+    for (int64_t k = 0; k < nq; ++k) keep[(size_t)k] = vertex(order[(size_t)k], outv[(size_t)k], ne[(size_t)k]) ? 1 : 0;
+    resp->vertices.reserve((size_t)nq);
+    for (int64_t k = 0; k < nq; ++k) {
+      resp->edges += ne[(size_t)k];
+      if (keep[(size_t)k]) resp->vertices.push_back(std::move(outv[(size_t)k]));
+    }
   }
   // --- onProcessFinished: schemas of the returned columns
   for (auto& tc : tctx) {
