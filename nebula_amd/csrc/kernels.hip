@@ -1438,28 +1438,39 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
         uint32_t srcv[V];   // (SRC: the list entry's id, loaded once for every column that needs it)
 #pragma unroll
         for (int i = 0; i < V; ++i) srcv[i] = NO_ROW;
-        for (int y = 0; y < fp.nyields; ++y) {
-          const int kind = fp.fast.ykind[y];
-          int64_t val[V];
+        constexpr int YG = 4;   // YIELD columns whose loads are in flight together
+        for (int y0 = 0; y0 < fp.nyields; y0 += YG) {
+          int64_t val[YG][V];
 #pragma unroll
-          for (int i = 0; i < V; ++i) {
-            val[i] = 0;
-            if (!((pmask >> i) & 1u)) continue;
-            switch (kind) {
-              case 0: val[i] = dv[i]; break;
-              case 1:
-                if (srcv[i] == NO_ROW) srcv[i] = list_id(a0 + vv[i]);
-                val[i] = a.vids[srcv[i]];
-                break;
-              case 2: val[i] = a.rank ? a.rank[jj[i]] : 0; break;
-              case 3: val[i] = load_col(fp.fast.ycol[y], fp.fast.ybytes[y], jj[i]); break;
-              case 5: val[i] = (int64_t)jj[i]; break;
-              default: val[i] = fp.yield_const[y]; break;
+          for (int u = 0; u < YG; ++u) {
+            const int y = y0 + u;
+            if (y >= fp.nyields) break;   // (uniform)
+            const int kind = fp.fast.ykind[y];
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+              val[u][i] = 0;
+              if (!((pmask >> i) & 1u)) continue;
+              switch (kind) {
+                case 0: val[u][i] = dv[i]; break;
+                case 1:
+                  if (srcv[i] == NO_ROW) srcv[i] = list_id(a0 + vv[i]);
+                  val[u][i] = a.vids[srcv[i]];
+                  break;
+                case 2: val[u][i] = a.rank ? a.rank[jj[i]] : 0; break;
+                case 3: val[u][i] = load_col(fp.fast.ycol[y], fp.fast.ybytes[y], jj[i]); break;
+                case 5: val[u][i] = (int64_t)jj[i]; break;
+                default: val[u][i] = fp.yield_const[y]; break;
+              }
             }
           }
 #pragma unroll
-          for (int i = 0; i < V; ++i)
-            if ((pmask >> i) & 1u) cols[y][rowv[i]] = val[i];
+          for (int u = 0; u < YG; ++u) {
+            const int y = y0 + u;
+            if (y >= fp.nyields) break;
+#pragma unroll
+            for (int i = 0; i < V; ++i)
+              if ((pmask >> i) & 1u) cols[y][rowv[i]] = val[u][i];
+          }
         }
       }
 #pragma unroll
@@ -3003,10 +3014,13 @@ hipError_t ws_end_query_wait(Workspace* w) {
 // the whole workgroup, one cell per thread (column-major within the segment); a result with more
 // than SMALL_SEGS non-empty segments is left to the host fetch like a large one.
 constexpr int SMALL_SEGS = 2048;
+constexpr int SMALL_WGS = 16;
 __global__ void __launch_bounds__(BLOCK) k_q_out_small(const unsigned long long* __restrict__ src, unsigned long long* dst,
                                                        uint32_t n8, const uint32_t* __restrict__ blk_rows, SmallPack sp,
                                                        int64_t* const* __restrict__ cols, int64_t* small) {
-  for (uint32_t i = threadIdx.x; i < n8; i += BLOCK) dst[i] = src[i];
+  // (every workgroup lists the segments; workgroup b copies segments b, b + grid, ... and a share
+  // of the state words: more stores over the host link in flight than one workgroup issues)
+  for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n8; i += gridDim.x * BLOCK) dst[i] = src[i];
   __shared__ uint32_t s_seg[SMALL_SEGS];        // t << 16 | b of the non-empty segments, in order
   __shared__ uint32_t s_off[SMALL_SEGS + 1];    // their first row in the packed result
   __shared__ uint32_t s_lds[WAVES];
@@ -3040,13 +3054,13 @@ __global__ void __launch_bounds__(BLOCK) k_q_out_small(const unsigned long long*
   }
   const uint64_t total = s_rows;
   if (over || total * (uint64_t)sp.ncols > SMALL_ROWS_WORDS) {
-    if (threadIdx.x == 0) small[0] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) small[0] = 0;
     return;
   }
   const uint32_t nseg = s_n;
   if (threadIdx.x == 0) s_off[nseg] = (uint32_t)total;
   __syncthreads();
-  for (uint32_t j = 0; j < nseg; ++j) {
+  for (uint32_t j = blockIdx.x; j < nseg; j += gridDim.x) {
     const uint32_t t = s_seg[j] >> 16, b = s_seg[j] & 0xFFFFu;
     const uint32_t off = s_off[j], n = s_off[j + 1] - off;
     const uint64_t base = sp.region[t] + (uint64_t)b * sp.blk_cap[t];
@@ -3055,8 +3069,8 @@ __global__ void __launch_bounds__(BLOCK) k_q_out_small(const unsigned long long*
       small[1 + (uint64_t)c * total + off + i] = cols[c][base + i];
     }
   }
-  __syncthreads();
-  if (threadIdx.x == 0) small[0] = (int64_t)total + 1;
+  // (the host reads the block after the kernel has completed: any workgroup may mark it)
+  if (blockIdx.x == 0 && threadIdx.x == 0) small[0] = (int64_t)total + 1;
 }
 
 hipError_t ws_end_query_async_small(Workspace* w, const SmallPack& sp) {
@@ -3065,7 +3079,7 @@ hipError_t ws_end_query_async_small(Workspace* w, const SmallPack& sp) {
   for (int t = 0; t < MAX_TYPES_Q; ++t)
     if (w->final_grid[t]) nt = t + 1;
   const size_t bytes = sizeof(QState) + (size_t)nt * EXPAND_GRID * 4;
-  hipLaunchKernelGGL(k_q_out_small, dim3(1), dim3(BLOCK), 0, w->stream, reinterpret_cast<const unsigned long long*>(w->q),
+  hipLaunchKernelGGL(k_q_out_small, dim3(SMALL_WGS), dim3(BLOCK), 0, w->stream, reinterpret_cast<const unsigned long long*>(w->q),
                      reinterpret_cast<unsigned long long*>(w->d_hq), (uint32_t)(bytes / 8), w->blk_rows, sp,
                      (int64_t* const*)w->d_row_cols, w->d_small);
   HIP_TRY(hipGetLastError());
