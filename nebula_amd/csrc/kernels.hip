@@ -873,7 +873,9 @@ __device__ __forceinline__ void run_program(const Ins* __restrict__ prog, const 
 // CDNA one counter, vmcnt, retires loads and stores in issue order)
 // MARKB: MARK that also records each reached vertex's root (VertexBackTracker::add, last write
 // wins as in the reference's unordered iteration) for queries that read $- / $var props
-enum Mode { MARK = 0, FINAL = 1, BFS = 2, FINALF = 3, FINALD = 4, MARKB = 5 };
+// FINALY: FINALF with many YIELD columns (getBound's rows): the loads of YG columns of every item
+// in flight together, at 4 waves/SIMD for the registers they need
+enum Mode { MARK = 0, FINAL = 1, BFS = 2, FINALF = 3, FINALD = 4, MARKB = 5, FINALY = 6 };
 
 struct DegsumArgs {
   int ntypes;
@@ -1042,7 +1044,7 @@ using InlineArg = typename std::conditional<INL, InlineList, NoInline>::type;
 // 6 waves per SIMD measured 307-338 us per RMAT-26 launch against 222 us at V = 4 and 8 waves,
 // profiles/r02_q_final_vt8_ab.json: the default V = VT is the only one launched.)
 template <int M, bool INL = false, int V = VT>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M == FINAL ? 4 : (V > VT ? 6 : 8))))
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(M == FINAL || M == FINALY ? 4 : (V > VT ? 6 : 8))))
 k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_t* __restrict__ seg_end,
          const uint32_t* __restrict__ seg_rs, uint8_t* __restrict__ flags, FinalParams fp, BfsParams bp,
          unsigned long long* stat_e, unsigned long long* stat_n, InlineArg<INL> il) {
@@ -1120,8 +1122,8 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
     if constexpr (INL) return sIl[2 * INLINE_STARTS + i];
     else return a.frontier[i];
   };
-  constexpr bool kFinal = M == FINAL || M == FINALF || M == FINALD;
-  constexpr bool kFast = M == FINALF || M == FINALD;
+  constexpr bool kFinal = M == FINAL || M == FINALF || M == FINALD || M == FINALY;
+  constexpr bool kFast = M == FINALF || M == FINALD || M == FINALY;
   constexpr bool kDefer = M == FINALD;
   int64_t pdv[V];                 // FINALD: the previous tile's _dst values, pass mask, first row
   uint32_t ppm = 0;
@@ -1423,22 +1425,10 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
       }
       int64_t* const* cols = fp.out_cols;   // kernel-argument array
       uint32_t off = 0;                     // rows of the earlier items of this tile
-      if (kFast && !kDefer) {
-        // the tile's rows first, then one YIELD column at a time with the loads of all V items
-        // in flight together (a load-store pair per item and column left one memory round trip
-        // per cell on the critical path)
-        uint64_t rowv[V];
-#pragma unroll
-        for (int i = 0; i < V; ++i) {
-          const bool pass = (pmask >> i) & 1u;
-          const unsigned long long bal = __ballot(pass);
-          rowv[i] = region + off + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-          off += (uint32_t)__popcll(bal);
-        }
-        uint32_t srcv[V];   // (SRC: the list entry's id, loaded once for every column that needs it)
-#pragma unroll
-        for (int i = 0; i < V; ++i) srcv[i] = NO_ROW;
-        constexpr int YG = 4;   // YIELD columns whose loads are in flight together
+      if (M == FINALY) {
+        // YG YIELD columns at a time, with the loads of all their cells in flight together (a
+        // load-store pair per cell left one memory round trip per cell on the critical path)
+        constexpr int YG = 4;
         for (int y0 = 0; y0 < fp.nyields; y0 += YG) {
           int64_t val[YG][V];
 #pragma unroll
@@ -1452,10 +1442,7 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
               if (!((pmask >> i) & 1u)) continue;
               switch (kind) {
                 case 0: val[u][i] = dv[i]; break;
-                case 1:
-                  if (srcv[i] == NO_ROW) srcv[i] = list_id(a0 + vv[i]);
-                  val[u][i] = a.vids[srcv[i]];
-                  break;
+                case 1: val[u][i] = a.vids[list_id(a0 + vv[i])]; break;
                 case 2: val[u][i] = a.rank ? a.rank[jj[i]] : 0; break;
                 case 3: val[u][i] = load_col(fp.fast.ycol[y], fp.fast.ybytes[y], jj[i]); break;
                 case 5: val[u][i] = (int64_t)jj[i]; break;
@@ -1463,23 +1450,43 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
               }
             }
           }
+          uint32_t roff = 0;
 #pragma unroll
-          for (int u = 0; u < YG; ++u) {
-            const int y = y0 + u;
-            if (y >= fp.nyields) break;
+          for (int i = 0; i < V; ++i) {
+            const bool pass = (pmask >> i) & 1u;
+            const unsigned long long bal = __ballot(pass);
+            const uint64_t row = region + roff + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+            roff += (uint32_t)__popcll(bal);
+            if (!pass) continue;
 #pragma unroll
-            for (int i = 0; i < V; ++i)
-              if ((pmask >> i) & 1u) cols[y][rowv[i]] = val[u][i];
+            for (int u = 0; u < YG; ++u)
+              if (y0 + u < fp.nyields) cols[y0 + u][row] = val[u][i];
           }
         }
       }
 #pragma unroll
-      for (int i = 0; i < V && !kFast; ++i) {
+      for (int i = 0; i < V && !kDefer && M != FINALY; ++i) {
         const bool pass = (pmask >> i) & 1u;
         const unsigned long long bal = __ballot(pass);
         if (!bal) continue;
         const uint64_t row = region + off + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
         off += (uint32_t)__popcll(bal);
+        if (kFast) {
+          if (pass) {
+            for (int y = 0; y < fp.nyields; ++y) {
+              int64_t val;
+              switch (fp.fast.ykind[y]) {
+                case 0: val = dv[i]; break;
+                case 1: val = a.vids[list_id(a0 + vv[i])]; break;
+                case 2: val = a.rank ? a.rank[jj[i]] : 0; break;
+                case 3: val = load_col(fp.fast.ycol[y], fp.fast.ybytes[y], jj[i]); break;
+                case 5: val = (int64_t)jj[i]; break;
+                default: val = fp.yield_const[y]; break;
+              }
+              cols[y][row] = val;
+            }
+          }
+        } else
         {
           bool yerr = false;
           EdgeCtx c{jj[i], pass ? list_id(a0 + vv[i]) : 0u};
@@ -2594,12 +2601,16 @@ hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound,
   size_t lds = fp.fast.enabled ? 0 : (size_t)(prog.nregs > 0 ? prog.nregs : 1) * BLOCK * sizeof(int64_t);
   bool dst_only = fp.fast.enabled;   // YIELDs are _dst / constants: the deferred-store instantiation
   for (int y = 0; y < fp.nyields; ++y) dst_only = dst_only && (fp.fast.ykind[y] == 0 || fp.fast.ykind[y] == 4);
+  const bool wide = fp.fast.enabled && !dst_only && fp.nyields >= 4;   // FINALY: many YIELD columns
   hipEvent_t p = prof_begin(w, K_EXPAND_FINAL);
   const dim3 grid(final_grid(n_bound, e_bound));
   unsigned long long* e_st = &w->q->e_st[step][tix];
   if (inl) {
     if (dst_only)
       hipLaunchKernelGGL((k_expand<FINALD, true>), grid, dim3(BLOCK), 0, w->stream, a, L.acc, l_end, l_rs,
+                         w->flags, fp, BfsParams{}, e_st, L.stat_n, *il);
+    else if (wide)
+      hipLaunchKernelGGL((k_expand<FINALY, true>), grid, dim3(BLOCK), 0, w->stream, a, L.acc, l_end, l_rs,
                          w->flags, fp, BfsParams{}, e_st, L.stat_n, *il);
     else if (fp.fast.enabled)
       hipLaunchKernelGGL((k_expand<FINALF, true>), grid, dim3(BLOCK), 0, w->stream, a, L.acc, l_end, l_rs,
@@ -2609,6 +2620,9 @@ hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound,
                          w->flags, fp, BfsParams{}, e_st, L.stat_n, *il);
   } else if (dst_only) {
     hipLaunchKernelGGL(k_expand<FINALD>, grid, dim3(BLOCK), 0, w->stream, a, L.acc, l_end, l_rs, w->flags,
+                       fp, BfsParams{}, e_st, L.stat_n, NoInline{});
+  } else if (wide) {
+    hipLaunchKernelGGL(k_expand<FINALY>, grid, dim3(BLOCK), 0, w->stream, a, L.acc, l_end, l_rs, w->flags,
                        fp, BfsParams{}, e_st, L.stat_n, NoInline{});
   } else if (fp.fast.enabled) {
     hipLaunchKernelGGL(k_expand<FINALF>, grid, dim3(BLOCK), 0, w->stream, a, L.acc, l_end, l_rs, w->flags,

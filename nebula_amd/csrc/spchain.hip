@@ -410,10 +410,11 @@ __device__ __forceinline__ void first_store(const ChArgs& A, const ChQ& q, const
 //     B[kf - k], claimed in LAB_M (push: in-edges of B[kf - k]; pull, k == 0 only: out-edges of
 //     forward level kf - 1).
 // (bid, nblk: this workgroup among the query's workgroups of the launch; NW waves per workgroup)
-// (first: step 0, whose source list {s} or {t} is f's registers)
+// (first: step 0, whose source list {s} or {t} is f0's registers — by value: a pointer to it
+// selected at run time put it in scratch memory)
 template <int NW>
 __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const ChSnap& P, int i, uint32_t bid,
-                                         uint32_t nblk, const ChFirst* first) {
+                                         uint32_t nblk, bool first, const ChFirst f0) {
   __shared__ uint32_t sEndAll[NW][CH_TILE + 2];
   __shared__ uint32_t sRsAll[NW][CH_TILE + 1];
   __shared__ uint16_t sSegAll[NW][CH_TILE];
@@ -472,8 +473,8 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
   unsigned long long* const out_acc = &C.lacc[i];
   // step 0: the one entry of the source list (s forward, t backward) from registers; s and t are
   // labelled level 0 of their sides (workgroup 0 stores those labels during this launch)
-  const uint32_t f_deg = first ? (side ? first->dsb : first->dsf) : 0u;
-  const uint32_t f_rs = first ? (side ? first->rsb : first->rsf) : 0u;
+  const uint32_t f_deg = first ? (side ? f0.dsb : f0.dsf) : 0u;
+  const uint32_t f_rs = first ? (side ? f0.rsb : f0.rsf) : 0u;
   const uint32_t f_own = first ? (side ? q.t : q.s) : NO_ROW, f_other = first ? (side ? q.s : q.t) : NO_ROW;
   const uint64_t n = scnt >> 32, total = scnt & 0xFFFFFFFFull;
   const uint32_t* __restrict__ col = A.col[side];
@@ -683,9 +684,19 @@ template <int NW>
 __device__ __forceinline__ bool ch_step(const ChArgs& A, const ChQ& q, int i, uint32_t bid, uint32_t nblk) {
   ChState* st = A.st;
   ChCtr& C = st->c[q.par];
-  uint32_t j = i == 0 ? 0u : (uint32_t)st->first[i];
+  // launch i runs step i while the search is on (first[i] == i, one step per launch): that
+  // snapshot's loads are issued with first[i]'s, not after it (one memory round trip, not two,
+  // before the level starts); a launch past the search, or after solo steps, reloads
+  uint32_t j = 0;
   ChFirst f0{};
-  ChSnap P = i == 0 ? first_snap(A, q, &f0) : snap_for(st, q, (int)j);
+  ChSnap P;
+  if (i == 0) {
+    P = first_snap(A, q, &f0);
+  } else {
+    j = (uint32_t)st->first[i];
+    const ChSnap Ps = snap_for(st, q, i);
+    P = j == (uint32_t)i ? Ps : snap_for(st, q, (int)j);
+  }
   const bool lead = bid == 0 && threadIdx.x == 0;
   if (i == 0 && bid == 0) {
     // the splits of {s} and {t} for later launches (a backward level from {t}, a pull B-set step
@@ -706,7 +717,7 @@ __device__ __forceinline__ bool ch_step(const ChArgs& A, const ChQ& q, int i, ui
       if (j > 0) st->snap[j] = P;   // (step j + 1 derives its snapshot from it; snap[0]: first_store)
       if (!solo) st->first[i + 1] = j + 1;
     }
-    ch_level<NW>(A, q, P, (int)j, solo ? 0u : bid, solo ? 1u : nblk, j == 0 ? &f0 : nullptr);
+    ch_level<NW>(A, q, P, (int)j, solo ? 0u : bid, solo ? 1u : nblk, j == 0, f0);
     if (!solo) return true;
     // this workgroup's stores and atomics before the next step's reads (labels, lists, counters;
     // the acquire drops L1 lines read before another wave's claims); the snapshot is read back
