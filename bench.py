@@ -137,12 +137,15 @@ def go_leg(eng, stmt, roots, args, barrier, inflight, profile=True):
     barrier()
     t0 = time.perf_counter()
     scanned = rows = 0
-    for _ in range(args.steps):
+    for k in range(args.steps):
         s, r = run_queries(stmt, roots, inflight)
         scanned += s
         rows += r
+        if time.perf_counter() - t0 > 60 and k + 1 < args.steps:   # (a long run says it is alive)
+            log(f"GO step {k + 1}/{args.steps}: {time.perf_counter() - t0:.1f}s")
     barrier()
     elapsed = time.perf_counter() - t0
+    log(f"GO timed steps done: {elapsed:.2f}s")
     lats = []
     for _ in range(4):   # per-query latency: one query at a time, 4 passes over the roots
         for r in roots:
@@ -150,6 +153,7 @@ def go_leg(eng, stmt, roots, args, barrier, inflight, profile=True):
             stmt.run_device([r]).free()
             lats.append(time.perf_counter() - q0)
     out = {"scanned": scanned, "rows": rows, "elapsed": elapsed, "lat": lats}
+    log("GO latency pass done")
     if profile and not args.no_profile:
         # roofline pass: the same K steps with HIP events around every launch of the dominant
         # (final-step) kernel on the engine's stream; the events cost ~10% of the wall time,
@@ -514,7 +518,10 @@ def main():
         dig.append(list(res.digest()) + [res.edges_scanned])
         res.free()
     stmt.free()
+    log("GO leg done")
     fixed = partitioned_costs(eng, roots[:4], barrier) if world > 1 else None
+    if fixed is not None:
+        log("partitioned fixed-cost leg done")
     sp = None
     replica = world > 1 and eng.path_replica_active
     if pairs and replica:

@@ -274,7 +274,7 @@ constexpr int TILE = 64 * VT;          // path items (frontier entries + edges) 
 constexpr int NSHARD = 64;             // row-output shards (one counter + region each)
 constexpr int MAX_STEPS = 32;          // GO N STEPS upper bound
 constexpr int MAX_TYPES_Q = 16;        // OVER types per query
-constexpr int INLINE_STARTS = 128;     // start lists up to this size travel in kernel arguments
+constexpr int INLINE_STARTS = 32;      // start lists up to this size travel in kernel arguments
 constexpr int MAX_TAG_BITS = 16;       // tags addressable by $$ (QState::tagbits: has | used << 16)
 constexpr int MAX_INPUT_COLS = 32;     // columns of a piped / variable input
 

@@ -75,7 +75,7 @@ for step in "$@"; do
         --master-port 29511 tools/rccl_probe.py --same-device > "$OUT/rccl8_probe.log" 2>&1 \
         || { tail -40 "$OUT/rccl8_probe.log"; exit 1; } ;;
     bench8)   # 8-rank bench rehearsal on one GPU (RMAT-20, socket transport)
-      NBG_SAME_DEVICE=1 timeout -k 10 900 python -u bench.py --gpus 8 --scale 20 --sp-pairs 2000 \
+      NBG_SAME_DEVICE=1 timeout -k 10 900 python -u bench.py --gpus 8 --scale 20 --sp-pairs 2000 --steps 3 --warmup 1 \
         > "$OUT/bench8_rmat20_same_device.json" 2> "$OUT/bench8.log" || { tail -40 "$OUT/bench8.log"; exit 1; } ;;
     diagnba)   # FindPathTest goldens over 8 / 7 in-process ranks, per case and mode
       NBG_COMM_TIMEOUT_S=60 timeout -k 10 300 python -u tools/diag_nba_paths.py 8 7 > "$OUT/diag_nba_paths.txt" 2>&1 \
