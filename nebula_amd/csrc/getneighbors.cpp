@@ -194,7 +194,7 @@ struct GnTrace {
             (unsigned long long)n, ms[0] / n, ms[1] / n, ms[2] / n, ms[3] / n, ms[4] / n);
   }
 };
-static GnTrace g_gn_trace;
+static thread_local GnTrace g_gn_trace;   // (per calling thread: engines may serve requests concurrently)
 
 // stats != nullptr: boundStats — accumulate per returned column (stat_types[i] per request column)
 static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_response* resp,
