@@ -58,6 +58,9 @@ for step in "$@"; do
     spprof26)   # kernel trace of the one-pair SP queries (default path)
       timeout -k 10 600 rocprofv3 --kernel-trace -d "$OUT/spprof26" -o run --output-format csv -- \
         python3 -u tools/sp_probe.py 26 400 > "$OUT/spprof26.txt" 2>&1 || { tail -30 "$OUT/spprof26.txt"; exit 1; } ;;
+    kpad)   # SHORTEST chain length A/B: one launch fewer / more than the sized chain
+      timeout -k 10 1000 bash tools/sp_ab.sh "$TAG/kpad" nebula_amd/libnbg.so nebula_amd/libnbg.so,NBG_SP_KPAD=-1 \
+        nebula_amd/libnbg.so,NBG_SP_KPAD=1 > "$OUT/kpad.txt" 2>&1 || { tail -30 "$OUT/kpad.txt"; exit 1; } ;;
     small)   # the small-request legs (C1 nba, getBound) with the getBound phase trace
       NBG_GN_TRACE=1 timeout -k 10 400 python -u bench.py --scale 16 --roots 4 --steps 1 --warmup 1 --sp-pairs 0 \
         --c2 0 --c5-scale 0 --c1-reqs 3000 --getbound-reqs 2000 --verify 0 --no-profile \
