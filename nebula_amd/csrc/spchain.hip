@@ -1154,11 +1154,14 @@ static hipError_t chain_prepare(ChainCtx* c, const SpTypes& fwd, const SpTypes& 
 // in which the greedy walk (or, with no path, the result) runs.
 static int chain_max(const ChainCtx* c) { return 2 * (int)c->q.upto; }
 
-// chain length for c's query: sized by the recent queries (NBG_SP_KPAD launches added: an empty
-// launch costs a few us, a continuation a host round trip); a longer query continues (chain_more)
+// chain length for c's query: sized by the recent queries, one launch under their rounded-up
+// mean (an empty launch costs a few us, a continuation a host round trip: RMAT-26 10 k pairs, p50
+// 0.1032-0.1036 ms against 0.1059-0.1062 at the mean, p90 / mean within 1.5 %,
+// profiles/r04_n_sp_chain_length_ab.txt); NBG_SP_KPAD adds launches.  A longer query continues
+// (chain_more).
 static int chain_length(const ChainCtx* c) {
   static const int kpad = getenv("NBG_SP_KPAD") ? atoi(getenv("NBG_SP_KPAD")) : 0;
-  return std::min(chain_max(c), std::max(2, (int)std::ceil(c->ema_launches) + kpad));
+  return std::min(chain_max(c), std::max(2, (int)std::ceil(c->ema_launches) - 1 + kpad));
 }
 
 hipError_t chain_launch(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible,
