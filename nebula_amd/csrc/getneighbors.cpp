@@ -510,9 +510,12 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
       if (!small && total && ws_fetch_rows_pinned(ws, segs, nc, total, hb) != hipSuccess)
         return E.fail(NBG_E_DEVICE, "row fetch failed");
       // key order: CSR index order (rows of one source are contiguous and sorted)
+      // (edge indices are < 2^32 per type and rows < 2^32: one packed key per row, sorted as
+      // plain integers, then unpacked to row numbers)
       std::vector<uint64_t> ord(total);
-      for (uint64_t r = 0; r < total; ++r) ord[r] = r;
-      std::sort(ord.begin(), ord.end(), [&](uint64_t x, uint64_t y) { return cols[1][x] < cols[1][y]; });
+      for (uint64_t r = 0; r < total; ++r) ord[r] = ((uint64_t)cols[1][r] << 32) | r;
+      std::sort(ord.begin(), ord.end());
+      for (uint64_t r = 0; r < total; ++r) ord[r] &= 0xFFFFFFFFull;
       if (i >= active.size()) {   // older versions: per vid in key order, tagged with their live edge
         const size_t k = active[olds[i - active.size()]];
         const DevEdgeType& od = *E.snap.types.at(ectx[k].type).old;
@@ -535,6 +538,7 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
         tr.eidx[r] = cols[1][ord[r]];
         for (size_t p = 0; p < ymap.size(); ++p) tr.vals[p][r] = cols[ymap[p]][ord[r]];
       }
+      tr.range.reserve(starts.size());
       for (uint64_t r = 0; r < total;) {
         uint64_t e = r;
         while (e < total && tr.vid[e] == tr.vid[r]) ++e;
