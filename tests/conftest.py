@@ -28,7 +28,6 @@ def nba_data():
 @pytest.fixture(params=["chain", "host"])
 def sp_mode(request, monkeypatch):
     """Both one-pair FIND SHORTEST PATH paths (NBG_SP_MODE, read per query): the
-    device-driven level loop (default), the host-driven level loop and the persistent search."""
-    monkeypatch.delenv("NBG_SP_PERSISTENT", raising=False)
+    device-driven level loop (default) and the host-driven level loop."""
     monkeypatch.setenv("NBG_SP_MODE", request.param)
     return request.param

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """FIND SHORTEST PATH latency probe (GPU box): RMAT-<scale>, <pairs> bench pairs one at a time,
 then with query slots.  Env NBG_SP_TRACE=1 prints the device phase breakdown at engine close;
-NBG_SP_MODE=host|persistent picks the host-driven level loop or the persistent search
+NBG_SP_MODE=host picks the host-driven level loop
 (default: the device-driven level loop).  Usage: sp_probe.py <scale> <pairs>"""
 import os
 import sys
