@@ -3041,30 +3041,42 @@ __global__ void __launch_bounds__(BLOCK) k_q_out_small(const unsigned long long*
   __shared__ uint32_t s_n, s_rows;
   if (threadIdx.x == 0) s_n = s_rows = 0;
   __syncthreads();
+  // thread k takes the SMALL_PER consecutive segments [k * SMALL_PER, ...) of each type: one
+  // pair of block scans per type lists them in order
+  constexpr int SMALL_PER = EXPAND_GRID / BLOCK;
+  static_assert(EXPAND_GRID % BLOCK == 0, "segments split evenly over the threads");
   bool over = false;
   for (int t = 0; t < sp.ntypes && !over; ++t) {
-    for (uint32_t b0 = 0; b0 < sp.grid[t]; b0 += BLOCK) {
-      const uint32_t b = b0 + threadIdx.x;
-      const uint32_t n = b < sp.grid[t] ? blk_rows[(size_t)t * EXPAND_GRID + b] : 0u;
-      uint32_t tn = 0, tr = 0;
-      const uint32_t xn = block_excl_scan<BLOCK>(n ? 1u : 0u, &tn, s_lds);
-      const uint32_t xr = block_excl_scan<BLOCK>(n, &tr, s_lds);
-      const uint32_t base_n = s_n, base_r = s_rows;
-      if (base_n + tn > SMALL_SEGS) {   // (uniform)
-        over = true;
-        break;
-      }
-      if (n) {
-        s_seg[base_n + xn] = ((uint32_t)t << 16) | b;
-        s_off[base_n + xn] = base_r + xr;
-      }
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        s_n = base_n + tn;
-        s_rows = base_r + tr;
-      }
-      __syncthreads();
+    uint32_t nn[SMALL_PER], cn = 0, cr = 0;
+    const uint32_t b0 = threadIdx.x * SMALL_PER;
+#pragma unroll
+    for (int k = 0; k < SMALL_PER; ++k) {
+      nn[k] = b0 + k < sp.grid[t] ? blk_rows[(size_t)t * EXPAND_GRID + b0 + k] : 0u;
+      cn += nn[k] ? 1u : 0u;
+      cr += nn[k];
     }
+    uint32_t tn = 0, tr = 0;
+    uint32_t xn = block_excl_scan<BLOCK>(cn, &tn, s_lds);
+    uint32_t xr = block_excl_scan<BLOCK>(cr, &tr, s_lds);
+    const uint32_t base_n = s_n, base_r = s_rows;
+    if (base_n + tn > SMALL_SEGS) {   // (uniform)
+      over = true;
+      break;
+    }
+#pragma unroll
+    for (int k = 0; k < SMALL_PER; ++k) {
+      if (!nn[k]) continue;
+      s_seg[base_n + xn] = ((uint32_t)t << 16) | (b0 + k);
+      s_off[base_n + xn] = base_r + xr;
+      ++xn;
+      xr += nn[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      s_n = base_n + tn;
+      s_rows = base_r + tr;
+    }
+    __syncthreads();
   }
   const uint64_t total = s_rows;
   if (over || total * (uint64_t)sp.ncols > SMALL_ROWS_WORDS) {
