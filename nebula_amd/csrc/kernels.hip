@@ -2601,7 +2601,9 @@ hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound,
   size_t lds = fp.fast.enabled ? 0 : (size_t)(prog.nregs > 0 ? prog.nregs : 1) * BLOCK * sizeof(int64_t);
   bool dst_only = fp.fast.enabled;   // YIELDs are _dst / constants: the deferred-store instantiation
   for (int y = 0; y < fp.nyields; ++y) dst_only = dst_only && (fp.fast.ykind[y] == 0 || fp.fast.ykind[y] == 4);
-  const bool wide = fp.fast.enabled && !dst_only && fp.nyields >= 4;   // FINALY: many YIELD columns
+  // FINALY: many YIELD columns over a small expansion (getBound-sized: latency-bound, where four
+  // columns' loads in flight beat the 8-wave occupancy FINALF keeps for bandwidth-bound steps)
+  const bool wide = fp.fast.enabled && !dst_only && fp.nyields >= 4 && e_bound <= (1ull << 20);
   hipEvent_t p = prof_begin(w, K_EXPAND_FINAL);
   const dim3 grid(final_grid(n_bound, e_bound));
   unsigned long long* e_st = &w->q->e_st[step][tix];
