@@ -45,56 +45,80 @@ namespace {
 // ------------------------------------------------------------------ RowWriter (schema-less mode)
 // QueryBaseProcessor writes rows with RowWriter(nullptr): a SchemaWriter records the columns, the
 // header carries no schema version (RowWriter.cpp:49-75); a block offset every 16 columns.
+// The column bytes go into a plain buffer (room() grows it, the writers store with memcpy): the
+// std::string push_back/append path cost ~25% more per row in the getBound encode.
 struct RowBytes {
-  std::string cord;
+  std::vector<char> cord = std::vector<char>(256);
+  size_t len = 0;
   std::vector<uint64_t> blocks;
   int64_t cols = 0;
+  char* room(size_t n) {
+    if (len + n > cord.size()) cord.resize(std::max(cord.size() * 2, len + n));
+    return cord.data() + len;
+  }
+  void bytes(const void* p, size_t n) {
+    memcpy(room(n), p, n);
+    len += n;
+  }
   void varint(uint64_t v) {
+    char* p = room(10);
+    size_t k = 0;
     while (v >= 0x80) {
-      cord.push_back((char)(v | 0x80));
+      p[k++] = (char)(v | 0x80);
       v >>= 7;
     }
-    cord.push_back((char)v);
+    p[k++] = (char)v;
+    len += k;
   }
   void done() {
     ++cols;
-    if ((cols & 15) == 0) blocks.push_back(cord.size());
+    if ((cols & 15) == 0) blocks.push_back(len);
   }
   void put_int(int64_t v) { varint((uint64_t)v); done(); }
-  void put_vid(int64_t v) { cord.append(reinterpret_cast<const char*>(&v), 8); done(); }
-  void put_double(int64_t bits) { cord.append(reinterpret_cast<const char*>(&bits), 8); done(); }
-  void put_bool(int64_t v) { cord.push_back(v ? 1 : 0); done(); }
-  void put_string(const std::string& s) { varint(s.size()); cord += s; done(); }
+  void put_vid(int64_t v) { bytes(&v, 8); done(); }
+  void put_double(int64_t bits) { bytes(&bits, 8); done(); }
+  void put_bool(int64_t v) { *room(1) = v ? 1 : 0; ++len; done(); }
+  void put_string(const std::string& s) { varint(s.size()); bytes(s.data(), s.size()); done(); }
   void clear() {   // (keeps the buffers: one RowBytes serves every row of a response)
-    cord.clear();
+    len = 0;
     blocks.clear();
     cols = 0;
   }
   int offset_bytes() const {
     int off = 0;
-    uint64_t n = cord.size();
+    uint64_t n = len;
     do { ++off; n >>= 8; } while (n);
     return off;
   }
   std::string encode() const {
-    const int off = offset_bytes();
-    std::string out(1, (char)(off - 1));
-    for (uint64_t b : blocks) out.append(reinterpret_cast<const char*>(&b), off);
-    return out + cord;
+    std::string out;
+    head(out, false);
+    out.append(cord.data(), len);
+    return out;
   }
   // RowSetWriter::addRow(encode()) (RowSetWriter.cpp:21-43) without the temporaries: varint
   // length, then the row
   void append_to(std::string& rs) const {
+    head(rs, true);
+    rs.append(cord.data(), len);
+  }
+  // [varint row length] offset-width byte, block offsets (RowWriter.cpp:49-75), built in one
+  // small buffer
+  void head(std::string& out, bool with_len) const {
     const int off = offset_bytes();
-    uint64_t v = 1 + blocks.size() * (uint64_t)off + cord.size();
-    while (v >= 0x80) {
-      rs.push_back((char)(v | 0x80));
-      v >>= 7;
+    char hdr[16];
+    size_t k = 0;
+    if (with_len) {
+      uint64_t v = 1 + blocks.size() * (uint64_t)off + len;
+      while (v >= 0x80) {
+        hdr[k++] = (char)(v | 0x80);
+        v >>= 7;
+      }
+      hdr[k++] = (char)v;
     }
-    rs.push_back((char)v);
-    rs.push_back((char)(off - 1));
-    for (uint64_t b : blocks) rs.append(reinterpret_cast<const char*>(&b), off);
-    rs += cord;
+    hdr[k++] = (char)(off - 1);
+    out.append(hdr, k);
+    for (uint64_t b : blocks) out.append(reinterpret_cast<const char*>(&b), off);
   }
 };
 
