@@ -41,6 +41,9 @@ for step in "$@"; do
       timeout -k 10 600 python -u bench.py --sp-pairs 0 --no-cpu-baseline --verify 4 --c2 0 --c5-scale 0 \
         --getbound-reqs 0 > "$OUT/$step.json" 2> "$OUT/$step.log" || { tail -30 "$OUT/$step.log"; exit 1; }
       unset NBG_MARK_FLAGS ;;
+    anat26)   # GO 3 STEPS per-query anatomy, kernel-traced
+      timeout -k 10 600 rocprofv3 --kernel-trace -d "$OUT/anat26" -o run --output-format csv -- \
+        python3 -u tools/mark_probe.py 26 16 > "$OUT/anat26.txt" 2>&1 || { tail -30 "$OUT/anat26.txt"; exit 1; } ;;
     ptest)
       timeout -k 10 400 python -u -m pytest tests/test_gpu_path.py tests/test_gpu_configs.py -x -v --timeout 300 \
         --timeout-method thread > "$OUT/pytest_path.log" 2>&1 || { tail -40 "$OUT/pytest_path.log"; exit 1; } ;;
