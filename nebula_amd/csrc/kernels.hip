@@ -132,6 +132,13 @@ struct Workspace {
   QState* d_hq = nullptr;         // its device address
   int64_t* h_small = nullptr;     // mapped pinned: [0] = rows + 1 when packed, then the cells
   int64_t* d_small = nullptr;     // its device address
+  // the host's wake-up (NBG_WAKE, default flag): the end-of-query kernel stores wake_seq into
+  // the mapped word h_wake after its host-visible stores; the host polls it instead of an event
+  unsigned long long* h_wake = nullptr;
+  unsigned long long* d_wake = nullptr;
+  unsigned int* d_ticket = nullptr;   // last-workgroup ticket of a multi-workgroup end kernel
+  unsigned long long wake_seq = 0;
+  bool wake_armed = false;            // the enqueued end kernel will store wake_seq
   uint32_t* h_starts = nullptr;   // pinned staging for start ids
   uint64_t cap_starts = 0;
   Ins* h_prog = nullptr;          // pinned staging for programs
@@ -2011,6 +2018,8 @@ static double prof_bytes_path(const Prof::Rec& r, const PState& p) {
   }
 }
 static void prof_flush(Workspace* w, const QState* q, const PState* ps = nullptr) {
+  // (a host woken by the end kernel's flag may be ahead of the last events)
+  if (!w->prof.pending.empty()) (void)hipEventSynchronize(w->prof.pending.back().b);
   for (auto& r : w->prof.pending) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
@@ -2099,6 +2108,11 @@ Workspace* ws_create(uint64_t max_frontier, uint64_t nv, uint64_t e_max, hipStre
     e = hipHostMalloc((void**)&w->h_small, (SMALL_ROWS_WORDS + 1) * 8, hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&w->d_small, w->h_small, 0);
   if (e == hipSuccess) w->h_small[0] = 0;
+  if (e == hipSuccess) e = hipHostMalloc((void**)&w->h_wake, 64, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&w->d_wake, w->h_wake, 0);
+  if (e == hipSuccess) w->h_wake[0] = 0;
+  if (e == hipSuccess) e = hipMalloc((void**)&w->d_ticket, 64);
+  if (e == hipSuccess) e = hipMemsetAsync(w->d_ticket, 0, 64, s);
   if (e == hipSuccess) {
     w->blk_rows = reinterpret_cast<uint32_t*>(w->q + 1);
     w->h_blk_rows = reinterpret_cast<uint32_t*>(w->h_q + 1);
@@ -2126,10 +2140,10 @@ void ws_destroy(Workspace* w) {
                   (void*)w->d_row_cols, (void*)w->d_prog, (void*)w->dtab, (void*)w->dkeep, (void*)w->dseg,
                   (void*)w->dcnt, (void*)w->dkinds, (void*)w->bt, (void*)w->walk_arena, (void*)w->sarena, (void*)w->xown,
                   (void*)w->xcnt, (void*)w->xsend, (void*)w->xrecv, (void*)w->bt_out, (void*)w->bt_recv,
-                  (void*)w->bt_pack, (void*)w->bt_pre, (void*)w->bt_boff, (void*)w->bt_disp})
+                  (void*)w->bt_pack, (void*)w->bt_pre, (void*)w->bt_boff, (void*)w->bt_disp, (void*)w->d_ticket})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)w->h_q, (void*)w->h_starts, (void*)w->h_prog, (void*)w->h_ps, (void*)w->h_path,
-                  (void*)w->h_stage, (void*)w->h_small})
+                  (void*)w->h_stage, (void*)w->h_small, (void*)w->h_wake})
     if (p) (void)hipHostFree(p);
   if (w->h_pgst) (void)hipHostFree(w->h_pgst);
   if (w->done_ev) (void)hipEventDestroy(w->done_ev);
@@ -2983,9 +2997,60 @@ hipError_t ws_rows_digest(Workspace* w, const std::vector<std::pair<uint64_t, ui
 
 // QState + row counts -> the mapped host mirror with a kernel's stores: a hipMemcpyAsync of these
 // ~13 KB took the copy engine's path, ~130 us against ~3 us (profiles/r03_l_d2h_probe.json).
+// The host's wake-up at the end of a query's last kernel (called by every thread): each thread's
+// stores are released to system scope, then the last workgroup to get here (a ticket, reset for
+// the next query) stores seq into the mapped wake word the host polls.  The host so reads the
+// results as soon as they are visible, not after the kernel has retired and an event behind it
+// has been signalled.
+struct Wake {
+  unsigned long long* word;   // nullptr: the host waits on an event (NBG_WAKE=event)
+  unsigned int* ticket;
+  unsigned long long seq;
+};
+__device__ void wake_host(const Wake& wk) {
+  if (!wk.word) return;
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  if (gridDim.x > 1) {
+    const unsigned got = __hip_atomic_fetch_add(wk.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (got != gridDim.x - 1) return;
+    __hip_atomic_store(wk.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __hip_atomic_store(wk.word, wk.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ void __launch_bounds__(BLOCK) k_q_out(const unsigned long long* __restrict__ src, unsigned long long* dst,
-                                                 uint32_t n8) {
+                                                 uint32_t n8, Wake wk) {
   for (uint32_t i = threadIdx.x; i < n8; i += BLOCK) dst[i] = src[i];
+  wake_host(wk);
+}
+
+static bool wake_by_flag() {
+  static const bool on = !(getenv("NBG_WAKE") && strcmp(getenv("NBG_WAKE"), "event") == 0);
+  return on;
+}
+
+// the Wake of the end kernel being enqueued (arms the host's poll)
+static Wake arm_wake(Workspace* w) {
+  w->wake_armed = wake_by_flag() && !w->comm;
+  if (!w->wake_armed) return Wake{nullptr, nullptr, 0};
+  return Wake{w->d_wake, w->d_ticket, ++w->wake_seq};
+}
+
+// Poll the wake word; the event behind the end kernel is looked at now and then, so a failed
+// launch or a faulted kernel still ends the wait with its error.
+static hipError_t wait_wake(Workspace* w) {
+  const unsigned long long want = w->wake_seq;
+  for (unsigned k = 1;; ++k) {
+    if (__atomic_load_n(w->h_wake, __ATOMIC_ACQUIRE) == want) return hipSuccess;
+    if ((k & 255) == 0) {
+      const hipError_t e = hipEventQuery(w->done_ev);
+      if (e == hipErrorNotReady) continue;
+      if (__atomic_load_n(w->h_wake, __ATOMIC_ACQUIRE) == want) return hipSuccess;
+      return e == hipSuccess ? hipErrorLaunchFailure : e;   // (completed without the store: a bug)
+    }
+  }
 }
 
 // The end of a query in two halves: the QState / row-count store into host memory and an event
@@ -2996,8 +3061,9 @@ hipError_t ws_end_query_async(Workspace* w) {
     if (w->final_grid[t]) nt = t + 1;
   static_assert(sizeof(QState) % 8 == 0 && EXPAND_GRID % 2 == 0, "k_q_out copies 8-byte words");
   const size_t bytes = sizeof(QState) + (size_t)nt * EXPAND_GRID * 4;
+  const Wake wk = arm_wake(w);
   hipLaunchKernelGGL(k_q_out, dim3(1), dim3(BLOCK), 0, w->stream, reinterpret_cast<const unsigned long long*>(w->q),
-                     reinterpret_cast<unsigned long long*>(w->d_hq), (uint32_t)(bytes / 8));
+                     reinterpret_cast<unsigned long long*>(w->d_hq), (uint32_t)(bytes / 8), wk);
   HIP_TRY(hipGetLastError());
   if (w->h_small) w->h_small[0] = 0;   // (this query's rows are not packed: the device does not run
                                        // ahead of this host write, the stream is idle on this slot)
@@ -3009,6 +3075,9 @@ hipError_t ws_end_query_wait(Workspace* w) {
   static const bool blocking = getenv("NBG_BLOCKING_SYNC") != nullptr;
   if (w->comm) {
     HIP_TRY(ws_sync(w));   // bounded: a peer that never arrives aborts the communicator
+  } else if (w->wake_armed) {
+    w->wake_armed = false;
+    HIP_TRY(wait_wake(w));
   } else if (blocking) {
     HIP_TRY(hipEventSynchronize(w->done_ev));
   } else {
@@ -3033,7 +3102,7 @@ constexpr int SMALL_SEGS = 2048;
 constexpr int SMALL_WGS = 16;
 __global__ void __launch_bounds__(BLOCK) k_q_out_small(const unsigned long long* __restrict__ src, unsigned long long* dst,
                                                        uint32_t n8, const uint32_t* __restrict__ blk_rows, SmallPack sp,
-                                                       int64_t* const* __restrict__ cols, int64_t* small) {
+                                                       int64_t* const* __restrict__ cols, int64_t* small, Wake wk) {
   // (every workgroup lists the segments; workgroup b copies segments b, b + grid, ... and a share
   // of the state words: more stores over the host link in flight than one workgroup issues)
   for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n8; i += gridDim.x * BLOCK) dst[i] = src[i];
@@ -3083,6 +3152,7 @@ __global__ void __launch_bounds__(BLOCK) k_q_out_small(const unsigned long long*
   const uint64_t total = s_rows;
   if (over || total * (uint64_t)sp.ncols > SMALL_ROWS_WORDS) {
     if (blockIdx.x == 0 && threadIdx.x == 0) small[0] = 0;
+    wake_host(wk);
     return;
   }
   const uint32_t nseg = s_n;
@@ -3097,8 +3167,9 @@ __global__ void __launch_bounds__(BLOCK) k_q_out_small(const unsigned long long*
       small[1 + (uint64_t)c * total + off + i] = cols[c][base + i];
     }
   }
-  // (the host reads the block after the kernel has completed: any workgroup may mark it)
+  // (the host reads the block after the wake or the kernel's completion: any workgroup may mark it)
   if (blockIdx.x == 0 && threadIdx.x == 0) small[0] = (int64_t)total + 1;
+  wake_host(wk);
 }
 
 hipError_t ws_end_query_async_small(Workspace* w, const SmallPack& sp) {
@@ -3107,9 +3178,10 @@ hipError_t ws_end_query_async_small(Workspace* w, const SmallPack& sp) {
   for (int t = 0; t < MAX_TYPES_Q; ++t)
     if (w->final_grid[t]) nt = t + 1;
   const size_t bytes = sizeof(QState) + (size_t)nt * EXPAND_GRID * 4;
+  const Wake wk = arm_wake(w);
   hipLaunchKernelGGL(k_q_out_small, dim3(SMALL_WGS), dim3(BLOCK), 0, w->stream, reinterpret_cast<const unsigned long long*>(w->q),
                      reinterpret_cast<unsigned long long*>(w->d_hq), (uint32_t)(bytes / 8), w->blk_rows, sp,
-                     (int64_t* const*)w->d_row_cols, w->d_small);
+                     (int64_t* const*)w->d_row_cols, w->d_small, wk);
   HIP_TRY(hipGetLastError());
   if (!w->done_ev) HIP_TRY(hipEventCreateWithFlags(&w->done_ev, hipEventDisableTiming));
   return hipEventRecord(w->done_ev, w->stream);
@@ -3145,6 +3217,7 @@ struct TinyParams {
   int64_t* const* cols;            // the workspace's row columns (device)
   unsigned long long* hq;          // mapped: QState, then the per-workgroup row counts
   int64_t* small;                  // mapped: [0] = rows + 1, then the cells column by column
+  Wake wk;
 };
 
 constexpr uint32_t TINY_HASH = 2 * TINY_EDGES;   // set slots (power of two, half full at most)
@@ -3286,6 +3359,7 @@ __global__ void __launch_bounds__(BLOCK) k_go_tiny(TinyParams t) {
     for (uint32_t i = tid; i < nrows; i += BLOCK) t.small[1 + (uint64_t)y * nrows + i] = t.cols[y][i];
   __syncthreads();
   if (tid == 0) t.small[0] = fits ? (int64_t)nrows + 1 : 0;
+  wake_host(t.wk);
 }
 
 // Walk bounds of one CSR for the tiny path: W_k(v) = deg(v) + sum over v's (capped) edges of
@@ -3361,6 +3435,7 @@ hipError_t ws_go_tiny(Workspace* w, const ExpandArgs& a, const uint32_t* starts,
   t.cols = (int64_t* const*)w->d_row_cols;
   t.hq = reinterpret_cast<unsigned long long*>(w->d_hq);
   t.small = w->d_small;
+  t.wk = arm_wake(w);
   for (auto& g : w->final_grid) g = 0;
   w->final_grid[0] = 1;   // (one workgroup's rows: go_collect reads one count)
   const size_t lds = (size_t)(prog.nregs > 0 ? prog.nregs : 1) * BLOCK * sizeof(int64_t);

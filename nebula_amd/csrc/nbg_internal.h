@@ -419,6 +419,7 @@ hipError_t chain_launch(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, con
                         const int64_t* vids, uint32_t* const lab[3], uint32_t epoch, uint32_t s, uint32_t t,
                         uint32_t upto);
 bool chain_more(ChainCtx* c, hipError_t* he);   // false: a continuation batch was enqueued
+bool chain_woken(const ChainCtx* c);   // the current batch's last launch has stored the result
 // one query of a batched chain (spchain.hip, chain_launch_batch)
 struct ChainQuery {
   const SpTypes* fwd;

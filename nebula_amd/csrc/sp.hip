@@ -120,19 +120,35 @@ hipError_t sp_launch_batch(SpCtx* const* cs, int n, const SpPair* pairs) {
   return hipSuccess;
 }
 
-bool sp_ready(SpCtx* c) { return hipEventQuery(c->done) == hipSuccess; }
+// NBG_WAKE=event: wait for the event behind the batch only (the A/B baseline)
+static bool wake_by_flag() {
+  static const bool on = !(getenv("NBG_WAKE") && strcmp(getenv("NBG_WAKE"), "event") == 0);
+  return on;
+}
+
+bool sp_ready(SpCtx* c) { return (wake_by_flag() && chain_woken(c->chain)) || hipEventQuery(c->done) == hipSuccess; }
+
+// The batch's end: its last launch's wake word (the result is readable before the launch has
+// retired and the event behind it is signalled), or the event — a batch that ended inside the
+// search stores nothing, and a failed launch ends the wait with its error.
+static hipError_t wait_batch(SpCtx* c) {
+  const bool flag = wake_by_flag();
+  for (unsigned k = 1;; ++k) {
+    if (flag && chain_woken(c->chain)) return hipSuccess;
+    if (!flag || (k & 255) == 0) {
+      const hipError_t e = hipEventQuery(c->done);
+      if (e != hipErrorNotReady) return e;
+    }
+  }
+}
 
 hipError_t sp_wait(SpCtx* c, SpResult* out) {
-  hipError_t e;
-  while ((e = hipEventQuery(c->done)) == hipErrorNotReady) {
-  }
+  hipError_t e = wait_batch(c);
   if (e != hipSuccess) return e;
   while (!chain_more(c->chain, &e)) {   // a continuation batch: wait for it too
     if (e == hipSuccess) e = hipEventRecord(c->done, c->stream);
     if (e != hipSuccess) return e;
-    while ((e = hipEventQuery(c->done)) == hipErrorNotReady) {
-    }
-    if (e != hipSuccess) return e;
+    if ((e = wait_batch(c)) != hipSuccess) return e;
   }
   if (e != hipSuccess) return e;
   chain_result(c->chain, out);

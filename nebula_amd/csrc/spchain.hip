@@ -124,6 +124,7 @@ struct ChOut {
   unsigned long long busy;             // ChState::busy
   unsigned long long tag;              // ChQ::tag of the batch whose launch stored this
   long long path[1 + 3 * MAX_PATH_LEN];
+  unsigned long long wake;             // = tag, stored last (system-scope release): the host polls it
 };
 
 struct ChArgs {         // device memory (indexed at run time: never a by-value kernel argument)
@@ -927,6 +928,10 @@ __device__ __forceinline__ void ch_out(const ChArgs& A, const ChQ& q, int steps,
   }
   unsigned long long* nxt = reinterpret_cast<unsigned long long*>(&st->c[q.par ^ 1u]);
   for (uint32_t k = threadIdx.x; k < sizeof(ChCtr) / 8; k += blockDim.x) nxt[k] = 0;
+  // the host's wake-up: every thread's stores released to system scope, then the tag
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(&out->wake, q.tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // One query per launch (the chain of one pair): step launch 0 starts the search (no set-up
@@ -1025,7 +1030,8 @@ struct ChainCtx {
     (void)hipEventRecord(r.b, stream);
     pend.push_back(r);
   }
-  void flush() {   // the stream has passed every pending event
+  void flush() {   // (a host woken by the result's flag may be ahead of the last event)
+    if (!pend.empty()) (void)hipEventSynchronize(pend.back().b);
     for (auto& r : pend) {
       float t = 0;
       if (hipEventElapsedTime(&t, r.a, r.b) == hipSuccess) ms[r.kind] += t;
@@ -1059,6 +1065,7 @@ ChainCtx* chain_create(uint64_t nv, uint64_t edge_cap, hipStream_t s, std::strin
   M((void**)&c->d_args, sizeof(ChArgs));
   if (he == hipSuccess) he = hipHostMalloc((void**)&c->h_out, sizeof(ChOut), hipHostMallocMapped | hipHostMallocCoherent);
   if (he == hipSuccess) he = hipHostGetDevicePointer((void**)&c->d_out, c->h_out, 0);
+  if (he == hipSuccess) c->h_out->wake = 0;
   if (he == hipSuccess) he = hipHostMalloc((void**)&c->h_args, sizeof(ChArgs), hipHostMallocDefault);
   if (he == hipSuccess) he = hipMemsetAsync(c->d_st, 0, sizeof(ChState), s);
   if (he == hipSuccess) he = hipStreamSynchronize(s);
@@ -1218,6 +1225,10 @@ hipError_t chain_launch_batch(ChainCtx* const* cs, int n, const ChainQuery* qs) 
 
 // After a batch's copy completed: the query's final state, or false with a continuation batch
 // enqueued (the caller waits again).
+bool chain_woken(const ChainCtx* c) {
+  return c && c->h_out && __atomic_load_n(&c->h_out->wake, __ATOMIC_ACQUIRE) == c->q.tag;
+}
+
 bool chain_more(ChainCtx* c, hipError_t* he) {
   *he = hipSuccess;
   const ChOut& h = *c->h_out;

@@ -44,6 +44,19 @@ for step in "$@"; do
     anat26)   # GO 3 STEPS per-query anatomy, kernel-traced
       timeout -k 10 600 rocprofv3 --kernel-trace -d "$OUT/anat26" -o run --output-format csv -- \
         python3 -u tools/mark_probe.py 26 16 > "$OUT/anat26.txt" 2>&1 || { tail -30 "$OUT/anat26.txt"; exit 1; } ;;
+    wake)   # host wake-up after a query's last kernel: event poll vs mapped-flag poll
+      timeout -k 10 120 ./tools/wake_probe > "$OUT/wake.txt" 2>&1 || { tail -30 "$OUT/wake.txt"; exit 1; } ;;
+    wakeab)   # GO leg and small legs with the flag wake-up vs the event wait
+      timeout -k 10 700 bash tools/go_ab.sh "$TAG/wakeab" nebula_amd/libnbg.so nebula_amd/libnbg.so,NBG_WAKE=event \
+        > "$OUT/wakeab.txt" 2>&1 || { tail -30 "$OUT/wakeab.txt"; exit 1; }
+      for wk in flag event; do
+        NBG_WAKE=$wk timeout -k 10 400 python -u bench.py --scale 16 --roots 4 --steps 1 --warmup 1 --sp-pairs 0 \
+          --c2 0 --c5-scale 0 --c1-reqs 3000 --getbound-reqs 2000 --verify 0 --no-profile --no-cpu-baseline \
+          > "$OUT/small_$wk.json" 2> "$OUT/small_$wk.log" || { tail -30 "$OUT/small_$wk.log"; exit 1; }
+      done ;;
+    spwake)   # SHORTEST latency with the flag wake-up vs the event wait
+      timeout -k 10 1000 bash tools/sp_ab.sh "$TAG/spwake" nebula_amd/libnbg.so nebula_amd/libnbg.so,NBG_WAKE=event \
+        > "$OUT/spwake.txt" 2>&1 || { tail -30 "$OUT/spwake.txt"; exit 1; } ;;
     ptest)
       timeout -k 10 400 python -u -m pytest tests/test_gpu_path.py tests/test_gpu_configs.py -x -v --timeout 300 \
         --timeout-method thread > "$OUT/pytest_path.log" 2>&1 || { tail -40 "$OUT/pytest_path.log"; exit 1; } ;;
