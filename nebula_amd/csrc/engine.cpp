@@ -849,9 +849,13 @@ struct GoPending {
 // pre_rc: a failure the caller already had on this rank (nbg_go_submit's slot stream); it is
 // reported through the same agreement as the preparation failures below, so the peers' collective
 // sequence for the query still matches.
+// sync: the caller waits for this query next (nbg_go_execute): its end kernel wakes the host by
+// the mapped flag.  A submitted query is waited for by its event: the other slots' queries hide
+// the wake-up, and the event lets the runtime retire finished work (six in flight ran ~1 %
+// slower on the flag, profiles/r04_w/x_go_wake_ab*.txt).
 static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts, uint64_t num_starts, bool device,
-                         Workspace** wsp, hipStream_t stream, Comm* qcomm, GoPending* p, int32_t pre_rc = NBG_OK,
-                         const char* pre_msg = nullptr) {
+                         Workspace** wsp, hipStream_t stream, Comm* qcomm, GoPending* p, bool sync,
+                         int32_t pre_rc = NBG_OK, const char* pre_msg = nullptr) {
   if (num_starts && !starts) return E.fail(NBG_E_INVALID_ARGUMENT, "null argument");
   if (hipSetDevice(E.cfg.device) != hipSuccess) return E.fail(NBG_E_DEVICE, "hipSetDevice failed");
   const bool part = E.partitioned();
@@ -939,6 +943,7 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
     }
   }
   Workspace* ws = *wsp;
+  if (ws) ws_set_wake(ws, sync);
   int64_t *bt = nullptr, *bt_in = nullptr;   // VertexBackTracker roots ($- / $var props after >= 2 steps)
   if (ws) ws_backtracker_off(ws);
   if (!lrc && st->uses_input) {
@@ -1410,7 +1415,7 @@ static int32_t go_execute(Engine& E, const nbg_go_stmt* st, const int64_t* start
   if (!out) return E.fail(NBG_E_INVALID_ARGUMENT, "null argument");
   *out = nullptr;
   GoPending p;
-  int32_t rc = go_launch(E, st, starts, num_starts, device, &E.ws, E.stream, E.comm.get(), &p);
+  int32_t rc = go_launch(E, st, starts, num_starts, device, &E.ws, E.stream, E.comm.get(), &p, true);
   if (rc) return rc;
   return go_collect(E, st, &p, out);
 }
@@ -1580,7 +1585,7 @@ int32_t nbg_go_submit(nbg_go_stmt* st, const int64_t* starts, uint64_t num_start
   auto* t = new nbg_go_ticket();
   t->st = st;
   t->slot = slot;
-  int32_t rc = go_launch(E, st, starts, num_starts, device != 0, &q.ws, qstream, qcomm, &t->p, pre_rc,
+  int32_t rc = go_launch(E, st, starts, num_starts, device != 0, &q.ws, qstream, qcomm, &t->p, false, pre_rc,
                          "hipStreamCreate failed");
   // an in-band failure keeps its slot like any submitted query (the peers' slot holds theirs);
   // nbg_go_wait returns the code

@@ -592,6 +592,7 @@ hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a, uint64_t n_bound, u
 // after all types of a non-final step (single engine): the claimed list becomes the frontier
 hipError_t ws_finish_step(Workspace* w, int step, const ExpandArgs* next0);
 void ws_set_mark_claims(Workspace* w, bool claims);   // per query, before its first step
+void ws_set_wake(Workspace* w, bool flag);   // the next end kernel wakes the host by its mapped flag
 // step N, per OVER type: scan + WHERE/YIELD + sharded row emission into [region_base, +NSHARD*shard_cap)
 hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a, uint64_t n_bound, uint64_t e_bound, int step, int tix,
                            const TypeProgram& prog, uint64_t region_base, uint64_t blk_cap, const InlineList* il = nullptr);

@@ -134,7 +134,10 @@ bool sp_ready(SpCtx* c) { return (wake_by_flag() && chain_woken(c->chain)) || hi
 static hipError_t wait_batch(SpCtx* c) {
   const bool flag = wake_by_flag();
   for (unsigned k = 1;; ++k) {
-    if (flag && chain_woken(c->chain)) return hipSuccess;
+    if (flag && chain_woken(c->chain)) {
+      (void)hipEventQuery(c->done);   // (lets the runtime retire what it has finished)
+      return hipSuccess;
+    }
     if (!flag || (k & 255) == 0) {
       const hipError_t e = hipEventQuery(c->done);
       if (e != hipErrorNotReady) return e;

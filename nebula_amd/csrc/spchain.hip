@@ -929,7 +929,7 @@ __device__ __forceinline__ void ch_out(const ChArgs& A, const ChQ& q, int steps,
   unsigned long long* nxt = reinterpret_cast<unsigned long long*>(&st->c[q.par ^ 1u]);
   for (uint32_t k = threadIdx.x; k < sizeof(ChCtr) / 8; k += blockDim.x) nxt[k] = 0;
   // the host's wake-up: every thread's stores released to system scope, then the tag
-  __threadfence_system();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // (release only, at system scope: no cache invalidation)
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(&out->wake, q.tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
