@@ -1165,8 +1165,9 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
   if (he == hipSuccess && part) he = ws_global_stats(ws, (int)over.size());
   // a single engine's result that will be fetched to the host is packed there by the end-of-query
   // kernel when it is small (one host round trip less for it; YIELD DISTINCT compacts the rows
-  // after this point, so it fetches them the usual way)
-  if (he == hipSuccess && !part && !st->distinct && ncols > 0) {
+  // after this point, so it fetches them the usual way).  A device result (rows left in HBM) is
+  // not: its end kernel is the one-workgroup state copy, a later nbg_rows_fetch copies the rows.
+  if (he == hipSuccess && !part && !st->distinct && ncols > 0 && !device) {
     SmallPack sp{};
     sp.ntypes = (int)over.size();
     sp.ncols = ncols;
@@ -1396,7 +1397,7 @@ static int32_t go_collect(Engine& E, const nbg_go_stmt* st, GoPending* p, nbg_ro
     }
   }
   for (int c = 0; c < ncols; ++c) rows->dcols.push_back(ws_row_col(ws, c));
-  rows->small_ok = !E.partitioned() && !st->distinct;   // (go_launch packed a small result)
+  rows->small_ok = !E.partitioned() && !st->distinct && !device;   // (go_launch packed a small result)
   if (!device) {
     int32_t rc = materialize_rows(rows);
     if (rc) {

@@ -57,6 +57,9 @@ for step in "$@"; do
     spwake)   # SHORTEST latency with the flag wake-up vs the event wait
       timeout -k 10 1000 bash tools/sp_ab.sh "$TAG/spwake" nebula_amd/libnbg.so nebula_amd/libnbg.so,NBG_WAKE=event \
         > "$OUT/spwake.txt" 2>&1 || { tail -30 "$OUT/spwake.txt"; exit 1; } ;;
+    goprev)   # GO leg: this build vs nebula_amd/libnbg_prev.so (the previous commit's)
+      timeout -k 10 700 bash tools/go_ab.sh "$TAG/goprev" nebula_amd/libnbg.so nebula_amd/libnbg_prev.so \
+        > "$OUT/goprev.txt" 2>&1 || { tail -30 "$OUT/goprev.txt"; exit 1; } ;;
     ptest)
       timeout -k 10 400 python -u -m pytest tests/test_gpu_path.py tests/test_gpu_configs.py -x -v --timeout 300 \
         --timeout-method thread > "$OUT/pytest_path.log" 2>&1 || { tail -40 "$OUT/pytest_path.log"; exit 1; } ;;
