@@ -3165,14 +3165,20 @@ __global__ void __launch_bounds__(BLOCK) k_q_out_small(const unsigned long long*
   const uint32_t nseg = s_n;
   if (threadIdx.x == 0) s_off[nseg] = (uint32_t)total;
   __syncthreads();
-  for (uint32_t j = blockIdx.x; j < nseg; j += gridDim.x) {
-    const uint32_t t = s_seg[j] >> 16, b = s_seg[j] & 0xFFFFu;
-    const uint32_t off = s_off[j], n = s_off[j + 1] - off;
-    const uint64_t base = sp.region[t] + (uint64_t)b * sp.blk_cap[t];
-    for (uint32_t k = threadIdx.x; k < n * (uint32_t)sp.ncols; k += BLOCK) {
-      const uint32_t c = k / n, i = k - c * n;
-      small[1 + (uint64_t)c * total + off + i] = cols[c][base + i];
+  // the packed cells split evenly over every workgroup's threads (a small result has few
+  // segments: a workgroup per segment left most of the grid idle and each thread a long chain of
+  // reads); cell k = column c, packed row r, found in the segment list by a binary search in LDS
+  const uint32_t rows = (uint32_t)total, cells = rows * (uint32_t)sp.ncols;
+  for (uint32_t k = blockIdx.x * BLOCK + threadIdx.x; k < cells; k += gridDim.x * BLOCK) {
+    const uint32_t c = k / rows, r = k - c * rows;
+    uint32_t lo = 0, hi = nseg;   // the last segment whose first packed row is <= r
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (s_off[mid] <= r) lo = mid;
+      else hi = mid;
     }
+    const uint32_t t = s_seg[lo] >> 16, b = s_seg[lo] & 0xFFFFu;
+    small[1 + (uint64_t)k] = cols[c][sp.region[t] + (uint64_t)b * sp.blk_cap[t] + (r - s_off[lo])];
   }
   // (the host reads the block after the wake or the kernel's completion: any workgroup may mark it)
   if (blockIdx.x == 0 && threadIdx.x == 0) small[0] = (int64_t)total + 1;

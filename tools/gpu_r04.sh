@@ -60,6 +60,16 @@ for step in "$@"; do
     goprev)   # GO leg: this build vs nebula_amd/libnbg_prev.so (the previous commit's)
       timeout -k 10 700 bash tools/go_ab.sh "$TAG/goprev" nebula_amd/libnbg.so nebula_amd/libnbg_prev.so \
         > "$OUT/goprev.txt" 2>&1 || { tail -30 "$OUT/goprev.txt"; exit 1; } ;;
+    smallab)   # the small legs: this build vs nebula_amd/libnbg_prev.so, two rounds
+      for round in 1 2; do
+        for lib in libnbg libnbg_prev; do
+          NBG_LIB=$PWD/nebula_amd/$lib.so NBG_GN_TRACE=1 timeout -k 10 400 python -u bench.py --scale 16 --roots 4 --steps 1 \
+            --warmup 1 --sp-pairs 0 --c2 0 --c5-scale 0 --c1-reqs 3000 --getbound-reqs 2000 --verify 0 --no-profile \
+            --no-cpu-baseline > "$OUT/small_${lib}_r$round.json" 2> "$OUT/small_${lib}_r$round.log" \
+            || { tail -30 "$OUT/small_${lib}_r$round.log"; exit 1; }
+          python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); g=d['getbound']; c=d['c1_nba']; print(sys.argv[2], 'getBound p50', round(g['p50_ms'],4), 'p90', round(g['p90_ms'],4), 'C1 p50', round(c['p50_ms'],4), 'C ABI', round(c['c_abi_p50_ms'],4))" "$OUT/small_${lib}_r$round.json" "$lib" | tee -a "$OUT/smallab.txt"
+        done
+      done ;;
     ptest)
       timeout -k 10 400 python -u -m pytest tests/test_gpu_path.py tests/test_gpu_configs.py -x -v --timeout 300 \
         --timeout-method thread > "$OUT/pytest_path.log" 2>&1 || { tail -40 "$OUT/pytest_path.log"; exit 1; } ;;
