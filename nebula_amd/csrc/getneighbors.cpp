@@ -20,6 +20,8 @@
 #include <cstring>
 #include <unordered_map>
 
+#include <omp.h>
+
 #include "engine.h"
 
 using namespace nbg;
@@ -705,7 +707,11 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
     std::vector<nbg_gn_response::Vertex> outv((size_t)nq);
     std::vector<uint64_t> ne((size_t)nq, 0);
     std::vector<uint8_t> keep((size_t)nq, 0);
-#pragma omp parallel for schedule(dynamic, 16) if (nq >= 64)
+    // A team of 4 (NBG_GN_THREADS; 0: the OpenMP default): a QueryBoundBenchmark request's encode
+    // took 28-31 us with 4 threads against 50-56 with the box's 16 and 41-42 with 8, where waking
+    // and joining the larger team cost more than its share of the work (profiles/r04_af_gn_team_ab.txt)
+    static const int team = getenv("NBG_GN_THREADS") ? std::max(0, atoi(getenv("NBG_GN_THREADS"))) : 4;
+#pragma omp parallel for schedule(dynamic, 16) if (nq >= 64) num_threads(team > 0 ? team : omp_get_max_threads())
     for (int64_t k = 0; k < nq; ++k) keep[(size_t)k] = vertex(order[(size_t)k], outv[(size_t)k], ne[(size_t)k]) ? 1 : 0;
     resp->vertices.reserve((size_t)nq);
     for (int64_t k = 0; k < nq; ++k) {

@@ -70,6 +70,17 @@ for step in "$@"; do
           python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); g=d['getbound']; c=d['c1_nba']; print(sys.argv[2], 'getBound p50', round(g['p50_ms'],4), 'p90', round(g['p90_ms'],4), 'C1 p50', round(c['p50_ms'],4), 'C ABI', round(c['c_abi_p50_ms'],4))" "$OUT/small_${lib}_r$round.json" "$lib" | tee -a "$OUT/smallab.txt"
         done
       done ;;
+    gnteam)   # getBound: the encoding team size (NBG_GN_THREADS), two rounds
+      for round in 1 2; do
+        for tm in 0 2 4 8; do
+          NBG_GN_THREADS=$tm NBG_GN_TRACE=1 timeout -k 10 400 python -u bench.py --scale 16 --roots 4 --steps 1 \
+            --warmup 1 --sp-pairs 0 --c2 0 --c5-scale 0 --c1-reqs 0 --getbound-reqs 2000 --verify 0 --no-profile \
+            --no-cpu-baseline > "$OUT/gn_t${tm}_r$round.json" 2> "$OUT/gn_t${tm}_r$round.log" \
+            || { tail -30 "$OUT/gn_t${tm}_r$round.log"; exit 1; }
+          python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); g=d['getbound']; print('threads', sys.argv[2], 'getBound p50', round(g['p50_ms'],4), 'p90', round(g['p90_ms'],4))" "$OUT/gn_t${tm}_r$round.json" "$tm" | tee -a "$OUT/gnteam.txt"
+          grep 'gn trace' "$OUT/gn_t${tm}_r$round.log" | tail -1 | tee -a "$OUT/gnteam.txt"
+        done
+      done ;;
     ptest)
       timeout -k 10 400 python -u -m pytest tests/test_gpu_path.py tests/test_gpu_configs.py -x -v --timeout 300 \
         --timeout-method thread > "$OUT/pytest_path.log" 2>&1 || { tail -40 "$OUT/pytest_path.log"; exit 1; } ;;
