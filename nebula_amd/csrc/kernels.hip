@@ -3030,8 +3030,9 @@ __global__ void __launch_bounds__(BLOCK) k_q_out(const unsigned long long* __res
   wake_host(wk);
 }
 
-static bool wake_by_flag() {
-  static const bool on = !(getenv("NBG_WAKE") && strcmp(getenv("NBG_WAKE"), "event") == 0);
+static bool wake_by_flag() {   // (NBG_BLOCKING_SYNC: blocking waits, no polling)
+  static const bool on = !(getenv("NBG_WAKE") && strcmp(getenv("NBG_WAKE"), "event") == 0) &&
+                         getenv("NBG_BLOCKING_SYNC") == nullptr;
   return on;
 }
 

@@ -126,12 +126,18 @@ static bool wake_by_flag() {
   return on;
 }
 
+static bool blocking_sync() {   // NBG_BLOCKING_SYNC: the waits block instead of polling
+  static const bool on = getenv("NBG_BLOCKING_SYNC") != nullptr;
+  return on;
+}
+
 bool sp_ready(SpCtx* c) { return (wake_by_flag() && chain_woken(c->chain)) || hipEventQuery(c->done) == hipSuccess; }
 
 // The batch's end: its last launch's wake word (the result is readable before the launch has
 // retired and the event behind it is signalled), or the event — a batch that ended inside the
 // search stores nothing, and a failed launch ends the wait with its error.
 static hipError_t wait_batch(SpCtx* c) {
+  if (blocking_sync()) return hipEventSynchronize(c->done);
   const bool flag = wake_by_flag();
   for (unsigned k = 1;; ++k) {
     if (flag && chain_woken(c->chain)) {

@@ -3,7 +3,7 @@ synchronous GO query, getNeighbors and a SHORTEST chain end with the end kernel 
 number into a mapped word the host polls; NBG_WAKE=event restores the wait on the event behind
 the end kernel.  Both must return the same results: the same queries run here (the mapped word)
 and in a child process with NBG_WAKE=event (the setting is read once per process), and on the
-wake-word side also against the CPU oracle."""
+wake-word side also against the CPU oracle; NBG_BLOCKING_SYNC=1 (blocking waits) likewise."""
 import json
 import os
 import subprocess
@@ -63,7 +63,9 @@ def _child():
         eng.close()
 
 
-def test_event_wait_matches_wake_word():
+@pytest.mark.parametrize("var,val", [("NBG_WAKE", "event"), ("NBG_BLOCKING_SYNC", "1")])
+def test_event_wait_matches_wake_word(var, val):
+    """The child waits on events (polled, or blocking with NBG_BLOCKING_SYNC)."""
     src, dst, w = graphs.rmat_graph(12)
     eng = graphs.rmat_engine(src, dst, w)
     orc = graphs.rmat_oracle(src, dst, w)
@@ -72,7 +74,7 @@ def test_event_wait_matches_wake_word():
     finally:
         eng.close()
         orc.close()
-    env = dict(os.environ, NBG_WAKE="event")
+    env = dict(os.environ, **{var: val})
     p = subprocess.run([sys.executable, "-c", "from tests.test_gpu_wake import _child; _child()"], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stderr[-2000:]
