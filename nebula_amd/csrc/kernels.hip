@@ -140,6 +140,7 @@ struct Workspace {
   unsigned long long wake_seq = 0;
   bool wake_armed = false;            // the enqueued end kernel will store wake_seq
   bool wake_flag = true;              // ws_set_wake: the next end kernel may arm it
+  bool q_reset = false;               // the enqueued end kernel zeroes QState behind its copy
   uint32_t* h_starts = nullptr;   // pinned staging for start ids
   uint64_t cap_starts = 0;
   Ins* h_prog = nullptr;          // pinned staging for programs
@@ -3024,9 +3025,14 @@ __device__ void wake_host(const Wake& wk) {
   __hip_atomic_store(wk.word, wk.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ void __launch_bounds__(BLOCK) k_q_out(const unsigned long long* __restrict__ src, unsigned long long* dst,
-                                                 uint32_t n8, Wake wk) {
-  for (uint32_t i = threadIdx.x; i < n8; i += BLOCK) dst[i] = src[i];
+// (the QState words, the first nq8, are zeroed behind the copy for the next query: no host
+// memset call after the wait)
+__global__ void __launch_bounds__(BLOCK) k_q_out(unsigned long long* __restrict__ src, unsigned long long* dst,
+                                                 uint32_t n8, uint32_t nq8, Wake wk) {
+  for (uint32_t i = threadIdx.x; i < n8; i += BLOCK) {
+    dst[i] = src[i];
+    if (i < nq8) src[i] = 0;
+  }
   wake_host(wk);
 }
 
@@ -3070,8 +3076,10 @@ hipError_t ws_end_query_async(Workspace* w) {
   static_assert(sizeof(QState) % 8 == 0 && EXPAND_GRID % 2 == 0, "k_q_out copies 8-byte words");
   const size_t bytes = sizeof(QState) + (size_t)nt * EXPAND_GRID * 4;
   const Wake wk = arm_wake(w);
-  hipLaunchKernelGGL(k_q_out, dim3(1), dim3(BLOCK), 0, w->stream, reinterpret_cast<const unsigned long long*>(w->q),
-                     reinterpret_cast<unsigned long long*>(w->d_hq), (uint32_t)(bytes / 8), wk);
+  hipLaunchKernelGGL(k_q_out, dim3(1), dim3(BLOCK), 0, w->stream, reinterpret_cast<unsigned long long*>(w->q),
+                     reinterpret_cast<unsigned long long*>(w->d_hq), (uint32_t)(bytes / 8),
+                     (uint32_t)(sizeof(QState) / 8), wk);
+  w->q_reset = true;
   HIP_TRY(hipGetLastError());
   if (w->h_small) w->h_small[0] = 0;   // (this query's rows are not packed: the device does not run
                                        // ahead of this host write, the stream is idle on this slot)
@@ -3094,8 +3102,9 @@ hipError_t ws_end_query_wait(Workspace* w) {
     }
     HIP_TRY(e);
   }
-  // reset for the next query; runs while the host reads the results
-  HIP_TRY(hipMemsetAsync(w->q, 0, sizeof(QState), w->stream));
+  // reset for the next query (done by the end kernel itself, unless this query had none)
+  if (!w->q_reset) HIP_TRY(hipMemsetAsync(w->q, 0, sizeof(QState), w->stream));
+  w->q_reset = false;
   prof_flush(w, w->h_q);
   return hipSuccess;
 }
@@ -3108,12 +3117,17 @@ hipError_t ws_end_query_wait(Workspace* w) {
 // than SMALL_SEGS non-empty segments is left to the host fetch like a large one.
 constexpr int SMALL_SEGS = 2048;
 constexpr int SMALL_WGS = 16;
-__global__ void __launch_bounds__(BLOCK) k_q_out_small(const unsigned long long* __restrict__ src, unsigned long long* dst,
-                                                       uint32_t n8, const uint32_t* __restrict__ blk_rows, SmallPack sp,
+__global__ void __launch_bounds__(BLOCK) k_q_out_small(unsigned long long* __restrict__ src, unsigned long long* dst,
+                                                       uint32_t n8, uint32_t nq8, const uint32_t* __restrict__ blk_rows, SmallPack sp,
                                                        int64_t* const* __restrict__ cols, int64_t* small, Wake wk) {
   // (every workgroup lists the segments; workgroup b copies segments b, b + grid, ... and a share
   // of the state words: more stores over the host link in flight than one workgroup issues)
-  for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n8; i += gridDim.x * BLOCK) dst[i] = src[i];
+  // (the QState words, the first nq8, zeroed behind the copy as in k_q_out; the row counts after
+  // them are read below and rewritten by the next final step)
+  for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n8; i += gridDim.x * BLOCK) {
+    dst[i] = src[i];
+    if (i < nq8) src[i] = 0;
+  }
   __shared__ uint32_t s_seg[SMALL_SEGS];        // t << 16 | b of the non-empty segments, in order
   __shared__ uint32_t s_off[SMALL_SEGS + 1];    // their first row in the packed result
   __shared__ uint32_t s_lds[WAVES];
@@ -3193,9 +3207,10 @@ hipError_t ws_end_query_async_small(Workspace* w, const SmallPack& sp) {
     if (w->final_grid[t]) nt = t + 1;
   const size_t bytes = sizeof(QState) + (size_t)nt * EXPAND_GRID * 4;
   const Wake wk = arm_wake(w);
-  hipLaunchKernelGGL(k_q_out_small, dim3(SMALL_WGS), dim3(BLOCK), 0, w->stream, reinterpret_cast<const unsigned long long*>(w->q),
-                     reinterpret_cast<unsigned long long*>(w->d_hq), (uint32_t)(bytes / 8), w->blk_rows, sp,
-                     (int64_t* const*)w->d_row_cols, w->d_small, wk);
+  hipLaunchKernelGGL(k_q_out_small, dim3(SMALL_WGS), dim3(BLOCK), 0, w->stream, reinterpret_cast<unsigned long long*>(w->q),
+                     reinterpret_cast<unsigned long long*>(w->d_hq), (uint32_t)(bytes / 8),
+                     (uint32_t)(sizeof(QState) / 8), w->blk_rows, sp, (int64_t* const*)w->d_row_cols, w->d_small, wk);
+  w->q_reset = true;
   HIP_TRY(hipGetLastError());
   if (!w->done_ev) HIP_TRY(hipEventCreateWithFlags(&w->done_ev, hipEventDisableTiming));
   return hipEventRecord(w->done_ev, w->stream);
