@@ -81,6 +81,9 @@ for step in "$@"; do
           grep 'gn trace' "$OUT/gn_t${tm}_r$round.log" | tail -1 | tee -a "$OUT/gnteam.txt"
         done
       done ;;
+    spprev)   # SHORTEST: this build vs nebula_amd/libnbg_prev.so
+      timeout -k 10 1000 bash tools/sp_ab.sh "$TAG/spprev" nebula_amd/libnbg.so nebula_amd/libnbg_prev.so \
+        > "$OUT/spprev.txt" 2>&1 || { tail -30 "$OUT/spprev.txt"; exit 1; } ;;
     ptest)
       timeout -k 10 400 python -u -m pytest tests/test_gpu_path.py tests/test_gpu_configs.py -x -v --timeout 300 \
         --timeout-method thread > "$OUT/pytest_path.log" 2>&1 || { tail -40 "$OUT/pytest_path.log"; exit 1; } ;;
