@@ -34,6 +34,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+T_START = time.time()
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 METRIC = "GO 3 STEPS traversed edges/sec (TEPS) at 1/2/4/8 GPU; FIND SHORTEST PATH p50"
@@ -268,8 +269,23 @@ def host_delivered(stmt, roots):
     return out
 
 
-def shortest_path_leg(eng, pairs, args, barrier, batch=True):
-    """FIND SHORTEST PATH FROM s TO t OVER e UPTO n STEPS, one query per pair (C4)."""
+class Progress:
+    """A log line every `every` seconds of a long loop (runs are watched for silence)."""
+
+    def __init__(self, what, n, every=20.0):
+        self.what, self.n, self.every = what, n, every
+        self.t0 = self.last = time.perf_counter()
+
+    def __call__(self, i):
+        now = time.perf_counter()
+        if now - self.last >= self.every:
+            self.last = now
+            log(f"{self.what}: {i}/{self.n} after {now - self.t0:.0f}s")
+
+
+def shortest_path_leg(eng, pairs, args, barrier, batch=True, light=False):
+    """FIND SHORTEST PATH FROM s TO t OVER e UPTO n STEPS, one query per pair (C4).  light: the
+    latency pass only (a partitioned engine without a replica, where every pair is collective)."""
     if not args.sync:   # shortest-path contexts allocated now (start-up), not inside the first timed query
         eng.path_reserve(int(os.environ.get("NBG_QUERY_SLOTS", "6")), int(os.environ.get("NBG_SP_BATCH", "32")))
     for s, t in pairs[:16]:   # warm-up
@@ -282,8 +298,10 @@ def shortest_path_leg(eng, pairs, args, barrier, batch=True):
     out = C.c_void_p()
     barrier()
     lat, edges, found, hops = [], 0, 0, 0
+    tick = Progress("SP latency pass", nreq)
     t0 = time.perf_counter()
     for i in range(nreq):
+        tick(i)
         q0 = time.perf_counter()
         rc = lib.nbg_find_path(h, C.byref(arr[i]), C.byref(out))
         lat.append(time.perf_counter() - q0)
@@ -298,8 +316,9 @@ def shortest_path_leg(eng, pairs, args, barrier, batch=True):
     elapsed = time.perf_counter() - t0
     # throughput pass: the same pairs with queries in flight on the query slots
     # (nbg_find_path_submit / _wait; on a partitioned engine each query still runs collectively)
-    inflight = 0 if args.sync else int(os.environ.get("NBG_QUERY_SLOTS", "6"))
+    inflight = 0 if args.sync or light else int(os.environ.get("NBG_QUERY_SLOTS", "6"))
     conc = None
+    log(f"SP latency pass done ({nreq} pairs, {elapsed:.1f}s)")
     if inflight:
         barrier()
         c0 = time.perf_counter()
@@ -348,7 +367,7 @@ def shortest_path_leg(eng, pairs, args, barrier, batch=True):
                    "timing": f"nbg_find_path_batch over the same pairs, {chunk} requests per call (request "
                              f"arrays built before the clock; results left in their nbg_paths)"}
     kst, kall, prof_pairs, all_pairs = {}, {}, 0, 0
-    if not args.no_profile:
+    if not args.no_profile and not light:
         # roofline pass: HIP events around every step launch of the one-pair chains (k_ch_step; the
         # host-driven loop's k_expand<BFS> on a partitioned engine), with each pair's algorithmic
         # bytes (B_SP) from its device counters; then every launch of the chain
@@ -423,10 +442,24 @@ def load_engine(scale, args, world, rank, local, comm_init):
     eng.register_edge(1, "e", [("w", 2)])
     t0 = time.time()
     eng.load_edges(1, src, dst, [w])
-    eng.finalize()
+    t1 = time.time()
+    eng.finalize()   # (partitioned: dictionary all-gather, device build, FIND PATH replica)
     load_s = time.time() - t0
-    log(f"[rank {rank}] RMAT-{scale}: {len(src)} samples, snapshot {eng.stats()}, gen {gen_s:.1f}s load {load_s:.1f}s")
-    return src, dst, w, eng, gen_s, load_s
+    ready = {"gen_s": round(gen_s, 2), "stage_s": round(t1 - t0, 2), "finalize_s": round(time.time() - t1, 2),
+             "ready_s": round(time.time() - T_START, 2)}
+    log(f"[rank {rank}] RMAT-{scale}: {len(src)} samples, snapshot {eng.stats()}, gen {gen_s:.1f}s load {load_s:.1f}s "
+        f"(ready {ready})")
+    return src, dst, w, eng, gen_s, load_s, ready
+
+
+def rank_resources(eng, ready):
+    """This process's time-to-ready phases, peak host RSS, host CPU seconds and device bytes."""
+    import resource
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    st = eng.stats()
+    return dict(ready, peak_rss_gb=round(ru.ru_maxrss / 2**20, 2), host_cpu_s=round(ru.ru_utime + ru.ru_stime, 1),
+                wall_s=round(time.time() - T_START, 1), snapshot_gb=round(st["device_bytes"] / 2**30, 2),
+                replica=bool(eng.path_replica_active))
 
 
 # ------------------------------------------------------------------------------------ main
@@ -446,6 +479,9 @@ def main():
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--sp-pairs", type=int, default=10000, help="FIND SHORTEST PATH pairs (0 = skip)")
     ap.add_argument("--sp-upto", type=int, default=5)
+    ap.add_argument("--sp-coll-pairs", type=int, default=500,
+                    help="pairs of the collective search on a partitioned engine (the whole SHORTEST "
+                         "leg without a replica; a comparison sample beside the replica)")
     ap.add_argument("--sync", action="store_true", help="one query at a time (no query slots)")
     ap.add_argument("--c2", type=int, default=1, help="C2 leg (RMAT-22, 64 roots) when the headline is larger")
     ap.add_argument("--c5-scale", type=int, default=20,
@@ -497,7 +533,7 @@ def main():
     model, threads, ncpu = cpu_info()
 
     # ---------------- headline: GO 3 STEPS on RMAT-scale (C3 at N GPUs), FIND SHORTEST PATH (C4)
-    src, dst, w, eng, gen_s, load_s = load_engine(args.scale, args, world, rank, local, comm_init)
+    src, dst, w, eng, gen_s, load_s, ready = load_engine(args.scale, args, world, rank, local, comm_init)
     st = eng.stats()
     src_verts, all_verts = rmat.vertex_sets(args.scale)
     roots = [int(x) for x in rmat.pick_roots(src, args.roots, 42, verts=src_verts)]
@@ -551,10 +587,12 @@ def main():
                     sp[key]["seconds"] = round(max(secs), 3)
                     sp[key].pop("teps", None)
         eng.set_path_replica(0)
-        coll = pairs[:min(len(pairs), 500)]
+        coll = pairs[:min(len(pairs), args.sp_coll_pairs)]
         barrier()
         clat = []
-        for s_, t_ in coll:
+        tick = Progress("SP collective sample", len(coll))
+        for i_, (s_, t_) in enumerate(coll):
+            tick(i_)
             q0 = time.perf_counter()
             eng.find_path([s_], [t_], [1], args.sp_upto)
             clat.append(time.perf_counter() - q0)
@@ -567,11 +605,21 @@ def main():
                                 "timing": "the same pairs through the collective search over the partitioned "
                                           "snapshot (nbg_set_path_replica(e, 0)), every rank calling together"}
     elif pairs:
-        sp = shortest_path_leg(eng, pairs, args, barrier, batch=world == 1)
+        # without a replica a partitioned engine answers every pair collectively (a collective per
+        # level): a bounded sample keeps the run's length bounded
+        sp_pairs = pairs if world == 1 else pairs[:args.sp_coll_pairs]
+        sp = shortest_path_leg(eng, sp_pairs, args, barrier, batch=world == 1, light=world > 1)
         sp.pop("_raw", None)
+        if world > 1:
+            sp["mode"] = f"collective search over {world} ranks (no replica), first {len(sp_pairs)} pairs"
     sp_sample = []
     if pairs and args.verify:   # device paths for the verification sample
         sp_sample = [eng.find_path([s], [t], [1], args.sp_upto) for s, t in pairs[:64]]
+    res_mine = rank_resources(eng, ready)
+    ranks_res = [res_mine]
+    if dist is not None:
+        ranks_res = [None] * world
+        dist.all_gather_object(ranks_res, res_mine)
     eng.close()
 
     tot_scanned, max_elapsed, tot_rows = float(g["scanned"]), g["elapsed"], float(g["rows"])
@@ -702,8 +750,24 @@ def main():
         "partitioned_fixed_costs": fixed,
         "gen_seconds": round(gen_s, 2),
         "load_seconds": round(load_s, 2),
+        "ranks": ranks_res,
     }
+    # the metric's second half (FIND SHORTEST PATH p50) as top-level keys at the END of the line,
+    # so a reader that keeps only the line's tail (or its top-level keys) still sees it
+    if sp:
+        sroof = sp.get("roofline") or {}
+        out.update({"sp_pairs": sp.get("pairs"), "sp_p50_ms": sp.get("p50_ms"), "sp_p90_ms": sp.get("p90_ms"),
+                    "sp_p99_ms": sp.get("p99_ms"),
+                    "sp_batched_pairs_per_s": (sp.get("batched") or {}).get("pairs_per_s"),
+                    "sp_roofline_frac": sroof.get("frac")})
     print(json.dumps(out), flush=True)
+    if rank == 0:   # a one-line summary as the run's last stderr line (log tails end with it)
+        print("SUMMARY " + json.dumps({"go_teps": out["value"], "ms_per_step": out["ms_per_step"],
+                                       "final_roofline_frac": (roofline or {}).get("frac"),
+                                       **{k: out.get(k) for k in ("sp_p50_ms", "sp_p90_ms", "sp_p99_ms",
+                                                                  "sp_batched_pairs_per_s", "sp_roofline_frac")},
+                                       "verify_go": (verify or {}).get("go_match"),
+                                       "verify_sp": (verify or {}).get("sp_match")}), file=sys.stderr, flush=True)
     if dist is not None:
         dist.barrier()
 
@@ -712,7 +776,7 @@ def c2_leg(args, barrier, inflight):
     """RMAT-22 on one GPU, 64 roots, the same GO 3 STEPS query; FIND SHORTEST
     PATH over 10k pairs on the same graph."""
     from nebula_amd import expr as E, rmat
-    src, dst, w, eng, gen_s, load_s = load_engine(22, args, 1, 0, 0, None)
+    src, dst, w, eng, gen_s, load_s, _ = load_engine(22, args, 1, 0, 0, None)
     sv, av = rmat.vertex_sets(22)
     roots = [int(x) for x in rmat.pick_roots(src, 64, 42, verts=sv)]
     where = E.binop("<", E.edge_prop("e", "w"), E.const(50)).encode()

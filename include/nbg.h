@@ -146,10 +146,27 @@ typedef struct {
   uint64_t host_agreements;   /* partitioned GO queries that agreed on rank-local statuses on the
                                  host before their first collective ($- / $var inputs); the others
                                  carry them in band                                              */
+  uint64_t host_bytes;        /* host memory the finalized engine keeps beside its snapshot (row
+                                 offsets, dictionary, the tiny path's walk bounds)               */
 } nbg_stats;
 int32_t nbg_get_stats(const nbg_engine* e, nbg_stats* out);
 
 /* ---- GO N STEPS (GoExecutor semantics) ------------------------------------------------- */
+/* Expression wire (WHERE / YIELD bytes here and the storage filter of nbg_gn_request): the bytes
+ * of Expression::encode (src/common/filter/Expressions.cpp:93-98 and each class's encode), with
+ * ONE extension.  The reference's TypeCastingExpression::encode writes nothing
+ * (Expressions.cpp:801-802) and its decode throws (Expressions.h:830-832), so a cast cannot cross
+ * the reference's own wire.  Here a cast is encoded as
+ *     uint8 kind = 4 (kTypeCasting), uint8 ColumnType (0 INT, 1 STRING, 2 DOUBLE, 3 BIGINT,
+ *     4 BOOL, 5 TIMESTAMP; Expressions.h:21-23), then the operand's own encoding,
+ * which a graphd emits once its TypeCastingExpression::encode writes those three parts
+ * (INTEGRATION.md §2 shows the body).  An UNPATCHED graphd drops the cast and its whole operand
+ * from the bytes: the remaining tree is missing a subtree, so decoding runs out of bytes and
+ * nbg_go fails with NBG_E_INVALID_ARGUMENT (nbg_get_neighbors: E_INVALID_FILTER for every part,
+ * as the reference's processor answers a filter it cannot decode), never with rows.  A
+ * cast at the ROOT of a WHERE encodes to zero bytes, which means "no WHERE" (where_len = 0): the
+ * binding must reject a non-null filter_ whose encoding is empty.  Any other
+ * ColumnType byte, or bytes left over after the tree, is NBG_E_INVALID_ARGUMENT. */
 typedef struct {
   const int64_t* starts;          /* FROM vids; duplicates are kept (GoExecutor.cpp:136-195)  */
   uint64_t num_starts;

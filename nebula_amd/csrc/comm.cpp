@@ -53,11 +53,25 @@ bool Comm::agree_ready(std::string* err) {
   return true;
 }
 
+// Host polling budget of a collective wait: spin on the stream for NBG_COMM_SPIN_US (default
+// 200 us: a hop's all-to-all over xGMI completes well inside it), then yield the core between
+// polls up to 2 ms, then sleep 50 us between polls.  Eight ranks share a node's host cores with
+// their RCCL proxy threads; a long spin on every rank's slot streams starves those threads.
+static double comm_spin_s() {
+  static const double v = [] {
+    const char* e = getenv("NBG_COMM_SPIN_US");
+    const double us = e ? atof(e) : 200.0;
+    return (us >= 0 ? us : 200.0) * 1e-6;
+  }();
+  return v;
+}
+
 int Comm::wait(hipStream_t s) {
   // poll: a query's latency ends here (a blocking wait would add the wake-up latency), with a
   // bound so that a peer that never arrives cannot hold this rank forever
   const auto t0 = std::chrono::steady_clock::now();
   const double limit = comm_timeout_s();
+  const double spin_s = comm_spin_s();
   for (uint64_t spin = 0;; ++spin) {
     const hipError_t e = hipStreamQuery(s);
     if (e == hipSuccess) return 0;
@@ -66,15 +80,14 @@ int Comm::wait(hipStream_t s) {
       abort();
       return -1;
     }
-    if ((spin & 1023) == 0) {
-      const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-      if (el > limit) {
-        last = "collective timed out after " + std::to_string((int)limit) + " s (a peer rank failed or never arrived)";
-        abort();
-        return -1;
-      }
-      if (el > 0.01) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (el > limit) {
+      last = "collective timed out after " + std::to_string((int)limit) + " s (a peer rank failed or never arrived)";
+      abort();
+      return -1;
     }
+    if (el > 0.002 && el > spin_s) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    else if (el > spin_s) std::this_thread::yield();
   }
 }
 

@@ -473,6 +473,7 @@ struct nbg_go_stmt {
   // $- / $var input: index rows (the FROM vid, ascending; last row per vid) and their columns,
   // uploaded on first execution (the same index on every rank of a partitioned engine)
   bool derived = false;              // some YIELD stores derived strings (OP_SOUT: the string arena)
+  uint64_t sout_row_bytes = 0;       // arena bytes one final edge may store (the largest type's bound)
   uint64_t arena_bytes = 0;          // the arena a query reserves
   bool uses_input = false;
   std::vector<int64_t> in_ids;
@@ -631,11 +632,17 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
   std::map<std::string, std::set<std::string>> named;
   alias_props(where.get(), named);
   for (auto& y : yields) alias_props(y.get(), named);
+  if (E.max_dict_len_of != E.snap.strings.size()) {   // (cached: the dictionary is fixed after finalize)
+    E.max_dict_len = 0;
+    for (const std::string& x : E.snap.strings) E.max_dict_len = std::max<uint64_t>(E.max_dict_len, x.size());
+    E.max_dict_len_of = E.snap.strings.size();
+  }
   for (int32_t t : over) {
     auto it = E.snap.types.find(t);
     CompileEnv env{t, &over, &E.edges, &E.snap.strings,
                    it != E.snap.types.end() && it->second.valid != nullptr,
                    it != E.snap.types.end() && it->second.rank != nullptr};
+    env.max_dict_len = E.max_dict_len;
     // the response edge row schema of type t: _dst, then the props named on t (getStepOutProps,
     // GoExecutor.cpp:587-630)
     std::map<std::string, VKind> row_cols{{"_dst", VK_INT}};
@@ -714,6 +721,7 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
     tp.code = pb.code;
     tp.data = pb.data;
     for (const Ins& i : tp.code) tp.sout = tp.sout || i.op == OP_SOUT;
+    tp.sout_bytes = pb.sout_bytes;
     tp.probe_mask = probe;
     tp.nregs = std::max(1, pb.max_reg);
     if ((int)(tp.code.size() + tp.data.size()) > MAX_PROGRAM) return E.fail(NBG_E_UNSUPPORTED, "program too long");
@@ -785,7 +793,11 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
   // whatever produced it — the dictionary's, else STR_DERIVED | its content hash — so constant
   // strings absent from the dictionary take the hash code too (YIELD DISTINCT compares codes).
   bool derived = false;
-  for (auto& kv : progs) derived = derived || kv.second.sout;
+  uint64_t sout_row = 0;
+  for (auto& kv : progs) {
+    derived = derived || kv.second.sout;
+    sout_row = std::max(sout_row, kv.second.sout_bytes);
+  }
   if (derived)
     for (auto& kv : progs)
       for (int y = 0; y < ncols; ++y) {
@@ -798,6 +810,7 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
   static std::atomic<uint64_t> next_id{1};
   auto* st = new nbg_go_stmt();
   st->derived = derived;
+  st->sout_row_bytes = sout_row;
   st->eng = &E;
   st->id = next_id++;
   st->over = over;
@@ -1024,12 +1037,16 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
   }
   if (!lrc && ws_reserve_rows(ws, cap_rows, ncols) != hipSuccess) local_fail(NBG_E_OUT_OF_MEMORY, "result rows");
   if (!lrc && st->derived) {
-    // derived strings: 32 bytes per row and column (an entry's 16-byte header + 16 bytes) up to
-    // NBG_STR_ARENA_KB (default 2 GB); a query that needs more fails with E_OUT_OF_MEMORY
+    // derived strings: every final edge's OP_SOUTs may store up to the program's bound (the
+    // longest text its piece lists can spell, plus each entry's header; ProgramBuilder::sout_bytes)
+    // up to NBG_STR_ARENA_KB (default 2 GB); a query whose strings need more fails with
+    // E_OUT_OF_MEMORY.  The bound covers every row the result can hold, so below the cap the
+    // arena never overflows.
     static const uint64_t cap_kb =
         getenv("NBG_STR_ARENA_KB") ? strtoull(getenv("NBG_STR_ARENA_KB"), nullptr, 10) : (2ull << 20);
-    const uint64_t want = std::min<uint64_t>(std::max<uint64_t>(cap_rows * (uint64_t)ncols * 32, 1ull << 20),
-                                             std::max<uint64_t>(cap_kb, 1) << 10);
+    const uint64_t per_row = std::max<uint64_t>(st->sout_row_bytes, 32);
+    const uint64_t need = cap_rows > UINT64_MAX / per_row ? UINT64_MAX : cap_rows * per_row;
+    const uint64_t want = std::min<uint64_t>(std::max<uint64_t>(need, 1ull << 20), std::max<uint64_t>(cap_kb, 1) << 10);
     if (ws_reserve_arena(ws, want) != hipSuccess) local_fail(NBG_E_OUT_OF_MEMORY, "derived-string arena");
   }
   // ---- agreement: the query runs on every rank or on none.  A statement whose only collectives
@@ -1312,7 +1329,8 @@ static int32_t go_collect(Engine& E, const nbg_go_stmt* st, GoPending* p, nbg_ro
   }
   if (g_err >= ARENA_OVERFLOW) {
     delete rows;
-    return E.fail(NBG_E_OUT_OF_MEMORY, "the derived strings of the result exceed the string arena (NBG_STR_ARENA_KB)");
+    return E.fail(NBG_E_OUT_OF_MEMORY, "the derived strings of the result need " + std::to_string(q.arena_used >> 10) +
+                                       " KB, more than the string arena's cap (NBG_STR_ARENA_KB)");
   }
   if (g_err) { delete rows; return E.fail(NBG_E_EXECUTION_ERROR, "WHERE/YIELD evaluation error"); }
   // a $$ default read for a tag no final destination has: VertexHolder::defaultFor fails
@@ -1385,6 +1403,10 @@ static int32_t go_collect(Engine& E, const nbg_go_stmt* st, GoPending* p, nbg_ro
       }
     }
     if (de != hipSuccess) {
+      // a failure inside the owner exchange (after its first collective) leaves the peers in the
+      // later collectives of this query: abort the communicator, as for any device failure
+      // between collectives, so they fail at once instead of at NBG_COMM_TIMEOUT_S
+      if (E.partitioned()) ws_get_comm(ws)->abort();
       delete rows;
       return E.fail(NBG_E_DEVICE, std::string("HIP (distinct): ") + hipGetErrorString(de));
     }
@@ -1499,7 +1521,8 @@ int32_t nbg::engine_ready(Engine& E) {
     if (hipMalloc((void**)&E.snap.d_zero_rows, zb) != hipSuccess || hipMemset(E.snap.d_zero_rows, 0, zb) != hipSuccess)
       return E.fail(NBG_E_OUT_OF_MEMORY, "empty CSR rows");
   }
-  if (!E.partitioned()) {   // walk bounds of the tiny GO path (a failure only disables it)
+  static const bool tiny_on = !getenv("NBG_TINY") || atoi(getenv("NBG_TINY")) != 0;
+  if (!E.partitioned() && tiny_on) {   // walk bounds of the tiny GO path (a failure only disables it)
     const uint32_t cap = (uint32_t)(E.cfg.max_edge_returned_per_vertex <= 0 ? 0x7fffffff
                                                                             : E.cfg.max_edge_returned_per_vertex);
     for (auto& kv : E.snap.types)
@@ -1752,6 +1775,12 @@ int32_t nbg_get_stats(const nbg_engine* h, nbg_stats* out) {
   out->num_edge_types = (int32_t)E.snap.types.size();
   out->tiny_queries = E.tiny_queries;
   out->host_agreements = E.host_agreements;
+  uint64_t hb = 0;
+  for (const std::string& x : E.snap.strings) hb += x.size() + sizeof(std::string);
+  for (auto& kv : E.snap.types)
+    hb += (kv.second.h_row_ptr.size() + kv.second.h_w2.size() / 2 + kv.second.h_w3.size() / 2) * 4;
+  hb += E.snap.h_visible.size();
+  out->host_bytes = hb;
   return NBG_OK;
 }
 

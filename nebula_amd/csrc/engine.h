@@ -52,6 +52,8 @@ struct Engine {
   // launch chain, on workspaces sharing one stream
   std::vector<SpCtx*> batch_sp;
   hipStream_t batch_stream = nullptr;
+  uint64_t max_dict_len = 0;            // the longest dictionary string (derived-string arena bound),
+  uint64_t max_dict_len_of = ~0ull;     //   computed for a dictionary of this many strings
   uint64_t row_reserve = 0;             // result rows of the largest prepared GO statement (new
   int col_reserve = 0;                  // query workspaces are sized for it before their first query)
   int prof_mode = 0;

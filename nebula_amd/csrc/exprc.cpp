@@ -52,6 +52,9 @@ std::unique_ptr<Node> dec(Rd& r, int depth) {
     }
     case EK_UNARY: case EK_CAST:
       n->op = r.u8();
+      // the cast extension's ColumnType is one of INT, STRING, DOUBLE, BIGINT, BOOL, TIMESTAMP
+      // (Expressions.h:21-23; the wire extension is specified in include/nbg.h)
+      if (k == EK_CAST && n->op > 5) return nullptr;
       n->kids.push_back(dec(r, depth + 1));
       if (!n->kids[0]) return nullptr;
       break;
@@ -388,6 +391,10 @@ struct Ctx {
   }
   // a derived string as a result value: its canonical code (OP_SOUT)
   int value_reg(const Compiled& c) {
+    uint64_t most = 0;   // the longest text the pieces can spell
+    for (const Piece& p : c.pieces)
+      most += p.kind == PC_CONST ? p.text.size() : p.kind == PC_INT ? 20 : p.kind == PC_BOOL ? 5 : env.max_dict_len;
+    pb.sout_bytes += 16 + ((most + 7) & ~7ull);
     const int32_t h = emit_pieces(c.pieces);
     const int r = sink_reg(c.pieces);
     emit(OP_SOUT, r, 0, 0, h);

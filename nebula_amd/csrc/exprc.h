@@ -50,6 +50,7 @@ struct CompileEnv {
   // $-.col / $var.col: the input rows' columns (names, kinds); nullptr: the query has no input
   const std::vector<std::string>* input_names = nullptr;
   const std::vector<VKind>* input_kinds = nullptr;
+  uint64_t max_dict_len = 0;   // the longest dictionary string (bounds a derived string's bytes)
 };
 
 // One piece of a derived string (a STRING value built on the device: concatenation, casts to
@@ -85,6 +86,9 @@ struct ProgramBuilder {
   std::vector<Ins> data;
   int next_reg = 0;
   int max_reg = 0;
+  // arena bytes one evaluation of every OP_SOUT may store (str_store: a 16-byte header plus the
+  // string rounded up to 8), from each piece list's longest possible text
+  uint64_t sout_bytes = 0;
 };
 
 // yield_value: the expression is a YIELD column (a derived string becomes its canonical code,

@@ -2583,6 +2583,13 @@ uint64_t ws_shard_cap(uint64_t n_bound, uint64_t e_bound) {
   return cdiv(tiles, NSHARD) * TILE;
 }
 
+// NBG_FINAL_LEAN=0: the final step of a FINALD-shaped statement runs k_expand<FINALD> instead of
+// final.hip's k_final_dst (A/B)
+static bool lean_final() {
+  static const bool on = !getenv("NBG_FINAL_LEAN") || atoi(getenv("NBG_FINAL_LEAN")) != 0;
+  return on;
+}
+
 hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, uint64_t e_bound, int step, int tix,
                            const TypeProgram& prog, uint64_t region_base, uint64_t blk_cap, const InlineList* il) {
   if (step > MAX_STEPS || tix >= MAX_TYPES_Q) return hipErrorInvalidValue;
@@ -2638,6 +2645,30 @@ hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound,
     else
       hipLaunchKernelGGL((k_expand<FINAL, true>), grid, dim3(BLOCK), lds, w->stream, a, L.acc, l_end, l_rs,
                          w->flags, fp, BfsParams{}, e_st, L.stat_n, *il);
+  } else if (dst_only && lean_final() && fp.fast.dst_yield && a.dst_vid && (!fp.fast.has_where || fp.fast.wcol)) {
+    FinalDstArgs fa{};
+    fa.acc = L.acc;
+    fa.seg_end = l_end;
+    fa.seg_rs = l_rs;
+    fa.tsplit = a.tsplit;
+    fa.dst_vid = a.dst_vid;
+    fa.wcol = fp.fast.wcol;
+    fa.lo = fp.fast.lo;
+    fa.hi = fp.fast.hi;
+    fa.where_neg = fp.fast.where_neg;
+    fa.nyields = fp.nyields;
+    for (int y = 0; y < fp.nyields; ++y) {
+      if (fp.fast.ykind[y] != 0) fa.const_mask |= 1ull << y;
+      fa.yconst[y] = fp.yield_const[y];
+      fa.out[y] = fp.out_cols[y];
+    }
+    fa.region_base = region_base;
+    fa.blk_cap = blk_cap;
+    fa.blk_rows = fp.blk_rows;
+    fa.stat_e = e_st;
+    fa.stat_n = L.stat_n;
+    const bool one = fp.nyields == 1 && fa.const_mask == 0;
+    HIP_TRY(launch_final_dst(fa, fp.fast.has_where ? fp.fast.wbytes : 0, one, grid.x, w->stream));
   } else if (dst_only) {
     hipLaunchKernelGGL(k_expand<FINALD>, grid, dim3(BLOCK), 0, w->stream, a, L.acc, l_end, l_rs, w->flags,
                        fp, BfsParams{}, e_st, L.stat_n, NoInline{});
@@ -3018,8 +3049,11 @@ __device__ void wake_host(const Wake& wk) {
   if (threadIdx.x != 0) return;
   if (gridDim.x > 1) {
     const unsigned got = __hip_atomic_fetch_add(wk.ticket, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    // (no acquire: every workgroup's host stores are complete at system scope before its ticket)
     if (got != gridDim.x - 1) return;
+    // the last workgroup acquires what the others released with their tickets, so its system-scope
+    // release of the wake word below covers every workgroup's host stores (cumulativity); one
+    // acquire per launch, not one per workgroup
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     __hip_atomic_store(wk.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __hip_atomic_store(wk.word, wk.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

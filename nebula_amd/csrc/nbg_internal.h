@@ -259,6 +259,7 @@ struct TypeProgram {
   std::vector<std::string> yield_const_str;   // string constants (may be absent from the dictionary)
   std::vector<Ins> data;           // piece lists and constant bytes of derived strings (after `code`)
   bool sout = false;               // some YIELD stores a derived string (OP_SOUT: the string arena)
+  uint64_t sout_bytes = 0;         // arena bytes one row's OP_SOUTs may store (ProgramBuilder)
   bool needs_error_check = false;  // any op can raise an error
   uint32_t probe_mask = 0;         // tags read through $$: presence probed for every final edge
   bool keep_on_error = false;      // storage filter: an evaluation error keeps the edge (inl:444-448)
@@ -336,6 +337,29 @@ struct ExpandArgs {                // one (step, edge type) expansion
   const int64_t* const* in_cols;   // [col][k] 8-byte payloads of the indexed rows
   DevStrings str;                  // strings beyond dictionary codes (casts, concatenation)
 };
+
+// The lean final step (final.hip) for WHERE `col <cmp> const` (or none) with _dst / constant
+// YIELDs: the final list (packed count, edge offsets, row starts, tile splits), the _dst column,
+// the WHERE column at its stored width, and the rows' destination (as k_expand<FINALD>)
+struct FinalDstArgs {
+  const unsigned long long* acc;
+  const uint32_t* seg_end;
+  const uint32_t* seg_rs;
+  const uint32_t* tsplit;
+  const int64_t* dst_vid;
+  const void* wcol;
+  int64_t lo, hi;                  // pass = (lo <= w && w <= hi) != where_neg
+  int32_t where_neg;
+  int32_t nyields;
+  uint64_t const_mask;             // bit y: YIELD y is the constant yconst[y] (else _dst)
+  int64_t yconst[MAX_YIELDS];
+  int64_t* out[MAX_YIELDS];
+  uint64_t region_base, blk_cap;   // rows of workgroup b at region_base + b * blk_cap
+  uint32_t* blk_rows;
+  unsigned long long* stat_e;
+  unsigned long long* stat_n;
+};
+hipError_t launch_final_dst(const FinalDstArgs& a, int wbytes, bool one, unsigned grid, hipStream_t s);
 
 // ----------------------------------------------------------------------------- FIND PATH state
 // Vertex labels are epoch-stamped so no per-query clearing is needed: label = epoch << LVL_BITS |

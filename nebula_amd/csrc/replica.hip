@@ -218,6 +218,13 @@ uint64_t replica_bytes(const Engine& E, uint64_t n_all, uint64_t e_all_per_type,
   return b + (G + 1) * chunk * (12 + (ranks ? 8 : 0));
 }
 
+// the share of this rank's free HBM the replica may take (NBG_REPLICA_FIT, default 0.8)
+double replica_fit() {
+  const char* v = getenv("NBG_REPLICA_FIT");
+  const double f = v ? atof(v) : 0.8;
+  return f > 0 && f <= 1 ? f : 0.8;
+}
+
 }  // namespace
 
 bool path_replica_wanted(const Engine& E) {
@@ -306,7 +313,8 @@ int32_t build_path_replica(Engine& E) {
   int32_t local = NBG_OK;
   if (!path_replica_wanted(E)) local = NBG_E_UNSUPPORTED;
   else if (e_max >= 0xFFFFFFFFull || n_all >= NO_ROW) local = NBG_E_UNSUPPORTED;
-  else if (replica_bytes(E, n_all, e_max, types.size(), any_rank, CHUNK) > my_share / 10 * 8) local = NBG_E_OUT_OF_MEMORY;
+  else if ((double)replica_bytes(E, n_all, e_max, types.size(), any_rank, CHUNK) > (double)my_share * replica_fit())
+    local = NBG_E_OUT_OF_MEMORY;
   int32_t agreed = NBG_OK;
   if (cm->agree(st, local, &agreed)) return xfail("agreement");
   if (agreed) return NBG_OK;   // no replica on any rank: FIND PATH stays collective

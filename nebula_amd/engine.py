@@ -256,7 +256,7 @@ class Engine:
         self._check(self.lib.nbg_get_stats(self.h, C.byref(s)), "stats")
         return {"num_vertices": s.num_vertices, "num_edges": s.num_edges, "device_bytes": s.device_bytes,
                 "num_edge_types": s.num_edge_types, "tiny_queries": s.tiny_queries,
-                "host_agreements": s.host_agreements}
+                "host_agreements": s.host_agreements, "host_bytes": s.host_bytes}
 
     # ------------------------------------------------------------------ profiling
     def set_path_replica(self, mode: int):
@@ -388,9 +388,11 @@ class Engine:
         self._check(n if n < 0 else 0, "go_default_columns")
         return [int(x) for x in out[:n]]
 
-    def prepare_go(self, etypes, steps=1, where=b"", yields=(), distinct=False, over_all=False) -> "GoStatement":
-        """GoExecutor::prepare() once; ``GoStatement.run*`` executes it from start lists."""
-        req, keep = self._go_request([], etypes, steps, where, yields, distinct, over_all)
+    def prepare_go(self, etypes, steps=1, where=b"", yields=(), distinct=False, over_all=False,
+                   inputs=None) -> "GoStatement":
+        """GoExecutor::prepare() once; ``GoStatement.run*`` executes it from start lists.  ``inputs``:
+        the piped / variable rows of $-.x / $var.x props (indexed once, at prepare)."""
+        req, keep = self._go_request([], etypes, steps, where, yields, distinct, over_all, inputs)
         out = C.c_void_p()
         self._check(self.lib.nbg_go_prepare(self.h, C.byref(req), C.byref(out)), "go_prepare")
         return GoStatement(self, out)

@@ -2,9 +2,11 @@
 
 The C ABI (``include/nbg.h``) takes WHERE / YIELD expressions as the bytes
 ``Expression::encode`` produces (``src/common/filter/Expressions.cpp:93-116`` and the
-per-class ``encode`` methods).  One documented extension: the reference cannot encode a
-``TypeCastingExpression`` (its ``encode`` is empty, Expressions.cpp:801-802), so nebula_amd
-encodes it as ``kind=4, uint8 ColumnType, operand``.
+per-class ``encode`` methods).  One extension, specified in ``include/nbg.h`` ("Expression
+wire"): the reference cannot encode a ``TypeCastingExpression`` (its ``encode`` is empty,
+Expressions.cpp:801-802), so nebula_amd encodes it as ``kind=4, uint8 ColumnType, operand``
+(the graphd-side encoder body is in INTEGRATION.md §2; ``tests/support/wire.py`` produces the
+unpatched bytes).
 
 ``to_string`` follows each class's ``toString`` (used for default YIELD column names).
 """

@@ -52,8 +52,10 @@ std::unique_ptr<Expr> Dec::expr() {
     }
     case kTypeCasting: {
       // TypeCastingExpression::encode is empty in the reference (:801-802) and its decode
-      // throws (Expressions.h:830-832).  nebula_amd wire extension (documented in
-      // DESIGN.md): kind, uint8 ColumnType, operand.
+      // throws (Expressions.h:830-832).  nebula_amd wire extension (specified in include/nbg.h,
+      // "Expression wire"; the graphd-side encoder is in INTEGRATION.md §2): kind, uint8
+      // ColumnType, operand.  Bytes from an unpatched encoder lack the whole cast subtree and
+      // fail below for want of bytes, as the reference's decode does.
       if (!need(2)) return nullptr;
       e->castType = *p++;
       e->a = expr();

@@ -33,3 +33,23 @@ def test_expression_fixture_counts():
         by[c["test"]] = by.get(c["test"], 0) + 1
     assert by["LiteralConstantsRelational"] == 88 and by["LiteralConstantsLogical"] == 44
     assert by["InvalidExpressionTest"] == 17 and by["LiteralConstants"] == 11
+
+
+
+# --------------------------------------------------------------- the cast hole in the wire (r04 item 4)
+def test_unpatched_cast_bytes_fail_to_decode(orc):
+    """An unpatched graphd drops every TypeCastingExpression subtree from the wire
+    (Expressions.cpp:801-802).  The reference's decode then fails (a tree with a subtree missing
+    runs out of bytes); the oracle's decode restates that and rejects every shape, and the patched
+    bytes (nbg.h "Expression wire") evaluate."""
+    from nebula_amd.vidhash import std_hash
+    from tests.support import wire
+    from tests.support.oracle import OracleError
+    tim, like = std_hash("Tim Duncan"), orc.edge_types["like"]
+    for name, where, yields in wire.cast_shapes():
+        wb = wire.reference_encode(where) if where is not None else b""
+        yb = [wire.reference_encode(y) for y in yields]
+        with pytest.raises(OracleError):
+            orc.go([tim], [like], 1, wb, yb)
+        rows = orc.go([tim], [like], 1, where.encode() if where is not None else b"", [y.encode() for y in yields])
+        assert rows, name

@@ -190,6 +190,28 @@ def main():
                 graphs.sorted_rows(single.go([r0], [1], 3, where, yd, distinct=distinct))
             ok &= good
             print(f"after the stream failure (distinct={distinct}): GO {'OK' if good else 'MISMATCH'}", flush=True)
+    # (5b) the same stream failure on a submitted $- statement: such statements agree on the host
+    #      before their first collective (their input index is per rank), so the failing rank's
+    #      status reaches its peers through Comm::agree; the next submission on the slot runs
+    inputs = (["id", "tag"], [[r0, 700]], "id")
+    st6 = eng.prepare_go([1], 3, where, yin, inputs=inputs)
+    if rank == world - 1:
+        eng.lib.nbg_inject_fault(eng.h, L.FAULT_STREAM, 1)
+
+    def submit_wait_input():
+        st6.wait(st6.submit([r0], device=False)).free()
+    agreed("slot stream ($- input)", code_of(submit_wait_input), L.E_DEVICE)
+    res = st6.wait(st6.submit([r0], device=False))
+    mine = res.fetch()
+    res.free()
+    st6.free()
+    parts = [None] * world
+    dist.all_gather_object(parts, mine)
+    if rank == 0:
+        good = graphs.sorted_rows([row for p in parts for row in p]) == \
+            graphs.sorted_rows(single.go([r0], [1], 3, where, yin, inputs=inputs))
+        ok &= good
+        print(f"after the stream failure ($- input): GO {'OK' if good else 'MISMATCH'}", flush=True)
     dist.barrier()
     if rank == 0:
         print("RCCL partitioned probe:", "PASS" if ok else "FAIL", flush=True)
