@@ -13,11 +13,18 @@
 #include <algorithm>
 #include <atomic>
 #include <cstring>
+#include <ctime>
 #include <set>
 #include <iterator>
 #include <unordered_map>
 
 #include "engine.h"
+
+// a fresh seed for each query's rand32 / rand64 stream
+static uint64_t query_rand_seed() {
+  static std::atomic<uint64_t> ctr{(uint64_t)std::chrono::steady_clock::now().time_since_epoch().count() * 0x9e3779b97f4a7c15ull};
+  return ctr.fetch_add(0x9e3779b97f4a7c15ull, std::memory_order_relaxed);
+}
 
 using namespace nbg;
 
@@ -988,8 +995,14 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
     if (!lrc && steps > 1 && ws_backtracker(ws, &bt, &bt_in) != hipSuccess)
       local_fail(NBG_E_OUT_OF_MEMORY, "backtracker");
   }
+  // now() is the query's wall-clock second (WallClock::fastNowInSec); rand32 / rand64 draw from a
+  // stream of the query's own
+  const int64_t query_now = (int64_t)time(nullptr);
+  const uint64_t query_seed = query_rand_seed();
   auto args_for = [&](const DevEdgeType& dt) {
     ExpandArgs a{};
+    a.now_sec = query_now;
+    a.rand_seed = query_seed;
     a.row_ptr = dt.row_ptr;
     a.col = dt.col;
     a.dst_vid = dt.dst_vid;

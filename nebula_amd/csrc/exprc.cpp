@@ -13,6 +13,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <functional>
+#include <strings.h>
 
 namespace nbg {
 
@@ -255,6 +257,145 @@ bool evalLogic(uint8_t op, const CVal& l, const CVal& r, CVal* out) {   // Expre
   bool a = truthy(l), b = truthy(r);
   *out = op == 0 ? (a && b) : op == 1 ? (a || b) : (a != b);
   return true;
+}
+
+// ---- FunctionManager (src/common/filter/FunctionManager.cpp:20-487): the table of functions
+// with their arity bounds (FunctionManager::getInternal rejects other names and arities)
+struct FnDef {
+  const char* name;
+  int lo, hi;
+};
+constexpr FnDef kFns[] = {
+    {"abs", 1, 1},       {"floor", 1, 1},  {"ceil", 1, 1},     {"round", 1, 1},  {"sqrt", 1, 1},
+    {"cbrt", 1, 1},      {"hypot", 2, 2},  {"pow", 2, 2},      {"exp", 1, 1},    {"exp2", 1, 1},
+    {"log", 1, 1},       {"log2", 1, 1},   {"log10", 1, 1},    {"sin", 1, 1},    {"asin", 1, 1},
+    {"cos", 1, 1},       {"acos", 1, 1},   {"tan", 1, 1},      {"atan", 1, 1},   {"rand32", 0, 2},
+    {"rand64", 0, 2},    {"now", 0, 0},    {"strcasecmp", 2, 2}, {"lower", 1, 1}, {"upper", 1, 1},
+    {"length", 1, 1},    {"trim", 1, 1},   {"ltrim", 1, 1},    {"rtrim", 1, 1},  {"left", 2, 2},
+    {"right", 2, 2},     {"lpad", 3, 3},   {"rpad", 3, 3},     {"substr", 3, 3}, {"hash", 1, 1},
+    {"udf_is_in", 2, 1 << 30}};
+
+const FnDef* fn_def(const std::string& f) {
+  for (const FnDef& d : kFns)
+    if (f == d.name) return &d;
+  return nullptr;
+}
+
+// the one-argument double functions beyond abs / floor / ceil / round / sqrt, in OP_MATH1_F's order
+constexpr const char* kMath1[] = {"cbrt", "exp", "exp2", "log", "log2", "log10", "sin", "asin", "cos", "acos",
+                                  "tan", "atan"};
+int math1_id(const std::string& f) {
+  for (int i = 0; i < (int)(sizeof(kMath1) / sizeof(kMath1[0])); ++i)
+    if (f == kMath1[i]) return i;
+  return -1;
+}
+double math1(int id, double x) {
+  switch (id) {
+    case 0: return std::cbrt(x);
+    case 1: return std::exp(x);
+    case 2: return std::exp2(x);
+    case 3: return std::log(x);
+    case 4: return std::log2(x);
+    case 5: return std::log10(x);
+    case 6: return std::sin(x);
+    case 7: return std::asin(x);
+    case 8: return std::cos(x);
+    case 9: return std::acos(x);
+    case 10: return std::tan(x);
+    default: return std::atan(x);
+  }
+}
+
+// Expression::asDouble / asInt / asString (Expressions.h:217-246): boost::get, so an argument of
+// another kind throws (bad_get) — an evaluation error here
+bool as_double(const CVal& v, double* d) {
+  if (v.index() == 0) { *d = (double)std::get<0>(v); return true; }
+  if (v.index() == 1) { *d = std::get<1>(v); return true; }
+  return false;
+}
+
+// A function body of FunctionManager.cpp over constant arguments, as the reference runs it (on
+// the host the compiler's own std::hash is libstdc++'s, as the reference's).  false: the body
+// throws (an argument of another kind), or would not return (lpad / rpad with a negative size or,
+// padding, an empty pad: their loop never ends) — an evaluation error here.  rand32 / rand64 /
+// now are never folded (a value per evaluation / per query).
+bool fm_eval(const std::string& f, const std::vector<CVal>& a, CVal* out) {
+  double x = 0, y = 0;
+  if (f == "abs" || f == "floor" || f == "ceil" || f == "round" || f == "sqrt" || math1_id(f) >= 0) {
+    if (!as_double(a[0], &x)) return false;
+    *out = f == "abs" ? std::fabs(x) : f == "floor" ? std::floor(x) : f == "ceil" ? std::ceil(x)
+         : f == "round" ? std::round(x) : f == "sqrt" ? std::sqrt(x) : math1(math1_id(f), x);
+    return true;
+  }
+  if (f == "hypot" || f == "pow") {
+    if (!as_double(a[0], &x) || !as_double(a[1], &y)) return false;
+    *out = f == "hypot" ? std::hypot(x, y) : std::pow(x, y);
+    return true;
+  }
+  if (f == "hash") {
+    switch (a[0].index()) {
+      case 0: *out = (int64_t)std::hash<int64_t>{}(std::get<0>(a[0])); return true;
+      case 1: *out = (int64_t)std::hash<double>{}(std::get<1>(a[0])); return true;
+      case 2: *out = (int64_t)std::hash<bool>{}(std::get<2>(a[0])); return true;
+      default: *out = (int64_t)std::hash<std::string>{}(std::get<3>(a[0])); return true;
+    }
+  }
+  // string functions: asString of the first argument (and of strcasecmp's second / a pad)
+  for (size_t i = 0; i < a.size(); ++i) {
+    const bool str = i == 0 || (f == "strcasecmp") || ((f == "lpad" || f == "rpad") && i == 2);
+    if (str ? a[i].index() != 3 : a[i].index() != 0) return false;   // the others: asInt
+  }
+  const std::string& v = std::get<3>(a[0]);
+  if (f == "strcasecmp") {   // glibc's strcasecmp: the difference of the first differing lowered bytes
+    *out = (int64_t)::strcasecmp(v.c_str(), std::get<3>(a[1]).c_str());
+    return true;
+  }
+  if (f == "length") { *out = (int64_t)v.length(); return true; }
+  if (f == "lower" || f == "upper") {
+    std::string r = v;
+    for (char& ch : r) {
+      const unsigned char u = (unsigned char)ch;
+      if (f == "lower" && u >= 'A' && u <= 'Z') ch = (char)(u + 32);
+      if (f == "upper" && u >= 'a' && u <= 'z') ch = (char)(u - 32);
+    }
+    *out = r;
+    return true;
+  }
+  if (f == "trim" || f == "ltrim" || f == "rtrim") {
+    std::string r = v;
+    if (f != "rtrim") r.erase(0, r.find_first_not_of(" "));
+    if (f != "ltrim") r.erase(r.find_last_not_of(" ") + 1);
+    *out = r;
+    return true;
+  }
+  const int64_t n = std::get<0>(a[1]);
+  if (f == "left") { *out = n <= 0 ? std::string() : v.substr(0, (size_t)n); return true; }
+  if (f == "right") {
+    if (n <= 0) { *out = std::string(); return true; }
+    const size_t k = (uint64_t)n > v.size() ? v.size() : (size_t)n;
+    *out = v.substr(v.size() - k);
+    return true;
+  }
+  if (f == "lpad" || f == "rpad") {
+    const std::string& pad = std::get<3>(a[2]);
+    if (n < 0) return false;                       // size_t size: the padding loop never ends
+    if ((uint64_t)n < v.size()) { *out = v.substr(0, (size_t)n); return true; }
+    size_t need = (size_t)n - v.size();
+    if (need && pad.empty()) return false;         // the loop never ends
+    std::string p;
+    while (need > pad.size()) { p += pad; need -= pad.size(); }
+    p += pad.substr(0, need);
+    *out = f == "lpad" ? p + v : v + p;
+    return true;
+  }
+  if (f == "substr") {
+    const int64_t start = n, len = std::get<0>(a[2]);
+    const uint64_t ast = start == INT64_MIN ? (uint64_t)1 << 63 : (uint64_t)(start < 0 ? -start : start);
+    if (ast > v.size() || len <= 0 || start == 0) { *out = std::string(); return true; }
+    *out = start > 0 ? v.substr((size_t)start - 1, (size_t)len) : v.substr(v.size() - ast, (size_t)len);
+    return true;
+  }
+  return false;
 }
 
 }  // namespace
@@ -708,62 +849,111 @@ struct Ctx {
   }
 
   // FunctionCallExpression (Expressions.cpp:589-621) over FunctionManager's functions
-  // (FunctionManager.cpp): udf_is_in and the exact double math ones; a name the manager does not
-  // define, or the wrong arity, fails the statement as FunctionManager::get does.  Arguments are
-  // evaluated left to right before the call; an argument's error is the call's error.
+  // (FunctionManager.cpp:20-487): a name the manager does not define, or the wrong arity, fails
+  // the statement as FunctionManager::get does.  Arguments are evaluated left to right before the
+  // call; an argument's error is the call's error.  Constant arguments fold on the host with the
+  // reference's bodies (fm_eval); otherwise the call is a device op: the double math, hash,
+  // length, strcasecmp, rand32 / rand64 and now.  The string-valued functions (lower, upper, trim,
+  // ltrim, rtrim, left, right, lpad, rpad, substr) run on the device only over constants.
   int32_t function(const Node& e, Compiled* out) {
     const std::string& f = e.alias;
     const size_t n = e.kids.size();
-    static const char* math[] = {"abs", "floor", "ceil", "round", "sqrt"};
-    static const char* known[] = {"abs", "floor", "ceil", "round", "sqrt", "cbrt", "hypot", "pow", "exp", "exp2",
-                                  "log", "log2", "log10", "sin", "asin", "cos", "acos", "tan", "atan", "rand32",
-                                  "rand64", "now", "strcasecmp", "lower", "upper", "length", "trim", "ltrim",
-                                  "rtrim", "left", "right", "lpad", "rpad", "substr", "hash", "udf_is_in"};
-    bool defined = false;
-    for (const char* k : known) defined = defined || f == k;
-    if (!defined) {
+    const FnDef* def = fn_def(f);
+    if (!def) {
       *err = "Function `" + f + "' not defined";
       return NBG_E_EXECUTION_ERROR;
     }
-    int mi = -1;
-    for (int i = 0; i < 5; ++i)
-      if (f == math[i]) mi = i;
-    if (mi >= 0) {
-      if (n != 1) {
-        *err = "Arity not match for function `" + f + "'";
-        return NBG_E_EXECUTION_ERROR;
-      }
-      Compiled a;
-      int32_t rc = compile(*e.kids[0], &a);
-      if (rc) return rc;
-      if (a.always_error) { *out = a; return NBG_OK; }
-      // Expression::asDouble: an INT widens, a DOUBLE is itself, anything else is not a double
-      if (a.derived || (a.kind != VK_INT && a.kind != VK_DOUBLE)) { *out = make_error(); return NBG_OK; }
-      if (a.is_const) {
-        const double x = toD(a.cval);
-        const double r = mi == 0 ? std::fabs(x) : mi == 1 ? std::floor(x) : mi == 2 ? std::ceil(x)
-                       : mi == 3 ? std::round(x) : std::sqrt(x);
-        *out = make_const(CVal(r));
-        return NBG_OK;
-      }
-      Compiled c;
-      c.reg = a.reg;
-      if (a.kind == VK_INT) emit(OP_I2F, c.reg, c.reg);
-      static const uint8_t ops[] = {OP_ABS_F, OP_FLOOR_F, OP_CEIL_F, OP_ROUND_F, OP_SQRT_F};
-      emit(ops[mi], c.reg, c.reg);
-      c.kind = VK_DOUBLE;
-      *out = c;
-      return NBG_OK;
-    }
-    if (f != "udf_is_in") {
-      *err = "function `" + f + "' is not supported on the device";
-      return NBG_E_UNSUPPORTED;
-    }
-    if (n < 2) {
-      *err = "Arity not match for function `udf_is_in'";
+    if ((int)n < def->lo || (int)n > def->hi) {
+      *err = "Arity not match for function `" + f + "'";
       return NBG_E_EXECUTION_ERROR;
     }
-    return is_in(e, out);
+    if (f == "udf_is_in") return is_in(e, out);
+    std::vector<Compiled> args(n);
+    for (size_t i = 0; i < n; ++i) {
+      const int32_t rc = compile(*e.kids[i], &args[i]);
+      if (rc) return rc;
+    }
+    for (auto& x : args)
+      if (x.always_error) { *out = make_error(); return NBG_OK; }
+    const bool varying = f == "rand32" || f == "rand64" || f == "now";   // a value per evaluation / query
+    bool all_const = true;
+    for (auto& x : args) all_const = all_const && x.is_const && !x.derived;
+    if (all_const && !varying) {
+      std::vector<CVal> cv;
+      for (auto& x : args) cv.push_back(x.cval);
+      CVal r;
+      *out = fm_eval(f, cv, &r) ? make_const(r) : make_error();
+      return NBG_OK;
+    }
+    auto numeric = [](const Compiled& x) { return !x.derived && (x.kind == VK_INT || x.kind == VK_DOUBLE); };
+    auto as_double_reg = [&](Compiled& x) {   // Expression::asDouble: an INT widens
+      const int r = materialize(x);
+      if (x.kind == VK_INT) emit(OP_I2F, r, r);
+      return r;
+    };
+    Compiled c;
+    static const char* exact[] = {"abs", "floor", "ceil", "round", "sqrt"};
+    static const uint8_t exact_op[] = {OP_ABS_F, OP_FLOOR_F, OP_CEIL_F, OP_ROUND_F, OP_SQRT_F};
+    int xi = -1;
+    for (int i = 0; i < 5; ++i)
+      if (f == exact[i]) xi = i;
+    if (xi >= 0 || math1_id(f) >= 0) {
+      if (!numeric(args[0])) { *out = make_error(); return NBG_OK; }   // boost::bad_get
+      c.reg = as_double_reg(args[0]);
+      if (xi >= 0) emit(exact_op[xi], c.reg, c.reg);
+      else emit(OP_MATH1_F, c.reg, c.reg, 0, math1_id(f));
+      c.kind = VK_DOUBLE;
+    } else if (f == "pow" || f == "hypot") {
+      if (!numeric(args[0]) || !numeric(args[1])) { *out = make_error(); return NBG_OK; }
+      const int ra = as_double_reg(args[0]);
+      const int rb = as_double_reg(args[1]);
+      c.reg = std::min(ra, rb);
+      emit(OP_MATH2_F, c.reg, ra, rb, f == "pow" ? 0 : 1);
+      c.kind = VK_DOUBLE;
+    } else if (f == "hash") {
+      Compiled& x = args[0];
+      c.kind = VK_INT;
+      if (x.kind == VK_STRING) {   // std::hash<std::string>: the bytes, whatever made them
+        const std::vector<Piece> ps = pieces_of(x);
+        const int32_t h = emit_pieces(ps);
+        c.reg = sink_reg(ps);
+        emit(OP_HASH_S, c.reg, 0, 0, h);
+      } else {
+        c.reg = materialize(x);   // std::hash<int64_t> / <bool>: the value itself
+        if (x.kind == VK_DOUBLE) emit(OP_HASH_F, c.reg, c.reg);
+      }
+    } else if (f == "length" || f == "strcasecmp") {
+      for (auto& x : args)
+        if (x.kind != VK_STRING) { *out = make_error(); return NBG_OK; }   // asString: bad_get
+      const std::vector<Piece> pa = pieces_of(args[0]);
+      const std::vector<Piece> pq = n > 1 ? pieces_of(args[1]) : std::vector<Piece>{};
+      const int32_t ha = emit_pieces(pa);
+      const int32_t hb = n > 1 ? emit_pieces(pq) : 0;
+      c.reg = sink_reg(pa, pq);
+      if (f == "length") emit(OP_SLEN, c.reg, 0, 0, ha);
+      else emit(OP_SCASE, c.reg, 0, 0, ha, hb);
+      c.kind = VK_INT;
+    } else if (f == "rand32" || f == "rand64") {
+      int r[2] = {0, 0};
+      for (size_t i = 0; i < n; ++i) {
+        if (args[i].derived || args[i].kind != VK_INT) { *out = make_error(); return NBG_OK; }   // asInt
+        r[i] = materialize(args[i]);
+      }
+      c.reg = n ? std::min(r[0], n > 1 ? r[1] : r[0]) : push();
+      emit(OP_RAND, c.reg, r[0], r[1], (int32_t)n | (f == "rand64" ? 4 : 0));
+      c.kind = VK_INT;
+    } else if (f == "now") {
+      c.reg = push();
+      emit(OP_NOW, c.reg);
+      c.kind = VK_INT;
+    } else {
+      *err = "function `" + f + "' over per-edge values is not supported on the device";
+      return NBG_E_UNSUPPORTED;
+    }
+    top = c.reg + 1;
+    if (top > max_reg) max_reg = top;
+    *out = c;
+    return NBG_OK;
   }
 
   // udf_is_in(cmp, v1, ...) (FunctionManager.cpp:440-486): every vi converted to cmp's kind

@@ -18,6 +18,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstring>
+#include <ctime>
 #include <unordered_map>
 
 #include <omp.h>
@@ -454,6 +455,8 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
       const DevEdgeType& top = E.snap.types.at(ectx[active[i < active.size() ? i : olds[i - active.size()]]].type);
       const DevEdgeType& dt = i < active.size() ? top : *top.old;
       ExpandArgs a{};
+      a.now_sec = (int64_t)time(nullptr);   // now() in a storage filter: the request's second
+      a.rand_seed = (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count() * 0x9e3779b97f4a7c15ull;
       a.row_ptr = dt.row_ptr;
       a.col = dt.col;
       a.dst_vid = dt.dst_vid;

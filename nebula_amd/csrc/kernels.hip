@@ -661,6 +661,79 @@ __device__ bool str_to_double(StrIter& it, const DevStrings& S, const int64_t* r
   return true;
 }
 
+// libstdc++'s std::_Hash_bytes (the 64-bit MurmurHash2 variant under std::hash<std::string> and
+// std::hash<double>), seed 0xc70f6907: 8-byte little-endian words, then the tail bytes
+constexpr uint64_t HB_MUL = 0xc6a4a7935bd1e995ull;
+__device__ __forceinline__ uint64_t hb_shift_mix(uint64_t v) { return v ^ (v >> 47); }
+__device__ __forceinline__ uint64_t hb_word(uint64_t h, uint64_t w) {
+  return (h ^ (hb_shift_mix(w * HB_MUL) * HB_MUL)) * HB_MUL;
+}
+__device__ __forceinline__ uint64_t hb_final(uint64_t h, uint64_t tail, uint64_t ntail) {
+  if (ntail) h = (h ^ tail) * HB_MUL;
+  return hb_shift_mix(hb_shift_mix(h) * HB_MUL);
+}
+__device__ uint64_t str_hash_bytes(const Ins* data, int32_t hdr, const DevStrings& S, const int64_t* regs, int tid,
+                                   bool& bad) {
+  const uint64_t len = str_len(data, hdr, S, regs, tid, bad);
+  uint64_t h = 0xc70f6907ull ^ (len * HB_MUL), w = 0;
+  StrIter it;
+  str_open(it, data, hdr, S, regs, tid, bad);
+  for (uint64_t k = 0; k < len; ++k) {
+    w |= (uint64_t)(uint32_t)str_next(it, S, regs, tid, bad) << (8 * (k & 7));
+    if ((k & 7) == 7) {
+      h = hb_word(h, w);
+      w = 0;
+    }
+  }
+  return hb_final(h, w, len & 7);
+}
+__device__ __forceinline__ uint64_t hash_double_bits(int64_t bits) {   // std::hash<double>
+  if (as_f(bits) == 0.0) return 0;   // (+0.0 and -0.0)
+  return hb_final(hb_word(0xc70f6907ull ^ (8 * HB_MUL), (uint64_t)bits), 0, 0);
+}
+
+// glibc strcasecmp over two piece lists: the difference of the first differing lowered bytes (a
+// string's end reads as 0, so a proper prefix compares as the shorter one's NUL)
+__device__ int64_t str_casecmp(const Ins* data, int32_t ha, int32_t hb, const DevStrings& S, const int64_t* regs,
+                               int tid, bool& bad) {
+  StrIter x, y;
+  str_open(x, data, ha, S, regs, tid, bad);
+  str_open(y, data, hb, S, regs, tid, bad);
+  for (;;) {
+    int cx = str_next(x, S, regs, tid, bad), cy = str_next(y, S, regs, tid, bad);
+    if (cx < 0) cx = 0;
+    if (cy < 0) cy = 0;
+    const int lx = cx >= 'A' && cx <= 'Z' ? cx + 32 : cx, ly = cy >= 'A' && cy <= 'Z' ? cy + 32 : cy;
+    if (lx != ly || cx == 0) return lx - ly;
+  }
+}
+
+// rand32 / rand64 (FunctionManager.cpp:186-230 over folly::Random): a value per evaluation from
+// the query's seed, the edge and the instruction (random in the reference too; the ranges and the
+// integer conversions are what is restated)
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9e3779b97f4a7c15ull;
+  x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+  x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+  return x ^ (x >> 31);
+}
+__device__ int64_t rand_value(uint64_t seed, uint64_t j, uint32_t v, int pc, int nargs, bool r64, int64_t a0,
+                              int64_t a1) {
+  const uint64_t r = splitmix64(seed ^ splitmix64(j * 0x100000001b3ull + v) ^ ((uint64_t)pc << 56));
+  if (!r64) {
+    const uint32_t u = (uint32_t)r;
+    if (nargs == 0) return (int64_t)(int32_t)u;
+    const uint32_t lo = nargs == 2 ? (uint32_t)a0 : 0u, hi = (uint32_t)(nargs == 2 ? a1 : a0);
+    if (lo == hi) return 0;   // folly: an empty range
+    const uint32_t got = lo + (uint32_t)(((uint64_t)u * (uint32_t)(hi - lo)) >> 32);
+    return nargs == 1 ? (int64_t)(int32_t)got : (int64_t)got;
+  }
+  if (nargs == 0) return (int64_t)r;
+  const uint64_t lo = nargs == 2 ? (uint64_t)a0 : 0ull, hi = (uint64_t)(nargs == 2 ? a1 : a0);
+  if (lo == hi) return 0;
+  return (int64_t)(lo + __umul64hi(r, hi - lo));
+}
+
 // OP_SOUT: the derived string into the arena; its canonical code (dictionary code when the
 // dictionary holds it, else STR_DERIVED | content hash, str_derived_code)
 __device__ int64_t str_store(const Ins* data, int32_t hdr, const DevStrings& S, const int64_t* regs, int tid,
@@ -869,7 +942,43 @@ __device__ __forceinline__ void run_program(const Ins* __restrict__ prog, const 
       case OP_CEIL_F: r = fbits(ceil(as_f(x))); break;
       case OP_ROUND_F: r = fbits(round(as_f(x))); break;
       case OP_SQRT_F: r = fbits(sqrt(as_f(x))); break;
+      case OP_MATH1_F: {
+        const double v = as_f(x);
+        double o;
+        switch (ins.aux) {
+          case 0: o = cbrt(v); break;
+          case 1: o = exp(v); break;
+          case 2: o = exp2(v); break;
+          case 3: o = log(v); break;
+          case 4: o = log2(v); break;
+          case 5: o = log10(v); break;
+          case 6: o = sin(v); break;
+          case 7: o = asin(v); break;
+          case 8: o = cos(v); break;
+          case 9: o = acos(v); break;
+          case 10: o = tan(v); break;
+          default: o = atan(v); break;
+        }
+        r = fbits(o);
+        break;
+      }
+      case OP_MATH2_F: r = fbits(ins.aux == 0 ? pow(as_f(x), as_f(y)) : hypot(as_f(x), as_f(y))); break;
+      case OP_HASH_F: r = (int64_t)hash_double_bits(x); break;
+      case OP_HASH_S:
+      case OP_SLEN:
+      case OP_SCASE:
+        if (active) {
+          bool bad = false;
+          if (ins.op == OP_HASH_S) r = (int64_t)str_hash_bytes(data, ins.aux, a.str, regs, tid, bad);
+          else if (ins.op == OP_SLEN) r = (int64_t)str_len(data, ins.aux, a.str, regs, tid, bad);
+          else r = str_casecmp(data, ins.aux, (int32_t)ins.imm, a.str, regs, tid, bad);
+          err = err || bad;
+        }
+        break;
+      case OP_RAND: r = rand_value(a.rand_seed, c.j, c.v, pc, ins.aux & 3, (ins.aux & 4) != 0, x, y); break;
+      case OP_NOW: r = a.now_sec; break;
       default: break;
+
     }
     regs[ins.d * BLOCK + tid] = r;
   }

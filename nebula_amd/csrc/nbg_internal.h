@@ -187,6 +187,15 @@ enum Op : uint8_t {
   OP_ISIN_F,     // r[d] = r[b] || double(r[a]) == double(imm) (exact, as std::unordered_set<double>)
   OP_EQX_F,      // r[d] = double(r[a]) == double(r[b]) (exact)
   OP_ABS_F, OP_FLOOR_F, OP_CEIL_F, OP_ROUND_F, OP_SQRT_F,   // FunctionManager's exact math
+  // the rest of FunctionManager (FunctionManager.cpp:20-437) over per-edge values
+  OP_MATH1_F,    // r[d] = f(double(r[a])), aux: cbrt exp exp2 log log2 log10 sin asin cos acos tan atan
+  OP_MATH2_F,    // r[d] = aux 0: pow(r[a], r[b]), 1: hypot(r[a], r[b]) (doubles)
+  OP_HASH_F,     // r[d] = std::hash<double>(r[a]) (libstdc++ _Hash_bytes of the 8 bytes; 0.0 -> 0)
+  OP_HASH_S,     // r[d] = std::hash<std::string> of the piece list data[aux]
+  OP_SLEN,       // r[d] = the length of the piece list data[aux]
+  OP_SCASE,      // r[d] = strcasecmp(piece list data[aux], piece list data[imm]) (glibc's difference)
+  OP_RAND,       // r[d] = rand32 / rand64 (aux bit 2) over aux & 3 INT arguments r[a], r[b]
+  OP_NOW,        // r[d] = WallClock::fastNowInSec() of the query (ExpandArgs::now_sec)
   OP_COUNT_
 };
 
@@ -336,6 +345,8 @@ struct ExpandArgs {                // one (step, edge type) expansion
   uint64_t in_n;
   const int64_t* const* in_cols;   // [col][k] 8-byte payloads of the indexed rows
   DevStrings str;                  // strings beyond dictionary codes (casts, concatenation)
+  int64_t now_sec;                 // now(): the query's wall-clock second (set per query)
+  uint64_t rand_seed;              // rand32 / rand64: this query's stream (set per query)
 };
 
 // The lean final step (final.hip) for WHERE `col <cmp> const` (or none) with _dst / constant

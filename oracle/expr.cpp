@@ -1,6 +1,10 @@
 // Test infrastructure (oracle) — Expression wire decoder + tree-walking evaluator,
 // restated from src/common/filter/Expressions.{h,cpp}.
 #include <cmath>
+#include <functional>
+#include <strings.h>
+#include <cctype>
+#include <ctime>
 #include "orc.h"
 
 namespace orc {
@@ -166,20 +170,129 @@ bool toStr(const Value& v, std::string* out) {
 
 }  // namespace
 
-// FunctionManager's bodies (FunctionManager.cpp): the exact double math functions and udf_is_in
-// (:440-486, std::unordered_set membership after converting every candidate to the comparand's
-// alternative).  Other functions are not restated.
+// FunctionManager's bodies (src/common/filter/FunctionManager.cpp:20-487).  Arguments are read
+// with Expression::asDouble / asInt / asString (Expressions.h:217-246), i.e. boost::get: an
+// argument of another kind throws bad_get, an evaluation error here.  lpad / rpad with a negative
+// size, or padding with an empty pad, never return in the reference (their loop does not end):
+// an evaluation error here.  rand32 / rand64 / now are random / the clock: only their ranges are
+// restated.  udf_is_in (:440-486): std::unordered_set membership after converting every
+// candidate to the comparand's alternative.
+namespace {
+uint64_t splitmix(uint64_t x) {
+  x += 0x9e3779b97f4a7c15ull;
+  x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+  x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+  return x ^ (x >> 31);
+}
+uint64_t rand_bits() {
+  static uint64_t state = (uint64_t)time(nullptr) * 0x9e3779b97f4a7c15ull;
+  return splitmix(state += 0x9e3779b97f4a7c15ull);
+}
+}  // namespace
+
 OptValue callFunction(const std::string& f, const std::vector<Value>& av) {
-  static const char* math[] = {"abs", "floor", "ceil", "round", "sqrt"};
-  for (int i = 0; i < 5; ++i) {
-    if (f != math[i]) continue;
+  static const char* math1[] = {"abs", "floor", "ceil", "round", "sqrt", "cbrt", "exp", "exp2", "log",
+                                "log2", "log10", "sin", "asin", "cos", "acos", "tan", "atan"};
+  for (int i = 0; i < 17; ++i) {
+    if (f != math1[i]) continue;
     if (av.size() != 1) return Status::Err("Arity not match");
     if (!isArith(av[0])) return Status::Err("asDouble of a non-number");   // boost::bad_get
     const double x = asDouble(av[0]);
-    return Value(i == 0 ? std::fabs(x) : i == 1 ? std::floor(x) : i == 2 ? std::ceil(x) : i == 3 ? std::round(x)
-                                                                                                  : std::sqrt(x));
+    double (*const fn[17])(double) = {std::fabs, std::floor, std::ceil, std::round, std::sqrt, std::cbrt,
+                                      std::exp,  std::exp2,  std::log,  std::log2,  std::log10, std::sin,
+                                      std::asin, std::cos,   std::acos, std::tan,   std::atan};
+    return Value(fn[i](x));
   }
-  if (f != "udf_is_in") return Status::Err("function not restated by this oracle");
+  if (f == "hypot" || f == "pow") {
+    if (av.size() != 2) return Status::Err("Arity not match");
+    if (!isArith(av[0]) || !isArith(av[1])) return Status::Err("asDouble of a non-number");
+    const double x = asDouble(av[0]), y = asDouble(av[1]);
+    return Value(f == "hypot" ? std::hypot(x, y) : std::pow(x, y));
+  }
+  if (f == "rand32" || f == "rand64") {   // folly::Random::rand32 / rand64 (max), (min, max)
+    if (av.size() > 2) return Status::Err("Arity not match");
+    for (auto& v : av)
+      if (!isInt(v)) return Status::Err("asInt of a non-int");
+    const uint64_t r = rand_bits();
+    if (f == "rand32") {
+      if (av.empty()) return Value((int64_t)(int32_t)(uint32_t)r);
+      const uint32_t lo = av.size() == 2 ? (uint32_t)asInt(av[0]) : 0u, hi = (uint32_t)asInt(av.back());
+      if (lo == hi) return Value((int64_t)0);
+      const uint32_t got = lo + (uint32_t)(r % (uint32_t)(hi - lo));
+      return Value(av.size() == 1 ? (int64_t)(int32_t)got : (int64_t)got);
+    }
+    if (av.empty()) return Value((int64_t)r);
+    const uint64_t lo = av.size() == 2 ? (uint64_t)asInt(av[0]) : 0ull, hi = (uint64_t)asInt(av.back());
+    if (lo == hi) return Value((int64_t)0);
+    return Value((int64_t)(lo + r % (hi - lo)));
+  }
+  if (f == "now") {
+    if (!av.empty()) return Status::Err("Arity not match");
+    return Value((int64_t)time(nullptr));   // WallClock::fastNowInSec
+  }
+  if (f == "hash") {   // std::hash of the variant's alternative (libstdc++: identity for integers)
+    if (av.size() != 1) return Status::Err("Arity not match");
+    switch (av[0].index()) {
+      case 0: return Value((int64_t)std::hash<int64_t>{}(std::get<0>(av[0])));
+      case 1: return Value((int64_t)std::hash<double>{}(std::get<1>(av[0])));
+      case 2: return Value((int64_t)std::hash<bool>{}(std::get<2>(av[0])));
+      default: return Value((int64_t)std::hash<std::string>{}(std::get<3>(av[0])));
+    }
+  }
+  struct Sig {
+    const char* name;
+    size_t n;
+    const char* kinds;   // s: asString, i: asInt
+  };
+  static const Sig sigs[] = {{"strcasecmp", 2, "ss"}, {"lower", 1, "s"},  {"upper", 1, "s"},
+                             {"length", 1, "s"},      {"trim", 1, "s"},   {"ltrim", 1, "s"},
+                             {"rtrim", 1, "s"},       {"left", 2, "si"},  {"right", 2, "si"},
+                             {"lpad", 3, "sis"},      {"rpad", 3, "sis"}, {"substr", 3, "sii"}};
+  for (const Sig& g : sigs) {
+    if (f != g.name) continue;
+    if (av.size() != g.n) return Status::Err("Arity not match");
+    for (size_t k = 0; k < g.n; ++k)
+      if (g.kinds[k] == 's' ? !isStr(av[k]) : !isInt(av[k])) return Status::Err("bad_get");
+    std::string v = std::get<3>(av[0]);
+    if (f == "strcasecmp") return Value((int64_t)::strcasecmp(v.c_str(), std::get<3>(av[1]).c_str()));
+    if (f == "length") return Value((int64_t)v.length());
+    if (f == "lower" || f == "upper") {
+      for (char& c : v) c = (char)(f == "lower" ? std::tolower((unsigned char)c) : std::toupper((unsigned char)c));
+      return Value(v);
+    }
+    if (f == "trim" || f == "ltrim" || f == "rtrim") {
+      if (f != "rtrim") v.erase(0, v.find_first_not_of(" "));
+      if (f != "ltrim") v.erase(v.find_last_not_of(" ") + 1);
+      return Value(v);
+    }
+    const int64_t n = asInt(av[1]);
+    if (f == "left") return Value(n <= 0 ? std::string() : v.substr(0, (size_t)n));
+    if (f == "right") {
+      if (n <= 0) return Value(std::string());
+      const size_t k = (uint64_t)n > v.size() ? v.size() : (size_t)n;
+      return Value(v.substr(v.size() - k));
+    }
+    if (f == "lpad" || f == "rpad") {
+      const std::string& extra = std::get<3>(av[2]);
+      const size_t size = (size_t)n;
+      if (size < v.size()) return Value(v.substr(0, size));
+      if (n < 0 || (size > v.size() && extra.empty())) return Status::Err("padding never ends");
+      size_t need = size - v.size();
+      std::string pad;
+      while (need > extra.size()) {
+        pad += extra;
+        need -= extra.size();
+      }
+      pad += extra.substr(0, need);
+      return Value(f == "lpad" ? pad + v : v + pad);
+    }
+    // substr
+    const int64_t start = n, len = asInt(av[2]);
+    const uint64_t ast = start < 0 ? 0ull - (uint64_t)start : (uint64_t)start;
+    if (ast > v.size() || len <= 0 || start == 0) return Value(std::string());
+    return Value(start > 0 ? v.substr((size_t)start - 1, (size_t)len) : v.substr(v.size() - ast, (size_t)len));
+  }
+  if (f != "udf_is_in") return Status::Err("Function not defined");
   if (av.size() < 2) return Status::Err("Arity not match");
   const Value& cmp = av[0];
   bool found = false;

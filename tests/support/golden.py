@@ -121,3 +121,49 @@ def run_expr_case(backend, case):
         elif v != exp:
             return False, f"YIELD {v!r} != {exp!r}"
     return True, "ok"
+
+
+def _ulps_equal(a: float, b: float, ulps: int = 4) -> bool:
+    """gtest's ASSERT_DOUBLE_EQ: within 4 units in the last place."""
+    import struct
+    if a == b:
+        return True
+    ia = struct.unpack("<q", struct.pack("<d", a))[0]
+    ib = struct.unpack("<q", struct.pack("<d", b))[0]
+    # biased representation: negative doubles ordered below the positive ones
+    ia = -(ia & 0x7FFFFFFFFFFFFFFF) if ia < 0 else ia
+    ib = -(ib & 0x7FFFFFFFFFFFFFFF) if ib < 0 else ib
+    return abs(ia - ib) <= ulps
+
+
+def run_func_case(backend, case):
+    """(ok, message) for a FunctionCall / StringFunctionCall vector of ExpressionTest.cpp:585-745:
+    TEST_EXPR(expected, op, expr, type) asserts is<type>(v) and ASSERT_<op>(expected, v)
+    (ASSERT_DOUBLE_EQ for Double EQ: within 4 ulps).  The YIELD form gives the value; the WHERE form
+    keeps both edges iff asBool(value) (not checked for rand32 / rand64, a value per row)."""
+    import operator
+    s = ngql.Session(backend)
+    where_q, yield_q = expr_queries(case)
+    kind, op, exp = case["kind"], case["op"], case["expect"]
+    if kind == "Double":
+        exp = 2.7182818284590451 if exp == "euler" else float(exp)
+    elif kind == "Int":
+        exp = int(exp)
+    vals = [r[0] for r in s.execute(yield_q).rows]
+    if len(vals) != 2:
+        return False, f"YIELD gave {vals}"
+    cmp = {"EQ": operator.eq, "NE": operator.ne, "LT": operator.lt, "LE": operator.le, "GT": operator.gt,
+           "GE": operator.ge}[op]
+    for v in vals:
+        want = {"Double": float, "Int": int, "String": str}[kind]
+        if isinstance(v, bool) or not isinstance(v, want):
+            return False, f"YIELD {v!r} is not {kind}"
+        good = _ulps_equal(exp, v) if (kind == "Double" and op == "EQ") else cmp(exp, v)
+        if not good:
+            return False, f"ASSERT_{op}({exp!r}, {v!r}) fails"
+    if not case["expr"].startswith("rand"):
+        truthy = (vals[0] != 0) if kind != "String" else vals[0] == ""
+        rows = s.execute(where_q).rows
+        if len(rows) != (2 if truthy else 0):
+            return False, f"WHERE kept {len(rows)} rows"
+    return True, "ok"

@@ -1,4 +1,4 @@
-"""ExpressionTest.cpp's literal vectors on the MI355X: the device expression VM (storage-side
+"""ExpressionTest.cpp's literal and FunctionCall / StringFunctionCall vectors on the MI355X: the device expression VM (storage-side
 WHERE and graph-side YIELD of k_expand's final step) against the values the reference's test
 asserts — the same vectors the oracle is pinned to in tests/test_oracle_expr.py."""
 import pytest
@@ -8,7 +8,7 @@ from tests.support import golden
 
 pytestmark = pytest.mark.gpu
 
-CASES = [c for c in golden.load("expression_cases.json") if not c.get("function")]
+CASES = golden.load("expression_cases.json")
 
 
 @pytest.fixture(scope="module")
@@ -20,7 +20,8 @@ def nba(nba_data):
 
 @pytest.mark.parametrize("case", CASES, ids=[f"{c['test']}-{i}" for i, c in enumerate(CASES)])
 def test_expression_vector_on_gpu(nba, case):
-    ok, msg = golden.run_expr_case(nba, case)
+    run = golden.run_func_case if case.get("function") else golden.run_expr_case
+    ok, msg = run(nba, case)
     assert ok, (case["expr"], msg)
 
 

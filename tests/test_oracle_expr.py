@@ -1,6 +1,7 @@
 """Pin expression evaluation to the reference's expression unit test (ExpressionTest.cpp): every
-literal / arithmetic / relational / logical vector as a GO WHERE and a GO YIELD over the nba
-dataset on the CPU oracle; invalid expressions must fail.  Vectors: tests/golden/
+literal / arithmetic / relational / logical vector and every FunctionCall / StringFunctionCall
+vector (:585-745, FunctionManager's bodies) as a GO WHERE and a GO YIELD over the nba dataset on
+the CPU oracle; invalid expressions must fail.  Vectors: tests/golden/
 expression_cases.json (tools/make_golden_expr.py).  CPU only; the device runs the same vectors in
 tests/test_gpu_expr.py."""
 import pytest
@@ -20,9 +21,8 @@ def orc(nba_data):
 
 @pytest.mark.parametrize("case", CASES, ids=[f"{c['test']}-{i}" for i, c in enumerate(CASES)])
 def test_expression_vector_oracle(orc, case):
-    if case.get("function"):
-        pytest.skip("function calls (FunctionManager) are out of the hot path's scope")
-    ok, msg = golden.run_expr_case(orc, case)
+    run = golden.run_func_case if case.get("function") else golden.run_expr_case
+    ok, msg = run(orc, case)
     assert ok, (case["expr"], msg)
 
 
