@@ -41,7 +41,7 @@ METRIC = "GO 3 STEPS traversed edges/sec (TEPS) at 1/2/4/8 GPU; FIND SHORTEST PA
 # HBM traffic per launch from the committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
 # bench's default workload (tools/gpu_r02.sh pmc -> tools/pmc_summary.py; FETCH_SIZE doubled per
 # the gfx950 note), keyed by workload
-PMC_FILES = {("RMAT-26", 16): os.path.join(ROOT, "profiles", "r04_n_pmc_hbm_rmat26.json"),
+PMC_FILES = {("RMAT-26", 16): os.path.join(ROOT, "profiles", "r05_h_pmc_hbm_rmat26.json"),
              ("RMAT-22", 64): os.path.join(ROOT, "profiles", "r02_pmc_hbm_rmat22.json")}
 # library kernel id -> instantiations in the rocprof names, first match wins (FINAL: this bench's
 # range WHERE with a _dst YIELD runs k_expand<4> = FINALD; <3> FINALF; <1> the general interpreter;
@@ -50,7 +50,9 @@ PMC_FILES = {("RMAT-26", 16): os.path.join(ROOT, "profiles", "r04_n_pmc_hbm_rmat
 # names read k_expand<4, false, 4>; summaries written before that read k_expand<4, false>)
 PMC_NAMES = {k: [n for p in v for n in (p[:-1] + ", 4>", p)] for k, v in {
     "k_expand<MARK>": ["k_expand<0, false>", "k_expand<0, true>"],
-    "k_expand<FINAL>": ["k_expand<4, false>", "k_expand<4, true>", "k_expand<3, false>",
+    "k_expand<FINAL>": ["k_final_dst<1, true>", "k_final_dst<2, true>", "k_final_dst<4, true>",
+                        "k_final_dst<8, true>", "k_final_dst<0, true>",
+                        "k_expand<4, false>", "k_expand<4, true>", "k_expand<3, false>",
                         "k_expand<3, true>", "k_expand<1, false>", "k_expand<1, true>"],
     "k_expand<BFS>": ["k_expand<2, false>", "k_expand<2, true>"]}.items()}
 

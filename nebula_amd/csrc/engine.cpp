@@ -398,8 +398,11 @@ int32_t materialize_rows(nbg_rows* r) {
     std::vector<std::pair<uint64_t, uint64_t>> segs;
     segs.reserve(r->segs.size());
     for (auto& s : r->segs) segs.emplace_back(s.begin, s.end - s.begin);
-    if (ws_fetch_rows_pinned(r->ws ? r->ws : E.ws, segs, r->ncols, r->count, r->hbits) != hipSuccess)
-      return NBG_E_DEVICE;
+    const hipError_t he = ws_fetch_rows_pinned(r->ws ? r->ws : E.ws, segs, r->ncols, r->count, r->hbits);
+    if (he != hipSuccess)   // (named: round 4's one "row fetch failed" left no trace of the failing call)
+      return E.fail(NBG_E_DEVICE, std::string("row fetch failed: ") + hipGetErrorName(he) + " (" +
+                                      hipGetErrorString(he) + "), " + std::to_string(segs.size()) + " segments, " +
+                                      std::to_string(r->count) + " rows");
   }
   bool any_string = false;
   for (auto& kv : r->kinds)
@@ -1340,6 +1343,10 @@ static int32_t go_collect(Engine& E, const nbg_go_stmt* st, GoPending* p, nbg_ro
     delete rows;
     return E.fail(NBG_E_EXECUTION_ERROR, st->dst_unknown);
   }
+  if (g_err >= SPLIT_BAD) {
+    delete rows;
+    return E.fail(NBG_E_DEVICE, "internal: a frontier list's merge-path split did not describe its tile");
+  }
   if (g_err >= ARENA_OVERFLOW) {
     delete rows;
     return E.fail(NBG_E_OUT_OF_MEMORY, "the derived strings of the result need " + std::to_string(q.arena_used >> 10) +
@@ -1437,7 +1444,7 @@ static int32_t go_collect(Engine& E, const nbg_go_stmt* st, GoPending* p, nbg_ro
     int32_t rc = materialize_rows(rows);
     if (rc) {
       delete rows;
-      return rc == NBG_E_EXECUTION_ERROR ? rc : E.fail(rc, "row fetch failed");
+      return rc == NBG_E_EXECUTION_ERROR || rc == NBG_E_DEVICE ? rc : E.fail(rc, "row fetch failed");
     }
   } else if (rows->count) {
     E.holders[ws] = rows;   // the rows stay valid until nbg_rows_free (ws_release)

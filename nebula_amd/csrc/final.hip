@@ -11,12 +11,13 @@
 // of its large argument block), with the SIMDs issuing about every cycle
 // (profiles/r02_r_pmc_sq_stall_rmat26.json: 56.7 M VALU + 57.6 M SALU per RMAT-26 launch).
 // Here a tile's edge items find their frontier entry without a search:
-//   * each entry of the tile's window writes its index at the tile position of its first edge
-//     (a "head"), tagged with the wave's tile count so the head array is never cleared;
-//   * a wave-wide max-scan (DPP row shifts and row broadcasts) carries the last head forward, so
-//     every item knows its entry;
-//   * the entry's (row start - edge offset) was stored beside it, so an item's CSR index is one
-//     LDS read and one add.
+//   * each entry of the tile's window with edges in the tile sets the bit of its first edge's tile
+//     position in a 256-bit head mask (4 words in LDS) and stores its (row start - edge offset)
+//     at its rank among those entries (ballot prefix counts);
+//   * an item's entry is then the number of head bits at or before it: a popcount of the masked
+//     word plus the earlier words', so its CSR index is two popcounts, one LDS read and one add.
+// (Round 5's first version tagged heads with the tile count and carried the last head forward
+// with a DPP max-scan per item row: 12 VALU per item where the popcounts take 4.)
 // The WHERE column width and the single-_dst YIELD are template parameters: no per-tile switch.
 #include <hip/hip_runtime.h>
 
@@ -28,33 +29,12 @@ namespace {
 constexpr int FB = 256;        // threads per workgroup
 constexpr int FW = FB / 64;    // waves per workgroup
 constexpr int FV = VT;         // items per lane: a tile is the producers' TILE
-constexpr uint32_t HEAD_BITS = 9;   // an entry index within a tile's window: 0..TILE
-static_assert(TILE + 1 <= (1 << HEAD_BITS), "head index width");
+static_assert(FV == 4 && TILE == 256, "the head mask is 4 words of 64 tile positions");
 
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// max with the value DPP brings from another lane (lanes without a source, or in rows the mask
-// leaves out, read 0: the identity of max over indices)
-template <int CTRL, int ROWS>
-__device__ __forceinline__ uint32_t max_dpp(uint32_t v) {
-  const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, false);
-  return v > t ? v : t;
-}
-
-// inclusive max-scan over the wave's 64 lanes: within rows of 16 (row_shr 1, 2, 4, 8), then
-// row 15 into rows 1 and 3 (row_bcast:15) and lane 31 into rows 2 and 3 (row_bcast:31)
-__device__ __forceinline__ uint32_t wave_max_scan(uint32_t v) {
-  v = max_dpp<0x111, 0xf>(v);
-  v = max_dpp<0x112, 0xf>(v);
-  v = max_dpp<0x114, 0xf>(v);
-  v = max_dpp<0x118, 0xf>(v);
-  v = max_dpp<0x142, 0xa>(v);
-  v = max_dpp<0x143, 0xc>(v);
-  return v;
 }
 
 // A load the compiler issues where it is written: a relaxed wave-scope atomic load is a plain
@@ -71,16 +51,19 @@ template <> struct WType<1> { using T = int8_t; };
 template <> struct WType<2> { using T = int16_t; };
 template <> struct WType<4> { using T = int32_t; };
 
-// WB: the WHERE column's stored width (0: no WHERE).  ONE: the only YIELD is _dst.
+}  // namespace
+
+// WB: the WHERE column's stored width (0: no WHERE).  ONE: the only YIELD is _dst.  (Outside the
+// anonymous namespace so profilers name it nbg::k_final_dst<WB, ONE>.)
 template <int WB, bool ONE>
 __global__ void __launch_bounds__(FB) __attribute__((amdgpu_waves_per_eu(8)))
 k_final_dst(FinalDstArgs a) {
-  __shared__ uint32_t sHeadAll[FW][TILE];       // tile position -> (tag << HEAD_BITS | entry)
-  __shared__ uint32_t sDeltaAll[FW][TILE + 1];  // entry -> row start - edge offset
+  __shared__ unsigned long long sMaskAll[FW][FV];   // tile positions where an entry's edges start
+  __shared__ uint32_t sDeltaAll[FW][TILE + 1];      // head rank (1-based) -> row start - edge offset
   __shared__ unsigned long long sBase;          // rows this workgroup wrote
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint32_t* const sHead = sHeadAll[w];
+  unsigned long long* const sMask = sMaskAll[w];
   uint32_t* const sDelta = sDeltaAll[w];
   const unsigned long long packed = *a.acc;   // (list entries << 32 | edges)
   const uint64_t n = packed >> 32, total = packed & 0xFFFFFFFFull;
@@ -88,7 +71,6 @@ k_final_dst(FinalDstArgs a) {
     if (a.stat_e) *a.stat_e += total;
     if (a.stat_n) *a.stat_n = n;
   }
-  for (int k = lane; k < TILE; k += 64) sHead[k] = 0;   // (tag 0 is never a tile's)
   if (threadIdx.x == 0) sBase = 0;
   __syncthreads();
   const uint64_t npath = n + total;
@@ -107,21 +89,36 @@ k_final_dst(FinalDstArgs a) {
   // starts (the end of entry s0 - 1 + k) and ends, and its row start, loaded at clamped indices
   // with no branch; `window` applies the bounds when the values are used (a select right after
   // a load is a wait for it: the prefetch would be waited for in the tile that issued it)
+  // (32-bit: a list holds fewer than 2^32 - 2 * TILE entries, ws_cap_frontier; q = s + 1)
+  const uint32_t n32 = (uint32_t)n;
   auto stage = [&](uint64_t s0, uint32_t* x0, uint32_t* x1, uint32_t* rr) {
-    const int64_t i = (int64_t)s0 - 1 + lane;
-    const uint64_t c0 = i < 0 ? 0 : ((uint64_t)i < n ? (uint64_t)i : n - 1);
-    const uint64_t c1 = (uint64_t)(i + 1) < n ? (uint64_t)(i + 1) : n - 1;
+    const uint32_t q = (uint32_t)s0 + (uint32_t)lane;
+    const uint32_t c0 = q == 0 ? 0u : (q - 1 < n32 ? q - 1 : n32 - 1);
+    const uint32_t c1 = q < n32 ? q : n32 - 1;
     *x0 = ld(a.seg_end + c0);
     *x1 = ld(a.seg_end + c1);
     *rr = ld(a.seg_rs + c1);
   };
   auto window = [&](uint64_t s0, uint32_t x0, uint32_t x1, uint32_t rr, uint32_t* st, uint32_t* en, uint32_t* r) {
-    const int64_t i = (int64_t)s0 - 1 + lane;
-    *st = i < 0 ? 0u : ((uint64_t)i < n ? x0 : 0xFFFFFFFFu);
-    *en = (uint64_t)(i + 1) < n ? x1 : 0xFFFFFFFFu;
-    *r = (uint64_t)(i + 1) < n ? rr : 0u;
+    const uint32_t q = (uint32_t)s0 + (uint32_t)lane;
+    *st = q == 0 ? 0u : (q - 1 < n32 ? x0 : 0xFFFFFFFFu);
+    *en = q < n32 ? x1 : 0xFFFFFFFFu;
+    *r = q < n32 ? rr : 0u;
   };
   const typename WType<WB>::T* const wcol = static_cast<const typename WType<WB>::T*>(a.wcol);
+  // the WHERE `lo <= x <= hi` (!= where_neg) over a column of at most 4 bytes, as one 32-bit
+  // compare: the bounds clamped to int32 (the values' range), an empty range as the full range
+  // with the negation flipped, then (uint32)(x - lo) <= hi - lo
+  int64_t wlo = a.lo, whi = a.hi;
+  bool wneg = a.where_neg != 0;
+  if (wlo < INT32_MIN) wlo = INT32_MIN;
+  if (whi > INT32_MAX) whi = INT32_MAX;
+  if (wlo > whi) {
+    wlo = INT32_MIN;
+    whi = INT32_MAX;
+    wneg = !wneg;
+  }
+  const uint32_t wbase = (uint32_t)(int32_t)wlo, wspan = (uint32_t)(whi - wlo);
   // rows of one tile at `region`, in item order (ballots of the pass masks).  One predicated
   // store per item slot, none skipped by a branch: the count of memory instructions after the
   // tile's loads is fixed, so the wait for those loads is vmcnt(FV * nyields) and never waits for
@@ -132,7 +129,8 @@ k_final_dst(FinalDstArgs a) {
     for (int i = 0; i < FV; ++i) {
       const bool pass = (pm >> i) & 1u;
       const unsigned long long bal = __ballot(pass);
-      const uint64_t row = region + off + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+      const uint64_t row = region + off + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
       off += (uint32_t)__popcll(bal);
       if constexpr (ONE) {
         if (pass) a.out[0][row] = dv[i];
@@ -159,29 +157,38 @@ k_final_dst(FinalDstArgs a) {
     }
     stage(a0, &e_pre, &f_pre, &r_pre);
   }
-  uint32_t tag = 0;
+  // lanes at or below this one: the popcount mask of an item's own head word
+  const unsigned long long le = ~0ull >> (63 - lane);
   for (; t < ntiles; t += g) {
-    if (++tag == (1u << (32 - HEAD_BITS))) {   // (unreachable in practice: 2^23 tiles on one wave)
-      for (int k = lane; k < TILE; k += 64) sHead[k] = 0;
-      tag = 1;
-    }
     const uint64_t d0 = t * TILE;
     const uint64_t d1 = d0 + TILE < npath ? d0 + TILE : npath;
-    const uint32_t b0 = (uint32_t)(d0 - a0), b1 = (uint32_t)(d1 - a1);
-    const int na = (int)(a1 - a0);
+    // a split that does not describe this tile (stale list memory) skips it and fails the query
+    // (SPLIT_BAD) instead of indexing out of bounds
+    const bool bad = !(a0 <= a1 && a1 <= n && a1 - a0 <= d1 - d0 && d1 - a1 <= total && d0 - a0 <= d1 - a1);
+    if (bad && lane == 0) atomicOr(a.err_flag, SPLIT_BAD);
+    const uint32_t b0 = bad ? 0u : (uint32_t)(d0 - a0), b1 = bad ? 0u : (uint32_t)(d1 - a1);
+    const int na = bad ? 0 : (int)(a1 - a0);
     const int nb = (int)(b1 - b0);
-    // ---- heads and deltas of the window's entries 0..na (64 at a time; past the first 64 —
-    //      tiles of many low-degree entries — loaded here)
+    // ---- head bits and deltas of the window's entries 0..na that have edges in the tile (64
+    //      at a time; past the first 64 — tiles of many low-degree entries — loaded here).  The
+    //      previous tile's mask reads are earlier LDS instructions of this wave: in order
+    if (lane < FV) sMask[lane] = 0;
+    uint32_t heads = 0;
     for (int c = 0; c * 64 <= na; ++c) {   // (wave-uniform)
       const int s = c * 64 + lane;
       uint32_t x0 = e_pre, x1 = f_pre, rr = r_pre, st, en, rs;
       if (c > 0) stage(a0 + (uint64_t)c * 64, &x0, &x1, &rr);
       window(a0 + (uint64_t)c * 64, x0, x1, rr, &st, &en, &rs);
-      if (s <= na) {
-        sDelta[s] = rs - st;
-        const uint32_t lo = st > b0 ? st : b0, hi = en < b1 ? en : b1;
-        if (lo < hi) sHead[lo - b0] = (tag << HEAD_BITS) | (uint32_t)s;
+      const uint32_t lo = st > b0 ? st : b0, hi = en < b1 ? en : b1;
+      const bool head = s <= na && lo < hi;
+      const unsigned long long hb = __ballot(head);
+      if (head) {
+        const uint32_t p = lo - b0;   // < nb <= TILE
+        sDelta[heads + 1 + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(hb >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)hb, 0u))] = rs - st;
+        atomicOr(&sMask[p >> 6], 1ull << (p & 63));
       }
+      heads += (uint32_t)__popcll(hb);
     }
     // prefetch tile t + g's window and tile t + 2g's split
     const uint64_t na0 = n0, na1 = n1;
@@ -193,18 +200,19 @@ k_final_dst(FinalDstArgs a) {
       }
     }
     wave_lds_sync();
-    // ---- every item's entry (the last head at or before it) and CSR index
+    // ---- every item's entry (the head bits at or before it: item 0 of a tile with edges is
+    //      always a head) and CSR index; an item past the tile's edges may count 0 (sDelta[0]: any
+    //      value, its index is replaced below)
     uint32_t jj[FV];
-    uint32_t carry = 0;
+    {
+      uint32_t before = 0;
 #pragma unroll
-    for (int i = 0; i < FV; ++i) {
-      const int k = i * 64 + lane;
-      const uint32_t h = sHead[k];
-      uint32_t s = (h >> HEAD_BITS) == tag ? (h & ((1u << HEAD_BITS) - 1u)) : 0u;
-      s = wave_max_scan(s);
-      s = s > carry ? s : carry;
-      carry = (uint32_t)__builtin_amdgcn_readlane((int)s, 63);
-      jj[i] = b0 + (uint32_t)k + sDelta[s];
+      for (int i = 0; i < FV; ++i) {
+        const unsigned long long m = sMask[i];
+        const uint32_t c = before + (uint32_t)__popcll(m & le);
+        before += (uint32_t)__popcll(m);
+        jj[i] = b0 + (uint32_t)(i * 64 + lane) + sDelta[c];
+      }
     }
     wave_lds_sync();   // (the next tile rewrites the window)
     // ---- loads: every item's _dst, then its WHERE value, all in flight before the first wait.
@@ -232,9 +240,11 @@ k_final_dst(FinalDstArgs a) {
     for (int i = 0; i < FV; ++i) {
       const bool act = i * 64 + lane < nb;
       bool pass = act;
-      if constexpr (WB != 0) {
+      if constexpr (WB == 8) {
         const int64_t v = (int64_t)x[i];
         pass = act & (((v >= a.lo) & (v <= a.hi)) != (a.where_neg != 0));
+      } else if constexpr (WB != 0) {
+        pass = act & (((uint32_t)(int32_t)x[i] - wbase <= wspan) != wneg);
       }
       pm |= (uint32_t)pass << i;
     }
@@ -243,7 +253,8 @@ k_final_dst(FinalDstArgs a) {
     for (int i = 0; i < FV; ++i) run += (uint32_t)__popcll(__ballot((pm >> i) & 1u));
     unsigned long long base = 0;
     if (lane == 0 && run) base = atomicAdd(&sBase, (unsigned long long)run);
-    base = __shfl(base, 0, 64);
+    base = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(base >> 32), 0) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)base, 0);
 #pragma unroll
     for (int i = 0; i < FV; ++i) pdv[i] = dv[i];
     ppm = pm;
@@ -255,6 +266,8 @@ k_final_dst(FinalDstArgs a) {
   __syncthreads();              // every wave of the workgroup has reserved its rows
   if (threadIdx.x == 0) a.blk_rows[blockIdx.x] = (uint32_t)sBase;
 }
+
+namespace {
 
 template <int WB>
 void launch_wb(const FinalDstArgs& a, bool one, unsigned grid, hipStream_t s) {

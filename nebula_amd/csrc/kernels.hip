@@ -1293,8 +1293,13 @@ k_expand(ExpandArgs a, const unsigned long long* __restrict__ acc, const uint32_
   for (; t < ntiles; t += g) {
     const uint64_t d0 = t * TV;
     const uint64_t d1 = (d0 + TV < npath) ? d0 + TV : npath;
-    const uint64_t b0 = d0 - a0, b1 = d1 - a1;
-    const int na = (int)(a1 - a0), nb = (int)(b1 - b0);
+    // a split read from memory must describe this tile (entries within the list, in order, no more
+    // of them than the tile has items, its edges within the list's): a stale one skips the tile and
+    // fails the query (SPLIT_BAD) instead of indexing out of bounds
+    const bool bad = !(a0 <= a1 && a1 <= n && a1 - a0 <= d1 - d0 && d1 - a1 <= total && d0 - a0 <= d1 - a1);
+    if (bad && lane == 0 && fp.err_flag) atomicOr(fp.err_flag, SPLIT_BAD);
+    const uint64_t b0 = bad ? 0 : d0 - a0, b1 = bad ? 0 : d1 - a1;
+    const int na = bad ? 0 : (int)(a1 - a0), nb = bad ? 0 : (int)(b1 - b0);
 
     // the wave's window in LDS (entries past the prefetch loaded directly)
     if (lane <= na + 1) sEnd[lane] = e_pre;
@@ -2533,6 +2538,7 @@ hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, 
   a.frontier = L.ids;
   a.tsplit = set_split(w, L.set);
   FinalParams fp{};
+  fp.err_flag = &w->q->err;   // (SPLIT_BAD)
   hipEvent_t p = prof_begin(w, K_EXPAND_MARK);
   if (a.bt)
     hipLaunchKernelGGL(k_expand<MARKB>, dim3(mark_grid(n_bound, e_bound)), dim3(BLOCK), 0, w->stream, a, L.acc,
@@ -2666,13 +2672,13 @@ static FastProg detect_fast(const TypeProgram& prog, const ExpandArgs& a) {
   return f;
 }
 
-// The final step's grid: the expansion grid capped at 1920 workgroups (7.5 per CU instead of 8):
-// the room left beside the persistent FINAL workgroups lets the next queries' MARK launches run
-// alongside.  Same-box A/B on RMAT-26 with 6 queries in flight (profiles/r02_t_final_grid_ab.json):
-// 2048 -> 280-282 G edges/s, FINAL 231 us; 1920 -> 289-290, FINAL 226 us; 1792 -> 288-292;
-// 1664 -> 295-298 but FINAL 244 us.  NBG_FINAL_GRID overrides (0 = no cap).
+// The final step's grid: the expansion grid (8 workgroups per CU).  Round 2 capped it at 1920
+// (7.5 per CU) for the FINALD kernel (profiles/r02_t_final_grid_ab.json: 280-282 -> 289-290 G
+// edges/s); with k_final_dst a grid that is not a multiple of the CU count loses instead: half the
+// CUs hold one workgroup more and set the launch's time (r05_i_final_grid_sweep.txt: 1920 -> 210 us,
+// 1536 / 2048 / 2560 -> 202 us; GO 362-364 at 1920 and 2048).  NBG_FINAL_GRID caps it (0 = no cap).
 static unsigned final_grid(uint64_t n_bound, uint64_t e_bound) {
-  static const unsigned cap = getenv("NBG_FINAL_GRID") ? (unsigned)atoi(getenv("NBG_FINAL_GRID")) : 1920u;
+  static const unsigned cap = getenv("NBG_FINAL_GRID") ? (unsigned)atoi(getenv("NBG_FINAL_GRID")) : 0u;
   const unsigned g = expand_grid(n_bound, e_bound);
   return cap && cap < g ? cap : g;
 }
@@ -2776,6 +2782,7 @@ hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound,
     fa.blk_rows = fp.blk_rows;
     fa.stat_e = e_st;
     fa.stat_n = L.stat_n;
+    fa.err_flag = &w->q->err;
     const bool one = fp.nyields == 1 && fa.const_mask == 0;
     HIP_TRY(launch_final_dst(fa, fp.fast.has_where ? fp.fast.wbytes : 0, one, grid.x, w->stream));
   } else if (dst_only) {

@@ -247,6 +247,10 @@ struct DevStrings {
   unsigned long long* err_flag = nullptr;     // QState::err: an overflow ORs in ARENA_OVERFLOW
 };
 constexpr unsigned long long ARENA_OVERFLOW = 1ull << 32;   // (summed over ranks, still >= 2^32)
+// QState::err: a merge-path split read from a list did not describe a tile (entries out of the list,
+// out of order, or more than the tile holds); the tile is skipped, never read out of bounds, and
+// the query fails with NBG_E_DEVICE (summed over ranks, still >= 2^48)
+constexpr unsigned long long SPLIT_BAD = 1ull << 48;
 
 constexpr int MAX_REGS = 16;
 constexpr int MAX_PROGRAM = 256;   // instructions per query/type (WHERE + all YIELDs)
@@ -369,6 +373,7 @@ struct FinalDstArgs {
   uint32_t* blk_rows;
   unsigned long long* stat_e;
   unsigned long long* stat_n;
+  unsigned long long* err_flag;    // QState::err (SPLIT_BAD)
 };
 hipError_t launch_final_dst(const FinalDstArgs& a, int wbytes, bool one, unsigned grid, hipStream_t s);
 

@@ -506,8 +506,12 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
     }
     const uint64_t a0 = uniform64(__shfl(sp, 0, 64)), a1 = uniform64(__shfl(sp, 1, 64));
     const uint64_t d0 = t * CH_TILE, d1 = d0 + CH_TILE < npath ? d0 + CH_TILE : npath;
-    const uint64_t b0 = d0 - a0, b1 = d1 - a1;
-    const int na = (int)(a1 - a0), nb = (int)(b1 - b0);
+    // a split that does not describe this tile (stale list memory) skips it and fails the search
+    // (ChCtr::err bit 4, "device search aborted") instead of indexing out of bounds
+    const bool bad = !(a0 <= a1 && a1 <= n && a1 - a0 <= d1 - d0 && d1 - a1 <= total && d0 - a0 <= d1 - a1);
+    if (bad && lane == 0) atomicOr(&C.err, 4ull);
+    const uint64_t b0 = bad ? 0 : d0 - a0, b1 = bad ? 0 : d1 - a1;
+    const int na = bad ? 0 : (int)(a1 - a0), nb = bad ? 0 : (int)(b1 - b0);
     // the tile's window: sEnd[k] = seg_end[a0 - 1 + k], sRs[k] = seg_rs[a0 + k]
     for (int kk = lane; kk <= na + 1; kk += 64) {
       const int64_t e = (int64_t)a0 - 1 + kk;
