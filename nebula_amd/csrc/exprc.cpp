@@ -484,19 +484,48 @@ struct Ctx {
     if (c.is_const) return {Piece{PC_CONST, -1, c.const_str}};
     return {Piece{PC_DICT, c.reg, {}}};
   }
+  // the lowest register the pieces read (views: their arguments' and inner lists' too)
   static int low_reg(const std::vector<Piece>& ps) {
     int r = -1;
-    for (auto& p : ps)
-      if (p.reg >= 0 && (r < 0 || p.reg < r)) r = p.reg;
+    auto take = [&r](int q) {
+      if (q >= 0 && (r < 0 || q < r)) r = q;
+    };
+    for (auto& p : ps) {
+      take(p.reg);
+      take(p.reg_b);
+      take(low_reg(p.inner));
+      take(low_reg(p.pad));
+    }
     return r;
   }
+  // the longest text a piece list can spell (UINT64_MAX: unbounded)
+  uint64_t bound_of(const std::vector<Piece>& ps) const {
+    uint64_t most = 0;
+    for (const Piece& p : ps) {
+      const uint64_t b = p.kind == PC_CONST ? p.text.size() : p.kind == PC_INT ? 20 : p.kind == PC_BOOL ? 5
+                       : p.kind == PC_VIEW ? p.bound : env.max_dict_len;
+      most = b > UINT64_MAX - most ? UINT64_MAX : most + b;
+    }
+    return most;
+  }
   // header entry {d = pieces, aux = first piece}, the pieces {op = kind, d = reg, aux = byte offset
-  // of a constant's bytes from the data's start, imm = its length}, then the constants' bytes
+  // of a constant's bytes from the data's start, imm = its length}, then the constants' bytes.  A
+  // view's inner and pad lists are emitted first (flat lists: a view holds no view)
   int32_t emit_pieces(const std::vector<Piece>& ps) {
     auto& D = pb.data;
+    std::vector<std::pair<int32_t, int32_t>> sub(ps.size(), {0, 0});
+    for (size_t k = 0; k < ps.size(); ++k)
+      if (ps[k].kind == PC_VIEW) sub[k] = {emit_pieces(ps[k].inner), ps[k].pad.empty() ? 0 : emit_pieces(ps[k].pad)};
     const int32_t hdr = (int32_t)D.size();
     D.push_back(Ins{0, (uint8_t)ps.size(), 0, 0, hdr + 1, 0});
-    for (auto& p : ps) D.push_back(Ins{(uint8_t)p.kind, (uint8_t)(p.reg < 0 ? 0 : p.reg), 0, 0, 0, (int64_t)p.text.size()});
+    for (size_t k = 0; k < ps.size(); ++k) {
+      const Piece& p = ps[k];
+      if (p.kind == PC_VIEW)
+        D.push_back(Ins{(uint8_t)PC_VIEW, (uint8_t)(p.reg < 0 ? 0 : p.reg), p.fn, (uint8_t)(p.reg_b < 0 ? 0 : p.reg_b),
+                        sub[k].first, (int64_t)sub[k].second | (int64_t)p.cs << 32 | (int64_t)p.oc << 34});
+      else
+        D.push_back(Ins{(uint8_t)p.kind, (uint8_t)(p.reg < 0 ? 0 : p.reg), 0, 0, 0, (int64_t)p.text.size()});
+    }
     for (size_t k = 0; k < ps.size(); ++k) {
       if (ps[k].kind != PC_CONST || ps[k].text.empty()) continue;
       const size_t at = D.size();
@@ -532,10 +561,11 @@ struct Ctx {
   }
   // a derived string as a result value: its canonical code (OP_SOUT)
   int value_reg(const Compiled& c) {
-    uint64_t most = 0;   // the longest text the pieces can spell
-    for (const Piece& p : c.pieces)
-      most += p.kind == PC_CONST ? p.text.size() : p.kind == PC_INT ? 20 : p.kind == PC_BOOL ? 5 : env.max_dict_len;
-    pb.sout_bytes += 16 + ((most + 7) & ~7ull);
+    // the longest text the pieces can spell (an unbounded one, lpad / rpad to a per-edge length,
+    // reserves the arena's cap: past it the query fails with E_OUT_OF_MEMORY)
+    const uint64_t most = std::min<uint64_t>(bound_of(c.pieces), 1ull << 40);
+    const uint64_t add = 16 + ((most + 7) & ~7ull);
+    pb.sout_bytes = add > UINT64_MAX - pb.sout_bytes ? UINT64_MAX : pb.sout_bytes + add;
     const int32_t h = emit_pieces(c.pieces);
     const int r = sink_reg(c.pieces);
     emit(OP_SOUT, r, 0, 0, h);
@@ -853,8 +883,16 @@ struct Ctx {
   // the statement as FunctionManager::get does.  Arguments are evaluated left to right before the
   // call; an argument's error is the call's error.  Constant arguments fold on the host with the
   // reference's bodies (fm_eval); otherwise the call is a device op: the double math, hash,
-  // length, strcasecmp, rand32 / rand64 and now.  The string-valued functions (lower, upper, trim,
-  // ltrim, rtrim, left, right, lpad, rpad, substr) run on the device only over constants.
+  // length, strcasecmp, rand32 / rand64 and now; the string-valued functions (lower, upper, trim,
+  // ltrim, rtrim, left, right, lpad, rpad, substr) become PC_VIEW pieces of a derived string (one
+  // level: a string function over another's per-edge result is NBG_E_UNSUPPORTED).
+  static int view_fn(const std::string& f) {
+    static const char* const names[] = {"lower", "upper", "trim", "ltrim", "rtrim", "left", "right", "lpad", "rpad",
+                                        "substr"};
+    for (int i = 0; i < 10; ++i)
+      if (f == names[i]) return i;
+    return -1;
+  }
   int32_t function(const Node& e, Compiled* out) {
     const std::string& f = e.alias;
     const size_t n = e.kids.size();
@@ -946,6 +984,72 @@ struct Ctx {
       c.reg = push();
       emit(OP_NOW, c.reg);
       c.kind = VK_INT;
+    } else if (view_fn(f) >= 0) {
+      const uint8_t vf = (uint8_t)view_fn(f);
+      const bool pads = vf == VF_LPAD || vf == VF_RPAD;
+      const size_t nint = vf == VF_SUBSTR ? 2 : (vf == VF_LEFT || vf == VF_RIGHT || pads) ? 1 : 0;
+      if (args[0].kind != VK_STRING || (pads && args[2].kind != VK_STRING)) { *out = make_error(); return NBG_OK; }
+      for (size_t i = 1; i <= nint; ++i)
+        if (args[i].derived || args[i].kind != VK_INT) { *out = make_error(); return NBG_OK; }   // asInt
+      Piece v;
+      v.kind = PC_VIEW;
+      v.fn = vf;
+      v.inner = pieces_of(args[0]);
+      if (pads) v.pad = pieces_of(args[2]);
+      bool nested = false;
+      for (const auto* l : {&v.inner, &v.pad})
+        for (const Piece& p : *l) nested = nested || p.kind == PC_VIEW;
+      const bool casefn = vf == VF_LOWER || vf == VF_UPPER;
+      if (nested && casefn) {
+        // lower / upper over a list holding views: every byte mapped.  Runs of flat pieces become
+        // case views; a view keeps its function and gets the map over all its bytes (pads too)
+        std::vector<Piece> mapped, run;
+        auto flush = [&] {
+          if (run.empty()) return;
+          Piece w;
+          w.kind = PC_VIEW;
+          w.fn = vf;
+          w.inner = std::move(run);
+          w.bound = bound_of(w.inner);
+          mapped.push_back(std::move(w));
+          run.clear();
+        };
+        for (Piece& p : v.inner) {
+          if (p.kind != PC_VIEW) {
+            run.push_back(std::move(p));
+            continue;
+          }
+          flush();
+          p.oc = vf == VF_LOWER ? 1 : 2;
+          mapped.push_back(std::move(p));
+        }
+        flush();
+        *out = derived_of(std::move(mapped));
+        return NBG_OK;
+      }
+      bool pad_views = false;
+      for (const Piece& p : v.pad) pad_views = pad_views || p.kind == PC_VIEW;
+      if (nested && !pad_views && v.inner.size() == 1 && v.inner[0].kind == PC_VIEW && !v.inner[0].oc &&
+          (v.inner[0].fn == VF_LOWER || v.inner[0].fn == VF_UPPER)) {
+        // a window / trim / pad over lower(x) or upper(x): case maps keep lengths and spaces, so
+        // the window is the same over x, its bytes mapped (cs); pads stay as they are
+        Piece in = std::move(v.inner[0]);
+        v.cs = in.fn == VF_LOWER ? 1 : 2;
+        v.inner = std::move(in.inner);
+        nested = false;
+        for (const Piece& p : v.inner) nested = nested || p.kind == PC_VIEW;
+      }
+      if (nested) {
+        *err = "function `" + f + "' over another string function's per-edge result is not supported on the device";
+        return NBG_E_UNSUPPORTED;
+      }
+      if (nint >= 1) v.reg = materialize(args[1]);
+      if (nint >= 2) v.reg_b = materialize(args[2]);
+      v.bound = bound_of(v.inner);
+      if (pads) v.bound = args[1].is_const ? std::max<uint64_t>(v.bound, (uint64_t)std::max<int64_t>(args[1].const_bits, 0))
+                                           : UINT64_MAX;
+      *out = derived_of({std::move(v)});   // (its registers stay live until a sink reads it)
+      return NBG_OK;
     } else {
       *err = "function `" + f + "' over per-edge values is not supported on the device";
       return NBG_E_UNSUPPORTED;

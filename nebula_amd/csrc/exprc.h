@@ -54,12 +54,22 @@ struct CompileEnv {
 };
 
 // One piece of a derived string (a STRING value built on the device: concatenation, casts to
-// string): its bytes are those of a dictionary string (register holding a code), of an INT
-// register in decimal, of a BOOL register ("true" / "false"), or of a constant.
+// string, string functions): its bytes are those of a dictionary string (register holding a
+// code), of an INT register in decimal, of a BOOL register ("true" / "false"), of a constant, or
+// (PC_VIEW) a FunctionManager string function over an inner piece list without views: a window of
+// its bytes, case-mapped, between pad bytes drawn cyclically from a second list.
 struct Piece {
   PieceKind kind;
   int reg = -1;
-  std::string text;   // PC_CONST
+  std::string text;            // PC_CONST
+  // PC_VIEW: the function (ViewFn), its INT arguments' registers (-1: none), the inner list and
+  // the pad list (lpad / rpad)
+  uint8_t fn = 0;
+  uint8_t cs = 0;              // a case map of the inner bytes merged into a window function (1 lower, 2 upper)
+  uint8_t oc = 0;              // a case map of every byte, pads included (an outer lower / upper)
+  int reg_b = -1;
+  std::vector<Piece> inner, pad;
+  uint64_t bound = 0;          // the longest text it can spell (UINT64_MAX: unbounded)
 };
 
 // Result of compiling one expression for one edge type.

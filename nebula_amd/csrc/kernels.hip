@@ -496,6 +496,7 @@ __device__ __forceinline__ PieceView piece_view(const Ins& pc, const char* dbase
       break;
     case PC_CONST: v.p = dbase + pc.aux; v.len = (uint32_t)pc.imm; break;
     case PC_BOOL: v.p = kTrueFalse + (x ? 0 : 4); v.len = x ? 4u : 5u; break;
+    case PC_VIEW: bad = true; break;   // (a view inside a flat list: never emitted)
     default: {   // PC_INT: folly::to<std::string>(int64_t)
       v.p = nullptr;
       v.neg = x < 0;
@@ -518,7 +519,8 @@ __device__ __forceinline__ uint32_t piece_byte(const PieceView& v, uint32_t i) {
   return '0' + (uint32_t)((v.u / kPow10[v.nd - 1 - i]) % 10);
 }
 
-struct StrIter {
+// A flat piece list (no views): the inner list of a view, a pad list
+struct FlatIter {
   const Ins* list;   // the pieces
   const char* dbase;
   int n, k;
@@ -526,8 +528,8 @@ struct StrIter {
   PieceView v;
 };
 
-__device__ __forceinline__ void str_open(StrIter& it, const Ins* data, int32_t hdr, const DevStrings& S,
-                                         const int64_t* regs, int tid, bool& bad) {
+__device__ __forceinline__ void flat_open(FlatIter& it, const Ins* data, int32_t hdr, const DevStrings& S,
+                                          const int64_t* regs, int tid, bool& bad) {
   const Ins h = data[hdr];
   it.list = data + h.aux;
   it.dbase = reinterpret_cast<const char*>(data);
@@ -539,7 +541,7 @@ __device__ __forceinline__ void str_open(StrIter& it, const Ins* data, int32_t h
 }
 
 // the next byte (-1 at the end)
-__device__ __forceinline__ int str_next(StrIter& it, const DevStrings& S, const int64_t* regs, int tid, bool& bad) {
+__device__ __forceinline__ int flat_next(FlatIter& it, const DevStrings& S, const int64_t* regs, int tid, bool& bad) {
   while (it.i >= it.v.len) {
     if (++it.k >= it.n) return -1;
     it.v = piece_view(it.list[it.k], it.dbase, S, regs, tid, bad);
@@ -548,11 +550,238 @@ __device__ __forceinline__ int str_next(StrIter& it, const DevStrings& S, const 
   return (int)piece_byte(it.v, it.i++);
 }
 
+__device__ void flat_skip(FlatIter& it, uint64_t m, const DevStrings& S, const int64_t* regs, int tid, bool& bad) {
+  while (m) {
+    if (it.i < it.v.len) {
+      const uint32_t d = (uint64_t)(it.v.len - it.i) < m ? it.v.len - it.i : (uint32_t)m;
+      it.i += d;
+      m -= d;
+    } else {
+      if (++it.k >= it.n) return;
+      it.v = piece_view(it.list[it.k], it.dbase, S, regs, tid, bad);
+      it.i = 0;
+    }
+  }
+}
+
+__device__ uint64_t flat_len(const Ins* data, int32_t hdr, const DevStrings& S, const int64_t* regs, int tid,
+                             bool& bad) {
+  const Ins h = data[hdr];
+  uint64_t n = 0;
+  for (int k = 0; k < h.d; ++k) n += piece_view(data[h.aux + k], reinterpret_cast<const char*>(data), S, regs, tid, bad).len;
+  return n;
+}
+
+// byte m of a flat list (a pad: read cyclically, one piece walk per byte; pads are short)
+__device__ uint32_t flat_byte_at(const Ins* data, int32_t hdr, uint64_t m, const DevStrings& S, const int64_t* regs,
+                                 int tid, bool& bad) {
+  const Ins h = data[hdr];
+  for (int k = 0; k < h.d; ++k) {
+    const PieceView v = piece_view(data[h.aux + k], reinterpret_cast<const char*>(data), S, regs, tid, bad);
+    if (m < v.len) return piece_byte(v, (uint32_t)m);
+    m -= v.len;
+  }
+  return 0;
+}
+
+// A PC_VIEW piece (FunctionManager.cpp:249-409 over its inner list's bytes, L of them): `pre` pad
+// bytes, the inner bytes [w0, w0 + mid) case-mapped, `post` pad bytes.  The reference's failures
+// (lpad / rpad to a negative length: a size_t that never stops padding; an empty pad) and results
+// over 2^31 bytes set `bad` (an evaluation error).
+struct ViewGeom {
+  uint64_t w0, pre, mid, post, padlen;
+  uint32_t cs;   // the inner bytes: 0 as is, 1 tolower, 2 toupper ("C" locale: ASCII letters)
+  uint32_t oc;   // every byte, pads included (an outer lower / upper over this view)
+};
+
+__device__ ViewGeom view_geom(const Ins& pc, const Ins* data, const DevStrings& S, const int64_t* regs, int tid,
+                              bool& bad) {
+  ViewGeom g{0, 0, 0, 0, 0, (uint32_t)(pc.imm >> 32) & 3u, (uint32_t)(pc.imm >> 34) & 3u};
+  const uint64_t L = flat_len(data, pc.aux, S, regs, tid, bad);
+  const int32_t padh = (int32_t)(pc.imm & 0xFFFFFFFFll);
+  const int64_t na = regs[pc.d * BLOCK + tid], nb = regs[pc.b * BLOCK + tid];
+  g.mid = L;
+  switch (pc.a) {
+    case VF_LOWER: g.cs = 1; break;
+    case VF_UPPER: g.cs = 2; break;
+    case VF_TRIM:
+    case VF_LTRIM:
+    case VF_RTRIM: {   // find_first_not_of(" ") / find_last_not_of(" ") + 1
+      FlatIter it;
+      flat_open(it, data, pc.aux, S, regs, tid, bad);
+      uint64_t first = L, last = 0;
+      for (uint64_t k = 0; k < L; ++k)
+        if (flat_next(it, S, regs, tid, bad) != ' ') {
+          if (first == L) first = k;
+          last = k + 1;
+        }
+      g.w0 = pc.a == VF_RTRIM ? 0 : first;
+      const uint64_t end = pc.a == VF_LTRIM ? L : last;
+      g.mid = end > g.w0 ? end - g.w0 : 0;
+      break;
+    }
+    case VF_LEFT: g.mid = na <= 0 ? 0 : ((uint64_t)na < L ? (uint64_t)na : L); break;
+    case VF_RIGHT: {
+      const uint64_t k = na <= 0 ? 0 : ((uint64_t)na < L ? (uint64_t)na : L);
+      g.w0 = L - k;
+      g.mid = k;
+      break;
+    }
+    case VF_LPAD:
+    case VF_RPAD: {
+      if (na < 0) {
+        bad = true;
+        g.mid = 0;
+        break;
+      }
+      if ((uint64_t)na < L) {
+        g.mid = (uint64_t)na;
+        break;
+      }
+      const uint64_t need = (uint64_t)na - L;
+      g.padlen = flat_len(data, padh, S, regs, tid, bad);
+      if (need && !g.padlen) {
+        bad = true;
+        break;
+      }
+      if (pc.a == VF_LPAD) g.pre = need;
+      else g.post = need;
+      break;
+    }
+    default: {   // VF_SUBSTR
+      const uint64_t ast = na == INT64_MIN ? 1ull << 63 : (uint64_t)(na < 0 ? -na : na);
+      if (ast > L || nb <= 0 || na == 0) {
+        g.mid = 0;
+      } else {
+        g.w0 = na > 0 ? (uint64_t)na - 1 : L - ast;
+        const uint64_t room = L - g.w0;
+        g.mid = (uint64_t)nb < room ? (uint64_t)nb : room;
+      }
+    }
+  }
+  if (g.pre + g.mid + g.post >= (1ull << 31)) {
+    bad = true;
+    g.pre = g.post = 0;
+    g.mid = 0;
+  }
+  return g;
+}
+
+// A view being read: out of line (view_open / view_next / view_len are calls) so that the string
+// ops that never meet a view keep the registers they had; the inlined paths only test a piece's
+// kind.  `bad` travels in return values (no escaping reference).
+struct ViewIter {
+  FlatIter in;  // the inner list, positioned at the window
+  int32_t padh;
+  uint32_t padlen, pre, mid, total, pos, cs, oc;
+};
+
+// false: bad
+__device__ __noinline__ bool view_open(ViewIter* w, const Ins pc, const Ins* data, const DevStrings* S,
+                                       const int64_t* regs, int tid) {
+  bool bad = false;
+  const ViewGeom g = view_geom(pc, data, *S, regs, tid, bad);
+  flat_open(w->in, data, pc.aux, *S, regs, tid, bad);
+  flat_skip(w->in, g.w0, *S, regs, tid, bad);
+  w->padh = (int32_t)(pc.imm & 0xFFFFFFFFll);
+  w->padlen = (uint32_t)g.padlen;
+  w->pre = (uint32_t)g.pre;
+  w->mid = (uint32_t)g.mid;
+  w->total = (uint32_t)(g.pre + g.mid + g.post);
+  w->pos = 0;
+  w->cs = g.cs;
+  w->oc = g.oc;
+  return !bad;
+}
+
+// the view's next byte; -1 at its end, -2 bad
+__device__ __noinline__ int view_next(ViewIter* w, const Ins* data, const DevStrings* S, const int64_t* regs,
+                                      int tid) {
+  if (w->pos >= w->total) return -1;
+  bool bad = false;
+  const uint32_t p = w->pos++;
+  int c;
+  if (p < w->pre) {
+    c = (int)flat_byte_at(data, w->padh, p % w->padlen, *S, regs, tid, bad);
+  } else if (p - w->pre < w->mid) {
+    c = flat_next(w->in, *S, regs, tid, bad);
+    if (c < 0) c = 0;
+    if (w->cs == 1 && c >= 'A' && c <= 'Z') c += 32;
+    if (w->cs == 2 && c >= 'a' && c <= 'z') c -= 32;
+  } else {
+    c = (int)flat_byte_at(data, w->padh, (p - w->pre - w->mid) % w->padlen, *S, regs, tid, bad);
+  }
+  if (w->oc == 1 && c >= 'A' && c <= 'Z') c += 32;
+  if (w->oc == 2 && c >= 'a' && c <= 'z') c -= 32;
+  return bad ? -2 : c;
+}
+
+// the view's length; -1: bad
+__device__ __noinline__ int64_t view_len(const Ins pc, const Ins* data, const DevStrings* S, const int64_t* regs,
+                                         int tid) {
+  bool bad = false;
+  const ViewGeom g = view_geom(pc, data, *S, regs, tid, bad);
+  return bad ? -1 : (int64_t)(g.pre + g.mid + g.post);
+}
+
+// A derived string's piece list streamed byte by byte, views included
+struct StrIter {
+  FlatIter o;   // the list; its current piece when not in a view
+  ViewIter vw;
+  const Ins* data;
+  bool view;
+};
+
+__device__ __forceinline__ void str_open(StrIter& it, const Ins* data, int32_t hdr, const DevStrings&,
+                                         const int64_t*, int, bool&) {
+  const Ins h = data[hdr];
+  it.o.list = data + h.aux;
+  it.o.dbase = reinterpret_cast<const char*>(data);
+  it.o.n = h.d;
+  it.o.k = -1;
+  it.o.i = 0;
+  it.o.v = PieceView{it.o.dbase, 0, 0, 0, 0};
+  it.data = data;
+  it.view = false;
+}
+
+// the next byte (-1 at the end)
+__device__ __forceinline__ int str_next(StrIter& it, const DevStrings& S, const int64_t* regs, int tid, bool& bad) {
+  for (;;) {
+    if (it.view) {
+      const int c = view_next(&it.vw, it.data, &S, regs, tid);
+      if (c >= 0) return c;
+      bad = bad || c == -2;
+      it.view = false;
+    } else if (it.o.i < it.o.v.len) {
+      return (int)piece_byte(it.o.v, it.o.i++);
+    }
+    if (++it.o.k >= it.o.n) return -1;
+    const Ins pc = it.o.list[it.o.k];
+    if (pc.op == PC_VIEW) {
+      bad = !view_open(&it.vw, pc, it.data, &S, regs, tid) || bad;
+      it.view = true;
+    } else {
+      it.o.v = piece_view(pc, it.o.dbase, S, regs, tid, bad);
+      it.o.i = 0;
+    }
+  }
+}
+
 __device__ __forceinline__ uint64_t str_len(const Ins* data, int32_t hdr, const DevStrings& S, const int64_t* regs,
                                             int tid, bool& bad) {
   const Ins h = data[hdr];
   uint64_t n = 0;
-  for (int k = 0; k < h.d; ++k) n += piece_view(data[h.aux + k], reinterpret_cast<const char*>(data), S, regs, tid, bad).len;
+  for (int k = 0; k < h.d; ++k) {
+    const Ins pc = data[h.aux + k];
+    if (pc.op == PC_VIEW) {
+      const int64_t l = view_len(pc, data, &S, regs, tid);
+      bad = bad || l < 0;
+      n += l < 0 ? 0 : (uint64_t)l;
+    } else {
+      n += piece_view(pc, reinterpret_cast<const char*>(data), S, regs, tid, bad).len;
+    }
+  }
   return n;
 }
 

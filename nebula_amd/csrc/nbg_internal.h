@@ -206,7 +206,12 @@ struct Ins {
 };
 static_assert(sizeof(Ins) == 16, "Ins layout");
 // piece kinds of a derived string's piece list (exprc.cpp emit_pieces, kernels.hip piece_view)
-enum PieceKind : uint8_t { PC_DICT = 1, PC_INT = 2, PC_BOOL = 3, PC_CONST = 4 };
+enum PieceKind : uint8_t { PC_DICT = 1, PC_INT = 2, PC_BOOL = 3, PC_CONST = 4, PC_VIEW = 5 };
+// PC_VIEW's function (FunctionManager.cpp:249-409): piece {op PC_VIEW, d = the first INT argument's
+// register, a = ViewFn, b = the second's (substr's length), aux = the inner list's header, imm =
+// the pad list's header (lpad / rpad)}
+enum ViewFn : uint8_t { VF_LOWER = 0, VF_UPPER, VF_TRIM, VF_LTRIM, VF_RTRIM, VF_LEFT, VF_RIGHT, VF_LPAD, VF_RPAD,
+                        VF_SUBSTR };
 
 // A derived string's code in a result / register: the tag bit plus a 62-bit content hash, so
 // equal strings have equal codes (YIELD DISTINCT, the partitioned owner exchange); its bytes are

@@ -72,6 +72,8 @@ struct ChList {
 struct ChSnap {         // the search state before one step launch
   uint32_t phase, kf, kb, dir, met, L, bstep, err;
   uint32_t cur[2];                     // current list of each side (F0/F1, B0/B1)
+  uint32_t both;                       // BFS: this step expands both sides (ChQ::both_items)
+  uint32_t spare;
   unsigned long long cnt[2];           // packed (entries << 32 | edges) of each side's current list
   unsigned long long fprev;            // ... of the forward list one level back
   unsigned long long bcnt;             // ... of the B-set step's source list
@@ -87,8 +89,10 @@ struct ChSnap {         // the search state before one step launch
 // no set-up launch, and nothing of the current query (whose workgroups may still be reading its
 // own set) is touched.
 struct ChCtr {
-  unsigned long long lacc[CH_MAXS];    // packed output list of step launch i
-  unsigned long long lmeet[CH_MAXS];   // meet vertices found by step launch i
+  unsigned long long lacc[CH_MAXS];    // packed output list of step launch i (both sides: forward's)
+  unsigned long long lmeet[CH_MAXS];   // meet vertices found by step launch i (both sides: at position kf)
+  unsigned long long lacc2[CH_MAXS];   // both sides: the backward output list
+  unsigned long long lmeet2[CH_MAXS];  // both sides: meets at position kf + 1 (claimed by both sides)
   unsigned long long macc;             // packed meet list (over in-edges)
   unsigned long long err;              // 1 reconstruction failure, 3 list overflow
   unsigned long long hlaunch;          // greedy launches that did work
@@ -149,18 +153,73 @@ struct ChQ {
                                        // by workgroup 0 alone, which goes on with the next step (0: off)
   uint32_t par;                        // the query's counter set (ChState::c)
   uint32_t tag;                        // this batch of launches (ChOut::tag: which batch stored)
+  uint32_t both_items;                 // a BFS level expands both sides when each has at most this many
+                                       // items (entries + edges) and UPTO allows two levels (0: never)
 };
+
+// Both sides in one launch: while both frontiers are small a level's launch costs the same for one
+// side or two (its time is the dependent chain of one tile, not the items), so two levels take one
+// launch.  Forward claims level kf + 1, backward level kb + 1, at once.  The shortest length is
+// kf + kb + 1 when a vertex at forward level kf gets backward level kb + 1 (the backward claims test
+// the forward labels, which this launch does not write at level <= kf: a complete, race-free meet
+// set at position kf; every such path also has one); otherwise kf + kb + 2 when a vertex is claimed
+// by both sides in this launch — each claimer re-reads the other side's label after its own CAS
+// returned, so of two claims at least one sees the other (both CAS before either re-read): the meet
+// set at position kf + 1 is complete too (LAB_M stamps only; the first B-set step then pulls).
+__host__ __device__ __forceinline__ uint32_t both_next(const ChSnap& s, uint32_t upto, uint32_t items) {
+  const unsigned long long a = (s.cnt[0] >> 32) + (s.cnt[0] & 0xFFFFFFFFull);
+  const unsigned long long b = (s.cnt[1] >> 32) + (s.cnt[1] & 0xFFFFFFFFull);
+  return items && s.kf + s.kb + 2 <= upto && a <= items && b <= items ? 1u : 0u;
+}
 
 // The state after step launch `i` (snapshot p before it, its results from st): every step launch
 // and the host derive it the same way.
 __host__ __device__ __forceinline__ ChSnap ch_advance(const ChSnap& p, unsigned long long out, unsigned long long meets,
-                                              unsigned long long macc, unsigned long long err, uint32_t upto) {
+                                              unsigned long long macc, unsigned long long err, uint32_t upto,
+                                              unsigned long long out2, unsigned long long meets2, uint32_t items) {
   ChSnap s = p;
   constexpr unsigned long long M32 = 0xFFFFFFFFull;
   auto bytes_of = [](unsigned long long src, unsigned long long dst) {
     return 12ull * (src >> 32) + 4ull * (src & M32) + 4ull * (dst >> 32);
   };
-  if (p.phase == PH_BFS) {
+  s.both = 0;
+  if (p.phase == PH_BFS && p.both) {   // both sides expanded: forward `out`, backward `out2`
+    s.abytes += bytes_of(p.cnt[0], out) + bytes_of(p.cnt[1], out2);
+    s.edges += (p.cnt[0] & M32) + (p.cnt[1] & M32);
+    s.levels += 2;
+    // the backward side advanced in every case
+    s.cnt[1] = out2;
+    s.cur[1] ^= 1u;
+    ++s.kb;
+    if (err) {
+      s.phase = PH_DONE;
+      s.err = 1;
+    } else if (meets) {   // length kf + kb (+1): meet set at forward position kf, listed (push)
+      s.met = 1;
+      s.L = s.kf + s.kb;
+      s.bstep = 0;
+      s.bcnt = macc;
+      s.fprev = M32;      // (the forward side's other list now holds level kf + 1: no pull)
+      s.phase = s.kf >= 2 ? PH_BSET : PH_DONE;
+    } else {
+      s.fprev = p.cnt[0];
+      s.cnt[0] = out;
+      s.cur[0] ^= 1u;
+      ++s.kf;
+      if (meets2) {       // length kf + kb (+2): meet set at position kf + 1, LAB_M stamps only (pull)
+        s.met = 1;
+        s.L = s.kf + s.kb;
+        s.bstep = 0;
+        s.bcnt = M32;
+        s.phase = s.kf >= 2 ? PH_BSET : PH_DONE;
+      } else if ((out >> 32) == 0 || (out2 >> 32) == 0 || s.kf + s.kb >= upto) {
+        s.phase = PH_DONE;
+      } else {
+        s.dir = (s.cnt[0] & M32) <= (s.cnt[1] & M32) ? 0u : 1u;
+        s.both = both_next(s, upto, items);
+      }
+    }
+  } else if (p.phase == PH_BFS) {
     // (constant indices only: a runtime index into the snapshot's arrays puts it in scratch memory)
     const bool fwd = p.dir == 0;
     const unsigned long long pc = fwd ? p.cnt[0] : p.cnt[1];
@@ -190,6 +249,7 @@ __host__ __device__ __forceinline__ ChSnap ch_advance(const ChSnap& p, unsigned 
       s.phase = PH_DONE;   // a side has no further edges, or UPTO reached: no path
     } else {
       s.dir = (s.cnt[0] & 0xFFFFFFFFull) <= (s.cnt[1] & 0xFFFFFFFFull) ? 0u : 1u;
+      s.both = both_next(s, upto, items);
     }
   } else if (p.phase == PH_BSET) {
     // (the source list of this B-set step, as ch_step chose it: pull from the forward level or push)
@@ -358,7 +418,8 @@ __device__ __forceinline__ void wave_append(const ChArgs& A, const ChList& L, un
 __device__ __forceinline__ ChSnap snap_for(const ChState* st, const ChQ& q, int i) {
   if (i == 0) return st->snap[0];
   const ChCtr& C = st->c[q.par];
-  return ch_advance(st->snap[i - 1], C.lacc[i - 1], C.lmeet[i - 1], C.macc, C.err, q.upto);
+  return ch_advance(st->snap[i - 1], C.lacc[i - 1], C.lmeet[i - 1], C.macc, C.err, q.upto, C.lacc2[i - 1],
+                    C.lmeet2[i - 1], q.both_items);
 }
 
 }  // namespace
@@ -383,6 +444,7 @@ __device__ __forceinline__ ChSnap first_snap(const ChArgs& A, const ChQ& q, ChFi
   s.dir = f->dsf <= f->dsb ? 0u : 1u;
   s.cnt[0] = (1ull << 32) | f->dsf;
   s.cnt[1] = (1ull << 32) | f->dsb;
+  s.both = s.phase == PH_BFS ? both_next(s, q.upto, q.both_items) : 0u;
   return s;
 }
 
@@ -421,7 +483,9 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
   __shared__ uint16_t sSegAll[NW][CH_TILE];
   ChState* st = A.st;
   const bool bfs = P.phase == PH_BFS;
-  // ---- this launch's lists, labels and stamps (uniform)
+  const bool both = bfs && P.both;   // forward level kf + 1 and backward level kb + 1 in one launch
+  // ---- this launch's lists, labels and stamps (uniform; a two-sided level's backward tiles switch
+  //      to the backward side's below)
   int side;              // CSR expanded
   ChList S, D;           // source list, output list
   unsigned long long scnt;
@@ -434,7 +498,7 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
   int oside;             // CSR of the output list's edge space
   bool append = true;
   if (bfs) {
-    side = (int)P.dir;
+    side = both ? 0 : (int)P.dir;
     const int src = side * 2 + (int)(side ? P.cur[1] : P.cur[0]);
     S = A.list[src];
     D = A.list[src ^ 1];
@@ -471,15 +535,24 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
   }
   const bool pull = tlab != nullptr;
   ChCtr& C = st->c[q.par];
-  unsigned long long* const out_acc = &C.lacc[i];
+  unsigned long long* out_acc = &C.lacc[i];
   // step 0: the one entry of the source list (s forward, t backward) from registers; s and t are
   // labelled level 0 of their sides (workgroup 0 stores those labels during this launch)
-  const uint32_t f_deg = first ? (side ? f0.dsb : f0.dsf) : 0u;
-  const uint32_t f_rs = first ? (side ? f0.rsb : f0.rsf) : 0u;
-  const uint32_t f_own = first ? (side ? q.t : q.s) : NO_ROW, f_other = first ? (side ? q.s : q.t) : NO_ROW;
-  const uint64_t n = scnt >> 32, total = scnt & 0xFFFFFFFFull;
+  uint32_t f_deg = first ? (side ? f0.dsb : f0.dsf) : 0u;
+  uint32_t f_rs = first ? (side ? f0.rsb : f0.rsf) : 0u;
+  uint32_t f_own = first ? (side ? q.t : q.s) : NO_ROW, f_other = first ? (side ? q.s : q.t) : NO_ROW;
+  uint64_t n = scnt >> 32, total = scnt & 0xFFFFFFFFull;
   const uint32_t* __restrict__ col = A.col[side];
-  const uint64_t npath = n + total, ntiles = (npath + CH_TILE - 1) / CH_TILE;
+  uint64_t npath = n + total, ntiles = (npath + CH_TILE - 1) / CH_TILE;
+  // a two-sided level: tiles [0, nt0) are the forward side's, [nt0, nt0 + nt1) the backward's.
+  // Meets: a backward claim of a vertex at forward level kf (l1stamp; LAB_M stamp kf, the meet list,
+  // lmeet) or a vertex both sides claim in this launch (l2other, the other side's new stamp; LAB_M
+  // stamp kf + 1, lmeet2); forward claims of vertices at backward level <= kb are no meets here
+  const uint64_t nt0 = ntiles;
+  const uint64_t nt1 = both ? (((P.cnt[1] >> 32) + (P.cnt[1] & 0xFFFFFFFFull)) + CH_TILE - 1) / CH_TILE : 0;
+  const uint32_t l1stamp = stamp_of(q.ef, P.kf), l2m = stamp_of(q.em, P.kf + 1);
+  uint32_t l2other = stamp_of(q.eb, P.kb + 1);
+  if (both) mstamp = 0;   // (forward tiles record no position-kf meets)
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t* const sEnd = sEndAll[w];
@@ -489,12 +562,42 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
   // CUs as it has tiles (up to the grid) before any CU gets a second one.  A tile's random loads
   // and atomics (8 per lane) queue at its CU, so tiles packed 4 to a workgroup had 4 waves' misses
   // in one CU's queue while most CUs idled
-  for (uint64_t t = (uint64_t)w * nblk + bid; t < ntiles; t += (uint64_t)nblk * NW) {
+  for (uint64_t tg = (uint64_t)w * nblk + bid; tg < nt0 + nt1; tg += (uint64_t)nblk * NW) {
+    uint64_t t = tg;
+    if (both && tg >= nt0 && side == 0) {   // (wave-uniform) the backward side's tiles from here on
+      t = tg - nt0;
+      side = 1;
+      const int src = 2 + (int)P.cur[1];
+      S = A.list[src];
+      D = A.list[src ^ 1];
+      scnt = P.cnt[1];
+      lab = A.lab[1];
+      epoch = q.eb;
+      stamp = stamp_of(q.eb, P.kb + 1);
+      olab = A.lab[0];
+      oepoch = q.ef;
+      mstamp = stamp_of(q.em, P.kf);
+      oside = 1;
+      out_acc = &C.lacc2[i];
+      f_deg = first ? f0.dsb : 0u;
+      f_rs = first ? f0.rsb : 0u;
+      f_own = first ? q.t : NO_ROW;
+      f_other = first ? q.s : NO_ROW;
+      n = scnt >> 32;
+      total = scnt & 0xFFFFFFFFull;
+      col = A.col[1];
+      npath = n + total;
+      ntiles = nt1;
+      l2other = stamp_of(q.ef, P.kf + 1);
+    } else if (both && side == 1) {
+      t = tg - nt0;
+    }
     uint32_t c[CH_VT];   // the vertex a claim is about: the neighbour, or (pull) the list entry
     uint32_t cm = 0, mm = 0;
     // once this level has met, its claims are not expanded again: their appends are skipped
-    // (read now, used after the claims: the load is off the critical path)
-    const unsigned long long met_now = bfs ? ld_agent(&C.lmeet[i]) : 0ull;
+    // (read now, used after the claims: the load is off the critical path).  A two-sided level
+    // runs to its end (a meet at position kf + 1 needs every claim of both sides)
+    const unsigned long long met_now = bfs && !both ? ld_agent(&C.lmeet[i]) : 0ull;
     uint64_t sp = 0;
     if (first) {   // one entry: every tile's split is 0, the last tile's end is 1
       sp = lane == 1 && (t + 1) * CH_TILE >= npath ? n : 0;
@@ -624,10 +727,36 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
         cm |= 1u << j;
       }
     }
-    if (spec) {   // meet test: the claimed vertices the other side has labelled
+    if (spec && !both) {   // meet test: the claimed vertices the other side has labelled
 #pragma unroll
       for (int j = 0; j < CH_VT; ++j)
         if (((cm >> j) & 1u) && live(sol[j], oepoch)) mm |= 1u << j;
+    } else if (both) {
+      uint32_t m2 = 0;
+#pragma unroll
+      for (int j = 0; j < CH_VT; ++j) {
+        if (!((cm >> j) & 1u)) continue;
+        uint32_t o = sol[j];
+        if (side == 1 && o == l1stamp) {   // backward level kb + 1 at forward level kf
+          mm |= 1u << j;
+          continue;
+        }
+        // claimed by the other side in this launch: seen before our claim, or re-read after it
+        if (!live(o, oepoch)) o = __hip_atomic_load(olab + c[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (o == l2other) m2 |= 1u << j;
+      }
+      if (__ballot(m2 != 0)) {
+        uint32_t n2 = 0;
+#pragma unroll
+        for (int j = 0; j < CH_VT; ++j)
+          if ((m2 >> j) & 1u) {
+            gst(A.lab[2], c[j], A.nv, l2m, 10, st);   // (both claimers may store it: the same value)
+            ++n2;
+          }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) n2 += __shfl_xor(n2, o, 64);
+        if (lane == 0) atomicAdd(&C.lmeet2[i], (unsigned long long)n2);
+      }
     }
     if (!__ballot((cm | mm) != 0)) continue;
     // appends: one packed atomic per wave and list (aggregating them per workgroup behind two
@@ -672,7 +801,9 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
 // Items (entries + edges) of the source list of step P (as ch_level picks it).
 __device__ __forceinline__ uint64_t step_items(const ChSnap& P) {
   unsigned long long c;
-  if (P.phase == PH_BFS) {
+  if (P.phase == PH_BFS && P.both) {
+    return (P.cnt[0] >> 32) + (P.cnt[0] & 0xFFFFFFFFull) + (P.cnt[1] >> 32) + (P.cnt[1] & 0xFFFFFFFFull);
+  } else if (P.phase == PH_BFS) {
     c = P.dir ? P.cnt[1] : P.cnt[0];
   } else {
     const bool pull = P.bstep == 0 && (P.fprev & 0xFFFFFFFFull) < (P.bcnt & 0xFFFFFFFFull);
@@ -731,7 +862,7 @@ __device__ __forceinline__ bool ch_step(const ChArgs& A, const ChQ& q, int i, ui
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     P = ch_advance(st->snap[j], ld_agent(&C.lacc[j]), ld_agent(&C.lmeet[j]), ld_agent(&C.macc),
-                   ld_agent(&C.err), q.upto);
+                   ld_agent(&C.err), q.upto, ld_agent(&C.lacc2[j]), ld_agent(&C.lmeet2[j]), q.both_items);
     ++j;
     if (P.phase == PH_DONE || step_items(P) > q.solo || j + 1 >= (uint32_t)CH_MAXS) break;
   }
@@ -1002,6 +1133,7 @@ struct ChainCtx {
   // NBG_SP_GRID overrides.
   unsigned grid = 256;
   uint32_t solo = 0;               // ChQ::solo (NBG_SP_SOLO items)
+  uint32_t both = 16384;           // ChQ::both_items (NBG_SP_BOTH; 0: one side per level)
   // the query in flight: what has been enqueued
   ChQ q{};
   int steps = 0, hops = 0;
@@ -1057,6 +1189,8 @@ ChainCtx* chain_create(uint64_t nv, uint64_t edge_cap, hipStream_t s, std::strin
   if (g && atoi(g) > 0) c->grid = (unsigned)atoi(g);
   const char* so = getenv("NBG_SP_SOLO");
   if (so) c->solo = (uint32_t)strtoul(so, nullptr, 10);
+  const char* bo = getenv("NBG_SP_BOTH");
+  if (bo) c->both = (uint32_t)strtoul(bo, nullptr, 10);
   hipError_t he = hipSuccess;
   auto M = [&](void** p, size_t b) { if (he == hipSuccess) he = hipMalloc(p, b); };
   for (auto& L : c->list) {
@@ -1151,7 +1285,7 @@ static hipError_t chain_prepare(ChainCtx* c, const SpTypes& fwd, const SpTypes& 
     c->args_valid = true;
   }
   c->par ^= 1u;
-  c->q = ChQ{s, t, upto, epoch, epoch, epoch, c->solo, c->par, 0};
+  c->q = ChQ{s, t, upto, epoch, epoch, epoch, c->solo, c->par, 0, c->both};
   c->steps = c->hops = 0;
   c->last_batched = false;
   ++c->queries;

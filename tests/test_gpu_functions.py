@@ -5,7 +5,8 @@ Constant calls fold on the host with the reference's bodies (ExpressionTest's Fu
 StringFunctionCall vectors: tests/test_gpu_expr.py).  Here the arguments are columns, so the
 device ops run: the double math (OP_MATH1_F / OP_MATH2_F), hash over ints, doubles, bools and
 strings (libstdc++'s _Hash_bytes restated on the device), length and strcasecmp over dictionary
-strings and derived piece lists, rand32 / rand64 and now.
+strings and derived piece lists, rand32 / rand64 and now, and the string-valued bodies (lower,
+upper, trim, ltrim, rtrim, left, right, lpad, rpad, substr) as views over piece lists.
 
 Tolerance: integer, string and hash results must be equal; the exactly rounded functions (sqrt,
 abs, floor, ceil, round) bit-exact; the transcendental ones (cbrt, exp, exp2, log*, trig, pow,
@@ -17,7 +18,7 @@ import time
 
 import pytest
 
-from nebula_amd import NbgError, _lib as L, ngql
+from nebula_amd import LocalCluster, NbgError, _lib as L, kvgen, ngql
 from nebula_amd.engine import nba_engine
 from tests.support.golden import _ulps_equal
 from tests.support.oracle import OracleError, nba_oracle
@@ -125,10 +126,87 @@ def test_rand_ranges_and_now(nba):
     assert len(kept) == len(s.execute(f'GO FROM {TD} OVER like').rows)
 
 
-def test_string_valued_functions_on_columns_unsupported(nba):
-    """lower / upper / trim / left / right / lpad / rpad / substr fold over constants; over
-    per-edge strings the engine says so (NBG_E_UNSUPPORTED) rather than return other values."""
+# the string-valued bodies over per-edge values (FunctionManager.cpp:249-409): PC_VIEW pieces of a
+# derived string, in WHERE, YIELD and under other string ops (length, hash, strcasecmp, compare,
+# concatenation, DISTINCT); the bodies' failures (asInt / asString of the wrong kind, a negative
+# or pad-less padding) fail the query on both sides
+STRING_FNS = [
+    f'GO FROM {TD}, {TP} OVER like YIELD lower($$.player.name) AS a, upper($^.player.name) AS b, '
+    f'(string)upper((string)like.likeness) AS c',
+    f'GO FROM {TD}, {TP} OVER like YIELD left($$.player.name, 3) AS a, (string)right($$.player.name, like.likeness / 10) AS b, '
+    f'left($$.player.name, 0) AS c, right($$.player.name, 100) AS d, left($^.player.name, -2) AS e',
+    f'GO FROM {TD}, {TP} OVER like YIELD substr($$.player.name, 2, 4) AS a, substr($$.player.name, -3, 2) AS b, '
+    f'substr($$.player.name, 0, 1) AS c, substr($$.player.name, 100, 1) AS d, substr($$.player.name, 1, -1) AS e, '
+    f'substr($$.player.name, -100, 3) AS f, (string)substr($$.player.name, like.likeness / 20, like.likeness / 30) AS g',
+    f'GO FROM {TD}, {TP} OVER like YIELD lpad($$.player.name, 20, "*-") AS a, (string)rpad($$.player.name, like.likeness / 5, "ab") AS b, '
+    f'lpad($$.player.name, 3, "x") AS c, rpad($^.player.name, 0, "") AS d, lpad($$.player.name, like.likeness / 4, $^.player.name) AS e',
+    f'GO FROM {TD}, {TP} OVER like YIELD trim("  " + $$.player.name + "   ") AS a, ltrim(" " + $$.player.name + " ") AS b, '
+    f'rtrim(" " + $$.player.name + " ") AS c, trim("   ") AS d, trim(lower(" a B ")) AS e, '
+    f'ltrim("  " + $^.player.name) AS f',
+    f'GO FROM {TD}, {TP} OVER like YIELD (int)length(upper($$.player.name)) AS a, (int)hash(lower($$.player.name)) AS b, '
+    f'(int)strcasecmp(upper($$.player.name), lower($$.player.name)) AS c, lower($^.player.name) + "->" + upper($$.player.name) AS d',
+    f'GO FROM {TD}, {TP} OVER like WHERE lower($$.player.name) == "tony parker" YIELD $$.player.name',
+    f'GO FROM {TD}, {TP} OVER like WHERE left($$.player.name, 1) < "M" YIELD $$.player.name, left($$.player.name, 1) AS f',
+    f'GO 2 STEPS FROM {TD} OVER like YIELD DISTINCT left($$.player.name, 1) AS f, upper(right($^.player.name, 2)) AS g',
+    f'GO FROM {TD}, {TP} OVER like YIELD (int)substr((string)like.likeness, 1, 1) AS a, '
+    f'(double)rpad((string)like.likeness, 4, "5") AS b',
+    f'GO FROM {TD} OVER serve YIELD upper($$.team.name) AS a, (string)lpad((string)serve.start_year, 6, "#") AS b',
+    # case maps composed with the other functions (a case map commutes with windows and trims)
+    f'GO FROM {TD}, {TP} OVER like YIELD lower(upper($$.player.name) + "X") AS a, trim(lower(" " + $$.player.name + " ")) AS b, '
+    f'lpad(upper($$.player.name), 15, "ab") AS c, upper(lpad($$.player.name, 15, "ab")) AS d, '
+    f'lower(left($^.player.name, 4) + right($$.player.name, 4)) AS e',
+    # the bodies' failures
+    f'GO FROM {TD} OVER like YIELD lpad($$.player.name, 0 - like.likeness, "x")',
+    f'GO FROM {TD} OVER like YIELD rpad($$.player.name, 40, "")',
+    f'GO FROM {TD} OVER like YIELD left($$.player.name, "3")',
+    f'GO FROM {TD} OVER like YIELD lower(like.likeness)',
+    f'GO FROM {TD} OVER like YIELD substr($$.player.name, 1.5, 2)',
+    f'GO FROM {TD} OVER like YIELD lpad($$.player.name, 12, 7)',
+]
+
+
+@pytest.mark.parametrize("q", STRING_FNS)
+def test_string_functions_on_columns(nba, q):
+    eng, orc = nba
+    (rg, eg), (ro, eo) = _run(eng, q), _run(orc, q)
+    assert (eg is None) == (eo is None), (q, eg, eo)
+    assert rg == ro, (q, rg, ro)
+
+
+def test_string_functions_on_columns_return_rows(nba):
+    """Guard against the comparison passing because both sides failed: the first 12 return rows."""
     eng, _ = nba
-    with pytest.raises(NbgError) as ei:
-        ngql.Session(eng).execute(f'GO FROM {TD} OVER like YIELD lower($$.player.name)')
-    assert ei.value.code == L.E_UNSUPPORTED
+    assert all(_run(eng, q)[0] for q in STRING_FNS[:12])
+
+
+def test_string_functions_partitioned(nba_data):
+    """Three ranks: the views travel with their rows (and through YIELD DISTINCT's exchange)."""
+    c = LocalCluster(7, 3)
+    for (kind, name), cols in kvgen.NBA_SCHEMAS.items():
+        if kind == "edge":
+            c.register_edge(kvgen.NBA_EDGES[name], name, cols)
+        else:
+            c.register_tag(kvgen.NBA_TAGS[name], name, cols)
+    c.load_builder(kvgen.nba_kv(nba_data, 7))
+    orc = nba_oracle(nba_data, 7)
+    try:
+        for q in STRING_FNS[:12]:
+            (rg, eg), (ro, eo) = _run(c, q), _run(orc, q)
+            assert eg is None and eo is None and rg == ro, (q, eg, eo)
+    finally:
+        c.close()
+        orc.close()
+
+
+def test_nested_string_functions_on_columns_unsupported(nba):
+    """A window, trim or pad over another window, trim or pad of a per-edge string says so
+    (NBG_E_UNSUPPORTED) rather than return other values; over constants any nesting folds."""
+    eng, orc = nba
+    for q in (f'GO FROM {TD} OVER like YIELD trim(left($$.player.name, 4))',
+              f'GO FROM {TD} OVER like YIELD substr(lpad($$.player.name, 20, "-"), 2, 5)',
+              f'GO FROM {TD} OVER like YIELD lpad($$.player.name, 20, right($^.player.name, 2))'):
+        with pytest.raises(NbgError) as ei:
+            ngql.Session(eng).execute(q)
+        assert ei.value.code == L.E_UNSUPPORTED, q
+    q = f'GO FROM {TD} OVER like YIELD trim(left(" Abc ", 3)) AS a, $$.player.name'
+    assert _run(eng, q) == _run(orc, q)

@@ -65,6 +65,35 @@ def test_rmat_shortest_single_pairs(rmat12, upto, sp_mode):
         assert found > 0
 
 
+@pytest.mark.parametrize("both", ["0", "64", "1000000000"])
+def test_rmat_shortest_two_sided_levels(both, monkeypatch):
+    """The chain's two-sided levels (NBG_SP_BOTH items per side; 0: one side per level, 64: only
+    the first levels, 10^9: every level UPTO allows), including meets at position kf (a backward
+    claim of a forward-level-kf vertex) and at kf + 1 (a vertex both sides claim in one launch):
+    the same entry lists as the oracle for every pair, UPTO 1..6, s == t included."""
+    monkeypatch.setenv("NBG_SP_BOTH", both)
+    src, dst, w = graphs.rmat_graph(12)
+    eng = graphs.rmat_engine(src, dst, w)
+    orc = graphs.rmat_oracle(src, dst, w)
+    try:
+        found = 0
+        for upto in (1, 2, 3, 4, 6):
+            ps = pairs(src, dst, 40, seed=100 + upto)
+            ps += [(s, s) for s, _ in ps[:4]]
+            for s, t in ps:
+                got = eng.find_path([s], [t], [1], upto)
+                exp = orc.find_path([s], [t], [1], upto, True, mode=1)
+                assert got == sorted(exp), (s, t, upto, both)
+                found += len(got)
+        assert found > 50
+        # the batched chain runs the same steps
+        reqs = [([s], [t], [1], 4, True) for s, t in pairs(src, dst, 64, seed=9)]
+        assert eng.find_path_batch(reqs) == [eng.find_path(*r[:4]) for r in reqs]
+    finally:
+        eng.close()
+        orc.close()
+
+
 def test_rmat_shortest_self_and_unknown(rmat12, sp_mode):
     """s == t needs a cycle (walk length >= 1); unknown vids have no rows."""
     src, dst, eng, orc = rmat12

@@ -211,3 +211,29 @@ def test_arena_overflow_fails_cleanly(monkeypatch):
     env = dict(os.environ, NBG_STR_ARENA_KB="4")
     p = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=120)
     assert "CODE -1004" in p.stdout and "NEXT [('12x',)]" in p.stdout, p.stdout + p.stderr
+
+
+def test_long_derived_strings_of_a_large_result():
+    """Derived strings longer than 16 bytes over a result far above 1 MB: the arena is
+    sized from each program's bound on its pieces' text (ProgramBuilder::sout_bytes), so a hub's
+    40,000 rows of ~60-byte concatenations fit, equal to the oracle's."""
+    parts = 3
+    kb = kvgen.KVBuilder(parts)
+    now = 1_600_000_000_000_000
+    n = 40000
+    for i in range(n):
+        kb.insert_edge(1, 1000 + i, REL, 0, REL_S, ["x" * 24 + str(i), i], now)
+    eng = Engine(parts)
+    eng.register_edge(REL, "rel", REL_S)
+    eng.load_builder(kb)
+    orc = Oracle(parts)
+    orc.register(True, REL, "rel", REL_S)
+    orc.load_builder(kb)
+    try:
+        q = 'GO FROM 1 OVER rel YIELD rel.s + "/" + rel.s AS a, (string)rel.n + rel.s AS b'
+        got, exp = _run(eng, q), _run(orc, q)
+        _same(got, exp, q)
+        assert len(got[0]) == n and sum(len(a) + len(b) for a, b in got[0]) > (3 << 20)
+    finally:
+        eng.close()
+        orc.close()
