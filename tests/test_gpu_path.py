@@ -94,6 +94,44 @@ def test_rmat_shortest_two_sided_levels(both, monkeypatch):
         orc.close()
 
 
+@pytest.mark.parametrize("hits", ["spread", "head", "tail", "budget"])
+def test_shortest_through_a_hub(hits, sp_mode):
+    """Greedy hops through a hub (more than 4096 out-edges): without a rank column one workgroup
+    scans the row in the canonical order — the negative vids (the row's unsigned tail) first — and
+    stops at the first chunk holding a candidate; a hub whose candidates lie past the scan's budget
+    is left to the next launch's spread scan.  s -> hub -> x -> t for 10,000 x of both signs, with
+    the x that reach t chosen among the smallest negative vids (head of the canonical order), the
+    largest positive ones (its end: past the budget), at random, or spread over the row."""
+    rng = np.random.default_rng({"spread": 1, "head": 2, "tail": 3, "budget": 4}[hits])
+    s_v, hub, t_v = 5, 6, 7
+    xs = np.unique(rng.integers(-(1 << 62), 1 << 62, 10000, dtype=np.int64))
+    xs = xs[(xs != s_v) & (xs != hub) & (xs != t_v)]
+    order = np.argsort(xs)             # signed order: the canonical one
+    if hits == "head":
+        reach = xs[order[:3]]
+    elif hits == "budget":
+        reach = xs[order[-3:]]
+    elif hits == "tail":
+        reach = xs[order[len(xs) // 2 + rng.integers(0, 40, 5)]]
+    else:
+        reach = rng.choice(xs, 40, replace=False)
+    src = np.concatenate([[s_v], np.full(len(xs), hub), reach, rng.choice(xs, 300)])
+    dst = np.concatenate([[hub], xs, np.full(len(reach), t_v), rng.choice(xs, 300)])
+    w = np.zeros(len(src), np.int64)
+    eng = graphs.rmat_engine(src, dst, w)
+    orc = graphs.rmat_oracle(src, dst, w)
+    try:
+        for a, b, upto in ((s_v, t_v, 3), (s_v, t_v, 5), (hub, t_v, 2), (s_v, int(reach[0]), 4)):
+            got = eng.find_path([a], [b], [1], upto)
+            exp = orc.find_path([a], [b], [1], upto, True, mode=1)
+            assert got == sorted(exp) and got, (hits, a, b, upto)
+        reqs = [([s_v], [t_v], [1], 4, True), ([hub], [t_v], [1], 3, True)]
+        assert eng.find_path_batch(reqs) == [eng.find_path(*r[:4]) for r in reqs]
+    finally:
+        eng.close()
+        orc.close()
+
+
 def test_rmat_shortest_self_and_unknown(rmat12, sp_mode):
     """s == t needs a cycle (walk length >= 1); unknown vids have no rows."""
     src, dst, eng, orc = rmat12
