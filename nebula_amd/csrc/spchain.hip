@@ -55,7 +55,6 @@ constexpr int CH_HOP_WGS = 64;            // workgroups scanning one greedy hop
 constexpr int CH_HOP_U = 4;               // neighbours per thread in flight (greedy)
 constexpr int CH_MAXS = 2 * MAX_PATH_LEN + 2;   // step launches of one query, at most
 
-
 enum ChListId : int { CL_F0 = 0, CL_F1 = 1, CL_B0 = 2, CL_B1 = 3, CL_M = 4, CH_NLISTS = 5 };
 enum ChPhase : uint32_t { PH_BFS = 0, PH_BSET = 1, PH_DONE = 2 };
 // profiled launch kinds (nbg_profile_read names: kChainKernelNames)
@@ -104,9 +103,7 @@ struct ChState {        // device; the host reads what the result launch derives
   ChCtr c[2];
   unsigned long long gerr;             // CH_GUARD builds: bit 8 + site of a bounds violation
   unsigned long long gticket;          // greedy hop: workgroups done (the last one reduces, resets)
-  // greedy launch h starts from hstart[h] = (HS_SPREAD | position << 32 | current vertex: the flag
-  // says the hop at `position` is a hub whose ordered scan found nothing within its budget, so the
-  // next launch spreads it over the grid) and exactly one of
+  // greedy launch h starts from hstart[h] = (position << 32 | current vertex) and exactly one of
   // its workgroups writes hstart[h + 1]: state that no launch mutates while its own workgroups
   // may still read it (workgroups of one launch start at different times).  Greedy launches are
   // the step launches that find the search over (hop_first) and then the k_ch_hop launches.
@@ -126,7 +123,7 @@ struct ChState {        // device; the host reads what the result launch derives
 struct ChOut {
   ChSnap F;                            // the state after the last step launch
   unsigned long long err;              // ChState::err
-  unsigned long long hpos;             // hstart[hops] (HS_SPREAD | position << 32 | vertex)
+  unsigned long long hpos;             // hstart[hops] (position << 32 | vertex)
   unsigned long long hlaunch;
   unsigned long long busy;             // ChState::busy
   unsigned long long tag;              // ChQ::tag of the batch whose launch stored this
@@ -158,7 +155,6 @@ struct ChQ {
   uint32_t tag;                        // this batch of launches (ChOut::tag: which batch stored)
   uint32_t both_items;                 // a BFS level expands both sides when each has at most this many
                                        // items (entries + edges) and UPTO allows two levels (0: never)
-  uint32_t ordered;                    // greedy hub hops scanned in order first (hop_ordered; 0: spread)
 };
 
 // Both sides in one launch: while both frontiers are small a level's launch costs the same for one
@@ -886,8 +882,6 @@ __device__ __forceinline__ bool cand_less(const Cand& a, const Cand& b) {
   return a.v < b.v;
 }
 constexpr uint32_t CH_SOLO_DEG = 4 * CH_BLOCK * CH_HOP_U;   // a hop one workgroup takes alone
-constexpr uint64_t HS_SPREAD = 1ull << 62;                  // hstart flag (ChState::hstart)
-constexpr uint32_t CH_ORDERED_BUDGET = 8 * CH_BLOCK * CH_HOP_U;   // edges of a hub's ordered scan
 
 // Workgroup-wide minimum (every thread gets it).
 __device__ __forceinline__ Cand block_min(Cand b, Cand* lds) {
@@ -934,58 +928,6 @@ __device__ __forceinline__ Cand hop_scan(const ChArgs& A, const uint32_t* vlab, 
   return best;
 }
 
-// A hub's hop in the canonical order, by one workgroup, stopping at the first chunk holding a
-// candidate.  Without a rank column a row is in key order = ascending dst vid read as unsigned
-// (QueryBaseProcessor's memcmp order of the big-endian key), while the greedy takes the minimum
-// (type, rank, vid) read as signed: the row's tail of negative vids comes first, then its head.
-// So chunks of CH_BLOCK * CH_HOP_U edges are scanned in that order and the first one with a
-// candidate holds the minimum.  *done: the minimum was found, or the whole row holds none; false
-// when `budget` edges held none (the caller leaves the hop to a spread scan).
-__device__ Cand hop_ordered(const ChArgs& A, const uint32_t* vlab, uint32_t want, uint32_t rs, uint32_t re,
-                            uint32_t budget, Cand* lds, bool* done) {
-  const Cand none{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
-  // split = the first negative vid: none when the last is not negative (one load), else a
-  // 256-ary search (every thread probes one point per round)
-  uint32_t lo = rs, hi = re;
-  if (gld(A.dst_vid, (uint64_t)re - 1, A.ne[0], 13, A.st) >= 0) {
-    lo = re;
-  } else {
-    while (lo < hi) {   // the answer is in [lo, hi]: dst_vid[hi] (if hi < re) is negative
-      const uint32_t step = (hi - lo + CH_BLOCK - 1) / CH_BLOCK;
-      const uint32_t j = lo + threadIdx.x * step;
-      const bool nonneg = j < hi && gld(A.dst_vid, j, A.ne[0], 13, A.st) >= 0;
-      const int k = __syncthreads_count(nonneg);   // probes lo, lo + step, ... are monotone
-      if (k == 0) {
-        hi = lo;
-      } else {
-        lo = lo + (uint32_t)(k - 1) * step + 1;
-        const uint32_t nh = lo - 1 + step;
-        hi = nh < hi ? nh : hi;
-      }
-    }
-  }
-  const uint32_t split = lo;
-  const uint32_t seg_lo[2] = {split, rs}, seg_hi[2] = {re, split};
-  uint32_t scanned = 0;
-  for (int sg = 0; sg < 2; ++sg) {
-    for (uint32_t j0 = seg_lo[sg]; j0 < seg_hi[sg]; j0 += CH_BLOCK * CH_HOP_U) {
-      if (scanned >= budget) {
-        *done = false;
-        return none;
-      }
-      const uint32_t j1 = j0 + CH_BLOCK * CH_HOP_U < seg_hi[sg] ? j0 + CH_BLOCK * CH_HOP_U : seg_hi[sg];
-      const Cand b = block_min(hop_scan(A, vlab, want, j0, j1, threadIdx.x, CH_BLOCK), lds);
-      scanned += j1 - j0;
-      if (b.d != NO_ROW) {
-        *done = true;
-        return b;
-      }
-    }
-  }
-  *done = true;   // no candidate in the whole row
-  return none;
-}
-
 }  // namespace
 
 // Greedy hops (CH_HOP_WGS workgroups), launch h of the query.  The state after step launch
@@ -1005,10 +947,9 @@ __device__ __forceinline__ bool ch_hop(const ChArgs& A, const ChQ& q, int nl, in
   ChCtr& C = st->c[q.par];
   const ChSnap F = snap_for(st, q, (int)st->first[nl]);   // the state after the nl step launches
   const unsigned long long H = st->hstart[h];
-  uint32_t pos = (uint32_t)((H & ~HS_SPREAD) >> 32), c = (uint32_t)H;
-  const bool force_spread = (H & HS_SPREAD) != 0;
-  auto finish = [&](uint32_t p, uint32_t v, bool spread = false) {   // (thread 0 of the one writer)
-    st->hstart[h + 1] = (spread ? HS_SPREAD : 0ull) | ((unsigned long long)p << 32) | v;
+  uint32_t pos = (uint32_t)(H >> 32), c = (uint32_t)H;
+  auto finish = [&](uint32_t p, uint32_t v) {   // (thread 0 of the one writer)
+    st->hstart[h + 1] = ((unsigned long long)p << 32) | v;
   };
   if (!F.met || F.phase != PH_DONE || F.err || pos >= F.L || c == NO_ROW) {
     if (bid == 0 && threadIdx.x == 0) finish(pos, c);
@@ -1040,11 +981,9 @@ __device__ __forceinline__ bool ch_hop(const ChArgs& A, const ChQ& q, int nl, in
     gst(st->path, 3 + 3 * (uint64_t)p, 1 + 3 * (uint64_t)MAX_PATH_LEN, (long long)r.v, 15, st);
     return true;
   };
-  // hubs without a rank column are first scanned in order by one workgroup (hop_ordered)
-  const bool ordered = A.rank == nullptr && q.ordered;
   uint32_t rs, re;
   range(c, &rs, &re);
-  if (re - rs > CH_SOLO_DEG && (!ordered || force_spread)) {   // a hub: every workgroup scans a share
+  if (re - rs > CH_SOLO_DEG) {   // a hub: every workgroup scans a share
     const uint32_t* vlab;
     const uint32_t want = want_of(pos, &vlab);
     Cand best = hop_scan(A, vlab, want, rs, re, (uint64_t)bid * CH_BLOCK + threadIdx.x, (uint64_t)nblk * CH_BLOCK);
@@ -1082,21 +1021,10 @@ __device__ __forceinline__ bool ch_hop(const ChArgs& A, const ChQ& q, int nl, in
   if (threadIdx.x == 0) C.hlaunch += 1;
   while (pos < L) {
     range(c, &rs, &re);
+    if (re - rs > CH_SOLO_DEG) break;   // a hub: the next launch spreads it
     const uint32_t* vlab;
     const uint32_t want = want_of(pos, &vlab);
-    Cand r;
-    if (re - rs > CH_SOLO_DEG) {
-      // a hub: in order with early exit, or left to the next launch's spread scan
-      if (!ordered) break;
-      bool done = false;
-      r = hop_ordered(A, vlab, want, rs, re, CH_ORDERED_BUDGET, lds, &done);
-      if (!done) {
-        if (threadIdx.x == 0) finish(pos, c, true);
-        return true;
-      }
-    } else {
-      r = block_min(hop_scan(A, vlab, want, rs, re, threadIdx.x, CH_BLOCK), lds);
-    }
+    const Cand r = block_min(hop_scan(A, vlab, want, rs, re, threadIdx.x, CH_BLOCK), lds);
     if (threadIdx.x == 0) s_last = record(pos, r);
     __syncthreads();
     if (!s_last) return true;
@@ -1206,7 +1134,6 @@ struct ChainCtx {
   unsigned grid = 256;
   uint32_t solo = 0;               // ChQ::solo (NBG_SP_SOLO items)
   uint32_t both = 16384;           // ChQ::both_items (NBG_SP_BOTH; 0: one side per level)
-  uint32_t ordered = 1;            // ChQ::ordered (NBG_SP_ORDERED)
   // the query in flight: what has been enqueued
   ChQ q{};
   int steps = 0, hops = 0;
@@ -1264,8 +1191,6 @@ ChainCtx* chain_create(uint64_t nv, uint64_t edge_cap, hipStream_t s, std::strin
   if (so) c->solo = (uint32_t)strtoul(so, nullptr, 10);
   const char* bo = getenv("NBG_SP_BOTH");
   if (bo) c->both = (uint32_t)strtoul(bo, nullptr, 10);
-  const char* od = getenv("NBG_SP_ORDERED");
-  if (od) c->ordered = (uint32_t)strtoul(od, nullptr, 10);
   hipError_t he = hipSuccess;
   auto M = [&](void** p, size_t b) { if (he == hipSuccess) he = hipMalloc(p, b); };
   for (auto& L : c->list) {
@@ -1360,7 +1285,7 @@ static hipError_t chain_prepare(ChainCtx* c, const SpTypes& fwd, const SpTypes& 
     c->args_valid = true;
   }
   c->par ^= 1u;
-  c->q = ChQ{s, t, upto, epoch, epoch, epoch, c->solo, c->par, 0, c->both, c->ordered};
+  c->q = ChQ{s, t, upto, epoch, epoch, epoch, c->solo, c->par, 0, c->both};
   c->steps = c->hops = 0;
   c->last_batched = false;
   ++c->queries;
@@ -1456,7 +1381,7 @@ bool chain_more(ChainCtx* c, hipError_t* he) {
     *he = chain_batch(c, chain_max(c) - c->steps, 0);
     return false;
   }
-  const uint32_t hpos = (uint32_t)((h.hpos & ~HS_SPREAD) >> 32);
+  const uint32_t hpos = (uint32_t)(h.hpos >> 32);
   if (F.met && !F.err && !h.err && hpos < F.L && c->hops < CH_MAXS) {
     *he = chain_batch(c, 0, (int)F.L - (int)hpos);
     return false;
@@ -1477,7 +1402,7 @@ void chain_result(const ChainCtx* c, SpResult* out) {
   out->levels = F.levels;
   out->abytes = F.abytes;
   out->launches = (unsigned long long)(c->steps + c->hops);
-  const uint32_t hpos = (uint32_t)((h.hpos & ~HS_SPREAD) >> 32);
+  const uint32_t hpos = (uint32_t)(h.hpos >> 32);
   out->L = (F.met && !h.err && hpos == F.L) ? F.L : 0;
   if (F.met && !h.err && hpos != F.L) out->err = 2;   // (cannot happen: the hops were enqueued)
   if (out->L) memcpy(out->path, h.path, (1 + 3 * (size_t)out->L) * sizeof(long long));

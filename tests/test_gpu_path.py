@@ -96,12 +96,11 @@ def test_rmat_shortest_two_sided_levels(both, monkeypatch):
 
 @pytest.mark.parametrize("hits", ["spread", "head", "tail", "budget"])
 def test_shortest_through_a_hub(hits, sp_mode):
-    """Greedy hops through a hub (more than 4096 out-edges): without a rank column one workgroup
-    scans the row in the canonical order — the negative vids (the row's unsigned tail) first — and
-    stops at the first chunk holding a candidate; a hub whose candidates lie past the scan's budget
-    is left to the next launch's spread scan.  s -> hub -> x -> t for 10,000 x of both signs, with
-    the x that reach t chosen among the smallest negative vids (head of the canonical order), the
-    largest positive ones (its end: past the budget), at random, or spread over the row."""
+    """Greedy hops through a hub (more than 4096 out-edges, scanned by 64 workgroups and reduced by
+    the last): s -> hub -> x -> t for 10,000 x of both signs, the x that reach t chosen among the
+    smallest vids, the largest, in the middle, or at random.  The canonical minimum is over the
+    signed (type, rank, vid) while a row is in key order (byte-reversed vids): round 5's
+    early-exit scan of hub rows in row order assumed otherwise, and this test caught it."""
     rng = np.random.default_rng({"spread": 1, "head": 2, "tail": 3, "budget": 4}[hits])
     s_v, hub, t_v = 5, 6, 7
     xs = np.unique(rng.integers(-(1 << 62), 1 << 62, 10000, dtype=np.int64))
