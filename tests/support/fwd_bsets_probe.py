@@ -16,7 +16,7 @@ def main():
     ok, found = True, 0
     for scale, world, npairs in ((11, 2, 24), (16, 2, 24), (16, 3, 12)):
         src, dst, w = graphs.rmat_graph(scale)
-        single = graphs.rmat_engine(src, dst, w)
+        single = graphs.one_sided_engine(src, dst, w)
         c = LocalCluster(100, world)
         c.set_path_replica(0)
         c.register_edge(graphs.E_TYPE, "e", graphs.E_SCHEMA)

@@ -38,6 +38,25 @@ def rmat_engine(src, dst, w, parts=100, via_kv=False, max_edge=0x7FFFFFFF):
     return e
 
 
+def one_sided_engine(src, dst, w, parts=100):
+    """rmat_engine whose synchronous one-pair SHORTEST chain expands one side per BFS level
+    (NBG_SP_BOTH=0, read when the chain is created: nbg_path_reserve creates it now).  The
+    partitioned engines' collective search is one-sided, so the edges it expands then equal this
+    engine's (the tests compare them); the two-sided default expands more for the same paths."""
+    import os
+    old = os.environ.get("NBG_SP_BOTH")
+    os.environ["NBG_SP_BOTH"] = "0"
+    try:
+        e = rmat_engine(src, dst, w, parts)
+        e.path_reserve(0, 0)
+    finally:
+        if old is None:
+            os.environ.pop("NBG_SP_BOTH", None)
+        else:
+            os.environ["NBG_SP_BOTH"] = old
+    return e
+
+
 def sorted_rows(rows):
     return sorted(tuple(r) for r in rows)
 

@@ -47,7 +47,7 @@ def _codes(c, fn):
 @pytest.fixture(scope="module")
 def rmat14():
     src, dst, w = graphs.rmat_graph(14)
-    single = graphs.rmat_engine(src, dst, w)
+    single = graphs.one_sided_engine(src, dst, w)
     orc = graphs.rmat_oracle(src, dst, w)
     c = _cluster(src, dst, w)
     yield src, dst, w, single, orc, c
@@ -355,7 +355,7 @@ def test_rmat16_go_and_shortest_digests():
     """RMAT-16 (65 k vertices, 1 M samples): larger frontiers, hub rows spanning many tiles, and
     SHORTEST levels that switch between slot arrays and bitmaps on 8 ranks."""
     src, dst, w = graphs.rmat_graph(16)
-    single = graphs.rmat_engine(src, dst, w)
+    single = graphs.one_sided_engine(src, dst, w)
     c = _cluster(src, dst, w)
     try:
         wb = WHERE.encode()

@@ -36,7 +36,7 @@ def cluster_for(src, dst, w, world, parts=100, max_edge=0x7FFFFFFF, replica=Fals
 @pytest.fixture(scope="module")
 def rmat11():
     src, dst, w = graphs.rmat_graph(11)
-    single = graphs.rmat_engine(src, dst, w)
+    single = graphs.one_sided_engine(src, dst, w)
     orc = graphs.rmat_oracle(src, dst, w)
     clusters = {g: cluster_for(src, dst, w, g) for g in (2, 3, 4)}
     yield src, single, orc, clusters
@@ -162,7 +162,7 @@ def test_partitioned_shortest_sparse_and_bitmap_levels(world):
     the oracle pins at RMAT-11 above."""
     from nebula_amd import rmat
     src, dst, w = graphs.rmat_graph(16)
-    single = graphs.rmat_engine(src, dst, w)
+    single = graphs.one_sided_engine(src, dst, w)
     c = cluster_for(src, dst, w, world)
     try:
         found = 0
