@@ -41,7 +41,7 @@ METRIC = "GO 3 STEPS traversed edges/sec (TEPS) at 1/2/4/8 GPU; FIND SHORTEST PA
 # HBM traffic per launch from the committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
 # bench's default workload (tools/gpu_r02.sh pmc -> tools/pmc_summary.py; FETCH_SIZE doubled per
 # the gfx950 note), keyed by workload
-PMC_FILES = {("RMAT-26", 16): os.path.join(ROOT, "profiles", "r05_h_pmc_hbm_rmat26.json"),
+PMC_FILES = {("RMAT-26", 16): os.path.join(ROOT, "profiles", "r05_finb_pmc_hbm_rmat26.json"),
              ("RMAT-22", 64): os.path.join(ROOT, "profiles", "r02_pmc_hbm_rmat22.json")}
 # library kernel id -> instantiations in the rocprof names, first match wins (FINAL: this bench's
 # range WHERE with a _dst YIELD runs k_expand<4> = FINALD; <3> FINALF; <1> the general interpreter;
