@@ -907,6 +907,28 @@ __device__ __forceinline__ Cand block_min(Cand b, Cand* lds) {
   return b;
 }
 
+// Workgroup-wide minimum with ONE barrier (the solo walk's hops): each wave reduces, writes its
+// candidate to slot set `par` (alternating per hop, so a wave still reading the previous hop's
+// slots is never overwritten), and every thread reduces the CH_WAVES slots itself.
+__device__ __forceinline__ Cand block_min1(Cand b, Cand (*slots)[CH_WAVES], uint32_t par) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Cand y;
+    y.t = __shfl_down(b.t, o, 64);
+    y.r = __shfl_down(b.r, o, 64);
+    y.v = __shfl_down(b.v, o, 64);
+    y.d = __shfl_down(b.d, o, 64);
+    if ((threadIdx.x & 63) + o < 64 && cand_less(y, b)) b = y;
+  }
+  if ((threadIdx.x & 63) == 0) slots[par][threadIdx.x >> 6] = b;
+  __syncthreads();
+  b = slots[par][0];
+#pragma unroll
+  for (int k = 1; k < CH_WAVES; ++k)
+    if (cand_less(slots[par][k], b)) b = slots[par][k];
+  return b;
+}
+
 // This thread's best candidate among c's out-edges [rs + g, re) step G into B[pos + 1].
 __device__ __forceinline__ Cand hop_scan(const ChArgs& A, const uint32_t* vlab, uint32_t want, uint32_t rs,
                                          uint32_t re, uint64_t g, uint64_t G) {
@@ -942,6 +964,7 @@ __device__ __forceinline__ Cand hop_scan(const ChArgs& A, const uint32_t* vlab, 
 // (bid, nblk: this workgroup among the query's nblk <= CH_HOP_WGS workgroups of the launch)
 __device__ __forceinline__ bool ch_hop(const ChArgs& A, const ChQ& q, int nl, int h, uint32_t bid, uint32_t nblk) {
   __shared__ Cand lds[CH_WAVES + 1];
+  __shared__ Cand hop_slots[2][CH_WAVES];
   __shared__ int s_last;
   ChState* st = A.st;
   ChCtr& C = st->c[q.par];
@@ -1024,10 +1047,10 @@ __device__ __forceinline__ bool ch_hop(const ChArgs& A, const ChQ& q, int nl, in
     if (re - rs > CH_SOLO_DEG) break;   // a hub: the next launch spreads it
     const uint32_t* vlab;
     const uint32_t want = want_of(pos, &vlab);
-    const Cand r = block_min(hop_scan(A, vlab, want, rs, re, threadIdx.x, CH_BLOCK), lds);
-    if (threadIdx.x == 0) s_last = record(pos, r);
-    __syncthreads();
-    if (!s_last) return true;
+    // (one barrier per hop: every thread has the minimum, so none waits for thread 0's record)
+    const Cand r = block_min1(hop_scan(A, vlab, want, rs, re, threadIdx.x, CH_BLOCK), hop_slots, pos & 1u);
+    if (threadIdx.x == 0) record(pos, r);
+    if (r.d == NO_ROW) return true;   // (a reconstruction failure: recorded and finished)
     c = r.d;
     ++pos;
   }
