@@ -97,8 +97,6 @@ struct ChCtr {
   unsigned long long err;              // 1 reconstruction failure, 3 list overflow
   unsigned long long hlaunch;          // greedy launches that did work
   unsigned long long busy;             // step launches that ran a step
-  unsigned long long tick[CH_MAXS];    // NBG_SP_TAIL: workgroups of step launch i done with its step
-  unsigned long long tailw;            // the walk ran in the search's last step launch: 1 part, 2 whole
 };
 
 struct ChState {        // device; the host reads what the result launch derives from it (ChOut)
@@ -128,7 +126,6 @@ struct ChOut {
   unsigned long long hpos;             // hstart[hops] (position << 32 | vertex)
   unsigned long long hlaunch;
   unsigned long long busy;             // ChState::busy
-  unsigned long long tail;             // ChCtr::tailw
   unsigned long long tag;              // ChQ::tag of the batch whose launch stored this
   long long path[1 + 3 * MAX_PATH_LEN];
   unsigned long long wake;             // = tag, stored last (system-scope release): the host polls it
@@ -158,7 +155,6 @@ struct ChQ {
   uint32_t tag;                        // this batch of launches (ChOut::tag: which batch stored)
   uint32_t both_items;                 // a BFS level expands both sides when each has at most this many
                                        // items (entries + edges) and UPTO allows two levels (0: never)
-  uint32_t tail;                       // NBG_SP_TAIL: the last workgroup of the search's last step walks
 };
 
 // Both sides in one launch: while both frontiers are small a level's launch costs the same for one
@@ -480,7 +476,7 @@ __device__ __forceinline__ void first_store(const ChArgs& A, const ChQ& q, const
 // (first: step 0, whose source list {s} or {t} is f0's registers — by value: a pointer to it
 // selected at run time put it in scratch memory)
 template <int NW>
-__device__ __forceinline__ bool ch_level(const ChArgs& A, const ChQ& q, const ChSnap& P, int i, uint32_t bid,
+__device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const ChSnap& P, int i, uint32_t bid,
                                          uint32_t nblk, bool first, const ChFirst f0) {
   __shared__ uint32_t sEndAll[NW][CH_TILE + 2];
   __shared__ uint32_t sRsAll[NW][CH_TILE + 1];
@@ -800,7 +796,6 @@ __device__ __forceinline__ bool ch_level(const ChArgs& A, const ChQ& q, const Ch
       wave_append(A, A.list[CL_M], &C.macc, &C.err, c, mm, dg, rs);
     }
   }
-  return bid < nt0 + nt1;   // this workgroup had tiles (wave 0's first is tile bid)
 }
 
 // Items (entries + edges) of the source list of step P (as ch_level picks it).
@@ -822,8 +817,7 @@ __device__ __forceinline__ uint64_t step_items(const ChSnap& P) {
 // needs the grid (the launch boundary then orders it after this workgroup's writes).
 // Returns false when the search was over before this launch (the launch is then a greedy one).
 template <int NW>
-__device__ __forceinline__ bool ch_step(const ChArgs& A, const ChQ& q, int i, uint32_t bid, uint32_t nblk,
-                                        ChSnap* ran, bool* wrote) {
+__device__ __forceinline__ bool ch_step(const ChArgs& A, const ChQ& q, int i, uint32_t bid, uint32_t nblk) {
   ChState* st = A.st;
   ChCtr& C = st->c[q.par];
   // launch i runs step i while the search is on (first[i] == i, one step per launch): that
@@ -859,12 +853,8 @@ __device__ __forceinline__ bool ch_step(const ChArgs& A, const ChQ& q, int i, ui
       if (j > 0) st->snap[j] = P;   // (step j + 1 derives its snapshot from it; snap[0]: first_store)
       if (!solo) st->first[i + 1] = j + 1;
     }
-    const bool had = ch_level<NW>(A, q, P, (int)j, solo ? 0u : bid, solo ? 1u : nblk, j == 0, f0);
-    if (!solo) {
-      *ran = P;   // (the step this launch ran, for the tail: ch_tail)
-      *wrote = had || bid == 0;
-      return true;
-    }
+    ch_level<NW>(A, q, P, (int)j, solo ? 0u : bid, solo ? 1u : nblk, j == 0, f0);
+    if (!solo) return true;
     // this workgroup's stores and atomics before the next step's reads (labels, lists, counters;
     // the acquire drops L1 lines read before another wave's claims); the snapshot is read back
     // rather than kept in registers across the step
@@ -962,45 +952,6 @@ __device__ __forceinline__ Cand hop_scan(const ChArgs& A, const uint32_t* vlab, 
 
 }  // namespace
 
-// The greedy walk by one workgroup from hop `pos` at vertex c (path length L, meet position kf):
-// hop after hop while the current row has at most CH_SOLO_DEG edges; thread 0 records each hop
-// and writes hstart[h + 1] (where the walk stopped; NO_ROW after a reconstruction failure, also
-// flagged in ChCtr::err).  Returns true when the path is complete (or failed).
-__device__ bool walk_solo(const ChArgs& A, const ChQ& q, uint32_t L, uint32_t kf, int h, uint32_t pos, uint32_t c,
-                          Cand (*slots)[CH_WAVES]) {
-  ChState* st = A.st;
-  ChCtr& C = st->c[q.par];
-  while (pos < L) {
-    uint32_t rs = 0, re = 0;
-    if (c != NO_ROW && (!A.visible || gld(A.visible, c, A.nv, 14, st))) {
-      rs = gld(A.row_ptr[0], c, A.nv + 1, 14, st);
-      re = gld(A.row_ptr[0], (uint64_t)c + 1, A.nv + 1, 14, st);
-    }
-    if (re - rs > CH_SOLO_DEG) break;   // a hub: the next launch spreads it
-    const bool by_m = pos + 1 <= kf;
-    const uint32_t* vlab = by_m ? A.lab[2] : A.lab[1];
-    const uint32_t want = by_m ? stamp_of(q.em, pos + 1) : stamp_of(q.eb, L - pos - 1);
-    // (one barrier per hop: every thread has the minimum, so none waits for thread 0's record)
-    const Cand r = block_min1(hop_scan(A, vlab, want, rs, re, threadIdx.x, CH_BLOCK), slots, pos & 1u);
-    if (r.d == NO_ROW) {   // reconstruction failure
-      if (threadIdx.x == 0) {
-        atomicOr(&C.err, 1ull);
-        st->hstart[h + 1] = ((unsigned long long)pos << 32) | NO_ROW;
-      }
-      return true;
-    }
-    if (threadIdx.x == 0) {
-      gst(st->path, 1 + 3 * (uint64_t)pos, 1 + 3 * (uint64_t)MAX_PATH_LEN, (long long)r.t, 15, st);
-      gst(st->path, 2 + 3 * (uint64_t)pos, 1 + 3 * (uint64_t)MAX_PATH_LEN, (long long)r.r, 15, st);
-      gst(st->path, 3 + 3 * (uint64_t)pos, 1 + 3 * (uint64_t)MAX_PATH_LEN, (long long)r.v, 15, st);
-    }
-    c = r.d;
-    ++pos;
-  }
-  if (threadIdx.x == 0) st->hstart[h + 1] = ((unsigned long long)pos << 32) | c;
-  return pos >= L;
-}
-
 // Greedy hops (CH_HOP_WGS workgroups), launch h of the query.  The state after step launch
 // `last` says whether the sides met and the path length L; the launch starts from hstart[h] =
 // (pos, c): hop pos (< L) takes the minimum (type, rank, dst vid) out-edge of the current vertex c
@@ -1091,16 +1042,26 @@ __device__ __forceinline__ bool ch_hop(const ChArgs& A, const ChQ& q, int nl, in
   }
   // this workgroup alone: small hops
   if (threadIdx.x == 0) C.hlaunch += 1;
-  walk_solo(A, q, L, kf, h, pos, c, hop_slots);
+  while (pos < L) {
+    range(c, &rs, &re);
+    if (re - rs > CH_SOLO_DEG) break;   // a hub: the next launch spreads it
+    const uint32_t* vlab;
+    const uint32_t want = want_of(pos, &vlab);
+    // (one barrier per hop: every thread has the minimum, so none waits for thread 0's record)
+    const Cand r = block_min1(hop_scan(A, vlab, want, rs, re, threadIdx.x, CH_BLOCK), hop_slots, pos & 1u);
+    if (threadIdx.x == 0) record(pos, r);
+    if (r.d == NO_ROW) return true;   // (a reconstruction failure: recorded and finished)
+    c = r.d;
+    ++pos;
+  }
+  if (threadIdx.x == 0) finish(pos, c);
   return true;
 }
 
 // The first greedy launch of the query: the first step launch that finds the search over (busy =
-// the step launches that ran a step), never launch 0 (it stores the greedy's start) — unless the
-// walk began in the search's last step launch (ch_tail): that launch is greedy launch 0.
+// the step launches that ran a step), never launch 0 (it stores the greedy's start).
 __device__ __forceinline__ int hop_first(const ChCtr& C) {
   const int b = (int)C.busy;
-  if (C.tailw) return b - 1;
   return b > 1 ? b : 1;
 }
 
@@ -1108,9 +1069,10 @@ __device__ __forceinline__ int hop_first(const ChCtr& C) {
 // The chain's result (the state after `steps` step launches; the greedy's position hstart[hend])
 // into the host's ChOut (one workgroup; vector stores over the mapped pinned page), and the next
 // query's counter set zeroed.
-__device__ __forceinline__ void ch_out_F(const ChArgs& A, const ChQ& q, const ChSnap& F, int hend, ChOut* out) {
+__device__ __forceinline__ void ch_out(const ChArgs& A, const ChQ& q, int steps, int hend, ChOut* out) {
   ChState* st = A.st;
   __syncthreads();   // (the writing workgroup's own stores: the path, hstart)
+  const ChSnap F = snap_for(st, q, (int)st->first[steps]);
   const ChCtr& C = st->c[q.par];
   const uint32_t L = F.met && F.L <= MAX_PATH_LEN ? F.L : 0;
   for (uint32_t k = threadIdx.x; k < 1 + 3 * L; k += blockDim.x) out->path[k] = st->path[k];
@@ -1121,7 +1083,6 @@ __device__ __forceinline__ void ch_out_F(const ChArgs& A, const ChQ& q, const Ch
     out->tag = q.tag;
     out->hlaunch = C.hlaunch;
     out->busy = C.busy;
-    out->tail = C.tailw;
   }
   unsigned long long* nxt = reinterpret_cast<unsigned long long*>(&st->c[q.par ^ 1u]);
   for (uint32_t k = threadIdx.x; k < sizeof(ChCtr) / 8; k += blockDim.x) nxt[k] = 0;
@@ -1129,38 +1090,6 @@ __device__ __forceinline__ void ch_out_F(const ChArgs& A, const ChQ& q, const Ch
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // (release only, at system scope: no cache invalidation)
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(&out->wake, q.tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-__device__ __forceinline__ void ch_out(const ChArgs& A, const ChQ& q, int steps, int hend, ChOut* out) {
-  ch_out_F(A, q, snap_for(A.st, q, (int)A.st->first[steps]), hend, out);
-}
-
-// NBG_SP_TAIL: after a step, every workgroup that wrote releases its writes at agent scope and
-// takes a ticket; the last one derives the state after the step (the counters are final) and, if
-// the search is over with a path, walks it at once as greedy launch 0 (hstart[0] = (0, s) ->
-// hstart[1]) instead of in the next launch; if the walk completes and this is the batch's last
-// launch, it also stores the result.  (Workgroups without tiles wrote nothing: no release.)
-template <int NW>
-__device__ __forceinline__ void ch_tail(const ChArgs& A, const ChQ& q, const ChSnap& P, int i, uint32_t nblk,
-                                        bool wrote, ChOut* out) {
-  __shared__ int s_tail;
-  __shared__ Cand tslots[2][CH_WAVES];
-  ChState* st = A.st;
-  ChCtr& C = st->c[q.par];
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (wrote) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    s_tail = __hip_atomic_fetch_add(&C.tick[i], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1;
-  }
-  __syncthreads();
-  if (!s_tail) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  const ChSnap F = ch_advance(P, ld_agent(&C.lacc[i]), ld_agent(&C.lmeet[i]), ld_agent(&C.macc), ld_agent(&C.err),
-                              q.upto, ld_agent(&C.lacc2[i]), ld_agent(&C.lmeet2[i]), q.both_items);
-  if (F.phase != PH_DONE || !F.met || F.err || F.L > MAX_PATH_LEN) return;
-  const bool done = walk_solo(A, q, F.L, F.kf, 0, 0u, q.s, tslots);
-  if (threadIdx.x == 0) C.tailw = done ? 2ull : 1ull;
-  if (done && out) ch_out_F(A, q, F, 1, out);
 }
 
 // One query per launch (the chain of one pair): step launch 0 starts the search (no set-up
@@ -1173,14 +1102,7 @@ __device__ __forceinline__ void ch_tail(const ChArgs& A, const ChQ& q, const ChS
 // the batch's last launch stores the result, when the search was over before it.)
 template <int NW>
 __device__ __forceinline__ void ch_any(const ChArgs& A, const ChQ& q, int i, uint32_t bid, uint32_t nblk, ChOut* out) {
-  ChSnap ran;
-  bool wrote = false;
-  ran.phase = PH_DONE;
-  if (ch_step<NW>(A, q, i, bid, nblk, &ran, &wrote)) {
-    if (q.tail && ran.phase != PH_DONE) ch_tail<NW>(A, q, ran, i, nblk, wrote, out);
-    return;
-  }
-  if (i == 0 || bid >= (uint32_t)CH_HOP_WGS) return;
+  if (ch_step<NW>(A, q, i, bid, nblk) || i == 0 || bid >= (uint32_t)CH_HOP_WGS) return;
   const int h = i - hop_first(A.st->c[q.par]);
   if (ch_hop(A, q, i, h, bid, nblk < (uint32_t)CH_HOP_WGS ? nblk : (uint32_t)CH_HOP_WGS) && out)
     ch_out(A, q, i, h + 1, out);
@@ -1235,7 +1157,6 @@ struct ChainCtx {
   unsigned grid = 256;
   uint32_t solo = 0;               // ChQ::solo (NBG_SP_SOLO items)
   uint32_t both = 16384;           // ChQ::both_items (NBG_SP_BOTH; 0: one side per level)
-  uint32_t tail = 0;               // ChQ::tail (NBG_SP_TAIL)
   // the query in flight: what has been enqueued
   ChQ q{};
   int steps = 0, hops = 0;
@@ -1293,8 +1214,6 @@ ChainCtx* chain_create(uint64_t nv, uint64_t edge_cap, hipStream_t s, std::strin
   if (so) c->solo = (uint32_t)strtoul(so, nullptr, 10);
   const char* bo = getenv("NBG_SP_BOTH");
   if (bo) c->both = (uint32_t)strtoul(bo, nullptr, 10);
-  const char* ta = getenv("NBG_SP_TAIL");
-  if (ta) c->tail = (uint32_t)strtoul(ta, nullptr, 10);
   hipError_t he = hipSuccess;
   auto M = [&](void** p, size_t b) { if (he == hipSuccess) he = hipMalloc(p, b); };
   for (auto& L : c->list) {
@@ -1389,7 +1308,7 @@ static hipError_t chain_prepare(ChainCtx* c, const SpTypes& fwd, const SpTypes& 
     c->args_valid = true;
   }
   c->par ^= 1u;
-  c->q = ChQ{s, t, upto, epoch, epoch, epoch, c->solo, c->par, 0, c->both, c->tail};
+  c->q = ChQ{s, t, upto, epoch, epoch, epoch, c->solo, c->par, 0, c->both};
   c->steps = c->hops = 0;
   c->last_batched = false;
   ++c->queries;
@@ -1492,7 +1411,7 @@ bool chain_more(ChainCtx* c, hipError_t* he) {
   }
   c->clean = true;   // (its result launch zeroed the next query's counters)
   // launches used (search steps, then the greedy's, at least one); decay toward this query's needs
-  const double used = (double)h.busy + (h.tail == 2 ? 0.0 : (double)std::max(1ull, h.hlaunch));
+  const double used = (double)h.busy + (double)std::max(1ull, h.hlaunch);
   c->ema_launches = 0.9 * c->ema_launches + 0.1 * (used + 0.3);
   return true;
 }

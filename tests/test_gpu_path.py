@@ -94,53 +94,6 @@ def test_rmat_shortest_two_sided_levels(both, monkeypatch):
         orc.close()
 
 
-@pytest.mark.parametrize("both", ["0", "16384"])
-def test_rmat_shortest_tail_walk(both, monkeypatch):
-    """NBG_SP_TAIL=1: the last workgroup of the search's last step launch (a ticket after each
-    writer's agent-scope release) walks the greedy path at once; paths, batched chains and hub
-    hops (a continuation of the walk) equal the oracle's, with and without two-sided levels."""
-    monkeypatch.setenv("NBG_SP_TAIL", "1")
-    monkeypatch.setenv("NBG_SP_BOTH", both)
-    src, dst, w = graphs.rmat_graph(12)
-    eng = graphs.rmat_engine(src, dst, w)
-    orc = graphs.rmat_oracle(src, dst, w)
-    try:
-        found = 0
-        for upto in (1, 2, 3, 5):
-            ps = pairs(src, dst, 40, seed=200 + upto)
-            ps += [(s, s) for s, _ in ps[:3]]
-            for s, t in ps:
-                got = eng.find_path([s], [t], [1], upto)
-                assert got == sorted(orc.find_path([s], [t], [1], upto, True, mode=1)), (s, t, upto)
-                found += len(got)
-        assert found > 50
-        reqs = [([s], [t], [1], 4, True) for s, t in pairs(src, dst, 64, seed=10)]
-        assert eng.find_path_batch(reqs) == [eng.find_path(*r[:4]) for r in reqs]
-        tickets = [eng.find_path_submit([s], [t], [1], 5) for s, t in pairs(src, dst, 12, seed=11)]
-        for (s, t), tk in zip(pairs(src, dst, 12, seed=11), tickets):
-            assert eng.find_path_wait(tk) == sorted(orc.find_path([s], [t], [1], 5, True, mode=1))
-    finally:
-        eng.close()
-        orc.close()
-    # a hub on the path: the tail stops at it and the next launch spreads it
-    rng = np.random.default_rng(7)
-    xs = np.unique(rng.integers(-(1 << 62), 1 << 62, 10000, dtype=np.int64))
-    xs = xs[(xs != 5) & (xs != 6) & (xs != 7)]
-    reach = rng.choice(xs, 30, replace=False)
-    src = np.concatenate([[5], np.full(len(xs), 6), reach])
-    dst = np.concatenate([[6], xs, np.full(len(reach), 7)])
-    w = np.zeros(len(src), np.int64)
-    eng = graphs.rmat_engine(src, dst, w)
-    orc = graphs.rmat_oracle(src, dst, w)
-    try:
-        for a, b, upto in ((5, 7, 3), (5, 7, 5), (6, 7, 2)):
-            got = eng.find_path([a], [b], [1], upto)
-            assert got == sorted(orc.find_path([a], [b], [1], upto, True, mode=1)) and got, (a, b, upto)
-    finally:
-        eng.close()
-        orc.close()
-
-
 @pytest.mark.parametrize("hits", ["spread", "head", "tail", "budget"])
 def test_shortest_through_a_hub(hits, sp_mode):
     """Greedy hops through a hub (more than 4096 out-edges, scanned by 64 workgroups and reduced by

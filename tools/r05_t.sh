@@ -9,6 +9,6 @@ tail -1 $OUT/pytest_path_tail.log
 timeout -k 10 300 python -u -m pytest tests/test_gpu_path.py -x -q --timeout 170 -k "tail_walk or two_sided or hub" \
   --timeout-method thread > $OUT/pytest_path.log 2>&1 || { tail -40 $OUT/pytest_path.log; exit 1; }
 tail -1 $OUT/pytest_path.log
-timeout -k 10 700 bash tools/sp_ab.sh r05_t/ab nebula_amd/libnbg.so nebula_amd/libnbg.so,NBG_SP_TAIL=1 \
+timeout -k 10 900 bash tools/sp_ab.sh r05_t/ab nebula_amd/libnbg.so nebula_amd/libnbg.so,NBG_SP_TAIL=1 nebula_amd/libnbg_prev.so \
   > $OUT/sp_tail_ab.txt 2>&1 || { tail -20 $OUT/sp_tail_ab.txt; exit 1; }
 cat $OUT/sp_tail_ab.txt
