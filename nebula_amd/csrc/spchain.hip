@@ -49,8 +49,9 @@ constexpr int CH_WAVES = CH_BLOCK / 64;
 // RMAT-26 10k pairs, p50 0.131 ms at 8, 0.110 at 4, 0.107 at 2 (0.104 with a 256-workgroup step
 // grid), 0.103 at 1 but p99 0.30-0.34 ms and batched -17 % (profiles/r03_vt2_sp_vt_ab.txt,
 // r03_fin2_sp_vt2_batch_ab.txt)
-constexpr int CH_VT = 2;
-constexpr int CH_TILE = 64 * CH_VT;       // items (entries + edges) per wave tile
+constexpr int CH_VT = 2;                  // the batched chains' tiles (k_ch_step_b)
+constexpr int CH_VT1 = 1;                 // the one-pair chains' tiles (k_ch_step<1>)
+constexpr int CH_TILE_MIN = 64 * CH_VT1;  // (tile splits are allocated for the shorter tiles)
 constexpr int CH_HOP_WGS = 64;            // workgroups scanning one greedy hop
 constexpr int CH_HOP_U = 4;               // neighbours per thread in flight (greedy)
 constexpr int CH_MAXS = 2 * MAX_PATH_LEN + 2;   // step launches of one query, at most
@@ -353,14 +354,15 @@ constexpr uint32_t CH_SPLITS_SOLO = 4;   // an entry covering more tile boundari
 // Entry pos of list L: vertex v, its deg edges ending at edge offset end, from row rs.  The tile
 // boundaries its merge-path range [pos + end - deg, pos + end] covers, [*t0, *t1), get the entry
 // as their split; up to CH_SPLITS_SOLO of them are written here, the caller spreads the rest.
+template <int VT>
 __device__ __forceinline__ void list_put(const ChArgs& A, const ChList& L, uint32_t pos, uint32_t v, uint32_t end,
                                          uint32_t deg, uint32_t rs, uint64_t* t0, uint64_t* t1) {
   gst(L.ids, pos, A.list_cap, v, 2, A.st);
   gst(L.seg_end, pos, A.list_cap, end, 2, A.st);
   gst(L.seg_rs, pos, A.list_cap, rs, 2, A.st);
   const uint64_t lo = (uint64_t)pos + end - deg, hi = (uint64_t)pos + end;
-  const uint64_t a = (lo + CH_TILE - 1) / CH_TILE;
-  const uint64_t b = hi / CH_TILE + 1 < A.tsplit_cap ? hi / CH_TILE + 1 : A.tsplit_cap;
+  const uint64_t a = (lo + (64 * VT) - 1) / (64 * VT);
+  const uint64_t b = hi / (64 * VT) + 1 < A.tsplit_cap ? hi / (64 * VT) + 1 : A.tsplit_cap;
   *t0 = a;
   *t1 = a < b ? b : a;
   if (*t1 - *t0 <= CH_SPLITS_SOLO) {
@@ -372,13 +374,14 @@ __device__ __forceinline__ void list_put(const ChArgs& A, const ChList& L, uint3
 // Appends, per lane, the vertices x[i] with bit i of `m` and a nonzero degree (dg[i], rs[i]) to
 // list L (counter *acc): one packed atomic per wave for positions and edge offsets; the tile
 // splits of hubs (entries spanning many tiles) are written by the whole wave, lane-strided.
+template <int VT>
 __device__ __forceinline__ void wave_append(const ChArgs& A, const ChList& L, unsigned long long* acc,
-                                            unsigned long long* err, const uint32_t (&x)[CH_VT], uint32_t m,
-                                            const uint32_t (&dg)[CH_VT], const uint32_t (&rs)[CH_VT]) {
+                                            unsigned long long* err, const uint32_t (&x)[VT], uint32_t m,
+                                            const uint32_t (&dg)[VT], const uint32_t (&rs)[VT]) {
   const int lane = threadIdx.x & 63;
   uint32_t c = 0, d = 0;
 #pragma unroll
-  for (int i = 0; i < CH_VT; ++i)
+  for (int i = 0; i < VT; ++i)
     if (((m >> i) & 1u) && dg[i]) {
       ++c;
       d += dg[i];
@@ -396,12 +399,12 @@ __device__ __forceinline__ void wave_append(const ChArgs& A, const ChList& L, un
   uint32_t pos = (uint32_t)(old >> 32) + ic - c;
   uint32_t end = (uint32_t)old + id - d;
 #pragma unroll
-  for (int i = 0; i < CH_VT; ++i) {
+  for (int i = 0; i < VT; ++i) {
     uint64_t t0 = 0, t1 = 0;
     uint32_t p = pos;
     if (((m >> i) & 1u) && dg[i]) {
       end += dg[i];
-      list_put(A, L, pos++, x[i], end, dg[i], rs[i], &t0, &t1);
+      list_put<VT>(A, L, pos++, x[i], end, dg[i], rs[i], &t0, &t1);
     }
     unsigned long long bm = __ballot(t1 > t0);
     while (bm) {   // hubs of this round: the wave writes their tile splits
@@ -475,12 +478,12 @@ __device__ __forceinline__ void first_store(const ChArgs& A, const ChQ& q, const
 // (bid, nblk: this workgroup among the query's workgroups of the launch; NW waves per workgroup)
 // (first: step 0, whose source list {s} or {t} is f0's registers — by value: a pointer to it
 // selected at run time put it in scratch memory)
-template <int NW>
+template <int NW, int VT>
 __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const ChSnap& P, int i, uint32_t bid,
                                          uint32_t nblk, bool first, const ChFirst f0) {
-  __shared__ uint32_t sEndAll[NW][CH_TILE + 2];
-  __shared__ uint32_t sRsAll[NW][CH_TILE + 1];
-  __shared__ uint16_t sSegAll[NW][CH_TILE];
+  __shared__ uint32_t sEndAll[NW][(64 * VT) + 2];
+  __shared__ uint32_t sRsAll[NW][(64 * VT) + 1];
+  __shared__ uint16_t sSegAll[NW][(64 * VT)];
   ChState* st = A.st;
   const bool bfs = P.phase == PH_BFS;
   const bool both = bfs && P.both;   // forward level kf + 1 and backward level kb + 1 in one launch
@@ -543,13 +546,13 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
   uint32_t f_own = first ? (side ? q.t : q.s) : NO_ROW, f_other = first ? (side ? q.s : q.t) : NO_ROW;
   uint64_t n = scnt >> 32, total = scnt & 0xFFFFFFFFull;
   const uint32_t* __restrict__ col = A.col[side];
-  uint64_t npath = n + total, ntiles = (npath + CH_TILE - 1) / CH_TILE;
+  uint64_t npath = n + total, ntiles = (npath + (64 * VT) - 1) / (64 * VT);
   // a two-sided level: tiles [0, nt0) are the forward side's, [nt0, nt0 + nt1) the backward's.
   // Meets: a backward claim of a vertex at forward level kf (l1stamp; LAB_M stamp kf, the meet list,
   // lmeet) or a vertex both sides claim in this launch (l2other, the other side's new stamp; LAB_M
   // stamp kf + 1, lmeet2); forward claims of vertices at backward level <= kb are no meets here
   const uint64_t nt0 = ntiles;
-  const uint64_t nt1 = both ? (((P.cnt[1] >> 32) + (P.cnt[1] & 0xFFFFFFFFull)) + CH_TILE - 1) / CH_TILE : 0;
+  const uint64_t nt1 = both ? (((P.cnt[1] >> 32) + (P.cnt[1] & 0xFFFFFFFFull)) + (64 * VT) - 1) / (64 * VT) : 0;
   const uint32_t l1stamp = stamp_of(q.ef, P.kf), l2m = stamp_of(q.em, P.kf + 1);
   uint32_t l2other = stamp_of(q.eb, P.kb + 1);
   if (both) mstamp = 0;   // (forward tiles record no position-kf meets)
@@ -592,7 +595,7 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
     } else if (both && side == 1) {
       t = tg - nt0;
     }
-    uint32_t c[CH_VT];   // the vertex a claim is about: the neighbour, or (pull) the list entry
+    uint32_t c[VT];   // the vertex a claim is about: the neighbour, or (pull) the list entry
     uint32_t cm = 0, mm = 0;
     // once this level has met, its claims are not expanded again: their appends are skipped
     // (read now, used after the claims: the load is off the critical path).  A two-sided level
@@ -600,15 +603,15 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
     const unsigned long long met_now = bfs && !both ? ld_agent(&C.lmeet[i]) : 0ull;
     uint64_t sp = 0;
     if (first) {   // one entry: every tile's split is 0, the last tile's end is 1
-      sp = lane == 1 && (t + 1) * CH_TILE >= npath ? n : 0;
+      sp = lane == 1 && (t + 1) * (64 * VT) >= npath ? n : 0;
     } else if (ntiles > 1) {
       if (lane == 0) sp = gld(S.tsplit, t, A.tsplit_cap, 3, st);
-      if (lane == 1) sp = (t + 1) * CH_TILE >= npath ? n : gld(S.tsplit, t + 1, A.tsplit_cap, 3, st);
+      if (lane == 1) sp = (t + 1) * (64 * VT) >= npath ? n : gld(S.tsplit, t + 1, A.tsplit_cap, 3, st);
     } else {
       sp = lane == 1 ? n : 0;   // one tile: no split to read
     }
     const uint64_t a0 = uniform64(__shfl(sp, 0, 64)), a1 = uniform64(__shfl(sp, 1, 64));
-    const uint64_t d0 = t * CH_TILE, d1 = d0 + CH_TILE < npath ? d0 + CH_TILE : npath;
+    const uint64_t d0 = t * (64 * VT), d1 = d0 + (64 * VT) < npath ? d0 + (64 * VT) : npath;
     // a split that does not describe this tile (stale list memory) skips it and fails the search
     // (ChCtr::err bit 4, "device search aborted") instead of indexing out of bounds
     const bool bad = !(a0 <= a1 && a1 <= n && a1 - a0 <= d1 - d0 && d1 - a1 <= total && d0 - a0 <= d1 - a1);
@@ -629,7 +632,7 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
     wave_lds_sync();
     const uint32_t* Aend = sEnd + 1;   // Aend[j] = end of entry a0 + j
     {   // lane-level merge path: the entry of every edge item
-      const int diag = lane * CH_VT, dmax = na + nb;
+      const int diag = lane * VT, dmax = na + nb;
       if (diag < dmax) {
         int lo = diag > nb ? diag - nb : 0, hi = diag < na ? diag : na;
         while (lo < hi) {
@@ -639,7 +642,7 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
         }
         int ai = lo, bi = diag - lo;
 #pragma unroll
-        for (int kk = 0; kk < CH_VT; ++kk) {
+        for (int kk = 0; kk < VT; ++kk) {
           if (ai + bi >= dmax) break;
           if (ai < na && (bi >= nb || (uint64_t)Aend[ai] <= b0 + (uint64_t)bi)) {
             ++ai;
@@ -652,9 +655,9 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
     }
     wave_lds_sync();
     // neighbours (and, pulling, the list entry each edge belongs to), all loads in flight
-    uint32_t x[CH_VT], seg[CH_VT];
+    uint32_t x[VT], seg[VT];
 #pragma unroll
-    for (int j = 0; j < CH_VT; ++j) {
+    for (int j = 0; j < VT; ++j) {
       const int kk = j * 64 + lane;
       x[j] = NO_ROW;
       seg[j] = 0;
@@ -666,28 +669,28 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
     }
     wave_lds_sync();   // (the next tile rewrites the window)
     if (pull) {
-      uint32_t tl[CH_VT], vis[CH_VT];
+      uint32_t tl[VT], vis[VT];
 #pragma unroll
-      for (int j = 0; j < CH_VT; ++j) {
+      for (int j = 0; j < VT; ++j) {
         tl[j] = x[j] != NO_ROW ? gld(tlab, x[j], A.nv, 6, st) : 0u;
         vis[j] = x[j] != NO_ROW && A.visible ? gld(A.visible, x[j], A.nv, 6, st) : 1u;
       }
 #pragma unroll
-      for (int j = 0; j < CH_VT; ++j)
+      for (int j = 0; j < VT; ++j)
         c[j] = (x[j] != NO_ROW && tl[j] == tstamp && vis[j]) ? gld(S.ids, a0 + seg[j], A.list_cap, 7, st) : NO_ROW;
     } else {
 #pragma unroll
-      for (int j = 0; j < CH_VT; ++j) c[j] = x[j];
+      for (int j = 0; j < VT; ++j) c[j] = x[j];
     }
-    uint32_t old[CH_VT], gate[CH_VT];
+    uint32_t old[VT], gate[VT];
     // a BFS level before its meet: the other side's label and the degree / row start of EVERY
     // neighbour are loaded with its own label, so the meet test and the append do not wait for
     // two more round trips after the claim (the extra loads are cheap: a level runs far below the
     // HBM bandwidth, profiles/r03_t_sp_step_pmc.txt)
     const bool spec = bfs && !met_now;   // (wave-uniform)
-    uint32_t sol[CH_VT], sdg[CH_VT], srs[CH_VT];
+    uint32_t sol[VT], sdg[VT], srs[VT];
 #pragma unroll
-    for (int j = 0; j < CH_VT; ++j) {
+    for (int j = 0; j < VT; ++j) {
       old[j] = c[j] != NO_ROW ? gld(lab, c[j], A.nv, 8, st) : 0u;
       gate[j] = (c[j] != NO_ROW && rlab) ? gld(rlab, c[j], A.nv, 8, st) : rstamp;
       sol[j] = 0;
@@ -705,14 +708,14 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
     if (met_now) {
       // the level has met: only meet vertices matter now (B[kf] is the met set; this level's other
       // labels are read by nothing), so the other side's label is tested before claiming
-      uint32_t ol[CH_VT];
+      uint32_t ol[VT];
 #pragma unroll
-      for (int j = 0; j < CH_VT; ++j) {
+      for (int j = 0; j < VT; ++j) {
         ol[j] = (c[j] != NO_ROW && !live(old[j], epoch)) ? gld(olab, c[j], A.nv, 9, st) : 0u;
         if (first && c[j] == f_other) ol[j] = stamp_of(oepoch, 0);
       }
 #pragma unroll
-      for (int j = 0; j < CH_VT; ++j) {
+      for (int j = 0; j < VT; ++j) {
         if (c[j] == NO_ROW || live(old[j], epoch) || !live(ol[j], oepoch)) continue;
         if (CH_GUARD && c[j] >= A.nv) continue;
         if (atomicCAS(lab + c[j], old[j], stamp) != old[j]) continue;
@@ -720,7 +723,7 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < CH_VT; ++j) {
+      for (int j = 0; j < VT; ++j) {
         if (c[j] == NO_ROW || gate[j] != rstamp || live(old[j], epoch)) continue;
         if (CH_GUARD && c[j] >= A.nv) continue;
         if (atomicCAS(lab + c[j], old[j], stamp) != old[j]) continue;
@@ -729,12 +732,12 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
     }
     if (spec && !both) {   // meet test: the claimed vertices the other side has labelled
 #pragma unroll
-      for (int j = 0; j < CH_VT; ++j)
+      for (int j = 0; j < VT; ++j)
         if (((cm >> j) & 1u) && live(sol[j], oepoch)) mm |= 1u << j;
     } else if (both) {
       uint32_t m2 = 0;
 #pragma unroll
-      for (int j = 0; j < CH_VT; ++j) {
+      for (int j = 0; j < VT; ++j) {
         if (!((cm >> j) & 1u)) continue;
         uint32_t o = sol[j];
         if (side == 1 && o == l1stamp) {   // backward level kb + 1 at forward level kf
@@ -748,7 +751,7 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
       if (__ballot(m2 != 0)) {
         uint32_t n2 = 0;
 #pragma unroll
-        for (int j = 0; j < CH_VT; ++j)
+        for (int j = 0; j < VT; ++j)
           if ((m2 >> j) & 1u) {
             gst(A.lab[2], c[j], A.nv, l2m, 10, st);   // (both claimers may store it: the same value)
             ++n2;
@@ -762,9 +765,9 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
     // appends: one packed atomic per wave and list (aggregating them per workgroup behind two
     // barriers measured 4 % slower, profiles/r03_v_sp_wg_append_ab.txt)
     const uint32_t am = append && !met_now ? cm : 0u;
-    uint32_t dg[CH_VT], rs[CH_VT];
+    uint32_t dg[VT], rs[VT];
 #pragma unroll
-    for (int j = 0; j < CH_VT; ++j) {
+    for (int j = 0; j < VT; ++j) {
       dg[j] = 0;
       rs[j] = 0;
       if ((am >> j) & 1u) {
@@ -776,11 +779,11 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
         }
       }
     }
-    if (append && !met_now) wave_append(A, D, out_acc, &C.err, c, am, dg, rs);   // (a wave-uniform condition)
+    if (append && !met_now) wave_append<VT>(A, D, out_acc, &C.err, c, am, dg, rs);   // (a wave-uniform condition)
     // the sides met: LAB_M stamps, the meet list over in-edges, the level's meet count
     uint32_t nm = 0;
 #pragma unroll
-    for (int j = 0; j < CH_VT; ++j) {
+    for (int j = 0; j < VT; ++j) {
       dg[j] = 0;
       rs[j] = 0;
       if ((mm >> j) & 1u) {
@@ -793,7 +796,7 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) nm += __shfl_xor(nm, o, 64);
       if (lane == 0) atomicAdd(&C.lmeet[i], (unsigned long long)nm);
-      wave_append(A, A.list[CL_M], &C.macc, &C.err, c, mm, dg, rs);
+      wave_append<VT>(A, A.list[CL_M], &C.macc, &C.err, c, mm, dg, rs);
     }
   }
 }
@@ -816,7 +819,7 @@ __device__ __forceinline__ uint64_t step_items(const ChSnap& P) {
 // q.solo items — steps run by workgroup 0 alone, back to back, until the search is over or a step
 // needs the grid (the launch boundary then orders it after this workgroup's writes).
 // Returns false when the search was over before this launch (the launch is then a greedy one).
-template <int NW>
+template <int NW, int VT>
 __device__ __forceinline__ bool ch_step(const ChArgs& A, const ChQ& q, int i, uint32_t bid, uint32_t nblk) {
   ChState* st = A.st;
   ChCtr& C = st->c[q.par];
@@ -837,8 +840,8 @@ __device__ __forceinline__ bool ch_step(const ChArgs& A, const ChQ& q, int i, ui
   if (i == 0 && bid == 0) {
     // the splits of {s} and {t} for later launches (a backward level from {t}, a pull B-set step
     // from {s}): one entry, so every tile's split is 0
-    for (uint64_t t = threadIdx.x; t * CH_TILE <= f0.dsf && t < A.tsplit_cap; t += CH_BLOCK) A.list[CL_F0].tsplit[t] = 0;
-    for (uint64_t t = threadIdx.x; t * CH_TILE <= f0.dsb && t < A.tsplit_cap; t += CH_BLOCK) A.list[CL_B0].tsplit[t] = 0;
+    for (uint64_t t = threadIdx.x; t * (64 * VT) <= f0.dsf && t < A.tsplit_cap; t += CH_BLOCK) A.list[CL_F0].tsplit[t] = 0;
+    for (uint64_t t = threadIdx.x; t * (64 * VT) <= f0.dsb && t < A.tsplit_cap; t += CH_BLOCK) A.list[CL_B0].tsplit[t] = 0;
     if (lead) first_store(A, q, f0, P);
   }
   if (P.phase == PH_DONE) {
@@ -853,7 +856,7 @@ __device__ __forceinline__ bool ch_step(const ChArgs& A, const ChQ& q, int i, ui
       if (j > 0) st->snap[j] = P;   // (step j + 1 derives its snapshot from it; snap[0]: first_store)
       if (!solo) st->first[i + 1] = j + 1;
     }
-    ch_level<NW>(A, q, P, (int)j, solo ? 0u : bid, solo ? 1u : nblk, j == 0, f0);
+    ch_level<NW, VT>(A, q, P, (int)j, solo ? 0u : bid, solo ? 1u : nblk, j == 0, f0);
     if (!solo) return true;
     // this workgroup's stores and atomics before the next step's reads (labels, lists, counters;
     // the acquire drops L1 lines read before another wave's claims); the snapshot is read back
@@ -1100,16 +1103,21 @@ __device__ __forceinline__ void ch_out(const ChArgs& A, const ChQ& q, int steps,
 // Step launch i: a search step, or — the search over — greedy launch i - hop_first (its first
 // CH_HOP_WGS workgroups), so the walk runs in the launches that used to return at once.  (out:
 // the batch's last launch stores the result, when the search was over before it.)
-template <int NW>
+template <int NW, int VT>
 __device__ __forceinline__ void ch_any(const ChArgs& A, const ChQ& q, int i, uint32_t bid, uint32_t nblk, ChOut* out) {
-  if (ch_step<NW>(A, q, i, bid, nblk) || i == 0 || bid >= (uint32_t)CH_HOP_WGS) return;
+  if (ch_step<NW, VT>(A, q, i, bid, nblk) || i == 0 || bid >= (uint32_t)CH_HOP_WGS) return;
   const int h = i - hop_first(A.st->c[q.par]);
   if (ch_hop(A, q, i, h, bid, nblk < (uint32_t)CH_HOP_WGS ? nblk : (uint32_t)CH_HOP_WGS) && out)
     ch_out(A, q, i, h + 1, out);
 }
 
+// VT: items per lane of a chain tile — 1 for one-pair chains (a level's critical path is the slowest
+// wave's chain of dependent accesses, so shorter tiles cut the latency: RMAT-26 p50 0.0871-0.0876
+// -> 0.0818-0.0836 ms, profiles/r05_u_sp_vt1_ab.txt), 2 for batched chains and their continuations
+// (2-item tiles keep the batched rate: 37.3-37.7 k -> 41.2-41.5 k pairs/s)
+template <int VT>
 __global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) k_ch_step(const ChArgs* __restrict__ Ap, ChQ q, int i, ChOut* out) {
-  ch_any<CH_WAVES>(*Ap, q, i, blockIdx.x, gridDim.x, out);
+  ch_any<CH_WAVES, VT>(*Ap, q, i, blockIdx.x, gridDim.x, out);
 }
 
 // Greedy launches of a continuation (a hub's hop ended the walk's launch): launch j after the nl
@@ -1133,7 +1141,7 @@ struct ChBatch {
 // (2 waves/SIMD: no spills; batched 33.3-33.9k -> 34.7-35.0k pairs/s, profiles/r03_y_sp_spec_ab.txt)
 __global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) k_ch_step_b(ChBatch b, int i, int last) {
   const uint32_t p = blockIdx.x / b.per;
-  if ((int)p < b.n) ch_any<CH_WAVES>(*b.A[p], b.q[p], i, blockIdx.x % b.per, b.per, last ? b.out[p] : nullptr);
+  if ((int)p < b.n) ch_any<CH_WAVES, CH_VT>(*b.A[p], b.q[p], i, blockIdx.x % b.per, b.per, last ? b.out[p] : nullptr);
 }
 
 // ---------------------------------------------------------------------------- host side
@@ -1207,7 +1215,7 @@ ChainCtx* chain_create(uint64_t nv, uint64_t edge_cap, hipStream_t s, std::strin
   c->stream = s;
   c->nv = nv;
   c->list_cap = nv + 1;
-  c->tsplit_cap = (nv + 1 + edge_cap) / CH_TILE + 2;
+  c->tsplit_cap = (nv + 1 + edge_cap) / CH_TILE_MIN + 2;
   const char* g = getenv("NBG_SP_GRID");
   if (g && atoi(g) > 0) c->grid = (unsigned)atoi(g);
   const char* so = getenv("NBG_SP_SOLO");
@@ -1264,8 +1272,13 @@ static hipError_t chain_batch(ChainCtx* c, int k, int h) {
   h = std::min(h, CH_MAXS - c->hops);
   for (int j = 0; j < k; ++j, ++c->steps)
     c->timed(CHK_STEP, [&] {
-      hipLaunchKernelGGL(k_ch_step, dim3(c->grid), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps,
-                         h <= 0 && j + 1 == k ? c->d_out : (ChOut*)nullptr);
+      // (a batched query's continuation keeps its chain's tile size: its lists' splits are per tile)
+      if (c->last_batched)
+        hipLaunchKernelGGL(k_ch_step<CH_VT>, dim3(c->grid), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps,
+                           h <= 0 && j + 1 == k ? c->d_out : (ChOut*)nullptr);
+      else
+        hipLaunchKernelGGL(k_ch_step<CH_VT1>, dim3(c->grid), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps,
+                           h <= 0 && j + 1 == k ? c->d_out : (ChOut*)nullptr);
     });
   for (int j = 0; j < h; ++j, ++c->hops)
     c->timed(CHK_HOP, [&] {
@@ -1425,6 +1438,11 @@ void chain_result(const ChainCtx* c, SpResult* out) {
   out->levels = F.levels;
   out->abytes = F.abytes;
   out->launches = (unsigned long long)(c->steps + c->hops);
+  // NBG_SP_TRACE=2: one line per query (the chain's step and greedy launches, batches, path length)
+  static const bool per_query = getenv("NBG_SP_TRACE") && atoi(getenv("NBG_SP_TRACE")) == 2;
+  if (per_query)
+    fprintf(stderr, "[sp q] steps %d hops %d busy %llu hlaunch %llu L %llu\n", c->steps, c->hops, h.busy, h.hlaunch,
+            (unsigned long long)out->L);
   const uint32_t hpos = (uint32_t)(h.hpos >> 32);
   out->L = (F.met && !h.err && hpos == F.L) ? F.L : 0;
   if (F.met && !h.err && hpos != F.L) out->err = 2;   // (cannot happen: the hops were enqueued)
