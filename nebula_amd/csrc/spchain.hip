@@ -1438,15 +1438,15 @@ void chain_result(const ChainCtx* c, SpResult* out) {
   out->levels = F.levels;
   out->abytes = F.abytes;
   out->launches = (unsigned long long)(c->steps + c->hops);
-  // NBG_SP_TRACE=2: one line per query (the chain's step and greedy launches, batches, path length)
-  static const bool per_query = getenv("NBG_SP_TRACE") && atoi(getenv("NBG_SP_TRACE")) == 2;
-  if (per_query)
-    fprintf(stderr, "[sp q] steps %d hops %d busy %llu hlaunch %llu L %llu\n", c->steps, c->hops, h.busy, h.hlaunch,
-            (unsigned long long)out->L);
   const uint32_t hpos = (uint32_t)(h.hpos >> 32);
   out->L = (F.met && !h.err && hpos == F.L) ? F.L : 0;
   if (F.met && !h.err && hpos != F.L) out->err = 2;   // (cannot happen: the hops were enqueued)
   if (out->L) memcpy(out->path, h.path, (1 + 3 * (size_t)out->L) * sizeof(long long));
+  // NBG_SP_TRACE=2: one line per query (the chain's step and greedy launches, path length)
+  static const bool per_query = getenv("NBG_SP_TRACE") && atoi(getenv("NBG_SP_TRACE")) == 2;
+  if (per_query)
+    fprintf(stderr, "[sp q] steps %d hops %d busy %llu hlaunch %llu L %llu\n", c->steps, c->hops, h.busy, h.hlaunch,
+            (unsigned long long)out->L);
 }
 
 // nbg_profile over the chain: mode 0 off, 1 every launch, 2 step launches only (counters reset)

@@ -26,7 +26,9 @@ for s, t in pairs[:32]:
 sys.stderr.flush()
 print("MARK", file=sys.stderr, flush=True)
 lat = []
-for s, t in pairs:
+for i, (s, t) in enumerate(pairs):
+    sys.stderr.write("Q %d\n" % i)
+    sys.stderr.flush()
     q0 = time.perf_counter()
     eng.find_path([s], [t], [1], 5)
     lat.append((time.perf_counter() - q0) * 1e3)

@@ -6,9 +6,17 @@ import sys
 import numpy as np
 
 lines = open(sys.argv[1]).read().split("MARK", 1)[1].splitlines()
-recs = [tuple(int(x) for x in re.findall(r"-?\d+", l)) for l in lines if l.startswith("[sp q]")]
 lat = np.load(sys.argv[2])
-assert len(recs) == len(lat), (len(recs), len(lat))
+# one "Q i" marker per query; queries answered without a chain (an endpoint with no edges) have
+# no "[sp q]" line and count as 0 steps / 0 hops / L 0
+recs = [(0, 0, 0, 0, 0)] * len(lat)
+q = -1
+for l in lines:
+    if l.startswith("Q "):
+        q = int(l.split()[1])
+    elif l.startswith("[sp q]"):
+        recs[q] = tuple(int(x) for x in re.findall(r"-?\d+", l))
+print("queries with a chain: %d of %d" % (sum(1 for r in recs if r[0] or r[1]), len(lat)))
 hops = np.array([r[1] for r in recs])
 steps = np.array([r[0] for r in recs])
 L = np.array([r[4] for r in recs])
