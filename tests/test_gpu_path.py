@@ -131,6 +131,50 @@ def test_shortest_through_a_hub(hits, sp_mode):
         orc.close()
 
 
+@pytest.mark.parametrize("hits", ["rank_first", "vid_first"])
+def test_shortest_through_a_ranked_hub(hits, sp_mode):
+    """A hub row with ranks (more than 4096 out-edges: its hop is spread over workgroups): 6,000
+    out-edges to 4,500 vids of both signs with ranks in [-3, 3], some vids twice under two ranks.  The x that reach t either win on rank with a large vid (rank_first) or tie on rank
+    and win on vid (vid_first); the greedy's minimum is the signed (rank, vid), whatever the
+    row's key order."""
+    from nebula_amd import Engine, kvgen
+    from tests.support.oracle import Oracle
+    rng = np.random.default_rng({"rank_first": 5, "vid_first": 6}[hits])
+    s_v, hub, t_v = 5, 6, 7
+    xs = np.unique(rng.integers(-(1 << 62), 1 << 62, 4500, dtype=np.int64))
+    xs = xs[(xs != s_v) & (xs != hub) & (xs != t_v)]
+    hx = np.concatenate([xs, rng.choice(xs, 1500, replace=False)])
+    hr = rng.integers(-3, 4, len(hx))
+    order = np.lexsort((hx, hr))          # signed (rank, vid): the canonical order
+    if hits == "rank_first":
+        reach = [int(hx[order[0]])] + [int(v) for v in rng.choice(xs, 20, replace=False)]
+    else:
+        reach = [int(hx[order[k]]) for k in (0, 1, 2)] + [int(v) for v in rng.choice(xs, 20, replace=False)]
+    kb = kvgen.KVBuilder(100)
+    ts = 1_600_000_000_000_000
+    kb.insert_edge(s_v, hub, graphs.E_TYPE, 0, graphs.E_SCHEMA, [1], ts)
+    for x, r in zip(hx.tolist(), hr.tolist()):
+        kb.insert_edge(hub, x, graphs.E_TYPE, r, graphs.E_SCHEMA, [2], ts)
+    for x in set(reach):
+        kb.insert_edge(x, t_v, graphs.E_TYPE, 0, graphs.E_SCHEMA, [3], ts)
+    eng = Engine(100)
+    eng.register_edge(graphs.E_TYPE, "e", graphs.E_SCHEMA)
+    eng.load_builder(kb)
+    orc = Oracle(100)
+    orc.register(True, graphs.E_TYPE, "e", graphs.E_SCHEMA)
+    orc.load_builder(kb)
+    try:
+        for a, b, upto in ((s_v, t_v, 3), (hub, t_v, 2), (s_v, t_v, 5)):
+            got = eng.find_path([a], [b], [1], upto)
+            exp = orc.find_path([a], [b], [1], upto, True, mode=1)
+            assert got == sorted(exp) and got, (hits, a, b, upto)
+        reqs = [([s_v], [t_v], [1], 4, True), ([hub], [t_v], [1], 3, True)]
+        assert eng.find_path_batch(reqs) == [eng.find_path(*r[:4]) for r in reqs]
+    finally:
+        eng.close()
+        orc.close()
+
+
 def test_rmat_shortest_self_and_unknown(rmat12, sp_mode):
     """s == t needs a cycle (walk length >= 1); unknown vids have no rows."""
     src, dst, eng, orc = rmat12
