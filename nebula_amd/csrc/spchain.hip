@@ -116,6 +116,13 @@ struct ChState {        // device; the host reads what the result launch derives
   ChSnap snap[CH_MAXS];
   long long path[1 + 3 * MAX_PATH_LEN];
   unsigned long long gpart[4 * CH_HOP_WGS];
+  // hub hops inside the walking workgroup's launch (ch_hop<true>): the walker posts job k of greedy
+  // launch h as hjob = (tag << 32 | h << 16 | k << 8 | pos) after its row range hjob_rng; helper
+  // workgroup b stores its share's minimum into hpart[4b..4b+3] and then htag[b] = the job word.
+  // Every word is tagged by the batch, launch and job, so nothing is reset between launches.
+  unsigned long long hjob, hjob_rng;
+  unsigned long long htag[CH_HOP_WGS];
+  unsigned long long hpart[4 * CH_HOP_WGS];
 };
 
 // What the host reads after a chain, stored by its last launch (ch_out) straight into mapped
@@ -955,20 +962,42 @@ __device__ __forceinline__ Cand hop_scan(const ChArgs& A, const uint32_t* vlab, 
 
 }  // namespace
 
+// Hub hops in the walk's launch (COOP): the workgroups that are not walking wait for the walker's
+// jobs instead of returning.  Every wait is bounded (wall clock): a helper gives up after
+// CH_HELP_IDLE without a job, the walker after CH_JOB_WAIT without every helper's answer, and then
+// leaves the hub to the next launch's spread scan as before.  Only one-pair chains use it (a
+// launch of at most CH_HOP_WGS walking workgroups per query, far below the chip's residency); a
+// batch's pairs do not all have their workgroups resident together.
+constexpr long long CH_HELP_IDLE = 20000;   // steady-counter ticks (100 MHz: 200 us)
+constexpr long long CH_JOB_WAIT = 10000;    // (100 us)
+constexpr unsigned CH_JOB_END = 255;        // the job number of "the walk is over"
+
+__device__ __forceinline__ unsigned long long job_word(const ChQ& q, int h, unsigned k, uint32_t pos) {
+  return ((unsigned long long)q.tag << 32) | ((unsigned long long)(h & 0xFFFF) << 16) | ((k & 0xFFu) << 8) | (pos & 0xFFu);
+}
+
+// The walker's end of the walk in launch h (thread 0): the helpers return.
+__device__ __forceinline__ void post_end(ChState* st, const ChQ& q, int h) {
+  __hip_atomic_store(&st->hjob, job_word(q, h, CH_JOB_END, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Greedy hops (CH_HOP_WGS workgroups), launch h of the query.  The state after step launch
 // `last` says whether the sides met and the path length L; the launch starts from hstart[h] =
 // (pos, c): hop pos (< L) takes the minimum (type, rank, dst vid) out-edge of the current vertex c
 // into B[pos + 1] (B[pos + 1] = LAB_M stamp pos + 1 for positions <= kf, backward level
 // L - pos - 1 beyond).  A hub's hop is scanned by every workgroup and reduced by the last one to
 // finish; small hops are taken by one workgroup alone (workgroup 0, or the reducing one after a
-// hub), which walks on until the path is complete or the next vertex is a hub — left to the next
-// launch — and writes hstart[h + 1].  Returns true in that one writing workgroup (every thread):
+// hub), which walks on until the path is complete.  A hub met on the way is spread over the
+// other workgroups as a job (COOP), or (no COOP, or a job unanswered) left to the next launch.
+// The walker writes hstart[h + 1].  Returns true in that one writing workgroup (every thread):
 // it is the launch's last to touch the query's state, so it may also store the result.
 // (bid, nblk: this workgroup among the query's nblk <= CH_HOP_WGS workgroups of the launch)
+template <bool COOP>
 __device__ __forceinline__ bool ch_hop(const ChArgs& A, const ChQ& q, int nl, int h, uint32_t bid, uint32_t nblk) {
   __shared__ Cand lds[CH_WAVES + 1];
   __shared__ Cand hop_slots[2][CH_WAVES];
   __shared__ int s_last;
+  __shared__ unsigned long long s_job[2];
   ChState* st = A.st;
   ChCtr& C = st->c[q.par];
   const ChSnap F = snap_for(st, q, (int)st->first[nl]);   // the state after the nl step launches
@@ -1007,6 +1036,48 @@ __device__ __forceinline__ bool ch_hop(const ChArgs& A, const ChQ& q, int nl, in
     gst(st->path, 3 + 3 * (uint64_t)p, 1 + 3 * (uint64_t)MAX_PATH_LEN, (long long)r.v, 15, st);
     return true;
   };
+  // a helper: jobs 1, 2, ... of this launch until the end of the walk (or CH_HELP_IDLE without one)
+  auto help = [&]() {
+    for (unsigned k = 1; k < CH_JOB_END; ++k) {
+      if (threadIdx.x == 0) {
+        const long long t0 = wall_clock64();
+        const unsigned long long mine = job_word(q, h, 0, 0) >> 16;   // (tag, launch)
+        unsigned long long a = 0;
+        for (;;) {
+          const unsigned long long x = __hip_atomic_load(&st->hjob, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((x >> 16) == mine && ((x >> 8) & 0xFFu) >= k) {
+            a = x;
+            break;
+          }
+          if (wall_clock64() - t0 > CH_HELP_IDLE) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        s_job[0] = a;
+        if (a) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          s_job[1] = ld_agent(&st->hjob_rng);
+        }
+      }
+      __syncthreads();
+      const unsigned long long a = s_job[0], rng = s_job[1];
+      __syncthreads();   // (thread 0 rewrites s_job for the next job)
+      if (!a || ((a >> 8) & 0xFFu) != k) return;   // the end, or no job within CH_HELP_IDLE
+      const uint32_t* vlab;
+      const uint32_t want = want_of((uint32_t)(a & 0xFFu), &vlab);
+      Cand best = hop_scan(A, vlab, want, (uint32_t)rng, (uint32_t)(rng >> 32), (uint64_t)bid * CH_BLOCK + threadIdx.x,
+                           (uint64_t)nblk * CH_BLOCK);
+      best = block_min(best, lds);
+      if (threadIdx.x == 0) {
+        unsigned long long* part = st->hpart + 4 * bid;
+        part[0] = (unsigned long long)best.t;
+        part[1] = (unsigned long long)best.r;
+        part[2] = (unsigned long long)best.v;
+        part[3] = best.d;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_store(&st->htag[bid], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  };
   uint32_t rs, re;
   range(c, &rs, &re);
   if (re - rs > CH_SOLO_DEG) {   // a hub: every workgroup scans a share
@@ -1024,7 +1095,10 @@ __device__ __forceinline__ bool ch_hop(const ChArgs& A, const ChQ& q, int nl, in
       s_last = atomicAdd(&st->gticket, 1ull) == nblk - 1;
     }
     __syncthreads();
-    if (!s_last) return false;
+    if (!s_last) {
+      if (COOP) help();
+      return false;
+    }
     __threadfence();
     Cand r = none;
     if (threadIdx.x < nblk) {
@@ -1035,29 +1109,94 @@ __device__ __forceinline__ bool ch_hop(const ChArgs& A, const ChQ& q, int nl, in
     if (threadIdx.x == 0) {
       st->gticket = 0;
       s_last = record(pos, r);
+      if (COOP && !s_last) post_end(st, q, h);
     }
     __syncthreads();
     if (!s_last) return true;   // (a reconstruction failure: recorded and finished)
     c = r.d;
     ++pos;
   } else if (bid != 0) {
+    if (COOP) help();
     return false;
   }
-  // this workgroup alone: small hops
+  // this workgroup alone: small hops, and (COOP) hubs' hops as jobs for the others
   if (threadIdx.x == 0) C.hlaunch += 1;
+  uint32_t par = 0;   // block_min1's slot set, alternating per reduction
+  unsigned jobs = 0;
   while (pos < L) {
     range(c, &rs, &re);
-    if (re - rs > CH_SOLO_DEG) break;   // a hub: the next launch spreads it
     const uint32_t* vlab;
     const uint32_t want = want_of(pos, &vlab);
-    // (one barrier per hop: every thread has the minimum, so none waits for thread 0's record)
-    const Cand r = block_min1(hop_scan(A, vlab, want, rs, re, threadIdx.x, CH_BLOCK), hop_slots, pos & 1u);
+    Cand r;
+    if (re - rs > CH_SOLO_DEG) {   // a hub
+      if (!COOP || nblk < 2 || jobs + 1 >= CH_JOB_END) break;   // the next launch spreads it
+      const unsigned long long a = job_word(q, h, ++jobs, pos);
+      if (threadIdx.x == 0) {
+        __hip_atomic_store(&st->hjob_rng, (unsigned long long)rs | ((unsigned long long)re << 32), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_store(&st->hjob, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      r = block_min(hop_scan(A, vlab, want, rs, re, (uint64_t)bid * CH_BLOCK + threadIdx.x, (uint64_t)nblk * CH_BLOCK),
+                    lds);
+      // wave 0 collects the helpers' answers: lane l waits for htag[l] == a (bounded)
+      if (threadIdx.x < 64) {
+        const uint32_t l = threadIdx.x;
+        const long long t0 = wall_clock64();
+        bool all = false;
+        for (;;) {
+          const bool ok = l >= nblk || l == bid || ld_agent(&st->htag[l]) == a;
+          all = __all(ok);
+          if (all || wall_clock64() - t0 > CH_JOB_WAIT) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        Cand x = none;
+        if (all) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          if (l < nblk && l != bid) {
+            const unsigned long long* p = st->hpart + 4 * l;
+            x = Cand{(int64_t)ld_agent(p), (int64_t)ld_agent(p + 1), (int64_t)ld_agent(p + 2), (uint32_t)ld_agent(p + 3)};
+          }
+        }
+        if (l == 0) {
+          if (cand_less(r, x)) x = r;   // (the walker's own share)
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          Cand y;
+          y.t = __shfl_down(x.t, o, 64);
+          y.r = __shfl_down(x.r, o, 64);
+          y.v = __shfl_down(x.v, o, 64);
+          y.d = __shfl_down(x.d, o, 64);
+          if (l + o < 64 && cand_less(y, x)) x = y;
+        }
+        if (l == 0) {
+          hop_slots[0][0] = x;
+          s_last = all;
+        }
+      }
+      __syncthreads();
+      const bool answered = s_last;
+      r = hop_slots[0][0];
+      __syncthreads();
+      if (!answered) break;   // a helper did not answer in time: the next launch spreads it
+    } else {
+      // (one barrier per reduction: every thread has the minimum, so none waits for thread 0's record)
+      r = block_min1(hop_scan(A, vlab, want, rs, re, threadIdx.x, CH_BLOCK), hop_slots, par);
+      par ^= 1u;
+    }
     if (threadIdx.x == 0) record(pos, r);
-    if (r.d == NO_ROW) return true;   // (a reconstruction failure: recorded and finished)
+    if (r.d == NO_ROW) {   // (a reconstruction failure: recorded and finished)
+      if (COOP && threadIdx.x == 0) post_end(st, q, h);
+      return true;
+    }
     c = r.d;
     ++pos;
   }
-  if (threadIdx.x == 0) finish(pos, c);
+  if (threadIdx.x == 0) {
+    finish(pos, c);
+    if (COOP) post_end(st, q, h);
+  }
   return true;
 }
 
@@ -1103,11 +1242,11 @@ __device__ __forceinline__ void ch_out(const ChArgs& A, const ChQ& q, int steps,
 // Step launch i: a search step, or — the search over — greedy launch i - hop_first (its first
 // CH_HOP_WGS workgroups), so the walk runs in the launches that used to return at once.  (out:
 // the batch's last launch stores the result, when the search was over before it.)
-template <int NW, int VT>
+template <int NW, int VT, bool COOP>
 __device__ __forceinline__ void ch_any(const ChArgs& A, const ChQ& q, int i, uint32_t bid, uint32_t nblk, ChOut* out) {
   if (ch_step<NW, VT>(A, q, i, bid, nblk) || i == 0 || bid >= (uint32_t)CH_HOP_WGS) return;
   const int h = i - hop_first(A.st->c[q.par]);
-  if (ch_hop(A, q, i, h, bid, nblk < (uint32_t)CH_HOP_WGS ? nblk : (uint32_t)CH_HOP_WGS) && out)
+  if (ch_hop<COOP>(A, q, i, h, bid, nblk < (uint32_t)CH_HOP_WGS ? nblk : (uint32_t)CH_HOP_WGS) && out)
     ch_out(A, q, i, h + 1, out);
 }
 
@@ -1117,14 +1256,14 @@ __device__ __forceinline__ void ch_any(const ChArgs& A, const ChQ& q, int i, uin
 // (2-item tiles keep the batched rate: 37.3-37.7 k -> 41.2-41.5 k pairs/s)
 template <int VT>
 __global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) k_ch_step(const ChArgs* __restrict__ Ap, ChQ q, int i, ChOut* out) {
-  ch_any<CH_WAVES, VT>(*Ap, q, i, blockIdx.x, gridDim.x, out);
+  ch_any<CH_WAVES, VT, true>(*Ap, q, i, blockIdx.x, gridDim.x, out);
 }
 
 // Greedy launches of a continuation (a hub's hop ended the walk's launch): launch j after the nl
 // step launches is greedy launch nl - hop_first + j; the batch's last stores the result.
 __global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ Ap, ChQ q, int nl, int j, ChOut* out) {
   const int h = nl - hop_first(Ap->st->c[q.par]) + j;
-  if (ch_hop(*Ap, q, nl, h, blockIdx.x, gridDim.x) && out) ch_out(*Ap, q, nl, h + 1, out);
+  if (ch_hop<true>(*Ap, q, nl, h, blockIdx.x, gridDim.x) && out) ch_out(*Ap, q, nl, h + 1, out);
 }
 
 // ... or up to CH_BMAX queries per launch (a batch of pairs, each with its own workspace, state and
@@ -1141,7 +1280,8 @@ struct ChBatch {
 // (2 waves/SIMD: no spills; batched 33.3-33.9k -> 34.7-35.0k pairs/s, profiles/r03_y_sp_spec_ab.txt)
 __global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) k_ch_step_b(ChBatch b, int i, int last) {
   const uint32_t p = blockIdx.x / b.per;
-  if ((int)p < b.n) ch_any<CH_WAVES, CH_VT>(*b.A[p], b.q[p], i, blockIdx.x % b.per, b.per, last ? b.out[p] : nullptr);
+  if ((int)p < b.n)
+    ch_any<CH_WAVES, CH_VT, false>(*b.A[p], b.q[p], i, blockIdx.x % b.per, b.per, last ? b.out[p] : nullptr);
 }
 
 // ---------------------------------------------------------------------------- host side
@@ -1408,13 +1548,16 @@ bool chain_more(ChainCtx* c, hipError_t* he) {
   const ChOut& h = *c->h_out;
   const ChSnap F = h.F;
   if (h.tag != c->q.tag || F.phase != PH_DONE) {
-    // the batch ended inside the search (its last launch stored nothing): the rest, at once; the
-    // last of them is past every search step, so it stores
+    // the batch ended inside the search (its last launch stored nothing): NBG_SP_KMORE (2) more
+    // launches, or the rest if fewer — most such searches ended in the batch's last launch or
+    // need one more step, and the launches past a search's end cost ~3 us each; a search still
+    // not over continues again.  The batch's last launch stores if the search was over before it.
     if (c->steps >= chain_max(c)) {   // (cannot happen: a search has at most 2 UPTO - 1 steps)
       *he = hipErrorUnknown;
       return true;
     }
-    *he = chain_batch(c, chain_max(c) - c->steps, 0);
+    static const int kmore = getenv("NBG_SP_KMORE") ? std::max(1, atoi(getenv("NBG_SP_KMORE"))) : 2;
+    *he = chain_batch(c, std::min(chain_max(c) - c->steps, kmore), 0);
     return false;
   }
   const uint32_t hpos = (uint32_t)(h.hpos >> 32);
