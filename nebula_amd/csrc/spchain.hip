@@ -990,7 +990,11 @@ __device__ __forceinline__ void post_end(ChState* st, const ChQ& q, int h) {
 // hub), which walks on until the path is complete.  A hub met on the way is spread over the
 // other workgroups as a job (COOP), or (no COOP, or a job unanswered) left to the next launch.
 // The walker writes hstart[h + 1].  Returns true in that one writing workgroup (every thread):
-// it is the launch's last to touch the query's state, so it may also store the result.
+// it is the launch's last to touch the query's state, so it may also store the result.  COOP
+// (one query per launch): true only where the result is final — the walk ended in this launch,
+// or there was nothing to walk and this is the first greedy launch — and every launch is given
+// the result block, so the host wakes as soon as the walk ends; the chain's later launches find
+// the walk over and return without storing.
 // (bid, nblk: this workgroup among the query's nblk <= CH_HOP_WGS workgroups of the launch)
 template <bool COOP>
 __device__ __forceinline__ bool ch_hop(const ChArgs& A, const ChQ& q, int nl, int h, uint32_t bid, uint32_t nblk) {
@@ -1008,7 +1012,7 @@ __device__ __forceinline__ bool ch_hop(const ChArgs& A, const ChQ& q, int nl, in
   };
   if (!F.met || F.phase != PH_DONE || F.err || pos >= F.L || c == NO_ROW) {
     if (bid == 0 && threadIdx.x == 0) finish(pos, c);
-    return bid == 0;
+    return bid == 0 && (!COOP || h == 0);   // (COOP: the walk's own launch stored, unless none ran)
   }
   const uint32_t L = F.L, kf = F.kf;
   const Cand none{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
@@ -1197,7 +1201,7 @@ __device__ __forceinline__ bool ch_hop(const ChArgs& A, const ChQ& q, int nl, in
     finish(pos, c);
     if (COOP) post_end(st, q, h);
   }
-  return true;
+  return !COOP || pos >= L;   // (COOP: a walk left at a hub is stored by the launch that ends it)
 }
 
 // The first greedy launch of the query: the first step launch that finds the search over (busy =
@@ -1241,7 +1245,8 @@ __device__ __forceinline__ void ch_out(const ChArgs& A, const ChQ& q, int steps,
 // per big level, were slower: RMAT-26 p50 0.137 -> 0.197 ms, profiles/r03_n_sp_block_ab.txt)
 // Step launch i: a search step, or — the search over — greedy launch i - hop_first (its first
 // CH_HOP_WGS workgroups), so the walk runs in the launches that used to return at once.  (out:
-// the batch's last launch stores the result, when the search was over before it.)
+// where ch_hop says the result is final — COOP: the launch that ends the walk; else the batch's
+// last launch, when the search was over before it.)
 template <int NW, int VT, bool COOP>
 __device__ __forceinline__ void ch_any(const ChArgs& A, const ChQ& q, int i, uint32_t bid, uint32_t nblk, ChOut* out) {
   if (ch_step<NW, VT>(A, q, i, bid, nblk) || i == 0 || bid >= (uint32_t)CH_HOP_WGS) return;
@@ -1259,8 +1264,8 @@ __global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(2
   ch_any<CH_WAVES, VT, true>(*Ap, q, i, blockIdx.x, gridDim.x, out);
 }
 
-// Greedy launches of a continuation (a hub's hop ended the walk's launch): launch j after the nl
-// step launches is greedy launch nl - hop_first + j; the batch's last stores the result.
+// Greedy launches of a continuation: launch j after the nl step launches is greedy launch
+// nl - hop_first + j; the one that ends the walk stores the result.
 __global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ Ap, ChQ q, int nl, int j, ChOut* out) {
   const int h = nl - hop_first(Ap->st->c[q.par]) + j;
   if (ch_hop<true>(*Ap, q, nl, h, blockIdx.x, gridDim.x) && out) ch_out(*Ap, q, nl, h + 1, out);
@@ -1403,9 +1408,9 @@ void chain_destroy(ChainCtx* c) {
   delete c;
 }
 
-// Enqueue step launches [steps, steps + k) then h greedy launches; the batch's last launch stores
-// the result (a step launch only when the search was over before it: else the stored tag stays
-// the previous batch's and chain_more continues).
+// Enqueue step launches [steps, steps + k) then h greedy launches.  The launch in which the walk
+// ends stores the result (ch_hop<true>); a batch that ends before that stores nothing, so the
+// stored tag stays the previous batch's and chain_more continues.
 static hipError_t chain_batch(ChainCtx* c, int k, int h) {
   const ChArgs* A = c->d_args;
   c->q.tag = ++c->tag_seq;
@@ -1414,16 +1419,13 @@ static hipError_t chain_batch(ChainCtx* c, int k, int h) {
     c->timed(CHK_STEP, [&] {
       // (a batched query's continuation keeps its chain's tile size: its lists' splits are per tile)
       if (c->last_batched)
-        hipLaunchKernelGGL(k_ch_step<CH_VT>, dim3(c->grid), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps,
-                           h <= 0 && j + 1 == k ? c->d_out : (ChOut*)nullptr);
+        hipLaunchKernelGGL(k_ch_step<CH_VT>, dim3(c->grid), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps, c->d_out);
       else
-        hipLaunchKernelGGL(k_ch_step<CH_VT1>, dim3(c->grid), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps,
-                           h <= 0 && j + 1 == k ? c->d_out : (ChOut*)nullptr);
+        hipLaunchKernelGGL(k_ch_step<CH_VT1>, dim3(c->grid), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps, c->d_out);
     });
   for (int j = 0; j < h; ++j, ++c->hops)
     c->timed(CHK_HOP, [&] {
-      hipLaunchKernelGGL(k_ch_hop, dim3(CH_HOP_WGS), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps, c->hops,
-                         j + 1 == h ? c->d_out : (ChOut*)nullptr);
+      hipLaunchKernelGGL(k_ch_hop, dim3(CH_HOP_WGS), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps, c->hops, c->d_out);
     });
   ++c->batches;
   return hipGetLastError();
@@ -1475,14 +1477,16 @@ static hipError_t chain_prepare(ChainCtx* c, const SpTypes& fwd, const SpTypes& 
 // in which the greedy walk (or, with no path, the result) runs.
 static int chain_max(const ChainCtx* c) { return 2 * (int)c->q.upto; }
 
-// chain length for c's query: sized by the recent queries, one launch under their rounded-up
-// mean (an empty launch costs a few us, a continuation a host round trip: RMAT-26 10 k pairs, p50
-// 0.1032-0.1036 ms against 0.1059-0.1062 at the mean, p90 / mean within 1.5 %,
-// profiles/r04_n_sp_chain_length_ab.txt); NBG_SP_KPAD adds launches.  A longer query continues
-// (chain_more).
+// chain length for c's query: sized by the recent queries, at their rounded-up mean.  The launch
+// that ends the walk stores the result (ch_hop<true>), so the launches past it cost the next
+// query a few us at most, while a chain one launch short costs a host round trip: RMAT-26 10 k
+// pairs, p50 0.0761 / 0.0753 ms one launch under the mean and 0.0766 / 0.0763 at it, p90 0.142 /
+// 0.140 against 0.1325 / 0.1317, six in flight 23.7-25.4 k against 28.7 k pairs/s
+// (profiles/r05_zb_sp_store_early_ab.txt).  NBG_SP_KPAD adds launches (negative: fewer).  A longer
+// query continues (chain_more).
 static int chain_length(const ChainCtx* c) {
   static const int kpad = getenv("NBG_SP_KPAD") ? atoi(getenv("NBG_SP_KPAD")) : 0;
-  return std::min(chain_max(c), std::max(2, (int)std::ceil(c->ema_launches) - 1 + kpad));
+  return std::min(chain_max(c), std::max(2, (int)std::ceil(c->ema_launches) + kpad));
 }
 
 hipError_t chain_launch(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible,
