@@ -944,16 +944,24 @@ __device__ __forceinline__ Cand hop_scan(const ChArgs& A, const uint32_t* vlab, 
                                          uint32_t re, uint64_t g, uint64_t G) {
   Cand best{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
   for (uint64_t j0 = rs + g; j0 < re; j0 += CH_HOP_U * G) {
+    // (an edge's dst vid and rank are loaded with its neighbour id, not after the label test: one
+    // dependent round trip less per hop, for 8-16 bytes more per scanned edge)
     uint32_t wv[CH_HOP_U], lv[CH_HOP_U];
+    int64_t dv[CH_HOP_U], rk[CH_HOP_U];
 #pragma unroll
-    for (int u = 0; u < CH_HOP_U; ++u) wv[u] = j0 + u * G < re ? gld(A.col[0], j0 + u * G, A.ne[0], 11, A.st) : NO_ROW;
+    for (int u = 0; u < CH_HOP_U; ++u) {
+      const uint64_t j = j0 + u * G;
+      const bool in = j < re;
+      wv[u] = in ? gld(A.col[0], j, A.ne[0], 11, A.st) : NO_ROW;
+      dv[u] = in ? gld(A.dst_vid, j, A.ne[0], 13, A.st) : 0;
+      rk[u] = in && A.rank ? gld(A.rank, j, A.ne[0], 13, A.st) : 0;
+    }
 #pragma unroll
     for (int u = 0; u < CH_HOP_U; ++u) lv[u] = wv[u] != NO_ROW ? gld(vlab, wv[u], A.nv, 12, A.st) : 0u;
 #pragma unroll
     for (int u = 0; u < CH_HOP_U; ++u) {
       if (wv[u] == NO_ROW || lv[u] != want) continue;
-      const uint64_t j = j0 + u * G;
-      const Cand x{A.type, A.rank ? gld(A.rank, j, A.ne[0], 13, A.st) : 0, gld(A.dst_vid, j, A.ne[0], 13, A.st), wv[u]};
+      const Cand x{A.type, rk[u], dv[u], wv[u]};
       if (cand_less(x, best)) best = x;
     }
   }
@@ -1016,11 +1024,15 @@ __device__ __forceinline__ bool ch_hop(const ChArgs& A, const ChQ& q, int nl, in
   }
   const uint32_t L = F.L, kf = F.kf;
   const Cand none{INT64_MAX, INT64_MAX, INT64_MAX, NO_ROW};
-  auto range = [&](uint32_t v, uint32_t* rs, uint32_t* re) {
+  auto range = [&](uint32_t v, uint32_t* rs, uint32_t* re) {   // (the three loads issued together)
     *rs = *re = 0;
-    if (v != NO_ROW && (!A.visible || gld(A.visible, v, A.nv, 14, st))) {
-      *rs = gld(A.row_ptr[0], v, A.nv + 1, 14, st);
-      *re = gld(A.row_ptr[0], (uint64_t)v + 1, A.nv + 1, 14, st);
+    if (v != NO_ROW) {
+      const uint32_t a = gld(A.row_ptr[0], v, A.nv + 1, 14, st);
+      const uint32_t b = gld(A.row_ptr[0], (uint64_t)v + 1, A.nv + 1, 14, st);
+      if (!A.visible || gld(A.visible, v, A.nv, 14, st)) {
+        *rs = a;
+        *re = b;
+      }
     }
   };
   auto want_of = [&](uint32_t p, const uint32_t** vlab) {
