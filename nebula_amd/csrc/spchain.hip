@@ -163,6 +163,8 @@ struct ChQ {
   uint32_t tag;                        // this batch of launches (ChOut::tag: which batch stored)
   uint32_t both_items;                 // a BFS level expands both sides when each has at most this many
                                        // items (entries + edges) and UPTO allows two levels (0: never)
+  uint32_t job_wait;                   // ch_hop<true>: the walker's wait for its helpers' answers to a
+                                       // hub job (steady-counter ticks; then the next launch spreads it)
 };
 
 // Both sides in one launch: while both frontiers are small a level's launch costs the same for one
@@ -977,7 +979,7 @@ __device__ __forceinline__ Cand hop_scan(const ChArgs& A, const uint32_t* vlab, 
 // launch of at most CH_HOP_WGS walking workgroups per query, far below the chip's residency); a
 // batch's pairs do not all have their workgroups resident together.
 constexpr long long CH_HELP_IDLE = 20000;   // steady-counter ticks (100 MHz: 200 us)
-constexpr long long CH_JOB_WAIT = 10000;    // (100 us)
+constexpr uint32_t CH_JOB_WAIT = 10000;     // (100 us; ChQ::job_wait, NBG_SP_JOB_WAIT)
 constexpr unsigned CH_JOB_END = 255;        // the job number of "the walk is over"
 
 __device__ __forceinline__ unsigned long long job_word(const ChQ& q, int h, unsigned k, uint32_t pos) {
@@ -1163,7 +1165,7 @@ __device__ __forceinline__ bool ch_hop(const ChArgs& A, const ChQ& q, int nl, in
         for (;;) {
           const bool ok = l >= nblk || l == bid || ld_agent(&st->htag[l]) == a;
           all = __all(ok);
-          if (all || wall_clock64() - t0 > CH_JOB_WAIT) break;
+          if (all || wall_clock64() - t0 > (long long)q.job_wait) break;
           __builtin_amdgcn_s_sleep(1);
         }
         Cand x = none;
@@ -1475,7 +1477,11 @@ static hipError_t chain_prepare(ChainCtx* c, const SpTypes& fwd, const SpTypes& 
     c->args_valid = true;
   }
   c->par ^= 1u;
-  c->q = ChQ{s, t, upto, epoch, epoch, epoch, c->solo, c->par, 0, c->both};
+  // (NBG_SP_JOB_WAIT, read per query: a test sets 0 so that every hub job goes unanswered and the
+  // fallback — the next launch's spread scan — runs)
+  const char* jw = getenv("NBG_SP_JOB_WAIT");
+  c->q = ChQ{s, t, upto, epoch, epoch, epoch, c->solo, c->par, 0, c->both,
+             jw ? (uint32_t)strtoul(jw, nullptr, 10) : CH_JOB_WAIT};
   c->steps = c->hops = 0;
   c->last_batched = false;
   ++c->queries;

@@ -94,13 +94,19 @@ def test_rmat_shortest_two_sided_levels(both, monkeypatch):
         orc.close()
 
 
+@pytest.mark.parametrize("job_wait", [None, "0"], ids=["jobs", "unanswered"])
 @pytest.mark.parametrize("hits", ["spread", "head", "tail", "budget"])
-def test_shortest_through_a_hub(hits, sp_mode):
+def test_shortest_through_a_hub(hits, sp_mode, job_wait, monkeypatch):
     """Greedy hops through a hub (more than 4096 out-edges, scanned by 64 workgroups and reduced by
     the last): s -> hub -> x -> t for 10,000 x of both signs, the x that reach t chosen among the
     smallest vids, the largest, in the middle, or at random.  The canonical minimum is over the
     signed (type, rank, vid) while a row is in key order (byte-reversed vids): round 5's
-    early-exit scan of hub rows in row order assumed otherwise, and this test caught it."""
+    early-exit scan of hub rows in row order assumed otherwise, and this test caught it.
+    A hub met by the walking workgroup is a job for the launch's other workgroups; with
+    NBG_SP_JOB_WAIT=0 the walker never waits for their answers, so every such hub falls back to
+    the next launch's spread scan (and, past the chain, a continuation)."""
+    if job_wait is not None:
+        monkeypatch.setenv("NBG_SP_JOB_WAIT", job_wait)
     rng = np.random.default_rng({"spread": 1, "head": 2, "tail": 3, "budget": 4}[hits])
     s_v, hub, t_v = 5, 6, 7
     xs = np.unique(rng.integers(-(1 << 62), 1 << 62, 10000, dtype=np.int64))
