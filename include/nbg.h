@@ -45,6 +45,21 @@ extern "C" {
 #define NBG_E_OUT_OF_MEMORY       (-1004)
 #define NBG_E_STATE               (-1005) /* e.g. query before nbg_finalize */
 
+/* ---- Device limits ----------------------------------------------------------------------
+ * A statement past one of these returns NBG_E_UNSUPPORTED before any row is produced (on every
+ * rank of a partitioned engine), so the caller can run the reference's own executor on it
+ * (tests/test_gpu_limits.py holds one test per limit):
+ *   more than NBG_MAX_YIELDS YIELD columns; more than NBG_MAX_OVER OVER types (OVER * included;
+ *   GO, FIND PATH, GetNeighbors); a WHERE + YIELD program over 256 instructions or 16 live
+ *   registers per OVER type; GO over 32 STEPS; FIND SHORTEST PATH UPTO over 63, FIND ALL PATH
+ *   UPTO over 32; $$ of a tag registered 17th or later; more than 32 $- / $var input columns.
+ * (A storage filter with a function call is E_INVALID_FILTER per part, as checkExp answers it,
+ * QueryBaseProcessor.inl:172-290.)
+ * Not limits: $- / $var input strings absent from the snapshot's dictionary, string functions
+ * nested to any depth in GO (both lifted in round 6). */
+#define NBG_MAX_YIELDS 32
+#define NBG_MAX_OVER   32
+
 /* ---- common.thrift SupportedType ------------------------------------------------------ */
 #define NBG_T_BOOL      1
 #define NBG_T_INT       2
@@ -324,6 +339,9 @@ int64_t nbg_path_len(const nbg_paths* p, int64_t i);
 const int64_t* nbg_path_entries(const nbg_paths* p, int64_t i);
 /* Adjacency entries the search scanned (both directions; TEPS numerator). */
 uint64_t nbg_paths_edges_scanned(const nbg_paths* p);
+/* Diagnostic: launch batches the device level loop needed for this result (1: the first chain
+ * finished it; more: the host continued it; 0: the host-driven loop answered). */
+uint32_t nbg_paths_chain_batches(const nbg_paths* p);
 void nbg_paths_free(nbg_paths* p);
 
 /* ---- GetNeighbors (storage boundary: StorageServiceHandler::future_getBound) -------------

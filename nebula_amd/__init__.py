@@ -2,7 +2,8 @@
 
 The product is the C ABI in ``include/nbg.h`` implemented by ``nebula_amd/libnbg.so``
 (host C++ + gfx950 HIP kernels).  This package is the Python host binding plus fixture
-tooling (KV record builders, an nGQL front end for GO / FIND PATH).
+tooling (KV record builders, the RMAT generator); the nGQL front end the parity tests drive it with
+is test harness (tests/support/ngql.py).
 """
 from .engine import DeviceRows, Engine, LocalCluster, NbgError, comm_unique_id, nba_engine  # noqa: F401
 

@@ -122,6 +122,7 @@ SIGNATURES = [
     ("nbg_path_len", i64, [vp, i64]),
     ("nbg_path_entries", P(i64), [vp, i64]),
     ("nbg_paths_edges_scanned", u64, [vp]),
+    ("nbg_paths_chain_batches", u32, [vp]),
     ("nbg_paths_free", None, [vp]),
     ("nbg_get_neighbors", i32, [vp, P(nbg_gn_request), P(vp)]),
     ("nbg_gn_num_failed", i32, [vp]),

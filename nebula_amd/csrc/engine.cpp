@@ -20,6 +20,9 @@
 
 #include "engine.h"
 
+static_assert(NBG_MAX_YIELDS == nbg::MAX_YIELDS && NBG_MAX_OVER == nbg::MAX_TYPES_Q,
+              "include/nbg.h device limits match the engine's");
+
 // a fresh seed for each query's rand32 / rand64 stream
 static uint64_t query_rand_seed() {
   static std::atomic<uint64_t> ctr{(uint64_t)std::chrono::steady_clock::now().time_since_epoch().count() * 0x9e3779b97f4a7c15ull};
@@ -491,8 +494,15 @@ struct nbg_go_stmt {
   int64_t* d_in_ids = nullptr;
   int64_t** d_in_cols = nullptr;
   std::vector<int64_t*> d_in_col_ptrs;
+  // input strings absent from the snapshot's dictionary (codes STR_INPUT | index), their bytes
+  // uploaded with the index
+  std::vector<std::string> in_xstr;
+  uint32_t* d_xoff = nullptr;
+  char* d_xbytes = nullptr;
   ~nbg_go_stmt() {
     if (d_in_ids) (void)hipFree(d_in_ids);
+    if (d_xoff) (void)hipFree(d_xoff);
+    if (d_xbytes) (void)hipFree(d_xbytes);
     for (auto* p : d_in_col_ptrs)
       if (p) (void)hipFree(p);
     if (d_in_cols) (void)hipFree(d_in_cols);
@@ -600,8 +610,11 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
   std::vector<VKind> in_kinds;
   std::vector<int64_t> in_ids;
   std::vector<std::vector<int64_t>> in_cols;
+  std::vector<std::string> in_xstr;   // input strings absent from the dictionary (sorted, unique)
   if (uses_input && rq->num_input_cols > 0) {
-    if (rq->num_input_cols > MAX_INPUT_COLS || !rq->input_names || !rq->input_kinds || !rq->input_cols ||
+    if (rq->num_input_cols > MAX_INPUT_COLS)
+      return E.fail(NBG_E_UNSUPPORTED, "more than " + std::to_string(MAX_INPUT_COLS) + " input columns");
+    if (!rq->input_names || !rq->input_kinds || !rq->input_cols ||
         rq->input_vid_col < 0 || rq->input_vid_col >= rq->num_input_cols)
       return E.fail(NBG_E_INVALID_ARGUMENT, "input table");
     const uint64_t n = rq->num_input_rows;
@@ -619,13 +632,25 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
     }
     in_cols.assign(rq->num_input_cols, std::vector<int64_t>(rowof.size()));
     for (auto& pr : rowof) in_ids.push_back(pr.first);
+    // strings the dictionary lacks (a string derived by an earlier statement of the pipe): a table of
+    // their own, so they keep their bytes (a dictionary code between neighbours would not)
+    for (int32_t c = 0; c < rq->num_input_cols; ++c)
+      if (in_kinds[c] == VK_STRING)
+        for (auto& pr : rowof) {
+          const char* str = static_cast<const char* const*>(rq->input_cols[c])[pr.second];
+          if (string_code(E.snap.strings, str ? str : "") & 1) in_xstr.emplace_back(str ? str : "");
+        }
+    std::sort(in_xstr.begin(), in_xstr.end());
+    in_xstr.erase(std::unique(in_xstr.begin(), in_xstr.end()), in_xstr.end());
     for (int32_t c = 0; c < rq->num_input_cols; ++c) {
       for (size_t k = 0; k < rowof.size(); ++k) {
         const uint64_t r = rowof[k].second;
         if (in_kinds[c] == VK_STRING) {
           const char* str = static_cast<const char* const*>(rq->input_cols[c])[r];
-          const int64_t code = string_code(E.snap.strings, str ? str : "");
-          if (code & 1) return E.fail(NBG_E_UNSUPPORTED, "an input string absent from the snapshot's dictionary");
+          int64_t code = string_code(E.snap.strings, str ? str : "");
+          if (code & 1)
+            code = STR_INPUT |
+                   (int64_t)(std::lower_bound(in_xstr.begin(), in_xstr.end(), std::string(str ? str : "")) - in_xstr.begin());
           in_cols[c][k] = code;
         } else {
           in_cols[c][k] = static_cast<const int64_t*>(rq->input_cols[c])[r];
@@ -673,6 +698,8 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
     if (uses_input) {
       env.input_names = &in_names;
       env.input_kinds = &in_kinds;
+      env.input_derived = !in_xstr.empty();
+      for (const std::string& x : in_xstr) env.max_dict_len = std::max<uint64_t>(env.max_dict_len, x.size());
     }
     ProgramBuilder pb;
     TypeProgram tp;
@@ -730,11 +757,14 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
     }
     tp.code = pb.code;
     tp.data = pb.data;
-    for (const Ins& i : tp.code) tp.sout = tp.sout || i.op == OP_SOUT;
+    for (const Ins& i : tp.code) tp.sout = tp.sout || i.op == OP_SOUT || i.op == OP_SMAT;   // (the arena)
     tp.sout_bytes = pb.sout_bytes;
     tp.probe_mask = probe;
     tp.nregs = std::max(1, pb.max_reg);
     if ((int)(tp.code.size() + tp.data.size()) > MAX_PROGRAM) return E.fail(NBG_E_UNSUPPORTED, "program too long");
+    if (tp.nregs > interp_max_regs())
+      return E.fail(NBG_E_UNSUPPORTED, "expression too deep for the device register file (" + std::to_string(tp.nregs) +
+                                           " registers, " + std::to_string(interp_max_regs()) + " fit the LDS)");
     progs[t] = std::move(tp);
   }
   if ((int)over.size() > MAX_TYPES_Q || rq->steps > (uint32_t)MAX_STEPS)
@@ -842,6 +872,7 @@ static int32_t go_prepare(Engine& E, const nbg_go_request* rq, nbg_go_stmt** out
   st->uses_input = uses_input;
   st->in_ids = std::move(in_ids);
   st->in_cols = std::move(in_cols);
+  st->in_xstr = std::move(in_xstr);
   *out = st;
   return NBG_OK;
 }
@@ -983,14 +1014,30 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
       ok = ok && hipMalloc((void**)&ms->d_in_cols, std::max<size_t>(ms->in_cols.size(), 1) * 8) == hipSuccess &&
            hipMemcpy(ms->d_in_cols, ms->d_in_col_ptrs.data(), ms->in_cols.size() * 8, hipMemcpyHostToDevice) ==
                hipSuccess;
+      if (ok && !ms->in_xstr.empty()) {   // the input-string table (DevStrings::x*)
+        std::vector<uint32_t> off{0};
+        std::string bytes;
+        for (const std::string& x : ms->in_xstr) {
+          bytes += x;
+          off.push_back((uint32_t)bytes.size());
+        }
+        ok = bytes.size() < 0xFFFFFFFFull && hipMalloc((void**)&ms->d_xoff, off.size() * 4) == hipSuccess &&
+             hipMemcpy(ms->d_xoff, off.data(), off.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
+             hipMalloc((void**)&ms->d_xbytes, std::max<size_t>(bytes.size(), 1)) == hipSuccess &&
+             hipMemcpy(ms->d_xbytes, bytes.data(), bytes.size(), hipMemcpyHostToDevice) == hipSuccess;
+      }
       if (!ok) {
         // a later execution retries the upload from scratch
         if (ms->d_in_ids) (void)hipFree(ms->d_in_ids);
         for (auto*& q : ms->d_in_col_ptrs)
           if (q) (void)hipFree(q);
         if (ms->d_in_cols) (void)hipFree(ms->d_in_cols);
+        if (ms->d_xoff) (void)hipFree(ms->d_xoff);
+        if (ms->d_xbytes) (void)hipFree(ms->d_xbytes);
         ms->d_in_ids = nullptr;
         ms->d_in_cols = nullptr;
+        ms->d_xoff = nullptr;
+        ms->d_xbytes = nullptr;
         ms->d_in_col_ptrs.clear();
         local_fail(NBG_E_OUT_OF_MEMORY, "input index upload");
       }
@@ -1028,6 +1075,9 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
       a.in_ids = st->d_in_ids;
       a.in_n = st->in_ids.size();
       a.in_cols = st->d_in_cols;
+      a.str.xoff = st->d_xoff;
+      a.str.xbytes = st->d_xbytes;
+      a.str.xn = st->in_xstr.size();
     }
     return a;
   };
@@ -1060,7 +1110,12 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
     // arena never overflows.
     static const uint64_t cap_kb =
         getenv("NBG_STR_ARENA_KB") ? strtoull(getenv("NBG_STR_ARENA_KB"), nullptr, 10) : (2ull << 20);
-    const uint64_t per_row = std::max<uint64_t>(st->sout_row_bytes, 32);
+    // (a pad length read per edge leaves the bound unknown — ProgramBuilder::value_reg's 2^40 — so
+    // such a statement reserves 256 bytes per row instead of the whole cap on every workspace, and a
+    // query whose strings outgrow that fails with E_OUT_OF_MEMORY through the arena's overflow
+    // flag, never truncates)
+    const uint64_t per_row =
+        st->sout_row_bytes >= (1ull << 40) ? 256 : std::max<uint64_t>(st->sout_row_bytes, 32);
     const uint64_t need = cap_rows > UINT64_MAX / per_row ? UINT64_MAX : cap_rows * per_row;
     const uint64_t want = std::min<uint64_t>(std::max<uint64_t>(need, 1ull << 20), std::max<uint64_t>(cap_kb, 1) << 10);
     if (ws_reserve_arena(ws, want) != hipSuccess) local_fail(NBG_E_OUT_OF_MEMORY, "derived-string arena");
@@ -1132,7 +1187,7 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
   static const bool tiny_on = !getenv("NBG_TINY") || atoi(getenv("NBG_TINY")) != 0;
   bool tiny = tiny_on && he == hipSuccess && !part && !device && !st->distinct && !st->uses_input && !st->derived &&
               over.size() == 1 && ncols > 0 && !deferred && !(plist[0].where_const && !plist[0].where_const_val) &&
-              f0.size() <= (size_t)INLINE_STARTS && steps <= 3;
+              f0.size() <= (size_t)INLINE_STARTS && steps <= 3 && plist[0].nregs <= tiny_max_regs();
   const DevEdgeType* tdt = nullptr;
   if (tiny) {
     auto it = E.snap.types.find(over[0]);
@@ -1278,7 +1333,8 @@ static int32_t derived_strings(Engine& E, const nbg_go_stmt* st, Workspace* ws, 
       memcpy(&code, buf.data() + o, 8);
       memcpy(&len, buf.data() + o + 8, 8);
       if (o + 16 + len > pr.first + pr.second) return E.fail(NBG_E_DEVICE, "derived-string arena entry");
-      if (!add(code, std::string(buf.data() + o + 16, len)))
+      // (an OP_SMAT entry, code 0, is a nested function's inner string: no result cell holds it)
+      if (is_derived_code(code) && !add(code, std::string(buf.data() + o + 16, len)))
         return E.fail(NBG_E_EXECUTION_ERROR, "derived-string hash collision");
       o += 16 + ((len + 7) & ~7ull);
     }
@@ -2028,6 +2084,7 @@ const int64_t* nbg_path_entries(const nbg_paths* p, int64_t i) {
   return (p && i >= 0 && i < (int64_t)p->paths.size()) ? p->paths[i].data() : nullptr;
 }
 uint64_t nbg_paths_edges_scanned(const nbg_paths* p) { return p ? p->edges : 0; }
+uint32_t nbg_paths_chain_batches(const nbg_paths* p) { return p ? p->batches : 0; }
 void nbg_paths_free(nbg_paths* p) { delete p; }
 
 }  // extern "C"

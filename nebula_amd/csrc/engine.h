@@ -160,4 +160,5 @@ struct nbg_engine {
 struct nbg_paths {
   std::vector<std::vector<int64_t>> paths;
   uint64_t edges = 0;   // BFS adjacency entries scanned, both directions
+  uint32_t batches = 0; // device chain: launch batches the host enqueued (1: none continued; 0: host loop)
 };

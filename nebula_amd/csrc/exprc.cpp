@@ -503,7 +503,7 @@ struct Ctx {
     uint64_t most = 0;
     for (const Piece& p : ps) {
       const uint64_t b = p.kind == PC_CONST ? p.text.size() : p.kind == PC_INT ? 20 : p.kind == PC_BOOL ? 5
-                       : p.kind == PC_VIEW ? p.bound : env.max_dict_len;
+                       : (p.kind == PC_VIEW || p.mat) ? p.bound : env.max_dict_len;
       most = b > UINT64_MAX - most ? UINT64_MAX : most + b;
     }
     return most;
@@ -766,6 +766,7 @@ struct Ctx {
         c.kind = (*env.input_kinds)[col];
         c.reg = push();
         emit(OP_INPUT, c.reg, 0, 0, col);
+        if (c.kind == VK_STRING && env.input_derived) c = derived_of({Piece{PC_DICT, c.reg, {}}});
         *out = c;
         return NBG_OK;
       }
@@ -1039,9 +1040,33 @@ struct Ctx {
         nested = false;
         for (const Piece& p : v.inner) nested = nested || p.kind == PC_VIEW;
       }
-      if (nested) {
-        *err = "function `" + f + "' over another string function's per-edge result is not supported on the device";
+      if (nested && env.storage) {   // (a storage filter runs without a string arena)
+        *err = "function `" + f + "' over another string function's per-edge result is not supported in a storage filter";
         return NBG_E_UNSUPPORTED;
+      }
+      if (nested) {
+        // a window / trim / pad over another one's per-edge result, or a pad drawn from one: each
+        // inner view is materialised into the arena (OP_SMAT) and read back as one flat piece, so
+        // views compose to any depth.  Its registers stay live (a fresh one holds the entry)
+        for (auto* l : {&v.inner, &v.pad})
+          for (Piece& p : *l) {
+            if (p.kind != PC_VIEW) continue;
+            std::vector<Piece> one;
+            one.push_back(std::move(p));
+            const uint64_t most = std::min<uint64_t>(bound_of(one), 1ull << 40);
+            const uint64_t add = 16 + ((most + 7) & ~7ull);
+            pb.sout_bytes = add > UINT64_MAX - pb.sout_bytes ? UINT64_MAX : pb.sout_bytes + add;
+            const int32_t h = emit_pieces(one);
+            const int r = push();
+            emit(OP_SMAT, r, 0, 0, h);
+            Piece d;
+            d.kind = PC_DICT;
+            d.reg = r;
+            d.mat = true;
+            d.bound = most;
+            p = std::move(d);
+          }
+        nested = false;
       }
       if (nint >= 1) v.reg = materialize(args[1]);
       if (nint >= 2) v.reg_b = materialize(args[2]);

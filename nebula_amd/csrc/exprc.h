@@ -50,6 +50,9 @@ struct CompileEnv {
   // $-.col / $var.col: the input rows' columns (names, kinds); nullptr: the query has no input
   const std::vector<std::string>* input_names = nullptr;
   const std::vector<VKind>* input_kinds = nullptr;
+  // the input holds strings absent from the dictionary (STR_INPUT codes): its string columns are
+  // read as derived strings, so compares, casts and YIELDs work on their bytes
+  bool input_derived = false;
   uint64_t max_dict_len = 0;   // the longest dictionary string (bounds a derived string's bytes)
 };
 
@@ -70,6 +73,7 @@ struct Piece {
   int reg_b = -1;
   std::vector<Piece> inner, pad;
   uint64_t bound = 0;          // the longest text it can spell (UINT64_MAX: unbounded)
+  bool mat = false;            // PC_DICT over a string OP_SMAT materialised (its bound is `bound`)
 };
 
 // Result of compiling one expression for one edge type.

@@ -418,6 +418,7 @@ static int32_t get_neighbors(Engine& E, const nbg_gn_request* rq, nbg_gn_respons
       tp.code = pb.code;
       tp.nregs = std::max(1, pb.max_reg);
       if ((int)tp.code.size() > MAX_PROGRAM) return E.fail(NBG_E_UNSUPPORTED, "program too long");
+      if (tp.nregs > interp_max_regs()) return E.fail(NBG_E_UNSUPPORTED, "too many return columns for the device's LDS");
       ncols = std::max(ncols, (int)tp.yield_reg.size());
       uint64_t eb = 0;
       for (uint32_t d : starts) eb += dt.h_row_ptr[d + 1] - dt.h_row_ptr[d];

@@ -278,7 +278,23 @@ __device__ __forceinline__ PieceView piece_view(const Ins& pc, const char* dbase
   switch (pc.op) {
     case PC_DICT:
       // -1: "" absent from the dictionary (the schema default of a string prop)
-      if (x != -1) {
+      if (((uint64_t)x >> 60) == 1) {   // a string materialised in the arena (OP_SMAT)
+        const uint64_t at = (uint64_t)(x & (STR_ARENA - 1));
+        if (!S.arena || at + 16 > S.arena_cap) {
+          bad = true;
+        } else {
+          v.p = S.arena + at + 16;
+          v.len = (uint32_t)*reinterpret_cast<const uint64_t*>(S.arena + at + 8);
+        }
+      } else if (((uint64_t)x >> 61) == 1) {   // (is_input_code) an input string absent from the dictionary (STR_INPUT | index)
+        const uint64_t i = (uint64_t)(x & (STR_INPUT - 1));
+        if (i >= S.xn) {
+          bad = true;
+        } else {
+          v.p = S.xbytes + S.xoff[i];
+          v.len = S.xoff[i + 1] - S.xoff[i];
+        }
+      } else if (x != -1) {
         if (x < 0 || (x & 1) || (uint64_t)(x >> 1) >= S.n) {
           bad = true;
         } else {
@@ -757,6 +773,27 @@ __device__ int64_t rand_value(uint64_t seed, uint64_t j, uint32_t v, int pc, int
   return (int64_t)(lo + __umul64hi(r, hi - lo));
 }
 
+// OP_SMAT: the piece list's bytes into an arena entry ([u64 0][u64 len][bytes]), STR_ARENA | its
+// offset (read back by the same lane through a PC_DICT piece)
+__device__ int64_t str_mat(const Ins* data, int32_t hdr, const DevStrings& S, const int64_t* regs, int tid, bool& bad,
+                           bool& err) {
+  const uint64_t len = str_len(data, hdr, S, regs, tid, bad);
+  const uint64_t need = 16 + ((len + 7) & ~7ull);
+  const uint64_t at = atomicAdd(S.arena_used, (unsigned long long)need);
+  if (!S.arena || at + need > S.arena_cap) {   // the host fails the query with E_OUT_OF_MEMORY
+    if (S.err_flag) atomicOr(S.err_flag, ARENA_OVERFLOW);
+    err = true;
+    return STR_ARENA | (STR_ARENA - 1);   // (no entry: a reader sees an offset past the arena)
+  }
+  char* e = S.arena + at;
+  StrIter it;
+  str_open(it, data, hdr, S, regs, tid, bad);
+  for (uint64_t i = 0; i < len; ++i) e[16 + i] = (char)str_next(it, S, regs, tid, bad);
+  *reinterpret_cast<uint64_t*>(e) = 0;
+  *reinterpret_cast<uint64_t*>(e + 8) = len;
+  return STR_ARENA | (int64_t)at;
+}
+
 // OP_SOUT: the derived string into the arena; its canonical code (dictionary code when the
 // dictionary holds it, else STR_DERIVED | content hash, str_derived_code)
 __device__ int64_t str_store(const Ins* data, int32_t hdr, const DevStrings& S, const int64_t* regs, int tid,
@@ -954,6 +991,13 @@ __device__ __forceinline__ void run_program(const Ins* __restrict__ prog, const 
         if (active) {
           bool bad = false;
           r = str_store(data, ins.aux, a.str, regs, tid, bad, err);
+          err = err || bad;
+        }
+        break;
+      case OP_SMAT:
+        if (active) {
+          bool bad = false;
+          r = str_mat(data, ins.aux, a.str, regs, tid, bad, err);
           err = err || bad;
         }
         break;
@@ -2283,6 +2327,20 @@ void ws_destroy(Workspace* w) {
 }
 
 uint64_t ws_cap_frontier(Workspace* w) { return w ? w->cap_frontier : 0; }
+
+static int lds_per_block() {
+  static const int v = [] {
+    int dev = 0, x = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&x, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) !=
+                                                hipSuccess)
+      x = 64 * 1024;
+    return x;
+  }();
+  return v;
+}
+// (static LDS: k_expand ~10.7 KB, k_go_tiny ~25.1 KB, rounded up)
+int interp_max_regs() { return std::max(1, std::min(MAX_REGS, (lds_per_block() - 12 * 1024) / (BLOCK * 8))); }
+int tiny_max_regs() { return std::max(0, std::min(MAX_REGS, (lds_per_block() - 26 * 1024) / (BLOCK * 8))); }
 uint64_t ws_cap_items(Workspace* w) { return w->cap_frontier + w->e_max; }
 unsigned ws_final_grid_of(Workspace* w, int tix) { return w->final_grid[tix]; }
 const uint32_t* ws_host_blk_rows(Workspace* w, int tix) { return w->h_blk_rows + (size_t)tix * EXPAND_GRID; }
@@ -2785,7 +2843,11 @@ hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound,
     fa.stat_n = L.stat_n;
     fa.err_flag = &w->q->err;
     const bool one = fp.nyields == 1 && fa.const_mask == 0;
-    HIP_TRY(launch_final_dst(fa, fp.fast.has_where ? fp.fast.wbytes : 0, one, grid.x, w->stream));
+    const hipError_t le = launch_final_dst(fa, fp.fast.has_where ? fp.fast.wbytes : 0, one, grid.x, w->stream);
+    if (le != hipSuccess) {
+      prof_end(w, p, K_EXPAND_FINAL, step, tix, 0.0, 0.0);   // (the profile's open event closed)
+      return le;
+    }
   } else if (dst_only) {
     hipLaunchKernelGGL(k_expand<FINALD>, grid, dim3(BLOCK), 0, w->stream, a, L.acc, l_end, l_rs, w->flags,
                        fp, BfsParams{}, e_st, L.stat_n, NoInline{});

@@ -196,6 +196,8 @@ enum Op : uint8_t {
   OP_SCASE,      // r[d] = strcasecmp(piece list data[aux], piece list data[imm]) (glibc's difference)
   OP_RAND,       // r[d] = rand32 / rand64 (aux bit 2) over aux & 3 INT arguments r[a], r[b]
   OP_NOW,        // r[d] = WallClock::fastNowInSec() of the query (ExpandArgs::now_sec)
+  OP_SMAT,       // r[d] = STR_ARENA | the arena offset of piece list data[aux], stored there: a string
+                 //        function's per-edge result that another window / trim / pad reads (nesting)
   OP_COUNT_
 };
 
@@ -220,6 +222,15 @@ constexpr int64_t STR_DERIVED = (int64_t)1 << 62;
 constexpr uint64_t STR_HASH_MASK = ((uint64_t)1 << 62) - 1;
 // (negative codes are dictionary codes too: -1 is "" when the dictionary lacks it)
 inline bool is_derived_code(int64_t c) { return ((uint64_t)c >> 62) == 1; }
+// A $- / $var input string absent from the snapshot's dictionary: STR_INPUT | its index in the
+// statement's input-string table (DevStrings::x*), the table sorted and unique.  Such a statement
+// reads its input string columns as derived strings (piece lists), so every compare is on bytes and
+// a YIELD stores the value into the arena (STR_DERIVED code).
+constexpr int64_t STR_INPUT = (int64_t)1 << 61;
+// A string materialised inside one edge's evaluation (OP_SMAT): STR_ARENA | its entry's offset in
+// the workspace's arena.  Only a piece of a later view reads it; it never reaches a result column.
+constexpr int64_t STR_ARENA = (int64_t)1 << 60;
+inline bool is_input_code(int64_t c) { return ((uint64_t)c >> 61) == 1; }
 constexpr uint64_t STR_HASH_INIT = 0xcbf29ce484222325ull;   // FNV-1a over the bytes, then mixed
 
 #if defined(__HIPCC__)
@@ -245,6 +256,10 @@ struct DevStrings {
   const int64_t* s2f = nullptr;     // [n] toDouble(string) bits
   const uint8_t* s2ok = nullptr;    // [n] bit 0: toInt ok, bit 1: toDouble ok
   uint64_t n = 0;
+  // the statement's input strings absent from the dictionary (codes STR_INPUT | index)
+  const uint32_t* xoff = nullptr;   // [xn + 1]
+  const char* xbytes = nullptr;
+  uint64_t xn = 0;
   // the query's derived-string arena (OP_SOUT): entries [u64 hash][u32 len][u32 0][bytes, 8-aligned]
   char* arena = nullptr;
   unsigned long long* arena_used = nullptr;   // bytes claimed (may exceed arena_cap: overflow)
@@ -257,9 +272,14 @@ constexpr unsigned long long ARENA_OVERFLOW = 1ull << 32;   // (summed over rank
 // the query fails with NBG_E_DEVICE (summed over ranks, still >= 2^48)
 constexpr unsigned long long SPLIT_BAD = 1ull << 48;
 
-constexpr int MAX_REGS = 16;
+constexpr int MAX_REGS = 48;       // the compiler's ceiling; the device's LDS sets the run-time one
+// The interpreter's registers are [nregs][BLOCK] x 8 B of dynamic LDS beside each kernel's static
+// LDS: the register counts a program may use on this device (k_expand / k_go_tiny), from the
+// device's LDS per workgroup
+int interp_max_regs();
+int tiny_max_regs();
 constexpr int MAX_PROGRAM = 256;   // instructions per query/type (WHERE + all YIELDs)
-constexpr int MAX_YIELDS = 16;
+constexpr int MAX_YIELDS = 32;
 
 // A compiled query for one OVER edge type.
 struct TypeProgram {
@@ -292,7 +312,7 @@ constexpr int VT = NBG_VT;             // k_expand: path items per thread
 constexpr int TILE = 64 * VT;          // path items (frontier entries + edges) per wave tile
 constexpr int NSHARD = 64;             // row-output shards (one counter + region each)
 constexpr int MAX_STEPS = 32;          // GO N STEPS upper bound
-constexpr int MAX_TYPES_Q = 16;        // OVER types per query
+constexpr int MAX_TYPES_Q = 32;        // OVER types per query
 constexpr int INLINE_STARTS = 32;      // start lists up to this size travel in kernel arguments
 constexpr int MAX_TAG_BITS = 16;       // tags addressable by $$ (QState::tagbits: has | used << 16)
 constexpr int MAX_INPUT_COLS = 32;     // columns of a piped / variable input
@@ -432,12 +452,21 @@ struct SpTypes {                     // the CSRs one search direction expands (O
 struct SpResult {                    // one query's result (from the chain's ChOut)
   unsigned long long L;              // path length, 0 = no path within UPTO
   unsigned long long edges;          // BFS adjacency entries scanned (both sides)
-  unsigned long long err;            // 1 reconstruction failure, 3 list overflow
+  unsigned long long err;            // 1 reconstruction failure, 3 list overflow, 4 a bad tile split,
+                                     // CH_ERR_WALK_CAP, 256 << site: CH_GUARD bounds violation
   unsigned long long levels;         // BFS levels run
   unsigned long long abytes;         // algorithmic bytes of its level / B-set launches (chain mode)
   unsigned long long launches;       // device launches of its chain (setup + steps + hops)
+  unsigned long long batches;        // launch batches the host enqueued (1: no continuation)
   long long path[1 + 3 * MAX_PATH_LEN];   // [v0, t0, r0, v1, ...]
 };
+constexpr unsigned long long CH_ERR_WALK_CAP = 64;   // the greedy walk did not end within its launch cap
+// the text of a failed search's SpResult::err (path.cpp's error messages)
+inline std::string sp_err_text(unsigned long long err) {
+  if (err == CH_ERR_WALK_CAP) return "greedy walk incomplete at the chain's launch cap";
+  if (err & 4) return "a frontier list's merge-path split did not describe its tile (code " + std::to_string(err) + ")";
+  return "device search aborted (code " + std::to_string(err) + ")";
+}
 struct SpCtx;                        // labels and level-loop buffers of one slot (sp.hip)
 // item_cap: items a list may hold = sum over a side's types of (nv + E_t / 64), plus slack
 // One query at a time per context; the level-loop buffers are allocated on its first use.

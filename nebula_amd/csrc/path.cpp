@@ -365,8 +365,9 @@ int32_t device_pair(PathCtx& c, int mode, uint32_t s, uint32_t t, uint32_t upto,
   if (he == hipSuccess) he = sp_wait(E.sp, &r);
   if (he != hipSuccess) return dev_fail(E, he, "shortest path");
   if (r.err == 1) return E.fail(NBG_E_UNKNOWN, "shortest-path reconstruction failed (in/out edges disagree)");
-  if (r.err) return E.fail(NBG_E_DEVICE, "shortest path: device search aborted (code " + std::to_string(r.err) + ")");
+  if (r.err) return E.fail(NBG_E_DEVICE, "shortest path: " + sp_err_text(r.err));
   c.edges += r.edges;
+  out->batches += (uint32_t)r.batches;
   if (r.L) out->paths.emplace_back(r.path, r.path + 1 + 3 * r.L);
   return NBG_OK;
 }
@@ -798,10 +799,11 @@ void path_complete_oldest(Engine& E) {
   } else if (r.err == 1) {
     t->rc = E.fail(NBG_E_UNKNOWN, "shortest-path reconstruction failed (in/out edges disagree)");
   } else if (r.err) {
-    t->rc = E.fail(NBG_E_DEVICE, "shortest path: device search aborted (code " + std::to_string(r.err) + ")");
+    t->rc = E.fail(NBG_E_DEVICE, "shortest path: " + sp_err_text(r.err));
   } else {
     auto* res = new nbg_paths();
     res->edges = r.edges;
+    res->batches = (uint32_t)r.batches;
     if (r.L) res->paths.emplace_back(r.path, r.path + 1 + 3 * r.L);
     t->result = res;
   }
@@ -815,6 +817,7 @@ namespace {
 nbg_paths* paths_of(const SpResult& r) {
   auto* res = new nbg_paths();
   res->edges = r.edges;
+  res->batches = (uint32_t)r.batches;
   if (r.L) res->paths.emplace_back(r.path, r.path + 1 + 3 * r.L);
   return res;
 }
@@ -949,7 +952,7 @@ int32_t nbg_find_path_batch(nbg_engine* h, const nbg_path_request* reqs, uint64_
         continue;
       }
       if (r.err) {
-        rcs[i] = E.fail(r.err == 1 ? NBG_E_UNKNOWN : NBG_E_DEVICE, "shortest path: device search failed");
+        rcs[i] = E.fail(r.err == 1 ? NBG_E_UNKNOWN : NBG_E_DEVICE, "shortest path: " + sp_err_text(r.err));
         continue;
       }
       out[i] = paths_of(r);
@@ -997,7 +1000,7 @@ int32_t nbg_find_path_batch(nbg_engine* h, const nbg_path_request* reqs, uint64_
       if (r.err == 1) {
         rcs[i] = E.fail(NBG_E_UNKNOWN, "shortest-path reconstruction failed (in/out edges disagree)");
       } else if (r.err) {
-        rcs[i] = E.fail(NBG_E_DEVICE, "shortest path: device search aborted (code " + std::to_string(r.err) + ")");
+        rcs[i] = E.fail(NBG_E_DEVICE, "shortest path: " + sp_err_text(r.err));
       } else {
         out[i] = paths_of(r);
       }

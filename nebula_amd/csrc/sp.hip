@@ -84,7 +84,9 @@ void sp_destroy(SpCtx* c) {
 }
 
 static hipError_t next_epoch(SpCtx* c) {
-  if (++c->epoch >= (1u << (32 - LVL_BITS))) {   // wrap: clear the labels once
+  // wrap (clear the labels once) below 2^24: spchain.hip's same-launch meet tags use the epochs
+  // with bit 24 or 25 set
+  if (++c->epoch >= (1u << 24)) {
     for (auto* l : c->lab) HIP_TRY_SP(hipMemsetAsync(l, 0, (c->nv + 1) * 4, c->stream));
     c->epoch = 1;
   }

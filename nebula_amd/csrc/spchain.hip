@@ -56,6 +56,11 @@ constexpr int CH_HOP_WGS = 64;            // workgroups scanning one greedy hop
 constexpr int CH_HOP_U = 4;               // neighbours per thread in flight (greedy)
 constexpr int CH_MAXS = 2 * MAX_PATH_LEN + 2;   // step launches of one query, at most
 
+// Same-launch meets of a two-sided level are exchanged through LAB_M under tag epochs: the query's
+// LAB_M epoch (< 2^24, sp.hip's next_epoch) with bit 25 (forward claim) or bit 24 (backward claim)
+constexpr uint32_t CH_TAG_F = 1u << 25, CH_TAG_B = 1u << 24;
+static_assert(CH_TAG_F < (1u << (32 - LVL_BITS)), "tag epochs fit the label's epoch field");
+
 enum ChListId : int { CL_F0 = 0, CL_F1 = 1, CL_B0 = 2, CL_B1 = 3, CL_M = 4, CH_NLISTS = 5 };
 enum ChPhase : uint32_t { PH_BFS = 0, PH_BSET = 1, PH_DONE = 2 };
 // profiled launch kinds (nbg_profile_read names: kChainKernelNames)
@@ -173,9 +178,10 @@ struct ChQ {
 // kf + kb + 1 when a vertex at forward level kf gets backward level kb + 1 (the backward claims test
 // the forward labels, which this launch does not write at level <= kf: a complete, race-free meet
 // set at position kf; every such path also has one); otherwise kf + kb + 2 when a vertex is claimed
-// by both sides in this launch — each claimer re-reads the other side's label after its own CAS
-// returned, so of two claims at least one sees the other (both CAS before either re-read): the meet
-// set at position kf + 1 is complete too (LAB_M stamps only; the first B-set step then pulls).
+// by both sides in this launch — each claimer then exchanges its side's tag into the vertex's LAB_M
+// word, and the later of the two exchanges (one location: a total modification order) returns the
+// earlier one's tag: the meet set at position kf + 1 is complete too (LAB_M stamps only; the first
+// B-set step then pulls).
 __host__ __device__ __forceinline__ uint32_t both_next(const ChSnap& s, uint32_t upto, uint32_t items) {
   const unsigned long long a = (s.cnt[0] >> 32) + (s.cnt[0] & 0xFFFFFFFFull);
   const unsigned long long b = (s.cnt[1] >> 32) + (s.cnt[1] & 0xFFFFFFFFull);
@@ -558,12 +564,14 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
   uint64_t npath = n + total, ntiles = (npath + (64 * VT) - 1) / (64 * VT);
   // a two-sided level: tiles [0, nt0) are the forward side's, [nt0, nt0 + nt1) the backward's.
   // Meets: a backward claim of a vertex at forward level kf (l1stamp; LAB_M stamp kf, the meet list,
-  // lmeet) or a vertex both sides claim in this launch (l2other, the other side's new stamp; LAB_M
-  // stamp kf + 1, lmeet2); forward claims of vertices at backward level <= kb are no meets here
+  // lmeet) or a vertex both sides claim in this launch (found by the exchange of mytag / otag in its
+  // LAB_M word; LAB_M stamp kf + 1, lmeet2); forward claims of vertices at backward level <= kb are
+  // no meets here
   const uint64_t nt0 = ntiles;
   const uint64_t nt1 = both ? (((P.cnt[1] >> 32) + (P.cnt[1] & 0xFFFFFFFFull)) + (64 * VT) - 1) / (64 * VT) : 0;
   const uint32_t l1stamp = stamp_of(q.ef, P.kf), l2m = stamp_of(q.em, P.kf + 1);
-  uint32_t l2other = stamp_of(q.eb, P.kb + 1);
+  // same-launch meet tags in LAB_M (tag epochs: never a query's live epoch, distinct per query)
+  uint32_t mytag = stamp_of(q.em | CH_TAG_F, P.kf + 1), otag = stamp_of(q.em | CH_TAG_B, P.kb + 1);
   if (both) mstamp = 0;   // (forward tiles record no position-kf meets)
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -600,7 +608,9 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
       col = A.col[1];
       npath = n + total;
       ntiles = nt1;
-      l2other = stamp_of(q.ef, P.kf + 1);
+      const uint32_t tt = mytag;
+      mytag = otag;
+      otag = tt;
     } else if (both && side == 1) {
       t = tg - nt0;
     }
@@ -753,16 +763,21 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
           mm |= 1u << j;
           continue;
         }
-        // claimed by the other side in this launch: seen before our claim, or re-read after it
-        if (!live(o, oepoch)) o = __hip_atomic_load(olab + c[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (o == l2other) m2 |= 1u << j;
+        // claimed by the other side in this launch too: both claimers exchange their side's tag into
+        // the vertex's ONE LAB_M word, so the later exchange in that word's modification order
+        // returns the earlier one's tag (a relaxed RMW reads the latest value of its location; a
+        // re-read of the other side's label after our own CAS would be the two-address store-buffer
+        // pattern, which the memory model lets both claimers miss)
+        const uint32_t prev = atomicExch(A.lab[2] + c[j], mytag);
+        if (prev == otag) m2 |= 1u << j;
       }
       if (__ballot(m2 != 0)) {
         uint32_t n2 = 0;
 #pragma unroll
         for (int j = 0; j < VT; ++j)
           if ((m2 >> j) & 1u) {
-            gst(A.lab[2], c[j], A.nv, l2m, 10, st);   // (both claimers may store it: the same value)
+            // (the one claimer that saw the other's tag; after both exchanges, so the stamp stays)
+            __hip_atomic_store(A.lab[2] + c[j], l2m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             ++n2;
           }
 #pragma unroll
@@ -1291,16 +1306,69 @@ __global__ void __launch_bounds__(CH_BLOCK) k_ch_hop(const ChArgs* __restrict__ 
 constexpr int CH_BMAX = 32;
 struct ChBatch {
   const ChArgs* A[CH_BMAX];
+  ChState* st[CH_BMAX];                // (A[p]->st, passed by value: the allocation's loads start at once)
   ChQ q[CH_BMAX];
   ChOut* out[CH_BMAX];
   int n;
-  uint32_t per;
+  uint32_t per;                        // fixed split: workgroups per pair (alloc == 0)
+  uint32_t alloc;                      // 1: the grid is split by each pair's work in this launch
+  uint32_t walk_items;                 // the work a pair whose search is over counts as (its walk)
 };
+
+// A pair's work in step launch i of a batch: the items of the step it runs (0 before launch 1:
+// every pair starts from one vertex per side), or walk_items once its search is over.  Every
+// workgroup derives it from the state the previous launch left, so all agree.
+__device__ __forceinline__ unsigned long long ch_batch_work(const ChBatch& b, int p, int i) {
+  if (i == 0) return 1;
+  const ChState* st = b.st[p];
+  const unsigned long long j = ld_agent(&st->first[i]);
+  const ChSnap P = snap_for(st, b.q[p], i);
+  if (j != (unsigned long long)i || P.phase == PH_DONE) return b.walk_items;
+  return step_items(P) + 1;
+}
+
+// Launch i of a batch: pair p takes nblk workgroups from `first` on.  alloc: 1 + (G - n) * work_p /
+// sum(work) workgroups each (a launch lasts as long as its slowest pair's step, so a pair's share
+// follows its step's size; a fixed 64 per pair left a hub level on 64 workgroups while most of
+// the grid returned at once); else the fixed `per`.
+__device__ __forceinline__ bool ch_batch_slot(const ChBatch& b, int i, uint32_t* p, uint32_t* bid, uint32_t* nblk) {
+  if (!b.alloc) {
+    *p = blockIdx.x / b.per;
+    *bid = blockIdx.x % b.per;
+    *nblk = b.per;
+    return (int)*p < b.n;
+  }
+  __shared__ uint32_t s_sel[3];
+  if (threadIdx.x < 64) {
+    const int l = threadIdx.x;
+    const unsigned long long w = l < b.n ? ch_batch_work(b, l, i) : 0ull;
+    unsigned long long W = w;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) W += __shfl_xor(W, o, 64);
+    const uint32_t G = gridDim.x, spare = G > (uint32_t)b.n ? G - (uint32_t)b.n : 0u;
+    const uint32_t a = l < b.n ? 1u + (uint32_t)(W ? ((unsigned long long)spare * w) / W : 0ull) : 0u;
+    const uint32_t incl = scan_incl(a), excl = incl - a;
+    if (l == 0) s_sel[0] = 0xFFFFFFFFu;
+    __builtin_amdgcn_wave_barrier();
+    if (a && blockIdx.x >= excl && blockIdx.x < incl) {
+      s_sel[0] = (uint32_t)l;
+      s_sel[1] = blockIdx.x - excl;
+      s_sel[2] = a;
+    }
+  }
+  __syncthreads();
+  *p = __builtin_amdgcn_readfirstlane(s_sel[0]);   // (uniform: kernel-argument arrays indexed by SGPRs)
+  *bid = __builtin_amdgcn_readfirstlane(s_sel[1]);
+  *nblk = __builtin_amdgcn_readfirstlane(s_sel[2]);
+  __syncthreads();   // (ch_level reuses LDS; s_sel is read once)
+  return *p != 0xFFFFFFFFu;
+}
+
 // (2 waves/SIMD: no spills; batched 33.3-33.9k -> 34.7-35.0k pairs/s, profiles/r03_y_sp_spec_ab.txt)
 __global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) k_ch_step_b(ChBatch b, int i, int last) {
-  const uint32_t p = blockIdx.x / b.per;
-  if ((int)p < b.n)
-    ch_any<CH_WAVES, CH_VT, false>(*b.A[p], b.q[p], i, blockIdx.x % b.per, b.per, last ? b.out[p] : nullptr);
+  uint32_t p, bid, nblk;
+  if (ch_batch_slot(b, i, &p, &bid, &nblk))
+    ch_any<CH_WAVES, CH_VT, false>(*b.A[p], b.q[p], i, bid, nblk, last ? b.out[p] : nullptr);
 }
 
 // ---------------------------------------------------------------------------- host side
@@ -1333,9 +1401,11 @@ struct ChainCtx {
   double ema_launches = 6;
   uint32_t tag_seq = 0;            // ChQ::tag of the next batch
   unsigned long long batches = 0, queries = 0;
+  uint32_t qbatches = 0;           // batches the query in flight has used (1: no continuation)
   // nbg_profile: HIP events around the chain's launches (mode 1 every launch, 2 step launches only)
   int prof = 0;
   bool last_batched = false;       // the query in flight ran in a batched chain
+  bool walk_cap = false;           // the walk did not end within CH_MAXS greedy launches (an error)
   struct PRec { int kind; hipEvent_t a, b; };
   std::vector<PRec> pend;
   std::vector<hipEvent_t> pool;
@@ -1442,6 +1512,7 @@ static hipError_t chain_batch(ChainCtx* c, int k, int h) {
       hipLaunchKernelGGL(k_ch_hop, dim3(CH_HOP_WGS), dim3(CH_BLOCK), 0, c->stream, A, c->q, c->steps, c->hops, c->d_out);
     });
   ++c->batches;
+  ++c->qbatches;
   return hipGetLastError();
 }
 
@@ -1484,6 +1555,8 @@ static hipError_t chain_prepare(ChainCtx* c, const SpTypes& fwd, const SpTypes& 
              jw ? (uint32_t)strtoul(jw, nullptr, 10) : CH_JOB_WAIT};
   c->steps = c->hops = 0;
   c->last_batched = false;
+  c->walk_cap = false;
+  c->qbatches = 0;
   ++c->queries;
   // the previous query's result launch zeroed this query's counters, unless it never ran
   if (!c->clean) HIP_TRY_CH(hipMemsetAsync(&c->d_st->c[c->par], 0, sizeof(ChCtr), c->stream));
@@ -1525,6 +1598,16 @@ hipError_t chain_launch_batch(ChainCtx* const* cs, int n, const ChainQuery* qs) 
   // (2048 workgroups for a full batch: 64 per pair at 32 pairs, 39.4-40.5 k pairs/s against
   // 34.3-34.7 k at 32 per pair with 2-item tiles, profiles/r03_fin2_sp_vt2_batch_ab.txt)
   b.per = per_env ? per_env : std::max(64u, 2048u / (unsigned)n);
+  // NBG_SP_BATCH_ALLOC (default 1): split the grid by each pair's step size; NBG_SP_BATCH_GRID
+  // workgroups per launch then (default 512: two per CU, every one resident at 2 waves per SIMD),
+  // NBG_SP_WALK_ITEMS the share of a walking pair
+  // (read per batch: one getenv per 32 pairs)
+  const int alloc_env = getenv("NBG_SP_BATCH_ALLOC") ? atoi(getenv("NBG_SP_BATCH_ALLOC")) : 1;
+  const unsigned grid_env = getenv("NBG_SP_BATCH_GRID") ? (unsigned)atoi(getenv("NBG_SP_BATCH_GRID")) : 512u;
+  const unsigned walk_env = getenv("NBG_SP_WALK_ITEMS") ? (unsigned)atoi(getenv("NBG_SP_WALK_ITEMS")) : 2048u;
+  b.alloc = alloc_env ? 1u : 0u;
+  b.walk_items = walk_env;
+  const unsigned grid = b.alloc ? std::max<unsigned>(grid_env, (unsigned)n) : (unsigned)n * b.per;
   int k = 1;
   for (int p = 0; p < n; ++p) {
     ChainCtx* c = cs[p];
@@ -1533,6 +1616,7 @@ hipError_t chain_launch_batch(ChainCtx* const* cs, int n, const ChainQuery* qs) 
     HIP_TRY_CH(chain_prepare(c, *x.fwd, *x.bwd, x.visible, x.vids, x.lab, x.epoch, x.s, x.t, x.upto));
     c->q.tag = ++c->tag_seq;
     b.A[p] = c->d_args;
+    b.st[p] = c->d_st;
     b.q[p] = c->q;
     b.out[p] = c->d_out;
     // the whole chain at once (every search step UPTO allows and one launch past them, which
@@ -1544,7 +1628,7 @@ hipError_t chain_launch_batch(ChainCtx* const* cs, int n, const ChainQuery* qs) 
   ChainCtx* c0 = cs[0];   // (the batch's launch events are kept by its first context)
   for (int j = 0; j < k; ++j)
     c0->timed(CHK_STEP_B, [&] {
-      hipLaunchKernelGGL(k_ch_step_b, dim3((unsigned)n * b.per), dim3(CH_BLOCK), 0, st, b, j, j + 1 == k);
+      hipLaunchKernelGGL(k_ch_step_b, dim3(grid), dim3(CH_BLOCK), 0, st, b, j, j + 1 == k);
     });
   HIP_TRY_CH(hipGetLastError());
   for (int p = 0; p < n; ++p) {
@@ -1555,6 +1639,7 @@ hipError_t chain_launch_batch(ChainCtx* const* cs, int n, const ChainQuery* qs) 
     c->steps = k;
     c->hops = 0;
     ++c->batches;
+    ++c->qbatches;
   }
   return hipSuccess;
 }
@@ -1574,16 +1659,29 @@ bool chain_more(ChainCtx* c, hipError_t* he) {
     // launches, or the rest if fewer — most such searches ended in the batch's last launch or
     // need one more step, and the launches past a search's end cost ~3 us each; a search still
     // not over continues again.  The batch's last launch stores if the search was over before it.
-    if (c->steps >= chain_max(c)) {   // (cannot happen: a search has at most 2 UPTO - 1 steps)
-      *he = hipErrorUnknown;
-      return true;
+    if (c->steps >= chain_max(c)) {
+      // a search has at most 2 UPTO - 1 steps, so it is over: the walk stopped at a hub whose job
+      // went unanswered in the chain's last launch.  Greedy continuation launches (k_ch_hop): each
+      // takes at least one hop (a hub's spread over its workgroups), the one that ends the walk
+      // stores the result, and the ones past it return at once
+      const int left = CH_MAXS - c->hops;
+      if (left <= 0) {   // (not reachable: every greedy launch advances the walk)
+        c->walk_cap = true;
+        return true;
+      }
+      *he = chain_batch(c, 0, std::min(left, (int)c->q.upto));
+      return false;
     }
     static const int kmore = getenv("NBG_SP_KMORE") ? std::max(1, atoi(getenv("NBG_SP_KMORE"))) : 2;
     *he = chain_batch(c, std::min(chain_max(c) - c->steps, kmore), 0);
     return false;
   }
   const uint32_t hpos = (uint32_t)(h.hpos >> 32);
-  if (F.met && !F.err && !h.err && hpos < F.L && c->hops < CH_MAXS) {
+  if (F.met && !F.err && !h.err && hpos < F.L) {
+    if (c->hops >= CH_MAXS) {
+      c->walk_cap = true;
+      return true;
+    }
     *he = chain_batch(c, 0, (int)F.L - (int)hpos);
     return false;
   }
@@ -1603,9 +1701,14 @@ void chain_result(const ChainCtx* c, SpResult* out) {
   out->levels = F.levels;
   out->abytes = F.abytes;
   out->launches = (unsigned long long)(c->steps + c->hops);
+  out->batches = c->qbatches;
   const uint32_t hpos = (uint32_t)(h.hpos >> 32);
-  out->L = (F.met && !h.err && hpos == F.L) ? F.L : 0;
-  if (F.met && !h.err && hpos != F.L) out->err = 2;   // (cannot happen: the hops were enqueued)
+  out->L = (F.met && !h.err && hpos == F.L && !c->walk_cap) ? F.L : 0;
+  if (c->walk_cap) {
+    out->err = CH_ERR_WALK_CAP;
+  } else if (F.met && !h.err && hpos != F.L) {
+    out->err = 2;   // (cannot happen: the hops were enqueued)
+  }
   if (out->L) memcpy(out->path, h.path, (1 + 3 * (size_t)out->L) * sizeof(long long));
   // NBG_SP_TRACE=2: one line per query (the chain's step and greedy launches, path length)
   static const bool per_query = getenv("NBG_SP_TRACE") && atoi(getenv("NBG_SP_TRACE")) == 2;

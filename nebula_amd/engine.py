@@ -5,7 +5,7 @@ Mirrors the reference's storage/graph operator surface for this path:
   * ``Engine.load_builder / load_part``     — KV records of a kvstore part
   * ``Engine.go``                           — GoExecutor result semantics
   * ``Engine.find_path``                    — FindPathExecutor result semantics
-The engine also implements the backend interface of ``nebula_amd.ngql.Session`` so nGQL text
+The engine also implements the backend interface of ``tests.support.ngql.Session`` (the test harness's nGQL front end) so nGQL text
 (GO / FIND PATH, pipes, variables) can be run against it.
 """
 from __future__ import annotations
@@ -486,6 +486,7 @@ class Engine:
                 paths.append(ptr[:n])   # one C-level slice per path
             if stats is not None:
                 stats["edges"] = int(self.lib.nbg_paths_edges_scanned(out))
+                stats["batches"] = int(self.lib.nbg_paths_chain_batches(out))
             return sorted(paths)
         finally:
             self.lib.nbg_paths_free(out)

@@ -40,6 +40,20 @@ inline uint64_t mix64(uint64_t z) {   // splitmix64 finaliser
 }
 inline uint64_t splitmix64(uint64_t x) { return mix64(x + 0x9E3779B97F4A7C15ull); }
 
+// per-query labels of one FIND SHORTEST PATH search (epoch-stamped: no clearing between queries);
+// one per concurrent search (orc_csr_shortest_many runs one per thread)
+struct SpCtx {
+  std::vector<uint32_t> labf, labb, mark;   // mark: B-set position, epoch-stamped like the labels
+  uint32_t epoch = 0;
+  void init(uint64_t nv) {
+    if (labf.size() == nv) return;
+    labf.assign(nv, 0);
+    labb.assign(nv, 0);
+    mark.assign(nv, 0);
+    epoch = 0;
+  }
+};
+
 struct Csr {
   uint64_t nv = 0, ne = 0;
   std::vector<int64_t> vid;                 // dense id -> vid (bucket-major; not sorted)
@@ -47,12 +61,10 @@ struct Csr {
   std::vector<uint32_t> nbr, inbr;          // out / in neighbour dense ids
   std::vector<int64_t> w;                   // out-edge weight column
   // vid -> dense id: hash bucket, then binary search inside the bucket's sorted vids
+  SpCtx sp;                                 // the single-query search's labels
   int bbits = 0;
   std::vector<uint64_t> bstart;             // [B + 1] first dense id of each bucket
   int threads = 1;
-  // per-query labels (epoch-stamped: no clearing between queries)
-  std::vector<uint32_t> labf, labb, mark;   // mark: B-set position, epoch-stamped like the labels
-  uint32_t epoch = 0;
 
   uint64_t bucket_of(int64_t v) const { return mix64((uint64_t)v) >> (64 - bbits); }
   int64_t dense(int64_t v) const {
@@ -198,9 +210,7 @@ Csr* build(const int64_t* src, const int64_t* dst, const int64_t* w, uint64_t n,
   for (int64_t d = 0; d < (int64_t)nv; ++d)
     for (uint64_t j = g->off[d]; j < g->off[d + 1]; ++j)
       g->inbr[__atomic_fetch_add(&icnt[g->nbr[j]], 1ull, __ATOMIC_RELAXED)] = (uint32_t)d;
-  g->labf.assign(nv, 0);
-  g->labb.assign(nv, 0);
-  g->mark.assign(nv, 0);
+  g->sp.init(nv);
   phase("csr");
   return g;
 }
@@ -335,25 +345,25 @@ uint64_t expand(const Csr& g, const std::vector<uint64_t>& off, const std::vecto
 }
 
 // returns the path length L (0: none within upto); path = [vid0, vid1, ..., vidL]
-int shortest(Csr& g, int64_t sv, int64_t tv, uint32_t upto, std::vector<int64_t>& path, uint64_t* scanned) {
+int shortest(const Csr& g, SpCtx& x, int T, int64_t sv, int64_t tv, uint32_t upto, std::vector<int64_t>& path,
+             uint64_t* scanned) {
   path.clear();
   *scanned = 0;
   const int64_t s64 = g.dense(sv), t64 = g.dense(tv);
   if (s64 < 0 || t64 < 0 || upto == 0) return 0;
   const uint32_t s = (uint32_t)s64, t = (uint32_t)t64;
-  const int T = g.threads;
-  if (++g.epoch >= (1u << (32 - LB))) {
-    std::fill(g.labf.begin(), g.labf.end(), 0);
-    std::fill(g.labb.begin(), g.labb.end(), 0);
-    std::fill(g.mark.begin(), g.mark.end(), 0);
-    g.epoch = 1;
+  if (++x.epoch >= (1u << (32 - LB))) {
+    std::fill(x.labf.begin(), x.labf.end(), 0);
+    std::fill(x.labb.begin(), x.labb.end(), 0);
+    std::fill(x.mark.begin(), x.mark.end(), 0);
+    x.epoch = 1;
   }
-  const uint32_t ep = g.epoch;
+  const uint32_t ep = x.epoch;
   auto lev = [&](const std::vector<uint32_t>& lab, uint32_t v) -> int {
     return (lab[v] >> LB) == ep ? (int)(lab[v] & ((1u << LB) - 1)) : -1;
   };
   std::vector<std::vector<uint32_t>> F{{s}}, Bk{{t}};
-  g.labf[s] = ep << LB;
+  x.labf[s] = ep << LB;
   uint32_t kf = 0, kb = 0, L = 0;
   std::vector<uint32_t> meet, next;
   if (s == t) {
@@ -367,15 +377,15 @@ int shortest(Csr& g, int64_t sv, int64_t tv, uint32_t upto, std::vector<int64_t>
       }
       if (hit) { L = kf + 1; break; }
       std::vector<uint32_t> m;
-      *scanned += expand(g, g.off, g.nbr, F[kf], g.labf, g.labb, ep, kf + 1, next, m, T);
+      *scanned += expand(g, g.off, g.nbr, F[kf], x.labf, x.labb, ep, kf + 1, next, m, T);
       F.push_back(next);
     }
     if (!L) return 0;
     // backward levels from t over in-edges up to L - 1 (t = s stamped at 0 on the b side)
-    g.labb[t] = ep << LB;
+    x.labb[t] = ep << LB;
     for (kb = 0; kb + 1 < L; ++kb) {
       std::vector<uint32_t> m;
-      *scanned += expand(g, g.ioff, g.inbr, Bk[kb], g.labb, g.labf, ep, kb + 1, next, m, T);
+      *scanned += expand(g, g.ioff, g.inbr, Bk[kb], x.labb, x.labf, ep, kb + 1, next, m, T);
       Bk.push_back(next);
     }
     path.push_back(g.vid[s]);
@@ -385,7 +395,7 @@ int shortest(Csr& g, int64_t sv, int64_t tv, uint32_t upto, std::vector<int64_t>
       uint32_t bu = 0;
       for (uint64_t j = g.off[c]; j < g.off[c + 1]; ++j) {
         const uint32_t u = g.nbr[j];
-        if (u == s || lev(g.labf, u) != (int)(i + 1) || lev(g.labb, u) != (int)(L - i - 1)) continue;
+        if (u == s || lev(x.labf, u) != (int)(i + 1) || lev(x.labb, u) != (int)(L - i - 1)) continue;
         if (best < 0 || g.vid[u] < best) { best = g.vid[u]; bu = u; }
       }
       if (best < 0) return 0;
@@ -395,7 +405,7 @@ int shortest(Csr& g, int64_t sv, int64_t tv, uint32_t upto, std::vector<int64_t>
     path.push_back(g.vid[s]);
     return (int)L;
   }
-  g.labb[t] = ep << LB;
+  x.labb[t] = ep << LB;
   // bidirectional level-synchronous BFS: expand the side whose frontier has the smaller degree
   // sum; the first level that claims a vertex labelled by the other side fixes L = kf + kb
   auto dsum = [&](const std::vector<uint32_t>& fr, const std::vector<uint64_t>& off) {
@@ -408,11 +418,11 @@ int shortest(Csr& g, int64_t sv, int64_t tv, uint32_t upto, std::vector<int64_t>
     if (F[kf].empty() || Bk[kb].empty()) return 0;
     const bool fwd = dsum(F[kf], g.off) <= dsum(Bk[kb], g.ioff);
     if (fwd) {
-      *scanned += expand(g, g.off, g.nbr, F[kf], g.labf, g.labb, ep, kf + 1, next, meet, T);
+      *scanned += expand(g, g.off, g.nbr, F[kf], x.labf, x.labb, ep, kf + 1, next, meet, T);
       F.push_back(next);
       ++kf;
     } else {
-      *scanned += expand(g, g.ioff, g.inbr, Bk[kb], g.labb, g.labf, ep, kb + 1, next, meet, T);
+      *scanned += expand(g, g.ioff, g.inbr, Bk[kb], x.labb, x.labf, ep, kb + 1, next, meet, T);
       Bk.push_back(next);
       ++kb;
     }
@@ -425,7 +435,7 @@ int shortest(Csr& g, int64_t sv, int64_t tv, uint32_t upto, std::vector<int64_t>
   // level i with an out-edge into B[i + 1]; positions > kf are backward levels L - i
   (void)fwd_last;
   std::vector<uint32_t> cur(meet);
-  std::vector<uint32_t>& mark = g.mark;    // ep << LB | position, for B-set members at positions <= kf
+  std::vector<uint32_t>& mark = x.mark;    // ep << LB | position, for B-set members at positions <= kf
   for (uint32_t v : cur) mark[v] = ep << LB | kf;
   for (int i = (int)kf - 1; i >= 0; --i) {
     std::vector<uint32_t> prev;
@@ -433,7 +443,7 @@ int shortest(Csr& g, int64_t sv, int64_t tv, uint32_t upto, std::vector<int64_t>
     for (uint32_t v : cur)
       for (uint64_t j = g.ioff[v]; j < g.ioff[v + 1]; ++j) {
         const uint32_t u = g.inbr[j];
-        if (lev(g.labf, u) == i && mark[u] != st) {
+        if (lev(x.labf, u) == i && mark[u] != st) {
           mark[u] = st;
           prev.push_back(u);
         }
@@ -447,7 +457,7 @@ int shortest(Csr& g, int64_t sv, int64_t tv, uint32_t upto, std::vector<int64_t>
     uint32_t bu = 0;
     for (uint64_t j = g.off[c]; j < g.off[c + 1]; ++j) {
       const uint32_t u = g.nbr[j];
-      const bool ok = (i + 1 <= kf) ? mark[u] == (ep << LB | (i + 1)) : lev(g.labb, u) == (int)(L - i - 1);
+      const bool ok = (i + 1 <= kf) ? mark[u] == (ep << LB | (i + 1)) : lev(x.labb, u) == (int)(L - i - 1);
       if (!ok) continue;
       if (best < 0 || g.vid[u] < best) { best = g.vid[u]; bu = u; }
     }
@@ -674,9 +684,33 @@ double orc_csr_go(void* h, const int64_t* starts, uint64_t ns, uint32_t steps, i
 // returns L (0: no path); *scanned = adjacency entries scanned (both directions).
 int32_t orc_csr_shortest(void* h, int64_t s, int64_t t, uint32_t upto, int64_t* path, uint64_t* scanned) {
   std::vector<int64_t> p;
-  const int L = shortest(*static_cast<Csr*>(h), s, t, upto, p, scanned);
+  Csr& g = *static_cast<Csr*>(h);
+  const int L = shortest(g, g.sp, g.threads, s, t, upto, p, scanned);
   for (size_t i = 0; L && i < p.size(); ++i) path[i] = p[i];
   return L;
+}
+
+// n independent searches, one per thread (each serial, with its own labels): path i's L + 1
+// vids at paths[i * (upto + 1)], len[i] = L (0: no path), scanned[i] its edges scanned
+void orc_csr_shortest_many(void* h, const int64_t* s, const int64_t* t, uint64_t n, uint32_t upto, int64_t* paths,
+                           int32_t* len, uint64_t* scanned) {
+  Csr& g = *static_cast<Csr*>(h);
+  const int T = g.threads;
+  std::vector<SpCtx> ctx(T);
+#pragma omp parallel num_threads(T)
+  {
+    SpCtx& c = ctx[omp_get_thread_num()];
+    c.init(g.nv);
+    std::vector<int64_t> p;
+#pragma omp for schedule(dynamic, 4)
+    for (int64_t i = 0; i < (int64_t)n; ++i) {
+      uint64_t sc = 0;
+      const int L = shortest(g, c, 1, s[i], t[i], upto, p, &sc);
+      len[i] = L;
+      scanned[i] = sc;
+      for (size_t k = 0; L && k < p.size(); ++k) paths[i * (upto + 1) + k] = p[k];
+    }
+  }
 }
 
 }  // extern "C"

@@ -4,7 +4,7 @@ from __future__ import annotations
 import json
 import os
 
-from nebula_amd import ngql
+from tests.support import ngql
 
 GOLDEN = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "golden")
 

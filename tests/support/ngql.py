@@ -1,4 +1,5 @@
-"""A small nGQL front end for the traversal statements (GO / FIND PATH), pipes and
+"""TEST HARNESS (not product code; SURVEY.md §2 puts the nGQL front end out of scope): a small
+nGQL front end for the traversal statements (GO / FIND PATH), pipes and
 variables — enough to drive the engine the way graphd does, so parity tests read like the
 reference's GoTest / FindPathTest.
 
@@ -17,8 +18,8 @@ import re
 from dataclasses import dataclass, field
 from typing import List, Optional
 
-from . import expr as E
-from .vidhash import std_hash
+from nebula_amd import expr as E
+from nebula_amd.vidhash import std_hash
 
 _TOK = re.compile(r"""\s*(?:
     (?P<double>\d+\.\d*(?:[eE][+-]?\d+)?|\.\d+(?:[eE][+-]?\d+)?)

@@ -329,6 +329,8 @@ class CsrOracle:
         L.orc_csr_go.argtypes = [vp, vp, u64, u32, i32, i64, i32, vp, vp, u64]
         L.orc_csr_shortest.restype = i32
         L.orc_csr_shortest.argtypes = [vp, i64, i64, u32, vp, C.POINTER(u64)]
+        L.orc_csr_shortest_many.restype = None
+        L.orc_csr_shortest_many.argtypes = [vp, vp, vp, u64, u32, vp, vp, vp]
         L.orc_csr_go_multi.restype = C.c_double
         L.orc_csr_go_multi.argtypes = [vp, i32, vp, u64, u32, vp]
         L.orc_csr_walk_counts.argtypes = [vp, i64, i64, u32, vp]
@@ -378,15 +380,28 @@ class CsrOracle:
         n = self.L.orc_csr_shortest(self.h, int(s), int(t), upto, _ptr(buf), C.byref(sc))
         return ([int(x) for x in buf[:n + 1]] if n else []), sc.value
 
+    def shortest_many(self, s, t, upto=5):
+        """Many independent searches, one per oracle thread: -> (list of vid paths ([] = none),
+        uint64 edges scanned per pair)."""
+        s = np.ascontiguousarray(s, np.int64)
+        t = np.ascontiguousarray(t, np.int64)
+        n = len(s)
+        paths = np.zeros((max(n, 1), upto + 1), np.int64)
+        ln = np.zeros(max(n, 1), np.int32)
+        sc = np.zeros(max(n, 1), np.uint64)
+        self.L.orc_csr_shortest_many(self.h, _ptr(s), _ptr(t), n, upto, _ptr(paths), _ptr(ln), _ptr(sc))
+        return [[int(x) for x in paths[i, :ln[i] + 1]] if ln[i] else [] for i in range(n)], sc[:n]
+
     @staticmethod
-    def go_multi(csrs, starts, steps):
+    def go_multi(csrs, starts, steps, seconds=False):
         """GO `steps` STEPS OVER several types (one CsrOracle per OVER type, in OVER order), default
-        YIELD (one _dst column per type): -> (digest, edges scanned)."""
+        YIELD (one _dst column per type): -> (digest, edges scanned[, seconds])."""
         s = np.asarray(starts, np.int64)
         hs = (C.c_void_p * len(csrs))(*[c.h for c in csrs])
         out = np.zeros(4, np.uint64)
-        csrs[0].L.orc_csr_go_multi(hs, len(csrs), _ptr(s), len(s), steps, _ptr(out))
-        return (int(out[0]), int(out[1]), int(out[2])), int(out[3])
+        sec = csrs[0].L.orc_csr_go_multi(hs, len(csrs), _ptr(s), len(s), steps, _ptr(out))
+        res = (int(out[0]), int(out[1]), int(out[2])), int(out[3])
+        return res + (sec,) if seconds else res
 
     def rank_edges(self, starts, steps, parts, world):
         """Edges each rank scans per step when every start is its own GO `steps` STEPS query on

@@ -7,9 +7,9 @@
       oracle's digest for the bench's 16 roots, a sampled full compare for 2 roots, and 64
       SHORTEST pairs; the same graph PARTITIONED over 2 ranks (P = 100, parts p % 2), digests
       summed over ranks for the 16 roots and 32 SHORTEST pairs entry by entry
-  C5  the LDBC substitute at the bench's size (knows RMAT-20 + likes RMAT-19): GO 4 STEPS OVER
-      knows, likes by digest for the bench's 16 roots (two-type CSR oracle), FIND ALL PATH UPTO 4
-      for its 64 pairs: path counts vs walk counts, entry lists where a pair has <= 20 k paths
+  C5  the LDBC substitute at the bench's size (knows RMAT-24 + likes RMAT-23): GO 4
+      STEPS OVER knows, likes by digest for the bench's 16 roots (two-type CSR oracle), FIND ALL PATH
+      UPTO 4 for its 64 pairs: path counts vs walk counts, entry lists where a pair has <= 20 k paths
 
 The checker is oracle/csr.cpp (CSR restatement, pinned to the storaged-faithful oracle on
 RMAT <= 12 by tests/test_oracle_csr.py).  Graphs are the bench's own (nebula_amd.rmat)."""
@@ -202,6 +202,38 @@ def test_c4_batched_pairs_rmat26(rmat26):
     assert found > 30
 
 
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("job_wait", [None, "0"], ids=["jobs", "unanswered"])
+def test_c4_rmat26_bench_pairs_every_pass(rmat26, job_wait, monkeypatch):
+    """C4 at full size on the timing-dependent paths: the bench's first 1,200 SHORTEST pairs
+    (RMAT-26, seed 7, UPTO 5) one at a time, six in flight and batched, every result entry by entry
+    against orc_csr_shortest_many.  With NBG_SP_JOB_WAIT=0 no hub job of a one-pair chain is ever
+    answered, so every hub on a walk falls back to the next launch's spread scan or a continuation.
+    Pairs whose chain needed a continuation batch (nbg_paths_chain_batches > 1) are counted: they
+    are among the pairs compared."""
+    if job_wait is not None:
+        monkeypatch.setenv("NBG_SP_JOB_WAIT", job_wait)
+    src, dst, eng, csr, _, av = rmat26
+    pairs = rmat.pick_pairs(src, dst, 10000, 7, verts=av)[:1200]
+    exp, _ = csr.shortest_many([p[0] for p in pairs], [p[1] for p in pairs], 5)
+    want = [[[x for v in p[:-1] for x in (v, 1, 0)] + [p[-1]]] if p else [] for p in exp]
+    cont = 0
+    for (s, t), w in zip(pairs, want):
+        st = {}
+        assert eng.find_path([s], [t], [1], 5, stats=st) == w, (s, t, job_wait)
+        cont += st["batches"] > 1
+    pending, got = [], []
+    for s, t in pairs:
+        if len(pending) == 6:
+            got.append(eng.find_path_wait(pending.pop(0)))
+        pending.append(eng.find_path_submit([s], [t], [1], 5))
+    got += [eng.find_path_wait(tk) for tk in pending]
+    assert got == want
+    assert eng.find_path_batch([([s], [t], [1], 5, True) for s, t in pairs]) == want
+    assert sum(1 for p in exp if p) > 600
+    assert cont > 0, "no pair needed a continuation: the continuation path went unexercised"
+
+
 def _c5_graph(k):
     """BASELINE C5's synthetic substitute (bench.py c5_leg) at scale k: knows = RMAT-k over persons,
     likes = a bipartite RMAT-(k-1) from persons to posts (post vids in a disjoint range)."""
@@ -249,9 +281,9 @@ def test_c5_substitute_go4_and_all_paths():
 
 @pytest.fixture(scope="module")
 def c5_bench():
-    """The bench's C5 graph (bench.py c5_leg at its default --c5-scale 20) on one engine and as two
+    """The bench's C5 graph (bench.py c5_leg at its default --c5-scale 24) on one engine and as two
     CSR oracles (knows, likes)."""
-    (ks, kd, kw), (ls, ld, lw) = _c5_graph(20)
+    (ks, kd, kw), (ls, ld, lw) = _c5_graph(24)
     eng = Engine(100)
     eng.register_edge(1, "knows", [("w", 2)])
     eng.register_edge(2, "likes", [("w", 2)])
@@ -267,7 +299,7 @@ def c5_bench():
 
 
 @pytest.mark.timeout(900)
-def test_c5_rmat20_go4_digests(c5_bench):
+def test_c5_rmat24_go4_digests(c5_bench):
     """GO 4 STEPS OVER knows, likes (default YIELD knows._dst, likes._dst) from the bench's 16
     roots: device digest and scanned edges equal the two-type CSR oracle's."""
     ks, kd, eng, ck, cl = c5_bench
@@ -288,17 +320,24 @@ def test_c5_rmat20_go4_digests(c5_bench):
 
 
 @pytest.mark.timeout(900)
-def test_c5_rmat20_all_paths(c5_bench):
+def test_c5_rmat24_all_paths(c5_bench):
     """FIND ALL PATH UPTO 4 STEPS OVER knows for the bench's 64 pairs: every pair's path count equals
     the number of walks of 1..4 edges (walk-count DP); pairs with at most 20 k paths are compared
-    entry list by entry list with the oracle's walk enumeration."""
+    entry list by entry list with the oracle's walk enumeration.  A pair over the engine's walk cap
+    (NBG_MAX_WALKS partial walks) must fail with a status, never return a truncated list."""
+    from nebula_amd import NbgError
     ks, kd, eng, ck, cl = c5_bench
     persons = np.union1d(np.unique(ks), np.unique(kd))
     pairs = rmat.pick_pairs(ks, kd, 64, 7, verts=persons)
     total = compared = 0
     for s, t in pairs:
-        got = eng.find_path([s], [t], [1], 4, shortest=False)
-        assert len(got) == sum(ck.walk_counts(s, t, 4)[1:]), (s, t)
+        n = sum(ck.walk_counts(s, t, 4)[1:])
+        try:
+            got = eng.find_path([s], [t], [1], 4, shortest=False)
+        except NbgError:
+            assert n > 1 << 20, (s, t, n)   # (only a pair with a huge answer may exceed the cap)
+            continue
+        assert len(got) == n, (s, t)
         total += len(got)
         if len(got) <= 20000:
             walks = ck.all_walks(s, t, 4, cap=20000)

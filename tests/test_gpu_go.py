@@ -274,7 +274,7 @@ def test_c1_go_2_steps_nba(nba, nba_data):
     """BASELINE configs[0] (C1): GO 2 STEPS FROM "Tim Duncan" OVER like (the `follow` edge of
     later releases is this reference's `like`) — device vs the oracle, plus
     YIELD variants on the same hop pattern."""
-    from nebula_amd import ngql
+    from tests.support import ngql
     from nebula_amd.vidhash import std_hash
     orc = nba_oracle(nba_data)
     try:

@@ -137,6 +137,42 @@ def test_shortest_through_a_hub(hits, sp_mode, job_wait, monkeypatch):
         orc.close()
 
 
+@pytest.mark.parametrize("job_wait", [None, "0"], ids=["jobs", "unanswered"])
+def test_shortest_hub_walk_at_the_chain_cap(job_wait, sp_mode, monkeypatch):
+    """L == UPTO with the search using every step launch a chain has: a target with 30,000
+    in-edges keeps the backward side unexpanded (kb = 0), so s -> a -> hub -> x -> b -> t takes 5
+    BFS levels and 4 B-set steps (2 UPTO - 1 launches), leaving the chain one greedy launch.  Its
+    walk reaches the hub (10,000 out-edges) as a job; unanswered (NBG_SP_JOB_WAIT=0) the walk
+    stops there and the chain's launches are spent: the query continues with greedy launches
+    (round 5's chain_more failed it with a bare hipErrorUnknown).  Entry lists as the oracle, one
+    at a time and batched."""
+    if job_wait is not None:
+        monkeypatch.setenv("NBG_SP_JOB_WAIT", job_wait)
+    rng = np.random.default_rng(11)
+    s_v, a_v, hub, b_v, t_v = 5, 6, 7, 8, 9
+    xs = np.unique(rng.integers(1000, 1 << 40, 10000, dtype=np.int64))
+    ys = np.unique(rng.integers(-(1 << 40), -1000, 30000, dtype=np.int64))
+    reach = rng.choice(xs, 40, replace=False)
+    src = np.concatenate([[s_v, a_v], np.full(len(xs), hub), reach, [b_v], ys, rng.choice(xs, 300)])
+    dst = np.concatenate([[a_v, hub], xs, np.full(len(reach), b_v), [t_v], np.full(len(ys), t_v),
+                          rng.choice(xs, 300)])
+    w = np.zeros(len(src), np.int64)
+    eng = graphs.rmat_engine(src, dst, w)
+    orc = graphs.rmat_oracle(src, dst, w)
+    try:
+        for _ in range(3):   # (the chain is sized by recent queries: the first and later ones differ)
+            for a, b, upto in ((s_v, t_v, 5), (s_v, t_v, 6), (a_v, t_v, 4)):
+                got = eng.find_path([a], [b], [1], upto)
+                exp = orc.find_path([a], [b], [1], upto, True, mode=1)
+                assert got == sorted(exp) and got, (a, b, upto, job_wait)
+                assert len(got[0]) == 3 * (5 if a == s_v else 4) + 1
+        reqs = [([s_v], [t_v], [1], 5, True), ([a_v], [t_v], [1], 4, True)]
+        assert eng.find_path_batch(reqs) == [eng.find_path(*r[:4]) for r in reqs]
+    finally:
+        eng.close()
+        orc.close()
+
+
 @pytest.mark.parametrize("hits", ["rank_first", "vid_first"])
 def test_shortest_through_a_ranked_hub(hits, sp_mode):
     """A hub row with ranks (more than 4096 out-edges: its hop is spread over workgroups): 6,000

@@ -126,7 +126,7 @@ def test_capped_nba_findpath_cases(nba_data, k):
     kb = kvgen.nba_kv(nba_data, 1)
     eng.load_builder(kb)
     orc.load_builder(kb)
-    from nebula_amd import ngql
+    from tests.support import ngql
     try:
         differs = 0
         for case in golden.load("findpath_golden.json"):

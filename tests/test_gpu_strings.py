@@ -11,7 +11,8 @@ both through the nGQL front end; rows are compared as sorted multisets, and a qu
 must fail on both."""
 import pytest
 
-from nebula_amd import Engine, LocalCluster, NbgError, kvgen, ngql
+from nebula_amd import Engine, LocalCluster, NbgError, kvgen
+from tests.support import ngql
 from nebula_amd.engine import nba_engine
 from tests.support.oracle import Oracle, OracleError, nba_oracle
 
@@ -200,7 +201,7 @@ def test_arena_overflow_fails_cleanly(monkeypatch):
         "eng, orc = _numbers(3)\n"
         "big = ' + '.join(['rel.s'] * 8)\n"
         "q = 'GO FROM 1 OVER rel YIELD ' + ' , '.join([big] * 4)\n"
-        "from nebula_amd import ngql\n"
+        "from tests.support import ngql\n"
         "try:\n"
         "    ngql.Session(eng).execute(q)\n"
         "    print('NO-ERROR')\n"

@@ -5,7 +5,7 @@ Pinned to ScannerTest.cpp:415-430 (values and lexical errors); the longest-match
 follow the scanner's rules directly.  CPU only."""
 import pytest
 
-from nebula_amd.ngql import ParseError, int_literal, parse
+from tests.support.ngql import ParseError, int_literal, parse
 
 # ScannerTest.cpp:415-430 (int64 values: the sscanf conversions wrap)
 PINNED = [("123", 123), ("0x123", 0x123), ("0xdeadbeef", 0xdeadbeef), ("0123", 0o123),

@@ -88,6 +88,22 @@ def test_shortest_modes_agree(scale):
         csr.close()
 
 
+def test_shortest_many_equals_one_at_a_time():
+    """orc_csr_shortest_many (one serial search per thread, own labels) = orc_csr_shortest pair by
+    pair: paths and edges scanned, self-pairs and unknown vids included."""
+    src, dst, w = graphs.rmat_graph(12)
+    csr = CsrOracle(src, dst, w, threads=4)
+    try:
+        pairs = _pairs(src, dst, 300, seed=5) + [(int(src[0]), int(src[0])), (int(src[1]), -12345)]
+        many, sc = csr.shortest_many([p[0] for p in pairs], [p[1] for p in pairs], 5)
+        assert sum(1 for p in many if p) > 50
+        for (s, t), got, g_sc in zip(pairs, many, sc):
+            exp, e_sc = csr.shortest(s, t, 5)
+            assert got == exp and int(g_sc) == e_sc, (s, t)
+    finally:
+        csr.close()
+
+
 def test_shortest_csr_self_cycles():
     """FROM s TO s: the shortest cycle through s (length >= 1)."""
     src, dst, w = graphs.rmat_graph(9)
