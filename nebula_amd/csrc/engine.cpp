@@ -1126,6 +1126,17 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
   // collectives, with zero bitmaps and its status word in the statistics, and every rank fails the
   // query when it reads them (go_collect).  Other statements agree first (Comm::agree).
   static const bool force_agree = getenv("NBG_GO_AGREE") && atoi(getenv("NBG_GO_AGREE")) != 0;
+  // A small first hop travels as per-owner slot arrays instead of npad-bit bitmaps (ws_set_hop_slots:
+  // the single-root hop is one row on one rank, and sent 3.6 MB per rank at RMAT-26 / G = 8).  Its
+  // bound comes from the degrees every rank holds (Engine::first_hop_bound), so every rank — a
+  // failing one too — picks the same format.  NBG_GO_SLOTS=0 keeps bitmaps (read per query).
+  uint64_t hop1_slots = 0;
+  if (part && steps >= 2 && over.size() == 1 && !(st->uses_input && steps > 1) &&
+      !(getenv("NBG_GO_SLOTS") && atoi(getenv("NBG_GO_SLOTS")) == 0)) {
+    const uint64_t b = E.first_hop_bound(over[0], starts, num_starts, cap);
+    const uint64_t stride = b == UINT64_MAX ? 0 : std::max<uint64_t>(64, (b + 63) / 64 * 64);
+    if (stride && stride * 4 * 2 <= E.npad / 8) hop1_slots = stride;
+  }
   // (YIELD DISTINCT too: its owner exchange runs in go_collect, which every rank leaves at the
   // in-band status before reaching it)
   const bool in_band = part && !st->uses_input && !force_agree;
@@ -1133,7 +1144,7 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
     if (lrc) {
       int32_t agreed = NBG_OK;
       const hipError_t he = part_empty_query(qcomm, stream, (int)steps - 1, E.fb_send, E.fb_recv, E.npad / 8,
-                                             E.fb_gst, E.fb_hgst, lrc, &agreed);
+                                             hop1_slots * 4, E.fb_gst, E.fb_hgst, lrc, &agreed);
       if (he != hipSuccess) {
         qcomm->abort();
         return E.fail(NBG_E_DEVICE, "query statistics exchange: " + qcomm->last);
@@ -1236,6 +1247,7 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
       ExpandArgs a = args_for(it->second);
       a.bt_first = s == 1;
       if (!final) {
+        if (s == 1 && i == 0) ws_set_hop_slots(ws, hop1_slots);
         he = ws_expand_mark(ws, a, n_bound, it->second.num_edges, (int)s, (int)i, inl_of(i, s), np0);
       } else if (deferred || (plist[i].where_const && !plist[i].where_const_val)) {
         he = ws_scan_only(ws, a, n_bound, (int)s, (int)i);

@@ -74,6 +74,15 @@ struct Engine {
   std::unique_ptr<Comm> comm;
   uint64_t npad = 0;
   bool partitioned() const { return cfg.num_gpus > 1; }
+  // partitioned: every rank's dictionary (global id order) and every vertex's out-degree per positive
+  // type over the global id space, host copies from finalize, so that every rank bounds a GO first
+  // hop's edges per owner alike (go_launch sends a small hop as slot arrays instead of bitmaps)
+  std::vector<int64_t> h_gdict;
+  std::vector<uint64_t> h_gcount;
+  std::map<int32_t, std::vector<uint32_t>> h_gdeg;
+  int32_t gather_degrees();   // (collective, at finalize)
+  // the most edges (capped degrees) the starts hold on any one rank; UINT64_MAX when unknown
+  uint64_t first_hop_bound(int32_t type, const int64_t* starts, uint64_t n, uint32_t cap) const;
 
   // FIND PATH replica of a partitioned snapshot (replica.hip): a single-GPU engine over every
   // rank's path CSRs; FIND PATH runs on it rank-locally while it is in use

@@ -1801,6 +1801,42 @@ __global__ void __launch_bounds__(BLOCK) k_bits_compact(const unsigned long long
   }
 }
 
+// Owner side of a small hop's slot exchange (ws_set_hop_slots): recv = world segments of `stride`
+// local ids (NO_ROW: empty).  A vertex may arrive several times, so each arrival is claimed
+// against the step's stamp (CAS); the winners are listed, with their edge space over ds, as
+// k_bits_compact lists a bitmap's (the union is getDstIdsFromResp's per-step set).
+constexpr int SC_ITEMS = 4;
+__global__ void __launch_bounds__(BLOCK) k_slots_compact(const uint32_t* __restrict__ recv, uint64_t slots,
+                                                         uint32_t* __restrict__ lab, uint32_t stamp, uint64_t nv,
+                                                         DegSrc ds, ListOut o) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *o.zero_next = 0;
+  const uint64_t base = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) * SC_ITEMS;
+  uint32_t v[SC_ITEMS], dg[SC_ITEMS], rs[SC_ITEMS], c = 0, d = 0;
+#pragma unroll
+  for (int k = 0; k < SC_ITEMS; ++k) v[k] = base + k < slots ? recv[base + k] : NO_ROW;
+#pragma unroll
+  for (int k = 0; k < SC_ITEMS; ++k) {
+    if (v[k] >= nv) {   // (NO_ROW, or an id past this rank's vertices: dropped)
+      v[k] = NO_ROW;
+    } else {
+      const uint32_t old = lab[v[k]];
+      if (old == stamp || atomicCAS(lab + v[k], old, stamp) != old) v[k] = NO_ROW;
+    }
+    dg[k] = v[k] != NO_ROW ? vdeg(ds, v[k], &rs[k]) : 0u;
+    c += v[k] != NO_ROW ? 1u : 0u;
+    d += dg[k];
+  }
+  uint32_t pc, pd;
+  reserve<BLOCK>(c, d, o.acc, &pc, &pd);
+#pragma unroll
+  for (int k = 0; k < SC_ITEMS; ++k) {   // (every lane: wave_splits is wave-wide)
+    uint64_t t0 = 0, t1 = 0;
+    const uint32_t pp = pc;
+    if (v[k] != NO_ROW) list_put(o, ds, pc++, v[k], &pd, dg[k], rs[k], &t0, &t1);
+    wave_splits(o.tsplit, t0, t1, pp);
+  }
+}
+
 // Partitioned roots, 1 of 3: the popcount before every bitmap word within its block of RW_BLOCK
 // words, and each block's total, over the send bitmap (blocks [0, nb)) and the received one
 // ([nb, 2 nb)); 4 words per thread.
@@ -2573,7 +2609,15 @@ hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, 
   // partitioned MARK (not MARKB, whose roots ride with the byte flags): straight into the hop's
   // send bitmap, which ws_exchange then sends without a pack pass
   if (w->comm && !a0.bt && !bits_off()) {
-    bp.bits = w->sendbits;
+    if (w->hop_slots) {   // a small hop: edge e's neighbour into slot e of its owner's segment
+      if (tix == 0)
+        HIP_TRY(hipMemsetAsync(w->sendbits, 0xFF, (uint64_t)w->comm->world * w->hop_slots * 4, w->stream));
+      bp.sparse = reinterpret_cast<uint32_t*>(w->sendbits);
+      bp.sp_stride = (uint32_t)w->hop_slots;
+      bp.sp_npad = (uint32_t)w->npad;
+    } else {
+      bp.bits = w->sendbits;
+    }
     w->hop_bits = true;
   }
   if (inline_start_list(w, tix, il)) {   // no k_relist: the list travels in the kernel arguments
@@ -2737,7 +2781,10 @@ static FastProg detect_fast(const TypeProgram& prog, const ExpandArgs& a) {
 // CUs hold one workgroup more and set the launch's time (r05_i_final_grid_sweep.txt: 1920 -> 210 us,
 // 1536 / 2048 / 2560 -> 202 us; GO 362-364 at 1920 and 2048).  NBG_FINAL_GRID caps it (0 = no cap).
 static unsigned final_grid(uint64_t n_bound, uint64_t e_bound) {
-  static const unsigned cap = getenv("NBG_FINAL_GRID") ? (unsigned)atoi(getenv("NBG_FINAL_GRID")) : 0u;
+  // (read per call: a statement's row regions are sized with the grid its launches use, and
+  // both read it within one query)
+  const char* ev = getenv("NBG_FINAL_GRID");
+  const unsigned cap = ev ? (unsigned)atoi(ev) : 0u;
   const unsigned g = expand_grid(n_bound, e_bound);
   return cap && cap < g ? cap : g;
 }
@@ -3713,10 +3760,11 @@ hipError_t ws_set_partition(Workspace* w, Comm* comm, uint64_t npad) {
 // all-reduce with zero statistics and its status word.  Synchronous; *agreed = the first failing
 // rank's status.
 hipError_t part_empty_query(Comm* c, hipStream_t s, int hops, const void* send0, void* recv, size_t seg_bytes,
-                            unsigned long long* gst, unsigned long long* h_gst, int32_t status, int32_t* agreed) {
+                            size_t first_bytes, unsigned long long* gst, unsigned long long* h_gst, int32_t status,
+                            int32_t* agreed) {
   const int G = c->world;
-  for (int h = 0; h < hops; ++h)
-    if (c->alltoall(send0, recv, seg_bytes, s)) return hipErrorUnknown;
+  for (int h = 0; h < hops; ++h)   // (the first hop may be a slot exchange: first_bytes per peer)
+    if (c->alltoall(send0, recv, h == 0 && first_bytes ? first_bytes : seg_bytes, s)) return hipErrorUnknown;
   HIP_TRY(hipMemsetAsync(gst, 0, GST_N * sizeof(unsigned long long), s));
   hipLaunchKernelGGL(k_gst_status, dim3(1), dim3(64), 0, s, gst, G, c->rank, (long long)status);
   HIP_TRY(hipGetLastError());
@@ -3771,11 +3819,43 @@ static hipError_t ws_roots(Workspace* w, int step) {
   return hipSuccess;
 }
 
+void ws_set_hop_slots(Workspace* w, uint64_t stride) {
+  if (w) w->hop_slots = stride && w->comm && stride * 4 * 2 <= w->npad / 8 ? stride : 0;
+}
+
 hipError_t ws_exchange(Workspace* w, int step, const ExpandArgs* next0) {
   if (!w->comm) return hipErrorInvalidValue;
   const uint64_t G = (uint64_t)w->comm->world;
   const uint64_t nwords = G * w->npad / 64, seg_words = w->npad / 64, nb = w->npad / BITS_BLOCK;
   hipEvent_t p = nullptr;
+  if (w->hop_slots && w->hop_bits && !w->bt_active) {
+    // a small hop's slot arrays: stride ids per peer instead of npad / 8 bytes; the owner claims
+    // the arrivals against the step's stamp (a vertex may arrive from several edges and ranks)
+    const uint64_t stride = w->hop_slots;
+    w->hop_slots = 0;
+    w->hop_bits = false;
+    p = prof_begin(w, K_ALLTOALL);
+    if (w->comm->alltoall(w->sendbits, w->recvbits, stride * 4, w->stream)) return hipErrorUnknown;
+    prof_end(w, p, K_ALLTOALL, step, 0, (double)((G - 1) * stride * 4));
+    HIP_TRY(hipMemsetAsync(w->sendbits, 0, G * stride * 4, w->stream));   // (all-zero between hops)
+    if (++w->seen_stamp == 0) {   // wrap: clear the stamps once
+      HIP_TRY(hipMemsetAsync(w->seen, 0, (w->nv + 1) * 4, w->stream));
+      w->seen_stamp = 1;
+    }
+    unsigned long long* acc = &w->q->acc[2 + w->pc];
+    unsigned long long* other = &w->q->acc[2 + (w->pc ^ 1)];
+    w->pc ^= 1;
+    p = prof_begin(w, K_BITS_COMPACT);
+    hipLaunchKernelGGL(k_slots_compact, dim3((unsigned)cdiv(G * stride, (uint64_t)BLOCK * SC_ITEMS)), dim3(BLOCK), 0,
+                       w->stream, reinterpret_cast<const uint32_t*>(w->recvbits), G * stride, w->seen, w->seen_stamp,
+                       w->nv, deg_src(next0), list_out(w, w->frontier[w->cur ^ 1], acc, other, nullptr, w->cur ^ 1));
+    prof_end(w, p, K_BITS_COMPACT, step, 0);
+    w->cur ^= 1;
+    w->list_acc = acc;
+    w->seg_ready = next0 != nullptr;
+    return hipGetLastError();
+  }
+  w->hop_slots = 0;
   if (!w->hop_bits) {   // byte flags (MARKB): pack them into the send bitmap
     p = prof_begin(w, K_PACK);
     hipLaunchKernelGGL(k_pack_bits, dim3((unsigned)cdiv(nwords, BLOCK)), dim3(BLOCK), 0, w->stream, w->flags, nwords,

@@ -708,10 +708,14 @@ hipError_t ws_set_partition(Workspace* w, Comm* comm, uint64_t npad);
 Comm* ws_get_comm(const Workspace* w);   // the communicator of a partitioned workspace (else nullptr)
 hipStream_t ws_stream(const Workspace* w);
 hipError_t ws_exchange(Workspace* w, int step, const ExpandArgs* next0);   // replaces ws_compact
+// the next hop (its MARKs and ws_exchange) sends per-owner slot arrays of `stride` local ids
+// instead of npad-bit bitmap segments; the caller guarantees the hop's edges on every rank fit
+void ws_set_hop_slots(Workspace* w, uint64_t stride);
 hipError_t ws_global_stats(Workspace* w, int ntypes);      // before ws_end_query
 int32_t ws_host_gstatus(Workspace* w);                     // after it: the first failing rank's status
 hipError_t part_empty_query(Comm* c, hipStream_t s, int hops, const void* send0, void* recv, size_t seg_bytes,
-                            unsigned long long* gst, unsigned long long* h_gst, int32_t status, int32_t* agreed);
+                            size_t first_bytes, unsigned long long* gst, unsigned long long* h_gst, int32_t status,
+                            int32_t* agreed);
 size_t part_gst_words(int world);
 void ws_host_gstats(Workspace* w, unsigned long long* err, unsigned long long* step_n, unsigned long long* esum,
                     unsigned long long* tagbits);

@@ -128,6 +128,9 @@ struct ChState {        // device; the host reads what the result launch derives
   unsigned long long hjob, hjob_rng;
   unsigned long long htag[CH_HOP_WGS];
   unsigned long long hpart[4 * CH_HOP_WGS];
+  // the batch tag (ChQ::tag) of the launch in which this query's walk ended (or found nothing to
+  // walk): a batched chain's later launches give the pair one workgroup (ch_batch_work)
+  unsigned long long walk_end;
 };
 
 // What the host reads after a chain, stored by its last launch (ch_out) straight into mapped
@@ -1034,6 +1037,7 @@ __device__ __forceinline__ bool ch_hop(const ChArgs& A, const ChQ& q, int nl, in
   uint32_t pos = (uint32_t)(H >> 32), c = (uint32_t)H;
   auto finish = [&](uint32_t p, uint32_t v) {   // (thread 0 of the one writer)
     st->hstart[h + 1] = ((unsigned long long)p << 32) | v;
+    if (v == NO_ROW || !F.met || F.err || p >= F.L) st->walk_end = q.tag;
   };
   if (!F.met || F.phase != PH_DONE || F.err || pos >= F.L || c == NO_ROW) {
     if (bid == 0 && threadIdx.x == 0) finish(pos, c);
@@ -1322,7 +1326,9 @@ __device__ __forceinline__ unsigned long long ch_batch_work(const ChBatch& b, in
   if (i == 0) return 1;
   const ChState* st = b.st[p];
   const unsigned long long j = ld_agent(&st->first[i]);
+  const unsigned long long we = ld_agent(&st->walk_end);
   const ChSnap P = snap_for(st, b.q[p], i);
+  if (we == (unsigned long long)b.q[p].tag) return 0;   // its walk is over: one workgroup, which returns
   if (j != (unsigned long long)i || P.phase == PH_DONE) return b.walk_items;
   return step_items(P) + 1;
 }
@@ -1604,7 +1610,7 @@ hipError_t chain_launch_batch(ChainCtx* const* cs, int n, const ChainQuery* qs) 
   // (read per batch: one getenv per 32 pairs)
   const int alloc_env = getenv("NBG_SP_BATCH_ALLOC") ? atoi(getenv("NBG_SP_BATCH_ALLOC")) : 1;
   const unsigned grid_env = getenv("NBG_SP_BATCH_GRID") ? (unsigned)atoi(getenv("NBG_SP_BATCH_GRID")) : 512u;
-  const unsigned walk_env = getenv("NBG_SP_WALK_ITEMS") ? (unsigned)atoi(getenv("NBG_SP_WALK_ITEMS")) : 2048u;
+  const unsigned walk_env = getenv("NBG_SP_WALK_ITEMS") ? (unsigned)atoi(getenv("NBG_SP_WALK_ITEMS")) : 16384u;
   b.alloc = alloc_env ? 1u : 0u;
   b.walk_items = walk_env;
   const unsigned grid = b.alloc ? std::max<unsigned>(grid_env, (unsigned)n) : (unsigned)n * b.per;

@@ -173,6 +173,7 @@ struct Workspace {
   unsigned long long* ar_buf = nullptr;     // ws_allreduce_host scratch (grow-only)
   uint64_t ar_cap = 0;
   bool hop_bits = false;                    // this hop's MARKs set sendbits directly (no pack)
+  uint64_t hop_slots = 0;                   // this hop sends slot arrays of this stride (0: bitmaps)
   uint64_t* fetch_meta = nullptr;           // ws_fetch_rows staging (grow-only)
   size_t fetch_meta_cap = 0;
   int64_t* fetch_out = nullptr;

@@ -83,6 +83,38 @@ def test_go_matches_single_and_oracle(rmat14, steps, where):
             assert got == graphs.sorted_rows(orc.go([r], [1], steps, wb, yb))
 
 
+def test_go_first_hop_slot_exchange(rmat14, monkeypatch):
+    """A small first hop (its per-owner edge bound from the degrees every rank holds) is exchanged
+    as slot arrays of local ids instead of npad-bit bitmap segments: the rows equal the bitmap
+    exchange's (NBG_GO_SLOTS=0) and the single engine's, for single roots (slots), a start list
+    with hubs whose bound passes the threshold (bitmaps) and duplicated starts; and a single root's
+    first hop moves (G - 1) x 4 x stride bytes per rank instead of (G - 1) x npad / 8."""
+    src, dst, w, single, orc, c = rmat14
+    wb = WHERE.encode()
+    yb = [y.encode() for y in YIELDS]
+
+    def run(starts, steps, slots):
+        monkeypatch.setenv("NBG_GO_SLOTS", slots)
+        c.each(lambda e: e.profile(True))
+        rows = graphs.sorted_rows(c.go(starts, [1], steps, wb, yb))
+        prof = c.each(lambda e: e.profile_read())
+        c.each(lambda e: e.profile(False))
+        return rows, prof[0].get("alltoall(xGMI)", {}).get("algo_bytes", 0)
+
+    small = graphs.roots(src, 6, seed=5)
+    cases = [[r] for r in small] + [graphs.roots(src, 200, seed=6), small + small[:2] + [987654321]]
+    fewer = 0
+    for starts in cases:
+        for steps in (2, 3):
+            ref = graphs.sorted_rows(single.go(starts, [1], steps, wb, yb))
+            bits, bb = run(starts, steps, "0")
+            slots, sb = run(starts, steps, "1")
+            assert slots == bits == ref, (starts[:3], steps)
+            assert sb <= bb
+            fewer += sb < bb
+    assert fewer >= 6   # (the single roots: their first hop is a slot exchange)
+
+
 def test_go_multi_start_duplicates_and_unknown(rmat14):
     src, dst, w, single, orc, c = rmat14
     rs = graphs.roots(src, 12, seed=9)
