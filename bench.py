@@ -39,7 +39,7 @@ T_START = time.time()
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 METRIC = "GO 3 STEPS traversed edges/sec (TEPS) at 1/2/4/8 GPU; FIND SHORTEST PATH p50"
 # HBM traffic per launch from the committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
-# bench's default workload (tools/gpu_r02.sh pmc -> tools/pmc_summary.py; FETCH_SIZE doubled per
+# bench's default workload (tools/gpu_steps.sh pmc26 / pmc22 -> tools/pmc_summary.py; FETCH_SIZE doubled per
 # the gfx950 note), keyed by workload
 PMC_FILES = {("RMAT-26", 16): os.path.join(ROOT, "profiles", "r05_finb_pmc_hbm_rmat26.json"),
              ("RMAT-22", 64): os.path.join(ROOT, "profiles", "r02_pmc_hbm_rmat22.json")}

@@ -176,12 +176,6 @@ int32_t greedy_path(PathCtx& c, const PathGreedy& g, std::vector<int64_t>* path)
   return NBG_OK;
 }
 
-// NBG_PART_FWD_BSETS (partitioned): true B-sets past kf before the greedy (see bidirectional)
-bool fwd_bsets_on() {
-  static const bool on = getenv("NBG_PART_FWD_BSETS") && atoi(getenv("NBG_PART_FWD_BSETS")) != 0;
-  return on;
-}
-
 // s, t: local ids (NO_ROW on a rank that does not own them); partitioned: s_gid / s_vid = the
 // source's global id and vid on every rank (the greedy's v0 without an exchange), deg = deg(s),
 // deg(t) over ranks when known (null: a set-up exchange)
@@ -270,7 +264,6 @@ int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_pat
     }
     if (c.part) {   // the first B-set steps' bounds (backward, and forward past kf)
       T(ws_path_meet_degsum(ws, S_MEET, c.bwd));
-      if (fwd_bsets_on()) T(ws_path_meet_degsum(ws, S_MEET, c.fwd, true));
     }
     mark(forward ? "fwd_enq" : "bwd_enq");
     T(sync(c, &ps));
@@ -296,36 +289,9 @@ int32_t bidirectional(PathCtx& c, uint32_t s, uint32_t t, uint32_t upto, nbg_pat
     int slot = S_MEET;
     T(bsets(c, S_MEET, ps.n[S_MEET], kf, 1, ef, em, 0, fn, &slot, c.part ? ps.mdsum : 0));
   }
-  int gkf = kf;
-  // NBG_PART_FWD_BSETS=1 (partitioned, off by default): the positions past kf get true B-sets
-  // too, forward from the meet set over out-edges (B[i] = out-neighbours of B[i-1] at backward
-  // level L - i), and B[L] = {t}; the greedy then tests LAB_M at every position and scans the
-  // in-edge rows of path vertices only instead of whole backward BFS levels.  It costs a bitmap
-  // all-to-all per position past kf + 1; on the same-device rehearsal that outweighed the scans
-  // it saves (RMAT-20 p50 0.99 -> 1.21 ms, RMAT-26 2.01 -> 2.03 ms, profiles/r02_mm_*).
-  if (c.part && fwd_bsets_on() && kb >= 1 && he == hipSuccess) {
-    int cur = S_MEET;
-    uint64_t nb = ps.n[S_MEET];
-    for (int i = kf + 1; i < L && he == hipSuccess; ++i) {
-      PathLevel lv;
-      const bool first = i == kf + 1 && ps.mdsum_out;
-      lv.global_bound = first;   // the meet list's out-degree sum over every rank
-      lv.lab = LAB_M;
-      lv.stamp = stamp(em, (uint32_t)i);
-      lv.rlab = LAB_B;
-      lv.rstamp = stamp(eb, (uint32_t)(L - i));
-      const int dst = cur == S_F0 ? S_F0 + 1 : S_F0;
-      he = level(c, c.fwd, cur, nb, first ? ps.mdsum_out : c.bwd_edges, dst, lv);
-      cur = dst;
-      nb = (size_t)(L - i) < bn.size() ? bn[L - i] : c.E.snap.nv;
-    }
-    T(upload1(ws, S_B0, t));
-    T(ws_path_stamp(ws, S_B0, 1, LAB_M, stamp(em, (uint32_t)L)));
-    gkf = L;
-  }
   if (he != hipSuccess) return dev_fail(c.E, he, "path B-sets");
   mark("bsets_enq");
-  PathGreedy g{L, gkf, em, eb, start_slot};
+  PathGreedy g{L, kf, em, eb, start_slot};
   g.v0_gid = s_gid;   // B[0] = {s}
   g.v0_vid = s_vid;
   std::vector<int64_t> p;

@@ -115,8 +115,7 @@ struct ChState {        // device; the host reads what the result launch derives
   // the step launches that find the search over (hop_first) and then the k_ch_hop launches.
   unsigned long long hstart[2 * CH_MAXS + 2];
   // step launch i starts at step first[i] (a BFS level or B-set step; first[0] = 0) and writes
-  // first[i + 1]: one step, several (a workgroup alone runs small steps back to back, ChQ::solo)
-  // or none (the search is over)
+  // first[i + 1]: one step, or none (the search is over)
   unsigned long long first[CH_MAXS + 1];
   ChSnap snap[CH_MAXS];
   long long path[1 + 3 * MAX_PATH_LEN];
@@ -128,8 +127,10 @@ struct ChState {        // device; the host reads what the result launch derives
   unsigned long long hjob, hjob_rng;
   unsigned long long htag[CH_HOP_WGS];
   unsigned long long hpart[4 * CH_HOP_WGS];
-  // the batch tag (ChQ::tag) of the launch in which this query's walk ended (or found nothing to
-  // walk): a batched chain's later launches give the pair one workgroup (ch_batch_work)
+  // (ChQ::tag << 32 | launch index) of the launch in which this query's walk ended (or found nothing
+  // to walk): a batched chain's LATER launches give the pair one workgroup (ch_batch_work).  Written
+  // inside a launch, so the launch that writes it must not act on it (its workgroups start at
+  // different times and must all derive the same split)
   unsigned long long walk_end;
 };
 
@@ -165,8 +166,6 @@ struct ChArgs {         // device memory (indexed at run time: never a by-value 
 struct ChQ {
   uint32_t s, t, upto;
   uint32_t ef, eb, em;
-  uint32_t solo;                       // a step over at most this many items (entries + edges) is run
-                                       // by workgroup 0 alone, which goes on with the next step (0: off)
   uint32_t par;                        // the query's counter set (ChState::c)
   uint32_t tag;                        // this batch of launches (ChOut::tag: which batch stored)
   uint32_t both_items;                 // a BFS level expands both sides when each has at most this many
@@ -842,17 +841,16 @@ __device__ __forceinline__ uint64_t step_items(const ChSnap& P) {
   return (c >> 32) + (c & 0xFFFFFFFFull);
 }
 
-// Step launch i: from step first[i], one step over the whole grid, or — for a step of at most
-// q.solo items — steps run by workgroup 0 alone, back to back, until the search is over or a step
-// needs the grid (the launch boundary then orders it after this workgroup's writes).
-// Returns false when the search was over before this launch (the launch is then a greedy one).
+// Step launch i: step first[i] (= i while the search is on) over the whole grid.  (Round 4's solo
+// steps — small steps run back to back by workgroup 0 — measured neutral and were removed in
+// round 6.)  Returns false when the search was over before this launch (a greedy launch then).
 template <int NW, int VT>
 __device__ __forceinline__ bool ch_step(const ChArgs& A, const ChQ& q, int i, uint32_t bid, uint32_t nblk) {
   ChState* st = A.st;
   ChCtr& C = st->c[q.par];
   // launch i runs step i while the search is on (first[i] == i, one step per launch): that
   // snapshot's loads are issued with first[i]'s, not after it (one memory round trip, not two,
-  // before the level starts); a launch past the search, or after solo steps, reloads
+  // before the level starts); a launch past the search reloads
   uint32_t j = 0;
   ChFirst f0{};
   ChSnap P;
@@ -875,28 +873,12 @@ __device__ __forceinline__ bool ch_step(const ChArgs& A, const ChQ& q, int i, ui
     if (lead) st->first[i + 1] = j;
     return false;
   }
-  const bool solo = step_items(P) <= q.solo;
-  if (solo && bid != 0) return true;
-  if (lead) C.busy += 1;
-  for (;;) {   // (one call site of ch_level: the grid's step and the solo steps share its registers)
-    if (lead) {
-      if (j > 0) st->snap[j] = P;   // (step j + 1 derives its snapshot from it; snap[0]: first_store)
-      if (!solo) st->first[i + 1] = j + 1;
-    }
-    ch_level<NW, VT>(A, q, P, (int)j, solo ? 0u : bid, solo ? 1u : nblk, j == 0, f0);
-    if (!solo) return true;
-    // this workgroup's stores and atomics before the next step's reads (labels, lists, counters;
-    // the acquire drops L1 lines read before another wave's claims); the snapshot is read back
-    // rather than kept in registers across the step
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    P = ch_advance(st->snap[j], ld_agent(&C.lacc[j]), ld_agent(&C.lmeet[j]), ld_agent(&C.macc),
-                   ld_agent(&C.err), q.upto, ld_agent(&C.lacc2[j]), ld_agent(&C.lmeet2[j]), q.both_items);
-    ++j;
-    if (P.phase == PH_DONE || step_items(P) > q.solo || j + 1 >= (uint32_t)CH_MAXS) break;
+  if (lead) {
+    C.busy += 1;
+    if (j > 0) st->snap[j] = P;   // (step j + 1 derives its snapshot from it; snap[0]: first_store)
+    st->first[i + 1] = j + 1;
   }
-  if (lead) st->first[i + 1] = j;
+  ch_level<NW, VT>(A, q, P, (int)j, bid, nblk, j == 0, f0);
   return true;
 }
 
@@ -1037,7 +1019,7 @@ __device__ __forceinline__ bool ch_hop(const ChArgs& A, const ChQ& q, int nl, in
   uint32_t pos = (uint32_t)(H >> 32), c = (uint32_t)H;
   auto finish = [&](uint32_t p, uint32_t v) {   // (thread 0 of the one writer)
     st->hstart[h + 1] = ((unsigned long long)p << 32) | v;
-    if (v == NO_ROW || !F.met || F.err || p >= F.L) st->walk_end = q.tag;
+    if (v == NO_ROW || !F.met || F.err || p >= F.L) st->walk_end = ((unsigned long long)q.tag << 32) | (uint32_t)nl;
   };
   if (!F.met || F.phase != PH_DONE || F.err || pos >= F.L || c == NO_ROW) {
     if (bid == 0 && threadIdx.x == 0) finish(pos, c);
@@ -1328,7 +1310,7 @@ __device__ __forceinline__ unsigned long long ch_batch_work(const ChBatch& b, in
   const unsigned long long j = ld_agent(&st->first[i]);
   const unsigned long long we = ld_agent(&st->walk_end);
   const ChSnap P = snap_for(st, b.q[p], i);
-  if (we == (unsigned long long)b.q[p].tag) return 0;   // its walk is over: one workgroup, which returns
+  if ((we >> 32) == b.q[p].tag && (uint32_t)we < (uint32_t)i) return 0;   // walk over before launch i
   if (j != (unsigned long long)i || P.phase == PH_DONE) return b.walk_items;
   return step_items(P) + 1;
 }
@@ -1396,7 +1378,6 @@ struct ChainCtx {
   // 0.109-0.113 at 128 (profiles/r03_vt3_sp_grid_ab.txt, r03_fin2_sp_vt2_batch_ab.txt).
   // NBG_SP_GRID overrides.
   unsigned grid = 256;
-  uint32_t solo = 0;               // ChQ::solo (NBG_SP_SOLO items)
   uint32_t both = 16384;           // ChQ::both_items (NBG_SP_BOTH; 0: one side per level)
   // the query in flight: what has been enqueued
   ChQ q{};
@@ -1453,8 +1434,6 @@ ChainCtx* chain_create(uint64_t nv, uint64_t edge_cap, hipStream_t s, std::strin
   c->tsplit_cap = (nv + 1 + edge_cap) / CH_TILE_MIN + 2;
   const char* g = getenv("NBG_SP_GRID");
   if (g && atoi(g) > 0) c->grid = (unsigned)atoi(g);
-  const char* so = getenv("NBG_SP_SOLO");
-  if (so) c->solo = (uint32_t)strtoul(so, nullptr, 10);
   const char* bo = getenv("NBG_SP_BOTH");
   if (bo) c->both = (uint32_t)strtoul(bo, nullptr, 10);
   hipError_t he = hipSuccess;
@@ -1557,7 +1536,7 @@ static hipError_t chain_prepare(ChainCtx* c, const SpTypes& fwd, const SpTypes& 
   // (NBG_SP_JOB_WAIT, read per query: a test sets 0 so that every hub job goes unanswered and the
   // fallback — the next launch's spread scan — runs)
   const char* jw = getenv("NBG_SP_JOB_WAIT");
-  c->q = ChQ{s, t, upto, epoch, epoch, epoch, c->solo, c->par, 0, c->both,
+  c->q = ChQ{s, t, upto, epoch, epoch, epoch, c->par, 0, c->both,
              jw ? (uint32_t)strtoul(jw, nullptr, 10) : CH_JOB_WAIT};
   c->steps = c->hops = 0;
   c->last_batched = false;

@@ -1,5 +1,7 @@
 #!/bin/bash
-# Round-5 GPU-box steps (from the repo root, via gpurun): bash tools/gpu_r05.sh <tag> <step>...
+# Named GPU-box steps (from the repo root, via gpurun): bash tools/gpu_steps.sh <tag> <step>...
+# (The one-off round scripts of rounds 1-5 are folded into these steps; tools/gpu_run.sh runs
+# ad-hoc '<name>|<seconds>|<command>' steps the same way.)
 #   tests  — pytest -m gpu;  load26 — RMAT-26 generate + load + GO leg only (load time);
 #   bench  — default bench.py
 set -u
@@ -111,10 +113,9 @@ for step in "$@"; do
     kpad)   # SHORTEST chain length A/B: one launch fewer / more than the sized chain
       timeout -k 10 1000 bash tools/sp_ab.sh "$TAG/kpad" nebula_amd/libnbg.so nebula_amd/libnbg.so,NBG_SP_KPAD=-1 \
         nebula_amd/libnbg.so,NBG_SP_KPAD=1 > "$OUT/kpad.txt" 2>&1 || { tail -30 "$OUT/kpad.txt"; exit 1; } ;;
-    spgrid)   # SHORTEST step-grid / solo-step A/B after the round-4 chain changes
+    spgrid)   # SHORTEST step-grid A/B
       timeout -k 10 1100 bash tools/sp_ab.sh "$TAG/spgrid" nebula_amd/libnbg.so nebula_amd/libnbg.so,NBG_SP_GRID=128 \
-        nebula_amd/libnbg.so,NBG_SP_GRID=512 nebula_amd/libnbg.so,NBG_SP_SOLO=1024 > "$OUT/spgrid.txt" 2>&1 \
-        || { tail -30 "$OUT/spgrid.txt"; exit 1; } ;;
+        nebula_amd/libnbg.so,NBG_SP_GRID=512 > "$OUT/spgrid.txt" 2>&1 || { tail -30 "$OUT/spgrid.txt"; exit 1; } ;;
     small)   # the small-request legs (C1 nba, getBound) with the getBound phase trace
       NBG_GN_TRACE=1 timeout -k 10 400 python -u bench.py --scale 16 --roots 4 --steps 1 --warmup 1 --sp-pairs 0 \
         --c2 0 --c5-scale 0 --c1-reqs 3000 --getbound-reqs 2000 --verify 0 --no-profile \

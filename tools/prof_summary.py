@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise a rocprofv3 kernel trace of bench.py (tools/gpu_r02.sh prof26) for profiles/: per
+"""Summarise a rocprofv3 kernel trace of bench.py (tools/gpu_steps.sh prof26) for profiles/: per
 kernel the launch count and mean duration over all launches and over the launches that overlap
 no other kernel (queries run 6 in flight, so overlapping launches read longer), plus the FIND
 SHORTEST PATH level-loop kernels against the SP leg's edge count.
