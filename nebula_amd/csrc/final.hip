@@ -65,6 +65,19 @@ k_final_dst(FinalDstArgs a) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   unsigned long long* const sMask = sMaskAll[w];
   uint32_t* const sDelta = sDeltaAll[w];
+  const uint64_t g = (uint64_t)gridDim.x * FW;
+  uint64_t t = (uint64_t)blockIdx.x * FW + w;   // adjacent tiles in one workgroup (shared lines)
+  // merge-path split of tile tt: entries consumed before its start (which 0) / its end (which 1).
+  // A tile's split is wave-uniform: read through the scalar cache (address space 4), so its wait
+  // is on lgkmcnt and never on the vector memory counter that the row stores share
+  const __attribute__((address_space(4))) uint32_t* const tsplit =
+      (const __attribute__((address_space(4))) uint32_t*)a.tsplit;
+  // the splits of this wave's first two tiles are loaded with the list's size, not after it (one
+  // memory round trip less before the stream starts; the size then says which of them are used)
+  const uint64_t tmax = a.tsplit_n ? a.tsplit_n - 1 : 0;
+  auto clampt = [&](uint64_t x) { return x < tmax ? x : tmax; };
+  const uint32_t sp0 = tsplit[clampt(t)], sp1 = tsplit[clampt(t + 1)];
+  const uint32_t sq0 = tsplit[clampt(t + g)], sq1 = tsplit[clampt(t + g + 1)];
   const unsigned long long packed = *a.acc;   // (list entries << 32 | edges)
   const uint64_t n = packed >> 32, total = packed & 0xFFFFFFFFull;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -75,12 +88,6 @@ k_final_dst(FinalDstArgs a) {
   __syncthreads();
   const uint64_t npath = n + total;
   const uint64_t ntiles = (npath + TILE - 1) / TILE;
-  const uint64_t g = (uint64_t)gridDim.x * FW;
-  // merge-path split of tile tt: entries consumed before its start (which 0) / its end (which 1).
-  // A tile's split is wave-uniform: read through the scalar cache (address space 4), so its wait
-  // is on lgkmcnt and never on the vector memory counter that the row stores share
-  const __attribute__((address_space(4))) uint32_t* const tsplit =
-      (const __attribute__((address_space(4))) uint32_t*)a.tsplit;
   auto split_of = [&](uint64_t tt, int which) -> uint64_t {
     if (which == 0) return tsplit[tt];
     return (tt + 1) * TILE >= npath ? n : tsplit[tt + 1];
@@ -145,15 +152,14 @@ k_final_dst(FinalDstArgs a) {
   uint64_t preg = 0;
 #pragma unroll
   for (int i = 0; i < FV; ++i) pdv[i] = 0;
-  uint64_t t = (uint64_t)blockIdx.x * FW + w;   // adjacent tiles in one workgroup (shared lines)
   uint64_t a0 = 0, a1 = 0, n0 = 0, n1 = 0;   // splits of tiles t and t + g
   uint32_t e_pre = 0, f_pre = 0, r_pre = 0;   // lane's window entry of tile t
   if (t < ntiles) {
-    a0 = split_of(t, 0);
-    a1 = split_of(t, 1);
+    a0 = sp0;
+    a1 = (t + 1) * TILE >= npath ? n : sp1;
     if (t + g < ntiles) {
-      n0 = split_of(t + g, 0);
-      n1 = split_of(t + g, 1);
+      n0 = sq0;
+      n1 = (t + g + 1) * TILE >= npath ? n : sq1;
     }
     stage(a0, &e_pre, &f_pre, &r_pre);
   }

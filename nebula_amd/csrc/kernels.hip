@@ -2872,6 +2872,7 @@ hipError_t ws_expand_final(Workspace* w, const ExpandArgs& a0, uint64_t n_bound,
     fa.seg_end = l_end;
     fa.seg_rs = l_rs;
     fa.tsplit = a.tsplit;
+    fa.tsplit_n = w->cap_tiles;
     fa.dst_vid = a.dst_vid;
     fa.wcol = fp.fast.wcol;
     fa.lo = fp.fast.lo;

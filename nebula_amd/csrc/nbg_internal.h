@@ -386,6 +386,7 @@ struct FinalDstArgs {
   const uint32_t* seg_end;
   const uint32_t* seg_rs;
   const uint32_t* tsplit;
+  uint64_t tsplit_n;               // entries tsplit holds (the first splits are read before the list's size)
   const int64_t* dst_vid;
   const void* wcol;
   int64_t lo, hi;                  // pass = (lo <= w && w <= hi) != where_neg
