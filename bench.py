@@ -297,7 +297,8 @@ def shortest_path_leg(eng, pairs, args, barrier, batch=True, light=False):
     import ctypes as C
     arr, nreq, keep = eng.path_batch_prepare([([s], [t], [1], args.sp_upto, True) for s, t in pairs])
     lib, h = eng.lib, eng.h
-    outs = (C.c_void_p * max(1, nreq))()   # every pass's results are kept for the verification
+    out = C.c_void_p()
+    outs = []   # every pass's results are kept for the verification
     barrier()
     lat, edges, found, hops = [], 0, 0, 0
     tick = Progress("SP latency pass", nreq)
@@ -305,14 +306,15 @@ def shortest_path_leg(eng, pairs, args, barrier, batch=True, light=False):
     for i in range(nreq):
         tick(i)
         q0 = time.perf_counter()
-        rc = lib.nbg_find_path(h, C.byref(arr[i]), C.byref(outs, i * C.sizeof(C.c_void_p)))
+        rc = lib.nbg_find_path(h, C.byref(arr[i]), C.byref(out))
         lat.append(time.perf_counter() - q0)
         if rc:
             raise RuntimeError(f"nbg_find_path failed: {rc}")
-        edges += int(lib.nbg_paths_edges_scanned(outs[i]))
-        if lib.nbg_paths_count(outs[i]):
+        outs.append(out.value)
+        edges += int(lib.nbg_paths_edges_scanned(out))
+        if lib.nbg_paths_count(out):
             found += 1
-            hops += (lib.nbg_path_len(outs[i], 0) - 1) // 3
+            hops += (lib.nbg_path_len(out, 0) - 1) // 3
     barrier()
     elapsed = time.perf_counter() - t0
     got = {"latency": [eng._paths(C.c_void_p(outs[i]), None) for i in range(nreq)]}

@@ -477,7 +477,7 @@ void sp_destroy(SpCtx* c);
 // enqueue the search for s -> t (local dense ids, s != t): the device-driven level loop
 // (spchain.hip, one OVER type per direction), its result stored into mapped host memory
 hipError_t sp_launch(SpCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible, const int64_t* vids,
-                     uint32_t s, uint32_t t, uint32_t upto);
+                     uint32_t s, uint32_t t, uint32_t upto, uint64_t dmin = 0);
 bool sp_ready(SpCtx* c);
 struct SpPair {                 // one query of sp_launch_batch
   const SpTypes* fwd;
@@ -492,7 +492,7 @@ ChainCtx* chain_create(uint64_t nv, uint64_t edge_cap, hipStream_t s, std::strin
 void chain_destroy(ChainCtx* c);
 hipError_t chain_launch(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible,
                         const int64_t* vids, uint32_t* const lab[3], uint32_t epoch, uint32_t s, uint32_t t,
-                        uint32_t upto);
+                        uint32_t upto, uint64_t dmin = 0);
 bool chain_more(ChainCtx* c, hipError_t* he);   // false: a continuation batch was enqueued
 bool chain_woken(const ChainCtx* c);   // the current batch's last launch has stored the result
 // one query of a batched chain (spchain.hip, chain_launch_batch)

@@ -325,8 +325,10 @@ int32_t device_pair(PathCtx& c, int mode, uint32_t s, uint32_t t, uint32_t upto,
     E.sp = E.new_sp(E.stream, &err);
     if (!E.sp) return E.fail(NBG_E_OUT_OF_MEMORY, err);
   }
-  if (!host_degree(c, c.fwd, s) || !host_degree(c, c.bwd, t)) return NBG_OK;   // an endpoint without edges
-  hipError_t he = sp_launch(E.sp, sp_types(c.E, c.fwd), sp_types(c.E, c.bwd), E.snap.d_visible, E.snap.d_vids, s, t, upto);
+  const uint64_t ds = host_degree(c, c.fwd, s), dt = host_degree(c, c.bwd, t);
+  if (!ds || !dt) return NBG_OK;   // an endpoint without edges
+  hipError_t he = sp_launch(E.sp, sp_types(c.E, c.fwd), sp_types(c.E, c.bwd), E.snap.d_visible, E.snap.d_vids, s, t, upto,
+                            std::min(ds, dt));
   SpResult r;
   if (he == hipSuccess) he = sp_wait(E.sp, &r);
   if (he != hipSuccess) return dev_fail(E, he, "shortest path");
@@ -476,6 +478,7 @@ struct PairLaunch {
   int mode = SP_CHAIN;
   SpTypes fwd, bwd;
   uint32_t s = NO_ROW, t = NO_ROW, upto = 0;
+  uint64_t dmin = 0;   // min(out-degree of s, in-degree of t): the chain's length hint (sp_launch)
 };
 constexpr int32_t PAIR_DEFERRED = 1;
 
@@ -688,7 +691,9 @@ int32_t find_path_locked(Engine& E, const nbg_path_request* rq, nbg_paths** out,
   const int pmode = pair && !c.part ? sp_mode(c) : PM_HOST;
   if (pmode != PM_HOST) {
     const uint32_t s0 = S.empty() ? NO_ROW : S[0];
-    if (pl && host_degree(c, c.fwd, s0) && host_degree(c, c.bwd, Tg[0])) {
+    const uint64_t ds0 = host_degree(c, c.fwd, s0), dt0 = host_degree(c, c.bwd, Tg[0]);
+    if (pl && ds0 && dt0) {
+      pl->dmin = std::min(ds0, dt0);
       pl->mode = pmode;
       pl->fwd = sp_types(c.E, c.fwd);
       pl->bwd = sp_types(c.E, c.bwd);
@@ -868,7 +873,7 @@ int32_t nbg_find_path_submit(nbg_engine* h, const nbg_path_request* rq, nbg_path
     ps.sp = E.new_sp(ps.stream, &err);
     if (!ps.sp) { delete t; return E.fail(NBG_E_OUT_OF_MEMORY, err); }
   }
-  hipError_t he = sp_launch(ps.sp, pl.fwd, pl.bwd, E.snap.d_visible, E.snap.d_vids, pl.s, pl.t, pl.upto);
+  hipError_t he = sp_launch(ps.sp, pl.fwd, pl.bwd, E.snap.d_visible, E.snap.d_vids, pl.s, pl.t, pl.upto, pl.dmin);
   if (he != hipSuccess) { delete t; return dev_fail(E, he, "shortest path"); }
   t->slot = slot;
   ps.ticket = t;
@@ -910,7 +915,7 @@ int32_t nbg_find_path_batch(nbg_engine* h, const nbg_path_request* reqs, uint64_
         }
       }
       SpResult r;
-      hipError_t he = sp_launch(E.sp, x.fwd, x.bwd, E.snap.d_visible, E.snap.d_vids, x.s, x.t, x.upto);
+      hipError_t he = sp_launch(E.sp, x.fwd, x.bwd, E.snap.d_visible, E.snap.d_vids, x.s, x.t, x.upto, x.dmin);
       if (he == hipSuccess) he = sp_wait(E.sp, &r);
       delete res;
       if (he != hipSuccess) {

@@ -94,11 +94,11 @@ static hipError_t next_epoch(SpCtx* c) {
 }
 
 hipError_t sp_launch(SpCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible, const int64_t* vids,
-                     uint32_t s, uint32_t t, uint32_t upto) {
+                     uint32_t s, uint32_t t, uint32_t upto, uint64_t dmin) {
   if (upto > MAX_PATH_LEN || s == NO_ROW || t == NO_ROW) return hipErrorInvalidValue;
   HIP_TRY_SP(next_epoch(c));
   HIP_TRY_SP(sp_reserve_chain(c));
-  HIP_TRY_SP(chain_launch(c->chain, fwd, bwd, visible, vids, c->lab, c->epoch, s, t, upto));
+  HIP_TRY_SP(chain_launch(c->chain, fwd, bwd, visible, vids, c->lab, c->epoch, s, t, upto, dmin));
   return hipEventRecord(c->done, c->stream);
 }
 

@@ -1565,11 +1565,18 @@ static int chain_length(const ChainCtx* c) {
   return std::min(chain_max(c), std::max(2, (int)std::ceil(c->ema_launches) + kpad));
 }
 
+// dmin: min(out-degree of s, in-degree of t) when the caller knows it.  An endpoint of degree 1
+// (a third of the RMAT-26 bench pairs) leaves its side a one-vertex frontier per level, so those
+// searches run longer: 6.5 % of them needed a continuation (a host round trip) against 0.4 % for
+// degree 2-3 and none above (tools/sp_tail_probe.py, profiles/r06_d_sp_tail.txt); their chains
+// get NBG_SP_LOWDEG_PAD (1) more launches.
 hipError_t chain_launch(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible,
                         const int64_t* vids, uint32_t* const lab[3], uint32_t epoch, uint32_t s, uint32_t t,
-                        uint32_t upto) {
+                        uint32_t upto, uint64_t dmin) {
   HIP_TRY_CH(chain_prepare(c, fwd, bwd, visible, vids, lab, epoch, s, t, upto));
-  return chain_batch(c, chain_length(c), 0);
+  const char* lp = getenv("NBG_SP_LOWDEG_PAD");
+  const int pad = dmin == 1 ? (lp ? atoi(lp) : 1) : 0;
+  return chain_batch(c, std::min(chain_max(c), chain_length(c) + pad), 0);
 }
 
 // n <= CH_BMAX queries (contexts on one stream) in one chain of batched launches; each context
