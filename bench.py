@@ -271,6 +271,31 @@ def host_delivered(stmt, roots):
     return out
 
 
+class Heartbeat:
+    """A log line every `every` seconds while a block runs (long CPU oracle calls print nothing
+    themselves, and runs are watched for silence)."""
+
+    def __init__(self, what, every=30.0):
+        import threading
+        self.what, self.every = what, every
+        self.stop = threading.Event()
+        self.th = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        t0 = time.perf_counter()
+        while not self.stop.wait(self.every):
+            log(f"{self.what}: still running after {time.perf_counter() - t0:.0f}s")
+
+    def __enter__(self):
+        self.th.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        self.th.join()
+        return False
+
+
 class Progress:
     """A log line every `every` seconds of a long loop (runs are watched for silence)."""
 
@@ -692,7 +717,8 @@ def main():
                 match = list(exp) == d[:3] and scanned == d[3]
                 ok = ok and match
                 checked.append({"root": r, "rows": d[0], "match": match})
-            sp_check = verify_shortest(csr, pairs, sp_paths, args.sp_upto)
+            with Heartbeat("SHORTEST verification"):
+                sp_check = verify_shortest(csr, pairs, sp_paths, args.sp_upto)
             verify = {"go_roots_checked": len(checked), "go_match": ok, "shortest": sp_check,
                       "sp_pairs_checked": min((v["checked"] for v in sp_check["passes"].values()), default=0),
                       "sp_match": sp_check["match"], "sp_found": sp_check["found"],
@@ -700,9 +726,11 @@ def main():
                                 "and edges scanned vs oracle/csr.cpp on the same graph; SHORTEST: every timed pass's "
                                 "own results, entry by entry, vs orc_csr_shortest_many",
                       "oracle_build_s": round(build_s, 1)}
-            part_load = partition_load(csr, roots, args)
+            with Heartbeat("partition load model"):
+                part_load = partition_load(csr, roots, args)
             if not args.no_cpu_baseline and world == 1:
-                cpu_csr = csr_baseline(csr, roots, pairs, args, threads, model, ncpu)
+                with Heartbeat("CSR cpu baseline"):
+                    cpu_csr = csr_baseline(csr, roots, pairs, args, threads, model, ncpu)
             csr.close()
         except Exception as ex:  # pragma: no cover
             log(f"verification / CSR baseline unavailable: {ex}")
@@ -1254,51 +1282,58 @@ def c5_leg(args, barrier, threads, model, ncpu):
                                         "(2^28 partial walks) is counted in over_walk_cap, not in the latencies"}}
     # ---- the CSR oracle (two types): verification and the leg's cpu_baseline
     try:
-        from tests.support.oracle import CsrOracle
-        c0 = time.time()
-        ck, cl = CsrOracle(ks, kd, kw, threads=threads), CsrOracle(ls, ld, lw, threads=threads)
-        log(f"C5 CSR oracles built in {time.time() - c0:.1f}s")
-        go_ok, cpu_runs = True, []
-        for run in range(3):
-            secs = scanned = 0.0
-            for r, (dg, sc) in zip(roots, dig):
-                d_, s_, sec = CsrOracle.go_multi([ck, cl], [r], 4, seconds=True)
-                if run == 0:
-                    go_ok = go_ok and d_ == dg and s_ == sc
-                secs += sec
-                scanned += s_
-            cpu_runs.append((scanned / secs if secs else 0.0, secs))
-            if secs > 15:   # (bounded sample: one run is enough past 15 s)
-                break
-        cpu_runs.sort()
-        teps, secs = cpu_runs[len(cpu_runs) // 2]
-        counts_ok, lists_ok, listed = True, True, 0
-        for i, ((s_, t_), p) in enumerate(zip(pairs, per)):
-            n = sum(ck.walk_counts(s_, t_, 4)[1:])
-            counts_ok = counts_ok and (n == p[0] if p[0] is not None else n > 0)
-            if i in kept:
-                walks = ck.all_walks(s_, t_, 4, cap=20000)
-                exp = sorted([w[0]] + [x for v in w[1:] for x in (1, 0, v)] for w in walks)
-                lists_ok = lists_ok and kept[i] == exp
-                listed += 1
-        out_["verification"] = {"go_roots_checked": len(roots), "go_match": go_ok,
-                                "all_path_pairs_counted": len(pairs), "all_path_counts_match": counts_ok,
-                                "all_path_pairs_listed": listed, "all_path_lists_match": lists_ok,
-                                "method": "device nbg_rows_digest + edges scanned vs oracle/csr.cpp go_multi (two "
-                                          "CSRs); ALL PATH counts vs the walk-count DP, entry lists vs the oracle's "
-                                          "walk enumeration for the first 16 pairs with <= 20 k paths"}
-        out_["go4"]["cpu_baseline"] = {"value": teps, "unit": "TEPS", "cores": threads, "kind": "port",
-                                       "mode": "csr_openmp",
-                                       "sample": f"all {len(roots)} roots, GO 4 STEPS OVER knows, likes, median of "
-                                                 f"{len(cpu_runs)} run(s) ({secs:.2f}s per run); oracle/csr.cpp "
-                                                 f"go_multi, {threads} threads",
-                                       "model": model, "host_cpus": ncpu}
-        log(f"C5 verification {out_['verification']}")
-        ck.close()
-        cl.close()
+        with Heartbeat("C5 oracle phase"):
+            _c5_oracle(out_, ks, kd, kw, ls, ld, lw, roots, dig, pairs, per, kept, threads, model, ncpu)
     except Exception as ex:  # pragma: no cover
         log(f"C5 verification / CPU baseline unavailable: {ex}")
     return out_
+
+
+def _c5_oracle(out_, ks, kd, kw, ls, ld, lw, roots, dig, pairs, per, kept, threads, model, ncpu):
+    """C5's CSR oracle phase: verification of the device results and the GO leg's cpu_baseline."""
+    from tests.support.oracle import CsrOracle
+    c0 = time.time()
+    ck, cl = CsrOracle(ks, kd, kw, threads=threads), CsrOracle(ls, ld, lw, threads=threads)
+    log(f"C5 CSR oracles built in {time.time() - c0:.1f}s")
+    go_ok, cpu_runs = True, []
+    for run in range(3):
+        secs = scanned = 0.0
+        for r, (dg, sc) in zip(roots, dig):
+            d_, s_, sec = CsrOracle.go_multi([ck, cl], [r], 4, seconds=True)
+            if run == 0:
+                go_ok = go_ok and d_ == dg and s_ == sc
+            secs += sec
+            scanned += s_
+        cpu_runs.append((scanned / secs if secs else 0.0, secs))
+        log(f"C5 oracle GO run {run}: {secs:.1f}s")
+        if secs > 15:   # (bounded sample: one run is enough past 15 s)
+            break
+    cpu_runs.sort()
+    teps, secs = cpu_runs[len(cpu_runs) // 2]
+    counts_ok, lists_ok, listed = True, True, 0
+    for i, ((s_, t_), p) in enumerate(zip(pairs, per)):
+        n = sum(ck.walk_counts(s_, t_, 4)[1:])
+        counts_ok = counts_ok and (n == p[0] if p[0] is not None else n > 0)
+        if i in kept:
+            walks = ck.all_walks(s_, t_, 4, cap=20000)
+            exp = sorted([w[0]] + [x for v in w[1:] for x in (1, 0, v)] for w in walks)
+            lists_ok = lists_ok and kept[i] == exp
+            listed += 1
+    out_["verification"] = {"go_roots_checked": len(roots), "go_match": go_ok,
+                            "all_path_pairs_counted": len(pairs), "all_path_counts_match": counts_ok,
+                            "all_path_pairs_listed": listed, "all_path_lists_match": lists_ok,
+                            "method": "device nbg_rows_digest + edges scanned vs oracle/csr.cpp go_multi (two "
+                                      "CSRs); ALL PATH counts vs the walk-count DP, entry lists vs the oracle's "
+                                      "walk enumeration for the first 16 pairs with <= 20 k paths"}
+    out_["go4"]["cpu_baseline"] = {"value": teps, "unit": "TEPS", "cores": threads, "kind": "port",
+                                   "mode": "csr_openmp",
+                                   "sample": f"all {len(roots)} roots, GO 4 STEPS OVER knows, likes, median of "
+                                             f"{len(cpu_runs)} run(s) ({secs:.2f}s per run); oracle/csr.cpp "
+                                             f"go_multi, {threads} threads",
+                                   "model": model, "host_cpus": ncpu}
+    log(f"C5 verification {out_['verification']}")
+    ck.close()
+    cl.close()
 
 
 if __name__ == "__main__":

@@ -103,12 +103,15 @@ struct ChCtr {
   unsigned long long err;              // 1 reconstruction failure, 3 list overflow
   unsigned long long hlaunch;          // greedy launches that did work
   unsigned long long busy;             // step launches that ran a step
+  // greedy hub hop: workgroups done (the last one reduces and resets it).  Per query, so a hop
+  // whose workgroups disagreed about their count (a failed query) cannot leave the next query's
+  // hops a stale ticket
+  unsigned long long gticket;
 };
 
 struct ChState {        // device; the host reads what the result launch derives from it (ChOut)
   ChCtr c[2];
   unsigned long long gerr;             // CH_GUARD builds: bit 8 + site of a bounds violation
-  unsigned long long gticket;          // greedy hop: workgroups done (the last one reduces, resets)
   // greedy launch h starts from hstart[h] = (position << 32 | current vertex) and exactly one of
   // its workgroups writes hstart[h + 1]: state that no launch mutates while its own workgroups
   // may still read it (workgroups of one launch start at different times).  Greedy launches are
@@ -130,7 +133,11 @@ struct ChState {        // device; the host reads what the result launch derives
   // (ChQ::tag << 32 | launch index) of the launch in which this query's walk ended (or found nothing
   // to walk): a batched chain's LATER launches give the pair one workgroup (ch_batch_work).  Written
   // inside a launch, so the launch that writes it must not act on it (its workgroups start at
-  // different times and must all derive the same split)
+  // different times and must all derive the same split), and written ONCE per query: the launches
+  // after the walk's end find the same vertex and would rewrite it with their own index, which a
+  // late-starting workgroup of such a launch read as "not over before this launch" while its
+  // early peers had read the old value — two splits of one launch (round 6: a hub hop's ticket
+  // then never reached its count, and every later query of that context failed)
   unsigned long long walk_end;
 };
 
@@ -1019,7 +1026,8 @@ __device__ __forceinline__ bool ch_hop(const ChArgs& A, const ChQ& q, int nl, in
   uint32_t pos = (uint32_t)(H >> 32), c = (uint32_t)H;
   auto finish = [&](uint32_t p, uint32_t v) {   // (thread 0 of the one writer)
     st->hstart[h + 1] = ((unsigned long long)p << 32) | v;
-    if (v == NO_ROW || !F.met || F.err || p >= F.L) st->walk_end = ((unsigned long long)q.tag << 32) | (uint32_t)nl;
+    if ((v == NO_ROW || !F.met || F.err || p >= F.L) && (ld_agent(&st->walk_end) >> 32) != q.tag)
+      st->walk_end = ((unsigned long long)q.tag << 32) | (uint32_t)nl;
   };
   if (!F.met || F.phase != PH_DONE || F.err || pos >= F.L || c == NO_ROW) {
     if (bid == 0 && threadIdx.x == 0) finish(pos, c);
@@ -1111,7 +1119,7 @@ __device__ __forceinline__ bool ch_hop(const ChArgs& A, const ChQ& q, int nl, in
       part[2] = (unsigned long long)best.v;
       part[3] = best.d;
       __threadfence();
-      s_last = atomicAdd(&st->gticket, 1ull) == nblk - 1;
+      s_last = atomicAdd(&C.gticket, 1ull) == nblk - 1;
     }
     __syncthreads();
     if (!s_last) {
@@ -1126,7 +1134,7 @@ __device__ __forceinline__ bool ch_hop(const ChArgs& A, const ChQ& q, int nl, in
     }
     r = block_min(r, lds);
     if (threadIdx.x == 0) {
-      st->gticket = 0;
+      C.gticket = 0;
       s_last = record(pos, r);
       if (COOP && !s_last) post_end(st, q, h);
     }

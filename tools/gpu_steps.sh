@@ -41,6 +41,17 @@ for step in "$@"; do
         --verify 0 --c2 0 --c5-scale 0 --getbound-reqs 0 --c1-reqs 0 > "$OUT/sq26.json" 2> "$OUT/sq26.log" \
         || { tail -30 "$OUT/sq26.log"; exit 1; }
       python3 tools/pmc_summary.py $(find "$OUT/sq26" -name '*counter_collection.csv') > "$OUT/pmc_sq_rmat26.json" ;;
+    pmcsp)   # SHORTEST kernels (batched k_ch_step_b, one-pair k_ch_step<1>): HBM bytes and SQ cycles
+      i=0
+      for c in FETCH_SIZE WRITE_SIZE "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU"; do
+        i=$((i + 1))
+        PROBE_ROUNDS=1 timeout -s KILL 400 rocprofv3 --pmc $c -d "$OUT/pmcsp_$i" -o run --output-format csv -- \
+          python3 -u tools/sp_batch_probe.py 26 2000 default > "$OUT/pmcsp_$i.txt" 2>&1 \
+          || { tail -30 "$OUT/pmcsp_$i.txt"; exit 1; }
+      done
+      python3 tools/pmc_summary.py $(find "$OUT/pmcsp_1" "$OUT/pmcsp_2" -name '*counter_collection.csv') \
+        > "$OUT/pmc_hbm_sp_rmat26.json"
+      python3 tools/pmc_summary.py $(find "$OUT/pmcsp_3" -name '*counter_collection.csv') > "$OUT/pmc_sq_sp_rmat26.json" ;;
     prof26)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof26" -o run --output-format csv -- \
         python3 -u bench.py --sp-pairs 2000 --no-cpu-baseline --verify 0 --c2 0 --c5-scale 0 --getbound-reqs 0 --c1-reqs 0 \

@@ -28,7 +28,7 @@ chunk = 2000
 preps = [eng.path_batch_prepare(reqs[k:k + chunk]) for k in range(0, len(reqs), chunk)]
 base = None
 print(f"RMAT-{scale}, {len(pairs)} pairs", flush=True)
-for rnd in range(2):
+for rnd in range(int(os.environ.get('PROBE_ROUNDS', '2'))):
     for spec in settings:
         env = {} if spec == "default" else dict(kv.split("=", 1) for kv in spec.split(","))
         old = {k: os.environ.get(k) for k in env}
@@ -46,7 +46,11 @@ for rnd in range(2):
                         got.append(None)
                         continue
                     got.append(eng._paths(outs[i], None))
-            for idx, rc in fails[:8]:
+            msg = eng.lib.nbg_last_error(eng.h)
+            if fails:
+                print(f"   {len(fails)} failed; last error: {msg.decode() if msg else ''}; codes "
+                      f"{sorted(set(rc for _, rc in fails))}; first indices {[i for i, _ in fails[:12]]}", flush=True)
+            for idx, rc in fails[:3]:
                 s_, t_ = pairs[idx]
                 one = eng.find_path([s_], [t_], [1], 5)
                 print(f"   FAILED pair {idx} ({s_}, {t_}) rc {rc}; batch slot {idx % 32}; one-pair: {one}", flush=True)
