@@ -1176,6 +1176,25 @@ def getbound_leg(args):
     return out
 
 
+def c5_graph(k, parts):
+    """C5's graph (c5_leg): `knows` = RMAT-k over persons, `likes` = RMAT-(k-1) from persons to
+    posts (vids with bit 61 set), loaded and finalized.  Returns (engine, knows arrays, likes
+    arrays, persons)."""
+    from nebula_amd import Engine, rmat
+    ks, kd, kw = rmat.rmat_edges_fast(k)
+    ls, ld, lw = rmat.rmat_edges_fast(k - 1, seed=rmat.SEED_BASE ^ 0x6C696B6573)
+    persons = np.union1d(np.unique(ks), np.unique(kd))
+    ls = persons[(ls.astype(np.uint64) % np.uint64(len(persons))).astype(np.int64)]
+    ld = ld ^ (1 << 61)                       # posts: a vid range disjoint from the persons
+    eng = Engine(parts)
+    eng.register_edge(1, "knows", [("w", 2)])
+    eng.register_edge(2, "likes", [("w", 2)])
+    eng.load_edges(1, ks, kd, [kw])
+    eng.load_edges(2, ls, ld, [lw])
+    eng.finalize()
+    return eng, (ks, kd, kw), (ls, ld, lw), persons
+
+
 def c5_leg(args, barrier, threads, model, ncpu):
     """SURVEY §8(d) C5 substitute (LDBC SNB SF100 is not available offline): `knows` = RMAT-k
     over persons (k = --c5-scale, default 24 as §8(d) sizes it), `likes` = a bipartite RMAT-(k-1)
@@ -1185,20 +1204,10 @@ def c5_leg(args, barrier, threads, model, ncpu):
     every root's device digest and the ALL PATH counts / entry lists, and times the same GO as the
     leg's cpu_baseline."""
     import ctypes as C
-    from nebula_amd import Engine, rmat
+    from nebula_amd import rmat
     k = args.c5_scale
     t0 = time.time()
-    ks, kd, kw = rmat.rmat_edges_fast(k)
-    ls, ld, lw = rmat.rmat_edges_fast(k - 1, seed=rmat.SEED_BASE ^ 0x6C696B6573)
-    persons = np.union1d(np.unique(ks), np.unique(kd))
-    ls = persons[(ls.astype(np.uint64) % np.uint64(len(persons))).astype(np.int64)]
-    ld = ld ^ (1 << 61)                       # posts: a vid range disjoint from the persons
-    eng = Engine(args.parts)
-    eng.register_edge(1, "knows", [("w", 2)])
-    eng.register_edge(2, "likes", [("w", 2)])
-    eng.load_edges(1, ks, kd, [kw])
-    eng.load_edges(2, ls, ld, [lw])
-    eng.finalize()
+    eng, (ks, kd, kw), (ls, ld, lw), persons = c5_graph(k, args.parts)
     load_s = time.time() - t0
     log(f"C5 RMAT-{k}: loaded in {load_s:.1f}s, {eng.stats()}")
     roots = [int(x) for x in rmat.pick_roots(ks, 16, 42)]

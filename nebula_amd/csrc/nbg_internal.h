@@ -505,8 +505,23 @@ struct ChainQuery {
   uint32_t epoch, s, t, upto;
 };
 hipError_t chain_launch_batch(ChainCtx* const* cs, int n, const ChainQuery* qs);
+// a rolling run (spchain.hip chain_roll): slot l = a context, its labels and its first epoch
+struct ChainSlot {
+  ChainCtx* c;
+  uint32_t* const* lab;   // [3]
+  uint32_t ebase;         // the run uses epochs ebase + 1 .. ebase + n + 1
+};
+constexpr uint32_t CH_ROLL_UPTO = 32;   // rolling runs: UPTO at most this (CH_MAXS launches per pair suffice)
+constexpr int CH_ROLL_SLOTS = 64;       // slots of a rolling run, at most
+hipError_t chain_roll(const ChainSlot* slots, int nslots, const SpTypes& fwd, const SpTypes& bwd,
+                      const uint8_t* visible, const int64_t* vids, const uint32_t* s, const uint32_t* t, uint32_t n,
+                      uint32_t upto, SpResult* results);
+// n pairs on nslots slot contexts (one stream) as one rolling run (sp.hip)
+hipError_t sp_roll(SpCtx* const* cs, int nslots, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible,
+                   const int64_t* vids, const uint32_t* s, const uint32_t* t, uint32_t n, uint32_t upto,
+                   SpResult* results);
 void chain_result(const ChainCtx* c, SpResult* out);
-constexpr int CHAIN_KINDS = 6;                       // profiled chain launch kinds
+constexpr int CHAIN_KINDS = 4;                       // profiled chain launch kinds
 extern const char* const kChainKernelNames[CHAIN_KINDS];
 void chain_profile(ChainCtx* c, int mode);           // nbg_profile modes; resets the counters
 void chain_profile_done(ChainCtx* c, const SpResult& r);

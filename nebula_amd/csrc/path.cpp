@@ -797,7 +797,7 @@ int sp_batch_size() {
   static const int n = [] {
     const char* v = getenv("NBG_SP_BATCH");
     const int k = v ? atoi(v) : 32;   // RMAT-22: 16 -> 35.6 k, 32 -> 44.8 k pairs/s
-    return k < 1 ? 1 : (k > 32 ? 32 : k);
+    return k < 1 ? 1 : (k > CH_ROLL_SLOTS ? CH_ROLL_SLOTS : k);
   }();
   return n;
 }
@@ -954,29 +954,79 @@ int32_t nbg_find_path_batch(nbg_engine* h, const nbg_path_request* reqs, uint64_
   }
   if (E.batch_sp.empty()) return fail_rest(E.fail(NBG_E_OUT_OF_MEMORY, cerr));
   const int B = std::min<int>(want, (int)E.batch_sp.size());
-  for (size_t b0 = 0; b0 < pl.size(); b0 += (size_t)B) {
-    const int nb = (int)std::min<size_t>((size_t)B, pl.size() - b0);
-    std::vector<SpPair> sp(nb);
-    for (int p = 0; p < nb; ++p) {
-      const PairLaunch& x = pl[b0 + p];
-      sp[p] = SpPair{&x.fwd, &x.bwd, E.snap.d_visible, E.snap.d_vids, x.s, x.t, x.upto};
+  auto finish = [&](size_t k, const SpResult& r) {
+    const uint64_t i = at[k];
+    ran[k] = 1;
+    if (r.err == 1) {
+      rcs[i] = E.fail(NBG_E_UNKNOWN, "shortest-path reconstruction failed (in/out edges disagree)");
+    } else if (r.err) {
+      rcs[i] = E.fail(NBG_E_DEVICE, "shortest path: " + sp_err_text(r.err));
+    } else {
+      out[i] = paths_of(r);
     }
-    hipError_t he = sp_launch_batch(E.batch_sp.data(), nb, sp.data());
-    for (int p = 0; p < nb; ++p) {
-      const uint64_t i = at[b0 + p];
-      SpResult r;
-      if (he == hipSuccess) he = sp_wait(E.batch_sp[p], &r);
-      if (he != hipSuccess) break;
-      ran[b0 + p] = 1;
-      if (r.err == 1) {
-        rcs[i] = E.fail(NBG_E_UNKNOWN, "shortest-path reconstruction failed (in/out edges disagree)");
-      } else if (r.err) {
-        rcs[i] = E.fail(NBG_E_DEVICE, "shortest path: " + sp_err_text(r.err));
-      } else {
-        out[i] = paths_of(r);
+  };
+  // (read per call: the tests run both paths and small runs in one process)
+  auto env_int = [](const char* k, int dflt) { return getenv(k) ? atoi(getenv(k)) : dflt; };
+  const bool roll = env_int("NBG_SP_ROLL", 1) != 0;
+  const size_t chunk = (size_t)std::max(1, env_int("NBG_SP_ROLL_CHUNK", 4096));
+  const int roll_slots = std::max(1, std::min(B, env_int("NBG_SP_ROLL_SLOTS", B)));
+  // pairs [k0, k1) of one query shape as rolling runs (a slot takes the next pair as soon as its
+  // pair is done; spchain.hip k_ch_roll) of at most NBG_SP_ROLL_CHUNK (4096) pairs over
+  // NBG_SP_ROLL_SLOTS (NBG_SP_BATCH) slots
+  auto run_roll = [&](size_t k0, size_t k1) -> hipError_t {
+    std::vector<uint32_t> ss, ts;
+    std::vector<SpResult> res;
+    for (size_t c0 = k0; c0 < k1; c0 += chunk) {
+      const size_t c1 = std::min(k1, c0 + chunk), m = c1 - c0;
+      ss.resize(m);
+      ts.resize(m);
+      res.resize(m);
+      for (size_t k = 0; k < m; ++k) {
+        ss[k] = pl[c0 + k].s;
+        ts[k] = pl[c0 + k].t;
       }
+      const int slots = (int)std::min<size_t>((size_t)roll_slots, m);
+      const PairLaunch& x = pl[c0];
+      if (hipError_t he = sp_roll(E.batch_sp.data(), slots, x.fwd, x.bwd, E.snap.d_visible, E.snap.d_vids, ss.data(),
+                                  ts.data(), (uint32_t)m, x.upto, res.data()))
+        return he;
+      for (size_t k = 0; k < m; ++k) finish(c0 + k, res[k]);
     }
+    return hipSuccess;
+  };
+  // ... or as batches of B pairs, each running the whole chain UPTO allows (UPTO over
+  // CH_ROLL_UPTO, or NBG_SP_ROLL=0)
+  auto run_fixed = [&](size_t k0, size_t k1) -> hipError_t {
+    const int Bf = std::min(B, 32);
+    for (size_t b0 = k0; b0 < k1; b0 += (size_t)Bf) {
+      const int nb = (int)std::min<size_t>((size_t)Bf, k1 - b0);
+      std::vector<SpPair> sp(nb);
+      for (int p = 0; p < nb; ++p) {
+        const PairLaunch& x = pl[b0 + p];
+        sp[p] = SpPair{&x.fwd, &x.bwd, E.snap.d_visible, E.snap.d_vids, x.s, x.t, x.upto};
+      }
+      hipError_t he = sp_launch_batch(E.batch_sp.data(), nb, sp.data());
+      for (int p = 0; p < nb && he == hipSuccess; ++p) {
+        SpResult r;
+        he = sp_wait(E.batch_sp[p], &r);
+        if (he == hipSuccess) finish(b0 + p, r);
+      }
+      if (he != hipSuccess) return he;
+    }
+    return hipSuccess;
+  };
+  auto same_shape = [&](const PairLaunch& a, const PairLaunch& b) {
+    return a.upto == b.upto && a.fwd.row_ptr[0] == b.fwd.row_ptr[0] && a.fwd.col[0] == b.fwd.col[0] &&
+           a.bwd.row_ptr[0] == b.bwd.row_ptr[0] && a.bwd.col[0] == b.bwd.col[0] && a.fwd.type[0] == b.fwd.type[0] &&
+           a.fwd.dst_vid[0] == b.fwd.dst_vid[0] && a.fwd.rank[0] == b.fwd.rank[0] && a.fwd.ne[0] == b.fwd.ne[0] &&
+           a.bwd.ne[0] == b.bwd.ne[0];
+  };
+  for (size_t k0 = 0; k0 < pl.size();) {
+    size_t k1 = k0 + 1;
+    while (k1 < pl.size() && same_shape(pl[k0], pl[k1])) ++k1;
+    const hipError_t he = roll && pl[k0].upto <= CH_ROLL_UPTO ? run_roll(k0, k1) : run_fixed(k0, k1);
     if (he != hipSuccess) return fail_rest(dev_fail(E, he, "shortest path batch"));
+    k0 = k1;
   }
   return NBG_OK;
 }

@@ -122,6 +122,28 @@ hipError_t sp_launch_batch(SpCtx* const* cs, int n, const SpPair* pairs) {
   return hipSuccess;
 }
 
+// n pairs over nslots slots as one rolling run (spchain.hip chain_roll): each slot reserves n + 2
+// label epochs (its pairs' ordinals are below n + 1), clearing its labels first when they would
+// reach the tag bits
+hipError_t sp_roll(SpCtx* const* cs, int nslots, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible,
+                   const int64_t* vids, const uint32_t* s, const uint32_t* t, uint32_t n, uint32_t upto,
+                   SpResult* results) {
+  if (nslots < 1 || nslots > CH_ROLL_SLOTS || n >= (1u << 22)) return hipErrorInvalidValue;
+  std::vector<ChainSlot> sl(nslots);
+  for (int l = 0; l < nslots; ++l) {
+    SpCtx* c = cs[l];
+    if (c->stream != cs[0]->stream) return hipErrorInvalidValue;
+    HIP_TRY_SP(sp_reserve_chain(c));
+    if (c->epoch + n + 2 >= (1u << 24)) {
+      for (auto* lb : c->lab) HIP_TRY_SP(hipMemsetAsync(lb, 0, (c->nv + 1) * 4, c->stream));
+      c->epoch = 0;
+    }
+    sl[l] = ChainSlot{c->chain, c->lab, c->epoch};
+    c->epoch += n + 2;
+  }
+  return chain_roll(sl.data(), nslots, fwd, bwd, visible, vids, s, t, n, upto, results);
+}
+
 // NBG_WAKE=event: wait for the event behind the batch only (the A/B baseline)
 static bool wake_by_flag() {
   static const bool on = !(getenv("NBG_WAKE") && strcmp(getenv("NBG_WAKE"), "event") == 0);

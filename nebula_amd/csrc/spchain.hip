@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstddef>
 #include <cstring>
@@ -64,7 +65,7 @@ static_assert(CH_TAG_F < (1u << (32 - LVL_BITS)), "tag epochs fit the label's ep
 enum ChListId : int { CL_F0 = 0, CL_F1 = 1, CL_B0 = 2, CL_B1 = 3, CL_M = 4, CH_NLISTS = 5 };
 enum ChPhase : uint32_t { PH_BFS = 0, PH_BSET = 1, PH_DONE = 2 };
 // profiled launch kinds (nbg_profile_read names: kChainKernelNames)
-enum ChKind : int { CHK_SETUP = 0, CHK_STEP, CHK_HOP, CHK_SETUP_B, CHK_STEP_B, CHK_HOP_B, CH_NKINDS };
+enum ChKind : int { CHK_STEP = 0, CHK_HOP, CHK_STEP_B, CHK_ROLL, CH_NKINDS };
 
 }  // namespace
 
@@ -1367,7 +1368,187 @@ __global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(2
     ch_any<CH_WAVES, CH_VT, false>(*b.A[p], b.q[p], i, bid, nblk, last ? b.out[p] : nullptr);
 }
 
+// ---------------------------------------------------------------------------- rolling batches
+// A batch of 32 pairs ran the whole chain UPTO allows (2 UPTO launches) although a pair needs 4
+// on average: most of each launch's slots sat idle behind the batch's longest search.  A rolling
+// run keeps `nslots` contexts (slots) busy over a queue of n pairs: when a slot's pair has stored
+// its result, the slot takes the next queued pair in the next launch, whose workgroups start that
+// pair's step 0 beside the other slots' later steps.  Every workgroup derives launch i's
+// assignment from state final at the launch boundary — the previous launch's assignment (R, one
+// buffer per launch parity: launch i reads s[(i - 1) & 1] and its workgroup 0 writes s[i & 1]) and
+// each slot's walk_end — so all agree.  A pair runs under its local launch index i - i0, with its
+// own tag (tag0 + its index), counter set (its ordinal in the slot & 1: the previous pair's result
+// launch zeroed it) and label epoch (ebase + ordinal + 1).  Its result is stored, straight into
+// its own mapped ChOut, by the launch in which its walk ends.
+constexpr int CH_RMAX = CH_ROLL_SLOTS;         // slots of a rolling run (one wave's lanes)
+static_assert(CH_RMAX <= 64, "one lane per slot");
+constexpr uint32_t CH_RNONE = 0xFFFFFFFFu;     // an idle slot (the queue is empty)
+constexpr uint32_t CH_RDEAD = 0xFFFFFFFEu;     // a slot whose pair reached CH_MAXS launches (retired)
+struct ChRollSlot {
+  uint32_t p, i0, o, pad;                      // pair, its first launch, its ordinal in the slot
+};
+constexpr int CH_RTRACE = 4096;                // launches whose work NBG_SP_TRACE=2 records
+struct ChRollState {                           // device
+  ChRollSlot s[2][CH_RMAX];
+  uint32_t qhead[2];                           // pairs handed out by launch i's assignment
+  unsigned long long wmax[CH_RTRACE], wsum[CH_RTRACE];   // launch i's largest and total work (trace)
+};
+struct ChRollPair {
+  uint32_t s, t;
+};
+struct ChRoll {
+  const ChArgs* A[CH_RMAX];
+  ChState* st[CH_RMAX];
+  uint32_t ebase[CH_RMAX];
+  const ChRollPair* pairs;                     // device [n]
+  ChOut* outs;                                 // mapped pinned [n]
+  ChRollState* R;
+  unsigned long long* prog;                    // mapped pinned: ((i + 1) << 1) | (every pair done)
+  uint32_t n, nslots, tag0, upto, both, walk_items;
+};
+
+__device__ __forceinline__ ChQ roll_q(const ChRoll& r, int l, uint32_t p, uint32_t o, uint32_t s, uint32_t t) {
+  const uint32_t e = r.ebase[l] + o + 1;
+  return ChQ{s, t, r.upto, e, e, e, o & 1u, r.tag0 + p, r.both, 0u};
+}
+
+// (2 waves per SIMD, as k_ch_step_b; VT: items per lane of a tile, NBG_SP_ROLL_VT)
+template <int VT>
+__global__ void __launch_bounds__(CH_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) k_ch_roll(ChRoll r, int i) {
+  __shared__ uint32_t s_sel[6];
+  __shared__ int s_end;
+  if (threadIdx.x < 64) {
+    const int l = threadIdx.x;
+    const bool slot = l < (int)r.nslots;
+    ChRollSlot a{CH_RNONE, 0, 0, 0};
+    uint32_t qh;
+    if (i == 0) {
+      if (slot && (uint32_t)l < r.n) a.p = (uint32_t)l;
+      qh = r.n < r.nslots ? r.n : r.nslots;
+    } else {
+      const ChRollSlot pv = slot ? r.R->s[(i - 1) & 1][l] : a;
+      const uint32_t qp = r.R->qhead[(i - 1) & 1];
+      bool take = false;
+      if (slot && pv.p < r.n) {
+        const unsigned long long we = ld_agent(&r.st[l]->walk_end);
+        if ((we >> 32) == r.tag0 + pv.p && (uint32_t)we < (uint32_t)i - pv.i0) take = true;   // stored before launch i
+        else if ((uint32_t)i - pv.i0 >= (uint32_t)CH_MAXS) a = ChRollSlot{CH_RDEAD, 0, pv.o, 0};
+        else a = pv;
+      } else if (slot) {
+        take = pv.p == CH_RNONE;
+        a = pv;
+      }
+      const unsigned long long m = __ballot(take);
+      if (take) {
+        const uint32_t np = qp + (uint32_t)__popcll(m & ((1ull << l) - 1ull));
+        const uint32_t no = pv.p == CH_RNONE ? pv.o : pv.o + 1;   // (an idle slot keeps its next ordinal)
+        a = ChRollSlot{np < r.n ? np : CH_RNONE, (uint32_t)i, no, 0};
+      }
+      const uint32_t t = qp + (uint32_t)__popcll(m);
+      qh = t < r.n ? t : r.n;
+    }
+    // this launch's work per active slot (as ch_batch_work) and the grid's split
+    const bool act = slot && a.p < r.n;
+    unsigned long long w = 0;
+    if (act) {
+      const int li = i - (int)a.i0;
+      if (li == 0) {
+        w = 1;
+      } else {
+        const ChState* st = r.st[l];
+        const ChQ q = roll_q(r, l, a.p, a.o, 0, 0);
+        const unsigned long long j = ld_agent(&st->first[li]);
+        const ChSnap P = snap_for(st, q, li);
+        w = (j != (unsigned long long)li || P.phase == PH_DONE) ? r.walk_items : step_items(P) + 1;
+      }
+    }
+    unsigned long long W = w, Wm = w;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      W += __shfl_xor(W, o, 64);
+      const unsigned long long y = __shfl_xor(Wm, o, 64);
+      Wm = y > Wm ? y : Wm;
+    }
+    const uint32_t nact = (uint32_t)__popcll(__ballot(act));
+    const uint32_t G = gridDim.x, spare = G > nact ? G - nact : 0u;
+    const uint32_t na = act ? 1u + (uint32_t)(W ? ((unsigned long long)spare * w) / W : 0ull) : 0u;
+    const uint32_t incl = scan_incl(na), excl = incl - na;
+    if (l == 0) s_sel[0] = CH_RNONE;
+    __builtin_amdgcn_wave_barrier();
+    if (na && blockIdx.x >= excl && blockIdx.x < incl) {
+      s_sel[0] = (uint32_t)l;
+      s_sel[1] = blockIdx.x - excl;
+      s_sel[2] = na;
+      s_sel[3] = a.p;
+      s_sel[4] = a.i0;
+      s_sel[5] = a.o;
+    }
+    if (blockIdx.x == 0) {   // the assignment for launch i + 1 to derive its own from
+      if (slot) r.R->s[i & 1][l] = a;
+      if (l == 0) {
+        r.R->qhead[i & 1] = qh;
+        if (i < CH_RTRACE) {
+          r.R->wmax[i] = Wm;
+          r.R->wsum[i] = W;
+        }
+        __hip_atomic_store(r.prog, ((unsigned long long)(i + 1) << 1) | (qh >= r.n && nact == 0 ? 1ull : 0ull),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+  __syncthreads();
+  const uint32_t l = __builtin_amdgcn_readfirstlane(s_sel[0]);
+  const uint32_t bid = __builtin_amdgcn_readfirstlane(s_sel[1]), nblk = __builtin_amdgcn_readfirstlane(s_sel[2]);
+  const uint32_t p = __builtin_amdgcn_readfirstlane(s_sel[3]), i0 = __builtin_amdgcn_readfirstlane(s_sel[4]);
+  const uint32_t o = __builtin_amdgcn_readfirstlane(s_sel[5]);
+  __syncthreads();   // (ch_level reuses LDS)
+  if (l == CH_RNONE) return;
+  const ChRollPair pr = r.pairs[p];
+  const ChQ q = roll_q(r, (int)l, p, o, pr.s, pr.t);
+  const ChArgs& A = *r.A[l];
+  const int li = i - (int)i0;
+  if (ch_step<CH_WAVES, VT>(A, q, li, bid, nblk) || li == 0 || bid >= (uint32_t)CH_HOP_WGS) return;
+  const int h = li - hop_first(A.st->c[q.par]);
+  if (!ch_hop<false>(A, q, li, h, bid, nblk < (uint32_t)CH_HOP_WGS ? nblk : (uint32_t)CH_HOP_WGS)) return;
+  // the launch's writer: the result is final when the walk ended in this launch (walk_end is
+  // written once per query, by the writer, which reads its own store back)
+  if (threadIdx.x == 0) s_end = ld_agent(&A.st->walk_end) == (((unsigned long long)q.tag << 32) | (uint32_t)li);
+  __syncthreads();
+  if (s_end) ch_out(A, q, li, h + 1, r.outs + p);
+}
+
+// Zeroes both counter sets of every slot (block b: slot b) before a rolling run.
+__global__ void __launch_bounds__(CH_BLOCK) k_ch_roll_init(ChRoll r) {
+  unsigned long long* c = reinterpret_cast<unsigned long long*>(r.st[blockIdx.x]->c);
+  for (uint32_t k = threadIdx.x; k < 2 * sizeof(ChCtr) / 8; k += blockDim.x) c[k] = 0;
+}
+
 // ---------------------------------------------------------------------------- host side
+// A rolling run's buffers (kept by the run's first context, grown to the largest run)
+struct RollBuf {
+  ChRollState* R = nullptr;
+  ChRollPair* d_pairs = nullptr;
+  ChRollPair* h_pairs = nullptr;   // pinned staging of the pairs' upload
+  ChOut* h_outs = nullptr;         // mapped pinned: every pair's result
+  ChOut* d_outs = nullptr;
+  unsigned long long* h_prog = nullptr;   // mapped pinned progress word
+  unsigned long long* d_prog = nullptr;
+  uint32_t cap = 0;
+  uint32_t tag_next = 1u << 31;    // pair tags (a context's own chains count theirs from 1)
+  void release() {
+    if (R) (void)hipFree(R);
+    if (d_pairs) (void)hipFree(d_pairs);
+    if (h_pairs) (void)hipHostFree(h_pairs);
+    if (h_outs) (void)hipHostFree(h_outs);
+    if (h_prog) (void)hipHostFree(h_prog);
+    R = nullptr;
+    d_pairs = h_pairs = nullptr;
+    h_outs = d_outs = nullptr;
+    h_prog = d_prog = nullptr;
+    cap = 0;
+  }
+};
+
 struct ChainCtx {
   hipStream_t stream = nullptr;
   uint64_t nv = 0, list_cap = 0, tsplit_cap = 0;
@@ -1401,6 +1582,7 @@ struct ChainCtx {
   int prof = 0;
   bool last_batched = false;       // the query in flight ran in a batched chain
   bool walk_cap = false;           // the walk did not end within CH_MAXS greedy launches (an error)
+  struct RollBuf* roll = nullptr;  // rolling runs led by this context (chain_roll)
   struct PRec { int kind; hipEvent_t a, b; };
   std::vector<PRec> pend;
   std::vector<hipEvent_t> pool;
@@ -1414,7 +1596,7 @@ struct ChainCtx {
   // one launch between two events (kind: CHK_*), when profiling that kind
   template <class F>
   void timed(int kind, F&& launch) {
-    if (!prof || (prof == 2 && kind != CHK_STEP && kind != CHK_STEP_B)) { launch(); return; }
+    if (!prof || (prof == 2 && kind != CHK_STEP && kind != CHK_STEP_B && kind != CHK_ROLL)) { launch(); return; }
     PRec r{kind, ev(), ev()};
     (void)hipEventRecord(r.a, stream);
     launch();
@@ -1480,6 +1662,10 @@ void chain_destroy(ChainCtx* c) {
   if (c->d_args) (void)hipFree(c->d_args);
   if (c->h_out) (void)hipHostFree(c->h_out);
   if (c->h_args) (void)hipHostFree(c->h_args);
+  if (c->roll) {
+    c->roll->release();
+    delete c->roll;
+  }
   for (auto& r : c->pend) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
   for (auto e : c->pool) (void)hipEventDestroy(e);
   delete c;
@@ -1510,10 +1696,10 @@ static hipError_t chain_batch(ChainCtx* c, int k, int h) {
 }
 
 // The query's arguments into c (uploaded when they changed) and its ChQ; nothing launched.
-static hipError_t chain_prepare(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible,
-                                const int64_t* vids, uint32_t* const lab[3], uint32_t epoch, uint32_t s, uint32_t t,
-                                uint32_t upto) {
-  if (fwd.n != 1 || bwd.n != 1 || upto < 1 || upto > MAX_PATH_LEN) return hipErrorInvalidValue;
+// The CSRs, labels and buffers of c's queries into its device ChArgs (uploaded when they changed).
+static hipError_t chain_args(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible,
+                             const int64_t* vids, uint32_t* const lab[3]) {
+  if (fwd.n != 1 || bwd.n != 1) return hipErrorInvalidValue;
   ChArgs a;
   memset(&a, 0, sizeof(a));   // compared bytewise: no indeterminate padding
   a.row_ptr[0] = fwd.row_ptr[0];
@@ -1540,6 +1726,14 @@ static hipError_t chain_prepare(ChainCtx* c, const SpTypes& fwd, const SpTypes& 
     c->cached = a;
     c->args_valid = true;
   }
+  return hipSuccess;
+}
+
+static hipError_t chain_prepare(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible,
+                                const int64_t* vids, uint32_t* const lab[3], uint32_t epoch, uint32_t s, uint32_t t,
+                                uint32_t upto) {
+  if (upto < 1 || upto > MAX_PATH_LEN) return hipErrorInvalidValue;
+  HIP_TRY_CH(chain_args(c, fwd, bwd, visible, vids, lab));
   c->par ^= 1u;
   // (NBG_SP_JOB_WAIT, read per query: a test sets 0 so that every hub job goes unanswered and the
   // fallback — the next launch's spread scan — runs)
@@ -1644,6 +1838,158 @@ hipError_t chain_launch_batch(ChainCtx* const* cs, int n, const ChainQuery* qs) 
   return hipSuccess;
 }
 
+// A rolling run (k_ch_roll): n pairs (s[k], t[k]) of one query shape over nslots contexts that
+// share one stream; every pair's result into results[k].  The host keeps NBG_SP_ROLL_AHEAD (4)
+// launches queued past the one the device has started (the progress word, written at each
+// launch's start), and stops when a launch finds every pair done; the launches queued past that
+// return at once.  A pair whose walk did not end within CH_MAXS launches of its own (not
+// reachable at UPTO <= CH_ROLL_UPTO) gets CH_ERR_WALK_CAP, and its slot takes no more pairs.
+static void out_result(const ChOut& h, bool walk_cap, SpResult* out);
+
+hipError_t chain_roll(const ChainSlot* slots, int nslots, const SpTypes& fwd, const SpTypes& bwd,
+                      const uint8_t* visible, const int64_t* vids, const uint32_t* s, const uint32_t* t, uint32_t n,
+                      uint32_t upto, SpResult* results) {
+  if (nslots < 1 || nslots > CH_RMAX || upto < 1 || upto > CH_ROLL_UPTO) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
+  ChainCtx* c0 = slots[0].c;
+  const hipStream_t st = c0->stream;
+  ChRoll r;
+  memset(&r, 0, sizeof(r));
+  for (int l = 0; l < nslots; ++l) {
+    ChainCtx* c = slots[l].c;
+    if (c->stream != st) return hipErrorInvalidValue;
+    HIP_TRY_CH(chain_args(c, fwd, bwd, visible, vids, slots[l].lab));
+    r.A[l] = c->d_args;
+    r.st[l] = c->d_st;
+    r.ebase[l] = slots[l].ebase;
+  }
+  if (!c0->roll) c0->roll = new RollBuf();
+  RollBuf& B = *c0->roll;
+  if (B.cap < n) {   // (the previous run has completed: the buffers are idle)
+    B.release();
+    hipError_t he = hipMalloc((void**)&B.R, sizeof(ChRollState));
+    if (he == hipSuccess) he = hipMalloc((void**)&B.d_pairs, (size_t)n * sizeof(ChRollPair));
+    if (he == hipSuccess) he = hipHostMalloc((void**)&B.h_pairs, (size_t)n * sizeof(ChRollPair), hipHostMallocDefault);
+    if (he == hipSuccess)
+      he = hipHostMalloc((void**)&B.h_outs, (size_t)n * sizeof(ChOut), hipHostMallocMapped | hipHostMallocCoherent);
+    if (he == hipSuccess) he = hipHostGetDevicePointer((void**)&B.d_outs, B.h_outs, 0);
+    if (he == hipSuccess)
+      he = hipHostMalloc((void**)&B.h_prog, sizeof(unsigned long long), hipHostMallocMapped | hipHostMallocCoherent);
+    if (he == hipSuccess) he = hipHostGetDevicePointer((void**)&B.d_prog, B.h_prog, 0);
+    if (he != hipSuccess) {
+      B.release();
+      return he;
+    }
+    B.cap = n;
+  }
+  for (uint32_t k = 0; k < n; ++k) B.h_pairs[k] = ChRollPair{s[k], t[k]};
+  HIP_TRY_CH(hipMemcpyAsync(B.d_pairs, B.h_pairs, (size_t)n * sizeof(ChRollPair), hipMemcpyHostToDevice, st));
+  __atomic_store_n(B.h_prog, 0ull, __ATOMIC_RELEASE);
+  if (B.tag_next > 0xF0000000u - n) B.tag_next = 1u << 31;
+  r.pairs = B.d_pairs;
+  r.outs = B.d_outs;
+  r.R = B.R;
+  r.prog = B.d_prog;
+  r.n = n;
+  r.nslots = (uint32_t)nslots;
+  r.tag0 = B.tag_next;
+  B.tag_next += n;
+  r.upto = upto;
+  r.both = getenv("NBG_SP_ROLL_BOTH") ? (uint32_t)strtoul(getenv("NBG_SP_ROLL_BOTH"), nullptr, 10) : c0->both;
+  // (read per run, as the fixed batches read theirs per batch).  RMAT-26, 10 k pairs
+  // (profiles/r06_i_sp_roll_grid_vt.txt, r06_j_*): 4-item tiles on 1024 workgroups 50.6-54.9 k
+  // pairs/s against 44.6-45.0 k with the fixed batches' 2-item tiles on 512 (8-item tiles 47.6-49.1 k)
+  const unsigned grid_env = getenv("NBG_SP_ROLL_GRID") ? (unsigned)atoi(getenv("NBG_SP_ROLL_GRID")) : 1024u;
+  const unsigned walk_env = getenv("NBG_SP_WALK_ITEMS") ? (unsigned)atoi(getenv("NBG_SP_WALK_ITEMS")) : 16384u;
+  const int ahead = getenv("NBG_SP_ROLL_AHEAD") ? std::max(1, atoi(getenv("NBG_SP_ROLL_AHEAD"))) : 4;
+  const int vt = getenv("NBG_SP_ROLL_VT") ? atoi(getenv("NBG_SP_ROLL_VT")) : 4;
+  auto kern = vt == 8 ? k_ch_roll<8> : vt == 4 ? k_ch_roll<4> : vt == 1 ? k_ch_roll<1> : k_ch_roll<2>;
+  const auto t_start = std::chrono::steady_clock::now();
+  r.walk_items = walk_env;
+  const unsigned grid = std::max(grid_env, (unsigned)nslots);
+  hipLaunchKernelGGL(k_ch_roll_init, dim3(nslots), dim3(CH_BLOCK), 0, st, r);
+  HIP_TRY_CH(hipGetLastError());
+  // launches: at most CH_MAXS per pair on each slot (a safety bound; a run takes ~4-5 per pair / nslots)
+  const uint64_t cap = ((uint64_t)n + (uint64_t)nslots) * CH_MAXS;
+  uint64_t enq = 0;
+  // NBG_SP_TRACE=2: an event before every launch, and each launch's work (largest pair, total)
+  static const bool trace2 = getenv("NBG_SP_TRACE") && atoi(getenv("NBG_SP_TRACE")) == 2;
+  std::vector<hipEvent_t> tev;
+  for (unsigned spin = 1;; ++spin) {
+    const unsigned long long pw = __atomic_load_n(B.h_prog, __ATOMIC_ACQUIRE);
+    if (pw & 1ull) break;
+    const uint64_t seen = pw >> 1;   // launches started
+    if (enq < seen + (uint64_t)ahead && enq < cap) {
+      const int i = (int)enq;
+      if (trace2 && i < CH_RTRACE) {
+        tev.push_back(c0->ev());
+        (void)hipEventRecord(tev.back(), st);
+      }
+      c0->timed(CHK_ROLL, [&] { hipLaunchKernelGGL(kern, dim3(grid), dim3(CH_BLOCK), 0, st, r, i); });
+      HIP_TRY_CH(hipGetLastError());
+      ++enq;
+      continue;
+    }
+    if ((spin & 1023) == 0) {   // a failed launch never writes progress: its error ends the run
+      const hipError_t e = hipStreamQuery(st);
+      if (e != hipErrorNotReady && e != hipSuccess) return e;
+      if (e == hipSuccess && enq >= cap) break;   // (not reachable: every pair ends within the bound)
+    }
+  }
+  if (trace2) {
+    tev.push_back(c0->ev());
+    (void)hipEventRecord(tev.back(), st);
+  }
+  HIP_TRY_CH(hipStreamSynchronize(st));
+  if (trace2 && tev.size() > 1) {   // per launch: duration against its largest pair's work (log2 buckets)
+    const size_t nl = tev.size() - 1;
+    std::vector<unsigned long long> wm(nl), ws(nl);
+    (void)hipMemcpy(wm.data(), B.R->wmax, nl * 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(ws.data(), B.R->wsum, nl * 8, hipMemcpyDeviceToHost);
+    double cnt[48] = {}, ms[48] = {}, sum[48] = {};
+    for (size_t k = 0; k < nl; ++k) {
+      float t = 0;
+      (void)hipEventElapsedTime(&t, tev[k], tev[k + 1]);
+      int b = 0;
+      while (b < 47 && (1ull << (b + 1)) <= wm[k]) ++b;
+      cnt[b] += 1;
+      ms[b] += t;
+      sum[b] += (double)ws[k];
+    }
+    double tot = 0;
+    for (int b = 0; b < 48; ++b) tot += ms[b];
+    for (int b = 0; b < 48; ++b)
+      if (cnt[b])
+        fprintf(stderr, "[sp roll launches] largest pair work in [2^%d, 2^%d): %5.0f launches, %8.2f us each, %5.1f%% of the time, mean total work %.0f\n",
+                b, b + 1, cnt[b], 1e3 * ms[b] / cnt[b], 100.0 * ms[b] / tot, sum[b] / cnt[b]);
+    fprintf(stderr, "[sp roll launches] %zu launches, %.3f ms\n", nl, tot);
+    for (auto e : tev) c0->pool.push_back(e);
+  }
+  if (getenv("NBG_SP_TRACE"))
+    fprintf(stderr, "[sp roll] %u pairs, %d slots, %llu launches enqueued, done at launch %llu, %.3f ms\n", n, nslots,
+            (unsigned long long)enq, (unsigned long long)(__atomic_load_n(B.h_prog, __ATOMIC_ACQUIRE) >> 1),
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count());
+  double abytes = 0;
+  for (uint32_t k = 0; k < n; ++k) {
+    const ChOut& h = B.h_outs[k];
+    const bool stored = __atomic_load_n(&h.wake, __ATOMIC_ACQUIRE) == (unsigned long long)(r.tag0 + k);
+    out_result(h, !stored, &results[k]);
+    results[k].launches = stored ? h.busy + std::max(1ull, h.hlaunch) : 0;
+    results[k].batches = 1;
+    abytes += stored ? (double)h.F.abytes : 0.0;
+  }
+  for (int l = 0; l < nslots; ++l) {
+    ChainCtx* c = slots[l].c;
+    c->clean = false;   // (the next one-pair query zeroes its counter set)
+    c->queries += 1;
+  }
+  if (c0->prof) {
+    c0->flush();
+    c0->bytes[CHK_ROLL] += abytes;
+  }
+  return hipSuccess;
+}
+
 // After a batch's copy completed: the query's final state, or false with a continuation batch
 // enqueued (the caller waits again).
 bool chain_woken(const ChainCtx* c) {
@@ -1692,24 +2038,29 @@ bool chain_more(ChainCtx* c, hipError_t* he) {
   return true;
 }
 
-// the final state -> SpResult
-void chain_result(const ChainCtx* c, SpResult* out) {
-  const ChOut& h = *c->h_out;
+// a stored result -> SpResult (walk_cap: the walk never ended)
+static void out_result(const ChOut& h, bool walk_cap, SpResult* out) {
   const ChSnap& F = h.F;
   out->err = h.err;
   out->edges = F.edges;
   out->levels = F.levels;
   out->abytes = F.abytes;
-  out->launches = (unsigned long long)(c->steps + c->hops);
-  out->batches = c->qbatches;
   const uint32_t hpos = (uint32_t)(h.hpos >> 32);
-  out->L = (F.met && !h.err && hpos == F.L && !c->walk_cap) ? F.L : 0;
-  if (c->walk_cap) {
+  out->L = (F.met && !h.err && hpos == F.L && !walk_cap) ? F.L : 0;
+  if (walk_cap) {
     out->err = CH_ERR_WALK_CAP;
   } else if (F.met && !h.err && hpos != F.L) {
     out->err = 2;   // (cannot happen: the hops were enqueued)
   }
   if (out->L) memcpy(out->path, h.path, (1 + 3 * (size_t)out->L) * sizeof(long long));
+}
+
+// the final state -> SpResult
+void chain_result(const ChainCtx* c, SpResult* out) {
+  const ChOut& h = *c->h_out;
+  out_result(h, c->walk_cap, out);
+  out->launches = (unsigned long long)(c->steps + c->hops);
+  out->batches = c->qbatches;
   // NBG_SP_TRACE=2: one line per query (the chain's step and greedy launches, path length)
   static const bool per_query = getenv("NBG_SP_TRACE") && atoi(getenv("NBG_SP_TRACE")) == 2;
   if (per_query)
@@ -1733,8 +2084,7 @@ void chain_profile_done(ChainCtx* c, const SpResult& r) {
 }
 
 static_assert(CH_NKINDS == CHAIN_KINDS, "chain kinds");
-const char* const kChainKernelNames[CH_NKINDS] = {"k_ch_setup", "k_ch_step", "k_ch_hop",
-                                                  "k_ch_setup_b", "k_ch_step_b", "k_ch_hop_b"};
+const char* const kChainKernelNames[CH_NKINDS] = {"k_ch_step", "k_ch_hop", "k_ch_step_b", "k_ch_roll"};
 
 void chain_profile_accum(const ChainCtx* c, double* launches, double* ms, double* bytes) {
   for (int k = 0; k < CH_NKINDS; ++k) {

@@ -328,11 +328,17 @@ def test_async_path_submit_wait_parity(sp_mode):
         orc.close()
 
 
-def test_find_path_batch_matches_single(sp_mode):
-    """nbg_find_path_batch: one-pair SHORTEST requests run NBG_SP_BATCH at a time as one batched
-    device level loop; mixed in are requests that run on their own (s == t, several sources,
-    unknown vids, FIND ALL PATH, an endpoint without edges).  Every result equals nbg_find_path's,
-    the edge counts too, and the oracle's paths."""
+@pytest.mark.parametrize("batch_env", [{}, {"NBG_SP_ROLL_SLOTS": "3", "NBG_SP_ROLL_CHUNK": "29"}, {"NBG_SP_ROLL": "0"}],
+                         ids=["rolling", "rolling-3-slots", "fixed"])
+def test_find_path_batch_matches_single(sp_mode, batch_env, monkeypatch):
+    """nbg_find_path_batch: one-pair SHORTEST requests run as rolling runs (a slot takes the next
+    queued pair when its pair is done: k_ch_roll), here also over 3 slots in runs of 29 pairs (every
+    slot refilled many times), or NBG_SP_ROLL=0 as fixed batches of NBG_SP_BATCH; mixed in are
+    requests that run on their own (s == t, several sources, unknown vids, FIND ALL PATH, an
+    endpoint without edges) and pairs of another UPTO (runs split by query shape).  Every result
+    equals nbg_find_path's, the edge counts too, and the oracle's paths."""
+    for k, v in batch_env.items():
+        monkeypatch.setenv(k, v)
     src, dst, w = graphs.rmat_graph(11)
     eng = graphs.rmat_engine(src, dst, w)
     orc = graphs.rmat_oracle(src, dst, w)
@@ -343,6 +349,7 @@ def test_find_path_batch_matches_single(sp_mode):
         reqs += [([ps[0][0]], [ps[0][0]], [1], 4, True), ([ps[1][0], ps[2][0]], [ps[3][1]], [1], 4, True),
                  ([123456789], [ps[4][1]], [1], 5, True), ([ps[5][0]], [ps[6][1]], [1], 3, False),
                  ([ps[7][0]], [ps[8][1]], [1], 2, True)]
+        reqs += [([s], [t], [1], 3, True) for s, t in ps[:9]] + [([s], [t], [1], 40, True) for s, t in ps[9:13]]
         st = []
         got = eng.find_path_batch(reqs, stats=st)
         assert len(got) == len(reqs)

@@ -52,6 +52,15 @@ for step in "$@"; do
       python3 tools/pmc_summary.py $(find "$OUT/pmcsp_1" "$OUT/pmcsp_2" -name '*counter_collection.csv') \
         > "$OUT/pmc_hbm_sp_rmat26.json"
       python3 tools/pmc_summary.py $(find "$OUT/pmcsp_3" -name '*counter_collection.csv') > "$OUT/pmc_sq_sp_rmat26.json" ;;
+    pmcc5)   # C5 GO 4 STEPS OVER knows, likes (RMAT-24): HBM bytes per kernel
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 400 rocprofv3 --pmc $c -d "$OUT/pmcc5_$c" -o run --output-format csv -- \
+          python3 -u tools/c5_probe.py 24 2 > "$OUT/pmcc5_$c.txt" 2>&1 || { tail -30 "$OUT/pmcc5_$c.txt"; exit 1; }
+      done
+      python3 tools/pmc_summary.py $(find "$OUT/pmcc5_FETCH_SIZE" "$OUT/pmcc5_WRITE_SIZE" -name '*counter_collection.csv') \
+        > "$OUT/pmc_hbm_c5_rmat24.json"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/profc5" -o run --output-format csv -- \
+        python3 -u tools/c5_probe.py 24 2 > "$OUT/profc5.txt" 2>&1 || { tail -30 "$OUT/profc5.txt"; exit 1; } ;;
     prof26)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof26" -o run --output-format csv -- \
         python3 -u bench.py --sp-pairs 2000 --no-cpu-baseline --verify 0 --c2 0 --c5-scale 0 --getbound-reqs 0 --c1-reqs 0 \
