@@ -1241,13 +1241,14 @@ static int32_t go_launch(Engine& E, const nbg_go_stmt* st, const int64_t* starts
         np0 = &next0;
       }
     }
+    // (before the MARKs, on every rank: one without edges of the type runs none)
+    if (s == 1 && !final && hop1_slots) he = ws_set_hop_slots(ws, hop1_slots);
     for (size_t i = 0; he == hipSuccess && i < over.size(); ++i) {
       auto it = E.snap.types.find(over[i]);
       if (it == E.snap.types.end()) continue;
       ExpandArgs a = args_for(it->second);
       a.bt_first = s == 1;
       if (!final) {
-        if (s == 1 && i == 0) ws_set_hop_slots(ws, hop1_slots);
         he = ws_expand_mark(ws, a, n_bound, it->second.num_edges, (int)s, (int)i, inl_of(i, s), np0);
       } else if (deferred || (plist[i].where_const && !plist[i].where_const_val)) {
         he = ws_scan_only(ws, a, n_bound, (int)s, (int)i);

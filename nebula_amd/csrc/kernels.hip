@@ -2385,9 +2385,7 @@ hipError_t ws_expand_mark(Workspace* w, const ExpandArgs& a0, uint64_t n_bound, 
   // partitioned MARK (not MARKB, whose roots ride with the byte flags): straight into the hop's
   // send bitmap, which ws_exchange then sends without a pack pass
   if (w->comm && !a0.bt && !bits_off()) {
-    if (w->hop_slots) {   // a small hop: edge e's neighbour into slot e of its owner's segment
-      if (tix == 0)
-        HIP_TRY(hipMemsetAsync(w->sendbits, 0xFF, (uint64_t)w->comm->world * w->hop_slots * 4, w->stream));
+    if (w->hop_slots) {   // a small hop: edge e's neighbour into slot e of its owner's segment (NO_ROW-filled)
       bp.sparse = reinterpret_cast<uint32_t*>(w->sendbits);
       bp.sp_stride = (uint32_t)w->hop_slots;
       bp.sp_npad = (uint32_t)w->npad;
@@ -3286,8 +3284,16 @@ static hipError_t ws_roots(Workspace* w, int step) {
   return hipSuccess;
 }
 
-void ws_set_hop_slots(Workspace* w, uint64_t stride) {
-  if (w) w->hop_slots = stride && w->comm && stride * 4 * 2 <= w->npad / 8 ? stride : 0;
+// Every rank calls it before the hop's MARKs, a rank without edges of the OVER type (no MARK)
+// too: its slots are empty (NO_ROW) and ws_exchange takes the slot format on every rank.  (Round 6
+// first set the format and the NO_ROW fill inside the MARK: a part-less rank then sent its
+// all-zero bitmap, which the owners read as local id 0 — an extra vertex on every rank — and
+// exchanged bitmap-sized segments while its peers exchanged slots.)
+hipError_t ws_set_hop_slots(Workspace* w, uint64_t stride) {
+  if (!w) return hipErrorInvalidValue;
+  w->hop_slots = stride && w->comm && stride * 4 * 2 <= w->npad / 8 ? stride : 0;
+  if (!w->hop_slots) return hipSuccess;
+  return hipMemsetAsync(w->sendbits, 0xFF, (uint64_t)w->comm->world * w->hop_slots * 4, w->stream);
 }
 
 hipError_t ws_exchange(Workspace* w, int step, const ExpandArgs* next0) {
@@ -3295,7 +3301,7 @@ hipError_t ws_exchange(Workspace* w, int step, const ExpandArgs* next0) {
   const uint64_t G = (uint64_t)w->comm->world;
   const uint64_t nwords = G * w->npad / 64, seg_words = w->npad / 64, nb = w->npad / BITS_BLOCK;
   hipEvent_t p = nullptr;
-  if (w->hop_slots && w->hop_bits && !w->bt_active) {
+  if (w->hop_slots && !w->bt_active) {
     // a small hop's slot arrays: stride ids per peer instead of npad / 8 bytes; the owner claims
     // the arrivals against the step's stamp (a vertex may arrive from several edges and ranks)
     const uint64_t stride = w->hop_slots;

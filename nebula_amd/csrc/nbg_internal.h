@@ -726,7 +726,7 @@ hipStream_t ws_stream(const Workspace* w);
 hipError_t ws_exchange(Workspace* w, int step, const ExpandArgs* next0);   // replaces ws_compact
 // the next hop (its MARKs and ws_exchange) sends per-owner slot arrays of `stride` local ids
 // instead of npad-bit bitmap segments; the caller guarantees the hop's edges on every rank fit
-void ws_set_hop_slots(Workspace* w, uint64_t stride);
+hipError_t ws_set_hop_slots(Workspace* w, uint64_t stride);
 hipError_t ws_global_stats(Workspace* w, int ntypes);      // before ws_end_query
 int32_t ws_host_gstatus(Workspace* w);                     // after it: the first failing rank's status
 hipError_t part_empty_query(Comm* c, hipStream_t s, int hops, const void* send0, void* recv, size_t seg_bytes,

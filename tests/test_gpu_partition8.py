@@ -402,3 +402,37 @@ def test_rmat16_go_and_shortest_digests():
     finally:
         c.close()
         single.close()
+
+
+def test_first_hop_slots_with_an_empty_rank(nba_data, monkeypatch):
+    """The first-hop slot exchange where rank 0 serves no part (7 parts over 8 ranks): that rank
+    runs no MARK, yet sends empty slots in the slot format.  (Round 6's first version set the
+    format and the NO_ROW fill inside the MARK: the part-less rank sent its all-zero bitmap, which
+    every owner read as its local vertex 0, and 2- and 3-step rows gained those vertices' edges.)
+    Rows equal the oracle's with slots and with bitmaps (NBG_GO_SLOTS=0)."""
+    from tests.support import ngql
+    c = LocalCluster(7, G)
+    for (kind, name), cols in kvgen.NBA_SCHEMAS.items():
+        if kind == "edge":
+            c.register_edge(kvgen.NBA_EDGES[name], name, cols)
+        else:
+            c.register_tag(kvgen.NBA_TAGS[name], name, cols)
+    c.load_builder(kvgen.nba_kv(nba_data, 7))
+    orc = nba_oracle(nba_data, 7)
+    td, tp = 'hash("Tim Duncan")', 'hash("Tony Parker")'
+    qs = [f'GO 2 STEPS FROM {td} OVER like YIELD like._dst',
+          f'GO 2 STEPS FROM {td} OVER like YIELD $$.player.name, like._src',
+          f'GO 2 STEPS FROM {td} OVER like YIELD DISTINCT left(right($$.player.name, 4), 2) AS f',
+          f'GO 3 STEPS FROM {tp} OVER like YIELD like._dst',
+          f'GO 2 STEPS FROM {td}, {tp} OVER like WHERE like.likeness > 80 YIELD like._dst, like.likeness']
+    try:
+        for q in qs:
+            want = sorted(tuple(r) for r in ngql.Session(orc).execute(q).rows)
+            assert want, q
+            for slots in ("1", "0"):
+                monkeypatch.setenv("NBG_GO_SLOTS", slots)
+                got = sorted(tuple(r) for r in ngql.Session(c).execute(q).rows)
+                assert got == want, (slots, q)
+    finally:
+        c.close()
+        orc.close()
