@@ -39,10 +39,11 @@ T_START = time.time()
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 METRIC = "GO 3 STEPS traversed edges/sec (TEPS) at 1/2/4/8 GPU; FIND SHORTEST PATH p50"
 # HBM traffic per launch from the committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
-# bench's default workload (tools/gpu_steps.sh pmc26 / pmc22 -> tools/pmc_summary.py; FETCH_SIZE doubled per
-# the gfx950 note), keyed by workload
+# bench's default workload (tools/gpu_steps.sh pmc26 / pmc22 / pmcc5 -> tools/pmc_summary.py; FETCH_SIZE
+# doubled per the gfx950 note), keyed by workload
 PMC_FILES = {("RMAT-26", 16): os.path.join(ROOT, "profiles", "r05_finb_pmc_hbm_rmat26.json"),
-             ("RMAT-22", 64): os.path.join(ROOT, "profiles", "r02_pmc_hbm_rmat22.json")}
+             ("RMAT-22", 64): os.path.join(ROOT, "profiles", "r02_pmc_hbm_rmat22.json"),
+             ("C5-RMAT-24", 16): os.path.join(ROOT, "profiles", "r06_u_pmc_hbm_c5_rmat24.json")}
 # library kernel id -> instantiations in the rocprof names, first match wins (FINAL: this bench's
 # range WHERE with a _dst YIELD runs k_expand<4> = FINALD; <3> FINALF; <1> the general interpreter;
 # the bool is the inline-start-list variant)
@@ -51,7 +52,9 @@ PMC_FILES = {("RMAT-26", 16): os.path.join(ROOT, "profiles", "r05_finb_pmc_hbm_r
 PMC_NAMES = {k: [n for p in v for n in (p[:-1] + ", 4>", p)] for k, v in {
     "k_expand<MARK>": ["k_expand<0, false>", "k_expand<0, true>"],
     "k_expand<FINAL>": ["k_final_dst<1, true>", "k_final_dst<2, true>", "k_final_dst<4, true>",
-                        "k_final_dst<8, true>", "k_final_dst<0, true>",
+                        "k_final_dst<8, true>", "k_final_dst<0, true>", "k_final_dst<0, false>",
+                        "k_final_dst<1, false>", "k_final_dst<2, false>", "k_final_dst<4, false>",
+                        "k_final_dst<8, false>",
                         "k_expand<4, false>", "k_expand<4, true>", "k_expand<3, false>",
                         "k_expand<3, true>", "k_expand<1, false>", "k_expand<1, true>"],
     "k_expand<BFS>": ["k_expand<2, false>", "k_expand<2, true>"]}.items()}
@@ -880,7 +883,25 @@ def partitioned_costs(eng, roots, barrier):
     bits = prof.get("alltoall(xGMI)", {})
     rts = prof.get("alltoallv(roots)", {})
     hops = max(1, rts.get("launches", 0))
-    return {"distinct": {"query": "GO 3 STEPS FROM <root> OVER e WHERE e.w < 50 YIELD DISTINCT e.w",
+
+    def exchanged(slots):   # one single-root GO 3 STEPS: its hops' all-to-alls (NBG_GO_SLOTS, per query)
+        os.environ["NBG_GO_SLOTS"] = slots
+        eng.profile(True)
+        barrier()
+        eng.go([roots[0]], [1], 3, where)
+        x = eng.profile_read().get("alltoall(xGMI)", {})
+        eng.profile(False)
+        return x.get("launches", 0), x.get("algo_bytes", 0)
+    (h1, b1), (h0, b0) = exchanged("1"), exchanged("0")
+    os.environ.pop("NBG_GO_SLOTS", None)
+    per_bitmap_hop = b0 / h0 if h0 else 0
+    return {"go_exchange": {"query": "GO 3 STEPS FROM <root> OVER e WHERE e.w < 50 (one root; bytes each rank sends)",
+                            "hops": h1, "bytes_per_query": b1, "bytes_per_query_all_bitmaps": b0,
+                            "bitmap_hop_bytes": per_bitmap_hop,
+                            "first_hop_bytes": b1 - per_bitmap_hop * (h1 - 1) if h1 else 0,
+                            "note": "first hop as per-owner slot arrays (stride = the root's capped degree "
+                                    "rounded to 64, 4 B each) when it fits, else a bitmap (npad / 8 per peer)"},
+            "distinct": {"query": "GO 3 STEPS FROM <root> OVER e WHERE e.w < 50 YIELD DISTINCT e.w",
                          "p50_ms": float(np.percentile(np.array(lat) * 1e3, 50)), "queries": len(lat),
                          "host_agreements": a1 - a0},
             "input_props": {"query": "GO 3 STEPS FROM $-.id (2 roots) OVER e WHERE e.w < 50 YIELD DISTINCT $-.tag",
