@@ -164,7 +164,8 @@ struct ChArgs {         // device memory (indexed at run time: never a by-value 
   int64_t type;
   const uint8_t* visible;
   const int64_t* vids;
-  uint32_t* lab[3];                    // forward, backward, B-set (LAB_M)
+  uint32_t* lab[3];                    // forward, backward, B-set (LAB_M): words 0, 1, 2 of each
+                                       // vertex's CH_LAB_WORDS-word record (index lrec(v))
   ChList list[CH_NLISTS];
   uint64_t list_cap, tsplit_cap;
   uint64_t nv, ne[2];                  // vertices, edges per direction (bounds of the checked build)
@@ -321,6 +322,8 @@ __device__ __forceinline__ void gst(T* p, uint64_t i, uint64_t n, T v, int site,
 
 __device__ __forceinline__ uint32_t stamp_of(uint32_t epoch, uint32_t level) { return (epoch << LVL_BITS) | level; }
 __device__ __forceinline__ bool live(uint32_t lab, uint32_t epoch) { return (lab >> LVL_BITS) == epoch; }
+// word v of a label array: a vertex's three labels are one record (ChArgs::lab)
+__device__ __forceinline__ uint64_t lrec(uint64_t v) { return v * CH_LAB_WORDS; }
 __device__ __forceinline__ unsigned long long ld_agent(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -479,8 +482,8 @@ __device__ __forceinline__ ChSnap first_snap(const ChArgs& A, const ChQ& q, ChFi
 __device__ __forceinline__ void first_store(const ChArgs& A, const ChQ& q, const ChFirst& f, const ChSnap& s) {
   ChState* st = A.st;
   st->snap[0] = s;
-  A.lab[0][q.s] = stamp_of(q.ef, 0);
-  A.lab[1][q.t] = stamp_of(q.eb, 0);
+  A.lab[0][lrec(q.s)] = stamp_of(q.ef, 0);
+  A.lab[1][lrec(q.t)] = stamp_of(q.eb, 0);
   const ChList& F = A.list[CL_F0];
   F.ids[0] = q.s;
   F.seg_end[0] = f.dsf;
@@ -701,7 +704,7 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
       uint32_t tl[VT], vis[VT];
 #pragma unroll
       for (int j = 0; j < VT; ++j) {
-        tl[j] = x[j] != NO_ROW ? gld(tlab, x[j], A.nv, 6, st) : 0u;
+        tl[j] = x[j] != NO_ROW ? gld(tlab, lrec(x[j]), lrec(A.nv), 6, st) : 0u;
         vis[j] = x[j] != NO_ROW && A.visible ? gld(A.visible, x[j], A.nv, 6, st) : 1u;
       }
 #pragma unroll
@@ -720,13 +723,13 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
     uint32_t sol[VT], sdg[VT], srs[VT];
 #pragma unroll
     for (int j = 0; j < VT; ++j) {
-      old[j] = c[j] != NO_ROW ? gld(lab, c[j], A.nv, 8, st) : 0u;
-      gate[j] = (c[j] != NO_ROW && rlab) ? gld(rlab, c[j], A.nv, 8, st) : rstamp;
+      old[j] = c[j] != NO_ROW ? gld(lab, lrec(c[j]), lrec(A.nv), 8, st) : 0u;
+      gate[j] = (c[j] != NO_ROW && rlab) ? gld(rlab, lrec(c[j]), lrec(A.nv), 8, st) : rstamp;
       sol[j] = 0;
       sdg[j] = 0;
       srs[j] = 0;
       if (spec && c[j] != NO_ROW) {
-        sol[j] = gld(olab, c[j], A.nv, 9, st);
+        sol[j] = gld(olab, lrec(c[j]), lrec(A.nv), 9, st);
         sdg[j] = vdeg_spec(A, oside, c[j], &srs[j]);
       }
       if (first) {   // (the stores of these labels may still be in flight)
@@ -740,14 +743,14 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
       uint32_t ol[VT];
 #pragma unroll
       for (int j = 0; j < VT; ++j) {
-        ol[j] = (c[j] != NO_ROW && !live(old[j], epoch)) ? gld(olab, c[j], A.nv, 9, st) : 0u;
+        ol[j] = (c[j] != NO_ROW && !live(old[j], epoch)) ? gld(olab, lrec(c[j]), lrec(A.nv), 9, st) : 0u;
         if (first && c[j] == f_other) ol[j] = stamp_of(oepoch, 0);
       }
 #pragma unroll
       for (int j = 0; j < VT; ++j) {
         if (c[j] == NO_ROW || live(old[j], epoch) || !live(ol[j], oepoch)) continue;
         if (CH_GUARD && c[j] >= A.nv) continue;
-        if (atomicCAS(lab + c[j], old[j], stamp) != old[j]) continue;
+        if (atomicCAS(lab + lrec(c[j]), old[j], stamp) != old[j]) continue;
         mm |= 1u << j;
       }
     } else {
@@ -755,7 +758,7 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
       for (int j = 0; j < VT; ++j) {
         if (c[j] == NO_ROW || gate[j] != rstamp || live(old[j], epoch)) continue;
         if (CH_GUARD && c[j] >= A.nv) continue;
-        if (atomicCAS(lab + c[j], old[j], stamp) != old[j]) continue;
+        if (atomicCAS(lab + lrec(c[j]), old[j], stamp) != old[j]) continue;
         cm |= 1u << j;
       }
     }
@@ -778,7 +781,7 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
         // returns the earlier one's tag (a relaxed RMW reads the latest value of its location; a
         // re-read of the other side's label after our own CAS would be the two-address store-buffer
         // pattern, which the memory model lets both claimers miss)
-        const uint32_t prev = atomicExch(A.lab[2] + c[j], mytag);
+        const uint32_t prev = atomicExch(A.lab[2] + lrec(c[j]), mytag);
         if (prev == otag) m2 |= 1u << j;
       }
       if (__ballot(m2 != 0)) {
@@ -787,7 +790,7 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
         for (int j = 0; j < VT; ++j)
           if ((m2 >> j) & 1u) {
             // (the one claimer that saw the other's tag; after both exchanges, so the stamp stays)
-            __hip_atomic_store(A.lab[2] + c[j], l2m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(A.lab[2] + lrec(c[j]), l2m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             ++n2;
           }
 #pragma unroll
@@ -821,7 +824,7 @@ __device__ __forceinline__ void ch_level(const ChArgs& A, const ChQ& q, const Ch
       dg[j] = 0;
       rs[j] = 0;
       if ((mm >> j) & 1u) {
-        gst(A.lab[2], c[j], A.nv, mstamp, 10, st);
+        gst(A.lab[2], lrec(c[j]), lrec(A.nv), mstamp, 10, st);
         dg[j] = vdeg(A, 1, c[j], &rs[j]);
         ++nm;
       }
@@ -967,7 +970,7 @@ __device__ __forceinline__ Cand hop_scan(const ChArgs& A, const uint32_t* vlab, 
       rk[u] = in && A.rank ? gld(A.rank, j, A.ne[0], 13, A.st) : 0;
     }
 #pragma unroll
-    for (int u = 0; u < CH_HOP_U; ++u) lv[u] = wv[u] != NO_ROW ? gld(vlab, wv[u], A.nv, 12, A.st) : 0u;
+    for (int u = 0; u < CH_HOP_U; ++u) lv[u] = wv[u] != NO_ROW ? gld(vlab, lrec(wv[u]), lrec(A.nv), 12, A.st) : 0u;
 #pragma unroll
     for (int u = 0; u < CH_HOP_U; ++u) {
       if (wv[u] == NO_ROW || lv[u] != want) continue;
@@ -1895,7 +1898,7 @@ hipError_t chain_roll(const ChainSlot* slots, int nslots, const SpTypes& fwd, co
   r.tag0 = B.tag_next;
   B.tag_next += n;
   r.upto = upto;
-  r.both = getenv("NBG_SP_ROLL_BOTH") ? (uint32_t)strtoul(getenv("NBG_SP_ROLL_BOTH"), nullptr, 10) : c0->both;
+  r.both = c0->both;
   // (read per run, as the fixed batches read theirs per batch).  RMAT-26, 10 k pairs
   // (profiles/r06_i_sp_roll_grid_vt.txt, r06_j_*): 4-item tiles on 1024 workgroups 50.6-54.9 k
   // pairs/s against 44.6-45.0 k with the fixed batches' 2-item tiles on 512 (8-item tiles 47.6-49.1 k)
