@@ -468,6 +468,11 @@ inline std::string sp_err_text(unsigned long long err) {
   if (err & 4) return "a frontier list's merge-path split did not describe its tile (code " + std::to_string(err) + ")";
   return "device search aborted (code " + std::to_string(err) + ")";
 }
+// A vertex's forward, backward and B-set labels (epoch << LVL_BITS | level) are one 16-byte
+// record: a BFS claim tests its own side's label and the other side's, a B-set step the forward
+// label and LAB_M, so each item's label tests touch one line, not two or three (sp.hip allocates
+// (nv + 1) records; SpCtx::lab[i] points at word i of record 0)
+constexpr uint32_t CH_LAB_WORDS = 4;
 struct SpCtx;                        // labels and level-loop buffers of one slot (sp.hip)
 // item_cap: items a list may hold = sum over a side's types of (nv + E_t / 64), plus slack
 // One query at a time per context; the level-loop buffers are allocated on its first use.

@@ -28,11 +28,14 @@ struct SpCtx {
   hipStream_t stream = nullptr;
   uint64_t nv = 0, cap = 0, edge_cap = 0;
   ChainCtx* chain = nullptr;       // the level-loop buffers (first query)
-  uint32_t* lab[3] = {};           // forward, backward, B-set labels (epoch << LVL_BITS | level)
+  uint32_t* lab_rec = nullptr;     // (nv + 1) label records of CH_LAB_WORDS words
+  uint32_t* lab[3] = {};           // forward, backward, B-set labels: words 0, 1, 2 of the records
   uint32_t epoch = 0;
   hipEvent_t done = nullptr;
   int prof = 0;                    // nbg_profile mode, applied to the chain when it is created
 };
+
+static size_t lab_bytes(uint64_t nv) { return (size_t)(nv + 1) * CH_LAB_WORDS * 4; }
 
 hipError_t sp_reserve_chain(SpCtx* c) {
   if (c->chain) return hipSuccess;
@@ -60,11 +63,10 @@ SpCtx* sp_create(uint64_t nv, uint64_t item_cap, uint64_t edge_cap, hipStream_t 
   c->cap = item_cap;
   c->edge_cap = edge_cap;
   hipError_t he = hipSuccess;
-  for (auto& l : c->lab)
-    if (he == hipSuccess) he = hipMalloc((void**)&l, (nv + 1) * 4);
+  he = hipMalloc((void**)&c->lab_rec, lab_bytes(nv));
+  for (int i = 0; i < 3 && he == hipSuccess; ++i) c->lab[i] = c->lab_rec + i;
   if (he == hipSuccess) he = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
-  for (auto& l : c->lab)
-    if (he == hipSuccess) he = hipMemsetAsync(l, 0, (nv + 1) * 4, s);
+  if (he == hipSuccess) he = hipMemsetAsync(c->lab_rec, 0, lab_bytes(nv), s);
   if (he == hipSuccess) he = hipStreamSynchronize(s);
   if (he != hipSuccess) {
     if (err) *err = std::string("shortest-path workspace: ") + hipGetErrorString(he);
@@ -76,8 +78,7 @@ SpCtx* sp_create(uint64_t nv, uint64_t item_cap, uint64_t edge_cap, hipStream_t 
 
 void sp_destroy(SpCtx* c) {
   if (!c) return;
-  for (auto* l : c->lab)
-    if (l) (void)hipFree(l);
+  if (c->lab_rec) (void)hipFree(c->lab_rec);
   chain_destroy(c->chain);
   if (c->done) (void)hipEventDestroy(c->done);
   delete c;
@@ -87,7 +88,7 @@ static hipError_t next_epoch(SpCtx* c) {
   // wrap (clear the labels once) below 2^24: spchain.hip's same-launch meet tags use the epochs
   // with bit 24 or 25 set
   if (++c->epoch >= (1u << 24)) {
-    for (auto* l : c->lab) HIP_TRY_SP(hipMemsetAsync(l, 0, (c->nv + 1) * 4, c->stream));
+    HIP_TRY_SP(hipMemsetAsync(c->lab_rec, 0, lab_bytes(c->nv), c->stream));
     c->epoch = 1;
   }
   return hipSuccess;
@@ -135,7 +136,7 @@ hipError_t sp_roll(SpCtx* const* cs, int nslots, const SpTypes& fwd, const SpTyp
     if (c->stream != cs[0]->stream) return hipErrorInvalidValue;
     HIP_TRY_SP(sp_reserve_chain(c));
     if (c->epoch + n + 2 >= (1u << 24)) {
-      for (auto* lb : c->lab) HIP_TRY_SP(hipMemsetAsync(lb, 0, (c->nv + 1) * 4, c->stream));
+      HIP_TRY_SP(hipMemsetAsync(c->lab_rec, 0, lab_bytes(c->nv), c->stream));
       c->epoch = 0;
     }
     sl[l] = ChainSlot{c->chain, c->lab, c->epoch};
