@@ -317,7 +317,8 @@ def shortest_path_leg(eng, pairs, args, barrier, batch=True, light=False):
     """FIND SHORTEST PATH FROM s TO t OVER e UPTO n STEPS, one query per pair (C4).  light: the
     latency pass only (a partitioned engine without a replica, where every pair is collective)."""
     if not args.sync:   # shortest-path contexts allocated now (start-up), not inside the first timed query
-        eng.path_reserve(int(os.environ.get("NBG_QUERY_SLOTS", "6")), int(os.environ.get("NBG_SP_BATCH", "32")))
+        # (the batch contexts: as many as the library's NBG_SP_BATCH default, path.cpp sp_batch_size)
+        eng.path_reserve(int(os.environ.get("NBG_QUERY_SLOTS", "6")), 64)
     for s, t in pairs[:16]:   # warm-up
         eng.find_path([s], [t], [1], args.sp_upto)
     # the requests are input: their C structs are built before the clock, and each query is one
@@ -397,7 +398,7 @@ def shortest_path_leg(eng, pairs, args, barrier, batch=True, light=False):
                 b_found += eng.lib.nbg_paths_count(bouts[i]) > 0
                 b_paths.append(eng._paths(C.c_void_p(bouts[i]), None))   # (frees it)
         got["batched"] = b_paths
-        batched = {"batch": int(os.environ.get("NBG_SP_BATCH", "32")), "pairs_per_s": len(pairs) / b_el if b_el else None,
+        batched = {"batch": int(os.environ.get("NBG_SP_BATCH", "48")), "pairs_per_s": len(pairs) / b_el if b_el else None,
                    "teps": b_edges / b_el if b_el else None, "seconds": round(b_el, 3), "found": b_found,
                    "timing": f"nbg_find_path_batch over the same pairs, {chunk} requests per call (request "
                              f"arrays built before the clock; results left in their nbg_paths)"}

@@ -319,20 +319,22 @@ int32_t nbg_find_path_wait(nbg_path_ticket* ticket, nbg_paths** out);
 /* n independent FIND PATH requests at once (a graphd serving many FindPathExecutor queries,
  * src/graph/FindPathExecutor.cpp:145-411, each with its own result): out[i] / rcs[i] receive
  * request i's paths (free each with nbg_paths_free; NULL when rcs[i] != NBG_OK) and status.
- * One-pair SHORTEST requests on a single engine run NBG_SP_BATCH (default 32, at most 32) at a
- * time as one batched device level loop (every launch serves the whole batch; each of the batch's
- * workspaces holds 3 label arrays and 5 list buffers of nv entries); other requests run as
- * nbg_find_path would.  Results equal nbg_find_path's.  Every request gets its status in rcs[i]
- * (out[i] is NULL exactly when rcs[i] != NBG_OK), also when the batch itself fails part way (the
- * requests that did not run carry that failure's code).  Returns NBG_OK unless the batch itself
- * could not run (arguments, device set-up).  The batched chains use as many per-pair contexts
- * (~72 B per vertex each) as NBG_SP_BATCH asks for and HBM allows. */
+ * One-pair SHORTEST requests on a single engine (UPTO <= 32) run as rolling device runs over
+ * NBG_SP_BATCH (default 48, at most 64) contexts: every launch serves every context, and a
+ * context takes the next queued pair as soon as its pair is done (UPTO over 32: fixed batches of
+ * at most 32).  Each context holds a 16-byte label record and 5 list buffers per vertex (~76 B
+ * per vertex plus tile splits: ~3.2 GB at RMAT-26); as many are used as HBM allows.  Other
+ * requests run as nbg_find_path would.  Results equal nbg_find_path's.  Every request gets its
+ * status in rcs[i] (out[i] is NULL exactly when rcs[i] != NBG_OK), also when the batch itself
+ * fails part way (the requests that did not run carry that failure's code).  Returns NBG_OK
+ * unless the batch itself could not run (arguments, device set-up). */
 int32_t nbg_find_path_batch(nbg_engine* e, const nbg_path_request* reqs, uint64_t n, nbg_paths** out,
                             int32_t* rcs);
 /* Allocate the one-pair SHORTEST contexts now instead of at their first query (what a server
  * does at start-up): the engine's own, `slots` of nbg_find_path_submit's (at most NBG_QUERY_SLOTS)
- * and `batch` of nbg_find_path_batch's (at most NBG_SP_BATCH).  Each context holds ~72 B per
- * vertex plus its level-loop lists.  No-op on a partitioned engine. */
+ * and `batch` of nbg_find_path_batch's (at most NBG_SP_BATCH; as many as fit in HBM, at least
+ * one, else NBG_E_OUT_OF_MEMORY).  Each context holds ~76 B per vertex plus its lists' tile
+ * splits.  No-op on a partitioned engine. */
 int32_t nbg_path_reserve(nbg_engine* e, int32_t slots, int32_t batch);
 int64_t nbg_paths_count(const nbg_paths* p);
 int64_t nbg_path_len(const nbg_paths* p, int64_t i);

@@ -796,7 +796,9 @@ nbg_paths* paths_of(const SpResult& r) {
 int sp_batch_size() {
   static const int n = [] {
     const char* v = getenv("NBG_SP_BATCH");
-    const int k = v ? atoi(v) : 32;   // RMAT-22: 16 -> 35.6 k, 32 -> 44.8 k pairs/s
+    // RMAT-22 fixed batches: 16 -> 35.6 k, 32 -> 44.8 k pairs/s; RMAT-26 rolling runs: 32 -> 55.9 k,
+    // 48 -> 60.3 k (profiles/r06_y_sp_slots_ab.txt; 64 contexts of ~3.2 GB do not fit beside the graph)
+    const int k = v ? atoi(v) : 48;
     return k < 1 ? 1 : (k > CH_ROLL_SLOTS ? CH_ROLL_SLOTS : k);
   }();
   return n;
@@ -947,9 +949,14 @@ int32_t nbg_find_path_batch(nbg_engine* h, const nbg_path_request* reqs, uint64_
   // allows — a context that cannot be allocated only makes the batches smaller
   const int want = std::min<int>(sp_batch_size(), (int)pl.size());
   std::string cerr;
-  while ((int)E.batch_sp.size() < want) {
+  while ((int)E.batch_sp.size() < want) {   // (with its level-loop buffers: a run allocates nothing)
     SpCtx* c = E.new_sp(E.batch_stream, &cerr);
     if (!c) break;
+    if (sp_reserve_chain(c) != hipSuccess) {
+      sp_destroy(c);
+      cerr = "shortest-path chain buffers";
+      break;
+    }
     E.batch_sp.push_back(c);
   }
   if (E.batch_sp.empty()) return fail_rest(E.fail(NBG_E_OUT_OF_MEMORY, cerr));
@@ -1055,14 +1062,18 @@ int32_t nbg_path_reserve(nbg_engine* h, int32_t slots, int32_t batch) {
   const int want = std::min(batch, sp_batch_size());
   if (want > 0 && !E.batch_stream && hipStreamCreateWithFlags(&E.batch_stream, hipStreamNonBlocking) != hipSuccess)
     return E.fail(NBG_E_DEVICE, "hipStreamCreate failed");
+  // (batch contexts as HBM allows, as nbg_find_path_batch allocates them: one that does not fit
+  // only makes the rolling runs narrower)
   while ((int)E.batch_sp.size() < want) {
-    SpCtx* c = nullptr;
-    if (int32_t rc = ready(c, E.batch_stream)) {
-      if (c) sp_destroy(c);
-      return rc;
+    SpCtx* c = E.new_sp(E.batch_stream, &err);
+    if (!c) break;
+    if (sp_reserve_chain(c) != hipSuccess) {
+      sp_destroy(c);
+      break;
     }
     E.batch_sp.push_back(c);
   }
+  if (want > 0 && E.batch_sp.empty()) return E.fail(NBG_E_OUT_OF_MEMORY, "shortest-path batch contexts");
   return NBG_OK;
 }
 

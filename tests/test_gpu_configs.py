@@ -187,7 +187,7 @@ def test_c4_shortest_pairs_rmat26(rmat26, sp_mode):
 
 @pytest.mark.timeout(600)
 def test_c4_batched_pairs_rmat26(rmat26):
-    """nbg_find_path_batch at the C4 size: 96 pairs as one rolling run over 32 slots (the bench's
+    """nbg_find_path_batch at the C4 size: 96 pairs as one rolling run over 48 slots (the bench's
     throughput pass), every path and edge count equal to the one-at-a-time query's."""
     src, dst, eng, csr, _, av = rmat26
     pairs = rmat.pick_pairs(src, dst, 96, 7, verts=av)
@@ -206,7 +206,7 @@ def test_c4_batched_pairs_rmat26(rmat26):
 @pytest.mark.parametrize("job_wait", [None, "0"], ids=["jobs", "unanswered"])
 def test_c4_rmat26_bench_pairs_every_pass(rmat26, job_wait, monkeypatch):
     """C4 at full size on the timing-dependent paths: the bench's first 1,200 SHORTEST pairs
-    (RMAT-26, seed 7, UPTO 5) one at a time, six in flight and batched (rolling over 32 and over 7
+    (RMAT-26, seed 7, UPTO 5) one at a time, six in flight and batched (rolling over 48 and over 7
     slots, and fixed batches), every result entry by entry
     against orc_csr_shortest_many.  With NBG_SP_JOB_WAIT=0 no hub job of a one-pair chain is ever
     answered, so every hub on a walk falls back to the next launch's spread scan or a continuation.
@@ -231,7 +231,7 @@ def test_c4_rmat26_bench_pairs_every_pass(rmat26, job_wait, monkeypatch):
     got += [eng.find_path_wait(tk) for tk in pending]
     assert got == want
     reqs = [([s], [t], [1], 5, True) for s, t in pairs]
-    assert eng.find_path_batch(reqs) == want   # rolling runs (k_ch_roll)
+    assert eng.find_path_batch(reqs) == want   # rolling runs (k_ch_roll, 48 slots)
     monkeypatch.setenv("NBG_SP_ROLL_SLOTS", "7")
     assert eng.find_path_batch(reqs) == want   # every slot refilled ~170 times
     monkeypatch.setenv("NBG_SP_ROLL", "0")

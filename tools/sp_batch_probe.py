@@ -22,7 +22,7 @@ eng.finalize()
 _, av = rmat.vertex_sets(scale)
 pairs = rmat.pick_pairs(src, dst, 10000, 7, verts=av)[:npairs]
 del src, dst, w
-eng.path_reserve(6, 32)
+eng.path_reserve(6, 64)   # (the library's NBG_SP_BATCH contexts)
 reqs = [([s], [t], [1], 5, True) for s, t in pairs]
 chunk = 2000
 preps = [eng.path_batch_prepare(reqs[k:k + chunk]) for k in range(0, len(reqs), chunk)]
