@@ -1570,7 +1570,10 @@ struct ChainCtx {
   // 0.109-0.113 at 128 (profiles/r03_vt3_sp_grid_ab.txt, r03_fin2_sp_vt2_batch_ab.txt).
   // NBG_SP_GRID overrides.
   unsigned grid = 256;
-  uint32_t both = 16384;           // ChQ::both_items (NBG_SP_BOTH; 0: one side per level)
+  // ChQ::both_items (NBG_SP_BOTH; 0: one side per level).  RMAT-26 10 k pairs, round 6 (label
+  // records): 16384 -> 32768 p50 0.0746-0.0748 -> 0.0736-0.0739 ms, p99 0.212-0.213 -> 0.210-0.212,
+  // 65536 no better (profiles/r06_ae_sp_both_threshold_ab.txt)
+  uint32_t both = 32768;
   // the query in flight: what has been enqueued
   ChQ q{};
   int steps = 0, hops = 0;
