@@ -381,6 +381,9 @@ def shortest_path_leg(eng, pairs, args, barrier, batch=True, light=False):
     # batched pass: nbg_find_path_batch, one-pair queries NBG_SP_BATCH at a time per device chain
     batched = None
     if batch and not args.sync:
+        # warm-up (as the one-pair passes'): one run that gives every batch context a pair, so each
+        # has its CSR arguments and its records' topology words before the clock
+        eng.find_path_batch([([s], [t], [1], args.sp_upto, True) for s, t in pairs[:128]])
         chunk = 2000
         preps = [eng.path_batch_prepare([([s], [t], [1], args.sp_upto, True) for s, t in pairs[k:k + chunk]])
                  for k in range(0, len(pairs), chunk)]   # the requests: input, built before the clock

@@ -51,6 +51,7 @@ struct Engine {
   // nbg_find_path_batch: one-pair SHORTEST queries run NBG_SP_BATCH at a time as one batched
   // launch chain, on workspaces sharing one stream
   std::vector<SpCtx*> batch_sp;
+  bool batch_sp_full = false;     // the last growth stopped at the HBM reserve (nbg_path_reserve retries)
   hipStream_t batch_stream = nullptr;
   uint64_t max_dict_len = 0;            // the longest dictionary string (derived-string arena bound),
   uint64_t max_dict_len_of = ~0ull;     //   computed for a dictionary of this many strings

@@ -884,6 +884,39 @@ int32_t nbg_find_path_submit(nbg_engine* h, const nbg_path_request* rq, nbg_path
   return NBG_OK;
 }
 
+// Batch contexts (with their level-loop buffers: a run allocates nothing) up to `want`, as HBM
+// allows while leaving NBG_SP_BATCH_RESERVE_GB (default 8) free for the engine's other queries: a
+// context that does not fit only makes the rolling runs narrower.  A growth that stopped short is
+// retried by nbg_path_reserve only, not by every batch (each try allocates and frees gigabytes).
+static void grow_batch_contexts(Engine& E, int want, std::string* err, bool retry) {
+  if (E.batch_sp_full && !retry) return;   // (not every batch: a failed growth allocates and frees GBs)
+  E.batch_sp_full = false;
+  static const double reserve_gb = getenv("NBG_SP_BATCH_RESERVE_GB") ? atof(getenv("NBG_SP_BATCH_RESERVE_GB")) : -1.0;
+  while ((int)E.batch_sp.size() < want) {
+    SpCtx* c = E.new_sp(E.batch_stream, err);
+    if (!c) {
+      E.batch_sp_full = true;
+      break;
+    }
+    size_t free_b = 0, total_b = 0;
+    const bool ok = sp_reserve_chain(c) == hipSuccess && hipMemGetInfo(&free_b, &total_b) == hipSuccess;
+    const double reserve = (reserve_gb >= 0 ? reserve_gb : 8.0) * (1ull << 30);
+    if (!ok || (!E.batch_sp.empty() && (double)free_b < reserve)) {
+      sp_destroy(c);
+      if (!ok && err) *err = "shortest-path chain buffers";
+      E.batch_sp_full = true;
+      break;
+    }
+    E.batch_sp.push_back(c);
+  }
+  if (getenv("NBG_SP_TRACE")) {
+    size_t free_b = 0, total_b = 0;
+    (void)hipMemGetInfo(&free_b, &total_b);
+    fprintf(stderr, "[sp batch] %zu contexts (wanted %d), %.1f GB of HBM free\n", E.batch_sp.size(), want,
+            free_b / 1073741824.0);
+  }
+}
+
 int32_t nbg_find_path_batch(nbg_engine* h, const nbg_path_request* reqs, uint64_t n, nbg_paths** out, int32_t* rcs) {
   if (!h || (n && (!reqs || !out || !rcs))) return NBG_E_INVALID_ARGUMENT;
   Engine& E = *h->e.path_engine();
@@ -949,16 +982,7 @@ int32_t nbg_find_path_batch(nbg_engine* h, const nbg_path_request* reqs, uint64_
   // allows — a context that cannot be allocated only makes the batches smaller
   const int want = std::min<int>(sp_batch_size(), (int)pl.size());
   std::string cerr;
-  while ((int)E.batch_sp.size() < want) {   // (with its level-loop buffers: a run allocates nothing)
-    SpCtx* c = E.new_sp(E.batch_stream, &cerr);
-    if (!c) break;
-    if (sp_reserve_chain(c) != hipSuccess) {
-      sp_destroy(c);
-      cerr = "shortest-path chain buffers";
-      break;
-    }
-    E.batch_sp.push_back(c);
-  }
+  grow_batch_contexts(E, want, &cerr, false);
   if (E.batch_sp.empty()) return fail_rest(E.fail(NBG_E_OUT_OF_MEMORY, cerr));
   const int B = std::min<int>(want, (int)E.batch_sp.size());
   auto finish = [&](size_t k, const SpResult& r) {
@@ -1064,15 +1088,7 @@ int32_t nbg_path_reserve(nbg_engine* h, int32_t slots, int32_t batch) {
     return E.fail(NBG_E_DEVICE, "hipStreamCreate failed");
   // (batch contexts as HBM allows, as nbg_find_path_batch allocates them: one that does not fit
   // only makes the rolling runs narrower)
-  while ((int)E.batch_sp.size() < want) {
-    SpCtx* c = E.new_sp(E.batch_stream, &err);
-    if (!c) break;
-    if (sp_reserve_chain(c) != hipSuccess) {
-      sp_destroy(c);
-      break;
-    }
-    E.batch_sp.push_back(c);
-  }
+  grow_batch_contexts(E, want, &err, true);
   if (want > 0 && E.batch_sp.empty()) return E.fail(NBG_E_OUT_OF_MEMORY, "shortest-path batch contexts");
   return NBG_OK;
 }
