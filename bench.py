@@ -401,7 +401,7 @@ def shortest_path_leg(eng, pairs, args, barrier, batch=True, light=False):
                 b_found += eng.lib.nbg_paths_count(bouts[i]) > 0
                 b_paths.append(eng._paths(C.c_void_p(bouts[i]), None))   # (frees it)
         got["batched"] = b_paths
-        batched = {"batch": int(os.environ.get("NBG_SP_BATCH", "48")), "pairs_per_s": len(pairs) / b_el if b_el else None,
+        batched = {"batch": eng.stats()["path_batch_contexts"], "reruns": eng.stats()["path_batch_reruns"], "pairs_per_s": len(pairs) / b_el if b_el else None,
                    "teps": b_edges / b_el if b_el else None, "seconds": round(b_el, 3), "found": b_found,
                    "timing": f"nbg_find_path_batch over the same pairs, {chunk} requests per call (request "
                              f"arrays built before the clock; results left in their nbg_paths)"}

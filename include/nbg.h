@@ -163,6 +163,9 @@ typedef struct {
                                  carry them in band                                              */
   uint64_t host_bytes;        /* host memory the finalized engine keeps beside its snapshot (row
                                  offsets, dictionary, the tiny path's walk bounds)               */
+  uint64_t path_batch_contexts;  /* nbg_find_path_batch's contexts (rolling-run slots)          */
+  uint64_t path_batch_reruns;    /* batched pairs whose search outgrew a context's lists and ran
+                                    again on the engine's full-size one                          */
 } nbg_stats;
 int32_t nbg_get_stats(const nbg_engine* e, nbg_stats* out);
 
@@ -320,10 +323,11 @@ int32_t nbg_find_path_wait(nbg_path_ticket* ticket, nbg_paths** out);
  * src/graph/FindPathExecutor.cpp:145-411, each with its own result): out[i] / rcs[i] receive
  * request i's paths (free each with nbg_paths_free; NULL when rcs[i] != NBG_OK) and status.
  * One-pair SHORTEST requests on a single engine (UPTO <= 32) run as rolling device runs over
- * NBG_SP_BATCH (default 48, at most 64) contexts: every launch serves every context, and a
+ * NBG_SP_BATCH (default 64, at most 64) contexts: every launch serves every context, and a
  * context takes the next queued pair as soon as its pair is done (UPTO over 32: fixed batches of
- * at most 32).  Each context holds a 16-byte label record and 5 list buffers per vertex (~76 B
- * per vertex plus tile splits: ~3.2 GB at RMAT-26); as many are used as HBM allows.  Other
+ * at most 32).  Each context holds a 16-byte label record per vertex and 5 lists of a quarter of
+ * the vertices (NBG_SP_BATCH_LIST; ~1.2 GB at RMAT-26; a pair outgrowing them runs again on the
+ * engine's full-size context, nbg_stats.path_batch_reruns); as many are made as HBM allows.  Other
  * requests run as nbg_find_path would.  Results equal nbg_find_path's.  Every request gets its
  * status in rcs[i] (out[i] is NULL exactly when rcs[i] != NBG_OK), also when the batch itself
  * fails part way (the requests that did not run carry that failure's code).  Returns NBG_OK
@@ -333,8 +337,8 @@ int32_t nbg_find_path_batch(nbg_engine* e, const nbg_path_request* reqs, uint64_
 /* Allocate the one-pair SHORTEST contexts now instead of at their first query (what a server
  * does at start-up): the engine's own, `slots` of nbg_find_path_submit's (at most NBG_QUERY_SLOTS)
  * and `batch` of nbg_find_path_batch's (at most NBG_SP_BATCH; as many as fit in HBM, at least
- * one, else NBG_E_OUT_OF_MEMORY).  Each context holds ~76 B per vertex plus its lists' tile
- * splits.  No-op on a partitioned engine. */
+ * one, else NBG_E_OUT_OF_MEMORY).  A one-pair context holds ~76 B per vertex plus its lists' tile
+ * splits, a batch context ~31 B.  No-op on a partitioned engine. */
 int32_t nbg_path_reserve(nbg_engine* e, int32_t slots, int32_t batch);
 int64_t nbg_paths_count(const nbg_paths* p);
 int64_t nbg_path_len(const nbg_paths* p, int64_t i);

@@ -47,7 +47,8 @@ class nbg_column_def(C.Structure):
 class nbg_stats(C.Structure):
     _fields_ = [("num_vertices", u64), ("num_edges", u64), ("device_bytes", u64),
                 ("num_edge_types", i32), ("reserved", i32), ("tiny_queries", u64),
-                ("host_agreements", u64), ("host_bytes", u64)]
+                ("host_agreements", u64), ("host_bytes", u64), ("path_batch_contexts", u64),
+                ("path_batch_reruns", u64)]
 
 
 class nbg_kernel_stat(C.Structure):

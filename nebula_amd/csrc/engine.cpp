@@ -1864,6 +1864,8 @@ int32_t nbg_get_stats(const nbg_engine* h, nbg_stats* out) {
   out->num_edge_types = (int32_t)E.snap.types.size();
   out->tiny_queries = E.tiny_queries;
   out->host_agreements = E.host_agreements;
+  out->path_batch_contexts = E.batch_sp.size();
+  out->path_batch_reruns = E.batch_reruns;
   uint64_t hb = 0;
   for (const std::string& x : E.snap.strings) hb += x.size() + sizeof(std::string);
   for (auto& kv : E.snap.types)

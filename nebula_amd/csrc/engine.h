@@ -52,6 +52,7 @@ struct Engine {
   // launch chain, on workspaces sharing one stream
   std::vector<SpCtx*> batch_sp;
   bool batch_sp_full = false;     // the last growth stopped at the HBM reserve (nbg_path_reserve retries)
+  unsigned long long batch_reruns = 0;   // batched pairs rerun on `sp` after a list overflow
   hipStream_t batch_stream = nullptr;
   uint64_t max_dict_len = 0;            // the longest dictionary string (derived-string arena bound),
   uint64_t max_dict_len_of = ~0ull;     //   computed for a dictionary of this many strings

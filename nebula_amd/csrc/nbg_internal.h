@@ -493,7 +493,10 @@ struct SpPair {                 // one query of sp_launch_batch
 };
 hipError_t sp_launch_batch(SpCtx* const* cs, int n, const SpPair* pairs);
 struct ChainCtx;
-ChainCtx* chain_create(uint64_t nv, uint64_t edge_cap, hipStream_t s, std::string* err);
+// list_cap: entries each frontier / meet list holds (0: nv + 1, every vertex); a search that
+// would outgrow a smaller one fails with err 3 (list overflow) and its caller reruns it
+ChainCtx* chain_create(uint64_t nv, uint64_t edge_cap, hipStream_t s, std::string* err, uint64_t list_cap = 0);
+void sp_set_list_cap(SpCtx* c, uint64_t list_cap);   // before the level-loop buffers exist
 void chain_destroy(ChainCtx* c);
 hipError_t chain_launch(ChainCtx* c, const SpTypes& fwd, const SpTypes& bwd, const uint8_t* visible,
                         const int64_t* vids, uint32_t* const lab[3], uint32_t epoch, uint32_t s, uint32_t t,

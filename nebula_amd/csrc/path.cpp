@@ -798,7 +798,9 @@ int sp_batch_size() {
     const char* v = getenv("NBG_SP_BATCH");
     // RMAT-22 fixed batches: 16 -> 35.6 k, 32 -> 44.8 k pairs/s; RMAT-26 rolling runs: 32 -> 55.9 k,
     // 48 -> 60.3 k (profiles/r06_y_sp_slots_ab.txt; 64 contexts of ~3.2 GB do not fit beside the graph)
-    const int k = v ? atoi(v) : 48;
+    // (64 with quarter-size lists, batch_list_cap: 61.4-62.0 k -> 63.4-64.2 k pairs/s, 87 GB of HBM
+    // left free against 42 GB with 48 full-size contexts, profiles/r06_ap_sp_batch_lists_ab.txt)
+    const int k = v ? atoi(v) : 64;
     return k < 1 ? 1 : (k > CH_ROLL_SLOTS ? CH_ROLL_SLOTS : k);
   }();
   return n;
@@ -884,6 +886,16 @@ int32_t nbg_find_path_submit(nbg_engine* h, const nbg_path_request* rq, nbg_path
   return NBG_OK;
 }
 
+// A batch context's list capacity: NBG_SP_BATCH_LIST (default 1/4, read when contexts are made) of
+// the vertices, at least 64 entries.  A pair whose search would outgrow it fails in the run with a
+// list overflow and is rerun on the engine's full-size context; the lists are most of a context's
+// memory (RMAT-26: 3.2 -> 1.2 GB per context), so 64 contexts take less HBM than 48 did.
+static uint64_t batch_list_cap(const Engine& E) {
+  const double frac = getenv("NBG_SP_BATCH_LIST") ? atof(getenv("NBG_SP_BATCH_LIST")) : 0.25;
+  const uint64_t nv = E.snap.nv;
+  return frac >= 1.0 || frac <= 0.0 ? 0 : std::max<uint64_t>(64, (uint64_t)((double)nv * frac) + 1);
+}
+
 // Batch contexts (with their level-loop buffers: a run allocates nothing) up to `want`, as HBM
 // allows while leaving NBG_SP_BATCH_RESERVE_GB (default 8) free for the engine's other queries: a
 // context that does not fit only makes the rolling runs narrower.  A growth that stopped short is
@@ -898,6 +910,7 @@ static void grow_batch_contexts(Engine& E, int want, std::string* err, bool retr
       E.batch_sp_full = true;
       break;
     }
+    sp_set_list_cap(c, batch_list_cap(E));
     size_t free_b = 0, total_b = 0;
     const bool ok = sp_reserve_chain(c) == hipSuccess && hipMemGetInfo(&free_b, &total_b) == hipSuccess;
     const double reserve = (reserve_gb >= 0 ? reserve_gb : 8.0) * (1ull << 30);
@@ -912,8 +925,9 @@ static void grow_batch_contexts(Engine& E, int want, std::string* err, bool retr
   if (getenv("NBG_SP_TRACE")) {
     size_t free_b = 0, total_b = 0;
     (void)hipMemGetInfo(&free_b, &total_b);
-    fprintf(stderr, "[sp batch] %zu contexts (wanted %d), %.1f GB of HBM free\n", E.batch_sp.size(), want,
-            free_b / 1073741824.0);
+    fprintf(stderr, "[sp batch] %zu contexts (wanted %d, lists of %llu entries), %.1f GB of HBM free; %llu pairs rerun so far\n",
+            E.batch_sp.size(), want, (unsigned long long)batch_list_cap(E), free_b / 1073741824.0,
+            (unsigned long long)E.batch_reruns);
   }
 }
 
@@ -985,8 +999,20 @@ int32_t nbg_find_path_batch(nbg_engine* h, const nbg_path_request* reqs, uint64_
   grow_batch_contexts(E, want, &cerr, false);
   if (E.batch_sp.empty()) return fail_rest(E.fail(NBG_E_OUT_OF_MEMORY, cerr));
   const int B = std::min<int>(want, (int)E.batch_sp.size());
-  auto finish = [&](size_t k, const SpResult& r) {
+  // a pair whose search outgrew its batch context's lists (err bit 2: list overflow; batch_list_cap)
+  // runs again on the engine's own full-size context
+  auto finish = [&](size_t k, SpResult r) -> hipError_t {
     const uint64_t i = at[k];
+    if (r.err & 2) {
+      const PairLaunch& x = pl[k];
+      std::string err;
+      if (!E.sp) E.sp = E.new_sp(E.stream, &err);
+      if (!E.sp) return hipErrorOutOfMemory;
+      hipError_t he = sp_launch(E.sp, x.fwd, x.bwd, E.snap.d_visible, E.snap.d_vids, x.s, x.t, x.upto, x.dmin);
+      if (he == hipSuccess) he = sp_wait(E.sp, &r);
+      if (he != hipSuccess) return he;
+      ++E.batch_reruns;
+    }
     ran[k] = 1;
     if (r.err == 1) {
       rcs[i] = E.fail(NBG_E_UNKNOWN, "shortest-path reconstruction failed (in/out edges disagree)");
@@ -995,6 +1021,7 @@ int32_t nbg_find_path_batch(nbg_engine* h, const nbg_path_request* reqs, uint64_
     } else {
       out[i] = paths_of(r);
     }
+    return hipSuccess;
   };
   // (read per call: the tests run both paths and small runs in one process)
   auto env_int = [](const char* k, int dflt) { return getenv(k) ? atoi(getenv(k)) : dflt; };
@@ -1021,7 +1048,8 @@ int32_t nbg_find_path_batch(nbg_engine* h, const nbg_path_request* reqs, uint64_
       if (hipError_t he = sp_roll(E.batch_sp.data(), slots, x.fwd, x.bwd, E.snap.d_visible, E.snap.d_vids, ss.data(),
                                   ts.data(), (uint32_t)m, x.upto, res.data()))
         return he;
-      for (size_t k = 0; k < m; ++k) finish(c0 + k, res[k]);
+      for (size_t k = 0; k < m; ++k)
+        if (hipError_t he = finish(c0 + k, res[k])) return he;
     }
     return hipSuccess;
   };
@@ -1040,7 +1068,7 @@ int32_t nbg_find_path_batch(nbg_engine* h, const nbg_path_request* reqs, uint64_
       for (int p = 0; p < nb && he == hipSuccess; ++p) {
         SpResult r;
         he = sp_wait(E.batch_sp[p], &r);
-        if (he == hipSuccess) finish(b0 + p, r);
+        if (he == hipSuccess) he = finish(b0 + p, r);
       }
       if (he != hipSuccess) return he;
     }

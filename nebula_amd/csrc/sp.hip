@@ -27,6 +27,7 @@ namespace nbg {
 struct SpCtx {
   hipStream_t stream = nullptr;
   uint64_t nv = 0, cap = 0, edge_cap = 0;
+  uint64_t list_cap = 0;           // the chain's list capacity (0: nv + 1)
   ChainCtx* chain = nullptr;       // the level-loop buffers (first query)
   uint32_t* lab_rec = nullptr;     // (nv + 1) label records of CH_LAB_WORDS words
   uint32_t* lab[3] = {};           // forward, backward, B-set labels: words 0, 1, 2 of the records
@@ -40,10 +41,14 @@ static size_t lab_bytes(uint64_t nv) { return (size_t)(nv + 1) * CH_LAB_WORDS * 
 hipError_t sp_reserve_chain(SpCtx* c) {
   if (c->chain) return hipSuccess;
   std::string err;
-  c->chain = chain_create(c->nv, c->edge_cap, c->stream, &err);
+  c->chain = chain_create(c->nv, c->edge_cap, c->stream, &err, c->list_cap);
   if (!c->chain) return hipErrorOutOfMemory;
   if (c->prof) chain_profile(c->chain, c->prof);
   return hipSuccess;
+}
+
+void sp_set_list_cap(SpCtx* c, uint64_t list_cap) {
+  if (c && !c->chain) c->list_cap = list_cap;
 }
 
 void sp_profile(SpCtx* c, int mode) {

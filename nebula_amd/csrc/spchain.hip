@@ -1622,11 +1622,11 @@ struct ChainCtx {
   }
 };
 
-ChainCtx* chain_create(uint64_t nv, uint64_t edge_cap, hipStream_t s, std::string* err) {
+ChainCtx* chain_create(uint64_t nv, uint64_t edge_cap, hipStream_t s, std::string* err, uint64_t list_cap) {
   auto* c = new ChainCtx();
   c->stream = s;
   c->nv = nv;
-  c->list_cap = nv + 1;
+  c->list_cap = list_cap && list_cap < nv + 1 ? list_cap : nv + 1;
   c->tsplit_cap = (nv + 1 + edge_cap) / CH_TILE_MIN + 2;
   const char* g = getenv("NBG_SP_GRID");
   if (g && atoi(g) > 0) c->grid = (unsigned)atoi(g);

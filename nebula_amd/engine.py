@@ -256,7 +256,8 @@ class Engine:
         self._check(self.lib.nbg_get_stats(self.h, C.byref(s)), "stats")
         return {"num_vertices": s.num_vertices, "num_edges": s.num_edges, "device_bytes": s.device_bytes,
                 "num_edge_types": s.num_edge_types, "tiny_queries": s.tiny_queries,
-                "host_agreements": s.host_agreements, "host_bytes": s.host_bytes}
+                "host_agreements": s.host_agreements, "host_bytes": s.host_bytes,
+                "path_batch_contexts": s.path_batch_contexts, "path_batch_reruns": s.path_batch_reruns}
 
     # ------------------------------------------------------------------ profiling
     def set_path_replica(self, mode: int):

@@ -367,3 +367,30 @@ def test_find_path_batch_matches_single(sp_mode, batch_env, monkeypatch):
     finally:
         eng.close()
         orc.close()
+
+
+def test_find_path_batch_list_overflow_reruns(monkeypatch):
+    """Batch contexts hold lists of NBG_SP_BATCH_LIST x nv entries (default 1/4); a search that
+    outgrows them fails in its rolling run with a list overflow and runs again on the engine's
+    full-size context.  Here the lists hold 64 entries on RMAT-11, so many pairs overflow: every
+    result still equals nbg_find_path's and the oracle's, and the reruns are counted."""
+    monkeypatch.setenv("NBG_SP_BATCH_LIST", "0.001")
+    src, dst, w = graphs.rmat_graph(11)
+    eng = graphs.rmat_engine(src, dst, w)
+    orc = graphs.rmat_oracle(src, dst, w)
+    try:
+        ps = rmat.pick_pairs(src, dst, 80, seed=31)
+        reqs = [([s], [t], [1], 5, True) for s, t in ps]
+        got = eng.find_path_batch(reqs)
+        st = eng.stats()
+        assert st["path_batch_contexts"] > 0
+        assert st["path_batch_reruns"] > 0
+        found = 0
+        for (f, t, e, upto, _), g in zip(reqs, got):
+            assert g == eng.find_path(f, t, e, upto), (f, t)
+            assert g == sorted(orc.find_path(f, t, e, upto, True, mode=1)), (f, t)
+            found += bool(g)
+        assert found > 20
+    finally:
+        eng.close()
+        orc.close()
