@@ -2,8 +2,10 @@
 # Named GPU-box steps (from the repo root, via gpurun): bash tools/gpu_steps.sh <tag> <step>...
 # (The one-off round scripts of rounds 1-5 are folded into these steps; tools/gpu_run.sh runs
 # ad-hoc '<name>|<seconds>|<command>' steps the same way.)
-#   tests  — pytest -m gpu;  load26 — RMAT-26 generate + load + GO leg only (load time);
-#   bench  — default bench.py
+#   tests  — pytest -m gpu;  smoke — __graft_entry__.smoke();  bench — default bench.py;
+#   load26 — RMAT-26 generate + load + GO leg only (load time);  prof26 — kernel trace of the bench;
+#   pmc26 / pmc22 / sq26 — GO HBM / SQ counters;  pmcsp — SHORTEST (rolling + one-pair) HBM and SQ
+#   counters;  pmcc5 — C5 GO 4 STEPS HBM counters and kernel trace;  bench8 — 8-rank rehearsal
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 TAG=$1; shift
