@@ -43,7 +43,7 @@ for step in "$@"; do
         --verify 0 --c2 0 --c5-scale 0 --getbound-reqs 0 --c1-reqs 0 > "$OUT/sq26.json" 2> "$OUT/sq26.log" \
         || { tail -30 "$OUT/sq26.log"; exit 1; }
       python3 tools/pmc_summary.py $(find "$OUT/sq26" -name '*counter_collection.csv') > "$OUT/pmc_sq_rmat26.json" ;;
-    pmcsp)   # SHORTEST kernels (batched k_ch_step_b, one-pair k_ch_step<1>): HBM bytes and SQ cycles
+    pmcsp)   # SHORTEST kernels (rolling k_ch_roll<4>, one-pair k_ch_step<1>): HBM bytes and SQ cycles
       i=0
       for c in FETCH_SIZE WRITE_SIZE "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU"; do
         i=$((i + 1))
