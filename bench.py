@@ -42,7 +42,7 @@ METRIC = "GO 3 STEPS traversed edges/sec (TEPS) at 1/2/4/8 GPU; FIND SHORTEST PA
 # bench's default workload (tools/gpu_steps.sh pmc26 / pmc22 / pmcc5 -> tools/pmc_summary.py; FETCH_SIZE
 # doubled per the gfx950 note), keyed by workload
 PMC_FILES = {("RMAT-26", 16): os.path.join(ROOT, "profiles", "r05_finb_pmc_hbm_rmat26.json"),
-             ("RMAT-22", 64): os.path.join(ROOT, "profiles", "r02_pmc_hbm_rmat22.json"),
+             ("RMAT-22", 64): os.path.join(ROOT, "profiles", "r06_as_pmc_hbm_rmat22.json"),
              ("C5-RMAT-24", 16): os.path.join(ROOT, "profiles", "r06_u_pmc_hbm_c5_rmat24.json")}
 # library kernel id -> instantiations in the rocprof names, first match wins (FINAL: this bench's
 # range WHERE with a _dst YIELD runs k_expand<4> = FINALD; <3> FINALF; <1> the general interpreter;
